@@ -1,0 +1,119 @@
+/*
+ * mer.h -- C-ABI of the MI355X-native (gfx950 / CDNA4) multimodal-emotion-recognition hot path.
+ *
+ * Drop-in boundary for the reference's fusion train/inference path
+ * (Wionerlol/MultimodalEmotionRecognition: src/models/{fusion,video,wavlm_audio,temporal}.py,
+ * src/train.py:200-228, src/optimized_runtime.py:99-108).  The reference is pure Python over
+ * torch / torchvision / transformers; every entry point below replaces the device math of one
+ * of its call sites, cited per function.  The Python host layer
+ * (multimodalemotionrecognition_amd/*.py) binds these through ctypes.
+ *
+ * Conventions (every function):
+ *   - returns 0 on success or a hipError_t value (e.g. 1 = hipErrorInvalidValue on bad shapes);
+ *   - all tensor arguments are DEVICE pointers; the caller allocates every output/workspace;
+ *   - `stream` is a hipStream_t passed as void*; work is enqueued asynchronously on it;
+ *   - no internal allocation, no global mutable state; reentrant per stream;
+ *   - element strides/leading dimensions are in ELEMENTS; dtype codes: 0 = fp32, 1 = bf16;
+ *   - activation codes: 0 none, 1 ReLU, 2 exact-erf GELU.
+ * Plain C types only: int = int32, long = int64, unsigned long long = uint64 (RNG seeds).
+ */
+#ifndef MER_H_
+#define MER_H_
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ============================ fusion head (fp32) ============================ */
+
+/* C[m,n] (+)= act(sum_k A(m,k) B(k,n) + bias[n]), batched over grid z.
+ * A(m,k) = A[m*sam + k*sak] (+ batch*bsa), B(k,n) = B[k*sbk + n*sbn]; C row-major (ldc).
+ * beta=1 accumulates into C; splitk>1 atomically adds K slices (act must be 0).
+ * Replaces every nn.Linear of the head: fusion.py:269-274 (v_in_proj/a_in_proj/audio_seq_proj),
+ * fusion.py:312-326 (xattn_mlp / xattn_gate / xattn_classifier), the MHA in/out projections
+ * (TORCH:6576-6606) and their backward GEMMs (dX = dY W, dW = dY^T X). */
+int mer_gemm_f32(int M, int N, int K, const void* A, int a_dtype, long sam, long sak, long bsa, const void* B,
+                 int b_dtype, long sbk, long sbn, long bsb, float* C, long ldc, long bsc, const float* bias, int beta,
+                 int act, int splitk, int batch, void* stream);
+
+/* out[n] += sum_m X[m*ldx + n]  (bias gradients; out must be initialised). */
+int mer_colsum_f32(int M, int N, const float* X, long ldx, float* out, void* stream);
+
+/* Multi-head attention core of nn.MultiheadAttention (fusion.py:276-281,394,398 -> TORCH:6576-6606):
+ * P = softmax(scale * Q_h K_h^T + bias[b]); O_h = dropout(P) V_h.  Rows: X + (b*L+i)*ld + h*dh.
+ * bias [B,Lq,Lk] is the per-sample emotion-prior mask repeated over heads (fusion.py:351-354), or NULL.
+ * P [B,H,Lq,Lk] receives the pre-dropout probabilities (saved for backward).  dh must divide 64. */
+int mer_mha_fwd(int B, int H, int Lq, int Lk, int dh, const float* Q, long ldq, const float* K, long ldk,
+                const float* V, long ldv, const float* bias, float* O, long ldo, float* P, float scale, float drop_p,
+                unsigned long long seed, void* stream);
+
+/* Backward of mer_mha_fwd: writes dQ, dK, dV (not accumulated) and dbias[b] = sum_h dS (if non-NULL). */
+int mer_mha_bwd(int B, int H, int Lq, int Lk, int dh, const float* Q, long ldq, const float* K, long ldk,
+                const float* V, long ldv, const float* P, const float* dO, long lddo, float* dQ, long lddq, float* dK,
+                long lddk, float* dV, long lddv, float* dbias, float scale, float drop_p, unsigned long long seed,
+                void* stream);
+
+/* y = LayerNorm(x + s_b * r) with StochasticDepth scale s_b regenerated from (seed, row/rows_per_sample)
+ * (fusion.py:11-26, 284-285, 395, 399).  r may be NULL.  Saves sum/mean/rstd when non-NULL. */
+int mer_add_ln_fwd(int rows, int d, int rows_per_sample, const float* x, const float* r, float dp_p,
+                   unsigned long long seed, const float* gamma, const float* beta, float eps, float* y, float* sum_out,
+                   float* mean_out, float* rstd_out, void* stream);
+
+/* Backward of mer_add_ln_fwd: dx = dsum, dr = s_b*dsum (dr may be NULL); dgamma/dbeta accumulate. */
+int mer_add_ln_bwd(int rows, int d, int rows_per_sample, const float* dy, const float* s, const float* mean,
+                   const float* rstd, const float* gamma, float dp_p, unsigned long long seed, float* dx, float* dr,
+                   float* dgamma, float* dbeta, void* stream);
+
+/* TemporalPooler 'mean' (temporal.py:108-109): y[b*ldy + c] = mean_l x[b,l,c]; and its backward. */
+int mer_mean_pool_fwd(int B, int L, int D, const float* x, float* y, long ldy, void* stream);
+int mer_mean_pool_bwd(int B, int L, int D, const float* dy, long lddy, float* dx, int accumulate, void* stream);
+
+/* nn.CrossEntropyLoss(label_smoothing) (train.py:1033) or, late=1, NLLLoss(log(p+1e-8)) (train.py:212-214),
+ * mean over the batch, fused with dloss/dlogits (for dloss = 1).  labels are int64. */
+int mer_cross_entropy(int B, int C, const float* logits, const long long* labels, float label_smoothing, int late,
+                      float* loss, float* dlogits, void* stream);
+
+/* y = x * s[0] with s a device scalar (autograd grad_output of the loss). */
+int mer_scale_dev(long n, const float* x, const float* s, float* y, void* stream);
+
+/* In-place nn.Dropout(p) (train mode) over a row-strided matrix; mask regenerated from (seed, index). */
+int mer_dropout_inplace(int rows, int cols, float* x, long ldx, float p, unsigned long long seed, void* stream);
+
+/* Backward of dropout(relu(z)) given y: dy <- dy * (y > 0) * keep/(1-p), in place. */
+int mer_relu_dropout_bwd(int rows, int cols, float* dy, long lddy, const float* y, long ldy, float p,
+                         unsigned long long seed, void* stream);
+
+/* Gated xattn head (fusion.py:318-327, 408-411): g = sigmoid(z[b]); out = g*v + (1-g)*a; and backward
+ * (dv/da ACCUMULATE, dz written). */
+int mer_gate_mix_fwd(int B, int D, const float* z, const float* v, long ldv, const float* a, long lda, float* out,
+                     float* g_out, void* stream);
+int mer_gate_mix_bwd(int B, int D, const float* g, const float* v, long ldv, const float* a, long lda,
+                     const float* dout, float* dz, float* dv, long lddv, float* da, long ldda, void* stream);
+
+/* EmotionPriorBiasAdapter._token_bias (fusion.py:170-176):
+ * bias[b,i,j] = tanh(qt[b,i] + qp[b] + kt[b,j] + kp[b]) * scale[0]; and backward
+ * (dqp == dkp == row-total; dscale_part[b] = per-sample partial of dscale). */
+int mer_token_bias_fwd(int B, int Lq, int Lk, const float* qt, const float* qp, const float* kt, const float* kp,
+                       const float* scale, float* out, void* stream);
+int mer_token_bias_bwd(int B, int Lq, int Lk, const float* qt, const float* qp, const float* kt, const float* kp,
+                       const float* scale, const float* dbias, float* dqt, float* dkt, float* dqp, float* dkp,
+                       float* dscale_part, void* stream);
+
+/* late fusion (fusion.py:358-363): out = (softmax(za) + softmax(zv)) / 2 (row-wise, [B,C]), saving both
+ * softmaxes; and its backward (da, dv written). */
+int mer_softmax_avg_fwd(int B, int C, const float* za, const float* zv, float* out, float* pa, float* pv, void* stream);
+int mer_softmax_avg_bwd(int B, int C, const float* pa, const float* pv, const float* dout, float* da, float* dv,
+                        void* stream);
+
+/* out (+)= sum_i x[i]  (single-block deterministic reduce). */
+int mer_vec_sum(int n, const float* x, float* out, int accumulate, void* stream);
+
+/* torch.optim.Adam step (train.py:872,902; L2 weight decay added to the gradient) over one flat fp32
+ * buffer; `step` is the 1-based step count used for bias correction.  16-byte aligned buffers. */
+int mer_adam_step(long n, float* p, const float* g, float* m, float* v, float lr, float b1, float b2, float eps,
+                  float wd, int step, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MER_H_ */

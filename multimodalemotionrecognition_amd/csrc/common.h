@@ -1,0 +1,75 @@
+// Shared device helpers for the MI355X (gfx950 / CDNA4) fusion-path kernels.
+// Wave64 everywhere: every reduction below assumes 64 lanes.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define MER_API extern "C" __attribute__((visibility("default")))
+
+typedef uint16_t bf16_t;  // raw bfloat16 storage
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+
+enum MerDType { MER_F32 = 0, MER_BF16 = 1 };
+enum MerAct { MER_ACT_NONE = 0, MER_ACT_RELU = 1, MER_ACT_GELU = 2 };
+
+__device__ __forceinline__ float bf2f(bf16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
+
+// round-to-nearest-even; NaN stays NaN (quiet bit forced)
+__device__ __forceinline__ bf16_t f2bf(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x007fffffu)) return (bf16_t)((u >> 16) | 0x40);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (bf16_t)(u >> 16);
+}
+
+template <typename T> __device__ __forceinline__ float ldf(const T* p, long i);
+template <> __device__ __forceinline__ float ldf<float>(const float* p, long i) { return p[i]; }
+template <> __device__ __forceinline__ float ldf<bf16_t>(const bf16_t* p, long i) { return bf2f(p[i]); }
+
+template <typename T> __device__ __forceinline__ void stf(T* p, long i, float v);
+template <> __device__ __forceinline__ void stf<float>(float* p, long i, float v) { p[i] = v; }
+template <> __device__ __forceinline__ void stf<bf16_t>(bf16_t* p, long i, float v) { p[i] = f2bf(v); }
+
+__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+__device__ __forceinline__ float gelu_erf_grad(float x) {
+  const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
+  const float pdf = 0.39894228040143267794f * __expf(-0.5f * x * x);
+  return cdf + x * pdf;
+}
+
+__device__ __forceinline__ float apply_act(float v, int act) {
+  if (act == MER_ACT_RELU) return v > 0.f ? v : 0.f;
+  if (act == MER_ACT_GELU) return gelu_erf(v);
+  return v;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Counter-based RNG (splitmix64 finaliser over (seed, stream, index)): the same mask is
+// regenerated in backward from the same (seed, index) -- no mask tensor is stored.
+__device__ __forceinline__ uint32_t mer_hash(uint64_t seed, uint64_t idx) {
+  uint64_t z = seed + 0x9E3779B97F4A7C15ull * (idx + 1);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (uint32_t)z;
+}
+// keep with probability keep_p; returns 1/keep_p when kept, else 0
+__device__ __forceinline__ float dropout_scale(uint64_t seed, uint64_t idx, float p) {
+  if (p <= 0.f) return 1.f;
+  const float u = (mer_hash(seed, idx) >> 8) * (1.0f / 16777216.0f);
+  return u >= p ? 1.0f / (1.0f - p) : 0.0f;
+}
+
+#define MER_LAUNCH_CHECK() return (int)hipGetLastError()

@@ -1,0 +1,803 @@
+// fp32 kernels of the fusion head (fusion.py:153-184, 351-411, temporal.py:105-110, train.py:212-228).
+//
+// The head is tiny next to the encoders (1.1 GFLOP fwd at B=32) and the parity bar
+// for it is "logits within 1e-3 of the fp32 CPU reference", so everything here computes
+// in exact fp32: the GEMM uses the f32-input MFMA (v_mfma_f32_16x16x4_f32, bit-identical
+// to an fma chain), softmax / LayerNorm reductions use wave64 shuffles.
+#include "common.h"
+#include "mer.h"
+
+// ---------------------------------------------------------------------------------------
+// Strided-batched fp32 GEMM on f32 MFMA:  C[m,n] (+)= act( sum_k A[m,k] B[k,n] + bias[n] )
+// A(m,k) at A[m*sam + k*sak], B(k,n) at B[k*sbk + n*sbn]; C row-major with ldc.
+// 64x64x16 tile, 256 threads = 4 waves of 32x32 (2x2 MFMA 16x16 tiles).
+// splitk > 1: each K slice atomically adds into C (caller pre-initialises C; act must be 0).
+// ---------------------------------------------------------------------------------------
+template <typename TA, typename TB, bool A_KCONTIG, bool B_NCONTIG>
+__global__ __launch_bounds__(256) void gemm_f32_kernel(int M, int N, int K, const TA* __restrict__ A, long sam,
+                                                       long sak, long bsa, const TB* __restrict__ B, long sbk,
+                                                       long sbn, long bsb, float* __restrict__ C, long ldc,
+                                                       long bsc, const float* __restrict__ bias, int beta,
+                                                       int act, int splitk) {
+  __shared__ float As[16][64 + 4];
+  __shared__ float Bs[16][64 + 4];
+  const int bz = blockIdx.z, batch = bz / splitk, ks = bz % splitk;
+  A += batch * bsa;
+  B += batch * bsb;
+  C += batch * bsc;
+  const int m0 = blockIdx.y * 64, n0 = blockIdx.x * 64;
+  const int kchunk = ((K + splitk - 1) / splitk + 15) / 16 * 16;
+  const int kbeg = ks * kchunk, kend = min(K, kbeg + kchunk);
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int wm = (w >> 1) * 32, wn = (w & 1) * 32;
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int k0 = kbeg; k0 < kend; k0 += 16) {
+    float ra[4], rb[4];
+    int am[4], ak[4], bk[4], bn[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int e = t + 256 * i;
+      if (A_KCONTIG) { am[i] = e >> 4; ak[i] = e & 15; } else { ak[i] = e >> 6; am[i] = e & 63; }
+      const int gm = m0 + am[i], gk = k0 + ak[i];
+      ra[i] = (gm < M && gk < kend) ? ldf<TA>(A, (long)gm * sam + (long)gk * sak) : 0.f;
+      if (B_NCONTIG) { bk[i] = e >> 6; bn[i] = e & 63; } else { bn[i] = e >> 4; bk[i] = e & 15; }
+      const int gn = n0 + bn[i], gk2 = k0 + bk[i];
+      rb[i] = (gn < N && gk2 < kend) ? ldf<TB>(B, (long)gk2 * sbk + (long)gn * sbn) : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      As[ak[i]][am[i]] = ra[i];
+      Bs[bk[i]][bn[i]] = rb[i];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const int kr = kk * 4 + (lane >> 4);
+      float a[2], b[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) a[i] = As[kr][wm + i * 16 + (lane & 15)];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) b[j] = Bs[kr][wn + j * 16 + (lane & 15)];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wm + i * 16 + (lane >> 4) * 4 + r;
+        const int col = n0 + wn + j * 16 + (lane & 15);
+        if (row < M && col < N) {
+          float v = acc[i][j][r];
+          if (bias && ks == 0) v += bias[col];
+          float* cp = C + (long)row * ldc + col;
+          if (splitk > 1) {
+            atomicAdd(cp, v);
+          } else {
+            if (beta) v += *cp;
+            *cp = apply_act(v, act);
+          }
+        }
+      }
+}
+
+template <typename TA, typename TB>
+static int launch_gemm_f32(int M, int N, int K, const void* A, long sam, long sak, long bsa, const void* B, long sbk,
+                           long sbn, long bsb, float* C, long ldc, long bsc, const float* bias, int beta, int act,
+                           int splitk, int batch, hipStream_t st) {
+  dim3 grid((N + 63) / 64, (M + 63) / 64, batch * splitk);
+  const bool akc = (sak == 1), bnc = (sbn == 1);
+#define L(AK, BN)                                                                                                     \
+  hipLaunchKernelGGL((gemm_f32_kernel<TA, TB, AK, BN>), grid, dim3(256), 0, st, M, N, K, (const TA*)A, sam, sak, bsa, \
+                     (const TB*)B, sbk, sbn, bsb, C, ldc, bsc, bias, beta, act, splitk)
+  if (akc && bnc) L(true, true); else if (akc) L(true, false); else if (bnc) L(false, true); else L(false, false);
+#undef L
+  MER_LAUNCH_CHECK();
+}
+
+MER_API int mer_gemm_f32(int M, int N, int K, const void* A, int a_dtype, long sam, long sak, long bsa, const void* B,
+                         int b_dtype, long sbk, long sbn, long bsb, float* C, long ldc, long bsc, const float* bias,
+                         int beta, int act, int splitk, int batch, void* stream) {
+  if (M <= 0 || N <= 0 || batch <= 0) return 0;
+  if (splitk < 1) splitk = 1;
+  if (splitk > 1 && act != MER_ACT_NONE) return (int)hipErrorInvalidValue;
+  hipStream_t st = (hipStream_t)stream;
+  if (a_dtype == MER_F32 && b_dtype == MER_F32)
+    return launch_gemm_f32<float, float>(M, N, K, A, sam, sak, bsa, B, sbk, sbn, bsb, C, ldc, bsc, bias, beta, act, splitk, batch, st);
+  if (a_dtype == MER_BF16 && b_dtype == MER_F32)
+    return launch_gemm_f32<bf16_t, float>(M, N, K, A, sam, sak, bsa, B, sbk, sbn, bsb, C, ldc, bsc, bias, beta, act, splitk, batch, st);
+  if (a_dtype == MER_F32 && b_dtype == MER_BF16)
+    return launch_gemm_f32<float, bf16_t>(M, N, K, A, sam, sak, bsa, B, sbk, sbn, bsb, C, ldc, bsc, bias, beta, act, splitk, batch, st);
+  return launch_gemm_f32<bf16_t, bf16_t>(M, N, K, A, sam, sak, bsa, B, sbk, sbn, bsb, C, ldc, bsc, bias, beta, act, splitk, batch, st);
+}
+
+// ---------------------------------------------------------------------------------------
+// Column sum (bias gradient): out[n] (+)= sum_m X[m*ldx + n]
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void colsum_kernel(int M, int N, const float* __restrict__ X, long ldx,
+                                                     float* __restrict__ out, int rows_per_block) {
+  __shared__ float red[4][64];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int rg = threadIdx.x >> 6;
+  const int r0 = blockIdx.y * rows_per_block, r1 = min(M, r0 + rows_per_block);
+  float s = 0.f;
+  if (c < N)
+    for (int r = r0 + rg; r < r1; r += 4) s += X[(long)r * ldx + c];
+  red[rg][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (rg == 0 && c < N) {
+    s = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+    atomicAdd(out + c, s);
+  }
+}
+
+MER_API int mer_colsum_f32(int M, int N, const float* X, long ldx, float* out, void* stream) {
+  if (M <= 0 || N <= 0) return 0;
+  const int rpb = 256;
+  dim3 grid((N + 63) / 64, (M + rpb - 1) / rpb);
+  hipLaunchKernelGGL(colsum_kernel, grid, dim3(256), 0, (hipStream_t)stream, M, N, X, ldx, out, rpb);
+  MER_LAUNCH_CHECK();
+}
+
+// ---------------------------------------------------------------------------------------
+// Multi-head attention core (TORCH:6576-6606 explicit path) for the xattn blocks and the
+// temporal transformer pooler:  P = softmax(scale Q_h K_h^T + bias[b]);  O_h = drop(P) V_h.
+// q/k/v/o rows: X + (b*L + i)*ld + h*dh.  bias: [B, Lq, Lk] (per sample, shared across heads,
+// fusion.py:351-354) or null.  Saves P (pre-dropout) [B,H,Lq,Lk] for backward.
+// One workgroup = (b, h, 16 query rows); K_h and V_h staged in LDS.
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void mha_fwd_kernel(int B, int H, int Lq, int Lk, int dh, const float* __restrict__ Q,
+                                                      long ldq, const float* __restrict__ K, long ldk,
+                                                      const float* __restrict__ V, long ldv, const float* __restrict__ bias,
+                                                      float* __restrict__ O, long ldo, float* __restrict__ P,
+                                                      float scale, float drop_p, unsigned long long seed) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int dp = dh + 1;
+  float* Ks = smem;                 // [Lk][dp]
+  float* Vs = Ks + Lk * dp;         // [Lk][dp]
+  float* qs = Vs + Lk * dp;         // [4][dh]
+  float* ps = qs + 4 * dh;          // [4][Lk]
+  const int b = blockIdx.x / H, h = blockIdx.x % H;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  for (int e = t; e < Lk * dh; e += 256) {
+    const int j = e / dh, c = e % dh;
+    Ks[j * dp + c] = K[((long)b * Lk + j) * ldk + h * dh + c];
+    Vs[j * dp + c] = V[((long)b * Lk + j) * ldv + h * dh + c];
+  }
+  __syncthreads();
+  const int nsub = 64 / dh > 0 ? 64 / dh : 1;  // key subsets in the PV reduction
+  for (int ii = w; ii < 16; ii += 4) {  // every wave runs 4 rounds: syncs stay uniform
+    const int i = blockIdx.y * 16 + ii;
+    const bool valid = i < Lq;
+    if (valid) {
+      const float* qrow = Q + ((long)b * Lq + i) * ldq + h * dh;
+      for (int c = lane; c < dh; c += 64) qs[w * dh + c] = qrow[c];
+    }
+    __syncthreads();
+    if (valid) {
+      float mx = -INFINITY;
+      for (int j = lane; j < Lk; j += 64) {
+        float s = 0.f;
+        for (int c = 0; c < dh; ++c) s += qs[w * dh + c] * Ks[j * dp + c];
+        s *= scale;
+        if (bias) s += bias[((long)b * Lq + i) * Lk + j];
+        ps[w * Lk + j] = s;
+        mx = fmaxf(mx, s);
+      }
+      mx = wave_max(mx);
+      float sum = 0.f;
+      for (int j = lane; j < Lk; j += 64) {
+        const float e = __expf(ps[w * Lk + j] - mx);
+        ps[w * Lk + j] = e;
+        sum += e;
+      }
+      sum = wave_sum(sum);
+      const float inv = 1.f / sum;
+      const long prow = (((long)b * H + h) * Lq + i) * Lk;
+      for (int j = lane; j < Lk; j += 64) {
+        const float pr = ps[w * Lk + j] * inv;
+        P[prow + j] = pr;
+        ps[w * Lk + j] = pr * dropout_scale(seed, prow + j, drop_p);
+      }
+    }
+    __syncthreads();
+    if (valid) {
+      // O_i[c] = sum_j p'_j V[j][c]: lane -> (c = lane % dh, key subset lane / dh)
+      const int c = lane % dh, sub = lane / dh;
+      float o = 0.f;
+      if (sub < nsub)
+        for (int j = sub; j < Lk; j += nsub) o += ps[w * Lk + j] * Vs[j * dp + c];
+      for (int off = dh; off < 64; off <<= 1) o += __shfl_down(o, off, 64);
+      if (lane < dh) O[((long)b * Lq + i) * ldo + h * dh + c] = o;
+    }
+    __syncthreads();
+  }
+}
+
+MER_API int mer_mha_fwd(int B, int H, int Lq, int Lk, int dh, const float* Q, long ldq, const float* K, long ldk,
+                        const float* V, long ldv, const float* bias, float* O, long ldo, float* P, float scale,
+                        float drop_p, unsigned long long seed, void* stream) {
+  if (dh > 64 || (64 % dh) != 0) return (int)hipErrorInvalidValue;
+  const size_t lds = sizeof(float) * ((size_t)2 * Lk * (dh + 1) + 4 * dh + 4 * Lk);
+  if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
+  dim3 grid(B * H, (Lq + 15) / 16);
+  hipLaunchKernelGGL(mha_fwd_kernel, grid, dim3(256), lds, (hipStream_t)stream, B, H, Lq, Lk, dh, Q, ldq, K, ldk, V,
+                     ldv, bias, O, ldo, P, scale, drop_p, seed);
+  MER_LAUNCH_CHECK();
+}
+
+// Backward.  One workgroup per sample b, heads in sequence (so dbias[b] = sum_h dS needs no
+// atomics): dV_j = sum_i p'_ij dO_i; dP = (dO V^T) . mask; dS = P (dP - rowsum(P dP));
+// dQ = scale dS K; dK = scale dS^T Q.  dQ/dK/dV are written (not accumulated).
+__global__ __launch_bounds__(256) void mha_bwd_kernel(int B, int H, int Lq, int Lk, int dh, const float* __restrict__ Q,
+                                                      long ldq, const float* __restrict__ K, long ldk,
+                                                      const float* __restrict__ V, long ldv, const float* __restrict__ P,
+                                                      const float* __restrict__ dO, long lddo, float* __restrict__ dQ,
+                                                      long lddq, float* __restrict__ dK, long lddk, float* __restrict__ dV,
+                                                      long lddv, float* __restrict__ dbias, float scale, float drop_p,
+                                                      unsigned long long seed) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int dp = dh + 1;
+  float* Ks = smem;               // [Lk][dp]
+  float* Vs = Ks + Lk * dp;       // [Lk][dp]
+  float* dKs = Vs + Lk * dp;      // [Lk][dp]
+  float* dVs = dKs + Lk * dp;     // [Lk][dp]
+  float* rowq = dVs + Lk * dp;    // [4][dh]
+  float* rowdo = rowq + 4 * dh;   // [4][dh]
+  float* ds = rowdo + 4 * dh;     // [4][Lk]
+  const int b = blockIdx.x;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int nsub = 64 / dh;
+  for (int h = 0; h < H; ++h) {
+    for (int e = t; e < Lk * dh; e += 256) {
+      const int j = e / dh, c = e % dh;
+      Ks[j * dp + c] = K[((long)b * Lk + j) * ldk + h * dh + c];
+      Vs[j * dp + c] = V[((long)b * Lk + j) * ldv + h * dh + c];
+      dKs[j * dp + c] = 0.f;
+      dVs[j * dp + c] = 0.f;
+    }
+    __syncthreads();
+    const int rounds = (Lq + 3) / 4;
+    for (int rr = 0; rr < rounds; ++rr) {
+      const int i = rr * 4 + w;
+      const bool valid = i < Lq;
+      if (valid) {
+        for (int c = lane; c < dh; c += 64) {
+          rowq[w * dh + c] = Q[((long)b * Lq + i) * ldq + h * dh + c];
+          rowdo[w * dh + c] = dO[((long)b * Lq + i) * lddo + h * dh + c];
+        }
+      }
+      __syncthreads();
+      if (valid) {
+        const long prow = (((long)b * H + h) * Lq + i) * Lk;
+        float dot = 0.f;
+        for (int j = lane; j < Lk; j += 64) {
+          float dpv = 0.f;
+          for (int c = 0; c < dh; ++c) dpv += rowdo[w * dh + c] * Vs[j * dp + c];
+          const float m = dropout_scale(seed, prow + j, drop_p);
+          const float pj = P[prow + j];
+          dpv *= m;
+          ds[w * Lk + j] = dpv;
+          dot += pj * dpv;
+        }
+        dot = wave_sum(dot);
+        for (int j = lane; j < Lk; j += 64) {
+          const float pj = P[prow + j];
+          const float m = dropout_scale(seed, prow + j, drop_p);
+          const float dsv = pj * (ds[w * Lk + j] - dot);
+          ds[w * Lk + j] = dsv;
+          if (dbias) {
+            float* dbp = dbias + ((long)b * Lq + i) * Lk + j;
+            *dbp = (h == 0 ? 0.f : *dbp) + dsv;
+          }
+          // dK_j += scale ds_j q_i ; dV_j += p'_j dO_i   (LDS float atomics: rows of 4 waves race)
+          for (int c = 0; c < dh; ++c) {
+            atomicAdd(&dKs[j * dp + c], scale * dsv * rowq[w * dh + c]);
+            atomicAdd(&dVs[j * dp + c], pj * m * rowdo[w * dh + c]);
+          }
+        }
+        __builtin_amdgcn_wave_barrier();
+        const int c = lane % dh, sub = lane / dh;
+        float g = 0.f;
+        if (sub < nsub)
+          for (int j = sub; j < Lk; j += nsub) g += ds[w * Lk + j] * Ks[j * dp + c];
+        for (int off = dh; off < 64; off <<= 1) g += __shfl_down(g, off, 64);
+        if (lane < dh) dQ[((long)b * Lq + i) * lddq + h * dh + c] = scale * g;
+      }
+      __syncthreads();
+    }
+    for (int e = t; e < Lk * dh; e += 256) {
+      const int j = e / dh, c = e % dh;
+      dK[((long)b * Lk + j) * lddk + h * dh + c] = dKs[j * dp + c];
+      dV[((long)b * Lk + j) * lddv + h * dh + c] = dVs[j * dp + c];
+    }
+    __syncthreads();
+  }
+}
+
+MER_API int mer_mha_bwd(int B, int H, int Lq, int Lk, int dh, const float* Q, long ldq, const float* K, long ldk,
+                        const float* V, long ldv, const float* P, const float* dO, long lddo, float* dQ, long lddq,
+                        float* dK, long lddk, float* dV, long lddv, float* dbias, float scale, float drop_p,
+                        unsigned long long seed, void* stream) {
+  if (dh > 64 || (64 % dh) != 0) return (int)hipErrorInvalidValue;
+  const size_t lds = sizeof(float) * ((size_t)4 * Lk * (dh + 1) + 8 * dh + 4 * Lk);
+  if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(mha_bwd_kernel, dim3(B), dim3(256), lds, (hipStream_t)stream, B, H, Lq, Lk, dh, Q, ldq, K, ldk, V,
+                     ldv, P, dO, lddo, dQ, lddq, dK, lddk, dV, lddv, dbias, scale, drop_p, seed);
+  MER_LAUNCH_CHECK();
+}
+
+// ---------------------------------------------------------------------------------------
+// y = LayerNorm(x + s_b * r) (fusion.py:395,399 with StochasticDepth fusion.py:11-26):
+// s_b = per-sample drop-path scale regenerated from (seed, b); r may be null.
+// Saves the pre-norm sum (for backward), mean and rstd.  One wave per row.
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void add_ln_fwd_kernel(int rows, int d, int rows_per_sample, const float* __restrict__ x,
+                                                         const float* __restrict__ r, float dp_p,
+                                                         unsigned long long seed, const float* __restrict__ gamma,
+                                                         const float* __restrict__ beta, float eps, float* __restrict__ y,
+                                                         float* __restrict__ sum_out, float* __restrict__ mean_out,
+                                                         float* __restrict__ rstd_out) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const float sc = r ? dropout_scale(seed, row / rows_per_sample, dp_p) : 0.f;
+  const float* xr = x + (long)row * d;
+  const float* rr = r ? r + (long)row * d : nullptr;
+  float s = 0.f;
+  for (int c = lane; c < d; c += 64) {
+    const float v = xr[c] + (rr ? sc * rr[c] : 0.f);
+    if (sum_out) sum_out[(long)row * d + c] = v;
+    s += v;
+  }
+  const float mean = wave_sum(s) / d;
+  float q = 0.f;
+  for (int c = lane; c < d; c += 64) {
+    const float v = xr[c] + (rr ? sc * rr[c] : 0.f) - mean;
+    q += v * v;
+  }
+  const float rstd = rsqrtf(wave_sum(q) / d + eps);
+  for (int c = lane; c < d; c += 64) {
+    const float v = xr[c] + (rr ? sc * rr[c] : 0.f);
+    y[(long)row * d + c] = (v - mean) * rstd * gamma[c] + beta[c];
+  }
+  if (lane == 0) {
+    if (mean_out) mean_out[row] = mean;
+    if (rstd_out) rstd_out[row] = rstd;
+  }
+}
+
+MER_API int mer_add_ln_fwd(int rows, int d, int rows_per_sample, const float* x, const float* r, float dp_p,
+                           unsigned long long seed, const float* gamma, const float* beta, float eps, float* y,
+                           float* sum_out, float* mean_out, float* rstd_out, void* stream) {
+  if (rows <= 0) return 0;
+  hipLaunchKernelGGL(add_ln_fwd_kernel, dim3((rows + 3) / 4), dim3(256), 0, (hipStream_t)stream, rows, d,
+                     rows_per_sample, x, r, dp_p, seed, gamma, beta, eps, y, sum_out, mean_out, rstd_out);
+  MER_LAUNCH_CHECK();
+}
+
+// dsum = rstd*(g - mean(g) - xhat*mean(g*xhat)), g = gamma*dy; dx = dsum, dr = s_b*dsum.
+// dgamma += sum_rows dy*xhat, dbeta += sum_rows dy (block partials + one atomic per column).
+__global__ __launch_bounds__(256) void add_ln_bwd_kernel(int rows, int d, int rows_per_sample, const float* __restrict__ dy,
+                                                         const float* __restrict__ s, const float* __restrict__ mean,
+                                                         const float* __restrict__ rstd, const float* __restrict__ gamma,
+                                                         float dp_p, unsigned long long seed, float* __restrict__ dx,
+                                                         float* __restrict__ dr, float* __restrict__ dgamma,
+                                                         float* __restrict__ dbeta, int rows_per_block) {
+  extern __shared__ __attribute__((aligned(16))) float red[];  // [2][4][d]
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int c = threadIdx.x; c < 8 * d; c += 256) red[c] = 0.f;
+  __syncthreads();
+  const int r0 = blockIdx.x * rows_per_block, r1 = min(rows, r0 + rows_per_block);
+  for (int row = r0 + w; row < r1; row += 4) {
+    const float mu = mean[row], rs = rstd[row];
+    const float* dyr = dy + (long)row * d;
+    const float* sr = s + (long)row * d;
+    float a = 0.f, bsum = 0.f;
+    for (int c = lane; c < d; c += 64) {
+      const float xh = (sr[c] - mu) * rs;
+      const float g = gamma[c] * dyr[c];
+      a += g;
+      bsum += g * xh;
+      red[(0 * 4 + w) * d + c] += dyr[c] * xh;
+      red[(1 * 4 + w) * d + c] += dyr[c];
+    }
+    a = wave_sum(a) / d;
+    bsum = wave_sum(bsum) / d;
+    const float sc = dr ? dropout_scale(seed, row / rows_per_sample, dp_p) : 0.f;
+    for (int c = lane; c < d; c += 64) {
+      const float xh = (sr[c] - mu) * rs;
+      const float v = rs * (gamma[c] * dyr[c] - a - xh * bsum);
+      dx[(long)row * d + c] = v;
+      if (dr) dr[(long)row * d + c] = sc * v;
+    }
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < d; c += 256) {
+    const float g = red[0 * d + c] + red[1 * d + c] + red[2 * d + c] + red[3 * d + c];
+    const float bb = red[4 * d + c] + red[5 * d + c] + red[6 * d + c] + red[7 * d + c];
+    if (dgamma) atomicAdd(dgamma + c, g);
+    if (dbeta) atomicAdd(dbeta + c, bb);
+  }
+}
+
+MER_API int mer_add_ln_bwd(int rows, int d, int rows_per_sample, const float* dy, const float* s, const float* mean,
+                           const float* rstd, const float* gamma, float dp_p, unsigned long long seed, float* dx,
+                           float* dr, float* dgamma, float* dbeta, void* stream) {
+  if (rows <= 0) return 0;
+  if ((size_t)8 * d * sizeof(float) > 160 * 1024) return (int)hipErrorInvalidValue;
+  const int rpb = 64;
+  hipLaunchKernelGGL(add_ln_bwd_kernel, dim3((rows + rpb - 1) / rpb), dim3(256), 8 * d * sizeof(float),
+                     (hipStream_t)stream, rows, d, rows_per_sample, dy, s, mean, rstd, gamma, dp_p, seed, dx, dr,
+                     dgamma, dbeta, rpb);
+  MER_LAUNCH_CHECK();
+}
+
+// ---------------------------------------------------------------------------------------
+// Mean over dim 1 (TemporalPooler 'mean', temporal.py:108-109): [B,L,D] -> y[b*ldy + c].
+// ---------------------------------------------------------------------------------------
+__global__ void mean_pool_fwd_kernel(int B, int L, int D, const float* __restrict__ x, float* __restrict__ y, long ldy) {
+  const int b = blockIdx.y, c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= D) return;
+  float s = 0.f;
+  for (int l = 0; l < L; ++l) s += x[((long)b * L + l) * D + c];
+  y[(long)b * ldy + c] = s / L;
+}
+__global__ void mean_pool_bwd_kernel(int B, int L, int D, const float* __restrict__ dy, long lddy, float* __restrict__ dx,
+                                     int accumulate) {
+  const long n = (long)B * L * D;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < n; e += (long)gridDim.x * blockDim.x) {
+    const int c = e % D;
+    const int b = e / ((long)L * D);
+    const float g = dy[(long)b * lddy + c] / L;
+    dx[e] = accumulate ? dx[e] + g : g;
+  }
+}
+MER_API int mer_mean_pool_fwd(int B, int L, int D, const float* x, float* y, long ldy, void* stream) {
+  hipLaunchKernelGGL(mean_pool_fwd_kernel, dim3((D + 127) / 128, B), dim3(128), 0, (hipStream_t)stream, B, L, D, x, y, ldy);
+  MER_LAUNCH_CHECK();
+}
+MER_API int mer_mean_pool_bwd(int B, int L, int D, const float* dy, long lddy, float* dx, int accumulate, void* stream) {
+  const long n = (long)B * L * D;
+  const int grid = (int)((n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096);
+  hipLaunchKernelGGL(mean_pool_bwd_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, B, L, D, dy, lddy, dx, accumulate);
+  MER_LAUNCH_CHECK();
+}
+
+// ---------------------------------------------------------------------------------------
+// Cross entropy with label smoothing (train.py:1033, mean reduction) fused with its gradient:
+// loss = mean_b [(1-eps) * nll_b + eps * mean_c(-logp_bc)];  dlogits = (softmax - q) / B.
+// late mode (train.py:212-214): inputs are probabilities p, loss = NLL(log(p + 1e-8)).
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void ce_kernel(int B, int C, const float* __restrict__ logits,
+                                                 const long long* __restrict__ labels, float eps_ls, int late,
+                                                 float* __restrict__ loss, float* __restrict__ dlogits) {
+  __shared__ float part[4];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  float acc = 0.f;
+  for (int b = w; b < B; b += 4) {
+    const float* z = logits + (long)b * C;
+    const long long y = labels[b];
+    if (late) {
+      for (int c = lane; c < C; c += 64) {
+        const float pc = z[c];
+        if (c == y) acc += -logf(pc + 1e-8f);
+        if (dlogits) dlogits[(long)b * C + c] = (c == y) ? -1.0f / ((pc + 1e-8f) * B) : 0.f;
+      }
+      continue;
+    }
+    float mx = -INFINITY;
+    for (int c = lane; c < C; c += 64) mx = fmaxf(mx, z[c]);
+    mx = wave_max(mx);
+    float se = 0.f, sz = 0.f;
+    for (int c = lane; c < C; c += 64) { se += __expf(z[c] - mx); sz += z[c]; }
+    se = wave_sum(se);
+    sz = wave_sum(sz);
+    const float lse = mx + logf(se);
+    if (lane == 0) acc += (1.f - eps_ls) * (lse - z[y]) + eps_ls * (lse - sz / C);
+    for (int c = lane; c < C; c += 64) {
+      const float sm = __expf(z[c] - lse);
+      const float q = (c == y ? 1.f - eps_ls : 0.f) + eps_ls / C;
+      if (dlogits) dlogits[(long)b * C + c] = (sm - q) / B;
+    }
+  }
+  acc = wave_sum(acc);
+  if (lane == 0) part[w] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) *loss = (part[0] + part[1] + part[2] + part[3]) / B;
+}
+MER_API int mer_cross_entropy(int B, int C, const float* logits, const long long* labels, float label_smoothing,
+                              int late, float* loss, float* dlogits, void* stream) {
+  hipLaunchKernelGGL(ce_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, B, C, logits, labels, label_smoothing, late,
+                     loss, dlogits);
+  MER_LAUNCH_CHECK();
+}
+
+// ---------------------------------------------------------------------------------------
+// Elementwise helpers
+// ---------------------------------------------------------------------------------------
+// y = x * s[0] (device scalar, e.g. autograd's grad_output of a 0-d loss)
+__global__ void scale_dev_kernel(long n, const float* __restrict__ x, const float* __restrict__ s, float* __restrict__ y) {
+  const float k = *s;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < n; e += (long)gridDim.x * blockDim.x) y[e] = x[e] * k;
+}
+MER_API int mer_scale_dev(long n, const float* x, const float* s, float* y, void* stream) {
+  const int grid = (int)((n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096);
+  hipLaunchKernelGGL(scale_dev_kernel, dim3(grid > 0 ? grid : 1), dim3(256), 0, (hipStream_t)stream, n, x, s, y);
+  MER_LAUNCH_CHECK();
+}
+
+// in-place dropout on rows with stride (nn.Dropout in train mode): x *= keep/(1-p)
+__global__ void dropout_kernel(int rows, int cols, float* __restrict__ x, long ldx, float p, unsigned long long seed) {
+  const long n = (long)rows * cols;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < n; e += (long)gridDim.x * blockDim.x) {
+    const int r = e / cols, c = e % cols;
+    x[(long)r * ldx + c] *= dropout_scale(seed, e, p);
+  }
+}
+MER_API int mer_dropout_inplace(int rows, int cols, float* x, long ldx, float p, unsigned long long seed, void* stream) {
+  if (p <= 0.f) return 0;
+  const long n = (long)rows * cols;
+  const int grid = (int)((n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096);
+  hipLaunchKernelGGL(dropout_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, rows, cols, x, ldx, p, seed);
+  MER_LAUNCH_CHECK();
+}
+
+// backward of y = dropout(relu(z)) given y: dz = dy * (y > 0) * drop_scale  (in place on dy)
+__global__ void relu_dropout_bwd_kernel(int rows, int cols, float* __restrict__ dy, long lddy, const float* __restrict__ y,
+                                        long ldy, float p, unsigned long long seed) {
+  const long n = (long)rows * cols;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < n; e += (long)gridDim.x * blockDim.x) {
+    const int r = e / cols, c = e % cols;
+    const float yy = y[(long)r * ldy + c];
+    float g = dy[(long)r * lddy + c];
+    g = yy > 0.f ? g * dropout_scale(seed, e, p) : 0.f;
+    dy[(long)r * lddy + c] = g;
+  }
+}
+MER_API int mer_relu_dropout_bwd(int rows, int cols, float* dy, long lddy, const float* y, long ldy, float p,
+                                 unsigned long long seed, void* stream) {
+  const long n = (long)rows * cols;
+  const int grid = (int)((n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096);
+  hipLaunchKernelGGL(relu_dropout_bwd_kernel, dim3(grid > 0 ? grid : 1), dim3(256), 0, (hipStream_t)stream, rows, cols,
+                     dy, lddy, y, ldy, p, seed);
+  MER_LAUNCH_CHECK();
+}
+
+// gated mix (fusion.py:408-411):  g = sigmoid(z[b]);  out = g*v + (1-g)*a
+__global__ void gate_mix_fwd_kernel(int B, int D, const float* __restrict__ z, const float* __restrict__ v, long ldv,
+                                    const float* __restrict__ a, long lda, float* __restrict__ out, float* __restrict__ g_out) {
+  const int b = blockIdx.x;
+  const float g = 1.f / (1.f + __expf(-z[b]));
+  if (threadIdx.x == 0 && g_out) g_out[b] = g;
+  for (int c = threadIdx.x; c < D; c += blockDim.x)
+    out[(long)b * D + c] = g * v[(long)b * ldv + c] + (1.f - g) * a[(long)b * lda + c];
+}
+// dz = sum_c dout*(v-a) * g(1-g); dv = g*dout; da = (1-g)*dout  (dv/da accumulate into given buffers)
+__global__ void gate_mix_bwd_kernel(int B, int D, const float* __restrict__ g_in, const float* __restrict__ v, long ldv,
+                                    const float* __restrict__ a, long lda, const float* __restrict__ dout,
+                                    float* __restrict__ dz, float* __restrict__ dv, long lddv, float* __restrict__ da,
+                                    long ldda) {
+  __shared__ float red[4];
+  const int b = blockIdx.x;
+  const float g = g_in[b];
+  float s = 0.f;
+  for (int c = threadIdx.x; c < D; c += blockDim.x) {
+    const float d = dout[(long)b * D + c];
+    s += d * (v[(long)b * ldv + c] - a[(long)b * lda + c]);
+    dv[(long)b * lddv + c] += g * d;
+    da[(long)b * ldda + c] += (1.f - g) * d;
+  }
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) dz[b] = (red[0] + red[1] + red[2] + red[3]) * g * (1.f - g);
+}
+MER_API int mer_gate_mix_fwd(int B, int D, const float* z, const float* v, long ldv, const float* a, long lda,
+                             float* out, float* g_out, void* stream) {
+  hipLaunchKernelGGL(gate_mix_fwd_kernel, dim3(B), dim3(256), 0, (hipStream_t)stream, B, D, z, v, ldv, a, lda, out, g_out);
+  MER_LAUNCH_CHECK();
+}
+MER_API int mer_gate_mix_bwd(int B, int D, const float* g, const float* v, long ldv, const float* a, long lda,
+                             const float* dout, float* dz, float* dv, long lddv, float* da, long ldda, void* stream) {
+  hipLaunchKernelGGL(gate_mix_bwd_kernel, dim3(B), dim3(256), 0, (hipStream_t)stream, B, D, g, v, ldv, a, lda, dout, dz,
+                     dv, lddv, da, ldda);
+  MER_LAUNCH_CHECK();
+}
+
+// ---------------------------------------------------------------------------------------
+// Emotion-prior token bias (fusion.py:170-176):
+//   bias[b,i,j] = tanh(qt[b,i] + qp[b] + kt[b,j] + kp[b]) * scale
+// where qt/kt are the token halves of query_head/key_head and qp/kp the prior halves (+bias).
+// ---------------------------------------------------------------------------------------
+__global__ void token_bias_fwd_kernel(int B, int Lq, int Lk, const float* __restrict__ qt, const float* __restrict__ qp,
+                                      const float* __restrict__ kt, const float* __restrict__ kp,
+                                      const float* __restrict__ scale, float* __restrict__ out) {
+  const int b = blockIdx.y;
+  const float s = *scale, base = qp[b] + kp[b];
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < Lq * Lk; e += gridDim.x * blockDim.x) {
+    const int i = e / Lk, j = e % Lk;
+    out[(long)b * Lq * Lk + e] = tanhf(qt[(long)b * Lq + i] + kt[(long)b * Lk + j] + base) * s;
+  }
+}
+// g = dbias*scale*(1-tanh^2): dqt[b,i] = sum_j g, dkt[b,j] = sum_i g, dqp[b] = dkp[b] = sum g,
+// dscale += sum dbias*tanh.  One workgroup per sample, deterministic.
+__global__ __launch_bounds__(256) void token_bias_bwd_kernel(int B, int Lq, int Lk, const float* __restrict__ qt,
+                                                             const float* __restrict__ qp, const float* __restrict__ kt,
+                                                             const float* __restrict__ kp, const float* __restrict__ scale,
+                                                             const float* __restrict__ dbias, float* __restrict__ dqt,
+                                                             float* __restrict__ dkt, float* __restrict__ dqp,
+                                                             float* __restrict__ dkp, float* __restrict__ dscale_part) {
+  __shared__ float red[2][4];
+  const int b = blockIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const float s = *scale, base = qp[b] + kp[b];
+  const float* db = dbias + (long)b * Lq * Lk;
+  float tot = 0.f, dsc = 0.f;
+  for (int i = w; i < Lq; i += 4) {
+    float acc = 0.f;
+    for (int j = lane; j < Lk; j += 64) {
+      const float th = tanhf(qt[(long)b * Lq + i] + kt[(long)b * Lk + j] + base);
+      const float d = db[(long)i * Lk + j];
+      acc += d * s * (1.f - th * th);
+      dsc += d * th;
+    }
+    acc = wave_sum(acc);
+    if (lane == 0) dqt[(long)b * Lq + i] = acc;
+    tot += lane == 0 ? acc : 0.f;
+  }
+  for (int j = threadIdx.x; j < Lk; j += 256) {
+    float acc = 0.f;
+    for (int i = 0; i < Lq; ++i) {
+      const float th = tanhf(qt[(long)b * Lq + i] + kt[(long)b * Lk + j] + base);
+      acc += db[(long)i * Lk + j] * s * (1.f - th * th);
+    }
+    dkt[(long)b * Lk + j] = acc;
+  }
+  tot = wave_sum(tot);
+  dsc = wave_sum(dsc);
+  if (lane == 0) { red[0][w] = tot; red[1][w] = dsc; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float tt = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+    dqp[b] = tt;
+    dkp[b] = tt;
+    dscale_part[b] = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+  }
+}
+MER_API int mer_token_bias_fwd(int B, int Lq, int Lk, const float* qt, const float* qp, const float* kt, const float* kp,
+                               const float* scale, float* out, void* stream) {
+  dim3 grid((Lq * Lk + 255) / 256, B);
+  hipLaunchKernelGGL(token_bias_fwd_kernel, grid, dim3(256), 0, (hipStream_t)stream, B, Lq, Lk, qt, qp, kt, kp, scale, out);
+  MER_LAUNCH_CHECK();
+}
+MER_API int mer_token_bias_bwd(int B, int Lq, int Lk, const float* qt, const float* qp, const float* kt, const float* kp,
+                               const float* scale, const float* dbias, float* dqt, float* dkt, float* dqp, float* dkp,
+                               float* dscale_part, void* stream) {
+  hipLaunchKernelGGL(token_bias_bwd_kernel, dim3(B), dim3(256), 0, (hipStream_t)stream, B, Lq, Lk, qt, qp, kt, kp, scale,
+                     dbias, dqt, dkt, dqp, dkp, dscale_part);
+  MER_LAUNCH_CHECK();
+}
+
+// ---------------------------------------------------------------------------------------
+// Sum of a small vector into a scalar (deterministic single-block reduce), optional accumulate.
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void vec_sum_kernel(int n, const float* __restrict__ x, float* __restrict__ out, int acc) {
+  __shared__ float red[4];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < n; i += 256) s += x[i];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float v = red[0] + red[1] + red[2] + red[3];
+    *out = acc ? *out + v : v;
+  }
+}
+MER_API int mer_vec_sum(int n, const float* x, float* out, int accumulate, void* stream) {
+  hipLaunchKernelGGL(vec_sum_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, n, x, out, accumulate);
+  MER_LAUNCH_CHECK();
+}
+
+// ---------------------------------------------------------------------------------------
+// Fused Adam over one flat fp32 buffer (torch.optim.Adam semantics, train.py:872,902):
+//   g += wd*p; m = b1 m + (1-b1) g; v = b2 v + (1-b2) g^2; p -= lr/bc1 * m / (sqrt(v)/sqrt(bc2) + eps)
+// HBM-bound: 16 B read + 12 B written per parameter... vectorised 4-wide.
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void adam_kernel(long n, float* __restrict__ p, const float* __restrict__ g,
+                                                   float* __restrict__ m, float* __restrict__ v, float lr, float b1,
+                                                   float b2, float eps, float wd, float bc1, float bc2_sqrt) {
+  const long n4 = n / 4;
+  const float step = lr / bc1;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < n4; e += (long)gridDim.x * blockDim.x) {
+    float4 pp = reinterpret_cast<float4*>(p)[e];
+    const float4 gg = reinterpret_cast<const float4*>(g)[e];
+    float4 mm = reinterpret_cast<float4*>(m)[e];
+    float4 vv = reinterpret_cast<float4*>(v)[e];
+#define ADAM1(c)                                                  \
+  {                                                               \
+    const float gr = gg.c + wd * pp.c;                            \
+    mm.c = b1 * mm.c + (1.f - b1) * gr;                           \
+    vv.c = b2 * vv.c + (1.f - b2) * gr * gr;                      \
+    pp.c -= step * mm.c / (sqrtf(vv.c) / bc2_sqrt + eps);         \
+  }
+    ADAM1(x) ADAM1(y) ADAM1(z) ADAM1(w)
+#undef ADAM1
+    reinterpret_cast<float4*>(p)[e] = pp;
+    reinterpret_cast<float4*>(m)[e] = mm;
+    reinterpret_cast<float4*>(v)[e] = vv;
+  }
+  for (long e = n4 * 4 + blockIdx.x * (long)blockDim.x + threadIdx.x; e < n; e += (long)gridDim.x * blockDim.x) {
+    const float gr = g[e] + wd * p[e];
+    m[e] = b1 * m[e] + (1.f - b1) * gr;
+    v[e] = b2 * v[e] + (1.f - b2) * gr * gr;
+    p[e] -= step * m[e] / (sqrtf(v[e]) / bc2_sqrt + eps);
+  }
+}
+MER_API int mer_adam_step(long n, float* p, const float* g, float* m, float* v, float lr, float b1, float b2, float eps,
+                          float wd, int step, void* stream) {
+  if (n <= 0) return 0;
+  if (((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) return (int)hipErrorInvalidValue;
+  const float bc1 = 1.f - powf(b1, (float)step);
+  const float bc2s = sqrtf(1.f - powf(b2, (float)step));
+  const long n4 = (n + 3) / 4;
+  const int grid = (int)((n4 + 255) / 256 < 2048 ? (n4 + 255) / 256 : 2048);
+  hipLaunchKernelGGL(adam_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, n, p, g, m, v, lr, b1, b2, eps, wd,
+                     bc1, bc2s);
+  MER_LAUNCH_CHECK();
+}
+
+// ---------------------------------------------------------------------------------------
+// late fusion (fusion.py:358-363): out = (softmax(za) + softmax(zv)) / 2, one wave per row.
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ void softmax_row(const float* z, float* p, int C, int lane) {
+  float mx = -INFINITY;
+  for (int c = lane; c < C; c += 64) mx = fmaxf(mx, z[c]);
+  mx = wave_max(mx);
+  float s = 0.f;
+  for (int c = lane; c < C; c += 64) s += __expf(z[c] - mx);
+  s = wave_sum(s);
+  for (int c = lane; c < C; c += 64) p[c] = __expf(z[c] - mx) / s;
+}
+__global__ void softmax_avg_fwd_kernel(int B, int C, const float* __restrict__ za, const float* __restrict__ zv,
+                                       float* __restrict__ out, float* __restrict__ pa, float* __restrict__ pv) {
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (b >= B) return;
+  softmax_row(za + (long)b * C, pa + (long)b * C, C, lane);
+  softmax_row(zv + (long)b * C, pv + (long)b * C, C, lane);
+  __builtin_amdgcn_wave_barrier();
+  for (int c = lane; c < C; c += 64) out[(long)b * C + c] = 0.5f * (pa[(long)b * C + c] + pv[(long)b * C + c]);
+}
+__global__ void softmax_avg_bwd_kernel(int B, int C, const float* __restrict__ pa, const float* __restrict__ pv,
+                                       const float* __restrict__ dout, float* __restrict__ da, float* __restrict__ dv) {
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (b >= B) return;
+  const float* g = dout + (long)b * C;
+  float sa = 0.f, sv = 0.f;
+  for (int c = lane; c < C; c += 64) { sa += pa[(long)b * C + c] * g[c]; sv += pv[(long)b * C + c] * g[c]; }
+  sa = wave_sum(sa);
+  sv = wave_sum(sv);
+  for (int c = lane; c < C; c += 64) {
+    da[(long)b * C + c] = 0.5f * pa[(long)b * C + c] * (g[c] - sa);
+    dv[(long)b * C + c] = 0.5f * pv[(long)b * C + c] * (g[c] - sv);
+  }
+}
+MER_API int mer_softmax_avg_fwd(int B, int C, const float* za, const float* zv, float* out, float* pa, float* pv,
+                                void* stream) {
+  hipLaunchKernelGGL(softmax_avg_fwd_kernel, dim3((B + 3) / 4), dim3(256), 0, (hipStream_t)stream, B, C, za, zv, out, pa, pv);
+  MER_LAUNCH_CHECK();
+}
+MER_API int mer_softmax_avg_bwd(int B, int C, const float* pa, const float* pv, const float* dout, float* da, float* dv,
+                                void* stream) {
+  hipLaunchKernelGGL(softmax_avg_bwd_kernel, dim3((B + 3) / 4), dim3(256), 0, (hipStream_t)stream, B, C, pa, pv, dout, da, dv);
+  MER_LAUNCH_CHECK();
+}

@@ -1,0 +1,140 @@
+"""concat / gated / late fusion heads (fusion.py:358-363, 413-435) on the HIP kernels.
+
+Inputs are the encoders' pooled embeddings (``audio_model.encode`` -> [B, Da],
+``video_model.encode`` -> [B, Dv]).  fp32 math; one autograd node per head.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import kernels as K
+from .xattn_head import site_seed
+
+
+def _grad_buf(p):
+    from .fusion import grad_buffer
+    return grad_buffer(p)
+
+
+class _EmbHeadFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, a_emb, v_emb, mode, training, seed, drop_a, drop_v, names, *params):
+        p = dict(zip(names, params))
+        B = a_emb.shape[0]
+        dev = a_emb.device
+        e = lambda *s: torch.empty(s, device=dev, dtype=torch.float32)  # noqa: E731
+        cd = p["audio_proj.weight"].shape[0]
+        cat = e(B, 2 * cd)
+        a, v = cat[:, :cd], cat[:, cd:]
+        K.linear_fwd(a_emb, p["audio_proj.weight"], p["audio_proj.bias"], a)
+        K.linear_fwd(v_emb, p["video_proj.weight"], p["video_proj.bias"], v)
+        if drop_a:
+            a.zero_()
+        if drop_v:
+            v.zero_()
+        dp = 0.2 if training else 0.0
+        sv = {"cat": cat}
+        if mode == "concat":
+            w0 = p["fusion.0.weight"]
+            h = K.linear_fwd(cat, w0, p["fusion.0.bias"], e(B, w0.shape[0]), act="relu")
+            K.dropout_(h, dp, site_seed(seed, 11))
+            w3 = p["fusion.3.weight"]
+            out = K.linear_fwd(h, w3, p["fusion.3.bias"], e(B, w3.shape[0]))
+            sv["h"] = h
+        else:
+            w0 = p["gate.0.weight"]
+            h = K.linear_fwd(cat, w0, p["gate.0.bias"], e(B, w0.shape[0]), act="relu")
+            K.dropout_(h, dp, site_seed(seed, 11))
+            z = K.linear_fwd(h, p["gate.3.weight"], p["gate.3.bias"], e(B, 1))
+            fused, g = e(B, cd), e(B)
+            K.gate_mix_fwd(z, a, v, fused, g)  # g*a + (1-g)*v  (fusion.py:434)
+            wc = p["classifier.weight"]
+            out = K.linear_fwd(fused, wc, p["classifier.bias"], e(B, wc.shape[0]))
+            sv.update(h=h, g=g, fused=fused)
+        ctx.sv, ctx.p, ctx.names, ctx.params = sv, p, names, params
+        ctx.mode, ctx.dp, ctx.seed, ctx.drops = mode, dp, seed, (drop_a, drop_v)
+        ctx.a_emb, ctx.v_emb = a_emb, v_emb
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        p, sv = ctx.p, ctx.sv
+        dout = dout.contiguous().float()
+        B = dout.shape[0]
+        dev = dout.device
+        e = lambda *s: torch.empty(s, device=dev, dtype=torch.float32)  # noqa: E731
+        used = ["audio_proj.weight", "audio_proj.bias", "video_proj.weight", "video_proj.bias"]
+        used += (["fusion.0.weight", "fusion.0.bias", "fusion.3.weight", "fusion.3.bias"] if ctx.mode == "concat" else
+                 ["gate.0.weight", "gate.0.bias", "gate.3.weight", "gate.3.bias", "classifier.weight", "classifier.bias"])
+        grads = {n: _grad_buf(p[n]) for n in used}
+        cat = sv["cat"]
+        cd = cat.shape[1] // 2
+        dcat = e(B, 2 * cd)
+        if ctx.mode == "concat":
+            h = sv["h"]
+            dh = e(B, h.shape[1])
+            K.linear_bwd(h, p["fusion.3.weight"], dout, dx=dh, dw=grads["fusion.3.weight"], db=grads["fusion.3.bias"])
+            K.relu_dropout_bwd_(dh, h, ctx.dp, site_seed(ctx.seed, 11))
+            K.linear_bwd(cat, p["fusion.0.weight"], dh, dx=dcat, dw=grads["fusion.0.weight"], db=grads["fusion.0.bias"])
+        else:
+            h, g, fused = sv["h"], sv["g"], sv["fused"]
+            dfused = e(B, cd)
+            K.linear_bwd(fused, p["classifier.weight"], dout, dx=dfused, dw=grads["classifier.weight"],
+                         db=grads["classifier.bias"])
+            dcat.zero_()
+            dz = e(B, 1)
+            K.gate_mix_bwd(g, cat[:, :cd], cat[:, cd:], dfused, dz, dcat[:, :cd], dcat[:, cd:])
+            dh = e(B, h.shape[1])
+            K.linear_bwd(h, p["gate.3.weight"], dz, dx=dh, dw=grads["gate.3.weight"], db=grads["gate.3.bias"])
+            K.relu_dropout_bwd_(dh, h, ctx.dp, site_seed(ctx.seed, 11))
+            K.linear_bwd(cat, p["gate.0.weight"], dh, dx=dcat, dw=grads["gate.0.weight"], db=grads["gate.0.bias"],
+                         dx_beta=1)
+        if ctx.drops[0]:
+            dcat[:, :cd].zero_()
+        if ctx.drops[1]:
+            dcat[:, cd:].zero_()
+        need_a, need_v = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        da = e(*ctx.a_emb.shape) if need_a else None
+        dv = e(*ctx.v_emb.shape) if need_v else None
+        K.linear_bwd(ctx.a_emb, p["audio_proj.weight"], dcat[:, :cd], dx=da, dw=grads["audio_proj.weight"],
+                     db=grads["audio_proj.bias"])
+        K.linear_bwd(ctx.v_emb, p["video_proj.weight"], dcat[:, cd:], dx=dv, dw=grads["video_proj.weight"],
+                     db=grads["video_proj.bias"])
+        out = [grads.get(n) if (n in grads and t.requires_grad) else None for n, t in zip(ctx.names, ctx.params)]
+        return (da, dv, None, None, None, None, None, None, *out)
+
+
+def embedding_head(model, a_emb, v_emb, drop_a=False, drop_v=False):
+    names, params = [], []
+    for n, q in model.named_parameters():
+        if n.startswith(("audio_model.", "video_model.")):
+            continue
+        names.append(n)
+        params.append(q)
+    seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if model.training else 0
+    return _EmbHeadFn.apply(a_emb.contiguous(), v_emb.contiguous(), model.mode, model.training, seed,
+                            bool(drop_a), bool(drop_v), tuple(names), *params)
+
+
+class _LateFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, a_logits, v_logits):
+        a_logits = a_logits.contiguous().float()
+        v_logits = v_logits.contiguous().float()
+        out = torch.empty_like(a_logits)
+        pa, pv = torch.empty_like(a_logits), torch.empty_like(v_logits)
+        K.softmax_avg_fwd(a_logits, v_logits, out, pa, pv)
+        ctx.save_for_backward(pa, pv)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        pa, pv = ctx.saved_tensors
+        da, dv = torch.empty_like(pa), torch.empty_like(pv)
+        K.softmax_avg_bwd(pa, pv, dout.contiguous().float(), da, dv)
+        return da, dv
+
+
+def late_probs(a_logits, v_logits):
+    """late mode (fusion.py:358-363): (softmax(a) + softmax(v)) / 2 -- probabilities."""
+    return _LateFn.apply(a_logits, v_logits)

@@ -1,0 +1,276 @@
+"""``FusionModel`` and friends -- drop-in mirror of ``src/models/fusion.py`` on the MI355X kernels.
+
+Same class names, constructor keyword arguments, module attribute names (hence state-dict
+keys: reference checkpoints load unchanged) and forward signatures as the reference
+(``fusion.py:11-437``).  The math runs in ``libmer_hip.so``: the xattn head through the
+explicit schedule in ``xattn_head.py`` (one autograd node), the concat / gated / late heads
+through ``embedding_head.py``.  There is no CPU path: calling the model on CPU tensors raises.
+"""
+from __future__ import annotations
+
+import math
+import random
+from typing import Optional
+
+import torch
+from torch import nn
+
+from . import embedding_head as EH
+from . import xattn_head as XH
+from .temporal import TemporalPooler
+
+
+def _require_device(*ts):
+    for t in ts:
+        if isinstance(t, torch.Tensor) and not t.is_cuda:
+            raise RuntimeError("multimodalemotionrecognition_amd runs on MI355X (HIP) only; move the model and "
+                               "inputs to a 'cuda' device (the CPU reference lives in oracle/, test-only)")
+
+
+def _next_seed() -> int:
+    # host-side draw so that torch.manual_seed() makes runs reproducible (train.py:951 set_seed)
+    return int(torch.randint(0, 2 ** 62, (1,)).item())
+
+
+class StochasticDepth(nn.Module):
+    """Per-sample drop-path (fusion.py:11-26); applied inside the fused residual+LayerNorm kernel."""
+
+    def __init__(self, drop_prob: float = 0.0) -> None:
+        super().__init__()
+        self.drop_prob = float(max(0.0, min(1.0, drop_prob)))
+
+
+class ModalityDropout(nn.Module):
+    """Batch-wide modality dropout (fusion.py:29-55): one host draw per modality per batch."""
+
+    def __init__(self, audio_dropout_p: float = 0.2, video_dropout_p: float = 0.2):
+        super().__init__()
+        self.audio_dropout_p = audio_dropout_p
+        self.video_dropout_p = video_dropout_p
+
+    def draw(self):
+        if not self.training:
+            return False, False
+        return (torch.rand(1).item() < self.audio_dropout_p, torch.rand(1).item() < self.video_dropout_p)
+
+
+class ClipStyleAlignment(nn.Module):
+    """fusion.py:127-150 (parameters only; the alignment loss path is not on the north-star path)."""
+
+    def __init__(self, audio_dim: int, video_dim: int, align_dim: int, init_temperature: float = 0.07) -> None:
+        super().__init__()
+        self.audio_proj = nn.Linear(audio_dim, align_dim)
+        self.video_proj = nn.Linear(video_dim, align_dim)
+        safe_temp = max(float(init_temperature), 1e-3)
+        self.logit_scale = nn.Parameter(torch.tensor(math.log(1.0 / safe_temp), dtype=torch.float32))
+
+
+class EmotionPriorBiasAdapter(nn.Module):
+    """fusion.py:153-184 (parameters; the math is fused into the xattn head schedule)."""
+
+    def __init__(self, token_dim: int, prior_dim: int, hidden_dim: int, dropout: float = 0.1) -> None:
+        super().__init__()
+        self.prior_net = nn.Sequential(nn.Linear(token_dim * 2, hidden_dim), nn.ReLU(inplace=True),
+                                       nn.Dropout(dropout), nn.Linear(hidden_dim, prior_dim))
+        self.v_query_bias = nn.Linear(token_dim + prior_dim, 1)
+        self.a_key_bias = nn.Linear(token_dim + prior_dim, 1)
+        self.a_query_bias = nn.Linear(token_dim + prior_dim, 1)
+        self.v_key_bias = nn.Linear(token_dim + prior_dim, 1)
+        self.bias_scale = nn.Parameter(torch.tensor(1.0, dtype=torch.float32))
+        self.dropout = float(dropout)
+
+
+def grad_buffer(param: torch.Tensor) -> torch.Tensor:
+    """Where a backward kernel should accumulate ``param``'s gradient.
+
+    When a ``FusedAdam`` owns the parameter and ``param.grad`` is unset, this is the param's
+    zeroed view into the optimizer's flat gradient buffer (autograd then adopts it without a
+    copy); otherwise a fresh zero buffer (autograd accumulates it into an existing ``.grad``).
+    """
+    view = getattr(param, "_mer_grad_view", None)
+    if view is not None and param.grad is None:
+        return view
+    return torch.zeros_like(param, dtype=torch.float32)
+
+
+class _XattnHeadFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, v_feat, a_seq, cfg, training, seed, names, *params):
+        p = dict(zip(names, params))
+        logits, hctx = XH.head_forward(p, cfg, v_feat, a_seq, training, seed)
+        ctx.hctx, ctx.names, ctx.params = hctx, names, params
+        ctx.used = set(XH.used_param_names(cfg))
+        return logits
+
+    @staticmethod
+    def backward(ctx, dlogits):
+        p = dict(zip(ctx.names, ctx.params))
+        grads = {}
+        for n, t in p.items():
+            if n in ctx.used and t.requires_grad:
+                grads[n] = grad_buffer(t)
+            elif n in ctx.used:
+                grads[n] = torch.zeros_like(t)
+        dl = dlogits.contiguous().float()
+        need_v = ctx.needs_input_grad[0]
+        need_a = ctx.needs_input_grad[1]
+        dv, da = XH.head_backward(p, ctx.hctx, dl, grads, need_dv_feat=need_v, need_da_seq=need_a)
+        out_grads = [grads.get(n) if (n in ctx.used and t.requires_grad) else None for n, t in p.items()]
+        return (dv, da, None, None, None, None, *out_grads)
+
+
+class FusionModel(nn.Module):
+    def __init__(
+        self,
+        audio_model: nn.Module,
+        video_model: nn.Module,
+        num_classes: int,
+        mode: str = "late",
+        common_dim: int = 256,
+        xattn_head: str = "concat",
+        d_model: int = 128,
+        num_heads: int = 4,
+        audio_n_mels: int = 64,
+        xattn_attn_dropout: float = 0.1,
+        xattn_stochastic_depth: float = 0.1,
+        temporal_pooling: str = "mean",
+        temporal_num_heads: int = 4,
+        temporal_num_layers: int = 1,
+        temporal_dropout: float = 0.1,
+        fusion_align_mode: str = "none",
+        fusion_align_dim: int = 256,
+        fusion_align_temperature: float = 0.07,
+        xattn_use_emotion_prior: bool = False,
+        xattn_emotion_prior_dim: int = 8,
+        xattn_emotion_prior_hidden_dim: int = 64,
+        xattn_emotion_prior_dropout: float = 0.1,
+    ) -> None:
+        super().__init__()
+        self.audio_model = audio_model
+        self.video_model = video_model
+        self.mode = mode
+        self.d_model = d_model
+        self.num_heads = num_heads
+        self.audio_n_mels = audio_n_mels
+        self.fusion_align_mode = fusion_align_mode
+        self.alignment_loss = None
+        self.semantic_alignment = None
+        self.xattn_use_emotion_prior = xattn_use_emotion_prior
+        self.num_classes = num_classes
+
+        if mode in {"concat", "gated"}:
+            fusion_audio_dim = audio_model.embedding_dim
+            fusion_video_dim = video_model.embedding_dim
+            if fusion_align_mode == "clip":
+                self.semantic_alignment = ClipStyleAlignment(audio_model.embedding_dim, video_model.embedding_dim,
+                                                             fusion_align_dim, fusion_align_temperature)
+                fusion_audio_dim = fusion_video_dim = fusion_align_dim
+            self.audio_proj = nn.Linear(fusion_audio_dim, common_dim)
+            self.video_proj = nn.Linear(fusion_video_dim, common_dim)
+            if mode == "concat":
+                self.fusion = nn.Sequential(nn.Linear(common_dim * 2, common_dim), nn.ReLU(inplace=True),
+                                            nn.Dropout(0.2), nn.Linear(common_dim, num_classes))
+            else:
+                self.modality_dropout = ModalityDropout(audio_dropout_p=0.2, video_dropout_p=0.2)
+                self.gate = nn.Sequential(nn.Linear(common_dim * 2, common_dim), nn.ReLU(inplace=True),
+                                          nn.Dropout(0.2), nn.Linear(common_dim, 1), nn.Sigmoid())
+                self.classifier = nn.Linear(common_dim, num_classes)
+                with torch.no_grad():  # fusion.py:329-336: both gate Linear biases become -1
+                    self.gate[0].bias.fill_(-1.0)
+                    self.gate[3].bias.fill_(-1.0)
+
+        if mode in {"xattn", "xattn_concat", "xattn_gated"}:
+            self.v_dim = getattr(video_model, "embedding_dim", 512)
+            self.audio_sequence_dim = getattr(audio_model, "sequence_dim", d_model)
+            self.a_dim = d_model
+            self.v_in_proj = nn.Linear(self.v_dim, d_model)
+            self.a_in_proj = nn.Linear(self.a_dim, d_model)
+            # dead on the WavLM path but checkpointed (fusion.py:273)
+            self.audio_time_conv = nn.Conv1d(audio_n_mels, self.a_dim, kernel_size=3, padding=1)
+            self.audio_seq_proj = nn.Linear(self.audio_sequence_dim, self.a_dim)
+            self.v2a_attn = nn.MultiheadAttention(d_model, num_heads, dropout=xattn_attn_dropout, batch_first=True)
+            self.a2v_attn = nn.MultiheadAttention(d_model, num_heads, dropout=xattn_attn_dropout, batch_first=True)
+            self.v_drop_path = StochasticDepth(drop_prob=xattn_stochastic_depth)
+            self.a_drop_path = StochasticDepth(drop_prob=xattn_stochastic_depth)
+            self.v_norm = nn.LayerNorm(d_model)
+            self.a_norm = nn.LayerNorm(d_model)
+            if xattn_use_emotion_prior:
+                self.emotion_prior_bias = EmotionPriorBiasAdapter(d_model, xattn_emotion_prior_dim,
+                                                                  xattn_emotion_prior_hidden_dim,
+                                                                  xattn_emotion_prior_dropout)
+            else:
+                self.emotion_prior_bias = None
+            self.v_temporal_pool = TemporalPooler(d_model, temporal_pooling, temporal_num_heads,
+                                                  temporal_num_layers, temporal_dropout)
+            self.a_temporal_pool = TemporalPooler(d_model, temporal_pooling, temporal_num_heads,
+                                                  temporal_num_layers, temporal_dropout)
+            self.xattn_head = xattn_head
+            self.attn_dropout = float(xattn_attn_dropout)
+            self.temporal_pooling = temporal_pooling
+            if xattn_head == "concat":
+                self.xattn_mlp = nn.Sequential(nn.Linear(d_model * 2, common_dim), nn.ReLU(inplace=True),
+                                               nn.Dropout(0.2), nn.Linear(common_dim, num_classes))
+            elif xattn_head == "gated":
+                self.xattn_gate = nn.Sequential(nn.Linear(d_model * 2, d_model), nn.ReLU(inplace=True),
+                                                nn.Dropout(0.2), nn.Linear(d_model, 1), nn.Sigmoid())
+                self.xattn_classifier = nn.Linear(d_model, num_classes)
+                with torch.no_grad():  # fusion.py:338-344: BOTH gate Linear biases become -1
+                    self.xattn_gate[0].bias.fill_(-1.0)
+                    self.xattn_gate[3].bias.fill_(-1.0)
+
+    def pop_alignment_loss(self) -> Optional[torch.Tensor]:
+        loss = self.alignment_loss
+        self.alignment_loss = None
+        return loss
+
+    # -------------------------------------------------------------------------------------
+    def head_config(self) -> XH.HeadConfig:
+        return XH.HeadConfig(num_heads=self.num_heads, xattn_head=self.xattn_head,
+                             use_prior=self.emotion_prior_bias is not None, attn_dropout=self.attn_dropout,
+                             drop_path=self.v_drop_path.drop_prob, mlp_dropout=0.2,
+                             prior_dropout=(self.emotion_prior_bias.dropout if self.emotion_prior_bias is not None else 0.0),
+                             temporal_pooling=self.temporal_pooling)
+
+    def head_params(self):
+        names, params = [], []
+        for n, q in self.named_parameters():
+            if n.startswith(("audio_model.", "video_model.")):
+                continue
+            names.append(n)
+            params.append(q)
+        return tuple(names), params
+
+    def xattn_from_features(self, v_feat: torch.Tensor, a_seq: torch.Tensor) -> torch.Tensor:
+        """xattn head on encoder features: v_feat [B,T,v_dim] (backbone output), a_seq [B,Ta,seq_dim]."""
+        _require_device(v_feat, a_seq)
+        names, params = self.head_params()
+        return _XattnHeadFn.apply(v_feat.contiguous(), a_seq.contiguous(), self.head_config(), self.training,
+                                  _next_seed() if self.training else 0, names, *params)
+
+    def forward(self, video: torch.Tensor, audio: torch.Tensor):
+        self.alignment_loss = None
+        _require_device(video, audio)
+        if self.mode == "late":
+            a_logits = self.audio_model(audio)
+            v_logits = self.video_model(video)
+            return EH.late_probs(a_logits, v_logits)
+
+        if self.mode in {"xattn", "xattn_concat", "xattn_gated"}:
+            b, t, c, h, w = video.shape
+            v_in = video.view(b * t, c, h, w)
+            v_feat = self.video_model.backbone(v_in).view(b, t, self.v_dim)
+            if hasattr(self.audio_model, "encode_sequence"):
+                a_seq = self.audio_model.encode_sequence(audio)
+            else:
+                raise NotImplementedError("mel AudioNet fallback (fusion.py:379-384) is out of scope: the north-star "
+                                          "path is WavLM encode_sequence")
+            return self.xattn_from_features(v_feat, a_seq)
+
+        if self.mode not in {"concat", "gated"}:
+            raise ValueError(f"Unknown fusion mode: {self.mode}")
+        a_emb = self.audio_model.encode(audio)
+        v_emb = self.video_model.encode(video)
+        if self.semantic_alignment is not None:
+            raise NotImplementedError("fusion_align_mode='clip' is not on the north-star path")
+        drop_a, drop_v = self.modality_dropout.draw() if self.mode == "gated" else (False, False)
+        return EH.embedding_head(self, a_emb, v_emb, drop_a, drop_v)

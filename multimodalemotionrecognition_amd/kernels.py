@@ -1,0 +1,210 @@
+"""Thin tensor-level wrappers over the C-ABI (``include/mer.h``).
+
+PyTorch is plumbing here: it owns device memory (caching allocator) and the current
+HIP stream; every byte of math runs in ``libmer_hip.so``.  Wrappers validate shapes
+and dtypes on the host before launching (a mis-sized launch is a GPU fault, not an
+exception), then pass raw pointers and the current stream.
+"""
+from __future__ import annotations
+
+import torch
+
+from ._lib import LIB
+
+F32, BF16 = 0, 1
+ACT = {"none": 0, "relu": 1, "gelu": 2}
+
+
+def stream_ptr() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _dt(t: torch.Tensor) -> int:
+    if t.dtype == torch.float32:
+        return F32
+    if t.dtype == torch.bfloat16:
+        return BF16
+    raise TypeError(f"unsupported dtype {t.dtype}")
+
+
+def _ptr(t):
+    return 0 if t is None else t.data_ptr()
+
+
+def _check_dev(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError("MI355X kernels need device tensors (HIP); got a CPU tensor")
+
+
+def gemm(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, trans_a: bool = False, trans_b: bool = False,
+         bias=None, beta: int = 0, act: str = "none", splitk: int = 1) -> torch.Tensor:
+    """out[M,N] (+)= op(a) @ op(b) (+ bias) on the fp32 MFMA GEMM.
+
+    ``a`` is [M,K] (or [K,M] with trans_a), ``b`` is [K,N] (or [N,K] with trans_b); both may be
+    strided 2-D views with one unit stride.  ``out`` is fp32 [M,N] with unit column stride.
+    """
+    _check_dev(a, b, out, bias)
+    if trans_a:
+        K, M = a.shape
+        sam, sak = a.stride(1), a.stride(0)
+    else:
+        M, K = a.shape
+        sam, sak = a.stride(0), a.stride(1)
+    if trans_b:
+        N, K2 = b.shape
+        sbk, sbn = b.stride(1), b.stride(0)
+    else:
+        K2, N = b.shape
+        sbk, sbn = b.stride(0), b.stride(1)
+    if K != K2 or tuple(out.shape) != (M, N) or out.stride(1) != 1 or out.dtype != torch.float32:
+        raise ValueError(f"gemm shape mismatch: a{tuple(a.shape)} b{tuple(b.shape)} out{tuple(out.shape)}")
+    if bias is not None and (bias.numel() != N or not bias.is_contiguous()):
+        raise ValueError("bias must be contiguous [N]")
+    if splitk > 1:
+        splitk = max(1, min(splitk, (K + 255) // 256))
+    LIB("mer_gemm_f32", M, N, K, a.data_ptr(), _dt(a), sam, sak, 0, b.data_ptr(), _dt(b), sbk, sbn, 0,
+        out.data_ptr(), out.stride(0), 0, _ptr(bias), int(beta), ACT[act], int(splitk), 1, stream_ptr())
+    return out
+
+
+def auto_splitk(M: int, N: int, K: int) -> int:
+    tiles = ((M + 63) // 64) * ((N + 63) // 64)
+    if tiles >= 128 or K < 1024:
+        return 1
+    return int(max(1, min(32, 256 // tiles, K // 512)))
+
+
+def linear_fwd(x2d, w, b, out, act="none"):
+    """nn.Linear: out = x W^T + b."""
+    return gemm(x2d, w, out, trans_b=True, bias=b, act=act)
+
+
+def linear_bwd(x2d, w, dy, dx=None, dw=None, db=None, dx_beta=0):
+    """Given dy [M,N] for out = x W^T + b: dx (+)= dy W ; dw += dy^T x ; db += colsum(dy).
+
+    dw / db must be initialised (they are accumulated: split-K adds atomically).
+    """
+    M, N = dy.shape
+    K = x2d.shape[1]
+    if dx is not None:
+        gemm(dy, w, dx, beta=dx_beta)
+    if dw is not None:
+        gemm(dy, x2d, dw, trans_a=True, beta=1, splitk=auto_splitk(N, K, M))
+    if db is not None:
+        colsum(dy, db)
+
+
+def colsum(x2d, out):
+    _check_dev(x2d, out)
+    LIB("mer_colsum_f32", x2d.shape[0], x2d.shape[1], x2d.data_ptr(), x2d.stride(0), out.data_ptr(), stream_ptr())
+
+
+def mha_fwd(q, k, v, bias, out, P, B, H, Lq, Lk, drop_p=0.0, seed=0):
+    d = out.shape[-1]
+    dh = d // H
+    LIB("mer_mha_fwd", B, H, Lq, Lk, dh, q.data_ptr(), q.stride(0), k.data_ptr(), k.stride(0), v.data_ptr(),
+        v.stride(0), _ptr(bias), out.data_ptr(), out.stride(0), P.data_ptr(), float(dh ** -0.5), float(drop_p),
+        int(seed), stream_ptr())
+
+
+def mha_bwd(q, k, v, P, dout, dq, dk, dv, dbias, B, H, Lq, Lk, drop_p=0.0, seed=0):
+    d = dout.shape[-1]
+    dh = d // H
+    LIB("mer_mha_bwd", B, H, Lq, Lk, dh, q.data_ptr(), q.stride(0), k.data_ptr(), k.stride(0), v.data_ptr(),
+        v.stride(0), P.data_ptr(), dout.data_ptr(), dout.stride(0), dq.data_ptr(), dq.stride(0), dk.data_ptr(),
+        dk.stride(0), dv.data_ptr(), dv.stride(0), _ptr(dbias), float(dh ** -0.5), float(drop_p), int(seed),
+        stream_ptr())
+
+
+def add_ln_fwd(x, r, gamma, beta, y, s_out, mean, rstd, rows_per_sample, dp_p=0.0, seed=0, eps=1e-5):
+    rows, d = x.shape
+    LIB("mer_add_ln_fwd", rows, d, rows_per_sample, x.data_ptr(), _ptr(r), float(dp_p), int(seed),
+        gamma.data_ptr(), beta.data_ptr(), float(eps), y.data_ptr(), _ptr(s_out), _ptr(mean), _ptr(rstd),
+        stream_ptr())
+
+
+def add_ln_bwd(dy, s, mean, rstd, gamma, dx, dr, dgamma, dbeta, rows_per_sample, dp_p=0.0, seed=0):
+    rows, d = dy.shape
+    LIB("mer_add_ln_bwd", rows, d, rows_per_sample, dy.data_ptr(), s.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
+        gamma.data_ptr(), float(dp_p), int(seed), dx.data_ptr(), _ptr(dr), _ptr(dgamma), _ptr(dbeta), stream_ptr())
+
+
+def mean_pool_fwd(x3d, y, ldy=None):
+    B, L, D = x3d.shape
+    LIB("mer_mean_pool_fwd", B, L, D, x3d.data_ptr(), y.data_ptr(), int(ldy if ldy is not None else y.stride(0)),
+        stream_ptr())
+
+
+def mean_pool_bwd(dy, dx3d, accumulate=False):
+    B, L, D = dx3d.shape
+    LIB("mer_mean_pool_bwd", B, L, D, dy.data_ptr(), dy.stride(0), dx3d.data_ptr(), int(accumulate), stream_ptr())
+
+
+def cross_entropy(logits, labels, loss, dlogits, label_smoothing=0.0, late=False):
+    B, C = logits.shape
+    if labels.dtype != torch.int64 or labels.numel() != B:
+        raise ValueError("labels must be int64 [B]")
+    LIB("mer_cross_entropy", B, C, logits.data_ptr(), labels.data_ptr(), float(label_smoothing), int(late),
+        loss.data_ptr(), _ptr(dlogits), stream_ptr())
+
+
+def scale_dev(x, s, y):
+    LIB("mer_scale_dev", x.numel(), x.data_ptr(), s.data_ptr(), y.data_ptr(), stream_ptr())
+
+
+def dropout_(x2d, p, seed):
+    if p > 0:
+        LIB("mer_dropout_inplace", x2d.shape[0], x2d.shape[1], x2d.data_ptr(), x2d.stride(0), float(p), int(seed),
+            stream_ptr())
+
+
+def relu_dropout_bwd_(dy, y, p, seed):
+    LIB("mer_relu_dropout_bwd", dy.shape[0], dy.shape[1], dy.data_ptr(), dy.stride(0), y.data_ptr(), y.stride(0),
+        float(p), int(seed), stream_ptr())
+
+
+def gate_mix_fwd(z, v, a, out, g):
+    B, D = out.shape
+    LIB("mer_gate_mix_fwd", B, D, z.data_ptr(), v.data_ptr(), v.stride(0), a.data_ptr(), a.stride(0),
+        out.data_ptr(), g.data_ptr(), stream_ptr())
+
+
+def gate_mix_bwd(g, v, a, dout, dz, dv, da):
+    B, D = dout.shape
+    LIB("mer_gate_mix_bwd", B, D, g.data_ptr(), v.data_ptr(), v.stride(0), a.data_ptr(), a.stride(0),
+        dout.data_ptr(), dz.data_ptr(), dv.data_ptr(), dv.stride(0), da.data_ptr(), da.stride(0), stream_ptr())
+
+
+def token_bias_fwd(qt, qp, kt, kp, scale, out):
+    B, Lq, Lk = out.shape
+    LIB("mer_token_bias_fwd", B, Lq, Lk, qt.data_ptr(), qp.data_ptr(), kt.data_ptr(), kp.data_ptr(),
+        scale.data_ptr(), out.data_ptr(), stream_ptr())
+
+
+def token_bias_bwd(qt, qp, kt, kp, scale, dbias, dqt, dkt, dqp, dkp, dscale_part):
+    B, Lq, Lk = dbias.shape
+    LIB("mer_token_bias_bwd", B, Lq, Lk, qt.data_ptr(), qp.data_ptr(), kt.data_ptr(), kp.data_ptr(),
+        scale.data_ptr(), dbias.data_ptr(), dqt.data_ptr(), dkt.data_ptr(), dqp.data_ptr(), dkp.data_ptr(),
+        dscale_part.data_ptr(), stream_ptr())
+
+
+def vec_sum(x, out, accumulate=False):
+    LIB("mer_vec_sum", x.numel(), x.data_ptr(), out.data_ptr(), int(accumulate), stream_ptr())
+
+
+def adam_step(p, g, m, v, lr, b1, b2, eps, wd, step):
+    LIB("mer_adam_step", p.numel(), p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), float(lr), float(b1),
+        float(b2), float(eps), float(wd), int(step), stream_ptr())
+
+
+def softmax_avg_fwd(za, zv, out, pa, pv):
+    B, C = za.shape
+    LIB("mer_softmax_avg_fwd", B, C, za.data_ptr(), zv.data_ptr(), out.data_ptr(), pa.data_ptr(), pv.data_ptr(),
+        stream_ptr())
+
+
+def softmax_avg_bwd(pa, pv, dout, da, dv):
+    B, C = pa.shape
+    LIB("mer_softmax_avg_bwd", B, C, pa.data_ptr(), pv.data_ptr(), dout.data_ptr(), da.data_ptr(), dv.data_ptr(),
+        stream_ptr())

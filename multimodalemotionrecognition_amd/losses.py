@@ -1,0 +1,43 @@
+"""Loss modules of the train step (``src/train.py:1030-1033`` and ``212-225``) on the HIP kernels."""
+from __future__ import annotations
+
+import torch
+from torch import nn
+
+from . import kernels as K
+
+
+class _CEFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, labels, label_smoothing, late):
+        logits = logits.contiguous().float()
+        loss = torch.empty((), device=logits.device, dtype=torch.float32)
+        dlogits = torch.empty_like(logits)
+        K.cross_entropy(logits, labels.contiguous(), loss, dlogits, label_smoothing, late)
+        ctx.save_for_backward(dlogits)
+        return loss
+
+    @staticmethod
+    def backward(ctx, gloss):
+        (dlogits,) = ctx.saved_tensors
+        out = torch.empty_like(dlogits)
+        K.scale_dev(dlogits, gloss.contiguous().float().reshape(1), out)
+        return out, None, None, None
+
+
+class CrossEntropyLoss(nn.Module):
+    """``nn.CrossEntropyLoss(label_smoothing=...)`` with mean reduction (train.py:1033)."""
+
+    def __init__(self, label_smoothing: float = 0.0) -> None:
+        super().__init__()
+        self.label_smoothing = float(label_smoothing)
+
+    def forward(self, logits: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
+        return _CEFn.apply(logits, labels, self.label_smoothing, False)
+
+
+class LateNLLLoss(nn.Module):
+    """late-mode loss ``NLLLoss()(log(probs + 1e-8), labels)`` (train.py:1031, 212-214), given probabilities."""
+
+    def forward(self, probs: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
+        return _CEFn.apply(probs, labels, 0.0, True)

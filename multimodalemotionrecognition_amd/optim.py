@@ -1,0 +1,89 @@
+"""FusedAdam: ``torch.optim.Adam`` semantics (train.py:872,902) as ONE HIP kernel per contiguous run.
+
+Each param group's parameters are re-homed into one flat fp32 buffer (``p.data`` becomes a
+16-byte-aligned view), with a matching flat gradient buffer whose views the backward kernels
+write into directly (``fusion.grad_buffer``), and flat ``exp_avg`` / ``exp_avg_sq`` state.
+The flat gradient buffer is also what the data-parallel all-reduce ships (one bucket per
+region, see ``dist.py``).  Like torch's Adam, parameters whose ``.grad`` is None are skipped
+(no moment decay, no weight decay): the kernel runs over maximal runs of params that have grads.
+"""
+from __future__ import annotations
+
+from typing import List
+
+import torch
+
+from . import kernels as K
+
+
+def _align4(n: int) -> int:
+    return (n + 3) // 4 * 4
+
+
+class FusedAdam(torch.optim.Optimizer):
+    def __init__(self, params, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0):
+        defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay)
+        super().__init__(params, defaults)
+        self._flat = []
+        for group in self.param_groups:
+            ps: List[torch.Tensor] = group["params"]
+            if not ps:
+                self._flat.append(None)
+                continue
+            dev = ps[0].device
+            offs, total = [], 0
+            for p in ps:
+                if p.dtype != torch.float32:
+                    raise TypeError("FusedAdam keeps fp32 master weights")
+                offs.append(total)
+                total += _align4(p.numel())
+            flat = torch.zeros(total, device=dev, dtype=torch.float32)
+            gflat = torch.zeros(total, device=dev, dtype=torch.float32)
+            with torch.no_grad():
+                for p, o in zip(ps, offs):
+                    flat[o:o + p.numel()].copy_(p.detach().reshape(-1))
+                    p.data = flat[o:o + p.numel()].view_as(p)
+                    p._mer_grad_view = gflat[o:o + p.numel()].view_as(p)
+            self._flat.append(dict(flat=flat, gflat=gflat, m=torch.zeros_like(flat), v=torch.zeros_like(flat),
+                                   offs=offs, step=0))
+
+    def flat_grads(self):
+        return [f["gflat"] for f in self._flat if f is not None]
+
+    def zero_grad(self, set_to_none: bool = True) -> None:
+        for f, group in zip(self._flat, self.param_groups):
+            if f is None:
+                continue
+            f["gflat"].zero_()
+            for p in group["params"]:
+                p.grad = None
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = closure() if closure is not None else None
+        for f, group in zip(self._flat, self.param_groups):
+            if f is None:
+                continue
+            ps = group["params"]
+            runs, cur = [], None
+            for p, o in zip(ps, f["offs"]):
+                has = p.grad is not None
+                if has and p.grad.data_ptr() != p._mer_grad_view.data_ptr():
+                    p._mer_grad_view.copy_(p.grad)  # grad produced outside our kernels: bring it home
+                if has:
+                    end = o + _align4(p.numel())
+                    if cur is not None and cur[1] == o:
+                        cur[1] = end
+                    else:
+                        cur = [o, end]
+                        runs.append(cur)
+                else:
+                    cur = None
+            if not runs:
+                continue
+            f["step"] += 1
+            b1, b2 = group["betas"]
+            for s, e in runs:
+                K.adam_step(f["flat"][s:e], f["gflat"][s:e], f["m"][s:e], f["v"][s:e], group["lr"], b1, b2,
+                            group["eps"], group["weight_decay"], f["step"])
+        return loss

@@ -1,0 +1,60 @@
+"""Builders shared by the GPU parity tests and smoke(): product models fed with oracle weights."""
+from __future__ import annotations
+
+import numpy as np
+import torch
+from torch import nn
+
+from oracle import fusion_ref, params
+
+
+class IdentityBackbone(nn.Module):
+    """Test stub like the reference's _DummyBackbone (test_attention_integration.py:26-34): feature-level input."""
+
+    def forward(self, x):
+        return x
+
+
+class StubVideo(nn.Module):
+    def __init__(self, dim=512):
+        super().__init__()
+        self.embedding_dim = dim
+        self.backbone = IdentityBackbone()
+
+
+class StubAudio(nn.Module):
+    def __init__(self, dim=768):
+        super().__init__()
+        self.sequence_dim = dim
+        self.embedding_dim = dim
+
+    def encode_sequence(self, x):
+        return x
+
+
+def head_model(xattn_head="concat", use_prior=False, d_model=128, heads=4, v_dim=512, seq_dim=768, device="cuda"):
+    from multimodalemotionrecognition_amd.fusion import FusionModel
+
+    m = FusionModel(StubAudio(seq_dim), StubVideo(v_dim), num_classes=8, mode="xattn", xattn_head=xattn_head,
+                    d_model=d_model, num_heads=heads, audio_n_mels=768, xattn_use_emotion_prior=use_prior)
+    sd = m.state_dict()
+    new = {k: torch.from_numpy(params.init_tensor(k, tuple(v.shape), 0)) for k, v in sd.items()}
+    fusion_ref.gated_bias_init(new, xattn_head)
+    m.load_state_dict(new)
+    return m.to(device)
+
+
+def oracle_head_params(xattn_head="concat", use_prior=False, **kw):
+    p = {k: torch.from_numpy(v) for k, v in
+         params.init_state(fusion_ref.xattn_head_param_shapes(xattn_head=xattn_head, use_prior=use_prior, **kw)).items()}
+    fusion_ref.gated_bias_init(p, xattn_head)
+    return p
+
+
+def feats(batch, t, ta, v_dim=512, a_dim=768, seed=20261015, device="cuda"):
+    v, a = params.feature_inputs(batch, t, ta, v_dim, a_dim, seed)
+    return torch.from_numpy(v).to(device), torch.from_numpy(a).to(device)
+
+
+def max_abs(a, b):
+    return float((a.detach().float().cpu() - torch.as_tensor(b).float()).abs().max())

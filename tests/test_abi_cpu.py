@@ -1,0 +1,71 @@
+"""CPU-side checks: the C-ABI library builds, loads and exports every symbol of include/mer.h;
+host mirrors of the reference API keep its names; the product path refuses CPU tensors."""
+import subprocess
+from pathlib import Path
+
+import numpy as np
+import pytest
+import torch
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def _ensure_built():
+    from multimodalemotionrecognition_amd import lib_path
+    if not lib_path().exists():
+        subprocess.run(["make", "-C", str(ROOT / "multimodalemotionrecognition_amd" / "csrc"), "-j8"], check=True)
+
+
+def test_library_exports_every_header_symbol():
+    _ensure_built()
+    import ctypes
+    from multimodalemotionrecognition_amd._lib import LIB, lib_path, parse_header
+
+    sigs = parse_header()
+    assert len(sigs) >= 20
+    dll = ctypes.CDLL(str(lib_path()))
+    for name in sigs:
+        assert hasattr(dll, name), f"{name} declared in include/mer.h but not exported"
+    assert sorted(LIB.symbols()) == sorted(sigs)
+
+
+def test_hip_sources_include_the_header():
+    for src in (ROOT / "multimodalemotionrecognition_amd" / "csrc").glob("*.hip"):
+        assert '#include "mer.h"' in src.read_text(), src.name
+
+
+def test_fusion_state_dict_names_match_reference_listing():
+    from multimodalemotionrecognition_amd.fusion import FusionModel
+    from oracle import fusion_ref
+    from tests.gpu_helpers import StubAudio, StubVideo
+
+    for head in ("concat", "gated"):
+        for prior in (False, True):
+            m = FusionModel(StubAudio(), StubVideo(), num_classes=8, mode="xattn", xattn_head=head,
+                            audio_n_mels=768, xattn_use_emotion_prior=prior)
+            got = [(k, tuple(v.shape)) for k, v in m.state_dict().items()]
+            assert got == fusion_ref.xattn_head_param_shapes(xattn_head=head, use_prior=prior)
+    g = np.load(ROOT / "tests" / "golden" / "c4_gated.npz")
+    m = FusionModel(StubAudio(), StubVideo(), num_classes=8, mode="gated")
+    ref = sorted(str(n) for n in g["names"] if not str(n).startswith(("audio_model", "video_model")))
+    assert sorted(m.state_dict()) == ref
+    # gated bias init quirk (fusion.py:329-336): both Linear biases are -1
+    assert torch.all(m.gate[0].bias == -1) and torch.all(m.gate[3].bias == -1)
+
+
+def test_product_path_refuses_cpu():
+    from multimodalemotionrecognition_amd.fusion import FusionModel
+    from tests.gpu_helpers import StubAudio, StubVideo
+
+    m = FusionModel(StubAudio(), StubVideo(), num_classes=8, mode="xattn", audio_n_mels=768)
+    with pytest.raises(RuntimeError):
+        m(torch.zeros(2, 8, 512, 1, 1), torch.zeros(2, 64, 768))
+
+
+def test_unknown_mode_raises():
+    from multimodalemotionrecognition_amd.fusion import FusionModel
+    from tests.gpu_helpers import StubAudio, StubVideo
+
+    m = FusionModel(StubAudio(), StubVideo(), num_classes=8, mode="bogus")
+    with pytest.raises((ValueError, RuntimeError)):
+        m(torch.zeros(2, 8, 512, 1, 1), torch.zeros(2, 64, 768))
