@@ -6,7 +6,7 @@
  * src/train.py:200-228, src/optimized_runtime.py:99-108).  The reference is pure Python over
  * torch / torchvision / transformers; every entry point below replaces the device math of one
  * of its call sites, cited per function.  The Python host layer
- * (multimodalemotionrecognition_amd/*.py) binds these through ctypes.
+ * (multimodalemotionrecognition_amd/ *.py) binds these through ctypes.
  *
  * Conventions (every function):
  *   - returns 0 on success or a hipError_t value (e.g. 1 = hipErrorInvalidValue on bad shapes);
@@ -112,6 +112,53 @@ int mer_vec_sum(int n, const float* x, float* out, int accumulate, void* stream)
  * buffer; `step` is the 1-based step count used for bias correction.  16-byte aligned buffers. */
 int mer_adam_step(long n, float* p, const float* g, float* m, float* v, float lr, float b1, float b2, float eps,
                   float wd, int step, void* stream);
+
+/* ============================ encoders (bf16 MFMA) ============================ */
+
+/* C[m,n] = act(sum_k A(m,k) W[n,k] + bias[n]) (+ R[m,n]), bf16 operands, fp32 accumulate, C bf16 (c_dtype=1)
+ * or fp32 (0).  Row m of A starts at A + (m / a_rpg)*a_gstride + (m % a_rpg)*a_rstride (K contiguous):
+ * a_rpg = M, a_rstride = lda is a plain GEMM (WavLM projections/FFN, TF:108-296); a_rpg = L_out,
+ * a_rstride = stride*C_in, a_gstride = L_in*C_in is a channel-last Conv1d (WavLM conv1-6, TF:675-745).
+ * W is [N][K] (ldw).  K, strides multiple of 8; A, W 16-byte aligned.  bias / R may be NULL. */
+int mer_gemm_bf16(int M, int N, int K, const void* A, long a_gstride, long a_rstride, int a_rpg, const void* W,
+                  long ldw, void* C, int c_dtype, long ldc, const float* bias, const void* R, long ldr, int act,
+                  void* stream);
+
+/* Grouped positional Conv1d of WavLM (TF:48-90): out[b,t,g*Cg+n] = act(sum_{tap,c} X[b,t+tap-pad,g*Cg+c]
+ * Wp[g][n][tap][c] + bias) (+ R), rows t in [0, L) (the SamePad crop).  Wp is the weight-normed, bf16
+ * repacked kernel (mer_weightnorm_scale + mer_permute3_bf16). */
+int mer_posconv_gemm_bf16(int B, int L, int C_total, int groups, int taps, int pad, const void* X, long ldx,
+                          const void* Wp, void* out, int out_dtype, long ldo, const float* bias, const void* R,
+                          long ldr, int act, void* stream);
+
+/* WavLM feature-extractor conv0 (TF:723-745): Conv1d(1,512,k=10,s=5) of wav [B,S] fp32 -> bf16 [B,Lout,512],
+ * plus GroupNorm statistics stats[b][c] = (sum, sum of squares) accumulated (pre-zero stats). */
+int mer_wavlm_conv0(int B, int S, int Lout, const float* wav, const float* w0, void* out, float* stats, void* stream);
+
+/* GroupNorm(C, C) apply + GELU from those statistics (bf16 in/out, channel-last [B,L,C]). */
+int mer_groupnorm_gelu(int B, int L, int C, const void* x, const float* stats, const float* gamma, const float* beta,
+                       float eps, void* y, void* stream);
+
+/* Row LayerNorm (nn.LayerNorm(d), TF:93-105, 314-336, 418): x (x_dtype) -> y (y_dtype), d <= 1024. */
+int mer_layernorm(int rows, int d, const void* x, int x_dtype, long ldx, const float* gamma, const float* beta,
+                  float eps, void* y, int y_dtype, long ldy, void* stream);
+
+/* WavLM self-attention with gated relative position bias (TF:147-271), one workgroup per (b,h):
+ * qkv bf16 [B*L, 3*H*64] (q|k|v), x bf16 layer input (gate source), gate_w [8][64], gate_b [8],
+ * gate_const [H], rel_emb [320][H], bucket int32 [2L-1] (bucket of relative position j-i), out bf16. L <= 256. */
+int mer_wavlm_attention(int B, int L, int H, const void* qkv, long ldqkv, const void* x, long ldx, const float* gate_w,
+                        const float* gate_b, const float* gate_const, const float* rel_emb, const int* bucket,
+                        void* out, long ldo, float scale, void* stream);
+
+/* dst[i0][i1][i2] = bf16(src[i0*s0 + i1*s1 + i2*s2] * (scale ? scale[i1] : 1))  (weight repacking). */
+int mer_permute3_bf16(int n0, int n1, int n2, const float* src, long s0, long s1, long s2, const float* scale,
+                      void* dst, void* stream);
+
+/* weight_norm(dim=2) factors of the positional conv: scale[k] = g[k] / ||v[:,:,k]||_2, v [n01][taps]. */
+int mer_weightnorm_scale(int n01, int taps, const float* v, const float* g, float* scale, void* stream);
+
+/* y = bf16(x), contiguous. */
+int mer_cast_bf16(long n, const float* x, void* y, void* stream);
 
 #ifdef __cplusplus
 }

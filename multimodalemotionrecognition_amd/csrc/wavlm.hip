@@ -1,0 +1,369 @@
+// WavLM-base forward kernels (frozen encoder of the north-star path, wavlm_audio.py:165-183).
+// Citations TF:<line> are transformers' modeling_wavlm.py (installed 5.15.0).
+#include "common.h"
+#include "mer.h"
+
+typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;
+
+// ---------------------------------------------------------------------------------------
+// conv0 of the feature extractor (TF:723-745): Conv1d(1, 512, k=10, s=5, bias=False) on the raw
+// waveform, channel-last bf16 output [B, Lout, 512], fused with the GroupNorm(512, 512) statistics
+// (per (b, c) sum and sum of squares over time, fp32 atomics into stats[b][c][2], pre-zeroed).
+// Bandwidth-bound direct conv: one block = 32 output steps of one clip, 2 channels per thread.
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void wavlm_conv0_kernel(int S, int Lout, const float* __restrict__ wav,
+                                                          const float* __restrict__ w, bf16_t* __restrict__ out,
+                                                          float* __restrict__ stats) {
+  constexpr int TS = 32, KW = 10, ST = 5;
+  __shared__ float xs[TS * ST + KW];
+  const int b = blockIdx.y, t0 = blockIdx.x * TS;
+  const float* x = wav + (long)b * S;
+  for (int i = threadIdx.x; i < TS * ST + KW; i += 256) {
+    const long si = (long)t0 * ST + i;
+    xs[i] = si < S ? x[si] : 0.f;
+  }
+  float wr[2][KW];
+  const int c0 = threadIdx.x, c1 = threadIdx.x + 256;
+#pragma unroll
+  for (int k = 0; k < KW; ++k) { wr[0][k] = w[c0 * KW + k]; wr[1][k] = w[c1 * KW + k]; }
+  __syncthreads();
+  float s0 = 0.f, q0 = 0.f, s1 = 0.f, q1 = 0.f;
+  const int tn = min(TS, Lout - t0);
+  for (int tt = 0; tt < tn; ++tt) {
+    float a0 = 0.f, a1 = 0.f;
+#pragma unroll
+    for (int k = 0; k < KW; ++k) {
+      const float xv = xs[tt * ST + k];
+      a0 += wr[0][k] * xv;
+      a1 += wr[1][k] * xv;
+    }
+    const bf16_t h0 = f2bf(a0), h1 = f2bf(a1);
+    bf16_t* o = out + ((long)b * Lout + t0 + tt) * 512;
+    o[c0] = h0;
+    o[c1] = h1;
+    // statistics of the values GroupNorm will actually see (the bf16-rounded activations)
+    const float r0 = bf2f(h0), r1 = bf2f(h1);
+    s0 += r0; q0 += r0 * r0; s1 += r1; q1 += r1 * r1;
+  }
+  float* st = stats + (long)b * 512 * 2;
+  atomicAdd(st + c0 * 2, s0);
+  atomicAdd(st + c0 * 2 + 1, q0);
+  atomicAdd(st + c1 * 2, s1);
+  atomicAdd(st + c1 * 2 + 1, q1);
+}
+
+MER_API int mer_wavlm_conv0(int B, int S, int Lout, const float* wav, const float* w0, void* out, float* stats,
+                            void* stream) {
+  if (Lout != (S - 10) / 5 + 1) return (int)hipErrorInvalidValue;
+  dim3 grid((Lout + 31) / 32, B);
+  hipLaunchKernelGGL(wavlm_conv0_kernel, grid, dim3(256), 0, (hipStream_t)stream, S, Lout, wav, w0, (bf16_t*)out, stats);
+  MER_LAUNCH_CHECK();
+}
+
+// GroupNorm(C, C) apply + GELU (TF:740-745): y = gelu((x - mu_bc) * rstd_bc * gamma_c + beta_c), bf16 in/out,
+// 8 channels (16 B) per thread.
+__global__ __launch_bounds__(256) void gn_gelu_kernel(int B, int L, int C, const bf16_t* __restrict__ x,
+                                                      const float* __restrict__ stats, const float* __restrict__ gamma,
+                                                      const float* __restrict__ beta, float eps, bf16_t* __restrict__ y) {
+  const long nvec = (long)B * L * C / 8;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < nvec; e += (long)gridDim.x * blockDim.x) {
+    const long base = e * 8;
+    const int c0 = base % C;
+    const int b = base / ((long)L * C);
+    u32x4 v = *reinterpret_cast<const u32x4*>(x + base);
+    const bf16_t* hv = reinterpret_cast<const bf16_t*>(&v);
+    u32x4 o;
+    bf16_t* ho = reinterpret_cast<bf16_t*>(&o);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int c = c0 + i;
+      const float mu = stats[((long)b * C + c) * 2] / L;
+      const float var = fmaxf(stats[((long)b * C + c) * 2 + 1] / L - mu * mu, 0.f);
+      const float xn = (bf2f(hv[i]) - mu) * rsqrtf(var + eps) * gamma[c] + beta[c];
+      ho[i] = f2bf(gelu_erf(xn));
+    }
+    *reinterpret_cast<u32x4*>(y + base) = o;
+  }
+}
+
+MER_API int mer_groupnorm_gelu(int B, int L, int C, const void* x, const float* stats, const float* gamma,
+                               const float* beta, float eps, void* y, void* stream) {
+  if (C % 8) return (int)hipErrorInvalidValue;
+  const long nvec = (long)B * L * C / 8;
+  const int grid = (int)((nvec + 255) / 256 < 8192 ? (nvec + 255) / 256 : 8192);
+  hipLaunchKernelGGL(gn_gelu_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, B, L, C, (const bf16_t*)x, stats,
+                     gamma, beta, eps, (bf16_t*)y);
+  MER_LAUNCH_CHECK();
+}
+
+// ---------------------------------------------------------------------------------------
+// Row LayerNorm (feature projection TF:93-105, encoder LN TF:418, post-LN layers TF:314-336).
+// x fp32 or bf16 [rows, d] (ldx), y bf16 or fp32 [rows, d] (ldy).  One wave per row.
+// ---------------------------------------------------------------------------------------
+template <typename TI, typename TO>
+__global__ __launch_bounds__(256) void layernorm_kernel(int rows, int d, const TI* __restrict__ x, long ldx,
+                                                        const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                        float eps, TO* __restrict__ y, long ldy) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const TI* xr = x + (long)row * ldx;
+  float vals[16];  // d <= 1024
+  float s = 0.f;
+  int n = 0;
+  for (int c = lane; c < d; c += 64, ++n) {
+    vals[n] = ldf<TI>(xr, c);
+    s += vals[n];
+  }
+  const float mean = wave_sum(s) / d;
+  float q = 0.f;
+  for (int i = 0; i < n; ++i) { const float v = vals[i] - mean; q += v * v; }
+  const float rstd = rsqrtf(wave_sum(q) / d + eps);
+  n = 0;
+  for (int c = lane; c < d; c += 64, ++n) stf<TO>(y + (long)row * ldy, c, (vals[n] - mean) * rstd * gamma[c] + beta[c]);
+}
+
+MER_API int mer_layernorm(int rows, int d, const void* x, int x_dtype, long ldx, const float* gamma,
+                          const float* beta, float eps, void* y, int y_dtype, long ldy, void* stream) {
+  if (d > 1024 || rows <= 0) return rows <= 0 ? 0 : (int)hipErrorInvalidValue;
+  dim3 grid((rows + 3) / 4);
+  hipStream_t st = (hipStream_t)stream;
+#define L(TI, TO) hipLaunchKernelGGL((layernorm_kernel<TI, TO>), grid, dim3(256), 0, st, rows, d, (const TI*)x, ldx, gamma, beta, eps, (TO*)y, ldy)
+  if (x_dtype == MER_F32 && y_dtype == MER_BF16) L(float, bf16_t);
+  else if (x_dtype == MER_BF16 && y_dtype == MER_BF16) L(bf16_t, bf16_t);
+  else if (x_dtype == MER_F32 && y_dtype == MER_F32) L(float, float);
+  else L(bf16_t, float);
+#undef L
+  MER_LAUNCH_CHECK();
+}
+
+// ---------------------------------------------------------------------------------------
+// Self-attention with WavLM's gated relative position bias (TF:147-241), one workgroup per (b, h):
+//   gate_i = sigmoid(a_i) * (sigmoid(b_i) * const_h - 1) + 2,  (a_i, b_i) = pair-sums of
+//            gru_rel_pos_linear(x_i[h*dh:(h+1)*dh])                          (TF:163-177)
+//   S_ij   = scale * q_i.k_j + gate_i * emb[bucket(j - i), h]                 (TF:243-271)
+//   O_i    = softmax_j(S_i) V
+// Q/K/V come from one fused projection [B*L, 3*768] (q | k | v).  L <= 256, dh = 64.
+// QK^T and PV on v_mfma_f32_16x16x32_bf16; softmax in fp32 with wave shuffles.
+// ---------------------------------------------------------------------------------------
+namespace {
+constexpr int ADH = 64, APAD = ADH + 8;
+}
+
+__global__ __launch_bounds__(256) void wavlm_attn_kernel(int L, int H, const bf16_t* __restrict__ qkv, long ldqkv,
+                                                         const bf16_t* __restrict__ x, long ldx,
+                                                         const float* __restrict__ gw, const float* __restrict__ gb,
+                                                         const float* __restrict__ gconst,
+                                                         const float* __restrict__ rel_emb,
+                                                         const int* __restrict__ bucket, bf16_t* __restrict__ out,
+                                                         long ldo, float scale) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  const int LP = (L + 15) / 16 * 16;
+  const int VTP = LP + 8;
+  bf16_t* Qs = reinterpret_cast<bf16_t*>(smem_raw);   // [LP][APAD]
+  bf16_t* Ks = Qs + LP * APAD;                        // [LP][APAD]
+  bf16_t* Vt = Ks + LP * APAD;                        // [ADH][VTP]
+  bf16_t* Ps = Vt + ADH * VTP;                        // [4][16][VTP]
+  float* gate = reinterpret_cast<float*>(Ps + 4 * 16 * VTP);  // [LP]
+  float* tbl = gate + LP;                              // [2L-1]
+  const int b = blockIdx.x / H, h = blockIdx.x % H;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int D = H * ADH;
+
+  // stage Q, K (row-major, padded) and V^T; zero the padding rows
+  for (int c = t; c < LP * 8; c += 256) {
+    const int row = c >> 3, ch = c & 7;
+    u32x4 q = {0u, 0u, 0u, 0u}, k = q, v = q;
+    if (row < L) {
+      const bf16_t* base = qkv + ((long)b * L + row) * ldqkv + h * ADH + ch * 8;
+      q = *reinterpret_cast<const u32x4*>(base);
+      k = *reinterpret_cast<const u32x4*>(base + D);
+      v = *reinterpret_cast<const u32x4*>(base + 2 * D);
+    }
+    *reinterpret_cast<u32x4*>(&Qs[row * APAD + ch * 8]) = q;
+    *reinterpret_cast<u32x4*>(&Ks[row * APAD + ch * 8]) = k;
+    const bf16_t* hv = reinterpret_cast<const bf16_t*>(&v);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) Vt[(ch * 8 + i) * VTP + row] = hv[i];
+  }
+  for (int r = t; r < 2 * L - 1; r += 256) tbl[r] = rel_emb[(long)bucket[r] * H + h];
+  // gate per query row (fp32, from the layer input slice)
+  for (int i = t; i < LP; i += 256) {
+    float gsum = 1.f;
+    if (i < L) {
+      float pr[8];
+#pragma unroll
+      for (int o = 0; o < 8; ++o) pr[o] = gb[o];
+      const bf16_t* xr = x + ((long)b * L + i) * ldx + h * ADH;
+      for (int c = 0; c < ADH; ++c) {
+        const float xv = bf2f(xr[c]);
+#pragma unroll
+        for (int o = 0; o < 8; ++o) pr[o] += xv * gw[o * ADH + c];
+      }
+      const float ga = 1.f / (1.f + __expf(-(pr[0] + pr[1] + pr[2] + pr[3])));
+      const float gbv = 1.f / (1.f + __expf(-(pr[4] + pr[5] + pr[6] + pr[7])));
+      gsum = ga * (gbv * gconst[h] - 1.f) + 2.f;
+    }
+    gate[i] = gsum;
+  }
+  __syncthreads();
+
+  const int NT = LP / 16;  // key tiles
+  bf16_t* Pw = Ps + w * 16 * VTP;
+  for (int rb = w; rb < NT; rb += 4) {
+    // S = Q K^T for 16 query rows x LP keys
+    f32x4 s[16];
+#pragma unroll
+    for (int ct = 0; ct < 16; ++ct) s[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const bf16x8 a = *reinterpret_cast<const bf16x8*>(&Qs[(rb * 16 + (lane & 15)) * APAD + kk * 32 + (lane >> 4) * 8]);
+#pragma unroll
+      for (int ct = 0; ct < 16; ++ct) {
+        if (ct < NT) {
+          const bf16x8 bk = *reinterpret_cast<const bf16x8*>(&Ks[(ct * 16 + (lane & 15)) * APAD + kk * 32 + (lane >> 4) * 8]);
+          s[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bk, s[ct], 0, 0, 0);
+        }
+      }
+    }
+    float mx[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+#pragma unroll
+    for (int ct = 0; ct < 16; ++ct) {
+      if (ct < NT) {
+        const int j = ct * 16 + (lane & 15);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int i = rb * 16 + (lane >> 4) * 4 + r;
+          float v = -INFINITY;
+          if (j < L) v = s[ct][r] * scale + gate[i] * tbl[j - i + L - 1 < 0 ? 0 : (j - i + L - 1 > 2 * L - 2 ? 2 * L - 2 : j - i + L - 1)];
+          s[ct][r] = v;
+          mx[r] = fmaxf(mx[r], v);
+        }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) mx[r] = fmaxf(mx[r], __shfl_xor(mx[r], o, 64));
+    float sum[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ct = 0; ct < 16; ++ct) {
+      if (ct < NT) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float p = __expf(s[ct][r] - mx[r]);
+          const bf16_t pb = f2bf(p);
+          sum[r] += bf2f(pb);  // normalise with the same rounded weights that enter PV
+          Pw[((lane >> 4) * 4 + r) * VTP + ct * 16 + (lane & 15)] = pb;
+        }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) sum[r] += __shfl_xor(sum[r], o, 64);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    // O = P V  (16 rows x 64 dims)
+    f32x4 o[4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) o[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int kk = 0; kk < LP / 32; ++kk) {
+      const bf16x8 a = *reinterpret_cast<const bf16x8*>(&Pw[(lane & 15) * VTP + kk * 32 + (lane >> 4) * 8]);
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        const bf16x8 bv = *reinterpret_cast<const bf16x8*>(&Vt[(nt * 16 + (lane & 15)) * VTP + kk * 32 + (lane >> 4) * 8]);
+        o[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bv, o[nt], 0, 0, 0);
+      }
+    }
+    if (LP % 32) {  // odd 16-key tail
+      const int kk = LP / 32;
+      bf16x8 a = *reinterpret_cast<const bf16x8*>(&Pw[(lane & 15) * VTP + kk * 32 + (lane >> 4) * 8]);
+      if ((lane >> 4) >= 2) a = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        bf16x8 bv = *reinterpret_cast<const bf16x8*>(&Vt[(nt * 16 + (lane & 15)) * VTP + kk * 32 + (lane >> 4) * 8]);
+        if ((lane >> 4) >= 2) bv = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+        o[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bv, o[nt], 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = rb * 16 + (lane >> 4) * 4 + r;
+        if (i < L) out[((long)b * L + i) * ldo + h * ADH + nt * 16 + (lane & 15)] = f2bf(o[nt][r] / sum[r]);
+      }
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+MER_API int mer_wavlm_attention(int B, int L, int H, const void* qkv, long ldqkv, const void* x, long ldx,
+                                const float* gate_w, const float* gate_b, const float* gate_const,
+                                const float* rel_emb, const int* bucket, void* out, long ldo, float scale,
+                                void* stream) {
+  if (L > 256 || L <= 0) return (int)hipErrorInvalidValue;
+  const int LP = (L + 15) / 16 * 16;
+  const size_t lds = sizeof(bf16_t) * ((size_t)2 * LP * APAD + (size_t)ADH * (LP + 8) + 4 * 16 * (LP + 8)) +
+                     sizeof(float) * (LP + 2 * L);
+  hipLaunchKernelGGL(wavlm_attn_kernel, dim3(B * H), dim3(256), lds, (hipStream_t)stream, L, H, (const bf16_t*)qkv,
+                     ldqkv, (const bf16_t*)x, ldx, gate_w, gate_b, gate_const, rel_emb, bucket, (bf16_t*)out, ldo,
+                     scale);
+  MER_LAUNCH_CHECK();
+}
+
+// ---------------------------------------------------------------------------------------
+// Weight preparation (frozen weights: run once per weight version, never in the hot loop).
+// dst[i0][i1][i2] = bf16(src[i0*s0 + i1*s1 + i2*s2] * (scale ? scale[i1] : 1))
+// e.g. Conv1d [Cout][Cin][k] -> [Cout][k][Cin] (K-contiguous im2col order).
+// ---------------------------------------------------------------------------------------
+__global__ void permute3_bf16_kernel(int n0, int n1, int n2, const float* __restrict__ src, long s0, long s1, long s2,
+                                     const float* __restrict__ scale, bf16_t* __restrict__ dst) {
+  const long n = (long)n0 * n1 * n2;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < n; e += (long)gridDim.x * blockDim.x) {
+    const int i2 = e % n2;
+    const int i1 = (e / n2) % n1;
+    const int i0 = e / ((long)n1 * n2);
+    float v = src[(long)i0 * s0 + (long)i1 * s1 + (long)i2 * s2];
+    if (scale) v *= scale[i1];
+    dst[e] = f2bf(v);
+  }
+}
+MER_API int mer_permute3_bf16(int n0, int n1, int n2, const float* src, long s0, long s1, long s2, const float* scale,
+                              void* dst, void* stream) {
+  const long n = (long)n0 * n1 * n2;
+  const int grid = (int)((n + 255) / 256 < 8192 ? (n + 255) / 256 : 8192);
+  hipLaunchKernelGGL(permute3_bf16_kernel, dim3(grid > 0 ? grid : 1), dim3(256), 0, (hipStream_t)stream, n0, n1, n2,
+                     src, s0, s1, s2, scale, (bf16_t*)dst);
+  MER_LAUNCH_CHECK();
+}
+
+// weight_norm(dim=2) scale of the positional conv (TF:58-78): scale[k] = g[k] / ||v[:, :, k]||_2
+__global__ __launch_bounds__(256) void weightnorm_scale_kernel(int n01, int taps, const float* __restrict__ v,
+                                                               const float* __restrict__ g, float* __restrict__ scale) {
+  __shared__ float red[4];
+  const int k = blockIdx.x;
+  float s = 0.f;
+  for (int i = threadIdx.x; i < n01; i += 256) {
+    const float x = v[(long)i * taps + k];
+    s += x * x;
+  }
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) scale[k] = g[k] / sqrtf(red[0] + red[1] + red[2] + red[3]);
+}
+MER_API int mer_weightnorm_scale(int n01, int taps, const float* v, const float* g, float* scale, void* stream) {
+  hipLaunchKernelGGL(weightnorm_scale_kernel, dim3(taps), dim3(256), 0, (hipStream_t)stream, n01, taps, v, g, scale);
+  MER_LAUNCH_CHECK();
+}
+
+// fp32 -> bf16 cast (contiguous), 4 elements per thread-iteration.
+__global__ void cast_bf16_kernel(long n, const float* __restrict__ x, bf16_t* __restrict__ y) {
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < n; e += (long)gridDim.x * blockDim.x) y[e] = f2bf(x[e]);
+}
+MER_API int mer_cast_bf16(long n, const float* x, void* y, void* stream) {
+  const int grid = (int)((n + 255) / 256 < 8192 ? (n + 255) / 256 : 8192);
+  hipLaunchKernelGGL(cast_bf16_kernel, dim3(grid > 0 ? grid : 1), dim3(256), 0, (hipStream_t)stream, n, x, (bf16_t*)y);
+  MER_LAUNCH_CHECK();
+}

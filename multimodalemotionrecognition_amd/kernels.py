@@ -198,6 +198,78 @@ def adam_step(p, g, m, v, lr, b1, b2, eps, wd, step):
         float(b2), float(eps), float(wd), int(step), stream_ptr())
 
 
+def _aligned16(*ts):
+    for t in ts:
+        if t is not None and t.data_ptr() % 16:
+            raise ValueError("bf16 GEMM operands must be 16-byte aligned")
+
+
+def gemm_bf16(a, w, out, *, M=None, K=None, rows=None, bias=None, residual=None, act="none"):
+    """out[M,N] = act(A W^T + bias) (+ residual) on bf16 MFMA.
+
+    ``a``: bf16 [M,K] (row stride a.stride(0)), or a raw bf16 buffer with ``rows=(rpg, rstride, gstride)``
+    describing the channel-last Conv1d im2col rows.  ``w``: bf16 [N,K].  ``out``: bf16 or fp32 [M,N].
+    """
+    N = w.shape[0]
+    if rows is None:
+        M, K = a.shape
+        rows = (M, a.stride(0), 0)
+    if w.dtype != torch.bfloat16 or a.dtype != torch.bfloat16 or w.shape[1] != K or w.stride(1) != 1:
+        raise ValueError("gemm_bf16 expects bf16 A and W[N,K]")
+    if out.shape[-1] != N or out.numel() != M * N:
+        raise ValueError(f"gemm_bf16 out shape {tuple(out.shape)} != ({M},{N})")
+    _aligned16(a, w)
+    LIB("mer_gemm_bf16", M, N, K, a.data_ptr(), rows[2], rows[1], rows[0], w.data_ptr(), w.stride(0),
+        out.data_ptr(), _dt(out), N if out.dim() < 2 else out.stride(-2), _ptr(bias), _ptr(residual),
+        0 if residual is None else residual.stride(-2), ACT[act], stream_ptr())
+    return out
+
+
+def posconv_gemm_bf16(x, wp, out, B, L, C, groups, taps, pad, bias, residual, act="gelu"):
+    LIB("mer_posconv_gemm_bf16", B, L, C, groups, taps, pad, x.data_ptr(), x.stride(-2), wp.data_ptr(), out.data_ptr(),
+        _dt(out), out.stride(-2), _ptr(bias), _ptr(residual), 0 if residual is None else residual.stride(-2),
+        ACT[act], stream_ptr())
+
+
+def wavlm_conv0(wav, w0, out, stats):
+    B, S = wav.shape
+    Lout = out.shape[1]
+    LIB("mer_wavlm_conv0", B, S, Lout, wav.data_ptr(), w0.data_ptr(), out.data_ptr(), stats.data_ptr(), stream_ptr())
+
+
+def groupnorm_gelu(x, stats, gamma, beta, y, eps=1e-5):
+    B, L, C = x.shape
+    LIB("mer_groupnorm_gelu", B, L, C, x.data_ptr(), stats.data_ptr(), gamma.data_ptr(), beta.data_ptr(), float(eps),
+        y.data_ptr(), stream_ptr())
+
+
+def layernorm(x2d, gamma, beta, y2d, eps=1e-5):
+    rows, d = x2d.shape
+    LIB("mer_layernorm", rows, d, x2d.data_ptr(), _dt(x2d), x2d.stride(0), gamma.data_ptr(), beta.data_ptr(),
+        float(eps), y2d.data_ptr(), _dt(y2d), y2d.stride(0), stream_ptr())
+
+
+def wavlm_attention(qkv, x, gate_w, gate_b, gate_const, rel_emb, bucket, out, B, L, H, scale):
+    LIB("mer_wavlm_attention", B, L, H, qkv.data_ptr(), qkv.stride(0), x.data_ptr(), x.stride(0), gate_w.data_ptr(),
+        gate_b.data_ptr(), gate_const.data_ptr(), rel_emb.data_ptr(), bucket.data_ptr(), out.data_ptr(),
+        out.stride(0), float(scale), stream_ptr())
+
+
+def permute3_bf16(src, shape3, strides3, dst, scale=None):
+    n0, n1, n2 = shape3
+    LIB("mer_permute3_bf16", n0, n1, n2, src.data_ptr(), strides3[0], strides3[1], strides3[2], _ptr(scale),
+        dst.data_ptr(), stream_ptr())
+
+
+def weightnorm_scale(v, g, scale):
+    n01 = v.shape[0] * v.shape[1]
+    LIB("mer_weightnorm_scale", n01, v.shape[2], v.data_ptr(), g.data_ptr(), scale.data_ptr(), stream_ptr())
+
+
+def cast_bf16(x, y):
+    LIB("mer_cast_bf16", x.numel(), x.data_ptr(), y.data_ptr(), stream_ptr())
+
+
 def softmax_avg_fwd(za, zv, out, pa, pv):
     B, C = za.shape
     LIB("mer_softmax_avg_fwd", B, C, za.data_ptr(), zv.data_ptr(), out.data_ptr(), pa.data_ptr(), pv.data_ptr(),

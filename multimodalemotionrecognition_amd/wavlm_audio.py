@@ -1,0 +1,346 @@
+"""``WavLMAudioEncoder`` mirror (``src/models/wavlm_audio.py``) with a WavLM-base forward on HIP kernels.
+
+The module tree reproduces transformers' ``WavLMModel`` attribute names, so state-dict keys are
+identical (``audio_model.wavlm.encoder.layers.3.attention.q_proj.weight``, the positional conv's
+``parametrizations.weight.original0/1`` ...) and reference checkpoints load unchanged.  The model
+is built offline from the WavLM-base config (the reference's ``from_pretrained`` network fetch has
+its own offline fallback to exactly this, wavlm_audio.py:35-41).
+
+Forward (``encode_sequence``, wavlm_audio.py:165-183 -> TF:1032-1085), all bf16 activations with
+fp32 accumulation:
+  conv0 (direct, + GroupNorm stats) -> GroupNorm+GELU -> conv1..6 (Conv1d-as-GEMM, GELU epilogue)
+  -> LayerNorm(512) -> projection GEMM -> grouped pos-conv GEMM (+GELU +residual) -> LayerNorm
+  -> 12 x [fused QKV GEMM -> gated-rel-pos attention -> out-proj GEMM (+residual) -> LN
+           -> FFN GEMM (+GELU) -> FFN GEMM (+residual) -> LN]
+Frozen by default (no backward); stage-2 fine-tuning of the last layers is a later build row.
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, Optional
+
+import numpy as np
+import torch
+from torch import nn
+
+from . import kernels as K
+from .nn_ops import hip_dropout, hip_linear
+from .temporal import TemporalPooler
+
+CONV_DIM = 512
+CONV_KERNEL = (10, 3, 3, 3, 3, 2, 2)
+CONV_STRIDE = (5, 2, 2, 2, 2, 2, 2)
+
+
+class WavLMConfigLite:
+    """The WavLM-base hyper-parameters used by ``WavLMModel(WavLMConfig())`` (TF config defaults)."""
+
+    hidden_size = 768
+    num_attention_heads = 12
+    num_hidden_layers = 12
+    intermediate_size = 3072
+    num_buckets = 320
+    max_bucket_distance = 800
+    num_conv_pos_embeddings = 128
+    num_conv_pos_embedding_groups = 16
+    layer_norm_eps = 1e-5
+
+
+class _ConvLayer(nn.Module):
+    def __init__(self, layer_id: int):
+        super().__init__()
+        cin = 1 if layer_id == 0 else CONV_DIM
+        self.conv = nn.Conv1d(cin, CONV_DIM, CONV_KERNEL[layer_id], stride=CONV_STRIDE[layer_id], bias=False)
+        if layer_id == 0:
+            self.layer_norm = nn.GroupNorm(CONV_DIM, CONV_DIM, affine=True)
+
+
+class _FeatureExtractor(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.conv_layers = nn.ModuleList([_ConvLayer(i) for i in range(len(CONV_KERNEL))])
+
+
+class _FeatureProjection(nn.Module):
+    def __init__(self, cfg):
+        super().__init__()
+        self.layer_norm = nn.LayerNorm(CONV_DIM, eps=cfg.layer_norm_eps)
+        self.projection = nn.Linear(CONV_DIM, cfg.hidden_size)
+
+
+class _PosConv(nn.Module):
+    def __init__(self, cfg):
+        super().__init__()
+        conv = nn.Conv1d(cfg.hidden_size, cfg.hidden_size, cfg.num_conv_pos_embeddings,
+                         padding=cfg.num_conv_pos_embeddings // 2, groups=cfg.num_conv_pos_embedding_groups)
+        self.conv = nn.utils.parametrizations.weight_norm(conv, name="weight", dim=2)
+
+
+class _Attention(nn.Module):
+    def __init__(self, cfg, has_bias: bool):
+        super().__init__()
+        d, h = cfg.hidden_size, cfg.num_attention_heads
+        self.k_proj = nn.Linear(d, d)
+        self.v_proj = nn.Linear(d, d)
+        self.q_proj = nn.Linear(d, d)
+        self.out_proj = nn.Linear(d, d)
+        self.gru_rel_pos_const = nn.Parameter(torch.ones(1, h, 1, 1))
+        self.gru_rel_pos_linear = nn.Linear(d // h, 8)
+        if has_bias:
+            self.rel_attn_embed = nn.Embedding(cfg.num_buckets, h)
+
+
+class _FeedForward(nn.Module):
+    def __init__(self, cfg):
+        super().__init__()
+        self.intermediate_dense = nn.Linear(cfg.hidden_size, cfg.intermediate_size)
+        self.output_dense = nn.Linear(cfg.intermediate_size, cfg.hidden_size)
+
+
+class _EncoderLayer(nn.Module):
+    def __init__(self, cfg, has_bias):
+        super().__init__()
+        self.attention = _Attention(cfg, has_bias)
+        self.layer_norm = nn.LayerNorm(cfg.hidden_size, eps=cfg.layer_norm_eps)
+        self.feed_forward = _FeedForward(cfg)
+        self.final_layer_norm = nn.LayerNorm(cfg.hidden_size, eps=cfg.layer_norm_eps)
+
+
+class _Encoder(nn.Module):
+    def __init__(self, cfg):
+        super().__init__()
+        self.pos_conv_embed = _PosConv(cfg)
+        self.layer_norm = nn.LayerNorm(cfg.hidden_size, eps=cfg.layer_norm_eps)
+        self.layers = nn.ModuleList([_EncoderLayer(cfg, i == 0) for i in range(cfg.num_hidden_layers)])
+
+
+def relative_position_buckets(length: int, num_buckets: int = 320, max_distance: int = 800) -> np.ndarray:
+    """Bucket of every relative position j - i in [-(L-1), L-1] (TF:253-271), int32 [2L-1]."""
+    rel = np.arange(-(length - 1), length, dtype=np.int64)
+    nb = num_buckets // 2
+    buckets = (rel > 0).astype(np.int64) * nb
+    r = np.abs(rel)
+    max_exact = nb // 2
+    with np.errstate(divide="ignore"):
+        large = np.log(np.maximum(r, 1).astype(np.float32) / max_exact) / math.log(max_distance / max_exact) * (nb - max_exact)
+    large = np.minimum((max_exact + large).astype(np.int64), nb - 1)
+    return (buckets + np.where(r < max_exact, r, large)).astype(np.int32)
+
+
+class WavLMBackbone(nn.Module):
+    """Parameter container named like transformers' ``WavLMModel`` + the HIP forward schedule."""
+
+    def __init__(self, cfg: Optional[WavLMConfigLite] = None):
+        super().__init__()
+        self.config = cfg or WavLMConfigLite()
+        self.feature_extractor = _FeatureExtractor()
+        self.feature_projection = _FeatureProjection(self.config)
+        self.masked_spec_embed = nn.Parameter(torch.empty(self.config.hidden_size).uniform_())
+        self.encoder = _Encoder(self.config)
+        self._packed = None
+        self._packed_key = None
+        self._buckets: Dict[tuple, torch.Tensor] = {}
+
+    # ---- frozen-weight preparation (runs once per weight version, on the GPU kernels) ----
+    def _weights_key(self):
+        return tuple((q.data_ptr(), q._version) for q in self.parameters())
+
+    @torch.no_grad()
+    def packed_weights(self):
+        key = self._weights_key()
+        if self._packed is not None and self._packed_key == key:
+            return self._packed
+        dev = self.masked_spec_embed.device
+        cfg = self.config
+        pk = {"conv": []}
+        fe = self.feature_extractor.conv_layers
+        pk["conv0_w"] = fe[0].conv.weight.detach().reshape(CONV_DIM, CONV_KERNEL[0]).contiguous()
+        for i in range(1, len(CONV_KERNEL)):
+            w = fe[i].conv.weight.detach()  # [Cout, Cin, k] -> [Cout, k, Cin]
+            k = CONV_KERNEL[i]
+            dst = torch.empty(CONV_DIM, k, CONV_DIM, device=dev, dtype=torch.bfloat16)
+            K.permute3_bf16(w.contiguous(), (CONV_DIM, k, CONV_DIM), (CONV_DIM * k, 1, k), dst)
+            pk["conv"].append(dst.view(CONV_DIM, k * CONV_DIM))
+        pk["proj_w"] = self._bf16(self.feature_projection.projection.weight)
+        pc = self.encoder.pos_conv_embed.conv
+        g = pc.parametrizations.weight.original0.detach().reshape(-1).contiguous()
+        v = pc.parametrizations.weight.original1.detach().contiguous()  # [768, 48, 128]
+        scale = torch.empty(cfg.num_conv_pos_embeddings, device=dev, dtype=torch.float32)
+        K.weightnorm_scale(v, g, scale)
+        taps, cg = cfg.num_conv_pos_embeddings, cfg.hidden_size // cfg.num_conv_pos_embedding_groups
+        wp = torch.empty(cfg.hidden_size, taps, cg, device=dev, dtype=torch.bfloat16)  # [g*Cg+n][tap][c]
+        K.permute3_bf16(v, (cfg.hidden_size, taps, cg), (cg * taps, 1, taps), wp, scale=scale)
+        pk["posconv_w"] = wp
+        layers = []
+        for layer in self.encoder.layers:
+            at = layer.attention
+            qkv = torch.empty(3 * cfg.hidden_size, cfg.hidden_size, device=dev, dtype=torch.bfloat16)
+            for j, lin in enumerate((at.q_proj, at.k_proj, at.v_proj)):
+                K.cast_bf16(lin.weight.detach().contiguous(), qkv[j * cfg.hidden_size:(j + 1) * cfg.hidden_size])
+            qkv_b = torch.cat([at.q_proj.bias, at.k_proj.bias, at.v_proj.bias]).detach().contiguous()
+            layers.append(dict(qkv_w=qkv, qkv_b=qkv_b, out_w=self._bf16(at.out_proj.weight),
+                               ff1_w=self._bf16(layer.feed_forward.intermediate_dense.weight),
+                               ff2_w=self._bf16(layer.feed_forward.output_dense.weight),
+                               gate_c=at.gru_rel_pos_const.detach().reshape(-1).contiguous()))
+        pk["layers"] = layers
+        pk["rel_emb"] = self.encoder.layers[0].attention.rel_attn_embed.weight.detach().contiguous()
+        self._packed, self._packed_key = pk, key
+        return pk
+
+    @staticmethod
+    def _bf16(w):
+        dst = torch.empty(w.shape, device=w.device, dtype=torch.bfloat16)
+        K.cast_bf16(w.detach().contiguous(), dst)
+        return dst
+
+    def buckets(self, length: int, device) -> torch.Tensor:
+        key = (length, str(device))
+        if key not in self._buckets:
+            cfg = self.config
+            self._buckets[key] = torch.from_numpy(relative_position_buckets(length, cfg.num_buckets,
+                                                                            cfg.max_bucket_distance)).to(device)
+        return self._buckets[key]
+
+    @torch.no_grad()
+    def forward_hip(self, wav: torch.Tensor, out_dtype=torch.bfloat16, num_layers: Optional[int] = None,
+                    capture: Optional[dict] = None):
+        """Raw waveform [B, S] fp32 -> last_hidden_state [B, L, 768] (bf16 or fp32).
+
+        ``capture`` (tests): receives copies of 'extract_features' (post-LN conv features, what HF
+        returns as ``extract_features``) and 'layer0' (output of encoder layer 0)."""
+        if not wav.is_cuda:
+            raise RuntimeError("WavLM runs on the MI355X kernels; move the waveform to the GPU")
+        cfg = self.config
+        pk = self.packed_weights()
+        wav = wav.contiguous().float()
+        B, S = wav.shape
+        dev = wav.device
+        bf = torch.bfloat16
+        L = (S - CONV_KERNEL[0]) // CONV_STRIDE[0] + 1
+        x = torch.empty(B, L, CONV_DIM, device=dev, dtype=bf)
+        stats = torch.zeros(B, CONV_DIM, 2, device=dev, dtype=torch.float32)
+        K.wavlm_conv0(wav, pk["conv0_w"], x, stats)
+        gn = self.feature_extractor.conv_layers[0].layer_norm
+        xg = torch.empty_like(x)
+        K.groupnorm_gelu(x, stats, gn.weight, gn.bias, xg, eps=gn.eps)
+        x = xg
+        for i in range(1, len(CONV_KERNEL)):
+            k, s = CONV_KERNEL[i], CONV_STRIDE[i]
+            L_out = (L - k) // s + 1
+            y = torch.empty(B, L_out, CONV_DIM, device=dev, dtype=bf)
+            K.gemm_bf16(x, pk["conv"][i - 1], y, M=B * L_out, K=k * CONV_DIM,
+                        rows=(L_out, s * CONV_DIM, L * CONV_DIM), act="gelu")
+            x, L = y, L_out
+        D = cfg.hidden_size
+        fp = self.feature_projection
+        xn = torch.empty(B * L, CONV_DIM, device=dev, dtype=bf)
+        K.layernorm(x.view(B * L, CONV_DIM), fp.layer_norm.weight, fp.layer_norm.bias, xn, eps=fp.layer_norm.eps)
+        if capture is not None:
+            capture["extract_features"] = xn.view(B, L, CONV_DIM).clone()
+        h = torch.empty(B * L, D, device=dev, dtype=bf)
+        K.gemm_bf16(xn, pk["proj_w"], h, bias=fp.projection.bias)
+        # positional conv: h + gelu(posconv(h) + bias)  (TF:82-90, 414-416)
+        pc = self.encoder.pos_conv_embed.conv
+        hp = torch.empty(B * L, D, device=dev, dtype=bf)
+        K.posconv_gemm_bf16(h, pk["posconv_w"], hp, B, L, D, cfg.num_conv_pos_embedding_groups,
+                            cfg.num_conv_pos_embeddings, cfg.num_conv_pos_embeddings // 2, pc.bias, h, act="gelu")
+        x = torch.empty(B * L, D, device=dev, dtype=bf)
+        K.layernorm(hp, self.encoder.layer_norm.weight, self.encoder.layer_norm.bias, x, eps=cfg.layer_norm_eps)
+        bucket = self.buckets(L, dev)
+        H = cfg.num_attention_heads
+        scale = (D // H) ** -0.5
+        nl = cfg.num_hidden_layers if num_layers is None else num_layers
+        qkv = torch.empty(B * L, 3 * D, device=dev, dtype=bf)
+        att = torch.empty(B * L, D, device=dev, dtype=bf)
+        y32 = torch.empty(B * L, D, device=dev, dtype=torch.float32)
+        x1 = torch.empty(B * L, D, device=dev, dtype=bf)
+        ff = torch.empty(B * L, cfg.intermediate_size, device=dev, dtype=bf)
+        for li in range(nl):
+            layer = self.encoder.layers[li]
+            lw = pk["layers"][li]
+            at = layer.attention
+            K.gemm_bf16(x, lw["qkv_w"], qkv, bias=lw["qkv_b"])
+            K.wavlm_attention(qkv, x, at.gru_rel_pos_linear.weight, at.gru_rel_pos_linear.bias, lw["gate_c"],
+                              pk["rel_emb"], bucket, att, B, L, H, scale)
+            K.gemm_bf16(att, lw["out_w"], y32, bias=at.out_proj.bias, residual=x)
+            K.layernorm(y32, layer.layer_norm.weight, layer.layer_norm.bias, x1, eps=cfg.layer_norm_eps)
+            K.gemm_bf16(x1, lw["ff1_w"], ff, bias=layer.feed_forward.intermediate_dense.bias, act="gelu")
+            K.gemm_bf16(ff, lw["ff2_w"], y32, bias=layer.feed_forward.output_dense.bias, residual=x1)
+            last = li == nl - 1
+            xo = torch.empty(B * L, D, device=dev, dtype=out_dtype) if last else x
+            K.layernorm(y32, layer.final_layer_norm.weight, layer.final_layer_norm.bias, xo, eps=cfg.layer_norm_eps)
+            x = xo
+            if capture is not None and li == 0:
+                capture["layer0"] = x.view(B, L, D).clone()
+        return x.view(B, L, D)
+
+
+class WavLMAudioEncoder(nn.Module):
+    """wavlm_audio.py:13-183 -- same constructor, stage helpers and encode API."""
+
+    def __init__(self, num_classes: int, embedding_dim: int = 768, model_name: str = "microsoft/wavlm-base",
+                 temporal_pooling: str = "mean", temporal_num_heads: int = 4, temporal_num_layers: int = 1,
+                 temporal_dropout: float = 0.1):
+        super().__init__()
+        self.num_classes = num_classes
+        self.embedding_dim = embedding_dim
+        self.model_name = model_name
+        # offline build of the WavLM-base architecture (the reference's own fallback, wavlm_audio.py:35-41)
+        self.wavlm = WavLMBackbone()
+        actual_hidden_size = self.wavlm.config.hidden_size
+        self.sequence_dim = actual_hidden_size
+        self.temporal_pool = TemporalPooler(actual_hidden_size, temporal_pooling, temporal_num_heads,
+                                            temporal_num_layers, temporal_dropout)
+        self.classifier = nn.Sequential(nn.Linear(actual_hidden_size, embedding_dim), nn.ReLU(inplace=True),
+                                        nn.Dropout(0.2), nn.Linear(embedding_dim, num_classes))
+        self._freeze_backbone()
+
+    def _freeze_backbone(self):
+        for param in self.wavlm.parameters():
+            param.requires_grad = False
+
+    def _unfreeze_last_n_layers(self, n: int = 2):
+        if n == 0:
+            return
+        num_layers = len(self.wavlm.encoder.layers)
+        for i in range(max(0, num_layers - n), num_layers):
+            for param in self.wavlm.encoder.layers[i].parameters():
+                param.requires_grad = True
+
+    def unfreeze_backbone(self, num_last_layers: int = 2):
+        self._unfreeze_last_n_layers(num_last_layers)
+
+    def get_stage1_params(self):
+        return list(self.classifier.parameters())
+
+    def get_stage2_params(self):
+        backbone, head = [], []
+        for name, param in self.named_parameters():
+            if param.requires_grad:
+                (head if ("classifier" in name or "head" in name) else backbone).append(param)
+        return {"backbone": backbone, "head": head}
+
+    def _wav(self, x):
+        return x.squeeze(1) if x.dim() == 3 else x
+
+    def encode_sequence(self, x: torch.Tensor, out_dtype=torch.bfloat16) -> torch.Tensor:
+        """[B,1,S] or [B,S] -> [B, Ta, 768] hidden states (bf16 activations; wavlm_audio.py:165-183)."""
+        trainable = any(q.requires_grad for q in self.wavlm.parameters())
+        if self.training and trainable and torch.is_grad_enabled():
+            raise NotImplementedError("WavLM stage-2 fine-tuning (backward through the encoder) is a later build "
+                                      "row; the north-star path trains with WavLM frozen (wavlm_audio.py:62-68)")
+        return self.wavlm.forward_hip(self._wav(x), out_dtype=out_dtype)
+
+    def encode(self, x: torch.Tensor) -> torch.Tensor:
+        hidden = self.encode_sequence(x, out_dtype=torch.float32)
+        a_emb = self.temporal_pool(hidden)
+        if a_emb.size(-1) != self.embedding_dim:
+            a_emb = hip_linear(a_emb, self.classifier[0])
+        return a_emb
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        hidden = self.encode_sequence(x, out_dtype=torch.float32)
+        a_emb = self.temporal_pool(hidden)
+        h = hip_linear(a_emb, self.classifier[0], act="relu")
+        h = hip_dropout(h, 0.2, self.training)
+        return hip_linear(h, self.classifier[3])

@@ -51,7 +51,7 @@ def test_xattn_c2_grads_and_fused_adam():
     logits = m.xattn_from_features(v, a)
     loss = CrossEntropyLoss()(logits, labels)
     loss.backward()
-    assert abs(float(loss) - float(g["loss"])) < 1e-5
+    assert abs(float(loss.detach()) - float(g["loss"])) < 1e-5
     assert max_abs(v.grad[:2], g["grad_v"]) < 1e-6
     for n, q in trainable:
         key = "grad." + n
@@ -61,11 +61,17 @@ def test_xattn_c2_grads_and_fused_adam():
             assert max_abs(q.grad, ref) / scale < 1e-4, n
         else:
             assert q.grad is None, f"{n} must receive no gradient (dead on the WavLM path)"
+    # Adam's first step is ~lr*sign(g): feed the reference's own gradients so the optimizer
+    # kernel is checked exactly, independent of 1e-9 gradient noise on |g|~eps elements.
+    with torch.no_grad():
+        for n, q in trainable:
+            if "grad." + n in g.files:
+                q.grad.copy_(torch.from_numpy(g["grad." + n]))
     opt.step()
     for n, q in trainable:
         key = "adam1." + n
         if key in g.files:
-            assert max_abs(q, g[key]) < 5e-5, n
+            assert max_abs(q, g[key]) < 2e-6, n
 
 
 @pytest.mark.parametrize("head", ["concat", "gated"])
@@ -84,7 +90,7 @@ def test_xattn_prior_grads_vs_oracle(head):
     ref, _ = fusion_ref.xattn_forward(p, v.cpu(), a.cpu(), xattn_head=head, use_prior=True)
     rl = fusion_ref.cross_entropy(ref, labels.cpu(), label_smoothing=0.1)
     rl.backward()
-    assert abs(float(loss) - float(rl)) < 1e-5
+    assert abs(float(loss.detach()) - float(rl.detach())) < 1e-5
     for n, q in m.named_parameters():
         if n.startswith(("audio_model", "video_model")) or n.startswith("audio_time_conv"):
             continue
@@ -168,7 +174,7 @@ def test_late_and_ce_kernels():
     rl = fusion_ref.late_nll(rp, y)
     rl.backward()
     assert max_abs(pr, rp) < 1e-6
-    assert abs(float(loss) - float(rl)) < 1e-5
+    assert abs(float(loss.detach()) - float(rl.detach())) < 1e-5
     assert max_abs(zad.grad, za.grad) < 1e-6
     z = torch.randn(5, 8, requires_grad=True)
     zd = z.detach().cuda().requires_grad_(True)
@@ -177,7 +183,7 @@ def test_late_and_ce_kernels():
     l1.backward()
     l2 = torch.nn.functional.cross_entropy(z, y, label_smoothing=0.1) * 3.0
     l2.backward()
-    assert abs(float(l1) - float(l2)) < 1e-5
+    assert abs(float(l1.detach()) - float(l2.detach())) < 1e-5
     assert max_abs(zd.grad, z.grad) < 1e-6
 
 
