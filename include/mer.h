@@ -160,6 +160,57 @@ int mer_weightnorm_scale(int n01, int taps, const float* v, const float* g, floa
 /* y = bf16(x), contiguous. */
 int mer_cast_bf16(long n, const float* x, void* y, void* stream);
 
+/* ============================ ResNet18 frame trunk (bf16 MFMA, NHWC) ============================
+ * VideoNet.backbone (video.py:21-23 -> torchvision resnet18 children[:-1]).  Activations are NHWC bf16
+ * with channels padded to a multiple of 8. */
+
+/* y[n,oh,ow,k] = sum_{r,s,c} x[n,oh*st-pad+r,ow*st-pad+s,c] w[k][r][s][c]  (bf16 out); if stats != NULL,
+ * stats[k] += (sum, sum of squares) of the stored outputs (BatchNorm batch statistics, pre-zeroed). */
+int mer_conv_fwd(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, const void* x,
+                 const void* w_packed, void* y, float* stats, void* stream);
+
+/* dx[n,h,w,c] = sum_{r,s,k} dy[n,(h+pad-r)/st,(w+pad-s)/st,k] wt[c][r][s][k] (+ residual where mask > 0). */
+int mer_conv_dgrad(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, const void* dy,
+                   const void* wt_packed, void* dx, const void* residual, const void* residual_mask, void* stream);
+
+/* dw[k][c][r][s] += sum_p dy[p][k] x(p; r,s,c) for c < Creal, fp32 PyTorch layout; split over `splits`
+ * pixel ranges with fp32 atomics (dw must be initialised). */
+int mer_conv_wgrad(int N, int H, int W, int C, int Creal, int K, int R, int S, int stride, int pad, const void* x,
+                   const void* dy, float* dw, int splits, void* stream);
+
+/* NCHW fp32 frames -> NHWC bf16 with channels zero-padded to Cp (<= 16). */
+int mer_pack_input_nhwc(int N, int C, int H, int W, int Cp, const float* x, void* y, void* stream);
+
+/* PyTorch conv weight [K][C][R][S] fp32 -> bf16 [K][R][S][Cp] (transpose=0, forward) or [Cp][R][S][K]
+ * (transpose=1, data-gradient operand); channels >= C are zero. */
+int mer_pack_conv_weight(int K, int C, int R, int S, int Cp, int transpose, const float* w, void* out, void* stream);
+
+/* BatchNorm2d finalize: ms[c] = (mean, rstd) from stats over M values and, when non-NULL, updates
+ * running_mean / running_var (unbiased) with `momentum` and increments num_batches_tracked (train mode).
+ * stats == NULL is eval mode: ms = (running_mean, 1/sqrt(running_var + eps)), nothing updated. */
+int mer_bn_finalize(int C, long M, const float* stats, float eps, float momentum, float* ms, float* rmean,
+                    float* rvar, long long* num_batches_tracked, void* stream);
+
+/* y = [relu](bn(x) + (ms2 ? bn2(res) : res)), ms = (mean, rstd) pairs; res may be NULL. */
+int mer_bn_apply(long M, int C, const void* x, const float* ms, const float* gamma, const float* beta, const void* res,
+                 const float* ms2, const float* gamma2, const float* beta2, int relu, void* y, void* stream);
+
+/* BN backward reduction: red[c] += (sum g, sum g*xhat), g = dy * (mask > 0) (mask = ReLU output or NULL). */
+int mer_bn_bwd_reduce(long M, int C, const void* dy, const void* mask, const void* x, const float* ms, float* red,
+                      void* stream);
+
+/* BN backward apply: dx = gamma*rstd*(g - s1/M - xhat*s2/M) (bf16); dgamma += s2, dbeta += s1. */
+int mer_bn_bwd_apply(long M, int C, const void* dy, const void* mask, const void* x, const float* ms,
+                     const float* gamma, const float* red, void* dx, float* dgamma, float* dbeta, void* stream);
+
+/* MaxPool2d(3, 2, 1) forward (argmax tap saved as uint8) and gather backward. */
+int mer_maxpool_fwd(int N, int H, int W, int C, const void* x, void* y, void* argmax, void* stream);
+int mer_maxpool_bwd(int N, int H, int W, int C, const void* dy, const void* argmax, void* dx, void* stream);
+
+/* AdaptiveAvgPool2d(1): NHWC bf16 -> [N,C] fp32, and backward (dx = dy / HW, bf16). */
+int mer_avgpool_fwd(int N, int HW, int C, const void* x, float* y, void* stream);
+int mer_avgpool_bwd(int N, int HW, int C, const float* dy, void* dx, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,685 @@
+// ResNet18 frame trunk (VideoNet.backbone, video.py:21-23 -> torchvision resnet18) on MFMA.
+//
+// Activations are NHWC bf16 (channels padded to a multiple of 8 so every 16-byte chunk of an
+// im2col row is 8 channels of ONE tap).  Convolutions are implicit GEMMs on
+// v_mfma_f32_16x16x32_bf16 with fp32 accumulation:
+//   fwd   : Y[m=(n,oh,ow)][k]      = sum_{r,s,c} X[n, oh*st-pad+r, ow*st-pad+s, c] W[k][r][s][c]
+//   dgrad : dX[m=(n,h,w)][c]       = sum_{r,s,k} dY[n, (h+pad-r)/st, (w+pad-s)/st, k] W'[c][r][s][k]
+//           (taps whose (h+pad-r) is not a multiple of st contribute zero)
+//   wgrad : dW[k][(r,s,c)]         = sum_{p=(n,oh,ow)} dY[p][k] X[n, oh*st-pad+r, ow*st-pad+s, c]
+// fwd/dgrad stage K-contiguous tiles (ds_read_b128 fragments); wgrad reduces over pixels, so both
+// operands are staged [pixel][channel] and read with the gfx950 LDS transpose (ds_read_b64_tr_b16).
+// BatchNorm (train mode: batch statistics, running-stat update with momentum 0.1 / unbiased var)
+// is split into a stats reduction fused into the conv epilogue, a finalize, and an apply pass.
+#include "common.h"
+#include "mer.h"
+
+typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+
+namespace {
+
+constexpr int CBK = 64;  // K step
+
+struct ConvGeom {
+  int N, OH, OW;          // GEMM output spatial dims (fwd: Ho,Wo; dgrad: H,W)
+  int IH, IW, IC;         // A-source spatial dims / channels (fwd: H,W,C; dgrad: Ho,Wo,K)
+  int R, S, st, pad;
+  int Ncols;              // GEMM N (fwd: Cout; dgrad: Cin)
+  int Kred;               // R*S*IC
+  const bf16_t* X;        // A source
+  const bf16_t* Wt;       // [Ncols][Kred]
+  bf16_t* Y;              // [M][ldy]
+  long ldy;
+  float* stats;           // fwd: per column (sum, sumsq), may be null
+  const bf16_t* R_;       // residual added in the epilogue (dgrad), may be null
+  const bf16_t* Rmask;    // residual is added only where Rmask > 0 (relu mask), may be null
+};
+
+template <bool DGRAD>
+__device__ __forceinline__ u32x4 conv_a_chunk(const ConvGeom& g, int n, int oh, int ow, bool rowok, int kk) {
+  u32x4 v = {0u, 0u, 0u, 0u};
+  if (!rowok || kk >= g.Kred) return v;
+  const int tap = kk / g.IC, c = kk - tap * g.IC;
+  const int r = tap / g.S, s = tap - r * g.S;
+  int ih, iw;
+  if (!DGRAD) {
+    ih = oh * g.st - g.pad + r;
+    iw = ow * g.st - g.pad + s;
+  } else {
+    const int th = oh + g.pad - r, tw = ow + g.pad - s;
+    if (th < 0 || tw < 0 || (th % g.st) || (tw % g.st)) return v;
+    ih = th / g.st;
+    iw = tw / g.st;
+  }
+  if (ih < 0 || ih >= g.IH || iw < 0 || iw >= g.IW) return v;
+  return *reinterpret_cast<const u32x4*>(g.X + (((long)n * g.IH + ih) * g.IW + iw) * g.IC + c);
+}
+
+// fwd / dgrad implicit GEMM. BM_ x BN_ tile, 4 waves as 2x2.
+template <bool DGRAD, int BM_, int BN_>
+__global__ __launch_bounds__(256, 2) void conv_kernel(ConvGeom g) {
+  constexpr int LDK = CBK + 8;
+  constexpr int IT = BM_ / 32, JT = BN_ / 32;           // 16x16 tiles per wave
+  constexpr int ACH = BM_ * 8 / 256, BCH = BN_ * 8 / 256;  // 16B chunks per thread per K step
+  __shared__ __attribute__((aligned(16))) bf16_t lds[2][(BM_ + BN_) * LDK];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int M = g.N * g.OH * g.OW;
+  const int m0 = blockIdx.y * BM_, n0 = blockIdx.x * BN_;
+  const int wm = (w >> 1) * (BM_ / 2), wn = (w & 1) * (BN_ / 2);
+  const int crow = t >> 3, ckc = t & 7;
+
+  int an[ACH], aoh[ACH], aow[ACH];
+  bool aok[ACH];
+#pragma unroll
+  for (int i = 0; i < ACH; ++i) {
+    const int m = m0 + crow + 32 * i;
+    aok[i] = m < M;
+    const int mm = aok[i] ? m : 0;
+    an[i] = mm / (g.OH * g.OW);
+    const int rem = mm - an[i] * g.OH * g.OW;
+    aoh[i] = rem / g.OW;
+    aow[i] = rem - aoh[i] * g.OW;
+  }
+  u32x4 ra[ACH], rb[BCH];
+  auto gload = [&](int k0) {
+    const int kk = k0 + ckc * 8;
+#pragma unroll
+    for (int i = 0; i < ACH; ++i) ra[i] = conv_a_chunk<DGRAD>(g, an[i], aoh[i], aow[i], aok[i], kk);
+#pragma unroll
+    for (int i = 0; i < BCH; ++i) {
+      const int n = n0 + crow + 32 * i;
+      rb[i] = (n < g.Ncols && kk < g.Kred) ? *reinterpret_cast<const u32x4*>(g.Wt + (long)n * g.Kred + kk)
+                                            : u32x4{0u, 0u, 0u, 0u};
+    }
+  };
+  auto lstore = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < ACH; ++i)
+      *reinterpret_cast<u32x4*>(&lds[buf][(crow + 32 * i) * LDK + ckc * 8]) = ra[i];
+#pragma unroll
+    for (int i = 0; i < BCH; ++i)
+      *reinterpret_cast<u32x4*>(&lds[buf][(BM_ + crow + 32 * i) * LDK + ckc * 8]) = rb[i];
+  };
+  f32x4 acc[IT][JT];
+#pragma unroll
+  for (int i = 0; i < IT; ++i)
+#pragma unroll
+    for (int j = 0; j < JT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (g.Kred + CBK - 1) / CBK;
+  gload(0);
+  lstore(0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) gload((kt + 1) * CBK);
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int kof = s * 32 + (lane >> 4) * 8;
+      bf16x8 af[IT], bfr[JT];
+#pragma unroll
+      for (int i = 0; i < IT; ++i)
+        af[i] = *reinterpret_cast<const bf16x8*>(&lds[cur][(wm + i * 16 + (lane & 15)) * LDK + kof]);
+#pragma unroll
+      for (int j = 0; j < JT; ++j)
+        bfr[j] = *reinterpret_cast<const bf16x8*>(&lds[cur][(BM_ + wn + j * 16 + (lane & 15)) * LDK + kof]);
+#pragma unroll
+      for (int i = 0; i < IT; ++i)
+#pragma unroll
+        for (int j = 0; j < JT; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < nk) lstore(cur ^ 1);
+    __syncthreads();
+  }
+
+#pragma unroll
+  for (int j = 0; j < JT; ++j) {
+    const int col = n0 + wn + j * 16 + (lane & 15);
+    float csum = 0.f, csq = 0.f;
+#pragma unroll
+    for (int i = 0; i < IT; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wm + i * 16 + (lane >> 4) * 4 + r;
+        if (row < M && col < g.Ncols) {
+          float v = acc[i][j][r];
+          if (g.R_) {
+            const long ri = (long)row * g.ldy + col;
+            if (!g.Rmask || bf2f(g.Rmask[ri]) > 0.f) v += bf2f(g.R_[ri]);
+          }
+          const bf16_t h = f2bf(v);
+          g.Y[(long)row * g.ldy + col] = h;
+          const float hv = bf2f(h);
+          csum += hv;
+          csq += hv * hv;
+        }
+      }
+    if (g.stats) {
+      csum += __shfl_xor(csum, 16, 64);
+      csum += __shfl_xor(csum, 32, 64);
+      csq += __shfl_xor(csq, 16, 64);
+      csq += __shfl_xor(csq, 32, 64);
+      if ((lane >> 4) == 0 && col < g.Ncols) {
+        atomicAdd(g.stats + 2 * col, csum);
+        atomicAdd(g.stats + 2 * col + 1, csq);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// wgrad: dW[k][(r,s,c)] += sum_p dY[p][k] X(p; r,s,c).  Split-K over pixels (grid z), fp32
+// atomics straight into the PyTorch-layout fp32 gradient [Cout][Cin_real][R][S].
+// LDS images [pixel][channel] (+16 pad); MFMA fragments via ds_read_b64_tr_b16.
+// ---------------------------------------------------------------------------------------
+struct WgradGeom {
+  int N, H, W, C;         // X (input activation, NHWC, C padded)
+  int Ho, Wo, K;          // dY
+  int R, S, st, pad;
+  int Creal;              // real input channels (<= C) of the weight
+  const bf16_t* X;
+  const bf16_t* dY;
+  float* dW;              // [K][Creal][R][S] fp32, accumulated
+  int pix_per_split;
+};
+
+template <int BM_, int BN_>
+__global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradGeom g) {
+  constexpr int LDM = BM_ + 16, LDN = BN_ + 16;
+  constexpr int IT = BM_ / 32, JT = BN_ / 32;
+  constexpr int ACH = BM_ * 64 / 8 / 256, BCH = BN_ * 64 / 8 / 256;  // 16B chunks per thread
+  __shared__ __attribute__((aligned(16))) bf16_t lds[2][64 * LDM + 64 * LDN];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int Ntot = g.R * g.S * g.C;
+  const int P = g.N * g.Ho * g.Wo;
+  const int m0 = blockIdx.y * BM_, n0 = blockIdx.x * BN_;
+  const int p_beg = blockIdx.z * g.pix_per_split, p_end = min(P, p_beg + g.pix_per_split);
+  const int wm = (w >> 1) * (BM_ / 2), wn = (w & 1) * (BN_ / 2);
+  constexpr int ACPR = BM_ / 8, BCPR = BN_ / 8;  // chunks per LDS row
+
+  u32x4 ra[ACH], rb[BCH];
+  auto gload = [&](int p0) {
+#pragma unroll
+    for (int i = 0; i < ACH; ++i) {
+      const int ch = t + 256 * i;
+      const int pr = ch / ACPR, cc = ch % ACPR;
+      const int p = p0 + pr, k = m0 + cc * 8;
+      ra[i] = (p < p_end && k < g.K) ? *reinterpret_cast<const u32x4*>(g.dY + (long)p * g.K + k) : u32x4{0u, 0u, 0u, 0u};
+    }
+#pragma unroll
+    for (int i = 0; i < BCH; ++i) {
+      const int ch = t + 256 * i;
+      const int pr = ch / BCPR, cc = ch % BCPR;
+      const int p = p0 + pr, nn = n0 + cc * 8;
+      u32x4 v = {0u, 0u, 0u, 0u};
+      if (p < p_end && nn < Ntot) {
+        const int tap = nn / g.C, c = nn - tap * g.C;
+        const int r = tap / g.S, s = tap - r * g.S;
+        const int n = p / (g.Ho * g.Wo);
+        const int rem = p - n * g.Ho * g.Wo;
+        const int oh = rem / g.Wo, ow = rem - (rem / g.Wo) * g.Wo;
+        const int ih = oh * g.st - g.pad + r, iw = ow * g.st - g.pad + s;
+        if (ih >= 0 && ih < g.H && iw >= 0 && iw < g.W)
+          v = *reinterpret_cast<const u32x4*>(g.X + (((long)n * g.H + ih) * g.W + iw) * g.C + c);
+      }
+      rb[i] = v;
+    }
+  };
+  auto lstore = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < ACH; ++i) {
+      const int ch = t + 256 * i;
+      *reinterpret_cast<u32x4*>(&lds[buf][(ch / ACPR) * LDM + (ch % ACPR) * 8]) = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < BCH; ++i) {
+      const int ch = t + 256 * i;
+      *reinterpret_cast<u32x4*>(&lds[buf][64 * LDM + (ch / BCPR) * LDN + (ch % BCPR) * 8]) = rb[i];
+    }
+  };
+  // transposed fragment: elements j=0..7 = Img[k0 + 8*(lane>>4) + j][c0 + (lane&15)]
+  auto tr_frag = [&](const bf16_t* img, int ld, int k0, int c0) -> bf16x8 {
+    const int q = (lane & 15) >> 2, p4 = (lane & 3) * 4;
+    const int kr = k0 + 8 * (lane >> 4);
+    typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + (kr + q) * ld + c0 + p4));
+    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + (kr + 4 + q) * ld + c0 + p4));
+    typedef __attribute__((ext_vector_type(8))) short s16x8;
+    s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8, v);
+  };
+
+  f32x4 acc[IT][JT];
+#pragma unroll
+  for (int i = 0; i < IT; ++i)
+#pragma unroll
+    for (int j = 0; j < JT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (p_end - p_beg + 63) / 64;
+  if (nk > 0) {
+    gload(p_beg);
+    lstore(0);
+  }
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) gload(p_beg + (kt + 1) * 64);
+    const bf16_t* Aimg = &lds[cur][0];
+    const bf16_t* Bimg = &lds[cur][64 * LDM];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8 af[IT], bfr[JT];
+#pragma unroll
+      for (int i = 0; i < IT; ++i) af[i] = tr_frag(Aimg, LDM, s * 32, wm + i * 16);
+#pragma unroll
+      for (int j = 0; j < JT; ++j) bfr[j] = tr_frag(Bimg, LDN, s * 32, wn + j * 16);
+#pragma unroll
+      for (int i = 0; i < IT; ++i)
+#pragma unroll
+        for (int j = 0; j < JT; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < nk) lstore(cur ^ 1);
+    __syncthreads();
+  }
+  if (nk == 0) return;
+#pragma unroll
+  for (int i = 0; i < IT; ++i)
+#pragma unroll
+    for (int j = 0; j < JT; ++j) {
+      const int nn = n0 + wn + j * 16 + (lane & 15);
+      if (nn >= Ntot) continue;
+      const int tap = nn / g.C, c = nn - tap * g.C;
+      if (c >= g.Creal) continue;
+      const int r = tap / g.S, s = tap - r * g.S;
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int k = m0 + wm + i * 16 + (lane >> 4) * 4 + rr;
+        if (k < g.K) atomicAdd(g.dW + (((long)k * g.Creal + c) * g.R + r) * g.S + s, acc[i][j][rr]);
+      }
+    }
+}
+
+template <bool DGRAD>
+int launch_conv(ConvGeom& g, hipStream_t st) {
+  const int M = g.N * g.OH * g.OW;
+  if (g.Ncols <= 64) {
+    dim3 grid((g.Ncols + 63) / 64, (M + 127) / 128);
+    hipLaunchKernelGGL((conv_kernel<DGRAD, 128, 64>), grid, dim3(256), 0, st, g);
+  } else {
+    dim3 grid((g.Ncols + 127) / 128, (M + 127) / 128);
+    hipLaunchKernelGGL((conv_kernel<DGRAD, 128, 128>), grid, dim3(256), 0, st, g);
+  }
+  return (int)hipGetLastError();
+}
+
+}  // namespace
+
+MER_API int mer_conv_fwd(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, const void* x,
+                         const void* w_packed, void* y, float* stats, void* stream) {
+  if (C % 8) return (int)hipErrorInvalidValue;
+  ConvGeom g{};
+  g.N = N; g.IH = H; g.IW = W; g.IC = C;
+  g.OH = (H + 2 * pad - R) / stride + 1; g.OW = (W + 2 * pad - S) / stride + 1;
+  g.R = R; g.S = S; g.st = stride; g.pad = pad;
+  g.Ncols = K; g.Kred = R * S * C;
+  g.X = (const bf16_t*)x; g.Wt = (const bf16_t*)w_packed; g.Y = (bf16_t*)y; g.ldy = K; g.stats = stats;
+  return launch_conv<false>(g, (hipStream_t)stream);
+}
+
+MER_API int mer_conv_dgrad(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, const void* dy,
+                           const void* wt_packed, void* dx, const void* residual, const void* residual_mask,
+                           void* stream) {
+  if (K % 8 || C % 8) return (int)hipErrorInvalidValue;
+  ConvGeom g{};
+  g.N = N; g.OH = H; g.OW = W;
+  g.IH = (H + 2 * pad - R) / stride + 1; g.IW = (W + 2 * pad - S) / stride + 1; g.IC = K;
+  g.R = R; g.S = S; g.st = stride; g.pad = pad;
+  g.Ncols = C; g.Kred = R * S * K;
+  g.X = (const bf16_t*)dy; g.Wt = (const bf16_t*)wt_packed; g.Y = (bf16_t*)dx; g.ldy = C; g.stats = nullptr;
+  g.R_ = (const bf16_t*)residual; g.Rmask = (const bf16_t*)residual_mask;
+  return launch_conv<true>(g, (hipStream_t)stream);
+}
+
+MER_API int mer_conv_wgrad(int N, int H, int W, int C, int Creal, int K, int R, int S, int stride, int pad,
+                           const void* x, const void* dy, float* dw, int splits, void* stream) {
+  if (C % 8 || K % 8) return (int)hipErrorInvalidValue;
+  WgradGeom g{};
+  g.N = N; g.H = H; g.W = W; g.C = C; g.Creal = Creal;
+  g.Ho = (H + 2 * pad - R) / stride + 1; g.Wo = (W + 2 * pad - S) / stride + 1; g.K = K;
+  g.R = R; g.S = S; g.st = stride; g.pad = pad;
+  g.X = (const bf16_t*)x; g.dY = (const bf16_t*)dy; g.dW = dw;
+  const int P = N * g.Ho * g.Wo;
+  if (splits < 1) splits = 1;
+  g.pix_per_split = ((P + splits - 1) / splits + 63) / 64 * 64;
+  splits = (P + g.pix_per_split - 1) / g.pix_per_split;
+  const int Ntot = R * S * C;
+  hipStream_t st = (hipStream_t)stream;
+  if (K <= 64) {
+    dim3 grid((Ntot + 127) / 128, (K + 63) / 64, splits);
+    hipLaunchKernelGGL((wgrad_kernel<64, 128>), grid, dim3(256), 0, st, g);
+  } else {
+    dim3 grid((Ntot + 127) / 128, (K + 127) / 128, splits);
+    hipLaunchKernelGGL((wgrad_kernel<128, 128>), grid, dim3(256), 0, st, g);
+  }
+  MER_LAUNCH_CHECK();
+}
+
+// ---------------------------------------------------------------------------------------
+// Packing kernels
+// ---------------------------------------------------------------------------------------
+// video frames NCHW fp32 -> NHWC bf16 with channels zero-padded to Cp
+__global__ void pack_input_kernel(int N, int C, int H, int W, int Cp, const float* __restrict__ x, bf16_t* __restrict__ y) {
+  const long total = (long)N * H * W;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    const int n = e / ((long)H * W);
+    const long hw = e - (long)n * H * W;
+    bf16_t v[16];
+    for (int c = 0; c < Cp; ++c) v[c] = c < C ? f2bf(x[((long)n * C + c) * H * W + hw]) : (bf16_t)0;
+    for (int c = 0; c < Cp; ++c) y[e * Cp + c] = v[c];
+  }
+}
+MER_API int mer_pack_input_nhwc(int N, int C, int H, int W, int Cp, const float* x, void* y, void* stream) {
+  if (Cp > 16 || Cp < C) return (int)hipErrorInvalidValue;
+  const long total = (long)N * H * W;
+  const int grid = (int)((total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192);
+  hipLaunchKernelGGL(pack_input_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, N, C, H, W, Cp, x, (bf16_t*)y);
+  MER_LAUNCH_CHECK();
+}
+
+// PyTorch conv weight [K][C][R][S] fp32 -> fwd [K][R][S][Cp] (transpose=0) or dgrad [Cp][R][S][Kp] (transpose=1)
+__global__ void pack_w_kernel(int K, int C, int R, int S, int Cp, int transpose, const float* __restrict__ w,
+                              bf16_t* __restrict__ out) {
+  const long total = (long)K * R * S * Cp;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    int k, r, s, c;
+    if (!transpose) {
+      c = e % Cp; long q = e / Cp; s = q % S; q /= S; r = q % R; k = q / R;
+    } else {
+      k = e % K; long q = e / K; s = q % S; q /= S; r = q % R; c = q / R;
+    }
+    out[e] = c < C ? f2bf(w[(((long)k * C + c) * R + r) * S + s]) : (bf16_t)0;
+  }
+}
+MER_API int mer_pack_conv_weight(int K, int C, int R, int S, int Cp, int transpose, const float* w, void* out,
+                                 void* stream) {
+  const long total = (long)K * R * S * Cp;
+  const int grid = (int)((total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192);
+  hipLaunchKernelGGL(pack_w_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, K, C, R, S, Cp, transpose, w,
+                     (bf16_t*)out);
+  MER_LAUNCH_CHECK();
+}
+
+// ---------------------------------------------------------------------------------------
+// BatchNorm2d (train mode), channel-last.  stats[c] = (sum, sumsq) over M = N*H*W values.
+// finalize: ms[c] = (mean, rstd); running_mean = (1-mom) rm + mom*mean; running_var uses the
+// unbiased variance (torch semantics); num_batches_tracked += 1.
+// ---------------------------------------------------------------------------------------
+__global__ void bn_finalize_kernel(int C, long M, const float* __restrict__ stats, float eps, float momentum,
+                                   float* __restrict__ ms, float* __restrict__ rmean, float* __restrict__ rvar,
+                                   long long* __restrict__ nbt) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  if (!stats) {  // eval mode: normalise with the running statistics, no update
+    ms[2 * c] = rmean[c];
+    ms[2 * c + 1] = rsqrtf(rvar[c] + eps);
+    return;
+  }
+  const float mean = stats[2 * c] / M;
+  const float var = fmaxf(stats[2 * c + 1] / M - mean * mean, 0.f);
+  ms[2 * c] = mean;
+  ms[2 * c + 1] = rsqrtf(var + eps);
+  if (rmean) rmean[c] = (1.f - momentum) * rmean[c] + momentum * mean;
+  if (rvar) rvar[c] = (1.f - momentum) * rvar[c] + momentum * var * ((float)M / (float)(M > 1 ? M - 1 : 1));
+  if (nbt && c == 0) *nbt += 1;
+}
+MER_API int mer_bn_finalize(int C, long M, const float* stats, float eps, float momentum, float* ms, float* rmean,
+                            float* rvar, long long* num_batches_tracked, void* stream) {
+  if (!stats && (!rmean || !rvar)) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, (hipStream_t)stream, C, M, stats, eps,
+                     momentum, ms, rmean, rvar, num_batches_tracked);
+  MER_LAUNCH_CHECK();
+}
+
+// y = [relu]( bn(x) + (res_bn ? bn2(res) : res) ), 8 channels per thread (C % 8 == 0).
+// ms = (mean, rstd) pairs; eval mode passes (running_mean, 1/sqrt(running_var+eps)) the same way.
+__global__ __launch_bounds__(256) void bn_apply_kernel(long M, int C, const bf16_t* __restrict__ x,
+                                                       const float* __restrict__ ms, const float* __restrict__ gamma,
+                                                       const float* __restrict__ beta, const bf16_t* __restrict__ res,
+                                                       const float* __restrict__ ms2, const float* __restrict__ gamma2,
+                                                       const float* __restrict__ beta2, int relu,
+                                                       bf16_t* __restrict__ y) {
+  const long nvec = M * C / 8;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < nvec; e += (long)gridDim.x * blockDim.x) {
+    const int c0 = (e * 8) % C;
+    const u32x4 xv = *reinterpret_cast<const u32x4*>(x + e * 8);
+    u32x4 rv = {0u, 0u, 0u, 0u};
+    if (res) rv = *reinterpret_cast<const u32x4*>(res + e * 8);
+    const bf16_t* xh = reinterpret_cast<const bf16_t*>(&xv);
+    const bf16_t* rh = reinterpret_cast<const bf16_t*>(&rv);
+    u32x4 ov;
+    bf16_t* oh = reinterpret_cast<bf16_t*>(&ov);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int c = c0 + i;
+      float v = (bf2f(xh[i]) - ms[2 * c]) * ms[2 * c + 1] * gamma[c] + beta[c];
+      if (res) {
+        float r = bf2f(rh[i]);
+        if (ms2) r = (r - ms2[2 * c]) * ms2[2 * c + 1] * gamma2[c] + beta2[c];
+        v += r;
+      }
+      if (relu) v = fmaxf(v, 0.f);
+      oh[i] = f2bf(v);
+    }
+    *reinterpret_cast<u32x4*>(y + e * 8) = ov;
+  }
+}
+MER_API int mer_bn_apply(long M, int C, const void* x, const float* ms, const float* gamma, const float* beta,
+                         const void* res, const float* ms2, const float* gamma2, const float* beta2, int relu, void* y,
+                         void* stream) {
+  if (C % 8) return (int)hipErrorInvalidValue;
+  const long nvec = M * C / 8;
+  const int grid = (int)((nvec + 255) / 256 < 8192 ? (nvec + 255) / 256 : 8192);
+  hipLaunchKernelGGL(bn_apply_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, M, C, (const bf16_t*)x, ms,
+                     gamma, beta, (const bf16_t*)res, ms2, gamma2, beta2, relu, (bf16_t*)y);
+  MER_LAUNCH_CHECK();
+}
+
+// BN backward reduction: g = dy * (mask > 0) (mask = the ReLU output, or null), xhat from x and ms:
+//   red[c] = (sum g, sum g*xhat)   (fp32 atomics, red pre-zeroed).  C <= 512, C % 8 == 0.
+__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(long M, int C, const bf16_t* __restrict__ dy,
+                                                            const bf16_t* __restrict__ mask,
+                                                            const bf16_t* __restrict__ x, const float* __restrict__ ms,
+                                                            float* __restrict__ red, long rows_per_block) {
+  __shared__ float part[2][512];
+  for (int i = threadIdx.x; i < 2 * 512; i += 256) (&part[0][0])[i] = 0.f;
+  __syncthreads();
+  const int cpr = C / 8;                     // 16B chunks per row
+  const int rows_per_iter = 256 / cpr > 0 ? 256 / cpr : 1;
+  const int tc = threadIdx.x % cpr, tr = threadIdx.x / cpr;
+  const long r0 = blockIdx.x * rows_per_block, r1 = min(M, r0 + rows_per_block);
+  float s1[8] = {0.f}, s2[8] = {0.f};
+  if (tr < rows_per_iter) {
+    float mean[8], rstd[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { mean[i] = ms[2 * (tc * 8 + i)]; rstd[i] = ms[2 * (tc * 8 + i) + 1]; }
+    for (long r = r0 + tr; r < r1; r += rows_per_iter) {
+      const long off = r * C + tc * 8;
+      const u32x4 gv = *reinterpret_cast<const u32x4*>(dy + off);
+      const u32x4 xv = *reinterpret_cast<const u32x4*>(x + off);
+      u32x4 mv = {1u, 1u, 1u, 1u};
+      if (mask) mv = *reinterpret_cast<const u32x4*>(mask + off);
+      const bf16_t* gh = reinterpret_cast<const bf16_t*>(&gv);
+      const bf16_t* xh = reinterpret_cast<const bf16_t*>(&xv);
+      const bf16_t* mh = reinterpret_cast<const bf16_t*>(&mv);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float g = (!mask || bf2f(mh[i]) > 0.f) ? bf2f(gh[i]) : 0.f;
+        s1[i] += g;
+        s2[i] += g * (bf2f(xh[i]) - mean[i]) * rstd[i];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      atomicAdd(&part[0][tc * 8 + i], s1[i]);
+      atomicAdd(&part[1][tc * 8 + i], s2[i]);
+    }
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += 256) {
+    atomicAdd(red + 2 * c, part[0][c]);
+    atomicAdd(red + 2 * c + 1, part[1][c]);
+  }
+}
+MER_API int mer_bn_bwd_reduce(long M, int C, const void* dy, const void* mask, const void* x, const float* ms,
+                              float* red, void* stream) {
+  if (C % 8 || C > 512) return (int)hipErrorInvalidValue;
+  const long rpb = 512;
+  const long blocks = (M + rpb - 1) / rpb;
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, M, C,
+                     (const bf16_t*)dy, (const bf16_t*)mask, (const bf16_t*)x, ms, red, rpb);
+  MER_LAUNCH_CHECK();
+}
+
+// dx = gamma*rstd*(g - s1/M - xhat*s2/M) (bf16), and (block 0) dgamma += s2, dbeta += s1.
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(long M, int C, const bf16_t* __restrict__ dy,
+                                                           const bf16_t* __restrict__ mask,
+                                                           const bf16_t* __restrict__ x, const float* __restrict__ ms,
+                                                           const float* __restrict__ gamma,
+                                                           const float* __restrict__ red, bf16_t* __restrict__ dx,
+                                                           float* __restrict__ dgamma, float* __restrict__ dbeta) {
+  if (blockIdx.x == 0) {
+    for (int c = threadIdx.x; c < C; c += 256) {
+      if (dgamma) dgamma[c] += red[2 * c + 1];
+      if (dbeta) dbeta[c] += red[2 * c];
+    }
+  }
+  const long nvec = M * C / 8;
+  const float invM = 1.f / (float)M;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < nvec; e += (long)gridDim.x * blockDim.x) {
+    const int c0 = (e * 8) % C;
+    const u32x4 gv = *reinterpret_cast<const u32x4*>(dy + e * 8);
+    const u32x4 xv = *reinterpret_cast<const u32x4*>(x + e * 8);
+    u32x4 mv = {1u, 1u, 1u, 1u};
+    if (mask) mv = *reinterpret_cast<const u32x4*>(mask + e * 8);
+    const bf16_t* gh = reinterpret_cast<const bf16_t*>(&gv);
+    const bf16_t* xh = reinterpret_cast<const bf16_t*>(&xv);
+    const bf16_t* mh = reinterpret_cast<const bf16_t*>(&mv);
+    u32x4 ov;
+    bf16_t* oh = reinterpret_cast<bf16_t*>(&ov);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int c = c0 + i;
+      const float g = (!mask || bf2f(mh[i]) > 0.f) ? bf2f(gh[i]) : 0.f;
+      const float rs = ms[2 * c + 1];
+      const float xhat = (bf2f(xh[i]) - ms[2 * c]) * rs;
+      oh[i] = f2bf(gamma[c] * rs * (g - red[2 * c] * invM - xhat * red[2 * c + 1] * invM));
+    }
+    *reinterpret_cast<u32x4*>(dx + e * 8) = ov;
+  }
+}
+MER_API int mer_bn_bwd_apply(long M, int C, const void* dy, const void* mask, const void* x, const float* ms,
+                             const float* gamma, const float* red, void* dx, float* dgamma, float* dbeta, void* stream) {
+  if (C % 8) return (int)hipErrorInvalidValue;
+  const long nvec = M * C / 8;
+  const int grid = (int)((nvec + 255) / 256 < 8192 ? (nvec + 255) / 256 : 8192);
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, M, C, (const bf16_t*)dy,
+                     (const bf16_t*)mask, (const bf16_t*)x, ms, gamma, red, (bf16_t*)dx, dgamma, dbeta);
+  MER_LAUNCH_CHECK();
+}
+
+// ---------------------------------------------------------------------------------------
+// MaxPool2d(3, 2, 1) (resnet stem) channel-last, with the argmax tap (0..8) saved for backward.
+// ---------------------------------------------------------------------------------------
+__global__ void maxpool_fwd_kernel(int N, int H, int W, int C, int Ho, int Wo, const bf16_t* __restrict__ x,
+                                   bf16_t* __restrict__ y, uint8_t* __restrict__ arg) {
+  const long total = (long)N * Ho * Wo * C;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    const int c = e % C;
+    long q = e / C;
+    const int ow = q % Wo; q /= Wo;
+    const int oh = q % Ho;
+    const int n = q / Ho;
+    float best = -INFINITY;
+    int bi = 0;
+    for (int r = 0; r < 3; ++r)
+      for (int s = 0; s < 3; ++s) {
+        const int ih = oh * 2 - 1 + r, iw = ow * 2 - 1 + s;
+        if (ih < 0 || ih >= H || iw < 0 || iw >= W) continue;
+        const float v = bf2f(x[(((long)n * H + ih) * W + iw) * C + c]);
+        if (v > best) { best = v; bi = r * 3 + s; }  // first max wins, like torch's CPU kernel
+      }
+    y[e] = f2bf(best);
+    arg[e] = (uint8_t)bi;
+  }
+}
+MER_API int mer_maxpool_fwd(int N, int H, int W, int C, const void* x, void* y, void* argmax, void* stream) {
+  const int Ho = (H + 2 - 3) / 2 + 1, Wo = (W + 2 - 3) / 2 + 1;
+  const long total = (long)N * Ho * Wo * C;
+  const int grid = (int)((total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192);
+  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, N, H, W, C, Ho, Wo,
+                     (const bf16_t*)x, (bf16_t*)y, (uint8_t*)argmax);
+  MER_LAUNCH_CHECK();
+}
+// gather backward: dx[n,h,w,c] = sum of dy over the (<= 4) windows whose argmax is (h,w)
+__global__ void maxpool_bwd_kernel(int N, int H, int W, int C, int Ho, int Wo, const bf16_t* __restrict__ dy,
+                                   const uint8_t* __restrict__ arg, bf16_t* __restrict__ dx) {
+  const long total = (long)N * H * W * C;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    const int c = e % C;
+    long q = e / C;
+    const int w = q % W; q /= W;
+    const int h = q % H;
+    const int n = q / H;
+    float acc = 0.f;
+    for (int oh = (h + 1) / 2 - 1; oh <= (h + 1) / 2; ++oh) {
+      if (oh < 0 || oh >= Ho) continue;
+      const int r = h - (oh * 2 - 1);
+      if (r < 0 || r > 2) continue;
+      for (int ow = (w + 1) / 2 - 1; ow <= (w + 1) / 2; ++ow) {
+        if (ow < 0 || ow >= Wo) continue;
+        const int s = w - (ow * 2 - 1);
+        if (s < 0 || s > 2) continue;
+        const long oi = (((long)n * Ho + oh) * Wo + ow) * C + c;
+        if (arg[oi] == r * 3 + s) acc += bf2f(dy[oi]);
+      }
+    }
+    dx[e] = f2bf(acc);
+  }
+}
+MER_API int mer_maxpool_bwd(int N, int H, int W, int C, const void* dy, const void* argmax, void* dx, void* stream) {
+  const int Ho = (H + 2 - 3) / 2 + 1, Wo = (W + 2 - 3) / 2 + 1;
+  const long total = (long)N * H * W * C;
+  const int grid = (int)((total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192);
+  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, N, H, W, C, Ho, Wo,
+                     (const bf16_t*)dy, (const uint8_t*)argmax, (bf16_t*)dx);
+  MER_LAUNCH_CHECK();
+}
+
+// global average pool (AdaptiveAvgPool2d(1)): NHWC bf16 -> [N, C] fp32; backward broadcasts dy/HW.
+__global__ void avgpool_fwd_kernel(int N, int HW, int C, const bf16_t* __restrict__ x, float* __restrict__ y) {
+  const int n = blockIdx.y, c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float s = 0.f;
+  for (int p = 0; p < HW; ++p) s += bf2f(x[((long)n * HW + p) * C + c]);
+  y[(long)n * C + c] = s / HW;
+}
+__global__ void avgpool_bwd_kernel(int N, int HW, int C, const float* __restrict__ dy, bf16_t* __restrict__ dx) {
+  const long total = (long)N * HW * C;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    const int c = e % C;
+    const long n = e / ((long)HW * C);
+    dx[e] = f2bf(dy[n * C + c] / HW);
+  }
+}
+MER_API int mer_avgpool_fwd(int N, int HW, int C, const void* x, float* y, void* stream) {
+  hipLaunchKernelGGL(avgpool_fwd_kernel, dim3((C + 255) / 256, N), dim3(256), 0, (hipStream_t)stream, N, HW, C,
+                     (const bf16_t*)x, y);
+  MER_LAUNCH_CHECK();
+}
+MER_API int mer_avgpool_bwd(int N, int HW, int C, const float* dy, void* dx, void* stream) {
+  const long total = (long)N * HW * C;
+  const int grid = (int)((total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192);
+  hipLaunchKernelGGL(avgpool_bwd_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, N, HW, C, dy, (bf16_t*)dx);
+  MER_LAUNCH_CHECK();
+}

@@ -270,6 +270,95 @@ def cast_bf16(x, y):
     LIB("mer_cast_bf16", x.numel(), x.data_ptr(), y.data_ptr(), stream_ptr())
 
 
+def conv_fwd(x, wp, y, stats, R, S, stride, pad):
+    N, H, W, C = x.shape
+    Kc = y.shape[-1]
+    Ho, Wo = (H + 2 * pad - R) // stride + 1, (W + 2 * pad - S) // stride + 1
+    if tuple(y.shape) != (N, Ho, Wo, Kc) or tuple(wp.shape) != (Kc, R * S * C):
+        raise ValueError(f"conv_fwd shapes x{tuple(x.shape)} w{tuple(wp.shape)} y{tuple(y.shape)}")
+    LIB("mer_conv_fwd", N, H, W, C, Kc, R, S, stride, pad, x.data_ptr(), wp.data_ptr(), y.data_ptr(), _ptr(stats),
+        stream_ptr())
+
+
+def conv_dgrad(dy, wt, dx, R, S, stride, pad, residual=None, mask=None):
+    N, H, W, C = dx.shape
+    Kc = dy.shape[-1]
+    Ho, Wo = (H + 2 * pad - R) // stride + 1, (W + 2 * pad - S) // stride + 1
+    if tuple(dy.shape) != (N, Ho, Wo, Kc) or tuple(wt.shape) != (C, R * S * Kc):
+        raise ValueError(f"conv_dgrad shapes dy{tuple(dy.shape)} wt{tuple(wt.shape)} dx{tuple(dx.shape)}")
+    LIB("mer_conv_dgrad", N, H, W, C, Kc, R, S, stride, pad, dy.data_ptr(), wt.data_ptr(), dx.data_ptr(),
+        _ptr(residual), _ptr(mask), stream_ptr())
+
+
+def conv_wgrad(x, dy, dw, R, S, stride, pad, creal=None):
+    N, H, W, C = x.shape
+    Kc = dy.shape[-1]
+    Ho, Wo = (H + 2 * pad - R) // stride + 1, (W + 2 * pad - S) // stride + 1
+    creal = C if creal is None else creal
+    if tuple(dy.shape) != (N, Ho, Wo, Kc) or tuple(dw.shape) != (Kc, creal, R, S) or dw.dtype != torch.float32:
+        raise ValueError("conv_wgrad shapes")
+    P = N * Ho * Wo
+    tiles = ((Kc + 127) // 128) * ((R * S * C + 127) // 128)
+    splits = int(max(1, min(P // 512, max(1, 1024 // tiles))))
+    LIB("mer_conv_wgrad", N, H, W, C, creal, Kc, R, S, stride, pad, x.data_ptr(), dy.data_ptr(), dw.data_ptr(),
+        splits, stream_ptr())
+
+
+def pack_input_nhwc(x, y):
+    N, C, H, W = x.shape
+    LIB("mer_pack_input_nhwc", N, C, H, W, y.shape[-1], x.data_ptr(), y.data_ptr(), stream_ptr())
+
+
+def pack_conv_weight(w, out, cp, transpose):
+    Kc, C, R, S = w.shape
+    LIB("mer_pack_conv_weight", Kc, C, R, S, cp, int(transpose), w.data_ptr(), out.data_ptr(), stream_ptr())
+
+
+def bn_finalize(stats, M, eps, momentum, ms, rmean=None, rvar=None, nbt=None):
+    C = ms.shape[0]
+    LIB("mer_bn_finalize", C, int(M), _ptr(stats), float(eps), float(momentum), ms.data_ptr(), _ptr(rmean),
+        _ptr(rvar), _ptr(nbt), stream_ptr())
+
+
+def bn_apply(x, ms, gamma, beta, y, relu, res=None, ms2=None, gamma2=None, beta2=None):
+    C = x.shape[-1]
+    M = x.numel() // C
+    LIB("mer_bn_apply", M, C, x.data_ptr(), ms.data_ptr(), gamma.data_ptr(), beta.data_ptr(), _ptr(res), _ptr(ms2),
+        _ptr(gamma2), _ptr(beta2), int(relu), y.data_ptr(), stream_ptr())
+
+
+def bn_bwd_reduce(dy, mask, x, ms, red):
+    C = x.shape[-1]
+    LIB("mer_bn_bwd_reduce", x.numel() // C, C, dy.data_ptr(), _ptr(mask), x.data_ptr(), ms.data_ptr(),
+        red.data_ptr(), stream_ptr())
+
+
+def bn_bwd_apply(dy, mask, x, ms, gamma, red, dx, dgamma, dbeta):
+    C = x.shape[-1]
+    LIB("mer_bn_bwd_apply", x.numel() // C, C, dy.data_ptr(), _ptr(mask), x.data_ptr(), ms.data_ptr(),
+        gamma.data_ptr(), red.data_ptr(), dx.data_ptr(), _ptr(dgamma), _ptr(dbeta), stream_ptr())
+
+
+def maxpool_fwd(x, y, arg):
+    N, H, W, C = x.shape
+    LIB("mer_maxpool_fwd", N, H, W, C, x.data_ptr(), y.data_ptr(), arg.data_ptr(), stream_ptr())
+
+
+def maxpool_bwd(dy, arg, dx):
+    N, H, W, C = dx.shape
+    LIB("mer_maxpool_bwd", N, H, W, C, dy.data_ptr(), arg.data_ptr(), dx.data_ptr(), stream_ptr())
+
+
+def avgpool_fwd(x, y):
+    N, H, W, C = x.shape
+    LIB("mer_avgpool_fwd", N, H * W, C, x.data_ptr(), y.data_ptr(), stream_ptr())
+
+
+def avgpool_bwd(dy, dx):
+    N, H, W, C = dx.shape
+    LIB("mer_avgpool_bwd", N, H * W, C, dy.data_ptr(), dx.data_ptr(), stream_ptr())
+
+
 def softmax_avg_fwd(za, zv, out, pa, pv):
     B, C = za.shape
     LIB("mer_softmax_avg_fwd", B, C, za.data_ptr(), zv.data_ptr(), out.data_ptr(), pa.data_ptr(), pv.data_ptr(),

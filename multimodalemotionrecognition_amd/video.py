@@ -1,0 +1,277 @@
+"""``VideoNet`` mirror (``src/models/video.py``) with the ResNet18 trunk on HIP kernels.
+
+``backbone`` is an ``nn.Sequential`` with torchvision resnet18's children[:-1] at the same indices
+(0 conv1, 1 bn1, 2 relu, 3 maxpool, 4..7 layer1..4, 8 avgpool), so state-dict keys
+(``video_model.backbone.5.0.downsample.1.running_var`` ...) match reference checkpoints.  Its
+forward is ONE autograd node running the explicit NHWC-bf16 schedule below (implicit-GEMM convs
+with fused BatchNorm statistics, BN-apply(+residual)+ReLU passes, maxpool / avgpool), train-mode
+BatchNorm with running-stat updates, and an explicit reverse schedule for backward.
+Pretrained ImageNet weights are a network fetch in the reference (video.py:21); offline, the
+trunk starts from random init (``pretrained`` is accepted and ignored with a warning).
+"""
+from __future__ import annotations
+
+import warnings
+from typing import List
+
+import torch
+from torch import nn
+
+from . import kernels as K
+from .nn_ops import hip_linear
+from .temporal import TemporalPooler
+
+CP_IN = 8  # RGB padded to 8 channels so one 16-byte im2col chunk = one tap
+
+
+class BasicBlock(nn.Module):
+    expansion = 1
+
+    def __init__(self, inplanes: int, planes: int, stride: int = 1, downsample: nn.Module = None):
+        super().__init__()
+        self.conv1 = nn.Conv2d(inplanes, planes, 3, stride, 1, bias=False)
+        self.bn1 = nn.BatchNorm2d(planes)
+        self.relu = nn.ReLU(inplace=True)
+        self.conv2 = nn.Conv2d(planes, planes, 3, 1, 1, bias=False)
+        self.bn2 = nn.BatchNorm2d(planes)
+        self.downsample = downsample
+        self.stride = stride
+
+
+def _layer(inplanes, planes, stride):
+    ds = None
+    if stride != 1 or inplanes != planes:
+        ds = nn.Sequential(nn.Conv2d(inplanes, planes, 1, stride, bias=False), nn.BatchNorm2d(planes))
+    return nn.Sequential(BasicBlock(inplanes, planes, stride, ds), BasicBlock(planes, planes))
+
+
+def _init_resnet(module: nn.Module) -> None:
+    """torchvision's resnet init: kaiming_normal_(fan_out, relu) convs, BN weight 1 / bias 0."""
+    for m in module.modules():
+        if isinstance(m, nn.Conv2d):
+            nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+        elif isinstance(m, nn.BatchNorm2d):
+            nn.init.constant_(m.weight, 1)
+            nn.init.constant_(m.bias, 0)
+
+
+def _blocks(trunk) -> List[BasicBlock]:
+    return [b for layer in (trunk[4], trunk[5], trunk[6], trunk[7]) for b in layer]
+
+
+def _bn_tensors(bn: nn.BatchNorm2d):
+    return bn.weight, bn.bias
+
+
+class _TrunkFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, trunk, training, *params):
+        feats, saved = trunk_forward(trunk, x, training)
+        ctx.saved, ctx.trunk, ctx.training = saved, trunk, training
+        return feats.view(feats.shape[0], feats.shape[1], 1, 1)
+
+    @staticmethod
+    def backward(ctx, dfeat):
+        grads = trunk_backward(ctx.trunk, ctx.saved, dfeat.reshape(dfeat.shape[0], -1).contiguous().float())
+        params = list(ctx.trunk.parameters())
+        return (None, None, None, *[grads.get(id(q)) for q in params])
+
+
+class ResNet18Trunk(nn.Sequential):
+    """torchvision resnet18 children[:-1] (video.py:21-23) with a HIP forward."""
+
+    def __init__(self):
+        super().__init__(nn.Conv2d(3, 64, 7, 2, 3, bias=False), nn.BatchNorm2d(64), nn.ReLU(inplace=True),
+                         nn.MaxPool2d(3, 2, 1), _layer(64, 64, 1), _layer(64, 128, 2), _layer(128, 256, 2),
+                         _layer(256, 512, 2), nn.AdaptiveAvgPool2d((1, 1)))
+        _init_resnet(self)
+        self._pack_cache = {}
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if not x.is_cuda:
+            raise RuntimeError("ResNet18 trunk runs on the MI355X kernels; move the frames to the GPU")
+        return _TrunkFn.apply(x.contiguous().float(), self, self.training, *self.parameters())
+
+    # ---- bf16 weight packing: per step in training (weights move), cached by version in eval ----
+    def packed(self, conv: nn.Conv2d, cp: int, transpose: bool):
+        w = conv.weight
+        key = (id(conv), transpose)
+        ver = (w.data_ptr(), w._version)
+        hit = self._pack_cache.get(key)
+        if hit is not None and hit[0] == ver:
+            return hit[1]
+        Kc, C, R, S = w.shape
+        if not transpose:
+            out = torch.empty(Kc, R * S * cp, device=w.device, dtype=torch.bfloat16)
+        else:
+            out = torch.empty(cp, R * S * Kc, device=w.device, dtype=torch.bfloat16)
+        K.pack_conv_weight(w.detach(), out, cp, transpose)
+        self._pack_cache[key] = (ver, out)
+        return out
+
+
+def _bn_forward(bn: nn.BatchNorm2d, c: torch.Tensor, stats, training: bool):
+    C = c.shape[-1]
+    ms = torch.empty(C, 2, device=c.device, dtype=torch.float32)
+    M = c.numel() // C
+    if training:
+        mom = 0.1 if bn.momentum is None else bn.momentum
+        K.bn_finalize(stats, M, bn.eps, mom, ms, bn.running_mean, bn.running_var, bn.num_batches_tracked)
+    else:
+        K.bn_finalize(None, M, bn.eps, 0.0, ms, bn.running_mean, bn.running_var)
+    return ms
+
+
+def _conv_bn(trunk, conv, bn, x, stride, pad, training):
+    """conv (+ fused batch stats) -> (conv output, (mean, rstd))."""
+    Kc, _, R, S = conv.weight.shape
+    N, H, W, C = x.shape
+    Ho, Wo = (H + 2 * pad - R) // stride + 1, (W + 2 * pad - S) // stride + 1
+    y = torch.empty(N, Ho, Wo, Kc, device=x.device, dtype=torch.bfloat16)
+    stats = torch.zeros(Kc, 2, device=x.device, dtype=torch.float32) if training else None
+    K.conv_fwd(x, trunk.packed(conv, C, False), y, stats, R, S, stride, pad)
+    return y, _bn_forward(bn, y, stats, training)
+
+
+@torch.no_grad()
+def trunk_forward(trunk: ResNet18Trunk, video: torch.Tensor, training: bool):
+    N, C, H, W = video.shape
+    dev = video.device
+    bf = torch.bfloat16
+    x0 = torch.empty(N, H, W, CP_IN, device=dev, dtype=bf)
+    K.pack_input_nhwc(video, x0)
+    conv1, bn1 = trunk[0], trunk[1]
+    c1, ms1 = _conv_bn(trunk, conv1, bn1, x0, 2, 3, training)
+    a1 = torch.empty_like(c1)
+    K.bn_apply(c1, ms1, bn1.weight, bn1.bias, a1, relu=True)
+    Hp, Wp = (a1.shape[1] - 1) // 2 + 1, (a1.shape[2] - 1) // 2 + 1
+    p1 = torch.empty(N, Hp, Wp, 64, device=dev, dtype=bf)
+    arg = torch.empty(N, Hp, Wp, 64, device=dev, dtype=torch.uint8)
+    K.maxpool_fwd(a1, p1, arg)
+    saved = {"stem": (x0, c1, ms1, a1, arg), "blocks": []}
+    x = p1
+    for blk in _blocks(trunk):
+        s = blk.stride
+        bc1, bms1 = _conv_bn(trunk, blk.conv1, blk.bn1, x, s, 1, training)
+        ba1 = torch.empty_like(bc1)
+        K.bn_apply(bc1, bms1, blk.bn1.weight, blk.bn1.bias, ba1, relu=True)
+        bc2, bms2 = _conv_bn(trunk, blk.conv2, blk.bn2, ba1, 1, 1, training)
+        out = torch.empty_like(bc2)
+        if blk.downsample is not None:
+            cd, msd = _conv_bn(trunk, blk.downsample[0], blk.downsample[1], x, s, 0, training)
+            dbn = blk.downsample[1]
+            K.bn_apply(bc2, bms2, blk.bn2.weight, blk.bn2.bias, out, relu=True, res=cd, ms2=msd, gamma2=dbn.weight,
+                       beta2=dbn.bias)
+        else:
+            cd = msd = None
+            K.bn_apply(bc2, bms2, blk.bn2.weight, blk.bn2.bias, out, relu=True, res=x)
+        saved["blocks"].append((x, bc1, bms1, ba1, bc2, bms2, cd, msd, out))
+        x = out
+    feats = torch.empty(N, x.shape[-1], device=dev, dtype=torch.float32)
+    K.avgpool_fwd(x, feats)
+    saved["final"] = x
+    return feats, saved
+
+
+def _grad(param, grads):
+    from .fusion import grad_buffer
+
+    if not param.requires_grad:
+        return None
+    g = grads.get(id(param))
+    if g is None:
+        g = grad_buffer(param)
+        grads[id(param)] = g
+    return g
+
+
+@torch.no_grad()
+def trunk_backward(trunk: ResNet18Trunk, saved, dfeat: torch.Tensor):
+    grads = {}
+    dev = dfeat.device
+    bf = torch.bfloat16
+    x = saved["final"]
+    dx = torch.empty_like(x)
+    K.avgpool_bwd(dfeat, dx)
+    blocks = _blocks(trunk)
+    for blk, sv in zip(reversed(blocks), reversed(saved["blocks"])):
+        xin, bc1, bms1, ba1, bc2, bms2, cd, msd, out = sv
+        g_out = dx
+        s = blk.stride
+        C2 = bc2.shape[-1]
+        red2 = torch.zeros(C2, 2, device=dev, dtype=torch.float32)
+        K.bn_bwd_reduce(g_out, out, bc2, bms2, red2)
+        dc2 = torch.empty_like(bc2)
+        K.bn_bwd_apply(g_out, out, bc2, bms2, blk.bn2.weight, red2, dc2, _grad(blk.bn2.weight, grads),
+                       _grad(blk.bn2.bias, grads))
+        if cd is not None:
+            dbn = blk.downsample[1]
+            redd = torch.zeros(C2, 2, device=dev, dtype=torch.float32)
+            K.bn_bwd_reduce(g_out, out, cd, msd, redd)
+            dcd = torch.empty_like(cd)
+            K.bn_bwd_apply(g_out, out, cd, msd, dbn.weight, redd, dcd, _grad(dbn.weight, grads), _grad(dbn.bias, grads))
+        # conv2
+        w2 = _grad(blk.conv2.weight, grads)
+        if w2 is not None:
+            K.conv_wgrad(ba1, dc2, w2, 3, 3, 1, 1)
+        da1 = torch.empty_like(ba1)
+        K.conv_dgrad(dc2, trunk.packed(blk.conv2, C2, True), da1, 3, 3, 1, 1)
+        # bn1 (relu mask = ba1)
+        C1 = bc1.shape[-1]
+        red1 = torch.zeros(C1, 2, device=dev, dtype=torch.float32)
+        K.bn_bwd_reduce(da1, ba1, bc1, bms1, red1)
+        dc1 = torch.empty_like(bc1)
+        K.bn_bwd_apply(da1, ba1, bc1, bms1, blk.bn1.weight, red1, dc1, _grad(blk.bn1.weight, grads),
+                       _grad(blk.bn1.bias, grads))
+        # conv1 (+ downsample) -> dx of the block input
+        w1 = _grad(blk.conv1.weight, grads)
+        if w1 is not None:
+            K.conv_wgrad(xin, dc1, w1, 3, 3, s, 1)
+        dxin = torch.empty_like(xin)
+        Cin = xin.shape[-1]
+        if cd is not None:
+            wd = _grad(blk.downsample[0].weight, grads)
+            if wd is not None:
+                K.conv_wgrad(xin, dcd, wd, 1, 1, s, 0)
+            dxd = torch.empty_like(xin)
+            K.conv_dgrad(dcd, trunk.packed(blk.downsample[0], Cin, True), dxd, 1, 1, s, 0)
+            K.conv_dgrad(dc1, trunk.packed(blk.conv1, Cin, True), dxin, 3, 3, s, 1, residual=dxd)
+        else:
+            K.conv_dgrad(dc1, trunk.packed(blk.conv1, Cin, True), dxin, 3, 3, s, 1, residual=g_out, mask=out)
+        dx = dxin
+    # stem: maxpool -> bn1/relu -> conv1 (no data gradient for the frames)
+    x0, c1, ms1, a1, arg = saved["stem"]
+    da1 = torch.empty_like(a1)
+    K.maxpool_bwd(dx, arg, da1)
+    red = torch.zeros(c1.shape[-1], 2, device=dev, dtype=torch.float32)
+    K.bn_bwd_reduce(da1, a1, c1, ms1, red)
+    dc1 = torch.empty_like(c1)
+    K.bn_bwd_apply(da1, a1, c1, ms1, trunk[1].weight, red, dc1, _grad(trunk[1].weight, grads), _grad(trunk[1].bias, grads))
+    w = _grad(trunk[0].weight, grads)
+    if w is not None:
+        K.conv_wgrad(x0, dc1, w, 7, 7, 2, 3, creal=3)
+    return grads
+
+
+class VideoNet(nn.Module):
+    """video.py:10-44 -- same constructor and encode/forward API."""
+
+    def __init__(self, num_classes: int, pretrained: bool = True, temporal_pooling: str = "mean",
+                 temporal_num_heads: int = 4, temporal_num_layers: int = 1, temporal_dropout: float = 0.1) -> None:
+        super().__init__()
+        if pretrained:
+            warnings.warn("ImageNet weights are a network fetch in the reference (video.py:21); building the "
+                          "resnet18 trunk from random init offline")
+        self.backbone = ResNet18Trunk()
+        self.embedding_dim = 512
+        self.temporal_pool = TemporalPooler(self.embedding_dim, temporal_pooling, temporal_num_heads,
+                                            temporal_num_layers, temporal_dropout)
+        self.classifier = nn.Linear(self.embedding_dim, num_classes)
+
+    def encode(self, x: torch.Tensor) -> torch.Tensor:
+        b, t, c, h, w = x.shape
+        feat = self.backbone(x.view(b * t, c, h, w)).view(b, t, self.embedding_dim)
+        return self.temporal_pool(feat)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        return hip_linear(self.encode(x), self.classifier)

@@ -1,0 +1,130 @@
+"""ResNet18 trunk on HIP (NHWC bf16 implicit-GEMM convs, train-mode BatchNorm) vs the fp32 CPU oracle.
+
+The oracle's ResNet18 is a restatement of torchvision's topology (torchvision is absent here:
+parity UNPINNED against the reference package itself).  Kernel-level checks compare
+each conv against torch.nn.functional on the same bf16-rounded operands (tight), the whole trunk
+against the oracle with bf16 tolerances (relative RMS, stated below).
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import params, resnet18_ref
+
+pytestmark = pytest.mark.gpu
+
+REL_RMS_FEAT = 3e-2
+REL_RMS_GRAD = 6e-2
+
+
+def rel_rms(y, ref):
+    y = y.detach().float().cpu()
+    ref = ref.detach().float().cpu()
+    return float((y - ref).pow(2).mean().sqrt() / ref.pow(2).mean().sqrt().clamp_min(1e-12))
+
+
+def to_nhwc(x):
+    return x.permute(0, 2, 3, 1).contiguous()
+
+
+@pytest.mark.parametrize("N,H,C,Kc,R,stride,pad", [
+    (2, 28, 64, 64, 3, 1, 1), (2, 28, 64, 128, 3, 2, 1), (2, 28, 64, 128, 1, 2, 0),
+    (2, 7, 256, 512, 3, 2, 1), (3, 17, 16, 24, 3, 1, 1), (2, 30, 8, 64, 7, 2, 3)])
+def test_conv_fwd_dgrad_wgrad_vs_torch(N, H, C, Kc, R, stride, pad):
+    from multimodalemotionrecognition_amd import kernels as K
+
+    torch.manual_seed(0)
+    x = torch.randn(N, C, H, H).bfloat16().float()
+    w = (torch.randn(Kc, C, R, R) / (C * R * R) ** 0.5).bfloat16().float()
+    x.requires_grad_(True)
+    w.requires_grad_(True)
+    y = F.conv2d(x, w, stride=stride, padding=pad)
+    dy = torch.randn_like(y).bfloat16().float()
+    y.backward(dy)
+    Ho = y.shape[2]
+    xd = to_nhwc(x.detach()).bfloat16().cuda()
+    wp = torch.empty(Kc, R * R * C, device="cuda", dtype=torch.bfloat16)
+    K.pack_conv_weight(w.detach().cuda(), wp, C, False)
+    yd = torch.empty(N, Ho, Ho, Kc, device="cuda", dtype=torch.bfloat16)
+    stats = torch.zeros(Kc, 2, device="cuda")
+    K.conv_fwd(xd, wp, yd, stats, R, R, stride, pad)
+    yr = to_nhwc(y.detach())
+    assert rel_rms(yd, yr) < 1e-2
+    ys = yd.float().cpu()
+    assert torch.allclose(stats[:, 0].cpu(), ys.sum((0, 1, 2)), rtol=1e-3, atol=1e-2)
+    # dgrad
+    wt = torch.empty(C, R * R * Kc, device="cuda", dtype=torch.bfloat16)
+    K.pack_conv_weight(w.detach().cuda(), wt, C, True)
+    dxd = torch.empty(N, H, H, C, device="cuda", dtype=torch.bfloat16)
+    K.conv_dgrad(to_nhwc(dy).bfloat16().cuda(), wt, dxd, R, R, stride, pad)
+    assert rel_rms(dxd, to_nhwc(x.grad)) < 1e-2
+    # wgrad (fp32 PyTorch layout, accumulated)
+    dw = torch.zeros(Kc, C, R, R, device="cuda")
+    K.conv_wgrad(xd, to_nhwc(dy).bfloat16().cuda(), dw, R, R, stride, pad)
+    assert rel_rms(dw, w.grad) < 1e-2
+
+
+def build_trunk(seed=0):
+    from multimodalemotionrecognition_amd.video import ResNet18Trunk
+
+    m = ResNet18Trunk()
+    sd = m.state_dict()
+    names = [(k, tuple(v.shape)) for k, v in sd.items()]
+    assert sorted(("backbone." + k, s) for k, s in names) == sorted(resnet18_ref.param_shapes())
+    new = {k: torch.from_numpy(params.init_tensor("backbone." + k, s, seed)) for k, s in names}
+    m.load_state_dict(new)
+    ref = {"backbone." + k: v.clone() for k, v in new.items()}
+    return m.cuda(), ref
+
+
+@pytest.mark.parametrize("training", [True, False])
+def test_trunk_forward_backward_vs_oracle(training):
+    m, p = build_trunk()
+    m.train(training)
+    video, _, _ = params.clip_inputs(1, frames=4, seed=41)
+    x = torch.from_numpy(video[0])  # [4,3,112,112]
+    for k in p:
+        if p[k].dtype == torch.float32 and not k.endswith(("running_mean", "running_var")):
+            p[k].requires_grad_(True)
+    ref = resnet18_ref.resnet18_trunk(p, x, training=training)
+    y = m(x.cuda())
+    assert tuple(y.shape) == (4, 512, 1, 1)
+    e = rel_rms(y, ref)
+    print("trunk feat rel-rms", e)
+    assert e < REL_RMS_FEAT
+    if training:  # running stats updated like torch (momentum 0.1, unbiased var)
+        for n in ("1.running_mean", "1.running_var", "7.1.bn2.running_var"):
+            assert rel_rms(m.state_dict()[n], p["backbone." + n]) < 2e-2, n
+        assert int(m.state_dict()["1.num_batches_tracked"]) == 1
+    g = torch.randn(4, 512, 1, 1)
+    ref.backward(g)
+    y.backward(g.cuda())
+    worst = 0.0
+    for n, q in m.named_parameters():
+        r = p["backbone." + n].grad
+        e = rel_rms(q.grad, r)
+        worst = max(worst, e)
+        assert e < REL_RMS_GRAD, (n, e)
+    print("trunk worst grad rel-rms", worst)
+
+
+def test_maxpool_avgpool_kernels():
+    from multimodalemotionrecognition_amd import kernels as K
+
+    torch.manual_seed(0)
+    x = torch.randn(2, 8, 9, 9).bfloat16().float().requires_grad_(True)
+    y = F.max_pool2d(x, 3, 2, 1)
+    dy = torch.randn_like(y).bfloat16().float()
+    y.backward(dy)
+    xd = to_nhwc(x.detach()).bfloat16().cuda()
+    yd = torch.empty(2, 5, 5, 8, device="cuda", dtype=torch.bfloat16)
+    arg = torch.empty(2, 5, 5, 8, device="cuda", dtype=torch.uint8)
+    K.maxpool_fwd(xd, yd, arg)
+    assert torch.equal(yd.float().cpu(), to_nhwc(y.detach()))
+    dxd = torch.empty_like(xd)
+    K.maxpool_bwd(to_nhwc(dy).bfloat16().cuda(), arg, dxd)
+    assert rel_rms(dxd, to_nhwc(x.grad)) < 1e-2
+    feats = torch.empty(2, 8, device="cuda")
+    K.avgpool_fwd(xd, feats)
+    assert torch.allclose(feats.cpu(), x.detach().mean((2, 3)), atol=1e-3)
