@@ -199,9 +199,11 @@ int mer_bn_apply(long M, int C, const void* x, const float* ms, const float* gam
 int mer_bn_bwd_reduce(long M, int C, const void* dy, const void* mask, const void* x, const float* ms, float* red,
                       void* stream);
 
-/* BN backward apply: dx = gamma*rstd*(g - s1/M - xhat*s2/M) (bf16); dgamma += s2, dbeta += s1. */
+/* BN backward apply: dx = gamma*rstd*(g - s1/M - xhat*s2/M) with batch statistics (batch_stats=1, train
+ * mode) or dx = gamma*rstd*g with running statistics (batch_stats=0, eval mode); dgamma += s2, dbeta += s1. */
 int mer_bn_bwd_apply(long M, int C, const void* dy, const void* mask, const void* x, const float* ms,
-                     const float* gamma, const float* red, void* dx, float* dgamma, float* dbeta, void* stream);
+                     const float* gamma, const float* red, int batch_stats, void* dx, float* dgamma, float* dbeta,
+                     void* stream);
 
 /* MaxPool2d(3, 2, 1) forward (argmax tap saved as uint8) and gather backward. */
 int mer_maxpool_fwd(int N, int H, int W, int C, const void* x, void* y, void* argmax, void* stream);

@@ -546,8 +546,9 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(long M, int C, const 
                                                            const bf16_t* __restrict__ mask,
                                                            const bf16_t* __restrict__ x, const float* __restrict__ ms,
                                                            const float* __restrict__ gamma,
-                                                           const float* __restrict__ red, bf16_t* __restrict__ dx,
-                                                           float* __restrict__ dgamma, float* __restrict__ dbeta) {
+                                                           const float* __restrict__ red, int batch_stats,
+                                                           bf16_t* __restrict__ dx, float* __restrict__ dgamma,
+                                                           float* __restrict__ dbeta) {
   if (blockIdx.x == 0) {
     for (int c = threadIdx.x; c < C; c += 256) {
       if (dgamma) dgamma[c] += red[2 * c + 1];
@@ -573,18 +574,22 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(long M, int C, const 
       const float g = (!mask || bf2f(mh[i]) > 0.f) ? bf2f(gh[i]) : 0.f;
       const float rs = ms[2 * c + 1];
       const float xhat = (bf2f(xh[i]) - ms[2 * c]) * rs;
-      oh[i] = f2bf(gamma[c] * rs * (g - red[2 * c] * invM - xhat * red[2 * c + 1] * invM));
+      // batch statistics (train): the mean/var terms carry gradient; running stats (eval): they do not
+      oh[i] = f2bf(batch_stats ? gamma[c] * rs * (g - red[2 * c] * invM - xhat * red[2 * c + 1] * invM)
+                               : gamma[c] * rs * g);
     }
     *reinterpret_cast<u32x4*>(dx + e * 8) = ov;
   }
 }
 MER_API int mer_bn_bwd_apply(long M, int C, const void* dy, const void* mask, const void* x, const float* ms,
-                             const float* gamma, const float* red, void* dx, float* dgamma, float* dbeta, void* stream) {
+                             const float* gamma, const float* red, int batch_stats, void* dx, float* dgamma,
+                             float* dbeta, void* stream) {
   if (C % 8) return (int)hipErrorInvalidValue;
   const long nvec = M * C / 8;
   const int grid = (int)((nvec + 255) / 256 < 8192 ? (nvec + 255) / 256 : 8192);
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, M, C, (const bf16_t*)dy,
-                     (const bf16_t*)mask, (const bf16_t*)x, ms, gamma, red, (bf16_t*)dx, dgamma, dbeta);
+                     (const bf16_t*)mask, (const bf16_t*)x, ms, gamma, red, batch_stats, (bf16_t*)dx, dgamma,
+                     dbeta);
   MER_LAUNCH_CHECK();
 }
 

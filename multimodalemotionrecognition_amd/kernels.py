@@ -333,10 +333,10 @@ def bn_bwd_reduce(dy, mask, x, ms, red):
         red.data_ptr(), stream_ptr())
 
 
-def bn_bwd_apply(dy, mask, x, ms, gamma, red, dx, dgamma, dbeta):
+def bn_bwd_apply(dy, mask, x, ms, gamma, red, dx, dgamma, dbeta, batch_stats=True):
     C = x.shape[-1]
     LIB("mer_bn_bwd_apply", x.numel() // C, C, dy.data_ptr(), _ptr(mask), x.data_ptr(), ms.data_ptr(),
-        gamma.data_ptr(), red.data_ptr(), dx.data_ptr(), _ptr(dgamma), _ptr(dbeta), stream_ptr())
+        gamma.data_ptr(), red.data_ptr(), int(batch_stats), dx.data_ptr(), _ptr(dgamma), _ptr(dbeta), stream_ptr())
 
 
 def maxpool_fwd(x, y, arg):

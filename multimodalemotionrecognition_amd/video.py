@@ -72,7 +72,8 @@ class _TrunkFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dfeat):
-        grads = trunk_backward(ctx.trunk, ctx.saved, dfeat.reshape(dfeat.shape[0], -1).contiguous().float())
+        grads = trunk_backward(ctx.trunk, ctx.saved, dfeat.reshape(dfeat.shape[0], -1).contiguous().float(),
+                               ctx.training)
         params = list(ctx.trunk.parameters())
         return (None, None, None, *[grads.get(id(q)) for q in params])
 
@@ -134,6 +135,26 @@ def _conv_bn(trunk, conv, bn, x, stride, pad, training):
 
 
 @torch.no_grad()
+def block_forward(trunk, blk: BasicBlock, x: torch.Tensor, training: bool):
+    """BasicBlock (torchvision): relu(bn2(conv2(relu(bn1(conv1(x))))) + [bn_d(conv_d(x)) | x])."""
+    s = blk.stride
+    bc1, bms1 = _conv_bn(trunk, blk.conv1, blk.bn1, x, s, 1, training)
+    ba1 = torch.empty_like(bc1)
+    K.bn_apply(bc1, bms1, blk.bn1.weight, blk.bn1.bias, ba1, relu=True)
+    bc2, bms2 = _conv_bn(trunk, blk.conv2, blk.bn2, ba1, 1, 1, training)
+    out = torch.empty_like(bc2)
+    if blk.downsample is not None:
+        cd, msd = _conv_bn(trunk, blk.downsample[0], blk.downsample[1], x, s, 0, training)
+        dbn = blk.downsample[1]
+        K.bn_apply(bc2, bms2, blk.bn2.weight, blk.bn2.bias, out, relu=True, res=cd, ms2=msd, gamma2=dbn.weight,
+                   beta2=dbn.bias)
+    else:
+        cd = msd = None
+        K.bn_apply(bc2, bms2, blk.bn2.weight, blk.bn2.bias, out, relu=True, res=x)
+    return out, (x, bc1, bms1, ba1, bc2, bms2, cd, msd, out)
+
+
+@torch.no_grad()
 def trunk_forward(trunk: ResNet18Trunk, video: torch.Tensor, training: bool):
     N, C, H, W = video.shape
     dev = video.device
@@ -151,22 +172,8 @@ def trunk_forward(trunk: ResNet18Trunk, video: torch.Tensor, training: bool):
     saved = {"stem": (x0, c1, ms1, a1, arg), "blocks": []}
     x = p1
     for blk in _blocks(trunk):
-        s = blk.stride
-        bc1, bms1 = _conv_bn(trunk, blk.conv1, blk.bn1, x, s, 1, training)
-        ba1 = torch.empty_like(bc1)
-        K.bn_apply(bc1, bms1, blk.bn1.weight, blk.bn1.bias, ba1, relu=True)
-        bc2, bms2 = _conv_bn(trunk, blk.conv2, blk.bn2, ba1, 1, 1, training)
-        out = torch.empty_like(bc2)
-        if blk.downsample is not None:
-            cd, msd = _conv_bn(trunk, blk.downsample[0], blk.downsample[1], x, s, 0, training)
-            dbn = blk.downsample[1]
-            K.bn_apply(bc2, bms2, blk.bn2.weight, blk.bn2.bias, out, relu=True, res=cd, ms2=msd, gamma2=dbn.weight,
-                       beta2=dbn.bias)
-        else:
-            cd = msd = None
-            K.bn_apply(bc2, bms2, blk.bn2.weight, blk.bn2.bias, out, relu=True, res=x)
-        saved["blocks"].append((x, bc1, bms1, ba1, bc2, bms2, cd, msd, out))
-        x = out
+        x, sv = block_forward(trunk, blk, x, training)
+        saved["blocks"].append(sv)
     feats = torch.empty(N, x.shape[-1], device=dev, dtype=torch.float32)
     K.avgpool_fwd(x, feats)
     saved["final"] = x
@@ -186,7 +193,57 @@ def _grad(param, grads):
 
 
 @torch.no_grad()
-def trunk_backward(trunk: ResNet18Trunk, saved, dfeat: torch.Tensor):
+def block_backward(trunk, blk: BasicBlock, sv, dx: torch.Tensor, grads, training: bool = True):
+    """Reverse of block_forward given dx = dL/d(block output); returns dL/d(block input)."""
+    dev = dx.device
+    xin, bc1, bms1, ba1, bc2, bms2, cd, msd, out = sv
+    g_out = dx
+    s = blk.stride
+    C2 = bc2.shape[-1]
+    red2 = torch.zeros(C2, 2, device=dev, dtype=torch.float32)
+    K.bn_bwd_reduce(g_out, out, bc2, bms2, red2)
+    dc2 = torch.empty_like(bc2)
+    K.bn_bwd_apply(g_out, out, bc2, bms2, blk.bn2.weight, red2, dc2, _grad(blk.bn2.weight, grads),
+                   _grad(blk.bn2.bias, grads), training)
+    if cd is not None:
+        dbn = blk.downsample[1]
+        redd = torch.zeros(C2, 2, device=dev, dtype=torch.float32)
+        K.bn_bwd_reduce(g_out, out, cd, msd, redd)
+        dcd = torch.empty_like(cd)
+        K.bn_bwd_apply(g_out, out, cd, msd, dbn.weight, redd, dcd, _grad(dbn.weight, grads), _grad(dbn.bias, grads), training)
+    # conv2
+    w2 = _grad(blk.conv2.weight, grads)
+    if w2 is not None:
+        K.conv_wgrad(ba1, dc2, w2, 3, 3, 1, 1)
+    da1 = torch.empty_like(ba1)
+    K.conv_dgrad(dc2, trunk.packed(blk.conv2, C2, True), da1, 3, 3, 1, 1)
+    # bn1 (relu mask = ba1)
+    C1 = bc1.shape[-1]
+    red1 = torch.zeros(C1, 2, device=dev, dtype=torch.float32)
+    K.bn_bwd_reduce(da1, ba1, bc1, bms1, red1)
+    dc1 = torch.empty_like(bc1)
+    K.bn_bwd_apply(da1, ba1, bc1, bms1, blk.bn1.weight, red1, dc1, _grad(blk.bn1.weight, grads),
+                   _grad(blk.bn1.bias, grads), training)
+    # conv1 (+ downsample) -> dx of the block input
+    w1 = _grad(blk.conv1.weight, grads)
+    if w1 is not None:
+        K.conv_wgrad(xin, dc1, w1, 3, 3, s, 1)
+    dxin = torch.empty_like(xin)
+    Cin = xin.shape[-1]
+    if cd is not None:
+        wd = _grad(blk.downsample[0].weight, grads)
+        if wd is not None:
+            K.conv_wgrad(xin, dcd, wd, 1, 1, s, 0)
+        dxd = torch.empty_like(xin)
+        K.conv_dgrad(dcd, trunk.packed(blk.downsample[0], Cin, True), dxd, 1, 1, s, 0)
+        K.conv_dgrad(dc1, trunk.packed(blk.conv1, Cin, True), dxin, 3, 3, s, 1, residual=dxd)
+    else:
+        K.conv_dgrad(dc1, trunk.packed(blk.conv1, Cin, True), dxin, 3, 3, s, 1, residual=g_out, mask=out)
+    return dxin
+
+
+@torch.no_grad()
+def trunk_backward(trunk: ResNet18Trunk, saved, dfeat: torch.Tensor, training: bool = True):
     grads = {}
     dev = dfeat.device
     bf = torch.bfloat16
@@ -195,50 +252,7 @@ def trunk_backward(trunk: ResNet18Trunk, saved, dfeat: torch.Tensor):
     K.avgpool_bwd(dfeat, dx)
     blocks = _blocks(trunk)
     for blk, sv in zip(reversed(blocks), reversed(saved["blocks"])):
-        xin, bc1, bms1, ba1, bc2, bms2, cd, msd, out = sv
-        g_out = dx
-        s = blk.stride
-        C2 = bc2.shape[-1]
-        red2 = torch.zeros(C2, 2, device=dev, dtype=torch.float32)
-        K.bn_bwd_reduce(g_out, out, bc2, bms2, red2)
-        dc2 = torch.empty_like(bc2)
-        K.bn_bwd_apply(g_out, out, bc2, bms2, blk.bn2.weight, red2, dc2, _grad(blk.bn2.weight, grads),
-                       _grad(blk.bn2.bias, grads))
-        if cd is not None:
-            dbn = blk.downsample[1]
-            redd = torch.zeros(C2, 2, device=dev, dtype=torch.float32)
-            K.bn_bwd_reduce(g_out, out, cd, msd, redd)
-            dcd = torch.empty_like(cd)
-            K.bn_bwd_apply(g_out, out, cd, msd, dbn.weight, redd, dcd, _grad(dbn.weight, grads), _grad(dbn.bias, grads))
-        # conv2
-        w2 = _grad(blk.conv2.weight, grads)
-        if w2 is not None:
-            K.conv_wgrad(ba1, dc2, w2, 3, 3, 1, 1)
-        da1 = torch.empty_like(ba1)
-        K.conv_dgrad(dc2, trunk.packed(blk.conv2, C2, True), da1, 3, 3, 1, 1)
-        # bn1 (relu mask = ba1)
-        C1 = bc1.shape[-1]
-        red1 = torch.zeros(C1, 2, device=dev, dtype=torch.float32)
-        K.bn_bwd_reduce(da1, ba1, bc1, bms1, red1)
-        dc1 = torch.empty_like(bc1)
-        K.bn_bwd_apply(da1, ba1, bc1, bms1, blk.bn1.weight, red1, dc1, _grad(blk.bn1.weight, grads),
-                       _grad(blk.bn1.bias, grads))
-        # conv1 (+ downsample) -> dx of the block input
-        w1 = _grad(blk.conv1.weight, grads)
-        if w1 is not None:
-            K.conv_wgrad(xin, dc1, w1, 3, 3, s, 1)
-        dxin = torch.empty_like(xin)
-        Cin = xin.shape[-1]
-        if cd is not None:
-            wd = _grad(blk.downsample[0].weight, grads)
-            if wd is not None:
-                K.conv_wgrad(xin, dcd, wd, 1, 1, s, 0)
-            dxd = torch.empty_like(xin)
-            K.conv_dgrad(dcd, trunk.packed(blk.downsample[0], Cin, True), dxd, 1, 1, s, 0)
-            K.conv_dgrad(dc1, trunk.packed(blk.conv1, Cin, True), dxin, 3, 3, s, 1, residual=dxd)
-        else:
-            K.conv_dgrad(dc1, trunk.packed(blk.conv1, Cin, True), dxin, 3, 3, s, 1, residual=g_out, mask=out)
-        dx = dxin
+        dx = block_backward(trunk, blk, sv, dx, grads, training)
     # stem: maxpool -> bn1/relu -> conv1 (no data gradient for the frames)
     x0, c1, ms1, a1, arg = saved["stem"]
     da1 = torch.empty_like(a1)
@@ -246,7 +260,8 @@ def trunk_backward(trunk: ResNet18Trunk, saved, dfeat: torch.Tensor):
     red = torch.zeros(c1.shape[-1], 2, device=dev, dtype=torch.float32)
     K.bn_bwd_reduce(da1, a1, c1, ms1, red)
     dc1 = torch.empty_like(c1)
-    K.bn_bwd_apply(da1, a1, c1, ms1, trunk[1].weight, red, dc1, _grad(trunk[1].weight, grads), _grad(trunk[1].bias, grads))
+    K.bn_bwd_apply(da1, a1, c1, ms1, trunk[1].weight, red, dc1, _grad(trunk[1].weight, grads), _grad(trunk[1].bias, grads),
+                   training)
     w = _grad(trunk[0].weight, grads)
     if w is not None:
         K.conv_wgrad(x0, dc1, w, 7, 7, 2, 3, creal=3)
