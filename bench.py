@@ -1,0 +1,169 @@
+"""North-star benchmark: 3 s-clip train steps/s (B=32 per GPU, xattn fusion) on MI355X.
+
+    python bench.py --gpus N --steps K --warmup W
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+One step = the full reference train step (src/train.py:200-228) of FusionModel(mode='xattn') with
+WavLM-base (frozen, forward) + ResNet18 trunk (train-mode BN, forward+backward) + xattn head
+(forward+backward) + CrossEntropy + Adam, on one B=32 batch of synthetic 3 s clips
+([32,8,3,112,112] frames, [32,1,48000] waveform) resident in HBM.  Weak scaling: each rank runs
+B=32; `value` = steps completed by all ranks / wall time (max over ranks).
+
+Extra fields: `roofline` for the dominant kernel (HIP events around its launches inside the timed
+region) and `cpu_baseline` (the fp32 CPU oracle of the same step, rank 0, N=1, bounded sample).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import torch
+import torch.distributed as dist
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+from multimodalemotionrecognition_amd import kernels as K  # noqa: E402
+from multimodalemotionrecognition_amd.dist import GradAllReduce, init_distributed, is_dist  # noqa: E402
+from multimodalemotionrecognition_amd.train import TrainStep, build_model, build_optimizer, make_loss  # noqa: E402
+
+BATCH, FRAMES, SIZE, SAMPLES, CLASSES = 32, 8, 112, 48000, 8
+PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, spec)
+PEAK_HBM_GBS = 8000.0       # HBM3E spec
+# Dominant kernel (largest share of step time in profiles/): the WavLM feature-extractor conv1 as an
+# implicit GEMM: M = B*4799 output frames, N = 512 channels, K = 3 taps * 512.
+PROBE = ("gemm_bf16", (BATCH * 4799, 512, 1536))
+
+
+def synthetic_batch(device, seed):
+    """ravdess.py:386-389,505-513 layouts: ImageNet-normalised frames, waveform in [-1,1], labels."""
+    g = torch.Generator(device=device).manual_seed(seed)
+    mean = torch.tensor([0.485, 0.456, 0.406], device=device).view(1, 1, 3, 1, 1)
+    std = torch.tensor([0.229, 0.224, 0.225], device=device).view(1, 1, 3, 1, 1)
+    video = (torch.rand(BATCH, FRAMES, 3, SIZE, SIZE, device=device, generator=g) - mean) / std
+    audio = (0.1 * torch.randn(BATCH, 1, SAMPLES, device=device, generator=g)).clamp_(-1, 1)
+    labels = torch.randint(0, CLASSES, (BATCH,), device=device, generator=g)
+    return video.contiguous(), audio.contiguous(), labels
+
+
+def cpu_baseline(threads: int, steps: int = 2):
+    """The fp32 CPU oracle of the same train step at B=32 (test infrastructure, timed as the baseline)."""
+    from oracle import params as OP
+    from oracle import fusion_ref, resnet18_ref, train_ref, wavlm_ref
+
+    torch.set_num_threads(threads)
+    shapes = [("video_model." + n, s) for n, s in resnet18_ref.param_shapes()]
+    shapes += [("audio_model.wavlm." + n, s) for n, s in wavlm_ref.wavlm_param_shapes()]
+    shapes += fusion_ref.xattn_head_param_shapes()
+    p = {k: torch.from_numpy(v) for k, v in OP.init_state(shapes).items()}
+    trainable = [k for k in p if (k.startswith("video_model.") and not k.endswith(
+        ("running_mean", "running_var", "num_batches_tracked"))) or
+        (not k.startswith(("video_model.", "audio_model.")) and not k.startswith("audio_time_conv"))]
+    for k in trainable:
+        p[k].requires_grad_(True)
+    opt = train_ref.AdamRef([p[k] for k in trainable], lr=1e-3, weight_decay=1e-4)
+    video, audio, labels = OP.clip_inputs(BATCH)
+    video, audio, labels = torch.from_numpy(video), torch.from_numpy(audio), torch.from_numpy(labels)
+    train_ref.train_step(p, trainable, opt, video, audio, labels)  # warm-up
+    t = time.perf_counter()
+    for _ in range(steps):
+        train_ref.train_step(p, trainable, opt, video, audio, labels)
+    dt = (time.perf_counter() - t) / steps
+    return {"value": round(1.0 / dt, 4), "unit": "steps/s", "cores": threads, "kind": "port",
+            "sample": f"{steps} timed steps (+1 warm-up) of the fp32 oracle train step at B=32 "
+                      f"({dt:.2f} s/step, {BATCH / dt:.2f} clips/s), torch CPU eager, {threads} threads"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    args = ap.parse_args()
+
+    world, rank, local = init_distributed()
+    dev = torch.device("cuda", local)
+    torch.manual_seed(1234)  # identical init on every rank
+    model = build_model(CLASSES, "xattn", pretrained_video=False, use_wavlm=True).to(dev)
+    opt = build_optimizer(model, lr=1e-3, weight_decay=1e-4)
+    step = TrainStep(model, opt, make_loss("xattn"), "xattn", GradAllReduce(opt) if is_dist() else None)
+    video, audio, labels = synthetic_batch(dev, 20261015 + rank)
+
+    for _ in range(args.warmup):
+        step(video, audio, labels)
+    torch.cuda.synchronize()
+
+    probe = K.KernelProbe(PROBE[0], PROBE[1], units=2.0 * PROBE[1][0] * PROBE[1][1] * PROBE[1][2])
+    probe.active = True
+    K.PROBE = probe
+    if is_dist():
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    loss = None
+    for _ in range(args.steps):
+        loss, _ = step(video, audio, labels)
+    torch.cuda.synchronize()
+    if is_dist():
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    probe.active = False
+    K.PROBE = None
+
+    t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+    if is_dist():
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    if rank != 0:
+        if is_dist():
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+
+    kms = probe.avg_ms()
+    roof = None
+    if kms:
+        achieved = probe.units / (kms * 1e-3) / 1e12
+        roof = {"bound": "mfma", "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None,
+                "kernel": f"gemm_bf16_kernel<0,bf16> (WavLM conv1 implicit GEMM {PROBE[1][0]}x{PROBE[1][1]}x{PROBE[1][2]})",
+                "avg_ms": round(kms, 4), "launches": len(probe.pairs)}
+    out = {
+        "metric": "3s-clip train steps/sec (B=32, xattn fusion) at 1/2/4/8 MI355X",
+        "value": round(world * args.steps / elapsed, 3),
+        "unit": "steps/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "bf16",
+        "data": "synthetic (seeded 3 s clips resident in HBM; random-init weights)",
+        "config": {"workload": "ResNet18 + WavLM-base (frozen) + xattn fusion train step (fwd+bwd+Adam)",
+                   "per_gpu_batch": BATCH, "global_batch": BATCH * world, "frames": FRAMES, "image": SIZE,
+                   "audio_samples": SAMPLES, "parallelism": f"dp{world}"},
+        "clips_per_s": round(world * BATCH * args.steps / elapsed, 1),
+        "final_loss": round(float(loss), 4) if loss is not None else None,
+        "roofline": roof,
+        "cpu_baseline": None,
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+        out["cpu_baseline"] = cpu_baseline(threads)
+    print(json.dumps(out), flush=True)
+    if is_dist():
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

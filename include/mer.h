@@ -109,9 +109,10 @@ int mer_softmax_avg_bwd(int B, int C, const float* pa, const float* pv, const fl
 int mer_vec_sum(int n, const float* x, float* out, int accumulate, void* stream);
 
 /* torch.optim.Adam step (train.py:872,902; L2 weight decay added to the gradient) over one flat fp32
- * buffer; `step` is the 1-based step count used for bias correction.  16-byte aligned buffers. */
+ * buffer; `step` is the 1-based step count used for bias correction; the gradient is multiplied by
+ * grad_scale first (1/world_size after a SUM all-reduce).  16-byte aligned buffers. */
 int mer_adam_step(long n, float* p, const float* g, float* m, float* v, float lr, float b1, float b2, float eps,
-                  float wd, int step, void* stream);
+                  float wd, int step, float grad_scale, void* stream);
 
 /* ============================ encoders (bf16 MFMA) ============================ */
 

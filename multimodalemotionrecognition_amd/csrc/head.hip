@@ -715,7 +715,8 @@ MER_API int mer_vec_sum(int n, const float* x, float* out, int accumulate, void*
 // ---------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void adam_kernel(long n, float* __restrict__ p, const float* __restrict__ g,
                                                    float* __restrict__ m, float* __restrict__ v, float lr, float b1,
-                                                   float b2, float eps, float wd, float bc1, float bc2_sqrt) {
+                                                   float b2, float eps, float wd, float bc1, float bc2_sqrt,
+                                                   float gscale) {
   const long n4 = n / 4;
   const float step = lr / bc1;
   for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < n4; e += (long)gridDim.x * blockDim.x) {
@@ -725,7 +726,7 @@ __global__ __launch_bounds__(256) void adam_kernel(long n, float* __restrict__ p
     float4 vv = reinterpret_cast<float4*>(v)[e];
 #define ADAM1(c)                                                  \
   {                                                               \
-    const float gr = gg.c + wd * pp.c;                            \
+    const float gr = gscale * gg.c + wd * pp.c;                   \
     mm.c = b1 * mm.c + (1.f - b1) * gr;                           \
     vv.c = b2 * vv.c + (1.f - b2) * gr * gr;                      \
     pp.c -= step * mm.c / (sqrtf(vv.c) / bc2_sqrt + eps);         \
@@ -737,14 +738,14 @@ __global__ __launch_bounds__(256) void adam_kernel(long n, float* __restrict__ p
     reinterpret_cast<float4*>(v)[e] = vv;
   }
   for (long e = n4 * 4 + blockIdx.x * (long)blockDim.x + threadIdx.x; e < n; e += (long)gridDim.x * blockDim.x) {
-    const float gr = g[e] + wd * p[e];
+    const float gr = gscale * g[e] + wd * p[e];
     m[e] = b1 * m[e] + (1.f - b1) * gr;
     v[e] = b2 * v[e] + (1.f - b2) * gr * gr;
     p[e] -= step * m[e] / (sqrtf(v[e]) / bc2_sqrt + eps);
   }
 }
 MER_API int mer_adam_step(long n, float* p, const float* g, float* m, float* v, float lr, float b1, float b2, float eps,
-                          float wd, int step, void* stream) {
+                          float wd, int step, float grad_scale, void* stream) {
   if (n <= 0) return 0;
   if (((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) return (int)hipErrorInvalidValue;
   const float bc1 = 1.f - powf(b1, (float)step);
@@ -752,7 +753,7 @@ MER_API int mer_adam_step(long n, float* p, const float* g, float* m, float* v, 
   const long n4 = (n + 3) / 4;
   const int grid = (int)((n4 + 255) / 256 < 2048 ? (n4 + 255) / 256 : 2048);
   hipLaunchKernelGGL(adam_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, n, p, g, m, v, lr, b1, b2, eps, wd,
-                     bc1, bc2s);
+                     bc1, bc2s, grad_scale);
   MER_LAUNCH_CHECK();
 }
 

@@ -19,6 +19,39 @@ def stream_ptr() -> int:
     return torch.cuda.current_stream().cuda_stream
 
 
+class KernelProbe:
+    """Brackets launches of ONE kernel (by name + shape key) with HIP events on the launching stream, so
+    bench.py can report that kernel's average device time inside the timed region."""
+
+    def __init__(self, name: str, key: tuple, units: float):
+        self.name, self.key, self.units = name, tuple(key), units  # units = algorithmic FLOP or bytes / launch
+        self.pairs = []
+        self.active = False
+
+    def matches(self, name, key):
+        return self.active and name == self.name and tuple(key) == self.key
+
+    def avg_ms(self):
+        if not self.pairs:
+            return None
+        return sum(a.elapsed_time(b) for a, b in self.pairs) / len(self.pairs)
+
+
+PROBE = None
+
+
+def _launch(name, key, fn, *args):
+    if PROBE is not None and PROBE.matches(name, key):
+        s = torch.cuda.current_stream()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(s)
+        LIB(fn, *args)
+        b.record(s)
+        PROBE.pairs.append((a, b))
+    else:
+        LIB(fn, *args)
+
+
 def _dt(t: torch.Tensor) -> int:
     if t.dtype == torch.float32:
         return F32
@@ -193,9 +226,9 @@ def vec_sum(x, out, accumulate=False):
     LIB("mer_vec_sum", x.numel(), x.data_ptr(), out.data_ptr(), int(accumulate), stream_ptr())
 
 
-def adam_step(p, g, m, v, lr, b1, b2, eps, wd, step):
+def adam_step(p, g, m, v, lr, b1, b2, eps, wd, step, grad_scale=1.0):
     LIB("mer_adam_step", p.numel(), p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), float(lr), float(b1),
-        float(b2), float(eps), float(wd), int(step), stream_ptr())
+        float(b2), float(eps), float(wd), int(step), float(grad_scale), stream_ptr())
 
 
 def _aligned16(*ts):
@@ -219,7 +252,7 @@ def gemm_bf16(a, w, out, *, M=None, K=None, rows=None, bias=None, residual=None,
     if out.shape[-1] != N or out.numel() != M * N:
         raise ValueError(f"gemm_bf16 out shape {tuple(out.shape)} != ({M},{N})")
     _aligned16(a, w)
-    LIB("mer_gemm_bf16", M, N, K, a.data_ptr(), rows[2], rows[1], rows[0], w.data_ptr(), w.stride(0),
+    _launch("gemm_bf16", (M, N, K), "mer_gemm_bf16", M, N, K, a.data_ptr(), rows[2], rows[1], rows[0], w.data_ptr(), w.stride(0),
         out.data_ptr(), _dt(out), N if out.dim() < 2 else out.stride(-2), _ptr(bias), _ptr(residual),
         0 if residual is None else residual.stride(-2), ACT[act], stream_ptr())
     return out
@@ -276,8 +309,8 @@ def conv_fwd(x, wp, y, stats, R, S, stride, pad):
     Ho, Wo = (H + 2 * pad - R) // stride + 1, (W + 2 * pad - S) // stride + 1
     if tuple(y.shape) != (N, Ho, Wo, Kc) or tuple(wp.shape) != (Kc, R * S * C):
         raise ValueError(f"conv_fwd shapes x{tuple(x.shape)} w{tuple(wp.shape)} y{tuple(y.shape)}")
-    LIB("mer_conv_fwd", N, H, W, C, Kc, R, S, stride, pad, x.data_ptr(), wp.data_ptr(), y.data_ptr(), _ptr(stats),
-        stream_ptr())
+    _launch("conv_fwd", (N, H, W, C, Kc, R, stride), "mer_conv_fwd", N, H, W, C, Kc, R, S, stride, pad, x.data_ptr(),
+            wp.data_ptr(), y.data_ptr(), _ptr(stats), stream_ptr())
 
 
 def conv_dgrad(dy, wt, dx, R, S, stride, pad, residual=None, mask=None):
@@ -286,8 +319,8 @@ def conv_dgrad(dy, wt, dx, R, S, stride, pad, residual=None, mask=None):
     Ho, Wo = (H + 2 * pad - R) // stride + 1, (W + 2 * pad - S) // stride + 1
     if tuple(dy.shape) != (N, Ho, Wo, Kc) or tuple(wt.shape) != (C, R * S * Kc):
         raise ValueError(f"conv_dgrad shapes dy{tuple(dy.shape)} wt{tuple(wt.shape)} dx{tuple(dx.shape)}")
-    LIB("mer_conv_dgrad", N, H, W, C, Kc, R, S, stride, pad, dy.data_ptr(), wt.data_ptr(), dx.data_ptr(),
-        _ptr(residual), _ptr(mask), stream_ptr())
+    _launch("conv_dgrad", (N, H, W, C, Kc, R, stride), "mer_conv_dgrad", N, H, W, C, Kc, R, S, stride, pad,
+            dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), _ptr(residual), _ptr(mask), stream_ptr())
 
 
 def conv_wgrad(x, dy, dw, R, S, stride, pad, creal=None):
@@ -300,8 +333,8 @@ def conv_wgrad(x, dy, dw, R, S, stride, pad, creal=None):
     P = N * Ho * Wo
     tiles = ((Kc + 127) // 128) * ((R * S * C + 127) // 128)
     splits = int(max(1, min(P // 512, max(1, 1024 // tiles))))
-    LIB("mer_conv_wgrad", N, H, W, C, creal, Kc, R, S, stride, pad, x.data_ptr(), dy.data_ptr(), dw.data_ptr(),
-        splits, stream_ptr())
+    _launch("conv_wgrad", (N, H, W, C, Kc, R, stride), "mer_conv_wgrad", N, H, W, C, creal, Kc, R, S, stride, pad,
+            x.data_ptr(), dy.data_ptr(), dw.data_ptr(), splits, stream_ptr())
 
 
 def pack_input_nhwc(x, y):

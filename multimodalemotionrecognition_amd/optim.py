@@ -24,6 +24,7 @@ class FusedAdam(torch.optim.Optimizer):
     def __init__(self, params, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0):
         defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay)
         super().__init__(params, defaults)
+        self.grad_scale = 1.0  # set to 1/world_size by the data-parallel wrapper (SUM all-reduce)
         self._flat = []
         for group in self.param_groups:
             ps: List[torch.Tensor] = group["params"]
@@ -85,5 +86,5 @@ class FusedAdam(torch.optim.Optimizer):
             b1, b2 = group["betas"]
             for s, e in runs:
                 K.adam_step(f["flat"][s:e], f["gflat"][s:e], f["m"][s:e], f["v"][s:e], group["lr"], b1, b2,
-                            group["eps"], group["weight_decay"], f["step"])
+                            group["eps"], group["weight_decay"], f["step"], self.grad_scale)
         return loss

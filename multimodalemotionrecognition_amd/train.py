@@ -1,0 +1,132 @@
+"""Train-step entry points mirroring ``src/train.py`` on the MI355X path.
+
+* ``build_model`` -- the reference's config switch (train.py:329-470 / eval.py:66-198) building the
+  HIP-backed ``FusionModel`` / ``VideoNet`` / ``WavLMAudioEncoder``.
+* ``train_one_epoch`` -- same loop semantics as train.py:185-244 (zero_grad, forward, CE or late NLL,
+  backward, Adam step), but losses/preds stay on the device (no per-step ``.item()`` host syncs).
+* ``TrainStep`` -- one explicit step (the unit ``bench.py`` times), with the optional RCCL gradient
+  all-reduce between backward and the optimizer.
+"""
+from __future__ import annotations
+
+from typing import Dict, Optional
+
+import torch
+from torch import nn
+
+from .dist import GradAllReduce
+from .fusion import FusionModel
+from .losses import CrossEntropyLoss, LateNLLLoss
+from .optim import FusedAdam
+from .video import VideoNet
+from .wavlm_audio import WavLMAudioEncoder
+
+
+def build_model(num_classes: int, fusion: str, pretrained_video: bool = True, xattn_head: str = "concat",
+                xattn_d_model: int = 128, xattn_heads: int = 4, xattn_attn_dropout: float = 0.1,
+                xattn_stochastic_depth: float = 0.1, temporal_pooling: str = "mean", temporal_num_heads: int = 4,
+                temporal_num_layers: int = 1, temporal_dropout: float = 0.1, audio_n_mels: int = 64,
+                use_resnet_audio: bool = True, use_wavlm: bool = False, fusion_align_mode: str = "none",
+                fusion_align_dim: int = 256, fusion_align_temperature: float = 0.07,
+                xattn_use_emotion_prior: bool = False, xattn_emotion_prior_dim: int = 8,
+                xattn_emotion_prior_hidden_dim: int = 64, xattn_emotion_prior_dropout: float = 0.1,
+                forward_emotion_prior_flags: bool = False) -> nn.Module:
+    """train.py:329-470.
+
+    Reference quirk kept on purpose: the reference never forwards the ``xattn_use_emotion_prior*``
+    flags to ``FusionModel`` (train.py:454-469, eval.py:182-197), so its checkpoints have no prior
+    weights; pass ``forward_emotion_prior_flags=True`` to actually enable the prior-bias path.
+    The mel ``AudioNet`` encoder (use_wavlm=False) is outside the north-star path.
+    """
+    if not use_wavlm and fusion in {"audio", "late", "concat", "gated", "xattn", "xattn_concat", "xattn_gated"}:
+        raise NotImplementedError("mel AudioNet (use_wavlm=False) is out of scope; the MI355X path is WavLM")
+    tp = dict(temporal_pooling=temporal_pooling, temporal_num_heads=temporal_num_heads,
+              temporal_num_layers=temporal_num_layers, temporal_dropout=temporal_dropout)
+    if fusion == "audio":
+        return WavLMAudioEncoder(num_classes=num_classes, **tp)
+    if fusion == "video":
+        return VideoNet(num_classes=num_classes, pretrained=pretrained_video, **tp)
+    audio = WavLMAudioEncoder(num_classes=num_classes, **tp)
+    video = VideoNet(num_classes=num_classes, pretrained=pretrained_video, **tp)
+    if fusion in {"late", "concat", "gated"}:
+        return FusionModel(audio, video, num_classes=num_classes, mode=fusion, fusion_align_mode=fusion_align_mode,
+                           fusion_align_dim=fusion_align_dim, fusion_align_temperature=fusion_align_temperature)
+    if fusion in {"xattn", "xattn_concat", "xattn_gated"}:
+        head = {"xattn_concat": "concat", "xattn_gated": "gated"}.get(fusion, xattn_head)
+        prior = dict(xattn_use_emotion_prior=xattn_use_emotion_prior, xattn_emotion_prior_dim=xattn_emotion_prior_dim,
+                     xattn_emotion_prior_hidden_dim=xattn_emotion_prior_hidden_dim,
+                     xattn_emotion_prior_dropout=xattn_emotion_prior_dropout) if forward_emotion_prior_flags else {}
+        return FusionModel(audio, video, num_classes=num_classes, mode="xattn", xattn_head=head, d_model=xattn_d_model,
+                           num_heads=xattn_heads, audio_n_mels=768, xattn_attn_dropout=xattn_attn_dropout,
+                           xattn_stochastic_depth=xattn_stochastic_depth, **tp, **prior)
+    raise ValueError(f"Unknown fusion mode: {fusion}")
+
+
+def build_optimizer(model: nn.Module, lr: float = 1e-3, weight_decay: float = 1e-4) -> FusedAdam:
+    """train.py:899-902: Adam over every requires_grad parameter (params that get no grad are skipped)."""
+    params = [p for p in model.parameters() if p.requires_grad]
+    if not params:
+        raise RuntimeError("No trainable parameters found for optimizer.")
+    return FusedAdam(params, lr=lr, weight_decay=weight_decay)
+
+
+def make_loss(fusion_mode: str, label_smoothing: float = 0.0) -> nn.Module:
+    """train.py:1030-1033."""
+    return LateNLLLoss() if fusion_mode == "late" else CrossEntropyLoss(label_smoothing=label_smoothing)
+
+
+class TrainStep:
+    """One training step of train.py:200-228 on the HIP path: returns (loss, preds) as device tensors."""
+
+    def __init__(self, model: nn.Module, optimizer: FusedAdam, loss_fn: nn.Module, fusion_mode: str,
+                 grad_sync: Optional[GradAllReduce] = None):
+        self.model, self.opt, self.loss_fn, self.mode = model, optimizer, loss_fn, fusion_mode
+        self.grad_sync = grad_sync
+
+    def __call__(self, video: torch.Tensor, audio: torch.Tensor, labels: torch.Tensor):
+        self.model.train()
+        self.opt.zero_grad()
+        if self.mode in {"audio", "video"}:
+            outputs = self.model(audio if self.mode == "audio" else video)
+        else:
+            outputs = self.model(video, audio)
+        loss = self.loss_fn(outputs, labels)
+        loss.backward()
+        if self.grad_sync is not None:
+            self.grad_sync()
+        self.opt.step()
+        return loss.detach(), outputs.detach().argmax(dim=1)
+
+
+def train_one_epoch(model: nn.Module, loader, optimizer: FusedAdam, device: torch.device, loss_fn: nn.Module,
+                    fusion_mode: str, fusion_align_weight: float = 0.0,
+                    grad_sync: Optional[GradAllReduce] = None) -> Dict[str, float]:
+    """train.py:185-244 (accuracy / macro-F1 computed once at the end, on the host)."""
+    step = TrainStep(model, optimizer, loss_fn, fusion_mode, grad_sync)
+    losses, preds, targets = [], [], []
+    n = 0
+    for video, audio, labels, _ in loader:
+        video, audio, labels = video.to(device), audio.to(device), labels.to(device)
+        loss, pred = step(video, audio, labels)
+        losses.append(loss * labels.numel())
+        preds.append(pred)
+        targets.append(labels)
+        n += labels.numel()
+    preds_t = torch.cat(preds).cpu()
+    targets_t = torch.cat(targets).cpu()
+    total = float(torch.stack(losses).sum().cpu()) / max(n, 1)
+    acc = float((preds_t == targets_t).float().mean()) if n else 0.0
+    return {"loss": total, "cls_loss": total, "contrastive_loss": 0.0, "acc": acc, "f1": macro_f1(preds_t, targets_t)}
+
+
+def macro_f1(preds: torch.Tensor, targets: torch.Tensor) -> float:
+    """sklearn f1_score(average='macro') over the labels present (utils/metrics.py:13-16)."""
+    labels = torch.unique(torch.cat([preds, targets]))
+    f1s = []
+    for c in labels:
+        tp = ((preds == c) & (targets == c)).sum().item()
+        fp = ((preds == c) & (targets != c)).sum().item()
+        fn = ((preds != c) & (targets == c)).sum().item()
+        denom = 2 * tp + fp + fn
+        f1s.append(0.0 if denom == 0 else 2 * tp / denom)
+    return float(sum(f1s) / len(f1s)) if f1s else 0.0
