@@ -72,4 +72,9 @@ __device__ __forceinline__ float dropout_scale(uint64_t seed, uint64_t idx, floa
   return u >= p ? 1.0f / (1.0f - p) : 0.0f;
 }
 
+// a / d for 0 <= a < 2^22 with inv_d = 1.0f / d (d >= 1): exact, ~3 VALU ops instead of an
+// integer-division sequence.  (a + 0.5) / d sits >= 0.5/d away from any integer, far more than the
+// float rounding error at these magnitudes.
+__device__ __forceinline__ int fdiv(int a, float inv_d) { return (int)(((float)a + 0.5f) * inv_d); }
+
 #define MER_LAUNCH_CHECK() return (int)hipGetLastError()

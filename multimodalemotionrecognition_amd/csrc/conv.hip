@@ -37,20 +37,29 @@ struct ConvGeom {
 };
 
 template <bool DGRAD>
-__device__ __forceinline__ u32x4 conv_a_chunk(const ConvGeom& g, int n, int oh, int ow, bool rowok, int kk) {
+__device__ __forceinline__ u32x4 conv_a_chunk(const ConvGeom& g, int n, int oh, int ow, bool rowok, int kk, int tap,
+                                              int c, int r, int s) {
   u32x4 v = {0u, 0u, 0u, 0u};
   if (!rowok || kk >= g.Kred) return v;
-  const int tap = kk / g.IC, c = kk - tap * g.IC;
-  const int r = tap / g.S, s = tap - r * g.S;
   int ih, iw;
   if (!DGRAD) {
     ih = oh * g.st - g.pad + r;
     iw = ow * g.st - g.pad + s;
   } else {
     const int th = oh + g.pad - r, tw = ow + g.pad - s;
-    if (th < 0 || tw < 0 || (th % g.st) || (tw % g.st)) return v;
-    ih = th / g.st;
-    iw = tw / g.st;
+    if (th < 0 || tw < 0) return v;
+    if (g.st == 1) {
+      ih = th;
+      iw = tw;
+    } else if (g.st == 2) {
+      if ((th | tw) & 1) return v;
+      ih = th >> 1;
+      iw = tw >> 1;
+    } else {
+      if ((th % g.st) || (tw % g.st)) return v;
+      ih = th / g.st;
+      iw = tw / g.st;
+    }
   }
   if (ih < 0 || ih >= g.IH || iw < 0 || iw >= g.IW) return v;
   return *reinterpret_cast<const u32x4*>(g.X + (((long)n * g.IH + ih) * g.IW + iw) * g.IC + c);
@@ -82,10 +91,13 @@ __global__ __launch_bounds__(256, 2) void conv_kernel(ConvGeom g) {
     aow[i] = rem - aoh[i] * g.OW;
   }
   u32x4 ra[ACH], rb[BCH];
+  const float inv_IC = 1.f / g.IC, inv_S = 1.f / g.S;
   auto gload = [&](int k0) {
     const int kk = k0 + ckc * 8;
+    const int tap = fdiv(kk, inv_IC), c = kk - tap * g.IC;
+    const int r = fdiv(tap, inv_S), s = tap - r * g.S;
 #pragma unroll
-    for (int i = 0; i < ACH; ++i) ra[i] = conv_a_chunk<DGRAD>(g, an[i], aoh[i], aow[i], aok[i], kk);
+    for (int i = 0; i < ACH; ++i) ra[i] = conv_a_chunk<DGRAD>(g, an[i], aoh[i], aow[i], aok[i], kk, tap, c, r, s);
 #pragma unroll
     for (int i = 0; i < BCH; ++i) {
       const int n = n0 + crow + 32 * i;
@@ -199,29 +211,34 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradGeom g) {
   constexpr int ACPR = BM_ / 8, BCPR = BN_ / 8;  // chunks per LDS row
 
   u32x4 ra[ACH], rb[BCH];
+  // Per-thread constants: a thread always stages the same 16-byte column chunk, so its (tap, c) and the
+  // row offsets of its chunks are fixed; only the pixel base moves (by 64) per K step.
+  const int a_cc = t % ACPR, a_pr0 = t / ACPR;
+  const int b_cc = t % BCPR, b_pr0 = t / BCPR;
+  const int b_nn = n0 + b_cc * 8;
+  const bool b_colok = b_nn < Ntot;
+  const float inv_C = 1.f / g.C, inv_S = 1.f / g.S, inv_HoWo = 1.f / (g.Ho * g.Wo), inv_Wo = 1.f / g.Wo;
+  const int b_tap = b_colok ? fdiv(b_nn, inv_C) : 0;
+  const int b_c = b_nn - b_tap * g.C;
+  const int b_r = fdiv(b_tap, inv_S), b_s = b_tap - fdiv(b_tap, inv_S) * g.S;
+  const int HoWo = g.Ho * g.Wo;
   auto gload = [&](int p0) {
 #pragma unroll
     for (int i = 0; i < ACH; ++i) {
-      const int ch = t + 256 * i;
-      const int pr = ch / ACPR, cc = ch % ACPR;
-      const int p = p0 + pr, k = m0 + cc * 8;
+      const int p = p0 + a_pr0 + i * (256 / ACPR), k = m0 + a_cc * 8;
       ra[i] = (p < p_end && k < g.K) ? *reinterpret_cast<const u32x4*>(g.dY + (long)p * g.K + k) : u32x4{0u, 0u, 0u, 0u};
     }
 #pragma unroll
     for (int i = 0; i < BCH; ++i) {
-      const int ch = t + 256 * i;
-      const int pr = ch / BCPR, cc = ch % BCPR;
-      const int p = p0 + pr, nn = n0 + cc * 8;
+      const int p = p0 + b_pr0 + i * (256 / BCPR);
       u32x4 v = {0u, 0u, 0u, 0u};
-      if (p < p_end && nn < Ntot) {
-        const int tap = nn / g.C, c = nn - tap * g.C;
-        const int r = tap / g.S, s = tap - r * g.S;
-        const int n = p / (g.Ho * g.Wo);
-        const int rem = p - n * g.Ho * g.Wo;
-        const int oh = rem / g.Wo, ow = rem - (rem / g.Wo) * g.Wo;
-        const int ih = oh * g.st - g.pad + r, iw = ow * g.st - g.pad + s;
+      if (p < p_end && b_colok) {
+        const int n = fdiv(p, inv_HoWo);
+        const int rem = p - n * HoWo;
+        const int oh = fdiv(rem, inv_Wo), ow = rem - oh * g.Wo;
+        const int ih = oh * g.st - g.pad + b_r, iw = ow * g.st - g.pad + b_s;
         if (ih >= 0 && ih < g.H && iw >= 0 && iw < g.W)
-          v = *reinterpret_cast<const u32x4*>(g.X + (((long)n * g.H + ih) * g.W + iw) * g.C + c);
+          v = *reinterpret_cast<const u32x4*>(g.X + (((long)n * g.H + ih) * g.W + iw) * g.C + b_c);
       }
       rb[i] = v;
     }
@@ -369,21 +386,23 @@ MER_API int mer_conv_wgrad(int N, int H, int W, int C, int Creal, int K, int R, 
 // Packing kernels
 // ---------------------------------------------------------------------------------------
 // video frames NCHW fp32 -> NHWC bf16 with channels zero-padded to Cp
-__global__ void pack_input_kernel(int N, int C, int H, int W, int Cp, const float* __restrict__ x, bf16_t* __restrict__ y) {
-  const long total = (long)N * H * W;
-  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
-    const int n = e / ((long)H * W);
-    const long hw = e - (long)n * H * W;
-    bf16_t v[16];
-    for (int c = 0; c < Cp; ++c) v[c] = c < C ? f2bf(x[((long)n * C + c) * H * W + hw]) : (bf16_t)0;
-    for (int c = 0; c < Cp; ++c) y[e * Cp + c] = v[c];
+// one frame per blockIdx.y; Cp == 8: one 16-byte store per pixel
+__global__ void pack_input_kernel(int C, int HW, const float* __restrict__ x, bf16_t* __restrict__ y) {
+  const int n = blockIdx.y;
+  const float* xn = x + (long)n * C * HW;
+  u32x4* yn = reinterpret_cast<u32x4*>(y + (long)n * HW * 8);
+  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < HW; p += gridDim.x * blockDim.x) {
+    u32x4 o = {0u, 0u, 0u, 0u};
+    bf16_t* oh = reinterpret_cast<bf16_t*>(&o);
+    for (int c = 0; c < C; ++c) oh[c] = f2bf(xn[(long)c * HW + p]);
+    yn[p] = o;
   }
 }
 MER_API int mer_pack_input_nhwc(int N, int C, int H, int W, int Cp, const float* x, void* y, void* stream) {
-  if (Cp > 16 || Cp < C) return (int)hipErrorInvalidValue;
-  const long total = (long)N * H * W;
-  const int grid = (int)((total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192);
-  hipLaunchKernelGGL(pack_input_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, N, C, H, W, Cp, x, (bf16_t*)y);
+  if (Cp != 8 || C > 8) return (int)hipErrorInvalidValue;
+  const int HW = H * W;
+  dim3 grid((HW + 255) / 256 < 64 ? (HW + 255) / 256 : 64, N);
+  hipLaunchKernelGGL(pack_input_kernel, grid, dim3(256), 0, (hipStream_t)stream, C, HW, x, (bf16_t*)y);
   MER_LAUNCH_CHECK();
 }
 
@@ -449,9 +468,25 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(long M, int C, const bf16
                                                        const float* __restrict__ ms2, const float* __restrict__ gamma2,
                                                        const float* __restrict__ beta2, int relu,
                                                        bf16_t* __restrict__ y) {
+  // 256 % (C/8) == 0 and the grid stride is a multiple of 256, so a thread always owns the same 8
+  // channels: fold BN into one (scale, shift) per channel once, outside the streaming loop.
   const long nvec = M * C / 8;
-  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < nvec; e += (long)gridDim.x * blockDim.x) {
-    const int c0 = (e * 8) % C;
+  const long tid0 = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  const int c0 = (int)(tid0 % (C / 8)) * 8;
+  float sc[8], sh[8], sc2[8], sh2[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int c = c0 + i;
+    sc[i] = ms[2 * c + 1] * gamma[c];
+    sh[i] = beta[c] - ms[2 * c] * sc[i];
+    sc2[i] = 1.f;
+    sh2[i] = 0.f;
+    if (ms2) {
+      sc2[i] = ms2[2 * c + 1] * gamma2[c];
+      sh2[i] = beta2[c] - ms2[2 * c] * sc2[i];
+    }
+  }
+  for (long e = tid0; e < nvec; e += (long)gridDim.x * blockDim.x) {
     const u32x4 xv = *reinterpret_cast<const u32x4*>(x + e * 8);
     u32x4 rv = {0u, 0u, 0u, 0u};
     if (res) rv = *reinterpret_cast<const u32x4*>(res + e * 8);
@@ -461,13 +496,8 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(long M, int C, const bf16
     bf16_t* oh = reinterpret_cast<bf16_t*>(&ov);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      const int c = c0 + i;
-      float v = (bf2f(xh[i]) - ms[2 * c]) * ms[2 * c + 1] * gamma[c] + beta[c];
-      if (res) {
-        float r = bf2f(rh[i]);
-        if (ms2) r = (r - ms2[2 * c]) * ms2[2 * c + 1] * gamma2[c] + beta2[c];
-        v += r;
-      }
+      float v = bf2f(xh[i]) * sc[i] + sh[i];
+      if (res) v += bf2f(rh[i]) * sc2[i] + sh2[i];
       if (relu) v = fmaxf(v, 0.f);
       oh[i] = f2bf(v);
     }
@@ -477,7 +507,7 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(long M, int C, const bf16
 MER_API int mer_bn_apply(long M, int C, const void* x, const float* ms, const float* gamma, const float* beta,
                          const void* res, const float* ms2, const float* gamma2, const float* beta2, int relu, void* y,
                          void* stream) {
-  if (C % 8) return (int)hipErrorInvalidValue;
+  if (C % 8 || 256 % (C / 8)) return (int)hipErrorInvalidValue;
   const long nvec = M * C / 8;
   const int grid = (int)((nvec + 255) / 256 < 8192 ? (nvec + 255) / 256 : 8192);
   hipLaunchKernelGGL(bn_apply_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, M, C, (const bf16_t*)x, ms,
@@ -555,10 +585,25 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(long M, int C, const 
       if (dbeta) dbeta[c] += red[2 * c];
     }
   }
+  // dx = k1*g + k2*x + k0 per channel (the BN backward is affine in (g, x) once the sums are known);
+  // a thread always owns the same 8 channels (see bn_apply_kernel), so the constants are hoisted.
   const long nvec = M * C / 8;
   const float invM = 1.f / (float)M;
-  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < nvec; e += (long)gridDim.x * blockDim.x) {
-    const int c0 = (e * 8) % C;
+  const long tid0 = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  const int c0 = (int)(tid0 % (C / 8)) * 8;
+  float k1[8], k2[8], k0[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int c = c0 + i;
+    const float mu = ms[2 * c], rs = ms[2 * c + 1], gr = gamma[c] * rs;
+    // batch statistics (train): the mean/var terms carry gradient; running stats (eval): they do not
+    const float a = batch_stats ? red[2 * c] * invM : 0.f;
+    const float b = batch_stats ? red[2 * c + 1] * invM : 0.f;
+    k1[i] = gr;
+    k2[i] = -gr * b * rs;
+    k0[i] = -gr * a + gr * b * rs * mu;
+  }
+  for (long e = tid0; e < nvec; e += (long)gridDim.x * blockDim.x) {
     const u32x4 gv = *reinterpret_cast<const u32x4*>(dy + e * 8);
     const u32x4 xv = *reinterpret_cast<const u32x4*>(x + e * 8);
     u32x4 mv = {1u, 1u, 1u, 1u};
@@ -570,13 +615,8 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(long M, int C, const 
     bf16_t* oh = reinterpret_cast<bf16_t*>(&ov);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      const int c = c0 + i;
       const float g = (!mask || bf2f(mh[i]) > 0.f) ? bf2f(gh[i]) : 0.f;
-      const float rs = ms[2 * c + 1];
-      const float xhat = (bf2f(xh[i]) - ms[2 * c]) * rs;
-      // batch statistics (train): the mean/var terms carry gradient; running stats (eval): they do not
-      oh[i] = f2bf(batch_stats ? gamma[c] * rs * (g - red[2 * c] * invM - xhat * red[2 * c + 1] * invM)
-                               : gamma[c] * rs * g);
+      oh[i] = f2bf(k1[i] * g + k2[i] * bf2f(xh[i]) + k0[i]);
     }
     *reinterpret_cast<u32x4*>(dx + e * 8) = ov;
   }
@@ -584,7 +624,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(long M, int C, const 
 MER_API int mer_bn_bwd_apply(long M, int C, const void* dy, const void* mask, const void* x, const float* ms,
                              const float* gamma, const float* red, int batch_stats, void* dx, float* dgamma,
                              float* dbeta, void* stream) {
-  if (C % 8) return (int)hipErrorInvalidValue;
+  if (C % 8 || 256 % (C / 8)) return (int)hipErrorInvalidValue;
   const long nvec = M * C / 8;
   const int grid = (int)((nvec + 255) / 256 < 8192 ? (nvec + 255) / 256 : 8192);
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, M, C, (const bf16_t*)dy,
@@ -596,31 +636,49 @@ MER_API int mer_bn_bwd_apply(long M, int C, const void* dy, const void* mask, co
 // ---------------------------------------------------------------------------------------
 // MaxPool2d(3, 2, 1) (resnet stem) channel-last, with the argmax tap (0..8) saved for backward.
 // ---------------------------------------------------------------------------------------
+// 8 channels (16 B) per thread; pixel index decomposed with fdiv (N*Ho*Wo < 2^22)
 __global__ void maxpool_fwd_kernel(int N, int H, int W, int C, int Ho, int Wo, const bf16_t* __restrict__ x,
                                    bf16_t* __restrict__ y, uint8_t* __restrict__ arg) {
-  const long total = (long)N * Ho * Wo * C;
-  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
-    const int c = e % C;
-    long q = e / C;
-    const int ow = q % Wo; q /= Wo;
-    const int oh = q % Ho;
-    const int n = q / Ho;
-    float best = -INFINITY;
-    int bi = 0;
+  const int cpr = C / 8;
+  const int total = N * Ho * Wo * cpr;
+  const float inv_cpr = 1.f / cpr, inv_Wo = 1.f / Wo, inv_Ho = 1.f / Ho;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
+    const int q = fdiv(e, inv_cpr);
+    const int c0 = (e - q * cpr) * 8;
+    const int q2 = fdiv(q, inv_Wo);
+    const int ow = q - q2 * Wo;
+    const int n = fdiv(q2, inv_Ho);
+    const int oh = q2 - n * Ho;
+    float best[8];
+    int bi[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { best[i] = -INFINITY; bi[i] = 0; }
     for (int r = 0; r < 3; ++r)
       for (int s = 0; s < 3; ++s) {
         const int ih = oh * 2 - 1 + r, iw = ow * 2 - 1 + s;
         if (ih < 0 || ih >= H || iw < 0 || iw >= W) continue;
-        const float v = bf2f(x[(((long)n * H + ih) * W + iw) * C + c]);
-        if (v > best) { best = v; bi = r * 3 + s; }  // first max wins, like torch's CPU kernel
+        const u32x4 v = *reinterpret_cast<const u32x4*>(x + (((long)n * H + ih) * W + iw) * C + c0);
+        const bf16_t* vh = reinterpret_cast<const bf16_t*>(&v);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const float f = bf2f(vh[i]);
+          if (f > best[i]) { best[i] = f; bi[i] = r * 3 + s; }  // first max wins, like torch
+        }
       }
-    y[e] = f2bf(best);
-    arg[e] = (uint8_t)bi;
+    u32x4 o;
+    bf16_t* oh8 = reinterpret_cast<bf16_t*>(&o);
+    uint2 a;
+    uint8_t* a8 = reinterpret_cast<uint8_t*>(&a);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { oh8[i] = f2bf(best[i]); a8[i] = (uint8_t)bi[i]; }
+    *reinterpret_cast<u32x4*>(y + (long)q * C + c0) = o;
+    *reinterpret_cast<uint2*>(arg + (long)q * C + c0) = a;
   }
 }
 MER_API int mer_maxpool_fwd(int N, int H, int W, int C, const void* x, void* y, void* argmax, void* stream) {
   const int Ho = (H + 2 - 3) / 2 + 1, Wo = (W + 2 - 3) / 2 + 1;
-  const long total = (long)N * Ho * Wo * C;
+  if (C % 8 || (long)N * H * W >= (1L << 22)) return (int)hipErrorInvalidValue;
+  const long total = (long)N * Ho * Wo * C / 8;
   const int grid = (int)((total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192);
   hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, N, H, W, C, Ho, Wo,
                      (const bf16_t*)x, (bf16_t*)y, (uint8_t*)argmax);
@@ -629,14 +687,17 @@ MER_API int mer_maxpool_fwd(int N, int H, int W, int C, const void* x, void* y, 
 // gather backward: dx[n,h,w,c] = sum of dy over the (<= 4) windows whose argmax is (h,w)
 __global__ void maxpool_bwd_kernel(int N, int H, int W, int C, int Ho, int Wo, const bf16_t* __restrict__ dy,
                                    const uint8_t* __restrict__ arg, bf16_t* __restrict__ dx) {
-  const long total = (long)N * H * W * C;
-  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
-    const int c = e % C;
-    long q = e / C;
-    const int w = q % W; q /= W;
-    const int h = q % H;
-    const int n = q / H;
-    float acc = 0.f;
+  const int cpr = C / 8;
+  const int total = N * H * W * cpr;
+  const float inv_cpr = 1.f / cpr, inv_W = 1.f / W, inv_H = 1.f / H;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
+    const int q = fdiv(e, inv_cpr);
+    const int c0 = (e - q * cpr) * 8;
+    const int q2 = fdiv(q, inv_W);
+    const int w = q - q2 * W;
+    const int n = fdiv(q2, inv_H);
+    const int h = q2 - n * H;
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     for (int oh = (h + 1) / 2 - 1; oh <= (h + 1) / 2; ++oh) {
       if (oh < 0 || oh >= Ho) continue;
       const int r = h - (oh * 2 - 1);
@@ -645,16 +706,27 @@ __global__ void maxpool_bwd_kernel(int N, int H, int W, int C, int Ho, int Wo, c
         if (ow < 0 || ow >= Wo) continue;
         const int s = w - (ow * 2 - 1);
         if (s < 0 || s > 2) continue;
-        const long oi = (((long)n * Ho + oh) * Wo + ow) * C + c;
-        if (arg[oi] == r * 3 + s) acc += bf2f(dy[oi]);
+        const long oi = (((long)n * Ho + oh) * Wo + ow) * C + c0;
+        const u32x4 g = *reinterpret_cast<const u32x4*>(dy + oi);
+        const uint2 a = *reinterpret_cast<const uint2*>(arg + oi);
+        const bf16_t* gh = reinterpret_cast<const bf16_t*>(&g);
+        const uint8_t* a8 = reinterpret_cast<const uint8_t*>(&a);
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          if (a8[i] == r * 3 + s) acc[i] += bf2f(gh[i]);
       }
     }
-    dx[e] = f2bf(acc);
+    u32x4 o;
+    bf16_t* oh8 = reinterpret_cast<bf16_t*>(&o);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) oh8[i] = f2bf(acc[i]);
+    *reinterpret_cast<u32x4*>(dx + (long)q * C + c0) = o;
   }
 }
 MER_API int mer_maxpool_bwd(int N, int H, int W, int C, const void* dy, const void* argmax, void* dx, void* stream) {
   const int Ho = (H + 2 - 3) / 2 + 1, Wo = (W + 2 - 3) / 2 + 1;
-  const long total = (long)N * H * W * C;
+  if (C % 8 || (long)N * H * W >= (1L << 22)) return (int)hipErrorInvalidValue;
+  const long total = (long)N * H * W * C / 8;
   const int grid = (int)((total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192);
   hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, N, H, W, C, Ho, Wo,
                      (const bf16_t*)dy, (const uint8_t*)argmax, (bf16_t*)dx);
@@ -670,11 +742,10 @@ __global__ void avgpool_fwd_kernel(int N, int HW, int C, const bf16_t* __restric
   y[(long)n * C + c] = s / HW;
 }
 __global__ void avgpool_bwd_kernel(int N, int HW, int C, const float* __restrict__ dy, bf16_t* __restrict__ dx) {
-  const long total = (long)N * HW * C;
-  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+  const int n = blockIdx.y;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < HW * C; e += gridDim.x * blockDim.x) {
     const int c = e % C;
-    const long n = e / ((long)HW * C);
-    dx[e] = f2bf(dy[n * C + c] / HW);
+    dx[(long)n * HW * C + e] = f2bf(dy[(long)n * C + c] / HW);
   }
 }
 MER_API int mer_avgpool_fwd(int N, int HW, int C, const void* x, float* y, void* stream) {
@@ -683,8 +754,7 @@ MER_API int mer_avgpool_fwd(int N, int HW, int C, const void* x, float* y, void*
   MER_LAUNCH_CHECK();
 }
 MER_API int mer_avgpool_bwd(int N, int HW, int C, const float* dy, void* dx, void* stream) {
-  const long total = (long)N * HW * C;
-  const int grid = (int)((total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192);
-  hipLaunchKernelGGL(avgpool_bwd_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, N, HW, C, dy, (bf16_t*)dx);
+  dim3 grid((HW * C + 255) / 256, N);
+  hipLaunchKernelGGL(avgpool_bwd_kernel, grid, dim3(256), 0, (hipStream_t)stream, N, HW, C, dy, (bf16_t*)dx);
   MER_LAUNCH_CHECK();
 }

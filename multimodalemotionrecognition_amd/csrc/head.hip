@@ -237,9 +237,11 @@ MER_API int mer_mha_fwd(int B, int H, int Lq, int Lk, int dh, const float* Q, lo
   MER_LAUNCH_CHECK();
 }
 
-// Backward.  One workgroup per sample b, heads in sequence (so dbias[b] = sum_h dS needs no
-// atomics): dV_j = sum_i p'_ij dO_i; dP = (dO V^T) . mask; dS = P (dP - rowsum(P dP));
-// dQ = scale dS K; dK = scale dS^T Q.  dQ/dK/dV are written (not accumulated).
+// Backward.  One workgroup per sample b, heads in sequence (dbias[b] = sum_h dS stays deterministic,
+// no atomics); within a head every (i,j) score and every output element is its own thread:
+//   dP'_ij = dO_i . V_j;  dP_ij = dP'_ij * mask_ij;  dS_ij = P_ij (dP_ij - sum_j' P_ij' dP_ij')
+//   dQ_i = scale sum_j dS_ij K_j;  dK_j = scale sum_i dS_ij Q_i;  dV_j = sum_i P'_ij dO_i
+// dQ/dK/dV are written (not accumulated).  Q,K,V,dO of the head + the Lq x Lk score tiles live in LDS.
 __global__ __launch_bounds__(256) void mha_bwd_kernel(int B, int H, int Lq, int Lk, int dh, const float* __restrict__ Q,
                                                       long ldq, const float* __restrict__ K, long ldk,
                                                       const float* __restrict__ V, long ldv, const float* __restrict__ P,
@@ -248,79 +250,71 @@ __global__ __launch_bounds__(256) void mha_bwd_kernel(int B, int H, int Lq, int 
                                                       long lddv, float* __restrict__ dbias, float scale, float drop_p,
                                                       unsigned long long seed) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int dp = dh + 1;
-  float* Ks = smem;               // [Lk][dp]
-  float* Vs = Ks + Lk * dp;       // [Lk][dp]
-  float* dKs = Vs + Lk * dp;      // [Lk][dp]
-  float* dVs = dKs + Lk * dp;     // [Lk][dp]
-  float* rowq = dVs + Lk * dp;    // [4][dh]
-  float* rowdo = rowq + 4 * dh;   // [4][dh]
-  float* ds = rowdo + 4 * dh;     // [4][Lk]
+  const int dp = dh + 1, lkp = Lk + 1;
+  float* Qs = smem;              // [Lq][dp]
+  float* dOs = Qs + Lq * dp;     // [Lq][dp]
+  float* Ks = dOs + Lq * dp;     // [Lk][dp]
+  float* Vs = Ks + Lk * dp;      // [Lk][dp]
+  float* dS = Vs + Lk * dp;      // [Lq][lkp]
+  float* Pd = dS + Lq * lkp;     // [Lq][lkp]  dropped-out probabilities p'
+  float* rdot = Pd + Lq * lkp;   // [Lq]
   const int b = blockIdx.x;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const int nsub = 64 / dh;
   for (int h = 0; h < H; ++h) {
+    for (int e = t; e < Lq * dh; e += 256) {
+      const int i = e / dh, c = e - (e / dh) * dh;
+      Qs[i * dp + c] = Q[((long)b * Lq + i) * ldq + h * dh + c];
+      dOs[i * dp + c] = dO[((long)b * Lq + i) * lddo + h * dh + c];
+    }
     for (int e = t; e < Lk * dh; e += 256) {
-      const int j = e / dh, c = e % dh;
+      const int j = e / dh, c = e - (e / dh) * dh;
       Ks[j * dp + c] = K[((long)b * Lk + j) * ldk + h * dh + c];
       Vs[j * dp + c] = V[((long)b * Lk + j) * ldv + h * dh + c];
-      dKs[j * dp + c] = 0.f;
-      dVs[j * dp + c] = 0.f;
     }
     __syncthreads();
-    const int rounds = (Lq + 3) / 4;
-    for (int rr = 0; rr < rounds; ++rr) {
-      const int i = rr * 4 + w;
-      const bool valid = i < Lq;
-      if (valid) {
-        for (int c = lane; c < dh; c += 64) {
-          rowq[w * dh + c] = Q[((long)b * Lq + i) * ldq + h * dh + c];
-          rowdo[w * dh + c] = dO[((long)b * Lq + i) * lddo + h * dh + c];
-        }
+    const long pbase = ((long)b * H + h) * Lq * Lk;
+    for (int e = t; e < Lq * Lk; e += 256) {
+      const int i = e / Lk, j = e - (e / Lk) * Lk;
+      float dpv = 0.f;
+      for (int c = 0; c < dh; ++c) dpv += dOs[i * dp + c] * Vs[j * dp + c];
+      const float m = dropout_scale(seed, pbase + e, drop_p);
+      const float pj = P[pbase + e];
+      dS[i * lkp + j] = dpv * m;
+      Pd[i * lkp + j] = pj * m;
+    }
+    __syncthreads();
+    for (int i = w; i < Lq; i += 4) {
+      float dot = 0.f;
+      for (int j = lane; j < Lk; j += 64) dot += P[pbase + (long)i * Lk + j] * dS[i * lkp + j];
+      dot = wave_sum(dot);
+      if (lane == 0) rdot[i] = dot;
+    }
+    __syncthreads();
+    for (int e = t; e < Lq * Lk; e += 256) {
+      const int i = e / Lk, j = e - (e / Lk) * Lk;
+      const float v = P[pbase + e] * (dS[i * lkp + j] - rdot[i]);
+      dS[i * lkp + j] = v;
+      if (dbias) {
+        float* dbp = dbias + (long)b * Lq * Lk + e;
+        *dbp = (h == 0 ? 0.f : *dbp) + v;  // same thread owns element e for every head
       }
-      __syncthreads();
-      if (valid) {
-        const long prow = (((long)b * H + h) * Lq + i) * Lk;
-        float dot = 0.f;
-        for (int j = lane; j < Lk; j += 64) {
-          float dpv = 0.f;
-          for (int c = 0; c < dh; ++c) dpv += rowdo[w * dh + c] * Vs[j * dp + c];
-          const float m = dropout_scale(seed, prow + j, drop_p);
-          const float pj = P[prow + j];
-          dpv *= m;
-          ds[w * Lk + j] = dpv;
-          dot += pj * dpv;
-        }
-        dot = wave_sum(dot);
-        for (int j = lane; j < Lk; j += 64) {
-          const float pj = P[prow + j];
-          const float m = dropout_scale(seed, prow + j, drop_p);
-          const float dsv = pj * (ds[w * Lk + j] - dot);
-          ds[w * Lk + j] = dsv;
-          if (dbias) {
-            float* dbp = dbias + ((long)b * Lq + i) * Lk + j;
-            *dbp = (h == 0 ? 0.f : *dbp) + dsv;
-          }
-          // dK_j += scale ds_j q_i ; dV_j += p'_j dO_i   (LDS float atomics: rows of 4 waves race)
-          for (int c = 0; c < dh; ++c) {
-            atomicAdd(&dKs[j * dp + c], scale * dsv * rowq[w * dh + c]);
-            atomicAdd(&dVs[j * dp + c], pj * m * rowdo[w * dh + c]);
-          }
-        }
-        __builtin_amdgcn_wave_barrier();
-        const int c = lane % dh, sub = lane / dh;
-        float g = 0.f;
-        if (sub < nsub)
-          for (int j = sub; j < Lk; j += nsub) g += ds[w * Lk + j] * Ks[j * dp + c];
-        for (int off = dh; off < 64; off <<= 1) g += __shfl_down(g, off, 64);
-        if (lane < dh) dQ[((long)b * Lq + i) * lddq + h * dh + c] = scale * g;
-      }
-      __syncthreads();
+    }
+    __syncthreads();
+    for (int e = t; e < Lq * dh; e += 256) {
+      const int i = e / dh, c = e - (e / dh) * dh;
+      float g = 0.f;
+      for (int j = 0; j < Lk; ++j) g += dS[i * lkp + j] * Ks[j * dp + c];
+      dQ[((long)b * Lq + i) * lddq + h * dh + c] = scale * g;
     }
     for (int e = t; e < Lk * dh; e += 256) {
-      const int j = e / dh, c = e % dh;
-      dK[((long)b * Lk + j) * lddk + h * dh + c] = dKs[j * dp + c];
-      dV[((long)b * Lk + j) * lddv + h * dh + c] = dVs[j * dp + c];
+      const int j = e / dh, c = e - (e / dh) * dh;
+      float gk = 0.f, gv = 0.f;
+      for (int i = 0; i < Lq; ++i) {
+        gk += dS[i * lkp + j] * Qs[i * dp + c];
+        gv += Pd[i * lkp + j] * dOs[i * dp + c];
+      }
+      dK[((long)b * Lk + j) * lddk + h * dh + c] = scale * gk;
+      dV[((long)b * Lk + j) * lddv + h * dh + c] = gv;
     }
     __syncthreads();
   }
@@ -331,7 +325,8 @@ MER_API int mer_mha_bwd(int B, int H, int Lq, int Lk, int dh, const float* Q, lo
                         float* dK, long lddk, float* dV, long lddv, float* dbias, float scale, float drop_p,
                         unsigned long long seed, void* stream) {
   if (dh > 64 || (64 % dh) != 0) return (int)hipErrorInvalidValue;
-  const size_t lds = sizeof(float) * ((size_t)4 * Lk * (dh + 1) + 8 * dh + 4 * Lk);
+  const size_t lds = sizeof(float) * ((size_t)2 * Lq * (dh + 1) + (size_t)2 * Lk * (dh + 1) +
+                                      (size_t)2 * Lq * (Lk + 1) + Lq);
   if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(mha_bwd_kernel, dim3(B), dim3(256), lds, (hipStream_t)stream, B, H, Lq, Lk, dh, Q, ldq, K, ldk, V,
                      ldv, P, dO, lddo, dQ, lddq, dK, lddk, dV, lddv, dbias, scale, drop_p, seed);

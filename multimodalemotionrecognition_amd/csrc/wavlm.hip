@@ -65,33 +65,39 @@ MER_API int mer_wavlm_conv0(int B, int S, int Lout, const float* wav, const floa
 __global__ __launch_bounds__(256) void gn_gelu_kernel(int B, int L, int C, const bf16_t* __restrict__ x,
                                                       const float* __restrict__ stats, const float* __restrict__ gamma,
                                                       const float* __restrict__ beta, float eps, bf16_t* __restrict__ y) {
-  const long nvec = (long)B * L * C / 8;
-  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < nvec; e += (long)gridDim.x * blockDim.x) {
-    const long base = e * 8;
-    const int c0 = base % C;
-    const int b = base / ((long)L * C);
-    u32x4 v = *reinterpret_cast<const u32x4*>(x + base);
+  // clip b = blockIdx.y; 256 % (C/8) == 0 so each thread owns fixed channels: hoist scale/shift
+  const int b = blockIdx.y;
+  const int nvec = L * C / 8;
+  const int tid0 = blockIdx.x * blockDim.x + threadIdx.x;
+  const int c0 = (tid0 % (C / 8)) * 8;
+  float sc[8], sh[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int c = c0 + i;
+    const float mu = stats[((long)b * C + c) * 2] / L;
+    const float var = fmaxf(stats[((long)b * C + c) * 2 + 1] / L - mu * mu, 0.f);
+    sc[i] = rsqrtf(var + eps) * gamma[c];
+    sh[i] = beta[c] - mu * sc[i];
+  }
+  const bf16_t* xb = x + (long)b * L * C;
+  bf16_t* yb = y + (long)b * L * C;
+  for (int e = tid0; e < nvec; e += gridDim.x * blockDim.x) {
+    u32x4 v = *reinterpret_cast<const u32x4*>(xb + (long)e * 8);
     const bf16_t* hv = reinterpret_cast<const bf16_t*>(&v);
     u32x4 o;
     bf16_t* ho = reinterpret_cast<bf16_t*>(&o);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int c = c0 + i;
-      const float mu = stats[((long)b * C + c) * 2] / L;
-      const float var = fmaxf(stats[((long)b * C + c) * 2 + 1] / L - mu * mu, 0.f);
-      const float xn = (bf2f(hv[i]) - mu) * rsqrtf(var + eps) * gamma[c] + beta[c];
-      ho[i] = f2bf(gelu_erf(xn));
-    }
-    *reinterpret_cast<u32x4*>(y + base) = o;
+    for (int i = 0; i < 8; ++i) ho[i] = f2bf(gelu_erf(bf2f(hv[i]) * sc[i] + sh[i]));
+    *reinterpret_cast<u32x4*>(yb + (long)e * 8) = o;
   }
 }
 
 MER_API int mer_groupnorm_gelu(int B, int L, int C, const void* x, const float* stats, const float* gamma,
                                const float* beta, float eps, void* y, void* stream) {
-  if (C % 8) return (int)hipErrorInvalidValue;
-  const long nvec = (long)B * L * C / 8;
-  const int grid = (int)((nvec + 255) / 256 < 8192 ? (nvec + 255) / 256 : 8192);
-  hipLaunchKernelGGL(gn_gelu_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, B, L, C, (const bf16_t*)x, stats,
+  if (C % 8 || 256 % (C / 8)) return (int)hipErrorInvalidValue;
+  const long nvec = (long)L * C / 8;
+  dim3 grid((unsigned)((nvec + 255) / 256 < 1024 ? (nvec + 255) / 256 : 1024), B);
+  hipLaunchKernelGGL(gn_gelu_kernel, grid, dim3(256), 0, (hipStream_t)stream, B, L, C, (const bf16_t*)x, stats,
                      gamma, beta, eps, (bf16_t*)y);
   MER_LAUNCH_CHECK();
 }

@@ -87,9 +87,10 @@ def grad_buffer(param: torch.Tensor) -> torch.Tensor:
     zeroed view into the optimizer's flat gradient buffer (autograd then adopts it without a
     copy); otherwise a fresh zero buffer (autograd accumulates it into an existing ``.grad``).
     """
-    view = getattr(param, "_mer_grad_view", None)
-    if view is not None and param.grad is None:
-        return view
+    slot = getattr(param, "_mer_grad_slot", None)
+    if slot is not None and param.grad is None:
+        flat, off = slot
+        return flat.narrow(0, off, param.numel()).view(param.shape)  # zeroed by FusedAdam.zero_grad
     return torch.zeros_like(param, dtype=torch.float32)
 
 

@@ -44,7 +44,9 @@ class FusedAdam(torch.optim.Optimizer):
                 for p, o in zip(ps, offs):
                     flat[o:o + p.numel()].copy_(p.detach().reshape(-1))
                     p.data = flat[o:o + p.numel()].view_as(p)
-                    p._mer_grad_view = gflat[o:o + p.numel()].view_as(p)
+                    # (buffer, offset): a FRESH view is built per backward (fusion.grad_buffer) so autograd's
+                    # AccumulateGrad can adopt it without a copy (a view we also kept alive would be cloned)
+                    p._mer_grad_slot = (gflat, o)
             self._flat.append(dict(flat=flat, gflat=gflat, m=torch.zeros_like(flat), v=torch.zeros_like(flat),
                                    offs=offs, step=0))
 
@@ -67,10 +69,11 @@ class FusedAdam(torch.optim.Optimizer):
                 continue
             ps = group["params"]
             runs, cur = [], None
+            gflat = f["gflat"]
             for p, o in zip(ps, f["offs"]):
                 has = p.grad is not None
-                if has and p.grad.data_ptr() != p._mer_grad_view.data_ptr():
-                    p._mer_grad_view.copy_(p.grad)  # grad produced outside our kernels: bring it home
+                if has and p.grad.data_ptr() != gflat[o:].data_ptr():
+                    gflat[o:o + p.numel()].view_as(p).copy_(p.grad)  # grad produced elsewhere: bring it home
                 if has:
                     end = o + _align4(p.numel())
                     if cur is not None and cur[1] == o:

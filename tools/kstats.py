@@ -1,0 +1,11 @@
+"""Summarise a rocprofv3 kernel_stats.csv per train step: python tools/kstats.py <csv> <steps_in_trace>."""
+import csv
+import sys
+
+rows = list(csv.DictReader(open(sys.argv[1])))
+steps = float(sys.argv[2]) if len(sys.argv) > 2 else 1.0
+tot = sum(float(r["TotalDurationNs"]) for r in rows)
+for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"]))[: int(sys.argv[3]) if len(sys.argv) > 3 else 30]:
+    print(f"{float(r['TotalDurationNs']) / 1e6 / steps:8.3f} ms/step {float(r['Percentage']):6.2f}%  "
+          f"calls/step {int(r['Calls']) / steps:6.1f}  avg {float(r['AverageNs']) / 1e3:8.1f}us  {r['Name'][:100]}")
+print(f"total kernel time per step: {tot / 1e6 / steps:.3f} ms")
