@@ -174,10 +174,11 @@ int mer_conv_fwd(int N, int H, int W, int C, int K, int R, int S, int stride, in
 int mer_conv_dgrad(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, const void* dy,
                    const void* wt_packed, void* dx, const void* residual, const void* residual_mask, void* stream);
 
-/* dw[k][c][r][s] += sum_p dy[p][k] x(p; r,s,c) for c < Creal, fp32 PyTorch layout; split over `splits`
- * pixel ranges with fp32 atomics (dw must be initialised). */
+/* dw[k][c][r][s] += sum_p dy[p][k] x(p; r,s,c) for c < Creal, fp32 PyTorch layout (dw initialised).  The
+ * pixel reduction is split `splits` ways; each split writes an fp32 slab [K][R*S*C] into `workspace`
+ * (splits*K*R*S*C floats), then a reduce pass sums the slabs into dw (deterministic, no atomics). */
 int mer_conv_wgrad(int N, int H, int W, int C, int Creal, int K, int R, int S, int stride, int pad, const void* x,
-                   const void* dy, float* dw, int splits, void* stream);
+                   const void* dy, float* dw, int splits, float* workspace, void* stream);
 
 /* NCHW fp32 frames -> NHWC bf16 with channels zero-padded to Cp (<= 16). */
 int mer_pack_input_nhwc(int N, int C, int H, int W, int Cp, const float* x, void* y, void* stream);

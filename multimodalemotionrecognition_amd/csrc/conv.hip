@@ -181,8 +181,9 @@ __global__ __launch_bounds__(256, 2) void conv_kernel(ConvGeom g) {
 }
 
 // ---------------------------------------------------------------------------------------
-// wgrad: dW[k][(r,s,c)] += sum_p dY[p][k] X(p; r,s,c).  Split-K over pixels (grid z), fp32
-// atomics straight into the PyTorch-layout fp32 gradient [Cout][Cin_real][R][S].
+// wgrad: dW[k][(r,s,c)] += sum_p dY[p][k] X(p; r,s,c).  Split-K over pixels (grid z): each split
+// stores a coalesced fp32 slab, wgrad_reduce sums them into the PyTorch-layout gradient [Cout][Cin][R][S]
+// (scattered fp32 atomics at stride R*S ran ~17x under the atomic peak: MI355X_MICROARCH 'Global float atomics').
 // LDS images [pixel][channel] (+16 pad); MFMA fragments via ds_read_b64_tr_b16.
 // ---------------------------------------------------------------------------------------
 struct WgradGeom {
@@ -192,7 +193,7 @@ struct WgradGeom {
   int Creal;              // real input channels (<= C) of the weight
   const bf16_t* X;
   const bf16_t* dY;
-  float* dW;              // [K][Creal][R][S] fp32, accumulated
+  float* ws;              // [splits][K][R*S*C] fp32 partial slabs
   int pix_per_split;
 };
 
@@ -299,33 +300,61 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradGeom g) {
     if (kt + 1 < nk) lstore(cur ^ 1);
     __syncthreads();
   }
-  if (nk == 0) return;
+  // partial tile -> this split's fp32 slab [K][R*S*C] (plain coalesced stores; summed by wgrad_reduce)
+  float* slab = g.ws + (long)blockIdx.z * g.K * Ntot;
 #pragma unroll
   for (int i = 0; i < IT; ++i)
 #pragma unroll
     for (int j = 0; j < JT; ++j) {
       const int nn = n0 + wn + j * 16 + (lane & 15);
       if (nn >= Ntot) continue;
-      const int tap = nn / g.C, c = nn - tap * g.C;
-      if (c >= g.Creal) continue;
-      const int r = tap / g.S, s = tap - r * g.S;
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
         const int k = m0 + wm + i * 16 + (lane >> 4) * 4 + rr;
-        if (k < g.K) atomicAdd(g.dW + (((long)k * g.Creal + c) * g.R + r) * g.S + s, acc[i][j][rr]);
+        if (k < g.K) slab[(long)k * Ntot + nn] = acc[i][j][rr];
       }
     }
+}
+
+// dw[k][c][r][s] += sum_z ws[z][k][(r*S+s)*C + c]  for c < Creal (reads coalesced along c)
+__global__ void wgrad_reduce_kernel(int K, int C, int Creal, int R, int S, int splits, const float* __restrict__ ws,
+                                    float* __restrict__ dw) {
+  const int RSC = R * S * C;
+  const long total = (long)K * RSC;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    const int k = (int)(e / RSC);
+    const int rem = (int)(e - (long)k * RSC);
+    const int tap = rem / C, c = rem - tap * C;
+    if (c >= Creal) continue;
+    float acc = 0.f;
+    for (int z = 0; z < splits; ++z) acc += ws[(long)z * total + e];
+    const int r = tap / S, s = tap - r * S;
+    dw[(((long)k * Creal + c) * R + r) * S + s] += acc;
+  }
 }
 
 template <bool DGRAD>
 int launch_conv(ConvGeom& g, hipStream_t st) {
   const int M = g.N * g.OH * g.OW;
-  if (g.Ncols <= 64) {
-    dim3 grid((g.Ncols + 63) / 64, (M + 127) / 128);
-    hipLaunchKernelGGL((conv_kernel<DGRAD, 128, 64>), grid, dim3(256), 0, st, g);
+  const int bn = g.Ncols <= 64 ? 64 : 128;
+  const long tiles128 = (long)((M + 127) / 128) * ((g.Ncols + bn - 1) / bn);
+  const bool small_m = tiles128 < 384;  // deep layers (layer3/4): halve BM so the grid fills 256 CUs
+  if (bn == 64) {
+    if (small_m) {
+      dim3 grid((g.Ncols + 63) / 64, (M + 63) / 64);
+      hipLaunchKernelGGL((conv_kernel<DGRAD, 64, 64>), grid, dim3(256), 0, st, g);
+    } else {
+      dim3 grid((g.Ncols + 63) / 64, (M + 127) / 128);
+      hipLaunchKernelGGL((conv_kernel<DGRAD, 128, 64>), grid, dim3(256), 0, st, g);
+    }
   } else {
-    dim3 grid((g.Ncols + 127) / 128, (M + 127) / 128);
-    hipLaunchKernelGGL((conv_kernel<DGRAD, 128, 128>), grid, dim3(256), 0, st, g);
+    if (small_m) {
+      dim3 grid((g.Ncols + 127) / 128, (M + 63) / 64);
+      hipLaunchKernelGGL((conv_kernel<DGRAD, 64, 128>), grid, dim3(256), 0, st, g);
+    } else {
+      dim3 grid((g.Ncols + 127) / 128, (M + 127) / 128);
+      hipLaunchKernelGGL((conv_kernel<DGRAD, 128, 128>), grid, dim3(256), 0, st, g);
+    }
   }
   return (int)hipGetLastError();
 }
@@ -359,17 +388,17 @@ MER_API int mer_conv_dgrad(int N, int H, int W, int C, int K, int R, int S, int 
 }
 
 MER_API int mer_conv_wgrad(int N, int H, int W, int C, int Creal, int K, int R, int S, int stride, int pad,
-                           const void* x, const void* dy, float* dw, int splits, void* stream) {
+                           const void* x, const void* dy, float* dw, int splits, float* workspace, void* stream) {
   if (C % 8 || K % 8) return (int)hipErrorInvalidValue;
   WgradGeom g{};
   g.N = N; g.H = H; g.W = W; g.C = C; g.Creal = Creal;
   g.Ho = (H + 2 * pad - R) / stride + 1; g.Wo = (W + 2 * pad - S) / stride + 1; g.K = K;
   g.R = R; g.S = S; g.st = stride; g.pad = pad;
-  g.X = (const bf16_t*)x; g.dY = (const bf16_t*)dy; g.dW = dw;
+  g.X = (const bf16_t*)x; g.dY = (const bf16_t*)dy; g.ws = workspace;
   const int P = N * g.Ho * g.Wo;
   if (splits < 1) splits = 1;
   g.pix_per_split = ((P + splits - 1) / splits + 63) / 64 * 64;
-  splits = (P + g.pix_per_split - 1) / g.pix_per_split;
+  splits = (P + g.pix_per_split - 1) / g.pix_per_split;  // every split non-empty (<= requested)
   const int Ntot = R * S * C;
   hipStream_t st = (hipStream_t)stream;
   if (K <= 64) {
@@ -379,6 +408,9 @@ MER_API int mer_conv_wgrad(int N, int H, int W, int C, int Creal, int K, int R, 
     dim3 grid((Ntot + 127) / 128, (K + 127) / 128, splits);
     hipLaunchKernelGGL((wgrad_kernel<128, 128>), grid, dim3(256), 0, st, g);
   }
+  const long total = (long)K * Ntot;
+  const int rgrid = (int)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(rgrid), dim3(256), 0, st, K, C, Creal, R, S, splits, workspace, dw);
   MER_LAUNCH_CHECK();
 }
 
@@ -564,7 +596,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(long M, int C, const
 MER_API int mer_bn_bwd_reduce(long M, int C, const void* dy, const void* mask, const void* x, const float* ms,
                               float* red, void* stream) {
   if (C % 8 || C > 512) return (int)hipErrorInvalidValue;
-  const long rpb = 512;
+  const long rpb = (M + 511) / 512 > 32 ? (M + 511) / 512 : 32;  // ~512 blocks whatever the layer size
   const long blocks = (M + rpb - 1) / rpb;
   hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, M, C,
                      (const bf16_t*)dy, (const bf16_t*)mask, (const bf16_t*)x, ms, red, rpb);

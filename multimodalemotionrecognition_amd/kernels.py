@@ -332,9 +332,10 @@ def conv_wgrad(x, dy, dw, R, S, stride, pad, creal=None):
         raise ValueError("conv_wgrad shapes")
     P = N * Ho * Wo
     tiles = ((Kc + 127) // 128) * ((R * S * C + 127) // 128)
-    splits = int(max(1, min(P // 512, max(1, 1024 // tiles))))
+    splits = int(max(1, min(-(-512 // tiles), P // 2048)))
+    ws = torch.empty(splits * Kc * R * S * C, device=x.device, dtype=torch.float32)
     _launch("conv_wgrad", (N, H, W, C, Kc, R, stride), "mer_conv_wgrad", N, H, W, C, creal, Kc, R, S, stride, pad,
-            x.data_ptr(), dy.data_ptr(), dw.data_ptr(), splits, stream_ptr())
+            x.data_ptr(), dy.data_ptr(), dw.data_ptr(), splits, ws.data_ptr(), stream_ptr())
 
 
 def pack_input_nhwc(x, y):
