@@ -77,4 +77,15 @@ __device__ __forceinline__ float dropout_scale(uint64_t seed, uint64_t idx, floa
 // float rounding error at these magnitudes.
 __device__ __forceinline__ int fdiv(int a, float inv_d) { return (int)(((float)a + 0.5f) * inv_d); }
 
+// XCD-aware tile order (cdna_hip_programming.md T1, bijective form): blocks are dealt round-robin over
+// the 8 XCDs, so give each XCD (block-id residue class mod 8) a CONTIGUOUS chunk of the row-major tile
+// list.  Tiles that share an A row-panel (same ty, consecutive tx) then run on one XCD and hit its L2
+// instead of being fetched once per XCD.  Placement only changes speed, never results.
+__device__ __forceinline__ void xcd_tile(int pid, int nx, int ntiles, int& tx, int& ty) {
+  const int q = ntiles / 8, r = ntiles % 8, xcd = pid % 8, loc = pid / 8;
+  const int tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+  ty = tile / nx;
+  tx = tile - ty * nx;
+}
+
 #define MER_LAUNCH_CHECK() return (int)hipGetLastError()

@@ -74,7 +74,10 @@ __global__ __launch_bounds__(256, 2) void conv_kernel(ConvGeom g) {
   __shared__ __attribute__((aligned(16))) bf16_t lds[2][(BM_ + BN_) * LDK];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int M = g.N * g.OH * g.OW;
-  const int m0 = blockIdx.y * BM_, n0 = blockIdx.x * BN_;
+  const int nx = (g.Ncols + BN_ - 1) / BN_, ny = (M + BM_ - 1) / BM_;
+  int tx, ty;
+  xcd_tile(blockIdx.x, nx, nx * ny, tx, ty);
+  const int m0 = ty * BM_, n0 = tx * BN_;
   const int wm = (w >> 1) * (BM_ / 2), wn = (w & 1) * (BN_ / 2);
   const int crow = t >> 3, ckc = t & 7;
 
@@ -206,7 +209,10 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradGeom g) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int Ntot = g.R * g.S * g.C;
   const int P = g.N * g.Ho * g.Wo;
-  const int m0 = blockIdx.y * BM_, n0 = blockIdx.x * BN_;
+  const int wnx = (Ntot + BN_ - 1) / BN_, wny = (g.K + BM_ - 1) / BM_;
+  int wtx, wty;
+  xcd_tile(blockIdx.x, wnx, wnx * wny, wtx, wty);
+  const int m0 = wty * BM_, n0 = wtx * BN_;
   const int p_beg = blockIdx.z * g.pix_per_split, p_end = min(P, p_beg + g.pix_per_split);
   const int wm = (w >> 1) * (BM_ / 2), wn = (w & 1) * (BN_ / 2);
   constexpr int ACPR = BM_ / 8, BCPR = BN_ / 8;  // chunks per LDS row
@@ -339,21 +345,18 @@ int launch_conv(ConvGeom& g, hipStream_t st) {
   const int bn = g.Ncols <= 64 ? 64 : 128;
   const long tiles128 = (long)((M + 127) / 128) * ((g.Ncols + bn - 1) / bn);
   const bool small_m = tiles128 < 384;  // deep layers (layer3/4): halve BM so the grid fills 256 CUs
+  const int nx = (g.Ncols + bn - 1) / bn;
   if (bn == 64) {
     if (small_m) {
-      dim3 grid((g.Ncols + 63) / 64, (M + 63) / 64);
-      hipLaunchKernelGGL((conv_kernel<DGRAD, 64, 64>), grid, dim3(256), 0, st, g);
+      hipLaunchKernelGGL((conv_kernel<DGRAD, 64, 64>), dim3(nx * ((M + 63) / 64)), dim3(256), 0, st, g);
     } else {
-      dim3 grid((g.Ncols + 63) / 64, (M + 127) / 128);
-      hipLaunchKernelGGL((conv_kernel<DGRAD, 128, 64>), grid, dim3(256), 0, st, g);
+      hipLaunchKernelGGL((conv_kernel<DGRAD, 128, 64>), dim3(nx * ((M + 127) / 128)), dim3(256), 0, st, g);
     }
   } else {
     if (small_m) {
-      dim3 grid((g.Ncols + 127) / 128, (M + 63) / 64);
-      hipLaunchKernelGGL((conv_kernel<DGRAD, 64, 128>), grid, dim3(256), 0, st, g);
+      hipLaunchKernelGGL((conv_kernel<DGRAD, 64, 128>), dim3(nx * ((M + 63) / 64)), dim3(256), 0, st, g);
     } else {
-      dim3 grid((g.Ncols + 127) / 128, (M + 127) / 128);
-      hipLaunchKernelGGL((conv_kernel<DGRAD, 128, 128>), grid, dim3(256), 0, st, g);
+      hipLaunchKernelGGL((conv_kernel<DGRAD, 128, 128>), dim3(nx * ((M + 127) / 128)), dim3(256), 0, st, g);
     }
   }
   return (int)hipGetLastError();
@@ -402,10 +405,10 @@ MER_API int mer_conv_wgrad(int N, int H, int W, int C, int Creal, int K, int R, 
   const int Ntot = R * S * C;
   hipStream_t st = (hipStream_t)stream;
   if (K <= 64) {
-    dim3 grid((Ntot + 127) / 128, (K + 63) / 64, splits);
+    dim3 grid(((Ntot + 127) / 128) * ((K + 63) / 64), 1, splits);
     hipLaunchKernelGGL((wgrad_kernel<64, 128>), grid, dim3(256), 0, st, g);
   } else {
-    dim3 grid((Ntot + 127) / 128, (K + 127) / 128, splits);
+    dim3 grid(((Ntot + 127) / 128) * ((K + 127) / 128), 1, splits);
     hipLaunchKernelGGL((wgrad_kernel<128, 128>), grid, dim3(256), 0, st, g);
   }
   const long total = (long)K * Ntot;

@@ -65,7 +65,10 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs g) {
   __shared__ __attribute__((aligned(16))) bf16_t lds[2][2][BM * LDSK];  // [buf][A/B][row*LDSK + k]
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int z = blockIdx.z;
-  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  const int nx = (g.N + BN - 1) / BN, ny = (g.M + BM - 1) / BM;
+  int tx, ty;
+  xcd_tile(blockIdx.x, nx, nx * ny, tx, ty);
+  const int m0 = ty * BM, n0 = tx * BN;
   const bf16_t* Bz = g.B + (long)z * g.b_zstride;
   const int wm = (w >> 1) * 64, wn = (w & 1) * 64;
 
@@ -144,7 +147,7 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs g) {
 
 template <int AMODE>
 int launch(const GemmArgs& g, int out_dtype, int groups, hipStream_t st) {
-  dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM, groups);
+  dim3 grid(((g.N + BN - 1) / BN) * ((g.M + BM - 1) / BM), 1, groups);
   if (out_dtype == MER_BF16)
     hipLaunchKernelGGL((gemm_bf16_kernel<AMODE, bf16_t>), grid, dim3(256), 0, st, g);
   else
