@@ -215,6 +215,28 @@ int mer_maxpool_bwd(int N, int H, int W, int C, const void* dy, const void* argm
 int mer_avgpool_fwd(int N, int HW, int C, const void* x, float* y, void* stream);
 int mer_avgpool_bwd(int N, int HW, int C, const float* dy, void* dx, void* stream);
 
+/* ============================ dynamic INT8 Linear (inference) ============================
+ * TorchModelRunner(enable_dynamic_quant=True): optimized_runtime.py:95-96
+ * (torch.quantization.quantize_dynamic(model, {nn.Linear}, qint8), fbgemm semantics -- oracle/int8_ref.py).
+ * qparams are 4 floats on the device: {scale, 1/scale, zero_point, 0}. */
+
+/* min/max over x[0:n] (partial = 2*512 floats of workspace) -> qparams.  mode 0: activation
+ * (fbgemm ChooseQuantizationParams, range [0,127] = reduce_range); mode 1: symmetric weight scale
+ * max(amax/127.5, FLT_EPSILON), zero point 0. */
+int mer_quant_params_f32(long n, const float* x, float* partial, int mode, float* qparams, void* stream);
+
+/* qw[n, 0:ldq] = int8 clamp(rint(W[n,k] / ws)) (zero for k >= K); colsum[n] = sum_k qw[n,k].
+ * ldq % 16 == 0.  Run once per Linear when the model is quantized. */
+int mer_quantize_weight_s8(int N, int K, const float* w, long ldw, const float* qparams, void* qw, long ldq,
+                           int* colsum, void* stream);
+
+/* out[m,n] = act(fma(sum_k qx[m,k] qw[n,k] - zp * colsum[n], xs*ws, bias[n])) with
+ * qx = clamp(rint(fma(x, 1/xs, zp)), 0, 255) computed on the fly from fp32 x (K % 16 == 0;
+ * act 0 or 1).  The quantized Linear forward (torch.ao.nn.quantized.dynamic.Linear). */
+int mer_gemm_i8dyn(int M, int N, int K, const float* x, long ldx, const float* x_qparams, const void* qw, long ldq,
+                   const float* w_qparams, const int* colsum, const float* bias, int act, float* out, long ldo,
+                   void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -8,7 +8,7 @@ from __future__ import annotations
 import torch
 
 from . import kernels as K
-from .xattn_head import site_seed
+from .xattn_head import linear_runner, site_seed
 
 
 def _grad_buf(p):
@@ -18,16 +18,17 @@ def _grad_buf(p):
 
 class _EmbHeadFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, a_emb, v_emb, mode, training, seed, drop_a, drop_v, names, *params):
+    def forward(ctx, a_emb, v_emb, mode, training, seed, drop_a, drop_v, qlin, names, *params):
         p = dict(zip(names, params))
+        lin = linear_runner(p, qlin)
         B = a_emb.shape[0]
         dev = a_emb.device
         e = lambda *s: torch.empty(s, device=dev, dtype=torch.float32)  # noqa: E731
         cd = p["audio_proj.weight"].shape[0]
         cat = e(B, 2 * cd)
         a, v = cat[:, :cd], cat[:, cd:]
-        K.linear_fwd(a_emb, p["audio_proj.weight"], p["audio_proj.bias"], a)
-        K.linear_fwd(v_emb, p["video_proj.weight"], p["video_proj.bias"], v)
+        lin("audio_proj", a_emb, a)
+        lin("video_proj", v_emb, v)
         if drop_a:
             a.zero_()
         if drop_v:
@@ -36,20 +37,20 @@ class _EmbHeadFn(torch.autograd.Function):
         sv = {"cat": cat}
         if mode == "concat":
             w0 = p["fusion.0.weight"]
-            h = K.linear_fwd(cat, w0, p["fusion.0.bias"], e(B, w0.shape[0]), act="relu")
+            h = lin("fusion.0", cat, e(B, w0.shape[0]), act="relu")
             K.dropout_(h, dp, site_seed(seed, 11))
             w3 = p["fusion.3.weight"]
-            out = K.linear_fwd(h, w3, p["fusion.3.bias"], e(B, w3.shape[0]))
+            out = lin("fusion.3", h, e(B, w3.shape[0]))
             sv["h"] = h
         else:
             w0 = p["gate.0.weight"]
-            h = K.linear_fwd(cat, w0, p["gate.0.bias"], e(B, w0.shape[0]), act="relu")
+            h = lin("gate.0", cat, e(B, w0.shape[0]), act="relu")
             K.dropout_(h, dp, site_seed(seed, 11))
-            z = K.linear_fwd(h, p["gate.3.weight"], p["gate.3.bias"], e(B, 1))
+            z = lin("gate.3", h, e(B, 1))
             fused, g = e(B, cd), e(B)
             K.gate_mix_fwd(z, a, v, fused, g)  # g*a + (1-g)*v  (fusion.py:434)
             wc = p["classifier.weight"]
-            out = K.linear_fwd(fused, wc, p["classifier.bias"], e(B, wc.shape[0]))
+            out = lin("classifier", fused, e(B, wc.shape[0]))
             sv.update(h=h, g=g, fused=fused)
         ctx.sv, ctx.p, ctx.names, ctx.params = sv, p, names, params
         ctx.mode, ctx.dp, ctx.seed, ctx.drops = mode, dp, seed, (drop_a, drop_v)
@@ -101,7 +102,7 @@ class _EmbHeadFn(torch.autograd.Function):
         K.linear_bwd(ctx.v_emb, p["video_proj.weight"], dcat[:, cd:], dx=dv, dw=grads["video_proj.weight"],
                      db=grads["video_proj.bias"])
         out = [grads.get(n) if (n in grads and t.requires_grad) else None for n, t in zip(ctx.names, ctx.params)]
-        return (da, dv, None, None, None, None, None, None, *out)
+        return (da, dv, None, None, None, None, None, None, None, *out)
 
 
 def embedding_head(model, a_emb, v_emb, drop_a=False, drop_v=False):
@@ -113,7 +114,12 @@ def embedding_head(model, a_emb, v_emb, drop_a=False, drop_v=False):
         params.append(q)
     seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if model.training else 0
     return _EmbHeadFn.apply(a_emb.contiguous(), v_emb.contiguous(), model.mode, model.training, seed,
-                            bool(drop_a), bool(drop_v), tuple(names), *params)
+                            bool(drop_a), bool(drop_v), int8_images(model), tuple(names), *params)
+
+
+def int8_images(model):
+    """The model's INT8 Linear images (int8.quantize_dynamic_hip) -- used in eval mode only."""
+    return None if model.training else getattr(model, "_mer_int8", None)
 
 
 class _LateFn(torch.autograd.Function):

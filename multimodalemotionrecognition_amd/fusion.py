@@ -228,9 +228,13 @@ class FusionModel(nn.Module):
     def head_config(self) -> XH.HeadConfig:
         return XH.HeadConfig(num_heads=self.num_heads, xattn_head=self.xattn_head,
                              use_prior=self.emotion_prior_bias is not None, attn_dropout=self.attn_dropout,
-                             drop_path=self.v_drop_path.drop_prob, mlp_dropout=0.2,
+                             drop_path=self.v_drop_path.drop_prob, mlp_dropout=self._mlp_dropout_p(),
                              prior_dropout=(self.emotion_prior_bias.dropout if self.emotion_prior_bias is not None else 0.0),
                              temporal_pooling=self.temporal_pooling)
+
+    def _mlp_dropout_p(self) -> float:
+        seq = self.xattn_mlp if self.xattn_head == "concat" else self.xattn_gate
+        return float(seq[2].p)  # the nn.Dropout(0.2) of fusion.py:312-324
 
     def head_params(self):
         names, params = [], []
@@ -245,6 +249,11 @@ class FusionModel(nn.Module):
         """xattn head on encoder features: v_feat [B,T,v_dim] (backbone output), a_seq [B,Ta,seq_dim]."""
         _require_device(v_feat, a_seq)
         names, params = self.head_params()
+        qlin = EH.int8_images(self)
+        if qlin is not None:  # INT8 inference (TorchModelRunner enable_dynamic_quant): forward only
+            with torch.no_grad():
+                return XH.head_forward(dict(zip(names, params)), self.head_config(), v_feat.contiguous(),
+                                       a_seq.contiguous(), False, 0, qlin=qlin)[0]
         return _XattnHeadFn.apply(v_feat.contiguous(), a_seq.contiguous(), self.head_config(), self.training,
                                   _next_seed() if self.training else 0, names, *params)
 

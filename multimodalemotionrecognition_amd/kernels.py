@@ -403,3 +403,35 @@ def softmax_avg_bwd(pa, pv, dout, da, dv):
     B, C = pa.shape
     LIB("mer_softmax_avg_bwd", B, C, pa.data_ptr(), pv.data_ptr(), dout.data_ptr(), da.data_ptr(), dv.data_ptr(),
         stream_ptr())
+
+
+# ---- dynamic INT8 Linear (TorchModelRunner enable_dynamic_quant) ----
+QP_PARTIAL = 2 * 512  # floats of min/max workspace for mer_quant_params_f32
+
+
+def quant_params(x, partial, qparams, mode):
+    """qparams[4] = {scale, 1/scale, zero_point, 0} from min/max over all of x (mode 0 act, 1 weight)."""
+    _check_dev(x, partial, qparams)
+    if not x.is_contiguous() or x.dtype != torch.float32 or x.data_ptr() % 16:
+        raise ValueError("quant_params needs a contiguous 16-byte aligned fp32 tensor")
+    LIB("mer_quant_params_f32", x.numel(), x.data_ptr(), partial.data_ptr(), int(mode), qparams.data_ptr(), stream_ptr())
+
+
+def quantize_weight_s8(w, qparams, qw, colsum):
+    N, K = w.shape
+    if qw.shape[0] != N or qw.shape[1] < K or qw.shape[1] % 16 or qw.dtype != torch.int8:
+        raise ValueError("qw must be int8 [N, ldq>=K], ldq % 16 == 0")
+    LIB("mer_quantize_weight_s8", N, K, w.data_ptr(), w.stride(0), qparams.data_ptr(), qw.data_ptr(), qw.stride(0),
+        colsum.data_ptr(), stream_ptr())
+
+
+def gemm_i8dyn(x2d, x_qparams, qw, w_qparams, colsum, bias, out, act="none"):
+    _check_dev(x2d, qw, out)
+    M, K = x2d.shape
+    N = qw.shape[0]
+    if x2d.stride(1) != 1 or K % 16 or out.shape != (M, N) or x2d.data_ptr() % 16:
+        raise ValueError(f"gemm_i8dyn: bad operands x{tuple(x2d.shape)} qw{tuple(qw.shape)} out{tuple(out.shape)}")
+    _launch("gemm_i8dyn", (M, N, K), "mer_gemm_i8dyn", M, N, K, x2d.data_ptr(), x2d.stride(0), x_qparams.data_ptr(),
+            qw.data_ptr(), qw.stride(0), w_qparams.data_ptr(), colsum.data_ptr(), _ptr(bias), ACT[act], out.data_ptr(),
+            out.stride(0), stream_ptr())
+    return out

@@ -50,9 +50,21 @@ def _e(shape, like, dtype=torch.float32):
     return torch.empty(shape, device=like.device, dtype=dtype)
 
 
+def linear_runner(p: Dict[str, torch.Tensor], qlin: Optional[dict] = None):
+    """``lin(name, x, out, act)`` for the Linear called ``name``: fp32 GEMM, or its dynamic-INT8 image
+    when ``qlin`` (int8.quantize_dynamic_hip) holds one."""
+
+    def lin(name, x, out, act="none"):
+        if qlin is not None and name in qlin:
+            return qlin[name](x, out, act)
+        return K.linear_fwd(x, p[name + ".weight"], p[name + ".bias"], out, act=act)
+
+    return lin
+
+
 def head_forward(p: Dict[str, torch.Tensor], cfg: HeadConfig, v_feat: torch.Tensor, a_seq: torch.Tensor,
-                 training: bool, seed: int = 0):
-    """Returns (logits [B, C], ctx)."""
+                 training: bool, seed: int = 0, qlin: Optional[dict] = None):
+    """Returns (logits [B, C], ctx).  ``qlin``: INT8 images of the plain Linears (inference only)."""
     if cfg.temporal_pooling != "mean":
         raise NotImplementedError("HIP head implements temporal_pooling='mean' (fusion default); "
                                   "attn/transformer pooling are a later row of the build plan")
@@ -70,9 +82,10 @@ def head_forward(p: Dict[str, torch.Tensor], cfg: HeadConfig, v_feat: torch.Tens
     af = a_seq.reshape(B * Ta, sd)
     sv["vf"], sv["af"] = vf, af
 
-    v = K.linear_fwd(vf, p["v_in_proj.weight"], p["v_in_proj.bias"], _e((B * T, d), vf))
-    a_s = K.linear_fwd(af, p["audio_seq_proj.weight"], p["audio_seq_proj.bias"], _e((B * Ta, d), af))
-    a = K.linear_fwd(a_s, p["a_in_proj.weight"], p["a_in_proj.bias"], _e((B * Ta, d), af))
+    lin = linear_runner(p, qlin)
+    v = lin("v_in_proj", vf, _e((B * T, d), vf))
+    a_s = lin("audio_seq_proj", af, _e((B * Ta, d), af))
+    a = lin("a_in_proj", a_s, _e((B * Ta, d), af))
     sv["v"], sv["a_s"], sv["a"] = v, a_s, a
 
     v2a_bias = a2v_bias = None
@@ -131,20 +144,20 @@ def head_forward(p: Dict[str, torch.Tensor], cfg: HeadConfig, v_feat: torch.Tens
 
     if cfg.xattn_head == "concat":
         w0 = p["xattn_mlp.0.weight"]
-        h = K.linear_fwd(emb, w0, p["xattn_mlp.0.bias"], _e((B, w0.shape[0]), v), act="relu")
+        h = lin("xattn_mlp.0", emb, _e((B, w0.shape[0]), v), act="relu")
         K.dropout_(h, dp_mlp, site_seed(seed, 6))
         w3 = p["xattn_mlp.3.weight"]
-        logits = K.linear_fwd(h, w3, p["xattn_mlp.3.bias"], _e((B, w3.shape[0]), v))
+        logits = lin("xattn_mlp.3", h, _e((B, w3.shape[0]), v))
         sv["h"] = h
     elif cfg.xattn_head == "gated":
         w0 = p["xattn_gate.0.weight"]
-        h = K.linear_fwd(emb, w0, p["xattn_gate.0.bias"], _e((B, w0.shape[0]), v), act="relu")
+        h = lin("xattn_gate.0", emb, _e((B, w0.shape[0]), v), act="relu")
         K.dropout_(h, dp_mlp, site_seed(seed, 6))
-        z = K.linear_fwd(h, p["xattn_gate.3.weight"], p["xattn_gate.3.bias"], _e((B, 1), v))
+        z = lin("xattn_gate.3", h, _e((B, 1), v))
         fused, g = _e((B, d), v), _e((B,), v)
         K.gate_mix_fwd(z, emb[:, :d], emb[:, d:], fused, g)
         wc = p["xattn_classifier.weight"]
-        logits = K.linear_fwd(fused, wc, p["xattn_classifier.bias"], _e((B, wc.shape[0]), v))
+        logits = lin("xattn_classifier", fused, _e((B, wc.shape[0]), v))
         sv.update(h=h, g=g, fused=fused)
     else:
         raise ValueError(f"Unknown xattn head: {cfg.xattn_head}")

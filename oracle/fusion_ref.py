@@ -21,7 +21,11 @@ Params = Dict[str, Tensor]
 
 
 def linear(x: Tensor, p: Params, name: str) -> Tensor:
-    """nn.Linear: ``x W^T + b``."""
+    """nn.Linear: ``x W^T + b`` (dynamic INT8 when ``int8_ref.quantize_params`` marked it)."""
+    if name + "._qweight" in p:
+        from .int8_ref import linear_int8_torch
+
+        return linear_int8_torch(x, p, name)
     y = x @ p[name + ".weight"].t()
     b = p.get(name + ".bias")
     return y + b if b is not None else y

@@ -49,6 +49,11 @@ def _bn(n: str, c: int):
 
 
 def batch_norm(x: Tensor, p: Dict[str, Tensor], n: str, training: bool) -> Tensor:
+    """nn.BatchNorm2d (momentum 0.1): train mode normalises with batch stats, updates the running
+    stats (unbiased var) and counts the batch in ``num_batches_tracked``; eval uses running stats."""
+    if training and (n + "num_batches_tracked") in p:
+        with torch.no_grad():
+            p[n + "num_batches_tracked"].add_(1)
     return F.batch_norm(x, p[n + "running_mean"], p[n + "running_var"], p[n + "weight"], p[n + "bias"],
                         training=training, momentum=0.1, eps=1e-5)
 

@@ -146,3 +146,33 @@ def test_resnet18_structure():
     x = torch.randn(2, 3, 112, 112)
     y = resnet18_ref.resnet18_trunk(p, x, training=True)
     assert tuple(y.shape) == (2, 512, 1, 1)
+
+
+def test_int8_head_c5():
+    """Dynamic-INT8 xattn head at B=64 (C5) vs the reference's CPU quantize_dynamic output."""
+    from oracle import int8_ref
+
+    g = golden("int8_head_b64.npz")
+    head_linears = sorted(n for n in g["quantized"] if not n.startswith(("audio_model.", "video_model.")))
+    assert head_linears == sorted(int8_ref.XATTN_INT8["concat"])
+    p = int8_ref.quantize_params(xattn_params("concat", False), head_linears)
+    v, a = params.feature_inputs(64, 8, 149, seed=21)
+    with torch.no_grad():
+        fp, _ = fusion_ref.xattn_forward(xattn_params("concat", False), torch.from_numpy(v), torch.from_numpy(a))
+        lq, _ = fusion_ref.xattn_forward(p, torch.from_numpy(v), torch.from_numpy(a))
+    np.testing.assert_allclose(fp.numpy(), g["logits_fp32"], atol=2e-5)
+    np.testing.assert_allclose(lq.numpy(), g["logits_int8"], atol=2e-5)
+    assert (lq.argmax(1).numpy() == g["logits_int8"].argmax(1)).all()
+
+
+def test_int8_qparams_edge_cases():
+    from oracle import int8_ref
+
+    # all-positive / all-negative / all-zero inputs (zero point pinned to the range ends; scale fallback)
+    assert int8_ref.choose_qparams(0.5, 2.0)[1] == 0
+    assert int8_ref.choose_qparams(-2.0, -0.5)[1] == 127
+    assert float(int8_ref.choose_qparams(0.0, 0.0)[0]) == np.float32(0.1)
+    s, _ = int8_ref.choose_qparams(-1e-6, 1e-6)
+    assert float(s) == np.float32(6.1e-5)
+    qw, ws = int8_ref.quantize_weight(np.array([[1.0, -2.0], [0.5, 0.0]], np.float32))
+    assert qw.min() >= -128 and qw.max() <= 127 and float(ws) == np.float32(2.0 / 127.5)
