@@ -125,6 +125,13 @@ int mer_gemm_bf16(int M, int N, int K, const void* A, long a_gstride, long a_rst
                   long ldw, void* C, int c_dtype, long ldc, const float* bias, const void* R, long ldr, int act,
                   void* stream);
 
+/* mer_gemm_bf16 with an explicit kernel variant: -1 auto (what mer_gemm_bf16 does), 0 the 128x128
+ * register-staged kernel (any K % 8 == 0), 1/2/3 the global_load_lds pipelined kernel with 256x256 /
+ * 256x128 / 128x128 tiles (K % 64 == 0; otherwise variant 0 runs). */
+int mer_gemm_bf16_ex(int M, int N, int K, const void* A, long a_gstride, long a_rstride, int a_rpg, const void* W,
+                     long ldw, void* C, int c_dtype, long ldc, const float* bias, const void* R, long ldr, int act,
+                     int variant, void* stream);
+
 /* Grouped positional Conv1d of WavLM (TF:48-90): out[b,t,g*Cg+n] = act(sum_{tap,c} X[b,t+tap-pad,g*Cg+c]
  * Wp[g][n][tap][c] + bias) (+ R), rows t in [0, L) (the SamePad crop).  Wp is the weight-normed, bf16
  * repacked kernel (mer_weightnorm_scale + mer_permute3_bf16). */
@@ -220,10 +227,10 @@ int mer_avgpool_bwd(int N, int HW, int C, const float* dy, void* dx, void* strea
  * (torch.quantization.quantize_dynamic(model, {nn.Linear}, qint8), fbgemm semantics -- oracle/int8_ref.py).
  * qparams are 4 floats on the device: {scale, 1/scale, zero_point, 0}. */
 
-/* min/max over x[0:n] (partial = 2*512 floats of workspace) -> qparams.  mode 0: activation
+/* min/max over x[0:n] (fp32 or bf16; partial = 2*512 floats of workspace) -> qparams.  mode 0: activation
  * (fbgemm ChooseQuantizationParams, range [0,127] = reduce_range); mode 1: symmetric weight scale
  * max(amax/127.5, FLT_EPSILON), zero point 0. */
-int mer_quant_params_f32(long n, const float* x, float* partial, int mode, float* qparams, void* stream);
+int mer_quant_params(long n, const void* x, int x_dtype, float* partial, int mode, float* qparams, void* stream);
 
 /* qw[n, 0:ldq] = int8 clamp(rint(W[n,k] / ws)) (zero for k >= K); colsum[n] = sum_k qw[n,k].
  * ldq % 16 == 0.  Run once per Linear when the model is quantized. */
@@ -231,10 +238,10 @@ int mer_quantize_weight_s8(int N, int K, const float* w, long ldw, const float* 
                            int* colsum, void* stream);
 
 /* out[m,n] = act(fma(sum_k qx[m,k] qw[n,k] - zp * colsum[n], xs*ws, bias[n])) with
- * qx = clamp(rint(fma(x, 1/xs, zp)), 0, 255) computed on the fly from fp32 x (K % 16 == 0;
+ * qx = clamp(rint(fma(x, 1/xs, zp)), 0, 255) computed on the fly from fp32 / bf16 x (K % 16 == 0;
  * act 0 or 1).  The quantized Linear forward (torch.ao.nn.quantized.dynamic.Linear). */
-int mer_gemm_i8dyn(int M, int N, int K, const float* x, long ldx, const float* x_qparams, const void* qw, long ldq,
-                   const float* w_qparams, const int* colsum, const float* bias, int act, float* out, long ldo,
+int mer_gemm_i8dyn(int M, int N, int K, const void* x, int x_dtype, long ldx, const float* x_qparams, const void* qw,
+                   long ldq, const float* w_qparams, const int* colsum, const float* bias, int act, float* out, long ldo,
                    void* stream);
 
 #ifdef __cplusplus

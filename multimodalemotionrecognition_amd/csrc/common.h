@@ -88,4 +88,9 @@ __device__ __forceinline__ void xcd_tile(int pid, int nx, int ntiles, int& tx, i
   tx = tile - ty * nx;
 }
 
+// 16-byte global -> LDS DMA (global_load_lds_dwordx4): lane i's 16 bytes land at lds + 16*i (the LDS
+// pointer must be wave-uniform).  Wrapped in a non-template function: used directly inside a kernel
+// TEMPLATE, hipcc (ROCm 7.2) silently drops the host launch stub (undefined symbol at load time).
+__device__ __forceinline__ void glds16(const void* g, void* lds) { __builtin_amdgcn_global_load_lds(g, lds, 16, 0, 0); }
+
 #define MER_LAUNCH_CHECK() return (int)hipGetLastError()

@@ -145,6 +145,159 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs g) {
     }
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// Pipelined variant (K % 64 == 0, mode 0): global_load_lds (16 B per lane) straight into a
+// double-buffered LDS image, next K-tile issued BEFORE the current one is consumed, one
+// vmcnt(0) + barrier per K-tile (cdna_hip_programming.md §5 "Minimum 2-phase").
+// LDS image per operand: [rows][64 bf16] = 128-byte rows of eight 16-byte chunks; chunk c of
+// row r lives at physical chunk c ^ ((r >> 1) & 7), so the 16 rows one ds_read_b128 lane group
+// touches (same logical chunk) cover all sixteen 16-byte bank slots of a 256-byte bank row.
+// glds writes lane-linear (base + 16*lane), so the XOR goes on each lane's SOURCE address and on
+// the fragment read (rule 21: both sides).  Rows past M/N are clamped to the last valid row (their
+// outputs are discarded); K is a multiple of 64, so no K tail.
+template <int BM_, int BN_, int WM_, int WN_>
+struct PipeCfg {
+  static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_;       // tile, waves along M / N
+  static constexpr int WAVES = WM * WN, NT = 64 * WAVES;
+  static constexpr int TM = BM / WM, TN = BN / WN;                  // per-wave output
+  static constexpr int FM = TM / 16, FN = TN / 16;                  // 16x16 fragments per wave
+  static constexpr int IA = BM / 8 / WAVES, IB = BN / 8 / WAVES;    // glds per wave per K-tile
+  static constexpr int BUF = (BM + BN) * 64;                        // bf16 elements per LDS buffer
+  static_assert(IA * 8 * WAVES == BM && IB * 8 * WAVES == BN, "tile rows must split into 8-row glds pieces");
+};
+
+__device__ __forceinline__ int swz_chunk(int row, int c) { return c ^ ((row >> 1) & 7); }
+
+template <class CF, typename TOUT>
+__global__ __launch_bounds__(CF::NT, 1) void gemm_pipe_kernel(GemmArgs g) {
+  extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int nx = (g.N + CF::BN - 1) / CF::BN, ny = (g.M + CF::BM - 1) / CF::BM;
+  int tx, ty;
+  xcd_tile(blockIdx.x, nx, nx * ny, tx, ty);
+  const int m0 = ty * CF::BM, n0 = tx * CF::BN;
+  const int wr = w / CF::WN, wc = w % CF::WN;
+
+  // per-lane source pointers (fixed over K; advanced by 64 elements per K-tile)
+  const bf16_t* pa[CF::IA];
+  const bf16_t* pb[CF::IB];
+  const int lrow = lane >> 3, lchunk = lane & 7;
+#pragma unroll
+  for (int j = 0; j < CF::IA; ++j) {
+    const int r = (w * CF::IA + j) * 8 + lrow;
+    int m = m0 + r;
+    m = m < g.M ? m : g.M - 1;
+    pa[j] = g.A + (long)(m / g.a_rpg) * g.a_gstride + (long)(m % g.a_rpg) * g.a_rstride + swz_chunk(r, lchunk) * 8;
+  }
+#pragma unroll
+  for (int j = 0; j < CF::IB; ++j) {
+    const int r = (w * CF::IB + j) * 8 + lrow;
+    int n = n0 + r;
+    n = n < g.N ? n : g.N - 1;
+    pb[j] = g.B + (long)n * g.ldb + swz_chunk(r, lchunk) * 8;
+  }
+  auto stage = [&](int buf, int k0) {
+    bf16_t* la = smem + buf * CF::BUF;
+    bf16_t* lb = la + CF::BM * 64;
+#pragma unroll
+    for (int j = 0; j < CF::IA; ++j)
+      glds16(pa[j] + k0, la + (w * CF::IA + j) * 512);
+#pragma unroll
+    for (int j = 0; j < CF::IB; ++j)
+      glds16(pb[j] + k0, lb + (w * CF::IB + j) * 512);
+  };
+
+  f32x4 acc[CF::FM][CF::FN];
+#pragma unroll
+  for (int i = 0; i < CF::FM; ++i)
+#pragma unroll
+    for (int j = 0; j < CF::FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // fragment read offsets (elements) inside one operand image, per k-step s: row*64 + phys_chunk*8
+  const int fr = lane & 15, fq = lane >> 4;
+  const int nk = g.K / 64;
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) stage(cur ^ 1, (kt + 1) * 64);
+    const bf16_t* la = smem + cur * CF::BUF;
+    const bf16_t* lb = la + CF::BM * 64;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8 af[CF::FM], bfr[CF::FN];
+#pragma unroll
+      for (int i = 0; i < CF::FM; ++i) {
+        const int r = wr * CF::TM + i * 16 + fr;
+        af[i] = *reinterpret_cast<const bf16x8*>(la + r * 64 + swz_chunk(r, s * 4 + fq) * 8);
+      }
+#pragma unroll
+      for (int j = 0; j < CF::FN; ++j) {
+        const int r = wc * CF::TN + j * 16 + fr;
+        bfr[j] = *reinterpret_cast<const bf16x8*>(lb + r * 64 + swz_chunk(r, s * 4 + fq) * 8);
+      }
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < CF::FM; ++i)
+#pragma unroll
+        for (int j = 0; j < CF::FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  TOUT* C = reinterpret_cast<TOUT*>(g.C);
+#pragma unroll
+  for (int j = 0; j < CF::FN; ++j) {
+    const int col = n0 + wc * CF::TN + j * 16 + fr;
+    if (col >= g.N) continue;
+    const float bv = g.bias ? g.bias[col] : 0.f;
+#pragma unroll
+    for (int i = 0; i < CF::FM; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wr * CF::TM + i * 16 + fq * 4 + r;
+        if (row >= g.M) continue;
+        float v = apply_act(acc[i][j][r] + bv, g.act);
+        if (g.R) v += bf2f(g.R[(long)row * g.ldr + col]);
+        stf<TOUT>(C, (long)row * g.ldc + col, v);
+      }
+  }
+}
+
+using CfgL = PipeCfg<256, 256, 2, 4>;  // 8 waves, 128x64 per wave, 128 KiB LDS
+using CfgM = PipeCfg<256, 128, 4, 2>;  // 8 waves, 64x64 per wave, 96 KiB LDS
+using CfgS = PipeCfg<128, 128, 2, 2>;  // 4 waves, 64x64 per wave, 64 KiB LDS
+
+template <class CF, typename TOUT>
+int launch_pipe_t(const GemmArgs& g, hipStream_t st) {
+  const long tiles = (long)((g.N + CF::BN - 1) / CF::BN) * ((g.M + CF::BM - 1) / CF::BM);
+  const size_t lds = 2 * CF::BUF * sizeof(bf16_t);
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_pipe_kernel<CF, TOUT>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+    return (int)hipErrorInvalidConfiguration;
+  hipLaunchKernelGGL((gemm_pipe_kernel<CF, TOUT>), dim3((unsigned)tiles), dim3(CF::NT), lds, st, g);
+  return (int)hipGetLastError();
+}
+
+template <class CF>
+int launch_pipe(const GemmArgs& g, int out_dtype, hipStream_t st) {
+  return out_dtype == MER_BF16 ? launch_pipe_t<CF, bf16_t>(g, st) : launch_pipe_t<CF, float>(g, st);
+}
+
+// Tile choice: the largest tile whose grid still gives every CU work (256 CUs), else smaller tiles.
+int pick_variant(int M, int N) {
+  const long tl = (long)((M + 255) / 256) * ((N + 255) / 256);
+  const long tm = (long)((M + 255) / 256) * ((N + 127) / 128);
+  if (tl >= 240) return 1;
+  if (tm >= 240) return 2;
+  return 3;
+}
+
 template <int AMODE>
 int launch(const GemmArgs& g, int out_dtype, int groups, hipStream_t st) {
   dim3 grid(((g.N + BN - 1) / BN) * ((g.M + BM - 1) / BM), 1, groups);
@@ -160,7 +313,15 @@ int launch(const GemmArgs& g, int out_dtype, int groups, hipStream_t st) {
 MER_API int mer_gemm_bf16(int M, int N, int K, const void* A, long a_gstride, long a_rstride, int a_rpg, const void* W,
                           long ldw, void* C, int c_dtype, long ldc, const float* bias, const void* R, long ldr, int act,
                           void* stream) {
+  return mer_gemm_bf16_ex(M, N, K, A, a_gstride, a_rstride, a_rpg, W, ldw, C, c_dtype, ldc, bias, R, ldr, act, -1,
+                          stream);
+}
+
+MER_API int mer_gemm_bf16_ex(int M, int N, int K, const void* A, long a_gstride, long a_rstride, int a_rpg,
+                             const void* W, long ldw, void* C, int c_dtype, long ldc, const float* bias, const void* R,
+                             long ldr, int act, int variant, void* stream) {
   if (M <= 0 || N <= 0) return 0;
+  if (variant < -1 || variant > 3) return (int)hipErrorInvalidValue;
   if (K % 8 != 0 || a_rpg <= 0 || (a_rstride % 8) != 0 || (a_gstride % 8) != 0 || (ldw % 8) != 0)
     return (int)hipErrorInvalidValue;
   if ((((uintptr_t)A) | ((uintptr_t)W)) & 15) return (int)hipErrorInvalidValue;
@@ -170,7 +331,15 @@ MER_API int mer_gemm_bf16(int M, int N, int K, const void* A, long a_gstride, lo
   g.B = (const bf16_t*)W; g.ldb = ldw; g.b_zstride = 0;
   g.C = C; g.ldc = ldc; g.c_zoff = 0;
   g.bias = bias; g.R = (const bf16_t*)R; g.ldr = ldr; g.act = act;
-  return launch<0>(g, c_dtype, 1, (hipStream_t)stream);
+  const hipStream_t st = (hipStream_t)stream;
+  if (K % 64 != 0) variant = 0;
+  if (variant == -1) variant = pick_variant(M, N);
+  switch (variant) {
+    case 1: return launch_pipe<CfgL>(g, c_dtype, st);
+    case 2: return launch_pipe<CfgM>(g, c_dtype, st);
+    case 3: return launch_pipe<CfgS>(g, c_dtype, st);
+    default: return launch<0>(g, c_dtype, 1, st);
+  }
 }
 
 MER_API int mer_posconv_gemm_bf16(int B, int L, int C_total, int groups, int taps, int pad, const void* X, long ldx,

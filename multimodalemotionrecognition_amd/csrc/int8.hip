@@ -21,19 +21,25 @@ typedef __attribute__((ext_vector_type(4))) int i32x4;
 
 constexpr int MM_BLOCKS = 512, MM_THREADS = 256;
 
-__global__ __launch_bounds__(MM_THREADS) void minmax_partial_kernel(long n, const float* __restrict__ x,
+template <typename T>
+__global__ __launch_bounds__(MM_THREADS) void minmax_partial_kernel(long n, const T* __restrict__ x,
                                                                     float* __restrict__ part) {
+  constexpr int V = 16 / sizeof(T);  // elements per 16-byte load
   float lo = INFINITY, hi = -INFINITY;
-  const long n4 = n >> 2;
-  const float4* x4 = reinterpret_cast<const float4*>(x);
-  for (long i = blockIdx.x * (long)MM_THREADS + threadIdx.x; i < n4; i += (long)gridDim.x * MM_THREADS) {
-    const float4 v = x4[i];
-    lo = fminf(lo, fminf(fminf(v.x, v.y), fminf(v.z, v.w)));
-    hi = fmaxf(hi, fmaxf(fmaxf(v.x, v.y), fmaxf(v.z, v.w)));
+  const long nv = n / V;
+  for (long i = blockIdx.x * (long)MM_THREADS + threadIdx.x; i < nv; i += (long)gridDim.x * MM_THREADS) {
+    const uint4 raw = reinterpret_cast<const uint4*>(x)[i];
+    const T* e = reinterpret_cast<const T*>(&raw);
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      const float v = ldf<T>(e, j);
+      lo = fminf(lo, v);
+      hi = fmaxf(hi, v);
+    }
   }
-  for (long i = (n4 << 2) + blockIdx.x * (long)MM_THREADS + threadIdx.x; i < n; i += (long)gridDim.x * MM_THREADS) {
-    lo = fminf(lo, x[i]);
-    hi = fmaxf(hi, x[i]);
+  for (long i = nv * V + blockIdx.x * (long)MM_THREADS + threadIdx.x; i < n; i += (long)gridDim.x * MM_THREADS) {
+    lo = fminf(lo, ldf<T>(x, i));
+    hi = fmaxf(hi, ldf<T>(x, i));
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -115,6 +121,26 @@ __global__ void minmax_final_kernel(int nparts, const float* __restrict__ part, 
 }
 
 // one block per output row n: quantize W[n, :] and its integer row sum (the zero-point correction)
+// 16 consecutive elements as fp32
+template <typename T> __device__ __forceinline__ void load16(const T* p, float4 (&f)[4]);
+template <> __device__ __forceinline__ void load16<float>(const float* p, float4 (&f)[4]) {
+  const float4* s = reinterpret_cast<const float4*>(p);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) f[i] = s[i];
+}
+template <> __device__ __forceinline__ void load16<bf16_t>(const bf16_t* p, float4 (&f)[4]) {
+  const uint4* s = reinterpret_cast<const uint4*>(p);
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const uint4 u = s[h];
+    const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      f[2 * h + j] = float4{__uint_as_float(w[2 * j] << 16), __uint_as_float(w[2 * j] & 0xffff0000u),
+                            __uint_as_float(w[2 * j + 1] << 16), __uint_as_float(w[2 * j + 1] & 0xffff0000u)};
+  }
+}
+
 __global__ __launch_bounds__(256) void quantize_weight_kernel(int K, const float* __restrict__ w, long ldw,
                                                               const float* __restrict__ qp, int8_t* __restrict__ qw,
                                                               long ldq, int* __restrict__ colsum) {
@@ -146,7 +172,8 @@ __device__ __forceinline__ uint32_t pack_q4(float4 v, float inv, float zp) {
   return q(v.x) | (q(v.y) << 8) | (q(v.z) << 16) | (q(v.w) << 24);
 }
 
-__global__ __launch_bounds__(256) void gemm_i8dyn_kernel(int M, int N, int K, const float* __restrict__ x, long ldx,
+template <typename T>
+__global__ __launch_bounds__(256) void gemm_i8dyn_kernel(int M, int N, int K, const T* __restrict__ x, long ldx,
                                                          const float* __restrict__ xqp, const int8_t* __restrict__ qw,
                                                          long ldq, const float* __restrict__ wqp,
                                                          const int* __restrict__ colsum, const float* __restrict__ bias,
@@ -172,11 +199,12 @@ __global__ __launch_bounds__(256) void gemm_i8dyn_kernel(int M, int N, int K, co
       const int m = m0 + r, k = k0 + kc;
       uint4 pk = {0u, 0u, 0u, 0u};  // zero bytes contribute nothing (W is zero-padded too)
       if (m < M && k < K) {
-        const float4* src = reinterpret_cast<const float4*>(x + (long)m * ldx + k);
-        pk.x = pack_q4(src[0], inv, zp);
-        pk.y = pack_q4(src[1], inv, zp);
-        pk.z = pack_q4(src[2], inv, zp);
-        pk.w = pack_q4(src[3], inv, zp);
+        float4 f[4];
+        load16<T>(x + (long)m * ldx + k, f);
+        pk.x = pack_q4(f[0], inv, zp);
+        pk.y = pack_q4(f[1], inv, zp);
+        pk.z = pack_q4(f[2], inv, zp);
+        pk.w = pack_q4(f[3], inv, zp);
       }
       *reinterpret_cast<uint4*>(&la[r * LDS_ROW + kc]) = pk;
     }
@@ -221,19 +249,26 @@ __global__ __launch_bounds__(256) void gemm_i8dyn_kernel(int M, int N, int K, co
   }
 }
 
-int minmax_qparams(long n, const float* x, float* part, int mode, float* qp, hipStream_t st) {
+int minmax_qparams(long n, const void* x, int dtype, float* part, int mode, float* qp, hipStream_t st) {
   long blocks = (n / 4 + MM_THREADS - 1) / MM_THREADS;
   blocks = blocks < 1 ? 1 : (blocks > MM_BLOCKS ? MM_BLOCKS : blocks);
-  hipLaunchKernelGGL(minmax_partial_kernel, dim3((unsigned)blocks), dim3(MM_THREADS), 0, st, n, x, part);
+  if (dtype == MER_BF16)
+    hipLaunchKernelGGL(minmax_partial_kernel<bf16_t>, dim3((unsigned)blocks), dim3(MM_THREADS), 0, st, n,
+                       (const bf16_t*)x, part);
+  else
+    hipLaunchKernelGGL(minmax_partial_kernel<float>, dim3((unsigned)blocks), dim3(MM_THREADS), 0, st, n,
+                       (const float*)x, part);
   hipLaunchKernelGGL(minmax_final_kernel, dim3(1), dim3(64), 0, st, (int)blocks, part, mode, qp);
   return (int)hipGetLastError();
 }
 
 }  // namespace
 
-MER_API int mer_quant_params_f32(long n, const float* x, float* partial, int mode, float* qparams, void* stream) {
-  if (n <= 0 || (mode != 0 && mode != 1) || (((uintptr_t)x) & 15)) return (int)hipErrorInvalidValue;
-  return minmax_qparams(n, x, partial, mode, qparams, (hipStream_t)stream);
+MER_API int mer_quant_params(long n, const void* x, int x_dtype, float* partial, int mode, float* qparams,
+                             void* stream) {
+  if (n <= 0 || (mode != 0 && mode != 1) || (((uintptr_t)x) & 15) || (mode == 1 && x_dtype != MER_F32))
+    return (int)hipErrorInvalidValue;
+  return minmax_qparams(n, x, x_dtype, partial, mode, qparams, (hipStream_t)stream);
 }
 
 MER_API int mer_quantize_weight_s8(int N, int K, const float* w, long ldw, const float* qparams, void* qw, long ldq,
@@ -244,14 +279,20 @@ MER_API int mer_quantize_weight_s8(int N, int K, const float* w, long ldw, const
   return (int)hipGetLastError();
 }
 
-MER_API int mer_gemm_i8dyn(int M, int N, int K, const float* x, long ldx, const float* x_qparams, const void* qw,
-                           long ldq, const float* w_qparams, const int* colsum, const float* bias, int act, float* out,
-                           long ldo, void* stream) {
+MER_API int mer_gemm_i8dyn(int M, int N, int K, const void* x, int x_dtype, long ldx, const float* x_qparams,
+                           const void* qw, long ldq, const float* w_qparams, const int* colsum, const float* bias,
+                           int act, float* out, long ldo, void* stream) {
   if (M <= 0 || N <= 0) return 0;
-  if (K % 16 != 0 || ldx % 4 != 0 || ldq < K || ldq % 16 != 0 || (((uintptr_t)x) & 15) || (((uintptr_t)qw) & 15))
+  if (K % 16 != 0 || ldx % 8 != 0 || ldq < K || ldq % 16 != 0 || (((uintptr_t)x) & 15) || (((uintptr_t)qw) & 15))
     return (int)hipErrorInvalidValue;
   const long tiles = (long)((M + BM - 1) / BM) * ((N + BN - 1) / BN);
-  hipLaunchKernelGGL(gemm_i8dyn_kernel, dim3((unsigned)tiles), dim3(256), 0, (hipStream_t)stream, M, N, K, x, ldx,
-                     x_qparams, (const int8_t*)qw, ldq, w_qparams, colsum, bias, act, out, ldo);
+  if (x_dtype == MER_BF16)
+    hipLaunchKernelGGL(gemm_i8dyn_kernel<bf16_t>, dim3((unsigned)tiles), dim3(256), 0, (hipStream_t)stream, M, N, K,
+                       (const bf16_t*)x, ldx, x_qparams, (const int8_t*)qw, ldq, w_qparams, colsum, bias, act, out,
+                       ldo);
+  else
+    hipLaunchKernelGGL(gemm_i8dyn_kernel<float>, dim3((unsigned)tiles), dim3(256), 0, (hipStream_t)stream, M, N, K,
+                       (const float*)x, ldx, x_qparams, (const int8_t*)qw, ldq, w_qparams, colsum, bias, act, out,
+                       ldo);
   return (int)hipGetLastError();
 }

@@ -237,7 +237,7 @@ def _aligned16(*ts):
             raise ValueError("bf16 GEMM operands must be 16-byte aligned")
 
 
-def gemm_bf16(a, w, out, *, M=None, K=None, rows=None, bias=None, residual=None, act="none"):
+def gemm_bf16(a, w, out, *, M=None, K=None, rows=None, bias=None, residual=None, act="none", variant=-1):
     """out[M,N] = act(A W^T + bias) (+ residual) on bf16 MFMA.
 
     ``a``: bf16 [M,K] (row stride a.stride(0)), or a raw bf16 buffer with ``rows=(rpg, rstride, gstride)``
@@ -252,9 +252,9 @@ def gemm_bf16(a, w, out, *, M=None, K=None, rows=None, bias=None, residual=None,
     if out.shape[-1] != N or out.numel() != M * N:
         raise ValueError(f"gemm_bf16 out shape {tuple(out.shape)} != ({M},{N})")
     _aligned16(a, w)
-    _launch("gemm_bf16", (M, N, K), "mer_gemm_bf16", M, N, K, a.data_ptr(), rows[2], rows[1], rows[0], w.data_ptr(), w.stride(0),
-        out.data_ptr(), _dt(out), N if out.dim() < 2 else out.stride(-2), _ptr(bias), _ptr(residual),
-        0 if residual is None else residual.stride(-2), ACT[act], stream_ptr())
+    _launch("gemm_bf16", (M, N, K), "mer_gemm_bf16_ex", M, N, K, a.data_ptr(), rows[2], rows[1], rows[0], w.data_ptr(),
+            w.stride(0), out.data_ptr(), _dt(out), N if out.dim() < 2 else out.stride(-2), _ptr(bias), _ptr(residual),
+            0 if residual is None else residual.stride(-2), ACT[act], int(variant), stream_ptr())
     return out
 
 
@@ -412,9 +412,10 @@ QP_PARTIAL = 2 * 512  # floats of min/max workspace for mer_quant_params_f32
 def quant_params(x, partial, qparams, mode):
     """qparams[4] = {scale, 1/scale, zero_point, 0} from min/max over all of x (mode 0 act, 1 weight)."""
     _check_dev(x, partial, qparams)
-    if not x.is_contiguous() or x.dtype != torch.float32 or x.data_ptr() % 16:
-        raise ValueError("quant_params needs a contiguous 16-byte aligned fp32 tensor")
-    LIB("mer_quant_params_f32", x.numel(), x.data_ptr(), partial.data_ptr(), int(mode), qparams.data_ptr(), stream_ptr())
+    if not x.is_contiguous() or x.data_ptr() % 16:
+        raise ValueError("quant_params needs a contiguous 16-byte aligned tensor")
+    LIB("mer_quant_params", x.numel(), x.data_ptr(), _dt(x), partial.data_ptr(), int(mode), qparams.data_ptr(),
+        stream_ptr())
 
 
 def quantize_weight_s8(w, qparams, qw, colsum):
@@ -429,9 +430,9 @@ def gemm_i8dyn(x2d, x_qparams, qw, w_qparams, colsum, bias, out, act="none"):
     _check_dev(x2d, qw, out)
     M, K = x2d.shape
     N = qw.shape[0]
-    if x2d.stride(1) != 1 or K % 16 or out.shape != (M, N) or x2d.data_ptr() % 16:
+    if x2d.stride(1) != 1 or x2d.stride(0) % 8 or K % 16 or out.shape != (M, N) or x2d.data_ptr() % 16:
         raise ValueError(f"gemm_i8dyn: bad operands x{tuple(x2d.shape)} qw{tuple(qw.shape)} out{tuple(out.shape)}")
-    _launch("gemm_i8dyn", (M, N, K), "mer_gemm_i8dyn", M, N, K, x2d.data_ptr(), x2d.stride(0), x_qparams.data_ptr(),
+    _launch("gemm_i8dyn", (M, N, K), "mer_gemm_i8dyn", M, N, K, x2d.data_ptr(), _dt(x2d), x2d.stride(0), x_qparams.data_ptr(),
             qw.data_ptr(), qw.stride(0), w_qparams.data_ptr(), colsum.data_ptr(), _ptr(bias), ACT[act], out.data_ptr(),
             out.stride(0), stream_ptr())
     return out

@@ -26,7 +26,7 @@ def _rng(seed: int, name: str) -> np.random.Generator:
 def init_tensor(name: str, shape: Tuple[int, ...], seed: int = 0) -> np.ndarray:
     """Name-driven init that keeps activations O(1) through every layer."""
     arr = _init_tensor(name, shape, seed)
-    return np.ascontiguousarray(np.asarray(arr).reshape(tuple(int(s) for s in shape)))
+    return np.array(np.asarray(arr).reshape(tuple(int(s) for s in shape)), order="C")
 
 
 def _init_tensor(name: str, shape: Tuple[int, ...], seed: int = 0):

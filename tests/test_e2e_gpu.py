@@ -65,13 +65,13 @@ def test_train_step_vs_oracle():
 
     after = m.state_dict()
     # train-mode BN side effects (running stats, counter) match the oracle's
-    for k in ("video_model.backbone.bn1.running_mean", "video_model.backbone.layer4.1.bn2.running_var"):
+    for k in ("video_model.backbone.1.running_mean", "video_model.backbone.7.1.bn2.running_var"):
         d = float((after[k].cpu() - p[k]).abs().max())
         assert d < 2e-2 * max(1.0, float(p[k].abs().max())), (k, d)
-    assert int(after["video_model.backbone.bn1.num_batches_tracked"]) == int(p["video_model.backbone.bn1.num_batches_tracked"]) == 1
+    assert int(after["video_model.backbone.1.num_batches_tracked"]) == int(p["video_model.backbone.1.num_batches_tracked"]) == 1
     # first Adam step is ~ -lr*sign(g): compare update directions
-    for k, lo in (("xattn_mlp.3.weight", 0.97), ("v_in_proj.weight", 0.9), ("video_model.backbone.layer4.1.conv2.weight", 0.75),
-                  ("video_model.backbone.conv1.weight", 0.75)):
+    for k, lo in (("xattn_mlp.3.weight", 0.97), ("v_in_proj.weight", 0.9), ("video_model.backbone.7.1.conv2.weight", 0.75),
+                  ("video_model.backbone.0.weight", 0.75)):
         dh = (after[k].cpu() - before[k].cpu()).flatten()
         dr = (p[k].detach() - torch.from_numpy(OP.init_state([(k, tuple(p[k].shape))])[k])).flatten()
         agree = float(((dh > 0) == (dr > 0)).float().mean())

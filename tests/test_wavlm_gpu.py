@@ -73,3 +73,34 @@ def test_gemm_bf16_shapes_vs_fp32():
         K.gemm_bf16(a.cuda(), w.cuda(), out, bias=b.cuda(), residual=r.cuda(), act="gelu")
         err = float((out.cpu() - ref).abs().max())
         assert err < 2e-2 * max(1.0, (Kd / 64) ** 0.5), (M, N, Kd, err)
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+def test_gemm_bf16_variants(variant):
+    """Every GEMM kernel variant (register-staged 128^2, glds-pipelined 256^2 / 256x128 / 128^2) on ragged
+    shapes and in Conv1d 'rows' mode, vs fp32 torch on the same bf16 operands."""
+    from multimodalemotionrecognition_amd import kernels as K
+
+    torch.manual_seed(variant)
+    for M, N, Kd in [(1, 8, 64), (300, 130, 192), (517, 2304, 768), (4768, 768, 3072)]:
+        a = torch.randn(M, Kd).bfloat16()
+        w = torch.randn(N, Kd).bfloat16()
+        b = torch.randn(N)
+        r = torch.randn(M, N).bfloat16()
+        ref = torch.nn.functional.gelu(a.float() @ w.float().t() + b) + r.float()
+        for odt in (torch.float32, torch.bfloat16):
+            out = torch.empty(M, N, device="cuda", dtype=odt)
+            K.gemm_bf16(a.cuda(), w.cuda(), out, bias=b.cuda(), residual=r.cuda(), act="gelu", variant=variant)
+            err = float((out.float().cpu() - ref).abs().max())
+            tol = (2e-2 * max(1.0, (Kd / 64) ** 0.5)) if odt == torch.float32 else 0.02 * float(ref.abs().max())
+            assert err < tol, (variant, M, N, Kd, odt, err)
+    # channel-last Conv1d(512, 512, k=3, s=2) as GEMM rows (WavLM conv1 layout), 3 clips
+    Bc, Lin, C = 3, 301, 512
+    Lout = (Lin - 3) // 2 + 1
+    x = torch.randn(Bc, Lin, C).bfloat16()
+    wc = torch.randn(C, 3 * C).bfloat16() * 0.05
+    ref = torch.nn.functional.conv1d(x.float().transpose(1, 2), wc.float().view(C, 3, C).permute(0, 2, 1), stride=2)
+    ref = ref.transpose(1, 2).reshape(Bc * Lout, C)
+    out = torch.empty(Bc * Lout, C, device="cuda", dtype=torch.float32)
+    K.gemm_bf16(x.cuda(), wc.cuda(), out, M=Bc * Lout, K=3 * C, rows=(Lout, 2 * C, Lin * C), variant=variant)
+    assert float((out.cpu() - ref).abs().max()) < 2e-2 * (3 * C / 64) ** 0.5 * 0.05 * 8

@@ -1,0 +1,51 @@
+"""Time every bf16 GEMM variant on the north-star's WavLM shapes (B=32): python tools/bench_gemm.py"""
+import sys
+from pathlib import Path
+
+import torch
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+from multimodalemotionrecognition_amd import kernels as K  # noqa: E402
+
+B = 32
+SHAPES = {
+    "conv1 (rows)": (B * 4799, 512, 1536, (4799, 1024, 9599 * 512), B * 9599 * 512),
+    "conv2 (rows)": (B * 2399, 512, 1536, (2399, 1024, 4799 * 512), B * 4799 * 512),
+    "qkv": (B * 149, 2304, 768, None, None),
+    "ffn1": (B * 149, 3072, 768, None, None),
+    "ffn2": (B * 149, 768, 3072, None, None),
+    "out_proj": (B * 149, 768, 768, None, None),
+}
+
+
+def main():
+    torch.manual_seed(0)
+    for name, (M, N, Kd, rows, alen) in SHAPES.items():
+        a = (torch.rand(alen if rows else M * Kd, device="cuda") * 2 - 1).bfloat16()
+        if not rows:
+            a = a.view(M, Kd)
+        w = (torch.rand(N, Kd, device="cuda") * 2 - 1).bfloat16()
+        outs = {}
+        for odt in (torch.bfloat16,):
+            for v in (0, 1, 2, 3):
+                out = torch.empty(M, N, device="cuda", dtype=odt)
+                kw = dict(M=M, K=Kd, rows=rows) if rows else {}
+                for _ in range(3):
+                    K.gemm_bf16(a, w, out, variant=v, **kw)
+                torch.cuda.synchronize()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                reps = 20
+                e0.record()
+                for _ in range(reps):
+                    K.gemm_bf16(a, w, out, variant=v, **kw)
+                e1.record()
+                torch.cuda.synchronize()
+                ms = e0.elapsed_time(e1) / reps
+                outs[v] = out.float()
+                d = float((outs[v] - outs[0]).abs().max()) if v else 0.0
+                print(f"{name:14s} M={M:6d} N={N:5d} K={Kd:5d} v{v}: {ms*1e3:8.1f} us {2*M*N*Kd/ms/1e9:7.1f} TF/s  maxdiff_vs_v0={d:.3g}",
+                      flush=True)
+
+
+if __name__ == "__main__":
+    main()
