@@ -20,6 +20,10 @@
 #ifndef MER_H_
 #define MER_H_
 
+/* BatchNorm batch statistics are accumulated by the conv epilogue into MER_BN_STAT_PARTS striped partial
+ * rows: a `stats` buffer is float[MER_BN_STAT_PARTS][C][2] (sum, sum of squares), zeroed by the caller. */
+#define MER_BN_STAT_PARTS 256
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -173,13 +177,22 @@ int mer_cast_bf16(long n, const float* x, void* y, void* stream);
  * with channels padded to a multiple of 8. */
 
 /* y[n,oh,ow,k] = sum_{r,s,c} x[n,oh*st-pad+r,ow*st-pad+s,c] w[k][r][s][c]  (bf16 out); if stats != NULL,
- * stats[k] += (sum, sum of squares) of the stored outputs (BatchNorm batch statistics, pre-zeroed). */
+ * stats[p][k] += (sum, sum of squares) of the stored outputs (BatchNorm batch statistics, striped over
+ * p < MER_BN_STAT_PARTS partial rows, pre-zeroed). */
 int mer_conv_fwd(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, const void* x,
                  const void* w_packed, void* y, float* stats, void* stream);
+
+/* mer_conv_fwd / mer_conv_dgrad with an explicit kernel: -1 auto, 0 the register-staged implicit GEMM,
+ * 1 the global_load_lds pipelined one (zero padding served from a zero chunk). */
+int mer_conv_fwd_ex(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, const void* x,
+                    const void* w_packed, void* y, float* stats, int variant, void* stream);
 
 /* dx[n,h,w,c] = sum_{r,s,k} dy[n,(h+pad-r)/st,(w+pad-s)/st,k] wt[c][r][s][k] (+ residual where mask > 0). */
 int mer_conv_dgrad(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, const void* dy,
                    const void* wt_packed, void* dx, const void* residual, const void* residual_mask, void* stream);
+int mer_conv_dgrad_ex(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, const void* dy,
+                      const void* wt_packed, void* dx, const void* residual, const void* residual_mask, int variant,
+                      void* stream);
 
 /* dw[k][c][r][s] += sum_p dy[p][k] x(p; r,s,c) for c < Creal, fp32 PyTorch layout (dw initialised).  The
  * pixel reduction is split `splits` ways; each split writes an fp32 slab [K][R*S*C] into `workspace`
@@ -194,7 +207,7 @@ int mer_pack_input_nhwc(int N, int C, int H, int W, int Cp, const float* x, void
  * (transpose=1, data-gradient operand); channels >= C are zero. */
 int mer_pack_conv_weight(int K, int C, int R, int S, int Cp, int transpose, const float* w, void* out, void* stream);
 
-/* BatchNorm2d finalize: ms[c] = (mean, rstd) from stats over M values and, when non-NULL, updates
+/* BatchNorm2d finalize: ms[c] = (mean, rstd) from the striped partial rows of stats over M values and, when non-NULL, updates
  * running_mean / running_var (unbiased) with `momentum` and increments num_batches_tracked (train mode).
  * stats == NULL is eval mode: ms = (running_mean, 1/sqrt(running_var + eps)), nothing updated. */
 int mer_bn_finalize(int C, long M, const float* stats, float eps, float momentum, float* ms, float* rmean,

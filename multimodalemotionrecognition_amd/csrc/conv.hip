@@ -176,8 +176,9 @@ __global__ __launch_bounds__(256, 2) void conv_kernel(ConvGeom g) {
       csq += __shfl_xor(csq, 16, 64);
       csq += __shfl_xor(csq, 32, 64);
       if ((lane >> 4) == 0 && col < g.Ncols) {
-        atomicAdd(g.stats + 2 * col, csum);
-        atomicAdd(g.stats + 2 * col + 1, csq);
+        float* slab = g.stats + (long)(ty % MER_BN_STAT_PARTS) * g.Ncols * 2;
+        atomicAdd(slab + 2 * col, csum);
+        atomicAdd(slab + 2 * col + 1, csq);
       }
     }
   }
@@ -339,6 +340,219 @@ __global__ void wgrad_reduce_kernel(int K, int C, int Creal, int R, int S, int s
   }
 }
 
+
+// ---------------------------------------------------------------------------------------
+// Pipelined fwd / dgrad implicit GEMM: the im2col A tile and the weight tile are DMA'd straight into
+// LDS with global_load_lds (16 B per lane), the next K-tile issued before the current one is consumed
+// (cdna_hip_programming.md §5 "Minimum 2-phase").  Same XOR-swizzled [rows][64] LDS image as
+// gemm_bf16.hip's pipelined kernel.  Zero padding (spatial borders, dgrad's stride holes, K tail,
+// rows past M / N) is served by pointing the lane at a 16-byte zero chunk in global memory.
+// ---------------------------------------------------------------------------------------
+__device__ __attribute__((aligned(16))) uint32_t mer_conv_zero16[4] = {0u, 0u, 0u, 0u};
+
+__device__ __forceinline__ int cswz(int row, int c) { return c ^ ((row >> 1) & 7); }
+
+template <bool DGRAD>
+__device__ __forceinline__ const bf16_t* conv_a_src(const ConvGeom& g, int n, int oh, int ow, bool rowok, int kk,
+                                                    float inv_IC, float inv_S) {
+  const bf16_t* zero = reinterpret_cast<const bf16_t*>(mer_conv_zero16);
+  if (!rowok || kk >= g.Kred) return zero;
+  const int tap = fdiv(kk, inv_IC), c = kk - tap * g.IC;
+  const int r = fdiv(tap, inv_S), s = tap - r * g.S;
+  int ih, iw;
+  if (!DGRAD) {
+    ih = oh * g.st - g.pad + r;
+    iw = ow * g.st - g.pad + s;
+  } else {
+    const int th = oh + g.pad - r, tw = ow + g.pad - s;
+    if (th < 0 || tw < 0) return zero;
+    if (g.st == 1) {
+      ih = th;
+      iw = tw;
+    } else {
+      if ((th | tw) & 1) return zero;  // st == 2 (checked on the host)
+      ih = th >> 1;
+      iw = tw >> 1;
+    }
+  }
+  if (ih < 0 || ih >= g.IH || iw < 0 || iw >= g.IW) return zero;
+  return g.X + (((long)n * g.IH + ih) * g.IW + iw) * g.IC + c;
+}
+
+template <bool DGRAD, int BM_, int BN_>
+__global__ __launch_bounds__(256, 2) void conv_pipe_kernel(ConvGeom g) {
+  constexpr int IA = BM_ / 32, IB = BN_ / 32;           // glds per wave per K-tile (8 rows each, 4 waves)
+  constexpr int TM = BM_ / 2, TN = BN_ / 2, FM = TM / 16, FN = TN / 16;
+  constexpr int BUF = (BM_ + BN_) * 64;
+  extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int M = g.N * g.OH * g.OW;
+  const int nx = (g.Ncols + BN_ - 1) / BN_, ny = (M + BM_ - 1) / BM_;
+  int tx, ty;
+  xcd_tile(blockIdx.x, nx, nx * ny, tx, ty);
+  const int m0 = ty * BM_, n0 = tx * BN_;
+  const int wr = w >> 1, wc = w & 1;
+
+  int an[IA], aoh[IA], aow[IA], acl[IA];
+  bool aok[IA];
+#pragma unroll
+  for (int j = 0; j < IA; ++j) {
+    const int r = (w * IA + j) * 8 + (lane >> 3);
+    const int m = m0 + r;
+    aok[j] = m < M;
+    const int mm = aok[j] ? m : 0;
+    an[j] = mm / (g.OH * g.OW);
+    const int rem = mm - an[j] * g.OH * g.OW;
+    aoh[j] = rem / g.OW;
+    aow[j] = rem - aoh[j] * g.OW;
+    acl[j] = cswz(r, lane & 7) * 8;
+  }
+  const bf16_t* pb[IB];
+  int bcl[IB];
+  bool bok[IB];
+#pragma unroll
+  for (int j = 0; j < IB; ++j) {
+    const int r = (w * IB + j) * 8 + (lane >> 3);
+    const int n = n0 + r;
+    bok[j] = n < g.Ncols;
+    pb[j] = g.Wt + (long)(bok[j] ? n : 0) * g.Kred;
+    bcl[j] = cswz(r, lane & 7) * 8;
+  }
+  const float inv_IC = 1.f / g.IC, inv_S = 1.f / g.S;
+  const bf16_t* zero = reinterpret_cast<const bf16_t*>(mer_conv_zero16);
+  auto stage = [&](int buf, int k0) {
+    bf16_t* la = smem + buf * BUF;
+    bf16_t* lb = la + BM_ * 64;
+#pragma unroll
+    for (int j = 0; j < IA; ++j)
+      glds16(conv_a_src<DGRAD>(g, an[j], aoh[j], aow[j], aok[j], k0 + acl[j], inv_IC, inv_S), la + (w * IA + j) * 512);
+#pragma unroll
+    for (int j = 0; j < IB; ++j) {
+      const int kk = k0 + bcl[j];
+      glds16((bok[j] && kk < g.Kred) ? pb[j] + kk : zero, lb + (w * IB + j) * 512);
+    }
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int fr = lane & 15, fq = lane >> 4;
+  const int nk = (g.Kred + CBK - 1) / CBK;
+  float part[FN][2];
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) stage(cur ^ 1, (kt + 1) * CBK);
+    const bf16_t* la = smem + cur * BUF;
+    const bf16_t* lb = la + BM_ * 64;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8 af[FM], bfr[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int r = wr * TM + i * 16 + fr;
+        af[i] = *reinterpret_cast<const bf16x8*>(la + r * 64 + cswz(r, s * 4 + fq) * 8);
+      }
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int r = wc * TN + j * 16 + fr;
+        bfr[j] = *reinterpret_cast<const bf16x8*>(lb + r * 64 + cswz(r, s * 4 + fq) * 8);
+      }
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int col = n0 + wc * TN + j * 16 + fr;
+    float csum = 0.f, csq = 0.f;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wr * TM + i * 16 + fq * 4 + r;
+        if (row < M && col < g.Ncols) {
+          float v = acc[i][j][r];
+          if (g.R_) {
+            const long ri = (long)row * g.ldy + col;
+            if (!g.Rmask || bf2f(g.Rmask[ri]) > 0.f) v += bf2f(g.R_[ri]);
+          }
+          const bf16_t h = f2bf(v);
+          g.Y[(long)row * g.ldy + col] = h;
+          const float hv = bf2f(h);
+          csum += hv;
+          csq += hv * hv;
+        }
+      }
+    if (g.stats) {
+      csum += __shfl_xor(csum, 16, 64);
+      csum += __shfl_xor(csum, 32, 64);
+      csq += __shfl_xor(csq, 16, 64);
+      csq += __shfl_xor(csq, 32, 64);
+      part[j][0] = csum;
+      part[j][1] = csq;
+    }
+  }
+  if (g.stats) {
+    // the two M-waves of a column pair meet in LDS (the staging buffers are idle now); one striped
+    // atomic per (block, column): slab row ty % MER_BN_STAT_PARTS keeps same-address atomics rare
+    float* red = reinterpret_cast<float*>(smem);
+    __syncthreads();
+    if (wr == 1 && fq == 0)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        red[(wc * FN + j) * 32 + fr * 2] = part[j][0];
+        red[(wc * FN + j) * 32 + fr * 2 + 1] = part[j][1];
+      }
+    __syncthreads();
+    if (wr == 0 && fq == 0) {
+      float* slab = g.stats + (long)(ty % MER_BN_STAT_PARTS) * g.Ncols * 2;
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int col = n0 + wc * TN + j * 16 + fr;
+        if (col < g.Ncols) {
+          atomicAdd(slab + 2 * col, part[j][0] + red[(wc * FN + j) * 32 + fr * 2]);
+          atomicAdd(slab + 2 * col + 1, part[j][1] + red[(wc * FN + j) * 32 + fr * 2 + 1]);
+        }
+      }
+    }
+  }
+}
+
+template <bool DGRAD, int BM_, int BN_>
+int launch_conv_pipe_t(ConvGeom& g, hipStream_t st) {
+  const int M = g.N * g.OH * g.OW;
+  const long tiles = (long)((M + BM_ - 1) / BM_) * ((g.Ncols + BN_ - 1) / BN_);
+  const size_t lds = 2 * (BM_ + BN_) * 64 * sizeof(bf16_t);
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_pipe_kernel<DGRAD, BM_, BN_>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+    return (int)hipErrorInvalidConfiguration;
+  hipLaunchKernelGGL((conv_pipe_kernel<DGRAD, BM_, BN_>), dim3((unsigned)tiles), dim3(256), lds, st, g);
+  return (int)hipGetLastError();
+}
+
+template <bool DGRAD>
+int launch_conv_pipe(ConvGeom& g, hipStream_t st) {
+  const int M = g.N * g.OH * g.OW;
+  const int bn = g.Ncols <= 64 ? 64 : 128;
+  const long tiles128 = (long)((M + 127) / 128) * ((g.Ncols + bn - 1) / bn);
+  const bool small_m = tiles128 < 384;
+  if (bn == 64) return small_m ? launch_conv_pipe_t<DGRAD, 64, 64>(g, st) : launch_conv_pipe_t<DGRAD, 128, 64>(g, st);
+  return small_m ? launch_conv_pipe_t<DGRAD, 64, 128>(g, st) : launch_conv_pipe_t<DGRAD, 128, 128>(g, st);
+}
+
 template <bool DGRAD>
 int launch_conv(ConvGeom& g, hipStream_t st) {
   const int M = g.N * g.OH * g.OW;
@@ -366,20 +580,32 @@ int launch_conv(ConvGeom& g, hipStream_t st) {
 
 MER_API int mer_conv_fwd(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, const void* x,
                          const void* w_packed, void* y, float* stats, void* stream) {
-  if (C % 8) return (int)hipErrorInvalidValue;
+  return mer_conv_fwd_ex(N, H, W, C, K, R, S, stride, pad, x, w_packed, y, stats, -1, stream);
+}
+
+MER_API int mer_conv_fwd_ex(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, const void* x,
+                            const void* w_packed, void* y, float* stats, int variant, void* stream) {
+  if (C % 8 || variant < -1 || variant > 1) return (int)hipErrorInvalidValue;
   ConvGeom g{};
   g.N = N; g.IH = H; g.IW = W; g.IC = C;
   g.OH = (H + 2 * pad - R) / stride + 1; g.OW = (W + 2 * pad - S) / stride + 1;
   g.R = R; g.S = S; g.st = stride; g.pad = pad;
   g.Ncols = K; g.Kred = R * S * C;
   g.X = (const bf16_t*)x; g.Wt = (const bf16_t*)w_packed; g.Y = (bf16_t*)y; g.ldy = K; g.stats = stats;
-  return launch_conv<false>(g, (hipStream_t)stream);
+  if (variant == 0) return launch_conv<false>(g, (hipStream_t)stream);
+  return launch_conv_pipe<false>(g, (hipStream_t)stream);
 }
 
 MER_API int mer_conv_dgrad(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, const void* dy,
                            const void* wt_packed, void* dx, const void* residual, const void* residual_mask,
                            void* stream) {
-  if (K % 8 || C % 8) return (int)hipErrorInvalidValue;
+  return mer_conv_dgrad_ex(N, H, W, C, K, R, S, stride, pad, dy, wt_packed, dx, residual, residual_mask, -1, stream);
+}
+
+MER_API int mer_conv_dgrad_ex(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, const void* dy,
+                              const void* wt_packed, void* dx, const void* residual, const void* residual_mask,
+                              int variant, void* stream) {
+  if (K % 8 || C % 8 || variant < -1 || variant > 1) return (int)hipErrorInvalidValue;
   ConvGeom g{};
   g.N = N; g.OH = H; g.OW = W;
   g.IH = (H + 2 * pad - R) / stride + 1; g.IW = (W + 2 * pad - S) / stride + 1; g.IC = K;
@@ -387,7 +613,8 @@ MER_API int mer_conv_dgrad(int N, int H, int W, int C, int K, int R, int S, int 
   g.Ncols = C; g.Kred = R * S * K;
   g.X = (const bf16_t*)dy; g.Wt = (const bf16_t*)wt_packed; g.Y = (bf16_t*)dx; g.ldy = C; g.stats = nullptr;
   g.R_ = (const bf16_t*)residual; g.Rmask = (const bf16_t*)residual_mask;
-  return launch_conv<true>(g, (hipStream_t)stream);
+  if (variant == 0 || stride > 2) return launch_conv<true>(g, (hipStream_t)stream);
+  return launch_conv_pipe<true>(g, (hipStream_t)stream);
 }
 
 MER_API int mer_conv_wgrad(int N, int H, int W, int C, int Creal, int K, int R, int S, int stride, int pad,
@@ -479,8 +706,13 @@ __global__ void bn_finalize_kernel(int C, long M, const float* __restrict__ stat
     ms[2 * c + 1] = rsqrtf(rvar[c] + eps);
     return;
   }
-  const float mean = stats[2 * c] / M;
-  const float var = fmaxf(stats[2 * c + 1] / M - mean * mean, 0.f);
+  float sum = 0.f, sq = 0.f;
+  for (int p = 0; p < MER_BN_STAT_PARTS; ++p) {
+    sum += stats[(long)p * 2 * C + 2 * c];
+    sq += stats[(long)p * 2 * C + 2 * c + 1];
+  }
+  const float mean = sum / M;
+  const float var = fmaxf(sq / M - mean * mean, 0.f);
   ms[2 * c] = mean;
   ms[2 * c + 1] = rsqrtf(var + eps);
   if (rmean) rmean[c] = (1.f - momentum) * rmean[c] + momentum * mean;

@@ -289,13 +289,12 @@ int launch_pipe(const GemmArgs& g, int out_dtype, hipStream_t st) {
   return out_dtype == MER_BF16 ? launch_pipe_t<CF, bf16_t>(g, st) : launch_pipe_t<CF, float>(g, st);
 }
 
-// Tile choice: the largest tile whose grid still gives every CU work (256 CUs), else smaller tiles.
+// Tile choice (measured on the WavLM shapes at B=32, tools/bench_gemm.py): the 256x256 tile only pays
+// when there are several waves of tiles (conv1: 1200 tiles); otherwise the 128x128 glds tile (2 blocks
+// per CU) wins or ties on every encoder GEMM.
 int pick_variant(int M, int N) {
   const long tl = (long)((M + 255) / 256) * ((N + 255) / 256);
-  const long tm = (long)((M + 255) / 256) * ((N + 127) / 128);
-  if (tl >= 240) return 1;
-  if (tm >= 240) return 2;
-  return 3;
+  return tl >= 1024 ? 1 : 3;
 }
 
 template <int AMODE>

@@ -303,24 +303,34 @@ def cast_bf16(x, y):
     LIB("mer_cast_bf16", x.numel(), x.data_ptr(), y.data_ptr(), stream_ptr())
 
 
-def conv_fwd(x, wp, y, stats, R, S, stride, pad):
+BN_STAT_PARTS = 256  # MER_BN_STAT_PARTS (include/mer.h)
+
+
+def bn_stats_buffer(C, device):
+    """Zeroed float[BN_STAT_PARTS][C][2] for conv_fwd's fused BatchNorm statistics."""
+    return torch.zeros(BN_STAT_PARTS, C, 2, device=device, dtype=torch.float32)
+
+
+def conv_fwd(x, wp, y, stats, R, S, stride, pad, variant=-1):
     N, H, W, C = x.shape
     Kc = y.shape[-1]
     Ho, Wo = (H + 2 * pad - R) // stride + 1, (W + 2 * pad - S) // stride + 1
     if tuple(y.shape) != (N, Ho, Wo, Kc) or tuple(wp.shape) != (Kc, R * S * C):
         raise ValueError(f"conv_fwd shapes x{tuple(x.shape)} w{tuple(wp.shape)} y{tuple(y.shape)}")
-    _launch("conv_fwd", (N, H, W, C, Kc, R, stride), "mer_conv_fwd", N, H, W, C, Kc, R, S, stride, pad, x.data_ptr(),
-            wp.data_ptr(), y.data_ptr(), _ptr(stats), stream_ptr())
+    if stats is not None and (stats.numel() != BN_STAT_PARTS * Kc * 2 or not stats.is_contiguous()):
+        raise ValueError("conv_fwd stats must be a contiguous float[BN_STAT_PARTS][K][2] buffer")
+    _launch("conv_fwd", (N, H, W, C, Kc, R, stride), "mer_conv_fwd_ex", N, H, W, C, Kc, R, S, stride, pad, x.data_ptr(),
+            wp.data_ptr(), y.data_ptr(), _ptr(stats), int(variant), stream_ptr())
 
 
-def conv_dgrad(dy, wt, dx, R, S, stride, pad, residual=None, mask=None):
+def conv_dgrad(dy, wt, dx, R, S, stride, pad, residual=None, mask=None, variant=-1):
     N, H, W, C = dx.shape
     Kc = dy.shape[-1]
     Ho, Wo = (H + 2 * pad - R) // stride + 1, (W + 2 * pad - S) // stride + 1
     if tuple(dy.shape) != (N, Ho, Wo, Kc) or tuple(wt.shape) != (C, R * S * Kc):
         raise ValueError(f"conv_dgrad shapes dy{tuple(dy.shape)} wt{tuple(wt.shape)} dx{tuple(dx.shape)}")
-    _launch("conv_dgrad", (N, H, W, C, Kc, R, stride), "mer_conv_dgrad", N, H, W, C, Kc, R, S, stride, pad,
-            dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), _ptr(residual), _ptr(mask), stream_ptr())
+    _launch("conv_dgrad", (N, H, W, C, Kc, R, stride), "mer_conv_dgrad_ex", N, H, W, C, Kc, R, S, stride, pad,
+            dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), _ptr(residual), _ptr(mask), int(variant), stream_ptr())
 
 
 def conv_wgrad(x, dy, dw, R, S, stride, pad, creal=None):

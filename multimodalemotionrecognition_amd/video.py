@@ -123,28 +123,46 @@ def _bn_forward(bn: nn.BatchNorm2d, c: torch.Tensor, stats, training: bool):
     return ms
 
 
-def _conv_bn(trunk, conv, bn, x, stride, pad, training):
+class _StatsArena:
+    """One zeroed buffer for every conv's striped BatchNorm partial sums of a trunk forward
+    (float[MER_BN_STAT_PARTS][C][2] per conv): one memset per forward instead of one per conv."""
+
+    def __init__(self, trunk, device):
+        total = sum(m.out_channels for m in trunk.modules() if isinstance(m, nn.Conv2d))
+        self.buf = torch.zeros(K.BN_STAT_PARTS * 2 * total, device=device, dtype=torch.float32)
+        self.off = 0
+
+    def take(self, C):
+        n = K.BN_STAT_PARTS * 2 * C
+        t = self.buf[self.off:self.off + n].view(K.BN_STAT_PARTS, C, 2)
+        self.off += n
+        return t
+
+
+def _conv_bn(trunk, conv, bn, x, stride, pad, training, arena=None):
     """conv (+ fused batch stats) -> (conv output, (mean, rstd))."""
     Kc, _, R, S = conv.weight.shape
     N, H, W, C = x.shape
     Ho, Wo = (H + 2 * pad - R) // stride + 1, (W + 2 * pad - S) // stride + 1
     y = torch.empty(N, Ho, Wo, Kc, device=x.device, dtype=torch.bfloat16)
-    stats = torch.zeros(Kc, 2, device=x.device, dtype=torch.float32) if training else None
+    stats = None
+    if training:
+        stats = arena.take(Kc) if arena is not None else K.bn_stats_buffer(Kc, x.device)
     K.conv_fwd(x, trunk.packed(conv, C, False), y, stats, R, S, stride, pad)
     return y, _bn_forward(bn, y, stats, training)
 
 
 @torch.no_grad()
-def block_forward(trunk, blk: BasicBlock, x: torch.Tensor, training: bool):
+def block_forward(trunk, blk: BasicBlock, x: torch.Tensor, training: bool, arena=None):
     """BasicBlock (torchvision): relu(bn2(conv2(relu(bn1(conv1(x))))) + [bn_d(conv_d(x)) | x])."""
     s = blk.stride
-    bc1, bms1 = _conv_bn(trunk, blk.conv1, blk.bn1, x, s, 1, training)
+    bc1, bms1 = _conv_bn(trunk, blk.conv1, blk.bn1, x, s, 1, training, arena)
     ba1 = torch.empty_like(bc1)
     K.bn_apply(bc1, bms1, blk.bn1.weight, blk.bn1.bias, ba1, relu=True)
-    bc2, bms2 = _conv_bn(trunk, blk.conv2, blk.bn2, ba1, 1, 1, training)
+    bc2, bms2 = _conv_bn(trunk, blk.conv2, blk.bn2, ba1, 1, 1, training, arena)
     out = torch.empty_like(bc2)
     if blk.downsample is not None:
-        cd, msd = _conv_bn(trunk, blk.downsample[0], blk.downsample[1], x, s, 0, training)
+        cd, msd = _conv_bn(trunk, blk.downsample[0], blk.downsample[1], x, s, 0, training, arena)
         dbn = blk.downsample[1]
         K.bn_apply(bc2, bms2, blk.bn2.weight, blk.bn2.bias, out, relu=True, res=cd, ms2=msd, gamma2=dbn.weight,
                    beta2=dbn.bias)
@@ -162,7 +180,8 @@ def trunk_forward(trunk: ResNet18Trunk, video: torch.Tensor, training: bool):
     x0 = torch.empty(N, H, W, CP_IN, device=dev, dtype=bf)
     K.pack_input_nhwc(video, x0)
     conv1, bn1 = trunk[0], trunk[1]
-    c1, ms1 = _conv_bn(trunk, conv1, bn1, x0, 2, 3, training)
+    arena = _StatsArena(trunk, dev) if training else None
+    c1, ms1 = _conv_bn(trunk, conv1, bn1, x0, 2, 3, training, arena)
     a1 = torch.empty_like(c1)
     K.bn_apply(c1, ms1, bn1.weight, bn1.bias, a1, relu=True)
     Hp, Wp = (a1.shape[1] - 1) // 2 + 1, (a1.shape[2] - 1) // 2 + 1
@@ -172,7 +191,7 @@ def trunk_forward(trunk: ResNet18Trunk, video: torch.Tensor, training: bool):
     saved = {"stem": (x0, c1, ms1, a1, arg), "blocks": []}
     x = p1
     for blk in _blocks(trunk):
-        x, sv = block_forward(trunk, blk, x, training)
+        x, sv = block_forward(trunk, blk, x, training, arena)
         saved["blocks"].append(sv)
     feats = torch.empty(N, x.shape[-1], device=dev, dtype=torch.float32)
     K.avgpool_fwd(x, feats)

@@ -47,8 +47,9 @@ def test_conv_fwd_dgrad_wgrad_vs_torch(N, H, C, Kc, R, stride, pad):
     wp = torch.empty(Kc, R * R * C, device="cuda", dtype=torch.bfloat16)
     K.pack_conv_weight(w.detach().cuda(), wp, C, False)
     yd = torch.empty(N, Ho, Ho, Kc, device="cuda", dtype=torch.bfloat16)
-    stats = torch.zeros(Kc, 2, device="cuda")
+    stats = K.bn_stats_buffer(Kc, "cuda")
     K.conv_fwd(xd, wp, yd, stats, R, R, stride, pad)
+    stats = stats.sum(0)  # striped partial rows
     yr = to_nhwc(y.detach())
     assert rel_rms(yd, yr) < 1e-2
     ys = yd.float().cpu()
@@ -205,3 +206,40 @@ def test_maxpool_avgpool_kernels():
     feats = torch.empty(2, 8, device="cuda")
     K.avgpool_fwd(xd, feats)
     assert torch.allclose(feats.cpu(), x.detach().mean((2, 3)), atol=1e-3)
+
+
+@pytest.mark.parametrize("N,H,C,Kc,R,stride,pad", [
+    (2, 28, 64, 64, 3, 1, 1), (2, 28, 64, 128, 3, 2, 1), (2, 28, 64, 128, 1, 2, 0),
+    (2, 7, 256, 512, 3, 2, 1), (3, 17, 16, 24, 3, 1, 1), (2, 30, 8, 64, 7, 2, 3), (5, 14, 256, 256, 3, 1, 1)])
+def test_conv_variants_bit_identical(N, H, C, Kc, R, stride, pad):
+    """The glds-pipelined conv (variant 1) against the register-staged one (variant 0): same fragment
+    order and K order, so fwd (incl. fused BN stats up to atomic order) and dgrad (incl. the masked residual)
+    agree bit for bit."""
+    from multimodalemotionrecognition_amd import kernels as K
+
+    torch.manual_seed(1)
+    Ho = (H + 2 * pad - R) // stride + 1
+    x = torch.randn(N, H, H, C, device="cuda").bfloat16()
+    w = (torch.randn(Kc, C, R, R, device="cuda") / (C * R * R) ** 0.5)
+    wp = torch.empty(Kc, R * R * C, device="cuda", dtype=torch.bfloat16)
+    K.pack_conv_weight(w, wp, C, False)
+    wt = torch.empty(C, R * R * Kc, device="cuda", dtype=torch.bfloat16)
+    K.pack_conv_weight(w, wt, C, True)
+    ys, sts = [], []
+    for v in (0, 1):
+        y = torch.empty(N, Ho, Ho, Kc, device="cuda", dtype=torch.bfloat16)
+        st = K.bn_stats_buffer(Kc, "cuda")
+        K.conv_fwd(x, wp, y, st, R, R, stride, pad, variant=v)
+        ys.append(y)
+        sts.append(st.sum(0))
+    assert torch.equal(ys[0], ys[1])
+    assert torch.allclose(sts[0], sts[1], rtol=1e-5, atol=1e-3)
+    dy = torch.randn(N, Ho, Ho, Kc, device="cuda").bfloat16()
+    res = torch.randn(N, H, H, C, device="cuda").bfloat16()
+    mask = torch.randn(N, H, H, C, device="cuda").bfloat16()
+    dxs = []
+    for v in (0, 1):
+        dx = torch.empty(N, H, H, C, device="cuda", dtype=torch.bfloat16)
+        K.conv_dgrad(dy, wt, dx, R, R, stride, pad, residual=res, mask=mask, variant=v)
+        dxs.append(dx)
+    assert torch.equal(dxs[0], dxs[1])

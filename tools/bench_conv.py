@@ -1,0 +1,55 @@
+"""Time conv fwd / dgrad kernel variants on the ResNet18 layers of the north-star step (256 frames of 112x112)."""
+import sys
+from pathlib import Path
+
+import torch
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+from multimodalemotionrecognition_amd import kernels as K  # noqa: E402
+
+NF = 256
+# (name, H_in, C, K, R, stride, pad)
+LAYERS = [("conv1 7x7", 112, 8, 64, 7, 2, 3), ("layer1 3x3", 56, 64, 64, 3, 1, 1), ("layer2.0 3x3 s2", 56, 64, 128, 3, 2, 1),
+          ("layer2 3x3", 28, 128, 128, 3, 1, 1), ("layer3.0 3x3 s2", 28, 128, 256, 3, 2, 1),
+          ("layer3 3x3", 14, 256, 256, 3, 1, 1), ("layer4.0 3x3 s2", 14, 256, 512, 3, 2, 1),
+          ("layer4 3x3", 7, 512, 512, 3, 1, 1), ("ds2 1x1 s2", 56, 64, 128, 1, 2, 0)]
+
+
+def timeit(fn, reps=20):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / reps
+
+
+def main():
+    torch.manual_seed(0)
+    for name, H, C, Kc, R, st, pad in LAYERS:
+        Ho = (H + 2 * pad - R) // st + 1
+        x = (torch.rand(NF, H, H, C, device="cuda") * 2 - 1).bfloat16()
+        w = torch.randn(Kc, C, R, R, device="cuda") * 0.05
+        wp = torch.empty(Kc, R * R * C, device="cuda", dtype=torch.bfloat16)
+        K.pack_conv_weight(w, wp, C, False)
+        wt = torch.empty(C, R * R * Kc, device="cuda", dtype=torch.bfloat16)
+        K.pack_conv_weight(w, wt, C, True)
+        y = torch.empty(NF, Ho, Ho, Kc, device="cuda", dtype=torch.bfloat16)
+        stats = K.bn_stats_buffer(Kc, "cuda")
+        dy = (torch.rand(NF, Ho, Ho, Kc, device="cuda") * 2 - 1).bfloat16()
+        dx = torch.empty(NF, H, H, C, device="cuda", dtype=torch.bfloat16)
+        flop = 2.0 * NF * Ho * Ho * Kc * R * R * C
+        line = f"{name:16s}"
+        for v in (0, 1):
+            tf = timeit(lambda: K.conv_fwd(x, wp, y, stats, R, R, st, pad, variant=v))
+            tb = timeit(lambda: K.conv_dgrad(dy, wt, dx, R, R, st, pad, variant=v))
+            line += f" | v{v} fwd {tf*1e3:7.1f}us {flop/tf/1e9:6.1f}TF dgrad {tb*1e3:7.1f}us {flop/tb/1e9:6.1f}TF"
+        print(line, flush=True)
+
+
+if __name__ == "__main__":
+    main()
