@@ -194,6 +194,19 @@ int mer_conv_dgrad_ex(int N, int H, int W, int C, int K, int R, int S, int strid
                       const void* wt_packed, void* dx, const void* residual, const void* residual_mask, int variant,
                       void* stream);
 
+/* mer_conv_dgrad_ex (pipelined kernel only) with the BatchNorm-backward reduction of the BN the gradient
+ * flows into fused into the epilogue: g = (bn_mask > 0) * dx (after the residual), bn_red[p][c] +=
+ * (sum g, sum g * (bn_x - mean) * rstd) with (mean, rstd) = bn_ms[c], and bn_red2 likewise for bn_x2 /
+ * bn_ms2 (may be NULL).  bn_red / bn_red2 are zeroed float[MER_BN_STAT_PARTS][C][2]; collapse them with
+ * mer_partials_sum before mer_bn_bwd_apply.  Replaces mer_bn_bwd_reduce after a conv backward. */
+int mer_conv_dgrad_bnr(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, const void* dy,
+                       const void* wt_packed, void* dx, const void* residual, const void* residual_mask,
+                       const void* bn_mask, const void* bn_x, const float* bn_ms, float* bn_red, const void* bn_x2,
+                       const float* bn_ms2, float* bn_red2, int variant, void* stream);
+
+/* out[c][0:2] = sum_p in[p][c][0:2] over `parts` striped partial rows. */
+int mer_partials_sum(int C, int parts, const float* in, float* out, void* stream);
+
 /* dw[k][c][r][s] += sum_p dy[p][k] x(p; r,s,c) for c < Creal, fp32 PyTorch layout (dw initialised).  The
  * pixel reduction is split `splits` ways; each split writes an fp32 slab [K][R*S*C] into `workspace`
  * (splits*K*R*S*C floats), then a reduce pass sums the slabs into dw (deterministic, no atomics). */

@@ -34,6 +34,17 @@ struct ConvGeom {
   float* stats;           // fwd: per column (sum, sumsq), may be null
   const bf16_t* R_;       // residual added in the epilogue (dgrad), may be null
   const bf16_t* Rmask;    // residual is added only where Rmask > 0 (relu mask), may be null
+  // dgrad only: the BatchNorm-backward reduction of the BN whose relu'd output this gradient flows
+  // into, fused into the epilogue (bn_bwd_reduce semantics; NULL bnr_red = off).  g = (mask > 0) * y,
+  // red[p][c] += (sum g, sum g * (x - mean) * rstd); red2 likewise for a second BN reading the same g
+  // (the downsample branch).  Striped over MER_BN_STAT_PARTS rows like the forward statistics.
+  const bf16_t* bnr_mask;
+  const bf16_t* bnr_x;
+  const float* bnr_ms;
+  float* bnr_red;
+  const bf16_t* bnr_x2;
+  const float* bnr_ms2;
+  float* bnr_red2;
 };
 
 template <bool DGRAD>
@@ -379,15 +390,53 @@ __device__ __forceinline__ const bf16_t* conv_a_src(const ConvGeom& g, int n, in
   return g.X + (((long)n * g.IH + ih) * g.IW + iw) * g.IC + c;
 }
 
-template <bool DGRAD, int BM_, int BN_>
+// Stride-2 dgrad, parity-decomposed (PAR): an input pixel (h, w) only receives taps with
+// (h + pad - r) and (w + pad - s) even, so the 4 parity classes (h&1, w&1) (blockIdx.y) are 4 dense
+// implicit GEMMs over just their taps -- 1/4 of the MFMA work of the masked 9-tap form for 3x3 and none
+// of its zero staging.  Class c: rows (n, hh, ww) -> pixel (n, 2hh+ph, 2ww+pw); taps r = r0 + 2ri,
+// s = s0 + 2si with r0 = (ph + pad) & 1; source row ih = hh + (ph + pad - r0)/2 - ri.
+struct ParClass {
+  int ph, pw, Hc, Wc, r0, s0, nr, ns, dh0, dw0;
+};
+
+__device__ __forceinline__ ParClass par_class(const ConvGeom& g, int cls) {
+  ParClass c;
+  c.ph = cls >> 1;
+  c.pw = cls & 1;
+  c.Hc = (g.OH - c.ph + 1) >> 1;
+  c.Wc = (g.OW - c.pw + 1) >> 1;
+  c.r0 = (c.ph + g.pad) & 1;
+  c.s0 = (c.pw + g.pad) & 1;
+  c.nr = (g.R - c.r0 + 1) >> 1;
+  c.ns = (g.S - c.s0 + 1) >> 1;
+  c.dh0 = (c.ph + g.pad - c.r0) >> 1;
+  c.dw0 = (c.pw + g.pad - c.s0) >> 1;
+  return c;
+}
+
+template <bool DGRAD, bool PAR, int BM_, int BN_>
 __global__ __launch_bounds__(256, 2) void conv_pipe_kernel(ConvGeom g) {
   constexpr int IA = BM_ / 32, IB = BN_ / 32;           // glds per wave per K-tile (8 rows each, 4 waves)
   constexpr int TM = BM_ / 2, TN = BN_ / 2, FM = TM / 16, FN = TN / 16;
   constexpr int BUF = (BM_ + BN_) * 64;
   extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const int M = g.N * g.OH * g.OW;
+  ParClass pc{};
+  int M, Kr, rowsH, rowsW;  // this launch's GEMM rows / reduction length, row -> (n, a, b) grid
+  if (PAR) {
+    pc = par_class(g, blockIdx.y);
+    M = g.N * pc.Hc * pc.Wc;
+    Kr = pc.nr * pc.ns * g.IC;
+    rowsH = pc.Hc;
+    rowsW = pc.Wc;
+  } else {
+    M = g.N * g.OH * g.OW;
+    Kr = g.Kred;
+    rowsH = g.OH;
+    rowsW = g.OW;
+  }
   const int nx = (g.Ncols + BN_ - 1) / BN_, ny = (M + BM_ - 1) / BM_;
+  if ((int)blockIdx.x >= nx * ny) return;  // grid sized for the largest parity class
   int tx, ty;
   xcd_tile(blockIdx.x, nx, nx * ny, tx, ty);
   const int m0 = ty * BM_, n0 = tx * BN_;
@@ -401,10 +450,10 @@ __global__ __launch_bounds__(256, 2) void conv_pipe_kernel(ConvGeom g) {
     const int m = m0 + r;
     aok[j] = m < M;
     const int mm = aok[j] ? m : 0;
-    an[j] = mm / (g.OH * g.OW);
-    const int rem = mm - an[j] * g.OH * g.OW;
-    aoh[j] = rem / g.OW;
-    aow[j] = rem - aoh[j] * g.OW;
+    an[j] = mm / (rowsH * rowsW);
+    const int rem = mm - an[j] * rowsH * rowsW;
+    aoh[j] = rem / rowsW;
+    aow[j] = rem - aoh[j] * rowsW;
     acl[j] = cswz(r, lane & 7) * 8;
   }
   const bf16_t* pb[IB];
@@ -418,18 +467,36 @@ __global__ __launch_bounds__(256, 2) void conv_pipe_kernel(ConvGeom g) {
     pb[j] = g.Wt + (long)(bok[j] ? n : 0) * g.Kred;
     bcl[j] = cswz(r, lane & 7) * 8;
   }
-  const float inv_IC = 1.f / g.IC, inv_S = 1.f / g.S;
+  const float inv_IC = 1.f / g.IC, inv_S = 1.f / g.S, inv_ns = PAR ? 1.f / pc.ns : 1.f;
   const bf16_t* zero = reinterpret_cast<const bf16_t*>(mer_conv_zero16);
+  // class-local reduction index kk -> (ri, si, c) -> source; the weight operand's offset of the same kk
+  auto par_a_src = [&](int n, int hh, int ww, bool rowok, int kk) -> const bf16_t* {
+    if (!rowok || kk >= Kr) return zero;
+    const int tap = fdiv(kk, inv_IC), c = kk - tap * g.IC;
+    const int ri = fdiv(tap, inv_ns), si = tap - ri * pc.ns;
+    const int ih = hh + pc.dh0 - ri, iw = ww + pc.dw0 - si;
+    if (ih < 0 || ih >= g.IH || iw < 0 || iw >= g.IW) return zero;
+    return g.X + (((long)n * g.IH + ih) * g.IW + iw) * g.IC + c;
+  };
+  auto par_b_off = [&](int kk) -> int {
+    const int tap = fdiv(kk, inv_IC), c = kk - tap * g.IC;
+    const int ri = fdiv(tap, inv_ns), si = tap - ri * pc.ns;
+    return ((pc.r0 + 2 * ri) * g.S + pc.s0 + 2 * si) * g.IC + c;
+  };
   auto stage = [&](int buf, int k0) {
     bf16_t* la = smem + buf * BUF;
     bf16_t* lb = la + BM_ * 64;
 #pragma unroll
-    for (int j = 0; j < IA; ++j)
-      glds16(conv_a_src<DGRAD>(g, an[j], aoh[j], aow[j], aok[j], k0 + acl[j], inv_IC, inv_S), la + (w * IA + j) * 512);
+    for (int j = 0; j < IA; ++j) {
+      const bf16_t* src = PAR ? par_a_src(an[j], aoh[j], aow[j], aok[j], k0 + acl[j])
+                              : conv_a_src<DGRAD>(g, an[j], aoh[j], aow[j], aok[j], k0 + acl[j], inv_IC, inv_S);
+      glds16(src, la + (w * IA + j) * 512);
+    }
 #pragma unroll
     for (int j = 0; j < IB; ++j) {
       const int kk = k0 + bcl[j];
-      glds16((bok[j] && kk < g.Kred) ? pb[j] + kk : zero, lb + (w * IB + j) * 512);
+      const bool ok = bok[j] && kk < Kr;
+      glds16(ok ? pb[j] + (PAR ? par_b_off(kk) : kk) : zero, lb + (w * IB + j) * 512);
     }
   };
 
@@ -440,11 +507,13 @@ __global__ __launch_bounds__(256, 2) void conv_pipe_kernel(ConvGeom g) {
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int fr = lane & 15, fq = lane >> 4;
-  const int nk = (g.Kred + CBK - 1) / CBK;
+  const int nk = (Kr + CBK - 1) / CBK;
   float part[FN][2];
-  stage(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+  if (nk > 0) {
+    stage(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
     if (kt + 1 < nk) stage(cur ^ 1, (kt + 1) * CBK);
@@ -474,29 +543,110 @@ __global__ __launch_bounds__(256, 2) void conv_pipe_kernel(ConvGeom g) {
     __syncthreads();
   }
 
+  // output row -> element offset of the pixel in Y
+  auto out_row = [&](int row) -> long {
+    if (!PAR) return (long)row;
+    const int n = row / (pc.Hc * pc.Wc);
+    const int rem = row - n * pc.Hc * pc.Wc;
+    const int hh = rem / pc.Wc, ww = rem - hh * pc.Wc;
+    return ((long)n * g.OH + 2 * hh + pc.ph) * g.OW + 2 * ww + pc.pw;
+  };
 #pragma unroll
-  for (int j = 0; j < FN; ++j) {
-    const int col = n0 + wc * TN + j * 16 + fr;
-    float csum = 0.f, csq = 0.f;
+  for (int i = 0; i < FM; ++i)
 #pragma unroll
-    for (int i = 0; i < FM; ++i)
+    for (int r = 0; r < 4; ++r) {
+      const int row = m0 + wr * TM + i * 16 + fq * 4 + r;
+      if (row >= M) continue;
+      const long orow = out_row(row) * g.ldy;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = m0 + wr * TM + i * 16 + fq * 4 + r;
-        if (row < M && col < g.Ncols) {
-          float v = acc[i][j][r];
-          if (g.R_) {
-            const long ri = (long)row * g.ldy + col;
-            if (!g.Rmask || bf2f(g.Rmask[ri]) > 0.f) v += bf2f(g.R_[ri]);
+      for (int j = 0; j < FN; ++j) {
+        const int col = n0 + wc * TN + j * 16 + fr;
+        if (col >= g.Ncols) continue;
+        float v = acc[i][j][r];
+        if (g.R_) {
+          const long ri = orow + col;
+          if (!g.Rmask || bf2f(g.Rmask[ri]) > 0.f) v += bf2f(g.R_[ri]);
+        }
+        const bf16_t h = f2bf(v);
+        g.Y[orow + col] = h;
+        acc[i][j][r] = bf2f(h);  // the stored value feeds the BN statistics
+      }
+    }
+  if (DGRAD && g.bnr_red) {
+    // fused bn_bwd_reduce over this tile's stored gradient: 3 sums per column (g, g*xhat, g*xhat2)
+    float ps[FN][3];
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int col = n0 + wc * TN + j * 16 + fr;
+      const bool cok = col < g.Ncols;
+      const float mu = cok ? g.bnr_ms[2 * col] : 0.f, rs = cok ? g.bnr_ms[2 * col + 1] : 0.f;
+      const float mu2 = (cok && g.bnr_x2) ? g.bnr_ms2[2 * col] : 0.f;
+      const float rs2 = (cok && g.bnr_x2) ? g.bnr_ms2[2 * col + 1] : 0.f;
+      float s1 = 0.f, s2 = 0.f, s3 = 0.f;
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = m0 + wr * TM + i * 16 + fq * 4 + r;
+          if (row < M && cok) {
+            const long e = out_row(row) * g.ldy + col;
+            const float gv = bf2f(g.bnr_mask[e]) > 0.f ? acc[i][j][r] : 0.f;
+            s1 += gv;
+            s2 += gv * (bf2f(g.bnr_x[e]) - mu) * rs;
+            if (g.bnr_x2) s3 += gv * (bf2f(g.bnr_x2[e]) - mu2) * rs2;
           }
-          const bf16_t h = f2bf(v);
-          g.Y[(long)row * g.ldy + col] = h;
-          const float hv = bf2f(h);
-          csum += hv;
-          csq += hv * hv;
+        }
+#pragma unroll
+      for (int o = 16; o < 64; o <<= 1) {
+        s1 += __shfl_xor(s1, o, 64);
+        s2 += __shfl_xor(s2, o, 64);
+        s3 += __shfl_xor(s3, o, 64);
+      }
+      ps[j][0] = s1;
+      ps[j][1] = s2;
+      ps[j][2] = s3;
+    }
+    float* red = reinterpret_cast<float*>(smem);
+    __syncthreads();
+    if (wr == 1 && fq == 0)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int q = 0; q < 3; ++q) red[((wc * FN + j) * 16 + fr) * 3 + q] = ps[j][q];
+    __syncthreads();
+    if (wr == 0 && fq == 0) {
+      const long slab = (long)(ty % MER_BN_STAT_PARTS) * g.Ncols * 2;
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int col = n0 + wc * TN + j * 16 + fr;
+        if (col < g.Ncols) {
+          const float* o = red + ((wc * FN + j) * 16 + fr) * 3;
+          atomicAdd(g.bnr_red + slab + 2 * col, ps[j][0] + o[0]);
+          atomicAdd(g.bnr_red + slab + 2 * col + 1, ps[j][1] + o[1]);
+          if (g.bnr_red2) {
+            atomicAdd(g.bnr_red2 + slab + 2 * col, ps[j][0] + o[0]);
+            atomicAdd(g.bnr_red2 + slab + 2 * col + 1, ps[j][2] + o[2]);
+          }
         }
       }
-    if (g.stats) {
+    }
+  }
+  if (g.stats) {
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int col = n0 + wc * TN + j * 16 + fr;
+      float csum = 0.f, csq = 0.f;
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = m0 + wr * TM + i * 16 + fq * 4 + r;
+          if (row < M && col < g.Ncols) {
+            const float hv = acc[i][j][r];
+            csum += hv;
+            csq += hv * hv;
+          }
+        }
       csum += __shfl_xor(csum, 16, 64);
       csum += __shfl_xor(csum, 32, 64);
       csq += __shfl_xor(csq, 16, 64);
@@ -504,8 +654,6 @@ __global__ __launch_bounds__(256, 2) void conv_pipe_kernel(ConvGeom g) {
       part[j][0] = csum;
       part[j][1] = csq;
     }
-  }
-  if (g.stats) {
     // the two M-waves of a column pair meet in LDS (the staging buffers are idle now); one striped
     // atomic per (block, column): slab row ty % MER_BN_STAT_PARTS keeps same-address atomics rare
     float* red = reinterpret_cast<float*>(smem);
@@ -531,26 +679,29 @@ __global__ __launch_bounds__(256, 2) void conv_pipe_kernel(ConvGeom g) {
   }
 }
 
-template <bool DGRAD, int BM_, int BN_>
+template <bool DGRAD, bool PAR, int BM_, int BN_>
 int launch_conv_pipe_t(ConvGeom& g, hipStream_t st) {
-  const int M = g.N * g.OH * g.OW;
-  const long tiles = (long)((M + BM_ - 1) / BM_) * ((g.Ncols + BN_ - 1) / BN_);
+  // PAR: grid.x covers the largest parity class (ph = pw = 0), grid.y = the 4 classes
+  const int Mg = PAR ? g.N * ((g.OH + 1) / 2) * ((g.OW + 1) / 2) : g.N * g.OH * g.OW;
+  const long tiles = (long)((Mg + BM_ - 1) / BM_) * ((g.Ncols + BN_ - 1) / BN_);
   const size_t lds = 2 * (BM_ + BN_) * 64 * sizeof(bf16_t);
-  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_pipe_kernel<DGRAD, BM_, BN_>),
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_pipe_kernel<DGRAD, PAR, BM_, BN_>),
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return (int)hipErrorInvalidConfiguration;
-  hipLaunchKernelGGL((conv_pipe_kernel<DGRAD, BM_, BN_>), dim3((unsigned)tiles), dim3(256), lds, st, g);
+  hipLaunchKernelGGL((conv_pipe_kernel<DGRAD, PAR, BM_, BN_>), dim3((unsigned)tiles, PAR ? 4 : 1), dim3(256), lds, st,
+                     g);
   return (int)hipGetLastError();
 }
 
-template <bool DGRAD>
+template <bool DGRAD, bool PAR>
 int launch_conv_pipe(ConvGeom& g, hipStream_t st) {
-  const int M = g.N * g.OH * g.OW;
+  const int M = PAR ? g.N * g.OH * g.OW / 4 : g.N * g.OH * g.OW;
   const int bn = g.Ncols <= 64 ? 64 : 128;
-  const long tiles128 = (long)((M + 127) / 128) * ((g.Ncols + bn - 1) / bn);
+  const long tiles128 = (long)((M + 127) / 128) * ((g.Ncols + bn - 1) / bn) * (PAR ? 4 : 1);
   const bool small_m = tiles128 < 384;
-  if (bn == 64) return small_m ? launch_conv_pipe_t<DGRAD, 64, 64>(g, st) : launch_conv_pipe_t<DGRAD, 128, 64>(g, st);
-  return small_m ? launch_conv_pipe_t<DGRAD, 64, 128>(g, st) : launch_conv_pipe_t<DGRAD, 128, 128>(g, st);
+  if (bn == 64)
+    return small_m ? launch_conv_pipe_t<DGRAD, PAR, 64, 64>(g, st) : launch_conv_pipe_t<DGRAD, PAR, 128, 64>(g, st);
+  return small_m ? launch_conv_pipe_t<DGRAD, PAR, 64, 128>(g, st) : launch_conv_pipe_t<DGRAD, PAR, 128, 128>(g, st);
 }
 
 template <bool DGRAD>
@@ -593,7 +744,7 @@ MER_API int mer_conv_fwd_ex(int N, int H, int W, int C, int K, int R, int S, int
   g.Ncols = K; g.Kred = R * S * C;
   g.X = (const bf16_t*)x; g.Wt = (const bf16_t*)w_packed; g.Y = (bf16_t*)y; g.ldy = K; g.stats = stats;
   if (variant == 0) return launch_conv<false>(g, (hipStream_t)stream);
-  return launch_conv_pipe<false>(g, (hipStream_t)stream);
+  return launch_conv_pipe<false, false>(g, (hipStream_t)stream);
 }
 
 MER_API int mer_conv_dgrad(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, const void* dy,
@@ -605,7 +756,17 @@ MER_API int mer_conv_dgrad(int N, int H, int W, int C, int K, int R, int S, int 
 MER_API int mer_conv_dgrad_ex(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, const void* dy,
                               const void* wt_packed, void* dx, const void* residual, const void* residual_mask,
                               int variant, void* stream) {
+  return mer_conv_dgrad_bnr(N, H, W, C, K, R, S, stride, pad, dy, wt_packed, dx, residual, residual_mask, nullptr,
+                            nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, variant, stream);
+}
+
+MER_API int mer_conv_dgrad_bnr(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, const void* dy,
+                               const void* wt_packed, void* dx, const void* residual, const void* residual_mask,
+                               const void* bn_mask, const void* bn_x, const float* bn_ms, float* bn_red,
+                               const void* bn_x2, const float* bn_ms2, float* bn_red2, int variant, void* stream) {
   if (K % 8 || C % 8 || variant < -1 || variant > 1) return (int)hipErrorInvalidValue;
+  if (bn_red && (!bn_mask || !bn_x || !bn_ms || (bn_x2 && (!bn_ms2 || !bn_red2)))) return (int)hipErrorInvalidValue;
+  if (bn_red && (variant == 0 || stride > 2)) return (int)hipErrorInvalidValue;  // fused only in the pipelined kernel
   ConvGeom g{};
   g.N = N; g.OH = H; g.OW = W;
   g.IH = (H + 2 * pad - R) / stride + 1; g.IW = (W + 2 * pad - S) / stride + 1; g.IC = K;
@@ -613,8 +774,11 @@ MER_API int mer_conv_dgrad_ex(int N, int H, int W, int C, int K, int R, int S, i
   g.Ncols = C; g.Kred = R * S * K;
   g.X = (const bf16_t*)dy; g.Wt = (const bf16_t*)wt_packed; g.Y = (bf16_t*)dx; g.ldy = C; g.stats = nullptr;
   g.R_ = (const bf16_t*)residual; g.Rmask = (const bf16_t*)residual_mask;
+  g.bnr_mask = (const bf16_t*)bn_mask; g.bnr_x = (const bf16_t*)bn_x; g.bnr_ms = bn_ms; g.bnr_red = bn_red;
+  g.bnr_x2 = (const bf16_t*)bn_x2; g.bnr_ms2 = bn_ms2; g.bnr_red2 = bn_red2;
   if (variant == 0 || stride > 2) return launch_conv<true>(g, (hipStream_t)stream);
-  return launch_conv_pipe<true>(g, (hipStream_t)stream);
+  if (stride == 2) return launch_conv_pipe<true, true>(g, (hipStream_t)stream);
+  return launch_conv_pipe<true, false>(g, (hipStream_t)stream);
 }
 
 MER_API int mer_conv_wgrad(int N, int H, int W, int C, int Creal, int K, int R, int S, int stride, int pad,
@@ -835,6 +999,21 @@ MER_API int mer_bn_bwd_reduce(long M, int C, const void* dy, const void* mask, c
   const long blocks = (M + rpb - 1) / rpb;
   hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, M, C,
                      (const bf16_t*)dy, (const bf16_t*)mask, (const bf16_t*)x, ms, red, rpb);
+  MER_LAUNCH_CHECK();
+}
+
+// out[c] = sum_p in[p][c] over `parts` striped partial rows of (a, b) pairs (fused-epilogue reductions)
+__global__ void partials_sum_kernel(int C, int parts, const float* __restrict__ in, float* __restrict__ out) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;  // (c, pair-slot)
+  if (e >= 2 * C) return;
+  float acc = 0.f;
+  for (int p = 0; p < parts; ++p) acc += in[(long)p * 2 * C + e];
+  out[e] = acc;
+}
+MER_API int mer_partials_sum(int C, int parts, const float* in, float* out, void* stream) {
+  if (C <= 0 || parts <= 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(partials_sum_kernel, dim3((2 * C + 255) / 256), dim3(256), 0, (hipStream_t)stream, C, parts, in,
+                     out);
   MER_LAUNCH_CHECK();
 }
 

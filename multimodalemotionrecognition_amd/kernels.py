@@ -323,14 +323,32 @@ def conv_fwd(x, wp, y, stats, R, S, stride, pad, variant=-1):
             wp.data_ptr(), y.data_ptr(), _ptr(stats), int(variant), stream_ptr())
 
 
-def conv_dgrad(dy, wt, dx, R, S, stride, pad, residual=None, mask=None, variant=-1):
+def conv_dgrad(dy, wt, dx, R, S, stride, pad, residual=None, mask=None, variant=-1, bnr=None):
+    """dx = conv-transpose(dy) (+ residual where mask > 0).  ``bnr``: optional fused BatchNorm-backward
+    reduction of the BN the gradient flows into, ``(mask, x, ms, red[, x2, ms2, red2])`` with red(2)
+    zeroed [BN_STAT_PARTS, C, 2] buffers (see mer_conv_dgrad_bnr)."""
     N, H, W, C = dx.shape
     Kc = dy.shape[-1]
     Ho, Wo = (H + 2 * pad - R) // stride + 1, (W + 2 * pad - S) // stride + 1
     if tuple(dy.shape) != (N, Ho, Wo, Kc) or tuple(wt.shape) != (C, R * S * Kc):
         raise ValueError(f"conv_dgrad shapes dy{tuple(dy.shape)} wt{tuple(wt.shape)} dx{tuple(dx.shape)}")
-    _launch("conv_dgrad", (N, H, W, C, Kc, R, stride), "mer_conv_dgrad_ex", N, H, W, C, Kc, R, S, stride, pad,
-            dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), _ptr(residual), _ptr(mask), int(variant), stream_ptr())
+    b = list(bnr) + [None] * (7 - len(bnr)) if bnr is not None else [None] * 7
+    for t in (b[0], b[1], b[4]):
+        if t is not None and tuple(t.shape) != tuple(dx.shape):
+            raise ValueError("conv_dgrad bnr tensors must match dx")
+    for t in (b[3], b[6]):
+        if t is not None and t.numel() != BN_STAT_PARTS * C * 2:
+            raise ValueError("conv_dgrad bnr red buffers must be [BN_STAT_PARTS, C, 2]")
+    _launch("conv_dgrad", (N, H, W, C, Kc, R, stride), "mer_conv_dgrad_bnr", N, H, W, C, Kc, R, S, stride, pad,
+            dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), _ptr(residual), _ptr(mask), *[_ptr(t) for t in b],
+            int(variant), stream_ptr())
+
+
+def partials_sum(parts_buf, out):
+    """out[C,2] = parts_buf[BN_STAT_PARTS, C, 2].sum(0) (collapse a fused-epilogue reduction)."""
+    P, C, _ = parts_buf.shape
+    LIB("mer_partials_sum", C, P, parts_buf.data_ptr(), out.data_ptr(), stream_ptr())
+    return out
 
 
 def conv_wgrad(x, dy, dw, R, S, stride, pad, creal=None):

@@ -211,76 +211,102 @@ def _grad(param, grads):
     return g
 
 
+def _bn_bwd(g, mask, x, ms, bn, red, grads, training):
+    """BatchNorm backward apply given the collapsed reduction red[C,2] = (sum g, sum g*xhat)."""
+    dx = torch.empty_like(x)
+    K.bn_bwd_apply(g, mask, x, ms, bn.weight, red, dx, _grad(bn.weight, grads), _grad(bn.bias, grads), training)
+    return dx
+
+
+def _bnr_target(blk_sv, blk, dev):
+    """The fused-reduction target for a gradient flowing into ``blk``'s output: its bn2 (and downsample
+    BN) read g = grad * (out > 0); returns (bnr tuple for conv_dgrad, partial buffers)."""
+    xin, bc1, bms1, ba1, bc2, bms2, cd, msd, out = blk_sv
+    C2 = bc2.shape[-1]
+    red2 = K.bn_stats_buffer(C2, dev)
+    if cd is None:
+        return (out, bc2, bms2, red2), (red2, None)
+    redd = K.bn_stats_buffer(C2, dev)
+    return (out, bc2, bms2, red2, cd, msd, redd), (red2, redd)
+
+
 @torch.no_grad()
-def block_backward(trunk, blk: BasicBlock, sv, dx: torch.Tensor, grads, training: bool = True):
-    """Reverse of block_forward given dx = dL/d(block output); returns dL/d(block input)."""
+def block_backward(trunk, blk: BasicBlock, sv, dx: torch.Tensor, grads, training: bool = True, pre=None,
+                   prev=None):
+    """Reverse of block_forward given dx = dL/d(block output); returns dL/d(block input).
+
+    ``pre``: this block's bn2 / downsample-BN reductions already accumulated by the producer of ``dx``
+    (partial buffers from the next block's fused dgrad), else they are reduced here.  ``prev``: the
+    (saved, block) of the preceding block, whose reductions this block's input-gradient dgrad fuses.
+    """
     dev = dx.device
     xin, bc1, bms1, ba1, bc2, bms2, cd, msd, out = sv
     g_out = dx
     s = blk.stride
     C2 = bc2.shape[-1]
-    red2 = torch.zeros(C2, 2, device=dev, dtype=torch.float32)
-    K.bn_bwd_reduce(g_out, out, bc2, bms2, red2)
-    dc2 = torch.empty_like(bc2)
-    K.bn_bwd_apply(g_out, out, bc2, bms2, blk.bn2.weight, red2, dc2, _grad(blk.bn2.weight, grads),
-                   _grad(blk.bn2.bias, grads), training)
-    if cd is not None:
-        dbn = blk.downsample[1]
-        redd = torch.zeros(C2, 2, device=dev, dtype=torch.float32)
-        K.bn_bwd_reduce(g_out, out, cd, msd, redd)
-        dcd = torch.empty_like(cd)
-        K.bn_bwd_apply(g_out, out, cd, msd, dbn.weight, redd, dcd, _grad(dbn.weight, grads), _grad(dbn.bias, grads), training)
-    # conv2
+    red2 = torch.empty(C2, 2, device=dev, dtype=torch.float32)
+    redd = torch.empty(C2, 2, device=dev, dtype=torch.float32) if cd is not None else None
+    if pre is not None:
+        K.partials_sum(pre[0], red2)
+        if cd is not None:
+            K.partials_sum(pre[1], redd)
+    else:
+        red2.zero_()
+        K.bn_bwd_reduce(g_out, out, bc2, bms2, red2)
+        if cd is not None:
+            redd.zero_()
+            K.bn_bwd_reduce(g_out, out, cd, msd, redd)
+    dc2 = _bn_bwd(g_out, out, bc2, bms2, blk.bn2, red2, grads, training)
+    dcd = _bn_bwd(g_out, out, cd, msd, blk.downsample[1], redd, grads, training) if cd is not None else None
+    # conv2 (its dgrad also reduces bn1's backward sums: g = da1 * (ba1 > 0))
     w2 = _grad(blk.conv2.weight, grads)
     if w2 is not None:
         K.conv_wgrad(ba1, dc2, w2, 3, 3, 1, 1)
     da1 = torch.empty_like(ba1)
-    K.conv_dgrad(dc2, trunk.packed(blk.conv2, C2, True), da1, 3, 3, 1, 1)
-    # bn1 (relu mask = ba1)
     C1 = bc1.shape[-1]
-    red1 = torch.zeros(C1, 2, device=dev, dtype=torch.float32)
-    K.bn_bwd_reduce(da1, ba1, bc1, bms1, red1)
-    dc1 = torch.empty_like(bc1)
-    K.bn_bwd_apply(da1, ba1, bc1, bms1, blk.bn1.weight, red1, dc1, _grad(blk.bn1.weight, grads),
-                   _grad(blk.bn1.bias, grads), training)
-    # conv1 (+ downsample) -> dx of the block input
+    red1p = K.bn_stats_buffer(C1, dev)
+    K.conv_dgrad(dc2, trunk.packed(blk.conv2, C2, True), da1, 3, 3, 1, 1, bnr=(ba1, bc1, bms1, red1p))
+    red1 = K.partials_sum(red1p, torch.empty(C1, 2, device=dev, dtype=torch.float32))
+    dc1 = _bn_bwd(da1, ba1, bc1, bms1, blk.bn1, red1, grads, training)
+    # conv1 (+ downsample) -> dx of the block input (+ the preceding block's bn2 / downsample reductions)
     w1 = _grad(blk.conv1.weight, grads)
     if w1 is not None:
         K.conv_wgrad(xin, dc1, w1, 3, 3, s, 1)
     dxin = torch.empty_like(xin)
     Cin = xin.shape[-1]
+    bnr, nxt = _bnr_target(prev[0], prev[1], dev) if prev is not None else (None, None)
     if cd is not None:
         wd = _grad(blk.downsample[0].weight, grads)
         if wd is not None:
             K.conv_wgrad(xin, dcd, wd, 1, 1, s, 0)
         dxd = torch.empty_like(xin)
         K.conv_dgrad(dcd, trunk.packed(blk.downsample[0], Cin, True), dxd, 1, 1, s, 0)
-        K.conv_dgrad(dc1, trunk.packed(blk.conv1, Cin, True), dxin, 3, 3, s, 1, residual=dxd)
+        K.conv_dgrad(dc1, trunk.packed(blk.conv1, Cin, True), dxin, 3, 3, s, 1, residual=dxd, bnr=bnr)
     else:
-        K.conv_dgrad(dc1, trunk.packed(blk.conv1, Cin, True), dxin, 3, 3, s, 1, residual=g_out, mask=out)
-    return dxin
+        K.conv_dgrad(dc1, trunk.packed(blk.conv1, Cin, True), dxin, 3, 3, s, 1, residual=g_out, mask=out, bnr=bnr)
+    return dxin, nxt
 
 
 @torch.no_grad()
 def trunk_backward(trunk: ResNet18Trunk, saved, dfeat: torch.Tensor, training: bool = True):
     grads = {}
     dev = dfeat.device
-    bf = torch.bfloat16
     x = saved["final"]
     dx = torch.empty_like(x)
     K.avgpool_bwd(dfeat, dx)
     blocks = _blocks(trunk)
-    for blk, sv in zip(reversed(blocks), reversed(saved["blocks"])):
-        dx = block_backward(trunk, blk, sv, dx, grads, training)
+    svs = saved["blocks"]
+    pre = None
+    for i in reversed(range(len(blocks))):
+        prev = (svs[i - 1], blocks[i - 1]) if i > 0 else None
+        dx, pre = block_backward(trunk, blocks[i], svs[i], dx, grads, training, pre=pre, prev=prev)
     # stem: maxpool -> bn1/relu -> conv1 (no data gradient for the frames)
     x0, c1, ms1, a1, arg = saved["stem"]
     da1 = torch.empty_like(a1)
     K.maxpool_bwd(dx, arg, da1)
     red = torch.zeros(c1.shape[-1], 2, device=dev, dtype=torch.float32)
     K.bn_bwd_reduce(da1, a1, c1, ms1, red)
-    dc1 = torch.empty_like(c1)
-    K.bn_bwd_apply(da1, a1, c1, ms1, trunk[1].weight, red, dc1, _grad(trunk[1].weight, grads), _grad(trunk[1].bias, grads),
-                   training)
+    dc1 = _bn_bwd(da1, a1, c1, ms1, trunk[1], red, grads, training)
     w = _grad(trunk[0].weight, grads)
     if w is not None:
         K.conv_wgrad(x0, dc1, w, 7, 7, 2, 3, creal=3)

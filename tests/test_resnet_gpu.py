@@ -102,7 +102,7 @@ def test_single_block_forward_backward_vs_oracle(layer, bi):
     assert rel_rms(out, to_nhwc(ref.detach())) < 1.5e-2
     g = torch.randn_like(ref).bfloat16().float()
     grads = {}
-    dxin = block_backward(m, blk, sv, to_nhwc(g).bfloat16().cuda(), grads)
+    dxin, _ = block_backward(m, blk, sv, to_nhwc(g).bfloat16().cuda(), grads)
     torch.cuda.synchronize()
     # Reference backward evaluated at OUR forward activations (same ReLU masks, same batch statistics):
     # an fp32 forward flips ~1% of near-zero ReLU decisions vs a bf16 forward, which alone moves masked
@@ -243,3 +243,39 @@ def test_conv_variants_bit_identical(N, H, C, Kc, R, stride, pad):
         K.conv_dgrad(dy, wt, dx, R, R, stride, pad, residual=res, mask=mask, variant=v)
         dxs.append(dx)
     assert torch.equal(dxs[0], dxs[1])
+
+
+@pytest.mark.parametrize("stride,ds", [(1, False), (2, True)])
+def test_dgrad_fused_bn_reduce_matches_standalone(stride, ds):
+    """mer_conv_dgrad_bnr's epilogue reduction == mer_bn_bwd_reduce over the stored gradient (both BNs)."""
+    from multimodalemotionrecognition_amd import kernels as K
+
+    torch.manual_seed(2)
+    N, H, C, Kc = 4, 14, 64, 128
+    Ho = (H + 2 - 3) // stride + 1
+    dy = torch.randn(N, Ho, Ho, Kc, device="cuda").bfloat16()
+    w = torch.randn(Kc, C, 3, 3, device="cuda") * 0.05
+    wt = torch.empty(C, 9 * Kc, device="cuda", dtype=torch.bfloat16)
+    K.pack_conv_weight(w, wt, C, True)
+    res = torch.randn(N, H, H, C, device="cuda").bfloat16()
+    mask = torch.randn(N, H, H, C, device="cuda").bfloat16()
+    x = torch.randn(N, H, H, C, device="cuda").bfloat16()
+    x2 = torch.randn(N, H, H, C, device="cuda").bfloat16()
+    ms = torch.stack([torch.randn(C), torch.rand(C) + 0.5], 1).cuda().contiguous()
+    ms2 = torch.stack([torch.randn(C), torch.rand(C) + 0.5], 1).cuda().contiguous()
+    red_p, red2_p = K.bn_stats_buffer(C, "cuda"), K.bn_stats_buffer(C, "cuda")
+    dx = torch.empty(N, H, H, C, device="cuda", dtype=torch.bfloat16)
+    bnr = (mask, x, ms, red_p, x2, ms2, red2_p) if ds else (mask, x, ms, red_p)
+    K.conv_dgrad(dy, wt, dx, 3, 3, stride, 1, residual=res, mask=mask, bnr=bnr)
+    dx_ref = torch.empty_like(dx)
+    K.conv_dgrad(dy, wt, dx_ref, 3, 3, stride, 1, residual=res, mask=mask)
+    assert torch.equal(dx, dx_ref)
+    red = K.partials_sum(red_p, torch.empty(C, 2, device="cuda"))
+    ref = torch.zeros(C, 2, device="cuda")
+    K.bn_bwd_reduce(dx_ref, mask, x, ms, ref)
+    assert torch.allclose(red, ref, rtol=1e-4, atol=1e-3)
+    if ds:
+        red2 = K.partials_sum(red2_p, torch.empty(C, 2, device="cuda"))
+        ref2 = torch.zeros(C, 2, device="cuda")
+        K.bn_bwd_reduce(dx_ref, mask, x2, ms2, ref2)
+        assert torch.allclose(red2, ref2, rtol=1e-4, atol=1e-3)
