@@ -93,4 +93,18 @@ __device__ __forceinline__ void xcd_tile(int pid, int nx, int ntiles, int& tx, i
 // TEMPLATE, hipcc (ROCm 7.2) silently drops the host launch stub (undefined symbol at load time).
 __device__ __forceinline__ void glds16(const void* g, void* lds) { __builtin_amdgcn_global_load_lds(g, lds, 16, 0, 0); }
 
+// xcd_tile plus grouped rasterisation inside each XCD's chunk: consecutive tiles walk a G-row band
+// column by column, so the ~64 tiles an XCD runs at once cover ~G x 64/G panels of A and B instead of
+// a few full rows (every B panel) -- a smaller working set for that XCD's 4 MB L2.
+__device__ __forceinline__ void xcd_tile_grouped(int pid, int nx, int ny, int G, int& tx, int& ty) {
+  const int ntiles = nx * ny;
+  const int q = ntiles / 8, r = ntiles % 8, xcd = pid % 8, loc = pid / 8;
+  const int tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+  const int band = G * nx, gid = tile / band, first = gid * G;
+  const int gsz = ny - first < G ? ny - first : G;
+  const int in = tile - gid * band;
+  ty = first + in % gsz;
+  tx = in / gsz;
+}
+
 #define MER_LAUNCH_CHECK() return (int)hipGetLastError()

@@ -175,7 +175,7 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_pipe_kernel(GemmArgs g) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int nx = (g.N + CF::BN - 1) / CF::BN, ny = (g.M + CF::BM - 1) / CF::BM;
   int tx, ty;
-  xcd_tile(blockIdx.x, nx, nx * ny, tx, ty);
+  xcd_tile_grouped(blockIdx.x, nx, ny, 8, tx, ty);
   const int m0 = ty * CF::BM, n0 = tx * CF::BN;
   const int wr = w / CF::WN, wc = w % CF::WN;
 

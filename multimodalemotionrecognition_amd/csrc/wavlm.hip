@@ -192,24 +192,47 @@ __global__ __launch_bounds__(256) void wavlm_attn_kernel(int L, int H, const bf1
     for (int i = 0; i < 8; ++i) Vt[(ch * 8 + i) * VTP + row] = hv[i];
   }
   for (int r = t; r < 2 * L - 1; r += 256) tbl[r] = rel_emb[(long)bucket[r] * H + h];
-  // gate per query row (fp32, from the layer input slice)
-  for (int i = t; i < LP; i += 256) {
-    float gsum = 1.f;
-    if (i < L) {
+  // gate per query row (fp32, from the layer input slice): 8 lanes per row, each lane one 16-byte
+  // chunk (8 channels) of x and the matching 8x8 block of gru_rel_pos_linear's weight in registers;
+  // the 8 projections are summed over the row's lanes with 3 xor-shuffles each.
+  {
+    const int sub = lane >> 3, cl = lane & 7;
+    float gwr[8][8];
+#pragma unroll
+    for (int o = 0; o < 8; ++o)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) gwr[o][e] = gw[o * ADH + cl * 8 + e];
+    for (int i0 = w * 8; i0 < LP; i0 += 32) {
+      const int i = i0 + sub;
       float pr[8];
 #pragma unroll
-      for (int o = 0; o < 8; ++o) pr[o] = gb[o];
-      const bf16_t* xr = x + ((long)b * L + i) * ldx + h * ADH;
-      for (int c = 0; c < ADH; ++c) {
-        const float xv = bf2f(xr[c]);
+      for (int o = 0; o < 8; ++o) pr[o] = 0.f;
+      if (i < L) {
+        const u32x4 xv = *reinterpret_cast<const u32x4*>(x + ((long)b * L + i) * ldx + h * ADH + cl * 8);
+        const bf16_t* xh = reinterpret_cast<const bf16_t*>(&xv);
 #pragma unroll
-        for (int o = 0; o < 8; ++o) pr[o] += xv * gw[o * ADH + c];
+        for (int e = 0; e < 8; ++e) {
+          const float xe = bf2f(xh[e]);
+#pragma unroll
+          for (int o = 0; o < 8; ++o) pr[o] += xe * gwr[o][e];
+        }
       }
-      const float ga = 1.f / (1.f + __expf(-(pr[0] + pr[1] + pr[2] + pr[3])));
-      const float gbv = 1.f / (1.f + __expf(-(pr[4] + pr[5] + pr[6] + pr[7])));
-      gsum = ga * (gbv * gconst[h] - 1.f) + 2.f;
+#pragma unroll
+      for (int o = 0; o < 8; ++o) {
+        pr[o] += __shfl_xor(pr[o], 1, 64);
+        pr[o] += __shfl_xor(pr[o], 2, 64);
+        pr[o] += __shfl_xor(pr[o], 4, 64);
+      }
+      if (cl == 0 && i < LP) {
+        float gsum = 1.f;
+        if (i < L) {
+          const float ga = 1.f / (1.f + __expf(-(pr[0] + pr[1] + pr[2] + pr[3] + gb[0] + gb[1] + gb[2] + gb[3])));
+          const float gbv = 1.f / (1.f + __expf(-(pr[4] + pr[5] + pr[6] + pr[7] + gb[4] + gb[5] + gb[6] + gb[7])));
+          gsum = ga * (gbv * gconst[h] - 1.f) + 2.f;
+        }
+        gate[i] = gsum;
+      }
     }
-    gate[i] = gsum;
   }
   __syncthreads();
 

@@ -20,7 +20,10 @@ SHAPES = {
 
 def main():
     torch.manual_seed(0)
+    quick = "--quick" in sys.argv  # profiling: fewer shapes / reps
     for name, (M, N, Kd, rows, alen) in SHAPES.items():
+        if quick and name not in ("conv1 (rows)", "qkv", "ffn2"):
+            continue
         a = (torch.rand(alen if rows else M * Kd, device="cuda") * 2 - 1).bfloat16()
         if not rows:
             a = a.view(M, Kd)
@@ -34,7 +37,7 @@ def main():
                     K.gemm_bf16(a, w, out, variant=v, **kw)
                 torch.cuda.synchronize()
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                reps = 20
+                reps = 5 if quick else 20
                 e0.record()
                 for _ in range(reps):
                     K.gemm_bf16(a, w, out, variant=v, **kw)
