@@ -38,6 +38,22 @@ PEAK_HBM_GBS = 8000.0       # HBM3E spec
 # Dominant kernel (largest share of step time in profiles/): the WavLM feature-extractor conv1 as an
 # implicit GEMM: M = B*4799 output frames, N = 512 channels, K = 3 taps * 512.
 PROBE = ("gemm_bf16", (BATCH * 4799, 512, 1536))
+# the kernel mer_gemm_bf16 dispatches for that shape (gemm_bf16.hip pick_variant: 1,200 tiles of 256x256)
+PROBE_KERNEL = "gemm_pipe_kernel<PipeCfg<256,256,2,4>, bf16>"
+PMC_FILE = ROOT / "profiles" / "pmc_traffic.json"
+
+
+def pmc_traffic():
+    """HBM bytes per launch of the probe kernel from the committed PMC passes (tools/pmc_traffic.py:
+    FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE, rocprofv3 --pmc in separate passes), or None when
+    no measurement of the current probe kernel is on file."""
+    try:
+        d = json.loads(PMC_FILE.read_text())
+    except (OSError, ValueError):
+        return None
+    if d.get("kernel_match") not in PROBE_KERNEL.replace(" ", "") or tuple(d.get("shape", ())) != PROBE[1]:
+        return None
+    return d.get("traffic_bytes_per_launch")
 
 
 def synthetic_batch(device, seed):
@@ -132,8 +148,8 @@ def main():
     if kms:
         achieved = probe.units / (kms * 1e-3) / 1e12
         roof = {"bound": "mfma", "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None,
-                "kernel": f"gemm_bf16_kernel<0,bf16> (WavLM conv1 implicit GEMM {PROBE[1][0]}x{PROBE[1][1]}x{PROBE[1][2]})",
+                "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": pmc_traffic(),
+                "kernel": f"{PROBE_KERNEL} (WavLM conv1 implicit GEMM {PROBE[1][0]}x{PROBE[1][1]}x{PROBE[1][2]})",
                 "avg_ms": round(kms, 4), "launches": len(probe.pairs)}
     out = {
         "metric": "3s-clip train steps/sec (B=32, xattn fusion) at 1/2/4/8 MI355X",

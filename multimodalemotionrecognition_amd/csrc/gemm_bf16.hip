@@ -169,10 +169,15 @@ struct PipeCfg {
 
 __device__ __forceinline__ int swz_chunk(int row, int c) { return c ^ ((row >> 1) & 7); }
 
-template <class CF, typename TOUT>
+__device__ __attribute__((aligned(16))) uint32_t mer_gemm_zero16[4] = {0u, 0u, 0u, 0u};
+
+// AMODE 0: rows mode; AMODE 1: grouped positional conv (group = blockIdx.z), A chunks gathered per
+// K-tile from x[b, t + tap - pad, z*cg + c] with out-of-range taps served from a zero chunk.
+template <class CF, typename TOUT, int AMODE>
 __global__ __launch_bounds__(CF::NT, 1) void gemm_pipe_kernel(GemmArgs g) {
   extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int z = blockIdx.z;
   const int nx = (g.N + CF::BN - 1) / CF::BN, ny = (g.M + CF::BM - 1) / CF::BM;
   int tx, ty;
   xcd_tile_grouped(blockIdx.x, nx, ny, 8, tx, ty);
@@ -182,27 +187,47 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_pipe_kernel(GemmArgs g) {
   // per-lane source pointers (fixed over K; advanced by 64 elements per K-tile)
   const bf16_t* pa[CF::IA];
   const bf16_t* pb[CF::IB];
+  int at[CF::IA], acl[CF::IA];  // AMODE 1: the row's time index and logical chunk
   const int lrow = lane >> 3, lchunk = lane & 7;
 #pragma unroll
   for (int j = 0; j < CF::IA; ++j) {
     const int r = (w * CF::IA + j) * 8 + lrow;
     int m = m0 + r;
     m = m < g.M ? m : g.M - 1;
-    pa[j] = g.A + (long)(m / g.a_rpg) * g.a_gstride + (long)(m % g.a_rpg) * g.a_rstride + swz_chunk(r, lchunk) * 8;
+    if (AMODE == 0) {
+      pa[j] = g.A + (long)(m / g.a_rpg) * g.a_gstride + (long)(m % g.a_rpg) * g.a_rstride + swz_chunk(r, lchunk) * 8;
+    } else {
+      const int b = m / g.pc_L;
+      at[j] = m - b * g.pc_L;
+      acl[j] = swz_chunk(r, lchunk) * 8;
+      pa[j] = g.A + (long)b * g.pc_L * g.pc_ldx + (long)z * g.pc_cg;
+    }
   }
+  const bf16_t* Bz = g.B + (long)z * g.b_zstride;
 #pragma unroll
   for (int j = 0; j < CF::IB; ++j) {
     const int r = (w * CF::IB + j) * 8 + lrow;
     int n = n0 + r;
     n = n < g.N ? n : g.N - 1;
-    pb[j] = g.B + (long)n * g.ldb + swz_chunk(r, lchunk) * 8;
+    pb[j] = Bz + (long)n * g.ldb + swz_chunk(r, lchunk) * 8;
   }
+  const float inv_cg = AMODE == 1 ? 1.f / g.pc_cg : 0.f;
   auto stage = [&](int buf, int k0) {
     bf16_t* la = smem + buf * CF::BUF;
     bf16_t* lb = la + CF::BM * 64;
 #pragma unroll
-    for (int j = 0; j < CF::IA; ++j)
-      glds16(pa[j] + k0, la + (w * CF::IA + j) * 512);
+    for (int j = 0; j < CF::IA; ++j) {
+      if (AMODE == 0) {
+        glds16(pa[j] + k0, la + (w * CF::IA + j) * 512);
+      } else {
+        const int k = k0 + acl[j];
+        const int tap = fdiv(k, inv_cg), c = k - tap * g.pc_cg;
+        const int src = at[j] + tap - g.pc_pad;
+        const bool ok = src >= 0 && src < g.pc_L;
+        glds16(ok ? pa[j] + (long)src * g.pc_ldx + c : reinterpret_cast<const bf16_t*>(mer_gemm_zero16),
+               la + (w * CF::IA + j) * 512);
+      }
+    }
 #pragma unroll
     for (int j = 0; j < CF::IB; ++j)
       glds16(pb[j] + k0, lb + (w * CF::IB + j) * 512);
@@ -250,12 +275,12 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_pipe_kernel(GemmArgs g) {
     __syncthreads();
   }
 
-  TOUT* C = reinterpret_cast<TOUT*>(g.C);
+  TOUT* C = reinterpret_cast<TOUT*>(g.C) + (long)z * g.c_zoff;
 #pragma unroll
   for (int j = 0; j < CF::FN; ++j) {
     const int col = n0 + wc * CF::TN + j * 16 + fr;
     if (col >= g.N) continue;
-    const float bv = g.bias ? g.bias[col] : 0.f;
+    const float bv = g.bias ? g.bias[(long)z * g.c_zoff + col] : 0.f;
 #pragma unroll
     for (int i = 0; i < CF::FM; ++i)
 #pragma unroll
@@ -263,7 +288,7 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_pipe_kernel(GemmArgs g) {
         const int row = m0 + wr * CF::TM + i * 16 + fq * 4 + r;
         if (row >= g.M) continue;
         float v = apply_act(acc[i][j][r] + bv, g.act);
-        if (g.R) v += bf2f(g.R[(long)row * g.ldr + col]);
+        if (g.R) v += bf2f(g.R[(long)row * g.ldr + (long)z * g.c_zoff + col]);
         stf<TOUT>(C, (long)row * g.ldc + col, v);
       }
   }
@@ -272,21 +297,23 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_pipe_kernel(GemmArgs g) {
 using CfgL = PipeCfg<256, 256, 2, 4>;  // 8 waves, 128x64 per wave, 128 KiB LDS
 using CfgM = PipeCfg<256, 128, 4, 2>;  // 8 waves, 64x64 per wave, 96 KiB LDS
 using CfgS = PipeCfg<128, 128, 2, 2>;  // 4 waves, 64x64 per wave, 64 KiB LDS
+using CfgP = PipeCfg<128, 64, 2, 2>;   // 4 waves, 64x32 per wave, 48 KiB LDS (pos-conv: 48 columns per group)
 
-template <class CF, typename TOUT>
-int launch_pipe_t(const GemmArgs& g, hipStream_t st) {
+template <class CF, typename TOUT, int AMODE>
+int launch_pipe_t(const GemmArgs& g, int groups, hipStream_t st) {
   const long tiles = (long)((g.N + CF::BN - 1) / CF::BN) * ((g.M + CF::BM - 1) / CF::BM);
   const size_t lds = 2 * CF::BUF * sizeof(bf16_t);
-  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_pipe_kernel<CF, TOUT>),
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_pipe_kernel<CF, TOUT, AMODE>),
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return (int)hipErrorInvalidConfiguration;
-  hipLaunchKernelGGL((gemm_pipe_kernel<CF, TOUT>), dim3((unsigned)tiles), dim3(CF::NT), lds, st, g);
+  hipLaunchKernelGGL((gemm_pipe_kernel<CF, TOUT, AMODE>), dim3((unsigned)tiles, 1, groups), dim3(CF::NT), lds, st, g);
   return (int)hipGetLastError();
 }
 
-template <class CF>
-int launch_pipe(const GemmArgs& g, int out_dtype, hipStream_t st) {
-  return out_dtype == MER_BF16 ? launch_pipe_t<CF, bf16_t>(g, st) : launch_pipe_t<CF, float>(g, st);
+template <class CF, int AMODE = 0>
+int launch_pipe(const GemmArgs& g, int out_dtype, hipStream_t st, int groups = 1) {
+  return out_dtype == MER_BF16 ? launch_pipe_t<CF, bf16_t, AMODE>(g, groups, st)
+                               : launch_pipe_t<CF, float, AMODE>(g, groups, st);
 }
 
 // Tile choice (measured on the WavLM shapes at B=32, tools/bench_gemm.py): the 256x256 tile only pays
@@ -352,5 +379,7 @@ MER_API int mer_posconv_gemm_bf16(int B, int L, int C_total, int groups, int tap
   g.B = (const bf16_t*)Wp; g.ldb = (long)taps * cg; g.b_zstride = (long)cg * taps * cg;
   g.C = out; g.ldc = ldo; g.c_zoff = cg;
   g.bias = bias; g.R = (const bf16_t*)R; g.ldr = ldr; g.act = act;
+  if (g.K % 64 == 0 && (((uintptr_t)X | (uintptr_t)Wp) & 15) == 0)
+    return launch_pipe<CfgP, 1>(g, out_dtype, (hipStream_t)stream, groups);
   return launch<1>(g, out_dtype, groups, (hipStream_t)stream);
 }

@@ -104,3 +104,26 @@ def test_gemm_bf16_variants(variant):
     out = torch.empty(Bc * Lout, C, device="cuda", dtype=torch.float32)
     K.gemm_bf16(x.cuda(), wc.cuda(), out, M=Bc * Lout, K=3 * C, rows=(Lout, 2 * C, Lin * C), variant=variant)
     assert float((out.cpu() - ref).abs().max()) < 2e-2 * (3 * C / 64) ** 0.5 * 0.05 * 8
+
+
+@pytest.mark.parametrize("L", [37, 149])
+def test_posconv_gemm_vs_torch(L):
+    """Grouped positional Conv1d(768, 768, k=128, pad=64, groups=16) + bias + GELU + residual
+    (TF:48-90) on the pipelined kernel vs torch fp32 on the same bf16 operands."""
+    from multimodalemotionrecognition_amd import kernels as K
+
+    torch.manual_seed(3)
+    B, C, G, taps = 2, 768, 16, 128
+    cg = C // G
+    x = torch.randn(B, L, C).bfloat16()
+    w = (torch.randn(C, cg, taps) * 0.02).bfloat16()
+    b = torch.randn(C) * 0.1
+    r = torch.randn(B, L, C).bfloat16()
+    ref = F_conv = torch.nn.functional.conv1d(x.float().transpose(1, 2), w.float(), b, padding=64, groups=G)
+    ref = torch.nn.functional.gelu(F_conv[:, :, :L].transpose(1, 2)) + r.float()
+    wp = w.view(G, cg, cg, taps).permute(0, 1, 3, 2).contiguous().view(C, taps * cg)  # [g*48+n][tap][c]
+    out = torch.empty(B * L, C, device="cuda", dtype=torch.float32)
+    K.posconv_gemm_bf16(x.cuda().view(B * L, C), wp.cuda(), out, B, L, C, G, taps, 64, b.cuda(),
+                        r.cuda().view(B * L, C), act="gelu")
+    err = float((out.cpu().view(B, L, C) - ref).abs().max())
+    assert err < 2e-2, err
