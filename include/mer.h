@@ -22,7 +22,7 @@
 
 /* BatchNorm batch statistics are accumulated by the conv epilogue into MER_BN_STAT_PARTS striped partial
  * rows: a `stats` buffer is float[MER_BN_STAT_PARTS][C][2] (sum, sum of squares), zeroed by the caller. */
-#define MER_BN_STAT_PARTS 256
+#define MER_BN_STAT_PARTS 64
 
 #ifdef __cplusplus
 extern "C" {

@@ -860,21 +860,35 @@ MER_API int mer_pack_conv_weight(int K, int C, int R, int S, int Cp, int transpo
 // finalize: ms[c] = (mean, rstd); running_mean = (1-mom) rm + mom*mean; running_var uses the
 // unbiased variance (torch semantics); num_batches_tracked += 1.
 // ---------------------------------------------------------------------------------------
-__global__ void bn_finalize_kernel(int C, long M, const float* __restrict__ stats, float eps, float momentum,
-                                   float* __restrict__ ms, float* __restrict__ rmean, float* __restrict__ rvar,
-                                   long long* __restrict__ nbt) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+// 64 channels per block; the 4 waves split the striped partial rows, then meet in LDS
+__global__ __launch_bounds__(256) void bn_finalize_kernel(int C, long M, const float* __restrict__ stats, float eps,
+                                                          float momentum, float* __restrict__ ms,
+                                                          float* __restrict__ rmean, float* __restrict__ rvar,
+                                                          long long* __restrict__ nbt) {
+  __shared__ float part[4][64][2];
+  const int cl = threadIdx.x & 63, pg = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
   if (!stats) {  // eval mode: normalise with the running statistics, no update
-    ms[2 * c] = rmean[c];
-    ms[2 * c + 1] = rsqrtf(rvar[c] + eps);
+    if (pg == 0 && c < C) {
+      ms[2 * c] = rmean[c];
+      ms[2 * c + 1] = rsqrtf(rvar[c] + eps);
+    }
     return;
   }
   float sum = 0.f, sq = 0.f;
-  for (int p = 0; p < MER_BN_STAT_PARTS; ++p) {
-    sum += stats[(long)p * 2 * C + 2 * c];
-    sq += stats[(long)p * 2 * C + 2 * c + 1];
+  if (c < C) {
+#pragma unroll 4
+    for (int p = pg; p < MER_BN_STAT_PARTS; p += 4) {
+      sum += stats[(long)p * 2 * C + 2 * c];
+      sq += stats[(long)p * 2 * C + 2 * c + 1];
+    }
   }
+  part[pg][cl][0] = sum;
+  part[pg][cl][1] = sq;
+  __syncthreads();
+  if (pg != 0 || c >= C) return;
+  sum = part[0][cl][0] + part[1][cl][0] + part[2][cl][0] + part[3][cl][0];
+  sq = part[0][cl][1] + part[1][cl][1] + part[2][cl][1] + part[3][cl][1];
   const float mean = sum / M;
   const float var = fmaxf(sq / M - mean * mean, 0.f);
   ms[2 * c] = mean;
@@ -886,7 +900,7 @@ __global__ void bn_finalize_kernel(int C, long M, const float* __restrict__ stat
 MER_API int mer_bn_finalize(int C, long M, const float* stats, float eps, float momentum, float* ms, float* rmean,
                             float* rvar, long long* num_batches_tracked, void* stream) {
   if (!stats && (!rmean || !rvar)) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, (hipStream_t)stream, C, M, stats, eps,
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, (hipStream_t)stream, C, M, stats, eps,
                      momentum, ms, rmean, rvar, num_batches_tracked);
   MER_LAUNCH_CHECK();
 }
@@ -1003,16 +1017,24 @@ MER_API int mer_bn_bwd_reduce(long M, int C, const void* dy, const void* mask, c
 }
 
 // out[c] = sum_p in[p][c] over `parts` striped partial rows of (a, b) pairs (fused-epilogue reductions)
-__global__ void partials_sum_kernel(int C, int parts, const float* __restrict__ in, float* __restrict__ out) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;  // (c, pair-slot)
-  if (e >= 2 * C) return;
+// 64 (c, slot) entries per block; the 4 waves split the partial rows, then meet in LDS
+__global__ __launch_bounds__(256) void partials_sum_kernel(int C, int parts, const float* __restrict__ in,
+                                                           float* __restrict__ out) {
+  __shared__ float part[4][64];
+  const int el = threadIdx.x & 63, pg = threadIdx.x >> 6;
+  const int e = blockIdx.x * 64 + el;
   float acc = 0.f;
-  for (int p = 0; p < parts; ++p) acc += in[(long)p * 2 * C + e];
-  out[e] = acc;
+  if (e < 2 * C) {
+#pragma unroll 4
+    for (int p = pg; p < parts; p += 4) acc += in[(long)p * 2 * C + e];
+  }
+  part[pg][el] = acc;
+  __syncthreads();
+  if (pg == 0 && e < 2 * C) out[e] = part[0][el] + part[1][el] + part[2][el] + part[3][el];
 }
 MER_API int mer_partials_sum(int C, int parts, const float* in, float* out, void* stream) {
   if (C <= 0 || parts <= 0) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(partials_sum_kernel, dim3((2 * C + 255) / 256), dim3(256), 0, (hipStream_t)stream, C, parts, in,
+  hipLaunchKernelGGL(partials_sum_kernel, dim3((2 * C + 63) / 64), dim3(256), 0, (hipStream_t)stream, C, parts, in,
                      out);
   MER_LAUNCH_CHECK();
 }

@@ -155,7 +155,7 @@ namespace {
 constexpr int ADH = 64, APAD = ADH + 8;
 }
 
-__global__ __launch_bounds__(256) void wavlm_attn_kernel(int L, int H, const bf16_t* __restrict__ qkv, long ldqkv,
+__global__ __launch_bounds__(256, 2) void wavlm_attn_kernel(int L, int H, const bf16_t* __restrict__ qkv, long ldqkv,
                                                          const bf16_t* __restrict__ x, long ldx,
                                                          const float* __restrict__ gw, const float* __restrict__ gb,
                                                          const float* __restrict__ gconst,
@@ -165,8 +165,7 @@ __global__ __launch_bounds__(256) void wavlm_attn_kernel(int L, int H, const bf1
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   const int LP = (L + 15) / 16 * 16;
   const int VTP = LP + 8;
-  bf16_t* Qs = reinterpret_cast<bf16_t*>(smem_raw);   // [LP][APAD]
-  bf16_t* Ks = Qs + LP * APAD;                        // [LP][APAD]
+  bf16_t* Ks = reinterpret_cast<bf16_t*>(smem_raw);   // [LP][APAD]
   bf16_t* Vt = Ks + LP * APAD;                        // [ADH][VTP]
   bf16_t* Ps = Vt + ADH * VTP;                        // [4][16][VTP]
   float* gate = reinterpret_cast<float*>(Ps + 4 * 16 * VTP);  // [LP]
@@ -175,21 +174,32 @@ __global__ __launch_bounds__(256) void wavlm_attn_kernel(int L, int H, const bf1
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int D = H * ADH;
 
-  // stage Q, K (row-major, padded) and V^T; zero the padding rows
-  for (int c = t; c < LP * 8; c += 256) {
-    const int row = c >> 3, ch = c & 7;
-    u32x4 q = {0u, 0u, 0u, 0u}, k = q, v = q;
-    if (row < L) {
-      const bf16_t* base = qkv + ((long)b * L + row) * ldqkv + h * ADH + ch * 8;
-      q = *reinterpret_cast<const u32x4*>(base);
-      k = *reinterpret_cast<const u32x4*>(base + D);
-      v = *reinterpret_cast<const u32x4*>(base + 2 * D);
-    }
-    *reinterpret_cast<u32x4*>(&Qs[row * APAD + ch * 8]) = q;
-    *reinterpret_cast<u32x4*>(&Ks[row * APAD + ch * 8]) = k;
-    const bf16_t* hv = reinterpret_cast<const bf16_t*>(&v);
+  // stage K (row-major, padded) and V^T; zero the padding rows.  All loads of the (<= 8) passes are
+  // issued before the first LDS store so their latencies overlap (L <= 256: LP*8/256 <= 8 passes).
+  // Q is not staged: each wave reads its 16 query rows' fragments straight from global memory.
+  {
+    u32x4 kr[8], vr[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) Vt[(ch * 8 + i) * VTP + row] = hv[i];
+    for (int it = 0; it < 8; ++it) {
+      const int c = t + it * 256, row = c >> 3, ch = c & 7;
+      kr[it] = u32x4{0u, 0u, 0u, 0u};
+      vr[it] = kr[it];
+      if (c < LP * 8 && row < L) {
+        const bf16_t* base = qkv + ((long)b * L + row) * ldqkv + D + h * ADH + ch * 8;
+        kr[it] = *reinterpret_cast<const u32x4*>(base);
+        vr[it] = *reinterpret_cast<const u32x4*>(base + D);
+      }
+    }
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+      const int c = t + it * 256, row = c >> 3, ch = c & 7;
+      if (c < LP * 8) {
+        *reinterpret_cast<u32x4*>(&Ks[row * APAD + ch * 8]) = kr[it];
+        const bf16_t* hv = reinterpret_cast<const bf16_t*>(&vr[it]);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) Vt[(ch * 8 + i) * VTP + row] = hv[i];
+      }
+    }
   }
   for (int r = t; r < 2 * L - 1; r += 256) tbl[r] = rel_emb[(long)bucket[r] * H + h];
   // gate per query row (fp32, from the layer input slice): 8 lanes per row, each lane one 16-byte
@@ -202,20 +212,28 @@ __global__ __launch_bounds__(256) void wavlm_attn_kernel(int L, int H, const bf1
     for (int o = 0; o < 8; ++o)
 #pragma unroll
       for (int e = 0; e < 8; ++e) gwr[o][e] = gw[o * ADH + cl * 8 + e];
-    for (int i0 = w * 8; i0 < LP; i0 += 32) {
-      const int i = i0 + sub;
+    u32x4 xr[8];
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+      const int i = w * 8 + it * 32 + sub;
+      xr[it] = u32x4{0u, 0u, 0u, 0u};
+      if (i < L) xr[it] = *reinterpret_cast<const u32x4*>(x + ((long)b * L + i) * ldx + h * ADH + cl * 8);
+    }
+    float gbs0 = gb[0] + gb[1] + gb[2] + gb[3], gbs1 = gb[4] + gb[5] + gb[6] + gb[7];
+    const float gc = gconst[h];
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+      const int i = w * 8 + it * 32 + sub;
+      if (w * 8 + it * 32 >= LP) break;  // wave-uniform
       float pr[8];
 #pragma unroll
       for (int o = 0; o < 8; ++o) pr[o] = 0.f;
-      if (i < L) {
-        const u32x4 xv = *reinterpret_cast<const u32x4*>(x + ((long)b * L + i) * ldx + h * ADH + cl * 8);
-        const bf16_t* xh = reinterpret_cast<const bf16_t*>(&xv);
+      const bf16_t* xh = reinterpret_cast<const bf16_t*>(&xr[it]);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float xe = bf2f(xh[e]);
+      for (int e = 0; e < 8; ++e) {
+        const float xe = bf2f(xh[e]);
 #pragma unroll
-          for (int o = 0; o < 8; ++o) pr[o] += xe * gwr[o][e];
-        }
+        for (int o = 0; o < 8; ++o) pr[o] += xe * gwr[o][e];
       }
 #pragma unroll
       for (int o = 0; o < 8; ++o) {
@@ -226,9 +244,9 @@ __global__ __launch_bounds__(256) void wavlm_attn_kernel(int L, int H, const bf1
       if (cl == 0 && i < LP) {
         float gsum = 1.f;
         if (i < L) {
-          const float ga = 1.f / (1.f + __expf(-(pr[0] + pr[1] + pr[2] + pr[3] + gb[0] + gb[1] + gb[2] + gb[3])));
-          const float gbv = 1.f / (1.f + __expf(-(pr[4] + pr[5] + pr[6] + pr[7] + gb[4] + gb[5] + gb[6] + gb[7])));
-          gsum = ga * (gbv * gconst[h] - 1.f) + 2.f;
+          const float ga = 1.f / (1.f + __expf(-(pr[0] + pr[1] + pr[2] + pr[3] + gbs0)));
+          const float gbv = 1.f / (1.f + __expf(-(pr[4] + pr[5] + pr[6] + pr[7] + gbs1)));
+          gsum = ga * (gbv * gc - 1.f) + 2.f;
         }
         gate[i] = gsum;
       }
@@ -243,9 +261,19 @@ __global__ __launch_bounds__(256) void wavlm_attn_kernel(int L, int H, const bf1
     f32x4 s[16];
 #pragma unroll
     for (int ct = 0; ct < 16; ++ct) s[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+    bf16x8 qa[2];
+    {
+      const int qrow = rb * 16 + (lane & 15);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        qa[kk] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+        if (qrow < L)
+          qa[kk] = *reinterpret_cast<const bf16x8*>(qkv + ((long)b * L + qrow) * ldqkv + h * ADH + kk * 32 + (lane >> 4) * 8);
+      }
+    }
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      const bf16x8 a = *reinterpret_cast<const bf16x8*>(&Qs[(rb * 16 + (lane & 15)) * APAD + kk * 32 + (lane >> 4) * 8]);
+      const bf16x8 a = qa[kk];
 #pragma unroll
       for (int ct = 0; ct < 16; ++ct) {
         if (ct < NT) {
@@ -333,7 +361,7 @@ MER_API int mer_wavlm_attention(int B, int L, int H, const void* qkv, long ldqkv
                                 void* stream) {
   if (L > 256 || L <= 0) return (int)hipErrorInvalidValue;
   const int LP = (L + 15) / 16 * 16;
-  const size_t lds = sizeof(bf16_t) * ((size_t)2 * LP * APAD + (size_t)ADH * (LP + 8) + 4 * 16 * (LP + 8)) +
+  const size_t lds = sizeof(bf16_t) * ((size_t)LP * APAD + (size_t)ADH * (LP + 8) + 4 * 16 * (LP + 8)) +
                      sizeof(float) * (LP + 2 * L);
   hipLaunchKernelGGL(wavlm_attn_kernel, dim3(B * H), dim3(256), lds, (hipStream_t)stream, L, H, (const bf16_t*)qkv,
                      ldqkv, (const bf16_t*)x, ldx, gate_w, gate_b, gate_const, rel_emb, bucket, (bf16_t*)out, ldo,

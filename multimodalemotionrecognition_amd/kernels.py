@@ -303,7 +303,7 @@ def cast_bf16(x, y):
     LIB("mer_cast_bf16", x.numel(), x.data_ptr(), y.data_ptr(), stream_ptr())
 
 
-BN_STAT_PARTS = 256  # MER_BN_STAT_PARTS (include/mer.h)
+BN_STAT_PARTS = 64  # MER_BN_STAT_PARTS (include/mer.h)
 
 
 def bn_stats_buffer(C, device):

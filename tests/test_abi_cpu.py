@@ -69,3 +69,13 @@ def test_unknown_mode_raises():
     m = FusionModel(StubAudio(), StubVideo(), num_classes=8, mode="bogus")
     with pytest.raises((ValueError, RuntimeError)):
         m(torch.zeros(2, 8, 512, 1, 1), torch.zeros(2, 64, 768))
+
+
+def test_bn_stat_parts_matches_header():
+    import re
+
+    from multimodalemotionrecognition_amd import kernels as K
+    from multimodalemotionrecognition_amd._lib import _HEADER
+
+    m = re.search(r"#define\s+MER_BN_STAT_PARTS\s+(\d+)", _HEADER.read_text())
+    assert m and int(m.group(1)) == K.BN_STAT_PARTS
