@@ -156,9 +156,10 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs g) {
 // glds writes lane-linear (base + 16*lane), so the XOR goes on each lane's SOURCE address and on
 // the fragment read (rule 21: both sides).  Rows past M/N are clamped to the last valid row (their
 // outputs are discarded); K is a multiple of 64, so no K tail.
-template <int BM_, int BN_, int WM_, int WN_>
+template <int BM_, int BN_, int WM_, int WN_, int STAGES_ = 2>
 struct PipeCfg {
   static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_;       // tile, waves along M / N
+  static constexpr int STAGES = STAGES_;                            // LDS ring depth (K-tiles)
   static constexpr int WAVES = WM * WN, NT = 64 * WAVES;
   static constexpr int TM = BM / WM, TN = BN / WN;                  // per-wave output
   static constexpr int FM = TM / 16, FN = TN / 16;                  // 16x16 fragments per wave
@@ -168,6 +169,21 @@ struct PipeCfg {
 };
 
 __device__ __forceinline__ int swz_chunk(int row, int c) { return c ^ ((row >> 1) & 7); }
+
+// s_waitcnt with only vmcnt constrained (gfx9 encoding: vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8] | vmcnt_hi[15:14])
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+}
+// wait until at most n (runtime, 0..3) tiles of G glds each are still in flight
+template <int G>
+__device__ __forceinline__ void wait_tiles_in_flight(int n) {
+  if (n <= 0) wait_vmcnt<0>();
+  else if (n == 1) wait_vmcnt<G>();
+  else if (n == 2) wait_vmcnt<2 * G>();
+  else wait_vmcnt<3 * G>();
+}
 
 __device__ __attribute__((aligned(16))) uint32_t mer_gemm_zero16[4] = {0u, 0u, 0u, 0u};
 
@@ -242,13 +258,22 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_pipe_kernel(GemmArgs g) {
   // fragment read offsets (elements) inside one operand image, per k-step s: row*64 + phys_chunk*8
   const int fr = lane & 15, fq = lane >> 4;
   const int nk = g.K / 64;
-  stage(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+  constexpr int S = CF::STAGES, G = CF::IA + CF::IB;
+  static_assert(S >= 2 && S <= 4 && (S - 2) * G < 64, "ring depth");
+  // Ring of S LDS buffers: tiles kt+1 .. kt+S-2 stay in flight (counted vmcnt) across the barrier
+  // that publishes tile kt; the barrier also retires every wave's reads of tile kt-1, whose buffer
+  // the tile kt+S-1 DMA then reuses.  Raw s_barrier: __syncthreads() would drain vmcnt to 0.
+#pragma unroll
+  for (int p = 0; p < S - 1; ++p)
+    if (p < nk) stage(p, p * 64);
   for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) stage(cur ^ 1, (kt + 1) * 64);
-    const bf16_t* la = smem + cur * CF::BUF;
+    const int ahead = (nk - 1 - kt) < (S - 2) ? (nk - 1 - kt) : (S - 2);
+    wait_tiles_in_flight<G>(ahead);
+    __builtin_amdgcn_s_waitcnt((15) | (7 << 4) | (0 << 8) | (3 << 14));  // lgkmcnt(0) only
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (kt + S - 1 < nk) stage((kt + S - 1) % S, (kt + S - 1) * 64);
+    const bf16_t* la = smem + (kt % S) * CF::BUF;
     const bf16_t* lb = la + CF::BM * 64;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -271,8 +296,6 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_pipe_kernel(GemmArgs g) {
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
       __builtin_amdgcn_s_setprio(0);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
   }
 
   TOUT* C = reinterpret_cast<TOUT*>(g.C) + (long)z * g.c_zoff;
@@ -298,11 +321,15 @@ using CfgL = PipeCfg<256, 256, 2, 4>;  // 8 waves, 128x64 per wave, 128 KiB LDS
 using CfgM = PipeCfg<256, 128, 4, 2>;  // 8 waves, 64x64 per wave, 96 KiB LDS
 using CfgS = PipeCfg<128, 128, 2, 2>;  // 4 waves, 64x64 per wave, 64 KiB LDS
 using CfgP = PipeCfg<128, 64, 2, 2>;   // 4 waves, 64x32 per wave, 48 KiB LDS (pos-conv: 48 columns per group)
+using CfgS3 = PipeCfg<128, 128, 2, 2, 3>;  // 3-deep ring, 96 KiB LDS (1 block / CU)
+using CfgS4 = PipeCfg<128, 128, 2, 2, 4>;  // 4-deep ring, 128 KiB LDS
+using CfgM3 = PipeCfg<256, 128, 4, 2, 3>;  // 8 waves, 3-deep ring, 144 KiB LDS
+using CfgT3 = PipeCfg<128, 64, 2, 2, 3>;   // 128x64 tiles, 3-deep ring, 72 KiB LDS (2 blocks / CU)
 
 template <class CF, typename TOUT, int AMODE>
 int launch_pipe_t(const GemmArgs& g, int groups, hipStream_t st) {
   const long tiles = (long)((g.N + CF::BN - 1) / CF::BN) * ((g.M + CF::BM - 1) / CF::BM);
-  const size_t lds = 2 * CF::BUF * sizeof(bf16_t);
+  const size_t lds = CF::STAGES * CF::BUF * sizeof(bf16_t);
   if (hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_pipe_kernel<CF, TOUT, AMODE>),
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return (int)hipErrorInvalidConfiguration;
@@ -347,7 +374,7 @@ MER_API int mer_gemm_bf16_ex(int M, int N, int K, const void* A, long a_gstride,
                              const void* W, long ldw, void* C, int c_dtype, long ldc, const float* bias, const void* R,
                              long ldr, int act, int variant, void* stream) {
   if (M <= 0 || N <= 0) return 0;
-  if (variant < -1 || variant > 3) return (int)hipErrorInvalidValue;
+  if (variant < -1 || variant > 7) return (int)hipErrorInvalidValue;
   if (K % 8 != 0 || a_rpg <= 0 || (a_rstride % 8) != 0 || (a_gstride % 8) != 0 || (ldw % 8) != 0)
     return (int)hipErrorInvalidValue;
   if ((((uintptr_t)A) | ((uintptr_t)W)) & 15) return (int)hipErrorInvalidValue;
@@ -364,6 +391,10 @@ MER_API int mer_gemm_bf16_ex(int M, int N, int K, const void* A, long a_gstride,
     case 1: return launch_pipe<CfgL>(g, c_dtype, st);
     case 2: return launch_pipe<CfgM>(g, c_dtype, st);
     case 3: return launch_pipe<CfgS>(g, c_dtype, st);
+    case 4: return launch_pipe<CfgS3>(g, c_dtype, st);
+    case 5: return launch_pipe<CfgS4>(g, c_dtype, st);
+    case 6: return launch_pipe<CfgM3>(g, c_dtype, st);
+    case 7: return launch_pipe<CfgT3>(g, c_dtype, st);
     default: return launch<0>(g, c_dtype, 1, st);
   }
 }

@@ -30,7 +30,7 @@ def main():
         w = (torch.rand(N, Kd, device="cuda") * 2 - 1).bfloat16()
         outs = {}
         for odt in (torch.bfloat16,):
-            for v in (0, 1, 2, 3):
+            for v in (0, 1, 2, 3, 4, 5, 6, 7):
                 out = torch.empty(M, N, device="cuda", dtype=odt)
                 kw = dict(M=M, K=Kd, rows=rows) if rows else {}
                 for _ in range(3):

@@ -23,6 +23,7 @@ for step in "$@"; do
     prof) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python $OLDPWD/bench.py --steps 5 --warmup 2 --no-cpu-baseline > $OUT/prof.log 2>&1); echo "== prof rc=$?" ;;
     pmcg) bash tools/pmc_gemm.sh $TAG/pmcg ;;
     pmc) bash tools/gpu_pmc.sh $TAG/pmc ;;
+    tprof) run torch_prof 300 python tools/torch_prof.py; cat $OUT/torch_prof.log ;;
   esac
 done
 echo SESSION_DONE
