@@ -325,6 +325,10 @@ using CfgS3 = PipeCfg<128, 128, 2, 2, 3>;  // 3-deep ring, 96 KiB LDS (1 block /
 using CfgS4 = PipeCfg<128, 128, 2, 2, 4>;  // 4-deep ring, 128 KiB LDS
 using CfgM3 = PipeCfg<256, 128, 4, 2, 3>;  // 8 waves, 3-deep ring, 144 KiB LDS
 using CfgT3 = PipeCfg<128, 64, 2, 2, 3>;   // 128x64 tiles, 3-deep ring, 72 KiB LDS (2 blocks / CU)
+using CfgT2 = PipeCfg<128, 64, 2, 2, 2>;   // 128x64 tiles, 2-deep ring, 48 KiB LDS (3 blocks / CU)
+using CfgW2 = PipeCfg<128, 128, 2, 4, 2>;  // 8 waves (64x32 each), 2-deep, 64 KiB LDS (2 blocks / CU)
+using CfgW3 = PipeCfg<128, 128, 2, 4, 3>;  // 8 waves, 3-deep, 96 KiB LDS
+using CfgV3 = PipeCfg<128, 64, 4, 1, 3>;   // 4 waves as 4x1 (32x64 each), 3-deep, 72 KiB LDS
 
 template <class CF, typename TOUT, int AMODE>
 int launch_pipe_t(const GemmArgs& g, int groups, hipStream_t st) {
@@ -374,7 +378,7 @@ MER_API int mer_gemm_bf16_ex(int M, int N, int K, const void* A, long a_gstride,
                              const void* W, long ldw, void* C, int c_dtype, long ldc, const float* bias, const void* R,
                              long ldr, int act, int variant, void* stream) {
   if (M <= 0 || N <= 0) return 0;
-  if (variant < -1 || variant > 7) return (int)hipErrorInvalidValue;
+  if (variant < -1 || variant > 11) return (int)hipErrorInvalidValue;
   if (K % 8 != 0 || a_rpg <= 0 || (a_rstride % 8) != 0 || (a_gstride % 8) != 0 || (ldw % 8) != 0)
     return (int)hipErrorInvalidValue;
   if ((((uintptr_t)A) | ((uintptr_t)W)) & 15) return (int)hipErrorInvalidValue;
@@ -395,6 +399,10 @@ MER_API int mer_gemm_bf16_ex(int M, int N, int K, const void* A, long a_gstride,
     case 5: return launch_pipe<CfgS4>(g, c_dtype, st);
     case 6: return launch_pipe<CfgM3>(g, c_dtype, st);
     case 7: return launch_pipe<CfgT3>(g, c_dtype, st);
+    case 8: return launch_pipe<CfgT2>(g, c_dtype, st);
+    case 9: return launch_pipe<CfgW2>(g, c_dtype, st);
+    case 10: return launch_pipe<CfgW3>(g, c_dtype, st);
+    case 11: return launch_pipe<CfgV3>(g, c_dtype, st);
     default: return launch<0>(g, c_dtype, 1, st);
   }
 }

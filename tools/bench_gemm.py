@@ -18,6 +18,10 @@ SHAPES = {
 }
 
 
+VARIANTS = [int(v) for v in next((a.split("=")[1] for a in sys.argv if a.startswith("--variants=")),
+                                  "0,1,2,3,4,5,6,7,8,9,10,11").split(",")]
+
+
 def main():
     torch.manual_seed(0)
     quick = "--quick" in sys.argv  # profiling: fewer shapes / reps
@@ -30,7 +34,7 @@ def main():
         w = (torch.rand(N, Kd, device="cuda") * 2 - 1).bfloat16()
         outs = {}
         for odt in (torch.bfloat16,):
-            for v in (0, 1, 2, 3, 4, 5, 6, 7):
+            for v in VARIANTS:
                 out = torch.empty(M, N, device="cuda", dtype=odt)
                 kw = dict(M=M, K=Kd, rows=rows) if rows else {}
                 for _ in range(3):
