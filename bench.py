@@ -38,8 +38,9 @@ PEAK_HBM_GBS = 8000.0       # HBM3E spec
 # Dominant kernel (largest share of step time in profiles/): the WavLM feature-extractor conv1 as an
 # implicit GEMM: M = B*4799 output frames, N = 512 channels, K = 3 taps * 512.
 PROBE = ("gemm_bf16", (BATCH * 4799, 512, 1536))
-# the kernel mer_gemm_bf16 dispatches for that shape (gemm_bf16.hip pick_variant: 1,200 tiles of 256x256)
-PROBE_KERNEL = "gemm_pipe_kernel<PipeCfg<256,256,2,4>, bf16>"
+# the kernel mer_gemm_bf16 dispatches for that shape (gemm_bf16.hip pick_variant: 1,200 tiles of 256x256,
+# 16 waves each)
+PROBE_KERNEL = "gemm_pipe_kernel<PipeCfg<256,256,4,4,2>, bf16>"
 PMC_FILE = ROOT / "profiles" / "pmc_traffic.json"
 
 

@@ -132,7 +132,8 @@ int mer_gemm_bf16(int M, int N, int K, const void* A, long a_gstride, long a_rst
 /* mer_gemm_bf16 with an explicit kernel variant: -1 auto (what mer_gemm_bf16 does), 0 the 128x128
  * register-staged kernel (any K % 8 == 0), 1/2/3 the global_load_lds pipelined kernel with 256x256 /
  * 256x128 / 128x128 tiles and a 2-deep LDS ring, 4/5 128x128 with a 3/4-deep ring, 6 256x128 3-deep,
- * 7 128x64 3-deep, 8 128x64 2-deep, 9/10 128x128 with 8 waves 2/3-deep, 11 128x64 as 4x1 waves 3-deep
+ * 7 128x64 3-deep, 8 128x64 2-deep, 9/10 128x128 with 8 waves 2/3-deep, 11 128x64 as 4x1 waves 3-deep,
+ * 12 256x128 with 16 waves, 13 256x256 with 16 waves
  * (K % 64 == 0; otherwise variant 0 runs). */
 int mer_gemm_bf16_ex(int M, int N, int K, const void* A, long a_gstride, long a_rstride, int a_rpg, const void* W,
                      long ldw, void* C, int c_dtype, long ldc, const float* bias, const void* R, long ldr, int act,
@@ -185,7 +186,7 @@ int mer_conv_fwd(int N, int H, int W, int C, int K, int R, int S, int stride, in
                  const void* w_packed, void* y, float* stats, void* stream);
 
 /* mer_conv_fwd / mer_conv_dgrad with an explicit kernel: -1 auto, 0 the register-staged implicit GEMM,
- * 1 the global_load_lds pipelined one (zero padding served from a zero chunk). */
+ * 1 the global_load_lds pipelined one (zero padding served from a zero chunk), 2 the same with 8-wave tiles. */
 int mer_conv_fwd_ex(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, const void* x,
                     const void* w_packed, void* y, float* stats, int variant, void* stream);
 

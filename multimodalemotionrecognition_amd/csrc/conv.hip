@@ -414,10 +414,12 @@ __device__ __forceinline__ ParClass par_class(const ConvGeom& g, int cls) {
   return c;
 }
 
-template <bool DGRAD, bool PAR, int BM_, int BN_>
-__global__ __launch_bounds__(256, 2) void conv_pipe_kernel(ConvGeom g) {
-  constexpr int IA = BM_ / 32, IB = BN_ / 32;           // glds per wave per K-tile (8 rows each, 4 waves)
-  constexpr int TM = BM_ / 2, TN = BN_ / 2, FM = TM / 16, FN = TN / 16;
+template <bool DGRAD, bool PAR, int BM_, int BN_, int WM = 2, int WN = 2>
+__global__ __launch_bounds__(64 * WM * WN, 2) void conv_pipe_kernel(ConvGeom g) {
+  constexpr int WAVES = WM * WN;
+  constexpr int IA = BM_ / 8 / WAVES, IB = BN_ / 8 / WAVES;  // glds per wave per K-tile (8 rows each)
+  static_assert(IA * 8 * WAVES == BM_ && IB * 8 * WAVES == BN_, "tile rows must split into 8-row glds pieces");
+  constexpr int TM = BM_ / WM, TN = BN_ / WN, FM = TM / 16, FN = TN / 16;
   constexpr int BUF = (BM_ + BN_) * 64;
   extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
@@ -440,7 +442,7 @@ __global__ __launch_bounds__(256, 2) void conv_pipe_kernel(ConvGeom g) {
   int tx, ty;
   xcd_tile(blockIdx.x, nx, nx * ny, tx, ty);
   const int m0 = ty * BM_, n0 = tx * BN_;
-  const int wr = w >> 1, wc = w & 1;
+  const int wr = w / WN, wc = w % WN;
 
   int an[IA], aoh[IA], aow[IA], acl[IA];
   bool aok[IA];
@@ -606,26 +608,34 @@ __global__ __launch_bounds__(256, 2) void conv_pipe_kernel(ConvGeom g) {
       ps[j][1] = s2;
       ps[j][2] = s3;
     }
+    // the WM waves sharing a column meet in LDS (staging buffers idle now): red[wr][col][3]
     float* red = reinterpret_cast<float*>(smem);
     __syncthreads();
-    if (wr == 1 && fq == 0)
+    if (wr > 0 && fq == 0)
 #pragma unroll
       for (int j = 0; j < FN; ++j)
 #pragma unroll
-        for (int q = 0; q < 3; ++q) red[((wc * FN + j) * 16 + fr) * 3 + q] = ps[j][q];
+        for (int q = 0; q < 3; ++q) red[((wr * WN + wc) * FN * 16 + j * 16 + fr) * 3 + q] = ps[j][q];
     __syncthreads();
     if (wr == 0 && fq == 0) {
       const long slab = (long)(ty % MER_BN_STAT_PARTS) * g.Ncols * 2;
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
         const int col = n0 + wc * TN + j * 16 + fr;
+        float t0 = ps[j][0], t1 = ps[j][1], t2 = ps[j][2];
+#pragma unroll
+        for (int q = 1; q < WM; ++q) {
+          const float* o = red + ((q * WN + wc) * FN * 16 + j * 16 + fr) * 3;
+          t0 += o[0];
+          t1 += o[1];
+          t2 += o[2];
+        }
         if (col < g.Ncols) {
-          const float* o = red + ((wc * FN + j) * 16 + fr) * 3;
-          atomicAdd(g.bnr_red + slab + 2 * col, ps[j][0] + o[0]);
-          atomicAdd(g.bnr_red + slab + 2 * col + 1, ps[j][1] + o[1]);
+          atomicAdd(g.bnr_red + slab + 2 * col, t0);
+          atomicAdd(g.bnr_red + slab + 2 * col + 1, t1);
           if (g.bnr_red2) {
-            atomicAdd(g.bnr_red2 + slab + 2 * col, ps[j][0] + o[0]);
-            atomicAdd(g.bnr_red2 + slab + 2 * col + 1, ps[j][2] + o[2]);
+            atomicAdd(g.bnr_red2 + slab + 2 * col, t0);
+            atomicAdd(g.bnr_red2 + slab + 2 * col + 1, t2);
           }
         }
       }
@@ -654,15 +664,15 @@ __global__ __launch_bounds__(256, 2) void conv_pipe_kernel(ConvGeom g) {
       part[j][0] = csum;
       part[j][1] = csq;
     }
-    // the two M-waves of a column pair meet in LDS (the staging buffers are idle now); one striped
+    // the WM waves sharing a column meet in LDS (the staging buffers are idle now); one striped
     // atomic per (block, column): slab row ty % MER_BN_STAT_PARTS keeps same-address atomics rare
     float* red = reinterpret_cast<float*>(smem);
     __syncthreads();
-    if (wr == 1 && fq == 0)
+    if (wr > 0 && fq == 0)
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
-        red[(wc * FN + j) * 32 + fr * 2] = part[j][0];
-        red[(wc * FN + j) * 32 + fr * 2 + 1] = part[j][1];
+        red[((wr * WN + wc) * FN * 16 + j * 16 + fr) * 2] = part[j][0];
+        red[((wr * WN + wc) * FN * 16 + j * 16 + fr) * 2 + 1] = part[j][1];
       }
     __syncthreads();
     if (wr == 0 && fq == 0) {
@@ -670,35 +680,50 @@ __global__ __launch_bounds__(256, 2) void conv_pipe_kernel(ConvGeom g) {
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
         const int col = n0 + wc * TN + j * 16 + fr;
+        float t0 = part[j][0], t1 = part[j][1];
+#pragma unroll
+        for (int q = 1; q < WM; ++q) {
+          t0 += red[((q * WN + wc) * FN * 16 + j * 16 + fr) * 2];
+          t1 += red[((q * WN + wc) * FN * 16 + j * 16 + fr) * 2 + 1];
+        }
         if (col < g.Ncols) {
-          atomicAdd(slab + 2 * col, part[j][0] + red[(wc * FN + j) * 32 + fr * 2]);
-          atomicAdd(slab + 2 * col + 1, part[j][1] + red[(wc * FN + j) * 32 + fr * 2 + 1]);
+          atomicAdd(slab + 2 * col, t0);
+          atomicAdd(slab + 2 * col + 1, t1);
         }
       }
     }
   }
 }
 
-template <bool DGRAD, bool PAR, int BM_, int BN_>
+template <bool DGRAD, bool PAR, int BM_, int BN_, int WM = 2, int WN = 2>
 int launch_conv_pipe_t(ConvGeom& g, hipStream_t st) {
   // PAR: grid.x covers the largest parity class (ph = pw = 0), grid.y = the 4 classes
   const int Mg = PAR ? g.N * ((g.OH + 1) / 2) * ((g.OW + 1) / 2) : g.N * g.OH * g.OW;
   const long tiles = (long)((Mg + BM_ - 1) / BM_) * ((g.Ncols + BN_ - 1) / BN_);
   const size_t lds = 2 * (BM_ + BN_) * 64 * sizeof(bf16_t);
-  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_pipe_kernel<DGRAD, PAR, BM_, BN_>),
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_pipe_kernel<DGRAD, PAR, BM_, BN_, WM, WN>),
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return (int)hipErrorInvalidConfiguration;
-  hipLaunchKernelGGL((conv_pipe_kernel<DGRAD, PAR, BM_, BN_>), dim3((unsigned)tiles, PAR ? 4 : 1), dim3(256), lds, st,
-                     g);
+  hipLaunchKernelGGL((conv_pipe_kernel<DGRAD, PAR, BM_, BN_, WM, WN>), dim3((unsigned)tiles, PAR ? 4 : 1),
+                     dim3(64 * WM * WN), lds, st, g);
   return (int)hipGetLastError();
 }
 
+// variant 1: 4-wave tiles; variant 2: 8-wave tiles (more waves per CU hide the DMA latency of the
+// 2-deep pipeline, cf. gemm_bf16.hip pick_variant)
 template <bool DGRAD, bool PAR>
-int launch_conv_pipe(ConvGeom& g, hipStream_t st) {
+int launch_conv_pipe(ConvGeom& g, hipStream_t st, int variant) {
   const int M = PAR ? g.N * g.OH * g.OW / 4 : g.N * g.OH * g.OW;
   const int bn = g.Ncols <= 64 ? 64 : 128;
   const long tiles128 = (long)((M + 127) / 128) * ((g.Ncols + bn - 1) / bn) * (PAR ? 4 : 1);
   const bool small_m = tiles128 < 384;
+  if (variant == 2) {
+    if (bn == 64)
+      return small_m ? launch_conv_pipe_t<DGRAD, PAR, 64, 64, 2, 2>(g, st)
+                     : launch_conv_pipe_t<DGRAD, PAR, 128, 64, 4, 2>(g, st);
+    return small_m ? launch_conv_pipe_t<DGRAD, PAR, 64, 128, 2, 4>(g, st)
+                   : launch_conv_pipe_t<DGRAD, PAR, 128, 128, 2, 4>(g, st);
+  }
   if (bn == 64)
     return small_m ? launch_conv_pipe_t<DGRAD, PAR, 64, 64>(g, st) : launch_conv_pipe_t<DGRAD, PAR, 128, 64>(g, st);
   return small_m ? launch_conv_pipe_t<DGRAD, PAR, 64, 128>(g, st) : launch_conv_pipe_t<DGRAD, PAR, 128, 128>(g, st);
@@ -736,7 +761,7 @@ MER_API int mer_conv_fwd(int N, int H, int W, int C, int K, int R, int S, int st
 
 MER_API int mer_conv_fwd_ex(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, const void* x,
                             const void* w_packed, void* y, float* stats, int variant, void* stream) {
-  if (C % 8 || variant < -1 || variant > 1) return (int)hipErrorInvalidValue;
+  if (C % 8 || variant < -1 || variant > 2) return (int)hipErrorInvalidValue;
   ConvGeom g{};
   g.N = N; g.IH = H; g.IW = W; g.IC = C;
   g.OH = (H + 2 * pad - R) / stride + 1; g.OW = (W + 2 * pad - S) / stride + 1;
@@ -744,7 +769,7 @@ MER_API int mer_conv_fwd_ex(int N, int H, int W, int C, int K, int R, int S, int
   g.Ncols = K; g.Kred = R * S * C;
   g.X = (const bf16_t*)x; g.Wt = (const bf16_t*)w_packed; g.Y = (bf16_t*)y; g.ldy = K; g.stats = stats;
   if (variant == 0) return launch_conv<false>(g, (hipStream_t)stream);
-  return launch_conv_pipe<false, false>(g, (hipStream_t)stream);
+  return launch_conv_pipe<false, false>(g, (hipStream_t)stream, variant);
 }
 
 MER_API int mer_conv_dgrad(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, const void* dy,
@@ -764,7 +789,7 @@ MER_API int mer_conv_dgrad_bnr(int N, int H, int W, int C, int K, int R, int S, 
                                const void* wt_packed, void* dx, const void* residual, const void* residual_mask,
                                const void* bn_mask, const void* bn_x, const float* bn_ms, float* bn_red,
                                const void* bn_x2, const float* bn_ms2, float* bn_red2, int variant, void* stream) {
-  if (K % 8 || C % 8 || variant < -1 || variant > 1) return (int)hipErrorInvalidValue;
+  if (K % 8 || C % 8 || variant < -1 || variant > 2) return (int)hipErrorInvalidValue;
   if (bn_red && (!bn_mask || !bn_x || !bn_ms || (bn_x2 && (!bn_ms2 || !bn_red2)))) return (int)hipErrorInvalidValue;
   if (bn_red && (variant == 0 || stride > 2)) return (int)hipErrorInvalidValue;  // fused only in the pipelined kernel
   ConvGeom g{};
@@ -777,8 +802,8 @@ MER_API int mer_conv_dgrad_bnr(int N, int H, int W, int C, int K, int R, int S, 
   g.bnr_mask = (const bf16_t*)bn_mask; g.bnr_x = (const bf16_t*)bn_x; g.bnr_ms = bn_ms; g.bnr_red = bn_red;
   g.bnr_x2 = (const bf16_t*)bn_x2; g.bnr_ms2 = bn_ms2; g.bnr_red2 = bn_red2;
   if (variant == 0 || stride > 2) return launch_conv<true>(g, (hipStream_t)stream);
-  if (stride == 2) return launch_conv_pipe<true, true>(g, (hipStream_t)stream);
-  return launch_conv_pipe<true, false>(g, (hipStream_t)stream);
+  if (stride == 2) return launch_conv_pipe<true, true>(g, (hipStream_t)stream, variant);
+  return launch_conv_pipe<true, false>(g, (hipStream_t)stream, variant);
 }
 
 MER_API int mer_conv_wgrad(int N, int H, int W, int C, int Creal, int K, int R, int S, int stride, int pad,

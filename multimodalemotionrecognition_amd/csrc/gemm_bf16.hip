@@ -329,6 +329,8 @@ using CfgT2 = PipeCfg<128, 64, 2, 2, 2>;   // 128x64 tiles, 2-deep ring, 48 KiB 
 using CfgW2 = PipeCfg<128, 128, 2, 4, 2>;  // 8 waves (64x32 each), 2-deep, 64 KiB LDS (2 blocks / CU)
 using CfgW3 = PipeCfg<128, 128, 2, 4, 3>;  // 8 waves, 3-deep, 96 KiB LDS
 using CfgV3 = PipeCfg<128, 64, 4, 1, 3>;   // 4 waves as 4x1 (32x64 each), 3-deep, 72 KiB LDS
+using CfgX2 = PipeCfg<256, 128, 4, 4, 2>;  // 16 waves (64x32 each), 2-deep, 96 KiB LDS (1 block / CU)
+using CfgY2 = PipeCfg<256, 256, 4, 4, 2>;  // 16 waves (64x64 each), 2-deep, 128 KiB LDS
 
 template <class CF, typename TOUT, int AMODE>
 int launch_pipe_t(const GemmArgs& g, int groups, hipStream_t st) {
@@ -347,12 +349,15 @@ int launch_pipe(const GemmArgs& g, int out_dtype, hipStream_t st, int groups = 1
                                : launch_pipe_t<CF, float, AMODE>(g, groups, st);
 }
 
-// Tile choice (measured on the WavLM shapes at B=32, tools/bench_gemm.py): the 256x256 tile only pays
-// when there are several waves of tiles (conv1: 1200 tiles); otherwise the 128x128 glds tile (2 blocks
-// per CU) wins or ties on every encoder GEMM.
-int pick_variant(int M, int N) {
+// Tile choice (tools/bench_gemm.py on the B=32 WavLM shapes, MI355X): occupancy (waves per CU) is what
+// hides the DMA latency of this 2-deep pipeline, so the 16-wave 256x256 tile wins wherever its grid covers
+// most of the 256 CUs (conv1/conv2 as GEMMs, QKV, FFN-up: 0.80 / 0.82 / 0.49 / 0.64 PF); the 768-column
+// GEMMs have too few such tiles: FFN-down (K = 3072) runs 128x64 tiles with a 3-deep ring, the output
+// projection 128x128 tiles with 8 waves.
+int pick_variant(int M, int N, int K) {
   const long tl = (long)((M + 255) / 256) * ((N + 255) / 256);
-  return tl >= 1024 ? 1 : 3;
+  if (tl >= 160) return 13;
+  return K >= 2048 ? 7 : 9;
 }
 
 template <int AMODE>
@@ -378,7 +383,7 @@ MER_API int mer_gemm_bf16_ex(int M, int N, int K, const void* A, long a_gstride,
                              const void* W, long ldw, void* C, int c_dtype, long ldc, const float* bias, const void* R,
                              long ldr, int act, int variant, void* stream) {
   if (M <= 0 || N <= 0) return 0;
-  if (variant < -1 || variant > 11) return (int)hipErrorInvalidValue;
+  if (variant < -1 || variant > 13) return (int)hipErrorInvalidValue;
   if (K % 8 != 0 || a_rpg <= 0 || (a_rstride % 8) != 0 || (a_gstride % 8) != 0 || (ldw % 8) != 0)
     return (int)hipErrorInvalidValue;
   if ((((uintptr_t)A) | ((uintptr_t)W)) & 15) return (int)hipErrorInvalidValue;
@@ -390,7 +395,7 @@ MER_API int mer_gemm_bf16_ex(int M, int N, int K, const void* A, long a_gstride,
   g.bias = bias; g.R = (const bf16_t*)R; g.ldr = ldr; g.act = act;
   const hipStream_t st = (hipStream_t)stream;
   if (K % 64 != 0) variant = 0;
-  if (variant == -1) variant = pick_variant(M, N);
+  if (variant == -1) variant = pick_variant(M, N, K);
   switch (variant) {
     case 1: return launch_pipe<CfgL>(g, c_dtype, st);
     case 2: return launch_pipe<CfgM>(g, c_dtype, st);
@@ -403,6 +408,8 @@ MER_API int mer_gemm_bf16_ex(int M, int N, int K, const void* A, long a_gstride,
     case 9: return launch_pipe<CfgW2>(g, c_dtype, st);
     case 10: return launch_pipe<CfgW3>(g, c_dtype, st);
     case 11: return launch_pipe<CfgV3>(g, c_dtype, st);
+    case 12: return launch_pipe<CfgX2>(g, c_dtype, st);
+    case 13: return launch_pipe<CfgY2>(g, c_dtype, st);
     default: return launch<0>(g, c_dtype, 1, st);
   }
 }
