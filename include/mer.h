@@ -186,7 +186,8 @@ int mer_conv_fwd(int N, int H, int W, int C, int K, int R, int S, int stride, in
                  const void* w_packed, void* y, float* stats, void* stream);
 
 /* mer_conv_fwd / mer_conv_dgrad with an explicit kernel: -1 auto, 0 the register-staged implicit GEMM,
- * 1 the global_load_lds pipelined one (zero padding served from a zero chunk), 2 the same with 8-wave tiles. */
+ * 1 the global_load_lds pipelined one (zero padding served from a zero chunk), 2 the same with 8-wave tiles
+ * (the default), 3 with 256-row tiles (8 or 16 waves) on large-M layers. */
 int mer_conv_fwd_ex(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, const void* x,
                     const void* w_packed, void* y, float* stats, int variant, void* stream);
 

@@ -709,15 +709,20 @@ int launch_conv_pipe_t(ConvGeom& g, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
-// variant 1: 4-wave tiles; variant 2: 8-wave tiles (more waves per CU hide the DMA latency of the
-// 2-deep pipeline, cf. gemm_bf16.hip pick_variant)
+// variant 1: 4-wave tiles; variant 2 (default): 8-wave tiles -- more waves per CU hide the DMA latency of
+// the 2-deep pipeline (tools/bench_conv.py: 1.1-1.3x on every ResNet layer), cf. gemm_bf16.hip
+// pick_variant; variant 3: 16-wave 256-row tiles on the large-M layers.
 template <bool DGRAD, bool PAR>
 int launch_conv_pipe(ConvGeom& g, hipStream_t st, int variant) {
   const int M = PAR ? g.N * g.OH * g.OW / 4 : g.N * g.OH * g.OW;
   const int bn = g.Ncols <= 64 ? 64 : 128;
   const long tiles128 = (long)((M + 127) / 128) * ((g.Ncols + bn - 1) / bn) * (PAR ? 4 : 1);
   const bool small_m = tiles128 < 384;
-  if (variant == 2) {
+  if (variant == 3 && !small_m) {  // 256-row tiles (8 / 16 waves) for the large-M layers
+    if (bn == 64) return launch_conv_pipe_t<DGRAD, PAR, 256, 64, 4, 2>(g, st);
+    return launch_conv_pipe_t<DGRAD, PAR, 256, 128, 4, 4>(g, st);
+  }
+  if (variant >= 2) {
     if (bn == 64)
       return small_m ? launch_conv_pipe_t<DGRAD, PAR, 64, 64, 2, 2>(g, st)
                      : launch_conv_pipe_t<DGRAD, PAR, 128, 64, 4, 2>(g, st);
@@ -761,7 +766,8 @@ MER_API int mer_conv_fwd(int N, int H, int W, int C, int K, int R, int S, int st
 
 MER_API int mer_conv_fwd_ex(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, const void* x,
                             const void* w_packed, void* y, float* stats, int variant, void* stream) {
-  if (C % 8 || variant < -1 || variant > 2) return (int)hipErrorInvalidValue;
+  if (C % 8 || variant < -1 || variant > 3) return (int)hipErrorInvalidValue;
+  if (variant == -1) variant = 2;
   ConvGeom g{};
   g.N = N; g.IH = H; g.IW = W; g.IC = C;
   g.OH = (H + 2 * pad - R) / stride + 1; g.OW = (W + 2 * pad - S) / stride + 1;
@@ -789,7 +795,8 @@ MER_API int mer_conv_dgrad_bnr(int N, int H, int W, int C, int K, int R, int S, 
                                const void* wt_packed, void* dx, const void* residual, const void* residual_mask,
                                const void* bn_mask, const void* bn_x, const float* bn_ms, float* bn_red,
                                const void* bn_x2, const float* bn_ms2, float* bn_red2, int variant, void* stream) {
-  if (K % 8 || C % 8 || variant < -1 || variant > 2) return (int)hipErrorInvalidValue;
+  if (K % 8 || C % 8 || variant < -1 || variant > 3) return (int)hipErrorInvalidValue;
+  if (variant == -1) variant = 2;
   if (bn_red && (!bn_mask || !bn_x || !bn_ms || (bn_x2 && (!bn_ms2 || !bn_red2)))) return (int)hipErrorInvalidValue;
   if (bn_red && (variant == 0 || stride > 2)) return (int)hipErrorInvalidValue;  // fused only in the pipelined kernel
   ConvGeom g{};

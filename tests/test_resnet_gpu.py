@@ -226,23 +226,23 @@ def test_conv_variants_bit_identical(N, H, C, Kc, R, stride, pad):
     wt = torch.empty(C, R * R * Kc, device="cuda", dtype=torch.bfloat16)
     K.pack_conv_weight(w, wt, C, True)
     ys, sts = [], []
-    for v in (0, 1, 2):
+    for v in (0, 1, 2, 3):
         y = torch.empty(N, Ho, Ho, Kc, device="cuda", dtype=torch.bfloat16)
         st = K.bn_stats_buffer(Kc, "cuda")
         K.conv_fwd(x, wp, y, st, R, R, stride, pad, variant=v)
         ys.append(y)
         sts.append(st.sum(0))
-    assert torch.equal(ys[0], ys[1]) and torch.equal(ys[0], ys[2])
-    assert torch.allclose(sts[0], sts[1], rtol=1e-5, atol=1e-3) and torch.allclose(sts[0], sts[2], rtol=1e-5, atol=1e-3)
+    assert all(torch.equal(ys[0], y) for y in ys[1:])
+    assert all(torch.allclose(sts[0], st, rtol=1e-5, atol=1e-3) for st in sts[1:])
     dy = torch.randn(N, Ho, Ho, Kc, device="cuda").bfloat16()
     res = torch.randn(N, H, H, C, device="cuda").bfloat16()
     mask = torch.randn(N, H, H, C, device="cuda").bfloat16()
     dxs = []
-    for v in (0, 1, 2):
+    for v in (0, 1, 2, 3):
         dx = torch.empty(N, H, H, C, device="cuda", dtype=torch.bfloat16)
         K.conv_dgrad(dy, wt, dx, R, R, stride, pad, residual=res, mask=mask, variant=v)
         dxs.append(dx)
-    assert torch.equal(dxs[0], dxs[1]) and torch.equal(dxs[0], dxs[2])
+    assert all(torch.equal(dxs[0], d) for d in dxs[1:])
 
 
 @pytest.mark.parametrize("stride,ds", [(1, False), (2, True)])
