@@ -216,6 +216,9 @@ int mer_partials_sum(int C, int parts, const float* in, float* out, void* stream
  * (splits*K*R*S*C floats), then a reduce pass sums the slabs into dw (deterministic, no atomics). */
 int mer_conv_wgrad(int N, int H, int W, int C, int Creal, int K, int R, int S, int stride, int pad, const void* x,
                    const void* dy, float* dw, int splits, float* workspace, void* stream);
+/* mer_conv_wgrad with an explicit kernel: -1 auto, 1 4-wave tiles, 2 8-wave tiles (the default). */
+int mer_conv_wgrad_ex(int N, int H, int W, int C, int Creal, int K, int R, int S, int stride, int pad, const void* x,
+                      const void* dy, float* dw, int splits, float* workspace, int variant, void* stream);
 
 /* NCHW fp32 frames -> NHWC bf16 with channels zero-padded to Cp (<= 16). */
 int mer_pack_input_nhwc(int N, int C, int H, int W, int Cp, const float* x, void* y, void* stream);

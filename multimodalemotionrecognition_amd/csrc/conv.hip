@@ -212,11 +212,13 @@ struct WgradGeom {
   int pix_per_split;
 };
 
-template <int BM_, int BN_>
-__global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradGeom g) {
+template <int BM_, int BN_, int WM = 2, int WN = 2>
+__global__ __launch_bounds__(64 * WM * WN, 2) void wgrad_kernel(WgradGeom g) {
+  constexpr int NT = 64 * WM * WN;
   constexpr int LDM = BM_ + 16, LDN = BN_ + 16;
-  constexpr int IT = BM_ / 32, JT = BN_ / 32;
-  constexpr int ACH = BM_ * 64 / 8 / 256, BCH = BN_ * 64 / 8 / 256;  // 16B chunks per thread
+  constexpr int IT = BM_ / WM / 16, JT = BN_ / WN / 16;
+  constexpr int ACH = BM_ * 64 / 8 / NT, BCH = BN_ * 64 / 8 / NT;  // 16B chunks per thread
+  static_assert(ACH * NT * 8 == BM_ * 64 && BCH * NT * 8 == BN_ * 64, "staging split");
   __shared__ __attribute__((aligned(16))) bf16_t lds[2][64 * LDM + 64 * LDN];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int Ntot = g.R * g.S * g.C;
@@ -226,7 +228,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradGeom g) {
   xcd_tile(blockIdx.x, wnx, wnx * wny, wtx, wty);
   const int m0 = wty * BM_, n0 = wtx * BN_;
   const int p_beg = blockIdx.z * g.pix_per_split, p_end = min(P, p_beg + g.pix_per_split);
-  const int wm = (w >> 1) * (BM_ / 2), wn = (w & 1) * (BN_ / 2);
+  const int wm = (w / WN) * (BM_ / WM), wn = (w % WN) * (BN_ / WN);
   constexpr int ACPR = BM_ / 8, BCPR = BN_ / 8;  // chunks per LDS row
 
   u32x4 ra[ACH], rb[BCH];
@@ -244,12 +246,12 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradGeom g) {
   auto gload = [&](int p0) {
 #pragma unroll
     for (int i = 0; i < ACH; ++i) {
-      const int p = p0 + a_pr0 + i * (256 / ACPR), k = m0 + a_cc * 8;
+      const int p = p0 + a_pr0 + i * (NT / ACPR), k = m0 + a_cc * 8;
       ra[i] = (p < p_end && k < g.K) ? *reinterpret_cast<const u32x4*>(g.dY + (long)p * g.K + k) : u32x4{0u, 0u, 0u, 0u};
     }
 #pragma unroll
     for (int i = 0; i < BCH; ++i) {
-      const int p = p0 + b_pr0 + i * (256 / BCPR);
+      const int p = p0 + b_pr0 + i * (NT / BCPR);
       u32x4 v = {0u, 0u, 0u, 0u};
       if (p < p_end && b_colok) {
         const int n = fdiv(p, inv_HoWo);
@@ -265,12 +267,12 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradGeom g) {
   auto lstore = [&](int buf) {
 #pragma unroll
     for (int i = 0; i < ACH; ++i) {
-      const int ch = t + 256 * i;
+      const int ch = t + NT * i;
       *reinterpret_cast<u32x4*>(&lds[buf][(ch / ACPR) * LDM + (ch % ACPR) * 8]) = ra[i];
     }
 #pragma unroll
     for (int i = 0; i < BCH; ++i) {
-      const int ch = t + 256 * i;
+      const int ch = t + NT * i;
       *reinterpret_cast<u32x4*>(&lds[buf][64 * LDM + (ch / BCPR) * LDN + (ch % BCPR) * 8]) = rb[i];
     }
   };
@@ -334,20 +336,28 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradGeom g) {
     }
 }
 
-// dw[k][c][r][s] += sum_z ws[z][k][(r*S+s)*C + c]  for c < Creal (reads coalesced along c)
-__global__ void wgrad_reduce_kernel(int K, int C, int Creal, int R, int S, int splits, const float* __restrict__ ws,
-                                    float* __restrict__ dw) {
-  const int RSC = R * S * C;
+// dw[k][c][r][s] += sum_z ws[z][k][(r*S+s)*C + c]  for c < Creal.  One block per output channel k:
+// the split slabs are summed with reads coalesced along (tap, c) into LDS, then written back in the
+// PyTorch order (c, r, s), also coalesced.  R*S*C <= 9 * 512 floats of LDS.
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(int K, int C, int Creal, int R, int S, int splits,
+                                                           const float* __restrict__ ws, float* __restrict__ dw) {
+  extern __shared__ float row[];
+  const int k = blockIdx.x;
+  const int RS = R * S, RSC = RS * C;
   const long total = (long)K * RSC;
-  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
-    const int k = (int)(e / RSC);
-    const int rem = (int)(e - (long)k * RSC);
-    const int tap = rem / C, c = rem - tap * C;
-    if (c >= Creal) continue;
+  const float* src = ws + (long)k * RSC;
+  for (int e = threadIdx.x; e < RSC; e += 256) {
     float acc = 0.f;
-    for (int z = 0; z < splits; ++z) acc += ws[(long)z * total + e];
-    const int r = tap / S, s = tap - r * S;
-    dw[(((long)k * Creal + c) * R + r) * S + s] += acc;
+    for (int z = 0; z < splits; ++z) acc += src[(long)z * total + e];
+    row[e] = acc;
+  }
+  __syncthreads();
+  const int n = Creal * RS;
+  const float inv_RS = 1.f / RS;
+  float* dst = dw + (long)k * n;
+  for (int e = threadIdx.x; e < n; e += 256) {  // e = c*RS + tap
+    const int c = fdiv(e, inv_RS), tap = e - c * RS;
+    dst[e] += row[tap * C + c];
   }
 }
 
@@ -815,7 +825,14 @@ MER_API int mer_conv_dgrad_bnr(int N, int H, int W, int C, int K, int R, int S, 
 
 MER_API int mer_conv_wgrad(int N, int H, int W, int C, int Creal, int K, int R, int S, int stride, int pad,
                            const void* x, const void* dy, float* dw, int splits, float* workspace, void* stream) {
-  if (C % 8 || K % 8) return (int)hipErrorInvalidValue;
+  return mer_conv_wgrad_ex(N, H, W, C, Creal, K, R, S, stride, pad, x, dy, dw, splits, workspace, -1, stream);
+}
+
+MER_API int mer_conv_wgrad_ex(int N, int H, int W, int C, int Creal, int K, int R, int S, int stride, int pad,
+                              const void* x, const void* dy, float* dw, int splits, float* workspace, int variant,
+                              void* stream) {
+  if (C % 8 || K % 8 || variant < -1 || variant > 2) return (int)hipErrorInvalidValue;
+  if (variant == -1) variant = 2;
   WgradGeom g{};
   g.N = N; g.H = H; g.W = W; g.C = C; g.Creal = Creal;
   g.Ho = (H + 2 * pad - R) / stride + 1; g.Wo = (W + 2 * pad - S) / stride + 1; g.K = K;
@@ -829,14 +846,19 @@ MER_API int mer_conv_wgrad(int N, int H, int W, int C, int Creal, int K, int R, 
   hipStream_t st = (hipStream_t)stream;
   if (K <= 64) {
     dim3 grid(((Ntot + 127) / 128) * ((K + 63) / 64), 1, splits);
-    hipLaunchKernelGGL((wgrad_kernel<64, 128>), grid, dim3(256), 0, st, g);
+    if (variant == 1)
+      hipLaunchKernelGGL((wgrad_kernel<64, 128>), grid, dim3(256), 0, st, g);
+    else
+      hipLaunchKernelGGL((wgrad_kernel<64, 128, 2, 4>), grid, dim3(512), 0, st, g);
   } else {
     dim3 grid(((Ntot + 127) / 128) * ((K + 127) / 128), 1, splits);
-    hipLaunchKernelGGL((wgrad_kernel<128, 128>), grid, dim3(256), 0, st, g);
+    if (variant == 1)
+      hipLaunchKernelGGL((wgrad_kernel<128, 128>), grid, dim3(256), 0, st, g);
+    else
+      hipLaunchKernelGGL((wgrad_kernel<128, 128, 2, 4>), grid, dim3(512), 0, st, g);
   }
-  const long total = (long)K * Ntot;
-  const int rgrid = (int)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(rgrid), dim3(256), 0, st, K, C, Creal, R, S, splits, workspace, dw);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(K), dim3(256), (size_t)Ntot * sizeof(float), st, K, C, Creal, R, S,
+                     splits, workspace, dw);
   MER_LAUNCH_CHECK();
 }
 

@@ -351,7 +351,7 @@ def partials_sum(parts_buf, out):
     return out
 
 
-def conv_wgrad(x, dy, dw, R, S, stride, pad, creal=None):
+def conv_wgrad(x, dy, dw, R, S, stride, pad, creal=None, variant=-1, splits=None):
     N, H, W, C = x.shape
     Kc = dy.shape[-1]
     Ho, Wo = (H + 2 * pad - R) // stride + 1, (W + 2 * pad - S) // stride + 1
@@ -360,10 +360,11 @@ def conv_wgrad(x, dy, dw, R, S, stride, pad, creal=None):
         raise ValueError("conv_wgrad shapes")
     P = N * Ho * Wo
     tiles = ((Kc + 127) // 128) * ((R * S * C + 127) // 128)
-    splits = int(max(1, min(-(-512 // tiles), P // 2048)))
+    if splits is None:
+        splits = int(max(1, min(-(-512 // tiles), P // 2048)))
     ws = torch.empty(splits * Kc * R * S * C, device=x.device, dtype=torch.float32)
-    _launch("conv_wgrad", (N, H, W, C, Kc, R, stride), "mer_conv_wgrad", N, H, W, C, creal, Kc, R, S, stride, pad,
-            x.data_ptr(), dy.data_ptr(), dw.data_ptr(), splits, ws.data_ptr(), stream_ptr())
+    _launch("conv_wgrad", (N, H, W, C, Kc, R, stride), "mer_conv_wgrad_ex", N, H, W, C, creal, Kc, R, S, stride, pad,
+            x.data_ptr(), dy.data_ptr(), dw.data_ptr(), int(splits), ws.data_ptr(), int(variant), stream_ptr())
 
 
 def pack_input_nhwc(x, y):

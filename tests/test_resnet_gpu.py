@@ -279,3 +279,22 @@ def test_dgrad_fused_bn_reduce_matches_standalone(stride, ds):
         ref2 = torch.zeros(C, 2, device="cuda")
         K.bn_bwd_reduce(dx_ref, mask, x2, ms2, ref2)
         assert torch.allclose(red2, ref2, rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("N,H,C,Kc,R,stride,pad", [(2, 28, 64, 64, 3, 1, 1), (2, 14, 128, 256, 3, 2, 1),
+                                                   (2, 30, 8, 64, 7, 2, 3), (4, 7, 512, 512, 3, 1, 1)])
+def test_wgrad_variants_bit_identical(N, H, C, Kc, R, stride, pad):
+    """8-wave wgrad (default) == 4-wave wgrad: same pixel order per split, same split sum order."""
+    from multimodalemotionrecognition_amd import kernels as K
+
+    torch.manual_seed(4)
+    Ho = (H + 2 * pad - R) // stride + 1
+    x = torch.randn(N, H, H, C, device="cuda").bfloat16()
+    dy = torch.randn(N, Ho, Ho, Kc, device="cuda").bfloat16()
+    creal = 3 if C == 8 else C
+    out = []
+    for v in (1, 2):
+        dw = torch.zeros(Kc, creal, R, R, device="cuda")
+        K.conv_wgrad(x, dy, dw, R, R, stride, pad, creal=creal, variant=v)
+        out.append(dw)
+    assert torch.equal(out[0], out[1])

@@ -43,7 +43,11 @@ def main():
         dy = (torch.rand(NF, Ho, Ho, Kc, device="cuda") * 2 - 1).bfloat16()
         dx = torch.empty(NF, H, H, C, device="cuda", dtype=torch.bfloat16)
         flop = 2.0 * NF * Ho * Ho * Kc * R * R * C
+        dw = torch.zeros(Kc, C, R, R, device="cuda")
         line = f"{name:16s}"
+        for v in (1, 2):
+            tw = timeit(lambda: K.conv_wgrad(x, dy, dw, R, R, st, pad, variant=v))
+            line += f" | wgrad v{v} {tw*1e3:7.1f}us {flop/tw/1e9:6.1f}TF"
         for v in (2, 3):
             tf = timeit(lambda: K.conv_fwd(x, wp, y, stats, R, R, st, pad, variant=v))
             tb = timeit(lambda: K.conv_dgrad(dy, wt, dx, R, R, st, pad, variant=v))
