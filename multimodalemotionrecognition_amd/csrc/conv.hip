@@ -336,28 +336,30 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void wgrad_kernel(WgradGeom g) {
     }
 }
 
-// dw[k][c][r][s] += sum_z ws[z][k][(r*S+s)*C + c]  for c < Creal.  One block per output channel k:
-// the split slabs are summed with reads coalesced along (tap, c) into LDS, then written back in the
-// PyTorch order (c, r, s), also coalesced.  R*S*C <= 9 * 512 floats of LDS.
+// dw[k][c][r][s] += sum_z ws[z][k][(r*S+s)*C + c]  for c < Creal.  Block (channel group of 32, k): the
+// split slabs are summed with reads coalesced along c (one 128-byte segment per tap) into an LDS
+// [tap][32] tile, written back in the PyTorch order (c, r, s) -- a contiguous run of 32*R*S floats.
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(int K, int C, int Creal, int R, int S, int splits,
                                                            const float* __restrict__ ws, float* __restrict__ dw) {
-  extern __shared__ float row[];
-  const int k = blockIdx.x;
-  const int RS = R * S, RSC = RS * C;
-  const long total = (long)K * RSC;
-  const float* src = ws + (long)k * RSC;
-  for (int e = threadIdx.x; e < RSC; e += 256) {
+  __shared__ float tile[49 * 32];  // R*S <= 49 (7x7 stem)
+  const int k = blockIdx.y, c0 = blockIdx.x * 32;
+  const int RS = R * S;
+  const long total = (long)K * RS * C;
+  const float* src = ws + (long)k * RS * C;
+  for (int idx = threadIdx.x; idx < RS * 32; idx += 256) {
+    const int tap = idx >> 5, c = c0 + (idx & 31);
     float acc = 0.f;
-    for (int z = 0; z < splits; ++z) acc += src[(long)z * total + e];
-    row[e] = acc;
+    if (c < Creal)
+      for (int z = 0; z < splits; ++z) acc += src[(long)z * total + tap * C + c];
+    tile[idx] = acc;
   }
   __syncthreads();
-  const int n = Creal * RS;
+  const int ncl = min(32, Creal - c0);
   const float inv_RS = 1.f / RS;
-  float* dst = dw + (long)k * n;
-  for (int e = threadIdx.x; e < n; e += 256) {  // e = c*RS + tap
-    const int c = fdiv(e, inv_RS), tap = e - c * RS;
-    dst[e] += row[tap * C + c];
+  float* dst = dw + ((long)k * Creal + c0) * RS;
+  for (int idx = threadIdx.x; idx < ncl * RS; idx += 256) {  // idx = cl*RS + tap
+    const int cl = fdiv(idx, inv_RS), tap = idx - cl * RS;
+    dst[idx] += tile[tap * 32 + cl];
   }
 }
 
@@ -831,7 +833,7 @@ MER_API int mer_conv_wgrad(int N, int H, int W, int C, int Creal, int K, int R, 
 MER_API int mer_conv_wgrad_ex(int N, int H, int W, int C, int Creal, int K, int R, int S, int stride, int pad,
                               const void* x, const void* dy, float* dw, int splits, float* workspace, int variant,
                               void* stream) {
-  if (C % 8 || K % 8 || variant < -1 || variant > 2) return (int)hipErrorInvalidValue;
+  if (C % 8 || K % 8 || variant < -1 || variant > 2 || R * S > 49) return (int)hipErrorInvalidValue;
   if (variant == -1) variant = 2;
   WgradGeom g{};
   g.N = N; g.H = H; g.W = W; g.C = C; g.Creal = Creal;
@@ -857,8 +859,8 @@ MER_API int mer_conv_wgrad_ex(int N, int H, int W, int C, int Creal, int K, int 
     else
       hipLaunchKernelGGL((wgrad_kernel<128, 128, 2, 4>), grid, dim3(512), 0, st, g);
   }
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(K), dim3(256), (size_t)Ntot * sizeof(float), st, K, C, Creal, R, S,
-                     splits, workspace, dw);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((Creal + 31) / 32, K), dim3(256), 0, st, K, C, Creal, R, S, splits,
+                     workspace, dw);
   MER_LAUNCH_CHECK();
 }
 
