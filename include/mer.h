@@ -46,14 +46,18 @@ int mer_colsum_f32(int M, int N, const float* X, long ldx, float* out, void* str
 /* Multi-head attention core of nn.MultiheadAttention (fusion.py:276-281,394,398 -> TORCH:6576-6606):
  * P = softmax(scale * Q_h K_h^T + bias[b]); O_h = dropout(P) V_h.  Rows: X + (b*L+i)*ld + h*dh.
  * bias [B,Lq,Lk] is the per-sample emotion-prior mask repeated over heads (fusion.py:351-354), or NULL.
- * P [B,H,Lq,Lk] receives the pre-dropout probabilities (saved for backward).  dh must divide 64. */
+ * P [B,H,Lq,Lk] receives the pre-dropout probabilities (saved for backward).  QK^T and PV on the exact-f32
+ * MFMA (v_mfma_f32_16x16x4_f32).  Limits: dh % 4 == 0, dh <= 64, Lk <= 256 (hipErrorInvalidValue else). */
 int mer_mha_fwd(int B, int H, int Lq, int Lk, int dh, const float* Q, long ldq, const float* K, long ldk,
                 const float* V, long ldv, const float* bias, float* O, long ldo, float* P, float scale, float drop_p,
                 unsigned long long seed, void* stream);
 
-/* Backward of mer_mha_fwd: writes dQ, dK, dV (not accumulated) and dbias[b] = sum_h dS (if non-NULL). */
+/* Backward of mer_mha_fwd: writes dQ, dK, dV (not accumulated) and dbias[b] = sum_h dS (if non-NULL).
+ * One workgroup per (b, h), all four products on the f32 MFMA.  When dbias is requested, P is overwritten
+ * with dS (the per-head scratch of the deterministic head sum).  Same limits as mer_mha_fwd, plus the
+ * LDS image 4*(Lq+Lk)*dh + 2*Lq*Lk floats (padded) must fit in 160 KiB. */
 int mer_mha_bwd(int B, int H, int Lq, int Lk, int dh, const float* Q, long ldq, const float* K, long ldk,
-                const float* V, long ldv, const float* P, const float* dO, long lddo, float* dQ, long lddq, float* dK,
+                const float* V, long ldv, float* P, const float* dO, long lddo, float* dQ, long lddq, float* dK,
                 long lddk, float* dV, long lddv, float* dbias, float scale, float drop_p, unsigned long long seed,
                 void* stream);
 

@@ -150,188 +150,7 @@ MER_API int mer_colsum_f32(int M, int N, const float* X, long ldx, float* out, v
   MER_LAUNCH_CHECK();
 }
 
-// ---------------------------------------------------------------------------------------
-// Multi-head attention core (TORCH:6576-6606 explicit path) for the xattn blocks and the
-// temporal transformer pooler:  P = softmax(scale Q_h K_h^T + bias[b]);  O_h = drop(P) V_h.
-// q/k/v/o rows: X + (b*L + i)*ld + h*dh.  bias: [B, Lq, Lk] (per sample, shared across heads,
-// fusion.py:351-354) or null.  Saves P (pre-dropout) [B,H,Lq,Lk] for backward.
-// One workgroup = (b, h, 16 query rows); K_h and V_h staged in LDS.
-// ---------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void mha_fwd_kernel(int B, int H, int Lq, int Lk, int dh, const float* __restrict__ Q,
-                                                      long ldq, const float* __restrict__ K, long ldk,
-                                                      const float* __restrict__ V, long ldv, const float* __restrict__ bias,
-                                                      float* __restrict__ O, long ldo, float* __restrict__ P,
-                                                      float scale, float drop_p, unsigned long long seed) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int dp = dh + 1;
-  float* Ks = smem;                 // [Lk][dp]
-  float* Vs = Ks + Lk * dp;         // [Lk][dp]
-  float* qs = Vs + Lk * dp;         // [4][dh]
-  float* ps = qs + 4 * dh;          // [4][Lk]
-  const int b = blockIdx.x / H, h = blockIdx.x % H;
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  for (int e = t; e < Lk * dh; e += 256) {
-    const int j = e / dh, c = e % dh;
-    Ks[j * dp + c] = K[((long)b * Lk + j) * ldk + h * dh + c];
-    Vs[j * dp + c] = V[((long)b * Lk + j) * ldv + h * dh + c];
-  }
-  __syncthreads();
-  const int nsub = 64 / dh > 0 ? 64 / dh : 1;  // key subsets in the PV reduction
-  for (int ii = w; ii < 16; ii += 4) {  // every wave runs 4 rounds: syncs stay uniform
-    const int i = blockIdx.y * 16 + ii;
-    const bool valid = i < Lq;
-    if (valid) {
-      const float* qrow = Q + ((long)b * Lq + i) * ldq + h * dh;
-      for (int c = lane; c < dh; c += 64) qs[w * dh + c] = qrow[c];
-    }
-    __syncthreads();
-    if (valid) {
-      float mx = -INFINITY;
-      for (int j = lane; j < Lk; j += 64) {
-        float s = 0.f;
-        for (int c = 0; c < dh; ++c) s += qs[w * dh + c] * Ks[j * dp + c];
-        s *= scale;
-        if (bias) s += bias[((long)b * Lq + i) * Lk + j];
-        ps[w * Lk + j] = s;
-        mx = fmaxf(mx, s);
-      }
-      mx = wave_max(mx);
-      float sum = 0.f;
-      for (int j = lane; j < Lk; j += 64) {
-        const float e = __expf(ps[w * Lk + j] - mx);
-        ps[w * Lk + j] = e;
-        sum += e;
-      }
-      sum = wave_sum(sum);
-      const float inv = 1.f / sum;
-      const long prow = (((long)b * H + h) * Lq + i) * Lk;
-      for (int j = lane; j < Lk; j += 64) {
-        const float pr = ps[w * Lk + j] * inv;
-        P[prow + j] = pr;
-        ps[w * Lk + j] = pr * dropout_scale(seed, prow + j, drop_p);
-      }
-    }
-    __syncthreads();
-    if (valid) {
-      // O_i[c] = sum_j p'_j V[j][c]: lane -> (c = lane % dh, key subset lane / dh)
-      const int c = lane % dh, sub = lane / dh;
-      float o = 0.f;
-      if (sub < nsub)
-        for (int j = sub; j < Lk; j += nsub) o += ps[w * Lk + j] * Vs[j * dp + c];
-      for (int off = dh; off < 64; off <<= 1) o += __shfl_down(o, off, 64);
-      if (lane < dh) O[((long)b * Lq + i) * ldo + h * dh + c] = o;
-    }
-    __syncthreads();
-  }
-}
-
-MER_API int mer_mha_fwd(int B, int H, int Lq, int Lk, int dh, const float* Q, long ldq, const float* K, long ldk,
-                        const float* V, long ldv, const float* bias, float* O, long ldo, float* P, float scale,
-                        float drop_p, unsigned long long seed, void* stream) {
-  if (dh > 64 || (64 % dh) != 0) return (int)hipErrorInvalidValue;
-  const size_t lds = sizeof(float) * ((size_t)2 * Lk * (dh + 1) + 4 * dh + 4 * Lk);
-  if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
-  dim3 grid(B * H, (Lq + 15) / 16);
-  hipLaunchKernelGGL(mha_fwd_kernel, grid, dim3(256), lds, (hipStream_t)stream, B, H, Lq, Lk, dh, Q, ldq, K, ldk, V,
-                     ldv, bias, O, ldo, P, scale, drop_p, seed);
-  MER_LAUNCH_CHECK();
-}
-
-// Backward.  One workgroup per sample b, heads in sequence (dbias[b] = sum_h dS stays deterministic,
-// no atomics); within a head every (i,j) score and every output element is its own thread:
-//   dP'_ij = dO_i . V_j;  dP_ij = dP'_ij * mask_ij;  dS_ij = P_ij (dP_ij - sum_j' P_ij' dP_ij')
-//   dQ_i = scale sum_j dS_ij K_j;  dK_j = scale sum_i dS_ij Q_i;  dV_j = sum_i P'_ij dO_i
-// dQ/dK/dV are written (not accumulated).  Q,K,V,dO of the head + the Lq x Lk score tiles live in LDS.
-__global__ __launch_bounds__(256) void mha_bwd_kernel(int B, int H, int Lq, int Lk, int dh, const float* __restrict__ Q,
-                                                      long ldq, const float* __restrict__ K, long ldk,
-                                                      const float* __restrict__ V, long ldv, const float* __restrict__ P,
-                                                      const float* __restrict__ dO, long lddo, float* __restrict__ dQ,
-                                                      long lddq, float* __restrict__ dK, long lddk, float* __restrict__ dV,
-                                                      long lddv, float* __restrict__ dbias, float scale, float drop_p,
-                                                      unsigned long long seed) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int dp = dh + 1, lkp = Lk + 1;
-  float* Qs = smem;              // [Lq][dp]
-  float* dOs = Qs + Lq * dp;     // [Lq][dp]
-  float* Ks = dOs + Lq * dp;     // [Lk][dp]
-  float* Vs = Ks + Lk * dp;      // [Lk][dp]
-  float* dS = Vs + Lk * dp;      // [Lq][lkp]
-  float* Pd = dS + Lq * lkp;     // [Lq][lkp]  dropped-out probabilities p'
-  float* rdot = Pd + Lq * lkp;   // [Lq]
-  const int b = blockIdx.x;
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  for (int h = 0; h < H; ++h) {
-    for (int e = t; e < Lq * dh; e += 256) {
-      const int i = e / dh, c = e - (e / dh) * dh;
-      Qs[i * dp + c] = Q[((long)b * Lq + i) * ldq + h * dh + c];
-      dOs[i * dp + c] = dO[((long)b * Lq + i) * lddo + h * dh + c];
-    }
-    for (int e = t; e < Lk * dh; e += 256) {
-      const int j = e / dh, c = e - (e / dh) * dh;
-      Ks[j * dp + c] = K[((long)b * Lk + j) * ldk + h * dh + c];
-      Vs[j * dp + c] = V[((long)b * Lk + j) * ldv + h * dh + c];
-    }
-    __syncthreads();
-    const long pbase = ((long)b * H + h) * Lq * Lk;
-    for (int e = t; e < Lq * Lk; e += 256) {
-      const int i = e / Lk, j = e - (e / Lk) * Lk;
-      float dpv = 0.f;
-      for (int c = 0; c < dh; ++c) dpv += dOs[i * dp + c] * Vs[j * dp + c];
-      const float m = dropout_scale(seed, pbase + e, drop_p);
-      const float pj = P[pbase + e];
-      dS[i * lkp + j] = dpv * m;
-      Pd[i * lkp + j] = pj * m;
-    }
-    __syncthreads();
-    for (int i = w; i < Lq; i += 4) {
-      float dot = 0.f;
-      for (int j = lane; j < Lk; j += 64) dot += P[pbase + (long)i * Lk + j] * dS[i * lkp + j];
-      dot = wave_sum(dot);
-      if (lane == 0) rdot[i] = dot;
-    }
-    __syncthreads();
-    for (int e = t; e < Lq * Lk; e += 256) {
-      const int i = e / Lk, j = e - (e / Lk) * Lk;
-      const float v = P[pbase + e] * (dS[i * lkp + j] - rdot[i]);
-      dS[i * lkp + j] = v;
-      if (dbias) {
-        float* dbp = dbias + (long)b * Lq * Lk + e;
-        *dbp = (h == 0 ? 0.f : *dbp) + v;  // same thread owns element e for every head
-      }
-    }
-    __syncthreads();
-    for (int e = t; e < Lq * dh; e += 256) {
-      const int i = e / dh, c = e - (e / dh) * dh;
-      float g = 0.f;
-      for (int j = 0; j < Lk; ++j) g += dS[i * lkp + j] * Ks[j * dp + c];
-      dQ[((long)b * Lq + i) * lddq + h * dh + c] = scale * g;
-    }
-    for (int e = t; e < Lk * dh; e += 256) {
-      const int j = e / dh, c = e - (e / dh) * dh;
-      float gk = 0.f, gv = 0.f;
-      for (int i = 0; i < Lq; ++i) {
-        gk += dS[i * lkp + j] * Qs[i * dp + c];
-        gv += Pd[i * lkp + j] * dOs[i * dp + c];
-      }
-      dK[((long)b * Lk + j) * lddk + h * dh + c] = scale * gk;
-      dV[((long)b * Lk + j) * lddv + h * dh + c] = gv;
-    }
-    __syncthreads();
-  }
-}
-
-MER_API int mer_mha_bwd(int B, int H, int Lq, int Lk, int dh, const float* Q, long ldq, const float* K, long ldk,
-                        const float* V, long ldv, const float* P, const float* dO, long lddo, float* dQ, long lddq,
-                        float* dK, long lddk, float* dV, long lddv, float* dbias, float scale, float drop_p,
-                        unsigned long long seed, void* stream) {
-  if (dh > 64 || (64 % dh) != 0) return (int)hipErrorInvalidValue;
-  const size_t lds = sizeof(float) * ((size_t)2 * Lq * (dh + 1) + (size_t)2 * Lk * (dh + 1) +
-                                      (size_t)2 * Lq * (Lk + 1) + Lq);
-  if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(mha_bwd_kernel, dim3(B), dim3(256), lds, (hipStream_t)stream, B, H, Lq, Lk, dh, Q, ldq, K, ldk, V,
-                     ldv, P, dO, lddo, dQ, lddq, dK, lddk, dV, lddv, dbias, scale, drop_p, seed);
-  MER_LAUNCH_CHECK();
-}
+// (multi-head attention core: attn.hip)
 
 // ---------------------------------------------------------------------------------------
 // y = LayerNorm(x + s_b * r) (fusion.py:395,399 with StochasticDepth fusion.py:11-26):
