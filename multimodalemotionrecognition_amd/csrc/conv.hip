@@ -336,30 +336,54 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void wgrad_kernel(WgradGeom g) {
     }
 }
 
-// dw[k][c][r][s] += sum_z ws[z][k][(r*S+s)*C + c]  for c < Creal.  Block (channel group of 32, k): the
-// split slabs are summed with reads coalesced along c (one 128-byte segment per tap) into an LDS
-// [tap][32] tile, written back in the PyTorch order (c, r, s) -- a contiguous run of 32*R*S floats.
-__global__ __launch_bounds__(256) void wgrad_reduce_kernel(int K, int C, int Creal, int R, int S, int splits,
-                                                           const float* __restrict__ ws, float* __restrict__ dw) {
+// slab0[i] = sum_z ws[z][i] over the flat [K][R*S*C] index.  A block owns E = 256/SG consecutive elements
+// and SG split-groups: thread (sg, e) sums splits sg, sg+SG, ... with 4 independent loads in flight (the
+// split count reaches ~100 on the stem / layer1, where one serial chain per element was latency-bound),
+// and the SG partials meet in LDS.
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(int K, int C, int Creal, int RS, int splits, int SG,
+                                                           float* __restrict__ ws) {
+  __shared__ float part[256];
+  const int E = 256 / SG, e = threadIdx.x % E, sg = threadIdx.x / E;
+  const long total = (long)K * RS * C;
+  const long idx = (long)blockIdx.x * E + e;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  if (idx < total) {
+    int z = sg;
+    for (; z + 3 * SG < splits; z += 4 * SG) {
+      a0 += ws[(long)z * total + idx];
+      a1 += ws[(long)(z + SG) * total + idx];
+      a2 += ws[(long)(z + 2 * SG) * total + idx];
+      a3 += ws[(long)(z + 3 * SG) * total + idx];
+    }
+    for (; z < splits; z += SG) a0 += ws[(long)z * total + idx];
+  }
+  part[threadIdx.x] = (a0 + a1) + (a2 + a3);
+  __syncthreads();
+  if (sg != 0 || idx >= total) return;
+  float s = 0.f;
+  for (int q = 0; q < SG; ++q) s += part[q * E + e];
+  ws[idx] = s;  // slab 0 (only this block ever reads element idx)
+}
+
+// dw[k][c][r][s] += slab0[k][(r*S+s)*C + c] for c < Creal.  Block (channel group of 32, k): reads coalesced
+// along c (one 128-byte segment per tap) into an LDS [tap][32] tile, written back in the PyTorch order
+// (c, r, s) -- a contiguous run of 32*R*S floats.
+__global__ __launch_bounds__(256) void wgrad_scatter_kernel(int C, int Creal, int RS, const float* __restrict__ ws,
+                                                            float* __restrict__ dw) {
   __shared__ float tile[49 * 32];  // R*S <= 49 (7x7 stem)
   const int k = blockIdx.y, c0 = blockIdx.x * 32;
-  const int RS = R * S;
-  const long total = (long)K * RS * C;
   const float* src = ws + (long)k * RS * C;
-  for (int idx = threadIdx.x; idx < RS * 32; idx += 256) {
-    const int tap = idx >> 5, c = c0 + (idx & 31);
-    float acc = 0.f;
-    if (c < Creal)
-      for (int z = 0; z < splits; ++z) acc += src[(long)z * total + tap * C + c];
-    tile[idx] = acc;
+  for (int i = threadIdx.x; i < RS * 32; i += 256) {
+    const int tap = i >> 5, c = c0 + (i & 31);
+    tile[i] = c < Creal ? src[tap * C + c] : 0.f;
   }
   __syncthreads();
   const int ncl = min(32, Creal - c0);
   const float inv_RS = 1.f / RS;
   float* dst = dw + ((long)k * Creal + c0) * RS;
-  for (int idx = threadIdx.x; idx < ncl * RS; idx += 256) {  // idx = cl*RS + tap
-    const int cl = fdiv(idx, inv_RS), tap = idx - cl * RS;
-    dst[idx] += tile[tap * 32 + cl];
+  for (int i = threadIdx.x; i < ncl * RS; i += 256) {  // i = cl*RS + tap
+    const int cl = fdiv(i, inv_RS), tap = i - cl * RS;
+    dst[i] += tile[tap * 32 + cl];
   }
 }
 
@@ -859,8 +883,14 @@ MER_API int mer_conv_wgrad_ex(int N, int H, int W, int C, int Creal, int K, int 
     else
       hipLaunchKernelGGL((wgrad_kernel<128, 128, 2, 4>), grid, dim3(512), 0, st, g);
   }
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((Creal + 31) / 32, K), dim3(256), 0, st, K, C, Creal, R, S, splits,
-                     workspace, dw);
+  if (splits > 1) {
+    const int SG = splits >= 64 ? 16 : splits >= 16 ? 8 : 4;
+    const long total = (long)K * R * S * C;
+    const int E = 256 / SG;
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((total + E - 1) / E)), dim3(256), 0, st, K, C, Creal, R * S,
+                       splits, SG, workspace);
+  }
+  hipLaunchKernelGGL(wgrad_scatter_kernel, dim3((Creal + 31) / 32, K), dim3(256), 0, st, C, Creal, R * S, workspace, dw);
   MER_LAUNCH_CHECK();
 }
 
@@ -963,34 +993,42 @@ MER_API int mer_bn_finalize(int C, long M, const float* stats, float eps, float 
 
 // y = [relu]( bn(x) + (res_bn ? bn2(res) : res) ), 8 channels per thread (C % 8 == 0).
 // ms = (mean, rstd) pairs; eval mode passes (running_mean, 1/sqrt(running_var+eps)) the same way.
+// BN is folded into one (scale, shift) per channel, computed once per block into LDS (C <= 512); a
+// thread always owns the same 8 channels (256 % (C/8) == 0 and the grid stride is a multiple of 256) and
+// streams two 16-byte vectors per iteration so the loads of both are in flight together.
 __global__ __launch_bounds__(256) void bn_apply_kernel(long M, int C, const bf16_t* __restrict__ x,
                                                        const float* __restrict__ ms, const float* __restrict__ gamma,
                                                        const float* __restrict__ beta, const bf16_t* __restrict__ res,
                                                        const float* __restrict__ ms2, const float* __restrict__ gamma2,
                                                        const float* __restrict__ beta2, int relu,
                                                        bf16_t* __restrict__ y) {
-  // 256 % (C/8) == 0 and the grid stride is a multiple of 256, so a thread always owns the same 8
-  // channels: fold BN into one (scale, shift) per channel once, outside the streaming loop.
+  __shared__ __attribute__((aligned(16))) float coef[4][512];  // scale, shift, scale2, shift2
+  for (int c = threadIdx.x; c < C; c += 256) {
+    const float sc = ms[2 * c + 1] * gamma[c];
+    coef[0][c] = sc;
+    coef[1][c] = beta[c] - ms[2 * c] * sc;
+    float sc2 = 1.f, sh2 = 0.f;
+    if (ms2) {
+      sc2 = ms2[2 * c + 1] * gamma2[c];
+      sh2 = beta2[c] - ms2[2 * c] * sc2;
+    }
+    coef[2][c] = sc2;
+    coef[3][c] = sh2;
+  }
+  __syncthreads();
   const long nvec = M * C / 8;
+  const long stride = (long)gridDim.x * blockDim.x;
   const long tid0 = blockIdx.x * (long)blockDim.x + threadIdx.x;
   const int c0 = (int)(tid0 % (C / 8)) * 8;
   float sc[8], sh[8], sc2[8], sh2[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    const int c = c0 + i;
-    sc[i] = ms[2 * c + 1] * gamma[c];
-    sh[i] = beta[c] - ms[2 * c] * sc[i];
-    sc2[i] = 1.f;
-    sh2[i] = 0.f;
-    if (ms2) {
-      sc2[i] = ms2[2 * c + 1] * gamma2[c];
-      sh2[i] = beta2[c] - ms2[2 * c] * sc2[i];
-    }
+    sc[i] = coef[0][c0 + i];
+    sh[i] = coef[1][c0 + i];
+    sc2[i] = coef[2][c0 + i];
+    sh2[i] = coef[3][c0 + i];
   }
-  for (long e = tid0; e < nvec; e += (long)gridDim.x * blockDim.x) {
-    const u32x4 xv = *reinterpret_cast<const u32x4*>(x + e * 8);
-    u32x4 rv = {0u, 0u, 0u, 0u};
-    if (res) rv = *reinterpret_cast<const u32x4*>(res + e * 8);
+  auto one = [&](const u32x4& xv, const u32x4& rv) -> u32x4 {
     const bf16_t* xh = reinterpret_cast<const bf16_t*>(&xv);
     const bf16_t* rh = reinterpret_cast<const bf16_t*>(&rv);
     u32x4 ov;
@@ -1002,15 +1040,35 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(long M, int C, const bf16
       if (relu) v = fmaxf(v, 0.f);
       oh[i] = f2bf(v);
     }
-    *reinterpret_cast<u32x4*>(y + e * 8) = ov;
+    return ov;
+  };
+  const u32x4 z = {0u, 0u, 0u, 0u};
+  long e = tid0;
+  for (; e + stride < nvec; e += 2 * stride) {
+    const u32x4 x0 = *reinterpret_cast<const u32x4*>(x + e * 8);
+    const u32x4 x1 = *reinterpret_cast<const u32x4*>(x + (e + stride) * 8);
+    const u32x4 r0 = res ? *reinterpret_cast<const u32x4*>(res + e * 8) : z;
+    const u32x4 r1 = res ? *reinterpret_cast<const u32x4*>(res + (e + stride) * 8) : z;
+    *reinterpret_cast<u32x4*>(y + e * 8) = one(x0, r0);
+    *reinterpret_cast<u32x4*>(y + (e + stride) * 8) = one(x1, r1);
+  }
+  if (e < nvec) {
+    const u32x4 x0 = *reinterpret_cast<const u32x4*>(x + e * 8);
+    const u32x4 r0 = res ? *reinterpret_cast<const u32x4*>(res + e * 8) : z;
+    *reinterpret_cast<u32x4*>(y + e * 8) = one(x0, r0);
   }
 }
+static int bn_stream_grid(long nvec) {
+  const long g = (nvec + 1023) / 1024;  // ~4 vectors per thread
+  return (int)(g < 1 ? 1 : g > 2048 ? 2048 : g);
+}
+
 MER_API int mer_bn_apply(long M, int C, const void* x, const float* ms, const float* gamma, const float* beta,
                          const void* res, const float* ms2, const float* gamma2, const float* beta2, int relu, void* y,
                          void* stream) {
-  if (C % 8 || 256 % (C / 8)) return (int)hipErrorInvalidValue;
+  if (C % 8 || C > 512 || 256 % (C / 8)) return (int)hipErrorInvalidValue;
   const long nvec = M * C / 8;
-  const int grid = (int)((nvec + 255) / 256 < 8192 ? (nvec + 255) / 256 : 8192);
+  const int grid = bn_stream_grid(nvec);
   hipLaunchKernelGGL(bn_apply_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, M, C, (const bf16_t*)x, ms,
                      gamma, beta, (const bf16_t*)res, ms2, gamma2, beta2, relu, (bf16_t*)y);
   MER_LAUNCH_CHECK();
@@ -1096,6 +1154,8 @@ MER_API int mer_partials_sum(int C, int parts, const float* in, float* out, void
 }
 
 // dx = gamma*rstd*(g - s1/M - xhat*s2/M) (bf16), and (block 0) dgamma += s2, dbeta += s1.
+// Affine in (g, x) once the sums are known: dx = k1*g + k2*x + k0 per channel, the constants computed once
+// per block into LDS; same thread/channel ownership and 2-vector streaming as bn_apply_kernel.
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(long M, int C, const bf16_t* __restrict__ dy,
                                                            const bf16_t* __restrict__ mask,
                                                            const bf16_t* __restrict__ x, const float* __restrict__ ms,
@@ -1103,35 +1163,34 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(long M, int C, const 
                                                            const float* __restrict__ red, int batch_stats,
                                                            bf16_t* __restrict__ dx, float* __restrict__ dgamma,
                                                            float* __restrict__ dbeta) {
-  if (blockIdx.x == 0) {
-    for (int c = threadIdx.x; c < C; c += 256) {
+  __shared__ __attribute__((aligned(16))) float coef[3][512];
+  const float invM = 1.f / (float)M;
+  for (int c = threadIdx.x; c < C; c += 256) {
+    if (blockIdx.x == 0) {
       if (dgamma) dgamma[c] += red[2 * c + 1];
       if (dbeta) dbeta[c] += red[2 * c];
     }
+    const float mu = ms[2 * c], rs = ms[2 * c + 1], gr = gamma[c] * rs;
+    // batch statistics (train): the mean/var terms carry gradient; running stats (eval): they do not
+    const float a = batch_stats ? red[2 * c] * invM : 0.f;
+    const float b = batch_stats ? red[2 * c + 1] * invM : 0.f;
+    coef[0][c] = gr;
+    coef[1][c] = -gr * b * rs;
+    coef[2][c] = -gr * a + gr * b * rs * mu;
   }
-  // dx = k1*g + k2*x + k0 per channel (the BN backward is affine in (g, x) once the sums are known);
-  // a thread always owns the same 8 channels (see bn_apply_kernel), so the constants are hoisted.
+  __syncthreads();
   const long nvec = M * C / 8;
-  const float invM = 1.f / (float)M;
+  const long stride = (long)gridDim.x * blockDim.x;
   const long tid0 = blockIdx.x * (long)blockDim.x + threadIdx.x;
   const int c0 = (int)(tid0 % (C / 8)) * 8;
   float k1[8], k2[8], k0[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    const int c = c0 + i;
-    const float mu = ms[2 * c], rs = ms[2 * c + 1], gr = gamma[c] * rs;
-    // batch statistics (train): the mean/var terms carry gradient; running stats (eval): they do not
-    const float a = batch_stats ? red[2 * c] * invM : 0.f;
-    const float b = batch_stats ? red[2 * c + 1] * invM : 0.f;
-    k1[i] = gr;
-    k2[i] = -gr * b * rs;
-    k0[i] = -gr * a + gr * b * rs * mu;
+    k1[i] = coef[0][c0 + i];
+    k2[i] = coef[1][c0 + i];
+    k0[i] = coef[2][c0 + i];
   }
-  for (long e = tid0; e < nvec; e += (long)gridDim.x * blockDim.x) {
-    const u32x4 gv = *reinterpret_cast<const u32x4*>(dy + e * 8);
-    const u32x4 xv = *reinterpret_cast<const u32x4*>(x + e * 8);
-    u32x4 mv = {1u, 1u, 1u, 1u};
-    if (mask) mv = *reinterpret_cast<const u32x4*>(mask + e * 8);
+  auto one = [&](const u32x4& gv, const u32x4& xv, const u32x4& mv) -> u32x4 {
     const bf16_t* gh = reinterpret_cast<const bf16_t*>(&gv);
     const bf16_t* xh = reinterpret_cast<const bf16_t*>(&xv);
     const bf16_t* mh = reinterpret_cast<const bf16_t*>(&mv);
@@ -1142,15 +1201,34 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(long M, int C, const 
       const float g = (!mask || bf2f(mh[i]) > 0.f) ? bf2f(gh[i]) : 0.f;
       oh[i] = f2bf(k1[i] * g + k2[i] * bf2f(xh[i]) + k0[i]);
     }
-    *reinterpret_cast<u32x4*>(dx + e * 8) = ov;
+    return ov;
+  };
+  const u32x4 one16 = {0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u};  // bf16 1.0 (no mask)
+  long e = tid0;
+  for (; e + stride < nvec; e += 2 * stride) {
+    const long e1 = e + stride;
+    const u32x4 g0 = *reinterpret_cast<const u32x4*>(dy + e * 8);
+    const u32x4 g1 = *reinterpret_cast<const u32x4*>(dy + e1 * 8);
+    const u32x4 x0 = *reinterpret_cast<const u32x4*>(x + e * 8);
+    const u32x4 x1 = *reinterpret_cast<const u32x4*>(x + e1 * 8);
+    const u32x4 m0 = mask ? *reinterpret_cast<const u32x4*>(mask + e * 8) : one16;
+    const u32x4 m1 = mask ? *reinterpret_cast<const u32x4*>(mask + e1 * 8) : one16;
+    *reinterpret_cast<u32x4*>(dx + e * 8) = one(g0, x0, m0);
+    *reinterpret_cast<u32x4*>(dx + e1 * 8) = one(g1, x1, m1);
+  }
+  if (e < nvec) {
+    const u32x4 g0 = *reinterpret_cast<const u32x4*>(dy + e * 8);
+    const u32x4 x0 = *reinterpret_cast<const u32x4*>(x + e * 8);
+    const u32x4 m0 = mask ? *reinterpret_cast<const u32x4*>(mask + e * 8) : one16;
+    *reinterpret_cast<u32x4*>(dx + e * 8) = one(g0, x0, m0);
   }
 }
 MER_API int mer_bn_bwd_apply(long M, int C, const void* dy, const void* mask, const void* x, const float* ms,
                              const float* gamma, const float* red, int batch_stats, void* dx, float* dgamma,
                              float* dbeta, void* stream) {
-  if (C % 8 || 256 % (C / 8)) return (int)hipErrorInvalidValue;
+  if (C % 8 || C > 512 || 256 % (C / 8)) return (int)hipErrorInvalidValue;
   const long nvec = M * C / 8;
-  const int grid = (int)((nvec + 255) / 256 < 8192 ? (nvec + 255) / 256 : 8192);
+  const int grid = bn_stream_grid(nvec);
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, M, C, (const bf16_t*)dy,
                      (const bf16_t*)mask, (const bf16_t*)x, ms, gamma, red, batch_stats, (bf16_t*)dx, dgamma,
                      dbeta);
