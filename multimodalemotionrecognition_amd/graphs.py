@@ -1,0 +1,78 @@
+"""HIP-graph capture of the fixed-shape launch schedules (the MI355X answer to a tracing compiler).
+
+A train step issues ~360 kernel launches from Python; through ctypes each costs ~20 us of host time, so
+the host, not the GPU, became the bound (tools/host_time.py).  The encoders' schedules are static for a
+given input shape -- the frozen WavLM forward and the ResNet18 trunk forward/backward have no RNG and no
+host decisions -- so each is captured once into a ``torch.cuda.CUDAGraph`` (hipGraph on ROCm: our ctypes
+launches go to torch's current stream, which is the capture stream inside ``torch.cuda.graph``) and
+replayed as ONE host call afterwards.  Inputs are copied into graph-owned static buffers; outputs are the
+graph's static tensors.  A graph is keyed by its shapes and by the device addresses of every parameter
+and buffer it reads, so moving / re-homing weights (``.to()``, ``FusedAdam`` flattening) recaptures.
+
+Set ``MER_GRAPHS=0`` to run every launch eagerly (A/B and debugging).
+"""
+from __future__ import annotations
+
+import os
+from typing import Callable, Dict, Optional
+
+import torch
+
+ENABLED = os.environ.get("MER_GRAPHS", "1") != "0"
+WARMUP_CALLS = 1  # eager calls per key before capturing (first-call caches: packed weights, bucket table)
+
+
+class StaticGraph:
+    """``fn(*static_inputs)`` captured once; ``replay(*inputs)`` copies inputs in and replays."""
+
+    def __init__(self, fn: Callable, example_inputs, stream: Optional[torch.cuda.Stream] = None):
+        self.static_in = [t.detach().clone() for t in example_inputs]
+        self.graph = torch.cuda.CUDAGraph()
+        cur = stream if stream is not None else torch.cuda.current_stream()
+        side = torch.cuda.Stream(device=cur.device)
+        side.wait_stream(cur)
+        with torch.cuda.graph(self.graph, stream=side):
+            self.out = fn(*self.static_in)
+        cur.wait_stream(side)
+
+    def replay(self, *inputs):
+        for st, x in zip(self.static_in, inputs):
+            if st.data_ptr() != x.data_ptr():
+                st.copy_(x)
+        self.graph.replay()
+        return self.out
+
+
+class GraphCache:
+    """Per-key call counter + captured graphs (eager for the first WARMUP_CALLS calls of a key)."""
+
+    def __init__(self):
+        self.calls: Dict[tuple, int] = {}
+        self.graphs: Dict[tuple, object] = {}
+
+    def ready(self, key) -> bool:
+        """True when ``key`` should run through a (possibly not yet captured) graph."""
+        if not ENABLED:
+            return False
+        n = self.calls.get(key, 0)
+        self.calls[key] = n + 1
+        return n >= WARMUP_CALLS
+
+    def get(self, key):
+        return self.graphs.get(key)
+
+    def put(self, key, g):
+        # keep one graph per shape family: drop graphs whose weight addresses are stale
+        for k in [k for k in self.graphs if k[:-1] == key[:-1] and k != key]:
+            del self.graphs[k]
+        self.graphs[key] = g
+        return g
+
+
+def tensor_addresses(module: torch.nn.Module) -> tuple:
+    """Device addresses of every parameter and buffer (part of a graph key)."""
+    return tuple(t.data_ptr() for t in module.parameters()) + tuple(t.data_ptr() for t in module.buffers())
+
+
+def capturing() -> bool:
+    return torch.cuda.is_current_stream_capturing()

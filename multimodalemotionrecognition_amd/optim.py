@@ -20,6 +20,13 @@ def _align4(n: int) -> int:
     return (n + 3) // 4 * 4
 
 
+def weight_version(p: torch.Tensor) -> tuple:
+    """Identity of a weight's current VALUE for derived-copy caches (bf16 packs, INT8 images): storage
+    address, autograd version counter, and the FusedAdam update count -- the Adam kernel writes the flat
+    buffer through a raw pointer, which PyTorch's version counter never sees."""
+    return (p.data_ptr(), p._version, getattr(p, "_mer_updates", 0))
+
+
 class FusedAdam(torch.optim.Optimizer):
     def __init__(self, params, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0):
         defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay)
@@ -90,4 +97,7 @@ class FusedAdam(torch.optim.Optimizer):
             for s, e in runs:
                 K.adam_step(f["flat"][s:e], f["gflat"][s:e], f["m"][s:e], f["v"][s:e], group["lr"], b1, b2,
                             group["eps"], group["weight_decay"], f["step"], self.grad_scale)
+            for p in ps:
+                if p.grad is not None:
+                    p._mer_updates = getattr(p, "_mer_updates", 0) + 1
         return loss

@@ -17,8 +17,10 @@ from typing import List
 import torch
 from torch import nn
 
+from . import graphs as G
 from . import kernels as K
 from .nn_ops import hip_linear
+from .optim import weight_version
 from .temporal import TemporalPooler
 
 CP_IN = 8  # RGB padded to 8 channels so one 16-byte im2col chunk = one tap
@@ -66,16 +68,58 @@ def _bn_tensors(bn: nn.BatchNorm2d):
 class _TrunkFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, trunk, training, *params):
-        feats, saved = trunk_forward(trunk, x, training)
-        ctx.saved, ctx.trunk, ctx.training = saved, trunk, training
+        runner = trunk.graph_runner(x, training)
+        if runner is not None:
+            feats, saved = runner.forward(x)
+        else:
+            feats, saved = trunk_forward(trunk, x, training)
+        ctx.saved, ctx.trunk, ctx.training, ctx.runner = saved, trunk, training, runner
         return feats.view(feats.shape[0], feats.shape[1], 1, 1)
 
     @staticmethod
     def backward(ctx, dfeat):
-        grads = trunk_backward(ctx.trunk, ctx.saved, dfeat.reshape(dfeat.shape[0], -1).contiguous().float(),
-                               ctx.training)
+        dfeat = dfeat.reshape(dfeat.shape[0], -1).contiguous().float()
         params = list(ctx.trunk.parameters())
+        if ctx.runner is not None and ctx.runner.backward_graphable(params):
+            grads = ctx.runner.backward(dfeat, params)
+        else:
+            grads = trunk_backward(ctx.trunk, ctx.saved, dfeat, ctx.training)
         return (None, None, None, *[grads.get(id(q)) for q in params])
+
+
+class _TrunkGraphs:
+    """Captured forward / backward hipGraphs of one (input shape, mode) of the trunk (graphs.py).
+
+    Forward graph: pack input -> ... -> avgpool, with the per-step weight packing and the BatchNorm
+    running-stat updates inside it; its saved activations are graph-owned static tensors.  Backward
+    graph: the whole reverse schedule, writing every parameter gradient straight into the optimizer's
+    flat gradient buffer (``FusedAdam`` slots, fixed addresses); returned to autograd as fresh views.
+    """
+
+    def __init__(self, trunk, training):
+        self.trunk, self.training = trunk, training
+        self.fwd = None
+        self.bwd = None
+
+    def forward(self, x):
+        if self.fwd is None:
+            self.fwd = G.StaticGraph(lambda xx: trunk_forward(self.trunk, xx, self.training, force_pack=True), [x])
+        feats, saved = self.fwd.replay(x)
+        return feats.clone(), saved
+
+    @staticmethod
+    def backward_graphable(params) -> bool:
+        return all(q.grad is None and getattr(q, "_mer_grad_slot", None) is not None
+                   for q in params if q.requires_grad)
+
+    def backward(self, dfeat, params):
+        if self.bwd is None:
+            _, saved = self.fwd.out
+            self.bwd = G.StaticGraph(lambda d: trunk_backward(self.trunk, saved, d, self.training, force_pack=True),
+                                     [dfeat])
+        self.bwd.replay(dfeat)
+        from .fusion import grad_buffer  # fresh views of the flat-buffer slots the graph wrote
+        return {id(q): grad_buffer(q) for q in params if q.requires_grad}
 
 
 class ResNet18Trunk(nn.Sequential):
@@ -87,19 +131,31 @@ class ResNet18Trunk(nn.Sequential):
                          _layer(256, 512, 2), nn.AdaptiveAvgPool2d((1, 1)))
         _init_resnet(self)
         self._pack_cache = {}
+        self._force_pack = False
+        self._graphs = G.GraphCache()
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if not x.is_cuda:
             raise RuntimeError("ResNet18 trunk runs on the MI355X kernels; move the frames to the GPU")
         return _TrunkFn.apply(x.contiguous().float(), self, self.training, *self.parameters())
 
+    def graph_runner(self, x: torch.Tensor, training: bool):
+        """The captured-graph runner for this input shape / mode, or None while warming up (graphs.py)."""
+        if G.capturing():
+            return None
+        key = (tuple(x.shape), bool(training), x.device.index, G.tensor_addresses(self))
+        if not self._graphs.ready(key):
+            return None
+        r = self._graphs.get(key)
+        return r if r is not None else self._graphs.put(key, _TrunkGraphs(self, training))
+
     # ---- bf16 weight packing: per step in training (weights move), cached by version in eval ----
     def packed(self, conv: nn.Conv2d, cp: int, transpose: bool):
         w = conv.weight
         key = (id(conv), transpose)
-        ver = (w.data_ptr(), w._version)
+        ver = weight_version(w)
         hit = self._pack_cache.get(key)
-        if hit is not None and hit[0] == ver:
+        if hit is not None and hit[0] == ver and not self._force_pack:
             return hit[1]
         Kc, C, R, S = w.shape
         if not transpose:
@@ -172,8 +228,28 @@ def block_forward(trunk, blk: BasicBlock, x: torch.Tensor, training: bool, arena
     return out, (x, bc1, bms1, ba1, bc2, bms2, cd, msd, out)
 
 
+class _ForcePack:
+    """Inside a graph capture every weight pack must be a captured kernel (the graph replays it each step),
+    so the version-keyed pack cache is bypassed."""
+
+    def __init__(self, trunk, on):
+        self.trunk, self.on = trunk, on
+
+    def __enter__(self):
+        self.prev = self.trunk._force_pack
+        self.trunk._force_pack = self.on or self.prev
+
+    def __exit__(self, *exc):
+        self.trunk._force_pack = self.prev
+
+
 @torch.no_grad()
-def trunk_forward(trunk: ResNet18Trunk, video: torch.Tensor, training: bool):
+def trunk_forward(trunk: ResNet18Trunk, video: torch.Tensor, training: bool, force_pack: bool = False):
+    with _ForcePack(trunk, force_pack):
+        return _trunk_forward(trunk, video, training)
+
+
+def _trunk_forward(trunk: ResNet18Trunk, video: torch.Tensor, training: bool):
     N, C, H, W = video.shape
     dev = video.device
     bf = torch.bfloat16
@@ -288,7 +364,12 @@ def block_backward(trunk, blk: BasicBlock, sv, dx: torch.Tensor, grads, training
 
 
 @torch.no_grad()
-def trunk_backward(trunk: ResNet18Trunk, saved, dfeat: torch.Tensor, training: bool = True):
+def trunk_backward(trunk: ResNet18Trunk, saved, dfeat: torch.Tensor, training: bool = True, force_pack: bool = False):
+    with _ForcePack(trunk, force_pack):
+        return _trunk_backward(trunk, saved, dfeat, training)
+
+
+def _trunk_backward(trunk: ResNet18Trunk, saved, dfeat: torch.Tensor, training: bool = True):
     grads = {}
     dev = dfeat.device
     x = saved["final"]

@@ -23,8 +23,10 @@ import numpy as np
 import torch
 from torch import nn
 
+from . import graphs as G
 from . import kernels as K
 from .nn_ops import hip_dropout, hip_linear
+from .optim import weight_version
 from .temporal import TemporalPooler
 
 CONV_DIM = 512
@@ -140,10 +142,11 @@ class WavLMBackbone(nn.Module):
         self._packed = None
         self._packed_key = None
         self._buckets: Dict[tuple, torch.Tensor] = {}
+        self._graphs = G.GraphCache()
 
     # ---- frozen-weight preparation (runs once per weight version, on the GPU kernels) ----
     def _weights_key(self):
-        return tuple((q.data_ptr(), q._version) for q in self.parameters())
+        return tuple(weight_version(q) for q in self.parameters())
 
     @torch.no_grad()
     def packed_weights(self):
@@ -207,30 +210,70 @@ class WavLMBackbone(nn.Module):
         """Raw waveform [B, S] fp32 -> last_hidden_state [B, L, 768] (bf16 or fp32).
 
         ``capture`` (tests): receives copies of 'extract_features' (post-LN conv features, what HF
-        returns as ``extract_features``) and 'layer0' (output of encoder layer 0)."""
+        returns as ``extract_features``) and 'layer0' (output of encoder layer 0).
+
+        After two eager calls per input shape the schedule runs as two captured hipGraphs (graphs.py):
+        [conv0, GroupNorm+GELU] and [conv2 .. final LayerNorm], with the conv1 GEMM launched eagerly
+        between them (it is the kernel bench.py times with HIP events)."""
         if not wav.is_cuda:
             raise RuntimeError("WavLM runs on the MI355X kernels; move the waveform to the GPU")
-        cfg = self.config
-        pk = self.packed_weights()
         wav = wav.contiguous().float()
+        if capture is None and num_layers is None and not G.capturing():
+            key = (tuple(wav.shape), out_dtype, wav.device.index, self._weights_key())
+            if self._graphs.ready(key):
+                return self._forward_graphed(wav, out_dtype, key)
+        x, L = self._stage_a(wav)
+        y = self._conv_layer(x, 1, L)
+        return self._stage_b(y, L, out_dtype, num_layers, capture)
+
+    def _forward_graphed(self, wav, out_dtype, key):
+        g = self._graphs.get(key)
+        if g is None:
+            ga = G.StaticGraph(lambda w: self._stage_a(w)[0], [wav])
+            B, L0 = wav.shape[0], ga.out.shape[1]
+            L1 = (L0 - CONV_KERNEL[1]) // CONV_STRIDE[1] + 1
+            y1 = torch.empty(B, L1, CONV_DIM, device=wav.device, dtype=torch.bfloat16)
+            gb = G.StaticGraph(lambda: self._stage_b(y1, L0, out_dtype, None, None), [])
+            g = self._graphs.put(key, (ga, y1, gb))
+        ga, y1, gb = g
+        x = ga.replay(wav)
+        self._conv_layer(x, 1, x.shape[1], out=y1)
+        return gb.replay().clone()
+
+    def _stage_a(self, wav):
+        """conv0 (+ GroupNorm statistics) -> GroupNorm + GELU: [B, S] -> [B, L0, 512] bf16."""
+        pk = self.packed_weights()
         B, S = wav.shape
-        dev = wav.device
-        bf = torch.bfloat16
         L = (S - CONV_KERNEL[0]) // CONV_STRIDE[0] + 1
-        x = torch.empty(B, L, CONV_DIM, device=dev, dtype=bf)
-        stats = torch.zeros(B, CONV_DIM, 2, device=dev, dtype=torch.float32)
+        x = torch.empty(B, L, CONV_DIM, device=wav.device, dtype=torch.bfloat16)
+        stats = torch.zeros(B, CONV_DIM, 2, device=wav.device, dtype=torch.float32)
         K.wavlm_conv0(wav, pk["conv0_w"], x, stats)
         gn = self.feature_extractor.conv_layers[0].layer_norm
         xg = torch.empty_like(x)
         K.groupnorm_gelu(x, stats, gn.weight, gn.bias, xg, eps=gn.eps)
-        x = xg
-        for i in range(1, len(CONV_KERNEL)):
-            k, s = CONV_KERNEL[i], CONV_STRIDE[i]
-            L_out = (L - k) // s + 1
-            y = torch.empty(B, L_out, CONV_DIM, device=dev, dtype=bf)
-            K.gemm_bf16(x, pk["conv"][i - 1], y, M=B * L_out, K=k * CONV_DIM,
-                        rows=(L_out, s * CONV_DIM, L * CONV_DIM), act="gelu")
-            x, L = y, L_out
+        return xg, L
+
+    def _conv_layer(self, x, i, L, out=None):
+        """Feature-extractor conv i >= 1 as an implicit GEMM with fused GELU (TF:723-782)."""
+        k, s = CONV_KERNEL[i], CONV_STRIDE[i]
+        B = x.shape[0]
+        L_out = (L - k) // s + 1
+        y = out if out is not None else torch.empty(B, L_out, CONV_DIM, device=x.device, dtype=torch.bfloat16)
+        K.gemm_bf16(x, self.packed_weights()["conv"][i - 1], y, M=B * L_out, K=k * CONV_DIM,
+                    rows=(L_out, s * CONV_DIM, L * CONV_DIM), act="gelu")
+        return y
+
+    def _stage_b(self, x, L0, out_dtype, num_layers, capture):
+        """conv2..6 -> feature projection -> positional conv -> 12 encoder layers (x = conv1 output)."""
+        cfg = self.config
+        pk = self.packed_weights()
+        B = x.shape[0]
+        dev = x.device
+        bf = torch.bfloat16
+        L = (L0 - CONV_KERNEL[1]) // CONV_STRIDE[1] + 1
+        for i in range(2, len(CONV_KERNEL)):
+            x = self._conv_layer(x, i, L)
+            L = x.shape[1]
         D = cfg.hidden_size
         fp = self.feature_projection
         xn = torch.empty(B * L, CONV_DIM, device=dev, dtype=bf)

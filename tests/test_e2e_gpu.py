@@ -80,6 +80,12 @@ def test_train_step_vs_oracle():
     # frozen encoder untouched
     k = "audio_model.wavlm.encoder.layers.0.attention.q_proj.weight"
     assert torch.equal(after[k], before[k])
+    # second step: its forward must see the Adam-updated conv weights (the bf16 weight packs are derived
+    # copies; a stale pack shows up as a loss that stays at the first step's value)
+    loss2, _ = step(video.cuda(), audio.cuda(), labels.cuda())
+    rloss2 = train_ref.train_step(p, trainable, ropt, video, audio, labels)
+    print("step-2 loss hip/oracle", float(loss2), rloss2)
+    assert abs(float(loss2) - rloss2) < 2e-2
 
 
 @pytest.mark.parametrize("int8", [False, True])
