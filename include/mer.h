@@ -150,13 +150,13 @@ int mer_posconv_gemm_bf16(int B, int L, int C_total, int groups, int taps, int p
                           const void* Wp, void* out, int out_dtype, long ldo, const float* bias, const void* R,
                           long ldr, int act, void* stream);
 
-/* WavLM feature-extractor conv0 (TF:723-745): Conv1d(1,512,k=10,s=5) of wav [B,S] fp32 -> bf16 [B,Lout,512],
- * plus GroupNorm statistics stats[b][c] = (sum, sum of squares) accumulated (pre-zero stats). */
-int mer_wavlm_conv0(int B, int S, int Lout, const float* wav, const float* w0, void* out, float* stats, void* stream);
-
-/* GroupNorm(C, C) apply + GELU from those statistics (bf16 in/out, channel-last [B,L,C]). */
-int mer_groupnorm_gelu(int B, int L, int C, const void* x, const float* stats, const float* gamma, const float* beta,
-                       float eps, void* y, void* stream);
+/* WavLM feature-extractor layer 0 (TF:723-745): Conv1d(1,512,k=10,s=5,no bias) of wav [B,S] fp32 ->
+ * GroupNorm(512,512) (per (clip, channel) statistics over time of the bf16-rounded conv output) -> GELU,
+ * written once as bf16 [B,Lout,512].  Two passes over the (cheap: 10 taps) conv: statistics into per-tile
+ * partial rows, reduced in a fixed order (deterministic, no atomics), then conv recompute + normalise +
+ * GELU.  workspace: float[B * (ceil(Lout/128) + 1) * 1024]. */
+int mer_wavlm_conv0_gn_gelu(int B, int S, int Lout, const float* wav, const float* w0, const float* gamma,
+                            const float* beta, float eps, float* workspace, void* out, void* stream);
 
 /* Row LayerNorm (nn.LayerNorm(d), TF:93-105, 314-336, 418): x (x_dtype) -> y (y_dtype), d <= 1024. */
 int mer_layernorm(int rows, int d, const void* x, int x_dtype, long ldx, const float* gamma, const float* beta,

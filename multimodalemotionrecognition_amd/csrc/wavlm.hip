@@ -6,99 +6,117 @@
 typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;
 
 // ---------------------------------------------------------------------------------------
-// conv0 of the feature extractor (TF:723-745): Conv1d(1, 512, k=10, s=5, bias=False) on the raw
-// waveform, channel-last bf16 output [B, Lout, 512], fused with the GroupNorm(512, 512) statistics
-// (per (b, c) sum and sum of squares over time, fp32 atomics into stats[b][c][2], pre-zeroed).
-// Bandwidth-bound direct conv: one block = 32 output steps of one clip, 2 channels per thread.
+// Feature-extractor layer 0 (TF:723-745): conv0 = Conv1d(1, 512, k=10, s=5, bias=False) on the raw
+// waveform, GroupNorm(512, 512) over time per (clip, channel), GELU; channel-last bf16 output.
+// The conv is 10 MACs per output, so instead of writing the conv output, reading it back for the
+// statistics and again for the normalisation (3 x 314 MB at B=32), pass 1 computes the conv tile by
+// tile and keeps only per-tile partial (sum, sumsq) rows, a finalize reduces them in a fixed order
+// (deterministic), and pass 2 recomputes the conv, normalises, applies GELU and writes once.
+// Statistics are taken over the bf16-ROUNDED conv outputs, the values GroupNorm sees in the bf16 path.
+// Block = 128 output steps of one clip, 2 channels per thread (256 threads x 2 = 512 channels).
 // ---------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void wavlm_conv0_kernel(int S, int Lout, const float* __restrict__ wav,
-                                                          const float* __restrict__ w, bf16_t* __restrict__ out,
-                                                          float* __restrict__ stats) {
-  constexpr int TS = 32, KW = 10, ST = 5;
-  __shared__ float xs[TS * ST + KW];
-  const int b = blockIdx.y, t0 = blockIdx.x * TS;
-  const float* x = wav + (long)b * S;
-  for (int i = threadIdx.x; i < TS * ST + KW; i += 256) {
-    const long si = (long)t0 * ST + i;
+namespace {
+constexpr int C0_TS = 128, C0_KW = 10, C0_ST = 5;
+
+__device__ __forceinline__ void conv0_tile_load(const float* __restrict__ x, int S, int t0, float* xs) {
+  for (int i = threadIdx.x; i < C0_TS * C0_ST + C0_KW; i += blockDim.x) {
+    const long si = (long)t0 * C0_ST + i;
     xs[i] = si < S ? x[si] : 0.f;
   }
-  float wr[2][KW];
+}
+}  // namespace
+
+__global__ __launch_bounds__(256) void wavlm_conv0_stats_kernel(int S, int Lout, const float* __restrict__ wav,
+                                                                const float* __restrict__ w,
+                                                                float* __restrict__ part) {
+  __shared__ float xs[C0_TS * C0_ST + C0_KW];
+  const int b = blockIdx.y, t0 = blockIdx.x * C0_TS;
+  conv0_tile_load(wav + (long)b * S, S, t0, xs);
+  float wr[2][C0_KW];
   const int c0 = threadIdx.x, c1 = threadIdx.x + 256;
 #pragma unroll
-  for (int k = 0; k < KW; ++k) { wr[0][k] = w[c0 * KW + k]; wr[1][k] = w[c1 * KW + k]; }
+  for (int k = 0; k < C0_KW; ++k) { wr[0][k] = w[c0 * C0_KW + k]; wr[1][k] = w[c1 * C0_KW + k]; }
   __syncthreads();
   float s0 = 0.f, q0 = 0.f, s1 = 0.f, q1 = 0.f;
-  const int tn = min(TS, Lout - t0);
+  const int tn = min(C0_TS, Lout - t0);
   for (int tt = 0; tt < tn; ++tt) {
     float a0 = 0.f, a1 = 0.f;
 #pragma unroll
-    for (int k = 0; k < KW; ++k) {
-      const float xv = xs[tt * ST + k];
+    for (int k = 0; k < C0_KW; ++k) {
+      const float xv = xs[tt * C0_ST + k];
       a0 += wr[0][k] * xv;
       a1 += wr[1][k] * xv;
     }
-    const bf16_t h0 = f2bf(a0), h1 = f2bf(a1);
-    bf16_t* o = out + ((long)b * Lout + t0 + tt) * 512;
-    o[c0] = h0;
-    o[c1] = h1;
-    // statistics of the values GroupNorm will actually see (the bf16-rounded activations)
-    const float r0 = bf2f(h0), r1 = bf2f(h1);
+    const float r0 = bf2f(f2bf(a0)), r1 = bf2f(f2bf(a1));
     s0 += r0; q0 += r0 * r0; s1 += r1; q1 += r1 * r1;
   }
-  float* st = stats + (long)b * 512 * 2;
-  atomicAdd(st + c0 * 2, s0);
-  atomicAdd(st + c0 * 2 + 1, q0);
-  atomicAdd(st + c1 * 2, s1);
-  atomicAdd(st + c1 * 2 + 1, q1);
+  float* pr = part + ((long)b * gridDim.x + blockIdx.x) * 1024;
+  pr[c0 * 2] = s0;
+  pr[c0 * 2 + 1] = q0;
+  pr[c1 * 2] = s1;
+  pr[c1 * 2 + 1] = q1;
 }
 
-MER_API int mer_wavlm_conv0(int B, int S, int Lout, const float* wav, const float* w0, void* out, float* stats,
-                            void* stream) {
-  if (Lout != (S - 10) / 5 + 1) return (int)hipErrorInvalidValue;
-  dim3 grid((Lout + 31) / 32, B);
-  hipLaunchKernelGGL(wavlm_conv0_kernel, grid, dim3(256), 0, (hipStream_t)stream, S, Lout, wav, w0, (bf16_t*)out, stats);
-  MER_LAUNCH_CHECK();
-}
-
-// GroupNorm(C, C) apply + GELU (TF:740-745): y = gelu((x - mu_bc) * rstd_bc * gamma_c + beta_c), bf16 in/out,
-// 8 channels (16 B) per thread.
-__global__ __launch_bounds__(256) void gn_gelu_kernel(int B, int L, int C, const bf16_t* __restrict__ x,
-                                                      const float* __restrict__ stats, const float* __restrict__ gamma,
-                                                      const float* __restrict__ beta, float eps, bf16_t* __restrict__ y) {
-  // clip b = blockIdx.y; 256 % (C/8) == 0 so each thread owns fixed channels: hoist scale/shift
-  const int b = blockIdx.y;
-  const int nvec = L * C / 8;
-  const int tid0 = blockIdx.x * blockDim.x + threadIdx.x;
-  const int c0 = (tid0 % (C / 8)) * 8;
-  float sc[8], sh[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int c = c0 + i;
-    const float mu = stats[((long)b * C + c) * 2] / L;
-    const float var = fmaxf(stats[((long)b * C + c) * 2 + 1] / L - mu * mu, 0.f);
-    sc[i] = rsqrtf(var + eps) * gamma[c];
-    sh[i] = beta[c] - mu * sc[i];
+// coef[b][c] = (scale, shift) of GroupNorm from the tile partials, summed in tile order
+__global__ __launch_bounds__(256) void wavlm_gn_finalize_kernel(int ntiles, int Lout, const float* __restrict__ part,
+                                                                const float* __restrict__ gamma,
+                                                                const float* __restrict__ beta, float eps,
+                                                                float* __restrict__ coef) {
+  const int b = blockIdx.y, c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= 512) return;
+  const float* p = part + (long)b * ntiles * 1024 + c * 2;
+  float s = 0.f, q = 0.f;
+  for (int t = 0; t < ntiles; ++t) {
+    s += p[(long)t * 1024];
+    q += p[(long)t * 1024 + 1];
   }
-  const bf16_t* xb = x + (long)b * L * C;
-  bf16_t* yb = y + (long)b * L * C;
-  for (int e = tid0; e < nvec; e += gridDim.x * blockDim.x) {
-    u32x4 v = *reinterpret_cast<const u32x4*>(xb + (long)e * 8);
-    const bf16_t* hv = reinterpret_cast<const bf16_t*>(&v);
-    u32x4 o;
-    bf16_t* ho = reinterpret_cast<bf16_t*>(&o);
+  const float mu = s / Lout;
+  const float var = fmaxf(q / Lout - mu * mu, 0.f);
+  const float sc = rsqrtf(var + eps) * gamma[c];
+  coef[((long)b * 512 + c) * 2] = sc;
+  coef[((long)b * 512 + c) * 2 + 1] = beta[c] - mu * sc;
+}
+
+__global__ __launch_bounds__(256) void wavlm_conv0_gn_gelu_kernel(int S, int Lout, const float* __restrict__ wav,
+                                                                  const float* __restrict__ w,
+                                                                  const float* __restrict__ coef,
+                                                                  bf16_t* __restrict__ out) {
+  __shared__ float xs[C0_TS * C0_ST + C0_KW];
+  const int b = blockIdx.y, t0 = blockIdx.x * C0_TS;
+  conv0_tile_load(wav + (long)b * S, S, t0, xs);
+  float wr[2][C0_KW];
+  const int c0 = threadIdx.x, c1 = threadIdx.x + 256;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) ho[i] = f2bf(gelu_erf(bf2f(hv[i]) * sc[i] + sh[i]));
-    *reinterpret_cast<u32x4*>(yb + (long)e * 8) = o;
+  for (int k = 0; k < C0_KW; ++k) { wr[0][k] = w[c0 * C0_KW + k]; wr[1][k] = w[c1 * C0_KW + k]; }
+  const float* cf = coef + (long)b * 1024;
+  const float sc0 = cf[c0 * 2], sh0 = cf[c0 * 2 + 1], sc1 = cf[c1 * 2], sh1 = cf[c1 * 2 + 1];
+  __syncthreads();
+  const int tn = min(C0_TS, Lout - t0);
+  for (int tt = 0; tt < tn; ++tt) {
+    float a0 = 0.f, a1 = 0.f;
+#pragma unroll
+    for (int k = 0; k < C0_KW; ++k) {
+      const float xv = xs[tt * C0_ST + k];
+      a0 += wr[0][k] * xv;
+      a1 += wr[1][k] * xv;
+    }
+    bf16_t* o = out + ((long)b * Lout + t0 + tt) * 512;
+    o[c0] = f2bf(gelu_erf(bf2f(f2bf(a0)) * sc0 + sh0));
+    o[c1] = f2bf(gelu_erf(bf2f(f2bf(a1)) * sc1 + sh1));
   }
 }
 
-MER_API int mer_groupnorm_gelu(int B, int L, int C, const void* x, const float* stats, const float* gamma,
-                               const float* beta, float eps, void* y, void* stream) {
-  if (C % 8 || 256 % (C / 8)) return (int)hipErrorInvalidValue;
-  const long nvec = (long)L * C / 8;
-  dim3 grid((unsigned)((nvec + 255) / 256 < 1024 ? (nvec + 255) / 256 : 1024), B);
-  hipLaunchKernelGGL(gn_gelu_kernel, grid, dim3(256), 0, (hipStream_t)stream, B, L, C, (const bf16_t*)x, stats,
-                     gamma, beta, eps, (bf16_t*)y);
+MER_API int mer_wavlm_conv0_gn_gelu(int B, int S, int Lout, const float* wav, const float* w0, const float* gamma,
+                                    const float* beta, float eps, float* workspace, void* out, void* stream) {
+  if (B <= 0 || Lout != (S - C0_KW) / C0_ST + 1) return (int)hipErrorInvalidValue;
+  const int ntiles = (Lout + C0_TS - 1) / C0_TS;
+  float* part = workspace;                             // [B][ntiles][512][2]
+  float* coef = workspace + (long)B * ntiles * 1024;   // [B][512][2]
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(wavlm_conv0_stats_kernel, dim3(ntiles, B), dim3(256), 0, st, S, Lout, wav, w0, part);
+  hipLaunchKernelGGL(wavlm_gn_finalize_kernel, dim3(2, B), dim3(256), 0, st, ntiles, Lout, part, gamma, beta, eps, coef);
+  hipLaunchKernelGGL(wavlm_conv0_gn_gelu_kernel, dim3(ntiles, B), dim3(256), 0, st, S, Lout, wav, w0, coef,
+                     (bf16_t*)out);
   MER_LAUNCH_CHECK();
 }
 

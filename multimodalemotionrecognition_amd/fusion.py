@@ -41,6 +41,10 @@ def _side_stream(device: torch.device):
     return s
 
 
+def _audio_key(audio: torch.Tensor) -> tuple:
+    return (audio.data_ptr(), audio._version, tuple(audio.shape), audio.dtype)
+
+
 def _next_seed() -> int:
     # host-side draw so that torch.manual_seed() makes runs reproducible (train.py:951 set_seed)
     return int(torch.randint(0, 2 ** 62, (1,)).item())
@@ -172,6 +176,7 @@ class FusionModel(nn.Module):
         self.semantic_alignment = None
         self.xattn_use_emotion_prior = xattn_use_emotion_prior
         self.num_classes = num_classes
+        self._prefetched = None  # (audio key, encoder output, stream) from prefetch_audio()
 
         if mode in {"concat", "gated"}:
             fusion_audio_dim = audio_model.embedding_dim
@@ -233,6 +238,26 @@ class FusionModel(nn.Module):
                     self.xattn_gate[0].bias.fill_(-1.0)
                     self.xattn_gate[3].bias.fill_(-1.0)
 
+    def audio_encoder_frozen(self) -> bool:
+        enc = getattr(self.audio_model, "wavlm", None)
+        return enc is not None and not any(q.requires_grad for q in enc.parameters())
+
+    def prefetch_audio(self, audio: torch.Tensor) -> bool:
+        """Start the frozen audio encoder on the NEXT batch's waveform, on the side stream, so it runs
+        concurrently with this step's backward (the encoder's output does not depend on the weights the
+        step updates).  The next ``forward`` whose ``audio`` is this same tensor (same storage, shape and
+        version) consumes the result; any other input runs the encoder inline as usual.  Returns whether
+        the prefetch was issued (xattn mode with a frozen WavLM encoder only)."""
+        if self.mode not in {"xattn", "xattn_concat", "xattn_gated"} or not self.audio_encoder_frozen():
+            return False
+        _require_device(audio)
+        side = _side_stream(audio.device)
+        side.wait_stream(torch.cuda.current_stream(audio.device))
+        with torch.cuda.stream(side):
+            a_seq = self.audio_model.encode_sequence(audio)
+        self._prefetched = (_audio_key(audio), a_seq, side)
+        return True
+
     def pop_alignment_loss(self) -> Optional[torch.Tensor]:
         loss = self.alignment_loss
         self.alignment_loss = None
@@ -287,7 +312,17 @@ class FusionModel(nn.Module):
                                           "path is WavLM encode_sequence")
             # The two encoders are independent until the xattn block (fusion.py:369-378): the (frozen,
             # forward-only) audio encoder runs on a side HIP stream concurrently with the frame trunk, so
-            # its GEMMs fill the CUs the trunk's smaller convs and BatchNorm passes leave idle.
+            # its GEMMs fill the CUs the trunk's smaller convs and BatchNorm passes leave idle.  When
+            # prefetch_audio() already started it for this very batch (during the previous step's
+            # backward), its result is taken over instead.
+            pf, self._prefetched = self._prefetched, None
+            if pf is not None and pf[0] == _audio_key(audio):
+                a_seq, side = pf[1], pf[2]
+                v_feat = self.video_model.backbone(v_in).view(b, t, self.v_dim)
+                cur = torch.cuda.current_stream(video.device)
+                cur.wait_stream(side)
+                a_seq.record_stream(cur)
+                return self.xattn_from_features(v_feat, a_seq)
             side = _side_stream(video.device) if _OVERLAP_ENCODERS else None
             if side is not None:
                 cur = torch.cuda.current_stream(video.device)

@@ -264,16 +264,15 @@ def posconv_gemm_bf16(x, wp, out, B, L, C, groups, taps, pad, bias, residual, ac
         ACT[act], stream_ptr())
 
 
-def wavlm_conv0(wav, w0, out, stats):
+def wavlm_conv0_gn_gelu(wav, w0, gamma, beta, out, eps=1e-5):
+    """conv0 -> GroupNorm(512, 512) -> GELU of the WavLM feature extractor (deterministic two-pass)."""
     B, S = wav.shape
     Lout = out.shape[1]
-    LIB("mer_wavlm_conv0", B, S, Lout, wav.data_ptr(), w0.data_ptr(), out.data_ptr(), stats.data_ptr(), stream_ptr())
-
-
-def groupnorm_gelu(x, stats, gamma, beta, y, eps=1e-5):
-    B, L, C = x.shape
-    LIB("mer_groupnorm_gelu", B, L, C, x.data_ptr(), stats.data_ptr(), gamma.data_ptr(), beta.data_ptr(), float(eps),
-        y.data_ptr(), stream_ptr())
+    if tuple(out.shape) != (B, (S - 10) // 5 + 1, 512) or out.dtype != torch.bfloat16:
+        raise ValueError(f"wavlm_conv0_gn_gelu out {tuple(out.shape)}")
+    ws = torch.empty(B * ((Lout + 127) // 128 + 1) * 1024, device=wav.device, dtype=torch.float32)
+    LIB("mer_wavlm_conv0_gn_gelu", B, S, Lout, wav.data_ptr(), w0.data_ptr(), gamma.data_ptr(), beta.data_ptr(),
+        float(eps), ws.data_ptr(), out.data_ptr(), stream_ptr())
 
 
 def layernorm(x2d, gamma, beta, y2d, eps=1e-5):

@@ -83,7 +83,11 @@ class TrainStep:
         self.model, self.opt, self.loss_fn, self.mode = model, optimizer, loss_fn, fusion_mode
         self.grad_sync = grad_sync
 
-    def __call__(self, video: torch.Tensor, audio: torch.Tensor, labels: torch.Tensor):
+    def __call__(self, video: torch.Tensor, audio: torch.Tensor, labels: torch.Tensor,
+                 next_audio: Optional[torch.Tensor] = None):
+        """``next_audio``: the NEXT step's waveform batch, already on the device.  With a frozen audio
+        encoder its forward is started on a side stream right after this step's forward, so it overlaps
+        this step's backward (``FusionModel.prefetch_audio``); results are identical either way."""
         self.model.train()
         self.opt.zero_grad()
         if self.mode in {"audio", "video"}:
@@ -91,6 +95,8 @@ class TrainStep:
         else:
             outputs = self.model(video, audio)
         loss = self.loss_fn(outputs, labels)
+        if next_audio is not None and hasattr(self.model, "prefetch_audio"):
+            self.model.prefetch_audio(next_audio)
         loss.backward()
         if self.grad_sync is not None:
             self.grad_sync()
@@ -105,9 +111,17 @@ def train_one_epoch(model: nn.Module, loader, optimizer: FusedAdam, device: torc
     step = TrainStep(model, optimizer, loss_fn, fusion_mode, grad_sync)
     losses, preds, targets = [], [], []
     n = 0
-    for video, audio, labels, _ in loader:
+    it = iter(loader)
+    nxt = next(it, None)
+    while nxt is not None:
+        video, audio, labels, _ = nxt
         video, audio, labels = video.to(device), audio.to(device), labels.to(device)
-        loss, pred = step(video, audio, labels)
+        nxt = next(it, None)  # one batch of lookahead: its audio feeds the encoder prefetch
+        nxt_audio = None
+        if nxt is not None:
+            nxt = (nxt[0], nxt[1].to(device), nxt[2], nxt[3])
+            nxt_audio = nxt[1]
+        loss, pred = step(video, audio, labels, next_audio=nxt_audio)
         losses.append(loss * labels.numel())
         preds.append(pred)
         targets.append(labels)

@@ -8,7 +8,7 @@ its own offline fallback to exactly this, wavlm_audio.py:35-41).
 
 Forward (``encode_sequence``, wavlm_audio.py:165-183 -> TF:1032-1085), all bf16 activations with
 fp32 accumulation:
-  conv0 (direct, + GroupNorm stats) -> GroupNorm+GELU -> conv1..6 (Conv1d-as-GEMM, GELU epilogue)
+  conv0 + GroupNorm + GELU (two-pass, deterministic) -> conv1..6 (Conv1d-as-GEMM, GELU epilogue)
   -> LayerNorm(512) -> projection GEMM -> grouped pos-conv GEMM (+GELU +residual) -> LayerNorm
   -> 12 x [fused QKV GEMM -> gated-rel-pos attention -> out-proj GEMM (+residual) -> LN
            -> FFN GEMM (+GELU) -> FFN GEMM (+residual) -> LN]
@@ -241,16 +241,13 @@ class WavLMBackbone(nn.Module):
         return gb.replay().clone()
 
     def _stage_a(self, wav):
-        """conv0 (+ GroupNorm statistics) -> GroupNorm + GELU: [B, S] -> [B, L0, 512] bf16."""
+        """conv0 -> GroupNorm + GELU (one fused deterministic kernel pair): [B, S] -> [B, L0, 512] bf16."""
         pk = self.packed_weights()
         B, S = wav.shape
         L = (S - CONV_KERNEL[0]) // CONV_STRIDE[0] + 1
-        x = torch.empty(B, L, CONV_DIM, device=wav.device, dtype=torch.bfloat16)
-        stats = torch.zeros(B, CONV_DIM, 2, device=wav.device, dtype=torch.float32)
-        K.wavlm_conv0(wav, pk["conv0_w"], x, stats)
+        xg = torch.empty(B, L, CONV_DIM, device=wav.device, dtype=torch.bfloat16)
         gn = self.feature_extractor.conv_layers[0].layer_norm
-        xg = torch.empty_like(x)
-        K.groupnorm_gelu(x, stats, gn.weight, gn.bias, xg, eps=gn.eps)
+        K.wavlm_conv0_gn_gelu(wav, pk["conv0_w"], gn.weight, gn.bias, xg, eps=gn.eps)
         return xg, L
 
     def _conv_layer(self, x, i, L, out=None):

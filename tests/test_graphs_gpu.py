@@ -1,10 +1,10 @@
 """Captured hipGraphs (graphs.py) replay exactly the eager launch schedule.
 
-* WavLM forward: graph replays are bit-identical to the eager forward (same kernels, no atomics).
-* Full train step (ResNet18 trunk fwd/bwd graphs + eager head + FusedAdam): parameters after several
-  steps match an eager-only twin model within fp32 reassociation noise (the BatchNorm statistics use
-  striped fp32 atomics, so bitwise equality is not expected), and BN running statistics advance once per
-  step in both.
+* WavLM forward: graph replays agree with the eager forward as closely as two eager runs agree.
+* Full train step (ResNet18 trunk fwd/bwd graphs + eager head + FusedAdam): loss and gradients match the
+  eager schedule at identical weights within fp32 reassociation noise (the BatchNorm statistics use
+  striped fp32 atomics, so bitwise equality is not expected); BN running statistics advance once per step.
+* Audio prefetch: the next batch's WavLM features (computed during the backward) are bit-identical.
 """
 import pytest
 import torch
@@ -62,34 +62,78 @@ def _twin(seed):
 
 
 def test_train_step_graphs_match_eager():
+    """Graphed train step vs the eager schedule at IDENTICAL weights: the graphed model runs three steps
+    (eager, capture + replay, replay -- its Adam updates exercise the per-step weight re-packing inside
+    the graphs), its state is copied into an eager twin, then both run one forward + backward on the same
+    batch.  Loss and every parameter gradient must agree up to the run-to-run noise of the fp32-atomic
+    BatchNorm statistics (gradient norms within 1e-2 relative)."""
     prev = G.ENABLED
     try:
-        G.ENABLED = False
-        me, se = _twin(7)
         G.ENABLED = True
         mg, sg = _twin(7)
         video, audio, labels = bench.synthetic_batch(torch.device("cuda"), 5)
         video, audio, labels = video[:4], audio[:4], labels[:4]
-        for it in range(4):
-            G.ENABLED = False
-            le, _ = se(video, audio, labels)
-            G.ENABLED = True
-            lg, _ = sg(video, audio, labels)
-            # fp32-atomic BN statistics: two eager runs drift apart by ~1e-3 in the loss after 4 steps
-            assert abs(float(le) - float(lg)) < 1e-2 * max(1.0, abs(float(le))), (it, float(le), float(lg))
+        for _ in range(3):
+            sg(video, audio, labels)
         assert mg.video_model.backbone._graphs.graphs, "trunk graphs were not captured"
         assert mg.audio_model.wavlm._graphs.graphs, "WavLM graphs were not captured"
-        se_sd, sg_sd = me.state_dict(), mg.state_dict()
-        for k, v in se_sd.items():
-            w = sg_sd[k]
-            if v.dtype in (torch.int64,):
-                assert torch.equal(v, w), k
-                continue
-            d = (v.float() - w.float()).abs()
-            # Adam moves each weight by <= ~lr per step: a near-zero gradient whose sign differs between
-            # the two (atomic-order) runs moves it by <= 2*lr per step; the bulk must agree closely
-            assert float(d.max()) <= 6 * 2e-3 + 1e-5 * float(v.abs().max()), k
-            assert float(d.mean()) <= 1e-4 + 1e-5 * float(v.abs().mean()), k
-        assert int(sg_sd["video_model.backbone.1.num_batches_tracked"]) == 4
+        assert int(mg.state_dict()["video_model.backbone.1.num_batches_tracked"]) == 3
+        G.ENABLED = False
+        me, se = _twin(8)
+        me.load_state_dict(mg.state_dict())
+        grads = {}
+        for tag, m, st, on in (("graph", mg, sg, True), ("eager", me, se, False), ("eager2", me, se, False)):
+            G.ENABLED = on
+            m.train()
+            st.opt.zero_grad()
+            loss = st.loss_fn(m(video, audio), labels)
+            loss.backward()
+            grads[tag] = (float(loss), {n: q.grad.detach().clone() for n, q in m.named_parameters()
+                                        if q.grad is not None})
+        (lg, gg), (le, ge), (le2, ge2) = grads["graph"], grads["eager"], grads["eager2"]
+        assert abs(lg - le) < 1e-3 * max(1.0, abs(le)), (lg, le)
+        assert set(gg) == set(ge) and len(gg) > 60
+        worst = []
+        for n in ge:
+            den = max(float(ge[n].norm()), 1e-6)
+            d_graph = float((gg[n] - ge[n]).norm()) / den
+            d_noise = float((ge2[n] - ge[n]).norm()) / den  # eager-vs-eager: the atomic-order noise floor
+            worst.append((d_graph, d_noise, n))
+            assert d_graph <= 4 * d_noise + 2e-3, (n, d_graph, d_noise)
+        print("worst graph-vs-eager gradient differences (rel, noise floor):", sorted(worst)[-3:])
+    finally:
+        G.ENABLED = prev
+
+
+def test_audio_prefetch_matches_inline():
+    """TrainStep(next_audio=...) runs the frozen WavLM of the next batch during this step's backward.
+    The WavLM path is deterministic, so the prefetched features must be bit-identical to an inline
+    encode of the same waveform; a prefetch is used only for the very tensor it was computed from."""
+    prev = G.ENABLED
+    try:
+        G.ENABLED = True
+        mb, sb = _twin(11)
+        video, audio, labels = bench.synthetic_batch(torch.device("cuda"), 6)
+        v1, a1, y1 = video[:4], audio[:4].clone(), labels[:4]
+        v2, a2, y2 = video[4:8], audio[4:8].clone(), labels[4:8]
+        seen = []
+        orig = mb.xattn_from_features
+        mb.xattn_from_features = lambda v, a: (seen.append(a.detach().clone()), orig(v, a))[1]
+        seq = [(v1, a1, y1), (v2, a2, y2), (v1, a1, y1)]
+        for i, (v, a, y) in enumerate(seq):
+            nxt = seq[i + 1][1] if i + 1 < len(seq) else None
+            sb(v, a, y, next_audio=nxt)
+        assert mb._prefetched is None  # consumed
+        for (v, a, y), feats in zip(seq, seen):
+            with torch.no_grad():
+                ref = mb.audio_model.encode_sequence(a)
+            assert torch.equal(feats, ref)
+        # a prefetch for a tensor that is then modified in place is not used
+        mb.prefetch_audio(a2)
+        a2.mul_(0.5)
+        seen.clear()
+        sb(v2, a2, y2)
+        with torch.no_grad():
+            assert torch.equal(seen[0], mb.audio_model.encode_sequence(a2))
     finally:
         G.ENABLED = prev
