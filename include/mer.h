@@ -16,6 +16,8 @@
  *   - element strides/leading dimensions are in ELEMENTS; dtype codes: 0 = fp32, 1 = bf16;
  *   - activation codes: 0 none, 1 ReLU, 2 exact-erf GELU.
  * Plain C types only: int = int32, long = int64, unsigned long long = uint64 (RNG seeds).
+ * Dropout / drop-path RNG: `seed` points to the step's uint64 RNG base in DEVICE memory (NULL when p == 0),
+ * `site` is a constant per call site; masks are hash(base, site, element) and are regenerated in backward.
  */
 #ifndef MER_H_
 #define MER_H_
@@ -50,7 +52,7 @@ int mer_colsum_f32(int M, int N, const float* X, long ldx, float* out, void* str
  * MFMA (v_mfma_f32_16x16x4_f32).  Limits: dh % 4 == 0, dh <= 64, Lk <= 256 (hipErrorInvalidValue else). */
 int mer_mha_fwd(int B, int H, int Lq, int Lk, int dh, const float* Q, long ldq, const float* K, long ldk,
                 const float* V, long ldv, const float* bias, float* O, long ldo, float* P, float scale, float drop_p,
-                unsigned long long seed, void* stream);
+                const unsigned long long* seed, unsigned long long site, void* stream);
 
 /* Backward of mer_mha_fwd: writes dQ, dK, dV (not accumulated) and dbias[b] = sum_h dS (if non-NULL).
  * One workgroup per (b, h), all four products on the f32 MFMA.  When dbias is requested, P is overwritten
@@ -58,18 +60,18 @@ int mer_mha_fwd(int B, int H, int Lq, int Lk, int dh, const float* Q, long ldq, 
  * LDS image 4*(Lq+Lk)*dh + 2*Lq*Lk floats (padded) must fit in 160 KiB. */
 int mer_mha_bwd(int B, int H, int Lq, int Lk, int dh, const float* Q, long ldq, const float* K, long ldk,
                 const float* V, long ldv, float* P, const float* dO, long lddo, float* dQ, long lddq, float* dK,
-                long lddk, float* dV, long lddv, float* dbias, float scale, float drop_p, unsigned long long seed,
+                long lddk, float* dV, long lddv, float* dbias, float scale, float drop_p, const unsigned long long* seed, unsigned long long site,
                 void* stream);
 
 /* y = LayerNorm(x + s_b * r) with StochasticDepth scale s_b regenerated from (seed, row/rows_per_sample)
  * (fusion.py:11-26, 284-285, 395, 399).  r may be NULL.  Saves sum/mean/rstd when non-NULL. */
 int mer_add_ln_fwd(int rows, int d, int rows_per_sample, const float* x, const float* r, float dp_p,
-                   unsigned long long seed, const float* gamma, const float* beta, float eps, float* y, float* sum_out,
+                   const unsigned long long* seed, unsigned long long site, const float* gamma, const float* beta, float eps, float* y, float* sum_out,
                    float* mean_out, float* rstd_out, void* stream);
 
 /* Backward of mer_add_ln_fwd: dx = dsum, dr = s_b*dsum (dr may be NULL); dgamma/dbeta accumulate. */
 int mer_add_ln_bwd(int rows, int d, int rows_per_sample, const float* dy, const float* s, const float* mean,
-                   const float* rstd, const float* gamma, float dp_p, unsigned long long seed, float* dx, float* dr,
+                   const float* rstd, const float* gamma, float dp_p, const unsigned long long* seed, unsigned long long site, float* dx, float* dr,
                    float* dgamma, float* dbeta, void* stream);
 
 /* TemporalPooler 'mean' (temporal.py:108-109): y[b*ldy + c] = mean_l x[b,l,c]; and its backward. */
@@ -81,15 +83,18 @@ int mer_mean_pool_bwd(int B, int L, int D, const float* dy, long lddy, float* dx
 int mer_cross_entropy(int B, int C, const float* logits, const long long* labels, float label_smoothing, int late,
                       float* loss, float* dlogits, void* stream);
 
+/* state = splitmix64(state + golden): the next step's RNG base, computed on the device (graph-capturable). */
+int mer_rng_advance(unsigned long long* state, void* stream);
+
 /* y = x * s[0] with s a device scalar (autograd grad_output of the loss). */
 int mer_scale_dev(long n, const float* x, const float* s, float* y, void* stream);
 
 /* In-place nn.Dropout(p) (train mode) over a row-strided matrix; mask regenerated from (seed, index). */
-int mer_dropout_inplace(int rows, int cols, float* x, long ldx, float p, unsigned long long seed, void* stream);
+int mer_dropout_inplace(int rows, int cols, float* x, long ldx, float p, const unsigned long long* seed, unsigned long long site, void* stream);
 
 /* Backward of dropout(relu(z)) given y: dy <- dy * (y > 0) * keep/(1-p), in place. */
 int mer_relu_dropout_bwd(int rows, int cols, float* dy, long lddy, const float* y, long ldy, float p,
-                         unsigned long long seed, void* stream);
+                         const unsigned long long* seed, unsigned long long site, void* stream);
 
 /* Gated xattn head (fusion.py:318-327, 408-411): g = sigmoid(z[b]); out = g*v + (1-g)*a; and backward
  * (dv/da ACCUMULATE, dz written). */
@@ -230,6 +235,11 @@ int mer_pack_input_nhwc(int N, int C, int H, int W, int Cp, const float* x, void
 /* PyTorch conv weight [K][C][R][S] fp32 -> bf16 [K][R][S][Cp] (transpose=0, forward) or [Cp][R][S][K]
  * (transpose=1, data-gradient operand); channels >= C are zero. */
 int mer_pack_conv_weight(int K, int C, int R, int S, int Cp, int transpose, const float* w, void* out, void* stream);
+
+/* n (<= 64) mer_pack_conv_weight layouts in one launch (the trunk's per-step re-pack).  desc: DEVICE table of
+ * n records of 9 int64 {w, out, K, C, R, S, Cp, transpose, first element}, records in output order, first
+ * elements the prefix sums of K*R*S*Cp; total = the sum. */
+int mer_pack_conv_weights(int n, const long long* desc, long total, void* stream);
 
 /* BatchNorm2d finalize: ms[c] = (mean, rstd) from the striped partial rows of stats over M values and, when non-NULL, updates
  * running_mean / running_var (unbiased) with `momentum` and increments num_batches_tracked (train mode).

@@ -57,7 +57,9 @@ __global__ __launch_bounds__(256) void mha_fwd_kernel(int B, int H, int Lq, int 
                                                       const float* __restrict__ V, long ldv,
                                                       const float* __restrict__ bias, float* __restrict__ O, long ldo,
                                                       float* __restrict__ P, float scale, float drop_p,
-                                                      unsigned long long seed) {
+                                                      const unsigned long long* __restrict__ seed_ptr,
+    unsigned long long site) {
+  const unsigned long long seed = mer_site_seed(seed_ptr, site);
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int LkP = pad16(Lk), dh16 = pad16(dh);
   const int KST = st_rows16(dh), VST = st_rows4(dh16), PST = LkP + 4;
@@ -179,7 +181,7 @@ static size_t mha_fwd_lds(int Lk, int dh, int waves) {
 
 MER_API int mer_mha_fwd(int B, int H, int Lq, int Lk, int dh, const float* Q, long ldq, const float* K, long ldk,
                         const float* V, long ldv, const float* bias, float* O, long ldo, float* P, float scale,
-                        float drop_p, unsigned long long seed, void* stream) {
+                        float drop_p, const unsigned long long* seed, unsigned long long site, void* stream) {
   if (B <= 0 || Lq <= 0) return 0;
   if (dh <= 0 || dh > 64 || (dh % 4) != 0 || Lk <= 0 || Lk > 16 * FWD_MAX_KT) return (int)hipErrorInvalidValue;
   const int waves = (Lq + 15) / 16 < 4 ? (Lq + 15) / 16 : 4;
@@ -190,7 +192,7 @@ MER_API int mer_mha_fwd(int B, int H, int Lq, int Lk, int dh, const float* Q, lo
     return (int)hipErrorInvalidConfiguration;
   dim3 grid(B * H, (Lq + 16 * waves - 1) / (16 * waves));
   hipLaunchKernelGGL(mha_fwd_kernel, grid, dim3(64 * waves), lds, (hipStream_t)stream, B, H, Lq, Lk, dh, Q, ldq, K, ldk,
-                     V, ldv, bias, O, ldo, P, scale, drop_p, seed);
+                     V, ldv, bias, O, ldo, P, scale, drop_p, seed, site);
   MER_LAUNCH_CHECK();
 }
 
@@ -208,7 +210,9 @@ __global__ __launch_bounds__(256) void mha_bwd_kernel(int B, int H, int Lq, int 
                                                       const float* __restrict__ dO, long lddo, float* __restrict__ dQ,
                                                       long lddq, float* __restrict__ dK, long lddk,
                                                       float* __restrict__ dV, long lddv, int save_ds, float scale,
-                                                      float drop_p, unsigned long long seed) {
+                                                      float drop_p, const unsigned long long* __restrict__ seed_ptr,
+    unsigned long long site) {
+  const unsigned long long seed = mer_site_seed(seed_ptr, site);
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int LqP = pad16(Lq), LkP = pad16(Lk), dh16 = pad16(dh);
   const int ST = st_rows16(dh16), SST = st_rows16(LkP);
@@ -340,7 +344,7 @@ static size_t mha_bwd_lds(int Lq, int Lk, int dh) {
 MER_API int mer_mha_bwd(int B, int H, int Lq, int Lk, int dh, const float* Q, long ldq, const float* K, long ldk,
                         const float* V, long ldv, float* P, const float* dO, long lddo, float* dQ, long lddq,
                         float* dK, long lddk, float* dV, long lddv, float* dbias, float scale, float drop_p,
-                        unsigned long long seed, void* stream) {
+                        const unsigned long long* seed, unsigned long long site, void* stream) {
   if (B <= 0) return 0;
   if (dh <= 0 || dh > 64 || (dh % 4) != 0 || Lq <= 0 || Lk <= 0 || Lk > 16 * FWD_MAX_KT)
     return (int)hipErrorInvalidValue;
@@ -351,7 +355,7 @@ MER_API int mer_mha_bwd(int B, int H, int Lq, int Lk, int dh, const float* Q, lo
     return (int)hipErrorInvalidConfiguration;
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(mha_bwd_kernel, dim3(B * H), dim3(256), lds, st, B, H, Lq, Lk, dh, Q, ldq, K, ldk, V, ldv, P, dO,
-                     lddo, dQ, lddq, dK, lddk, dV, lddv, dbias ? 1 : 0, scale, drop_p, seed);
+                     lddo, dQ, lddq, dK, lddk, dV, lddv, dbias ? 1 : 0, scale, drop_p, seed, site);
   if (dbias) {
     const long n = (long)B * Lq * Lk;
     const int grid = (int)((n + 255) / 256 < 2048 ? (n + 255) / 256 : 2048);

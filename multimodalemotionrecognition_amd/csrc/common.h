@@ -65,6 +65,13 @@ __device__ __forceinline__ uint32_t mer_hash(uint64_t seed, uint64_t idx) {
   z ^= z >> 31;
   return (uint32_t)z;
 }
+// Per-call-site dropout seed: the step's RNG base lives in DEVICE memory (so a captured hipGraph replays
+// with a fresh base every step, advanced in-graph by mer_rng_advance) and is mixed with a constant site
+// id; a NULL base means "no dropout" (p == 0) callers.
+__device__ __forceinline__ unsigned long long mer_site_seed(const unsigned long long* base, unsigned long long site) {
+  const unsigned long long b = base ? *base : 0ull;
+  return b * 0x100000001B3ull + site * 0x9E3779B97F4A7C15ull + 1ull;
+}
 // keep with probability keep_p; returns 1/keep_p when kept, else 0
 __device__ __forceinline__ float dropout_scale(uint64_t seed, uint64_t idx, float p) {
   if (p <= 0.f) return 1.f;

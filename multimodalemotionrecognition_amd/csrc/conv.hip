@@ -941,6 +941,55 @@ MER_API int mer_pack_conv_weight(int K, int C, int R, int S, int Cp, int transpo
   MER_LAUNCH_CHECK();
 }
 
+// All of a trunk's weight packs in ONE launch (the per-step re-pack in training is ~40 small layouts
+// whose separate launches cost more than their bytes).  desc: n records of 9 int64 =
+// {w, out, K, C, R, S, Cp, transpose, first element (unused here)}; grid.y = record.  Both layouts go
+// through an LDS tile so global reads AND writes are contiguous runs:
+//   transpose 0: block = one output channel k: w[k][c][rs] (C*RS contiguous floats) -> out[k][rs][c<Cp];
+//   transpose 1: block = (input channel c, 64 output channels k0..): w[k][c][rs] (runs of RS) ->
+//                out[c][rs][k0..k0+63].
+__global__ __launch_bounds__(256) void pack_w_batched_kernel(const long long* __restrict__ desc) {
+  __shared__ float tile[4608];  // max C*RS (512 * 9) or 64 * RS (RS <= 49 -> 3136)
+  const long long* r = desc + blockIdx.y * 9;
+  const float* w = reinterpret_cast<const float*>(r[0]);
+  bf16_t* out = reinterpret_cast<bf16_t*>(r[1]);
+  const int K = (int)r[2], C = (int)r[3], RS = (int)(r[4] * r[5]), Cp = (int)r[6];
+  if (!r[7]) {
+    const int k = blockIdx.x;
+    if (k >= K) return;
+    const float* src = w + (long)k * C * RS;
+    for (int i = threadIdx.x; i < C * RS; i += 256) tile[i] = src[i];  // [c][rs]
+    __syncthreads();
+    bf16_t* dst = out + (long)k * RS * Cp;
+    for (int i = threadIdx.x; i < RS * Cp; i += 256) {  // i = rs*Cp + c
+      const int rs = i / Cp, c = i - rs * Cp;
+      dst[i] = c < C ? f2bf(tile[c * RS + rs]) : (bf16_t)0;
+    }
+  } else {
+    const int kb = (K + 63) / 64;
+    const int c = blockIdx.x / kb, k0 = (blockIdx.x - c * kb) * 64;
+    if (c >= Cp) return;
+    const int nk = min(64, K - k0);
+    for (int i = threadIdx.x; i < nk * RS; i += 256) {  // [kk][rs]
+      const int kk = i / RS, rs = i - kk * RS;
+      tile[i] = c < C ? w[((long)(k0 + kk) * C + c) * RS + rs] : 0.f;
+    }
+    __syncthreads();
+    bf16_t* dst = out + (long)c * RS * K + k0;
+    for (int i = threadIdx.x; i < RS * nk; i += 256) {  // i = rs*nk + kk
+      const int rs = i / nk, kk = i - rs * nk;
+      dst[(long)rs * K + kk] = f2bf(tile[kk * RS + rs]);
+    }
+  }
+}
+MER_API int mer_pack_conv_weights(int n, const long long* desc, long total, void* stream) {
+  (void)total;
+  if (n <= 0 || n > 64) return (int)hipErrorInvalidValue;
+  // grid.x covers the largest record: 512 output channels (layout 0) or 512 x 8 (c, k-block) tiles
+  hipLaunchKernelGGL(pack_w_batched_kernel, dim3(512 * 8, n), dim3(256), 0, (hipStream_t)stream, desc);
+  MER_LAUNCH_CHECK();
+}
+
 // ---------------------------------------------------------------------------------------
 // BatchNorm2d (train mode), channel-last.  stats[c] = (sum, sumsq) over M = N*H*W values.
 // finalize: ms[c] = (mean, rstd); running_mean = (1-mom) rm + mom*mean; running_var uses the

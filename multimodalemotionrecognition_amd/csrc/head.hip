@@ -159,10 +159,12 @@ MER_API int mer_colsum_f32(int M, int N, const float* X, long ldx, float* out, v
 // ---------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void add_ln_fwd_kernel(int rows, int d, int rows_per_sample, const float* __restrict__ x,
                                                          const float* __restrict__ r, float dp_p,
-                                                         unsigned long long seed, const float* __restrict__ gamma,
+                                                         const unsigned long long* __restrict__ seed_ptr,
+    unsigned long long site, const float* __restrict__ gamma,
                                                          const float* __restrict__ beta, float eps, float* __restrict__ y,
                                                          float* __restrict__ sum_out, float* __restrict__ mean_out,
                                                          float* __restrict__ rstd_out) {
+  const unsigned long long seed = mer_site_seed(seed_ptr, site);
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (row >= rows) return;
   const float sc = r ? dropout_scale(seed, row / rows_per_sample, dp_p) : 0.f;
@@ -192,11 +194,11 @@ __global__ __launch_bounds__(256) void add_ln_fwd_kernel(int rows, int d, int ro
 }
 
 MER_API int mer_add_ln_fwd(int rows, int d, int rows_per_sample, const float* x, const float* r, float dp_p,
-                           unsigned long long seed, const float* gamma, const float* beta, float eps, float* y,
+                           const unsigned long long* seed, unsigned long long site, const float* gamma, const float* beta, float eps, float* y,
                            float* sum_out, float* mean_out, float* rstd_out, void* stream) {
   if (rows <= 0) return 0;
   hipLaunchKernelGGL(add_ln_fwd_kernel, dim3((rows + 3) / 4), dim3(256), 0, (hipStream_t)stream, rows, d,
-                     rows_per_sample, x, r, dp_p, seed, gamma, beta, eps, y, sum_out, mean_out, rstd_out);
+                     rows_per_sample, x, r, dp_p, seed, site, gamma, beta, eps, y, sum_out, mean_out, rstd_out);
   MER_LAUNCH_CHECK();
 }
 
@@ -205,9 +207,11 @@ MER_API int mer_add_ln_fwd(int rows, int d, int rows_per_sample, const float* x,
 __global__ __launch_bounds__(256) void add_ln_bwd_kernel(int rows, int d, int rows_per_sample, const float* __restrict__ dy,
                                                          const float* __restrict__ s, const float* __restrict__ mean,
                                                          const float* __restrict__ rstd, const float* __restrict__ gamma,
-                                                         float dp_p, unsigned long long seed, float* __restrict__ dx,
+                                                         float dp_p, const unsigned long long* __restrict__ seed_ptr,
+    unsigned long long site, float* __restrict__ dx,
                                                          float* __restrict__ dr, float* __restrict__ dgamma,
                                                          float* __restrict__ dbeta, int rows_per_block) {
+  const unsigned long long seed = mer_site_seed(seed_ptr, site);
   extern __shared__ __attribute__((aligned(16))) float red[];  // [2][4][d]
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   for (int c = threadIdx.x; c < 8 * d; c += 256) red[c] = 0.f;
@@ -246,13 +250,13 @@ __global__ __launch_bounds__(256) void add_ln_bwd_kernel(int rows, int d, int ro
 }
 
 MER_API int mer_add_ln_bwd(int rows, int d, int rows_per_sample, const float* dy, const float* s, const float* mean,
-                           const float* rstd, const float* gamma, float dp_p, unsigned long long seed, float* dx,
+                           const float* rstd, const float* gamma, float dp_p, const unsigned long long* seed, unsigned long long site, float* dx,
                            float* dr, float* dgamma, float* dbeta, void* stream) {
   if (rows <= 0) return 0;
   if ((size_t)8 * d * sizeof(float) > 160 * 1024) return (int)hipErrorInvalidValue;
   const int rpb = 64;
   hipLaunchKernelGGL(add_ln_bwd_kernel, dim3((rows + rpb - 1) / rpb), dim3(256), 8 * d * sizeof(float),
-                     (hipStream_t)stream, rows, d, rows_per_sample, dy, s, mean, rstd, gamma, dp_p, seed, dx, dr,
+                     (hipStream_t)stream, rows, d, rows_per_sample, dy, s, mean, rstd, gamma, dp_p, seed, site, dx, dr,
                      dgamma, dbeta, rpb);
   MER_LAUNCH_CHECK();
 }
@@ -338,6 +342,20 @@ MER_API int mer_cross_entropy(int B, int C, const float* logits, const long long
 }
 
 // ---------------------------------------------------------------------------------------
+// RNG base of a training step (device-resident, see mer_site_seed in common.h)
+// ---------------------------------------------------------------------------------------
+__global__ void rng_advance_kernel(unsigned long long* state) {
+  unsigned long long z = *state + 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  *state = (z ^ (z >> 31)) & 0x3FFFFFFFFFFFFFFFull;
+}
+MER_API int mer_rng_advance(unsigned long long* state, void* stream) {
+  hipLaunchKernelGGL(rng_advance_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, state);
+  MER_LAUNCH_CHECK();
+}
+
+// ---------------------------------------------------------------------------------------
 // Elementwise helpers
 // ---------------------------------------------------------------------------------------
 // y = x * s[0] (device scalar, e.g. autograd's grad_output of a 0-d loss)
@@ -352,24 +370,28 @@ MER_API int mer_scale_dev(long n, const float* x, const float* s, float* y, void
 }
 
 // in-place dropout on rows with stride (nn.Dropout in train mode): x *= keep/(1-p)
-__global__ void dropout_kernel(int rows, int cols, float* __restrict__ x, long ldx, float p, unsigned long long seed) {
+__global__ void dropout_kernel(int rows, int cols, float* __restrict__ x, long ldx, float p, const unsigned long long* __restrict__ seed_ptr,
+    unsigned long long site) {
+  const unsigned long long seed = mer_site_seed(seed_ptr, site);
   const long n = (long)rows * cols;
   for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < n; e += (long)gridDim.x * blockDim.x) {
     const int r = e / cols, c = e % cols;
     x[(long)r * ldx + c] *= dropout_scale(seed, e, p);
   }
 }
-MER_API int mer_dropout_inplace(int rows, int cols, float* x, long ldx, float p, unsigned long long seed, void* stream) {
+MER_API int mer_dropout_inplace(int rows, int cols, float* x, long ldx, float p, const unsigned long long* seed, unsigned long long site, void* stream) {
   if (p <= 0.f) return 0;
   const long n = (long)rows * cols;
   const int grid = (int)((n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096);
-  hipLaunchKernelGGL(dropout_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, rows, cols, x, ldx, p, seed);
+  hipLaunchKernelGGL(dropout_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, rows, cols, x, ldx, p, seed, site);
   MER_LAUNCH_CHECK();
 }
 
 // backward of y = dropout(relu(z)) given y: dz = dy * (y > 0) * drop_scale  (in place on dy)
 __global__ void relu_dropout_bwd_kernel(int rows, int cols, float* __restrict__ dy, long lddy, const float* __restrict__ y,
-                                        long ldy, float p, unsigned long long seed) {
+                                        long ldy, float p, const unsigned long long* __restrict__ seed_ptr,
+    unsigned long long site) {
+  const unsigned long long seed = mer_site_seed(seed_ptr, site);
   const long n = (long)rows * cols;
   for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < n; e += (long)gridDim.x * blockDim.x) {
     const int r = e / cols, c = e % cols;
@@ -380,11 +402,11 @@ __global__ void relu_dropout_bwd_kernel(int rows, int cols, float* __restrict__ 
   }
 }
 MER_API int mer_relu_dropout_bwd(int rows, int cols, float* dy, long lddy, const float* y, long ldy, float p,
-                                 unsigned long long seed, void* stream) {
+                                 const unsigned long long* seed, unsigned long long site, void* stream) {
   const long n = (long)rows * cols;
   const int grid = (int)((n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096);
   hipLaunchKernelGGL(relu_dropout_bwd_kernel, dim3(grid > 0 ? grid : 1), dim3(256), 0, (hipStream_t)stream, rows, cols,
-                     dy, lddy, y, ldy, p, seed);
+                     dy, lddy, y, ldy, p, seed, site);
   MER_LAUNCH_CHECK();
 }
 

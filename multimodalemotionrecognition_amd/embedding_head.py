@@ -8,7 +8,9 @@ from __future__ import annotations
 import torch
 
 from . import kernels as K
-from .xattn_head import linear_runner, site_seed
+from .xattn_head import linear_runner
+
+SITE_EMB_MLP = 11
 
 
 def _grad_buf(p):
@@ -18,7 +20,7 @@ def _grad_buf(p):
 
 class _EmbHeadFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, a_emb, v_emb, mode, training, seed, drop_a, drop_v, qlin, names, *params):
+    def forward(ctx, a_emb, v_emb, mode, training, rng, drop_a, drop_v, qlin, names, *params):
         p = dict(zip(names, params))
         lin = linear_runner(p, qlin)
         B = a_emb.shape[0]
@@ -38,14 +40,14 @@ class _EmbHeadFn(torch.autograd.Function):
         if mode == "concat":
             w0 = p["fusion.0.weight"]
             h = lin("fusion.0", cat, e(B, w0.shape[0]), act="relu")
-            K.dropout_(h, dp, site_seed(seed, 11))
+            K.dropout_(h, dp, rng, SITE_EMB_MLP)
             w3 = p["fusion.3.weight"]
             out = lin("fusion.3", h, e(B, w3.shape[0]))
             sv["h"] = h
         else:
             w0 = p["gate.0.weight"]
             h = lin("gate.0", cat, e(B, w0.shape[0]), act="relu")
-            K.dropout_(h, dp, site_seed(seed, 11))
+            K.dropout_(h, dp, rng, SITE_EMB_MLP)
             z = lin("gate.3", h, e(B, 1))
             fused, g = e(B, cd), e(B)
             K.gate_mix_fwd(z, a, v, fused, g)  # g*a + (1-g)*v  (fusion.py:434)
@@ -53,7 +55,7 @@ class _EmbHeadFn(torch.autograd.Function):
             out = lin("classifier", fused, e(B, wc.shape[0]))
             sv.update(h=h, g=g, fused=fused)
         ctx.sv, ctx.p, ctx.names, ctx.params = sv, p, names, params
-        ctx.mode, ctx.dp, ctx.seed, ctx.drops = mode, dp, seed, (drop_a, drop_v)
+        ctx.mode, ctx.dp, ctx.rng, ctx.drops = mode, dp, rng, (drop_a, drop_v)
         ctx.a_emb, ctx.v_emb = a_emb, v_emb
         return out
 
@@ -75,7 +77,7 @@ class _EmbHeadFn(torch.autograd.Function):
             h = sv["h"]
             dh = e(B, h.shape[1])
             K.linear_bwd(h, p["fusion.3.weight"], dout, dx=dh, dw=grads["fusion.3.weight"], db=grads["fusion.3.bias"])
-            K.relu_dropout_bwd_(dh, h, ctx.dp, site_seed(ctx.seed, 11))
+            K.relu_dropout_bwd_(dh, h, ctx.dp, ctx.rng, SITE_EMB_MLP)
             K.linear_bwd(cat, p["fusion.0.weight"], dh, dx=dcat, dw=grads["fusion.0.weight"], db=grads["fusion.0.bias"])
         else:
             h, g, fused = sv["h"], sv["g"], sv["fused"]
@@ -87,7 +89,7 @@ class _EmbHeadFn(torch.autograd.Function):
             K.gate_mix_bwd(g, cat[:, :cd], cat[:, cd:], dfused, dz, dcat[:, :cd], dcat[:, cd:])
             dh = e(B, h.shape[1])
             K.linear_bwd(h, p["gate.3.weight"], dz, dx=dh, dw=grads["gate.3.weight"], db=grads["gate.3.bias"])
-            K.relu_dropout_bwd_(dh, h, ctx.dp, site_seed(ctx.seed, 11))
+            K.relu_dropout_bwd_(dh, h, ctx.dp, ctx.rng, SITE_EMB_MLP)
             K.linear_bwd(cat, p["gate.0.weight"], dh, dx=dcat, dw=grads["gate.0.weight"], db=grads["gate.0.bias"],
                          dx_beta=1)
         if ctx.drops[0]:
@@ -112,8 +114,8 @@ def embedding_head(model, a_emb, v_emb, drop_a=False, drop_v=False):
             continue
         names.append(n)
         params.append(q)
-    seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if model.training else 0
-    return _EmbHeadFn.apply(a_emb.contiguous(), v_emb.contiguous(), model.mode, model.training, seed,
+    rng = model.step_rng(a_emb.device) if model.training else None
+    return _EmbHeadFn.apply(a_emb.contiguous(), v_emb.contiguous(), model.mode, model.training, rng,
                             bool(drop_a), bool(drop_v), int8_images(model), tuple(names), *params)
 
 

@@ -8,6 +8,7 @@ through ``embedding_head.py``.  There is no CPU path: calling the model on CPU t
 """
 from __future__ import annotations
 
+import dataclasses
 import math
 import os
 import random
@@ -17,6 +18,8 @@ import torch
 from torch import nn
 
 from . import embedding_head as EH
+from . import graphs as G
+from . import kernels as K
 from . import xattn_head as XH
 from .temporal import TemporalPooler
 
@@ -112,30 +115,92 @@ def grad_buffer(param: torch.Tensor) -> torch.Tensor:
     return torch.zeros_like(param, dtype=torch.float32)
 
 
+def _head_grads(p, used):
+    grads = {}
+    for n, t in p.items():
+        if n in used and t.requires_grad:
+            grads[n] = grad_buffer(t)
+        elif n in used:
+            grads[n] = torch.zeros_like(t)
+    return grads
+
+
 class _XattnHeadFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, v_feat, a_seq, cfg, training, seed, names, *params):
+    def forward(ctx, v_feat, a_seq, cfg, training, rng, names, runner, *params):
         p = dict(zip(names, params))
-        logits, hctx = XH.head_forward(p, cfg, v_feat, a_seq, training, seed)
-        ctx.hctx, ctx.names, ctx.params = hctx, names, params
+        if runner is not None:
+            logits, hctx = runner.forward(v_feat, a_seq)
+        else:
+            logits, hctx = XH.head_forward(p, cfg, v_feat, a_seq, training, rng)
+        ctx.hctx, ctx.names, ctx.params, ctx.runner = hctx, names, params, runner
         ctx.used = set(XH.used_param_names(cfg))
         return logits
 
     @staticmethod
     def backward(ctx, dlogits):
         p = dict(zip(ctx.names, ctx.params))
-        grads = {}
-        for n, t in p.items():
-            if n in ctx.used and t.requires_grad:
-                grads[n] = grad_buffer(t)
-            elif n in ctx.used:
-                grads[n] = torch.zeros_like(t)
         dl = dlogits.contiguous().float()
         need_v = ctx.needs_input_grad[0]
         need_a = ctx.needs_input_grad[1]
-        dv, da = XH.head_backward(p, ctx.hctx, dl, grads, need_dv_feat=need_v, need_da_seq=need_a)
+        if ctx.runner is not None and ctx.runner.backward_graphable(p, ctx.used, need_v, need_a):
+            dv, grads = ctx.runner.backward(dl)
+            da = None
+        else:
+            grads = _head_grads(p, ctx.used)
+            dv, da = XH.head_backward(p, ctx.hctx, dl, grads, need_dv_feat=need_v, need_da_seq=need_a)
+        if ctx.runner is not None:
+            ctx.runner.pending = False
         out_grads = [grads.get(n) if (n in ctx.used and t.requires_grad) else None for n, t in p.items()]
-        return (dv, da, None, None, None, None, *out_grads)
+        return (dv, da, None, None, None, None, None, *out_grads)
+
+
+class _HeadGraphs:
+    """Captured forward / backward hipGraphs of the xattn head for one input shape (graphs.py).
+
+    The dropout / drop-path masks stay random per step: the graph's RNG base is a static device scalar that
+    is refilled with the step's host-drawn seed right before each replay (so ``torch.manual_seed`` fixes
+    the masks exactly as in eager mode), and the backward graph regenerates the same masks from it.
+    ``pending`` marks a forward whose backward has not run yet: a second forward in between (gradient
+    accumulation) runs eagerly instead of overwriting the saved static activations.
+    """
+
+    def __init__(self, model, names, cfg, training):
+        self.model, self.names, self.cfg, self.training = model, names, cfg, training
+        self.fwd = self.bwd = None
+        self.pending = False
+        self.rng = None
+
+    def forward(self, v_feat, a_seq):
+        params = dict(zip(self.names, self.model.head_params()[1]))
+        if self.fwd is None:
+            self.rng = torch.zeros(1, dtype=torch.int64, device=v_feat.device)
+            self.fwd = G.StaticGraph(lambda v, a: XH.head_forward(params, self.cfg, v, a, self.training,
+                                                                  self.rng if self.training else None),
+                                     [v_feat, a_seq])
+        if self.training:  # this step's host-drawn RNG base, stream-ordered before the replay reads it
+            self.rng.fill_(_next_seed())
+        logits, hctx = self.fwd.replay(v_feat, a_seq)
+        return logits.clone(), hctx
+
+    def backward_graphable(self, p, used, need_v, need_a) -> bool:
+        return (not need_a) and all(t.grad is None and getattr(t, "_mer_grad_slot", None) is not None
+                                    for n, t in p.items() if n in used and t.requires_grad)
+
+    def backward(self, dlogits):
+        params = dict(zip(self.names, self.model.head_params()[1]))
+        used = set(XH.used_param_names(self.cfg))
+        if self.bwd is None:
+            _, hctx = self.fwd.out
+
+            def run(dl):
+                grads = _head_grads(params, used)
+                dv, _ = XH.head_backward(params, hctx, dl, grads, need_dv_feat=True, need_da_seq=False)
+                return dv
+
+            self.bwd = G.StaticGraph(run, [dlogits])
+        dv = self.bwd.replay(dlogits)
+        return dv.clone(), {n: grad_buffer(t) for n, t in params.items() if n in used and t.requires_grad}
 
 
 class FusionModel(nn.Module):
@@ -177,6 +242,7 @@ class FusionModel(nn.Module):
         self.xattn_use_emotion_prior = xattn_use_emotion_prior
         self.num_classes = num_classes
         self._prefetched = None  # (audio key, encoder output, stream) from prefetch_audio()
+        self._head_graphs = G.GraphCache()
 
         if mode in {"concat", "gated"}:
             fusion_audio_dim = audio_model.embedding_dim
@@ -238,6 +304,12 @@ class FusionModel(nn.Module):
                     self.xattn_gate[0].bias.fill_(-1.0)
                     self.xattn_gate[3].bias.fill_(-1.0)
 
+    def step_rng(self, device) -> torch.Tensor:
+        """This step's dropout RNG base: a fresh device int64 [1] tensor drawn from the host generator each
+        training forward (so ``torch.manual_seed`` reproduces the masks, train.py:951 set_seed); the
+        autograd context keeps it, so masks are regenerated correctly even with several forwards in flight."""
+        return torch.full((1,), _next_seed(), dtype=torch.int64, device=device)
+
     def audio_encoder_frozen(self) -> bool:
         enc = getattr(self.audio_model, "wavlm", None)
         return enc is not None and not any(q.requires_grad for q in enc.parameters())
@@ -292,9 +364,30 @@ class FusionModel(nn.Module):
         if qlin is not None:  # INT8 inference (TorchModelRunner enable_dynamic_quant): forward only
             with torch.no_grad():
                 return XH.head_forward(dict(zip(names, params)), self.head_config(), v_feat.contiguous(),
-                                       a_seq.contiguous(), False, 0, qlin=qlin)[0]
-        return _XattnHeadFn.apply(v_feat.contiguous(), a_seq.contiguous(), self.head_config(), self.training,
-                                  _next_seed() if self.training else 0, names, *params)
+                                       a_seq.contiguous(), False, None, qlin=qlin)[0]
+        cfg = self.head_config()
+        v_feat, a_seq = v_feat.contiguous(), a_seq.contiguous()
+        runner = self._head_runner(names, params, cfg, v_feat, a_seq)
+        rng = self.step_rng(v_feat.device) if (self.training and runner is None) else None
+        return _XattnHeadFn.apply(v_feat, a_seq, cfg, self.training, rng, names, runner, *params)
+
+    def _head_runner(self, names, params, cfg, v_feat, a_seq):
+        """The captured-graph runner of the head for these shapes, or None (eager) while warming up, during
+        a capture, for a second forward before the first one's backward, or with input gradients wanted
+        for the audio features (graphs.py)."""
+        if G.capturing() or a_seq.requires_grad:
+            return None
+        key = (tuple(v_feat.shape), tuple(a_seq.shape), a_seq.dtype, v_feat.device.index, self.training,
+               dataclasses.astuple(cfg), tuple(q.data_ptr() for q in params))
+        if not self._head_graphs.ready(key):
+            return None
+        r = self._head_graphs.get(key)
+        if r is None:
+            r = self._head_graphs.put(key, _HeadGraphs(self, names, cfg, self.training))
+        if r.pending:
+            return None
+        r.pending = torch.is_grad_enabled()
+        return r
 
     def forward(self, video: torch.Tensor, audio: torch.Tensor):
         self.alignment_loss = None

@@ -133,34 +133,48 @@ def colsum(x2d, out):
     LIB("mer_colsum_f32", x2d.shape[0], x2d.shape[1], x2d.data_ptr(), x2d.stride(0), out.data_ptr(), stream_ptr())
 
 
-def mha_fwd(q, k, v, bias, out, P, B, H, Lq, Lk, drop_p=0.0, seed=0):
+def rng_ptr(rng):
+    """Device address of a step's RNG base (int64 [1] tensor, see mer_site_seed) or 0 (no dropout)."""
+    if rng is None:
+        return 0
+    if rng.dtype != torch.int64 or rng.numel() != 1 or not rng.is_cuda:
+        raise ValueError("the RNG base must be a device int64 tensor of one element")
+    return rng.data_ptr()
+
+
+def rng_advance(rng):
+    """rng = splitmix64(rng): the next step's RNG base, on the device (capturable in a hipGraph)."""
+    LIB("mer_rng_advance", rng_ptr(rng), stream_ptr())
+
+
+def mha_fwd(q, k, v, bias, out, P, B, H, Lq, Lk, drop_p=0.0, rng=None, site=0):
     d = out.shape[-1]
     dh = d // H
     LIB("mer_mha_fwd", B, H, Lq, Lk, dh, q.data_ptr(), q.stride(0), k.data_ptr(), k.stride(0), v.data_ptr(),
         v.stride(0), _ptr(bias), out.data_ptr(), out.stride(0), P.data_ptr(), float(dh ** -0.5), float(drop_p),
-        int(seed), stream_ptr())
+        rng_ptr(rng), int(site), stream_ptr())
 
 
-def mha_bwd(q, k, v, P, dout, dq, dk, dv, dbias, B, H, Lq, Lk, drop_p=0.0, seed=0):
+def mha_bwd(q, k, v, P, dout, dq, dk, dv, dbias, B, H, Lq, Lk, drop_p=0.0, rng=None, site=0):
     d = dout.shape[-1]
     dh = d // H
     LIB("mer_mha_bwd", B, H, Lq, Lk, dh, q.data_ptr(), q.stride(0), k.data_ptr(), k.stride(0), v.data_ptr(),
         v.stride(0), P.data_ptr(), dout.data_ptr(), dout.stride(0), dq.data_ptr(), dq.stride(0), dk.data_ptr(),
-        dk.stride(0), dv.data_ptr(), dv.stride(0), _ptr(dbias), float(dh ** -0.5), float(drop_p), int(seed),
-        stream_ptr())
+        dk.stride(0), dv.data_ptr(), dv.stride(0), _ptr(dbias), float(dh ** -0.5), float(drop_p), rng_ptr(rng),
+        int(site), stream_ptr())
 
 
-def add_ln_fwd(x, r, gamma, beta, y, s_out, mean, rstd, rows_per_sample, dp_p=0.0, seed=0, eps=1e-5):
+def add_ln_fwd(x, r, gamma, beta, y, s_out, mean, rstd, rows_per_sample, dp_p=0.0, rng=None, site=0, eps=1e-5):
     rows, d = x.shape
-    LIB("mer_add_ln_fwd", rows, d, rows_per_sample, x.data_ptr(), _ptr(r), float(dp_p), int(seed),
+    LIB("mer_add_ln_fwd", rows, d, rows_per_sample, x.data_ptr(), _ptr(r), float(dp_p), rng_ptr(rng), int(site),
         gamma.data_ptr(), beta.data_ptr(), float(eps), y.data_ptr(), _ptr(s_out), _ptr(mean), _ptr(rstd),
         stream_ptr())
 
 
-def add_ln_bwd(dy, s, mean, rstd, gamma, dx, dr, dgamma, dbeta, rows_per_sample, dp_p=0.0, seed=0):
+def add_ln_bwd(dy, s, mean, rstd, gamma, dx, dr, dgamma, dbeta, rows_per_sample, dp_p=0.0, rng=None, site=0):
     rows, d = dy.shape
     LIB("mer_add_ln_bwd", rows, d, rows_per_sample, dy.data_ptr(), s.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
-        gamma.data_ptr(), float(dp_p), int(seed), dx.data_ptr(), _ptr(dr), _ptr(dgamma), _ptr(dbeta), stream_ptr())
+        gamma.data_ptr(), float(dp_p), rng_ptr(rng), int(site), dx.data_ptr(), _ptr(dr), _ptr(dgamma), _ptr(dbeta), stream_ptr())
 
 
 def mean_pool_fwd(x3d, y, ldy=None):
@@ -186,15 +200,15 @@ def scale_dev(x, s, y):
     LIB("mer_scale_dev", x.numel(), x.data_ptr(), s.data_ptr(), y.data_ptr(), stream_ptr())
 
 
-def dropout_(x2d, p, seed):
+def dropout_(x2d, p, rng=None, site=0):
     if p > 0:
-        LIB("mer_dropout_inplace", x2d.shape[0], x2d.shape[1], x2d.data_ptr(), x2d.stride(0), float(p), int(seed),
-            stream_ptr())
+        LIB("mer_dropout_inplace", x2d.shape[0], x2d.shape[1], x2d.data_ptr(), x2d.stride(0), float(p), rng_ptr(rng),
+            int(site), stream_ptr())
 
 
-def relu_dropout_bwd_(dy, y, p, seed):
+def relu_dropout_bwd_(dy, y, p, rng=None, site=0):
     LIB("mer_relu_dropout_bwd", dy.shape[0], dy.shape[1], dy.data_ptr(), dy.stride(0), y.data_ptr(), y.stride(0),
-        float(p), int(seed), stream_ptr())
+        float(p), rng_ptr(rng), int(site), stream_ptr())
 
 
 def gate_mix_fwd(z, v, a, out, g):
@@ -374,6 +388,13 @@ def pack_input_nhwc(x, y):
 def pack_conv_weight(w, out, cp, transpose):
     Kc, C, R, S = w.shape
     LIB("mer_pack_conv_weight", Kc, C, R, S, cp, int(transpose), w.data_ptr(), out.data_ptr(), stream_ptr())
+
+
+def pack_conv_weights(desc, total):
+    """Batched weight packing from a device int64 descriptor table [n, 9] (see mer_pack_conv_weights)."""
+    if desc.dtype != torch.int64 or desc.dim() != 2 or desc.shape[1] != 9 or not desc.is_cuda:
+        raise ValueError("pack descriptor table must be a device int64 [n, 9] tensor")
+    LIB("mer_pack_conv_weights", desc.shape[0], desc.data_ptr(), int(total), stream_ptr())
 
 
 def bn_finalize(stats, M, eps, momentum, ms, rmean=None, rvar=None, nbt=None):

@@ -41,21 +41,22 @@ def hip_linear(x: torch.Tensor, layer: torch.nn.Linear, act: str = "none") -> to
 
 class _DropoutFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, p, seed):
+    def forward(ctx, x, p, rng):
         y = x.contiguous().clone()
-        K.dropout_(y.view(-1, y.shape[-1]), p, seed)
-        ctx.p, ctx.seed = p, seed
+        K.dropout_(y.view(-1, y.shape[-1]), p, rng)
+        ctx.p, ctx.rng = p, rng
         return y
 
     @staticmethod
     def backward(ctx, dy):
         g = dy.contiguous().clone()
-        K.dropout_(g.view(-1, g.shape[-1]), ctx.p, ctx.seed)  # same (seed, index) -> same mask and scale
+        K.dropout_(g.view(-1, g.shape[-1]), ctx.p, ctx.rng)  # same (base, index) -> same mask and scale
         return g, None, None
 
 
 def hip_dropout(x: torch.Tensor, p: float, training: bool) -> torch.Tensor:
     if not training or p <= 0:
         return x
-    seed = int(torch.randint(0, 2 ** 62, (1,)).item())
-    return _DropoutFn.apply(x, p, seed)
+    seed = int(torch.randint(0, 2 ** 62, (1,)).item())  # host draw: torch.manual_seed reproduces it
+    rng = torch.tensor([seed], dtype=torch.int64).to(x.device, non_blocking=True)
+    return _DropoutFn.apply(x, p, rng)

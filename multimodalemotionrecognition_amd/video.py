@@ -67,8 +67,8 @@ def _bn_tensors(bn: nn.BatchNorm2d):
 
 class _TrunkFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, trunk, training, *params):
-        runner = trunk.graph_runner(x, training)
+    def forward(ctx, x, trunk, training, want_backward, *params):
+        runner = trunk.graph_runner(x, training, want_backward)
         if runner is not None:
             feats, saved = runner.forward(x)
         else:
@@ -84,7 +84,9 @@ class _TrunkFn(torch.autograd.Function):
             grads = ctx.runner.backward(dfeat, params)
         else:
             grads = trunk_backward(ctx.trunk, ctx.saved, dfeat, ctx.training)
-        return (None, None, None, *[grads.get(id(q)) for q in params])
+        if ctx.runner is not None:
+            ctx.runner.pending = False
+        return (None, None, None, None, *[grads.get(id(q)) for q in params])
 
 
 class _TrunkGraphs:
@@ -100,6 +102,7 @@ class _TrunkGraphs:
         self.trunk, self.training = trunk, training
         self.fwd = None
         self.bwd = None
+        self.pending = False  # a graphed forward whose backward has not run (its static activations are live)
 
     def forward(self, x):
         if self.fwd is None:
@@ -130,41 +133,78 @@ class ResNet18Trunk(nn.Sequential):
                          nn.MaxPool2d(3, 2, 1), _layer(64, 64, 1), _layer(64, 128, 2), _layer(128, 256, 2),
                          _layer(256, 512, 2), nn.AdaptiveAvgPool2d((1, 1)))
         _init_resnet(self)
-        self._pack_cache = {}
+        self._plans = {}
         self._force_pack = False
         self._graphs = G.GraphCache()
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if not x.is_cuda:
             raise RuntimeError("ResNet18 trunk runs on the MI355X kernels; move the frames to the GPU")
-        return _TrunkFn.apply(x.contiguous().float(), self, self.training, *self.parameters())
+        return _TrunkFn.apply(x.contiguous().float(), self, self.training, torch.is_grad_enabled(), *self.parameters())
 
-    def graph_runner(self, x: torch.Tensor, training: bool):
-        """The captured-graph runner for this input shape / mode, or None while warming up (graphs.py)."""
+    def graph_runner(self, x: torch.Tensor, training: bool, want_backward: bool = False):
+        """The captured-graph runner for this input shape / mode, or None (eager) while warming up, during a
+        capture, or for a second forward before the first one's backward (graphs.py)."""
         if G.capturing():
             return None
         key = (tuple(x.shape), bool(training), x.device.index, G.tensor_addresses(self))
         if not self._graphs.ready(key):
             return None
         r = self._graphs.get(key)
-        return r if r is not None else self._graphs.put(key, _TrunkGraphs(self, training))
+        if r is None:
+            r = self._graphs.put(key, _TrunkGraphs(self, training))
+        if r.pending:
+            return None
+        r.pending = bool(want_backward)
+        return r
 
-    # ---- bf16 weight packing: per step in training (weights move), cached by version in eval ----
+    # ---- bf16 weight packing: all convs in one launch, re-done whenever a weight's value changes ----
+    def _pack_plan(self, transpose: bool):
+        """Persistent packed-weight buffers + the device descriptor table of one batched pack launch.
+        Forward packs [K][R][S][Cp] for every conv (stem input padded to CP_IN); transposed packs
+        [Cp][R][S][K] for every conv but the stem (the frames need no data gradient)."""
+        convs = [m for m in self.modules() if isinstance(m, nn.Conv2d)]
+        if transpose:
+            convs = convs[1:]
+        ptrs = tuple(c.weight.data_ptr() for c in convs)
+        plan = self._plans.get(transpose)
+        if plan is not None and plan["ptrs"] == ptrs:
+            return plan
+        dev = convs[0].weight.device
+        outs, rows, first = {}, [], 0
+        for c in convs:
+            Kc, C, R, S = c.weight.shape
+            if C * R * S > 4608 or Kc > 512 or C > 512:  # the batched kernel's LDS tile / grid bounds
+                raise ValueError(f"conv {tuple(c.weight.shape)} exceeds mer_pack_conv_weights' tile bounds")
+            cp = max(CP_IN, (C + 7) // 8 * 8) if c is convs[0] and not transpose else C
+            shape = (cp, R * S * Kc) if transpose else (Kc, R * S * cp)
+            buf = torch.empty(shape, device=dev, dtype=torch.bfloat16)
+            outs[id(c)] = buf
+            rows.append([c.weight.data_ptr(), buf.data_ptr(), Kc, C, R, S, cp, int(transpose), first])
+            first += buf.numel()
+        plan = dict(convs=convs, ptrs=ptrs, outs=outs, total=first, vers=None,
+                    desc=torch.tensor(rows, dtype=torch.int64).to(dev))
+        self._plans[transpose] = plan
+        return plan
+
+    def pack_all(self, transpose: bool):
+        """(Re-)pack every conv weight in one launch when any weight changed (always inside a capture)."""
+        plan = self._pack_plan(transpose)
+        vers = tuple(weight_version(c.weight) for c in plan["convs"])
+        if self._force_pack or vers != plan["vers"]:
+            K.pack_conv_weights(plan["desc"], plan["total"])
+            plan["vers"] = vers
+
     def packed(self, conv: nn.Conv2d, cp: int, transpose: bool):
-        w = conv.weight
-        key = (id(conv), transpose)
-        ver = weight_version(w)
-        hit = self._pack_cache.get(key)
-        if hit is not None and hit[0] == ver and not self._force_pack:
-            return hit[1]
-        Kc, C, R, S = w.shape
-        if not transpose:
-            out = torch.empty(Kc, R * S * cp, device=w.device, dtype=torch.bfloat16)
-        else:
-            out = torch.empty(cp, R * S * Kc, device=w.device, dtype=torch.bfloat16)
-        K.pack_conv_weight(w.detach(), out, cp, transpose)
-        self._pack_cache[key] = (ver, out)
-        return out
+        """The packed weight of ``conv`` (trunk_forward / trunk_backward refresh all packs on entry; a direct
+        block-level call packs on first use)."""
+        plan = self._pack_plan(transpose)
+        if plan["vers"] is None:
+            self.pack_all(transpose)
+        buf = plan["outs"][id(conv)]
+        if (buf.shape[0] if transpose else buf.shape[1] // (conv.weight.shape[2] * conv.weight.shape[3])) != cp:
+            raise ValueError(f"packed weight channel padding {cp} does not match the plan")
+        return buf
 
 
 def _bn_forward(bn: nn.BatchNorm2d, c: torch.Tensor, stats, training: bool):
@@ -250,6 +290,7 @@ def trunk_forward(trunk: ResNet18Trunk, video: torch.Tensor, training: bool, for
 
 
 def _trunk_forward(trunk: ResNet18Trunk, video: torch.Tensor, training: bool):
+    trunk.pack_all(transpose=False)
     N, C, H, W = video.shape
     dev = video.device
     bf = torch.bfloat16
@@ -370,6 +411,7 @@ def trunk_backward(trunk: ResNet18Trunk, saved, dfeat: torch.Tensor, training: b
 
 
 def _trunk_backward(trunk: ResNet18Trunk, saved, dfeat: torch.Tensor, training: bool = True):
+    trunk.pack_all(transpose=True)
     grads = {}
     dev = dfeat.device
     x = saved["final"]

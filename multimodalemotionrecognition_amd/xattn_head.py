@@ -19,11 +19,10 @@ import torch
 
 from . import kernels as K
 
-_MASK64 = (1 << 64) - 1
-
-
-def site_seed(base: int, site: int) -> int:
-    return (base * 0x100000001B3 + site * 0x9E3779B97F4A7C15 + 1) & _MASK64
+# Dropout / drop-path sites: the step's RNG base is a device int64 [1] tensor (``rng``) mixed with a
+# constant site id in-kernel (mer_site_seed), so the masks are regenerated in backward from (base, site)
+# and a captured graph draws fresh masks every replay.
+SITE_PRIOR, SITE_V2A, SITE_VPATH, SITE_A2V, SITE_APATH, SITE_MLP = 1, 2, 3, 4, 5, 6
 
 
 @dataclass
@@ -42,7 +41,7 @@ class HeadConfig:
 class HeadCtx:
     saved: Dict[str, torch.Tensor] = field(default_factory=dict)
     dims: tuple = ()
-    seed: int = 0
+    rng: Optional[torch.Tensor] = None
     training: bool = False
 
 
@@ -63,8 +62,9 @@ def linear_runner(p: Dict[str, torch.Tensor], qlin: Optional[dict] = None):
 
 
 def head_forward(p: Dict[str, torch.Tensor], cfg: HeadConfig, v_feat: torch.Tensor, a_seq: torch.Tensor,
-                 training: bool, seed: int = 0, qlin: Optional[dict] = None):
-    """Returns (logits [B, C], ctx).  ``qlin``: INT8 images of the plain Linears (inference only)."""
+                 training: bool, rng: Optional[torch.Tensor] = None, qlin: Optional[dict] = None):
+    """Returns (logits [B, C], ctx).  ``rng``: the step's device RNG base (training dropout), ``qlin``: INT8
+    images of the plain Linears (inference only)."""
     if cfg.temporal_pooling != "mean":
         raise NotImplementedError("HIP head implements temporal_pooling='mean' (fusion default); "
                                   "attn/transformer pooling are a later row of the build plan")
@@ -72,7 +72,7 @@ def head_forward(p: Dict[str, torch.Tensor], cfg: HeadConfig, v_feat: torch.Tens
     _, Ta, sd = a_seq.shape
     d = p["v_in_proj.weight"].shape[0]
     H = cfg.num_heads
-    ctx = HeadCtx(dims=(B, T, Ta, d, H), seed=seed, training=training)
+    ctx = HeadCtx(dims=(B, T, Ta, d, H), rng=rng, training=training)
     sv = ctx.saved
     dp_attn = cfg.attn_dropout if training else 0.0
     dp_path = cfg.drop_path if training else 0.0
@@ -95,7 +95,7 @@ def head_forward(p: Dict[str, torch.Tensor], cfg: HeadConfig, v_feat: torch.Tens
         K.mean_pool_fwd(v.view(B, T, d), pg[:, :d], ldy=2 * d)
         K.mean_pool_fwd(a.view(B, Ta, d), pg[:, d:], ldy=2 * d)
         h1 = K.linear_fwd(pg, p[n + "prior_net.0.weight"], p[n + "prior_net.0.bias"], _e((B, p[n + "prior_net.0.weight"].shape[0]), v), act="relu")
-        K.dropout_(h1, dp_prior, site_seed(seed, 1))
+        K.dropout_(h1, dp_prior, rng, SITE_PRIOR)
         prior = K.linear_fwd(h1, p[n + "prior_net.3.weight"], p[n + "prior_net.3.bias"], _e((B, p[n + "prior_net.3.weight"].shape[0]), v))
         sv["pg"], sv["h1"], sv["prior"] = pg, h1, prior
         tok = {}
@@ -118,10 +118,10 @@ def head_forward(p: Dict[str, torch.Tensor], cfg: HeadConfig, v_feat: torch.Tens
     kv1 = K.linear_fwd(a, w1[d:], b1[d:], _e((B * Ta, 2 * d), v))
     o1 = _e((B * T, d), v)
     P1 = _e((B, H, T, Ta), v)
-    K.mha_fwd(q1, kv1[:, :d], kv1[:, d:], v2a_bias, o1, P1, B, H, T, Ta, dp_attn, site_seed(seed, 2))
+    K.mha_fwd(q1, kv1[:, :d], kv1[:, d:], v2a_bias, o1, P1, B, H, T, Ta, dp_attn, rng, SITE_V2A)
     v2 = K.linear_fwd(o1, p["v2a_attn.out_proj.weight"], p["v2a_attn.out_proj.bias"], _e((B * T, d), v))
     v1, s_v, mu_v, rs_v = _e((B * T, d), v), _e((B * T, d), v), _e((B * T,), v), _e((B * T,), v)
-    K.add_ln_fwd(v, v2, p["v_norm.weight"], p["v_norm.bias"], v1, s_v, mu_v, rs_v, T, dp_path, site_seed(seed, 3))
+    K.add_ln_fwd(v, v2, p["v_norm.weight"], p["v_norm.bias"], v1, s_v, mu_v, rs_v, T, dp_path, rng, SITE_VPATH)
     sv.update(q1=q1, kv1=kv1, o1=o1, P1=P1, v1=v1, s_v=s_v, mu_v=mu_v, rs_v=rs_v)
 
     # ---- a2v: a2 = MHA(q=a, k=v_new, v=v_new)  (fusion.py:398) ----
@@ -130,10 +130,10 @@ def head_forward(p: Dict[str, torch.Tensor], cfg: HeadConfig, v_feat: torch.Tens
     kv2 = K.linear_fwd(v1, w2[d:], b2[d:], _e((B * T, 2 * d), v))
     o2 = _e((B * Ta, d), v)
     P2 = _e((B, H, Ta, T), v)
-    K.mha_fwd(q2, kv2[:, :d], kv2[:, d:], a2v_bias, o2, P2, B, H, Ta, T, dp_attn, site_seed(seed, 4))
+    K.mha_fwd(q2, kv2[:, :d], kv2[:, d:], a2v_bias, o2, P2, B, H, Ta, T, dp_attn, rng, SITE_A2V)
     a2 = K.linear_fwd(o2, p["a2v_attn.out_proj.weight"], p["a2v_attn.out_proj.bias"], _e((B * Ta, d), v))
     a1, s_a, mu_a, rs_a = _e((B * Ta, d), v), _e((B * Ta, d), v), _e((B * Ta,), v), _e((B * Ta,), v)
-    K.add_ln_fwd(a, a2, p["a_norm.weight"], p["a_norm.bias"], a1, s_a, mu_a, rs_a, Ta, dp_path, site_seed(seed, 5))
+    K.add_ln_fwd(a, a2, p["a_norm.weight"], p["a_norm.bias"], a1, s_a, mu_a, rs_a, Ta, dp_path, rng, SITE_APATH)
     sv.update(q2=q2, kv2=kv2, o2=o2, P2=P2, a1=a1, s_a=s_a, mu_a=mu_a, rs_a=rs_a)
 
     # ---- temporal mean pooling -> emb = [v_emb ; a_emb]  (fusion.py:401-406) ----
@@ -145,14 +145,14 @@ def head_forward(p: Dict[str, torch.Tensor], cfg: HeadConfig, v_feat: torch.Tens
     if cfg.xattn_head == "concat":
         w0 = p["xattn_mlp.0.weight"]
         h = lin("xattn_mlp.0", emb, _e((B, w0.shape[0]), v), act="relu")
-        K.dropout_(h, dp_mlp, site_seed(seed, 6))
+        K.dropout_(h, dp_mlp, rng, SITE_MLP)
         w3 = p["xattn_mlp.3.weight"]
         logits = lin("xattn_mlp.3", h, _e((B, w3.shape[0]), v))
         sv["h"] = h
     elif cfg.xattn_head == "gated":
         w0 = p["xattn_gate.0.weight"]
         h = lin("xattn_gate.0", emb, _e((B, w0.shape[0]), v), act="relu")
-        K.dropout_(h, dp_mlp, site_seed(seed, 6))
+        K.dropout_(h, dp_mlp, rng, SITE_MLP)
         z = lin("xattn_gate.3", h, _e((B, 1), v))
         fused, g = _e((B, d), v), _e((B,), v)
         K.gate_mix_fwd(z, emb[:, :d], emb[:, d:], fused, g)
@@ -175,7 +175,7 @@ def head_backward(p: Dict[str, torch.Tensor], ctx: HeadCtx, dlogits: torch.Tenso
     cfg: HeadConfig = ctx.cfg
     sv = ctx.saved
     B, T, Ta, d, H = ctx.dims
-    seed = ctx.seed
+    rng = ctx.rng
     dp_attn, dp_path, dp_mlp, dp_prior = ctx.drops
     z = lambda *shape: torch.zeros(shape, device=dlogits.device, dtype=torch.float32)  # noqa: E731
     e = lambda *shape: torch.empty(shape, device=dlogits.device, dtype=torch.float32)  # noqa: E731
@@ -186,7 +186,7 @@ def head_backward(p: Dict[str, torch.Tensor], ctx: HeadCtx, dlogits: torch.Tenso
         h = sv["h"]
         dh = e(B, h.shape[1])
         K.linear_bwd(h, p["xattn_mlp.3.weight"], dlogits, dx=dh, dw=grads["xattn_mlp.3.weight"], db=grads["xattn_mlp.3.bias"])
-        K.relu_dropout_bwd_(dh, h, dp_mlp, site_seed(seed, 6))
+        K.relu_dropout_bwd_(dh, h, dp_mlp, rng, SITE_MLP)
         K.linear_bwd(emb, p["xattn_mlp.0.weight"], dh, dx=demb, dw=grads["xattn_mlp.0.weight"], db=grads["xattn_mlp.0.bias"])
     else:
         h, g, fused = sv["h"], sv["g"], sv["fused"]
@@ -198,7 +198,7 @@ def head_backward(p: Dict[str, torch.Tensor], ctx: HeadCtx, dlogits: torch.Tenso
         K.gate_mix_bwd(g, emb[:, :d], emb[:, d:], dfused, dz, demb[:, :d], demb[:, d:])
         dh = e(B, h.shape[1])
         K.linear_bwd(h, p["xattn_gate.3.weight"], dz, dx=dh, dw=grads["xattn_gate.3.weight"], db=grads["xattn_gate.3.bias"])
-        K.relu_dropout_bwd_(dh, h, dp_mlp, site_seed(seed, 6))
+        K.relu_dropout_bwd_(dh, h, dp_mlp, rng, SITE_MLP)
         K.linear_bwd(emb, p["xattn_gate.0.weight"], dh, dx=demb, dw=grads["xattn_gate.0.weight"],
                      db=grads["xattn_gate.0.bias"], dx_beta=1)
 
@@ -212,14 +212,14 @@ def head_backward(p: Dict[str, torch.Tensor], ctx: HeadCtx, dlogits: torch.Tenso
     da = e(B * Ta, d)
     da2 = e(B * Ta, d)
     K.add_ln_bwd(da1, sv["s_a"], sv["mu_a"], sv["rs_a"], p["a_norm.weight"], da, da2, grads["a_norm.weight"],
-                 grads["a_norm.bias"], Ta, dp_path, site_seed(seed, 5))
+                 grads["a_norm.bias"], Ta, dp_path, rng, SITE_APATH)
     do2 = e(B * Ta, d)
     K.linear_bwd(sv["o2"], p["a2v_attn.out_proj.weight"], da2, dx=do2, dw=grads["a2v_attn.out_proj.weight"],
                  db=grads["a2v_attn.out_proj.bias"])
     dq2, dkv2 = e(B * Ta, d), e(B * T, 2 * d)
     dbias_a2v = e(B, Ta, T) if cfg.use_prior else None
     K.mha_bwd(sv["q2"], sv["kv2"][:, :d], sv["kv2"][:, d:], sv["P2"], do2, dq2, dkv2[:, :d], dkv2[:, d:], dbias_a2v,
-              B, H, Ta, T, dp_attn, site_seed(seed, 4))
+              B, H, Ta, T, dp_attn, rng, SITE_A2V)
     w2 = p["a2v_attn.in_proj_weight"]
     gw2, gb2 = grads["a2v_attn.in_proj_weight"], grads["a2v_attn.in_proj_bias"]
     K.linear_bwd(sv["a"], w2[:d], dq2, dx=da, dw=gw2[:d], db=gb2[:d], dx_beta=1)
@@ -229,14 +229,14 @@ def head_backward(p: Dict[str, torch.Tensor], ctx: HeadCtx, dlogits: torch.Tenso
     dv = e(B * T, d)
     dv2 = e(B * T, d)
     K.add_ln_bwd(dv1, sv["s_v"], sv["mu_v"], sv["rs_v"], p["v_norm.weight"], dv, dv2, grads["v_norm.weight"],
-                 grads["v_norm.bias"], T, dp_path, site_seed(seed, 3))
+                 grads["v_norm.bias"], T, dp_path, rng, SITE_VPATH)
     do1 = e(B * T, d)
     K.linear_bwd(sv["o1"], p["v2a_attn.out_proj.weight"], dv2, dx=do1, dw=grads["v2a_attn.out_proj.weight"],
                  db=grads["v2a_attn.out_proj.bias"])
     dq1, dkv1 = e(B * T, d), e(B * Ta, 2 * d)
     dbias_v2a = e(B, T, Ta) if cfg.use_prior else None
     K.mha_bwd(sv["q1"], sv["kv1"][:, :d], sv["kv1"][:, d:], sv["P1"], do1, dq1, dkv1[:, :d], dkv1[:, d:], dbias_v2a,
-              B, H, T, Ta, dp_attn, site_seed(seed, 2))
+              B, H, T, Ta, dp_attn, rng, SITE_V2A)
     w1 = p["v2a_attn.in_proj_weight"]
     gw1, gb1 = grads["v2a_attn.in_proj_weight"], grads["v2a_attn.in_proj_bias"]
     K.linear_bwd(sv["v"], w1[:d], dq1, dx=dv, dw=gw1[:d], db=gb1[:d], dx_beta=1)
@@ -266,7 +266,7 @@ def head_backward(p: Dict[str, torch.Tensor], ctx: HeadCtx, dlogits: torch.Tenso
         dh1 = e(B, sv["h1"].shape[1])
         K.linear_bwd(sv["h1"], p[n + "prior_net.3.weight"], dprior, dx=dh1, dw=grads[n + "prior_net.3.weight"],
                      db=grads[n + "prior_net.3.bias"])
-        K.relu_dropout_bwd_(dh1, sv["h1"], dp_prior, site_seed(seed, 1))
+        K.relu_dropout_bwd_(dh1, sv["h1"], dp_prior, rng, SITE_PRIOR)
         dpg = e(B, 2 * d)
         K.linear_bwd(sv["pg"], p[n + "prior_net.0.weight"], dh1, dx=dpg, dw=grads[n + "prior_net.0.weight"],
                      db=grads[n + "prior_net.0.bias"])

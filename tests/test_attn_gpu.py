@@ -78,18 +78,19 @@ def test_mha_dropout_mask_regenerated_in_backward():
     torch.manual_seed(0)
     q = torch.randn(B * Lq, d, device="cuda")
     kv = torch.randn(B * Lk, 2 * d, device="cuda")
+    rng = torch.full((1,), 99, dtype=torch.int64, device="cuda")
     o0 = torch.empty(B * Lq, d, device="cuda")
     o1 = torch.empty(B * Lq, d, device="cuda")
     P = torch.empty(B, H, Lq, Lk, device="cuda")
-    K.mha_fwd(q, kv[:, :d], kv[:, d:], None, o0, P, B, H, Lq, Lk, drop_p=p, seed=99)
-    K.mha_fwd(q, kv[:, :d], kv[:, d:], None, o1, P, B, H, Lq, Lk, drop_p=p, seed=99)
+    K.mha_fwd(q, kv[:, :d], kv[:, d:], None, o0, P, B, H, Lq, Lk, drop_p=p, rng=rng, site=7)
+    K.mha_fwd(q, kv[:, :d], kv[:, d:], None, o1, P, B, H, Lq, Lk, drop_p=p, rng=rng, site=7)
     assert torch.equal(o0, o1)
     # dV = P'^T dO with dO = one-hot on one output column recovers column sums of P' per head
     dO = torch.zeros(B * Lq, d, device="cuda")
     dO[:, 0] = 1.0  # head 0, channel 0
     dq = torch.empty(B * Lq, d, device="cuda")
     dkv = torch.empty(B * Lk, 2 * d, device="cuda")
-    K.mha_bwd(q, kv[:, :d], kv[:, d:], P, dO, dq, dkv[:, :d], dkv[:, d:], None, B, H, Lq, Lk, drop_p=p, seed=99)
+    K.mha_bwd(q, kv[:, :d], kv[:, d:], P, dO, dq, dkv[:, :d], dkv[:, d:], None, B, H, Lq, Lk, drop_p=p, rng=rng, site=7)
     colsum_pd = dkv[:, d].view(B, Lk)  # sum_i P'[b,0,i,j]
     colsum_p = P[:, 0].sum(1)
     ratio = (colsum_pd / colsum_p).mean().item()

@@ -137,3 +137,41 @@ def test_audio_prefetch_matches_inline():
             assert torch.equal(seen[0], mb.audio_model.encode_sequence(a2))
     finally:
         G.ENABLED = prev
+
+
+@pytest.mark.parametrize("train", [False, True])
+def test_head_graph_matches_eager(train):
+    """xattn head alone (stub encoders, C2 feature shapes): graphed forward + backward reproduce the eager
+    head bit-for-bit except for fp32 atomics in the weight-gradient reductions (1e-5 relative), with dropout
+    masks drawn from the same host seeds in both modes."""
+    from multimodalemotionrecognition_amd.losses import CrossEntropyLoss
+    from multimodalemotionrecognition_amd.optim import FusedAdam
+    from tests.gpu_helpers import feats, head_model
+
+    prev = G.ENABLED
+    try:
+        v, a = feats(32, 8, 149, seed=7)
+        labels = torch.arange(32, device="cuda") % 8
+        runs = {}
+        for on in (False, True):
+            G.ENABLED = on
+            m = head_model("concat", False).train(train)
+            opt = FusedAdam([q for n, q in m.named_parameters() if not n.startswith(("audio_model", "video_model"))])
+            for it in range(3):  # eager, capture + replay, replay
+                opt.zero_grad()
+                vv = v.clone().requires_grad_(True)
+                torch.manual_seed(100 + it)
+                loss = CrossEntropyLoss()(m.xattn_from_features(vv, a), labels)
+                loss.backward()
+            runs[on] = (float(loss), vv.grad.clone(),
+                        {n: q.grad.clone() for n, q in m.named_parameters() if q.grad is not None})
+            if on:
+                assert m._head_graphs.graphs, "head graphs were not captured"
+        (le, dve, ge), (lg, dvg, gg) = runs[False], runs[True]
+        assert abs(le - lg) < 1e-6
+        assert float((dve - dvg).abs().max()) <= 1e-5 * float(dve.abs().max())
+        assert set(ge) == set(gg)
+        for n in ge:
+            assert float((ge[n] - gg[n]).abs().max()) <= 1e-4 * max(1e-6, float(ge[n].abs().max())), n
+    finally:
+        G.ENABLED = prev

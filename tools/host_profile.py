@@ -1,8 +1,8 @@
-"""Host-side issue cost of one train step vs its device time: python tools/host_time.py
-Enqueues a few steps without synchronising (the launch queue does not fill in 3 steps) and reports the
-host time per step next to the synchronised wall time per step."""
+"""cProfile of the host side of the bench train step (what the Python launcher spends per step):
+python tools/host_profile.py  -> top functions by cumulative / internal time over 10 steps."""
+import cProfile
+import pstats
 import sys
-import time
 from pathlib import Path
 
 import torch
@@ -22,14 +22,15 @@ def main():
     for _ in range(5):
         step(video, audio, labels, next_audio=audio)
     torch.cuda.synchronize()
-    for n in (1, 3):
-        t0 = time.perf_counter()
-        for _ in range(n):
-            step(video, audio, labels, next_audio=audio)
-        t1 = time.perf_counter()
-        torch.cuda.synchronize()
-        t2 = time.perf_counter()
-        print(f"{n} steps: host issue {1e3 * (t1 - t0) / n:.2f} ms/step, wall {1e3 * (t2 - t0) / n:.2f} ms/step")
+    pr = cProfile.Profile()
+    pr.enable()
+    for _ in range(10):
+        step(video, audio, labels, next_audio=audio)
+    pr.disable()
+    torch.cuda.synchronize()
+    st = pstats.Stats(pr)
+    st.sort_stats("tottime").print_stats(25)
+    st.sort_stats("cumulative").print_stats(30)
 
 
 if __name__ == "__main__":
