@@ -312,7 +312,7 @@ class FusionModel(nn.Module):
 
     def audio_encoder_frozen(self) -> bool:
         enc = getattr(self.audio_model, "wavlm", None)
-        return enc is not None and not any(q.requires_grad for q in enc.parameters())
+        return enc is not None and not enc.trainable()
 
     def prefetch_audio(self, audio: torch.Tensor) -> bool:
         """Start the frozen audio encoder on the NEXT batch's waveform, on the side stream, so it runs
@@ -348,13 +348,17 @@ class FusionModel(nn.Module):
         return float(seq[2].p)  # the nn.Dropout(0.2) of fusion.py:312-324
 
     def head_params(self):
-        names, params = [], []
-        for n, q in self.named_parameters():
-            if n.startswith(("audio_model.", "video_model.")):
-                continue
-            names.append(n)
-            params.append(q)
-        return tuple(names), params
+        """(names, params) of the fusion head (everything outside the two encoders), listed once."""
+        hp = self.__dict__.get("_mer_head_params")
+        if hp is None:
+            names, params = [], []
+            for n, q in self.named_parameters():
+                if n.startswith(("audio_model.", "video_model.")):
+                    continue
+                names.append(n)
+                params.append(q)
+            hp = self.__dict__["_mer_head_params"] = (tuple(names), params)
+        return hp
 
     def xattn_from_features(self, v_feat: torch.Tensor, a_seq: torch.Tensor) -> torch.Tensor:
         """xattn head on encoder features: v_feat [B,T,v_dim] (backbone output), a_seq [B,Ta,seq_dim]."""

@@ -69,9 +69,19 @@ class GraphCache:
         return g
 
 
+def module_tensors(module: torch.nn.Module) -> list:
+    """Every parameter and buffer of ``module``, listed once per module (the module tree is fixed after
+    construction; tensors are re-homed in place by .to() / FusedAdam, so the Python objects stay valid)."""
+    lst = module.__dict__.get("_mer_tensor_list")
+    if lst is None:
+        lst = list(module.parameters()) + list(module.buffers())
+        module.__dict__["_mer_tensor_list"] = lst
+    return lst
+
+
 def tensor_addresses(module: torch.nn.Module) -> tuple:
     """Device addresses of every parameter and buffer (part of a graph key)."""
-    return tuple(t.data_ptr() for t in module.parameters()) + tuple(t.data_ptr() for t in module.buffers())
+    return tuple(t.data_ptr() for t in module_tensors(module))
 
 
 def capturing() -> bool:

@@ -88,7 +88,8 @@ class TrainStep:
         """``next_audio``: the NEXT step's waveform batch, already on the device.  With a frozen audio
         encoder its forward is started on a side stream right after this step's forward, so it overlaps
         this step's backward (``FusionModel.prefetch_audio``); results are identical either way."""
-        self.model.train()
+        if not self.model.training:  # (a full module-tree walk; skipped when already in train mode)
+            self.model.train()
         self.opt.zero_grad()
         if self.mode in {"audio", "video"}:
             outputs = self.model(audio if self.mode == "audio" else video)

@@ -163,7 +163,9 @@ class ResNet18Trunk(nn.Sequential):
         """Persistent packed-weight buffers + the device descriptor table of one batched pack launch.
         Forward packs [K][R][S][Cp] for every conv (stem input padded to CP_IN); transposed packs
         [Cp][R][S][K] for every conv but the stem (the frames need no data gradient)."""
-        convs = [m for m in self.modules() if isinstance(m, nn.Conv2d)]
+        convs = self.__dict__.get("_mer_convs")
+        if convs is None:
+            convs = self.__dict__["_mer_convs"] = [m for m in self.modules() if isinstance(m, nn.Conv2d)]
         if transpose:
             convs = convs[1:]
         ptrs = tuple(c.weight.data_ptr() for c in convs)

@@ -145,8 +145,17 @@ class WavLMBackbone(nn.Module):
         self._graphs = G.GraphCache()
 
     # ---- frozen-weight preparation (runs once per weight version, on the GPU kernels) ----
+    def _param_list(self):
+        lst = self.__dict__.get("_mer_params")
+        if lst is None:
+            lst = self.__dict__["_mer_params"] = list(self.parameters())
+        return lst
+
     def _weights_key(self):
-        return tuple(weight_version(q) for q in self.parameters())
+        return tuple(weight_version(q) for q in self._param_list())
+
+    def trainable(self) -> bool:
+        return any(q.requires_grad for q in self._param_list())
 
     @torch.no_grad()
     def packed_weights(self):
@@ -365,7 +374,7 @@ class WavLMAudioEncoder(nn.Module):
 
     def encode_sequence(self, x: torch.Tensor, out_dtype=torch.bfloat16) -> torch.Tensor:
         """[B,1,S] or [B,S] -> [B, Ta, 768] hidden states (bf16 activations; wavlm_audio.py:165-183)."""
-        trainable = any(q.requires_grad for q in self.wavlm.parameters())
+        trainable = self.wavlm.trainable()
         if self.training and trainable and torch.is_grad_enabled():
             raise NotImplementedError("WavLM stage-2 fine-tuning (backward through the encoder) is a later build "
                                       "row; the north-star path trains with WavLM frozen (wavlm_audio.py:62-68)")
