@@ -78,6 +78,32 @@ int mer_add_ln_bwd(int rows, int d, int rows_per_sample, const float* dy, const 
 int mer_mean_pool_fwd(int B, int L, int D, const float* x, float* y, long ldy, void* stream);
 int mer_mean_pool_bwd(int B, int L, int D, const float* dy, long lddy, float* dx, int accumulate, void* stream);
 
+/* ---- temporal pooling (TemporalPooler 'attn' / 'transformer', temporal.py:9-75), fp32 ---- */
+
+/* y = dropout(gelu(z)) (exact erf GELU; temporal.py:18-19, the encoder layer's FFN) and its backward
+ * dz = dy * mask * gelu'(z); row-strided; mask index = row * cols + col. */
+int mer_gelu_dropout_fwd(int rows, int cols, const float* z, long ldz, float* y, long ldy, float p,
+                         const unsigned long long* seed, unsigned long long site, void* stream);
+int mer_gelu_dropout_bwd(int rows, int cols, const float* dy, long lddy, const float* z, long ldz, float* dz,
+                         long lddz, float p, const unsigned long long* seed, unsigned long long site, void* stream);
+
+/* y = x + dropout(r[row % r_period]) over contiguous rows (encoder residuals; r_period = L, p = 0 adds the
+ * sinusoidal positional encoding, temporal.py:42-43).  y may alias x. */
+int mer_add_dropout(int rows, int cols, const float* x, const float* r, int r_period, float p,
+                    const unsigned long long* seed, unsigned long long site, float* y, void* stream);
+
+/* Attention pooling (temporal.py:23-26): attn = softmax_L(scores [B,L]); y[b*ldy + c] = sum_l attn x[b,l,c];
+ * backward: dx (+)= attn dy, dscores = attn (dy.x_l - sum attn dy.x).  L <= 4096. */
+int mer_attn_pool_fwd(int B, int L, int D, const float* x, const float* scores, float* attn, float* y, long ldy,
+                      void* stream);
+int mer_attn_pool_bwd(int B, int L, int D, const float* x, const float* attn, const float* dy, long lddy, float* dx,
+                      int accumulate, float* dscores, void* stream);
+
+/* Softmax + dropout backward of head h for materialised attention (long self-attention whose fused kernel
+ * image exceeds LDS): dS = P (dPp m - rowsum(P dPp m)), Pd = P m; P [B,H,Lq,Lk], dPp/dS/Pd [B,Lq,Lk]. */
+int mer_softmax_dropout_bwd(int B, int H, int h, int Lq, int Lk, const float* P, const float* dPp, float* dS,
+                            float* Pd, float p, const unsigned long long* seed, unsigned long long site, void* stream);
+
 /* nn.CrossEntropyLoss(label_smoothing) (train.py:1033) or, late=1, NLLLoss(log(p+1e-8)) (train.py:212-214),
  * mean over the batch, fused with dloss/dlogits (for dloss = 1).  labels are int64. */
 int mer_cross_entropy(int B, int C, const float* logits, const long long* labels, float label_smoothing, int late,

@@ -293,6 +293,9 @@ class FusionModel(nn.Module):
             self.xattn_head = xattn_head
             self.attn_dropout = float(xattn_attn_dropout)
             self.temporal_pooling = temporal_pooling
+            self.temporal_num_heads = temporal_num_heads
+            self.temporal_num_layers = temporal_num_layers
+            self.temporal_dropout = float(temporal_dropout)
             if xattn_head == "concat":
                 self.xattn_mlp = nn.Sequential(nn.Linear(d_model * 2, common_dim), nn.ReLU(inplace=True),
                                                nn.Dropout(0.2), nn.Linear(common_dim, num_classes))
@@ -341,7 +344,8 @@ class FusionModel(nn.Module):
                              use_prior=self.emotion_prior_bias is not None, attn_dropout=self.attn_dropout,
                              drop_path=self.v_drop_path.drop_prob, mlp_dropout=self._mlp_dropout_p(),
                              prior_dropout=(self.emotion_prior_bias.dropout if self.emotion_prior_bias is not None else 0.0),
-                             temporal_pooling=self.temporal_pooling)
+                             temporal_pooling=self.temporal_pooling, temporal_num_heads=self.temporal_num_heads,
+                             temporal_num_layers=self.temporal_num_layers, temporal_dropout=self.temporal_dropout)
 
     def _mlp_dropout_p(self) -> float:
         seq = self.xattn_mlp if self.xattn_head == "concat" else self.xattn_gate

@@ -188,6 +188,57 @@ def mean_pool_bwd(dy, dx3d, accumulate=False):
     LIB("mer_mean_pool_bwd", B, L, D, dy.data_ptr(), dy.stride(0), dx3d.data_ptr(), int(accumulate), stream_ptr())
 
 
+def gelu_dropout_fwd(z, y, p=0.0, rng=None, site=0):
+    rows, cols = z.shape
+    LIB("mer_gelu_dropout_fwd", rows, cols, z.data_ptr(), z.stride(0), y.data_ptr(), y.stride(0), float(p),
+        rng_ptr(rng), int(site), stream_ptr())
+    return y
+
+
+def gelu_dropout_bwd(dy, z, dz, p=0.0, rng=None, site=0):
+    rows, cols = z.shape
+    LIB("mer_gelu_dropout_bwd", rows, cols, dy.data_ptr(), dy.stride(0), z.data_ptr(), z.stride(0), dz.data_ptr(),
+        dz.stride(0), float(p), rng_ptr(rng), int(site), stream_ptr())
+    return dz
+
+
+def add_dropout(x, r, y, r_period=None, p=0.0, rng=None, site=0):
+    """y = x + dropout(r[row % r_period]); all contiguous [rows, cols]."""
+    rows, cols = x.shape
+    _check_dev(x, r, y)
+    if not (x.is_contiguous() and r.is_contiguous() and y.is_contiguous()):
+        raise ValueError("add_dropout operands must be contiguous")
+    LIB("mer_add_dropout", rows, cols, x.data_ptr(), r.data_ptr(), int(r_period or rows), float(p), rng_ptr(rng),
+        int(site), y.data_ptr(), stream_ptr())
+    return y
+
+
+def attn_pool_fwd(x3d, scores, attn, y, ldy=None):
+    B, L, D = x3d.shape
+    LIB("mer_attn_pool_fwd", B, L, D, x3d.data_ptr(), scores.data_ptr(), attn.data_ptr(), y.data_ptr(),
+        int(ldy if ldy is not None else y.stride(0)), stream_ptr())
+
+
+def attn_pool_bwd(x3d, attn, dy, dx3d, dscores, accumulate=False):
+    B, L, D = x3d.shape
+    LIB("mer_attn_pool_bwd", B, L, D, x3d.data_ptr(), attn.data_ptr(), dy.data_ptr(), dy.stride(0), dx3d.data_ptr(),
+        int(accumulate), dscores.data_ptr(), stream_ptr())
+
+
+def softmax_dropout_bwd(P, dpp, ds, pd, h, p=0.0, rng=None, site=0):
+    B, H, Lq, Lk = P.shape
+    LIB("mer_softmax_dropout_bwd", B, H, int(h), Lq, Lk, P.data_ptr(), dpp.data_ptr(), ds.data_ptr(), pd.data_ptr(),
+        float(p), rng_ptr(rng), int(site), stream_ptr())
+
+
+def gemm_batched(a, b, out, *, M, N, K, sam, sak, bsa, sbk, sbn, bsb, ldc, bsc, batch, beta=0):
+    """out_z[M,N] (+)= A_z B_z over a batch of strided fp32 matrices (views into larger buffers)."""
+    _check_dev(a, b, out)
+    LIB("mer_gemm_f32", M, N, K, a.data_ptr(), _dt(a), sam, sak, bsa, b.data_ptr(), _dt(b), sbk, sbn, bsb,
+        out.data_ptr(), ldc, bsc, 0, int(beta), 0, 1, int(batch), stream_ptr())
+    return out
+
+
 def cross_entropy(logits, labels, loss, dlogits, label_smoothing=0.0, late=False):
     B, C = logits.shape
     if labels.dtype != torch.int64 or labels.numel() != B:

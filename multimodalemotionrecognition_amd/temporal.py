@@ -1,7 +1,7 @@
 """``TemporalPooler`` mirror (``src/models/temporal.py``): same constructor, submodule names and
-state-dict keys.  The 'mean' mode is the fusion default and runs in the HIP head kernels
-(``mer_mean_pool_fwd``); 'attn' / 'transformer' keep their parameters (checkpoint interop)
-and are a later row of the build plan.
+state-dict keys.  All three modes run on the HIP kernels: 'mean' (``mer_mean_pool_fwd``, the fusion
+default), 'attn' and 'transformer' through the explicit schedules of ``temporal_hip.py`` (one autograd
+node per pooler).
 """
 from __future__ import annotations
 
@@ -11,6 +11,7 @@ import torch
 from torch import nn
 
 from . import kernels as K
+from . import temporal_hip as TH
 
 
 class TemporalAttentionPooling(nn.Module):
@@ -62,6 +63,32 @@ class _MeanPoolFn(torch.autograd.Function):
         return dx
 
 
+class _PoolFn(torch.autograd.Function):
+    """'attn' / 'transformer' pooling of x [B, L, D] on the HIP schedule (temporal_hip.py)."""
+
+    @staticmethod
+    def forward(ctx, x, pooler, training, rng, names, *params):
+        from .fusion import grad_buffer  # noqa: F401  (imported for backward)
+
+        x = x.contiguous().float()
+        B, L, D = x.shape
+        p = dict(zip(names, params))
+        y = torch.empty(B, D, device=x.device, dtype=torch.float32)
+        ctx.pctx = TH.pool_forward(p, "pool", pooler.mode, x, y, num_heads=pooler.num_heads,
+                                   num_layers=pooler.num_layers, dropout=pooler.dropout if training else 0.0, rng=rng)
+        ctx.names, ctx.params = names, params
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        from .fusion import grad_buffer
+
+        p = dict(zip(ctx.names, ctx.params))
+        grads = {n: grad_buffer(t) for n, t in p.items() if t.requires_grad}
+        dx = TH.pool_backward(p, "pool", ctx.pctx, dy.contiguous().float(), grads)
+        return (dx, None, None, None, None, *[grads.get(n) for n in ctx.names])
+
+
 class TemporalPooler(nn.Module):
     """Configurable temporal aggregation: mean, attention, or transformer (temporal.py:78-110)."""
 
@@ -69,6 +96,7 @@ class TemporalPooler(nn.Module):
                  dropout: float = 0.1) -> None:
         super().__init__()
         self.mode = mode
+        self.num_heads, self.num_layers, self.dropout = num_heads, num_layers, float(dropout)
         if mode == "mean":
             self.pool = None
         elif mode == "attn":
@@ -85,4 +113,11 @@ class TemporalPooler(nn.Module):
             if not x.is_cuda:
                 raise RuntimeError("TemporalPooler runs on the MI355X kernels; move the input to the GPU")
             return _MeanPoolFn.apply(x)
-        raise NotImplementedError(f"temporal_pooling='{self.mode}' HIP kernels are a later build row")
+        if not x.is_cuda:
+            raise RuntimeError("TemporalPooler runs on the MI355X kernels; move the input to the GPU")
+        names, params = zip(*self.named_parameters())
+        rng = None
+        if self.training and self.dropout > 0:
+            seed = int(torch.randint(0, 2 ** 62, (1,)).item())  # host draw: torch.manual_seed reproduces it
+            rng = torch.full((1,), seed, dtype=torch.int64, device=x.device)
+        return _PoolFn.apply(x, self, self.training, rng, tuple(names), *params)

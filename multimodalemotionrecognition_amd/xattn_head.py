@@ -18,11 +18,13 @@ from typing import Dict, Optional
 import torch
 
 from . import kernels as K
+from . import temporal_hip as TH
 
 # Dropout / drop-path sites: the step's RNG base is a device int64 [1] tensor (``rng``) mixed with a
 # constant site id in-kernel (mer_site_seed), so the masks are regenerated in backward from (base, site)
 # and a captured graph draws fresh masks every replay.
 SITE_PRIOR, SITE_V2A, SITE_VPATH, SITE_A2V, SITE_APATH, SITE_MLP = 1, 2, 3, 4, 5, 6
+SITE_VPOOL, SITE_APOOL = 100, 300  # + 8 per transformer layer (temporal_hip.py)
 
 
 @dataclass
@@ -35,6 +37,9 @@ class HeadConfig:
     mlp_dropout: float = 0.2
     prior_dropout: float = 0.1
     temporal_pooling: str = "mean"
+    temporal_num_heads: int = 4
+    temporal_num_layers: int = 1
+    temporal_dropout: float = 0.1
 
 
 @dataclass
@@ -65,9 +70,6 @@ def head_forward(p: Dict[str, torch.Tensor], cfg: HeadConfig, v_feat: torch.Tens
                  training: bool, rng: Optional[torch.Tensor] = None, qlin: Optional[dict] = None):
     """Returns (logits [B, C], ctx).  ``rng``: the step's device RNG base (training dropout), ``qlin``: INT8
     images of the plain Linears (inference only)."""
-    if cfg.temporal_pooling != "mean":
-        raise NotImplementedError("HIP head implements temporal_pooling='mean' (fusion default); "
-                                  "attn/transformer pooling are a later row of the build plan")
     B, T, vd = v_feat.shape
     _, Ta, sd = a_seq.shape
     d = p["v_in_proj.weight"].shape[0]
@@ -136,10 +138,18 @@ def head_forward(p: Dict[str, torch.Tensor], cfg: HeadConfig, v_feat: torch.Tens
     K.add_ln_fwd(a, a2, p["a_norm.weight"], p["a_norm.bias"], a1, s_a, mu_a, rs_a, Ta, dp_path, rng, SITE_APATH)
     sv.update(q2=q2, kv2=kv2, o2=o2, P2=P2, a1=a1, s_a=s_a, mu_a=mu_a, rs_a=rs_a)
 
-    # ---- temporal mean pooling -> emb = [v_emb ; a_emb]  (fusion.py:401-406) ----
+    # ---- temporal pooling -> emb = [v_emb ; a_emb]  (fusion.py:401-406, temporal.py:105-110) ----
     emb = _e((B, 2 * d), v)
-    K.mean_pool_fwd(v1.view(B, T, d), emb[:, :d], ldy=2 * d)
-    K.mean_pool_fwd(a1.view(B, Ta, d), emb[:, d:], ldy=2 * d)
+    if cfg.temporal_pooling == "mean":
+        K.mean_pool_fwd(v1.view(B, T, d), emb[:, :d], ldy=2 * d)
+        K.mean_pool_fwd(a1.view(B, Ta, d), emb[:, d:], ldy=2 * d)
+    else:
+        dp_t = cfg.temporal_dropout if training else 0.0
+        kw = dict(num_heads=cfg.temporal_num_heads, num_layers=cfg.temporal_num_layers, dropout=dp_t, rng=rng)
+        sv["vpool"] = TH.pool_forward(p, "v_temporal_pool.pool", cfg.temporal_pooling, v1.view(B, T, d), emb[:, :d],
+                                      2 * d, site0=SITE_VPOOL, **kw)
+        sv["apool"] = TH.pool_forward(p, "a_temporal_pool.pool", cfg.temporal_pooling, a1.view(B, Ta, d),
+                                      emb[:, d:], 2 * d, site0=SITE_APOOL, **kw)
     sv["emb"] = emb
 
     if cfg.xattn_head == "concat":
@@ -203,10 +213,14 @@ def head_backward(p: Dict[str, torch.Tensor], ctx: HeadCtx, dlogits: torch.Tenso
                      db=grads["xattn_gate.0.bias"], dx_beta=1)
 
     # pooling backward
-    dv1 = e(B * T, d)
-    da1 = e(B * Ta, d)
-    K.mean_pool_bwd(demb[:, :d], dv1.view(B, T, d))
-    K.mean_pool_bwd(demb[:, d:], da1.view(B, Ta, d))
+    if cfg.temporal_pooling == "mean":
+        dv1 = e(B * T, d)
+        da1 = e(B * Ta, d)
+        K.mean_pool_bwd(demb[:, :d], dv1.view(B, T, d))
+        K.mean_pool_bwd(demb[:, d:], da1.view(B, Ta, d))
+    else:
+        dv1 = TH.pool_backward(p, "v_temporal_pool.pool", sv["vpool"], demb[:, :d], grads).view(B * T, d)
+        da1 = TH.pool_backward(p, "a_temporal_pool.pool", sv["apool"], demb[:, d:], grads).view(B * Ta, d)
 
     # ---- a2v backward ----
     da = e(B * Ta, d)
@@ -302,6 +316,9 @@ def used_param_names(cfg: HeadConfig):
                   n + "prior_net.3.bias"]
         for hname in ("v_query_bias", "a_key_bias", "a_query_bias", "v_key_bias"):
             names += [n + hname + ".weight", n + hname + ".bias"]
+    if cfg.temporal_pooling != "mean":
+        for pool in ("v_temporal_pool.pool", "a_temporal_pool.pool"):
+            names += TH.param_names(pool, cfg.temporal_pooling, cfg.temporal_num_layers)
     if cfg.xattn_head == "concat":
         names += ["xattn_mlp.0.weight", "xattn_mlp.0.bias", "xattn_mlp.3.weight", "xattn_mlp.3.bias"]
     else:

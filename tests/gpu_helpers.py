@@ -32,11 +32,14 @@ class StubAudio(nn.Module):
         return x
 
 
-def head_model(xattn_head="concat", use_prior=False, d_model=128, heads=4, v_dim=512, seq_dim=768, device="cuda"):
+def head_model(xattn_head="concat", use_prior=False, d_model=128, heads=4, v_dim=512, seq_dim=768, device="cuda",
+               pooling="mean", t_heads=4, t_layers=1, t_dropout=0.1):
     from multimodalemotionrecognition_amd.fusion import FusionModel
 
     m = FusionModel(StubAudio(seq_dim), StubVideo(v_dim), num_classes=8, mode="xattn", xattn_head=xattn_head,
-                    d_model=d_model, num_heads=heads, audio_n_mels=768, xattn_use_emotion_prior=use_prior)
+                    d_model=d_model, num_heads=heads, audio_n_mels=768, xattn_use_emotion_prior=use_prior,
+                    temporal_pooling=pooling, temporal_num_heads=t_heads, temporal_num_layers=t_layers,
+                    temporal_dropout=t_dropout)
     sd = m.state_dict()
     new = {k: torch.from_numpy(params.init_tensor(k, tuple(v.shape), 0)) for k, v in sd.items()}
     fusion_ref.gated_bias_init(new, xattn_head)
