@@ -317,6 +317,186 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_pipe_kernel(GemmArgs g) {
   }
 }
 
+// Phase-interleaved 256x256 tile (cdna_hip_programming.md §5 "256² 8-phase template", T3+T4), rows mode.
+// 8 waves as 2 (M) x 4 (N), 128x64 outputs each.  A K-tile (64 deep) is consumed in four phases, one
+// 64x32 accumulator quadrant per phase, and its LDS image is cut into four 16 KiB pieces in the order
+// the phases first read them:
+//   piece 0 = P0: A rows wr*128 + [0,64)    read in phase 0   (quadrants (0,0), (0,1))
+//   piece 1 = Q0: B rows wc*64  + [0,32)    read in phase 0   (quadrants (0,0), (1,0))
+//   piece 2 = Q1: B rows wc*64  + [32,64)   read in phase 1
+//   piece 3 = P1: A rows wr*128 + [64,128)  read in phase 2
+// Two K-tile buffers (128 KiB).  A piece of tile u+2 overwrites the same piece of tile u as soon as
+// every wave has read it (the barrier of the following phase proves that), one piece (2 glds per
+// thread) per phase:  phase (u,0) stages P1(u+1), (u,1) P0(u+2), (u,2) Q0(u+2), (u,3) Q1(u+2).
+// So each piece is issued 6-7 phases before its first read and five pieces (10 glds) stay in flight
+// across every barrier: phase p in {0,1,2} waits vmcnt(#younger glds) for its own piece, then one raw
+// s_barrier makes every wave's DMA visible.  Phase 3 reads nothing and needs no barrier.
+constexpr int PH_NT = 512, PH_PIECE = 128 * 64;  // threads; bf16 elements per piece
+
+__device__ __forceinline__ void wait_vm_even(int n) {  // n in {0,2,...,10}, wave-uniform
+  switch (n) {
+    case 10: wait_vmcnt<10>(); break;
+    case 8: wait_vmcnt<8>(); break;
+    case 6: wait_vmcnt<6>(); break;
+    case 4: wait_vmcnt<4>(); break;
+    case 2: wait_vmcnt<2>(); break;
+    default: wait_vmcnt<0>(); break;
+  }
+}
+
+template <typename TOUT>
+__global__ __launch_bounds__(PH_NT, 1) void gemm_phase_kernel(GemmArgs g) {
+  extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int nx = (g.N + 255) / 256, ny = (g.M + 255) / 256;
+  int tx, ty;
+  xcd_tile_grouped(blockIdx.x, nx, ny, 8, tx, ty);
+  const int m0 = ty * 256, n0 = tx * 256;
+  const int wr = w >> 2, wc = w & 3;
+  const int lrow = lane >> 3, lchunk = lane & 7;
+
+  // per-lane source of each piece's two glds (piece row pr = (w*2 + j)*8 + lrow)
+  const bf16_t* src[4][2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int pr = (w * 2 + j) * 8 + lrow;
+    const int sw = swz_chunk(pr, lchunk) * 8;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {  // A pieces P0 (h=0) / P1 (h=1)
+      int m = m0 + (pr >> 6) * 128 + h * 64 + (pr & 63);
+      m = m < g.M ? m : g.M - 1;
+      src[h ? 3 : 0][j] = g.A + (long)(m / g.a_rpg) * g.a_gstride + (long)(m % g.a_rpg) * g.a_rstride + sw;
+      int n = n0 + (pr >> 5) * 64 + h * 32 + (pr & 31);  // B pieces Q0 (h=0) / Q1 (h=1)
+      n = n < g.N ? n : g.N - 1;
+      src[1 + h][j] = g.B + (long)n * g.ldb + sw;
+    }
+  }
+  const int nk = g.K / 64;
+  // stage piece pc of K-tile u (skipped past the end)
+  auto stage = [&](int pc, int u) {
+    if (u >= nk) return;
+    bf16_t* dst = smem + ((u & 1) * 4 + pc) * PH_PIECE + w * 1024;
+    glds16(src[pc][0] + u * 64, dst);
+    glds16(src[pc][1] + u * 64, dst + 512);
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int fr = lane & 15, fq = lane >> 4;
+  auto read_frags = [&](const bf16_t* piece, int rbase, int n16, bf16x8 (*out)[2]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (i >= n16) break;
+      const int r = rbase + i * 16 + fr;
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+        out[i][s] = *reinterpret_cast<const bf16x8*>(piece + r * 64 + swz_chunk(r, s * 4 + fq) * 8);
+    }
+  };
+  auto sync = [&](int nyoung) {
+    wait_vm_even(nyoung);
+    __builtin_amdgcn_s_waitcnt((15) | (7 << 4) | (0 << 8) | (3 << 14));  // lgkmcnt(0) only
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  // prologue = the issues of virtual phases (-2,1..3) and (-1,0..3)
+  stage(0, 0); stage(1, 0); stage(2, 0); stage(3, 0);
+  stage(0, 1); stage(1, 1); stage(2, 1);
+
+  bf16x8 af[4][2], bq0[2][2], bq1[2][2];
+  for (int u = 0; u < nk; ++u) {
+    const int e1 = u + 1 < nk, e2 = u + 2 < nk;
+    const bf16_t* buf = smem + (u & 1) * 4 * PH_PIECE;
+    // phase 0: P0, Q0 -> quadrant (0,0)
+    sync(2 * (2 + 3 * e1));
+    stage(3, u + 1);
+    read_frags(buf + 0 * PH_PIECE, wr * 64, 4, af);
+    read_frags(buf + 1 * PH_PIECE, wc * 32, 2, bq0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][s], bq0[j][s], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    // phase 1: Q1 -> quadrant (0,1)
+    sync(2 * (1 + 4 * e1));
+    stage(0, u + 2);
+    read_frags(buf + 2 * PH_PIECE, wc * 32, 2, bq1);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][s], bq1[j][s], acc[i][2 + j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    // phase 2: P1 -> quadrant (1,0)
+    sync(2 * (4 * e1 + e2));
+    stage(1, u + 2);
+    read_frags(buf + 3 * PH_PIECE, wr * 64, 4, af);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][s], bq0[j][s], acc[4 + i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    // phase 3: no reads -> quadrant (1,1); Q1(u) was retired by every wave before phase 2's barrier
+    __builtin_amdgcn_sched_barrier(0);
+    stage(2, u + 2);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[4 + i][2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][s], bq1[j][s], acc[4 + i][2 + j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  }
+
+  TOUT* C = reinterpret_cast<TOUT*>(g.C);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int col = n0 + wc * 64 + j * 16 + fr;
+    if (col >= g.N) continue;
+    const float bv = g.bias ? g.bias[col] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wr * 128 + i * 16 + fq * 4 + r;
+        if (row >= g.M) continue;
+        float v = apply_act(acc[i][j][r] + bv, g.act);
+        if (g.R) v += bf2f(g.R[(long)row * g.ldr + col]);
+        stf<TOUT>(C, (long)row * g.ldc + col, v);
+      }
+  }
+}
+
+template <typename TOUT>
+int launch_phase_t(const GemmArgs& g, hipStream_t st) {
+  const long tiles = (long)((g.N + 255) / 256) * ((g.M + 255) / 256);
+  const size_t lds = 8 * PH_PIECE * sizeof(bf16_t);
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_phase_kernel<TOUT>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+    return (int)hipErrorInvalidConfiguration;
+  hipLaunchKernelGGL((gemm_phase_kernel<TOUT>), dim3((unsigned)tiles), dim3(PH_NT), lds, st, g);
+  return (int)hipGetLastError();
+}
+
 using CfgL = PipeCfg<256, 256, 2, 4>;  // 8 waves, 128x64 per wave, 128 KiB LDS
 using CfgM = PipeCfg<256, 128, 4, 2>;  // 8 waves, 64x64 per wave, 96 KiB LDS
 using CfgS = PipeCfg<128, 128, 2, 2>;  // 4 waves, 64x64 per wave, 64 KiB LDS
@@ -383,7 +563,7 @@ MER_API int mer_gemm_bf16_ex(int M, int N, int K, const void* A, long a_gstride,
                              const void* W, long ldw, void* C, int c_dtype, long ldc, const float* bias, const void* R,
                              long ldr, int act, int variant, void* stream) {
   if (M <= 0 || N <= 0) return 0;
-  if (variant < -1 || variant > 13) return (int)hipErrorInvalidValue;
+  if (variant < -1 || variant > 14) return (int)hipErrorInvalidValue;
   if (K % 8 != 0 || a_rpg <= 0 || (a_rstride % 8) != 0 || (a_gstride % 8) != 0 || (ldw % 8) != 0)
     return (int)hipErrorInvalidValue;
   if ((((uintptr_t)A) | ((uintptr_t)W)) & 15) return (int)hipErrorInvalidValue;
@@ -410,6 +590,7 @@ MER_API int mer_gemm_bf16_ex(int M, int N, int K, const void* A, long a_gstride,
     case 11: return launch_pipe<CfgV3>(g, c_dtype, st);
     case 12: return launch_pipe<CfgX2>(g, c_dtype, st);
     case 13: return launch_pipe<CfgY2>(g, c_dtype, st);
+    case 14: return c_dtype == MER_BF16 ? launch_phase_t<bf16_t>(g, st) : launch_phase_t<float>(g, st);
     default: return launch<0>(g, c_dtype, 1, st);
   }
 }

@@ -10,65 +10,125 @@
 // ---------------------------------------------------------------------------------------
 // Strided-batched fp32 GEMM on f32 MFMA:  C[m,n] (+)= act( sum_k A[m,k] B[k,n] + bias[n] )
 // A(m,k) at A[m*sam + k*sak], B(k,n) at B[k*sbk + n*sbn]; C row-major with ldc.
-// 64x64x16 tile, 256 threads = 4 waves of 32x32 (2x2 MFMA 16x16 tiles).
+// 64x64 tile, K chunks of 32, 256 threads = 4 waves of 32x32 (2x2 16x16 MFMA tiles).  Each thread
+// moves 8 consecutive elements of A and of B per chunk (16-byte loads where the operand's unit-stride
+// axis and alignment allow, VEC), the next chunk's loads are in flight while the current chunk is
+// multiplied out of the other LDS buffer (one barrier per chunk).  LDS images are k-major [k][m|n]
+// (+4 pad), so an MFMA operand read is 16 consecutive floats per k row.
 // splitk > 1: each K slice atomically adds into C (caller pre-initialises C; act must be 0).
 // ---------------------------------------------------------------------------------------
-template <typename TA, typename TB, bool A_KCONTIG, bool B_NCONTIG>
+constexpr int GF_BK = 32, GF_LD = 64 + 4;
+
+template <typename T>
+__device__ __forceinline__ void ld8(const T* p, float* v);
+template <>
+__device__ __forceinline__ void ld8<float>(const float* p, float* v) {
+  const f32x4 a = *reinterpret_cast<const f32x4*>(p), b = *reinterpret_cast<const f32x4*>(p + 4);
+  v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3]; v[4] = b[0]; v[5] = b[1]; v[6] = b[2]; v[7] = b[3];
+}
+template <>
+__device__ __forceinline__ void ld8<bf16_t>(const bf16_t* p, float* v) {
+  const uint4 u = *reinterpret_cast<const uint4*>(p);
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[2 * i] = __uint_as_float(w[i] << 16);
+    v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+
+// 8 elements of one operand: `lin` runs along the operand's unit-stride axis (8 consecutive
+// elements starting at lin0, valid below lin_end), `fix` is the other coordinate (valid when ok).
+template <typename T, bool VEC>
+__device__ __forceinline__ void load_seg(const T* base, long s_lin, long s_fix, int lin0, int lin_end, int fix, bool ok,
+                                         float* v) {
+  if (!ok) {
+#pragma unroll
+    for (int c = 0; c < 8; ++c) v[c] = 0.f;
+    return;
+  }
+  const T* p = base + (long)fix * s_fix + (long)lin0 * s_lin;
+  if (VEC && lin0 + 8 <= lin_end) {
+    ld8<T>(p, v);
+  } else {
+#pragma unroll
+    for (int c = 0; c < 8; ++c) v[c] = lin0 + c < lin_end ? ldf<T>(p, (long)c * s_lin) : 0.f;
+  }
+}
+
+template <typename TA, typename TB, bool A_KCONTIG, bool B_NCONTIG, bool VEC>
 __global__ __launch_bounds__(256) void gemm_f32_kernel(int M, int N, int K, const TA* __restrict__ A, long sam,
                                                        long sak, long bsa, const TB* __restrict__ B, long sbk,
                                                        long sbn, long bsb, float* __restrict__ C, long ldc,
                                                        long bsc, const float* __restrict__ bias, int beta,
                                                        int act, int splitk) {
-  __shared__ float As[16][64 + 4];
-  __shared__ float Bs[16][64 + 4];
+  __shared__ float As[2][GF_BK][GF_LD];
+  __shared__ float Bs[2][GF_BK][GF_LD];
   const int bz = blockIdx.z, batch = bz / splitk, ks = bz % splitk;
   A += batch * bsa;
   B += batch * bsb;
   C += batch * bsc;
   const int m0 = blockIdx.y * 64, n0 = blockIdx.x * 64;
-  const int kchunk = ((K + splitk - 1) / splitk + 15) / 16 * 16;
+  const int kchunk = ((K + splitk - 1) / splitk + GF_BK - 1) / GF_BK * GF_BK;
   const int kbeg = ks * kchunk, kend = min(K, kbeg + kchunk);
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int wm = (w >> 1) * 32, wn = (w & 1) * 32;
+  // this thread's segment: along k (row r = t>>2, k = (t&3)*8) or along m/n (k = t>>3, (t&7)*8)
+  const int sr = t >> 2, sk = (t & 3) * 8, tk = t >> 3, tc = (t & 7) * 8;
+  float ra[8], rb[8];
+  auto gload = [&](int k0) {
+    if (A_KCONTIG) load_seg<TA, VEC>(A, sak, sam, k0 + sk, kend, m0 + sr, m0 + sr < M, ra);
+    else load_seg<TA, VEC>(A, sam, sak, m0 + tc, M, k0 + tk, k0 + tk < kend, ra);
+    if (B_NCONTIG) load_seg<TB, VEC>(B, sbn, sbk, n0 + tc, N, k0 + tk, k0 + tk < kend, rb);
+    else load_seg<TB, VEC>(B, sbk, sbn, k0 + sk, kend, n0 + sr, n0 + sr < N, rb);
+  };
+  auto lstore = [&](int buf) {
+    if (A_KCONTIG) {
+#pragma unroll
+      for (int c = 0; c < 8; ++c) As[buf][sk + c][sr] = ra[c];
+    } else {
+      *reinterpret_cast<f32x4*>(&As[buf][tk][tc]) = f32x4{ra[0], ra[1], ra[2], ra[3]};
+      *reinterpret_cast<f32x4*>(&As[buf][tk][tc + 4]) = f32x4{ra[4], ra[5], ra[6], ra[7]};
+    }
+    if (B_NCONTIG) {
+      *reinterpret_cast<f32x4*>(&Bs[buf][tk][tc]) = f32x4{rb[0], rb[1], rb[2], rb[3]};
+      *reinterpret_cast<f32x4*>(&Bs[buf][tk][tc + 4]) = f32x4{rb[4], rb[5], rb[6], rb[7]};
+    } else {
+#pragma unroll
+      for (int c = 0; c < 8; ++c) Bs[buf][sk + c][sr] = rb[c];
+    }
+  };
+
   f32x4 acc[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  for (int k0 = kbeg; k0 < kend; k0 += 16) {
-    float ra[4], rb[4];
-    int am[4], ak[4], bk[4], bn[4];
+  if (kbeg < kend) {
+    gload(kbeg);
+    lstore(0);
+  }
+  __syncthreads();
+  int buf = 0;
+  for (int k0 = kbeg; k0 < kend; k0 += GF_BK, buf ^= 1) {
+    const bool more = k0 + GF_BK < kend;
+    if (more) gload(k0 + GF_BK);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int e = t + 256 * i;
-      if (A_KCONTIG) { am[i] = e >> 4; ak[i] = e & 15; } else { ak[i] = e >> 6; am[i] = e & 63; }
-      const int gm = m0 + am[i], gk = k0 + ak[i];
-      ra[i] = (gm < M && gk < kend) ? ldf<TA>(A, (long)gm * sam + (long)gk * sak) : 0.f;
-      if (B_NCONTIG) { bk[i] = e >> 6; bn[i] = e & 63; } else { bn[i] = e >> 4; bk[i] = e & 15; }
-      const int gn = n0 + bn[i], gk2 = k0 + bk[i];
-      rb[i] = (gn < N && gk2 < kend) ? ldf<TB>(B, (long)gk2 * sbk + (long)gn * sbn) : 0.f;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      As[ak[i]][am[i]] = ra[i];
-      Bs[bk[i]][bn[i]] = rb[i];
-    }
-    __syncthreads();
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk) {
+    for (int kk = 0; kk < GF_BK / 4; ++kk) {
       const int kr = kk * 4 + (lane >> 4);
       float a[2], b[2];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) a[i] = As[kr][wm + i * 16 + (lane & 15)];
+      for (int i = 0; i < 2; ++i) a[i] = As[buf][kr][wm + i * 16 + (lane & 15)];
 #pragma unroll
-      for (int j = 0; j < 2; ++j) b[j] = Bs[kr][wn + j * 16 + (lane & 15)];
+      for (int j = 0; j < 2; ++j) b[j] = Bs[buf][kr][wn + j * 16 + (lane & 15)];
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i], b[j], acc[i][j], 0, 0, 0);
     }
+    if (more) lstore(buf ^ 1);
+    __syncthreads();
   }
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -92,16 +152,32 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(int M, int N, int K, cons
       }
 }
 
+// VEC: the unit-stride axis of both operands allows 16-byte segment loads (8 elements of bf16,
+// 2 x 4 of fp32): base and every non-unit stride a multiple of the segment's alignment.
+template <typename T>
+static bool vec_ok(const void* p, long s1, long s2) {
+  const long al = 16 / (long)sizeof(T) >= 8 ? 8 : 4;  // elements per 16-byte load
+  return (((uintptr_t)p) & 15) == 0 && s1 % al == 0 && s2 % al == 0;
+}
+
 template <typename TA, typename TB>
 static int launch_gemm_f32(int M, int N, int K, const void* A, long sam, long sak, long bsa, const void* B, long sbk,
                            long sbn, long bsb, float* C, long ldc, long bsc, const float* bias, int beta, int act,
                            int splitk, int batch, hipStream_t st) {
   dim3 grid((N + 63) / 64, (M + 63) / 64, batch * splitk);
   const bool akc = (sak == 1), bnc = (sbn == 1);
-#define L(AK, BN)                                                                                                     \
-  hipLaunchKernelGGL((gemm_f32_kernel<TA, TB, AK, BN>), grid, dim3(256), 0, st, M, N, K, (const TA*)A, sam, sak, bsa, \
-                     (const TB*)B, sbk, sbn, bsb, C, ldc, bsc, bias, beta, act, splitk)
-  if (akc && bnc) L(true, true); else if (akc) L(true, false); else if (bnc) L(false, true); else L(false, false);
+  // the unit stride of each operand and its other strides must suit 16-byte loads
+  const bool va = akc ? vec_ok<TA>(A, sam, bsa) : (sam == 1 && vec_ok<TA>(A, sak, bsa));
+  const bool vb = bnc ? vec_ok<TB>(B, sbk, bsb) : (sbk == 1 && vec_ok<TB>(B, sbn, bsb));
+  const bool vec = va && vb;
+#define L(AK, BN, V)                                                                                                     \
+  hipLaunchKernelGGL((gemm_f32_kernel<TA, TB, AK, BN, V>), grid, dim3(256), 0, st, M, N, K, (const TA*)A, sam, sak, \
+                     bsa, (const TB*)B, sbk, sbn, bsb, C, ldc, bsc, bias, beta, act, splitk)
+  if (vec) {
+    if (akc && bnc) L(true, true, true); else if (akc) L(true, false, true); else if (bnc) L(false, true, true); else L(false, false, true);
+  } else {
+    if (akc && bnc) L(true, true, false); else if (akc) L(true, false, false); else if (bnc) L(false, true, false); else L(false, false, false);
+  }
 #undef L
   MER_LAUNCH_CHECK();
 }
@@ -144,8 +220,11 @@ __global__ __launch_bounds__(256) void colsum_kernel(int M, int N, const float* 
 
 MER_API int mer_colsum_f32(int M, int N, const float* X, long ldx, float* out, void* stream) {
   if (M <= 0 || N <= 0) return 0;
-  const int rpb = 256;
-  dim3 grid((N + 63) / 64, (M + rpb - 1) / rpb);
+  // ~1024 blocks of 4 row-groups: short per-thread row loops (latency-bound otherwise)
+  const int nx = (N + 63) / 64;
+  int rpb = (int)(((long)M * nx / 1024 + 3) / 4 * 4);
+  rpb = rpb < 16 ? 16 : (rpb > 256 ? 256 : rpb);
+  dim3 grid(nx, (M + rpb - 1) / rpb);
   hipLaunchKernelGGL(colsum_kernel, grid, dim3(256), 0, (hipStream_t)stream, M, N, X, ldx, out, rpb);
   MER_LAUNCH_CHECK();
 }

@@ -124,15 +124,56 @@ MER_API int mer_wavlm_conv0_gn_gelu(int B, int S, int Lout, const float* wav, co
 // Row LayerNorm (feature projection TF:93-105, encoder LN TF:418, post-LN layers TF:314-336).
 // x fp32 or bf16 [rows, d] (ldx), y bf16 or fp32 [rows, d] (ldy).  One wave per row.
 // ---------------------------------------------------------------------------------------
-template <typename TI, typename TO>
+template <typename T> __device__ __forceinline__ f32x4 ld4(const T* p);
+template <> __device__ __forceinline__ f32x4 ld4<float>(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
+template <> __device__ __forceinline__ f32x4 ld4<bf16_t>(const bf16_t* p) {
+  const uint2 u = *reinterpret_cast<const uint2*>(p);
+  return f32x4{__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
+               __uint_as_float(u.y & 0xffff0000u)};
+}
+template <typename T> __device__ __forceinline__ void st4(T* p, f32x4 v);
+template <> __device__ __forceinline__ void st4<float>(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
+template <> __device__ __forceinline__ void st4<bf16_t>(bf16_t* p, f32x4 v) {
+  *reinterpret_cast<uint2*>(p) = uint2{(uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16),
+                                       (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16)};
+}
+
+// VEC: d % 256 == 0 and 4-element aligned rows -- each lane moves 4 consecutive elements per access.
+template <typename TI, typename TO, bool VEC>
 __global__ __launch_bounds__(256) void layernorm_kernel(int rows, int d, const TI* __restrict__ x, long ldx,
                                                         const float* __restrict__ gamma, const float* __restrict__ beta,
                                                         float eps, TO* __restrict__ y, long ldy) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (row >= rows) return;
   const TI* xr = x + (long)row * ldx;
+  TO* yr = y + (long)row * ldy;
   float vals[16];  // d <= 1024
   float s = 0.f;
+  if (VEC) {
+    const int nv = d >> 8;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (i >= nv) break;
+      const f32x4 v = ld4<TI>(xr + (i * 64 + lane) * 4);
+      vals[4 * i] = v[0]; vals[4 * i + 1] = v[1]; vals[4 * i + 2] = v[2]; vals[4 * i + 3] = v[3];
+      s += (v[0] + v[1]) + (v[2] + v[3]);
+    }
+    const float mean = wave_sum(s) / d;
+    float q = 0.f;
+    for (int i = 0; i < 4 * nv; ++i) { const float v = vals[i] - mean; q += v * v; }
+    const float rstd = rsqrtf(wave_sum(q) / d + eps);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (i >= nv) break;
+      const int c = (i * 64 + lane) * 4;
+      const f32x4 g = *reinterpret_cast<const f32x4*>(gamma + c), b = *reinterpret_cast<const f32x4*>(beta + c);
+      f32x4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = (vals[4 * i + e] - mean) * rstd * g[e] + b[e];
+      st4<TO>(yr + c, o);
+    }
+    return;
+  }
   int n = 0;
   for (int c = lane; c < d; c += 64, ++n) {
     vals[n] = ldf<TI>(xr, c);
@@ -143,7 +184,7 @@ __global__ __launch_bounds__(256) void layernorm_kernel(int rows, int d, const T
   for (int i = 0; i < n; ++i) { const float v = vals[i] - mean; q += v * v; }
   const float rstd = rsqrtf(wave_sum(q) / d + eps);
   n = 0;
-  for (int c = lane; c < d; c += 64, ++n) stf<TO>(y + (long)row * ldy, c, (vals[n] - mean) * rstd * gamma[c] + beta[c]);
+  for (int c = lane; c < d; c += 64, ++n) stf<TO>(yr, c, (vals[n] - mean) * rstd * gamma[c] + beta[c]);
 }
 
 MER_API int mer_layernorm(int rows, int d, const void* x, int x_dtype, long ldx, const float* gamma,
@@ -151,7 +192,19 @@ MER_API int mer_layernorm(int rows, int d, const void* x, int x_dtype, long ldx,
   if (d > 1024 || rows <= 0) return rows <= 0 ? 0 : (int)hipErrorInvalidValue;
   dim3 grid((rows + 3) / 4);
   hipStream_t st = (hipStream_t)stream;
-#define L(TI, TO) hipLaunchKernelGGL((layernorm_kernel<TI, TO>), grid, dim3(256), 0, st, rows, d, (const TI*)x, ldx, gamma, beta, eps, (TO*)y, ldy)
+  const bool vec = d % 256 == 0 && ldx % 4 == 0 && ldy % 4 == 0 && ((((uintptr_t)x) | ((uintptr_t)y)) & 7) == 0 &&
+                   (((uintptr_t)x) & (x_dtype == MER_F32 ? 15 : 7)) == 0 &&
+                   (((uintptr_t)y) & (y_dtype == MER_F32 ? 15 : 7)) == 0 &&
+                   ((((uintptr_t)gamma) | ((uintptr_t)beta)) & 15) == 0;
+#define L(TI, TO)                                                                                              \
+  do {                                                                                                         \
+    if (vec)                                                                                                   \
+      hipLaunchKernelGGL((layernorm_kernel<TI, TO, true>), grid, dim3(256), 0, st, rows, d, (const TI*)x, ldx, \
+                         gamma, beta, eps, (TO*)y, ldy);                                                       \
+    else                                                                                                       \
+      hipLaunchKernelGGL((layernorm_kernel<TI, TO, false>), grid, dim3(256), 0, st, rows, d, (const TI*)x, ldx, \
+                         gamma, beta, eps, (TO*)y, ldy);                                                       \
+  } while (0)
   if (x_dtype == MER_F32 && y_dtype == MER_BF16) L(float, bf16_t);
   else if (x_dtype == MER_BF16 && y_dtype == MER_BF16) L(bf16_t, bf16_t);
   else if (x_dtype == MER_F32 && y_dtype == MER_F32) L(float, float);

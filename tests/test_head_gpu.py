@@ -149,6 +149,22 @@ def test_gemm_f32_transposes():
                 out = torch.empty(M, N, device="cuda")
                 K.gemm(ad, bd, out, trans_a=ta, trans_b=tb)
                 assert max_abs(out, ref) < 1e-3 * max(1.0, Kd ** 0.5), (M, N, Kd, ta, tb)
+    # bf16 operands (16-byte segment loads) and unaligned views (scalar segment path)
+    for (M, N, Kd) in [(37, 45, 70), (4768, 128, 768), (256, 512, 128)]:
+        a = torch.randn(M, Kd).bfloat16().float()
+        b = torch.randn(Kd, N).bfloat16().float()
+        ref = a @ b
+        for adt, bdt in ((torch.bfloat16, torch.float32), (torch.float32, torch.bfloat16), (torch.bfloat16, torch.bfloat16)):
+            for tb in (False, True):
+                bd = (b.t().contiguous() if tb else b).to(bdt).cuda()
+                out = torch.empty(M, N, device="cuda")
+                K.gemm(a.to(adt).cuda(), bd, out, trans_b=tb)
+                assert max_abs(out, ref) < 1e-3 * max(1.0, Kd ** 0.5), (M, N, Kd, adt, bdt, tb)
+        big = torch.randn(M, Kd + 1)
+        big[:, 1:] = a
+        out = torch.empty(M, N, device="cuda")
+        K.gemm(big.cuda()[:, 1:], b.cuda(), out)
+        assert max_abs(out, ref) < 1e-3 * max(1.0, Kd ** 0.5), (M, N, Kd, "unaligned")
     # split-K accumulate path
     a = torch.randn(4768, 128)
     x = torch.randn(4768, 768)
@@ -227,3 +243,27 @@ def test_c4_embedding_heads(mode):
         with torch.no_grad():
             out = m(torch.from_numpy(g["v_emb"]).cuda(), torch.from_numpy(g["a_emb"]).cuda())
     assert max_abs(out, g["out"]) < 1e-4
+
+
+def test_colsum_and_layernorm_paths():
+    """colsum (bias grads) and the row LayerNorm on its 4-wide (d % 256 == 0) and scalar paths."""
+    from multimodalemotionrecognition_amd import kernels as K
+
+    torch.manual_seed(3)
+    for M, N in [(1, 3), (4768, 128), (300, 768), (17, 1000)]:
+        x = torch.randn(M, N)
+        out = torch.zeros(N, device="cuda")
+        K.colsum(x.cuda(), out)
+        assert max_abs(out, x.sum(0)) < 1e-3 * max(1.0, M ** 0.5)
+    for rows, d in [(4768, 768), (5, 512), (33, 200), (7, 1024)]:
+        x = torch.randn(rows, d) * 3 + 1
+        g, b = torch.randn(d), torch.randn(d)
+        ref = torch.nn.functional.layer_norm(x, (d,), g, b, 1e-5)
+        for idt, odt in ((torch.float32, torch.bfloat16), (torch.float32, torch.float32), (torch.bfloat16, torch.bfloat16),
+                         (torch.bfloat16, torch.float32)):
+            xi = x.to(idt)
+            r = torch.nn.functional.layer_norm(xi.float(), (d,), g, b, 1e-5)
+            y = torch.empty(rows, d, device="cuda", dtype=odt)
+            K.layernorm(xi.cuda(), g.cuda(), b.cuda(), y)
+            tol = 2e-4 if odt == torch.float32 else 2e-2 * float(r.abs().max())
+            assert max_abs(y.float(), r) < tol, (rows, d, idt, odt)
