@@ -257,13 +257,18 @@ int mer_conv_wgrad_ex(int N, int H, int W, int C, int Creal, int K, int R, int S
 
 /* NCHW fp32 frames -> NHWC bf16 with channels zero-padded to Cp (<= 16). */
 int mer_pack_input_nhwc(int N, int C, int H, int W, int Cp, const float* x, void* y, void* stream);
+/* Space-to-depth stem input: fp32 NCHW [N][C<=4][H][W] (H, W even) -> bf16 [N][H/2+3][W/2+3][16].
+ * ResNet conv1 (7x7, stride 2, pad 3) then runs as a 4x4, stride-1, unpadded conv on 16 channels
+ * (K = 256 instead of 392), weights packed by mer_pack_conv_weights mode 2 (video.py:21-23 stem). */
+int mer_pack_input_s2d(int N, int C, int H, int W, const float* x, void* y, void* stream);
 
 /* PyTorch conv weight [K][C][R][S] fp32 -> bf16 [K][R][S][Cp] (transpose=0, forward) or [Cp][R][S][K]
  * (transpose=1, data-gradient operand); channels >= C are zero. */
 int mer_pack_conv_weight(int K, int C, int R, int S, int Cp, int transpose, const float* w, void* out, void* stream);
 
 /* n (<= 64) mer_pack_conv_weight layouts in one launch (the trunk's per-step re-pack).  desc: DEVICE table of
- * n records of 9 int64 {w, out, K, C, R, S, Cp, transpose, first element}, records in output order, first
+ * n records of 9 int64 {w, out, K, C, R, S, Cp, transpose, first element} (transpose 2: space-to-depth stem
+ * layout [K][(R+2)/2][(S+2)/2][Cp], see mer_pack_input_s2d), records in output order, first
  * elements the prefix sums of K*R*S*Cp; total = the sum. */
 int mer_pack_conv_weights(int n, const long long* desc, long total, void* stream);
 

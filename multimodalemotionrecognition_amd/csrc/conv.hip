@@ -918,6 +918,41 @@ MER_API int mer_pack_input_nhwc(int N, int C, int H, int W, int Cp, const float*
   MER_LAUNCH_CHECK();
 }
 
+// Space-to-depth stem input (ResNet conv1: 7x7, stride 2, pad 3 on C <= 4 channels, H and W even):
+// fp32 NCHW [N][C][H][W] -> bf16 [N][H/2+3][W/2+3][16], pixel (j, i) = 2x2 block (j-2, i-2) of the frame
+// with channel (dy*2 + dx)*C + c (zero for the 2 leading / 1 trailing border rows and columns and for
+// channels >= 4C).  The stride-2 7x7 conv then is a stride-1 4x4 conv with no padding on 16 channels
+// (K = 256 instead of 7*7*8 = 392 for the 8-channel-padded direct form); weights: pack mode 2 below.
+__global__ void pack_input_s2d_kernel(int N, int C, int H, int W, const float* __restrict__ x, bf16_t* __restrict__ y) {
+  const int Hs = H / 2 + 3, Ws = W / 2 + 3;
+  const long total = (long)N * Hs * Ws;
+  for (long p = blockIdx.x * (long)blockDim.x + threadIdx.x; p < total; p += (long)gridDim.x * blockDim.x) {
+    const int i = (int)(p % Ws);
+    const long q = p / Ws;
+    const int j = (int)(q % Hs), n = (int)(q / Hs);
+    uint32_t o[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+    const int jj = j - 2, ii = i - 2;
+    if (jj >= 0 && jj < H / 2 && ii >= 0 && ii < W / 2) {
+      const float* xn = x + (long)n * C * H * W;
+      for (int ch = 0; ch < 4 * C; ++ch) {
+        const int dydx = ch / C, c = ch - dydx * C;
+        const float v = xn[((long)c * H + 2 * jj + (dydx >> 1)) * W + 2 * ii + (dydx & 1)];
+        o[ch >> 1] |= (uint32_t)f2bf(v) << ((ch & 1) * 16);
+      }
+    }
+    u32x4* dst = reinterpret_cast<u32x4*>(y + p * 16);
+    dst[0] = u32x4{o[0], o[1], o[2], o[3]};
+    dst[1] = u32x4{o[4], o[5], o[6], o[7]};
+  }
+}
+MER_API int mer_pack_input_s2d(int N, int C, int H, int W, const float* x, void* y, void* stream) {
+  if (C < 1 || C > 4 || (H & 1) || (W & 1)) return (int)hipErrorInvalidValue;
+  const long total = (long)N * (H / 2 + 3) * (W / 2 + 3);
+  const int grid = (int)((total + 255) / 256 < 16384 ? (total + 255) / 256 : 16384);
+  hipLaunchKernelGGL(pack_input_s2d_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, N, C, H, W, x, (bf16_t*)y);
+  MER_LAUNCH_CHECK();
+}
+
 // PyTorch conv weight [K][C][R][S] fp32 -> fwd [K][R][S][Cp] (transpose=0) or dgrad [Cp][R][S][Kp] (transpose=1)
 __global__ void pack_w_kernel(int K, int C, int R, int S, int Cp, int transpose, const float* __restrict__ w,
                               bf16_t* __restrict__ out) {
@@ -943,7 +978,8 @@ MER_API int mer_pack_conv_weight(int K, int C, int R, int S, int Cp, int transpo
 
 // All of a trunk's weight packs in ONE launch (the per-step re-pack in training is ~40 small layouts
 // whose separate launches cost more than their bytes).  desc: n records of 9 int64 =
-// {w, out, K, C, R, S, Cp, transpose, first element (unused here)}; grid.y = record.  Both layouts go
+// {w, out, K, C, R, S, Cp, transpose (0, 1, or 2 = space-to-depth stem), first element (unused here)};
+// grid.y = record.  Both layouts go
 // through an LDS tile so global reads AND writes are contiguous runs:
 //   transpose 0: block = one output channel k: w[k][c][rs] (C*RS contiguous floats) -> out[k][rs][c<Cp];
 //   transpose 1: block = (input channel c, 64 output channels k0..): w[k][c][rs] (runs of RS) ->
@@ -954,7 +990,22 @@ __global__ __launch_bounds__(256) void pack_w_batched_kernel(const long long* __
   const float* w = reinterpret_cast<const float*>(r[0]);
   bf16_t* out = reinterpret_cast<bf16_t*>(r[1]);
   const int K = (int)r[2], C = (int)r[3], RS = (int)(r[4] * r[5]), Cp = (int)r[6];
-  if (!r[7]) {
+  if (r[7] == 2) {  // space-to-depth stem: out[k][ry][rx][ch], tap (r, s) = (2ry+dy-1, 2rx+dx-1), ch = (dy*2+dx)*C + c
+    const int k = blockIdx.x;
+    const int R = (int)r[4], S = (int)r[5], Ro = (R + 2) / 2, So = (S + 2) / 2;
+    if (k >= K) return;
+    const float* src = w + (long)k * C * RS;
+    for (int i = threadIdx.x; i < C * RS; i += 256) tile[i] = src[i];
+    __syncthreads();
+    bf16_t* dst = out + (long)k * Ro * So * Cp;
+    for (int i = threadIdx.x; i < Ro * So * Cp; i += 256) {
+      const int ch = i % Cp, q = i / Cp, rx = q % So, ry = q / So;
+      const int dydx = ch / C, c = ch - dydx * C;
+      const int rr = 2 * ry + (dydx >> 1) - 1, ss = 2 * rx + (dydx & 1) - 1;
+      const bool ok = dydx < 4 && rr >= 0 && rr < R && ss >= 0 && ss < S;
+      dst[i] = ok ? f2bf(tile[c * RS + rr * S + ss]) : (bf16_t)0;
+    }
+  } else if (!r[7]) {
     const int k = blockIdx.x;
     if (k >= K) return;
     const float* src = w + (long)k * C * RS;

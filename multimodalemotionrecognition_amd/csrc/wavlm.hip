@@ -214,19 +214,25 @@ MER_API int mer_layernorm(int rows, int d, const void* x, int x_dtype, long ldx,
 }
 
 // ---------------------------------------------------------------------------------------
-// Self-attention with WavLM's gated relative position bias (TF:147-241), one workgroup per (b, h):
+// Self-attention with WavLM's gated relative position bias (TF:147-241):
 //   gate_i = sigmoid(a_i) * (sigmoid(b_i) * const_h - 1) + 2,  (a_i, b_i) = pair-sums of
 //            gru_rel_pos_linear(x_i[h*dh:(h+1)*dh])                          (TF:163-177)
 //   S_ij   = scale * q_i.k_j + gate_i * emb[bucket(j - i), h]                 (TF:243-271)
 //   O_i    = softmax_j(S_i) V
 // Q/K/V come from one fused projection [B*L, 3*768] (q | k | v).  L <= 256, dh = 64.
-// QK^T and PV on v_mfma_f32_16x16x32_bf16; softmax in fp32 with wave shuffles.
+// Grid (B*H, ceil(L/64)): a workgroup stages K (row-major) and V^T of its (b, h) in LDS, and each
+// of its 4 waves owns 16 query rows.  The scores are computed TRANSPOSED, S^T = K Q^T
+// (v_mfma_f32_16x16x32_bf16, key j on the accumulator rows, query i = lane & 15), so every lane holds
+// whole key columns of one query: the softmax reduces in-lane plus two xor-shuffles, the gate is one
+// register per lane, and the accumulator tiles ARE the B operand of O^T = V^T P^T on
+// v_mfma_f32_16x16x16_bf16 (k = 4*(lane>>4) + e) -- P never goes through LDS.
 // ---------------------------------------------------------------------------------------
 namespace {
 constexpr int ADH = 64, APAD = ADH + 8;
+typedef __attribute__((ext_vector_type(4))) short s16x4;
 }
 
-__global__ __launch_bounds__(256, 2) void wavlm_attn_kernel(int L, int H, const bf16_t* __restrict__ qkv, long ldqkv,
+__global__ __launch_bounds__(256, 3) void wavlm_attn_kernel(int L, int H, const bf16_t* __restrict__ qkv, long ldqkv,
                                                          const bf16_t* __restrict__ x, long ldx,
                                                          const float* __restrict__ gw, const float* __restrict__ gb,
                                                          const float* __restrict__ gconst,
@@ -238,68 +244,86 @@ __global__ __launch_bounds__(256, 2) void wavlm_attn_kernel(int L, int H, const 
   const int VTP = LP + 8;
   bf16_t* Ks = reinterpret_cast<bf16_t*>(smem_raw);   // [LP][APAD]
   bf16_t* Vt = Ks + LP * APAD;                        // [ADH][VTP]
-  bf16_t* Ps = Vt + ADH * VTP;                        // [4][16][VTP]
-  float* gate = reinterpret_cast<float*>(Ps + 4 * 16 * VTP);  // [LP]
-  float* tbl = gate + LP;                              // [2L-1]
+  float* gate = reinterpret_cast<float*>(Vt + ADH * VTP);  // [4][16]
+  float* tbl = gate + 64;                              // [2L-1]
   const int b = blockIdx.x / H, h = blockIdx.x % H;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int D = H * ADH;
+  const int rb = blockIdx.y * 4 + w;  // this wave's 16-row query tile
+  const bool active = rb * 16 < L;    // wave-uniform
 
-  // stage K (row-major, padded) and V^T; zero the padding rows.  All loads of the (<= 8) passes are
-  // issued before the first LDS store so their latencies overlap (L <= 256: LP*8/256 <= 8 passes).
-  // Q is not staged: each wave reads its 16 query rows' fragments straight from global memory.
+  // this wave's Q fragments first (B operand of S^T = K Q^T: Q[i = lane&15][d = kk*32 + 8*(lane>>4) ..])
+  bf16x8 qb[2] = {bf16x8{0, 0, 0, 0, 0, 0, 0, 0}, bf16x8{0, 0, 0, 0, 0, 0, 0, 0}};
   {
-    u32x4 kr[8], vr[8];
+    const int qrow = rb * 16 + (lane & 15);
+    if (qrow < L)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+        qb[kk] = *reinterpret_cast<const bf16x8*>(qkv + ((long)b * L + qrow) * ldqkv + h * ADH + kk * 32 + (lane >> 4) * 8);
+  }
+  // stage K row-major (16-byte chunks) and V^T from 4-row groups (one 8-byte LDS store per channel);
+  // rows >= L are zero.  All global loads are issued before the first LDS store.
+  {
+    u32x4 kr[8];
 #pragma unroll
     for (int it = 0; it < 8; ++it) {
       const int c = t + it * 256, row = c >> 3, ch = c & 7;
       kr[it] = u32x4{0u, 0u, 0u, 0u};
-      vr[it] = kr[it];
-      if (c < LP * 8 && row < L) {
-        const bf16_t* base = qkv + ((long)b * L + row) * ldqkv + D + h * ADH + ch * 8;
-        kr[it] = *reinterpret_cast<const u32x4*>(base);
-        vr[it] = *reinterpret_cast<const u32x4*>(base + D);
+      if (c < LP * 8 && row < L)
+        kr[it] = *reinterpret_cast<const u32x4*>(qkv + ((long)b * L + row) * ldqkv + D + h * ADH + ch * 8);
+    }
+    u32x4 vr[2][4];
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+      const int q = t + it * 256, rq = q >> 3, ch = q & 7;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int row = rq * 4 + e;
+        vr[it][e] = u32x4{0u, 0u, 0u, 0u};
+        if (q < LP * 2 && row < L)
+          vr[it][e] = *reinterpret_cast<const u32x4*>(qkv + ((long)b * L + row) * ldqkv + 2 * D + h * ADH + ch * 8);
       }
     }
 #pragma unroll
     for (int it = 0; it < 8; ++it) {
       const int c = t + it * 256, row = c >> 3, ch = c & 7;
-      if (c < LP * 8) {
-        *reinterpret_cast<u32x4*>(&Ks[row * APAD + ch * 8]) = kr[it];
-        const bf16_t* hv = reinterpret_cast<const bf16_t*>(&vr[it]);
+      if (c < LP * 8) *reinterpret_cast<u32x4*>(&Ks[row * APAD + ch * 8]) = kr[it];
+    }
 #pragma unroll
-        for (int i = 0; i < 8; ++i) Vt[(ch * 8 + i) * VTP + row] = hv[i];
+    for (int it = 0; it < 2; ++it) {
+      const int q = t + it * 256, rq = q >> 3, ch = q & 7;
+      if (q < LP * 2) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {  // channel d = ch*8 + i: (V[4rq][d], .., V[4rq+3][d])
+          const int sh = (i & 1) * 16, wd = i >> 1;
+          const uint32_t v0 = (vr[it][0][wd] >> sh) & 0xffffu, v1 = (vr[it][1][wd] >> sh) & 0xffffu;
+          const uint32_t v2 = (vr[it][2][wd] >> sh) & 0xffffu, v3 = (vr[it][3][wd] >> sh) & 0xffffu;
+          *reinterpret_cast<uint2*>(&Vt[(ch * 8 + i) * VTP + rq * 4]) = uint2{v0 | (v1 << 16), v2 | (v3 << 16)};
+        }
       }
     }
   }
   for (int r = t; r < 2 * L - 1; r += 256) tbl[r] = rel_emb[(long)bucket[r] * H + h];
-  // gate per query row (fp32, from the layer input slice): 8 lanes per row, each lane one 16-byte
-  // chunk (8 channels) of x and the matching 8x8 block of gru_rel_pos_linear's weight in registers;
-  // the 8 projections are summed over the row's lanes with 3 xor-shuffles each.
-  {
+  // gate of this wave's 16 rows (fp32, from the layer input slice): 8 lanes per row, each lane one
+  // 16-byte chunk (8 channels) of x and the matching 8x8 block of gru_rel_pos_linear's weight.
+  if (active) {
     const int sub = lane >> 3, cl = lane & 7;
     float gwr[8][8];
 #pragma unroll
     for (int o = 0; o < 8; ++o)
 #pragma unroll
       for (int e = 0; e < 8; ++e) gwr[o][e] = gw[o * ADH + cl * 8 + e];
-    u32x4 xr[8];
-#pragma unroll
-    for (int it = 0; it < 8; ++it) {
-      const int i = w * 8 + it * 32 + sub;
-      xr[it] = u32x4{0u, 0u, 0u, 0u};
-      if (i < L) xr[it] = *reinterpret_cast<const u32x4*>(x + ((long)b * L + i) * ldx + h * ADH + cl * 8);
-    }
-    float gbs0 = gb[0] + gb[1] + gb[2] + gb[3], gbs1 = gb[4] + gb[5] + gb[6] + gb[7];
+    const float gbs0 = gb[0] + gb[1] + gb[2] + gb[3], gbs1 = gb[4] + gb[5] + gb[6] + gb[7];
     const float gc = gconst[h];
 #pragma unroll
-    for (int it = 0; it < 8; ++it) {
-      const int i = w * 8 + it * 32 + sub;
-      if (w * 8 + it * 32 >= LP) break;  // wave-uniform
+    for (int it = 0; it < 2; ++it) {
+      const int ri = it * 8 + sub, i = rb * 16 + ri;
+      u32x4 xr = u32x4{0u, 0u, 0u, 0u};
+      if (i < L) xr = *reinterpret_cast<const u32x4*>(x + ((long)b * L + i) * ldx + h * ADH + cl * 8);
       float pr[8];
 #pragma unroll
       for (int o = 0; o < 8; ++o) pr[o] = 0.f;
-      const bf16_t* xh = reinterpret_cast<const bf16_t*>(&xr[it]);
+      const bf16_t* xh = reinterpret_cast<const bf16_t*>(&xr);
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const float xe = bf2f(xh[e]);
@@ -312,117 +336,85 @@ __global__ __launch_bounds__(256, 2) void wavlm_attn_kernel(int L, int H, const 
         pr[o] += __shfl_xor(pr[o], 2, 64);
         pr[o] += __shfl_xor(pr[o], 4, 64);
       }
-      if (cl == 0 && i < LP) {
+      if (cl == 0) {
         float gsum = 1.f;
         if (i < L) {
           const float ga = 1.f / (1.f + __expf(-(pr[0] + pr[1] + pr[2] + pr[3] + gbs0)));
           const float gbv = 1.f / (1.f + __expf(-(pr[4] + pr[5] + pr[6] + pr[7] + gbs1)));
           gsum = ga * (gbv * gc - 1.f) + 2.f;
         }
-        gate[i] = gsum;
+        gate[w * 16 + ri] = gsum;
       }
     }
   }
   __syncthreads();
+  if (!active) return;
 
   const int NT = LP / 16;  // key tiles
-  bf16_t* Pw = Ps + w * 16 * VTP;
-  for (int rb = w; rb < NT; rb += 4) {
-    // S = Q K^T for 16 query rows x LP keys
-    f32x4 s[16];
+  const int i = rb * 16 + (lane & 15);
+  const float gi = gate[w * 16 + (lane & 15)];
+  // S^T tiles: s[ct][r] = S[i][j = ct*16 + 4*(lane>>4) + r]
+  f32x4 s[16];
 #pragma unroll
-    for (int ct = 0; ct < 16; ++ct) s[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
-    bf16x8 qa[2];
-    {
-      const int qrow = rb * 16 + (lane & 15);
+  for (int ct = 0; ct < 16; ++ct) s[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        qa[kk] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
-        if (qrow < L)
-          qa[kk] = *reinterpret_cast<const bf16x8*>(qkv + ((long)b * L + qrow) * ldqkv + h * ADH + kk * 32 + (lane >> 4) * 8);
-      }
-    }
+  for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const bf16x8 a = qa[kk];
-#pragma unroll
-      for (int ct = 0; ct < 16; ++ct) {
-        if (ct < NT) {
-          const bf16x8 bk = *reinterpret_cast<const bf16x8*>(&Ks[(ct * 16 + (lane & 15)) * APAD + kk * 32 + (lane >> 4) * 8]);
-          s[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bk, s[ct], 0, 0, 0);
-        }
-      }
-    }
-    float mx[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
-#pragma unroll
-    for (int ct = 0; ct < 16; ++ct) {
+    for (int ct = 0; ct < 16; ++ct)
       if (ct < NT) {
-        const int j = ct * 16 + (lane & 15);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int i = rb * 16 + (lane >> 4) * 4 + r;
-          float v = -INFINITY;
-          if (j < L) v = s[ct][r] * scale + gate[i] * tbl[j - i + L - 1 < 0 ? 0 : (j - i + L - 1 > 2 * L - 2 ? 2 * L - 2 : j - i + L - 1)];
-          s[ct][r] = v;
-          mx[r] = fmaxf(mx[r], v);
-        }
+        const bf16x8 ka = *reinterpret_cast<const bf16x8*>(&Ks[(ct * 16 + (lane & 15)) * APAD + kk * 32 + (lane >> 4) * 8]);
+        s[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka, qb[kk], s[ct], 0, 0, 0);
       }
-    }
+  float mx = -INFINITY;
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
-#pragma unroll
-      for (int o = 1; o < 16; o <<= 1) mx[r] = fmaxf(mx[r], __shfl_xor(mx[r], o, 64));
-    float sum[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int ct = 0; ct < 16; ++ct) {
-      if (ct < NT) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float p = __expf(s[ct][r] - mx[r]);
-          const bf16_t pb = f2bf(p);
-          sum[r] += bf2f(pb);  // normalise with the same rounded weights that enter PV
-          Pw[((lane >> 4) * 4 + r) * VTP + ct * 16 + (lane & 15)] = pb;
-        }
-      }
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-#pragma unroll
-      for (int o = 1; o < 16; o <<= 1) sum[r] += __shfl_xor(sum[r], o, 64);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    // O = P V  (16 rows x 64 dims)
-    f32x4 o[4];
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt) o[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int kk = 0; kk < LP / 32; ++kk) {
-      const bf16x8 a = *reinterpret_cast<const bf16x8*>(&Pw[(lane & 15) * VTP + kk * 32 + (lane >> 4) * 8]);
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt) {
-        const bf16x8 bv = *reinterpret_cast<const bf16x8*>(&Vt[(nt * 16 + (lane & 15)) * VTP + kk * 32 + (lane >> 4) * 8]);
-        o[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bv, o[nt], 0, 0, 0);
-      }
-    }
-    if (LP % 32) {  // odd 16-key tail
-      const int kk = LP / 32;
-      bf16x8 a = *reinterpret_cast<const bf16x8*>(&Pw[(lane & 15) * VTP + kk * 32 + (lane >> 4) * 8]);
-      if ((lane >> 4) >= 2) a = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt) {
-        bf16x8 bv = *reinterpret_cast<const bf16x8*>(&Vt[(nt * 16 + (lane & 15)) * VTP + kk * 32 + (lane >> 4) * 8]);
-        if ((lane >> 4) >= 2) bv = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
-        o[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bv, o[nt], 0, 0, 0);
-      }
-    }
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt)
+  for (int ct = 0; ct < 16; ++ct)
+    if (ct < NT)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int i = rb * 16 + (lane >> 4) * 4 + r;
-        if (i < L) out[((long)b * L + i) * ldo + h * ADH + nt * 16 + (lane & 15)] = f2bf(o[nt][r] / sum[r]);
+        const int j = ct * 16 + (lane >> 4) * 4 + r;
+        int rel = j - i + L - 1;
+        rel = rel < 0 ? 0 : (rel > 2 * L - 2 ? 2 * L - 2 : rel);
+        const float v = j < L ? s[ct][r] * scale + gi * tbl[rel] : -INFINITY;
+        s[ct][r] = v;
+        mx = fmaxf(mx, v);
       }
-    __builtin_amdgcn_wave_barrier();
+  mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  // P^T = exp(S^T - max) rounded to bf16 (the weights that enter PV also form the normaliser)
+  float sum = 0.f;
+  s16x4 pb[16];
+#pragma unroll
+  for (int ct = 0; ct < 16; ++ct)
+    if (ct < NT)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const bf16_t p = f2bf(__expf(s[ct][r] - mx));
+        sum += bf2f(p);
+        pb[ct][r] = (short)p;
+      }
+  sum += __shfl_xor(sum, 16, 64);
+  sum += __shfl_xor(sum, 32, 64);
+  // O^T[d][i] = sum_j V^T[d][j] P^T[j][i]: A = V^T (d = lane&15, j = ct*16 + 4*(lane>>4) + e)
+  f32x4 o[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ct = 0; ct < 16; ++ct)
+    if (ct < NT)
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const s16x4 va = *reinterpret_cast<const s16x4*>(&Vt[(dt * 16 + (lane & 15)) * VTP + ct * 16 + (lane >> 4) * 4]);
+        o[dt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(va, pb[ct], o[dt], 0, 0, 0);
+      }
+  if (i < L) {
+    const float inv = 1.f / sum;
+    bf16_t* orow = out + ((long)b * L + i) * ldo + h * ADH + (lane >> 4) * 4;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const uint32_t lo = (uint32_t)f2bf(o[dt][0] * inv) | ((uint32_t)f2bf(o[dt][1] * inv) << 16);
+      const uint32_t hi = (uint32_t)f2bf(o[dt][2] * inv) | ((uint32_t)f2bf(o[dt][3] * inv) << 16);
+      *reinterpret_cast<uint2*>(orow + dt * 16) = uint2{lo, hi};
+    }
   }
 }
 
@@ -431,12 +423,13 @@ MER_API int mer_wavlm_attention(int B, int L, int H, const void* qkv, long ldqkv
                                 const float* rel_emb, const int* bucket, void* out, long ldo, float scale,
                                 void* stream) {
   if (L > 256 || L <= 0) return (int)hipErrorInvalidValue;
+  if ((ldqkv % 8) || (ldx % 8) || (ldo % 4) || ((((uintptr_t)qkv) | ((uintptr_t)x)) & 15) || (((uintptr_t)out) & 7))
+    return (int)hipErrorInvalidValue;
   const int LP = (L + 15) / 16 * 16;
-  const size_t lds = sizeof(bf16_t) * ((size_t)LP * APAD + (size_t)ADH * (LP + 8) + 4 * 16 * (LP + 8)) +
-                     sizeof(float) * (LP + 2 * L);
-  hipLaunchKernelGGL(wavlm_attn_kernel, dim3(B * H), dim3(256), lds, (hipStream_t)stream, L, H, (const bf16_t*)qkv,
-                     ldqkv, (const bf16_t*)x, ldx, gate_w, gate_b, gate_const, rel_emb, bucket, (bf16_t*)out, ldo,
-                     scale);
+  const size_t lds = sizeof(bf16_t) * ((size_t)LP * APAD + (size_t)ADH * (LP + 8)) + sizeof(float) * (64 + 2 * L);
+  hipLaunchKernelGGL(wavlm_attn_kernel, dim3(B * H, (LP / 16 + 3) / 4), dim3(256), lds, (hipStream_t)stream, L, H,
+                     (const bf16_t*)qkv, ldqkv, (const bf16_t*)x, ldx, gate_w, gate_b, gate_const, rel_emb, bucket,
+                     (bf16_t*)out, ldo, scale);
   MER_LAUNCH_CHECK();
 }
 

@@ -26,19 +26,25 @@ class StaticGraph:
     """``fn(*static_inputs)`` captured once; ``replay(*inputs)`` copies inputs in and replays."""
 
     def __init__(self, fn: Callable, example_inputs, stream: Optional[torch.cuda.Stream] = None):
-        self.static_in = [t.detach().clone() for t in example_inputs]
-        self.graph = torch.cuda.CUDAGraph()
-        cur = stream if stream is not None else torch.cuda.current_stream()
-        side = torch.cuda.Stream(device=cur.device)
-        side.wait_stream(cur)
-        with torch.cuda.graph(self.graph, stream=side):
-            self.out = fn(*self.static_in)
-        cur.wait_stream(side)
+        # Static buffers and the capture are made outside inference mode even when the caller runs under
+        # torch.inference_mode() (the batch-inference runtime): inference tensors cannot be updated in place
+        # later by a replay's input copy, nor can the CUDA generator's graph-safe state tensors that the
+        # first capture of the process creates.
+        with torch.inference_mode(False):
+            self.static_in = [t.detach().clone() for t in example_inputs]
+            self.graph = torch.cuda.CUDAGraph()
+            cur = stream if stream is not None else torch.cuda.current_stream()
+            side = torch.cuda.Stream(device=cur.device)
+            side.wait_stream(cur)
+            with torch.cuda.graph(self.graph, stream=side):
+                self.out = fn(*self.static_in)
+            cur.wait_stream(side)
 
     def replay(self, *inputs):
         for st, x in zip(self.static_in, inputs):
             if st.data_ptr() != x.data_ptr():
-                st.copy_(x)
+                with torch.inference_mode(False):
+                    st.copy_(x)
         self.graph.replay()
         return self.out
 

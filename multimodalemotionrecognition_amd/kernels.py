@@ -431,6 +431,14 @@ def conv_wgrad(x, dy, dw, R, S, stride, pad, creal=None, variant=-1, splits=None
             x.data_ptr(), dy.data_ptr(), dw.data_ptr(), int(splits), ws.data_ptr(), int(variant), stream_ptr())
 
 
+def pack_input_s2d(x, y):
+    """fp32 NCHW frames -> space-to-depth bf16 [N][H/2+3][W/2+3][16] (the 4x4 stride-1 form of the stem conv)."""
+    N, C, H, W = x.shape
+    if tuple(y.shape) != (N, H // 2 + 3, W // 2 + 3, 16) or y.dtype != torch.bfloat16:
+        raise ValueError("pack_input_s2d shapes")
+    LIB("mer_pack_input_s2d", N, C, H, W, x.data_ptr(), y.data_ptr(), stream_ptr())
+
+
 def pack_input_nhwc(x, y):
     N, C, H, W = x.shape
     LIB("mer_pack_input_nhwc", N, C, H, W, y.shape[-1], x.data_ptr(), y.data_ptr(), stream_ptr())

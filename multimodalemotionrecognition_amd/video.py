@@ -23,7 +23,7 @@ from .nn_ops import hip_linear
 from .optim import weight_version
 from .temporal import TemporalPooler
 
-CP_IN = 8  # RGB padded to 8 channels so one 16-byte im2col chunk = one tap
+S2D_CH = 16  # stem input: 2x2 space-to-depth of RGB (12 channels) padded to 16 (mer_pack_input_s2d)
 
 
 class BasicBlock(nn.Module):
@@ -161,7 +161,7 @@ class ResNet18Trunk(nn.Sequential):
     # ---- bf16 weight packing: all convs in one launch, re-done whenever a weight's value changes ----
     def _pack_plan(self, transpose: bool):
         """Persistent packed-weight buffers + the device descriptor table of one batched pack launch.
-        Forward packs [K][R][S][Cp] for every conv (stem input padded to CP_IN); transposed packs
+        Forward packs [K][R][S][Cp] for every conv (the stem in its space-to-depth 4x4 form); transposed packs
         [Cp][R][S][K] for every conv but the stem (the frames need no data gradient)."""
         convs = self.__dict__.get("_mer_convs")
         if convs is None:
@@ -178,11 +178,16 @@ class ResNet18Trunk(nn.Sequential):
             Kc, C, R, S = c.weight.shape
             if C * R * S > 4608 or Kc > 512 or C > 512:  # the batched kernel's LDS tile / grid bounds
                 raise ValueError(f"conv {tuple(c.weight.shape)} exceeds mer_pack_conv_weights' tile bounds")
-            cp = max(CP_IN, (C + 7) // 8 * 8) if c is convs[0] and not transpose else C
-            shape = (cp, R * S * Kc) if transpose else (Kc, R * S * cp)
+            mode = int(transpose)
+            if c is convs[0] and not transpose:  # the stem: space-to-depth 4x4 layout (mer_pack_input_s2d)
+                mode, cp = 2, S2D_CH
+                shape = (Kc, ((R + 2) // 2) * ((S + 2) // 2) * cp)
+            else:
+                cp = C
+                shape = (cp, R * S * Kc) if transpose else (Kc, R * S * cp)
             buf = torch.empty(shape, device=dev, dtype=torch.bfloat16)
             outs[id(c)] = buf
-            rows.append([c.weight.data_ptr(), buf.data_ptr(), Kc, C, R, S, cp, int(transpose), first])
+            rows.append([c.weight.data_ptr(), buf.data_ptr(), Kc, C, R, S, cp, mode, first])
             first += buf.numel()
         plan = dict(convs=convs, ptrs=ptrs, outs=outs, total=first, vers=None,
                     desc=torch.tensor(rows, dtype=torch.int64).to(dev))
@@ -204,6 +209,8 @@ class ResNet18Trunk(nn.Sequential):
         if plan["vers"] is None:
             self.pack_all(transpose)
         buf = plan["outs"][id(conv)]
+        if conv is plan["convs"][0] and not transpose:
+            return buf  # the space-to-depth stem pack [K][4][4][16]
         if (buf.shape[0] if transpose else buf.shape[1] // (conv.weight.shape[2] * conv.weight.shape[3])) != cp:
             raise ValueError(f"packed weight channel padding {cp} does not match the plan")
         return buf
@@ -225,21 +232,46 @@ class _StatsArena:
     """One zeroed buffer for every conv's striped BatchNorm partial sums of a trunk forward
     (float[MER_BN_STAT_PARTS][C][2] per conv): one memset per forward instead of one per conv."""
 
-    def __init__(self, trunk, device):
+    def __init__(self, trunk, device, factor: int = 1):
         total = sum(m.out_channels for m in trunk.modules() if isinstance(m, nn.Conv2d))
-        self.buf = torch.zeros(K.BN_STAT_PARTS * 2 * total, device=device, dtype=torch.float32)
+        self.buf = torch.zeros(factor * K.BN_STAT_PARTS * 2 * total, device=device, dtype=torch.float32)
         self.off = 0
 
-    def take(self, C):
-        n = K.BN_STAT_PARTS * 2 * C
-        t = self.buf[self.off:self.off + n].view(K.BN_STAT_PARTS, C, 2)
+    def take(self, C, parts=None):
+        parts = K.BN_STAT_PARTS if parts is None else parts
+        n = parts * 2 * C
+        if self.off + n > self.buf.numel():
+            raise RuntimeError("BatchNorm statistics arena exhausted")
+        t = self.buf[self.off:self.off + n].view(parts, C, 2) if parts > 1 else self.buf[self.off:self.off + n].view(C, 2)
         self.off += n
         return t
 
 
-def _conv_bn(trunk, conv, bn, x, stride, pad, training, arena=None):
+def _check_stem(conv1, C, H, W):
+    if tuple(conv1.weight.shape[1:]) != (C, 7, 7) or conv1.stride != (2, 2) or conv1.padding != (3, 3) \
+            or C > 4 or H % 2 or W % 2:
+        raise ValueError("the space-to-depth stem expects conv1 = 7x7/s2/p3 on <= 4 channels and even H, W")
+
+
+def _stem_wgrad_index(R: int, S: int, C: int, device) -> torch.Tensor:
+    """Flat index into a [16][Ro][So] space-to-depth weight gradient for every (c, r, s) of the 7x7 one."""
+    So = (S + 2) // 2
+    Ro = (R + 2) // 2
+    idx = torch.empty(C, R, S, dtype=torch.int64)
+    for c in range(C):
+        for r in range(R):
+            for s_ in range(S):
+                ry, dy = divmod(r + 1, 2)
+                rx, dx = divmod(s_ + 1, 2)
+                idx[c, r, s_] = ((dy * 2 + dx) * C + c) * Ro * So + ry * So + rx
+    return idx.view(-1).to(device)
+
+
+def _conv_bn(trunk, conv, bn, x, stride, pad, training, arena=None, rs=None):
     """conv (+ fused batch stats) -> (conv output, (mean, rstd))."""
     Kc, _, R, S = conv.weight.shape
+    if rs is not None:
+        R, S = rs
     N, H, W, C = x.shape
     Ho, Wo = (H + 2 * pad - R) // stride + 1, (W + 2 * pad - S) // stride + 1
     y = torch.empty(N, Ho, Wo, Kc, device=x.device, dtype=torch.bfloat16)
@@ -296,11 +328,13 @@ def _trunk_forward(trunk: ResNet18Trunk, video: torch.Tensor, training: bool):
     N, C, H, W = video.shape
     dev = video.device
     bf = torch.bfloat16
-    x0 = torch.empty(N, H, W, CP_IN, device=dev, dtype=bf)
-    K.pack_input_nhwc(video, x0)
     conv1, bn1 = trunk[0], trunk[1]
+    _check_stem(conv1, C, H, W)
+    # stem conv 7x7/s2/p3 as a 4x4/s1/p0 conv on the 2x2 space-to-depth frames (K = 256, not 7*7*8)
+    x0 = torch.empty(N, H // 2 + 3, W // 2 + 3, S2D_CH, device=dev, dtype=bf)
+    K.pack_input_s2d(video, x0)
     arena = _StatsArena(trunk, dev) if training else None
-    c1, ms1 = _conv_bn(trunk, conv1, bn1, x0, 2, 3, training, arena)
+    c1, ms1 = _conv_bn(trunk, conv1, bn1, x0, 1, 0, training, arena, rs=(4, 4))
     a1 = torch.empty_like(c1)
     K.bn_apply(c1, ms1, bn1.weight, bn1.bias, a1, relu=True)
     Hp, Wp = (a1.shape[1] - 1) // 2 + 1, (a1.shape[2] - 1) // 2 + 1
@@ -337,21 +371,21 @@ def _bn_bwd(g, mask, x, ms, bn, red, grads, training):
     return dx
 
 
-def _bnr_target(blk_sv, blk, dev):
+def _bnr_target(blk_sv, blk, arena):
     """The fused-reduction target for a gradient flowing into ``blk``'s output: its bn2 (and downsample
     BN) read g = grad * (out > 0); returns (bnr tuple for conv_dgrad, partial buffers)."""
     xin, bc1, bms1, ba1, bc2, bms2, cd, msd, out = blk_sv
     C2 = bc2.shape[-1]
-    red2 = K.bn_stats_buffer(C2, dev)
+    red2 = arena.take(C2)
     if cd is None:
         return (out, bc2, bms2, red2), (red2, None)
-    redd = K.bn_stats_buffer(C2, dev)
+    redd = arena.take(C2)
     return (out, bc2, bms2, red2, cd, msd, redd), (red2, redd)
 
 
 @torch.no_grad()
 def block_backward(trunk, blk: BasicBlock, sv, dx: torch.Tensor, grads, training: bool = True, pre=None,
-                   prev=None):
+                   prev=None, arena=None):
     """Reverse of block_forward given dx = dL/d(block output); returns dL/d(block input).
 
     ``pre``: this block's bn2 / downsample-BN reductions already accumulated by the producer of ``dx``
@@ -359,21 +393,20 @@ def block_backward(trunk, blk: BasicBlock, sv, dx: torch.Tensor, grads, training
     (saved, block) of the preceding block, whose reductions this block's input-gradient dgrad fuses.
     """
     dev = dx.device
+    arena = _StatsArena(trunk, dev, factor=2) if arena is None else arena  # zeroed once per backward
     xin, bc1, bms1, ba1, bc2, bms2, cd, msd, out = sv
     g_out = dx
     s = blk.stride
     C2 = bc2.shape[-1]
-    red2 = torch.empty(C2, 2, device=dev, dtype=torch.float32)
-    redd = torch.empty(C2, 2, device=dev, dtype=torch.float32) if cd is not None else None
     if pre is not None:
-        K.partials_sum(pre[0], red2)
-        if cd is not None:
-            K.partials_sum(pre[1], redd)
+        red2 = K.partials_sum(pre[0], torch.empty(C2, 2, device=dev, dtype=torch.float32))
+        redd = K.partials_sum(pre[1], torch.empty(C2, 2, device=dev, dtype=torch.float32)) if cd is not None else None
     else:
-        red2.zero_()
+        red2 = arena.take(C2, parts=1)
         K.bn_bwd_reduce(g_out, out, bc2, bms2, red2)
+        redd = None
         if cd is not None:
-            redd.zero_()
+            redd = arena.take(C2, parts=1)
             K.bn_bwd_reduce(g_out, out, cd, msd, redd)
     dc2 = _bn_bwd(g_out, out, bc2, bms2, blk.bn2, red2, grads, training)
     dcd = _bn_bwd(g_out, out, cd, msd, blk.downsample[1], redd, grads, training) if cd is not None else None
@@ -383,7 +416,7 @@ def block_backward(trunk, blk: BasicBlock, sv, dx: torch.Tensor, grads, training
         K.conv_wgrad(ba1, dc2, w2, 3, 3, 1, 1)
     da1 = torch.empty_like(ba1)
     C1 = bc1.shape[-1]
-    red1p = K.bn_stats_buffer(C1, dev)
+    red1p = arena.take(C1)
     K.conv_dgrad(dc2, trunk.packed(blk.conv2, C2, True), da1, 3, 3, 1, 1, bnr=(ba1, bc1, bms1, red1p))
     red1 = K.partials_sum(red1p, torch.empty(C1, 2, device=dev, dtype=torch.float32))
     dc1 = _bn_bwd(da1, ba1, bc1, bms1, blk.bn1, red1, grads, training)
@@ -393,7 +426,7 @@ def block_backward(trunk, blk: BasicBlock, sv, dx: torch.Tensor, grads, training
         K.conv_wgrad(xin, dc1, w1, 3, 3, s, 1)
     dxin = torch.empty_like(xin)
     Cin = xin.shape[-1]
-    bnr, nxt = _bnr_target(prev[0], prev[1], dev) if prev is not None else (None, None)
+    bnr, nxt = _bnr_target(prev[0], prev[1], arena) if prev is not None else (None, None)
     if cd is not None:
         wd = _grad(blk.downsample[0].weight, grads)
         if wd is not None:
@@ -422,19 +455,27 @@ def _trunk_backward(trunk: ResNet18Trunk, saved, dfeat: torch.Tensor, training: 
     blocks = _blocks(trunk)
     svs = saved["blocks"]
     pre = None
+    arena = _StatsArena(trunk, dev, factor=2)  # every backward BatchNorm reduction: one memset
     for i in reversed(range(len(blocks))):
         prev = (svs[i - 1], blocks[i - 1]) if i > 0 else None
-        dx, pre = block_backward(trunk, blocks[i], svs[i], dx, grads, training, pre=pre, prev=prev)
+        dx, pre = block_backward(trunk, blocks[i], svs[i], dx, grads, training, pre=pre, prev=prev, arena=arena)
     # stem: maxpool -> bn1/relu -> conv1 (no data gradient for the frames)
     x0, c1, ms1, a1, arg = saved["stem"]
     da1 = torch.empty_like(a1)
     K.maxpool_bwd(dx, arg, da1)
-    red = torch.zeros(c1.shape[-1], 2, device=dev, dtype=torch.float32)
+    red = arena.take(c1.shape[-1], parts=1)
     K.bn_bwd_reduce(da1, a1, c1, ms1, red)
     dc1 = _bn_bwd(da1, a1, c1, ms1, trunk[1], red, grads, training)
     w = _grad(trunk[0].weight, grads)
-    if w is not None:
-        K.conv_wgrad(x0, dc1, w, 7, 7, 2, 3, creal=3)
+    if w is not None:  # wgrad of the 4x4 space-to-depth form, then gathered back to [64][3][7][7]
+        Kc, Cin, R, S = trunk[0].weight.shape
+        ws2d = torch.empty(Kc, S2D_CH, (R + 2) // 2, (S + 2) // 2, device=dev, dtype=torch.float32)
+        ws2d.zero_()
+        K.conv_wgrad(x0, dc1, ws2d, ws2d.shape[2], ws2d.shape[3], 1, 0)
+        idx = trunk.__dict__.get("_mer_stem_idx")
+        if idx is None or idx.device != dev:
+            idx = trunk.__dict__["_mer_stem_idx"] = _stem_wgrad_index(R, S, Cin, dev)
+        w.add_(ws2d.view(Kc, -1).index_select(1, idx).view_as(w))
     return grads
 
 

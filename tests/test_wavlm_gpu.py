@@ -7,6 +7,7 @@ import pytest
 import torch
 
 from oracle import params, wavlm_ref
+from tests.gpu_helpers import max_abs
 from tests.helpers import golden
 
 pytestmark = pytest.mark.gpu
@@ -127,3 +128,36 @@ def test_posconv_gemm_vs_torch(L):
                         r.cuda().view(B * L, C), act="gelu")
     err = float((out.cpu().view(B, L, C) - ref).abs().max())
     assert err < 2e-2, err
+
+
+@pytest.mark.parametrize("L", [1, 17, 64, 149, 200, 256])
+def test_wavlm_attention_vs_torch(L):
+    """Gated-relative-position self-attention kernel vs an fp32 torch restatement of TF:147-271 on the
+    same bf16 Q/K/V/x (tolerance: P is rounded to bf16 before PV -> 2e-2 of max|O|)."""
+    from multimodalemotionrecognition_amd import kernels as K
+    from multimodalemotionrecognition_amd.wavlm_audio import relative_position_buckets
+
+    torch.manual_seed(L)
+    B, H, dh = 2, 12, 64
+    D = H * dh
+    qkv = torch.randn(B * L, 3 * D).bfloat16()
+    x = torch.randn(B * L, D).bfloat16()
+    gw, gb = torch.randn(8, dh) * 0.1, torch.randn(8) * 0.1
+    gc = torch.rand(H) + 0.5
+    rel_emb = torch.randn(320, H)
+    bucket = torch.from_numpy(relative_position_buckets(L)).long()
+    scale = dh ** -0.5
+    out = torch.empty(B * L, D, dtype=torch.bfloat16, device="cuda")
+    K.wavlm_attention(qkv.cuda(), x.cuda(), gw.cuda(), gb.cuda(), gc.cuda(), rel_emb.cuda(),
+                      bucket.int().cuda(), out, B, L, H, scale)
+    q, k, v = (qkv.float()[:, i * D:(i + 1) * D].view(B, L, H, dh).transpose(1, 2) for i in range(3))
+    proj = x.float().view(B, L, H, dh) @ gw.t() + gb                       # [B,L,H,8]
+    ga = torch.sigmoid(proj[..., :4].sum(-1))
+    gbv = torch.sigmoid(proj[..., 4:].sum(-1))
+    gate = (ga * (gbv * gc - 1) + 2).transpose(1, 2)                        # [B,H,L]
+    rel = torch.arange(L)[None, :] - torch.arange(L)[:, None] + L - 1     # j - i + L - 1
+    bias = rel_emb[bucket[rel]].permute(2, 0, 1)                            # [H,L,L]
+    s = scale * q @ k.transpose(-1, -2) + gate[..., None] * bias[None]
+    ref = (torch.softmax(s, -1) @ v).transpose(1, 2).reshape(B * L, D)
+    err = max_abs(out.float(), ref)
+    assert err < 2e-2 * float(ref.abs().max()), err

@@ -15,7 +15,10 @@ SHAPES = {
     "ffn1": (B * 149, 3072, 768, None, None),
     "ffn2": (B * 149, 768, 3072, None, None),
     "out_proj": (B * 149, 768, 768, None, None),
+    "sq4096": (4096, 4096, 4096, None, None),
+    "sq8192": (8192, 8192, 8192, None, None),
 }
+ONLY = next((a.split("=")[1].split(",") for a in sys.argv if a.startswith("--shapes=")), None)
 
 
 VARIANTS = [int(v) for v in next((a.split("=")[1] for a in sys.argv if a.startswith("--variants=")),
@@ -27,6 +30,8 @@ def main():
     quick = "--quick" in sys.argv  # profiling: fewer shapes / reps
     for name, (M, N, Kd, rows, alen) in SHAPES.items():
         if quick and name not in ("conv1 (rows)", "qkv", "ffn2"):
+            continue
+        if (ONLY is None and name.startswith("sq")) or (ONLY is not None and name.split()[0] not in ONLY):
             continue
         a = (torch.rand(alen if rows else M * Kd, device="cuda") * 2 - 1).bfloat16()
         if not rows:
