@@ -292,6 +292,19 @@ int mer_bn_bwd_apply(long M, int C, const void* dy, const void* mask, const void
                      const float* gamma, const float* red, int batch_stats, void* dx, float* dgamma, float* dbeta,
                      void* stream);
 
+/* Fused stem tail (C % 8 == 0, C <= 512, N*H*W < 2^22; x = the stem conv output [N][H][W][C] bf16):
+ * y = maxpool3x3s2p1(bf16(relu(bn(x)))) with argmax taps, the BN/ReLU activation never stored.
+ * Replaces bn_apply + maxpool_fwd for torchvision's conv1 -> bn1 -> relu -> maxpool (video.py:21-23). */
+int mer_stem_bnrelu_maxpool_fwd(int N, int H, int W, int C, const void* x, const float* ms, const float* gamma,
+                                const float* beta, void* y, void* argmax, void* stream);
+/* Its backward to the conv output: the maxpool gather of dy is written to dx, then g = dx * relu'(bn(x)) (mask
+ * recomputed from x, no activation tensor) feeds a BatchNorm reduction (red[C][2] += (sum g, sum g*xhat); red
+ * zeroed by the caller) and an in-place apply pass
+ * dx = gamma*rstd*(g - [batch_stats] (sum g + xhat * sum g*xhat)/M); dgamma += sum g*xhat, dbeta += sum g. */
+int mer_stem_pool_bn_bwd(int N, int H, int W, int C, const void* dy, const void* argmax, const void* x,
+                         const float* ms, const float* gamma, const float* beta, float* red, int batch_stats,
+                         void* dx, float* dgamma, float* dbeta, void* stream);
+
 /* MaxPool2d(3, 2, 1) forward (argmax tap saved as uint8) and gather backward. */
 int mer_maxpool_fwd(int N, int H, int W, int C, const void* x, void* y, void* argmax, void* stream);
 int mer_maxpool_bwd(int N, int H, int W, int C, const void* dy, const void* argmax, void* dx, void* stream);

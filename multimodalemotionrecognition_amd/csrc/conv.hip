@@ -1174,11 +1174,23 @@ MER_API int mer_bn_apply(long M, int C, const void* x, const float* ms, const fl
   MER_LAUNCH_CHECK();
 }
 
+// BatchNorm folded to (scale, shift) for channel c from ms = (mean, rstd) pairs
+__device__ __forceinline__ void stem_bn_coef(int c, const float* ms, const float* gamma, const float* beta, float& sc,
+                                             float& sh) {
+  sc = ms[2 * c + 1] * gamma[c];
+  sh = beta[c] - ms[2 * c] * sc;
+}
+
 // BN backward reduction: g = dy * (mask > 0) (mask = the ReLU output, or null), xhat from x and ms:
 //   red[c] = (sum g, sum g*xhat)   (fp32 atomics, red pre-zeroed).  C <= 512, C % 8 == 0.
+// BNMASK: no mask tensor; the ReLU mask is recomputed as bf16(relu(x*scale + shift)) > 0 from (ms, mgamma,
+// mbeta) -- the fused stem, whose activation is never stored.
+template <bool BNMASK>
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(long M, int C, const bf16_t* __restrict__ dy,
                                                             const bf16_t* __restrict__ mask,
                                                             const bf16_t* __restrict__ x, const float* __restrict__ ms,
+                                                            const float* __restrict__ mgamma,
+                                                            const float* __restrict__ mbeta,
                                                             float* __restrict__ red, long rows_per_block) {
   __shared__ float part[2][512];
   for (int i = threadIdx.x; i < 2 * 512; i += 256) (&part[0][0])[i] = 0.f;
@@ -1189,21 +1201,27 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(long M, int C, const
   const long r0 = blockIdx.x * rows_per_block, r1 = min(M, r0 + rows_per_block);
   float s1[8] = {0.f}, s2[8] = {0.f};
   if (tr < rows_per_iter) {
-    float mean[8], rstd[8];
+    float mean[8], rstd[8], msc[8], msh[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) { mean[i] = ms[2 * (tc * 8 + i)]; rstd[i] = ms[2 * (tc * 8 + i) + 1]; }
+    for (int i = 0; i < 8; ++i) {
+      mean[i] = ms[2 * (tc * 8 + i)];
+      rstd[i] = ms[2 * (tc * 8 + i) + 1];
+      if (BNMASK) stem_bn_coef(tc * 8 + i, ms, mgamma, mbeta, msc[i], msh[i]);
+    }
     for (long r = r0 + tr; r < r1; r += rows_per_iter) {
       const long off = r * C + tc * 8;
       const u32x4 gv = *reinterpret_cast<const u32x4*>(dy + off);
       const u32x4 xv = *reinterpret_cast<const u32x4*>(x + off);
       u32x4 mv = {1u, 1u, 1u, 1u};
-      if (mask) mv = *reinterpret_cast<const u32x4*>(mask + off);
+      if (!BNMASK && mask) mv = *reinterpret_cast<const u32x4*>(mask + off);
       const bf16_t* gh = reinterpret_cast<const bf16_t*>(&gv);
       const bf16_t* xh = reinterpret_cast<const bf16_t*>(&xv);
       const bf16_t* mh = reinterpret_cast<const bf16_t*>(&mv);
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        const float g = (!mask || bf2f(mh[i]) > 0.f) ? bf2f(gh[i]) : 0.f;
+        const bool live = BNMASK ? bf2f(f2bf(fmaxf(bf2f(xh[i]) * msc[i] + msh[i], 0.f))) > 0.f
+                                 : (!mask || bf2f(mh[i]) > 0.f);
+        const float g = live ? bf2f(gh[i]) : 0.f;
         s1[i] += g;
         s2[i] += g * (bf2f(xh[i]) - mean[i]) * rstd[i];
       }
@@ -1225,8 +1243,9 @@ MER_API int mer_bn_bwd_reduce(long M, int C, const void* dy, const void* mask, c
   if (C % 8 || C > 512) return (int)hipErrorInvalidValue;
   const long rpb = (M + 511) / 512 > 32 ? (M + 511) / 512 : 32;  // ~512 blocks whatever the layer size
   const long blocks = (M + rpb - 1) / rpb;
-  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, M, C,
-                     (const bf16_t*)dy, (const bf16_t*)mask, (const bf16_t*)x, ms, red, rpb);
+  hipLaunchKernelGGL((bn_bwd_reduce_kernel<false>), dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, M, C,
+                     (const bf16_t*)dy, (const bf16_t*)mask, (const bf16_t*)x, ms, (const float*)nullptr,
+                     (const float*)nullptr, red, rpb);
   MER_LAUNCH_CHECK();
 }
 
@@ -1256,14 +1275,17 @@ MER_API int mer_partials_sum(int C, int parts, const float* in, float* out, void
 // dx = gamma*rstd*(g - s1/M - xhat*s2/M) (bf16), and (block 0) dgamma += s2, dbeta += s1.
 // Affine in (g, x) once the sums are known: dx = k1*g + k2*x + k0 per channel, the constants computed once
 // per block into LDS; same thread/channel ownership and 2-vector streaming as bn_apply_kernel.
-__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(long M, int C, const bf16_t* __restrict__ dy,
+// (BNMASK as in bn_bwd_reduce_kernel; dy and dx may alias: every element is read, then written, by one thread)
+template <bool BNMASK>
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(long M, int C, const bf16_t* dy,
                                                            const bf16_t* __restrict__ mask,
                                                            const bf16_t* __restrict__ x, const float* __restrict__ ms,
                                                            const float* __restrict__ gamma,
+                                                           const float* __restrict__ mbeta,
                                                            const float* __restrict__ red, int batch_stats,
-                                                           bf16_t* __restrict__ dx, float* __restrict__ dgamma,
+                                                           bf16_t* dx, float* __restrict__ dgamma,
                                                            float* __restrict__ dbeta) {
-  __shared__ __attribute__((aligned(16))) float coef[3][512];
+  __shared__ __attribute__((aligned(16))) float coef[5][512];
   const float invM = 1.f / (float)M;
   for (int c = threadIdx.x; c < C; c += 256) {
     if (blockIdx.x == 0) {
@@ -1277,18 +1299,21 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(long M, int C, const 
     coef[0][c] = gr;
     coef[1][c] = -gr * b * rs;
     coef[2][c] = -gr * a + gr * b * rs * mu;
+    if (BNMASK) stem_bn_coef(c, ms, gamma, mbeta, coef[3][c], coef[4][c]);
   }
   __syncthreads();
   const long nvec = M * C / 8;
   const long stride = (long)gridDim.x * blockDim.x;
   const long tid0 = blockIdx.x * (long)blockDim.x + threadIdx.x;
   const int c0 = (int)(tid0 % (C / 8)) * 8;
-  float k1[8], k2[8], k0[8];
+  float k1[8], k2[8], k0[8], msc[8], msh[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     k1[i] = coef[0][c0 + i];
     k2[i] = coef[1][c0 + i];
     k0[i] = coef[2][c0 + i];
+    msc[i] = BNMASK ? coef[3][c0 + i] : 0.f;
+    msh[i] = BNMASK ? coef[4][c0 + i] : 0.f;
   }
   auto one = [&](const u32x4& gv, const u32x4& xv, const u32x4& mv) -> u32x4 {
     const bf16_t* gh = reinterpret_cast<const bf16_t*>(&gv);
@@ -1298,7 +1323,9 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(long M, int C, const 
     bf16_t* oh = reinterpret_cast<bf16_t*>(&ov);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      const float g = (!mask || bf2f(mh[i]) > 0.f) ? bf2f(gh[i]) : 0.f;
+      const bool live = BNMASK ? bf2f(f2bf(fmaxf(bf2f(xh[i]) * msc[i] + msh[i], 0.f))) > 0.f
+                               : (!mask || bf2f(mh[i]) > 0.f);
+      const float g = live ? bf2f(gh[i]) : 0.f;
       oh[i] = f2bf(k1[i] * g + k2[i] * bf2f(xh[i]) + k0[i]);
     }
     return ov;
@@ -1311,15 +1338,15 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(long M, int C, const 
     const u32x4 g1 = *reinterpret_cast<const u32x4*>(dy + e1 * 8);
     const u32x4 x0 = *reinterpret_cast<const u32x4*>(x + e * 8);
     const u32x4 x1 = *reinterpret_cast<const u32x4*>(x + e1 * 8);
-    const u32x4 m0 = mask ? *reinterpret_cast<const u32x4*>(mask + e * 8) : one16;
-    const u32x4 m1 = mask ? *reinterpret_cast<const u32x4*>(mask + e1 * 8) : one16;
+    const u32x4 m0 = (!BNMASK && mask) ? *reinterpret_cast<const u32x4*>(mask + e * 8) : one16;
+    const u32x4 m1 = (!BNMASK && mask) ? *reinterpret_cast<const u32x4*>(mask + e1 * 8) : one16;
     *reinterpret_cast<u32x4*>(dx + e * 8) = one(g0, x0, m0);
     *reinterpret_cast<u32x4*>(dx + e1 * 8) = one(g1, x1, m1);
   }
   if (e < nvec) {
     const u32x4 g0 = *reinterpret_cast<const u32x4*>(dy + e * 8);
     const u32x4 x0 = *reinterpret_cast<const u32x4*>(x + e * 8);
-    const u32x4 m0 = mask ? *reinterpret_cast<const u32x4*>(mask + e * 8) : one16;
+    const u32x4 m0 = (!BNMASK && mask) ? *reinterpret_cast<const u32x4*>(mask + e * 8) : one16;
     *reinterpret_cast<u32x4*>(dx + e * 8) = one(g0, x0, m0);
   }
 }
@@ -1329,9 +1356,9 @@ MER_API int mer_bn_bwd_apply(long M, int C, const void* dy, const void* mask, co
   if (C % 8 || C > 512 || 256 % (C / 8)) return (int)hipErrorInvalidValue;
   const long nvec = M * C / 8;
   const int grid = bn_stream_grid(nvec);
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, M, C, (const bf16_t*)dy,
-                     (const bf16_t*)mask, (const bf16_t*)x, ms, gamma, red, batch_stats, (bf16_t*)dx, dgamma,
-                     dbeta);
+  hipLaunchKernelGGL((bn_bwd_apply_kernel<false>), dim3(grid), dim3(256), 0, (hipStream_t)stream, M, C,
+                     (const bf16_t*)dy, (const bf16_t*)mask, (const bf16_t*)x, ms, gamma, (const float*)nullptr, red,
+                     batch_stats, (bf16_t*)dx, dgamma, dbeta);
   MER_LAUNCH_CHECK();
 }
 
@@ -1432,6 +1459,89 @@ MER_API int mer_maxpool_bwd(int N, int H, int W, int C, const void* dy, const vo
   const int grid = (int)((total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192);
   hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, N, H, W, C, Ho, Wo,
                      (const bf16_t*)dy, (const uint8_t*)argmax, (bf16_t*)dx);
+  MER_LAUNCH_CHECK();
+}
+
+// ---------------------------------------------------------------------------------------
+// Fused ResNet stem tail (video.py:21-23 -> torchvision conv1/bn1/relu/maxpool), channel-last, C = 64:
+//   forward:  p = maxpool3x3s2p1( a ),  a = bf16(relu(x * scale + shift))  -- a is never stored;
+//   backward: g = bf16(maxpool gather of dp) * (a > 0), recomputed from (dp, argmax, x, BN) in both the
+//             BatchNorm reduction pass and the apply pass, so neither a nor da goes through HBM.
+// Same roundings, tap order and tie rule as bn_apply -> maxpool_fwd / maxpool_bwd -> bn_bwd_*.
+// ---------------------------------------------------------------------------------------
+
+__global__ void stem_bnrelu_maxpool_kernel(int N, int H, int W, int C, int Ho, int Wo, const bf16_t* __restrict__ x,
+                                           const float* __restrict__ ms, const float* __restrict__ gamma,
+                                           const float* __restrict__ beta, bf16_t* __restrict__ y,
+                                           uint8_t* __restrict__ arg) {
+  const int cpr = C / 8;
+  const int total = N * Ho * Wo * cpr;
+  const float inv_cpr = 1.f / cpr, inv_Wo = 1.f / Wo, inv_Ho = 1.f / Ho;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
+    const int q = fdiv(e, inv_cpr);
+    const int c0 = (e - q * cpr) * 8;
+    const int q2 = fdiv(q, inv_Wo);
+    const int ow = q - q2 * Wo;
+    const int n = fdiv(q2, inv_Ho);
+    const int oh = q2 - n * Ho;
+    float sc[8], sh[8], best[8];
+    int bi[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      stem_bn_coef(c0 + i, ms, gamma, beta, sc[i], sh[i]);
+      best[i] = -INFINITY;
+      bi[i] = 0;
+    }
+    for (int r = 0; r < 3; ++r)
+      for (int s = 0; s < 3; ++s) {
+        const int ih = oh * 2 - 1 + r, iw = ow * 2 - 1 + s;
+        if (ih < 0 || ih >= H || iw < 0 || iw >= W) continue;
+        const u32x4 v = *reinterpret_cast<const u32x4*>(x + (((long)n * H + ih) * W + iw) * C + c0);
+        const bf16_t* vh = reinterpret_cast<const bf16_t*>(&v);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const float f = bf2f(f2bf(fmaxf(bf2f(vh[i]) * sc[i] + sh[i], 0.f)));
+          if (f > best[i]) { best[i] = f; bi[i] = r * 3 + s; }
+        }
+      }
+    u32x4 o;
+    bf16_t* oh8 = reinterpret_cast<bf16_t*>(&o);
+    uint2 a;
+    uint8_t* a8 = reinterpret_cast<uint8_t*>(&a);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { oh8[i] = f2bf(best[i]); a8[i] = (uint8_t)bi[i]; }
+    *reinterpret_cast<u32x4*>(y + (long)q * C + c0) = o;
+    *reinterpret_cast<uint2*>(arg + (long)q * C + c0) = a;
+  }
+}
+
+MER_API int mer_stem_bnrelu_maxpool_fwd(int N, int H, int W, int C, const void* x, const float* ms, const float* gamma,
+                                        const float* beta, void* y, void* argmax, void* stream) {
+  const int Ho = (H + 2 - 3) / 2 + 1, Wo = (W + 2 - 3) / 2 + 1;
+  if (C % 8 || C > 512 || (long)N * H * W >= (1L << 22)) return (int)hipErrorInvalidValue;
+  const long total = (long)N * Ho * Wo * C / 8;
+  const int grid = (int)((total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192);
+  hipLaunchKernelGGL(stem_bnrelu_maxpool_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, N, H, W, C, Ho, Wo,
+                     (const bf16_t*)x, ms, gamma, beta, (bf16_t*)y, (uint8_t*)argmax);
+  MER_LAUNCH_CHECK();
+}
+
+MER_API int mer_stem_pool_bn_bwd(int N, int H, int W, int C, const void* dy, const void* argmax, const void* x,
+                                 const float* ms, const float* gamma, const float* beta, float* red, int batch_stats,
+                                 void* dx, float* dgamma, float* dbeta, void* stream) {
+  if (C % 8 || C > 512 || 256 % (C / 8) || (long)N * H * W >= (1L << 22)) return (int)hipErrorInvalidValue;
+  const hipStream_t st = (hipStream_t)stream;
+  const long M = (long)N * H * W;
+  // 1) maxpool gather backward into dx (as the pre-BN gradient); 2) BN reduction with the ReLU mask
+  // recomputed from (x, BN); 3) BN apply in place over dx (each element read, then written, by one thread)
+  int rc = mer_maxpool_bwd(N, H, W, C, dy, argmax, dx, stream);
+  if (rc) return rc;
+  const long rpb = (M + 511) / 512 > 32 ? (M + 511) / 512 : 32;
+  hipLaunchKernelGGL((bn_bwd_reduce_kernel<true>), dim3((unsigned)((M + rpb - 1) / rpb)), dim3(256), 0, st, M, C,
+                     (const bf16_t*)dx, (const bf16_t*)nullptr, (const bf16_t*)x, ms, gamma, beta, red, rpb);
+  hipLaunchKernelGGL((bn_bwd_apply_kernel<true>), dim3(bn_stream_grid(M * C / 8)), dim3(256), 0, st, M, C,
+                     (const bf16_t*)dx, (const bf16_t*)nullptr, (const bf16_t*)x, ms, gamma, beta, red, batch_stats,
+                     (bf16_t*)dx, dgamma, dbeta);
   MER_LAUNCH_CHECK();
 }
 

@@ -486,6 +486,21 @@ def maxpool_fwd(x, y, arg):
     LIB("mer_maxpool_fwd", N, H, W, C, x.data_ptr(), y.data_ptr(), arg.data_ptr(), stream_ptr())
 
 
+def stem_bnrelu_maxpool(x, ms, gamma, beta, y, arg):
+    """Fused stem tail: y/arg = maxpool3x3s2p1(relu(bn(x))) without storing the activation."""
+    N, H, W, C = x.shape
+    LIB("mer_stem_bnrelu_maxpool_fwd", N, H, W, C, x.data_ptr(), ms.data_ptr(), gamma.data_ptr(), beta.data_ptr(),
+        y.data_ptr(), arg.data_ptr(), stream_ptr())
+
+
+def stem_pool_bn_bwd(dy, arg, x, ms, gamma, beta, red, dx, dgamma, dbeta, batch_stats=True):
+    """Backward of stem_bnrelu_maxpool to the conv output x (red: zeroed float[C][2] scratch)."""
+    N, H, W, C = x.shape
+    LIB("mer_stem_pool_bn_bwd", N, H, W, C, dy.data_ptr(), arg.data_ptr(), x.data_ptr(), ms.data_ptr(),
+        gamma.data_ptr(), beta.data_ptr(), red.data_ptr(), int(batch_stats), dx.data_ptr(), _ptr(dgamma),
+        _ptr(dbeta), stream_ptr())
+
+
 def maxpool_bwd(dy, arg, dx):
     N, H, W, C = dx.shape
     LIB("mer_maxpool_bwd", N, H, W, C, dy.data_ptr(), arg.data_ptr(), dx.data_ptr(), stream_ptr())

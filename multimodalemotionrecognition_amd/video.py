@@ -335,13 +335,11 @@ def _trunk_forward(trunk: ResNet18Trunk, video: torch.Tensor, training: bool):
     K.pack_input_s2d(video, x0)
     arena = _StatsArena(trunk, dev) if training else None
     c1, ms1 = _conv_bn(trunk, conv1, bn1, x0, 1, 0, training, arena, rs=(4, 4))
-    a1 = torch.empty_like(c1)
-    K.bn_apply(c1, ms1, bn1.weight, bn1.bias, a1, relu=True)
-    Hp, Wp = (a1.shape[1] - 1) // 2 + 1, (a1.shape[2] - 1) // 2 + 1
-    p1 = torch.empty(N, Hp, Wp, 64, device=dev, dtype=bf)
-    arg = torch.empty(N, Hp, Wp, 64, device=dev, dtype=torch.uint8)
-    K.maxpool_fwd(a1, p1, arg)
-    saved = {"stem": (x0, c1, ms1, a1, arg), "blocks": []}
+    Hp, Wp = (c1.shape[1] - 1) // 2 + 1, (c1.shape[2] - 1) // 2 + 1
+    p1 = torch.empty(N, Hp, Wp, c1.shape[-1], device=dev, dtype=bf)
+    arg = torch.empty(N, Hp, Wp, c1.shape[-1], device=dev, dtype=torch.uint8)
+    K.stem_bnrelu_maxpool(c1, ms1, bn1.weight, bn1.bias, p1, arg)  # bn1 + relu + maxpool, activation not stored
+    saved = {"stem": (x0, c1, ms1, arg), "blocks": []}
     x = p1
     for blk in _blocks(trunk):
         x, sv = block_forward(trunk, blk, x, training, arena)
@@ -460,12 +458,12 @@ def _trunk_backward(trunk: ResNet18Trunk, saved, dfeat: torch.Tensor, training: 
         prev = (svs[i - 1], blocks[i - 1]) if i > 0 else None
         dx, pre = block_backward(trunk, blocks[i], svs[i], dx, grads, training, pre=pre, prev=prev, arena=arena)
     # stem: maxpool -> bn1/relu -> conv1 (no data gradient for the frames)
-    x0, c1, ms1, a1, arg = saved["stem"]
-    da1 = torch.empty_like(a1)
-    K.maxpool_bwd(dx, arg, da1)
+    x0, c1, ms1, arg = saved["stem"]
+    bn1 = trunk[1]
     red = arena.take(c1.shape[-1], parts=1)
-    K.bn_bwd_reduce(da1, a1, c1, ms1, red)
-    dc1 = _bn_bwd(da1, a1, c1, ms1, trunk[1], red, grads, training)
+    dc1 = torch.empty_like(c1)  # maxpool + relu + bn1 backward in one reduction pass and one apply pass
+    K.stem_pool_bn_bwd(dx, arg, c1, ms1, bn1.weight, bn1.bias, red, dc1, _grad(bn1.weight, grads),
+                       _grad(bn1.bias, grads), training)
     w = _grad(trunk[0].weight, grads)
     if w is not None:  # wgrad of the 4x4 space-to-depth form, then gathered back to [64][3][7][7]
         Kc, Cin, R, S = trunk[0].weight.shape

@@ -328,3 +328,41 @@ def test_space_to_depth_stem_vs_torch(H):
     K.conv_wgrad(xs, to_nhwc(dy).bfloat16().cuda(), ws, 4, 4, 1, 0)
     dw = ws.view(64, -1).index_select(1, _stem_wgrad_index(7, 7, 3, ws.device)).view(64, 3, 7, 7)
     assert rel_rms(dw, wr.grad) < 1e-2
+
+
+@pytest.mark.parametrize("training", [True, False])
+def test_fused_stem_tail_matches_unfused(training):
+    """stem_bnrelu_maxpool == bn_apply(relu) -> maxpool_fwd bit for bit; stem_pool_bn_bwd == maxpool_bwd ->
+    bn_bwd_reduce -> bn_bwd_apply (up to the fp32 atomic order of the channel sums)."""
+    from multimodalemotionrecognition_amd import kernels as K
+
+    torch.manual_seed(5)
+    N, H, C = 4, 56, 64
+    x = torch.randn(N, H, H, C, device="cuda").bfloat16()
+    ms = torch.stack([torch.randn(C) * 0.1, torch.rand(C) + 0.5], 1).cuda().contiguous()
+    g, b = (torch.rand(C) + 0.5).cuda(), (torch.randn(C) * 0.2).cuda()
+    Hp = (H - 1) // 2 + 1
+    a = torch.empty_like(x)
+    K.bn_apply(x, ms, g, b, a, relu=True)
+    p_ref = torch.empty(N, Hp, Hp, C, device="cuda", dtype=torch.bfloat16)
+    arg_ref = torch.empty(N, Hp, Hp, C, device="cuda", dtype=torch.uint8)
+    K.maxpool_fwd(a, p_ref, arg_ref)
+    p = torch.empty_like(p_ref)
+    arg = torch.empty_like(arg_ref)
+    K.stem_bnrelu_maxpool(x, ms, g, b, p, arg)
+    assert torch.equal(p, p_ref) and torch.equal(arg, arg_ref)
+    dp = torch.randn(N, Hp, Hp, C, device="cuda").bfloat16()
+    da = torch.empty_like(x)
+    K.maxpool_bwd(dp, arg, da)
+    red_ref = torch.zeros(C, 2, device="cuda")
+    K.bn_bwd_reduce(da, a, x, ms, red_ref)
+    dx_ref = torch.empty_like(x)
+    dg_ref, db_ref = torch.zeros(C, device="cuda"), torch.zeros(C, device="cuda")
+    K.bn_bwd_apply(da, a, x, ms, g, red_ref, dx_ref, dg_ref, db_ref, training)
+    red = torch.zeros(C, 2, device="cuda")
+    dx = torch.empty_like(x)
+    dg, db = torch.zeros(C, device="cuda"), torch.zeros(C, device="cuda")
+    K.stem_pool_bn_bwd(dp, arg, x, ms, g, b, red, dx, dg, db, training)
+    assert torch.allclose(red, red_ref, rtol=1e-4, atol=1e-2)
+    assert torch.allclose(dg, dg_ref, rtol=1e-4, atol=1e-2) and torch.allclose(db, db_ref, rtol=1e-4, atol=1e-2)
+    assert rel_rms(dx.float(), dx_ref.float()) < 1e-2
