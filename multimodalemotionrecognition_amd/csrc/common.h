@@ -98,6 +98,27 @@ __device__ __forceinline__ void xcd_tile(int pid, int nx, int ntiles, int& tx, i
 // 16-byte global -> LDS DMA (global_load_lds_dwordx4): lane i's 16 bytes land at lds + 16*i (the LDS
 // pointer must be wave-uniform).  Wrapped in a non-template function: used directly inside a kernel
 // TEMPLATE, hipcc (ROCm 7.2) silently drops the host launch stub (undefined symbol at load time).
+// s_waitcnt with only vmcnt constrained (gfx9 encoding: vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8] | vmcnt_hi[15:14])
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+}
+// wait until at most n (runtime, 0..3) tiles of G glds each are still in flight
+template <int G>
+__device__ __forceinline__ void wait_tiles_in_flight(int n) {
+  if (n <= 0) wait_vmcnt<0>();
+  else if (n == 1) wait_vmcnt<G>();
+  else if (n == 2) wait_vmcnt<2 * G>();
+  else wait_vmcnt<3 * G>();
+}
+// lgkmcnt(0) only (LDS reads retired), then a raw s_barrier: glds DMAs stay in flight across it
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_s_waitcnt((15) | (7 << 4) | (0 << 8) | (3 << 14));
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+}
+
 __device__ __forceinline__ void glds16(const void* g, void* lds) { __builtin_amdgcn_global_load_lds(g, lds, 16, 0, 0); }
 
 // xcd_tile plus grouped rasterisation inside each XCD's chunk: consecutive tiles walk a G-row band

@@ -450,7 +450,10 @@ __device__ __forceinline__ ParClass par_class(const ConvGeom& g, int cls) {
   return c;
 }
 
-template <bool DGRAD, bool PAR, int BM_, int BN_, int WM = 2, int WN = 2>
+// STAGES-deep LDS ring (cdna_hip_programming.md "Pipelining across barriers"): tiles kt+1 .. kt+STAGES-2 stay
+// in flight across the barrier that publishes tile kt (counted vmcnt, raw s_barrier); the barrier also retires
+// every wave's reads of tile kt-1, whose buffer the DMA of tile kt+STAGES-1 then reuses.
+template <bool DGRAD, bool PAR, int BM_, int BN_, int WM = 2, int WN = 2, int STAGES = 2>
 __global__ __launch_bounds__(64 * WM * WN, 2) void conv_pipe_kernel(ConvGeom g) {
   constexpr int WAVES = WM * WN;
   constexpr int IA = BM_ / 8 / WAVES, IB = BN_ / 8 / WAVES;  // glds per wave per K-tile (8 rows each)
@@ -547,15 +550,17 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_pipe_kernel(ConvGeom g) 
   const int fr = lane & 15, fq = lane >> 4;
   const int nk = (Kr + CBK - 1) / CBK;
   float part[FN][2];
-  if (nk > 0) {
-    stage(0, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  }
+  constexpr int G = IA + IB;
+  static_assert(STAGES >= 2 && STAGES <= 4, "ring depth");
+#pragma unroll
+  for (int p = 0; p < STAGES - 1; ++p)
+    if (p < nk) stage(p, p * CBK);
   for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) stage(cur ^ 1, (kt + 1) * CBK);
-    const bf16_t* la = smem + cur * BUF;
+    const int ahead = (nk - 1 - kt) < (STAGES - 2) ? (nk - 1 - kt) : (STAGES - 2);
+    wait_tiles_in_flight<G>(ahead);
+    lds_barrier();
+    if (kt + STAGES - 1 < nk) stage((kt + STAGES - 1) % STAGES, (kt + STAGES - 1) * CBK);
+    const bf16_t* la = smem + (kt % STAGES) * BUF;
     const bf16_t* lb = la + BM_ * 64;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -577,9 +582,8 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_pipe_kernel(ConvGeom g) 
         for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
       __builtin_amdgcn_s_setprio(0);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
   }
+  __syncthreads();  // every wave's last fragment reads are done before the epilogue reuses the ring
 
   // output row -> element offset of the pixel in Y
   auto out_row = [&](int row) -> long {
@@ -731,16 +735,16 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_pipe_kernel(ConvGeom g) 
   }
 }
 
-template <bool DGRAD, bool PAR, int BM_, int BN_, int WM = 2, int WN = 2>
+template <bool DGRAD, bool PAR, int BM_, int BN_, int WM = 2, int WN = 2, int STAGES = 2>
 int launch_conv_pipe_t(ConvGeom& g, hipStream_t st) {
   // PAR: grid.x covers the largest parity class (ph = pw = 0), grid.y = the 4 classes
   const int Mg = PAR ? g.N * ((g.OH + 1) / 2) * ((g.OW + 1) / 2) : g.N * g.OH * g.OW;
   const long tiles = (long)((Mg + BM_ - 1) / BM_) * ((g.Ncols + BN_ - 1) / BN_);
-  const size_t lds = 2 * (BM_ + BN_) * 64 * sizeof(bf16_t);
-  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_pipe_kernel<DGRAD, PAR, BM_, BN_, WM, WN>),
+  const size_t lds = STAGES * (BM_ + BN_) * 64 * sizeof(bf16_t);
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_pipe_kernel<DGRAD, PAR, BM_, BN_, WM, WN, STAGES>),
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return (int)hipErrorInvalidConfiguration;
-  hipLaunchKernelGGL((conv_pipe_kernel<DGRAD, PAR, BM_, BN_, WM, WN>), dim3((unsigned)tiles, PAR ? 4 : 1),
+  hipLaunchKernelGGL((conv_pipe_kernel<DGRAD, PAR, BM_, BN_, WM, WN, STAGES>), dim3((unsigned)tiles, PAR ? 4 : 1),
                      dim3(64 * WM * WN), lds, st, g);
   return (int)hipGetLastError();
 }
@@ -758,11 +762,23 @@ int launch_conv_pipe(ConvGeom& g, hipStream_t st, int variant) {
     if (bn == 64) return launch_conv_pipe_t<DGRAD, PAR, 256, 64, 4, 2>(g, st);
     return launch_conv_pipe_t<DGRAD, PAR, 256, 128, 4, 4>(g, st);
   }
-  if (variant >= 2) {
+  if (variant == 4) {  // variant-2 tiles on a 3-deep ring (two K-tiles in flight across each barrier)
     if (bn == 64)
-      return small_m ? launch_conv_pipe_t<DGRAD, PAR, 64, 64, 2, 2>(g, st)
+      return small_m ? launch_conv_pipe_t<DGRAD, PAR, 64, 64, 2, 2, 3>(g, st)
+                     : launch_conv_pipe_t<DGRAD, PAR, 128, 64, 4, 2, 3>(g, st);
+    return small_m ? launch_conv_pipe_t<DGRAD, PAR, 64, 128, 2, 4, 3>(g, st)
+                   : launch_conv_pipe_t<DGRAD, PAR, 128, 128, 2, 4, 3>(g, st);
+  }
+  if (variant >= 2) {
+    // deep layers (small M, one 64-row tile per CU or fewer): a 3-deep ring keeps two K-tiles in flight
+    // (tools/bench_conv.py: layer4 3x3 fwd 54.6 -> 44.8 us, dgrad 55.1 -> 47.1 us; the parity-class dgrad
+    // and the large-M layers run best on the 2-deep ring at 2 blocks per CU)
+    if (bn == 64)
+      return small_m ? (PAR ? launch_conv_pipe_t<DGRAD, PAR, 64, 64, 2, 2>(g, st)
+                            : launch_conv_pipe_t<DGRAD, PAR, 64, 64, 2, 2, 3>(g, st))
                      : launch_conv_pipe_t<DGRAD, PAR, 128, 64, 4, 2>(g, st);
-    return small_m ? launch_conv_pipe_t<DGRAD, PAR, 64, 128, 2, 4>(g, st)
+    return small_m ? (PAR ? launch_conv_pipe_t<DGRAD, PAR, 64, 128, 2, 4>(g, st)
+                          : launch_conv_pipe_t<DGRAD, PAR, 64, 128, 2, 4, 3>(g, st))
                    : launch_conv_pipe_t<DGRAD, PAR, 128, 128, 2, 4>(g, st);
   }
   if (bn == 64)
@@ -802,7 +818,7 @@ MER_API int mer_conv_fwd(int N, int H, int W, int C, int K, int R, int S, int st
 
 MER_API int mer_conv_fwd_ex(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, const void* x,
                             const void* w_packed, void* y, float* stats, int variant, void* stream) {
-  if (C % 8 || variant < -1 || variant > 3) return (int)hipErrorInvalidValue;
+  if (C % 8 || variant < -1 || variant > 4) return (int)hipErrorInvalidValue;
   if (variant == -1) variant = 2;
   ConvGeom g{};
   g.N = N; g.IH = H; g.IW = W; g.IC = C;
@@ -831,7 +847,7 @@ MER_API int mer_conv_dgrad_bnr(int N, int H, int W, int C, int K, int R, int S, 
                                const void* wt_packed, void* dx, const void* residual, const void* residual_mask,
                                const void* bn_mask, const void* bn_x, const float* bn_ms, float* bn_red,
                                const void* bn_x2, const float* bn_ms2, float* bn_red2, int variant, void* stream) {
-  if (K % 8 || C % 8 || variant < -1 || variant > 3) return (int)hipErrorInvalidValue;
+  if (K % 8 || C % 8 || variant < -1 || variant > 4) return (int)hipErrorInvalidValue;
   if (variant == -1) variant = 2;
   if (bn_red && (!bn_mask || !bn_x || !bn_ms || (bn_x2 && (!bn_ms2 || !bn_red2)))) return (int)hipErrorInvalidValue;
   if (bn_red && (variant == 0 || stride > 2)) return (int)hipErrorInvalidValue;  // fused only in the pipelined kernel

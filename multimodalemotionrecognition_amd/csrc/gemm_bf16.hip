@@ -37,9 +37,22 @@ struct GemmArgs {
   const bf16_t* R;
   long ldr;
   int act;
+  int vec_epi;  // pipelined kernels: 16-byte epilogue through LDS (N, ldc, ldr, c_zoff multiples of 8, aligned)
 };
 
 typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;
+
+template <typename T> __device__ __forceinline__ void store8(T* p, const float* v);
+template <> __device__ __forceinline__ void store8<float>(float* p, const float* v) {
+  *reinterpret_cast<f32x4*>(p) = f32x4{v[0], v[1], v[2], v[3]};
+  *reinterpret_cast<f32x4*>(p + 4) = f32x4{v[4], v[5], v[6], v[7]};
+}
+template <> __device__ __forceinline__ void store8<bf16_t>(bf16_t* p, const float* v) {
+  uint32_t w[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) w[e] = (uint32_t)f2bf(v[2 * e]) | ((uint32_t)f2bf(v[2 * e + 1]) << 16);
+  *reinterpret_cast<u32x4*>(p) = u32x4{w[0], w[1], w[2], w[3]};
+}
 
 template <int AMODE>
 __device__ __forceinline__ u32x4 load_a_chunk(const GemmArgs& g, int m, int k, int z) {
@@ -170,20 +183,6 @@ struct PipeCfg {
 
 __device__ __forceinline__ int swz_chunk(int row, int c) { return c ^ ((row >> 1) & 7); }
 
-// s_waitcnt with only vmcnt constrained (gfx9 encoding: vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8] | vmcnt_hi[15:14])
-template <int N>
-__device__ __forceinline__ void wait_vmcnt() {
-  static_assert(N >= 0 && N < 64, "vmcnt range");
-  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
-}
-// wait until at most n (runtime, 0..3) tiles of G glds each are still in flight
-template <int G>
-__device__ __forceinline__ void wait_tiles_in_flight(int n) {
-  if (n <= 0) wait_vmcnt<0>();
-  else if (n == 1) wait_vmcnt<G>();
-  else if (n == 2) wait_vmcnt<2 * G>();
-  else wait_vmcnt<3 * G>();
-}
 
 __device__ __attribute__((aligned(16))) uint32_t mer_gemm_zero16[4] = {0u, 0u, 0u, 0u};
 
@@ -299,6 +298,69 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_pipe_kernel(GemmArgs g) {
   }
 
   TOUT* C = reinterpret_cast<TOUT*>(g.C) + (long)z * g.c_zoff;
+  if (g.vec_epi) {
+    // Epilogue through LDS (the ring is idle once every wave is past its last fragment read): each wave
+    // stages act(acc + bias) of 16-row groups of its TM x TN sub-tile as fp32 [row][TN + 4] in its own slice
+    // of the ring (conflict-free: the 4 row-quads of a fragment land 16 banks apart), then every lane moves
+    // 8 consecutive columns of one row: a 16-byte residual load and 16-byte (bf16) / 2 x 16-byte (fp32)
+    // stores instead of one 2- or 4-byte access per accumulator element.  Same arithmetic and rounding as
+    // the direct path below.
+    constexpr int LDT = CF::TN + 4;
+    constexpr int WAVE_FLOATS = CF::STAGES * CF::BUF / 2 / CF::WAVES;  // bf16 ring elements / 2 = floats
+    constexpr int GI0 = WAVE_FLOATS / (16 * LDT);
+    constexpr int GI = GI0 < CF::FM ? GI0 : CF::FM;
+    static_assert(GI >= 1, "epilogue staging slice too small");
+    constexpr int LPR = CF::TN / 8, RPP = 64 / LPR;  // lanes per row, rows per pass
+    __syncthreads();
+    float* wl = reinterpret_cast<float*>(smem) + w * WAVE_FLOATS;
+    float bv[CF::FN];
+#pragma unroll
+    for (int j = 0; j < CF::FN; ++j) {
+      const int col = n0 + wc * CF::TN + j * 16 + fr;
+      bv[j] = (g.bias && col < g.N) ? g.bias[(long)z * g.c_zoff + col] : 0.f;
+    }
+    const int lr = lane / LPR, lc = (lane % LPR) * 8;
+    const int colv = n0 + wc * CF::TN + lc;
+#pragma unroll
+    for (int i0 = 0; i0 < CF::FM; i0 += GI) {
+#pragma unroll
+      for (int ii = 0; ii < GI; ++ii) {
+        if (i0 + ii >= CF::FM) break;
+#pragma unroll
+        for (int j = 0; j < CF::FN; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            wl[(ii * 16 + fq * 4 + r) * LDT + j * 16 + fr] = apply_act(acc[i0 + ii][j][r] + bv[j], g.act);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const int nrows = (CF::FM - i0 < GI ? CF::FM - i0 : GI) * 16;
+#pragma unroll
+      for (int rr = 0; rr < GI * 16; rr += RPP) {
+        const int rl = rr + lr;
+        const int row = m0 + wr * CF::TM + i0 * 16 + rl;
+        if (rl < nrows && row < g.M && colv < g.N) {
+          const f32x4 lo = *reinterpret_cast<const f32x4*>(&wl[rl * LDT + lc]);
+          const f32x4 hi = *reinterpret_cast<const f32x4*>(&wl[rl * LDT + lc + 4]);
+          float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          if (g.R) {
+            const u32x4 rv = *reinterpret_cast<const u32x4*>(g.R + (long)row * g.ldr + (long)z * g.c_zoff + colv);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              v[2 * e] += __uint_as_float(rv[e] << 16);
+              v[2 * e + 1] += __uint_as_float(rv[e] & 0xffff0000u);
+            }
+          }
+          store8<TOUT>(C + (long)row * g.ldc + colv, v);
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < CF::FN; ++j) {
     const int col = n0 + wc * CF::TN + j * 16 + fr;
@@ -552,6 +614,15 @@ int launch(const GemmArgs& g, int out_dtype, int groups, hipStream_t st) {
 
 }  // namespace
 
+namespace {
+// 16-byte epilogue accesses: 8-column runs never straddle N, and every row start is 16-byte aligned
+bool vec_epilogue_ok(int N, const void* C, long ldc, const void* R, long ldr, long c_zoff) {
+  if (N % 8 || ldc % 8 || c_zoff % 8 || (((uintptr_t)C) & 15)) return false;
+  if (R && (ldr % 8 || (((uintptr_t)R) & 15))) return false;
+  return true;
+}
+}  // namespace
+
 MER_API int mer_gemm_bf16(int M, int N, int K, const void* A, long a_gstride, long a_rstride, int a_rpg, const void* W,
                           long ldw, void* C, int c_dtype, long ldc, const float* bias, const void* R, long ldr, int act,
                           void* stream) {
@@ -573,6 +644,7 @@ MER_API int mer_gemm_bf16_ex(int M, int N, int K, const void* A, long a_gstride,
   g.B = (const bf16_t*)W; g.ldb = ldw; g.b_zstride = 0;
   g.C = C; g.ldc = ldc; g.c_zoff = 0;
   g.bias = bias; g.R = (const bf16_t*)R; g.ldr = ldr; g.act = act;
+  g.vec_epi = vec_epilogue_ok(N, C, ldc, R, ldr, 0);
   const hipStream_t st = (hipStream_t)stream;
   if (K % 64 != 0) variant = 0;
   if (variant == -1) variant = pick_variant(M, N, K);
@@ -606,6 +678,7 @@ MER_API int mer_posconv_gemm_bf16(int B, int L, int C_total, int groups, int tap
   g.B = (const bf16_t*)Wp; g.ldb = (long)taps * cg; g.b_zstride = (long)cg * taps * cg;
   g.C = out; g.ldc = ldo; g.c_zoff = cg;
   g.bias = bias; g.R = (const bf16_t*)R; g.ldr = ldr; g.act = act;
+  g.vec_epi = vec_epilogue_ok(cg, out, ldo, R, ldr, g.c_zoff);
   if (g.K % 64 == 0 && (((uintptr_t)X | (uintptr_t)Wp) & 15) == 0)
     return launch_pipe<CfgP, 1>(g, out_dtype, (hipStream_t)stream, groups);
   return launch<1>(g, out_dtype, groups, (hipStream_t)stream);

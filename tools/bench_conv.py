@@ -9,10 +9,14 @@ from multimodalemotionrecognition_amd import kernels as K  # noqa: E402
 
 NF = 256
 # (name, H_in, C, K, R, stride, pad)
-LAYERS = [("conv1 7x7", 112, 8, 64, 7, 2, 3), ("layer1 3x3", 56, 64, 64, 3, 1, 1), ("layer2.0 3x3 s2", 56, 64, 128, 3, 2, 1),
-          ("layer2 3x3", 28, 128, 128, 3, 1, 1), ("layer3.0 3x3 s2", 28, 128, 256, 3, 2, 1),
-          ("layer3 3x3", 14, 256, 256, 3, 1, 1), ("layer4.0 3x3 s2", 14, 256, 512, 3, 2, 1),
-          ("layer4 3x3", 7, 512, 512, 3, 1, 1), ("ds2 1x1 s2", 56, 64, 128, 1, 2, 0)]
+# 112x112 frames: stem (space-to-depth 4x4 form) -> 56x56, maxpool -> layer1 28x28, layer2 14, layer3 7, layer4 4
+LAYERS = [("stem s2d 4x4", 59, 16, 64, 4, 1, 0), ("layer1 3x3", 28, 64, 64, 3, 1, 1),
+          ("layer2.0 3x3 s2", 28, 64, 128, 3, 2, 1), ("layer2 3x3", 14, 128, 128, 3, 1, 1),
+          ("layer3.0 3x3 s2", 14, 128, 256, 3, 2, 1), ("layer3 3x3", 7, 256, 256, 3, 1, 1),
+          ("layer4.0 3x3 s2", 7, 256, 512, 3, 2, 1), ("layer4 3x3", 4, 512, 512, 3, 1, 1),
+          ("ds2 1x1 s2", 28, 64, 128, 1, 2, 0)]
+VARIANTS = [int(v) for v in next((a.split("=")[1] for a in sys.argv if a.startswith("--variants=")), "2,4").split(",")]
+WGRAD = "--no-wgrad" not in sys.argv
 
 
 def timeit(fn, reps=20):
@@ -45,12 +49,17 @@ def main():
         flop = 2.0 * NF * Ho * Ho * Kc * R * R * C
         dw = torch.zeros(Kc, C, R, R, device="cuda")
         line = f"{name:16s}"
-        for v in (1, 2):
+        for v in ((1, 2) if WGRAD else ()):
             tw = timeit(lambda: K.conv_wgrad(x, dy, dw, R, R, st, pad, variant=v))
             line += f" | wgrad v{v} {tw*1e3:7.1f}us {flop/tw/1e9:6.1f}TF"
-        for v in (2, 3):
+        ref_y = ref_dx = None
+        for v in VARIANTS:
             tf = timeit(lambda: K.conv_fwd(x, wp, y, stats, R, R, st, pad, variant=v))
-            tb = timeit(lambda: K.conv_dgrad(dy, wt, dx, R, R, st, pad, variant=v))
+            tb = timeit(lambda: K.conv_dgrad(dy, wt, dx, R, R, st, pad, variant=v)) if H != 59 else float("nan")
+            if ref_y is None:
+                ref_y, ref_dx = y.clone(), dx.clone()
+            elif not (torch.equal(ref_y, y) and (H == 59 or torch.equal(ref_dx, dx))):
+                line += " MISMATCH"
             line += f" | v{v} fwd {tf*1e3:7.1f}us {flop/tf/1e9:6.1f}TF dgrad {tb*1e3:7.1f}us {flop/tb/1e9:6.1f}TF"
         print(line, flush=True)
 
