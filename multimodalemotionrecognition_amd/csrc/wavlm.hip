@@ -26,35 +26,43 @@ __device__ __forceinline__ void conv0_tile_load(const float* __restrict__ x, int
 }
 }  // namespace
 
+typedef __attribute__((ext_vector_type(2))) float f32x2;
+
+// thread t owns the adjacent channels (2t, 2t+1): the two convolutions run as packed fp32 FMAs on one
+// broadcast sample, and the pair is stored as one 32-bit word
 __global__ __launch_bounds__(256) void wavlm_conv0_stats_kernel(int S, int Lout, const float* __restrict__ wav,
                                                                 const float* __restrict__ w,
                                                                 float* __restrict__ part) {
   __shared__ float xs[C0_TS * C0_ST + C0_KW];
   const int b = blockIdx.y, t0 = blockIdx.x * C0_TS;
   conv0_tile_load(wav + (long)b * S, S, t0, xs);
-  float wr[2][C0_KW];
-  const int c0 = threadIdx.x, c1 = threadIdx.x + 256;
+  const int c = 2 * threadIdx.x;
+  f32x2 wr[C0_KW];
 #pragma unroll
-  for (int k = 0; k < C0_KW; ++k) { wr[0][k] = w[c0 * C0_KW + k]; wr[1][k] = w[c1 * C0_KW + k]; }
+  for (int k = 0; k < C0_KW; ++k) wr[k] = f32x2{w[c * C0_KW + k], w[(c + 1) * C0_KW + k]};
   __syncthreads();
-  float s0 = 0.f, q0 = 0.f, s1 = 0.f, q1 = 0.f;
-  const int tn = min(C0_TS, Lout - t0);
-  for (int tt = 0; tt < tn; ++tt) {
-    float a0 = 0.f, a1 = 0.f;
+  // 4 time steps per iteration on 4 independent accumulator pairs (the sums are otherwise one serial chain);
+  // the partial sums are combined in a fixed order, so the statistics stay deterministic
+  f32x2 s[4], q[4];
 #pragma unroll
-    for (int k = 0; k < C0_KW; ++k) {
-      const float xv = xs[tt * C0_ST + k];
-      a0 += wr[0][k] * xv;
-      a1 += wr[1][k] * xv;
+  for (int u = 0; u < 4; ++u) s[u] = q[u] = f32x2{0.f, 0.f};
+  const int tn = min(C0_TS, Lout - t0);
+  for (int tt = 0; tt < tn; tt += 4) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (tt + u < tn) {
+        f32x2 a = {0.f, 0.f};
+#pragma unroll
+        for (int k = 0; k < C0_KW; ++k) a += wr[k] * xs[(tt + u) * C0_ST + k];
+        const f32x2 r = {bf2f(f2bf(a[0])), bf2f(f2bf(a[1]))};
+        s[u] += r;
+        q[u] += r * r;
+      }
     }
-    const float r0 = bf2f(f2bf(a0)), r1 = bf2f(f2bf(a1));
-    s0 += r0; q0 += r0 * r0; s1 += r1; q1 += r1 * r1;
   }
+  const f32x2 st = (s[0] + s[1]) + (s[2] + s[3]), qt = (q[0] + q[1]) + (q[2] + q[3]);
   float* pr = part + ((long)b * gridDim.x + blockIdx.x) * 1024;
-  pr[c0 * 2] = s0;
-  pr[c0 * 2 + 1] = q0;
-  pr[c1 * 2] = s1;
-  pr[c1 * 2 + 1] = q1;
+  *reinterpret_cast<f32x4*>(pr + c * 2) = f32x4{st[0], qt[0], st[1], qt[1]};
 }
 
 // coef[b][c] = (scale, shift) of GroupNorm from the tile partials, summed in tile order
@@ -84,25 +92,22 @@ __global__ __launch_bounds__(256) void wavlm_conv0_gn_gelu_kernel(int S, int Lou
   __shared__ float xs[C0_TS * C0_ST + C0_KW];
   const int b = blockIdx.y, t0 = blockIdx.x * C0_TS;
   conv0_tile_load(wav + (long)b * S, S, t0, xs);
-  float wr[2][C0_KW];
-  const int c0 = threadIdx.x, c1 = threadIdx.x + 256;
+  const int c = 2 * threadIdx.x;
+  f32x2 wr[C0_KW];
 #pragma unroll
-  for (int k = 0; k < C0_KW; ++k) { wr[0][k] = w[c0 * C0_KW + k]; wr[1][k] = w[c1 * C0_KW + k]; }
-  const float* cf = coef + (long)b * 1024;
-  const float sc0 = cf[c0 * 2], sh0 = cf[c0 * 2 + 1], sc1 = cf[c1 * 2], sh1 = cf[c1 * 2 + 1];
+  for (int k = 0; k < C0_KW; ++k) wr[k] = f32x2{w[c * C0_KW + k], w[(c + 1) * C0_KW + k]};
+  const f32x4 cf = *reinterpret_cast<const f32x4*>(coef + (long)b * 1024 + c * 2);
+  const f32x2 sc = {cf[0], cf[2]}, sh = {cf[1], cf[3]};
   __syncthreads();
   const int tn = min(C0_TS, Lout - t0);
+  uint32_t* o = reinterpret_cast<uint32_t*>(out + ((long)b * Lout + t0) * 512 + c);
+#pragma unroll 4
   for (int tt = 0; tt < tn; ++tt) {
-    float a0 = 0.f, a1 = 0.f;
+    f32x2 a = {0.f, 0.f};
 #pragma unroll
-    for (int k = 0; k < C0_KW; ++k) {
-      const float xv = xs[tt * C0_ST + k];
-      a0 += wr[0][k] * xv;
-      a1 += wr[1][k] * xv;
-    }
-    bf16_t* o = out + ((long)b * Lout + t0 + tt) * 512;
-    o[c0] = f2bf(gelu_erf(bf2f(f2bf(a0)) * sc0 + sh0));
-    o[c1] = f2bf(gelu_erf(bf2f(f2bf(a1)) * sc1 + sh1));
+    for (int k = 0; k < C0_KW; ++k) a += wr[k] * xs[tt * C0_ST + k];
+    const f32x2 z = f32x2{bf2f(f2bf(a[0])), bf2f(f2bf(a[1]))} * sc + sh;
+    o[(long)tt * 256] = (uint32_t)f2bf(gelu_erf(z[0])) | ((uint32_t)f2bf(gelu_erf(z[1])) << 16);
   }
 }
 
