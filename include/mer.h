@@ -22,9 +22,13 @@
 #ifndef MER_H_
 #define MER_H_
 
-/* BatchNorm batch statistics are accumulated by the conv epilogue into MER_BN_STAT_PARTS striped partial
- * rows: a `stats` buffer is float[MER_BN_STAT_PARTS][C][2] (sum, sum of squares), zeroed by the caller. */
+/* BatchNorm batch statistics of a conv forward (mer_conv_fwd `stats`): float[MER_BN_STAT_ROWS(M)][C][2]
+ * (sum, sum of squares), zeroed by the caller, M = N*Ho*Wo output pixels.  Each output row tile of the
+ * conv stores its own row (a single writer per element: deterministic), unused rows stay zero, and the last
+ * 64 rows are mer_bn_finalize's scratch.  Backward reductions (mer_conv_dgrad_bnr, mer_bn_bwd_reduce) use
+ * MER_BN_STAT_PARTS striped partial rows, float[MER_BN_STAT_PARTS][C][2], accumulated with fp32 atomics. */
 #define MER_BN_STAT_PARTS 64
+#define MER_BN_STAT_ROWS(M) (((M) + 63) / 64 + 64)
 
 #ifdef __cplusplus
 extern "C" {
@@ -195,7 +199,9 @@ int mer_layernorm(int rows, int d, const void* x, int x_dtype, long ldx, const f
 
 /* WavLM self-attention with gated relative position bias (TF:147-271), one workgroup per (b,h):
  * qkv bf16 [B*L, 3*H*64] (q|k|v), x bf16 layer input (gate source), gate_w [8][64], gate_b [8],
- * gate_const [H], rel_emb [320][H], bucket int32 [2L-1] (bucket of relative position j-i), out bf16. L <= 256. */
+ * gate_const [H], rel_emb [320][H], bucket int32 [2L-1] (bucket of relative position j-i), out bf16. L <= 256.
+ * bucket == NULL: rel_emb is instead the per-head bias table [H][2L-1] = rel_emb[bucket].T (precomputed once
+ * per forward: the position bias is shared by all 12 layers, TF:380-385). */
 int mer_wavlm_attention(int B, int L, int H, const void* qkv, long ldqkv, const void* x, long ldx, const float* gate_w,
                         const float* gate_b, const float* gate_const, const float* rel_emb, const int* bucket,
                         void* out, long ldo, float scale, void* stream);
@@ -215,8 +221,8 @@ int mer_cast_bf16(long n, const float* x, void* y, void* stream);
  * with channels padded to a multiple of 8. */
 
 /* y[n,oh,ow,k] = sum_{r,s,c} x[n,oh*st-pad+r,ow*st-pad+s,c] w[k][r][s][c]  (bf16 out); if stats != NULL,
- * stats[p][k] += (sum, sum of squares) of the stored outputs (BatchNorm batch statistics, striped over
- * p < MER_BN_STAT_PARTS partial rows, pre-zeroed). */
+ * stats (zeroed float[MER_BN_STAT_ROWS(M)][K][2]) receives, per output row tile, the (sum, sum of squares) of the
+ * stored outputs (BatchNorm batch statistics; deterministic, see MER_BN_STAT_ROWS). */
 int mer_conv_fwd(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, const void* x,
                  const void* w_packed, void* y, float* stats, void* stream);
 
@@ -272,7 +278,8 @@ int mer_pack_conv_weight(int K, int C, int R, int S, int Cp, int transpose, cons
  * elements the prefix sums of K*R*S*Cp; total = the sum. */
 int mer_pack_conv_weights(int n, const long long* desc, long total, void* stream);
 
-/* BatchNorm2d finalize: ms[c] = (mean, rstd) from the striped partial rows of stats over M values and, when non-NULL, updates
+/* BatchNorm2d finalize: ms[c] = (mean, rstd) from the MER_BN_STAT_ROWS(M) stats rows of a conv forward (summed in a
+ * fixed order, through the buffer's 64 scratch rows) over M values and, when non-NULL, updates
  * running_mean / running_var (unbiased) with `momentum` and increments num_batches_tracked (train mode).
  * stats == NULL is eval mode: ms = (running_mean, 1/sqrt(running_var + eps)), nothing updated. */
 int mer_bn_finalize(int C, long M, const float* stats, float eps, float momentum, float* ms, float* rmean,

@@ -187,7 +187,7 @@ __global__ __launch_bounds__(256, 2) void conv_kernel(ConvGeom g) {
       csq += __shfl_xor(csq, 16, 64);
       csq += __shfl_xor(csq, 32, 64);
       if ((lane >> 4) == 0 && col < g.Ncols) {
-        float* slab = g.stats + (long)(ty % MER_BN_STAT_PARTS) * g.Ncols * 2;
+        float* slab = g.stats + (long)ty * g.Ncols * 2;  // this row tile's own stats row (2 waves add)
         atomicAdd(slab + 2 * col, csum);
         atomicAdd(slab + 2 * col + 1, csq);
       }
@@ -704,8 +704,9 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_pipe_kernel(ConvGeom g) 
       part[j][0] = csum;
       part[j][1] = csq;
     }
-    // the WM waves sharing a column meet in LDS (the staging buffers are idle now); one striped
-    // atomic per (block, column): slab row ty % MER_BN_STAT_PARTS keeps same-address atomics rare
+    // the WM waves sharing a column meet in LDS (the staging buffers are idle now), in wave order; the block
+    // then STORES its per-column (sum, sumsq) into stats row ty -- every (row tile, column) has exactly one
+    // writer, so the statistics (and with them every BatchNorm output) are bitwise deterministic
     float* red = reinterpret_cast<float*>(smem);
     __syncthreads();
     if (wr > 0 && fq == 0)
@@ -716,7 +717,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_pipe_kernel(ConvGeom g) 
       }
     __syncthreads();
     if (wr == 0 && fq == 0) {
-      float* slab = g.stats + (long)(ty % MER_BN_STAT_PARTS) * g.Ncols * 2;
+      float* slab = g.stats + (long)ty * g.Ncols * 2;
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
         const int col = n0 + wc * TN + j * 16 + fr;
@@ -727,8 +728,8 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_pipe_kernel(ConvGeom g) 
           t1 += red[((q * WN + wc) * FN * 16 + j * 16 + fr) * 2 + 1];
         }
         if (col < g.Ncols) {
-          atomicAdd(slab + 2 * col, t0);
-          atomicAdd(slab + 2 * col + 1, t1);
+          slab[2 * col] = t0;
+          slab[2 * col + 1] = t1;
         }
       }
     }
@@ -1062,9 +1063,33 @@ MER_API int mer_pack_conv_weights(int n, const long long* desc, long total, void
 // finalize: ms[c] = (mean, rstd); running_mean = (1-mom) rm + mom*mean; running_var uses the
 // unbiased variance (torch semantics); num_batches_tracked += 1.
 // ---------------------------------------------------------------------------------------
-// 64 channels per block; the 4 waves split the striped partial rows, then meet in LDS
-__global__ __launch_bounds__(256) void bn_finalize_kernel(int C, long M, const float* __restrict__ stats, float eps,
-                                                          float momentum, float* __restrict__ ms,
+// Forward statistics layout (mer.h MER_BN_STAT_ROWS): one row per output row tile of the conv (<= ceil(M/64)
+// rows, unused rows zero) followed by 64 scratch rows.  Rows are summed in a fixed order: stage 1 (when
+// there are more than 64 rows) folds contiguous row groups into the 64 scratch rows, stage 2 folds <= 64
+// rows per channel -- deterministic whatever the tile size and block schedule were.
+__global__ __launch_bounds__(256) void bn_stat_rows_fold_kernel(int C2, int rows, int per, const float* __restrict__ in,
+                                                                float* __restrict__ out) {
+  __shared__ float part[4][64];
+  const int el = threadIdx.x & 63, pg = threadIdx.x >> 6;
+  const int e = blockIdx.x * 64 + el, grp = blockIdx.y;
+  const int r0 = grp * per, r1 = min(rows, r0 + per);
+  float a0 = 0.f, a1 = 0.f;
+  if (e < C2) {
+    int r = r0 + pg;
+    for (; r + 4 < r1; r += 8) {
+      a0 += in[(long)r * C2 + e];
+      a1 += in[(long)(r + 4) * C2 + e];
+    }
+    if (r < r1) a0 += in[(long)r * C2 + e];
+  }
+  part[pg][el] = a0 + a1;
+  __syncthreads();
+  if (pg == 0 && e < C2) out[(long)grp * C2 + e] = (part[0][el] + part[1][el]) + (part[2][el] + part[3][el]);
+}
+
+// 64 channels per block; the 4 waves split the (<= 64) rows, then meet in LDS
+__global__ __launch_bounds__(256) void bn_finalize_kernel(int C, long M, int rows, const float* __restrict__ stats,
+                                                          float eps, float momentum, float* __restrict__ ms,
                                                           float* __restrict__ rmean, float* __restrict__ rvar,
                                                           long long* __restrict__ nbt) {
   __shared__ float part[4][64][2];
@@ -1080,7 +1105,7 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(int C, long M, const f
   float sum = 0.f, sq = 0.f;
   if (c < C) {
 #pragma unroll 4
-    for (int p = pg; p < MER_BN_STAT_PARTS; p += 4) {
+    for (int p = pg; p < rows; p += 4) {
       sum += stats[(long)p * 2 * C + 2 * c];
       sq += stats[(long)p * 2 * C + 2 * c + 1];
     }
@@ -1102,8 +1127,20 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(int C, long M, const f
 MER_API int mer_bn_finalize(int C, long M, const float* stats, float eps, float momentum, float* ms, float* rmean,
                             float* rvar, long long* num_batches_tracked, void* stream) {
   if (!stats && (!rmean || !rvar)) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, (hipStream_t)stream, C, M, stats, eps,
-                     momentum, ms, rmean, rvar, num_batches_tracked);
+  hipStream_t st = (hipStream_t)stream;
+  const int tiles = (int)((M + 63) / 64);  // MER_BN_STAT_ROWS(M) - 64
+  const float* src = stats;
+  int rows = tiles;
+  if (stats && tiles > 64) {
+    float* scratch = const_cast<float*>(stats) + (long)tiles * 2 * C;
+    const int per = (tiles + 63) / 64;
+    hipLaunchKernelGGL(bn_stat_rows_fold_kernel, dim3((2 * C + 63) / 64, 64), dim3(256), 0, st, 2 * C, tiles, per,
+                       stats, scratch);
+    src = scratch;
+    rows = 64;
+  }
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, st, C, M, rows, src, eps, momentum, ms,
+                     rmean, rvar, num_batches_tracked);
   MER_LAUNCH_CHECK();
 }
 

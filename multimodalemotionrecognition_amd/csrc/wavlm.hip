@@ -250,7 +250,8 @@ __global__ __launch_bounds__(256, 3) void wavlm_attn_kernel(int L, int H, const 
   bf16_t* Ks = reinterpret_cast<bf16_t*>(smem_raw);   // [LP][APAD]
   bf16_t* Vt = Ks + LP * APAD;                        // [ADH][VTP]
   float* gate = reinterpret_cast<float*>(Vt + ADH * VTP);  // [4][16]
-  float* tbl = gate + 64;                              // [2L-1]
+  float* gws = gate + 64;                              // [8][64] gru_rel_pos_linear weight
+  float* tbl = gws + 512;                              // [2L-1]
   const int b = blockIdx.x / H, h = blockIdx.x % H;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int D = H * ADH;
@@ -266,8 +267,26 @@ __global__ __launch_bounds__(256, 3) void wavlm_attn_kernel(int L, int H, const 
       for (int kk = 0; kk < 2; ++kk)
         qb[kk] = *reinterpret_cast<const bf16x8*>(qkv + ((long)b * L + qrow) * ldqkv + h * ADH + kk * 32 + (lane >> 4) * 8);
   }
-  // stage K row-major (16-byte chunks) and V^T from 4-row groups (one 8-byte LDS store per channel);
-  // rows >= L are zero.  All global loads are issued before the first LDS store.
+  // Every global load of the prologue is issued before the first LDS store: K (row-major 16-byte chunks),
+  // V (4-row groups for the V^T image), the relative-position bias row of this head (precomputed table
+  // [H][2L-1] when bucket == nullptr, else gathered through the bucket index), gru_rel_pos_linear's weight
+  // and the x slices of this wave's 16 gate rows.  Rows >= L are zero.
+  const int sub = lane >> 3, cl = lane & 7;
+  u32x4 xg[2];
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const int i = rb * 16 + it * 8 + sub;
+    xg[it] = u32x4{0u, 0u, 0u, 0u};
+    if (active && i < L) xg[it] = *reinterpret_cast<const u32x4*>(x + ((long)b * L + i) * ldx + h * ADH + cl * 8);
+  }
+  float tb[2], gwv[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int r = t + 256 * k;
+    tb[k] = 0.f;
+    if (r < 2 * L - 1) tb[k] = bucket ? rel_emb[(long)bucket[r] * H + h] : rel_emb[(long)h * (2 * L - 1) + r];
+    gwv[k] = gw[r];  // 512 = 8 x 64 weights
+  }
   {
     u32x4 kr[8];
 #pragma unroll
@@ -290,6 +309,12 @@ __global__ __launch_bounds__(256, 3) void wavlm_attn_kernel(int L, int H, const 
       }
     }
 #pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int r = t + 256 * k;
+      if (r < 2 * L - 1) tbl[r] = tb[k];
+      gws[r] = gwv[k];
+    }
+#pragma unroll
     for (int it = 0; it < 8; ++it) {
       const int c = t + it * 256, row = c >> 3, ch = c & 7;
       if (c < LP * 8) *reinterpret_cast<u32x4*>(&Ks[row * APAD + ch * 8]) = kr[it];
@@ -308,27 +333,28 @@ __global__ __launch_bounds__(256, 3) void wavlm_attn_kernel(int L, int H, const 
       }
     }
   }
-  for (int r = t; r < 2 * L - 1; r += 256) tbl[r] = rel_emb[(long)bucket[r] * H + h];
-  // gate of this wave's 16 rows (fp32, from the layer input slice): 8 lanes per row, each lane one
-  // 16-byte chunk (8 channels) of x and the matching 8x8 block of gru_rel_pos_linear's weight.
-  if (active) {
-    const int sub = lane >> 3, cl = lane & 7;
+  __syncthreads();
+  if (!active) return;
+  // gate of this wave's 16 rows (fp32): 8 lanes per row, each lane one 16-byte chunk (8 channels) of x and
+  // the matching 8x8 block of the weight (from LDS); the 8 projections are summed over the row's lanes
+  {
     float gwr[8][8];
 #pragma unroll
-    for (int o = 0; o < 8; ++o)
-#pragma unroll
-      for (int e = 0; e < 8; ++e) gwr[o][e] = gw[o * ADH + cl * 8 + e];
+    for (int o = 0; o < 8; ++o) {
+      const f32x4 lo = *reinterpret_cast<const f32x4*>(&gws[o * ADH + cl * 8]);
+      const f32x4 hi = *reinterpret_cast<const f32x4*>(&gws[o * ADH + cl * 8 + 4]);
+      gwr[o][0] = lo[0]; gwr[o][1] = lo[1]; gwr[o][2] = lo[2]; gwr[o][3] = lo[3];
+      gwr[o][4] = hi[0]; gwr[o][5] = hi[1]; gwr[o][6] = hi[2]; gwr[o][7] = hi[3];
+    }
     const float gbs0 = gb[0] + gb[1] + gb[2] + gb[3], gbs1 = gb[4] + gb[5] + gb[6] + gb[7];
     const float gc = gconst[h];
 #pragma unroll
     for (int it = 0; it < 2; ++it) {
       const int ri = it * 8 + sub, i = rb * 16 + ri;
-      u32x4 xr = u32x4{0u, 0u, 0u, 0u};
-      if (i < L) xr = *reinterpret_cast<const u32x4*>(x + ((long)b * L + i) * ldx + h * ADH + cl * 8);
       float pr[8];
 #pragma unroll
       for (int o = 0; o < 8; ++o) pr[o] = 0.f;
-      const bf16_t* xh = reinterpret_cast<const bf16_t*>(&xr);
+      const bf16_t* xh = reinterpret_cast<const bf16_t*>(&xg[it]);
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const float xe = bf2f(xh[e]);
@@ -352,8 +378,9 @@ __global__ __launch_bounds__(256, 3) void wavlm_attn_kernel(int L, int H, const 
       }
     }
   }
-  __syncthreads();
-  if (!active) return;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
   const int NT = LP / 16;  // key tiles
   const int i = rb * 16 + (lane & 15);
@@ -431,7 +458,7 @@ MER_API int mer_wavlm_attention(int B, int L, int H, const void* qkv, long ldqkv
   if ((ldqkv % 8) || (ldx % 8) || (ldo % 4) || ((((uintptr_t)qkv) | ((uintptr_t)x)) & 15) || (((uintptr_t)out) & 7))
     return (int)hipErrorInvalidValue;
   const int LP = (L + 15) / 16 * 16;
-  const size_t lds = sizeof(bf16_t) * ((size_t)LP * APAD + (size_t)ADH * (LP + 8)) + sizeof(float) * (64 + 2 * L);
+  const size_t lds = sizeof(bf16_t) * ((size_t)LP * APAD + (size_t)ADH * (LP + 8)) + sizeof(float) * (64 + 512 + 2 * L);
   hipLaunchKernelGGL(wavlm_attn_kernel, dim3(B * H, (LP / 16 + 3) / 4), dim3(256), lds, (hipStream_t)stream, L, H,
                      (const bf16_t*)qkv, ldqkv, (const bf16_t*)x, ldx, gate_w, gate_b, gate_const, rel_emb, bucket,
                      (bf16_t*)out, ldo, scale);

@@ -347,8 +347,9 @@ def layernorm(x2d, gamma, beta, y2d, eps=1e-5):
 
 
 def wavlm_attention(qkv, x, gate_w, gate_b, gate_const, rel_emb, bucket, out, B, L, H, scale):
+    """``bucket`` None: ``rel_emb`` is the per-head bias table [H][2L-1] (``rel_emb[bucket].t()``)."""
     LIB("mer_wavlm_attention", B, L, H, qkv.data_ptr(), qkv.stride(0), x.data_ptr(), x.stride(0), gate_w.data_ptr(),
-        gate_b.data_ptr(), gate_const.data_ptr(), rel_emb.data_ptr(), bucket.data_ptr(), out.data_ptr(),
+        gate_b.data_ptr(), gate_const.data_ptr(), rel_emb.data_ptr(), _ptr(bucket), out.data_ptr(),
         out.stride(0), float(scale), stream_ptr())
 
 
@@ -370,9 +371,17 @@ def cast_bf16(x, y):
 BN_STAT_PARTS = 64  # MER_BN_STAT_PARTS (include/mer.h)
 
 
-def bn_stats_buffer(C, device):
-    """Zeroed float[BN_STAT_PARTS][C][2] for conv_fwd's fused BatchNorm statistics."""
-    return torch.zeros(BN_STAT_PARTS, C, 2, device=device, dtype=torch.float32)
+def bn_stat_rows(M: int) -> int:
+    """MER_BN_STAT_ROWS(M): rows of a conv forward's BatchNorm statistics buffer (one per <=64-row output tile,
+    plus 64 finalize scratch rows)."""
+    return (M + 63) // 64 + 64
+
+
+def bn_stats_buffer(C, device, M=None):
+    """Zeroed BatchNorm partial-sum buffer: conv_fwd statistics float[bn_stat_rows(M)][C][2] when the output
+    pixel count M is given, else the striped backward-reduction layout float[BN_STAT_PARTS][C][2]."""
+    rows = BN_STAT_PARTS if M is None else bn_stat_rows(M)
+    return torch.zeros(rows, C, 2, device=device, dtype=torch.float32)
 
 
 def conv_fwd(x, wp, y, stats, R, S, stride, pad, variant=-1):
@@ -381,8 +390,8 @@ def conv_fwd(x, wp, y, stats, R, S, stride, pad, variant=-1):
     Ho, Wo = (H + 2 * pad - R) // stride + 1, (W + 2 * pad - S) // stride + 1
     if tuple(y.shape) != (N, Ho, Wo, Kc) or tuple(wp.shape) != (Kc, R * S * C):
         raise ValueError(f"conv_fwd shapes x{tuple(x.shape)} w{tuple(wp.shape)} y{tuple(y.shape)}")
-    if stats is not None and (stats.numel() != BN_STAT_PARTS * Kc * 2 or not stats.is_contiguous()):
-        raise ValueError("conv_fwd stats must be a contiguous float[BN_STAT_PARTS][K][2] buffer")
+    if stats is not None and (stats.numel() != bn_stat_rows(N * Ho * Wo) * Kc * 2 or not stats.is_contiguous()):
+        raise ValueError("conv_fwd stats must be a contiguous zeroed float[bn_stat_rows(M)][K][2] buffer")
     _launch("conv_fwd", (N, H, W, C, Kc, R, stride), "mer_conv_fwd_ex", N, H, W, C, Kc, R, S, stride, pad, x.data_ptr(),
             wp.data_ptr(), y.data_ptr(), _ptr(stats), int(variant), stream_ptr())
 
@@ -458,6 +467,8 @@ def pack_conv_weights(desc, total):
 
 def bn_finalize(stats, M, eps, momentum, ms, rmean=None, rvar=None, nbt=None):
     C = ms.shape[0]
+    if stats is not None and (stats.numel() != bn_stat_rows(int(M)) * C * 2 or not stats.is_contiguous()):
+        raise ValueError("bn_finalize stats must be the conv_fwd float[bn_stat_rows(M)][C][2] buffer")
     LIB("mer_bn_finalize", C, int(M), _ptr(stats), float(eps), float(momentum), ms.data_ptr(), _ptr(rmean),
         _ptr(rvar), _ptr(nbt), stream_ptr())
 

@@ -228,16 +228,33 @@ def _bn_forward(bn: nn.BatchNorm2d, c: torch.Tensor, stats, training: bool):
     return ms
 
 
-class _StatsArena:
-    """One zeroed buffer for every conv's striped BatchNorm partial sums of a trunk forward
-    (float[MER_BN_STAT_PARTS][C][2] per conv): one memset per forward instead of one per conv."""
+def _fwd_stat_floats(trunk, N: int, H: int, W: int) -> int:
+    """Floats of every conv's forward BatchNorm statistics (MER_BN_STAT_ROWS(M) x C x 2) for [N,3,H,W] frames."""
+    h, w = H // 2, W // 2  # stem conv output (space-to-depth form)
+    total = K.bn_stat_rows(N * h * w) * trunk[0].out_channels * 2
+    h, w = (h - 1) // 2 + 1, (w - 1) // 2 + 1  # maxpool
+    for blk in _blocks(trunk):
+        s = blk.stride
+        h, w = (h + 2 - 3) // s + 1, (w + 2 - 3) // s + 1
+        convs = [blk.conv1, blk.conv2] + ([blk.downsample[0]] if blk.downsample is not None else [])
+        total += sum(K.bn_stat_rows(N * h * w) * c.out_channels * 2 for c in convs)
+    return total
 
-    def __init__(self, trunk, device, factor: int = 1):
+
+class _StatsArena:
+    """One zeroed buffer for all BatchNorm partial sums of a trunk pass: one memset instead of one per BN.
+    Forward: per-row-tile statistics rows (``take(C, M=...)``, float[MER_BN_STAT_ROWS(M)][C][2], sized by
+    ``_fwd_stat_floats``); backward: striped reduction rows (float[MER_BN_STAT_PARTS][C][2] or [C][2])."""
+
+    def __init__(self, trunk, device, factor: int = 1, floats: int = 0):
         total = sum(m.out_channels for m in trunk.modules() if isinstance(m, nn.Conv2d))
-        self.buf = torch.zeros(factor * K.BN_STAT_PARTS * 2 * total, device=device, dtype=torch.float32)
+        n = floats if floats else factor * K.BN_STAT_PARTS * 2 * total
+        self.buf = torch.zeros(n, device=device, dtype=torch.float32)
         self.off = 0
 
-    def take(self, C, parts=None):
+    def take(self, C, parts=None, M=None):
+        if M is not None:
+            parts = K.bn_stat_rows(M)
         parts = K.BN_STAT_PARTS if parts is None else parts
         n = parts * 2 * C
         if self.off + n > self.buf.numel():
@@ -277,7 +294,8 @@ def _conv_bn(trunk, conv, bn, x, stride, pad, training, arena=None, rs=None):
     y = torch.empty(N, Ho, Wo, Kc, device=x.device, dtype=torch.bfloat16)
     stats = None
     if training:
-        stats = arena.take(Kc) if arena is not None else K.bn_stats_buffer(Kc, x.device)
+        M = N * Ho * Wo
+        stats = arena.take(Kc, M=M) if arena is not None else K.bn_stats_buffer(Kc, x.device, M)
     K.conv_fwd(x, trunk.packed(conv, C, False), y, stats, R, S, stride, pad)
     return y, _bn_forward(bn, y, stats, training)
 
@@ -333,7 +351,7 @@ def _trunk_forward(trunk: ResNet18Trunk, video: torch.Tensor, training: bool):
     # stem conv 7x7/s2/p3 as a 4x4/s1/p0 conv on the 2x2 space-to-depth frames (K = 256, not 7*7*8)
     x0 = torch.empty(N, H // 2 + 3, W // 2 + 3, S2D_CH, device=dev, dtype=bf)
     K.pack_input_s2d(video, x0)
-    arena = _StatsArena(trunk, dev) if training else None
+    arena = _StatsArena(trunk, dev, floats=_fwd_stat_floats(trunk, N, H, W)) if training else None
     c1, ms1 = _conv_bn(trunk, conv1, bn1, x0, 1, 0, training, arena, rs=(4, 4))
     Hp, Wp = (c1.shape[1] - 1) // 2 + 1, (c1.shape[2] - 1) // 2 + 1
     p1 = torch.empty(N, Hp, Wp, c1.shape[-1], device=dev, dtype=bf)

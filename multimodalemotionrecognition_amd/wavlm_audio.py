@@ -295,8 +295,13 @@ class WavLMBackbone(nn.Module):
                             cfg.num_conv_pos_embeddings, cfg.num_conv_pos_embeddings // 2, pc.bias, h, act="gelu")
         x = torch.empty(B * L, D, device=dev, dtype=bf)
         K.layernorm(hp, self.encoder.layer_norm.weight, self.encoder.layer_norm.bias, x, eps=cfg.layer_norm_eps)
-        bucket = self.buckets(L, dev)
         H = cfg.num_attention_heads
+        # the relative-position bias rows of every head, gathered once per packed-weight version and length
+        # (layer 0's embedding serves all layers, TF:380-385): [H][2L-1], read directly by the attention kernel
+        tbls = pk.setdefault("bias_tables", {})
+        if L not in tbls:
+            tbls[L] = pk["rel_emb"][self.buckets(L, dev).long()].t().contiguous()
+        bias_tbl = tbls[L]
         scale = (D // H) ** -0.5
         nl = cfg.num_hidden_layers if num_layers is None else num_layers
         qkv = torch.empty(B * L, 3 * D, device=dev, dtype=bf)
@@ -310,7 +315,7 @@ class WavLMBackbone(nn.Module):
             at = layer.attention
             K.gemm_bf16(x, lw["qkv_w"], qkv, bias=lw["qkv_b"])
             K.wavlm_attention(qkv, x, at.gru_rel_pos_linear.weight, at.gru_rel_pos_linear.bias, lw["gate_c"],
-                              pk["rel_emb"], bucket, att, B, L, H, scale)
+                              bias_tbl, None, att, B, L, H, scale)
             K.gemm_bf16(att, lw["out_w"], y32, bias=at.out_proj.bias, residual=x)
             K.layernorm(y32, layer.layer_norm.weight, layer.layer_norm.bias, x1, eps=cfg.layer_norm_eps)
             K.gemm_bf16(x1, lw["ff1_w"], ff, bias=layer.feed_forward.intermediate_dense.bias, act="gelu")

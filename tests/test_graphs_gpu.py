@@ -82,7 +82,8 @@ def test_train_step_graphs_match_eager():
         me, se = _twin(8)
         me.load_state_dict(mg.state_dict())
         grads = {}
-        for tag, m, st, on in (("graph", mg, sg, True), ("eager", me, se, False), ("eager2", me, se, False)):
+        for tag, m, st, on in (("graph", mg, sg, True), ("eager", me, se, False), ("eager2", me, se, False),
+                               ("eager3", me, se, False)):
             G.ENABLED = on
             m.train()
             st.opt.zero_grad()
@@ -90,14 +91,15 @@ def test_train_step_graphs_match_eager():
             loss.backward()
             grads[tag] = (float(loss), {n: q.grad.detach().clone() for n, q in m.named_parameters()
                                         if q.grad is not None})
-        (lg, gg), (le, ge), (le2, ge2) = grads["graph"], grads["eager"], grads["eager2"]
+        (lg, gg), (le, ge), (le2, ge2), (_, ge3) = grads["graph"], grads["eager"], grads["eager2"], grads["eager3"]
         assert abs(lg - le) < 1e-3 * max(1.0, abs(le)), (lg, le)
         assert set(gg) == set(ge) and len(gg) > 60
         worst = []
         for n in ge:
             den = max(float(ge[n].norm()), 1e-6)
             d_graph = float((gg[n] - ge[n]).norm()) / den
-            d_noise = float((ge2[n] - ge[n]).norm()) / den  # eager-vs-eager: the atomic-order noise floor
+            # eager-vs-eager: the noise floor of the backward's fp32-atomic BatchNorm sums (two re-runs)
+            d_noise = max(float((ge2[n] - ge[n]).norm()), float((ge3[n] - ge[n]).norm())) / den
             worst.append((d_graph, d_noise, n))
             assert d_graph <= 4 * d_noise + 2e-3, (n, d_graph, d_noise)
         print("worst graph-vs-eager gradient differences (rel, noise floor):", sorted(worst)[-3:])

@@ -150,6 +150,10 @@ def test_wavlm_attention_vs_torch(L):
     out = torch.empty(B * L, D, dtype=torch.bfloat16, device="cuda")
     K.wavlm_attention(qkv.cuda(), x.cuda(), gw.cuda(), gb.cuda(), gc.cuda(), rel_emb.cuda(),
                       bucket.int().cuda(), out, B, L, H, scale)
+    out_tbl = torch.empty_like(out)  # precomputed per-head bias table path (bucket = None)
+    K.wavlm_attention(qkv.cuda(), x.cuda(), gw.cuda(), gb.cuda(), gc.cuda(), rel_emb[bucket].t().contiguous().cuda(),
+                      None, out_tbl, B, L, H, scale)
+    assert torch.equal(out, out_tbl)
     q, k, v = (qkv.float()[:, i * D:(i + 1) * D].view(B, L, H, dh).transpose(1, 2) for i in range(3))
     proj = x.float().view(B, L, H, dh) @ gw.t() + gb                       # [B,L,H,8]
     ga = torch.sigmoid(proj[..., :4].sum(-1))
