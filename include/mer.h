@@ -25,10 +25,14 @@
 /* BatchNorm batch statistics of a conv forward (mer_conv_fwd `stats`): float[MER_BN_STAT_ROWS(M)][C][2]
  * (sum, sum of squares), zeroed by the caller, M = N*Ho*Wo output pixels.  Each output row tile of the
  * conv stores its own row (a single writer per element: deterministic), unused rows stay zero, and the last
- * 64 rows are mer_bn_finalize's scratch.  Backward reductions (mer_conv_dgrad_bnr, mer_bn_bwd_reduce) use
- * MER_BN_STAT_PARTS striped partial rows, float[MER_BN_STAT_PARTS][C][2], accumulated with fp32 atomics. */
+ * 64 rows are mer_bn_finalize's scratch.  The backward reductions use the same single-writer rows
+ * (MER_BN_RED_ROWS, MER_BN_RED_WS_ROWS below), so the whole trunk step is free of fp32 atomics. */
 #define MER_BN_STAT_PARTS 64
 #define MER_BN_STAT_ROWS(M) (((M) + 63) / 64 + 64)
+/* Backward BatchNorm reductions: per-row-tile rows of mer_conv_dgrad_bnr (+4 for the stride-2 parity classes,
+ * +64 fold scratch) and the per-block rows of mer_bn_bwd_reduce (<= 512 blocks + 64 scratch). */
+#define MER_BN_RED_ROWS(M) (((M) + 63) / 64 + 4 + 64)
+#define MER_BN_RED_WS_ROWS 576
 
 #ifdef __cplusplus
 extern "C" {
@@ -240,17 +244,19 @@ int mer_conv_dgrad_ex(int N, int H, int W, int C, int K, int R, int S, int strid
                       void* stream);
 
 /* mer_conv_dgrad_ex (pipelined kernel only) with the BatchNorm-backward reduction of the BN the gradient
- * flows into fused into the epilogue: g = (bn_mask > 0) * dx (after the residual), bn_red[p][c] +=
- * (sum g, sum g * (bn_x - mean) * rstd) with (mean, rstd) = bn_ms[c], and bn_red2 likewise for bn_x2 /
- * bn_ms2 (may be NULL).  bn_red / bn_red2 are zeroed float[MER_BN_STAT_PARTS][C][2]; collapse them with
- * mer_partials_sum before mer_bn_bwd_apply.  Replaces mer_bn_bwd_reduce after a conv backward. */
+ * flows into fused into the epilogue: g = (bn_mask > 0) * dx (after the residual), each output row tile
+ * STORES its (sum g, sum g * (bn_x - mean) * rstd) row with (mean, rstd) = bn_ms[c] into bn_red, and bn_red2
+ * likewise for bn_x2 / bn_ms2 (may be NULL).  bn_red / bn_red2 are zeroed float[MER_BN_RED_ROWS(M)][C][2]
+ * (M = N*H*W gradient pixels); fold them with mer_partials_sum(C, MER_BN_RED_ROWS(M) - 64, ...) before
+ * mer_bn_bwd_apply (fixed-order sums: deterministic).  Replaces mer_bn_bwd_reduce after a conv backward. */
 int mer_conv_dgrad_bnr(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, const void* dy,
                        const void* wt_packed, void* dx, const void* residual, const void* residual_mask,
                        const void* bn_mask, const void* bn_x, const float* bn_ms, float* bn_red, const void* bn_x2,
                        const float* bn_ms2, float* bn_red2, int variant, void* stream);
 
-/* out[c][0:2] = sum_p in[p][c][0:2] over `parts` striped partial rows. */
-int mer_partials_sum(int C, int parts, const float* in, float* out, void* stream);
+/* out[c][0:2] = sum_p in[p][c][0:2] over `parts` partial rows, in a fixed order.  parts > 64 needs 64 more
+ * rows after them in `in` (fold scratch, overwritten). */
+int mer_partials_sum(int C, int parts, float* in, float* out, void* stream);
 
 /* dw[k][c][r][s] += sum_p dy[p][k] x(p; r,s,c) for c < Creal, fp32 PyTorch layout (dw initialised).  The
  * pixel reduction is split `splits` ways; each split writes an fp32 slab [K][R*S*C] into `workspace`
@@ -289,9 +295,10 @@ int mer_bn_finalize(int C, long M, const float* stats, float eps, float momentum
 int mer_bn_apply(long M, int C, const void* x, const float* ms, const float* gamma, const float* beta, const void* res,
                  const float* ms2, const float* gamma2, const float* beta2, int relu, void* y, void* stream);
 
-/* BN backward reduction: red[c] += (sum g, sum g*xhat), g = dy * (mask > 0) (mask = ReLU output or NULL). */
+/* BN backward reduction: red[c] = (sum g, sum g*xhat), g = dy * (mask > 0) (mask = ReLU output or NULL);
+ * per-block partial rows in workspace (float[MER_BN_RED_WS_ROWS][C][2]) folded in a fixed order. */
 int mer_bn_bwd_reduce(long M, int C, const void* dy, const void* mask, const void* x, const float* ms, float* red,
-                      void* stream);
+                      float* workspace, void* stream);
 
 /* BN backward apply: dx = gamma*rstd*(g - s1/M - xhat*s2/M) with batch statistics (batch_stats=1, train
  * mode) or dx = gamma*rstd*g with running statistics (batch_stats=0, eval mode); dgamma += s2, dbeta += s1. */
@@ -305,12 +312,12 @@ int mer_bn_bwd_apply(long M, int C, const void* dy, const void* mask, const void
 int mer_stem_bnrelu_maxpool_fwd(int N, int H, int W, int C, const void* x, const float* ms, const float* gamma,
                                 const float* beta, void* y, void* argmax, void* stream);
 /* Its backward to the conv output: the maxpool gather of dy is written to dx, then g = dx * relu'(bn(x)) (mask
- * recomputed from x, no activation tensor) feeds a BatchNorm reduction (red[C][2] += (sum g, sum g*xhat); red
- * zeroed by the caller) and an in-place apply pass
+ * recomputed from x, no activation tensor) feeds a BatchNorm reduction (red[C][2] = (sum g, sum g*xhat), through
+ * workspace float[MER_BN_RED_WS_ROWS][C][2] as mer_bn_bwd_reduce) and an in-place apply pass
  * dx = gamma*rstd*(g - [batch_stats] (sum g + xhat * sum g*xhat)/M); dgamma += sum g*xhat, dbeta += sum g. */
 int mer_stem_pool_bn_bwd(int N, int H, int W, int C, const void* dy, const void* argmax, const void* x,
                          const float* ms, const float* gamma, const float* beta, float* red, int batch_stats,
-                         void* dx, float* dgamma, float* dbeta, void* stream);
+                         void* dx, float* dgamma, float* dbeta, float* workspace, void* stream);
 
 /* MaxPool2d(3, 2, 1) forward (argmax tap saved as uint8) and gather backward. */
 int mer_maxpool_fwd(int N, int H, int W, int C, const void* x, void* y, void* argmax, void* stream);

@@ -37,7 +37,7 @@ struct ConvGeom {
   // dgrad only: the BatchNorm-backward reduction of the BN whose relu'd output this gradient flows
   // into, fused into the epilogue (bn_bwd_reduce semantics; NULL bnr_red = off).  g = (mask > 0) * y,
   // red[p][c] += (sum g, sum g * (x - mean) * rstd); red2 likewise for a second BN reading the same g
-  // (the downsample branch).  Striped over MER_BN_STAT_PARTS rows like the forward statistics.
+  // (the downsample branch).  One stored row per output row tile (MER_BN_RED_ROWS), like the forward statistics.
   const bf16_t* bnr_mask;
   const bf16_t* bnr_x;
   const float* bnr_ms;
@@ -658,7 +658,15 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_pipe_kernel(ConvGeom g) 
         for (int q = 0; q < 3; ++q) red[((wr * WN + wc) * FN * 16 + j * 16 + fr) * 3 + q] = ps[j][q];
     __syncthreads();
     if (wr == 0 && fq == 0) {
-      const long slab = (long)(ty % MER_BN_STAT_PARTS) * g.Ncols * 2;
+      // this block's own partial row (single writer per element -> deterministic after the fixed-order fold):
+      // row = ty, after the row tiles of the preceding parity classes in the PAR (stride-2) form
+      long row_id = ty;
+      if (PAR)
+        for (int c2 = 0; c2 < (int)blockIdx.y; ++c2) {
+          const ParClass q = par_class(g, c2);
+          row_id += (g.N * q.Hc * q.Wc + BM_ - 1) / BM_;
+        }
+      const long slab = row_id * g.Ncols * 2;
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
         const int col = n0 + wc * TN + j * 16 + fr;
@@ -671,11 +679,11 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_pipe_kernel(ConvGeom g) 
           t2 += o[2];
         }
         if (col < g.Ncols) {
-          atomicAdd(g.bnr_red + slab + 2 * col, t0);
-          atomicAdd(g.bnr_red + slab + 2 * col + 1, t1);
+          g.bnr_red[slab + 2 * col] = t0;
+          g.bnr_red[slab + 2 * col + 1] = t1;
           if (g.bnr_red2) {
-            atomicAdd(g.bnr_red2 + slab + 2 * col, t0);
-            atomicAdd(g.bnr_red2 + slab + 2 * col + 1, t2);
+            g.bnr_red2[slab + 2 * col] = t0;
+            g.bnr_red2[slab + 2 * col + 1] = t2;
           }
         }
       }
@@ -1244,10 +1252,10 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(long M, int C, const
                                                             const bf16_t* __restrict__ x, const float* __restrict__ ms,
                                                             const float* __restrict__ mgamma,
                                                             const float* __restrict__ mbeta,
-                                                            float* __restrict__ red, long rows_per_block) {
-  __shared__ float part[2][512];
-  for (int i = threadIdx.x; i < 2 * 512; i += 256) (&part[0][0])[i] = 0.f;
-  __syncthreads();
+                                                            float* __restrict__ rows, long rows_per_block) {
+  // per-thread sums over this block's rows, then the rows_per_iter threads of a channel chunk meet in LDS in
+  // thread order and the block STORES its partial row: no atomics, deterministic
+  __shared__ float part[2][2048];  // [s1|s2][tr * C + c], rows_per_iter * C <= 2048
   const int cpr = C / 8;                     // 16B chunks per row
   const int rows_per_iter = 256 / cpr > 0 ? 256 / cpr : 1;
   const int tc = threadIdx.x % cpr, tr = threadIdx.x / cpr;
@@ -1281,29 +1289,39 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(long M, int C, const
     }
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      atomicAdd(&part[0][tc * 8 + i], s1[i]);
-      atomicAdd(&part[1][tc * 8 + i], s2[i]);
+      part[0][tr * C + tc * 8 + i] = s1[i];
+      part[1][tr * C + tc * 8 + i] = s2[i];
     }
   }
   __syncthreads();
+  float* out = rows + (long)blockIdx.x * C * 2;
   for (int c = threadIdx.x; c < C; c += 256) {
-    atomicAdd(red + 2 * c, part[0][c]);
-    atomicAdd(red + 2 * c + 1, part[1][c]);
+    float a = 0.f, b = 0.f;
+    for (int q = 0; q < rows_per_iter; ++q) {
+      a += part[0][q * C + c];
+      b += part[1][q * C + c];
+    }
+    out[2 * c] = a;
+    out[2 * c + 1] = b;
   }
 }
+// rows_per_block keeps the block count <= 512 (the workspace holds MER_BN_RED_WS_ROWS = 512 + 64 rows)
+static long bn_bwd_reduce_rpb(long M) { return (M + 511) / 512 > 32 ? (M + 511) / 512 : 32; }
+static int partials_fold(int C, int parts, float* in, float* out, hipStream_t st);
 MER_API int mer_bn_bwd_reduce(long M, int C, const void* dy, const void* mask, const void* x, const float* ms,
-                              float* red, void* stream) {
+                              float* red, float* workspace, void* stream) {
   if (C % 8 || C > 512) return (int)hipErrorInvalidValue;
-  const long rpb = (M + 511) / 512 > 32 ? (M + 511) / 512 : 32;  // ~512 blocks whatever the layer size
-  const long blocks = (M + rpb - 1) / rpb;
+  const long rpb = bn_bwd_reduce_rpb(M);
+  const int blocks = (int)((M + rpb - 1) / rpb);
   hipLaunchKernelGGL((bn_bwd_reduce_kernel<false>), dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, M, C,
                      (const bf16_t*)dy, (const bf16_t*)mask, (const bf16_t*)x, ms, (const float*)nullptr,
-                     (const float*)nullptr, red, rpb);
-  MER_LAUNCH_CHECK();
+                     (const float*)nullptr, workspace, rpb);
+  return partials_fold(C, blocks, workspace, red, (hipStream_t)stream);
 }
 
-// out[c] = sum_p in[p][c] over `parts` striped partial rows of (a, b) pairs (fused-epilogue reductions)
-// 64 (c, slot) entries per block; the 4 waves split the partial rows, then meet in LDS
+// out[c] = sum_p in[p][c] over `parts` partial rows of (a, b) pairs (fused-epilogue reductions), in a fixed
+// order; 64 entries per block, the 4 waves split the rows, then meet in LDS.  More than 64 rows are first
+// folded (bn_stat_rows_fold_kernel) into the 64 scratch rows the caller provides after them.
 __global__ __launch_bounds__(256) void partials_sum_kernel(int C, int parts, const float* __restrict__ in,
                                                            float* __restrict__ out) {
   __shared__ float part[4][64];
@@ -1318,11 +1336,22 @@ __global__ __launch_bounds__(256) void partials_sum_kernel(int C, int parts, con
   __syncthreads();
   if (pg == 0 && e < 2 * C) out[e] = part[0][el] + part[1][el] + part[2][el] + part[3][el];
 }
-MER_API int mer_partials_sum(int C, int parts, const float* in, float* out, void* stream) {
-  if (C <= 0 || parts <= 0) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(partials_sum_kernel, dim3((2 * C + 63) / 64), dim3(256), 0, (hipStream_t)stream, C, parts, in,
-                     out);
+static int partials_fold(int C, int parts, float* in, float* out, hipStream_t st) {
+  const float* src = in;
+  if (parts > 64) {
+    float* scratch = in + (long)parts * 2 * C;
+    const int per = (parts + 63) / 64;
+    hipLaunchKernelGGL(bn_stat_rows_fold_kernel, dim3((2 * C + 63) / 64, 64), dim3(256), 0, st, 2 * C, parts, per, in,
+                       scratch);
+    src = scratch;
+    parts = 64;
+  }
+  hipLaunchKernelGGL(partials_sum_kernel, dim3((2 * C + 63) / 64), dim3(256), 0, st, C, parts, src, out);
   MER_LAUNCH_CHECK();
+}
+MER_API int mer_partials_sum(int C, int parts, float* in, float* out, void* stream) {
+  if (C <= 0 || parts <= 0) return (int)hipErrorInvalidValue;
+  return partials_fold(C, parts, in, out, (hipStream_t)stream);
 }
 
 // dx = gamma*rstd*(g - s1/M - xhat*s2/M) (bf16), and (block 0) dgamma += s2, dbeta += s1.
@@ -1581,7 +1610,7 @@ MER_API int mer_stem_bnrelu_maxpool_fwd(int N, int H, int W, int C, const void* 
 
 MER_API int mer_stem_pool_bn_bwd(int N, int H, int W, int C, const void* dy, const void* argmax, const void* x,
                                  const float* ms, const float* gamma, const float* beta, float* red, int batch_stats,
-                                 void* dx, float* dgamma, float* dbeta, void* stream) {
+                                 void* dx, float* dgamma, float* dbeta, float* workspace, void* stream) {
   if (C % 8 || C > 512 || 256 % (C / 8) || (long)N * H * W >= (1L << 22)) return (int)hipErrorInvalidValue;
   const hipStream_t st = (hipStream_t)stream;
   const long M = (long)N * H * W;
@@ -1589,9 +1618,12 @@ MER_API int mer_stem_pool_bn_bwd(int N, int H, int W, int C, const void* dy, con
   // recomputed from (x, BN); 3) BN apply in place over dx (each element read, then written, by one thread)
   int rc = mer_maxpool_bwd(N, H, W, C, dy, argmax, dx, stream);
   if (rc) return rc;
-  const long rpb = (M + 511) / 512 > 32 ? (M + 511) / 512 : 32;
-  hipLaunchKernelGGL((bn_bwd_reduce_kernel<true>), dim3((unsigned)((M + rpb - 1) / rpb)), dim3(256), 0, st, M, C,
-                     (const bf16_t*)dx, (const bf16_t*)nullptr, (const bf16_t*)x, ms, gamma, beta, red, rpb);
+  const long rpb = bn_bwd_reduce_rpb(M);
+  const int blocks = (int)((M + rpb - 1) / rpb);
+  hipLaunchKernelGGL((bn_bwd_reduce_kernel<true>), dim3((unsigned)blocks), dim3(256), 0, st, M, C, (const bf16_t*)dx,
+                     (const bf16_t*)nullptr, (const bf16_t*)x, ms, gamma, beta, workspace, rpb);
+  rc = partials_fold(C, blocks, workspace, red, st);
+  if (rc) return rc;
   hipLaunchKernelGGL((bn_bwd_apply_kernel<true>), dim3(bn_stream_grid(M * C / 8)), dim3(256), 0, st, M, C,
                      (const bf16_t*)dx, (const bf16_t*)nullptr, (const bf16_t*)x, ms, gamma, beta, red, batch_stats,
                      (bf16_t*)dx, dgamma, dbeta);

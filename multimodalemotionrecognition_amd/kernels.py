@@ -377,6 +377,14 @@ def bn_stat_rows(M: int) -> int:
     return (M + 63) // 64 + 64
 
 
+def bn_red_rows(M: int) -> int:
+    """MER_BN_RED_ROWS(M): rows of a fused BN-backward reduction buffer of a dgrad with M output pixels."""
+    return (M + 63) // 64 + 4 + 64
+
+
+BN_RED_WS_ROWS = 576  # MER_BN_RED_WS_ROWS: bn_bwd_reduce workspace rows
+
+
 def bn_stats_buffer(C, device, M=None):
     """Zeroed BatchNorm partial-sum buffer: conv_fwd statistics float[bn_stat_rows(M)][C][2] when the output
     pixel count M is given, else the striped backward-reduction layout float[BN_STAT_PARTS][C][2]."""
@@ -410,17 +418,20 @@ def conv_dgrad(dy, wt, dx, R, S, stride, pad, residual=None, mask=None, variant=
         if t is not None and tuple(t.shape) != tuple(dx.shape):
             raise ValueError("conv_dgrad bnr tensors must match dx")
     for t in (b[3], b[6]):
-        if t is not None and t.numel() != BN_STAT_PARTS * C * 2:
-            raise ValueError("conv_dgrad bnr red buffers must be [BN_STAT_PARTS, C, 2]")
+        if t is not None and t.numel() != bn_red_rows(N * H * W) * C * 2:
+            raise ValueError("conv_dgrad bnr red buffers must be zeroed [bn_red_rows(N*H*W), C, 2]")
     _launch("conv_dgrad", (N, H, W, C, Kc, R, stride), "mer_conv_dgrad_bnr", N, H, W, C, Kc, R, S, stride, pad,
             dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), _ptr(residual), _ptr(mask), *[_ptr(t) for t in b],
             int(variant), stream_ptr())
 
 
 def partials_sum(parts_buf, out):
-    """out[C,2] = parts_buf[BN_STAT_PARTS, C, 2].sum(0) (collapse a fused-epilogue reduction)."""
+    """out[C,2] = fixed-order sum of the data rows of a [bn_red_rows(M), C, 2] fused-epilogue reduction
+    buffer (its last 64 rows are the fold scratch)."""
     P, C, _ = parts_buf.shape
-    LIB("mer_partials_sum", C, P, parts_buf.data_ptr(), out.data_ptr(), stream_ptr())
+    if P <= 64:
+        raise ValueError("partials_sum expects a bn_red_rows(M) buffer (data rows + 64 scratch rows)")
+    LIB("mer_partials_sum", C, P - 64, parts_buf.data_ptr(), out.data_ptr(), stream_ptr())
     return out
 
 
@@ -480,10 +491,15 @@ def bn_apply(x, ms, gamma, beta, y, relu, res=None, ms2=None, gamma2=None, beta2
         _ptr(gamma2), _ptr(beta2), int(relu), y.data_ptr(), stream_ptr())
 
 
-def bn_bwd_reduce(dy, mask, x, ms, red):
+def bn_bwd_reduce(dy, mask, x, ms, red, workspace=None):
+    """red[C,2] = (sum g, sum g*xhat) (written); workspace: float[BN_RED_WS_ROWS * C * 2] or None."""
     C = x.shape[-1]
+    if workspace is None:
+        workspace = torch.empty(BN_RED_WS_ROWS * C * 2, device=x.device, dtype=torch.float32)
+    if workspace.numel() < BN_RED_WS_ROWS * C * 2:
+        raise ValueError("bn_bwd_reduce workspace too small")
     LIB("mer_bn_bwd_reduce", x.numel() // C, C, dy.data_ptr(), _ptr(mask), x.data_ptr(), ms.data_ptr(),
-        red.data_ptr(), stream_ptr())
+        red.data_ptr(), workspace.data_ptr(), stream_ptr())
 
 
 def bn_bwd_apply(dy, mask, x, ms, gamma, red, dx, dgamma, dbeta, batch_stats=True):
@@ -504,12 +520,17 @@ def stem_bnrelu_maxpool(x, ms, gamma, beta, y, arg):
         y.data_ptr(), arg.data_ptr(), stream_ptr())
 
 
-def stem_pool_bn_bwd(dy, arg, x, ms, gamma, beta, red, dx, dgamma, dbeta, batch_stats=True):
-    """Backward of stem_bnrelu_maxpool to the conv output x (red: zeroed float[C][2] scratch)."""
+def stem_pool_bn_bwd(dy, arg, x, ms, gamma, beta, red, dx, dgamma, dbeta, batch_stats=True, workspace=None):
+    """Backward of stem_bnrelu_maxpool to the conv output x (red: float[C][2] written; workspace as
+    bn_bwd_reduce)."""
     N, H, W, C = x.shape
+    if workspace is None:
+        workspace = torch.empty(BN_RED_WS_ROWS * C * 2, device=x.device, dtype=torch.float32)
+    if workspace.numel() < BN_RED_WS_ROWS * C * 2:
+        raise ValueError("stem_pool_bn_bwd workspace too small")
     LIB("mer_stem_pool_bn_bwd", N, H, W, C, dy.data_ptr(), arg.data_ptr(), x.data_ptr(), ms.data_ptr(),
         gamma.data_ptr(), beta.data_ptr(), red.data_ptr(), int(batch_stats), dx.data_ptr(), _ptr(dgamma),
-        _ptr(dbeta), stream_ptr())
+        _ptr(dbeta), workspace.data_ptr(), stream_ptr())
 
 
 def maxpool_bwd(dy, arg, dx):

@@ -387,15 +387,25 @@ def _bn_bwd(g, mask, x, ms, bn, red, grads, training):
     return dx
 
 
+def _block_bwd_floats(sv) -> int:
+    """Arena floats for one block_backward: its bn1 reduction rows, two bn_bwd_reduce workspaces and the
+    fused reductions of an upstream block's bn2 / downsample BN at the block input's resolution."""
+    xin, bc1, _, ba1, bc2, _, _, _, out = sv
+    C1, C2, Cin = bc1.shape[-1], bc2.shape[-1], xin.shape[-1]
+    return 2 * (K.bn_red_rows(ba1.numel() // C1) * C1 + 2 * K.BN_RED_WS_ROWS * C2 + C2 * 2
+                + 2 * K.bn_red_rows(xin.numel() // Cin) * Cin)
+
+
 def _bnr_target(blk_sv, blk, arena):
     """The fused-reduction target for a gradient flowing into ``blk``'s output: its bn2 (and downsample
     BN) read g = grad * (out > 0); returns (bnr tuple for conv_dgrad, partial buffers)."""
     xin, bc1, bms1, ba1, bc2, bms2, cd, msd, out = blk_sv
     C2 = bc2.shape[-1]
-    red2 = arena.take(C2)
+    rows = K.bn_red_rows(out.numel() // C2)  # one row per dgrad output row tile (+ scratch)
+    red2 = arena.take(C2, parts=rows)
     if cd is None:
         return (out, bc2, bms2, red2), (red2, None)
-    redd = arena.take(C2)
+    redd = arena.take(C2, parts=rows)
     return (out, bc2, bms2, red2, cd, msd, redd), (red2, redd)
 
 
@@ -409,8 +419,9 @@ def block_backward(trunk, blk: BasicBlock, sv, dx: torch.Tensor, grads, training
     (saved, block) of the preceding block, whose reductions this block's input-gradient dgrad fuses.
     """
     dev = dx.device
-    arena = _StatsArena(trunk, dev, factor=2) if arena is None else arena  # zeroed once per backward
     xin, bc1, bms1, ba1, bc2, bms2, cd, msd, out = sv
+    if arena is None:  # standalone call: room for this block's own reductions and one upstream target
+        arena = _StatsArena(trunk, dev, floats=_block_bwd_floats(sv))
     g_out = dx
     s = blk.stride
     C2 = bc2.shape[-1]
@@ -419,11 +430,11 @@ def block_backward(trunk, blk: BasicBlock, sv, dx: torch.Tensor, grads, training
         redd = K.partials_sum(pre[1], torch.empty(C2, 2, device=dev, dtype=torch.float32)) if cd is not None else None
     else:
         red2 = arena.take(C2, parts=1)
-        K.bn_bwd_reduce(g_out, out, bc2, bms2, red2)
+        K.bn_bwd_reduce(g_out, out, bc2, bms2, red2, arena.take(C2, parts=K.BN_RED_WS_ROWS))
         redd = None
         if cd is not None:
             redd = arena.take(C2, parts=1)
-            K.bn_bwd_reduce(g_out, out, cd, msd, redd)
+            K.bn_bwd_reduce(g_out, out, cd, msd, redd, arena.take(C2, parts=K.BN_RED_WS_ROWS))
     dc2 = _bn_bwd(g_out, out, bc2, bms2, blk.bn2, red2, grads, training)
     dcd = _bn_bwd(g_out, out, cd, msd, blk.downsample[1], redd, grads, training) if cd is not None else None
     # conv2 (its dgrad also reduces bn1's backward sums: g = da1 * (ba1 > 0))
@@ -432,7 +443,7 @@ def block_backward(trunk, blk: BasicBlock, sv, dx: torch.Tensor, grads, training
         K.conv_wgrad(ba1, dc2, w2, 3, 3, 1, 1)
     da1 = torch.empty_like(ba1)
     C1 = bc1.shape[-1]
-    red1p = arena.take(C1)
+    red1p = arena.take(C1, parts=K.bn_red_rows(ba1.numel() // C1))
     K.conv_dgrad(dc2, trunk.packed(blk.conv2, C2, True), da1, 3, 3, 1, 1, bnr=(ba1, bc1, bms1, red1p))
     red1 = K.partials_sum(red1p, torch.empty(C1, 2, device=dev, dtype=torch.float32))
     dc1 = _bn_bwd(da1, ba1, bc1, bms1, blk.bn1, red1, grads, training)
@@ -471,7 +482,8 @@ def _trunk_backward(trunk: ResNet18Trunk, saved, dfeat: torch.Tensor, training: 
     blocks = _blocks(trunk)
     svs = saved["blocks"]
     pre = None
-    arena = _StatsArena(trunk, dev, factor=2)  # every backward BatchNorm reduction: one memset
+    # every backward BatchNorm reduction buffer of this pass: one memset
+    arena = _StatsArena(trunk, dev, floats=sum(_block_bwd_floats(sv) for sv in svs) + 2 * K.BN_RED_WS_ROWS * 64 * 2)
     for i in reversed(range(len(blocks))):
         prev = (svs[i - 1], blocks[i - 1]) if i > 0 else None
         dx, pre = block_backward(trunk, blocks[i], svs[i], dx, grads, training, pre=pre, prev=prev, arena=arena)
@@ -481,7 +493,7 @@ def _trunk_backward(trunk: ResNet18Trunk, saved, dfeat: torch.Tensor, training: 
     red = arena.take(c1.shape[-1], parts=1)
     dc1 = torch.empty_like(c1)  # maxpool + relu + bn1 backward in one reduction pass and one apply pass
     K.stem_pool_bn_bwd(dx, arg, c1, ms1, bn1.weight, bn1.bias, red, dc1, _grad(bn1.weight, grads),
-                       _grad(bn1.bias, grads), training)
+                       _grad(bn1.bias, grads), training, workspace=arena.take(c1.shape[-1], parts=K.BN_RED_WS_ROWS))
     w = _grad(trunk[0].weight, grads)
     if w is not None:  # wgrad of the 4x4 space-to-depth form, then gathered back to [64][3][7][7]
         Kc, Cin, R, S = trunk[0].weight.shape
