@@ -42,16 +42,20 @@ extern "C" {
 
 /* C[m,n] (+)= act(sum_k A(m,k) B(k,n) + bias[n]), batched over grid z.
  * A(m,k) = A[m*sam + k*sak] (+ batch*bsa), B(k,n) = B[k*sbk + n*sbn]; C row-major (ldc).
- * beta=1 accumulates into C; splitk>1 atomically adds K slices (act must be 0).
+ * beta=1 accumulates into C.  splitk>1 (act must be 0, C initialised): each K slice writes its partial
+ * into workspace [batch][splitk][M][N] (fp32) and the slices are added into C in slice order -- results
+ * are run-to-run reproducible (no atomics).  workspace may be NULL when splitk == 1.
  * Replaces every nn.Linear of the head: fusion.py:269-274 (v_in_proj/a_in_proj/audio_seq_proj),
  * fusion.py:312-326 (xattn_mlp / xattn_gate / xattn_classifier), the MHA in/out projections
  * (TORCH:6576-6606) and their backward GEMMs (dX = dY W, dW = dY^T X). */
 int mer_gemm_f32(int M, int N, int K, const void* A, int a_dtype, long sam, long sak, long bsa, const void* B,
                  int b_dtype, long sbk, long sbn, long bsb, float* C, long ldc, long bsc, const float* bias, int beta,
-                 int act, int splitk, int batch, void* stream);
+                 int act, int splitk, int batch, float* workspace, void* stream);
 
-/* out[n] += sum_m X[m*ldx + n]  (bias gradients; out must be initialised). */
-int mer_colsum_f32(int M, int N, const float* X, long ldx, float* out, void* stream);
+/* out[n] += sum_m X[m*ldx + n]  (bias gradients; out must be initialised).  Deterministic: per-block
+ * partial rows in workspace (MER_COLSUM_WS_FLOATS(M, N) floats), folded in block order. */
+#define MER_COLSUM_WS_FLOATS(M, N) ((long)(((M) + 15) / 16) * (N))
+int mer_colsum_f32(int M, int N, const float* X, long ldx, float* out, float* workspace, void* stream);
 
 /* Multi-head attention core of nn.MultiheadAttention (fusion.py:276-281,394,398 -> TORCH:6576-6606):
  * P = softmax(scale * Q_h K_h^T + bias[b]); O_h = dropout(P) V_h.  Rows: X + (b*L+i)*ld + h*dh.
@@ -77,10 +81,12 @@ int mer_add_ln_fwd(int rows, int d, int rows_per_sample, const float* x, const f
                    const unsigned long long* seed, unsigned long long site, const float* gamma, const float* beta, float eps, float* y, float* sum_out,
                    float* mean_out, float* rstd_out, void* stream);
 
-/* Backward of mer_add_ln_fwd: dx = dsum, dr = s_b*dsum (dr may be NULL); dgamma/dbeta accumulate. */
+/* Backward of mer_add_ln_fwd: dx = dsum, dr = s_b*dsum (dr may be NULL); dgamma/dbeta accumulate (+=),
+ * deterministically: per-64-row-block partials in workspace (MER_ADD_LN_WS_FLOATS(rows, d) floats). */
+#define MER_ADD_LN_WS_FLOATS(rows, d) ((long)(((rows) + 63) / 64) * 2 * (d))
 int mer_add_ln_bwd(int rows, int d, int rows_per_sample, const float* dy, const float* s, const float* mean,
                    const float* rstd, const float* gamma, float dp_p, const unsigned long long* seed, unsigned long long site, float* dx, float* dr,
-                   float* dgamma, float* dbeta, void* stream);
+                   float* dgamma, float* dbeta, float* workspace, void* stream);
 
 /* TemporalPooler 'mean' (temporal.py:108-109): y[b*ldy + c] = mean_l x[b,l,c]; and its backward. */
 int mer_mean_pool_fwd(int B, int L, int D, const float* x, float* y, long ldy, void* stream);

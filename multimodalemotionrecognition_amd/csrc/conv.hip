@@ -187,7 +187,7 @@ __global__ __launch_bounds__(256, 2) void conv_kernel(ConvGeom g) {
       csq += __shfl_xor(csq, 16, 64);
       csq += __shfl_xor(csq, 32, 64);
       if ((lane >> 4) == 0 && col < g.Ncols) {
-        float* slab = g.stats + (long)ty * g.Ncols * 2;  // this row tile's own stats row (2 waves add)
+        float* slab = g.stats + (long)ty * g.Ncols * 2;  // this row tile's own stats row (exactly 2 adds onto 0: order-free)
         atomicAdd(slab + 2 * col, csum);
         atomicAdd(slab + 2 * col + 1, csq);
       }
@@ -1243,7 +1243,7 @@ __device__ __forceinline__ void stem_bn_coef(int c, const float* ms, const float
 }
 
 // BN backward reduction: g = dy * (mask > 0) (mask = the ReLU output, or null), xhat from x and ms:
-//   red[c] = (sum g, sum g*xhat)   (fp32 atomics, red pre-zeroed).  C <= 512, C % 8 == 0.
+//   red[c] = (sum g, sum g*xhat), one partial row per block folded in block order.  C <= 512, C % 8 == 0.
 // BNMASK: no mask tensor; the ReLU mask is recomputed as bf16(relu(x*scale + shift)) > 0 from (ms, mgamma,
 // mbeta) -- the fused stem, whose activation is never stored.
 template <bool BNMASK>

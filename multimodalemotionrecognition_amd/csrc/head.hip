@@ -15,7 +15,8 @@
 // axis and alignment allow, VEC), the next chunk's loads are in flight while the current chunk is
 // multiplied out of the other LDS buffer (one barrier per chunk).  LDS images are k-major [k][m|n]
 // (+4 pad), so an MFMA operand read is 16 consecutive floats per k row.
-// splitk > 1: each K slice atomically adds into C (caller pre-initialises C; act must be 0).
+// splitk > 1: each K slice stores its partial into the workspace [batch][splitk][M][N] and a fold kernel
+// adds the slices into C in slice order (deterministic; caller pre-initialises C; act must be 0).
 // ---------------------------------------------------------------------------------------
 constexpr int GF_BK = 32, GF_LD = 64 + 4;
 
@@ -61,7 +62,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(int M, int N, int K, cons
                                                        long sak, long bsa, const TB* __restrict__ B, long sbk,
                                                        long sbn, long bsb, float* __restrict__ C, long ldc,
                                                        long bsc, const float* __restrict__ bias, int beta,
-                                                       int act, int splitk) {
+                                                       int act, int splitk, float* __restrict__ ws) {
   __shared__ float As[2][GF_BK][GF_LD];
   __shared__ float Bs[2][GF_BK][GF_LD];
   const int bz = blockIdx.z, batch = bz / splitk, ks = bz % splitk;
@@ -142,8 +143,8 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(int M, int N, int K, cons
           float v = acc[i][j][r];
           if (bias && ks == 0) v += bias[col];
           float* cp = C + (long)row * ldc + col;
-          if (splitk > 1) {
-            atomicAdd(cp, v);
+          if (splitk > 1) {  // this K slice's own partial (summed in slice order by gemm_splitk_fold_kernel)
+            ws[((long)bz * M + row) * N + col] = v;
           } else {
             if (beta) v += *cp;
             *cp = apply_act(v, act);
@@ -160,10 +161,25 @@ static bool vec_ok(const void* p, long s1, long s2) {
   return (((uintptr_t)p) & 15) == 0 && s1 % al == 0 && s2 % al == 0;
 }
 
+// C[b][m][n] += sum_{ks < splitk} ws[b][ks][m][n], slices in order
+__global__ __launch_bounds__(256) void gemm_splitk_fold_kernel(int M, int N, int splitk, int batch,
+                                                               const float* __restrict__ ws, float* __restrict__ C,
+                                                               long ldc, long bsc) {
+  const long total = (long)batch * M * N;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    const long b = e / ((long)M * N), mn = e - b * M * N;
+    const int m = (int)(mn / N), n = (int)(mn - (long)m * N);
+    const float* p = ws + (b * splitk) * M * N + mn;
+    float acc = 0.f;
+    for (int k = 0; k < splitk; ++k) acc += p[(long)k * M * N];
+    C[b * bsc + (long)m * ldc + n] += acc;
+  }
+}
+
 template <typename TA, typename TB>
 static int launch_gemm_f32(int M, int N, int K, const void* A, long sam, long sak, long bsa, const void* B, long sbk,
                            long sbn, long bsb, float* C, long ldc, long bsc, const float* bias, int beta, int act,
-                           int splitk, int batch, hipStream_t st) {
+                           int splitk, int batch, float* ws, hipStream_t st) {
   dim3 grid((N + 63) / 64, (M + 63) / 64, batch * splitk);
   const bool akc = (sak == 1), bnc = (sbn == 1);
   // the unit stride of each operand and its other strides must suit 16-byte loads
@@ -172,37 +188,42 @@ static int launch_gemm_f32(int M, int N, int K, const void* A, long sam, long sa
   const bool vec = va && vb;
 #define L(AK, BN, V)                                                                                                     \
   hipLaunchKernelGGL((gemm_f32_kernel<TA, TB, AK, BN, V>), grid, dim3(256), 0, st, M, N, K, (const TA*)A, sam, sak, \
-                     bsa, (const TB*)B, sbk, sbn, bsb, C, ldc, bsc, bias, beta, act, splitk)
+                     bsa, (const TB*)B, sbk, sbn, bsb, C, ldc, bsc, bias, beta, act, splitk, ws)
   if (vec) {
     if (akc && bnc) L(true, true, true); else if (akc) L(true, false, true); else if (bnc) L(false, true, true); else L(false, false, true);
   } else {
     if (akc && bnc) L(true, true, false); else if (akc) L(true, false, false); else if (bnc) L(false, true, false); else L(false, false, false);
   }
 #undef L
+  if (splitk > 1) {
+    const long total = (long)batch * M * N;
+    const int grid = (int)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
+    hipLaunchKernelGGL(gemm_splitk_fold_kernel, dim3(grid), dim3(256), 0, st, M, N, splitk, batch, ws, C, ldc, bsc);
+  }
   MER_LAUNCH_CHECK();
 }
 
 MER_API int mer_gemm_f32(int M, int N, int K, const void* A, int a_dtype, long sam, long sak, long bsa, const void* B,
                          int b_dtype, long sbk, long sbn, long bsb, float* C, long ldc, long bsc, const float* bias,
-                         int beta, int act, int splitk, int batch, void* stream) {
+                         int beta, int act, int splitk, int batch, float* workspace, void* stream) {
   if (M <= 0 || N <= 0 || batch <= 0) return 0;
   if (splitk < 1) splitk = 1;
-  if (splitk > 1 && act != MER_ACT_NONE) return (int)hipErrorInvalidValue;
+  if (splitk > 1 && (act != MER_ACT_NONE || !workspace)) return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
   if (a_dtype == MER_F32 && b_dtype == MER_F32)
-    return launch_gemm_f32<float, float>(M, N, K, A, sam, sak, bsa, B, sbk, sbn, bsb, C, ldc, bsc, bias, beta, act, splitk, batch, st);
+    return launch_gemm_f32<float, float>(M, N, K, A, sam, sak, bsa, B, sbk, sbn, bsb, C, ldc, bsc, bias, beta, act, splitk, batch, workspace, st);
   if (a_dtype == MER_BF16 && b_dtype == MER_F32)
-    return launch_gemm_f32<bf16_t, float>(M, N, K, A, sam, sak, bsa, B, sbk, sbn, bsb, C, ldc, bsc, bias, beta, act, splitk, batch, st);
+    return launch_gemm_f32<bf16_t, float>(M, N, K, A, sam, sak, bsa, B, sbk, sbn, bsb, C, ldc, bsc, bias, beta, act, splitk, batch, workspace, st);
   if (a_dtype == MER_F32 && b_dtype == MER_BF16)
-    return launch_gemm_f32<float, bf16_t>(M, N, K, A, sam, sak, bsa, B, sbk, sbn, bsb, C, ldc, bsc, bias, beta, act, splitk, batch, st);
-  return launch_gemm_f32<bf16_t, bf16_t>(M, N, K, A, sam, sak, bsa, B, sbk, sbn, bsb, C, ldc, bsc, bias, beta, act, splitk, batch, st);
+    return launch_gemm_f32<float, bf16_t>(M, N, K, A, sam, sak, bsa, B, sbk, sbn, bsb, C, ldc, bsc, bias, beta, act, splitk, batch, workspace, st);
+  return launch_gemm_f32<bf16_t, bf16_t>(M, N, K, A, sam, sak, bsa, B, sbk, sbn, bsb, C, ldc, bsc, bias, beta, act, splitk, batch, workspace, st);
 }
 
 // ---------------------------------------------------------------------------------------
 // Column sum (bias gradient): out[n] (+)= sum_m X[m*ldx + n]
 // ---------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void colsum_kernel(int M, int N, const float* __restrict__ X, long ldx,
-                                                     float* __restrict__ out, int rows_per_block) {
+                                                     float* __restrict__ part, int rows_per_block) {
   __shared__ float red[4][64];
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
   const int rg = threadIdx.x >> 6;
@@ -212,20 +233,45 @@ __global__ __launch_bounds__(256) void colsum_kernel(int M, int N, const float* 
     for (int r = r0 + rg; r < r1; r += 4) s += X[(long)r * ldx + c];
   red[rg][threadIdx.x & 63] = s;
   __syncthreads();
-  if (rg == 0 && c < N) {
-    s = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
-    atomicAdd(out + c, s);
+  if (rg == 0 && c < N) part[(long)blockIdx.y * N + c] = (red[0][threadIdx.x] + red[1][threadIdx.x]) +
+                                                         (red[2][threadIdx.x] + red[3][threadIdx.x]);
+}
+
+// out0[e] (e < split) / out1[e - split] += sum_{r < rows} in[r*E + e]: fixed-order per-entry sums of
+// per-block partial rows (64 entries per block, the 4 waves split the rows and meet in LDS)
+__global__ __launch_bounds__(256) void rows_sum_add_kernel(int E, int rows, const float* __restrict__ in, int split,
+                                                           float* __restrict__ out0, float* __restrict__ out1) {
+  __shared__ float part[4][64];
+  const int el = threadIdx.x & 63, pg = threadIdx.x >> 6;
+  const int e = blockIdx.x * 64 + el;
+  float acc = 0.f;
+  if (e < E)
+    for (int r = pg; r < rows; r += 4) acc += in[(long)r * E + e];
+  part[pg][el] = acc;
+  __syncthreads();
+  if (pg == 0 && e < E) {
+    const float v = (part[0][el] + part[1][el]) + (part[2][el] + part[3][el]);
+    if (e < split) {
+      if (out0) out0[e] += v;
+    } else if (out1) {
+      out1[e - split] += v;
+    }
   }
 }
 
-MER_API int mer_colsum_f32(int M, int N, const float* X, long ldx, float* out, void* stream) {
-  if (M <= 0 || N <= 0) return 0;
-  // ~1024 blocks of 4 row-groups: short per-thread row loops (latency-bound otherwise)
+static int colsum_rows_per_block(int M, int N) {
   const int nx = (N + 63) / 64;
-  int rpb = (int)(((long)M * nx / 1024 + 3) / 4 * 4);
-  rpb = rpb < 16 ? 16 : (rpb > 256 ? 256 : rpb);
-  dim3 grid(nx, (M + rpb - 1) / rpb);
-  hipLaunchKernelGGL(colsum_kernel, grid, dim3(256), 0, (hipStream_t)stream, M, N, X, ldx, out, rpb);
+  int rpb = (int)(((long)M * nx / 1024 + 3) / 4 * 4);  // ~1024 blocks: short per-thread row loops
+  return rpb < 16 ? 16 : (rpb > 256 ? 256 : rpb);
+}
+MER_API int mer_colsum_f32(int M, int N, const float* X, long ldx, float* out, float* workspace, void* stream) {
+  if (M <= 0 || N <= 0) return 0;
+  const int rpb = colsum_rows_per_block(M, N);
+  const int ny = (M + rpb - 1) / rpb;
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(colsum_kernel, dim3((N + 63) / 64, ny), dim3(256), 0, st, M, N, X, ldx, workspace, rpb);
+  hipLaunchKernelGGL(rows_sum_add_kernel, dim3((N + 63) / 64), dim3(256), 0, st, N, ny, workspace, N, out,
+                     (float*)nullptr);
   MER_LAUNCH_CHECK();
 }
 
@@ -282,14 +328,15 @@ MER_API int mer_add_ln_fwd(int rows, int d, int rows_per_sample, const float* x,
 }
 
 // dsum = rstd*(g - mean(g) - xhat*mean(g*xhat)), g = gamma*dy; dx = dsum, dr = s_b*dsum.
-// dgamma += sum_rows dy*xhat, dbeta += sum_rows dy (block partials + one atomic per column).
+// dgamma += sum_rows dy*xhat, dbeta += sum_rows dy: each block stores its (dgamma | dbeta) partial row,
+// rows_sum_add_kernel adds the rows in block order (deterministic).
 __global__ __launch_bounds__(256) void add_ln_bwd_kernel(int rows, int d, int rows_per_sample, const float* __restrict__ dy,
                                                          const float* __restrict__ s, const float* __restrict__ mean,
                                                          const float* __restrict__ rstd, const float* __restrict__ gamma,
                                                          float dp_p, const unsigned long long* __restrict__ seed_ptr,
     unsigned long long site, float* __restrict__ dx,
-                                                         float* __restrict__ dr, float* __restrict__ dgamma,
-                                                         float* __restrict__ dbeta, int rows_per_block) {
+                                                         float* __restrict__ dr, float* __restrict__ part,
+                                                         int rows_per_block) {
   const unsigned long long seed = mer_site_seed(seed_ptr, site);
   extern __shared__ __attribute__((aligned(16))) float red[];  // [2][4][d]
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -320,23 +367,25 @@ __global__ __launch_bounds__(256) void add_ln_bwd_kernel(int rows, int d, int ro
     }
   }
   __syncthreads();
+  // this block's (dgamma | dbeta) partial row; rows_sum_add_kernel folds the rows in block order
+  float* pr = part + (long)blockIdx.x * 2 * d;
   for (int c = threadIdx.x; c < d; c += 256) {
-    const float g = red[0 * d + c] + red[1 * d + c] + red[2 * d + c] + red[3 * d + c];
-    const float bb = red[4 * d + c] + red[5 * d + c] + red[6 * d + c] + red[7 * d + c];
-    if (dgamma) atomicAdd(dgamma + c, g);
-    if (dbeta) atomicAdd(dbeta + c, bb);
+    pr[c] = red[0 * d + c] + red[1 * d + c] + red[2 * d + c] + red[3 * d + c];
+    pr[d + c] = red[4 * d + c] + red[5 * d + c] + red[6 * d + c] + red[7 * d + c];
   }
 }
 
 MER_API int mer_add_ln_bwd(int rows, int d, int rows_per_sample, const float* dy, const float* s, const float* mean,
                            const float* rstd, const float* gamma, float dp_p, const unsigned long long* seed, unsigned long long site, float* dx,
-                           float* dr, float* dgamma, float* dbeta, void* stream) {
+                           float* dr, float* dgamma, float* dbeta, float* workspace, void* stream) {
   if (rows <= 0) return 0;
   if ((size_t)8 * d * sizeof(float) > 160 * 1024) return (int)hipErrorInvalidValue;
   const int rpb = 64;
-  hipLaunchKernelGGL(add_ln_bwd_kernel, dim3((rows + rpb - 1) / rpb), dim3(256), 8 * d * sizeof(float),
-                     (hipStream_t)stream, rows, d, rows_per_sample, dy, s, mean, rstd, gamma, dp_p, seed, site, dx, dr,
-                     dgamma, dbeta, rpb);
+  const int nb = (rows + rpb - 1) / rpb;
+  hipLaunchKernelGGL(add_ln_bwd_kernel, dim3(nb), dim3(256), 8 * d * sizeof(float), (hipStream_t)stream, rows, d,
+                     rows_per_sample, dy, s, mean, rstd, gamma, dp_p, seed, site, dx, dr, workspace, rpb);
+  hipLaunchKernelGGL(rows_sum_add_kernel, dim3((2 * d + 63) / 64), dim3(256), 0, (hipStream_t)stream, 2 * d, nb,
+                     workspace, d, dgamma, dbeta);
   MER_LAUNCH_CHECK();
 }
 

@@ -96,8 +96,9 @@ def gemm(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, trans_a: bool =
         raise ValueError("bias must be contiguous [N]")
     if splitk > 1:
         splitk = max(1, min(splitk, (K + 255) // 256))
+    ws = _workspace(splitk * M * N, out.device) if splitk > 1 else None
     LIB("mer_gemm_f32", M, N, K, a.data_ptr(), _dt(a), sam, sak, 0, b.data_ptr(), _dt(b), sbk, sbn, 0,
-        out.data_ptr(), out.stride(0), 0, _ptr(bias), int(beta), ACT[act], int(splitk), 1, stream_ptr())
+        out.data_ptr(), out.stride(0), 0, _ptr(bias), int(beta), ACT[act], int(splitk), 1, _ptr(ws), stream_ptr())
     return out
 
 
@@ -116,7 +117,8 @@ def linear_fwd(x2d, w, b, out, act="none"):
 def linear_bwd(x2d, w, dy, dx=None, dw=None, db=None, dx_beta=0):
     """Given dy [M,N] for out = x W^T + b: dx (+)= dy W ; dw += dy^T x ; db += colsum(dy).
 
-    dw / db must be initialised (they are accumulated: split-K adds atomically).
+    dw / db must be initialised (they are accumulated; split-K slices and colsum partials are added in a
+    fixed order, so the result is run-to-run reproducible).
     """
     M, N = dy.shape
     K = x2d.shape[1]
@@ -128,9 +130,16 @@ def linear_bwd(x2d, w, dy, dx=None, dw=None, db=None, dx_beta=0):
         colsum(dy, db)
 
 
+def _workspace(floats, device):
+    """fp32 scratch for the fixed-order reductions; freed back to torch's stream-ordered cache on return."""
+    return torch.empty(max(1, int(floats)), device=device, dtype=torch.float32)
+
+
 def colsum(x2d, out):
     _check_dev(x2d, out)
-    LIB("mer_colsum_f32", x2d.shape[0], x2d.shape[1], x2d.data_ptr(), x2d.stride(0), out.data_ptr(), stream_ptr())
+    M, N = x2d.shape
+    ws = _workspace((M + 15) // 16 * N, out.device)  # MER_COLSUM_WS_FLOATS
+    LIB("mer_colsum_f32", M, N, x2d.data_ptr(), x2d.stride(0), out.data_ptr(), ws.data_ptr(), stream_ptr())
 
 
 def rng_ptr(rng):
@@ -174,7 +183,8 @@ def add_ln_fwd(x, r, gamma, beta, y, s_out, mean, rstd, rows_per_sample, dp_p=0.
 def add_ln_bwd(dy, s, mean, rstd, gamma, dx, dr, dgamma, dbeta, rows_per_sample, dp_p=0.0, rng=None, site=0):
     rows, d = dy.shape
     LIB("mer_add_ln_bwd", rows, d, rows_per_sample, dy.data_ptr(), s.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
-        gamma.data_ptr(), float(dp_p), rng_ptr(rng), int(site), dx.data_ptr(), _ptr(dr), _ptr(dgamma), _ptr(dbeta), stream_ptr())
+        gamma.data_ptr(), float(dp_p), rng_ptr(rng), int(site), dx.data_ptr(), _ptr(dr), _ptr(dgamma), _ptr(dbeta),
+        _workspace((rows + 63) // 64 * 2 * d, dy.device).data_ptr(), stream_ptr())  # MER_ADD_LN_WS_FLOATS
 
 
 def mean_pool_fwd(x3d, y, ldy=None):
@@ -235,7 +245,7 @@ def gemm_batched(a, b, out, *, M, N, K, sam, sak, bsa, sbk, sbn, bsb, ldc, bsc, 
     """out_z[M,N] (+)= A_z B_z over a batch of strided fp32 matrices (views into larger buffers)."""
     _check_dev(a, b, out)
     LIB("mer_gemm_f32", M, N, K, a.data_ptr(), _dt(a), sam, sak, bsa, b.data_ptr(), _dt(b), sbk, sbn, bsb,
-        out.data_ptr(), ldc, bsc, 0, int(beta), 0, 1, int(batch), stream_ptr())
+        out.data_ptr(), ldc, bsc, 0, int(beta), 0, 1, int(batch), 0, stream_ptr())
     return out
 
 

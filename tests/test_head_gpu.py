@@ -171,6 +171,10 @@ def test_gemm_f32_transposes():
     out = torch.zeros(128, 768, device="cuda")
     K.gemm(a.cuda(), x.cuda(), out, trans_a=True, beta=1, splitk=8)
     assert max_abs(out, a.t() @ x) < 5e-3
+    # the K slices are summed in slice order (no atomics): bitwise reproducible
+    out2 = torch.zeros(128, 768, device="cuda")
+    K.gemm(a.cuda(), x.cuda(), out2, trans_a=True, beta=1, splitk=8)
+    assert torch.equal(out, out2)
 
 
 def test_late_and_ce_kernels():
@@ -255,6 +259,9 @@ def test_colsum_and_layernorm_paths():
         out = torch.zeros(N, device="cuda")
         K.colsum(x.cuda(), out)
         assert max_abs(out, x.sum(0)) < 1e-3 * max(1.0, M ** 0.5)
+        out2 = torch.zeros(N, device="cuda")
+        K.colsum(x.cuda(), out2)
+        assert torch.equal(out, out2), (M, N)  # fixed-order block fold
     for rows, d in [(4768, 768), (5, 512), (33, 200), (7, 1024)]:
         x = torch.randn(rows, d) * 3 + 1
         g, b = torch.randn(d), torch.randn(d)
