@@ -226,6 +226,50 @@ int mer_weightnorm_scale(int n01, int taps, const float* v, const float* g, floa
 /* y = bf16(x), contiguous. */
 int mer_cast_bf16(long n, const float* x, void* y, void* stream);
 
+/* ============================ WavLM stage-2 fine-tuning (backward of the last N layers) ============================
+ * The reference unfreezes the last N encoder layers (wavlm_audio.py:70-88 _unfreeze_last_n_layers, called by
+ * train.py:817-822 _apply_two_stage_freeze_policy); these entry points are the backward of those layers
+ * (post-LN WavLMEncoderLayer TF:314-336, attention TF:147-186).  Deterministic: row reductions are stored as
+ * per-block partial rows and folded in a fixed order by mer_fold_rows. */
+
+/* LayerNorm backward (nn.LayerNorm(d), TF:326,329): g = dy_a (+ dy_b) (+ dy_c) (NULL addends skipped), x = the saved
+ * fp32 LN input; dx written fp32 (dx32) and/or bf16 (dx16) (either may be NULL).  part: float[ceil(rows/16)][3][d]
+ * = per-block (sum g*xhat, sum g, sum dx) -- fold with mer_fold_rows for dgamma, dbeta and the upstream bias.
+ * d % 256 == 0, d <= 1024. */
+int mer_ln_bwd(int rows, int d, const float* dy_a, const float* dy_b, const float* dy_c, const float* x,
+               const float* gamma, float eps, float* dx32, void* dx16, float* part, void* stream);
+
+/* out[k] += sum_{p < parts} part[p * ldp + k] for k < n, summed in a fixed order. */
+int mer_fold_rows(int parts, int n, const float* part, long ldp, float* out, void* stream);
+
+/* part[p][c] = sum of rows [64p, 64p+64) of x[:, c] (x_dtype 0 fp32 / 1 bf16): part is float[ceil(rows/64)][cols]. */
+int mer_colpart(int rows, int cols, const void* x, int x_dtype, long ldx, float* part, void* stream);
+
+/* f = gelu(z) elementwise, bf16 -> bf16, n % 8 == 0 (the FFN activation of a trainable layer, TF:286-296). */
+int mer_gelu_bf16(long n, const void* z, void* f, void* stream);
+
+/* dz = df * gelu'(z) -> bf16 [rows][cols]; part float[ceil(rows/64)][cols] column partial sums of dz (bias grad). */
+int mer_gelu_bwd(int rows, int cols, const float* df, const void* z, void* dz, float* part, void* stream);
+
+/* Linear weight gradient dw[n][k] += sum_m dy[m][n] x[m][k] (bf16 operands, fp32 dw), x [M][K] contiguous, dy rows
+ * of stride ldy (a column slice of a wider gradient works); bf16 MFMA (the 1x1 case of mer_conv_wgrad).
+ * workspace: splits * N * K floats.  K, N, ldy multiples of 8. */
+int mer_linear_wgrad(int M, int N, int K, const void* x, const void* dy, long ldy, float* dw, int splits,
+                     float* workspace, void* stream);
+
+/* Backward of mer_wavlm_attention (tbl form: per-head bias table [H][2L-1]), L <= 192.  dout fp32 [B*L][>=H*64]
+ * (gradient of the attention output; fp32 because dp_ij - sum_j p_ij dp_ij cancels for peaked rows), qkv / x as in the forward.  Writes dqkv bf16 [B*L][3*H*64] (dq | dk | dv),
+ * dx_gate fp32 (the gate path's gradient of the layer input x; may be NULL), P and dS scratch float[B*H][L][L],
+ * gate_part float[B*H*ceil(L/16)][8*64 + 8 + H] per-block partials of (d gru_rel_pos_linear.weight [8][64],
+ * .bias [8], d gru_rel_pos_const [H]) -- fold with mer_fold_rows. */
+int mer_wavlm_attention_bwd(int B, int L, int H, const void* qkv, long ldqkv, const void* x, long ldx,
+                            const void* dout, long ldo, const float* gate_w, const float* gate_b,
+                            const float* gate_const, const float* tbl, float scale, float* P, float* dS,
+                            void* dqkv, long lddq, float* dx_gate, long lddxg, float* gate_part, void* stream);
+
+/* dst[c][r] = src[r][c], bf16 (the transposed weight operands of the stage-2 data-gradient GEMMs). */
+int mer_transpose_bf16(int rows, int cols, const void* src, long lds, void* dst, long ldd, void* stream);
+
 /* ============================ ResNet18 frame trunk (bf16 MFMA, NHWC) ============================
  * VideoNet.backbone (video.py:21-23 -> torchvision resnet18 children[:-1]).  Activations are NHWC bf16
  * with channels padded to a multiple of 8. */

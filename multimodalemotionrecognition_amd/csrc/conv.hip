@@ -210,6 +210,7 @@ struct WgradGeom {
   const bf16_t* dY;
   float* ws;              // [splits][K][R*S*C] fp32 partial slabs
   int pix_per_split;
+  long ldy;               // dY row stride (elements; K for a conv, a column slice of a wider matrix for a Linear)
 };
 
 template <int BM_, int BN_, int WM = 2, int WN = 2>
@@ -247,7 +248,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void wgrad_kernel(WgradGeom g) {
 #pragma unroll
     for (int i = 0; i < ACH; ++i) {
       const int p = p0 + a_pr0 + i * (NT / ACPR), k = m0 + a_cc * 8;
-      ra[i] = (p < p_end && k < g.K) ? *reinterpret_cast<const u32x4*>(g.dY + (long)p * g.K + k) : u32x4{0u, 0u, 0u, 0u};
+      ra[i] = (p < p_end && k < g.K) ? *reinterpret_cast<const u32x4*>(g.dY + (long)p * g.ldy + k) : u32x4{0u, 0u, 0u, 0u};
     }
 #pragma unroll
     for (int i = 0; i < BCH; ++i) {
@@ -879,9 +880,9 @@ MER_API int mer_conv_wgrad(int N, int H, int W, int C, int Creal, int K, int R, 
   return mer_conv_wgrad_ex(N, H, W, C, Creal, K, R, S, stride, pad, x, dy, dw, splits, workspace, -1, stream);
 }
 
-MER_API int mer_conv_wgrad_ex(int N, int H, int W, int C, int Creal, int K, int R, int S, int stride, int pad,
-                              const void* x, const void* dy, float* dw, int splits, float* workspace, int variant,
-                              void* stream) {
+static int conv_wgrad_impl(int N, int H, int W, int C, int Creal, int K, int R, int S, int stride, int pad,
+                           const void* x, const void* dy, long ldy, float* dw, int splits, float* workspace,
+                           int variant, void* stream) {
   if (C % 8 || K % 8 || variant < -1 || variant > 2 || R * S > 49) return (int)hipErrorInvalidValue;
   if (variant == -1) variant = 2;
   WgradGeom g{};
@@ -889,6 +890,7 @@ MER_API int mer_conv_wgrad_ex(int N, int H, int W, int C, int Creal, int K, int 
   g.Ho = (H + 2 * pad - R) / stride + 1; g.Wo = (W + 2 * pad - S) / stride + 1; g.K = K;
   g.R = R; g.S = S; g.st = stride; g.pad = pad;
   g.X = (const bf16_t*)x; g.dY = (const bf16_t*)dy; g.ws = workspace;
+  g.ldy = ldy > 0 ? ldy : K;
   const int P = N * g.Ho * g.Wo;
   if (splits < 1) splits = 1;
   g.pix_per_split = ((P + splits - 1) / splits + 63) / 64 * 64;
@@ -917,6 +919,19 @@ MER_API int mer_conv_wgrad_ex(int N, int H, int W, int C, int Creal, int K, int 
   }
   hipLaunchKernelGGL(wgrad_scatter_kernel, dim3((Creal + 31) / 32, K), dim3(256), 0, st, C, Creal, R * S, workspace, dw);
   MER_LAUNCH_CHECK();
+}
+
+MER_API int mer_conv_wgrad_ex(int N, int H, int W, int C, int Creal, int K, int R, int S, int stride, int pad,
+                              const void* x, const void* dy, float* dw, int splits, float* workspace, int variant,
+                              void* stream) {
+  return conv_wgrad_impl(N, H, W, C, Creal, K, R, S, stride, pad, x, dy, K, dw, splits, workspace, variant, stream);
+}
+
+// Linear weight gradient as a 1x1 convolution over M "pixels": dw[n][k] += sum_m dy[m][n] x[m][k].
+MER_API int mer_linear_wgrad(int M, int N, int K, const void* x, const void* dy, long ldy, float* dw, int splits,
+                             float* workspace, void* stream) {
+  if (ldy < N || ldy % 8) return (int)hipErrorInvalidValue;
+  return conv_wgrad_impl(1, 1, M, K, K, N, 1, 1, 1, 0, x, dy, ldy, dw, splits, workspace, -1, stream);
 }
 
 // ---------------------------------------------------------------------------------------

@@ -601,3 +601,110 @@ def gemm_i8dyn(x2d, x_qparams, qw, w_qparams, colsum, bias, out, act="none"):
             qw.data_ptr(), qw.stride(0), w_qparams.data_ptr(), colsum.data_ptr(), _ptr(bias), ACT[act], out.data_ptr(),
             out.stride(0), stream_ptr())
     return out
+
+
+# ---------------------------------------------------------------------------------------------------
+# WavLM stage-2 fine-tuning (backward of the unfrozen last layers, csrc/wavlm_train.hip)
+def _ptr0(t):
+    return 0 if t is None else t.data_ptr()
+
+
+def fold_rows(part, parts, n, ldp, out, offset=0):
+    """out[k] += sum_p part[offset + p*ldp + k] (fixed order)."""
+    if out.dtype != torch.float32 or not out.is_contiguous() or out.numel() != n:
+        raise ValueError("fold_rows: out must be contiguous fp32 of n elements")
+    if offset + (parts - 1) * ldp + n > part.numel():
+        raise ValueError("fold_rows: partial rows out of range")
+    LIB("mer_fold_rows", int(parts), int(n), part.data_ptr() + 4 * offset, int(ldp), out.data_ptr(), stream_ptr())
+
+
+def ln_bwd(dy_a, x, gamma, eps, dy_b=None, dy_c=None, dx32=None, dx16=None):
+    """LayerNorm backward on rows of x (fp32 pre-LN input).  Returns the partial-row buffer
+    [ceil(rows/16)][3][d] (dgamma | dbeta | sum dx) for fold_rows."""
+    rows, d = x.shape
+    for t in (dy_a, dy_b, dy_c, dx32):
+        if t is not None and (t.dtype != torch.float32 or tuple(t.shape) != (rows, d) or not t.is_contiguous()):
+            raise ValueError("ln_bwd: fp32 [rows, d] contiguous operands expected")
+    if dx16 is not None and (dx16.dtype != torch.bfloat16 or tuple(dx16.shape) != (rows, d)):
+        raise ValueError("ln_bwd: dx16 must be bf16 [rows, d]")
+    if x.dtype != torch.float32 or not x.is_contiguous() or d % 256 or d > 1024:
+        raise ValueError("ln_bwd: x must be contiguous fp32 with d % 256 == 0, d <= 1024")
+    part = _workspace(((rows + 15) // 16) * 3 * d, x.device)
+    LIB("mer_ln_bwd", rows, d, dy_a.data_ptr(), _ptr0(dy_b), _ptr0(dy_c), x.data_ptr(), gamma.data_ptr(), float(eps),
+        _ptr0(dx32), _ptr0(dx16), part.data_ptr(), stream_ptr())
+    return part
+
+
+def ln_bwd_fold(part, rows, d, dgamma=None, dbeta=None, dbias=None):
+    parts = (rows + 15) // 16
+    for i, out in enumerate((dgamma, dbeta, dbias)):
+        if out is not None:
+            fold_rows(part, parts, d, 3 * d, out, offset=i * d)
+
+
+def colsum_into(x2d, out, col0=0, ncols=None):
+    """out += colsum(x2d[:, col0:col0+ncols]) (deterministic, fixed order)."""
+    rows, cols = x2d.shape
+    part = _workspace(((rows + 63) // 64) * cols, x2d.device)
+    LIB("mer_colpart", rows, cols, x2d.data_ptr(), _dt(x2d), x2d.stride(0), part.data_ptr(), stream_ptr())
+    ncols = cols - col0 if ncols is None else ncols
+    fold_rows(part, (rows + 63) // 64, ncols, cols, out, offset=col0)
+
+
+def gelu_bf16(z, f):
+    if z.dtype != torch.bfloat16 or f.dtype != torch.bfloat16 or z.numel() != f.numel() or z.numel() % 8:
+        raise ValueError("gelu_bf16: bf16 operands of equal size (multiple of 8)")
+    LIB("mer_gelu_bf16", z.numel(), z.data_ptr(), f.data_ptr(), stream_ptr())
+
+
+def gelu_bwd(df, z, dz, dbias):
+    """dz = df * gelu'(z) (bf16); dbias += colsum(dz)."""
+    rows, cols = z.shape
+    if df.dtype != torch.float32 or tuple(df.shape) != (rows, cols) or dz.dtype != torch.bfloat16:
+        raise ValueError("gelu_bwd shapes")
+    part = _workspace(((rows + 63) // 64) * cols, z.device)
+    LIB("mer_gelu_bwd", rows, cols, df.data_ptr(), z.data_ptr(), dz.data_ptr(), part.data_ptr(), stream_ptr())
+    fold_rows(part, (rows + 63) // 64, cols, cols, dbias)
+
+
+def linear_wgrad(x, dy, dw, col0=0):
+    """dw[N,K] += dy[:, col0:col0+N]^T x (bf16 MFMA); x bf16 [M,K] contiguous, dy bf16 [M, >= col0+N]."""
+    M, Kin = x.shape
+    N = dw.shape[0]
+    if (x.dtype != torch.bfloat16 or dy.dtype != torch.bfloat16 or dw.dtype != torch.float32 or not x.is_contiguous()
+            or tuple(dw.shape) != (N, Kin) or dy.shape[0] != M or dy.shape[1] < col0 + N or dy.stride(1) != 1
+            or Kin % 8 or N % 8 or col0 % 8 or dy.stride(0) % 8):
+        raise ValueError("linear_wgrad shapes")
+    tiles = ((N + 127) // 128) * ((Kin + 127) // 128)
+    splits = int(max(1, min(-(-512 // tiles), M // 512)))
+    ws = _workspace(splits * N * Kin, x.device)
+    LIB("mer_linear_wgrad", M, N, Kin, x.data_ptr(), dy.data_ptr() + 2 * col0, dy.stride(0), dw.data_ptr(), splits,
+        ws.data_ptr(), stream_ptr())
+
+
+def wavlm_attention_bwd(qkv, x, dout, gate_w, gate_b, gate_const, tbl, B, L, H, scale, dqkv, dx_gate=None):
+    """Backward of wavlm_attention (per-head table form).  Returns the gate partial rows
+    [B*H*ceil(L/16)][8*64 + 8 + H] for fold_rows."""
+    M = B * L
+    if L > 192 or tuple(qkv.shape) != (M, 3 * H * 64) or tuple(dqkv.shape) != (M, 3 * H * 64) or dout.shape[0] != M:
+        raise ValueError("wavlm_attention_bwd shapes")
+    if qkv.dtype != torch.bfloat16 or dout.dtype != torch.float32 or dqkv.dtype != torch.bfloat16:
+        raise ValueError("wavlm_attention_bwd expects bf16 qkv / dqkv and fp32 dout")
+    if tuple(tbl.shape) != (H, 2 * L - 1) or tbl.dtype != torch.float32:
+        raise ValueError("wavlm_attention_bwd: bias table [H, 2L-1] fp32")
+    P = torch.empty(B * H * L * L, device=qkv.device, dtype=torch.float32)
+    dS = torch.empty_like(P)
+    nrb = (L + 15) // 16
+    gpart = _workspace(B * H * nrb * (8 * 64 + 8 + H), qkv.device)
+    LIB("mer_wavlm_attention_bwd", B, L, H, qkv.data_ptr(), qkv.stride(0), x.data_ptr(), x.stride(0), dout.data_ptr(),
+        dout.stride(0), gate_w.data_ptr(), gate_b.data_ptr(), gate_const.data_ptr(), tbl.data_ptr(), float(scale),
+        P.data_ptr(), dS.data_ptr(), dqkv.data_ptr(), dqkv.stride(0), _ptr0(dx_gate),
+        dx_gate.stride(0) if dx_gate is not None else 0, gpart.data_ptr(), stream_ptr())
+    return gpart, B * H * nrb
+
+
+def transpose_bf16(src, dst):
+    rows, cols = src.shape
+    if src.dtype != torch.bfloat16 or dst.dtype != torch.bfloat16 or tuple(dst.shape) != (cols, rows):
+        raise ValueError("transpose_bf16 shapes")
+    LIB("mer_transpose_bf16", rows, cols, src.data_ptr(), src.stride(0), dst.data_ptr(), dst.stride(0), stream_ptr())

@@ -70,6 +70,76 @@ def build_optimizer(model: nn.Module, lr: float = 1e-3, weight_decay: float = 1e
     return FusedAdam(params, lr=lr, weight_decay=weight_decay)
 
 
+
+def _set_module_trainable(module: nn.Module, trainable: bool) -> None:
+    for param in module.parameters():
+        param.requires_grad = trainable
+
+
+def set_video_backbone_trainable(video_model: nn.Module, unfreeze_blocks: int) -> None:
+    """train.py:777-796: freeze the video branch, then unfreeze its last ``unfreeze_blocks`` parameterised
+    backbone children (and its classifier)."""
+    _set_module_trainable(video_model, False)
+    if unfreeze_blocks <= 0:
+        return
+    backbone = getattr(video_model, "backbone", None)
+    if not isinstance(backbone, nn.Sequential):
+        _set_module_trainable(video_model, True)
+        return
+    parameterized = [m for m in backbone if len(list(m.parameters())) > 0]
+    for m in parameterized[-unfreeze_blocks:]:
+        _set_module_trainable(m, True)
+    if hasattr(video_model, "classifier"):
+        _set_module_trainable(video_model.classifier, True)
+
+
+def apply_two_stage_freeze_policy(model: FusionModel, stage: int, unfreeze_wavlm_layers: int = 2,
+                                  unfreeze_video_blocks: int = 1, unfreeze_audio: bool = True) -> None:
+    """train.py:798-829 (defaults of --fusion_unfreeze_wavlm_layers / _video_blocks / _audio, train.py:629-648).
+    Stage 1: fusion head only.  Stage 2: + the last WavLM layers (their backward runs on
+    csrc/wavlm_train.hip) + the last video backbone blocks."""
+    for name, param in model.named_parameters():
+        if not name.startswith(("audio_model.", "video_model.")):
+            param.requires_grad = True
+    if stage == 1:
+        _set_module_trainable(model.audio_model, False)
+        _set_module_trainable(model.video_model, False)
+        return
+    if stage != 2:
+        raise ValueError(f"Unsupported stage for two-stage training: {stage}")
+    audio_model = model.audio_model
+    if isinstance(audio_model, WavLMAudioEncoder):
+        _set_module_trainable(audio_model, False)
+        _set_module_trainable(audio_model.classifier, True)
+        audio_model.unfreeze_backbone(max(0, int(unfreeze_wavlm_layers)))
+    else:
+        _set_module_trainable(audio_model, bool(unfreeze_audio))
+    set_video_backbone_trainable(model.video_model, max(0, int(unfreeze_video_blocks)))
+
+
+def build_fusion_stage_optimizer(model: nn.Module, stage: int, lr: float = 1e-3, audio_backbone_lr: float = 1e-5,
+                                 video_backbone_lr: float = 1e-5, weight_decay: float = 1e-4) -> FusedAdam:
+    """train.py:831-872: param groups fusion@lr, audio@audio_backbone_lr, video@video_backbone_lr."""
+    fusion, audio, video = [], [], []
+    for name, param in model.named_parameters():
+        if not param.requires_grad:
+            continue
+        (audio if name.startswith("audio_model.") else video if name.startswith("video_model.") else fusion).append(param)
+    groups = []
+    if stage == 1:
+        if not fusion:
+            raise RuntimeError("Stage-1 expects fusion parameters, but none are trainable.")
+        groups.append({"params": fusion, "lr": lr})
+    elif stage == 2:
+        for ps, glr in ((fusion, lr), (audio, audio_backbone_lr), (video, video_backbone_lr)):
+            if ps:
+                groups.append({"params": ps, "lr": glr})
+        if not groups:
+            raise RuntimeError("Stage-2 expects trainable parameters, but none are trainable.")
+    else:
+        raise ValueError(f"Unsupported optimizer stage: {stage}")
+    return FusedAdam(groups, lr=lr, weight_decay=weight_decay)
+
 def make_loss(fusion_mode: str, label_smoothing: float = 0.0) -> nn.Module:
     """train.py:1030-1033."""
     return LateNLLLoss() if fusion_mode == "late" else CrossEntropyLoss(label_smoothing=label_smoothing)

@@ -12,7 +12,9 @@ fp32 accumulation:
   -> LayerNorm(512) -> projection GEMM -> grouped pos-conv GEMM (+GELU +residual) -> LayerNorm
   -> 12 x [fused QKV GEMM -> gated-rel-pos attention -> out-proj GEMM (+residual) -> LN
            -> FFN GEMM (+GELU) -> FFN GEMM (+residual) -> LN]
-Frozen by default (no backward); stage-2 fine-tuning of the last layers is a later build row.
+Frozen by default (no backward).  Stage 2 (``unfreeze_backbone(n)``, wavlm_audio.py:70-88) runs the frozen
+prefix as above and the last n layers as one autograd node (``forward_train`` / ``tail_backward``,
+csrc/wavlm_train.hip), eval semantics (no dropout / LayerDrop).
 """
 from __future__ import annotations
 
@@ -154,6 +156,11 @@ class WavLMBackbone(nn.Module):
     def _weights_key(self):
         return tuple(weight_version(q) for q in self._param_list())
 
+    def _prefix_param_count(self, first_layer: int) -> int:
+        """Number of entries of _param_list() (module order) before encoder layer ``first_layer``."""
+        first = next(iter(self.encoder.layers[first_layer].parameters()))
+        return next(i for i, q in enumerate(self._param_list()) if q is first)
+
     def trainable(self) -> bool:
         return any(q.requires_grad for q in self._param_list())
 
@@ -162,6 +169,11 @@ class WavLMBackbone(nn.Module):
         key = self._weights_key()
         if self._packed is not None and self._packed_key == key:
             return self._packed
+        limit = self.__dict__.get("_pack_limit")  # stage-2 prefix call: only layers < limit are used
+        if limit is not None and self._packed is not None:
+            n = self._prefix_param_count(limit)
+            if self._packed_key[:n] == key[:n]:
+                return self._packed
         dev = self.masked_spec_embed.device
         cfg = self.config
         pk = {"conv": []}
@@ -329,6 +341,195 @@ class WavLMBackbone(nn.Module):
         return x.view(B, L, D)
 
 
+    # ---- stage-2 fine-tuning: backward through the unfrozen last layers ----
+    def first_trainable_layer(self) -> int:
+        """Index of the first encoder layer with trainable parameters.  Only a suffix of whole encoder layers
+        may train (what ``_unfreeze_last_n_layers`` produces, wavlm_audio.py:70-88); layer 0 owns the shared
+        relative-position embedding and the feature extractor / projection / pos-conv stay frozen."""
+        layers = self.encoder.layers
+        first = next((i for i, l in enumerate(layers) if any(q.requires_grad for q in l.parameters())), None)
+        if first is None:
+            raise RuntimeError("no trainable WavLM layer")
+        outside = [n for n, q in self.named_parameters() if q.requires_grad and not n.startswith("encoder.layers.")]
+        if first == 0 or outside or not all(all(q.requires_grad for q in l.parameters()) for l in layers[first:]):
+            raise NotImplementedError("WavLM fine-tuning supports unfreezing whole last layers 1..11 "
+                                      "(unfreeze_backbone(n), n <= 11); got a different trainable set")
+        return first
+
+    def forward_train(self, wav: torch.Tensor) -> torch.Tensor:
+        """Stage-2 forward: frozen conv stack + layers [0, first) on the inference schedule, then layers
+        [first, 12) saving their activations.  Returns fp32 [B, L, 768] tracked by autograd."""
+        if not wav.is_cuda:
+            raise RuntimeError("WavLM runs on the MI355X kernels; move the waveform to the GPU")
+        first = self.first_trainable_layer()
+        self.__dict__["_pack_limit"] = first  # the trainable layers' stale packs are not re-cast every step
+        try:
+            with torch.no_grad():
+                x = self.forward_hip(wav.contiguous().float(), out_dtype=torch.bfloat16, num_layers=first)
+            tbl = self.packed_weights()["bias_tables"][x.shape[1]]
+        finally:
+            self.__dict__["_pack_limit"] = None
+        names, params = [], []
+        for li in range(first, len(self.encoder.layers)):
+            for n, q in self.encoder.layers[li].named_parameters():
+                names.append((li, n))
+                params.append(q)
+        return _WavLMTailFn.apply(x, tbl, self, first, tuple(names), *params)
+
+    def tail_forward(self, x, tbl, first):
+        """Layers [first, 12) on bf16 x [B, L, D]; returns (fp32 output [B*L, D], saved activations)."""
+        cfg = self.config
+        B, L, D = x.shape
+        H = cfg.num_attention_heads
+        M = B * L
+        dev = x.device
+        bf = torch.bfloat16
+        scale = (D // H) ** -0.5
+        nl = len(self.encoder.layers)
+        h = x.reshape(M, D)
+        saved = []
+        for li in range(first, nl):
+            layer = self.encoder.layers[li]
+            at = layer.attention
+            lw = _pack_layer(layer, dev)
+            sv = dict(x=h, pack=lw)
+            qkv = torch.empty(M, 3 * D, device=dev, dtype=bf)
+            K.gemm_bf16(h, lw["qkv_w"], qkv, bias=lw["qkv_b"])
+            att = torch.empty(M, D, device=dev, dtype=bf)
+            K.wavlm_attention(qkv, h, at.gru_rel_pos_linear.weight, at.gru_rel_pos_linear.bias, lw["gate_c"], tbl, None,
+                              att, B, L, H, scale)
+            y1 = torch.empty(M, D, device=dev, dtype=torch.float32)
+            K.gemm_bf16(att, lw["out_w"], y1, bias=at.out_proj.bias, residual=h)
+            x1 = torch.empty(M, D, device=dev, dtype=bf)
+            K.layernorm(y1, layer.layer_norm.weight, layer.layer_norm.bias, x1, eps=cfg.layer_norm_eps)
+            z = torch.empty(M, cfg.intermediate_size, device=dev, dtype=bf)
+            K.gemm_bf16(x1, lw["ff1_w"], z, bias=layer.feed_forward.intermediate_dense.bias)
+            f = torch.empty_like(z)
+            K.gelu_bf16(z, f)
+            y2 = torch.empty(M, D, device=dev, dtype=torch.float32)
+            K.gemm_bf16(f, lw["ff2_w"], y2, bias=layer.feed_forward.output_dense.bias, residual=x1)
+            last = li == nl - 1
+            out = torch.empty(M, D, device=dev, dtype=torch.float32 if last else bf)
+            K.layernorm(y2, layer.final_layer_norm.weight, layer.final_layer_norm.bias, out, eps=cfg.layer_norm_eps)
+            sv.update(qkv=qkv, att=att, y1=y1, x1=x1, z=z, f=f, y2=y2)
+            saved.append(sv)
+            h = out
+        return h, saved
+
+    def tail_backward(self, dout, saved, tbl, first, B, L, grads):
+        """Backward of tail_forward given dout fp32 [B*L, D]; accumulates into ``grads`` {param: buffer}."""
+        cfg = self.config
+        D, H, FF = cfg.hidden_size, cfg.num_attention_heads, cfg.intermediate_size
+        M = B * L
+        dev = dout.device
+        bf, f32 = torch.bfloat16, torch.float32
+        eps = cfg.layer_norm_eps
+        scale = (D // H) ** -0.5
+        addends = (dout.reshape(M, D).contiguous(), None, None)
+        for k in range(len(saved) - 1, -1, -1):
+            li = first + k
+            sv, layer = saved[k], self.encoder.layers[li]
+            at, ff = layer.attention, layer.feed_forward
+            lw = sv["pack"]
+            g = grads
+            # final LayerNorm; its sum-of-dx partials are the FFN output bias gradient (residual: dy2 -> x1 too)
+            dy2, dy2h = torch.empty(M, D, device=dev, dtype=f32), torch.empty(M, D, device=dev, dtype=bf)
+            part = K.ln_bwd(addends[0], sv["y2"], layer.final_layer_norm.weight, eps, dy_b=addends[1],
+                            dy_c=addends[2], dx32=dy2, dx16=dy2h)
+            K.ln_bwd_fold(part, M, D, g[layer.final_layer_norm.weight], g[layer.final_layer_norm.bias],
+                          g[ff.output_dense.bias])
+            K.linear_wgrad(sv["f"], dy2h, g[ff.output_dense.weight])
+            df = torch.empty(M, FF, device=dev, dtype=f32)
+            K.gemm_bf16(dy2h, _transposed(lw, "ff2_w", dev), df)
+            dz = torch.empty(M, FF, device=dev, dtype=bf)
+            K.gelu_bwd(df, sv["z"], dz, g[ff.intermediate_dense.bias])
+            K.linear_wgrad(sv["x1"], dz, g[ff.intermediate_dense.weight])
+            dx1 = torch.empty(M, D, device=dev, dtype=f32)
+            K.gemm_bf16(dz, _transposed(lw, "ff1_w", dev), dx1)
+            # attention LayerNorm (input y1 = x + out_proj(att)); residual gradient dy2 joins here
+            dy1, dy1h = torch.empty(M, D, device=dev, dtype=f32), torch.empty(M, D, device=dev, dtype=bf)
+            part = K.ln_bwd(dx1, sv["y1"], layer.layer_norm.weight, eps, dy_b=dy2, dx32=dy1, dx16=dy1h)
+            K.ln_bwd_fold(part, M, D, g[layer.layer_norm.weight], g[layer.layer_norm.bias], g[at.out_proj.bias])
+            K.linear_wgrad(sv["att"], dy1h, g[at.out_proj.weight])
+            # gradient of the attention output in fp32 from fp32 operands (exact-f32 MFMA GEMM): the softmax
+            # backward's dp_ij - sum_j p_ij dp_ij cancels for peaked rows, so bf16 operands here would cost
+            # the score-path gradients (q/k/gate) ~10% (tests/test_wavlm_stage2_gpu.py)
+            datt = torch.empty(M, D, device=dev, dtype=f32)
+            if _DATT_F32:
+                K.gemm(dy1, at.out_proj.weight.detach(), datt)
+            else:
+                K.gemm_bf16(dy1h, _transposed(lw, "out_w", dev), datt)
+            need_dx = k > 0
+            dqkv = torch.empty(M, 3 * D, device=dev, dtype=bf)
+            dxg = torch.empty(M, D, device=dev, dtype=f32) if need_dx else None
+            gpart, nparts = K.wavlm_attention_bwd(sv["qkv"], sv["x"], datt, at.gru_rel_pos_linear.weight,
+                                                  at.gru_rel_pos_linear.bias, lw["gate_c"], tbl, B, L, H, scale,
+                                                  dqkv, dxg)
+            ldp = 8 * 64 + 8 + H
+            K.fold_rows(gpart, nparts, 8 * 64, ldp, g[at.gru_rel_pos_linear.weight], offset=0)
+            K.fold_rows(gpart, nparts, 8, ldp, g[at.gru_rel_pos_linear.bias], offset=8 * 64)
+            K.fold_rows(gpart, nparts, H, ldp, g[at.gru_rel_pos_const], offset=8 * 64 + 8)
+            cpart = K._workspace(((M + 63) // 64) * 3 * D, dev)
+            K.LIB("mer_colpart", M, 3 * D, dqkv.data_ptr(), K.BF16, dqkv.stride(0), cpart.data_ptr(), K.stream_ptr())
+            for j, lin in enumerate((at.q_proj, at.k_proj, at.v_proj)):
+                K.linear_wgrad(sv["x"], dqkv, g[lin.weight], col0=j * D)
+                K.fold_rows(cpart, (M + 63) // 64, D, 3 * D, g[lin.bias], offset=j * D)
+            if need_dx:
+                dxq = torch.empty(M, D, device=dev, dtype=f32)
+                K.gemm_bf16(dqkv, _transposed(lw, "qkv_w", dev), dxq)
+                addends = (dxq, dy1, dxg)
+
+
+_DATT_F32 = __import__("os").environ.get("MER_DATT_F32", "1") != "0"
+
+
+def _pack_layer(layer, dev):
+    """bf16 operands of one trainable encoder layer (re-cast every forward: the weights move each step)."""
+    at = layer.attention
+    D = at.q_proj.weight.shape[0]
+    qkv = torch.empty(3 * D, D, device=dev, dtype=torch.bfloat16)
+    for j, lin in enumerate((at.q_proj, at.k_proj, at.v_proj)):
+        K.cast_bf16(lin.weight.detach().contiguous(), qkv[j * D:(j + 1) * D])
+    qkv_b = torch.cat([at.q_proj.bias, at.k_proj.bias, at.v_proj.bias]).detach().contiguous()
+    return dict(qkv_w=qkv, qkv_b=qkv_b, out_w=WavLMBackbone._bf16(at.out_proj.weight),
+                ff1_w=WavLMBackbone._bf16(layer.feed_forward.intermediate_dense.weight),
+                ff2_w=WavLMBackbone._bf16(layer.feed_forward.output_dense.weight),
+                gate_c=at.gru_rel_pos_const.detach().reshape(-1))
+
+
+def _transposed(lw, name, dev):
+    """W^T (bf16) of a packed weight, built on first use in backward."""
+    key = name + "_t"
+    if key not in lw:
+        w = lw[name]
+        lw[key] = torch.empty(w.shape[1], w.shape[0], device=dev, dtype=torch.bfloat16)
+        K.transpose_bf16(w, lw[key])
+    return lw[key]
+
+
+class _WavLMTailFn(torch.autograd.Function):
+    """Autograd node of the unfrozen WavLM layers (stage 2): forward = tail_forward, backward =
+    tail_backward writing each parameter gradient straight into its ``grad_buffer`` slot."""
+
+    @staticmethod
+    def forward(ctx, x, tbl, enc, first, names, *params):
+        out, saved = enc.tail_forward(x, tbl, first)
+        B, L, D = x.shape
+        ctx.enc, ctx.first, ctx.saved, ctx.tbl, ctx.shape = enc, first, saved, tbl, (B, L)
+        ctx.params = params
+        return out.view(B, L, D)
+
+    @staticmethod
+    def backward(ctx, dout):
+        from .fusion import grad_buffer
+
+        B, L = ctx.shape
+        grads = {q: grad_buffer(q) for q in ctx.params}
+        ctx.enc.tail_backward(dout.float().contiguous(), ctx.saved, ctx.tbl, ctx.first, B, L, grads)
+        ctx.saved = None
+        return (None, None, None, None, None) + tuple(grads[q] if q.requires_grad else None for q in ctx.params)
+
+
 class WavLMAudioEncoder(nn.Module):
     """wavlm_audio.py:13-183 -- same constructor, stage helpers and encode API."""
 
@@ -379,10 +580,11 @@ class WavLMAudioEncoder(nn.Module):
 
     def encode_sequence(self, x: torch.Tensor, out_dtype=torch.bfloat16) -> torch.Tensor:
         """[B,1,S] or [B,S] -> [B, Ta, 768] hidden states (bf16 activations; wavlm_audio.py:165-183)."""
-        trainable = self.wavlm.trainable()
-        if self.training and trainable and torch.is_grad_enabled():
-            raise NotImplementedError("WavLM stage-2 fine-tuning (backward through the encoder) is a later build "
-                                      "row; the north-star path trains with WavLM frozen (wavlm_audio.py:62-68)")
+        if self.wavlm.trainable() and torch.is_grad_enabled():
+            # stage 2 (wavlm_audio.py:70-88 unfreeze_backbone): frozen prefix forward, then the unfrozen last
+            # layers as one autograd node whose backward runs csrc/wavlm_train.hip; fp32 output so the
+            # head's audio-input gradient arrives in the dtype the node produced
+            return self.wavlm.forward_train(self._wav(x))
         return self.wavlm.forward_hip(self._wav(x), out_dtype=out_dtype)
 
     def encode(self, x: torch.Tensor) -> torch.Tensor:
