@@ -30,7 +30,9 @@ sys.path.insert(0, str(ROOT))
 
 from multimodalemotionrecognition_amd import kernels as K  # noqa: E402
 from multimodalemotionrecognition_amd.dist import GradAllReduce, init_distributed, is_dist  # noqa: E402
-from multimodalemotionrecognition_amd.train import TrainStep, build_model, build_optimizer, make_loss  # noqa: E402
+from multimodalemotionrecognition_amd.train import (TrainStep, apply_two_stage_freeze_policy,  # noqa: E402
+                                                    build_fusion_stage_optimizer, build_model, build_optimizer,
+                                                    make_loss)
 
 BATCH, FRAMES, SIZE, SAMPLES, CLASSES = 32, 8, 112, 48000, 8
 PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, spec)
@@ -106,13 +108,20 @@ def main():
     ap.add_argument("--no-prefetch", action="store_true",
                     help="run the frozen WavLM inline in every step instead of overlapping the next batch's "
                          "WavLM forward with this step's backward")
+    ap.add_argument("--wavlm-unfreeze", type=int, default=0,
+                    help="stage-2 fine-tuning step instead (train.py:798-872 two-stage policy): unfreeze the last N "
+                         "WavLM layers and the last video block, stage optimizer groups (not the headline config)")
     args = ap.parse_args()
 
     world, rank, local = init_distributed()
     dev = torch.device("cuda", local)
     torch.manual_seed(1234)  # identical init on every rank
     model = build_model(CLASSES, "xattn", pretrained_video=False, use_wavlm=True).to(dev)
-    opt = build_optimizer(model, lr=1e-3, weight_decay=1e-4)
+    if args.wavlm_unfreeze > 0:
+        apply_two_stage_freeze_policy(model, stage=2, unfreeze_wavlm_layers=args.wavlm_unfreeze)
+        opt = build_fusion_stage_optimizer(model, stage=2, lr=1e-3, weight_decay=1e-4)
+    else:
+        opt = build_optimizer(model, lr=1e-3, weight_decay=1e-4)
     step = TrainStep(model, opt, make_loss("xattn"), "xattn", GradAllReduce(opt) if is_dist() else None)
     video, audio, labels = synthetic_batch(dev, 20261015 + rank)
 
@@ -171,7 +180,10 @@ def main():
         "vs_baseline": None,
         "dtype": "bf16",
         "data": "synthetic (seeded 3 s clips resident in HBM; random-init weights)",
-        "config": {"workload": "ResNet18 + WavLM-base (frozen) + xattn fusion train step (fwd+bwd+Adam)",
+        "config": {"workload": ("ResNet18 + WavLM-base (frozen) + xattn fusion train step (fwd+bwd+Adam)"
+                                if args.wavlm_unfreeze == 0 else
+                                f"stage-2 fine-tuning step: WavLM last {args.wavlm_unfreeze} layers + ResNet18 layer4 + "
+                                "xattn head trainable (fwd+bwd+Adam)"),
                    "per_gpu_batch": BATCH, "global_batch": BATCH * world, "frames": FRAMES, "image": SIZE,
                    "audio_samples": SAMPLES, "parallelism": f"dp{world}"},
         "clips_per_s": round(world * BATCH * args.steps / elapsed, 1),

@@ -239,8 +239,9 @@ int mer_cast_bf16(long n, const float* x, void* y, void* stream);
 int mer_ln_bwd(int rows, int d, const float* dy_a, const float* dy_b, const float* dy_c, const float* x,
                const float* gamma, float eps, float* dx32, void* dx16, float* part, void* stream);
 
-/* out[k] += sum_{p < parts} part[p * ldp + k] for k < n, summed in a fixed order. */
-int mer_fold_rows(int parts, int n, const float* part, long ldp, float* out, void* stream);
+/* out[k] += sum_{p < parts} part[p * ldp + k] for k < n, summed in a fixed order (deterministic).  parts > 64 runs
+ * two stages through workspace float[64 * n] (may be NULL when parts <= 64). */
+int mer_fold_rows(int parts, int n, const float* part, long ldp, float* out, float* workspace, void* stream);
 
 /* part[p][c] = sum of rows [64p, 64p+64) of x[:, c] (x_dtype 0 fp32 / 1 bf16): part is float[ceil(rows/64)][cols]. */
 int mer_colpart(int rows, int cols, const void* x, int x_dtype, long ldx, float* part, void* stream);
@@ -260,7 +261,7 @@ int mer_linear_wgrad(int M, int N, int K, const void* x, const void* dy, long ld
 /* Backward of mer_wavlm_attention (tbl form: per-head bias table [H][2L-1]), L <= 192.  dout fp32 [B*L][>=H*64]
  * (gradient of the attention output; fp32 because dp_ij - sum_j p_ij dp_ij cancels for peaked rows), qkv / x as in the forward.  Writes dqkv bf16 [B*L][3*H*64] (dq | dk | dv),
  * dx_gate fp32 (the gate path's gradient of the layer input x; may be NULL), P and dS scratch float[B*H][L][L],
- * gate_part float[B*H*ceil(L/16)][8*64 + 8 + H] per-block partials of (d gru_rel_pos_linear.weight [8][64],
+ * gate_part float[B*H*ceil(L/32)][8*64 + 8 + H] per-block partials of (d gru_rel_pos_linear.weight [8][64],
  * .bias [8], d gru_rel_pos_const [H]) -- fold with mer_fold_rows. */
 int mer_wavlm_attention_bwd(int B, int L, int H, const void* qkv, long ldqkv, const void* x, long ldx,
                             const void* dout, long ldo, const float* gate_w, const float* gate_b,

@@ -123,6 +123,28 @@ __global__ __launch_bounds__(256) void fold_rows_kernel(int parts, int n, const 
   out[k] += (s0 + s1) + (s2 + s3);
 }
 
+// First stage of a long fold: split s of gridDim.y sums parts [s*chunk, (s+1)*chunk) of 64 columns, the 4 waves
+// taking every 4th part, combined in a fixed order -> tmp[s][k].
+__global__ __launch_bounds__(256) void fold_split_kernel(int parts, int n, const float* __restrict__ part, long ldp,
+                                                         int chunk, float* __restrict__ tmp) {
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int k = blockIdx.x * 64 + lane;
+  const int p0 = blockIdx.y * chunk, p1 = min(parts, p0 + chunk);
+  float s0 = 0.f, s1 = 0.f;
+  if (k < n) {
+    int p = p0 + w;
+    for (; p + 4 < p1; p += 8) {
+      s0 += part[(long)p * ldp + k];
+      s1 += part[(long)(p + 4) * ldp + k];
+    }
+    if (p < p1) s0 += part[(long)p * ldp + k];
+  }
+  red[w][lane] = s0 + s1;
+  __syncthreads();
+  if (w == 0 && k < n) tmp[(long)blockIdx.y * n + k] = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+}
+
 // Column partial sums of a bf16 / fp32 matrix: part[blockIdx.y][c] = sum over COL_ROWS rows of x[r][c].
 constexpr int COL_ROWS = 64;
 template <typename T>
@@ -184,7 +206,7 @@ __global__ __launch_bounds__(256) void gelu_bwd_kernel(int rows, int cols, const
 // (fp32 scratch [B*H][L][L]) for the cols kernel, dq into dqkv, dx_gate, per-block gate-grad partials.
 constexpr int AB_LMAX = 192;  // 3 key columns per lane; 2 blocks per CU in LDS (3 s clips: L = 149)
 constexpr int AB_PITCH = 66;
-constexpr int AB_ROWS = 16;
+constexpr int AB_ROWS = 32;  // query rows per block (8 per wave): K/V staged once per 32 rows
 constexpr int GATE_PART = 8 * 64 + 8;  // + H (gate const) per partial row
 
 __global__ __launch_bounds__(256) void wavlm_attn_bwd_rows_kernel(
@@ -393,10 +415,19 @@ MER_API int mer_ln_bwd(int rows, int d, const float* dy_a, const float* dy_b, co
   MER_LAUNCH_CHECK();
 }
 
-MER_API int mer_fold_rows(int parts, int n, const float* part, long ldp, float* out, void* stream) {
+MER_API int mer_fold_rows(int parts, int n, const float* part, long ldp, float* out, float* workspace, void* stream) {
   if (parts <= 0 || n <= 0) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(fold_rows_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, parts, n, part, ldp,
-                     out);
+  hipStream_t st = (hipStream_t)stream;
+  if (parts > 64) {  // two stages: <= 64 split rows of the same fixed-order sum, then the short fold below
+    if (!workspace) return (int)hipErrorInvalidValue;
+    const int S = min(64, (parts + 63) / 64), chunk = (parts + S - 1) / S;
+    hipLaunchKernelGGL(fold_split_kernel, dim3((n + 63) / 64, S), dim3(256), 0, st, parts, n, part, ldp, chunk,
+                       workspace);
+    part = workspace;
+    ldp = n;
+    parts = S;
+  }
+  hipLaunchKernelGGL(fold_rows_kernel, dim3((n + 255) / 256), dim3(256), 0, st, parts, n, part, ldp, out);
   MER_LAUNCH_CHECK();
 }
 

@@ -215,3 +215,11 @@ def macro_f1(preds: torch.Tensor, targets: torch.Tensor) -> float:
         denom = 2 * tp + fp + fn
         f1s.append(0.0 if denom == 0 else 2 * tp / denom)
     return float(sum(f1s) / len(f1s)) if f1s else 0.0
+
+
+def save_checkpoint(model: nn.Module, path, val_f1: float, config: Optional[dict] = None) -> None:
+    """train.py:1141-1144 checkpoint format {"model", "val_f1", "config"} (state-dict keys identical to the
+    reference's, so ``optimized_runtime.TorchModelRunner`` and the reference's loaders read it).  Tensors are
+    moved to the host; after FusedAdam re-homing they are views of its flat buffers, so they are copied out."""
+    state = {k: v.detach().to("cpu", copy=True) for k, v in model.state_dict().items()}
+    torch.save({"model": state, "val_f1": float(val_f1), "config": dict(config or {})}, str(path))

@@ -44,3 +44,18 @@ def test_unsupported_wavlm_trainable_sets_raise():
         p.requires_grad = True
     with pytest.raises(NotImplementedError):
         wavlm.first_trainable_layer()
+
+
+def test_save_checkpoint_roundtrip(tmp_path):
+    import torch
+
+    from multimodalemotionrecognition_amd.optimized_runtime import infer_model_signature
+    from multimodalemotionrecognition_amd.train import save_checkpoint
+
+    m = build_model(8, "xattn", pretrained_video=False, use_wavlm=True)
+    ck = tmp_path / "best.pt"
+    save_checkpoint(m, ck, 0.25, {"fusion": "xattn", "use_wavlm": True})
+    blob = torch.load(ck, map_location="cpu", weights_only=True)
+    assert set(blob) == {"model", "val_f1", "config"} and blob["val_f1"] == 0.25
+    assert set(blob["model"]) == set(m.state_dict())
+    assert infer_model_signature(blob["model"]) is not None
