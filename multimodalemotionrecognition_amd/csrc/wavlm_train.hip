@@ -205,7 +205,7 @@ __global__ __launch_bounds__(256) void gelu_bwd_kernel(int rows, int cols, const
 // (bf16, 66-element row pitch: odd dword stride, conflict-free per-lane row reads); writes P and dS rows
 // (fp32 scratch [B*H][L][L]) for the cols kernel, dq into dqkv, dx_gate, per-block gate-grad partials.
 constexpr int AB_LMAX = 192;  // 3 key columns per lane; 2 blocks per CU in LDS (3 s clips: L = 149)
-constexpr int AB_PITCH = 66;
+constexpr int AB_PITCH = 68;  // bf16 row pitch: 8-byte aligned rows, 17j mod 32 banks -> conflict-free b64 reads
 constexpr int AB_ROWS = 32;  // query rows per block (8 per wave): K/V staged once per 32 rows
 constexpr int GATE_PART = 8 * 64 + 8;  // + H (gate const) per partial row
 
@@ -217,7 +217,9 @@ __global__ __launch_bounds__(256) void wavlm_attn_bwd_rows_kernel(
     float* __restrict__ gpart) {
   __shared__ __attribute__((aligned(16))) bf16_t Ks[AB_LMAX * AB_PITCH];
   __shared__ __attribute__((aligned(16))) bf16_t Vs[AB_LMAX * AB_PITCH];
-  __shared__ float qrow[4][64], dorow[4][64], dsrow[4][AB_LMAX];
+  __shared__ __attribute__((aligned(16))) float qrow[4][64];
+  __shared__ __attribute__((aligned(16))) float dorow[4][64];
+  __shared__ __attribute__((aligned(16))) float dsrow[4][AB_LMAX];
   __shared__ float gw[8][64];
   __shared__ float red[4][GATE_PART + 1];
   const int bh = blockIdx.y, b = bh / H, h = bh - b * H;
@@ -267,16 +269,24 @@ __global__ __launch_bounds__(256) void wavlm_attn_bwd_rows_kernel(
       s[jj] = -INFINITY;
       dp[jj] = 0.f;
       if (j < L) {
-        const uint32_t* kr = reinterpret_cast<const uint32_t*>(Ks + j * AB_PITCH);
-        const uint32_t* vr = reinterpret_cast<const uint32_t*>(Vs + j * AB_PITCH);
+        // 4 dims per step: one b64 K read, one b64 V read (per lane), one broadcast b128 read each of q and dO
+        const uint2* kr = reinterpret_cast<const uint2*>(Ks + j * AB_PITCH);
+        const uint2* vr = reinterpret_cast<const uint2*>(Vs + j * AB_PITCH);
+        const f32x4* q4 = reinterpret_cast<const f32x4*>(qrow[w]);
+        const f32x4* o4 = reinterpret_cast<const f32x4*>(dorow[w]);
         float a0 = 0.f, a1 = 0.f, c0 = 0.f, c1 = 0.f;
-#pragma unroll 8
-        for (int e = 0; e < 32; ++e) {
-          const uint32_t kk = kr[e], vv = vr[e];
-          a0 += qrow[w][2 * e] * bf2f((bf16_t)(kk & 0xffff));
-          a1 += qrow[w][2 * e + 1] * bf2f((bf16_t)(kk >> 16));
-          c0 += dorow[w][2 * e] * bf2f((bf16_t)(vv & 0xffff));
-          c1 += dorow[w][2 * e + 1] * bf2f((bf16_t)(vv >> 16));
+#pragma unroll 4
+        for (int e = 0; e < 16; ++e) {
+          const uint2 kk = kr[e], vv = vr[e];
+          const f32x4 qq = q4[e], oo = o4[e];
+          a0 += qq[0] * __uint_as_float(kk.x << 16);
+          a1 += qq[1] * __uint_as_float(kk.x & 0xffff0000u);
+          a0 += qq[2] * __uint_as_float(kk.y << 16);
+          a1 += qq[3] * __uint_as_float(kk.y & 0xffff0000u);
+          c0 += oo[0] * __uint_as_float(vv.x << 16);
+          c1 += oo[1] * __uint_as_float(vv.x & 0xffff0000u);
+          c0 += oo[2] * __uint_as_float(vv.y << 16);
+          c1 += oo[3] * __uint_as_float(vv.y & 0xffff0000u);
         }
         s[jj] = a0 + a1 + gate * th[j - i + L - 1];
         dp[jj] = c0 + c1;
@@ -314,11 +324,14 @@ __global__ __launch_bounds__(256) void wavlm_attn_bwd_rows_kernel(
     // dq_i[d] = scale * sum_j ds_ij k_j[d]   (lane = d)
     float q0 = 0.f, q1 = 0.f;
     int j = 0;
-    for (; j + 2 <= L; j += 2) {
-      q0 += dsrow[w][j] * bf2f(Ks[j * AB_PITCH + lane]);
-      q1 += dsrow[w][j + 1] * bf2f(Ks[(j + 1) * AB_PITCH + lane]);
+    for (; j + 4 <= L; j += 4) {
+      const f32x4 d4 = *reinterpret_cast<const f32x4*>(&dsrow[w][j]);
+      q0 += d4[0] * bf2f(Ks[j * AB_PITCH + lane]);
+      q1 += d4[1] * bf2f(Ks[(j + 1) * AB_PITCH + lane]);
+      q0 += d4[2] * bf2f(Ks[(j + 2) * AB_PITCH + lane]);
+      q1 += d4[3] * bf2f(Ks[(j + 3) * AB_PITCH + lane]);
     }
-    if (j < L) q0 += dsrow[w][j] * bf2f(Ks[j * AB_PITCH + lane]);
+    for (; j < L; ++j) q0 += dsrow[w][j] * bf2f(Ks[j * AB_PITCH + lane]);
     dqkv[row * lddq + h * 64 + lane] = f2bf((q0 + q1) * scale);
     // gate backward: gate = ga (gb c - 1) + 2
     const float dpa = dgate * (gb * gc - 1.f) * ga * (1.f - ga);
@@ -356,7 +369,7 @@ __global__ __launch_bounds__(256) void wavlm_attn_bwd_cols_kernel(int L, int H, 
                                                                   bf16_t* __restrict__ dqkv, long lddq) {
   __shared__ __attribute__((aligned(16))) bf16_t Qs[AB_LMAX * AB_PITCH];
   __shared__ __attribute__((aligned(16))) bf16_t Os[AB_LMAX * AB_PITCH];
-  __shared__ float Pc[AB_LMAX][17], Dc[AB_LMAX][17];
+  __shared__ float Pc[AB_LMAX][17], Dc[AB_LMAX][17];  // 17: keeps the block at 2 per CU in LDS
   const int bh = blockIdx.y, b = bh / H, h = bh - b * H;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int D = H * 64;
