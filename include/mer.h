@@ -82,8 +82,8 @@ int mer_add_ln_fwd(int rows, int d, int rows_per_sample, const float* x, const f
                    float* mean_out, float* rstd_out, void* stream);
 
 /* Backward of mer_add_ln_fwd: dx = dsum, dr = s_b*dsum (dr may be NULL); dgamma/dbeta accumulate (+=),
- * deterministically: per-64-row-block partials in workspace (MER_ADD_LN_WS_FLOATS(rows, d) floats). */
-#define MER_ADD_LN_WS_FLOATS(rows, d) ((long)(((rows) + 63) / 64) * 2 * (d))
+ * deterministically: per-16-row-block partials in workspace (MER_ADD_LN_WS_FLOATS(rows, d) floats). */
+#define MER_ADD_LN_WS_FLOATS(rows, d) ((long)(((rows) + 15) / 16) * 2 * (d))
 int mer_add_ln_bwd(int rows, int d, int rows_per_sample, const float* dy, const float* s, const float* mean,
                    const float* rstd, const float* gamma, float dp_p, const unsigned long long* seed, unsigned long long site, float* dx, float* dr,
                    float* dgamma, float* dbeta, float* workspace, void* stream);

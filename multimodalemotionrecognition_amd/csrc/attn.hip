@@ -36,11 +36,27 @@ __device__ __forceinline__ void wave_lds_sync() {
 }
 
 // Stage rows [0, Lp) x cols [0, cols_p) of head h into LDS (zero outside [0, L) x [0, dh)).
+// 16-byte chunks when the rows allow it (dh, ld, st multiples of 4 and a 16-byte aligned source: every
+// xattn call site), unrolled so several global loads are in flight per thread -- the element-wise loop was a
+// chain of ~80 dependent load -> LDS-store trips per thread for Lk = 149 (v2a forward: 75 us -> ~10 us).
 __device__ __forceinline__ void stage_head(float* dst, int st, int Lp, int cols_p, const float* __restrict__ src,
                                            long ld, int b, int L, int h, int dh) {
+  const float* base = src + (long)b * L * ld + h * dh;
+  if ((dh & 3) == 0 && (ld & 3) == 0 && (st & 3) == 0 && (cols_p & 3) == 0 &&
+      (reinterpret_cast<uintptr_t>(base) & 15) == 0) {
+    const int cq = cols_p >> 2, n = Lp * cq;
+#pragma unroll 4
+    for (int e = threadIdx.x; e < n; e += blockDim.x) {
+      const int j = e / cq, c = (e - j * cq) * 4;
+      f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (j < L && c < dh) v = *reinterpret_cast<const f32x4*>(base + (long)j * ld + c);
+      *reinterpret_cast<f32x4*>(dst + j * st + c) = v;
+    }
+    return;
+  }
   for (int e = threadIdx.x; e < Lp * cols_p; e += blockDim.x) {
     const int j = e / cols_p, c = e - j * cols_p;
-    dst[j * st + c] = (j < L && c < dh) ? src[((long)b * L + j) * ld + h * dh + c] : 0.f;
+    dst[j * st + c] = (j < L && c < dh) ? base[(long)j * ld + c] : 0.f;
   }
 }
 
@@ -184,7 +200,8 @@ MER_API int mer_mha_fwd(int B, int H, int Lq, int Lk, int dh, const float* Q, lo
                         float drop_p, const unsigned long long* seed, unsigned long long site, void* stream) {
   if (B <= 0 || Lq <= 0) return 0;
   if (dh <= 0 || dh > 64 || (dh % 4) != 0 || Lk <= 0 || Lk > 16 * FWD_MAX_KT) return (int)hipErrorInvalidValue;
-  const int waves = (Lq + 15) / 16 < 4 ? (Lq + 15) / 16 : 4;
+  // always 4 waves: all of them stage K/V, waves without query rows retire after the barrier
+  const int waves = 4;
   const size_t lds = mha_fwd_lds(Lk, dh, waves);
   if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
   if (hipFuncSetAttribute(reinterpret_cast<const void*>(&mha_fwd_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,

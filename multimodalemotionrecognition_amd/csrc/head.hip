@@ -238,19 +238,30 @@ __global__ __launch_bounds__(256) void colsum_kernel(int M, int N, const float* 
 }
 
 // out0[e] (e < split) / out1[e - split] += sum_{r < rows} in[r*E + e]: fixed-order per-entry sums of
-// per-block partial rows (64 entries per block, the 4 waves split the rows and meet in LDS)
-__global__ __launch_bounds__(256) void rows_sum_add_kernel(int E, int rows, const float* __restrict__ in, int split,
-                                                           float* __restrict__ out0, float* __restrict__ out1) {
-  __shared__ float part[4][64];
+// per-block partial rows (64 entries per block, the 16 waves split the rows and meet in LDS in a fixed tree
+// order; 16 rather than 4 waves: the per-thread row loop is a latency chain, 12.8 us at ~300 partial rows)
+__global__ __launch_bounds__(1024) void rows_sum_add_kernel(int E, int rows, const float* __restrict__ in, int split,
+                                                            float* __restrict__ out0, float* __restrict__ out1) {
+  __shared__ float part[16][64];
   const int el = threadIdx.x & 63, pg = threadIdx.x >> 6;
   const int e = blockIdx.x * 64 + el;
-  float acc = 0.f;
-  if (e < E)
-    for (int r = pg; r < rows; r += 4) acc += in[(long)r * E + e];
-  part[pg][el] = acc;
+  float a0 = 0.f, a1 = 0.f;
+  if (e < E) {
+    int r = pg;
+    for (; r + 16 < rows; r += 32) {
+      a0 += in[(long)r * E + e];
+      a1 += in[(long)(r + 16) * E + e];
+    }
+    if (r < rows) a0 += in[(long)r * E + e];
+  }
+  part[pg][el] = a0 + a1;
   __syncthreads();
   if (pg == 0 && e < E) {
-    const float v = (part[0][el] + part[1][el]) + (part[2][el] + part[3][el]);
+    float q[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+      q[g] = (part[4 * g][el] + part[4 * g + 1][el]) + (part[4 * g + 2][el] + part[4 * g + 3][el]);
+    const float v = (q[0] + q[1]) + (q[2] + q[3]);
     if (e < split) {
       if (out0) out0[e] += v;
     } else if (out1) {
@@ -270,7 +281,7 @@ MER_API int mer_colsum_f32(int M, int N, const float* X, long ldx, float* out, f
   const int ny = (M + rpb - 1) / rpb;
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(colsum_kernel, dim3((N + 63) / 64, ny), dim3(256), 0, st, M, N, X, ldx, workspace, rpb);
-  hipLaunchKernelGGL(rows_sum_add_kernel, dim3((N + 63) / 64), dim3(256), 0, st, N, ny, workspace, N, out,
+  hipLaunchKernelGGL(rows_sum_add_kernel, dim3((N + 63) / 64), dim3(1024), 0, st, N, ny, workspace, N, out,
                      (float*)nullptr);
   MER_LAUNCH_CHECK();
 }
@@ -380,11 +391,13 @@ MER_API int mer_add_ln_bwd(int rows, int d, int rows_per_sample, const float* dy
                            float* dr, float* dgamma, float* dbeta, float* workspace, void* stream) {
   if (rows <= 0) return 0;
   if ((size_t)8 * d * sizeof(float) > 160 * 1024) return (int)hipErrorInvalidValue;
-  const int rpb = 64;
+  // 16 rows per block (4 per wave): each row is a short chain of dependent loads and wave reductions, so the
+  // kernel is latency-bound and wants many blocks (64 rows per block made it 31 us at 256 rows AND at 4,768)
+  const int rpb = 16;
   const int nb = (rows + rpb - 1) / rpb;
   hipLaunchKernelGGL(add_ln_bwd_kernel, dim3(nb), dim3(256), 8 * d * sizeof(float), (hipStream_t)stream, rows, d,
                      rows_per_sample, dy, s, mean, rstd, gamma, dp_p, seed, site, dx, dr, workspace, rpb);
-  hipLaunchKernelGGL(rows_sum_add_kernel, dim3((2 * d + 63) / 64), dim3(256), 0, (hipStream_t)stream, 2 * d, nb,
+  hipLaunchKernelGGL(rows_sum_add_kernel, dim3((2 * d + 63) / 64), dim3(1024), 0, (hipStream_t)stream, 2 * d, nb,
                      workspace, d, dgamma, dbeta);
   MER_LAUNCH_CHECK();
 }

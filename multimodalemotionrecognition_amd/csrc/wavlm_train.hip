@@ -14,6 +14,8 @@
 
 namespace {
 
+typedef __attribute__((ext_vector_type(2))) float f32x2;
+
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }
 
 // make this wave's LDS writes visible to all of its lanes (per-wave row buffers)
@@ -274,22 +276,23 @@ __global__ __launch_bounds__(256) void wavlm_attn_bwd_rows_kernel(
         const uint2* vr = reinterpret_cast<const uint2*>(Vs + j * AB_PITCH);
         const f32x4* q4 = reinterpret_cast<const f32x4*>(qrow[w]);
         const f32x4* o4 = reinterpret_cast<const f32x4*>(dorow[w]);
-        float a0 = 0.f, a1 = 0.f, c0 = 0.f, c1 = 0.f;
+        // packed fp32 FMAs (v_pk_fma_f32): two dims per instruction
+        f32x2 a = {0.f, 0.f}, c = {0.f, 0.f};
 #pragma unroll 4
         for (int e = 0; e < 16; ++e) {
           const uint2 kk = kr[e], vv = vr[e];
           const f32x4 qq = q4[e], oo = o4[e];
-          a0 += qq[0] * __uint_as_float(kk.x << 16);
-          a1 += qq[1] * __uint_as_float(kk.x & 0xffff0000u);
-          a0 += qq[2] * __uint_as_float(kk.y << 16);
-          a1 += qq[3] * __uint_as_float(kk.y & 0xffff0000u);
-          c0 += oo[0] * __uint_as_float(vv.x << 16);
-          c1 += oo[1] * __uint_as_float(vv.x & 0xffff0000u);
-          c0 += oo[2] * __uint_as_float(vv.y << 16);
-          c1 += oo[3] * __uint_as_float(vv.y & 0xffff0000u);
+          const f32x2 k01 = {__uint_as_float(kk.x << 16), __uint_as_float(kk.x & 0xffff0000u)};
+          const f32x2 k23 = {__uint_as_float(kk.y << 16), __uint_as_float(kk.y & 0xffff0000u)};
+          const f32x2 v01 = {__uint_as_float(vv.x << 16), __uint_as_float(vv.x & 0xffff0000u)};
+          const f32x2 v23 = {__uint_as_float(vv.y << 16), __uint_as_float(vv.y & 0xffff0000u)};
+          a = __builtin_elementwise_fma(f32x2{qq[0], qq[1]}, k01, a);
+          a = __builtin_elementwise_fma(f32x2{qq[2], qq[3]}, k23, a);
+          c = __builtin_elementwise_fma(f32x2{oo[0], oo[1]}, v01, c);
+          c = __builtin_elementwise_fma(f32x2{oo[2], oo[3]}, v23, c);
         }
-        s[jj] = a0 + a1 + gate * th[j - i + L - 1];
-        dp[jj] = c0 + c1;
+        s[jj] = a[0] + a[1] + gate * th[j - i + L - 1];
+        dp[jj] = c[0] + c[1];
       }
       mx = fmaxf(mx, s[jj]);
     }

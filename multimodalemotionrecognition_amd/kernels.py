@@ -184,7 +184,7 @@ def add_ln_bwd(dy, s, mean, rstd, gamma, dx, dr, dgamma, dbeta, rows_per_sample,
     rows, d = dy.shape
     LIB("mer_add_ln_bwd", rows, d, rows_per_sample, dy.data_ptr(), s.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
         gamma.data_ptr(), float(dp_p), rng_ptr(rng), int(site), dx.data_ptr(), _ptr(dr), _ptr(dgamma), _ptr(dbeta),
-        _workspace((rows + 63) // 64 * 2 * d, dy.device).data_ptr(), stream_ptr())  # MER_ADD_LN_WS_FLOATS
+        _workspace((rows + 15) // 16 * 2 * d, dy.device).data_ptr(), stream_ptr())  # MER_ADD_LN_WS_FLOATS
 
 
 def mean_pool_fwd(x3d, y, ldy=None):
