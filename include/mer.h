@@ -271,6 +271,20 @@ int mer_wavlm_attention_bwd(int B, int L, int H, const void* qkv, long ldqkv, co
 /* dst[c][r] = src[r][c], bf16 (the transposed weight operands of the stage-2 data-gradient GEMMs). */
 int mer_transpose_bf16(int rows, int cols, const void* src, long lds, void* dst, long ldd, void* stream);
 
+/* ============================ clip assembly (first step) ============================ */
+
+/* Post-decode frame preprocessing of load_video_frames (ravdess.py:352 cv2.resize(frame, (S, S), INTER_LINEAR),
+ * :363 /255, :386-389 (x - mean) / std, HWC -> CHW): frames = N decoded RGB uint8 [H0][W0][3] images, frame_stride
+ * bytes apart -> out fp32 [N][3][S][S].  OpenCV's scalar fixed-point linear path (11-bit weights, exact 2x
+ * downscale = INTER_AREA 2x2 average). */
+int mer_frames_resize_normalize(int N, int H0, int W0, const void* frames, long frame_stride, int S, float mean0,
+                                float mean1, float mean2, float std0, float std1, float std2, float* out, void* stream);
+
+/* load_audio_wav pad / crop (ravdess.py:505-513): out[b][t] = t < lengths[b] ? packed[offsets[b] + t] : 0,
+ * out fp32 [B][target]; offsets / lengths are DEVICE int64 arrays (a ragged batch of decoded waveforms). */
+int mer_wav_pad_crop(int B, int target, const float* packed, const long long* offsets, const long long* lengths,
+                     float* out, void* stream);
+
 /* ============================ ResNet18 frame trunk (bf16 MFMA, NHWC) ============================
  * VideoNet.backbone (video.py:21-23 -> torchvision resnet18 children[:-1]).  Activations are NHWC bf16
  * with channels padded to a multiple of 8. */
