@@ -147,7 +147,7 @@ class ResNet18Trunk(nn.Sequential):
         capture, or for a second forward before the first one's backward (graphs.py)."""
         if G.capturing():
             return None
-        key = (tuple(x.shape), bool(training), x.device.index, G.tensor_addresses(self))
+        key = (tuple(x.shape), bool(training), x.device.index, G.tensor_addresses(self), self.backward_stop())
         if not self._graphs.ready(key):
             return None
         r = self._graphs.get(key)
@@ -157,6 +157,28 @@ class ResNet18Trunk(nn.Sequential):
             return None
         r.pending = bool(want_backward)
         return r
+
+    def backward_stop(self) -> int:
+        """Lowest BasicBlock index the backward must reach: -1 when the stem trains (full backward), else the
+        first block with a trainable parameter (train.py:777-796 unfreezes only the last backbone children; the
+        frames never need a gradient, so nothing below that block is computed), len(blocks) when frozen."""
+        flags = tuple(q.requires_grad for q in self._param_list())
+        cache = self.__dict__.get("_mer_bwd_stop")
+        if cache is not None and cache[0] == flags:
+            return cache[1]
+        if any(q.requires_grad for m in (self[0], self[1]) for q in m.parameters()):
+            stop = -1
+        else:
+            blocks = _blocks(self)
+            stop = next((i for i, b in enumerate(blocks) if any(q.requires_grad for q in b.parameters())), len(blocks))
+        self.__dict__["_mer_bwd_stop"] = (flags, stop)
+        return stop
+
+    def _param_list(self):
+        lst = self.__dict__.get("_mer_params")
+        if lst is None:
+            lst = self.__dict__["_mer_params"] = list(self.parameters())
+        return lst
 
     # ---- bf16 weight packing: all convs in one launch, re-done whenever a weight's value changes ----
     def _pack_plan(self, transpose: bool):
@@ -484,9 +506,12 @@ def _trunk_backward(trunk: ResNet18Trunk, saved, dfeat: torch.Tensor, training: 
     pre = None
     # every backward BatchNorm reduction buffer of this pass: one memset
     arena = _StatsArena(trunk, dev, floats=sum(_block_bwd_floats(sv) for sv in svs) + 2 * K.BN_RED_WS_ROWS * 64 * 2)
-    for i in reversed(range(len(blocks))):
+    stop = trunk.backward_stop()
+    for i in reversed(range(max(stop, 0), len(blocks))):
         prev = (svs[i - 1], blocks[i - 1]) if i > 0 else None
         dx, pre = block_backward(trunk, blocks[i], svs[i], dx, grads, training, pre=pre, prev=prev, arena=arena)
+    if stop >= 0:  # stem and the blocks below `stop` frozen (stage-2 video tail): nothing more is needed
+        return grads
     # stem: maxpool -> bn1/relu -> conv1 (no data gradient for the frames)
     x0, c1, ms1, arg = saved["stem"]
     bn1 = trunk[1]

@@ -244,3 +244,34 @@ def test_attention_backward_kernel_vs_fp64():
         e = rel_rms(g, r.numpy())
         print(f"  {n} rel-rms {e:.2e}")
         assert e < 1e-4, (n, e)
+
+
+def test_trunk_backward_stops_at_first_trainable_block():
+    """Stage-2 video tail (train.py:777-796, last backbone child trainable): the trunk backward stops after the
+    first trainable block; the gradients it does compute are bit-identical to those of a full backward."""
+    from multimodalemotionrecognition_amd.video import ResNet18Trunk
+
+    torch.manual_seed(3)
+    trunk = ResNet18Trunk().cuda().train()
+    x = torch.from_numpy(np.random.default_rng(12).standard_normal((4, 3, 112, 112)).astype(np.float32)).cuda()
+    G = torch.from_numpy(np.random.default_rng(13).standard_normal((4, 512, 1, 1)).astype(np.float32)).cuda()
+    state = {k: v.clone() for k, v in trunk.state_dict().items()}
+
+    def run():
+        trunk.load_state_dict(state)  # same BN running stats / weights for both passes
+        trunk.zero_grad(set_to_none=True)
+        (trunk(x) * G).sum().backward()
+        torch.cuda.synchronize()
+        return {n: (q.grad.clone() if q.grad is not None else None) for n, q in trunk.named_parameters()}
+
+    full = run()
+    assert trunk.backward_stop() == -1
+    for n, q in trunk.named_parameters():
+        q.requires_grad = n.startswith("7.")
+    assert trunk.backward_stop() == 6
+    tail = run()
+    for n, g in tail.items():
+        if n.startswith("7."):
+            assert g is not None and torch.equal(g, full[n]), n
+        else:
+            assert g is None, n
