@@ -323,14 +323,21 @@ class FusionModel(nn.Module):
         step updates).  The next ``forward`` whose ``audio`` is this same tensor (same storage, shape and
         version) consumes the result; any other input runs the encoder inline as usual.  Returns whether
         the prefetch was issued (xattn mode with a frozen WavLM encoder only)."""
-        if self.mode not in {"xattn", "xattn_concat", "xattn_gated"} or not self.audio_encoder_frozen():
+        if self.mode not in {"xattn", "xattn_concat", "xattn_gated"}:
+            return False
+        frozen = self.audio_encoder_frozen()
+        stage2 = (not frozen and hasattr(self.audio_model, "encode_prefix") and torch.is_grad_enabled()
+                  and getattr(self.audio_model, "wavlm", None) is not None)
+        if not (frozen or stage2):
             return False
         _require_device(audio)
         side = _side_stream(audio.device)
         side.wait_stream(torch.cuda.current_stream(audio.device))
         with torch.cuda.stream(side):
-            a_seq = self.audio_model.encode_sequence(audio)
-        self._prefetched = (_audio_key(audio), a_seq, side)
+            # stage 2: only the frozen prefix (conv stack + layers below the unfrozen ones) runs ahead; the
+            # trainable layers run in the step itself, after the optimizer has updated them
+            out = self.audio_model.encode_prefix(audio) if stage2 else self.audio_model.encode_sequence(audio)
+        self._prefetched = (_audio_key(audio), out, side, stage2)
         return True
 
     def pop_alignment_loss(self) -> Optional[torch.Tensor]:
@@ -417,12 +424,18 @@ class FusionModel(nn.Module):
             # prefetch_audio() already started it for this very batch (during the previous step's
             # backward), its result is taken over instead.
             pf, self._prefetched = self._prefetched, None
-            if pf is not None and pf[0] == _audio_key(audio):
-                a_seq, side = pf[1], pf[2]
+            if pf is not None and pf[0] == _audio_key(audio) and pf[3] == (not self.audio_encoder_frozen()):
+                side = pf[2]
                 v_feat = self.video_model.backbone(v_in).view(b, t, self.v_dim)
                 cur = torch.cuda.current_stream(video.device)
                 cur.wait_stream(side)
-                a_seq.record_stream(cur)
+                if pf[3]:  # stage 2: prefetched frozen prefix -> trainable tail now
+                    for tsr in pf[1]:
+                        tsr.record_stream(cur)
+                    a_seq = self.audio_model.encode_sequence(audio, prefix=pf[1])
+                else:
+                    a_seq = pf[1]
+                    a_seq.record_stream(cur)
                 return self.xattn_from_features(v_feat, a_seq)
             side = _side_stream(video.device) if _OVERLAP_ENCODERS else None
             if side is not None:

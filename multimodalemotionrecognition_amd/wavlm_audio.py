@@ -239,24 +239,30 @@ class WavLMBackbone(nn.Module):
         if not wav.is_cuda:
             raise RuntimeError("WavLM runs on the MI355X kernels; move the waveform to the GPU")
         wav = wav.contiguous().float()
-        if capture is None and num_layers is None and not G.capturing():
-            key = (tuple(wav.shape), out_dtype, wav.device.index, self._weights_key())
+        nl = None if num_layers is None or num_layers >= len(self.encoder.layers) else int(num_layers)
+        if capture is None and not G.capturing():
+            # a prefix run (stage 2) is keyed on the prefix's weights only: the trainable tail changes every step
+            wkey = self._weights_key()
+            key = (tuple(wav.shape), out_dtype, wav.device.index, nl,
+                   wkey if nl is None else wkey[:self._prefix_param_count(nl)])
             if self._graphs.ready(key):
-                return self._forward_graphed(wav, out_dtype, key)
+                return self._forward_graphed(wav, out_dtype, key, nl)
         x, L = self._stage_a(wav)
         y = self._conv_layer(x, 1, L)
-        return self._stage_b(y, L, out_dtype, num_layers, capture)
+        return self._stage_b(y, L, out_dtype, nl, capture)
 
-    def _forward_graphed(self, wav, out_dtype, key):
+    def _forward_graphed(self, wav, out_dtype, key, nl=None):
         g = self._graphs.get(key)
         if g is None:
             ga = G.StaticGraph(lambda w: self._stage_a(w)[0], [wav])
             B, L0 = wav.shape[0], ga.out.shape[1]
             L1 = (L0 - CONV_KERNEL[1]) // CONV_STRIDE[1] + 1
             y1 = torch.empty(B, L1, CONV_DIM, device=wav.device, dtype=torch.bfloat16)
-            gb = G.StaticGraph(lambda: self._stage_b(y1, L0, out_dtype, None, None), [])
-            g = self._graphs.put(key, (ga, y1, gb))
-        ga, y1, gb = g
+            gb = G.StaticGraph(lambda: self._stage_b(y1, L0, out_dtype, nl, None), [])
+            # the graphs read the packed weights captured with them: keep that pack alive (a later full repack,
+            # e.g. after the stage-2 tail moved, replaces self._packed while a prefix key still matches)
+            g = self._graphs.put(key, (ga, y1, gb, self._packed))
+        ga, y1, gb, _ = g
         x = ga.replay(wav)
         self._conv_layer(x, 1, x.shape[1], out=y1)
         return gb.replay().clone()
@@ -356,9 +362,9 @@ class WavLMBackbone(nn.Module):
                                       "(unfreeze_backbone(n), n <= 11); got a different trainable set")
         return first
 
-    def forward_train(self, wav: torch.Tensor) -> torch.Tensor:
-        """Stage-2 forward: frozen conv stack + layers [0, first) on the inference schedule, then layers
-        [first, 12) saving their activations.  Returns fp32 [B, L, 768] tracked by autograd."""
+    def forward_prefix(self, wav: torch.Tensor):
+        """The frozen part of a stage-2 forward: conv stack + layers [0, first) -> (bf16 [B, L, D], bias table).
+        Independent of the trainable weights, so it can run ahead (``FusionModel.prefetch_audio``)."""
         if not wav.is_cuda:
             raise RuntimeError("WavLM runs on the MI355X kernels; move the waveform to the GPU")
         first = self.first_trainable_layer()
@@ -366,9 +372,17 @@ class WavLMBackbone(nn.Module):
         try:
             with torch.no_grad():
                 x = self.forward_hip(wav.contiguous().float(), out_dtype=torch.bfloat16, num_layers=first)
-            tbl = self.packed_weights()["bias_tables"][x.shape[1]]
+                tbl = self.packed_weights()["bias_tables"][x.shape[1]]
         finally:
             self.__dict__["_pack_limit"] = None
+        return x, tbl
+
+    def forward_train(self, wav: torch.Tensor, prefix=None) -> torch.Tensor:
+        """Stage-2 forward: frozen conv stack + layers [0, first) on the inference schedule (or ``prefix``, a
+        ``forward_prefix`` result computed ahead), then layers [first, 12) saving their activations.  Returns
+        fp32 [B, L, 768] tracked by autograd."""
+        first = self.first_trainable_layer()
+        x, tbl = prefix if prefix is not None else self.forward_prefix(wav)
         names, params = [], []
         for li in range(first, len(self.encoder.layers)):
             for n, q in self.encoder.layers[li].named_parameters():
@@ -578,14 +592,20 @@ class WavLMAudioEncoder(nn.Module):
     def _wav(self, x):
         return x.squeeze(1) if x.dim() == 3 else x
 
-    def encode_sequence(self, x: torch.Tensor, out_dtype=torch.bfloat16) -> torch.Tensor:
+    def encode_sequence(self, x: torch.Tensor, out_dtype=torch.bfloat16, prefix=None) -> torch.Tensor:
         """[B,1,S] or [B,S] -> [B, Ta, 768] hidden states (bf16 activations; wavlm_audio.py:165-183)."""
         if self.wavlm.trainable() and torch.is_grad_enabled():
             # stage 2 (wavlm_audio.py:70-88 unfreeze_backbone): frozen prefix forward, then the unfrozen last
             # layers as one autograd node whose backward runs csrc/wavlm_train.hip; fp32 output so the
             # head's audio-input gradient arrives in the dtype the node produced
-            return self.wavlm.forward_train(self._wav(x))
+            return self.wavlm.forward_train(self._wav(x), prefix=prefix)
+        if prefix is not None:
+            raise RuntimeError("a frozen-prefix result is only consumed by a stage-2 (trainable tail) forward")
         return self.wavlm.forward_hip(self._wav(x), out_dtype=out_dtype)
+
+    def encode_prefix(self, x: torch.Tensor):
+        """The frozen part of a stage-2 ``encode_sequence`` (prefetchable; see WavLMBackbone.forward_prefix)."""
+        return self.wavlm.forward_prefix(self._wav(x))
 
     def encode(self, x: torch.Tensor) -> torch.Tensor:
         hidden = self.encode_sequence(x, out_dtype=torch.float32)
