@@ -25,7 +25,7 @@ class _LinearFn(torch.autograd.Function):
         dy2 = dy.reshape(-1, w.shape[0]).contiguous().float()
         if ctx.act == "relu":
             dy2 = dy2.clone()
-            K.relu_dropout_bwd_(dy2, out, 0.0, 0)
+            K.relu_dropout_bwd_(dy2, out, 0.0, None)
         elif ctx.act != "none":
             raise NotImplementedError(ctx.act)
         dx = torch.empty(x2.shape, device=dy.device, dtype=torch.float32) if ctx.needs_input_grad[0] else None

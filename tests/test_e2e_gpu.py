@@ -113,3 +113,20 @@ def test_runner_predict_probs_vs_oracle(int8, tmp_path):
     assert d < (1e-2 if int8 else 5e-3)
     rows = process_batch(r, list(video), list(audio))
     assert [row["top1"]["label"] for row in rows] == [r.labels[i] for i in probs.argmax(1).tolist()]
+
+
+@pytest.mark.parametrize("fusion", ["late", "concat", "gated"])
+def test_non_xattn_train_steps_full_encoders(fusion):
+    """C4 heads with the real encoders (ResNet18 trunk + frozen WavLM, B=2 3 s clips): full train steps run on
+    the HIP path (late: NLL of the averaged softmaxes through both encoder classifiers, train.py:212-214) and
+    the loss decreases on a repeated batch."""
+    from multimodalemotionrecognition_amd.train import TrainStep, build_optimizer, build_model, make_loss
+
+    torch.manual_seed(0)
+    m = build_model(8, fusion, pretrained_video=False, use_wavlm=True).cuda()
+    step = TrainStep(m, build_optimizer(m), make_loss(fusion), fusion)
+    video, audio, labels = OP.clip_inputs(2, seed=4)
+    video, audio, labels = torch.from_numpy(video).cuda(), torch.from_numpy(audio).cuda(), torch.from_numpy(labels).cuda()
+    losses = [float(step(video, audio, labels)[0]) for _ in range(4)]
+    assert all(np.isfinite(losses)), losses
+    assert losses[-1] < losses[0], losses
