@@ -108,6 +108,8 @@ def main():
     ap.add_argument("--no-prefetch", action="store_true",
                     help="run the frozen WavLM inline in every step instead of overlapping the next batch's "
                          "WavLM forward with this step's backward")
+    ap.add_argument("--emotion-prior", action="store_true",
+                    help="xattn with the emotion-prior attention bias (C4 variant, not the headline config)")
     ap.add_argument("--wavlm-unfreeze", type=int, default=0,
                     help="stage-2 fine-tuning step instead (train.py:798-872 two-stage policy): unfreeze the last N "
                          "WavLM layers and the last video block, stage optimizer groups (not the headline config)")
@@ -116,7 +118,8 @@ def main():
     world, rank, local = init_distributed()
     dev = torch.device("cuda", local)
     torch.manual_seed(1234)  # identical init on every rank
-    model = build_model(CLASSES, "xattn", pretrained_video=False, use_wavlm=True).to(dev)
+    prior = dict(xattn_use_emotion_prior=True, forward_emotion_prior_flags=True) if args.emotion_prior else {}
+    model = build_model(CLASSES, "xattn", pretrained_video=False, use_wavlm=True, **prior).to(dev)
     if args.wavlm_unfreeze > 0:
         apply_two_stage_freeze_policy(model, stage=2, unfreeze_wavlm_layers=args.wavlm_unfreeze)
         opt = build_fusion_stage_optimizer(model, stage=2, lr=1e-3, weight_decay=1e-4)

@@ -405,12 +405,24 @@ MER_API int mer_add_ln_bwd(int rows, int d, int rows_per_sample, const float* dy
 // ---------------------------------------------------------------------------------------
 // Mean over dim 1 (TemporalPooler 'mean', temporal.py:108-109): [B,L,D] -> y[b*ldy + c].
 // ---------------------------------------------------------------------------------------
-__global__ void mean_pool_fwd_kernel(int B, int L, int D, const float* __restrict__ x, float* __restrict__ y, long ldy) {
-  const int b = blockIdx.y, c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= D) return;
-  float s = 0.f;
-  for (int l = 0; l < L; ++l) s += x[((long)b * L + l) * D + c];
-  y[(long)b * ldy + c] = s / L;
+// 64 columns x 4 row groups per block, combined in a fixed order (a single thread walking all L rows was a
+// 149-long dependent load chain, ~20 us for the audio pooling)
+__global__ __launch_bounds__(256) void mean_pool_fwd_kernel(int B, int L, int D, const float* __restrict__ x,
+                                                            float* __restrict__ y, long ldy) {
+  __shared__ float part[4][64];
+  const int b = blockIdx.y, el = threadIdx.x & 63, g = threadIdx.x >> 6, c = blockIdx.x * 64 + el;
+  float s0 = 0.f, s1 = 0.f;
+  if (c < D) {
+    int l = g;
+    for (; l + 4 < L; l += 8) {
+      s0 += x[((long)b * L + l) * D + c];
+      s1 += x[((long)b * L + l + 4) * D + c];
+    }
+    if (l < L) s0 += x[((long)b * L + l) * D + c];
+  }
+  part[g][el] = s0 + s1;
+  __syncthreads();
+  if (g == 0 && c < D) y[(long)b * ldy + c] = ((part[0][el] + part[1][el]) + (part[2][el] + part[3][el])) / L;
 }
 __global__ void mean_pool_bwd_kernel(int B, int L, int D, const float* __restrict__ dy, long lddy, float* __restrict__ dx,
                                      int accumulate) {
@@ -423,7 +435,7 @@ __global__ void mean_pool_bwd_kernel(int B, int L, int D, const float* __restric
   }
 }
 MER_API int mer_mean_pool_fwd(int B, int L, int D, const float* x, float* y, long ldy, void* stream) {
-  hipLaunchKernelGGL(mean_pool_fwd_kernel, dim3((D + 127) / 128, B), dim3(128), 0, (hipStream_t)stream, B, L, D, x, y, ldy);
+  hipLaunchKernelGGL(mean_pool_fwd_kernel, dim3((D + 63) / 64, B), dim3(256), 0, (hipStream_t)stream, B, L, D, x, y, ldy);
   MER_LAUNCH_CHECK();
 }
 MER_API int mer_mean_pool_bwd(int B, int L, int D, const float* dy, long lddy, float* dx, int accumulate, void* stream) {
@@ -651,6 +663,58 @@ __global__ __launch_bounds__(256) void token_bias_bwd_kernel(int B, int Lq, int 
     dscale_part[b] = red[1][0] + red[1][1] + red[1][2] + red[1][3];
   }
 }
+// Same sums with g staged once in LDS (Lq*Lk <= TB_LDS): row sums per wave, column sums per thread from LDS --
+// the global-memory version walks a 149-long dependent column loop per thread (a2v: 32 us).
+constexpr int TB_LDS = 4096;
+__global__ __launch_bounds__(256) void token_bias_bwd_lds_kernel(int B, int Lq, int Lk, const float* __restrict__ qt,
+                                                                 const float* __restrict__ qp, const float* __restrict__ kt,
+                                                                 const float* __restrict__ kp, const float* __restrict__ scale,
+                                                                 const float* __restrict__ dbias, float* __restrict__ dqt,
+                                                                 float* __restrict__ dkt, float* __restrict__ dqp,
+                                                                 float* __restrict__ dkp, float* __restrict__ dscale_part) {
+  __shared__ float gs[TB_LDS];
+  __shared__ float red[2][4];
+  const int b = blockIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const float s = *scale, base = qp[b] + kp[b];
+  const float* db = dbias + (long)b * Lq * Lk;
+  float dsc = 0.f;
+  for (int e = threadIdx.x; e < Lq * Lk; e += 256) {
+    const int i = e / Lk, j = e - i * Lk;
+    const float th = tanhf(qt[(long)b * Lq + i] + kt[(long)b * Lk + j] + base);
+    const float d = db[e];
+    gs[e] = d * s * (1.f - th * th);
+    dsc += d * th;
+  }
+  __syncthreads();
+  float tot = 0.f;
+  for (int i = w; i < Lq; i += 4) {
+    float acc = 0.f;
+    for (int j = lane; j < Lk; j += 64) acc += gs[i * Lk + j];
+    acc = wave_sum(acc);
+    if (lane == 0) dqt[(long)b * Lq + i] = acc;
+    tot += lane == 0 ? acc : 0.f;
+  }
+  for (int j = threadIdx.x; j < Lk; j += 256) {
+    float a0 = 0.f, a1 = 0.f;
+    int i = 0;
+    for (; i + 2 <= Lq; i += 2) {
+      a0 += gs[i * Lk + j];
+      a1 += gs[(i + 1) * Lk + j];
+    }
+    if (i < Lq) a0 += gs[i * Lk + j];
+    dkt[(long)b * Lk + j] = a0 + a1;
+  }
+  tot = wave_sum(tot);
+  dsc = wave_sum(dsc);
+  if (lane == 0) { red[0][w] = tot; red[1][w] = dsc; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float tt = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+    dqp[b] = tt;
+    dkp[b] = tt;
+    dscale_part[b] = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+  }
+}
 MER_API int mer_token_bias_fwd(int B, int Lq, int Lk, const float* qt, const float* qp, const float* kt, const float* kp,
                                const float* scale, float* out, void* stream) {
   dim3 grid((Lq * Lk + 255) / 256, B);
@@ -660,8 +724,12 @@ MER_API int mer_token_bias_fwd(int B, int Lq, int Lk, const float* qt, const flo
 MER_API int mer_token_bias_bwd(int B, int Lq, int Lk, const float* qt, const float* qp, const float* kt, const float* kp,
                                const float* scale, const float* dbias, float* dqt, float* dkt, float* dqp, float* dkp,
                                float* dscale_part, void* stream) {
-  hipLaunchKernelGGL(token_bias_bwd_kernel, dim3(B), dim3(256), 0, (hipStream_t)stream, B, Lq, Lk, qt, qp, kt, kp, scale,
-                     dbias, dqt, dkt, dqp, dkp, dscale_part);
+  if ((long)Lq * Lk <= TB_LDS)
+    hipLaunchKernelGGL(token_bias_bwd_lds_kernel, dim3(B), dim3(256), 0, (hipStream_t)stream, B, Lq, Lk, qt, qp, kt, kp,
+                       scale, dbias, dqt, dkt, dqp, dkp, dscale_part);
+  else
+    hipLaunchKernelGGL(token_bias_bwd_kernel, dim3(B), dim3(256), 0, (hipStream_t)stream, B, Lq, Lk, qt, qp, kt, kp,
+                       scale, dbias, dqt, dkt, dqp, dkp, dscale_part);
   MER_LAUNCH_CHECK();
 }
 
