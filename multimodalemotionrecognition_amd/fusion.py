@@ -323,22 +323,40 @@ class FusionModel(nn.Module):
         step updates).  The next ``forward`` whose ``audio`` is this same tensor (same storage, shape and
         version) consumes the result; any other input runs the encoder inline as usual.  Returns whether
         the prefetch was issued (xattn mode with a frozen WavLM encoder only)."""
-        if self.mode not in {"xattn", "xattn_concat", "xattn_gated"}:
-            return False
+        xattn = self.mode in {"xattn", "xattn_concat", "xattn_gated"}
         frozen = self.audio_encoder_frozen()
-        stage2 = (not frozen and hasattr(self.audio_model, "encode_prefix") and torch.is_grad_enabled()
+        stage2 = (xattn and not frozen and hasattr(self.audio_model, "encode_prefix") and torch.is_grad_enabled()
                   and getattr(self.audio_model, "wavlm", None) is not None)
-        if not (frozen or stage2):
+        if not (frozen or stage2) or self.mode not in {"xattn", "xattn_concat", "xattn_gated", "late", "concat",
+                                                       "gated"}:
             return False
         _require_device(audio)
         side = _side_stream(audio.device)
         side.wait_stream(torch.cuda.current_stream(audio.device))
         with torch.cuda.stream(side):
             # stage 2: only the frozen prefix (conv stack + layers below the unfrozen ones) runs ahead; the
-            # trainable layers run in the step itself, after the optimizer has updated them
-            out = self.audio_model.encode_prefix(audio) if stage2 else self.audio_model.encode_sequence(audio)
-        self._prefetched = (_audio_key(audio), out, side, stage2)
+            # trainable layers run in the step itself, after the optimizer has updated them.  late / concat /
+            # gated: the fp32 hidden states their encode() / forward() pool (the pooling and classifier train)
+            if stage2:
+                kind, out = "prefix", self.audio_model.encode_prefix(audio)
+            elif xattn:
+                kind, out = "seq", self.audio_model.encode_sequence(audio)
+            else:
+                kind, out = "hidden", self.audio_model.encode_sequence(audio, out_dtype=torch.float32)
+        self._prefetched = (_audio_key(audio), out, side, kind)
         return True
+
+    def _take_prefetched(self, audio: torch.Tensor, kind: str):
+        """The prefetched result of ``kind`` for exactly this waveform tensor (now ordered after the side stream
+        on the current stream), or None."""
+        pf, self._prefetched = self._prefetched, None
+        if pf is None or pf[0] != _audio_key(audio) or pf[3] != kind:
+            return None
+        cur = torch.cuda.current_stream(audio.device)
+        cur.wait_stream(pf[2])
+        for tsr in (pf[1] if isinstance(pf[1], tuple) else (pf[1],)):
+            tsr.record_stream(cur)
+        return pf[1]
 
     def pop_alignment_loss(self) -> Optional[torch.Tensor]:
         loss = self.alignment_loss
@@ -408,7 +426,8 @@ class FusionModel(nn.Module):
         self.alignment_loss = None
         _require_device(video, audio)
         if self.mode == "late":
-            a_logits = self.audio_model(audio)
+            hidden = self._take_prefetched(audio, "hidden")
+            a_logits = self.audio_model(audio) if hidden is None else self.audio_model(audio, hidden=hidden)
             v_logits = self.video_model(video)
             return EH.late_probs(a_logits, v_logits)
 
@@ -423,20 +442,15 @@ class FusionModel(nn.Module):
             # its GEMMs fill the CUs the trunk's smaller convs and BatchNorm passes leave idle.  When
             # prefetch_audio() already started it for this very batch (during the previous step's
             # backward), its result is taken over instead.
-            pf, self._prefetched = self._prefetched, None
-            if pf is not None and pf[0] == _audio_key(audio) and pf[3] == (not self.audio_encoder_frozen()):
-                side = pf[2]
+            pf = self._prefetched
+            kind = "seq" if self.audio_encoder_frozen() else "prefix"
+            if pf is not None and pf[0] == _audio_key(audio) and pf[3] == kind:
                 v_feat = self.video_model.backbone(v_in).view(b, t, self.v_dim)
-                cur = torch.cuda.current_stream(video.device)
-                cur.wait_stream(side)
-                if pf[3]:  # stage 2: prefetched frozen prefix -> trainable tail now
-                    for tsr in pf[1]:
-                        tsr.record_stream(cur)
-                    a_seq = self.audio_model.encode_sequence(audio, prefix=pf[1])
-                else:
-                    a_seq = pf[1]
-                    a_seq.record_stream(cur)
+                got = self._take_prefetched(audio, kind)
+                # stage 2: prefetched frozen prefix -> trainable tail now
+                a_seq = self.audio_model.encode_sequence(audio, prefix=got) if kind == "prefix" else got
                 return self.xattn_from_features(v_feat, a_seq)
+            self._prefetched = None
             side = _side_stream(video.device) if _OVERLAP_ENCODERS else None
             if side is not None:
                 cur = torch.cuda.current_stream(video.device)
@@ -453,7 +467,8 @@ class FusionModel(nn.Module):
 
         if self.mode not in {"concat", "gated"}:
             raise ValueError(f"Unknown fusion mode: {self.mode}")
-        a_emb = self.audio_model.encode(audio)
+        hidden = self._take_prefetched(audio, "hidden")
+        a_emb = self.audio_model.encode(audio) if hidden is None else self.audio_model.encode(audio, hidden=hidden)
         v_emb = self.video_model.encode(video)
         if self.semantic_alignment is not None:
             raise NotImplementedError("fusion_align_mode='clip' is not on the north-star path")

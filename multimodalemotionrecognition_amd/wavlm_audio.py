@@ -607,15 +607,16 @@ class WavLMAudioEncoder(nn.Module):
         """The frozen part of a stage-2 ``encode_sequence`` (prefetchable; see WavLMBackbone.forward_prefix)."""
         return self.wavlm.forward_prefix(self._wav(x))
 
-    def encode(self, x: torch.Tensor) -> torch.Tensor:
-        hidden = self.encode_sequence(x, out_dtype=torch.float32)
+    def encode(self, x: torch.Tensor, hidden: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """``hidden``: this clip batch's ``encode_sequence(x, fp32)`` computed ahead (FusionModel.prefetch_audio)."""
+        hidden = self.encode_sequence(x, out_dtype=torch.float32) if hidden is None else hidden
         a_emb = self.temporal_pool(hidden)
         if a_emb.size(-1) != self.embedding_dim:
             a_emb = hip_linear(a_emb, self.classifier[0])
         return a_emb
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
-        hidden = self.encode_sequence(x, out_dtype=torch.float32)
+    def forward(self, x: torch.Tensor, hidden: Optional[torch.Tensor] = None) -> torch.Tensor:
+        hidden = self.encode_sequence(x, out_dtype=torch.float32) if hidden is None else hidden
         a_emb = self.temporal_pool(hidden)
         h = hip_linear(a_emb, self.classifier[0], act="relu")
         h = hip_dropout(h, 0.2, self.training)

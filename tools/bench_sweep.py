@@ -30,7 +30,7 @@ for name, fusion, kw in (("late", "late", {}), ("concat", "concat", {}), ("gated
     if kw:  # the reference never forwards the prior flags (train.py:454-469); set the module up explicitly
         assert model.emotion_prior_bias is not None, "emotion prior requested but not built"
     step = TrainStep(model, build_optimizer(model), make_loss(fusion), fusion)
-    nxt = audio if fusion.startswith("xattn") else None
+    nxt = audio  # every fusion mode prefetches the frozen WavLM output of the next batch
     for _ in range(args.warmup):
         step(video, audio, labels, next_audio=nxt)
     torch.cuda.synchronize()
