@@ -85,3 +85,45 @@ def test_single_process_is_noop():
     opt = _FakeOpt([g])
     GradAllReduce(opt)()
     assert torch.equal(g, torch.ones(8)) and opt.grad_scale == 1.0
+
+
+def _worker_groups(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    from multimodalemotionrecognition_amd.dist import GradAllReduce, init_distributed
+    from multimodalemotionrecognition_amd.optim import FusedAdam
+
+    try:
+        init_distributed(backend="gloo")
+        torch.manual_seed(0)
+        a, b = torch.nn.Linear(8, 4), torch.nn.Linear(6, 3)
+        # stage-2 style param groups (train.py:831-872): one flat gradient buffer per group, all all-reduced
+        opt = FusedAdam([{"params": list(a.parameters()), "lr": 1e-3}, {"params": list(b.parameters()), "lr": 1e-5}])
+        flats = opt.flat_grads()
+        for i, f in enumerate(flats):
+            f.copy_(torch.arange(f.numel(), dtype=torch.float32) * (rank + 1) + i)
+        GradAllReduce(opt, bucket_bytes=64)()
+        # sum over ranks of arange * (rank + 1) + i
+        ok = all(torch.equal(f, torch.arange(f.numel(), dtype=torch.float32) * sum(range(1, world + 1)) + i * world)
+                 for i, f in enumerate(flats))
+        q.put((rank, ok, len(flats), abs(opt.grad_scale - 1.0 / world) < 1e-12))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def test_grad_allreduce_stage_groups_world2_gloo():
+    world = 2
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker_groups, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=120)
+    res = sorted(q.get(timeout=10) for _ in range(world))
+    for p in procs:
+        assert p.exitcode == 0
+    for rank, ok, ngroups, ok_scale in res:
+        assert ok and ngroups == 2 and ok_scale, (rank, ok, ngroups, ok_scale)
