@@ -11,8 +11,8 @@ isolates the trainable layers.  Two oracles:
 * pure fp32 (oracle/wavlm_ref.py as is) -- output 1e-2; the gradients that flow through the softmax scores
   (q/k projections, the gate) depend on small differences dp_ij - sum_j p_ij dp_ij of nearly-equal value rows,
   so the bf16 rounding of q/k/v alone moves them by up to ~15% (the matched and the fp32 oracle -- both exact
-  arithmetic -- differ from EACH OTHER by 0.02-0.14 on these gradients at random init, measured on CPU); bar 0.25
-  for those against both oracles, 2e-2 for the rest.  The score-path arithmetic itself is pinned tightly by
+  arithmetic -- differ from EACH OTHER by 0.02-0.14 on these gradients at random init with 2 layers, more with 4);
+  bar max(0.25, 3x that oracle-vs-oracle disagreement on the tensor) against both oracles, 2e-2 for the rest.  The score-path arithmetic itself is pinned tightly by
   test_attention_backward_kernel_vs_fp64 (same bf16 inputs on both sides, fp64 autograd reference)."""
 import numpy as np
 import pytest
@@ -25,7 +25,8 @@ pytestmark = pytest.mark.gpu
 
 REL_RMS_OUT = 1e-2
 REL_RMS_GRAD = 2e-2
-REL_RMS_SCORE_GRAD_FP32 = 0.25  # q/k/gate gradients vs the pure fp32 oracle (see module docstring)
+REL_RMS_SCORE_GRAD_FP32 = 0.25  # q/k/gate gradients vs either oracle (see module docstring) ...
+SCORE_FLOOR_MULT = 3.0  # ... or 3x the two oracles' own disagreement on that tensor, whichever is larger
 SCORE_PATH = ("q_proj", "k_proj", "gru_rel_pos")
 
 
@@ -87,7 +88,7 @@ def _oracle_tail(m, x_bf16, first, G, matched=False):
     return x.detach(), {k: t.grad for k, t in tail.items()}
 
 
-@pytest.mark.parametrize("n_unfrozen", [2])
+@pytest.mark.parametrize("n_unfrozen", [2, 4])
 def test_wavlm_tail_forward_backward_vs_oracle(n_unfrozen):
     m = build_backbone()
     _unfreeze(m, n_unfrozen)
@@ -103,9 +104,14 @@ def test_wavlm_tail_forward_backward_vs_oracle(n_unfrozen):
     (out * G.cuda()).sum().backward()
     torch.cuda.synchronize()
     named = dict(m.named_parameters())
+    oracles = {matched: _oracle_tail(m, x_in, first, G, matched=matched) for matched in (True, False)}
+    # rounding-sensitivity floor of each score-path gradient: how far the two exact-arithmetic oracles, which
+    # differ only in where values are rounded to bf16, land from each other
+    floor = {k: rel_rms(g, oracles[False][1][k].numpy()) for k, g in oracles[True][1].items()
+             if any(sp in k for sp in SCORE_PATH)}
     bad = []
     for matched in (True, False):
-        bad += _compare(named, out, *_oracle_tail(m, x_in, first, G, matched=matched), matched)
+        bad += _compare(named, out, *oracles[matched], matched, floor)
     assert not bad, bad
     # frozen layers and the feature stack get no gradient
     for k, q in named.items():
@@ -113,7 +119,7 @@ def test_wavlm_tail_forward_backward_vs_oracle(n_unfrozen):
             assert q.grad is None, k
 
 
-def _compare(named, out, ref_out, ref_grads, matched):
+def _compare(named, out, ref_out, ref_grads, matched, floor):
     tag = "matched-bf16" if matched else "fp32"
     e = rel_rms(out, ref_out.numpy())
     print(f"[{tag} oracle] tail output rel-rms {e:.2e}")
@@ -135,7 +141,7 @@ def _compare(named, out, ref_out, ref_grads, matched):
             continue
         e = rel_rms(got, g.numpy())
         worst = max(worst, e)
-        bar = REL_RMS_SCORE_GRAD_FP32 if any(sp in k for sp in SCORE_PATH) else REL_RMS_GRAD
+        bar = max(REL_RMS_SCORE_GRAD_FP32, SCORE_FLOOR_MULT * floor[k]) if k in floor else REL_RMS_GRAD
         print(f"  {k:60s} grad rel-rms {e:.2e} (bar {bar:.0e})")
         if e > bar:
             bad.append((tag, k, e))
