@@ -75,6 +75,9 @@ int mer_mha_bwd(int B, int H, int Lq, int Lk, int dh, const float* Q, long ldq, 
                 long lddk, float* dV, long lddv, float* dbias, float scale, float drop_p, const unsigned long long* seed, unsigned long long site,
                 void* stream);
 
+/* Host-side query (no launch): the LDS bytes mer_mha_bwd needs for (Lq, Lk, dh), written to *bytes. */
+int mer_mha_bwd_lds_bytes(int Lq, int Lk, int dh, long* bytes);
+
 /* y = LayerNorm(x + s_b * r) with StochasticDepth scale s_b regenerated from (seed, row/rows_per_sample)
  * (fusion.py:11-26, 284-285, 395, 399).  r may be NULL.  Saves sum/mean/rstd when non-NULL. */
 int mer_add_ln_fwd(int rows, int d, int rows_per_sample, const float* x, const float* r, float dp_p,
@@ -117,6 +120,11 @@ int mer_attn_pool_bwd(int B, int L, int D, const float* x, const float* attn, co
  * image exceeds LDS): dS = P (dPp m - rowsum(P dPp m)), Pd = P m; P [B,H,Lq,Lk], dPp/dS/Pd [B,Lq,Lk]. */
 int mer_softmax_dropout_bwd(int B, int H, int h, int Lq, int Lk, const float* P, const float* dPp, float* dS,
                             float* Pd, float p, const unsigned long long* seed, unsigned long long site, void* stream);
+/* Its forward for head widths the fused mer_mha_fwd does not take (head_dim > 64, the encoders' transformer
+ * pooling at 512 / 768 wide, temporal.py:46-75): S = Q_h K_h^T of head h [B,Lq,Lk] -> P[b,h] = softmax(scale*S)
+ * (pre-dropout, mer_mha_fwd's layout) and Pd = dropout(P) [B,Lq,Lk] with the same mask index. */
+int mer_softmax_dropout_fwd(int B, int H, int h, int Lq, int Lk, const float* S, float scale, float* P, float* Pd,
+                            float p, const unsigned long long* seed, unsigned long long site, void* stream);
 
 /* nn.CrossEntropyLoss(label_smoothing) (train.py:1033) or, late=1, NLLLoss(log(p+1e-8)) (train.py:212-214),
  * mean over the batch, fused with dloss/dlogits (for dloss = 1).  labels are int64. */
@@ -413,6 +421,25 @@ int mer_quantize_weight_s8(int N, int K, const float* w, long ldw, const float* 
 int mer_gemm_i8dyn(int M, int N, int K, const void* x, int x_dtype, long ldx, const float* x_qparams, const void* qw,
                    long ldq, const float* w_qparams, const int* colsum, const float* bias, int act, float* out, long ldo,
                    void* stream);
+
+/* INT8 emotion-prior token-bias input rows (fusion.py:170-176): out[b*L + l] = [tok[b*L + l, :d], prior[b, :pd],
+ * zeros up to ldo] (ldo >= d + pd, a multiple of 16 for mer_gemm_i8dyn). */
+int mer_concat_prior_rows(int B, int L, int d, int pd, int ldo, const float* tok, const float* prior, float* out,
+                          void* stream);
+
+/* ============================ CLIP-style alignment (concat / gated, fusion_align_mode="clip") ============
+ * ClipStyleAlignment.forward after its two projections (fusion.py:137-150): a_n / v_n = F.normalize rows,
+ * logits = min(exp(logit_scale), 100) * a_n v_n^T, loss = (CE(logits, arange) + CE(logits^T, arange)) / 2.
+ * a, v fp32 [B, D]; outputs an, vn [B, D], norms [2B] (max(|x|, 1e-12)), logits [B, B], loss [1]. */
+int mer_clip_align_fwd(int B, int D, const float* a, const float* v, const float* log_scale, float* an, float* vn,
+                       float* norms, float* logits, float* loss, void* stream);
+/* Backward given the device scalar dloss: da, dv [B, D] (written), dlog_scale[0] += dL/dlogit_scale
+ * (NULL: not wanted); ws = B*B floats of workspace. */
+int mer_clip_align_bwd(int B, int D, const float* an, const float* vn, const float* norms, const float* logits,
+                       const float* log_scale, const float* dloss, float* ws, float* da, float* dv, float* dlog_scale,
+                       void* stream);
+/* out[0] = x[0] + w * y[0] (device scalars): train.py:225 loss = cls_loss + fusion_align_weight * align_loss. */
+int mer_add_scaled_scalar(const float* x, const float* y, float w, float* out, void* stream);
 
 #ifdef __cplusplus
 }

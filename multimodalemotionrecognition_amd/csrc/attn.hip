@@ -380,3 +380,10 @@ MER_API int mer_mha_bwd(int B, int H, int Lq, int Lk, int dh, const float* Q, lo
   }
   MER_LAUNCH_CHECK();
 }
+
+// LDS bytes mer_mha_bwd needs for these shapes (callers pick the materialised-score path above 160 KiB)
+MER_API int mer_mha_bwd_lds_bytes(int Lq, int Lk, int dh, long* bytes) {
+  if (Lq <= 0 || Lk <= 0 || dh <= 0 || !bytes) return (int)hipErrorInvalidValue;
+  *bytes = (long)mha_bwd_lds(Lq, Lk, dh);
+  return 0;
+}

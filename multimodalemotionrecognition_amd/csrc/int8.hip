@@ -296,3 +296,29 @@ MER_API int mer_gemm_i8dyn(int M, int N, int K, const void* x, int x_dtype, long
                        ldo);
   return (int)hipGetLastError();
 }
+
+// ---------------------------------------------------------------------------------------------
+// Input rows of the emotion-prior token-bias Linears under INT8 (fusion.py:170-176: the Linear sees
+// cat([token, prior expanded over L]) and quantize_dynamic quantizes that whole concatenated tensor per call):
+// out[(b*L + l), 0:ldo] = [tok[b*L + l, 0:d], prior[b, 0:pd], 0 ...].  The zero tail pads K to a multiple of 16
+// (zeros do not move the activation min/max -- the quantization range always contains 0 -- and meet zero weights).
+__global__ void concat_prior_rows_kernel(int B, int L, int d, int pd, int ldo, const float* __restrict__ tok,
+                                         const float* __restrict__ prior, float* __restrict__ out) {
+  const long n = (long)B * L * ldo;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < n; e += (long)gridDim.x * blockDim.x) {
+    const long r = e / ldo;
+    const int k = (int)(e - r * ldo);
+    const int b = (int)(r / L);
+    out[e] = k < d ? tok[r * d + k] : (k < d + pd ? prior[(long)b * pd + (k - d)] : 0.f);
+  }
+}
+
+MER_API int mer_concat_prior_rows(int B, int L, int d, int pd, int ldo, const float* tok, const float* prior, float* out,
+                                  void* stream) {
+  if (B <= 0 || L <= 0 || ldo < d + pd) return (int)hipErrorInvalidValue;
+  const long n = (long)B * L * ldo;
+  const int grid = (int)((n + 255) / 256 < 2048 ? (n + 255) / 256 : 2048);
+  hipLaunchKernelGGL(concat_prior_rows_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, B, L, d, pd, ldo, tok,
+                     prior, out);
+  MER_LAUNCH_CHECK();
+}

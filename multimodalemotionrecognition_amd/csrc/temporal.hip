@@ -204,3 +204,44 @@ MER_API int mer_softmax_dropout_bwd(int B, int H, int h, int Lq, int Lk, const f
                      Lk, P, dPp, dS, Pd, p, seed, site);
   MER_LAUNCH_CHECK();
 }
+
+// ---------------------------------------------------------------------------------------
+// Materialised-score attention forward for head widths the fused MFMA MHA kernel does not take (head_dim
+// > 64: TemporalPooler('transformer') at the encoders' widths, 512 / 768 with 4 heads, temporal.py:46-75):
+// given S_h = Q_h K_h^T of one head ([B][Lq][Lk], from the batched GEMM), P[b,h] = softmax(scale * S_h) (saved,
+// pre-dropout, the layout mer_mha_fwd writes) and Pd = dropout(P) (the same mask index as mer_mha_fwd /
+// mer_softmax_dropout_bwd: ((b*H + h)*Lq + i)*Lk + j).  One wave per (b, i) row.
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void softmax_dropout_fwd_kernel(int B, int H, int h, int Lq, int Lk,
+                                                                  const float* __restrict__ S, float scale,
+                                                                  float* __restrict__ P, float* __restrict__ Pd, float p,
+                                                                  const unsigned long long* __restrict__ seed_ptr,
+                                                                  unsigned long long site) {
+  const unsigned long long seed = mer_site_seed(seed_ptr, site);
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= B * Lq) return;
+  const int b = row / Lq, i = row - b * Lq;
+  const long pbase = (((long)b * H + h) * Lq + i) * Lk;
+  const long rbase = (long)row * Lk;
+  float m = -INFINITY;
+  for (int j = lane; j < Lk; j += 64) m = fmaxf(m, S[rbase + j] * scale);
+  m = wave_max(m);
+  float s = 0.f;
+  for (int j = lane; j < Lk; j += 64) s += __expf(S[rbase + j] * scale - m);
+  s = wave_sum(s);
+  const float inv = 1.f / s;
+  for (int j = lane; j < Lk; j += 64) {
+    const float pj = __expf(S[rbase + j] * scale - m) * inv;
+    P[pbase + j] = pj;
+    Pd[rbase + j] = pj * dropout_scale(seed, pbase + j, p);
+  }
+}
+MER_API int mer_softmax_dropout_fwd(int B, int H, int h, int Lq, int Lk, const float* S, float scale, float* P,
+                                    float* Pd, float p, const unsigned long long* seed, unsigned long long site,
+                                    void* stream) {
+  if (B <= 0 || Lq <= 0) return 0;
+  if (h < 0 || h >= H || Lk <= 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(softmax_dropout_fwd_kernel, dim3((B * Lq + 3) / 4), dim3(256), 0, (hipStream_t)stream, B, H, h, Lq,
+                     Lk, S, scale, P, Pd, p, seed, site);
+  MER_LAUNCH_CHECK();
+}

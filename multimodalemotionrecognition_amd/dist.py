@@ -1,21 +1,34 @@
 """Data parallelism over RCCL (torch.distributed 'nccl' backend == RCCL on ROCm), one process per GPU.
 
-The reference has no distributed code; this is the north star's DP layer:
-every rank runs the full train step on its own B=32 slice (weak scaling), BatchNorm keeps per-replica
-batch statistics (no SyncBN, like the reference's single-GPU semantics), and the only exchange is a
-SUM all-reduce of the flat fp32 gradient buffer owned by ``FusedAdam`` -- bucketed so each RCCL call
-moves a few tens of MB (xGMI rings are per-link bound; fewer, larger collectives win), with the
-1/world_size averaging folded into the Adam kernel (``grad_scale``) instead of an extra pass.
+The reference has no distributed code; this is the north star's DP layer
+(SURVEY.md section 8(e)): every rank runs the full train step on its own B=32 slice (weak scaling),
+BatchNorm keeps per-replica batch statistics (no SyncBN, like the reference's single-GPU semantics),
+and the only data-path exchange is a SUM all-reduce of ``FusedAdam``'s flat fp32 gradient buffers.
+
+* Only the USED trainables are in those buffers (``train.build_optimizer`` leaves out parameters the
+  selected fusion mode never reaches, e.g. ``audio_time_conv`` and the encoders' classifiers under
+  xattn), so no zeros cross xGMI.
+* The buffers are laid out in backward order (head first, then ResNet18 layer4, layer3, ...): the
+  bucket holding the head + layer4 gradients (~35 MB of the 46 MB) is launched as soon as the trunk's
+  layer4 backward has been enqueued (``ResNet18Trunk`` calls the registered ready-hook between its two
+  backward graphs), so its all-reduce runs on RCCL's stream while layer3..stem are still computing;
+  the remaining ~11 MB go out after the backward.  1/world_size is folded into the Adam kernel
+  (``grad_scale``) instead of an extra pass.
+* Which parameters count as "having a gradient" this step is the union over ranks (gated-mode
+  ModalityDropout and stage-2 LayerDrop leave some ``.grad`` None on some ranks): a host-side
+  all-reduce of the per-parameter flags over a gloo group, as DDP does for unused parameters --
+  host-to-host only, the GPU queue is not synchronised.
 """
 from __future__ import annotations
 
 import os
-from typing import List
+from typing import List, Optional, Tuple
 
 import torch
 import torch.distributed as dist
 
 BUCKET_BYTES = 32 << 20
+_CPU_GROUP = None
 
 
 def env_world():
@@ -37,26 +50,93 @@ def is_dist() -> bool:
     return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
 
 
+def cpu_group():
+    """A gloo group over the same ranks for small host-side collectives (created once)."""
+    global _CPU_GROUP
+    if _CPU_GROUP is None:
+        _CPU_GROUP = dist.group.WORLD if dist.get_backend() == "gloo" else dist.new_group(backend="gloo")
+    return _CPU_GROUP
+
+
 def buckets(flat: torch.Tensor, bucket_bytes: int = BUCKET_BYTES) -> List[torch.Tensor]:
     n = max(1, bucket_bytes // flat.element_size())
     return [flat[i:i + n] for i in range(0, flat.numel(), n)]
 
 
-class GradAllReduce:
-    """SUM all-reduce of the optimizer's flat gradient buckets; Adam then applies 1/world."""
+def _ranges(lo: int, hi: int, n: int) -> List[Tuple[int, int]]:
+    return [(i, min(hi, i + n)) for i in range(lo, hi, n)]
 
-    def __init__(self, optimizer, bucket_bytes: int = BUCKET_BYTES):
+
+class GradAllReduce:
+    """Bucketed SUM all-reduce of the optimizer's flat gradient buffers; Adam then applies 1/world.
+
+    ``model``: when given, parameters and buffers are broadcast from rank 0 once (identical replicas
+    before step 0), and the model's early-gradient hook (``register_grad_ready_hook``) is used to start
+    the head + layer4 bucket while the rest of the backward runs.  ``mask_sync``: union the per-parameter
+    "has a gradient" flags over ranks (default: ask the model whether some step can leave a trainable
+    parameter without a gradient)."""
+
+    def __init__(self, optimizer, bucket_bytes: int = BUCKET_BYTES, model: Optional[torch.nn.Module] = None,
+                 mask_sync: Optional[bool] = None):
         self.opt = optimizer
         self.bucket_bytes = bucket_bytes
         self.world = dist.get_world_size() if is_dist() else 1
         optimizer.grad_scale = 1.0 / self.world
+        self._pending = []      # async works launched this step
+        self._done = {}         # group index -> flat elements already launched (prefix)
+        if mask_sync is None:
+            mask_sync = bool(getattr(model, "may_skip_grads", lambda: True)()) if model is not None else True
+        self.mask_sync = mask_sync
+        if model is not None and self.world > 1:
+            broadcast_module(model)
+            with torch.no_grad():  # re-homed trainables: one broadcast per flat buffer
+                for f in optimizer.flat_params():
+                    dist.broadcast(f, 0)
+        if model is not None and hasattr(model, "register_grad_ready_hook"):
+            model.register_grad_ready_hook(self.grads_ready)
 
-    def __call__(self) -> None:
+    def _launch(self, gi: int, flat: torch.Tensor, lo: int, hi: int) -> None:
+        n = max(1, self.bucket_bytes // flat.element_size())
+        for a, b in _ranges(lo, hi, n):
+            self._pending.append(dist.all_reduce(flat[a:b], op=dist.ReduceOp.SUM, async_op=True))
+
+    def grads_ready(self, params) -> None:
+        """Early hook: ``params`` have their final local gradients in the flat buffers (enqueued on the current
+        stream).  Launches the longest flat-buffer PREFIX made of ready parameters."""
         if self.world == 1:
             return
-        for flat in self.opt.flat_grads():
-            for b in buckets(flat, self.bucket_bytes):
-                dist.all_reduce(b, op=dist.ReduceOp.SUM)
+        ready = {id(p) for p in params}
+        ends, stopped = {}, set()
+        for gi, p, o, n in self.opt.param_slices():
+            if gi in stopped:
+                continue
+            if id(p) in ready:
+                ends[gi] = o + (n + 3) // 4 * 4
+            else:
+                stopped.add(gi)
+        for gi, flat in enumerate(self.opt.flat_grads()):
+            end, start = ends.get(gi, 0), self._done.get(gi, 0)
+            if end > start:
+                self._launch(gi, flat, start, end)
+                self._done[gi] = end
+
+    def __call__(self) -> None:
+        used = self.opt.gather_grads()
+        if self.world == 1:
+            self._done = {}
+            return
+        if self.mask_sync:
+            flags = torch.tensor([int(u) for g in used for u in g], dtype=torch.int32)
+            dist.all_reduce(flags, op=dist.ReduceOp.MAX, group=cpu_group())
+            it = iter(flags.tolist())
+            self.opt.set_used([[bool(next(it)) for _ in g] for g in used])
+        for gi, flat in enumerate(self.opt.flat_grads()):
+            start = self._done.get(gi, 0)
+            if start < flat.numel():
+                self._launch(gi, flat, start, flat.numel())
+        for w in self._pending:
+            w.wait()
+        self._pending, self._done = [], {}
 
 
 @torch.no_grad()

@@ -69,6 +69,13 @@ class _EmbHeadFn(torch.autograd.Function):
         used = ["audio_proj.weight", "audio_proj.bias", "video_proj.weight", "video_proj.bias"]
         used += (["fusion.0.weight", "fusion.0.bias", "fusion.3.weight", "fusion.3.bias"] if ctx.mode == "concat" else
                  ["gate.0.weight", "gate.0.bias", "gate.3.weight", "gate.3.bias", "classifier.weight", "classifier.bias"])
+        drop_a, drop_v = ctx.drops
+        # a dropped modality's projection output was replaced by zeros (fusion.py:47-53 zeros_like): it and its
+        # encoder get no gradient at all (None, not zeros), so torch Adam's skip rule applies to them
+        if drop_a:
+            used = [n for n in used if not n.startswith("audio_proj.")]
+        if drop_v:
+            used = [n for n in used if not n.startswith("video_proj.")]
         grads = {n: _grad_buf(p[n]) for n in used}
         cat = sv["cat"]
         cd = cat.shape[1] // 2
@@ -92,17 +99,15 @@ class _EmbHeadFn(torch.autograd.Function):
             K.relu_dropout_bwd_(dh, h, ctx.dp, ctx.rng, SITE_EMB_MLP)
             K.linear_bwd(cat, p["gate.0.weight"], dh, dx=dcat, dw=grads["gate.0.weight"], db=grads["gate.0.bias"],
                          dx_beta=1)
-        if ctx.drops[0]:
-            dcat[:, :cd].zero_()
-        if ctx.drops[1]:
-            dcat[:, cd:].zero_()
-        need_a, need_v = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        need_a, need_v = ctx.needs_input_grad[0] and not drop_a, ctx.needs_input_grad[1] and not drop_v
         da = e(*ctx.a_emb.shape) if need_a else None
         dv = e(*ctx.v_emb.shape) if need_v else None
-        K.linear_bwd(ctx.a_emb, p["audio_proj.weight"], dcat[:, :cd], dx=da, dw=grads["audio_proj.weight"],
-                     db=grads["audio_proj.bias"])
-        K.linear_bwd(ctx.v_emb, p["video_proj.weight"], dcat[:, cd:], dx=dv, dw=grads["video_proj.weight"],
-                     db=grads["video_proj.bias"])
+        if not drop_a:
+            K.linear_bwd(ctx.a_emb, p["audio_proj.weight"], dcat[:, :cd], dx=da, dw=grads["audio_proj.weight"],
+                         db=grads["audio_proj.bias"])
+        if not drop_v:
+            K.linear_bwd(ctx.v_emb, p["video_proj.weight"], dcat[:, cd:], dx=dv, dw=grads["video_proj.weight"],
+                         db=grads["video_proj.bias"])
         out = [grads.get(n) if (n in grads and t.requires_grad) else None for n, t in zip(ctx.names, ctx.params)]
         return (da, dv, None, None, None, None, None, None, None, *out)
 
@@ -115,7 +120,10 @@ def embedding_head(model, a_emb, v_emb, drop_a=False, drop_v=False):
         names.append(n)
         params.append(q)
     rng = model.step_rng(a_emb.device) if model.training else None
-    return _EmbHeadFn.apply(a_emb.contiguous(), v_emb.contiguous(), model.mode, model.training, rng,
+    # a dropped modality is cut from the autograd graph (its encoder's backward never runs, as in the reference)
+    a_in = a_emb.detach() if drop_a else a_emb
+    v_in = v_emb.detach() if drop_v else v_emb
+    return _EmbHeadFn.apply(a_in.contiguous(), v_in.contiguous(), model.mode, model.training, rng,
                             bool(drop_a), bool(drop_v), int8_images(model), tuple(names), *params)
 
 

@@ -21,6 +21,7 @@ from . import embedding_head as EH
 from . import graphs as G
 from . import kernels as K
 from . import xattn_head as XH
+from .nn_ops import hip_linear
 from .temporal import TemporalPooler
 
 
@@ -42,10 +43,6 @@ def _side_stream(device: torch.device):
     if s is None:
         s = _SIDE_STREAMS[idx] = torch.cuda.Stream(device=idx)
     return s
-
-
-def _audio_key(audio: torch.Tensor) -> tuple:
-    return (audio.data_ptr(), audio._version, tuple(audio.shape), audio.dtype)
 
 
 def _next_seed() -> int:
@@ -75,8 +72,35 @@ class ModalityDropout(nn.Module):
         return (torch.rand(1).item() < self.audio_dropout_p, torch.rand(1).item() < self.video_dropout_p)
 
 
+class _ClipLossFn(torch.autograd.Function):
+    """Symmetric CLIP loss of fusion.py:141-149 on csrc/align.hip (one workgroup, exact fp32)."""
+
+    @staticmethod
+    def forward(ctx, a_al, v_al, logit_scale):
+        a_al, v_al = a_al.contiguous().float(), v_al.contiguous().float()
+        B, D = a_al.shape
+        an, vn = torch.empty_like(a_al), torch.empty_like(v_al)
+        norms = torch.empty(2 * B, device=a_al.device, dtype=torch.float32)
+        logits = torch.empty(B, B, device=a_al.device, dtype=torch.float32)
+        loss = torch.empty((), device=a_al.device, dtype=torch.float32)
+        K.clip_align_fwd(a_al, v_al, logit_scale.detach().reshape(1), an, vn, norms, logits, loss)
+        ctx.sv = (an, vn, norms, logits)
+        ctx.logit_scale = logit_scale
+        return loss
+
+    @staticmethod
+    def backward(ctx, dloss):
+        an, vn, norms, logits = ctx.sv
+        da, dv = torch.empty_like(an), torch.empty_like(vn)
+        ls = ctx.logit_scale
+        dls = grad_buffer(ls) if ctx.needs_input_grad[2] else None
+        K.clip_align_bwd(an, vn, norms, logits, ls.detach().reshape(1), dloss.contiguous().float().reshape(1), da, dv,
+                         dls.view(1) if dls is not None else None)
+        return da, dv, dls
+
+
 class ClipStyleAlignment(nn.Module):
-    """fusion.py:127-150 (parameters only; the alignment loss path is not on the north-star path)."""
+    """fusion.py:127-150: project audio / video embeddings into a shared space + symmetric CLIP loss."""
 
     def __init__(self, audio_dim: int, video_dim: int, align_dim: int, init_temperature: float = 0.07) -> None:
         super().__init__()
@@ -84,6 +108,13 @@ class ClipStyleAlignment(nn.Module):
         self.video_proj = nn.Linear(video_dim, align_dim)
         safe_temp = max(float(init_temperature), 1e-3)
         self.logit_scale = nn.Parameter(torch.tensor(math.log(1.0 / safe_temp), dtype=torch.float32))
+
+    def forward(self, audio_emb: torch.Tensor, video_emb: torch.Tensor):
+        """-> (a_aligned, v_aligned, loss), as fusion.py:137-150."""
+        _require_device(audio_emb, video_emb)
+        a_aligned = hip_linear(audio_emb, self.audio_proj)
+        v_aligned = hip_linear(video_emb, self.video_proj)
+        return a_aligned, v_aligned, _ClipLossFn.apply(a_aligned, v_aligned, self.logit_scale)
 
 
 class EmotionPriorBiasAdapter(nn.Module):
@@ -131,6 +162,8 @@ class _XattnHeadFn(torch.autograd.Function):
         p = dict(zip(names, params))
         if runner is not None:
             logits, hctx = runner.forward(v_feat, a_seq)
+            ctx.gen = runner.cur_gen
+            ctx.token = runner.token(ctx.gen)
         else:
             logits, hctx = XH.head_forward(p, cfg, v_feat, a_seq, training, rng)
         ctx.hctx, ctx.names, ctx.params, ctx.runner = hctx, names, params, runner
@@ -150,12 +183,12 @@ class _XattnHeadFn(torch.autograd.Function):
             grads = _head_grads(p, ctx.used)
             dv, da = XH.head_backward(p, ctx.hctx, dl, grads, need_dv_feat=need_v, need_da_seq=need_a)
         if ctx.runner is not None:
-            ctx.runner.pending = False
+            ctx.runner.release(ctx.gen)
         out_grads = [grads.get(n) if (n in ctx.used and t.requires_grad) else None for n, t in p.items()]
         return (dv, da, None, None, None, None, None, *out_grads)
 
 
-class _HeadGraphs:
+class _HeadGraphs(G.PendingGuard):
     """Captured forward / backward hipGraphs of the xattn head for one input shape (graphs.py).
 
     The dropout / drop-path masks stay random per step: the graph's RNG base is a static device scalar that
@@ -166,9 +199,10 @@ class _HeadGraphs:
     """
 
     def __init__(self, model, names, cfg, training):
+        super().__init__()
         self.model, self.names, self.cfg, self.training = model, names, cfg, training
         self.fwd = self.bwd = None
-        self.pending = False
+        self.cur_gen = 0
         self.rng = None
 
     def forward(self, v_feat, a_seq):
@@ -333,6 +367,8 @@ class FusionModel(nn.Module):
         _require_device(audio)
         side = _side_stream(audio.device)
         side.wait_stream(torch.cuda.current_stream(audio.device))
+        # the side stream reads `audio`: keep its block from being recycled to the main stream while it does
+        audio.record_stream(side)
         with torch.cuda.stream(side):
             # stage 2: only the frozen prefix (conv stack + layers below the unfrozen ones) runs ahead; the
             # trainable layers run in the step itself, after the optimizer has updated them.  late / concat /
@@ -343,20 +379,66 @@ class FusionModel(nn.Module):
                 kind, out = "seq", self.audio_model.encode_sequence(audio)
             else:
                 kind, out = "hidden", self.audio_model.encode_sequence(audio, out_dtype=torch.float32)
-        self._prefetched = (_audio_key(audio), out, side, kind)
+        # the tensor itself (not its address) identifies the batch: a recycled address cannot match
+        self._prefetched = (audio, audio._version, out, side, kind)
         return True
+
+    def _prefetch_matches(self, audio: torch.Tensor, kind: str) -> bool:
+        pf = self._prefetched
+        return pf is not None and pf[0] is audio and pf[1] == audio._version and pf[4] == kind
 
     def _take_prefetched(self, audio: torch.Tensor, kind: str):
         """The prefetched result of ``kind`` for exactly this waveform tensor (now ordered after the side stream
         on the current stream), or None."""
+        ok = self._prefetch_matches(audio, kind)
         pf, self._prefetched = self._prefetched, None
-        if pf is None or pf[0] != _audio_key(audio) or pf[3] != kind:
+        if not ok:
             return None
+        pf = (None, pf[2], pf[3], pf[4])
         cur = torch.cuda.current_stream(audio.device)
         cur.wait_stream(pf[2])
         for tsr in (pf[1] if isinstance(pf[1], tuple) else (pf[1],)):
             tsr.record_stream(cur)
         return pf[1]
+
+    # ---- data-parallel support (dist.GradAllReduce) ----
+    def unused_parameters(self):
+        """Trainable parameters the configured mode never reaches in forward, so they never get a gradient
+        (torch's Adam skips them forever): kept out of the optimizer's flat buffers and the all-reduce."""
+        dead = []
+        xattn = self.mode in {"xattn", "xattn_concat", "xattn_gated"}
+        if xattn:
+            dead += list(self.audio_time_conv.parameters())  # fusion.py:273, mel fallback only
+        if self.mode != "late":
+            # the encoders' own classifier heads are only used by late fusion (and audio/video-only models)
+            for enc in (self.audio_model, self.video_model):
+                cls = getattr(enc, "classifier", None)
+                if cls is None:
+                    continue
+                if enc is self.audio_model and not xattn and getattr(enc, "embedding_dim", 768) != enc.sequence_dim:
+                    dead += list(cls[3].parameters())  # encode() uses classifier[0] when the dims differ
+                else:
+                    dead += list(cls.parameters())
+            if xattn:  # the backbone / encode_sequence are called directly: the encoders' poolers are unused
+                for enc in (self.audio_model, self.video_model):
+                    tp = getattr(enc, "temporal_pool", None)
+                    if tp is not None:
+                        dead += list(tp.parameters())
+        return dead
+
+    def may_skip_grads(self) -> bool:
+        """True when some step can leave a used trainable parameter without a gradient (gated ModalityDropout;
+        WavLM LayerDrop over trainable encoder layers): the data-parallel "has a gradient" set is then synced."""
+        wav = getattr(self.audio_model, "wavlm", None)
+        return self.mode == "gated" or (wav is not None and wav.trainable())
+
+    def register_grad_ready_hook(self, fn) -> None:
+        """``fn(params)`` is called from the backward as soon as the head's and the ResNet18 layer4 gradients are
+        final (enqueued): the early all-reduce bucket (dist.GradAllReduce)."""
+        trunk = self.video_model.backbone
+        head = [q for n, q in self.named_parameters() if not n.startswith(("audio_model.", "video_model."))]
+        vid_head = [q for n, q in self.video_model.named_parameters() if not n.startswith("backbone.")]
+        trunk.grad_ready_hook = lambda ps: fn(head + vid_head + list(ps))
 
     def pop_alignment_loss(self) -> Optional[torch.Tensor]:
         loss = self.alignment_loss
@@ -419,7 +501,7 @@ class FusionModel(nn.Module):
             r = self._head_graphs.put(key, _HeadGraphs(self, names, cfg, self.training))
         if r.pending:
             return None
-        r.pending = torch.is_grad_enabled()
+        r.cur_gen = r.claim(torch.is_grad_enabled())
         return r
 
     def forward(self, video: torch.Tensor, audio: torch.Tensor):
@@ -442,9 +524,8 @@ class FusionModel(nn.Module):
             # its GEMMs fill the CUs the trunk's smaller convs and BatchNorm passes leave idle.  When
             # prefetch_audio() already started it for this very batch (during the previous step's
             # backward), its result is taken over instead.
-            pf = self._prefetched
             kind = "seq" if self.audio_encoder_frozen() else "prefix"
-            if pf is not None and pf[0] == _audio_key(audio) and pf[3] == kind:
+            if self._prefetch_matches(audio, kind):
                 v_feat = self.video_model.backbone(v_in).view(b, t, self.v_dim)
                 got = self._take_prefetched(audio, kind)
                 # stage 2: prefetched frozen prefix -> trainable tail now
@@ -470,7 +551,9 @@ class FusionModel(nn.Module):
         hidden = self._take_prefetched(audio, "hidden")
         a_emb = self.audio_model.encode(audio) if hidden is None else self.audio_model.encode(audio, hidden=hidden)
         v_emb = self.video_model.encode(video)
-        if self.semantic_alignment is not None:
-            raise NotImplementedError("fusion_align_mode='clip' is not on the north-star path")
+        if self.semantic_alignment is not None:  # fusion.py:417-418
+            a_emb, v_emb, self.alignment_loss = self.semantic_alignment(a_emb, v_emb)
+        # gated: ModalityDropout (fusion.py:430) replaces a projection by zeros_like -- the dropped branch and
+        # everything feeding only it get NO gradient (torch's Adam then skips them), see embedding_head
         drop_a, drop_v = self.modality_dropout.draw() if self.mode == "gated" else (False, False)
         return EH.embedding_head(self, a_emb, v_emb, drop_a, drop_v)

@@ -75,6 +75,40 @@ class GraphCache:
         return g
 
 
+class PendingGuard:
+    """Bookkeeping for a captured forward graph whose static activations a later backward graph reads.
+
+    ``claim()`` marks a forward as in flight (returns its generation); a second forward while one is in
+    flight must run eagerly.  The in-flight mark is released by the backward (``release(gen)``) or, when the
+    forward's autograd graph is dropped without a backward (a modality cut by ModalityDropout, an evaluation
+    forward under grad mode), by the token the forward stored in its autograd context."""
+
+    def __init__(self):
+        self.pending = 0
+        self._gen = 0
+
+    def claim(self, want_backward: bool) -> int:
+        self._gen += 1
+        if want_backward:
+            self.pending = self._gen
+        return self._gen
+
+    def release(self, gen: int) -> None:
+        if self.pending == gen:
+            self.pending = 0
+
+    def token(self, gen: int):
+        return _PendingToken(self, gen)
+
+
+class _PendingToken:
+    def __init__(self, guard: PendingGuard, gen: int):
+        self.guard, self.gen = guard, gen
+
+    def __del__(self):
+        self.guard.release(self.gen)
+
+
 def module_tensors(module: torch.nn.Module) -> list:
     """Every parameter and buffer of ``module``, listed once per module (the module tree is fixed after
     construction; tensors are re-homed in place by .to() / FusedAdam, so the Python objects stay valid)."""

@@ -27,12 +27,13 @@ class QuantizedLinear:
         if not w.is_cuda:
             raise RuntimeError("quantize on the device: move the model to 'cuda' first")
         N, Kd = w.shape
-        if Kd % 16:
-            raise NotImplementedError(f"INT8 Linear needs in_features % 16 == 0 (got {Kd})")
         dev = w.device
         self.in_features, self.out_features = Kd, N
+        # K padded to the i8 MFMA's multiple of 16 with zero weights; callers with in_features % 16 != 0 pass
+        # zero-padded input rows of width in_padded (the emotion-prior token-bias Linears, K = 136)
+        self.in_padded = (Kd + 15) // 16 * 16
         self.wqp = torch.empty(4, device=dev)
-        self.qw = torch.empty(N, Kd, device=dev, dtype=torch.int8)
+        self.qw = torch.empty(N, self.in_padded, device=dev, dtype=torch.int8)
         self.colsum = torch.empty(N, device=dev, dtype=torch.int32)
         self._part = torch.empty(K.QP_PARTIAL, device=dev)
         self.xqp = torch.empty(4, device=dev)
@@ -42,6 +43,8 @@ class QuantizedLinear:
 
     def __call__(self, x2d: torch.Tensor, out: torch.Tensor, act: str = "none") -> torch.Tensor:
         x2d = x2d.contiguous()
+        if x2d.shape[1] != self.in_padded:
+            raise ValueError(f"INT8 Linear expects rows of {self.in_padded} (zero-padded) features, got {x2d.shape[1]}")
         K.quant_params(x2d, self._part, self.xqp, mode=0)
         return K.gemm_i8dyn(x2d, self.xqp, self.qw, self.wqp, self.colsum, self.bias, out, act=act)
 
@@ -56,10 +59,9 @@ def quantizable_linears(model: nn.Module) -> Dict[str, nn.Linear]:
 
 
 def quantize_dynamic_hip(model: nn.Module) -> Dict[str, QuantizedLinear]:
-    """Attach int8 images of the head's Linears to ``model`` (``model._mer_int8``); returns them."""
-    if getattr(model, "emotion_prior_bias", None) is not None:
-        raise NotImplementedError("INT8 with the emotion-prior adapter is not implemented (the reference's "
-                                  "build_model never enables the prior, train.py:454-469)")
+    """Attach int8 images of the head's Linears to ``model`` (``model._mer_int8``); returns them.  With the
+    emotion-prior adapter this includes ``prior_net.0/3`` and the four token-bias Linears (their concatenated
+    [token; prior] input is quantized as one tensor, as quantize_dynamic does)."""
     q = {n: QuantizedLinear(m) for n, m in quantizable_linears(model).items()}
     model._mer_int8 = q
     return q

@@ -710,3 +710,55 @@ def transpose_bf16(src, dst):
     if src.dtype != torch.bfloat16 or dst.dtype != torch.bfloat16 or tuple(dst.shape) != (cols, rows):
         raise ValueError("transpose_bf16 shapes")
     LIB("mer_transpose_bf16", rows, cols, src.data_ptr(), src.stride(0), dst.data_ptr(), dst.stride(0), stream_ptr())
+
+
+# ---------------------------------------------------------------------------------------------------
+# CLIP-style alignment loss (csrc/align.hip)
+def clip_align_fwd(a, v, log_scale, an, vn, norms, logits, loss):
+    B, D = a.shape
+    for t in (a, v, an, vn):
+        if t.dtype != torch.float32 or not t.is_contiguous() or tuple(t.shape) != (B, D):
+            raise ValueError("clip_align_fwd: contiguous fp32 [B, D] operands expected")
+    if norms.numel() != 2 * B or logits.numel() != B * B or loss.numel() != 1 or log_scale.numel() != 1:
+        raise ValueError("clip_align_fwd: norms [2B], logits [B, B], loss [1], log_scale [1]")
+    _check_dev(a, v, log_scale, an, vn, norms, logits, loss)
+    LIB("mer_clip_align_fwd", B, D, a.data_ptr(), v.data_ptr(), log_scale.data_ptr(), an.data_ptr(), vn.data_ptr(),
+        norms.data_ptr(), logits.data_ptr(), loss.data_ptr(), stream_ptr())
+
+
+def clip_align_bwd(an, vn, norms, logits, log_scale, dloss, da, dv, dlog_scale=None):
+    B, D = an.shape
+    if tuple(da.shape) != (B, D) or tuple(dv.shape) != (B, D) or not (da.is_contiguous() and dv.is_contiguous()):
+        raise ValueError("clip_align_bwd: da / dv must be contiguous [B, D]")
+    ws = _workspace(B * B, an.device)
+    LIB("mer_clip_align_bwd", B, D, an.data_ptr(), vn.data_ptr(), norms.data_ptr(), logits.data_ptr(),
+        log_scale.data_ptr(), dloss.data_ptr(), ws.data_ptr(), da.data_ptr(), dv.data_ptr(), _ptr(dlog_scale),
+        stream_ptr())
+
+
+def add_scaled_scalar(x, y, w, out):
+    LIB("mer_add_scaled_scalar", x.data_ptr(), y.data_ptr(), float(w), out.data_ptr(), stream_ptr())
+
+
+def concat_prior_rows(tok, prior, out, L):
+    """out[b*L + l] = [tok[b*L + l], prior[b], 0 ...] (INT8 token-bias input rows)."""
+    rows, d = tok.shape
+    B, pd = prior.shape
+    if rows != B * L or out.shape[0] != rows or out.shape[1] < d + pd or not out.is_contiguous():
+        raise ValueError("concat_prior_rows shapes")
+    LIB("mer_concat_prior_rows", B, L, d, pd, out.shape[1], tok.contiguous().data_ptr(), prior.contiguous().data_ptr(),
+        out.data_ptr(), stream_ptr())
+    return out
+
+
+def softmax_dropout_fwd(S, scale, P, Pd, h, p=0.0, rng=None, site=0):
+    B, H, Lq, Lk = P.shape
+    LIB("mer_softmax_dropout_fwd", B, H, int(h), Lq, Lk, S.data_ptr(), float(scale), P.data_ptr(), Pd.data_ptr(),
+        float(p), rng_ptr(rng), int(site), stream_ptr())
+
+
+def mha_bwd_lds_bytes(Lq: int, Lk: int, dh: int) -> int:
+    import ctypes
+    out = ctypes.c_long(0)
+    LIB("mer_mha_bwd_lds_bytes", int(Lq), int(Lk), int(dh), ctypes.addressof(out))
+    return int(out.value)

@@ -41,3 +41,26 @@ class LateNLLLoss(nn.Module):
 
     def forward(self, probs: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
         return _CEFn.apply(probs, labels, 0.0, True)
+
+
+class _AddScaledFn(torch.autograd.Function):
+    """out = x + w * y over 0-d device losses (train.py:225: cls_loss + fusion_align_weight * align_loss)."""
+
+    @staticmethod
+    def forward(ctx, x, y, w):
+        out = torch.empty((), device=x.device, dtype=torch.float32)
+        K.add_scaled_scalar(x.contiguous().float(), y.contiguous().float(), w, out)
+        ctx.w = float(w)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        g = g.contiguous().float().reshape(())
+        gy = torch.empty((), device=g.device, dtype=torch.float32)
+        zero = torch.zeros((), device=g.device, dtype=torch.float32)
+        K.add_scaled_scalar(zero, g, ctx.w, gy)  # d/dy = w * g
+        return g, gy, None
+
+
+def add_scaled(x: torch.Tensor, y: torch.Tensor, w: float) -> torch.Tensor:
+    return _AddScaledFn.apply(x, y, float(w))

@@ -97,11 +97,10 @@ def _attn_pool_bwd(p, pfx, sv, dy, grads, drop, rng, site):
 # ---------------------------------------------------------------------------------------------
 def _mha_bwd(q, k, v, P, do, dq, dk, dv, B, H, L, drop, rng, site):
     dh = do.shape[1] // H
-    try:
+    # the fused kernel's LDS image must fit in 160 KiB (mer.h mer_mha_bwd)
+    if fused_mha_ok(L, dh) and K.mha_bwd_lds_bytes(L, L, dh) <= 160 * 1024:
         K.mha_bwd(q, k, v, P, do, dq, dk, dv, None, B, H, L, L, drop, rng, site)
         return
-    except Exception:  # noqa: BLE001 -- LDS image too large for the fused kernel: materialise per head
-        pass
     scale = dh ** -0.5
     dpp, ds, pd = _e((B, L, L), q), _e((B, L, L), q), _e((B, L, L), q)
     sc = torch.full((1,), scale, device=q.device, dtype=torch.float32)
@@ -119,6 +118,29 @@ def _mha_bwd(q, k, v, P, do, dq, dk, dv, B, H, L, drop, rng, site):
                        bsb=L * do.stride(0), ldc=dv.stride(0), bsc=L * dv.stride(0), batch=B)
 
 
+def fused_mha_ok(L: int, dh: int) -> bool:
+    """Shapes the fused MFMA MHA kernels (attn.hip) take: head_dim % 4 == 0, <= 64, L <= 256."""
+    return dh % 4 == 0 and dh <= 64 and L <= 256
+
+
+def _mha_fwd(q, k, v, o, P, B, H, L, drop, rng, site):
+    """Self-attention core; the materialised-score path (batched f32 MFMA GEMMs + a softmax/dropout pass per head)
+    for head widths > 64 -- the encoders' transformer pooling (512 / 768 wide, 4 heads: head_dim 128 / 192)."""
+    D = o.shape[1]
+    dh = D // H
+    if fused_mha_ok(L, dh):
+        K.mha_fwd(q, k, v, None, o, P, B, H, L, L, drop, rng, site)
+        return
+    S, Pd = _e((B, L, L), q), _e((B, L, L), q)
+    for h in range(H):
+        c = h * dh
+        K.gemm_batched(q[:, c:], k[:, c:], S, M=L, N=L, K=dh, sam=q.stride(0), sak=1, bsa=L * q.stride(0),
+                       sbk=1, sbn=k.stride(0), bsb=L * k.stride(0), ldc=L, bsc=L * L, batch=B)
+        K.softmax_dropout_fwd(S, dh ** -0.5, P, Pd, h, drop, rng, site)
+        K.gemm_batched(Pd, v[:, c:], o[:, c:], M=L, N=dh, K=L, sam=L, sak=1, bsa=L * L, sbk=v.stride(0), sbn=1,
+                       bsb=L * v.stride(0), ldc=o.stride(0), bsc=L * o.stride(0), batch=B)
+
+
 # ---------------------------------------------------------------------------------------------
 # transformer pooling
 # ---------------------------------------------------------------------------------------------
@@ -129,7 +151,7 @@ def _layer_fwd(p, ln, x, B, L, H, drop, rng, site):
     K.add_ln_fwd(x, None, p[ln + ".norm1.weight"], p[ln + ".norm1.bias"], h1, None, m1, r1, L)
     qkv = K.linear_fwd(h1, p[ln + ".self_attn.in_proj_weight"], p[ln + ".self_attn.in_proj_bias"], _e((rows, 3 * D), x))
     o, P = _e((rows, D), x), _e((B, H, L, L), x)
-    K.mha_fwd(qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], None, o, P, B, H, L, L, drop, rng, site)
+    _mha_fwd(qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], o, P, B, H, L, drop, rng, site)
     sa = K.linear_fwd(o, p[ln + ".self_attn.out_proj.weight"], p[ln + ".self_attn.out_proj.bias"], _e((rows, D), x))
     x1 = K.add_dropout(x, sa, _e((rows, D), x), None, drop, rng, site + 1)
     h2, m2, r2 = _e((rows, D), x), _e((rows,), x), _e((rows,), x)
@@ -192,9 +214,8 @@ def pool_forward(p: Dict[str, torch.Tensor], prefix: str, mode: str, x3: torch.T
         return ctx
     if mode != "transformer":
         raise ValueError(f"Unsupported temporal pooling mode: {mode}")
-    if D % num_heads or (D // num_heads) % 4 or D // num_heads > 64 or L > 256:
-        raise NotImplementedError(f"transformer pooling HIP path needs head_dim % 4 == 0, head_dim <= 64 and "
-                                  f"L <= 256 (got D={D}, heads={num_heads}, L={L})")
+    if D % num_heads:
+        raise ValueError(f"embed_dim {D} must be divisible by num_heads {num_heads}")
     if pe is None:
         pe = sinusoidal_pe(L, D, x3.device)
     rows = B * L

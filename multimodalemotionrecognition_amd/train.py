@@ -16,7 +16,7 @@ from torch import nn
 
 from .dist import GradAllReduce
 from .fusion import FusionModel
-from .losses import CrossEntropyLoss, LateNLLLoss
+from .losses import CrossEntropyLoss, LateNLLLoss, add_scaled
 from .optim import FusedAdam
 from .video import VideoNet
 from .wavlm_audio import WavLMAudioEncoder
@@ -62,12 +62,44 @@ def build_model(num_classes: int, fusion: str, pretrained_video: bool = True, xa
     raise ValueError(f"Unknown fusion mode: {fusion}")
 
 
+def _backward_order(model: nn.Module, params):
+    """``params`` in the order their gradients become final in the backward (fusion head, the video encoder's
+    head, ResNet18 layer4 .. stem, then the audio encoder), so the flat gradient buffer's prefix is what the
+    early data-parallel bucket ships (dist.GradAllReduce).  Adam is per-parameter: the order changes nothing
+    else."""
+    names = {id(q): n for n, q in model.named_parameters()}
+
+    def rank(q):
+        n = names.get(id(q), "")
+        if n.startswith("audio_model."):
+            return (3, 0)
+        if n.startswith("video_model.backbone."):
+            parts = n.split(".")
+            idx = int(parts[2])  # Sequential child: 0 conv1, 1 bn1, 4..7 layer1..4
+            blk = (idx - 4) * 2 + int(parts[3]) if 4 <= idx <= 7 else -1
+            return (2, -blk)
+        if n.startswith("video_model."):
+            return (1, 0)
+        return (0, 0)
+
+    return sorted(params, key=rank)  # stable: module order inside each rank
+
+
 def build_optimizer(model: nn.Module, lr: float = 1e-3, weight_decay: float = 1e-4) -> FusedAdam:
-    """train.py:899-902: Adam over every requires_grad parameter (params that get no grad are skipped)."""
-    params = [p for p in model.parameters() if p.requires_grad]
+    """train.py:899-902: Adam over every requires_grad parameter.  Parameters the configured mode never reaches
+    (``FusionModel.unused_parameters``: audio_time_conv, the encoders' classifiers under xattn ...) get no
+    gradient in the reference, so its Adam skips them on every step; they are left out of the flat buffers
+    (and the data-parallel all-reduce) here, which is the same update."""
+    params = build_optimizer_param_order(model)
     if not params:
         raise RuntimeError("No trainable parameters found for optimizer.")
     return FusedAdam(params, lr=lr, weight_decay=weight_decay)
+
+
+def build_optimizer_param_order(model: nn.Module):
+    """The used trainable parameters in flat-buffer (backward) order."""
+    dead = {id(q) for q in getattr(model, "unused_parameters", lambda: [])()}
+    return _backward_order(model, [p for p in model.parameters() if p.requires_grad and id(p) not in dead])
 
 
 
@@ -121,8 +153,9 @@ def build_fusion_stage_optimizer(model: nn.Module, stage: int, lr: float = 1e-3,
                                  video_backbone_lr: float = 1e-5, weight_decay: float = 1e-4) -> FusedAdam:
     """train.py:831-872: param groups fusion@lr, audio@audio_backbone_lr, video@video_backbone_lr."""
     fusion, audio, video = [], [], []
+    dead = {id(q) for q in getattr(model, "unused_parameters", lambda: [])()}
     for name, param in model.named_parameters():
-        if not param.requires_grad:
+        if not param.requires_grad or id(param) in dead:
             continue
         (audio if name.startswith("audio_model.") else video if name.startswith("video_model.") else fusion).append(param)
     groups = []
@@ -133,7 +166,7 @@ def build_fusion_stage_optimizer(model: nn.Module, stage: int, lr: float = 1e-3,
     elif stage == 2:
         for ps, glr in ((fusion, lr), (audio, audio_backbone_lr), (video, video_backbone_lr)):
             if ps:
-                groups.append({"params": ps, "lr": glr})
+                groups.append({"params": _backward_order(model, ps), "lr": glr})
         if not groups:
             raise RuntimeError("Stage-2 expects trainable parameters, but none are trainable.")
     else:
@@ -149,9 +182,11 @@ class TrainStep:
     """One training step of train.py:200-228 on the HIP path: returns (loss, preds) as device tensors."""
 
     def __init__(self, model: nn.Module, optimizer: FusedAdam, loss_fn: nn.Module, fusion_mode: str,
-                 grad_sync: Optional[GradAllReduce] = None):
+                 grad_sync: Optional[GradAllReduce] = None, fusion_align_weight: float = 0.0):
         self.model, self.opt, self.loss_fn, self.mode = model, optimizer, loss_fn, fusion_mode
         self.grad_sync = grad_sync
+        self.fusion_align_weight = float(fusion_align_weight)
+        self.last_losses = None  # (cls_loss, contrastive_loss) device scalars of the last step
 
     def __call__(self, video: torch.Tensor, audio: torch.Tensor, labels: torch.Tensor,
                  next_audio: Optional[torch.Tensor] = None):
@@ -165,7 +200,13 @@ class TrainStep:
             outputs = self.model(audio if self.mode == "audio" else video)
         else:
             outputs = self.model(video, audio)
-        loss = self.loss_fn(outputs, labels)
+        cls_loss = loss = self.loss_fn(outputs, labels)
+        align = None
+        if self.mode != "late" and self.fusion_align_weight > 0.0 and hasattr(self.model, "pop_alignment_loss"):
+            align = self.model.pop_alignment_loss()  # train.py:221-225
+            if align is not None:
+                loss = add_scaled(cls_loss, align, self.fusion_align_weight)
+        self.last_losses = (cls_loss.detach(), align.detach() if align is not None else None)
         if next_audio is not None and hasattr(self.model, "prefetch_audio"):
             self.model.prefetch_audio(next_audio)
         loss.backward()
@@ -179,8 +220,8 @@ def train_one_epoch(model: nn.Module, loader, optimizer: FusedAdam, device: torc
                     fusion_mode: str, fusion_align_weight: float = 0.0,
                     grad_sync: Optional[GradAllReduce] = None) -> Dict[str, float]:
     """train.py:185-244 (accuracy / macro-F1 computed once at the end, on the host)."""
-    step = TrainStep(model, optimizer, loss_fn, fusion_mode, grad_sync)
-    losses, preds, targets = [], [], []
+    step = TrainStep(model, optimizer, loss_fn, fusion_mode, grad_sync, fusion_align_weight=fusion_align_weight)
+    losses, cls_losses, con_losses, preds, targets = [], [], [], [], []
     n = 0
     it = iter(loader)
     nxt = next(it, None)
@@ -194,14 +235,21 @@ def train_one_epoch(model: nn.Module, loader, optimizer: FusedAdam, device: torc
             nxt_audio = nxt[1]
         loss, pred = step(video, audio, labels, next_audio=nxt_audio)
         losses.append(loss * labels.numel())
+        cls_l, con_l = step.last_losses
+        cls_losses.append(cls_l * labels.numel())
+        if con_l is not None:
+            con_losses.append(con_l * labels.numel())
         preds.append(pred)
         targets.append(labels)
         n += labels.numel()
     preds_t = torch.cat(preds).cpu()
     targets_t = torch.cat(targets).cpu()
     total = float(torch.stack(losses).sum().cpu()) / max(n, 1)
+    cls_total = float(torch.stack(cls_losses).sum().cpu()) / max(n, 1)
+    con_total = float(torch.stack(con_losses).sum().cpu()) / max(n, 1) if con_losses else 0.0
     acc = float((preds_t == targets_t).float().mean()) if n else 0.0
-    return {"loss": total, "cls_loss": total, "contrastive_loss": 0.0, "acc": acc, "f1": macro_f1(preds_t, targets_t)}
+    return {"loss": total, "cls_loss": cls_total, "contrastive_loss": con_total, "acc": acc,
+            "f1": macro_f1(preds_t, targets_t)}
 
 
 def macro_f1(preds: torch.Tensor, targets: torch.Tensor) -> float:

@@ -71,6 +71,9 @@ class _TrunkFn(torch.autograd.Function):
         runner = trunk.graph_runner(x, training, want_backward)
         if runner is not None:
             feats, saved = runner.forward(x)
+            # released by the backward, or when this graph is dropped without one (ModalityDropout cut)
+            ctx.gen = runner.cur_gen
+            ctx.token = runner.token(ctx.gen)
         else:
             feats, saved = trunk_forward(trunk, x, training)
         ctx.saved, ctx.trunk, ctx.training, ctx.runner = saved, trunk, training, runner
@@ -83,26 +86,29 @@ class _TrunkFn(torch.autograd.Function):
         if ctx.runner is not None and ctx.runner.backward_graphable(params):
             grads = ctx.runner.backward(dfeat, params)
         else:
-            grads = trunk_backward(ctx.trunk, ctx.saved, dfeat, ctx.training)
+            grads = trunk_backward(ctx.trunk, ctx.saved, dfeat, ctx.training, hook=ctx.trunk.grad_ready_hook)
         if ctx.runner is not None:
-            ctx.runner.pending = False
+            ctx.runner.release(ctx.gen)
         return (None, None, None, None, *[grads.get(id(q)) for q in params])
 
 
-class _TrunkGraphs:
+class _TrunkGraphs(G.PendingGuard):
     """Captured forward / backward hipGraphs of one (input shape, mode) of the trunk (graphs.py).
 
     Forward graph: pack input -> ... -> avgpool, with the per-step weight packing and the BatchNorm
-    running-stat updates inside it; its saved activations are graph-owned static tensors.  Backward
-    graph: the whole reverse schedule, writing every parameter gradient straight into the optimizer's
-    flat gradient buffer (``FusedAdam`` slots, fixed addresses); returned to autograd as fresh views.
+    running-stat updates inside it; its saved activations are graph-owned static tensors.  Backward:
+    the whole reverse schedule, writing every parameter gradient straight into the optimizer's flat
+    gradient buffer (``FusedAdam`` slots, fixed addresses); returned to autograd as fresh views.  With a
+    gradient-ready hook registered (data parallelism) the backward is two graphs -- layer4, then layer3 ..
+    stem -- and the hook runs between their replays, so the early all-reduce bucket overlaps the rest.
     """
 
     def __init__(self, trunk, training):
+        super().__init__()
         self.trunk, self.training = trunk, training
         self.fwd = None
         self.bwd = None
-        self.pending = False  # a graphed forward whose backward has not run (its static activations are live)
+        self.cur_gen = 0
 
     def forward(self, x):
         if self.fwd is None:
@@ -116,13 +122,30 @@ class _TrunkGraphs:
                    for q in params if q.requires_grad)
 
     def backward(self, dfeat, params):
-        if self.bwd is None:
+        hook = self.trunk.grad_ready_hook
+        split = SPLIT_BLOCK if hook is not None else 0
+        if self.bwd is None or self.bwd[0] != split:
             _, saved = self.fwd.out
-            self.bwd = G.StaticGraph(lambda d: trunk_backward(self.trunk, saved, d, self.training, force_pack=True),
-                                     [dfeat])
-        self.bwd.replay(dfeat)
+            tr, training = self.trunk, self.training
+            if split:
+                ga = G.StaticGraph(lambda d: trunk_backward_start(tr, saved, d, training, split, force_pack=True),
+                                   [dfeat])
+                gb = G.StaticGraph(lambda: trunk_backward_finish(tr, saved, ga.out, training, force_pack=True), [])
+            else:
+                ga = G.StaticGraph(lambda d: trunk_backward(tr, saved, d, training, force_pack=True), [dfeat])
+                gb = None
+            self.bwd = (split, ga, gb)
+        _, ga, gb = self.bwd
+        ga.replay(dfeat)
+        if gb is not None:
+            hook(self.trunk.split_params(split))
+            gb.replay()
         from .fusion import grad_buffer  # fresh views of the flat-buffer slots the graph wrote
         return {id(q): grad_buffer(q) for q in params if q.requires_grad}
+
+
+# First BasicBlock of the early gradient bucket: blocks 6, 7 = layer4 (8.4 M of the trunk's 11.2 M parameters)
+SPLIT_BLOCK = 6
 
 
 class ResNet18Trunk(nn.Sequential):
@@ -136,6 +159,11 @@ class ResNet18Trunk(nn.Sequential):
         self._plans = {}
         self._force_pack = False
         self._graphs = G.GraphCache()
+        self.grad_ready_hook = None  # fn(params): gradients of blocks >= SPLIT_BLOCK are final (dist.py)
+
+    def split_params(self, split: int):
+        """Parameters whose gradients are final once the backward has passed BasicBlock ``split``."""
+        return [q for b in _blocks(self)[split:] for q in b.parameters()]
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if not x.is_cuda:
@@ -155,7 +183,7 @@ class ResNet18Trunk(nn.Sequential):
             r = self._graphs.put(key, _TrunkGraphs(self, training))
         if r.pending:
             return None
-        r.pending = bool(want_backward)
+        r.cur_gen = r.claim(bool(want_backward))
         return r
 
     def backward_stop(self) -> int:
@@ -489,47 +517,72 @@ def block_backward(trunk, blk: BasicBlock, sv, dx: torch.Tensor, grads, training
 
 
 @torch.no_grad()
-def trunk_backward(trunk: ResNet18Trunk, saved, dfeat: torch.Tensor, training: bool = True, force_pack: bool = False):
+def trunk_backward(trunk: ResNet18Trunk, saved, dfeat: torch.Tensor, training: bool = True, force_pack: bool = False,
+                   hook=None):
+    """Whole reverse schedule -> {id(param): grad}.  ``hook(params)`` (data parallelism) is called once the
+    gradients of blocks >= SPLIT_BLOCK are enqueued, before the rest of the backward."""
+    split = SPLIT_BLOCK if hook is not None else 0
+    state = trunk_backward_start(trunk, saved, dfeat, training, split, force_pack=force_pack)
+    if hook is not None:
+        hook(trunk.split_params(split))
+    return trunk_backward_finish(trunk, saved, state, training, force_pack=force_pack)
+
+
+@torch.no_grad()
+def trunk_backward_start(trunk, saved, dfeat, training, split, force_pack=False):
+    """avgpool backward and BasicBlocks [max(split, stop), 8) in reverse; returns the state the rest needs."""
     with _ForcePack(trunk, force_pack):
-        return _trunk_backward(trunk, saved, dfeat, training)
+        trunk.pack_all(transpose=True)
+        dev = dfeat.device
+        x = saved["final"]
+        dx = torch.empty_like(x)
+        K.avgpool_bwd(dfeat, dx)
+        svs = saved["blocks"]
+        # every backward BatchNorm reduction buffer of this pass: one memset
+        arena = _StatsArena(trunk, dev, floats=sum(_block_bwd_floats(sv) for sv in svs) + 2 * K.BN_RED_WS_ROWS * 64 * 2)
+        state = dict(dx=dx, pre=None, grads={}, arena=arena, i=len(svs) - 1)
+        _backward_blocks(trunk, saved, state, max(split, trunk.backward_stop(), 0), training)
+        return state
 
 
-def _trunk_backward(trunk: ResNet18Trunk, saved, dfeat: torch.Tensor, training: bool = True):
-    trunk.pack_all(transpose=True)
-    grads = {}
-    dev = dfeat.device
-    x = saved["final"]
-    dx = torch.empty_like(x)
-    K.avgpool_bwd(dfeat, dx)
-    blocks = _blocks(trunk)
-    svs = saved["blocks"]
-    pre = None
-    # every backward BatchNorm reduction buffer of this pass: one memset
-    arena = _StatsArena(trunk, dev, floats=sum(_block_bwd_floats(sv) for sv in svs) + 2 * K.BN_RED_WS_ROWS * 64 * 2)
-    stop = trunk.backward_stop()
-    for i in reversed(range(max(stop, 0), len(blocks))):
+def _backward_blocks(trunk, saved, state, lo, training):
+    blocks, svs = _blocks(trunk), saved["blocks"]
+    while state["i"] >= lo:
+        i = state["i"]
         prev = (svs[i - 1], blocks[i - 1]) if i > 0 else None
-        dx, pre = block_backward(trunk, blocks[i], svs[i], dx, grads, training, pre=pre, prev=prev, arena=arena)
-    if stop >= 0:  # stem and the blocks below `stop` frozen (stage-2 video tail): nothing more is needed
+        state["dx"], state["pre"] = block_backward(trunk, blocks[i], svs[i], state["dx"], state["grads"], training,
+                                                   pre=state["pre"], prev=prev, arena=state["arena"])
+        state["i"] = i - 1
+
+
+@torch.no_grad()
+def trunk_backward_finish(trunk, saved, state, training, force_pack=False):
+    """The remaining BasicBlocks and the stem; returns {id(param): grad}."""
+    with _ForcePack(trunk, force_pack):
+        stop = trunk.backward_stop()
+        _backward_blocks(trunk, saved, state, max(stop, 0), training)
+        grads, arena, dx = state["grads"], state["arena"], state["dx"]
+        if stop >= 0:  # stem and the blocks below `stop` frozen (stage-2 video tail): nothing more is needed
+            return grads
+        dev = dx.device
+        # stem: maxpool -> bn1/relu -> conv1 (no data gradient for the frames)
+        x0, c1, ms1, arg = saved["stem"]
+        bn1 = trunk[1]
+        red = arena.take(c1.shape[-1], parts=1)
+        dc1 = torch.empty_like(c1)  # maxpool + relu + bn1 backward in one reduction pass and one apply pass
+        K.stem_pool_bn_bwd(dx, arg, c1, ms1, bn1.weight, bn1.bias, red, dc1, _grad(bn1.weight, grads),
+                           _grad(bn1.bias, grads), training, workspace=arena.take(c1.shape[-1], parts=K.BN_RED_WS_ROWS))
+        w = _grad(trunk[0].weight, grads)
+        if w is not None:  # wgrad of the 4x4 space-to-depth form, then gathered back to [64][3][7][7]
+            Kc, Cin, R, S = trunk[0].weight.shape
+            ws2d = torch.empty(Kc, S2D_CH, (R + 2) // 2, (S + 2) // 2, device=dev, dtype=torch.float32)
+            ws2d.zero_()
+            K.conv_wgrad(x0, dc1, ws2d, ws2d.shape[2], ws2d.shape[3], 1, 0)
+            idx = trunk.__dict__.get("_mer_stem_idx")
+            if idx is None or idx.device != dev:
+                idx = trunk.__dict__["_mer_stem_idx"] = _stem_wgrad_index(R, S, Cin, dev)
+            w.add_(ws2d.view(Kc, -1).index_select(1, idx).view_as(w))
         return grads
-    # stem: maxpool -> bn1/relu -> conv1 (no data gradient for the frames)
-    x0, c1, ms1, arg = saved["stem"]
-    bn1 = trunk[1]
-    red = arena.take(c1.shape[-1], parts=1)
-    dc1 = torch.empty_like(c1)  # maxpool + relu + bn1 backward in one reduction pass and one apply pass
-    K.stem_pool_bn_bwd(dx, arg, c1, ms1, bn1.weight, bn1.bias, red, dc1, _grad(bn1.weight, grads),
-                       _grad(bn1.bias, grads), training, workspace=arena.take(c1.shape[-1], parts=K.BN_RED_WS_ROWS))
-    w = _grad(trunk[0].weight, grads)
-    if w is not None:  # wgrad of the 4x4 space-to-depth form, then gathered back to [64][3][7][7]
-        Kc, Cin, R, S = trunk[0].weight.shape
-        ws2d = torch.empty(Kc, S2D_CH, (R + 2) // 2, (S + 2) // 2, device=dev, dtype=torch.float32)
-        ws2d.zero_()
-        K.conv_wgrad(x0, dc1, ws2d, ws2d.shape[2], ws2d.shape[3], 1, 0)
-        idx = trunk.__dict__.get("_mer_stem_idx")
-        if idx is None or idx.device != dev:
-            idx = trunk.__dict__["_mer_stem_idx"] = _stem_wgrad_index(R, S, Cin, dev)
-        w.add_(ws2d.view(Kc, -1).index_select(1, idx).view_as(w))
-    return grads
 
 
 class VideoNet(nn.Module):

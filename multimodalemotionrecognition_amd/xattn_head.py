@@ -96,15 +96,22 @@ def head_forward(p: Dict[str, torch.Tensor], cfg: HeadConfig, v_feat: torch.Tens
         pg = _e((B, 2 * d), v)
         K.mean_pool_fwd(v.view(B, T, d), pg[:, :d], ldy=2 * d)
         K.mean_pool_fwd(a.view(B, Ta, d), pg[:, d:], ldy=2 * d)
-        h1 = K.linear_fwd(pg, p[n + "prior_net.0.weight"], p[n + "prior_net.0.bias"], _e((B, p[n + "prior_net.0.weight"].shape[0]), v), act="relu")
+        h1 = lin(n + "prior_net.0", pg, _e((B, p[n + "prior_net.0.weight"].shape[0]), v), act="relu")
         K.dropout_(h1, dp_prior, rng, SITE_PRIOR)
-        prior = K.linear_fwd(h1, p[n + "prior_net.3.weight"], p[n + "prior_net.3.bias"], _e((B, p[n + "prior_net.3.weight"].shape[0]), v))
+        prior = lin(n + "prior_net.3", h1, _e((B, p[n + "prior_net.3.weight"].shape[0]), v))
         sv["pg"], sv["h1"], sv["prior"] = pg, h1, prior
         tok = {}
         for head, toks, L in (("v_query_bias", v, T), ("a_key_bias", a, Ta), ("a_query_bias", a, Ta), ("v_key_bias", v, T)):
             w = p[n + head + ".weight"]  # [1, d + pd]
-            tt = K.gemm(toks, w[:, :d], _e((toks.shape[0], 1), v), trans_b=True)
-            tp = K.gemm(prior, w[:, d:], _e((B, 1), v), trans_b=True, bias=p[n + head + ".bias"])
+            if qlin is not None and n + head in qlin:
+                # INT8 (inference): the Linear sees cat([token, prior]) (fusion.py:171-174), quantized as ONE tensor
+                ql = qlin[n + head]
+                rows = K.concat_prior_rows(toks, prior, _e((toks.shape[0], ql.in_padded), v), L)
+                tt = ql(rows, _e((toks.shape[0], 1), v))
+                tp = torch.zeros(B, 1, device=v.device, dtype=torch.float32)
+            else:
+                tt = K.gemm(toks, w[:, :d], _e((toks.shape[0], 1), v), trans_b=True)
+                tp = K.gemm(prior, w[:, d:], _e((B, 1), v), trans_b=True, bias=p[n + head + ".bias"])
             tok[head] = (tt, tp)
             sv["tt_" + head], sv["tp_" + head] = tt, tp
         v2a_bias = _e((B, T, Ta), v)

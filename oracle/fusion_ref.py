@@ -168,8 +168,30 @@ def xattn_forward(p: Params, v_feat: Tensor, a_seq: Tensor, *, num_heads: int = 
     return logits, inter
 
 
-def embedding_fusion_forward(p: Params, mode: str, a_emb: Tensor, v_emb: Tensor):
-    """Non-xattn ``concat`` / ``gated`` branch (fusion.py:413-435) after ``encode``; align mode none."""
+def clip_alignment(p: Params, a_emb: Tensor, v_emb: Tensor, name: str = "semantic_alignment"):
+    """``ClipStyleAlignment.forward`` (fusion.py:137-150) -> (a_aligned, v_aligned, loss)."""
+    a_al = linear(a_emb, p, name + ".audio_proj")
+    v_al = linear(v_emb, p, name + ".video_proj")
+    a_n = F.normalize(a_al, dim=-1)
+    v_n = F.normalize(v_al, dim=-1)
+    scale = p[name + ".logit_scale"].exp().clamp(max=100.0)
+    logits = scale * (a_n @ v_n.t())
+    t = torch.arange(logits.shape[0])
+    loss = 0.5 * (F.cross_entropy(logits, t) + F.cross_entropy(logits.t(), t))
+    return a_al, v_al, loss
+
+
+def embedding_fusion_forward(p: Params, mode: str, a_emb: Tensor, v_emb: Tensor, align: bool = False):
+    """Non-xattn ``concat`` / ``gated`` branch (fusion.py:413-435) after ``encode``.  ``align``: the
+    ``fusion_align_mode="clip"`` variant (fusion.py:417-418); returns (out, alignment loss) then."""
+    align_loss = None
+    if align:
+        a_emb, v_emb, align_loss = clip_alignment(p, a_emb, v_emb)
+    out = _embedding_head(p, mode, a_emb, v_emb)
+    return (out, align_loss) if align else out
+
+
+def _embedding_head(p: Params, mode: str, a_emb: Tensor, v_emb: Tensor):
     a = linear(a_emb, p, "audio_proj")
     v = linear(v_emb, p, "video_proj")
     if mode == "concat":

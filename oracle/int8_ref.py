@@ -112,3 +112,8 @@ XATTN_INT8 = {"concat": ("v_in_proj", "audio_seq_proj", "a_in_proj", "xattn_mlp.
               "gated": ("v_in_proj", "audio_seq_proj", "a_in_proj", "xattn_gate.0", "xattn_gate.3", "xattn_classifier")}
 EMB_INT8 = {"concat": ("audio_proj", "video_proj", "fusion.0", "fusion.3"),
             "gated": ("audio_proj", "video_proj", "gate.0", "gate.3", "classifier")}
+
+# With the emotion-prior adapter (fusion.py:153-184) quantize_dynamic also converts prior_net.0/3 and the four
+# token-bias Linear(d + prior_dim, 1) (their input is the concatenated [token; prior] row tensor).
+PRIOR_INT8 = tuple("emotion_prior_bias." + n for n in ("prior_net.0", "prior_net.3", "v_query_bias", "a_key_bias",
+                                                        "a_query_bias", "v_key_bias"))

@@ -35,25 +35,26 @@ def model_forward(p: Dict[str, Tensor], video: Tensor, audio: Tensor, *, num_hea
 
 
 class AdamRef:
-    """Restatement of ``torch.optim.Adam`` (single-tensor path, amsgrad=False, maximize=False)."""
+    """Restatement of ``torch.optim.Adam`` (single-tensor path, amsgrad=False, maximize=False): per-parameter
+    step counts (``state[p]['step']``), parameters whose ``.grad`` is None untouched."""
 
     def __init__(self, params: List[Tensor], lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
                  weight_decay: float = 0.0):
         self.params = params
         self.lr, self.b1, self.b2, self.eps, self.wd = lr, betas[0], betas[1], eps, weight_decay
-        self.step_count = 0
+        self.steps = [0] * len(params)
         self.m = [torch.zeros_like(q) for q in params]
         self.v = [torch.zeros_like(q) for q in params]
 
     @torch.no_grad()
     def step(self) -> None:
-        self.step_count += 1
-        t = self.step_count
-        bc1 = 1.0 - self.b1 ** t
-        bc2 = 1.0 - self.b2 ** t
-        for q, m, v in zip(self.params, self.m, self.v):
+        for i, (q, m, v) in enumerate(zip(self.params, self.m, self.v)):
             if q.grad is None:
                 continue
+            self.steps[i] += 1
+            t = self.steps[i]
+            bc1 = 1.0 - self.b1 ** t
+            bc2 = 1.0 - self.b2 ** t
             g = q.grad + self.wd * q
             m.mul_(self.b1).add_(g, alpha=1.0 - self.b1)
             v.mul_(self.b2).addcmul_(g, g, value=1.0 - self.b2)

@@ -23,3 +23,40 @@ def xattn_params(xattn_head="concat", use_prior=False, **kw):
     p = torch_state(fusion_ref.xattn_head_param_shapes(xattn_head=xattn_head, use_prior=use_prior, **kw))
     fusion_ref.gated_bias_init(p, xattn_head)
     return p
+
+
+def clip_head_params(mode: str):
+    """Parameters of FusionModel(mode, fusion_align_mode="clip") outside the encoders, numpy-seeded like
+    tools/gen_golden.py (logit_scale = log(1/0.07); gated: both gate biases -1)."""
+    d_al, cd = 256, 256
+    shapes = [("semantic_alignment.logit_scale", ()), ("semantic_alignment.audio_proj.weight", (d_al, 768)),
+              ("semantic_alignment.audio_proj.bias", (d_al,)), ("semantic_alignment.video_proj.weight", (d_al, 512)),
+              ("semantic_alignment.video_proj.bias", (d_al,)), ("audio_proj.weight", (cd, d_al)),
+              ("audio_proj.bias", (cd,)), ("video_proj.weight", (cd, d_al)), ("video_proj.bias", (cd,))]
+    if mode == "concat":
+        shapes += [("fusion.0.weight", (cd, 2 * cd)), ("fusion.0.bias", (cd,)), ("fusion.3.weight", (8, cd)),
+                   ("fusion.3.bias", (8,))]
+    else:
+        shapes += [("gate.0.weight", (cd, 2 * cd)), ("gate.0.bias", (cd,)), ("gate.3.weight", (1, cd)),
+                   ("gate.3.bias", (1,)), ("classifier.weight", (8, cd)), ("classifier.bias", (8,))]
+    p = torch_state(shapes)
+    p["semantic_alignment.logit_scale"] = torch.tensor(float(np.log(1.0 / 0.07)), dtype=torch.float32)
+    if mode == "gated":
+        p["gate.0.bias"].fill_(-1.0)
+        p["gate.3.bias"].fill_(-1.0)
+    return p
+
+
+def check_grad(g, key: str, grad, atol: float):
+    """Compare a gradient with a golden stored whole (``grad.<key>``) or trimmed (head rows + row/col sums)."""
+    grad = grad.detach().cpu().numpy() if hasattr(grad, "detach") else np.asarray(grad)
+    if "grad." + key in g.files:
+        ref = g["grad." + key]
+        np.testing.assert_allclose(grad, ref, atol=atol * max(1.0, float(np.abs(ref).max())), err_msg=key)
+        return
+    head = g["grad." + key + ".head"]
+    atol = atol * max(1.0, float(np.abs(head).max()))
+    np.testing.assert_allclose(grad[:head.shape[0]], head, atol=atol, err_msg=key)
+    scale = max(1.0, float(np.sqrt(grad.shape[0] * grad.shape[1])))
+    np.testing.assert_allclose(grad.sum(0), g["grad." + key + ".colsum"], atol=atol * scale, err_msg=key + " colsum")
+    np.testing.assert_allclose(grad.sum(1), g["grad." + key + ".rowsum"], atol=atol * scale, err_msg=key + " rowsum")

@@ -1,0 +1,133 @@
+"""C2 at its own batch size: the full xattn train step (ResNet18 trunk train-mode BN fwd+bwd, frozen WavLM-base,
+xattn head, CE, Adam) at B=32 x 8 frames x 48,000 samples on the HIP path vs the fp32 CPU oracle
+(train.py:200-228).  B=32 exercises the 256-frame conv tile picks and the M-dependent
+GEMM variants the bench runs.
+
+Bars (bf16 encoders, fp32 head):
+* logits max|d| < 5e-2 and |dloss| < 1e-2 against the full fp32 oracle step;
+* BatchNorm running statistics (every BN of the trunk) within 2e-2 relative;
+* the xattn head teacher-forced on the HIP encoders' own features: logits within 1e-4 and every head
+  gradient within 1e-3 relative (max|d| / max|ref|) of the fp32 oracle head -- the head is fp32 end to end;
+* the first Adam update (~ -lr * sign(g)): per-parameter sign agreement with the oracle's update >= 0.97 for
+  head parameters and >= 0.70 for every trunk parameter (bf16 trunk gradients; near-zero gradient elements
+  flip), and >= 0.85 averaged over the trunk;
+* trunk gradient cosine >= 0.9 per parameter against the oracle.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import fusion_ref, params as OP, resnet18_ref, train_ref, wavlm_ref
+
+pytestmark = pytest.mark.gpu
+
+B = 32
+
+
+def _state():
+    shapes = [("video_model." + n, s) for n, s in resnet18_ref.param_shapes()]
+    shapes += [("audio_model.wavlm." + n, s) for n, s in wavlm_ref.wavlm_param_shapes()]
+    shapes += fusion_ref.xattn_head_param_shapes()
+    return {k: torch.from_numpy(v) for k, v in OP.init_state(shapes).items()}
+
+
+def _rel(a, b):
+    a, b = a.detach().float().cpu(), b.detach().float().cpu()
+    return float((a - b).abs().max() / max(float(b.abs().max()), 1e-12))
+
+
+def test_c2_train_step_b32_vs_oracle():
+    from multimodalemotionrecognition_amd.train import build_model, build_optimizer, make_loss
+
+    p = _state()
+    m = build_model(8, "xattn", pretrained_video=False, use_wavlm=True)
+    m.load_state_dict({k: v.clone() for k, v in p.items()}, strict=False)
+    m = m.cuda().train()
+    m.attn_dropout = 0.0  # the oracle step is deterministic: dropout / drop-path off (SURVEY 7 "Stochastic ops")
+    m.v_drop_path.drop_prob = m.a_drop_path.drop_prob = 0.0
+    m.xattn_mlp[2].p = 0.0
+    wav = m.audio_model.wavlm
+    if hasattr(wav, "train_semantics"):
+        wav.train_semantics = False  # WavLM's own train-mode ops are stochastic: compared statistically elsewhere
+    opt = build_optimizer(m, lr=1e-3, weight_decay=1e-4)
+    loss_fn = make_loss("xattn")
+    video, audio, labels = OP.clip_inputs(B, seed=11)
+    video, audio, labels = torch.from_numpy(video), torch.from_numpy(audio), torch.from_numpy(labels)
+
+    cap = {}
+    orig = m.xattn_from_features
+
+    def capture(v_feat, a_seq):
+        cap["v"], cap["a"] = v_feat.detach().float().cpu(), a_seq.detach().float().cpu()
+        return orig(v_feat, a_seq)
+
+    m.xattn_from_features = capture
+    before = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
+    opt.zero_grad()
+    logits = m(video.cuda(), audio.cuda())
+    loss = loss_fn(logits, labels.cuda())
+    loss.backward()
+    hip_grads = {n: q.grad.detach().cpu().clone() for n, q in m.named_parameters() if q.grad is not None}
+    opt.step()
+    torch.cuda.synchronize()
+    after = {k: v.detach().cpu() for k, v in m.state_dict().items()}
+
+    # ---- full fp32 oracle step ----
+    trainable = [k for k in p if (k.startswith("video_model.") and not k.endswith(
+        ("running_mean", "running_var", "num_batches_tracked"))) or
+        (not k.startswith(("video_model.", "audio_model.")) and not k.startswith("audio_time_conv"))]
+    for k in trainable:
+        p[k].requires_grad_(True)
+    torch.set_num_threads(max(1, min(16, torch.get_num_threads())))
+    rlogits = train_ref.model_forward(p, video, audio)
+    rloss = fusion_ref.cross_entropy(rlogits, labels)
+    rloss.backward()
+    ref_grads = {k: p[k].grad.detach().clone() for k in trainable if p[k].grad is not None}
+    ropt = train_ref.AdamRef([p[k] for k in trainable], lr=1e-3, weight_decay=1e-4)
+    ropt.step()
+
+    dlog = float((logits.detach().cpu() - rlogits.detach()).abs().max())
+    dloss = abs(float(loss.detach()) - float(rloss.detach()))
+    print(f"B=32 logits max|d| {dlog:.3e}  loss hip {float(loss):.5f} oracle {float(rloss):.5f}")
+    assert dlog < 5e-2 and dloss < 1e-2
+
+    # ---- BatchNorm running statistics ----
+    worst = 0.0
+    for k in p:
+        if k.startswith("video_model.") and k.endswith(("running_mean", "running_var")):
+            worst = max(worst, _rel(after[k], p[k]))
+    print("BN running stats worst rel", worst)
+    assert worst < 2e-2
+    assert int(after["video_model.backbone.1.num_batches_tracked"]) == 1
+
+    # ---- fp32 head teacher-forced on the HIP encoders' features ----
+    hp = {k: before[k].clone().requires_grad_(True) for k in p
+          if not k.startswith(("video_model.", "audio_model.", "audio_time_conv"))}
+    tlogits, _ = fusion_ref.xattn_forward(hp, cap["v"], cap["a"])
+    fusion_ref.cross_entropy(tlogits, labels).backward()
+    dl_t = float((logits.detach().cpu() - tlogits.detach()).abs().max())
+    print("teacher-forced head logits max|d|", dl_t)
+    assert dl_t < 1e-4
+    for k, q in hp.items():
+        r = _rel(hip_grads[k], q.grad)
+        assert r < 1e-3, (k, r)
+
+    # ---- first Adam update direction, per parameter ----
+    agree_trunk = []
+    for k in trainable:
+        dh = (after[k] - before[k]).flatten()
+        dr = (p[k].detach() - before[k]).flatten()
+        agree = float(((dh > 0) == (dr > 0)).float().mean())
+        if k.startswith("video_model."):
+            agree_trunk.append(agree)
+            assert agree >= 0.70, (k, agree)
+            g1, g2 = hip_grads[k].flatten(), ref_grads[k].flatten()
+            cos = float(torch.dot(g1, g2) / (g1.norm() * g2.norm() + 1e-30))
+            assert cos >= 0.9, (k, cos)
+        else:
+            assert agree >= 0.97, (k, agree)
+    print("trunk update-sign agreement mean", np.mean(agree_trunk), "min", np.min(agree_trunk))
+    assert np.mean(agree_trunk) >= 0.85
+    # frozen encoder untouched, dead parameters untouched
+    for k in ("audio_model.wavlm.encoder.layers.0.attention.q_proj.weight", "audio_time_conv.weight"):
+        assert torch.equal(after[k], before[k])

@@ -8,7 +8,7 @@ import pytest
 import torch
 
 from oracle import fusion_ref, params, resnet18_ref, wavlm_ref
-from tests.helpers import golden, torch_state, xattn_params
+from tests.helpers import check_grad, clip_head_params, golden, torch_state, xattn_params
 
 
 @pytest.mark.parametrize("head", ["concat", "gated"])
@@ -176,3 +176,64 @@ def test_int8_qparams_edge_cases():
     assert float(s) == np.float32(6.1e-5)
     qw, ws = int8_ref.quantize_weight(np.array([[1.0, -2.0], [0.5, 0.0]], np.float32))
     assert qw.min() >= -128 and qw.max() <= 127 and float(ws) == np.float32(2.0 / 127.5)
+
+
+@pytest.mark.parametrize("mode", ["concat", "gated"])
+def test_c4_clip_alignment(mode):
+    """fusion_align_mode="clip" (fusion.py:127-150, 417-418): logits, the CLIP loss and the gradients of
+    CE + 0.5 * align (train.py:221-225) vs the imported reference."""
+    g = golden(f"c4_clip_{mode}.npz")
+    p = clip_head_params(mode)
+    assert sorted(p) == sorted(str(n) for n in g["names"] if not str(n).startswith(("audio_model.", "video_model.")))
+    for q in p.values():
+        q.requires_grad_(True)
+    a = torch.from_numpy(g["a_emb"]).requires_grad_(True)
+    v = torch.from_numpy(g["v_emb"]).requires_grad_(True)
+    out, align = fusion_ref.embedding_fusion_forward(p, mode, a, v, align=True)
+    loss = fusion_ref.cross_entropy(out, torch.from_numpy(g["labels"])) + 0.5 * align
+    loss.backward()
+    np.testing.assert_allclose(out.detach().numpy(), g["logits"], atol=2e-5)
+    assert abs(float(align) - float(g["align"])) < 2e-5 and abs(float(loss) - float(g["loss"])) < 2e-5
+    np.testing.assert_allclose(a.grad.numpy(), g["grad_a"], atol=2e-6)
+    np.testing.assert_allclose(v.grad.numpy(), g["grad_v"], atol=2e-6)
+    for k, q in p.items():
+        check_grad(g, k, q.grad, atol=2e-6)
+
+
+def test_int8_head_prior_c5():
+    """INT8 with the emotion-prior adapter: prior_net and the token-bias Linears are quantized too."""
+    from oracle import int8_ref
+
+    g = golden("int8_head_prior_b64.npz")
+    head_linears = sorted(str(n) for n in g["quantized"] if not str(n).startswith(("audio_model.", "video_model.")))
+    assert head_linears == sorted(int8_ref.XATTN_INT8["concat"] + int8_ref.PRIOR_INT8)
+    p = int8_ref.quantize_params(xattn_params("concat", True), head_linears)
+    v, a = params.feature_inputs(64, 8, 149, seed=22)
+    with torch.no_grad():
+        fp, _ = fusion_ref.xattn_forward(xattn_params("concat", True), torch.from_numpy(v), torch.from_numpy(a),
+                                         use_prior=True)
+        lq, _ = fusion_ref.xattn_forward(p, torch.from_numpy(v), torch.from_numpy(a), use_prior=True)
+    np.testing.assert_allclose(fp.numpy(), g["logits_fp32"], atol=2e-5)
+    np.testing.assert_allclose(lq.numpy(), g["logits_int8"], atol=1e-4)
+    assert (lq.argmax(1).numpy() == g["logits_int8"].argmax(1)).all()
+
+
+@pytest.mark.parametrize("dim", [512, 768])
+def test_encoder_transformer_pool(dim):
+    """TemporalPooler('transformer', 4 heads) at the encoders' widths (head_dim 128 / 192)."""
+    g = golden(f"temporal_transformer_d{dim}.npz")
+    shapes = fusion_ref._pool_shapes("tp", dim, "transformer", 1)
+    p = torch_state([(k[len("tp."):], s) for k, s in shapes])
+    assert sorted(p) == sorted(str(n) for n in g["names"] if not str(n).endswith("pe"))
+    for q in p.values():
+        q.requires_grad_(True)
+    x = torch.from_numpy(g["x"]).requires_grad_(True)
+    y = fusion_ref.transformer_pool(x, p, "pool", num_heads=4, num_layers=1)
+    (y * torch.from_numpy(g["w"])).sum().backward()
+    np.testing.assert_allclose(y.detach().numpy(), g["y"], atol=3e-5)
+    np.testing.assert_allclose(x.grad.numpy(), g["grad_x"], atol=3e-6)
+    for k, q in p.items():
+        if k == "pool.pool.score.4.bias":  # softmax is shift-invariant: this gradient is 0 up to rounding noise
+            assert abs(float(q.grad)) < 1e-4
+            continue
+        check_grad(g, k, q.grad, atol=5e-6)

@@ -234,10 +234,100 @@ def gen_wavlm():
     print("wavlm", out.last_hidden_state.shape, out.last_hidden_state[0, 0, :3])
 
 
+def gen_c4_clip():
+    """concat / gated with fusion_align_mode="clip" (fusion.py:127-150, 417-418) at feature level, eval mode
+    (no dropout, no ModalityDropout): logits, the alignment loss and the gradients of
+    CE(logits) + 0.5 * align_loss (train.py:221-225) w.r.t. every head parameter and both inputs."""
+    rng = np.random.Generator(np.random.PCG64(41))
+    a_emb = rng.standard_normal((6, 768)).astype(np.float32)
+    v_emb = rng.standard_normal((6, 512)).astype(np.float32)
+    labels = torch.from_numpy(rng.integers(0, 8, 6))
+    for mode in ("concat", "gated"):
+        m = FusionModel(StubAudio(), StubVideo(), num_classes=8, mode=mode, fusion_align_mode="clip",
+                        fusion_align_dim=256, fusion_align_temperature=0.07)
+
+        def fix(sd):
+            sd["semantic_alignment.logit_scale"].fill_(float(np.log(1.0 / 0.07)))
+            if mode == "gated":
+                sd["gate.0.bias"].fill_(-1.0)
+                sd["gate.3.bias"].fill_(-1.0)
+        load_numpy_init(m, 0, fix)
+        m.eval()
+        at = torch.from_numpy(a_emb).requires_grad_(True)
+        vt = torch.from_numpy(v_emb).requires_grad_(True)
+        logits = m(vt, at)
+        align = m.pop_alignment_loss()
+        loss = nn.CrossEntropyLoss()(logits, labels) + 0.5 * align
+        loss.backward()
+        out = {"a_emb": a_emb, "v_emb": v_emb, "labels": labels.numpy(), "logits": logits.detach().numpy(),
+               "align": np.float32(align.item()), "loss": np.float32(loss.item()),
+               "grad_a": at.grad.numpy(), "grad_v": vt.grad.numpy(), "names": np.array(list(m.state_dict().keys()))}
+        for n, q in m.named_parameters():
+            if q.grad is not None and not n.startswith(("audio_model.", "video_model.")):
+                out["grad." + n] = q.grad.numpy().copy()
+        np.savez_compressed(OUT / f"c4_clip_{mode}.npz", **_trim(out))
+        print("c4 clip", mode, float(align), float(loss))
+
+
+def gen_int8_head_prior():
+    """C5 INT8 with the emotion-prior adapter: quantize_dynamic({nn.Linear}) also quantizes prior_net and the
+    four token-bias Linears (optimized_runtime.py:95-96)."""
+    m = xattn_model("concat", True)
+    load_numpy_init(m, 0)
+    m.eval()
+    v, a = params.feature_inputs(64, 8, 149, seed=22)
+    vt, at = torch.from_numpy(v)[..., None, None], torch.from_numpy(a)
+    with torch.no_grad():
+        fp = m(vt, at)
+    q = torch.ao.quantization.quantize_dynamic(m, {nn.Linear}, dtype=torch.qint8)
+    with torch.no_grad():
+        lq = q(vt, at)
+    quantized = sorted(n for n, mod in q.named_modules() if type(mod).__name__ == "Linear" and "quantized" in type(mod).__module__)
+    np.savez_compressed(OUT / "int8_head_prior_b64.npz", logits_fp32=fp.numpy(), logits_int8=lq.numpy(),
+                        quantized=np.array(quantized))
+    print("int8 prior", (fp - lq).abs().max().item(), (fp.argmax(1) == lq.argmax(1)).float().mean().item(), quantized)
+
+
+def gen_encoder_transformer_pool():
+    """TemporalPooler('transformer', num_heads=4) at the encoders' widths (train.py:357-443 passes
+    temporal_pooling into both encoders): VideoNet.encode at 512 (head_dim 128) over T=8 frames and
+    WavLMAudioEncoder.encode at 768 (head_dim 192) over Ta=149 frames; eval mode, plus input / parameter
+    gradients of sum(y * w) for a fixed w."""
+    for dim, length, seed in ((512, 8, 51), (768, 149, 52)):
+        pool = TemporalPooler(dim=dim, mode="transformer", num_heads=4, num_layers=1, dropout=0.1)
+        load_numpy_init(pool, 0)
+        pool.eval()
+        x = torch.from_numpy(params.feature_inputs(3, length, 1, v_dim=dim, seed=seed)[0]).requires_grad_(True)
+        y = pool(x)
+        w = torch.from_numpy(np.random.Generator(np.random.PCG64(seed + 100)).standard_normal(tuple(y.shape))
+                             .astype(np.float32))
+        (y * w).sum().backward()
+        out = {"x": x.detach().numpy(), "y": y.detach().numpy(), "w": w.numpy(), "grad_x": x.grad.numpy(),
+               "names": np.array(list(pool.state_dict().keys()))}
+        for n, q in pool.named_parameters():
+            out["grad." + n] = q.grad.numpy().copy()
+        np.savez_compressed(OUT / f"temporal_transformer_d{dim}.npz", **_trim(out))
+        print("transformer pool", dim, y[0, :3])
+
+
+def _trim(out, limit=16384, rows=8):
+    """Keep fixtures small: a gradient larger than ``limit`` elements is stored as its first ``rows`` rows plus
+    its column sums and row sums (``<key>.head`` / ``.colsum`` / ``.rowsum``)."""
+    res = {}
+    for k, v in out.items():
+        if k.startswith("grad.") and isinstance(v, np.ndarray) and v.size > limit and v.ndim == 2:
+            res[k + ".head"] = v[:rows].copy()
+            res[k + ".colsum"] = v.sum(0, dtype=np.float64).astype(np.float32)
+            res[k + ".rowsum"] = v.sum(1, dtype=np.float64).astype(np.float32)
+        else:
+            res[k] = v
+    return res
+
+
+GENERATORS = dict(xattn_c1=gen_xattn_c1, xattn_c2=gen_xattn_c2_grads, small=gen_small_shapes, c4=gen_c4_heads,
+                  int8=gen_int8_head, wavlm=gen_wavlm, c4_clip=gen_c4_clip, int8_prior=gen_int8_head_prior,
+                  enc_transformer=gen_encoder_transformer_pool)
+
 if __name__ == "__main__":
-    gen_xattn_c1()
-    gen_xattn_c2_grads()
-    gen_small_shapes()
-    gen_c4_heads()
-    gen_int8_head()
-    gen_wavlm()
+    for name in (sys.argv[1:] or list(GENERATORS)):
+        GENERATORS[name]()
