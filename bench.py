@@ -10,8 +10,15 @@ WavLM-base (frozen, forward) + ResNet18 trunk (train-mode BN, forward+backward) 
 ([32,8,3,112,112] frames, [32,1,48000] waveform) resident in HBM.  Weak scaling: each rank runs
 B=32; `value` = steps completed by all ranks / wall time (max over ranks).
 
-Extra fields: `roofline` for the dominant kernel (HIP events around its launches inside the timed
-region) and `cpu_baseline` (the fp32 CPU oracle of the same step, rank 0, N=1, bounded sample).
+WavLM runs with the reference's train-mode semantics (the reference keeps the frozen WavLM in train mode
+under no_grad, train.py:194): SpecAugment, dropout and LayerDrop -- so the algorithmic FLOPs of a step count
+only the encoder layers actually executed; `wavlm_layers_per_step` reports them.
+
+Extra fields: `roofline` for the dominant kernel (HIP events around its launches, on the side stream it runs
+on, in `--probe-steps` instrumented steps that follow the timed region: the production WavLM forward is ONE
+captured graph, so the probe steps alone run it as two graphs around an eagerly launched conv1 GEMM) and
+`cpu_baseline` (the fp32 CPU oracle of the same step, rank 0, N=1: BASELINE.md section 3 -- warm-up steps,
+then the median of timed steps, on the threads of this process's CPU share, CPU model recorded).
 """
 from __future__ import annotations
 
@@ -44,6 +51,11 @@ PROBE = ("gemm_bf16", (BATCH * 4799, 512, 1536))
 # 16 waves each)
 PROBE_KERNEL = "gemm_pipe_kernel<PipeCfg<256,256,4,4,2>, bf16>"
 PMC_FILE = ROOT / "profiles" / "pmc_traffic.json"
+# Algorithmic work per clip: ResNet18 fwd+bwd over 8 frames 22.8 GFLOP, head fwd+bwd 0.141, WavLM
+# feature extractor 14.72 + pos-conv 1.42 + projection 0.12, and 2.177 GFLOP per EXECUTED encoder layer
+# (projections 0.703 + FFN 1.406 + attention 0.068; LayerDrop skips ~1.1 of 12 in train mode).
+STEP_GFLOP_PER_CLIP_FIXED = 22.8 + 0.141 + 14.72 + 1.42 + 0.12
+WAVLM_LAYER_GFLOP_PER_CLIP = 0.703 + 1.406 + 0.068
 
 
 def pmc_traffic():
@@ -70,8 +82,30 @@ def synthetic_batch(device, seed):
     return video.contiguous(), audio.contiguous(), labels
 
 
-def cpu_baseline(threads: int, steps: int = 2):
-    """The fp32 CPU oracle of the same train step at B=32 (test infrastructure, timed as the baseline)."""
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_share_threads() -> int:
+    """Threads of this process's CPU share: OMP_NUM_THREADS when the launcher set it (the GPU box sets it to its
+    16-CPU share; os.cpu_count() there reports the whole machine), else the affinity set."""
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        return int(env)
+    return len(os.sched_getaffinity(0))
+
+
+def cpu_baseline(threads: int, steps: int = 10, warmup: int = 10):
+    """The fp32 CPU oracle of the same train step at B=32 (test infrastructure, timed as the baseline):
+    ``warmup`` untimed steps, then the median of ``steps`` timed ones."""
+    import statistics
+
     from oracle import params as OP
     from oracle import fusion_ref, resnet18_ref, train_ref, wavlm_ref
 
@@ -88,23 +122,31 @@ def cpu_baseline(threads: int, steps: int = 2):
     opt = train_ref.AdamRef([p[k] for k in trainable], lr=1e-3, weight_decay=1e-4)
     video, audio, labels = OP.clip_inputs(BATCH)
     video, audio, labels = torch.from_numpy(video), torch.from_numpy(audio), torch.from_numpy(labels)
-    train_ref.train_step(p, trainable, opt, video, audio, labels)  # warm-up
-    t = time.perf_counter()
-    for _ in range(steps):
+    for _ in range(warmup):
         train_ref.train_step(p, trainable, opt, video, audio, labels)
-    dt = (time.perf_counter() - t) / steps
+    times = []
+    for _ in range(steps):
+        t = time.perf_counter()
+        train_ref.train_step(p, trainable, opt, video, audio, labels)
+        times.append(time.perf_counter() - t)
+    dt = statistics.median(times)
     return {"value": round(1.0 / dt, 4), "unit": "steps/s", "cores": threads, "kind": "port",
-            "sample": f"{steps} timed steps (+1 warm-up) of the fp32 oracle train step at B=32 "
-                      f"({dt:.2f} s/step, {BATCH / dt:.2f} clips/s), torch CPU eager, {threads} threads"}
+            "cpu_model": cpu_model(), "os_cpu_count": os.cpu_count(),
+            "sample": f"median of {steps} timed steps after {warmup} warm-up steps of the fp32 oracle train step at "
+                      f"B=32 ({dt:.2f} s/step, {BATCH / dt:.2f} clips/s), torch CPU eager, {threads} threads"}
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--probe-steps", type=int, default=10,
+                    help="instrumented steps after the timed region in which the dominant kernel is timed")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0: this process's CPU share (cpu_share_threads)")
+    ap.add_argument("--cpu-steps", type=int, default=10)
+    ap.add_argument("--cpu-warmup", type=int, default=10)
     ap.add_argument("--no-prefetch", action="store_true",
                     help="run the frozen WavLM inline in every step instead of overlapping the next batch's "
                          "WavLM forward with this step's backward")
@@ -125,7 +167,7 @@ def main():
         opt = build_fusion_stage_optimizer(model, stage=2, lr=1e-3, weight_decay=1e-4)
     else:
         opt = build_optimizer(model, lr=1e-3, weight_decay=1e-4)
-    step = TrainStep(model, opt, make_loss("xattn"), "xattn", GradAllReduce(opt) if is_dist() else None)
+    step = TrainStep(model, opt, make_loss("xattn"), "xattn", GradAllReduce(opt, model=model) if is_dist() else None)
     video, audio, labels = synthetic_batch(dev, 20261015 + rank)
 
     # The synthetic stream repeats one resident batch, so the next step's waveform is `audio` itself:
@@ -135,32 +177,38 @@ def main():
         step(video, audio, labels, next_audio=nxt)
     torch.cuda.synchronize()
 
-    probe = K.KernelProbe(PROBE[0], PROBE[1], units=2.0 * PROBE[1][0] * PROBE[1][1] * PROBE[1][2])
-    probe.active = True
-    K.PROBE = probe
+    wav = model.audio_model.wavlm
+    lay0, fwd0 = wav.executed_layers, wav.train_forwards
     if is_dist():
         dist.barrier()
     torch.cuda.synchronize()
+    marks = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     t0 = time.perf_counter()
+    marks[0].record()
     loss = None
-    for _ in range(args.steps):
+    for i in range(args.steps):
         loss, _ = step(video, audio, labels, next_audio=nxt)
+        marks[i + 1].record()
     torch.cuda.synchronize()
     if is_dist():
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    probe.active = False
-    K.PROBE = None
+    step_ms = sorted(marks[i].elapsed_time(marks[i + 1]) for i in range(args.steps))
+    median_ms = step_ms[len(step_ms) // 2] if len(step_ms) % 2 else 0.5 * (step_ms[len(step_ms) // 2 - 1] +
+                                                                           step_ms[len(step_ms) // 2])
+    layers = (wav.executed_layers - lay0) / max(1, wav.train_forwards - fwd0)
 
-    t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-    if is_dist():
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
-    if rank != 0:
-        if is_dist():
-            dist.barrier()
-            dist.destroy_process_group()
-        return
+    # probe steps (after the timed region): the dominant kernel bracketed by HIP events on its stream
+    probe = K.KernelProbe(PROBE[0], PROBE[1], units=2.0 * PROBE[1][0] * PROBE[1][1] * PROBE[1][2])
+    if args.probe_steps > 0:
+        probe.active = True
+        K.PROBE = probe
+        for _ in range(args.probe_steps + 2):  # the first two build the instrumented (split) WavLM graphs
+            step(video, audio, labels, next_audio=nxt)
+        torch.cuda.synchronize()
+        probe.pairs = probe.pairs[-args.probe_steps:]
+        probe.active = False
+        K.PROBE = None
 
     kms = probe.avg_ms()
     roof = None
@@ -169,7 +217,10 @@ def main():
         roof = {"bound": "mfma", "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": pmc_traffic(),
                 "kernel": f"{PROBE_KERNEL} (WavLM conv1 implicit GEMM {PROBE[1][0]}x{PROBE[1][1]}x{PROBE[1][2]})",
-                "avg_ms": round(kms, 4), "launches": len(probe.pairs)}
+                "avg_ms": round(kms, 4), "launches": len(probe.pairs),
+                "measured": f"HIP events on the launching stream in {len(probe.pairs)} probe steps after the timed "
+                            "region"}
+    step_gflop = BATCH * (STEP_GFLOP_PER_CLIP_FIXED + WAVLM_LAYER_GFLOP_PER_CLIP * layers)
     out = {
         "metric": "3s-clip train steps/sec (B=32, xattn fusion) at 1/2/4/8 MI355X",
         "value": round(world * args.steps / elapsed, 3),
@@ -178,11 +229,13 @@ def main():
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "ms_per_step_median": round(median_ms, 3),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "bf16",
-        "data": "synthetic (seeded 3 s clips resident in HBM; random-init weights)",
+        "data": "synthetic (seeded 3 s clips resident in HBM; random-init weights; WavLM in train mode as in the "
+                "reference: SpecAugment + dropout + LayerDrop)",
         "config": {"workload": ("ResNet18 + WavLM-base (frozen) + xattn fusion train step (fwd+bwd+Adam)"
                                 if args.wavlm_unfreeze == 0 else
                                 f"stage-2 fine-tuning step: WavLM last {args.wavlm_unfreeze} layers + ResNet18 layer4 + "
@@ -191,12 +244,15 @@ def main():
                    "audio_samples": SAMPLES, "parallelism": f"dp{world}"},
         "clips_per_s": round(world * BATCH * args.steps / elapsed, 1),
         "final_loss": round(float(loss), 4) if loss is not None else None,
+        "wavlm_layers_per_step": round(layers, 3),
+        "step_tflop": round(step_gflop / 1e3, 4),
+        "step_tflops_achieved": round(step_gflop / 1e3 / (median_ms * 1e-3), 1),
         "roofline": roof,
         "cpu_baseline": None,
     }
     if world == 1 and not args.no_cpu_baseline:
-        threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
-        out["cpu_baseline"] = cpu_baseline(threads)
+        threads = args.cpu_threads if args.cpu_threads > 0 else cpu_share_threads()
+        out["cpu_baseline"] = cpu_baseline(threads, steps=args.cpu_steps, warmup=args.cpu_warmup)
     print(json.dumps(out), flush=True)
     if is_dist():
         dist.barrier()

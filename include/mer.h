@@ -234,6 +234,46 @@ int mer_weightnorm_scale(int n01, int taps, const float* v, const float* g, floa
 /* y = bf16(x), contiguous. */
 int mer_cast_bf16(long n, const float* x, void* y, void* stream);
 
+/* ---- WavLM train-mode semantics (the reference runs the frozen WavLM in train mode under no_grad,
+ * train.py:194 + wavlm_audio.py:177-182): dropout, LayerDrop, SpecAugment time masking ----
+ * Common train-mode arguments: drop_p / seed / site = dropout probability, the step's device RNG base and a
+ * constant call-site id (mask = hash(base, site, element), regenerated by backward kernels); skip_mask /
+ * skip_bit = LayerDrop (TF:417-419): the launch is a no-op when bit skip_bit of the device int64 *skip_mask is
+ * set (one host-drawn bitmask per forward, so a captured hipGraph replays any layer subset). */
+
+/* mer_gemm_bf16_ex + dropout after the activation and before the residual (attention output dropout TF:323,
+ * FFN intermediate / output dropout TF:286-294; mask index row*N + col) + LayerDrop skip. */
+int mer_gemm_bf16_tr(int M, int N, int K, const void* A, long a_gstride, long a_rstride, int a_rpg, const void* W,
+                     long ldw, void* C, int c_dtype, long ldc, const float* bias, const void* R, long ldr, int act,
+                     float drop_p, const unsigned long long* seed, unsigned long long site, const long long* skip_mask,
+                     int skip_bit, int variant, void* stream);
+
+/* mer_layernorm + dropout of the OUTPUT (WavLMEncoder.dropout after the encoder LayerNorm, TF:406-407; mask index
+ * row*d + c) + LayerDrop skip (the post-LN layers' norms). */
+int mer_layernorm_tr(int rows, int d, const void* x, int x_dtype, long ldx, const float* gamma, const float* beta,
+                     float eps, void* y, int y_dtype, long ldy, float drop_p, const unsigned long long* seed,
+                     unsigned long long site, const long long* skip_mask, int skip_bit, void* stream);
+
+/* mer_wavlm_attention + attention-probability dropout (F.multi_head_attention_forward dropout_p, TF:206-228;
+ * mask index ((b*H + h)*L + i)*L + j) + LayerDrop skip. */
+int mer_wavlm_attention_tr(int B, int L, int H, const void* qkv, long ldqkv, const void* x, long ldx,
+                           const float* gate_w, const float* gate_b, const float* gate_const, const float* rel_emb,
+                           const int* bucket, void* out, long ldo, float scale, float drop_p,
+                           const unsigned long long* seed, unsigned long long site, const long long* skip_mask,
+                           int skip_bit, void* stream);
+
+/* SpecAugment time masking (WavLMModel._mask_hidden_states TF:985-1015, _compute_mask_indices TF:834-950):
+ * in the projected features h bf16 [B*L, D] (ldh), n spans of mask_len frames per sample are replaced by
+ * masked_spec_embed (fp32 [D]); n = max(int(mask_prob * L / mask_len + eps), min_masks) (capped as TF), eps
+ * shared by the batch, span starts distinct and uniform in [0, L - mask_len] (device hash RNG).  mask_out
+ * (optional, uint8 [B, L]) receives the masked-frame indicator. */
+int mer_wavlm_time_mask(int B, int L, int D, void* h, long ldh, const float* embed, float mask_prob, int mask_len,
+                        int min_masks, const unsigned long long* seed, unsigned long long site, unsigned char* mask_out,
+                        void* stream);
+
+/* y = x for a contiguous bf16 x, y bf16 (y_dtype 1) or fp32 (0). */
+int mer_bf16_convert(long n, const void* x, void* y, int y_dtype, void* stream);
+
 /* ============================ WavLM stage-2 fine-tuning (backward of the last N layers) ============================
  * The reference unfreezes the last N encoder layers (wavlm_audio.py:70-88 _unfreeze_last_n_layers, called by
  * train.py:817-822 _apply_two_stage_freeze_policy); these entry points are the backward of those layers

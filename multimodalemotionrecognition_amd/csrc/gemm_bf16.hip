@@ -38,7 +38,24 @@ struct GemmArgs {
   long ldr;
   int act;
   int vec_epi;  // pipelined kernels: 16-byte epilogue through LDS (N, ldc, ldr, c_zoff multiples of 8, aligned)
+  // train-mode extras (mer_gemm_bf16_tr): dropout after the activation, before the residual (nn.Dropout of
+  // WavLM's attention output / FFN, TF:286-294,323), mask index = row * N + col; and LayerDrop: the whole
+  // launch is a no-op when bit skip_bit of *skip_mask is set (TF:417-419)
+  float drop_p;
+  const unsigned long long* drop_seed;
+  unsigned long long drop_site;
+  const long long* skip_mask;
+  int skip_bit;
 };
+
+__device__ __forceinline__ bool layer_skipped(const long long* mask, int bit) {
+  return mask != nullptr && ((*mask >> bit) & 1ll);
+}
+// act -> dropout (train mode) of one epilogue element
+__device__ __forceinline__ float epi_act_drop(float v, int act, float p, unsigned long long seed, long idx) {
+  v = apply_act(v, act);
+  return p > 0.f ? v * dropout_scale(seed, (uint64_t)idx, p) : v;
+}
 
 typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;
 
@@ -76,6 +93,8 @@ __device__ __forceinline__ u32x4 load_a_chunk(const GemmArgs& g, int m, int k, i
 template <int AMODE, typename TOUT>
 __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs g) {
   __shared__ __attribute__((aligned(16))) bf16_t lds[2][2][BM * LDSK];  // [buf][A/B][row*LDSK + k]
+  if (layer_skipped(g.skip_mask, g.skip_bit)) return;
+  const unsigned long long dseed = mer_site_seed(g.drop_seed, g.drop_site);
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int z = blockIdx.z;
   const int nx = (g.N + BN - 1) / BN, ny = (g.M + BM - 1) / BM;
@@ -151,7 +170,7 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs g) {
       for (int r = 0; r < 4; ++r) {
         const int row = m0 + wm + i * 16 + (lane >> 4) * 4 + r;
         if (row >= g.M) continue;
-        float v = apply_act(acc[i][j][r] + bv, g.act);
+        float v = epi_act_drop(acc[i][j][r] + bv, g.act, g.drop_p, dseed, (long)row * g.N + col);
         if (g.R) v += bf2f(g.R[(long)row * g.ldr + (long)z * g.c_zoff + col]);
         stf<TOUT>(C, (long)row * g.ldc + col, v);
       }
@@ -191,6 +210,7 @@ __device__ __attribute__((aligned(16))) uint32_t mer_gemm_zero16[4] = {0u, 0u, 0
 template <class CF, typename TOUT, int AMODE>
 __global__ __launch_bounds__(CF::NT, 1) void gemm_pipe_kernel(GemmArgs g) {
   extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
+  if (layer_skipped(g.skip_mask, g.skip_bit)) return;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int z = blockIdx.z;
   const int nx = (g.N + CF::BN - 1) / CF::BN, ny = (g.M + CF::BM - 1) / CF::BM;
@@ -298,6 +318,7 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_pipe_kernel(GemmArgs g) {
   }
 
   TOUT* C = reinterpret_cast<TOUT*>(g.C) + (long)z * g.c_zoff;
+  const unsigned long long dseed = mer_site_seed(g.drop_seed, g.drop_site);
   if (g.vec_epi) {
     // Epilogue through LDS (the ring is idle once every wave is past its last fragment read): each wave
     // stages act(acc + bias) of 16-row groups of its TM x TN sub-tile as fp32 [row][TN + 4] in its own slice
@@ -344,6 +365,10 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_pipe_kernel(GemmArgs g) {
           const f32x4 lo = *reinterpret_cast<const f32x4*>(&wl[rl * LDT + lc]);
           const f32x4 hi = *reinterpret_cast<const f32x4*>(&wl[rl * LDT + lc + 4]);
           float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          if (g.drop_p > 0.f) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] *= dropout_scale(dseed, (uint64_t)((long)row * g.N + colv + e), g.drop_p);
+          }
           if (g.R) {
             const u32x4 rv = *reinterpret_cast<const u32x4*>(g.R + (long)row * g.ldr + (long)z * g.c_zoff + colv);
 #pragma unroll
@@ -372,7 +397,7 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_pipe_kernel(GemmArgs g) {
       for (int r = 0; r < 4; ++r) {
         const int row = m0 + wr * CF::TM + i * 16 + fq * 4 + r;
         if (row >= g.M) continue;
-        float v = apply_act(acc[i][j][r] + bv, g.act);
+        float v = epi_act_drop(acc[i][j][r] + bv, g.act, g.drop_p, dseed, (long)row * g.N + col);
         if (g.R) v += bf2f(g.R[(long)row * g.ldr + (long)z * g.c_zoff + col]);
         stf<TOUT>(C, (long)row * g.ldc + col, v);
       }
@@ -409,6 +434,7 @@ __device__ __forceinline__ void wait_vm_even(int n) {  // n in {0,2,...,10}, wav
 template <typename TOUT>
 __global__ __launch_bounds__(PH_NT, 1) void gemm_phase_kernel(GemmArgs g) {
   extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
+  if (layer_skipped(g.skip_mask, g.skip_bit)) return;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int nx = (g.N + 255) / 256, ny = (g.M + 255) / 256;
   int tx, ty;
@@ -530,6 +556,7 @@ __global__ __launch_bounds__(PH_NT, 1) void gemm_phase_kernel(GemmArgs g) {
   }
 
   TOUT* C = reinterpret_cast<TOUT*>(g.C);
+  const unsigned long long dseed = mer_site_seed(g.drop_seed, g.drop_site);
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int col = n0 + wc * 64 + j * 16 + fr;
@@ -541,7 +568,7 @@ __global__ __launch_bounds__(PH_NT, 1) void gemm_phase_kernel(GemmArgs g) {
       for (int r = 0; r < 4; ++r) {
         const int row = m0 + wr * 128 + i * 16 + fq * 4 + r;
         if (row >= g.M) continue;
-        float v = apply_act(acc[i][j][r] + bv, g.act);
+        float v = epi_act_drop(acc[i][j][r] + bv, g.act, g.drop_p, dseed, (long)row * g.N + col);
         if (g.R) v += bf2f(g.R[(long)row * g.ldr + col]);
         stf<TOUT>(C, (long)row * g.ldc + col, v);
       }
@@ -633,7 +660,18 @@ MER_API int mer_gemm_bf16(int M, int N, int K, const void* A, long a_gstride, lo
 MER_API int mer_gemm_bf16_ex(int M, int N, int K, const void* A, long a_gstride, long a_rstride, int a_rpg,
                              const void* W, long ldw, void* C, int c_dtype, long ldc, const float* bias, const void* R,
                              long ldr, int act, int variant, void* stream) {
+  return mer_gemm_bf16_tr(M, N, K, A, a_gstride, a_rstride, a_rpg, W, ldw, C, c_dtype, ldc, bias, R, ldr, act, 0.f,
+                          nullptr, 0ull, nullptr, 0, variant, stream);
+}
+
+MER_API int mer_gemm_bf16_tr(int M, int N, int K, const void* A, long a_gstride, long a_rstride, int a_rpg,
+                             const void* W, long ldw, void* C, int c_dtype, long ldc, const float* bias, const void* R,
+                             long ldr, int act, float drop_p, const unsigned long long* drop_seed,
+                             unsigned long long drop_site, const long long* skip_mask, int skip_bit, int variant,
+                             void* stream) {
   if (M <= 0 || N <= 0) return 0;
+  if (drop_p < 0.f || drop_p >= 1.f || (drop_p > 0.f && !drop_seed) || skip_bit < 0 || skip_bit > 62)
+    return (int)hipErrorInvalidValue;
   if (variant < -1 || variant > 14) return (int)hipErrorInvalidValue;
   if (K % 8 != 0 || a_rpg <= 0 || (a_rstride % 8) != 0 || (a_gstride % 8) != 0 || (ldw % 8) != 0)
     return (int)hipErrorInvalidValue;
@@ -645,6 +683,7 @@ MER_API int mer_gemm_bf16_ex(int M, int N, int K, const void* A, long a_gstride,
   g.C = C; g.ldc = ldc; g.c_zoff = 0;
   g.bias = bias; g.R = (const bf16_t*)R; g.ldr = ldr; g.act = act;
   g.vec_epi = vec_epilogue_ok(N, C, ldc, R, ldr, 0);
+  g.drop_p = drop_p; g.drop_seed = drop_seed; g.drop_site = drop_site; g.skip_mask = skip_mask; g.skip_bit = skip_bit;
   const hipStream_t st = (hipStream_t)stream;
   if (K % 64 != 0) variant = 0;
   if (variant == -1) variant = pick_variant(M, N, K);

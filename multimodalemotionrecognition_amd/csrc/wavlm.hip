@@ -144,12 +144,19 @@ template <> __device__ __forceinline__ void st4<bf16_t>(bf16_t* p, f32x4 v) {
 }
 
 // VEC: d % 256 == 0 and 4-element aligned rows -- each lane moves 4 consecutive elements per access.
+// Train mode (mer_layernorm_tr): dropout on the OUTPUT (WavLMEncoder.dropout after the encoder LayerNorm,
+// TF:406-407; mask index row * d + c) and the LayerDrop skip of the layer the LN belongs to (TF:417-419).
 template <typename TI, typename TO, bool VEC>
 __global__ __launch_bounds__(256) void layernorm_kernel(int rows, int d, const TI* __restrict__ x, long ldx,
                                                         const float* __restrict__ gamma, const float* __restrict__ beta,
-                                                        float eps, TO* __restrict__ y, long ldy) {
+                                                        float eps, TO* __restrict__ y, long ldy, float drop_p,
+                                                        const unsigned long long* __restrict__ seed_ptr,
+                                                        unsigned long long site, const long long* __restrict__ skip,
+                                                        int skip_bit) {
+  if (skip && ((*skip >> skip_bit) & 1ll)) return;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (row >= rows) return;
+  const unsigned long long seed = mer_site_seed(seed_ptr, site);
   const TI* xr = x + (long)row * ldx;
   TO* yr = y + (long)row * ldy;
   float vals[16];  // d <= 1024
@@ -174,7 +181,10 @@ __global__ __launch_bounds__(256) void layernorm_kernel(int rows, int d, const T
       const f32x4 g = *reinterpret_cast<const f32x4*>(gamma + c), b = *reinterpret_cast<const f32x4*>(beta + c);
       f32x4 o;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) o[e] = (vals[4 * i + e] - mean) * rstd * g[e] + b[e];
+      for (int e = 0; e < 4; ++e) {
+        o[e] = (vals[4 * i + e] - mean) * rstd * g[e] + b[e];
+        if (drop_p > 0.f) o[e] *= dropout_scale(seed, (uint64_t)((long)row * d + c + e), drop_p);
+      }
       st4<TO>(yr + c, o);
     }
     return;
@@ -189,12 +199,26 @@ __global__ __launch_bounds__(256) void layernorm_kernel(int rows, int d, const T
   for (int i = 0; i < n; ++i) { const float v = vals[i] - mean; q += v * v; }
   const float rstd = rsqrtf(wave_sum(q) / d + eps);
   n = 0;
-  for (int c = lane; c < d; c += 64, ++n) stf<TO>(yr, c, (vals[n] - mean) * rstd * gamma[c] + beta[c]);
+  for (int c = lane; c < d; c += 64, ++n) {
+    float o = (vals[n] - mean) * rstd * gamma[c] + beta[c];
+    if (drop_p > 0.f) o *= dropout_scale(seed, (uint64_t)((long)row * d + c), drop_p);
+    stf<TO>(yr, c, o);
+  }
 }
 
 MER_API int mer_layernorm(int rows, int d, const void* x, int x_dtype, long ldx, const float* gamma,
                           const float* beta, float eps, void* y, int y_dtype, long ldy, void* stream) {
+  return mer_layernorm_tr(rows, d, x, x_dtype, ldx, gamma, beta, eps, y, y_dtype, ldy, 0.f, nullptr, 0ull, nullptr, 0,
+                          stream);
+}
+
+MER_API int mer_layernorm_tr(int rows, int d, const void* x, int x_dtype, long ldx, const float* gamma,
+                             const float* beta, float eps, void* y, int y_dtype, long ldy, float drop_p,
+                             const unsigned long long* seed, unsigned long long site, const long long* skip_mask,
+                             int skip_bit, void* stream) {
   if (d > 1024 || rows <= 0) return rows <= 0 ? 0 : (int)hipErrorInvalidValue;
+  if (drop_p < 0.f || drop_p >= 1.f || (drop_p > 0.f && !seed) || skip_bit < 0 || skip_bit > 62)
+    return (int)hipErrorInvalidValue;
   dim3 grid((rows + 3) / 4);
   hipStream_t st = (hipStream_t)stream;
   const bool vec = d % 256 == 0 && ldx % 4 == 0 && ldy % 4 == 0 && ((((uintptr_t)x) | ((uintptr_t)y)) & 7) == 0 &&
@@ -205,10 +229,10 @@ MER_API int mer_layernorm(int rows, int d, const void* x, int x_dtype, long ldx,
   do {                                                                                                         \
     if (vec)                                                                                                   \
       hipLaunchKernelGGL((layernorm_kernel<TI, TO, true>), grid, dim3(256), 0, st, rows, d, (const TI*)x, ldx, \
-                         gamma, beta, eps, (TO*)y, ldy);                                                       \
+                         gamma, beta, eps, (TO*)y, ldy, drop_p, seed, site, skip_mask, skip_bit);             \
     else                                                                                                       \
       hipLaunchKernelGGL((layernorm_kernel<TI, TO, false>), grid, dim3(256), 0, st, rows, d, (const TI*)x, ldx, \
-                         gamma, beta, eps, (TO*)y, ldy);                                                       \
+                         gamma, beta, eps, (TO*)y, ldy, drop_p, seed, site, skip_mask, skip_bit);             \
   } while (0)
   if (x_dtype == MER_F32 && y_dtype == MER_BF16) L(float, bf16_t);
   else if (x_dtype == MER_BF16 && y_dtype == MER_BF16) L(bf16_t, bf16_t);
@@ -243,8 +267,12 @@ __global__ __launch_bounds__(256, 3) void wavlm_attn_kernel(int L, int H, const 
                                                          const float* __restrict__ gconst,
                                                          const float* __restrict__ rel_emb,
                                                          const int* __restrict__ bucket, bf16_t* __restrict__ out,
-                                                         long ldo, float scale) {
+                                                         long ldo, float scale, float drop_p,
+                                                         const unsigned long long* __restrict__ seed_ptr,
+                                                         unsigned long long site, const long long* __restrict__ skip,
+                                                         int skip_bit) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  if (skip && ((*skip >> skip_bit) & 1ll)) return;
   const int LP = (L + 15) / 16 * 16;
   const int VTP = LP + 8;
   bf16_t* Ks = reinterpret_cast<bf16_t*>(smem_raw);   // [LP][APAD]
@@ -412,7 +440,11 @@ __global__ __launch_bounds__(256, 3) void wavlm_attn_kernel(int L, int H, const 
       }
   mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
   mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-  // P^T = exp(S^T - max) rounded to bf16 (the weights that enter PV also form the normaliser)
+  // P^T = exp(S^T - max) rounded to bf16 (the weights that enter PV also form the normaliser).  Train mode:
+  // attention-probability dropout (F.multi_head_attention_forward dropout_p, TF:206-228): dropped weights do
+  // not enter PV, the kept ones are rescaled by 1/(1-p) with the normaliser (mask index ((b*H+h)*L + i)*L + j)
+  const unsigned long long dseed = mer_site_seed(seed_ptr, site);
+  const long mrow = (((long)b * H + h) * L + i) * L;
   float sum = 0.f;
   s16x4 pb[16];
 #pragma unroll
@@ -422,7 +454,9 @@ __global__ __launch_bounds__(256, 3) void wavlm_attn_kernel(int L, int H, const 
       for (int r = 0; r < 4; ++r) {
         const bf16_t p = f2bf(__expf(s[ct][r] - mx));
         sum += bf2f(p);
-        pb[ct][r] = (short)p;
+        const int j = ct * 16 + (lane >> 4) * 4 + r;
+        const bool keep = drop_p <= 0.f || dropout_scale(dseed, (uint64_t)(mrow + j), drop_p) != 0.f;
+        pb[ct][r] = keep ? (short)p : (short)0;
       }
   sum += __shfl_xor(sum, 16, 64);
   sum += __shfl_xor(sum, 32, 64);
@@ -439,7 +473,7 @@ __global__ __launch_bounds__(256, 3) void wavlm_attn_kernel(int L, int H, const 
         o[dt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(va, pb[ct], o[dt], 0, 0, 0);
       }
   if (i < L) {
-    const float inv = 1.f / sum;
+    const float inv = (drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f) / sum;
     bf16_t* orow = out + ((long)b * L + i) * ldo + h * ADH + (lane >> 4) * 4;
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) {
@@ -454,14 +488,25 @@ MER_API int mer_wavlm_attention(int B, int L, int H, const void* qkv, long ldqkv
                                 const float* gate_w, const float* gate_b, const float* gate_const,
                                 const float* rel_emb, const int* bucket, void* out, long ldo, float scale,
                                 void* stream) {
+  return mer_wavlm_attention_tr(B, L, H, qkv, ldqkv, x, ldx, gate_w, gate_b, gate_const, rel_emb, bucket, out, ldo,
+                                scale, 0.f, nullptr, 0ull, nullptr, 0, stream);
+}
+
+MER_API int mer_wavlm_attention_tr(int B, int L, int H, const void* qkv, long ldqkv, const void* x, long ldx,
+                                   const float* gate_w, const float* gate_b, const float* gate_const,
+                                   const float* rel_emb, const int* bucket, void* out, long ldo, float scale,
+                                   float drop_p, const unsigned long long* seed, unsigned long long site,
+                                   const long long* skip_mask, int skip_bit, void* stream) {
   if (L > 256 || L <= 0) return (int)hipErrorInvalidValue;
+  if (drop_p < 0.f || drop_p >= 1.f || (drop_p > 0.f && !seed) || skip_bit < 0 || skip_bit > 62)
+    return (int)hipErrorInvalidValue;
   if ((ldqkv % 8) || (ldx % 8) || (ldo % 4) || ((((uintptr_t)qkv) | ((uintptr_t)x)) & 15) || (((uintptr_t)out) & 7))
     return (int)hipErrorInvalidValue;
   const int LP = (L + 15) / 16 * 16;
   const size_t lds = sizeof(bf16_t) * ((size_t)LP * APAD + (size_t)ADH * (LP + 8)) + sizeof(float) * (64 + 512 + 2 * L);
   hipLaunchKernelGGL(wavlm_attn_kernel, dim3(B * H, (LP / 16 + 3) / 4), dim3(256), lds, (hipStream_t)stream, L, H,
                      (const bf16_t*)qkv, ldqkv, (const bf16_t*)x, ldx, gate_w, gate_b, gate_const, rel_emb, bucket,
-                     (bf16_t*)out, ldo, scale);
+                     (bf16_t*)out, ldo, scale, drop_p, seed, site, skip_mask, skip_bit);
   MER_LAUNCH_CHECK();
 }
 
@@ -518,5 +563,83 @@ __global__ void cast_bf16_kernel(long n, const float* __restrict__ x, bf16_t* __
 MER_API int mer_cast_bf16(long n, const float* x, void* y, void* stream) {
   const int grid = (int)((n + 255) / 256 < 8192 ? (n + 255) / 256 : 8192);
   hipLaunchKernelGGL(cast_bf16_kernel, dim3(grid > 0 ? grid : 1), dim3(256), 0, (hipStream_t)stream, n, x, (bf16_t*)y);
+  MER_LAUNCH_CHECK();
+}
+
+// ---------------------------------------------------------------------------------------
+// SpecAugment time masking of WavLM in train mode (WavLMModel._mask_hidden_states TF:985-1015 with
+// _compute_mask_indices TF:834-950, config mask_time_prob 0.05 / mask_time_length 10 / min_masks 2): the
+// projected features h [B*L, D] get `n` spans of `span` frames replaced by masked_spec_embed, n =
+// max(int(prob * L / span + eps), min_masks) capped as TF does, eps ~ U[0,1) shared by the batch, span starts
+// distinct and uniform over [0, L - span] per sample (Floyd's sampling without replacement -- the distribution
+// of TF's np.random.choice(..., replace=False); the random stream is the device hash, not numpy's).
+// One workgroup per sample; mask_out (optional, uint8 [B, L]) records the masked frames.
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void wavlm_time_mask_kernel(int L, int D, bf16_t* __restrict__ h, long ldh,
+                                                              const float* __restrict__ embed, float prob, int span,
+                                                              int min_masks, const unsigned long long* __restrict__ seed_ptr,
+                                                              unsigned long long site, unsigned char* __restrict__ mask_out) {
+  __shared__ int starts[64];
+  __shared__ int nsp;
+  const int b = blockIdx.x;
+  const unsigned long long seed = mer_site_seed(seed_ptr, site);
+  if (threadIdx.x == 0) {
+    const float eps = (mer_hash(seed, 0) >> 8) * (1.0f / 16777216.0f);
+    int n = (int)(prob * (float)L / (float)span + eps);
+    n = n > min_masks ? n : min_masks;
+    if (n * span > L) n = L / span;
+    if (L - (span - 1) < n) n = L - (span - 1) > 0 ? L - (span - 1) : 0;
+    n = n < 64 ? n : 64;
+    const int N = L - span + 1;
+    int cnt = 0;
+    for (int jj = N - n; jj < N; ++jj) {  // Floyd: uniform n-subset of [0, N)
+      const uint32_t r = mer_hash(seed, 1 + (uint64_t)b * 64 + cnt);
+      const int t = (int)(((uint64_t)r * (uint64_t)(jj + 1)) >> 32);
+      bool present = false;
+      for (int k = 0; k < cnt; ++k) present |= starts[k] == t;
+      starts[cnt++] = present ? jj : t;
+    }
+    nsp = cnt;
+  }
+  __syncthreads();
+  const int n = nsp;
+  if (mask_out) {
+    for (int r = threadIdx.x; r < L; r += blockDim.x) {
+      bool m = false;
+      for (int k = 0; k < n; ++k) m |= r >= starts[k] && r < starts[k] + span;
+      mask_out[(long)b * L + r] = m ? 1 : 0;
+    }
+  }
+  const long tot = (long)n * span * D;
+  for (long e = threadIdx.x; e < tot; e += blockDim.x) {
+    const int k = (int)(e / ((long)span * D));
+    const int rem = (int)(e - (long)k * span * D);
+    const int r = starts[k] + rem / D, c = rem % D;
+    h[((long)b * L + r) * ldh + c] = f2bf(embed[c]);
+  }
+}
+
+MER_API int mer_wavlm_time_mask(int B, int L, int D, void* h, long ldh, const float* embed, float mask_prob,
+                                int mask_len, int min_masks, const unsigned long long* seed, unsigned long long site,
+                                unsigned char* mask_out, void* stream) {
+  if (B <= 0) return 0;
+  if (mask_len < 1 || mask_len > L || !seed || mask_prob < 0.f) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(wavlm_time_mask_kernel, dim3(B), dim3(256), 0, (hipStream_t)stream, L, D, (bf16_t*)h, ldh, embed,
+                     mask_prob, mask_len, min_masks, seed, site, mask_out);
+  MER_LAUNCH_CHECK();
+}
+
+// y = x (bf16 -> bf16 or fp32), contiguous: the train-mode encoder output leaves the in-place layer buffer
+__global__ void bf16_convert_kernel(long n, const bf16_t* __restrict__ x, void* __restrict__ y, int to_f32) {
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < n; e += (long)gridDim.x * blockDim.x) {
+    if (to_f32) reinterpret_cast<float*>(y)[e] = bf2f(x[e]);
+    else reinterpret_cast<bf16_t*>(y)[e] = x[e];
+  }
+}
+MER_API int mer_bf16_convert(long n, const void* x, void* y, int y_dtype, void* stream) {
+  if (n <= 0) return 0;
+  const int grid = (int)((n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096);
+  hipLaunchKernelGGL(bf16_convert_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, n, (const bf16_t*)x, y,
+                     y_dtype == MER_F32 ? 1 : 0);
   MER_LAUNCH_CHECK();
 }

@@ -20,7 +20,7 @@ def _grad_buf(p):
 
 class _EmbHeadFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, a_emb, v_emb, mode, training, rng, drop_a, drop_v, qlin, names, *params):
+    def forward(ctx, a_emb, v_emb, mode, dp, rng, drop_a, drop_v, qlin, names, *params):
         p = dict(zip(names, params))
         lin = linear_runner(p, qlin)
         B = a_emb.shape[0]
@@ -35,7 +35,6 @@ class _EmbHeadFn(torch.autograd.Function):
             a.zero_()
         if drop_v:
             v.zero_()
-        dp = 0.2 if training else 0.0
         sv = {"cat": cat}
         if mode == "concat":
             w0 = p["fusion.0.weight"]
@@ -123,7 +122,9 @@ def embedding_head(model, a_emb, v_emb, drop_a=False, drop_v=False):
     # a dropped modality is cut from the autograd graph (its encoder's backward never runs, as in the reference)
     a_in = a_emb.detach() if drop_a else a_emb
     v_in = v_emb.detach() if drop_v else v_emb
-    return _EmbHeadFn.apply(a_in.contiguous(), v_in.contiguous(), model.mode, model.training, rng,
+    # the nn.Dropout(0.2) of fusion / gate (fusion.py:256-262), active in train mode only
+    dp = float((model.fusion if model.mode == "concat" else model.gate)[2].p) if model.training else 0.0
+    return _EmbHeadFn.apply(a_in.contiguous(), v_in.contiguous(), model.mode, dp, rng,
                             bool(drop_a), bool(drop_v), int8_images(model), tuple(names), *params)
 
 

@@ -41,7 +41,7 @@ PROBE = None
 
 
 def _launch(name, key, fn, *args):
-    if PROBE is not None and PROBE.matches(name, key):
+    if PROBE is not None and PROBE.matches(name, key) and not torch.cuda.is_current_stream_capturing():
         s = torch.cuda.current_stream()
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record(s)
@@ -312,11 +312,23 @@ def _aligned16(*ts):
             raise ValueError("bf16 GEMM operands must be 16-byte aligned")
 
 
-def gemm_bf16(a, w, out, *, M=None, K=None, rows=None, bias=None, residual=None, act="none", variant=-1):
+def _train_args(drop_p, rng, site, skip, skip_bit):
+    """(drop_p, seed ptr, site, skip-mask ptr, bit) of the *_tr entry points, validated."""
+    if drop_p > 0 and rng is None:
+        raise ValueError("dropout needs the step's device RNG base")
+    if skip is not None and (skip.dtype != torch.int64 or skip.numel() != 1 or not skip.is_cuda):
+        raise ValueError("the LayerDrop mask must be a device int64 tensor of one element")
+    return float(drop_p), rng_ptr(rng) if drop_p > 0 else 0, int(site), _ptr(skip), int(skip_bit)
+
+
+def gemm_bf16(a, w, out, *, M=None, K=None, rows=None, bias=None, residual=None, act="none", variant=-1,
+              drop_p=0.0, rng=None, site=0, skip=None, skip_bit=0):
     """out[M,N] = act(A W^T + bias) (+ residual) on bf16 MFMA.
 
     ``a``: bf16 [M,K] (row stride a.stride(0)), or a raw bf16 buffer with ``rows=(rpg, rstride, gstride)``
     describing the channel-last Conv1d im2col rows.  ``w``: bf16 [N,K].  ``out``: bf16 or fp32 [M,N].
+    Train mode: ``drop_p`` / ``rng`` / ``site`` dropout after the activation (before the residual);
+    ``skip`` / ``skip_bit``: LayerDrop (the launch is a no-op when that bit of the device mask is set).
     """
     N = w.shape[0]
     if rows is None:
@@ -327,9 +339,16 @@ def gemm_bf16(a, w, out, *, M=None, K=None, rows=None, bias=None, residual=None,
     if out.shape[-1] != N or out.numel() != M * N:
         raise ValueError(f"gemm_bf16 out shape {tuple(out.shape)} != ({M},{N})")
     _aligned16(a, w)
+    ldc = N if out.dim() < 2 else out.stride(-2)
+    ldr = 0 if residual is None else residual.stride(-2)
+    if drop_p > 0 or skip is not None:
+        _launch("gemm_bf16", (M, N, K), "mer_gemm_bf16_tr", M, N, K, a.data_ptr(), rows[2], rows[1], rows[0],
+                w.data_ptr(), w.stride(0), out.data_ptr(), _dt(out), ldc, _ptr(bias), _ptr(residual), ldr, ACT[act],
+                *_train_args(drop_p, rng, site, skip, skip_bit), int(variant), stream_ptr())
+        return out
     _launch("gemm_bf16", (M, N, K), "mer_gemm_bf16_ex", M, N, K, a.data_ptr(), rows[2], rows[1], rows[0], w.data_ptr(),
-            w.stride(0), out.data_ptr(), _dt(out), N if out.dim() < 2 else out.stride(-2), _ptr(bias), _ptr(residual),
-            0 if residual is None else residual.stride(-2), ACT[act], int(variant), stream_ptr())
+            w.stride(0), out.data_ptr(), _dt(out), ldc, _ptr(bias), _ptr(residual), ldr, ACT[act], int(variant),
+            stream_ptr())
     return out
 
 
@@ -350,17 +369,49 @@ def wavlm_conv0_gn_gelu(wav, w0, gamma, beta, out, eps=1e-5):
         float(eps), ws.data_ptr(), out.data_ptr(), stream_ptr())
 
 
-def layernorm(x2d, gamma, beta, y2d, eps=1e-5):
+def layernorm(x2d, gamma, beta, y2d, eps=1e-5, drop_p=0.0, rng=None, site=0, skip=None, skip_bit=0):
     rows, d = x2d.shape
+    if drop_p > 0 or skip is not None:
+        LIB("mer_layernorm_tr", rows, d, x2d.data_ptr(), _dt(x2d), x2d.stride(0), gamma.data_ptr(), beta.data_ptr(),
+            float(eps), y2d.data_ptr(), _dt(y2d), y2d.stride(0), *_train_args(drop_p, rng, site, skip, skip_bit),
+            stream_ptr())
+        return
     LIB("mer_layernorm", rows, d, x2d.data_ptr(), _dt(x2d), x2d.stride(0), gamma.data_ptr(), beta.data_ptr(),
         float(eps), y2d.data_ptr(), _dt(y2d), y2d.stride(0), stream_ptr())
 
 
-def wavlm_attention(qkv, x, gate_w, gate_b, gate_const, rel_emb, bucket, out, B, L, H, scale):
+def wavlm_attention(qkv, x, gate_w, gate_b, gate_const, rel_emb, bucket, out, B, L, H, scale, drop_p=0.0, rng=None,
+                    site=0, skip=None, skip_bit=0):
     """``bucket`` None: ``rel_emb`` is the per-head bias table [H][2L-1] (``rel_emb[bucket].t()``)."""
+    if drop_p > 0 or skip is not None:
+        LIB("mer_wavlm_attention_tr", B, L, H, qkv.data_ptr(), qkv.stride(0), x.data_ptr(), x.stride(0),
+            gate_w.data_ptr(), gate_b.data_ptr(), gate_const.data_ptr(), rel_emb.data_ptr(), _ptr(bucket),
+            out.data_ptr(), out.stride(0), float(scale), *_train_args(drop_p, rng, site, skip, skip_bit), stream_ptr())
+        return
     LIB("mer_wavlm_attention", B, L, H, qkv.data_ptr(), qkv.stride(0), x.data_ptr(), x.stride(0), gate_w.data_ptr(),
         gate_b.data_ptr(), gate_const.data_ptr(), rel_emb.data_ptr(), _ptr(bucket), out.data_ptr(),
         out.stride(0), float(scale), stream_ptr())
+
+
+def wavlm_time_mask(h, B, L, embed, mask_prob, mask_len, min_masks, rng, site, mask_out=None):
+    """SpecAugment time masking of the projected WavLM features h bf16 [B*L, D] in place."""
+    D = h.shape[-1]
+    if h.dtype != torch.bfloat16 or h.numel() != B * L * D or embed.numel() != D:
+        raise ValueError("wavlm_time_mask shapes")
+    if mask_len > L:
+        raise ValueError(f"`mask_length` has to be smaller than `sequence_length`, but got `mask_length`: {mask_len} "
+                         f"and `sequence_length`: {L}`")  # TF:863-867
+    if mask_out is not None and (mask_out.dtype != torch.uint8 or mask_out.numel() != B * L):
+        raise ValueError("mask_out must be uint8 [B, L]")
+    LIB("mer_wavlm_time_mask", B, L, D, h.data_ptr(), h.stride(-2), embed.detach().contiguous().data_ptr(),
+        float(mask_prob), int(mask_len), int(min_masks), rng_ptr(rng), int(site), _ptr(mask_out), stream_ptr())
+
+
+def bf16_convert(x, y):
+    if x.dtype != torch.bfloat16 or not x.is_contiguous() or not y.is_contiguous() or x.numel() != y.numel():
+        raise ValueError("bf16_convert: contiguous bf16 source of the same size")
+    LIB("mer_bf16_convert", x.numel(), x.data_ptr(), y.data_ptr(), _dt(y), stream_ptr())
+    return y
 
 
 def permute3_bf16(src, shape3, strides3, dst, scale=None):

@@ -127,6 +127,7 @@ class _TrunkGraphs(G.PendingGuard):
         if self.bwd is None or self.bwd[0] != split:
             _, saved = self.fwd.out
             tr, training = self.trunk, self.training
+            tr.prepare_backward(dfeat.device)  # host-side setup (H2D copies) must not happen inside a capture
             if split:
                 ga = G.StaticGraph(lambda d: trunk_backward_start(tr, saved, d, training, split, force_pack=True),
                                    [dfeat])
@@ -160,6 +161,16 @@ class ResNet18Trunk(nn.Sequential):
         self._force_pack = False
         self._graphs = G.GraphCache()
         self.grad_ready_hook = None  # fn(params): gradients of blocks >= SPLIT_BLOCK are final (dist.py)
+
+    def prepare_backward(self, device) -> None:
+        """Create the backward's lazily built device tables outside any graph capture: the transposed pack plan
+        and the stem's space-to-depth weight-gradient index (a gradient-cut first step -- gated ModalityDropout
+        -- can reach the first backward capture with neither built by an eager backward)."""
+        self._pack_plan(True)
+        idx = self.__dict__.get("_mer_stem_idx")
+        if idx is None or idx.device != device:
+            Kc, Cin, R, S = self[0].weight.shape
+            self.__dict__["_mer_stem_idx"] = _stem_wgrad_index(R, S, Cin, device)
 
     def split_params(self, split: int):
         """Parameters whose gradients are final once the backward has passed BasicBlock ``split``."""

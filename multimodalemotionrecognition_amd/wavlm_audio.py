@@ -48,6 +48,38 @@ class WavLMConfigLite:
     num_conv_pos_embeddings = 128
     num_conv_pos_embedding_groups = 16
     layer_norm_eps = 1e-5
+    # train-mode regularisers (WavLMConfig defaults; active whenever the module is in train mode, as in the
+    # reference, which keeps the frozen WavLM in train mode under no_grad: train.py:194, wavlm_audio.py:177-182)
+    hidden_dropout = 0.1
+    attention_dropout = 0.1
+    activation_dropout = 0.1
+    feat_proj_dropout = 0.0
+    layerdrop = 0.1
+    mask_time_prob = 0.05
+    mask_time_length = 10
+    mask_time_min_masks = 2
+
+
+# dropout call sites of the WavLM forward (mixed with the forward's RNG base, csrc/common.h mer_site_seed)
+SITE_TIME_MASK, SITE_ENC_DROPOUT = 1000, 1001
+
+
+def _layer_sites(li: int):
+    """(attention probs, attention output, FFN activation, FFN output) dropout sites of encoder layer li."""
+    b = 1100 + 8 * li
+    return b, b + 1, b + 2, b + 3
+
+
+class TrainCtl:
+    """Host-drawn randomness of one train-mode WavLM forward: the dropout / SpecAugment RNG base and the LayerDrop
+    bitmask (bit i set = layer i skipped; TF:417-419 draws torch.rand([]) per layer, layer 0 never skipped).
+    ``rng`` / ``skip`` are device int64 scalars the kernels read (graph-capturable)."""
+
+    def __init__(self, seed: int, mask: int, rng: torch.Tensor, skip: torch.Tensor):
+        self.seed, self.mask, self.rng, self.skip = seed, mask, rng, skip
+
+    def executed(self, num_layers: int) -> int:
+        return sum(1 for i in range(num_layers) if not (self.mask >> i) & 1)
 
 
 class _ConvLayer(nn.Module):
@@ -145,6 +177,46 @@ class WavLMBackbone(nn.Module):
         self._packed_key = None
         self._buckets: Dict[tuple, torch.Tensor] = {}
         self._graphs = G.GraphCache()
+        # reference semantics: train mode = dropout + LayerDrop + SpecAugment; False runs train mode with eval
+        # semantics (deterministic parity tests against the fp32 oracle)
+        self.train_semantics = True
+        self.executed_layers = 0  # encoder layers actually run by train-mode forwards (bench.py's FLOP count)
+        self.train_forwards = 0
+
+    # ---- train-mode randomness ----
+    def train_active(self) -> bool:
+        return self.training and self.train_semantics
+
+    def draw_train(self, num_layers: Optional[int] = None):
+        """(seed, LayerDrop mask) for one train-mode forward, from the host generators (torch.manual_seed
+        reproduces them); None in eval semantics."""
+        if not self.train_active():
+            return None
+        cfg = self.config
+        seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+        r = torch.rand(cfg.num_hidden_layers)
+        mask = 0
+        for i in range(1, cfg.num_hidden_layers):
+            if float(r[i]) < cfg.layerdrop:
+                mask |= 1 << i
+        nl = cfg.num_hidden_layers if num_layers is None else num_layers
+        self.executed_layers += sum(1 for i in range(nl) if not (mask >> i) & 1)
+        self.train_forwards += 1
+        return seed, mask
+
+    @staticmethod
+    def train_ctl(draw, device, rng=None, skip=None) -> Optional[TrainCtl]:
+        """Device scalars of a draw (fresh, or refilled static graph buffers)."""
+        if draw is None:
+            return None
+        seed, mask = draw
+        if rng is None:
+            rng = torch.full((1,), seed, dtype=torch.int64, device=device)
+            skip = torch.full((1,), mask, dtype=torch.int64, device=device)
+        else:
+            rng.fill_(seed)
+            skip.fill_(mask)
+        return TrainCtl(seed, mask, rng, skip)
 
     # ---- frozen-weight preparation (runs once per weight version, on the GPU kernels) ----
     def _param_list(self):
@@ -231,41 +303,65 @@ class WavLMBackbone(nn.Module):
         """Raw waveform [B, S] fp32 -> last_hidden_state [B, L, 768] (bf16 or fp32).
 
         ``capture`` (tests): receives copies of 'extract_features' (post-LN conv features, what HF
-        returns as ``extract_features``) and 'layer0' (output of encoder layer 0).
+        returns as ``extract_features``) and 'layer0' (output of encoder layer 0).  In train mode (reference
+        semantics) the forward applies SpecAugment time masking, dropout and LayerDrop (``draw_train``).
 
-        After two eager calls per input shape the schedule runs as two captured hipGraphs (graphs.py):
-        [conv0, GroupNorm+GELU] and [conv2 .. final LayerNorm], with the conv1 GEMM launched eagerly
-        between them (it is the kernel bench.py times with HIP events)."""
+        After one eager call per input shape the whole schedule (conv0 .. final LayerNorm) runs as one
+        captured hipGraph (graphs.py); a train-mode graph re-reads its RNG base and LayerDrop mask from two
+        device scalars refilled before each replay."""
         if not wav.is_cuda:
             raise RuntimeError("WavLM runs on the MI355X kernels; move the waveform to the GPU")
         wav = wav.contiguous().float()
         nl = None if num_layers is None or num_layers >= len(self.encoder.layers) else int(num_layers)
+        draw = self.draw_train(nl)
+        self.__dict__["_last_draw"] = draw
         if capture is None and not G.capturing():
             # a prefix run (stage 2) is keyed on the prefix's weights only: the trainable tail changes every step
             wkey = self._weights_key()
-            key = (tuple(wav.shape), out_dtype, wav.device.index, nl,
+            split = K.PROBE is not None and K.PROBE.active and K.PROBE.name == "gemm_bf16"
+            key = (tuple(wav.shape), out_dtype, wav.device.index, nl, draw is not None, split,
                    wkey if nl is None else wkey[:self._prefix_param_count(nl)])
             if self._graphs.ready(key):
-                return self._forward_graphed(wav, out_dtype, key, nl)
+                return self._forward_graphed(wav, out_dtype, key, nl, draw, split)
+        ctl = self.train_ctl(draw, wav.device)
         x, L = self._stage_a(wav)
         y = self._conv_layer(x, 1, L)
-        return self._stage_b(y, L, out_dtype, nl, capture)
+        return self._stage_b(y, L, out_dtype, nl, capture, ctl)
 
-    def _forward_graphed(self, wav, out_dtype, key, nl=None):
+    def _forward_graphed(self, wav, out_dtype, key, nl=None, draw=None, split=False):
+        """One captured graph per key.  ``split`` (bench.py's kernel probe only, never the timed schedule): two
+        graphs around an eager launch of the feature-extractor conv1 GEMM, which the probe brackets with HIP
+        events on its stream."""
         g = self._graphs.get(key)
         if g is None:
-            ga = G.StaticGraph(lambda w: self._stage_a(w)[0], [wav])
-            B, L0 = wav.shape[0], ga.out.shape[1]
-            L1 = (L0 - CONV_KERNEL[1]) // CONV_STRIDE[1] + 1
-            y1 = torch.empty(B, L1, CONV_DIM, device=wav.device, dtype=torch.bfloat16)
-            gb = G.StaticGraph(lambda: self._stage_b(y1, L0, out_dtype, nl, None), [])
-            # the graphs read the packed weights captured with them: keep that pack alive (a later full repack,
+            ctl = None
+            if draw is not None:  # static RNG-base / LayerDrop-mask scalars the graph reads
+                ctl = self.train_ctl(draw, wav.device)
+            if split:
+                ga = G.StaticGraph(lambda w: self._stage_a(w)[0], [wav])
+                B, L0 = wav.shape[0], ga.out.shape[1]
+                L1 = (L0 - CONV_KERNEL[1]) // CONV_STRIDE[1] + 1
+                y1 = torch.empty(B, L1, CONV_DIM, device=wav.device, dtype=torch.bfloat16)
+                gb = G.StaticGraph(lambda: self._stage_b(y1, L0, out_dtype, nl, None, ctl), [])
+                graph = (ga, y1, gb)
+            else:
+                def run(w):
+                    x, L0 = self._stage_a(w)
+                    return self._stage_b(self._conv_layer(x, 1, L0), L0, out_dtype, nl, None, ctl)
+
+                graph = G.StaticGraph(run, [wav])
+            # the graph reads the packed weights captured with it: keep that pack alive (a later full repack,
             # e.g. after the stage-2 tail moved, replaces self._packed while a prefix key still matches)
-            g = self._graphs.put(key, (ga, y1, gb, self._packed))
-        ga, y1, gb, _ = g
-        x = ga.replay(wav)
-        self._conv_layer(x, 1, x.shape[1], out=y1)
-        return gb.replay().clone()
+            g = self._graphs.put(key, (graph, ctl, self._packed))
+        graph, ctl, _ = g
+        if draw is not None:
+            self.train_ctl(draw, wav.device, ctl.rng, ctl.skip)
+        if split:
+            ga, y1, gb = graph
+            x = ga.replay(wav)
+            self._conv_layer(x, 1, x.shape[1], out=y1)
+            return gb.replay().clone()
+        return graph.replay(wav).clone()
 
     def _stage_a(self, wav):
         """conv0 -> GroupNorm + GELU (one fused deterministic kernel pair): [B, S] -> [B, L0, 512] bf16."""
@@ -287,8 +383,9 @@ class WavLMBackbone(nn.Module):
                     rows=(L_out, s * CONV_DIM, L * CONV_DIM), act="gelu")
         return y
 
-    def _stage_b(self, x, L0, out_dtype, num_layers, capture):
-        """conv2..6 -> feature projection -> positional conv -> 12 encoder layers (x = conv1 output)."""
+    def _stage_b(self, x, L0, out_dtype, num_layers, capture, ctl: Optional[TrainCtl] = None):
+        """conv2..6 -> feature projection (-> SpecAugment) -> positional conv -> encoder LN (-> dropout) -> encoder
+        layers (x = conv1 output).  ``ctl``: train-mode randomness (None = eval semantics)."""
         cfg = self.config
         pk = self.packed_weights()
         B = x.shape[0]
@@ -305,14 +402,21 @@ class WavLMBackbone(nn.Module):
         if capture is not None:
             capture["extract_features"] = xn.view(B, L, CONV_DIM).clone()
         h = torch.empty(B * L, D, device=dev, dtype=bf)
-        K.gemm_bf16(xn, pk["proj_w"], h, bias=fp.projection.bias)
+        K.gemm_bf16(xn, pk["proj_w"], h, bias=fp.projection.bias)  # feat_proj_dropout = 0 (TF:98-104)
+        tr = ctl is not None
+        if tr and cfg.mask_time_prob > 0:  # SpecAugment on the projected features (TF:1063 -> 1006-1015)
+            K.wavlm_time_mask(h, B, L, self.masked_spec_embed, cfg.mask_time_prob, cfg.mask_time_length,
+                              cfg.mask_time_min_masks, ctl.rng, SITE_TIME_MASK,
+                              mask_out=capture.get("mask_out") if capture is not None else None)
         # positional conv: h + gelu(posconv(h) + bias)  (TF:82-90, 414-416)
         pc = self.encoder.pos_conv_embed.conv
         hp = torch.empty(B * L, D, device=dev, dtype=bf)
         K.posconv_gemm_bf16(h, pk["posconv_w"], hp, B, L, D, cfg.num_conv_pos_embedding_groups,
                             cfg.num_conv_pos_embeddings, cfg.num_conv_pos_embeddings // 2, pc.bias, h, act="gelu")
         x = torch.empty(B * L, D, device=dev, dtype=bf)
-        K.layernorm(hp, self.encoder.layer_norm.weight, self.encoder.layer_norm.bias, x, eps=cfg.layer_norm_eps)
+        hd = cfg.hidden_dropout if tr else 0.0
+        K.layernorm(hp, self.encoder.layer_norm.weight, self.encoder.layer_norm.bias, x, eps=cfg.layer_norm_eps,
+                    drop_p=hd, rng=ctl.rng if tr else None, site=SITE_ENC_DROPOUT)
         H = cfg.num_attention_heads
         # the relative-position bias rows of every head, gathered once per packed-weight version and length
         # (layer 0's embedding serves all layers, TF:380-385): [H][2L-1], read directly by the attention kernel
@@ -327,25 +431,35 @@ class WavLMBackbone(nn.Module):
         y32 = torch.empty(B * L, D, device=dev, dtype=torch.float32)
         x1 = torch.empty(B * L, D, device=dev, dtype=bf)
         ff = torch.empty(B * L, cfg.intermediate_size, device=dev, dtype=bf)
+        ad, acd = (cfg.attention_dropout, cfg.activation_dropout) if tr else (0.0, 0.0)
+        rng = ctl.rng if tr else None
         for li in range(nl):
             layer = self.encoder.layers[li]
             lw = pk["layers"][li]
             at = layer.attention
-            K.gemm_bf16(x, lw["qkv_w"], qkv, bias=lw["qkv_b"])
+            # LayerDrop (train): every launch of a skipped layer is a no-op, so x passes through unchanged
+            sk = dict(skip=ctl.skip, skip_bit=li) if tr else {}
+            s_att, s_out, s_act, s_ffn = _layer_sites(li)
+            K.gemm_bf16(x, lw["qkv_w"], qkv, bias=lw["qkv_b"], **sk)
             K.wavlm_attention(qkv, x, at.gru_rel_pos_linear.weight, at.gru_rel_pos_linear.bias, lw["gate_c"],
-                              bias_tbl, None, att, B, L, H, scale)
-            K.gemm_bf16(att, lw["out_w"], y32, bias=at.out_proj.bias, residual=x)
-            K.layernorm(y32, layer.layer_norm.weight, layer.layer_norm.bias, x1, eps=cfg.layer_norm_eps)
-            K.gemm_bf16(x1, lw["ff1_w"], ff, bias=layer.feed_forward.intermediate_dense.bias, act="gelu")
-            K.gemm_bf16(ff, lw["ff2_w"], y32, bias=layer.feed_forward.output_dense.bias, residual=x1)
+                              bias_tbl, None, att, B, L, H, scale, drop_p=ad, rng=rng, site=s_att, **sk)
+            K.gemm_bf16(att, lw["out_w"], y32, bias=at.out_proj.bias, residual=x, drop_p=hd, rng=rng, site=s_out, **sk)
+            K.layernorm(y32, layer.layer_norm.weight, layer.layer_norm.bias, x1, eps=cfg.layer_norm_eps, **sk)
+            K.gemm_bf16(x1, lw["ff1_w"], ff, bias=layer.feed_forward.intermediate_dense.bias, act="gelu",
+                        drop_p=acd, rng=rng, site=s_act, **sk)
+            K.gemm_bf16(ff, lw["ff2_w"], y32, bias=layer.feed_forward.output_dense.bias, residual=x1, drop_p=hd,
+                        rng=rng, site=s_ffn, **sk)
             last = li == nl - 1
-            xo = torch.empty(B * L, D, device=dev, dtype=out_dtype) if last else x
-            K.layernorm(y32, layer.final_layer_norm.weight, layer.final_layer_norm.bias, xo, eps=cfg.layer_norm_eps)
+            # train mode writes every layer in place (a skipped last layer must leave x as the output)
+            xo = torch.empty(B * L, D, device=dev, dtype=out_dtype) if (last and not tr) else x
+            K.layernorm(y32, layer.final_layer_norm.weight, layer.final_layer_norm.bias, xo, eps=cfg.layer_norm_eps,
+                        **sk)
             x = xo
             if capture is not None and li == 0:
                 capture["layer0"] = x.view(B, L, D).clone()
+        if x.dtype != out_dtype:  # train mode (in-place layers) or an empty stack: the bf16 buffer -> out_dtype
+            x = K.bf16_convert(x, torch.empty(B * L, D, device=dev, dtype=out_dtype))
         return x.view(B, L, D)
-
 
     # ---- stage-2 fine-tuning: backward through the unfrozen last layers ----
     def first_trainable_layer(self) -> int:
@@ -363,8 +477,9 @@ class WavLMBackbone(nn.Module):
         return first
 
     def forward_prefix(self, wav: torch.Tensor):
-        """The frozen part of a stage-2 forward: conv stack + layers [0, first) -> (bf16 [B, L, D], bias table).
-        Independent of the trainable weights, so it can run ahead (``FusionModel.prefetch_audio``)."""
+        """The frozen part of a stage-2 forward: conv stack + layers [0, first) -> (bf16 [B, L, D], bias table,
+        LayerDrop mask of the forward -- its bits >= first decide the trainable layers).  Independent of the
+        trainable weights, so it can run ahead (``FusionModel.prefetch_audio``)."""
         if not wav.is_cuda:
             raise RuntimeError("WavLM runs on the MI355X kernels; move the waveform to the GPU")
         first = self.first_trainable_layer()
@@ -373,25 +488,30 @@ class WavLMBackbone(nn.Module):
             with torch.no_grad():
                 x = self.forward_hip(wav.contiguous().float(), out_dtype=torch.bfloat16, num_layers=first)
                 tbl = self.packed_weights()["bias_tables"][x.shape[1]]
+                draw = self.__dict__.get("_last_draw")
         finally:
             self.__dict__["_pack_limit"] = None
-        return x, tbl
+        if draw is not None:  # the trainable layers' executions (the prefix counted its own)
+            self.executed_layers += sum(1 for i in range(first, len(self.encoder.layers)) if not (draw[1] >> i) & 1)
+        return x, tbl, (draw[1] if draw is not None else 0)
 
     def forward_train(self, wav: torch.Tensor, prefix=None) -> torch.Tensor:
         """Stage-2 forward: frozen conv stack + layers [0, first) on the inference schedule (or ``prefix``, a
         ``forward_prefix`` result computed ahead), then layers [first, 12) saving their activations.  Returns
         fp32 [B, L, 768] tracked by autograd."""
         first = self.first_trainable_layer()
-        x, tbl = prefix if prefix is not None else self.forward_prefix(wav)
+        x, tbl, mask = prefix if prefix is not None else self.forward_prefix(wav)
         names, params = [], []
         for li in range(first, len(self.encoder.layers)):
             for n, q in self.encoder.layers[li].named_parameters():
                 names.append((li, n))
                 params.append(q)
-        return _WavLMTailFn.apply(x, tbl, self, first, tuple(names), *params)
+        return _WavLMTailFn.apply(x, tbl, self, first, mask, tuple(names), *params)
 
-    def tail_forward(self, x, tbl, first):
-        """Layers [first, 12) on bf16 x [B, L, D]; returns (fp32 output [B*L, D], saved activations)."""
+    def tail_forward(self, x, tbl, first, mask: int = 0):
+        """Layers [first, 12) on bf16 x [B, L, D]; returns (fp32 output [B*L, D], saved activations).  Layers
+        whose bit is set in the LayerDrop ``mask`` (train mode, TF:417-419) are skipped: no activations are saved
+        and their parameters get no gradient (torch Adam then leaves them alone, as in the reference)."""
         cfg = self.config
         B, L, D = x.shape
         H = cfg.num_attention_heads
@@ -403,6 +523,9 @@ class WavLMBackbone(nn.Module):
         h = x.reshape(M, D)
         saved = []
         for li in range(first, nl):
+            if (mask >> li) & 1:
+                saved.append(None)
+                continue
             layer = self.encoder.layers[li]
             at = layer.attention
             lw = _pack_layer(layer, dev)
@@ -428,6 +551,8 @@ class WavLMBackbone(nn.Module):
             sv.update(qkv=qkv, att=att, y1=y1, x1=x1, z=z, f=f, y2=y2)
             saved.append(sv)
             h = out
+        if h.dtype != torch.float32:  # the last layer(s) dropped: the output is the bf16 input of that layer
+            h = K.bf16_convert(h.contiguous(), torch.empty(M, D, device=dev, dtype=torch.float32))
         return h, saved
 
     def tail_backward(self, dout, saved, tbl, first, B, L, grads):
@@ -442,6 +567,8 @@ class WavLMBackbone(nn.Module):
         addends = (dout.reshape(M, D).contiguous(), None, None)
         for k in range(len(saved) - 1, -1, -1):
             li = first + k
+            if saved[k] is None:  # LayerDrop: the layer was the identity
+                continue
             sv, layer = saved[k], self.encoder.layers[li]
             at, ff = layer.attention, layer.feed_forward
             lw = sv["pack"]
@@ -526,11 +653,11 @@ class _WavLMTailFn(torch.autograd.Function):
     tail_backward writing each parameter gradient straight into its ``grad_buffer`` slot."""
 
     @staticmethod
-    def forward(ctx, x, tbl, enc, first, names, *params):
-        out, saved = enc.tail_forward(x, tbl, first)
+    def forward(ctx, x, tbl, enc, first, mask, names, *params):
+        out, saved = enc.tail_forward(x, tbl, first, mask)
         B, L, D = x.shape
         ctx.enc, ctx.first, ctx.saved, ctx.tbl, ctx.shape = enc, first, saved, tbl, (B, L)
-        ctx.params = params
+        ctx.params, ctx.names = params, names
         return out.view(B, L, D)
 
     @staticmethod
@@ -538,10 +665,12 @@ class _WavLMTailFn(torch.autograd.Function):
         from .fusion import grad_buffer
 
         B, L = ctx.shape
-        grads = {q: grad_buffer(q) for q in ctx.params}
+        ran = {ctx.first + k for k, sv in enumerate(ctx.saved) if sv is not None}
+        grads = {q: grad_buffer(q) for (li, _), q in zip(ctx.names, ctx.params) if li in ran}
         ctx.enc.tail_backward(dout.float().contiguous(), ctx.saved, ctx.tbl, ctx.first, B, L, grads)
         ctx.saved = None
-        return (None, None, None, None, None) + tuple(grads[q] if q.requires_grad else None for q in ctx.params)
+        return (None, None, None, None, None, None) + tuple(
+            grads[q] if (q.requires_grad and q in grads) else None for q in ctx.params)
 
 
 class WavLMAudioEncoder(nn.Module):

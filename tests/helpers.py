@@ -60,3 +60,28 @@ def check_grad(g, key: str, grad, atol: float):
     scale = max(1.0, float(np.sqrt(grad.shape[0] * grad.shape[1])))
     np.testing.assert_allclose(grad.sum(0), g["grad." + key + ".colsum"], atol=atol * scale, err_msg=key + " colsum")
     np.testing.assert_allclose(grad.sum(1), g["grad." + key + ".rowsum"], atol=atol * scale, err_msg=key + " rowsum")
+
+
+# ---- restatement of the kernels' counter-based dropout RNG (csrc/common.h mer_hash / mer_site_seed /
+# dropout_scale), so masks can be checked bit-exactly on the host ----
+_M64 = (1 << 64) - 1
+
+
+def site_seed(base: int, site: int) -> int:
+    return (base * 0x100000001B3 + site * 0x9E3779B97F4A7C15 + 1) & _M64
+
+
+def hash_u32(seed: int, idx: np.ndarray) -> np.ndarray:
+    idx = np.asarray(idx, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        z = np.uint64(seed) + np.uint64(0x9E3779B97F4A7C15) * (idx + np.uint64(1))
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z ^= z >> np.uint64(31)
+    return (z & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+
+
+def dropout_keep(base: int, site: int, idx: np.ndarray, p: float) -> np.ndarray:
+    """Boolean keep mask of the kernels' dropout for element indices ``idx``."""
+    u = (hash_u32(site_seed(base, site), idx) >> np.uint32(8)).astype(np.float32) * np.float32(1.0 / 16777216.0)
+    return u >= np.float32(p)

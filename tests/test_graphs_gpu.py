@@ -57,6 +57,7 @@ def _twin(seed):
     m.attn_dropout = 0.0
     m.v_drop_path.drop_prob = m.a_drop_path.drop_prob = 0.0
     m.xattn_mlp[2].p = 0.0
+    m.audio_model.wavlm.train_semantics = False  # (train-mode WavLM graphs: tests/test_wavlm_train_gpu.py)
     opt = build_optimizer(m)
     return m, TrainStep(m, opt, make_loss("xattn"), "xattn")
 

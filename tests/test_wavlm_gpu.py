@@ -30,6 +30,9 @@ def build_backbone():
     assert got == sorted(wavlm_ref.wavlm_param_shapes()), "state-dict names must match transformers' WavLMModel"
     sd = {k: torch.from_numpy(params.init_tensor(k, tuple(v.shape))) for k, v in m.state_dict().items()}
     m.load_state_dict(sd)
+    # deterministic parity against the oracle / the eval-mode golden: train-mode randomness (SpecAugment, dropout,
+    # LayerDrop) off; its statistics are tested in tests/test_wavlm_train_gpu.py
+    m.train_semantics = False
     return m.cuda()
 
 

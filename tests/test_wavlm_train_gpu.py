@@ -1,0 +1,213 @@
+"""WavLM train-mode semantics (the reference keeps the frozen WavLM in train mode under no_grad: train.py:194,
+wavlm_audio.py:177-182 -> TF:417-419 LayerDrop, TF:1006-1015 SpecAugment, dropout 0.1 at TF:206-228, 286-294,
+323, 407).  Stochastic ops cannot bit-match torch / numpy RNG streams, so they are pinned by:
+
+* bit-exact masks against a host restatement of the kernels' counter-based RNG (tests/helpers.dropout_keep):
+  the dropout epilogue of the bf16 GEMM, the encoder LayerNorm output dropout, the attention-probability
+  dropout (checked against an fp64 softmax-with-that-mask reference);
+* LayerDrop: forced masks reproduce shorter eval-semantics stacks bit for bit; the drawn rate of executed
+  layers is 1 + 11 * 0.9 = 10.9 per forward;
+* SpecAugment: the per-frame masking frequency matches transformers' own _compute_mask_indices (TF:834-950)
+  run on the same shape, every sample masks >= one full span, and masked frames carry masked_spec_embed;
+* reproducibility under torch.manual_seed, and the captured train-mode graph == the eager schedule.
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import params
+from tests.helpers import dropout_keep
+from tests.test_wavlm_gpu import build_backbone
+
+pytestmark = pytest.mark.gpu
+
+
+def _wav(b, seed):
+    _, audio, _ = params.clip_inputs(b, seed=seed)
+    return torch.from_numpy(audio).squeeze(1).cuda()
+
+
+def _train_backbone():
+    m = build_backbone()
+    m.train_semantics = True
+    return m.train()
+
+
+def test_gemm_dropout_epilogue_mask_is_exact():
+    from multimodalemotionrecognition_amd import kernels as K
+
+    torch.manual_seed(0)
+    M, N, Kd = 300, 768, 512
+    a = torch.randn(M, Kd, device="cuda").to(torch.bfloat16)
+    w = (0.05 * torch.randn(N, Kd, device="cuda")).to(torch.bfloat16)
+    bias = torch.randn(N, device="cuda")
+    rng = torch.full((1,), 123456789, dtype=torch.int64, device="cuda")
+    y0 = K.gemm_bf16(a, w, torch.empty(M, N, device="cuda"), bias=bias, act="gelu")
+    y1 = K.gemm_bf16(a, w, torch.empty(M, N, device="cuda"), bias=bias, act="gelu", drop_p=0.1, rng=rng, site=7)
+    keep = torch.from_numpy(dropout_keep(123456789, 7, np.arange(M * N), 0.1).reshape(M, N))
+    ref = torch.where(keep, y0.cpu() * np.float32(1 / 0.9), torch.zeros(()))
+    assert torch.equal(y1.cpu(), ref)
+    assert abs(float(keep.float().mean()) - 0.9) < 0.01
+    # LayerDrop: a set bit turns the launch into a no-op (the output buffer is left untouched)
+    skip = torch.full((1,), 1 << 5, dtype=torch.int64, device="cuda")
+    y2 = torch.full((M, N), 7.0, device="cuda")
+    K.gemm_bf16(a, w, y2, bias=bias, skip=skip, skip_bit=5)
+    assert bool((y2 == 7.0).all())
+    K.gemm_bf16(a, w, y2, bias=bias, act="gelu", skip=skip, skip_bit=4)
+    assert torch.equal(y2, y0)
+
+
+def test_attention_probability_dropout_exact_mask():
+    """mer_wavlm_attention_tr: dropped probabilities leave PV, kept ones are scaled by 1/(1-p) (torch
+    F.dropout on the softmax, TF:206-228); reference in fp64 with the kernel's mask."""
+    from multimodalemotionrecognition_amd import kernels as K
+
+    torch.manual_seed(1)
+    B, L, H, dh = 2, 149, 12, 64
+    D = H * dh
+    qkv = (0.5 * torch.randn(B * L, 3 * D, device="cuda")).to(torch.bfloat16)
+    x = torch.randn(B * L, D, device="cuda").to(torch.bfloat16)
+    gw, gb = 0.1 * torch.randn(8, dh, device="cuda"), 0.1 * torch.randn(8, device="cuda")
+    gc = torch.ones(H, device="cuda")
+    tbl = 0.1 * torch.randn(H, 2 * L - 1, device="cuda")
+    rng = torch.full((1,), 99, dtype=torch.int64, device="cuda")
+    out = torch.empty(B * L, D, device="cuda", dtype=torch.bfloat16)
+    K.wavlm_attention(qkv, x, gw, gb, gc, tbl, None, out, B, L, H, dh ** -0.5, drop_p=0.1, rng=rng, site=1100)
+    # fp64 reference with the same gate / bias / mask
+    q, k, v = [qkv[:, i * D:(i + 1) * D].double().cpu().view(B, L, H, dh).transpose(1, 2) for i in range(3)]
+    xs = x.double().cpu().view(B, L, H, dh).transpose(1, 2)
+    pr = (xs @ gw.double().cpu().t() + gb.double().cpu()).view(B, H, L, 2, 4).sum(-1)
+    ga, gbb = torch.sigmoid(pr).unbind(-1)
+    gate = ga * (gbb * gc.double().cpu().view(1, H, 1) - 1.0) + 2.0
+    rel = torch.arange(L)[None, :] - torch.arange(L)[:, None] + L - 1
+    bias = tbl.double().cpu()[:, rel]  # [H, L, L]
+    s = (q @ k.transpose(-1, -2)) * dh ** -0.5 + gate[..., None] * bias[None]
+    p = torch.softmax(s, -1)
+    idx = np.arange(B * H * L * L)
+    keep = torch.from_numpy(dropout_keep(99, 1100, idx, 0.1).reshape(B, H, L, L))
+    o = ((p * keep) @ v) / 0.9
+    ref = o.transpose(1, 2).reshape(B * L, D)
+    err = float((out.double().cpu() - ref).abs().max() / ref.abs().max())
+    print("attention dropout max rel err", err)
+    assert err < 2e-2  # bf16 probabilities / outputs
+
+
+def test_encoder_dropout_keep_rate_and_scale():
+    """WavLMEncoder.dropout after the encoder LayerNorm (TF:407): with no encoder layers run, the train-mode
+    output is the eval output times the kernel's keep mask / 0.9."""
+    m = _train_backbone()
+    m.config = type("Cfg", (m.config.__class__,), {"mask_time_prob": 0.0, "layerdrop": 0.0})()
+    wav = _wav(2, 41)
+    m.train_semantics = False
+    ref = m.forward_hip(wav, out_dtype=torch.float32, num_layers=0).cpu()
+    m.train_semantics = True
+    torch.manual_seed(5)
+    got = m.forward_hip(wav, out_dtype=torch.float32, num_layers=0).cpu()
+    torch.manual_seed(5)
+    seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+    from multimodalemotionrecognition_amd.wavlm_audio import SITE_ENC_DROPOUT
+    keep = torch.from_numpy(dropout_keep(seed, SITE_ENC_DROPOUT, np.arange(ref.numel()), 0.1).reshape(ref.shape))
+    # the kernel scales in fp32 before the bf16 store; the eval output is already bf16-rounded
+    exact = torch.where(keep, ref / np.float32(0.9), torch.zeros(()))
+    d = (got - exact).abs().max() / exact.abs().max()
+    assert float(d) < 1e-2, float(d)
+    assert abs(float((got == 0).float().mean()) - 0.1) < 0.01
+
+
+def test_layerdrop_forced_masks_match_shorter_stacks():
+    """Skipped layers are the identity (TF:419-433): every dropout / SpecAugment off, a forced LayerDrop mask
+    reproduces the eval-semantics stack of the kept prefix bit for bit."""
+    m = _train_backbone()
+    m.config = type("Cfg", (m.config.__class__,), {"mask_time_prob": 0.0, "hidden_dropout": 0.0,
+                                                    "attention_dropout": 0.0, "activation_dropout": 0.0})()
+    wav = _wav(2, 42)
+    m.train_semantics = False
+    ref1 = m.forward_hip(wav, num_layers=1).clone()
+    ref11 = m.forward_hip(wav, num_layers=11).clone()
+    m.train_semantics = True
+    for mask, ref in (((1 << 12) - 2, ref1), (1 << 11, ref11)):
+        m.draw_train = lambda nl=None, mask=mask: (77, mask)
+        got = m.forward_hip(wav)
+        assert torch.equal(got, ref), hex(mask)
+
+
+def test_layerdrop_rate():
+    m = _train_backbone()
+    torch.manual_seed(3)
+    n = 400
+    ex = [sum(1 for i in range(12) if not (m.draw_train()[1] >> i) & 1) for _ in range(n)]
+    mean = float(np.mean(ex))
+    print("executed layers per forward", mean)
+    assert abs(mean - 10.9) < 5 * math.sqrt(11 * 0.09 / n)
+    assert min(ex) >= 1  # layer 0 never skipped
+
+
+def test_spec_augment_matches_transformers_statistics():
+    from transformers.models.wavlm.modeling_wavlm import _compute_mask_indices
+
+    from multimodalemotionrecognition_amd import kernels as K
+
+    m = _train_backbone()
+    cfg = m.config
+    B, L, D, reps = 32, 149, 768, 40
+    freq = np.zeros(L)
+    per_sample = []
+    for r in range(reps):
+        h = torch.zeros(B * L, D, device="cuda", dtype=torch.bfloat16)
+        mo = torch.empty(B, L, device="cuda", dtype=torch.uint8)
+        rng = torch.full((1,), 1000 + r, dtype=torch.int64, device="cuda")
+        K.wavlm_time_mask(h, B, L, m.masked_spec_embed, cfg.mask_time_prob, cfg.mask_time_length,
+                          cfg.mask_time_min_masks, rng, 1000, mask_out=mo)
+        mk = mo.cpu().numpy().astype(bool)
+        freq += mk.sum(0)
+        per_sample += list(mk.sum(1))
+        # masked rows hold masked_spec_embed (bf16), the others are untouched
+        hh = h.view(B, L, D).float().cpu()
+        emb = m.masked_spec_embed.detach().to(torch.bfloat16).float().cpu()
+        assert torch.equal(hh[torch.from_numpy(mk)], emb.expand(int(mk.sum()), D))
+        assert bool((hh[torch.from_numpy(~mk)] == 0).all())
+    np.random.seed(0)
+    tf = np.zeros(L)
+    tf_per = []
+    for _ in range(reps):
+        mk = _compute_mask_indices((B, L), cfg.mask_time_prob, cfg.mask_time_length, min_masks=cfg.mask_time_min_masks)
+        tf += mk.sum(0)
+        tf_per += list(mk.sum(1))
+    n = B * reps
+    print("masked frames per sample: ours", np.mean(per_sample), "transformers", np.mean(tf_per))
+    assert min(per_sample) >= cfg.mask_time_length and max(per_sample) <= 2 * cfg.mask_time_length
+    assert abs(np.mean(per_sample) - np.mean(tf_per)) < 0.5
+    # per-frame masking probability, binned by 10 frames, within 5 sigma of transformers'
+    fo, ft = freq.reshape(-1)[:140].reshape(14, 10).sum(1) / n, tf[:140].reshape(14, 10).sum(1) / n
+    sig = np.sqrt(np.maximum(ft, 1e-3) * 10 / n)
+    assert np.all(np.abs(fo - ft) < 5 * sig + 0.02), (fo, ft)
+
+
+def test_train_forward_reproducible_and_graph_matches_eager():
+    from multimodalemotionrecognition_amd import graphs as G
+
+    wav = _wav(4, 43)
+    prev = G.ENABLED
+    try:
+        outs = {}
+        for on in (False, True):
+            G.ENABLED = on
+            m = _train_backbone()
+            res = []
+            for it in range(3):  # eager, capture + replay, replay
+                torch.manual_seed(200 + it)
+                res.append(m.forward_hip(wav).clone())
+            outs[on] = res
+            if on:
+                assert m._graphs.graphs, "train-mode WavLM graph was not captured"
+        for a, b in zip(outs[False], outs[True]):
+            assert torch.equal(a, b)
+        assert not torch.equal(outs[False][0], outs[False][1])  # different seeds -> different masks
+    finally:
+        G.ENABLED = prev
+    # eval semantics are deterministic and differ from train mode
+    m = build_backbone().eval()
+    e1, e2 = m.forward_hip(wav).clone(), m.forward_hip(wav).clone()
+    assert torch.equal(e1, e2) and not torch.equal(e1, outs[False][0])
