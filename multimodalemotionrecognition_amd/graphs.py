@@ -13,6 +13,7 @@ Set ``MER_GRAPHS=0`` to run every launch eagerly (A/B and debugging).
 """
 from __future__ import annotations
 
+import gc
 import os
 from typing import Callable, Dict, Optional
 
@@ -30,14 +31,24 @@ class StaticGraph:
         # torch.inference_mode() (the batch-inference runtime): inference tensors cannot be updated in place
         # later by a replay's input copy, nor can the CUDA generator's graph-safe state tensors that the
         # first capture of the process creates.
+        # No garbage collection while capturing: a collected cycle holding an older graph (or its memory pool)
+        # would destroy it mid-capture, which HIP refuses ("operation not permitted when stream is capturing")
+        # from inside a destructor -- an abort, not an exception.
+        was_enabled = gc.isenabled()
         with torch.inference_mode(False):
             self.static_in = [t.detach().clone() for t in example_inputs]
             self.graph = torch.cuda.CUDAGraph()
             cur = stream if stream is not None else torch.cuda.current_stream()
             side = torch.cuda.Stream(device=cur.device)
             side.wait_stream(cur)
-            with torch.cuda.graph(self.graph, stream=side):
-                self.out = fn(*self.static_in)
+            gc.collect()
+            gc.disable()
+            try:
+                with torch.cuda.graph(self.graph, stream=side):
+                    self.out = fn(*self.static_in)
+            finally:
+                if was_enabled:
+                    gc.enable()
             cur.wait_stream(side)
 
     def replay(self, *inputs):

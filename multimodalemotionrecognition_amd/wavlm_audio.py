@@ -570,6 +570,9 @@ class WavLMBackbone(nn.Module):
             if saved[k] is None:  # LayerDrop: the layer was the identity
                 continue
             sv, layer = saved[k], self.encoder.layers[li]
+            cap = self.__dict__.get("_capture_upstream")
+            if cap is not None:  # tests: the gradient arriving at this layer's output (sum of the addends)
+                cap[li] = tuple(a.detach().clone() if a is not None else None for a in addends)
             at, ff = layer.attention, layer.feed_forward
             lw = sv["pack"]
             g = grads
