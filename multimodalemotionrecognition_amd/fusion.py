@@ -398,7 +398,8 @@ class FusionModel(nn.Module):
         cur = torch.cuda.current_stream(audio.device)
         cur.wait_stream(pf[2])
         for tsr in (pf[1] if isinstance(pf[1], tuple) else (pf[1],)):
-            tsr.record_stream(cur)
+            if isinstance(tsr, torch.Tensor):
+                tsr.record_stream(cur)
         return pf[1]
 
     # ---- data-parallel support (dist.GradAllReduce) ----
