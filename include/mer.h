@@ -467,6 +467,53 @@ int mer_gemm_i8dyn(int M, int N, int K, const void* x, int x_dtype, long ldx, co
 int mer_concat_prior_rows(int B, int L, int d, int pd, int ldo, const float* tok, const float* prior, float* out,
                           void* stream);
 
+/* ============================ fused xattn head (csrc/xattn_fused.hip) ============================
+ * The xattn branch after the encoders (fusion.py:372-411: projections, v2a / a2v nn.MultiheadAttention with
+ * residual + StochasticDepth + LayerNorm, mean TemporalPooler, concat / gated head) in four launches, every
+ * product on split-bf16 MFMA (fp32 operands as bf16 hi + lo planes, fp32 accumulation).  d_model 128, 4 heads.
+ * Dropout / drop-path: attention-probability masks index ((b*H + h)*Lq + i)*Lk + j, drop-path one draw per
+ * sample, MLP dropout row*H1 + col -- the conventions of mer_mha_fwd / mer_add_ln_fwd / mer_dropout_inplace,
+ * so mer_mha_bwd / mer_add_ln_bwd and the rest of the unfused backward regenerate the same masks. */
+
+/* Split n fp32 weights into bf16 hi / lo planes for each descriptor row (src, hi, lo, n) of the device int64
+ * table desc[n_items][4]. */
+int mer_xh_split(int n_items, const long long* desc, void* stream);
+
+/* F1: a_s = aseq Ws^T + bs (aseq bf16 [M][S], the WavLM features), a = a_s Wa^T + ba, [q2 | kv1] = a Wc^T +
+ * [bq2 | bkv1] (Wc = [a2v in_proj q rows; v2a in_proj k, v rows], 384 x 128).  Outputs fp32: a_s, a, q2 [M][128],
+ * kv1 [M][256].  S % 32 == 0. */
+int mer_xh_audio_fwd(int M, int S, const void* aseq, long ldas, const void* Ws_hi, const void* Ws_lo, const float* bs,
+                     const void* Wa_hi, const void* Wa_lo, const float* ba, const void* Wc_hi, const void* Wc_lo,
+                     const float* bq2, const float* bkv1, float* a_s, float* a, float* q2, float* kv1, void* stream);
+
+/* F2 (one workgroup per sample, T <= 16, Ta <= 160): v = vfeat Wv^T + bv, q1 = v Wq1^T + bq1, v2a attention over
+ * kv1, o1 Wo1^T + bo1, v1 = LayerNorm(v + keep_b * v2) (saving the pre-LN sum, mean, rstd), kv2 = v1 Wkv2^T + bkv2,
+ * emb[b][0:128] = mean_t v1.  P1 [B][4][T][Ta] receives the pre-dropout probabilities. */
+int mer_xh_v2a_fwd(int B, int T, int Ta, int vdim, const float* vfeat, const void* Wv_hi, const void* Wv_lo,
+                   const float* bv, const void* Wq1_hi, const void* Wq1_lo, const float* bq1, const float* kv1,
+                   const void* Wo1_hi, const void* Wo1_lo, const float* bo1, const float* gamma, const float* beta,
+                   const void* Wkv2_hi, const void* Wkv2_lo, const float* bkv2, float attn_p, float path_p,
+                   const unsigned long long* seed, unsigned long long site_attn, unsigned long long site_path,
+                   float scale, float* v, float* q1, float* P1, float* o1, float* s_v, float* mean_v, float* rstd_v,
+                   float* v1, float* kv2, float* emb, long ld_emb, void* stream);
+
+/* F3 (one workgroup per (sample, 16 query rows)): a2v attention of q2 over kv2 (T keys), o2 Wo2^T + bo2,
+ * a1 = LayerNorm(a + keep_b * a2) (pre-LN sum / mean / rstd saved), part[b][tile][128] = column sums of a1 over the
+ * tile's rows.  P2 [B][4][Ta][T]. */
+int mer_xh_a2v_fwd(int B, int T, int Ta, const float* q2, const float* kv2, const float* a, const void* Wo2_hi,
+                   const void* Wo2_lo, const float* bo2, const float* gamma, const float* beta, float attn_p,
+                   float path_p, const unsigned long long* seed, unsigned long long site_attn,
+                   unsigned long long site_path, float scale, float* P2, float* o2, float* s_a, float* mean_a,
+                   float* rstd_a, float* part, void* stream);
+
+/* F4: emb[b][128:256] = sum_tiles part / Ta (tile order), then the classifier: concat (gated = 0):
+ * h = dropout(relu(emb W0^T + b0)) [B][H1], logits = h W3^T + b3; gated: h [B][H1 = 128], g = sigmoid(h W3^T + b3),
+ * fused = g emb_v + (1 - g) emb_a (gsave [B], fsave [B][128]), logits = fused Wc^T + bc.  Exact fp32 FMA. */
+int mer_xh_mlp_fwd(int B, int Ta, int gated, int H1, int C, const float* part, float* emb, const float* W0,
+                   const float* b0, const float* W3, const float* b3, const float* Wc, const float* bc, float mlp_p,
+                   const unsigned long long* seed, unsigned long long site, float* hsave, float* gsave, float* fsave,
+                   float* logits, void* stream);
+
 /* ============================ CLIP-style alignment (concat / gated, fusion_align_mode="clip") ============
  * ClipStyleAlignment.forward after its two projections (fusion.py:137-150): a_n / v_n = F.normalize rows,
  * logits = min(exp(logit_scale), 100) * a_n v_n^T, loss = (CE(logits, arange) + CE(logits^T, arange)) / 2.

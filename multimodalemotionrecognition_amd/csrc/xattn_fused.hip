@@ -1,0 +1,649 @@
+// Fused xattn head forward (fusion.py:366-411, the north-star block) on split-bf16 MFMA.
+//
+// Arithmetic: every matrix product runs on v_mfma_f32_16x16x32_bf16 with each fp32 operand split into
+// bf16 hi + lo planes (x = hi + lo to ~16 mantissa bits, both RNE): A.B ~= Ah.Bh + Ah.Bl + Al.Bh with fp32
+// accumulation (the dropped Al.Bl term is ~2^-16 relative).  Operands that are bf16 to begin with (the WavLM
+// features) have no lo plane and skip that pass.  This keeps the head at fp32-class accuracy (logits within
+// 1e-4 of the reference goldens) at 16/3 x the exact-f32 MFMA rate.  Weights are split once per step by
+// mer_xh_split (they change every Adam step); activations are split in registers as fragments are built.
+//
+// Four launches replace the ~40-launch schedule of xattn_head.py (mean temporal pooling; concat / gated):
+//   F1 xh_audio_fwd (grid B*Ta/32): a_seq(bf16) -> a_s = audio_seq_proj -> a = a_in_proj -> [q2 | k1 v1]
+//      (the a2v query projection and the v2a key/value projections share the input a)
+//   F2 xh_v2a_fwd (grid B): v = v_in_proj(v_feat) -> q1 -> MHA over the sample's Ta keys -> out-proj ->
+//      drop-path + residual + LayerNorm -> v1 -> [k2 v2] (the a2v key/value projections) + mean-pool of v1
+//   F3 xh_a2v_fwd (grid B * ceil(Ta/16)): MHA of 16 query rows over the sample's T keys -> out-proj ->
+//      drop-path + residual + LayerNorm -> a1, per-tile column sums of a1 (the a-side mean pool)
+//   F4 xh_mlp_fwd (grid ceil(B/4)): a-pool fold, concat MLP (or gated head) -> logits, exact fp32 FMA
+// Every tensor the backward (xattn_head.head_backward) reads is written out with the same layout as the
+// unfused schedule.  Fragment maps (v_mfma_f32_16x16x32_bf16): A lane l = row l&15, k = 8*(l>>4)..+7;
+// B lane l = col l&15, same k; C/D col = l&15, row = 4*(l>>4) + r.
+#include "common.h"
+#include "mer.h"
+
+namespace {
+
+constexpr int XD = 128;      // d_model
+constexpr int XH = 4;        // heads
+constexpr int XDH = 32;      // head dim
+constexpr int LDA = XD + 4;  // LDS row stride (floats) of 128-wide activation tiles
+
+typedef __attribute__((ext_vector_type(4))) uint32_t u4;
+
+union Frag {
+  bf16x8 v;
+  uint16_t h[8];
+  u4 u;
+};
+
+__device__ __forceinline__ f32x4 mma(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// 8 fp32 -> (hi, lo) bf16 fragments
+__device__ __forceinline__ void split8(const float (&x)[8], bf16x8& hi, bf16x8& lo) {
+  Frag H, L;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const uint16_t hb = f2bf(x[e]);
+    H.h[e] = hb;
+    L.h[e] = f2bf(x[e] - bf2f(hb));
+  }
+  hi = H.v;
+  lo = L.v;
+}
+
+// fp32 fragment: 8 consecutive k (stride 1) of one row; zero when !valid
+__device__ __forceinline__ void frag_row(const float* p, bool valid, bf16x8& hi, bf16x8& lo) {
+  float x[8];
+  if (valid) {
+    const f32x4 a = *reinterpret_cast<const f32x4*>(p), b = *reinterpret_cast<const f32x4*>(p + 4);
+    x[0] = a[0]; x[1] = a[1]; x[2] = a[2]; x[3] = a[3]; x[4] = b[0]; x[5] = b[1]; x[6] = b[2]; x[7] = b[3];
+  } else {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) x[e] = 0.f;
+  }
+  split8(x, hi, lo);
+}
+
+// fp32 fragment gathered with a k stride (transposed operand); element e valid while k0 + e < kmax
+__device__ __forceinline__ void frag_col(const float* p, long ks, int k0, int kmax, bool valid, bf16x8& hi,
+                                         bf16x8& lo) {
+  float x[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) x[e] = (valid && k0 + e < kmax) ? p[(long)e * ks] : 0.f;
+  split8(x, hi, lo);
+}
+
+// pre-split weight fragment (row n of [N][K] hi / lo planes)
+__device__ __forceinline__ void frag_w(const bf16_t* hi_p, const bf16_t* lo_p, bf16x8& hi, bf16x8& lo) {
+  Frag H, L;
+  H.u = *reinterpret_cast<const u4*>(hi_p);
+  L.u = *reinterpret_cast<const u4*>(lo_p);
+  hi = H.v;
+  lo = L.v;
+}
+
+__device__ __forceinline__ f32x4 mma3(bf16x8 ah, bf16x8 al, bf16x8 bh, bf16x8 bl, f32x4 c) {
+  c = mma(ah, bh, c);
+  c = mma(ah, bl, c);
+  return mma(al, bh, c);
+}
+
+__device__ __forceinline__ void wave_sync_lds() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+struct SplitW {  // one weight's pre-split planes [N][K]
+  const bf16_t* hi;
+  const bf16_t* lo;
+};
+
+// acc[i][j] (+)= A[rows 16i..][0:K] . W[cols c0 + 16j..][0:K]^T with A fp32 rows (row stride lda, 16-byte aligned),
+// rows >= rmax read as zero; W pre-split [N][K] (ldw elements)
+template <int TI, int TJ>
+__device__ __forceinline__ void mm_aw(f32x4 (&acc)[TI][TJ], const float* A, long lda, int rmax, int K, SplitW W,
+                                      long ldw, int c0) {
+  const int lane = threadIdx.x & 63, fr = lane & 15, fk = (lane >> 4) * 8;
+  for (int k = 0; k < K; k += 32) {
+    bf16x8 bh[TJ], bl[TJ];
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const long off = (long)(c0 + 16 * j + fr) * ldw + k + fk;
+      frag_w(W.hi + off, W.lo + off, bh[j], bl[j]);
+    }
+#pragma unroll
+    for (int i = 0; i < TI; ++i) {
+      const int r = 16 * i + fr;
+      bf16x8 ah, al;
+      frag_row(A + (long)r * lda + k + fk, r < rmax, ah, al);
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) acc[i][j] = mma3(ah, al, bh[j], bl[j], acc[i][j]);
+    }
+  }
+}
+
+template <int TI, int TJ>
+__device__ __forceinline__ void zero(f32x4 (&acc)[TI][TJ]) {
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+}
+
+// store acc + bias[col] into an fp32 LDS tile (stride lds_ld) and / or a global matrix (rows < rmax)
+template <int TI, int TJ>
+__device__ __forceinline__ void store_acc(const f32x4 (&acc)[TI][TJ], int c0, const float* bias, float* lds, int lds_ld,
+                                          float* g, long ldg, long grow0, int rmax) {
+  const int lane = threadIdx.x & 63, fr = lane & 15, fq = lane >> 4;
+#pragma unroll
+  for (int j = 0; j < TJ; ++j) {
+    const int col = c0 + 16 * j + fr;
+    const float bv = bias ? bias[col] : 0.f;
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = 16 * i + 4 * fq + r;
+        const float v = acc[i][j][r] + bv;
+        if (lds) lds[row * lds_ld + col] = row < rmax ? v : 0.f;
+        if (g && row < rmax) g[(grow0 + row) * ldg + col] = v;
+      }
+  }
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------------------------
+// weight split: dst_hi / dst_lo (bf16) of n fp32 values, for a table of (src, hi, lo, n) descriptors
+// ---------------------------------------------------------------------------------------------
+__global__ void xh_split_kernel(const long long* __restrict__ desc) {
+  const long long* d = desc + 4 * blockIdx.y;
+  const float* src = reinterpret_cast<const float*>(d[0]);
+  bf16_t* hi = reinterpret_cast<bf16_t*>(d[1]);
+  bf16_t* lo = reinterpret_cast<bf16_t*>(d[2]);
+  const long n = d[3];
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < n; e += (long)gridDim.x * blockDim.x) {
+    const float x = src[e];
+    const bf16_t h = f2bf(x);
+    hi[e] = h;
+    lo[e] = f2bf(x - bf2f(h));
+  }
+}
+
+MER_API int mer_xh_split(int n_items, const long long* desc, void* stream) {
+  if (n_items <= 0) return 0;
+  hipLaunchKernelGGL(xh_split_kernel, dim3(64, n_items), dim3(256), 0, (hipStream_t)stream, desc);
+  MER_LAUNCH_CHECK();
+}
+
+// ---------------------------------------------------------------------------------------------
+// F1: audio token chain.  32 rows per block, 4 waves.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void xh_audio_fwd_kernel(int M, int S, const bf16_t* __restrict__ aseq, long ldas,
+                                                           SplitW Ws, const float* __restrict__ bs, SplitW Wa,
+                                                           const float* __restrict__ ba, SplitW Wc,
+                                                           const float* __restrict__ bq2, const float* __restrict__ bkv1,
+                                                           float* __restrict__ a_s, float* __restrict__ a,
+                                                           float* __restrict__ q2, float* __restrict__ kv1) {
+  __shared__ __attribute__((aligned(16))) float asL[32 * LDA];
+  __shared__ __attribute__((aligned(16))) float aL[32 * LDA];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, fr = lane & 15, fk = (lane >> 4) * 8;
+  const long r0 = (long)blockIdx.x * 32;
+  const int rmax = (int)(M - r0 < 32 ? M - r0 : 32);
+  // a_s = a_seq Ws^T + bs  (A exact bf16: two passes)
+  {
+    f32x4 acc[2][2];
+    zero(acc);
+    const int c0 = 32 * w;
+    for (int k = 0; k < S; k += 32) {
+      bf16x8 bh[2], bl[2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const long off = (long)(c0 + 16 * j + fr) * S + k + fk;
+        frag_w(Ws.hi + off, Ws.lo + off, bh[j], bl[j]);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int r = 16 * i + fr;
+        Frag A;
+        A.u = r < rmax ? *reinterpret_cast<const u4*>(aseq + (r0 + r) * ldas + k + fk) : u4{0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          acc[i][j] = mma(A.v, bh[j], acc[i][j]);
+          acc[i][j] = mma(A.v, bl[j], acc[i][j]);
+        }
+      }
+    }
+    store_acc(acc, c0, bs, asL, LDA, a_s, XD, r0, rmax);
+  }
+  __syncthreads();
+  {  // a = a_s Wa^T + ba
+    f32x4 acc[2][2];
+    zero(acc);
+    mm_aw(acc, asL, LDA, 32, XD, Wa, XD, 32 * w);
+    store_acc(acc, 32 * w, ba, aL, LDA, a, XD, r0, rmax);
+  }
+  __syncthreads();
+  {  // [q2 | k1 v1] = a Wc^T + [bq2 | bkv1]: 384 columns, 96 per wave
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      f32x4 acc[2][3];
+      zero(acc);
+      const int c0 = 96 * w + 48 * half;
+      mm_aw(acc, aL, LDA, 32, XD, Wc, XD, c0);
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const int col = c0 + 16 * j + fr;
+        const bool isq = col < XD;
+        const float bv = isq ? bq2[col] : bkv1[col - XD];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = 16 * i + 4 * (lane >> 4) + r;
+            if (row >= rmax) continue;
+            const float v = acc[i][j][r] + bv;
+            if (isq) q2[(r0 + row) * XD + col] = v;
+            else kv1[(r0 + row) * 2 * XD + col - XD] = v;
+          }
+      }
+    }
+  }
+}
+
+MER_API int mer_xh_audio_fwd(int M, int S, const void* aseq, long ldas, const void* Ws_hi, const void* Ws_lo,
+                             const float* bs, const void* Wa_hi, const void* Wa_lo, const float* ba, const void* Wc_hi,
+                             const void* Wc_lo, const float* bq2, const float* bkv1, float* a_s, float* a, float* q2,
+                             float* kv1, void* stream) {
+  if (M <= 0) return 0;
+  if (S % 32 || ldas % 8 || ((uintptr_t)aseq & 15)) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(xh_audio_fwd_kernel, dim3((M + 31) / 32), dim3(256), 0, (hipStream_t)stream, M, S,
+                     (const bf16_t*)aseq, ldas, SplitW{(const bf16_t*)Ws_hi, (const bf16_t*)Ws_lo}, bs,
+                     SplitW{(const bf16_t*)Wa_hi, (const bf16_t*)Wa_lo}, ba,
+                     SplitW{(const bf16_t*)Wc_hi, (const bf16_t*)Wc_lo}, bq2, bkv1, a_s, a, q2, kv1);
+  MER_LAUNCH_CHECK();
+}
+
+// ---------------------------------------------------------------------------------------------
+// Shared attention pieces.  One wave owns one head: S (16 query rows x up to 16*NT keys) in registers,
+// softmax by in-lane + 16-lane xor reductions, P (pre-dropout) to global, P' = dropout(P) through the
+// wave's LDS tile into O_h = P' V_h.
+// ---------------------------------------------------------------------------------------------
+template <int NT>
+__device__ __forceinline__ void head_attention(int b, int h, int i0, int Lq, int Lk, const float* Qrows, long ldq,
+                                               const float* Krows, const float* Vrows, long ldkv, float scale,
+                                               float* P, float drop_p, unsigned long long dseed, float* PL, int pld,
+                                               float* oL) {
+  const int lane = threadIdx.x & 63, fr = lane & 15, fq = lane >> 4, fk = fq * 8;
+  // S = Q_h K_h^T: A = Q rows (k = head dims), B[n = key][k] = K rows
+  f32x4 s[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) s[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  {
+    bf16x8 ah, al;
+    frag_row(Qrows + (long)fr * ldq + h * XDH + fk, i0 + fr < Lq, ah, al);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int j = 16 * t + fr;
+      bf16x8 bh, bl;
+      frag_row(Krows + (long)j * ldkv + h * XDH + fk, j < Lk, bh, bl);
+      s[t] = mma3(ah, al, bh, bl, s[t]);
+    }
+  }
+  float mx[4], sum[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) mx[r] = -INFINITY;
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int j = 16 * t + fr;
+      s[t][r] = j < Lk ? s[t][r] * scale : -INFINITY;
+      mx[r] = fmaxf(mx[r], s[t][r]);
+    }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) mx[r] = fmaxf(mx[r], __shfl_xor(mx[r], o, 64));
+    sum[r] = 0.f;
+  }
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float e = 16 * t + fr < Lk ? __expf(s[t][r] - mx[r]) : 0.f;
+      s[t][r] = e;
+      sum[r] += e;
+    }
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) sum[r] += __shfl_xor(sum[r], o, 64);
+  const int KP = 16 * NT;  // keys padded to the tile; PV contracts over KP rounded up to 32
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = i0 + 4 * fq + r, j = 16 * t + fr;
+      float pd = 0.f;
+      if (i < Lq && j < Lk) {
+        const float pr = s[t][r] / sum[r];
+        const long pi = (((long)b * XH + h) * Lq + i) * Lk + j;
+        P[pi] = pr;
+        pd = pr * dropout_scale(dseed, pi, drop_p);
+      }
+      PL[(4 * fq + r) * pld + j] = pd;
+    }
+  if (KP % 32) {  // zero the pad chunk the contraction reads
+    for (int e = lane; e < 16 * 16; e += 64) PL[(e >> 4) * pld + KP + (e & 15)] = 0.f;
+  }
+  wave_sync_lds();
+  // O_h = P' V_h: A = P' (16 x KP32), B[n = head dim][k = key] = V rows (gathered with stride ldkv)
+  const int KC = (KP + 31) / 32 * 32;
+  f32x4 o[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+  for (int k = 0; k < KC; k += 32) {
+    bf16x8 ah, al;
+    frag_row(PL + fr * pld + k + fk, true, ah, al);
+#pragma unroll
+    for (int jt = 0; jt < 2; ++jt) {
+      bf16x8 bh, bl;
+      frag_col(Vrows + (long)(k + fk) * ldkv + h * XDH + 16 * jt + fr, ldkv, k + fk, Lk, true, bh, bl);
+      o[jt] = mma3(ah, al, bh, bl, o[jt]);
+    }
+  }
+#pragma unroll
+  for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) oL[(4 * fq + r) * LDA + h * XDH + 16 * jt + fr] = o[jt][r];
+}
+
+// s = x + keep_b * y; LayerNorm(s) over 128 columns for `nrows` rows of LDS tiles (one wave per row);
+// saves s / mean / rstd (global rows grow0 + r) and writes the normalised row to out (LDS) and / or g_out
+__device__ __forceinline__ void add_ln_rows(int nrows, const float* xL, const float* yL, float keep_scale,
+                                            const float* gamma, const float* beta, float* outL, float* s_g,
+                                            float* mean_g, float* rstd_g, long grow0) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int r = w; r < nrows; r += 4) {
+    const float v0 = xL[r * LDA + lane] + keep_scale * yL[r * LDA + lane];
+    const float v1 = xL[r * LDA + 64 + lane] + keep_scale * yL[r * LDA + 64 + lane];
+    const float mean = wave_sum(v0 + v1) / XD;
+    const float d0 = v0 - mean, d1 = v1 - mean;
+    const float rstd = rsqrtf(wave_sum(d0 * d0 + d1 * d1) / XD + 1e-5f);
+    outL[r * LDA + lane] = d0 * rstd * gamma[lane] + beta[lane];
+    outL[r * LDA + 64 + lane] = d1 * rstd * gamma[64 + lane] + beta[64 + lane];
+    s_g[(grow0 + r) * XD + lane] = v0;
+    s_g[(grow0 + r) * XD + 64 + lane] = v1;
+    if (lane == 0) {
+      mean_g[grow0 + r] = mean;
+      rstd_g[grow0 + r] = rstd;
+    }
+  }
+}
+
+struct XhDrop {  // dropout / drop-path of the head (train mode), sites as xattn_head.py
+  float attn, path;
+  const unsigned long long* seed;
+  unsigned long long site_attn, site_path;
+};
+
+// ---------------------------------------------------------------------------------------------
+// F2: v2a block, one workgroup per sample (T <= 16 query rows).
+// ---------------------------------------------------------------------------------------------
+constexpr int F2_KT = 10;                 // Ta <= 160 keys
+constexpr int F2_PLD = 16 * F2_KT + 20;   // P' tile stride (>= 32-padded keys)
+
+__global__ __launch_bounds__(256) void xh_v2a_fwd_kernel(
+    int T, int Ta, int vdim, const float* __restrict__ vfeat, SplitW Wv, const float* __restrict__ bv, SplitW Wq1,
+    const float* __restrict__ bq1, const float* __restrict__ kv1, SplitW Wo1, const float* __restrict__ bo1,
+    const float* __restrict__ gamma, const float* __restrict__ beta, SplitW Wkv2, const float* __restrict__ bkv2,
+    XhDrop dr, float scale, float* __restrict__ v, float* __restrict__ q1, float* __restrict__ P1,
+    float* __restrict__ o1, float* __restrict__ s_v, float* __restrict__ mean_v, float* __restrict__ rstd_v,
+    float* __restrict__ v1, float* __restrict__ kv2, float* __restrict__ emb, long ld_emb) {
+  extern __shared__ __attribute__((aligned(16))) float f2smem[];  // F2_LDS_BYTES
+  float* vL = f2smem;
+  float* qL = vL + 16 * LDA;
+  float* oL = qL + 16 * LDA;
+  float* PL = oL + 16 * LDA;  // [XH][16][F2_PLD]
+  float* tL = PL;             // the out-projection tile reuses P' once the attention is done
+  const int b = blockIdx.x, w = threadIdx.x >> 6;
+  const long row0 = (long)b * T;
+  const unsigned long long seed_attn = mer_site_seed(dr.seed, dr.site_attn);
+  const unsigned long long seed_path = mer_site_seed(dr.seed, dr.site_path);
+  {  // v = v_feat Wv^T + bv
+    f32x4 acc[1][2];
+    zero(acc);
+    mm_aw(acc, vfeat + row0 * vdim, vdim, T, vdim, Wv, vdim, 32 * w);
+    store_acc(acc, 32 * w, bv, vL, LDA, v, XD, row0, T);
+  }
+  __syncthreads();
+  {  // q1 = v Wq1^T + bq1
+    f32x4 acc[1][2];
+    zero(acc);
+    mm_aw(acc, vL, LDA, 16, XD, Wq1, XD, 32 * w);
+    store_acc(acc, 32 * w, bq1, qL, LDA, q1, XD, row0, T);
+  }
+  __syncthreads();
+  // attention: wave w = head w, keys = this sample's Ta rows of kv1 (k | v)
+  head_attention<F2_KT>(b, w, 0, T, Ta, qL, LDA, kv1 + (long)b * Ta * 2 * XD, kv1 + (long)b * Ta * 2 * XD + XD, 2 * XD,
+                        scale, P1, dr.attn, seed_attn, PL + w * 16 * F2_PLD, F2_PLD, oL);
+  __syncthreads();
+  for (int e = threadIdx.x; e < T * XD; e += 256) o1[row0 * XD + e] = oL[(e / XD) * LDA + e % XD];
+  {  // v2 = o Wo1^T + bo1
+    f32x4 acc[1][2];
+    zero(acc);
+    mm_aw(acc, oL, LDA, 16, XD, Wo1, XD, 32 * w);
+    store_acc(acc, 32 * w, bo1, tL, LDA, nullptr, 0, 0, 16);
+  }
+  __syncthreads();
+  // v1 = LN(v + keep_b * v2)  (StochasticDepth: one keep draw per sample, fusion.py:11-26)
+  add_ln_rows(T, vL, tL, dropout_scale(seed_path, b, dr.path), gamma, beta, qL, s_v, mean_v, rstd_v, row0);
+  __syncthreads();
+  for (int e = threadIdx.x; e < T * XD; e += 256) v1[row0 * XD + e] = qL[(e / XD) * LDA + e % XD];
+  for (int e = threadIdx.x; e < (16 - T) * XD; e += 256) qL[(T + e / XD) * LDA + e % XD] = 0.f;
+  if (threadIdx.x < XD) {  // mean temporal pool of v1 (temporal.py:108-109) -> emb[b, 0:d]
+    float s = 0.f;
+    for (int r = 0; r < T; ++r) s += qL[r * LDA + threadIdx.x];
+    emb[(long)b * ld_emb + threadIdx.x] = s / T;
+  }
+  __syncthreads();
+  {  // [k2 v2] = v1 Wkv2^T + bkv2: 256 columns, 64 per wave
+    f32x4 acc[1][4];
+    zero(acc);
+    mm_aw(acc, qL, LDA, 16, XD, Wkv2, XD, 64 * w);
+    store_acc(acc, 64 * w, bkv2, nullptr, 0, kv2, 2 * XD, row0, T);
+  }
+}
+
+constexpr size_t F2_LDS_BYTES = sizeof(float) * (3 * 16 * LDA + XH * 16 * F2_PLD);
+
+MER_API int mer_xh_v2a_fwd(int B, int T, int Ta, int vdim, const float* vfeat, const void* Wv_hi, const void* Wv_lo,
+                           const float* bv, const void* Wq1_hi, const void* Wq1_lo, const float* bq1, const float* kv1,
+                           const void* Wo1_hi, const void* Wo1_lo, const float* bo1, const float* gamma,
+                           const float* beta, const void* Wkv2_hi, const void* Wkv2_lo, const float* bkv2,
+                           float attn_p, float path_p, const unsigned long long* seed, unsigned long long site_attn,
+                           unsigned long long site_path, float scale, float* v, float* q1, float* P1, float* o1,
+                           float* s_v, float* mean_v, float* rstd_v, float* v1, float* kv2, float* emb, long ld_emb,
+                           void* stream) {
+  if (B <= 0) return 0;
+  if (T <= 0 || T > 16 || Ta <= 0 || Ta > 16 * F2_KT || vdim % 32) return (int)hipErrorInvalidValue;
+  if ((attn_p > 0.f || path_p > 0.f) && !seed) return (int)hipErrorInvalidValue;
+  XhDrop dr{attn_p, path_p, seed, site_attn, site_path};
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&xh_v2a_fwd_kernel),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)F2_LDS_BYTES) != hipSuccess)
+    return (int)hipErrorInvalidConfiguration;
+  hipLaunchKernelGGL(xh_v2a_fwd_kernel, dim3(B), dim3(256), F2_LDS_BYTES, (hipStream_t)stream, T, Ta, vdim, vfeat,
+                     SplitW{(const bf16_t*)Wv_hi, (const bf16_t*)Wv_lo}, bv,
+                     SplitW{(const bf16_t*)Wq1_hi, (const bf16_t*)Wq1_lo}, bq1, kv1,
+                     SplitW{(const bf16_t*)Wo1_hi, (const bf16_t*)Wo1_lo}, bo1, gamma, beta,
+                     SplitW{(const bf16_t*)Wkv2_hi, (const bf16_t*)Wkv2_lo}, bkv2, dr, scale, v, q1, P1, o1, s_v,
+                     mean_v, rstd_v, v1, kv2, emb, ld_emb);
+  MER_LAUNCH_CHECK();
+}
+
+// ---------------------------------------------------------------------------------------------
+// F3: a2v block, one workgroup per (sample, 16 query rows); keys = the sample's T (<= 16) v1 rows.
+// ---------------------------------------------------------------------------------------------
+constexpr int F3_PLD = 36;
+
+__global__ __launch_bounds__(256) void xh_a2v_fwd_kernel(int T, int Ta, int ntiles, const float* __restrict__ q2,
+                                                         const float* __restrict__ kv2, const float* __restrict__ a,
+                                                         SplitW Wo2, const float* __restrict__ bo2,
+                                                         const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                         XhDrop dr, float scale, float* __restrict__ P2,
+                                                         float* __restrict__ o2, float* __restrict__ s_a,
+                                                         float* __restrict__ mean_a, float* __restrict__ rstd_a,
+                                                         float* __restrict__ part) {
+  __shared__ __attribute__((aligned(16))) float aL[16 * LDA];
+  __shared__ __attribute__((aligned(16))) float oL[16 * LDA];
+  __shared__ __attribute__((aligned(16))) float tL[16 * LDA];
+  __shared__ __attribute__((aligned(16))) float PL[XH * 16 * F3_PLD];
+  const int b = blockIdx.x / ntiles, tile = blockIdx.x - b * ntiles, w = threadIdx.x >> 6;
+  const int i0 = tile * 16;
+  const int nr = Ta - i0 < 16 ? Ta - i0 : 16;
+  const long row0 = (long)b * Ta + i0;
+  const unsigned long long seed_attn = mer_site_seed(dr.seed, dr.site_attn);
+  const unsigned long long seed_path = mer_site_seed(dr.seed, dr.site_path);
+  head_attention<1>(b, w, i0, Ta, T, q2 + row0 * XD, XD, kv2 + (long)b * T * 2 * XD, kv2 + (long)b * T * 2 * XD + XD,
+                    2 * XD, scale, P2, dr.attn, seed_attn, PL + w * 16 * F3_PLD, F3_PLD, oL);
+  for (int e = threadIdx.x; e < 16 * XD; e += 256) {
+    const int r = e / XD, c = e - r * XD;
+    aL[r * LDA + c] = r < nr ? a[(row0 + r) * XD + c] : 0.f;
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < nr * XD; e += 256) o2[row0 * XD + e] = oL[(e / XD) * LDA + e % XD];
+  {  // a2 = o Wo2^T + bo2
+    f32x4 acc[1][2];
+    zero(acc);
+    mm_aw(acc, oL, LDA, 16, XD, Wo2, XD, 32 * w);
+    store_acc(acc, 32 * w, bo2, tL, LDA, nullptr, 0, 0, 16);
+  }
+  __syncthreads();
+  add_ln_rows(nr, aL, tL, dropout_scale(seed_path, b, dr.path), gamma, beta, oL, s_a, mean_a, rstd_a, row0);
+  __syncthreads();
+  if (threadIdx.x < XD) {  // this tile's column sums of a1 (the a-side mean pool, folded in tile order by F4)
+    float s = 0.f;
+    for (int r = 0; r < nr; ++r) s += oL[r * LDA + threadIdx.x];
+    part[((long)b * ntiles + tile) * XD + threadIdx.x] = s;
+  }
+}
+
+MER_API int mer_xh_a2v_fwd(int B, int T, int Ta, const float* q2, const float* kv2, const float* a, const void* Wo2_hi,
+                           const void* Wo2_lo, const float* bo2, const float* gamma, const float* beta, float attn_p,
+                           float path_p, const unsigned long long* seed, unsigned long long site_attn,
+                           unsigned long long site_path, float scale, float* P2, float* o2, float* s_a, float* mean_a,
+                           float* rstd_a, float* part, void* stream) {
+  if (B <= 0) return 0;
+  if (T <= 0 || T > 16 || Ta <= 0) return (int)hipErrorInvalidValue;
+  if ((attn_p > 0.f || path_p > 0.f) && !seed) return (int)hipErrorInvalidValue;
+  const int ntiles = (Ta + 15) / 16;
+  XhDrop dr{attn_p, path_p, seed, site_attn, site_path};
+  hipLaunchKernelGGL(xh_a2v_fwd_kernel, dim3(B * ntiles), dim3(256), 0, (hipStream_t)stream, T, Ta, ntiles, q2, kv2,
+                     a, SplitW{(const bf16_t*)Wo2_hi, (const bf16_t*)Wo2_lo}, bo2, gamma, beta, dr, scale, P2, o2, s_a,
+                     mean_a, rstd_a, part);
+  MER_LAUNCH_CHECK();
+}
+
+// ---------------------------------------------------------------------------------------------
+// F4: a-pool fold + classifier head (fusion.py:404-411), 4 samples per workgroup, exact fp32 FMA.
+//   concat: h = dropout(relu(emb W0^T + b0)), logits = h W3^T + b3
+//   gated:  h = dropout(relu(emb Wg0^T + b)), z = h Wg3^T + b, g = sigmoid(z),
+//           fused = g v_emb + (1 - g) a_emb, logits = fused Wc^T + bc
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void xh_mlp_fwd_kernel(int B, int Ta, int ntiles, int gated, int H1, int C,
+                                                         const float* __restrict__ part, float* __restrict__ emb,
+                                                         const float* __restrict__ W0, const float* __restrict__ b0,
+                                                         const float* __restrict__ W3, const float* __restrict__ b3,
+                                                         const float* __restrict__ Wc, const float* __restrict__ bc,
+                                                         float mlp_p, const unsigned long long* __restrict__ seed_ptr,
+                                                         unsigned long long site, float* __restrict__ hsave,
+                                                         float* __restrict__ gsave, float* __restrict__ fsave,
+                                                         float* __restrict__ logits) {
+  __shared__ float eL[4][2 * XD];
+  __shared__ float hL[4][256];
+  __shared__ float zL[4];
+  const int t = threadIdx.x, s0 = blockIdx.x * 4;
+  const unsigned long long seed = mer_site_seed(seed_ptr, site);
+  for (int e = t; e < 4 * 2 * XD; e += 256) {
+    const int s = e / (2 * XD), c = e - s * 2 * XD, bb = s0 + s;
+    float val = 0.f;
+    if (bb < B) {
+      if (c < XD) {
+        val = emb[(long)bb * 2 * XD + c];
+      } else {
+        float acc = 0.f;
+        for (int q = 0; q < ntiles; ++q) acc += part[((long)bb * ntiles + q) * XD + c - XD];
+        val = acc / Ta;
+        emb[(long)bb * 2 * XD + c] = val;
+      }
+    }
+    eL[s][c] = val;
+  }
+  __syncthreads();
+  if (t < H1) {
+    const float* wr = W0 + (long)t * 2 * XD;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int bb = s0 + s;
+      float acc = b0[t];
+      for (int k = 0; k < 2 * XD; ++k) acc = fmaf(eL[s][k], wr[k], acc);
+      float hv = acc > 0.f ? acc : 0.f;
+      if (bb < B) {
+        hv *= dropout_scale(seed, (uint64_t)((long)bb * H1 + t), mlp_p);
+        hsave[(long)bb * H1 + t] = hv;
+      }
+      hL[s][t] = hv;
+    }
+  }
+  __syncthreads();
+  if (!gated) {
+    if (t < 4 * C) {
+      const int s = t / C, c = t - s * C, bb = s0 + s;
+      if (bb < B) {
+        float acc = b3[c];
+        for (int k = 0; k < H1; ++k) acc = fmaf(hL[s][k], W3[(long)c * H1 + k], acc);
+        logits[(long)bb * C + c] = acc;
+      }
+    }
+    return;
+  }
+  if (t < 4) {  // z = h Wg3^T + b (one output), g = sigmoid(z)
+    const int bb = s0 + t;
+    float acc = b3[0];
+    for (int k = 0; k < H1; ++k) acc = fmaf(hL[t][k], W3[k], acc);
+    const float g = 1.f / (1.f + expf(-acc));
+    zL[t] = g;
+    if (bb < B) gsave[bb] = g;
+  }
+  __syncthreads();
+  for (int e = t; e < 4 * XD; e += 256) {
+    const int s = e / XD, c = e - s * XD, bb = s0 + s;
+    const float g = zL[s];
+    const float f = g * eL[s][c] + (1.f - g) * eL[s][XD + c];
+    hL[s][c] = f;  // h no longer needed
+    if (bb < B) fsave[(long)bb * XD + c] = f;
+  }
+  __syncthreads();
+  if (t < 4 * C) {
+    const int s = t / C, c = t - s * C, bb = s0 + s;
+    if (bb < B) {
+      float acc = bc[c];
+      for (int k = 0; k < XD; ++k) acc = fmaf(hL[s][k], Wc[(long)c * XD + k], acc);
+      logits[(long)bb * C + c] = acc;
+    }
+  }
+}
+
+MER_API int mer_xh_mlp_fwd(int B, int Ta, int gated, int H1, int C, const float* part, float* emb, const float* W0,
+                           const float* b0, const float* W3, const float* b3, const float* Wc, const float* bc,
+                           float mlp_p, const unsigned long long* seed, unsigned long long site, float* hsave,
+                           float* gsave, float* fsave, float* logits, void* stream) {
+  if (B <= 0) return 0;
+  if (H1 <= 0 || H1 > 256 || C <= 0 || 4 * C > 256 || (mlp_p > 0.f && !seed)) return (int)hipErrorInvalidValue;
+  if (gated && (!Wc || !bc || !gsave || !fsave || H1 > 256)) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(xh_mlp_fwd_kernel, dim3((B + 3) / 4), dim3(256), 0, (hipStream_t)stream, B, Ta, (Ta + 15) / 16,
+                     gated, H1, C, part, emb, W0, b0, W3, b3, Wc, bc, mlp_p, seed, site, hsave, gsave, fsave, logits);
+  MER_LAUNCH_CHECK();
+}

@@ -20,6 +20,7 @@ from torch import nn
 from . import embedding_head as EH
 from . import graphs as G
 from . import kernels as K
+from . import xattn_fused as XF
 from . import xattn_head as XH
 from .nn_ops import hip_linear
 from .temporal import TemporalPooler
@@ -208,6 +209,8 @@ class _HeadGraphs(G.PendingGuard):
     def forward(self, v_feat, a_seq):
         params = dict(zip(self.names, self.model.head_params()[1]))
         if self.fwd is None:
+            if XF.supported(self.cfg, params, v_feat, a_seq, None):
+                XF.planes_for(params)  # host-side setup (an H2D descriptor copy) outside the capture
             self.rng = torch.zeros(1, dtype=torch.int64, device=v_feat.device)
             self.fwd = G.StaticGraph(lambda v, a: XH.head_forward(params, self.cfg, v, a, self.training,
                                                                   self.rng if self.training else None),

@@ -813,3 +813,67 @@ def mha_bwd_lds_bytes(Lq: int, Lk: int, dh: int) -> int:
     out = ctypes.c_long(0)
     LIB("mer_mha_bwd_lds_bytes", int(Lq), int(Lk), int(dh), ctypes.addressof(out))
     return int(out.value)
+
+
+# ---------------------------------------------------------------------------------------------------
+# fused xattn head forward (csrc/xattn_fused.hip)
+def xh_split(desc):
+    if desc.dtype != torch.int64 or desc.dim() != 2 or desc.shape[1] != 4 or not desc.is_cuda:
+        raise ValueError("split descriptor table must be a device int64 [n, 4] tensor")
+    LIB("mer_xh_split", desc.shape[0], desc.data_ptr(), stream_ptr())
+
+
+def _planes(w):
+    hi, lo = w
+    return hi.data_ptr(), lo.data_ptr()
+
+
+def _f32c(*ts):
+    for t in ts:
+        if t is not None and (t.dtype != torch.float32 or not t.is_contiguous() or not t.is_cuda):
+            raise ValueError("fused head: contiguous fp32 device tensors expected")
+
+
+def xh_audio_fwd(af, Ws, bs, Wa, ba, Wc, bq2, bkv1, a_s, a, q2, kv1):
+    M, S = af.shape
+    if af.dtype != torch.bfloat16 or af.stride(1) != 1 or Ws[0].shape != (128, S) or Wc[0].shape != (384, 128):
+        raise ValueError("xh_audio_fwd shapes")
+    _f32c(a_s, a, q2, kv1)
+    _launch("xh_audio_fwd", (M, S), "mer_xh_audio_fwd", M, S, af.data_ptr(), af.stride(0), *_planes(Ws), bs.data_ptr(),
+            *_planes(Wa), ba.data_ptr(), *_planes(Wc), bq2.data_ptr(), bkv1.data_ptr(), a_s.data_ptr(), a.data_ptr(),
+            q2.data_ptr(), kv1.data_ptr(), stream_ptr())
+
+
+def xh_v2a_fwd(B, T, Ta, vf, Wv, bv, Wq1, bq1, kv1, Wo1, bo1, gamma, beta, Wkv2, bkv2, attn_p, path_p, rng, site_attn,
+               site_path, scale, v, q1, P1, o1, s_v, mu_v, rs_v, v1, kv2, emb):
+    vdim = vf.shape[1]
+    if tuple(vf.shape) != (B * T, vdim) or Wv[0].shape != (128, vdim) or tuple(kv1.shape) != (B * Ta, 256):
+        raise ValueError("xh_v2a_fwd shapes")
+    _f32c(vf, kv1, v, q1, P1, o1, s_v, mu_v, rs_v, v1, kv2, emb)
+    _launch("xh_v2a_fwd", (B, T, Ta), "mer_xh_v2a_fwd", B, T, Ta, vdim, vf.data_ptr(), *_planes(Wv), bv.data_ptr(),
+            *_planes(Wq1), bq1.data_ptr(), kv1.data_ptr(), *_planes(Wo1), bo1.data_ptr(), gamma.data_ptr(),
+            beta.data_ptr(), *_planes(Wkv2), bkv2.data_ptr(), float(attn_p), float(path_p), rng_ptr(rng),
+            int(site_attn), int(site_path), float(scale), v.data_ptr(), q1.data_ptr(), P1.data_ptr(), o1.data_ptr(),
+            s_v.data_ptr(), mu_v.data_ptr(), rs_v.data_ptr(), v1.data_ptr(), kv2.data_ptr(), emb.data_ptr(),
+            emb.stride(0), stream_ptr())
+
+
+def xh_a2v_fwd(B, T, Ta, q2, kv2, a, Wo2, bo2, gamma, beta, attn_p, path_p, rng, site_attn, site_path, scale, P2, o2,
+               s_a, mu_a, rs_a, part):
+    if tuple(q2.shape) != (B * Ta, 128) or tuple(kv2.shape) != (B * T, 256) or part.numel() != B * ((Ta + 15) // 16) * 128:
+        raise ValueError("xh_a2v_fwd shapes")
+    _f32c(q2, kv2, a, P2, o2, s_a, mu_a, rs_a, part)
+    _launch("xh_a2v_fwd", (B, T, Ta), "mer_xh_a2v_fwd", B, T, Ta, q2.data_ptr(), kv2.data_ptr(), a.data_ptr(),
+            *_planes(Wo2), bo2.data_ptr(), gamma.data_ptr(), beta.data_ptr(), float(attn_p), float(path_p),
+            rng_ptr(rng), int(site_attn), int(site_path), float(scale), P2.data_ptr(), o2.data_ptr(), s_a.data_ptr(),
+            mu_a.data_ptr(), rs_a.data_ptr(), part.data_ptr(), stream_ptr())
+
+
+def xh_mlp_fwd(B, Ta, gated, part, emb, W0, b0, W3, b3, Wc, bc, mlp_p, rng, site, h, g, fused, logits):
+    H1, C = W0.shape[0], logits.shape[1]
+    if W0.shape[1] != 256 or tuple(emb.shape) != (B, 256) or (gated and (W3.shape[0] != 1 or Wc is None)):
+        raise ValueError("xh_mlp_fwd shapes")
+    _f32c(part, emb, W0, b0, W3, b3, h, logits)
+    LIB("mer_xh_mlp_fwd", B, Ta, int(bool(gated)), H1, C, part.data_ptr(), emb.data_ptr(), W0.data_ptr(), b0.data_ptr(),
+        W3.data_ptr(), b3.data_ptr(), _ptr(Wc), _ptr(bc), float(mlp_p), rng_ptr(rng) if mlp_p > 0 else 0, int(site),
+        h.data_ptr(), _ptr(g), _ptr(fused), logits.data_ptr(), stream_ptr())

@@ -19,6 +19,7 @@ import torch
 
 from . import kernels as K
 from . import temporal_hip as TH
+from . import xattn_fused as XF
 
 # Dropout / drop-path sites: the step's RNG base is a device int64 [1] tensor (``rng``) mixed with a
 # constant site id in-kernel (mer_site_seed), so the masks are regenerated in backward from (base, site)
@@ -75,6 +76,10 @@ def head_forward(p: Dict[str, torch.Tensor], cfg: HeadConfig, v_feat: torch.Tens
     d = p["v_in_proj.weight"].shape[0]
     H = cfg.num_heads
     ctx = HeadCtx(dims=(B, T, Ta, d, H), rng=rng, training=training)
+    if XF.supported(cfg, p, v_feat, a_seq, qlin):  # four fused launches (csrc/xattn_fused.hip)
+        logits = XF.fused_forward(p, cfg, v_feat, a_seq, training, rng, ctx,
+                                  (SITE_PRIOR, SITE_V2A, SITE_VPATH, SITE_A2V, SITE_APATH, SITE_MLP))
+        return logits, ctx
     sv = ctx.saved
     dp_attn = cfg.attn_dropout if training else 0.0
     dp_path = cfg.drop_path if training else 0.0

@@ -1,0 +1,57 @@
+"""The fused xattn head forward (csrc/xattn_fused.hip, four launches on split-bf16 MFMA) against the unfused
+schedule (xattn_head.head_forward, exact-f32 MFMA -- itself pinned to the reference goldens at 1e-4) on the C2
+feature shapes (B=32, T=8, Ta=149), eval and train mode: the dropout / drop-path masks use the same indices,
+so the same RNG base must give the same logits and saved activations in both paths (fp32-class agreement,
+1e-5 relative), and the unchanged backward then gives the same gradients.  The C1 / C2 golden tests of
+tests/test_head_gpu.py run through the fused path too (it is the default)."""
+import numpy as np
+import pytest
+import torch
+
+from tests.gpu_helpers import feats, head_model
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    a, b = a.detach().float().cpu(), b.detach().float().cpu()
+    return float((a - b).abs().max() / max(float(b.abs().max()), 1e-30))
+
+
+@pytest.mark.parametrize("head", ["concat", "gated"])
+@pytest.mark.parametrize("training", [False, True])
+def test_fused_forward_matches_unfused(head, training):
+    from multimodalemotionrecognition_amd import xattn_fused as XF
+    from multimodalemotionrecognition_amd import xattn_head as XH
+    from multimodalemotionrecognition_amd.fusion import _head_grads
+
+    m = head_model(head, False).train(training)
+    names, params = m.head_params()
+    p = dict(zip(names, params))
+    cfg = m.head_config()
+    v, a = feats(32, 8, 149, seed=7)
+    a = a.to(torch.bfloat16)  # the frozen WavLM's features
+    rng = torch.full((1,), 4242, dtype=torch.int64, device="cuda")
+    out = {}
+    for fused in (False, True):
+        XF.ENABLED = fused
+        try:
+            logits, ctx = XH.head_forward(p, cfg, v, a, training, rng)
+            assert XF.supported(cfg, p, v, a, None)
+            dl = torch.from_numpy(np.random.default_rng(1).standard_normal(tuple(logits.shape)).astype(np.float32)).cuda()
+            grads = _head_grads(p, set(XH.used_param_names(cfg)))
+            grads = {n: torch.zeros_like(t) for n, t in grads.items()}
+            dv, _ = XH.head_backward(p, ctx, dl, grads, need_dv_feat=True)
+            out[fused] = (logits, ctx.saved, grads, dv)
+        finally:
+            XF.ENABLED = True
+    (l0, s0, g0, dv0), (l1, s1, g1, dv1) = out[False], out[True]
+    print(head, training, "logits rel", _rel(l1, l0))
+    assert _rel(l1, l0) < 1e-5
+    for k in ("v", "a_s", "a", "q1", "kv1", "o1", "P1", "v1", "s_v", "q2", "kv2", "o2", "P2", "s_a", "emb", "h"):
+        assert _rel(s1[k], s0[k]) < 2e-5, (k, _rel(s1[k], s0[k]))
+    for k in ("mu_v", "rs_v", "mu_a", "rs_a"):
+        assert _rel(s1[k], s0[k]) < 2e-5, k
+    for n in g0:
+        assert _rel(g1[n], g0[n]) < 1e-4, (n, _rel(g1[n], g0[n]))
+    assert _rel(dv1, dv0) < 1e-4
