@@ -479,12 +479,13 @@ int mer_concat_prior_rows(int B, int L, int d, int pd, int ldo, const float* tok
  * table desc[n_items][4]. */
 int mer_xh_split(int n_items, const long long* desc, void* stream);
 
-/* F1: a_s = aseq Ws^T + bs (aseq bf16 [M][S], the WavLM features), a = a_s Wa^T + ba, [q2 | kv1] = a Wc^T +
- * [bq2 | bkv1] (Wc = [a2v in_proj q rows; v2a in_proj k, v rows], 384 x 128).  Outputs fp32: a_s, a, q2 [M][128],
- * kv1 [M][256].  S % 32 == 0. */
-int mer_xh_audio_fwd(int M, int S, const void* aseq, long ldas, const void* Ws_hi, const void* Ws_lo, const float* bs,
-                     const void* Wa_hi, const void* Wa_lo, const float* ba, const void* Wc_hi, const void* Wc_lo,
-                     const float* bq2, const float* bkv1, float* a_s, float* a, float* q2, float* kv1, void* stream);
+/* F1: a_s = aseq Ws^T + bs (aseq [M][S] bf16 -- the WavLM features, exact -- or fp32), a = a_s Wa^T + ba,
+ * [q2 | kv1] = a Wc^T + [bq2 | bkv1] (Wc = [a2v in_proj q rows; v2a in_proj k, v rows], 384 x 128).  Outputs
+ * fp32: a_s, a, q2 [M][128], kv1 [M][256].  S % 32 == 0. */
+int mer_xh_audio_fwd(int M, int S, const void* aseq, int aseq_dtype, long ldas, const void* Ws_hi, const void* Ws_lo,
+                     const float* bs, const void* Wa_hi, const void* Wa_lo, const float* ba, const void* Wc_hi,
+                     const void* Wc_lo, const float* bq2, const float* bkv1, float* a_s, float* a, float* q2,
+                     float* kv1, void* stream);
 
 /* F2 (one workgroup per sample, T <= 16, Ta <= 160): v = vfeat Wv^T + bv, q1 = v Wq1^T + bq1, v2a attention over
  * kv1, o1 Wo1^T + bo1, v1 = LayerNorm(v + keep_b * v2) (saving the pre-LN sum, mean, rstd), kv2 = v1 Wkv2^T + bkv2,

@@ -182,7 +182,8 @@ MER_API int mer_xh_split(int n_items, const long long* desc, void* stream) {
 // ---------------------------------------------------------------------------------------------
 // F1: audio token chain.  32 rows per block, 4 waves.
 // ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void xh_audio_fwd_kernel(int M, int S, const bf16_t* __restrict__ aseq, long ldas,
+template <typename TA>  // bf16: the WavLM features (exact, two passes); float: fp32 features (split, three passes)
+__global__ __launch_bounds__(256) void xh_audio_fwd_kernel(int M, int S, const TA* __restrict__ aseq, long ldas,
                                                            SplitW Ws, const float* __restrict__ bs, SplitW Wa,
                                                            const float* __restrict__ ba, SplitW Wc,
                                                            const float* __restrict__ bq2, const float* __restrict__ bkv1,
@@ -208,12 +209,19 @@ __global__ __launch_bounds__(256) void xh_audio_fwd_kernel(int M, int S, const b
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const int r = 16 * i + fr;
-        Frag A;
-        A.u = r < rmax ? *reinterpret_cast<const u4*>(aseq + (r0 + r) * ldas + k + fk) : u4{0u, 0u, 0u, 0u};
+        if constexpr (sizeof(TA) == 2) {
+          Frag A;
+          A.u = r < rmax ? *reinterpret_cast<const u4*>(aseq + (r0 + r) * ldas + k + fk) : u4{0u, 0u, 0u, 0u};
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          acc[i][j] = mma(A.v, bh[j], acc[i][j]);
-          acc[i][j] = mma(A.v, bl[j], acc[i][j]);
+          for (int j = 0; j < 2; ++j) {
+            acc[i][j] = mma(A.v, bh[j], acc[i][j]);
+            acc[i][j] = mma(A.v, bl[j], acc[i][j]);
+          }
+        } else {
+          bf16x8 ah, al;
+          frag_row(reinterpret_cast<const float*>(aseq) + (r0 + r) * ldas + k + fk, r < rmax, ah, al);
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[i][j] = mma3(ah, al, bh[j], bl[j], acc[i][j]);
         }
       }
     }
@@ -254,16 +262,20 @@ __global__ __launch_bounds__(256) void xh_audio_fwd_kernel(int M, int S, const b
   }
 }
 
-MER_API int mer_xh_audio_fwd(int M, int S, const void* aseq, long ldas, const void* Ws_hi, const void* Ws_lo,
-                             const float* bs, const void* Wa_hi, const void* Wa_lo, const float* ba, const void* Wc_hi,
-                             const void* Wc_lo, const float* bq2, const float* bkv1, float* a_s, float* a, float* q2,
-                             float* kv1, void* stream) {
+MER_API int mer_xh_audio_fwd(int M, int S, const void* aseq, int aseq_dtype, long ldas, const void* Ws_hi,
+                             const void* Ws_lo, const float* bs, const void* Wa_hi, const void* Wa_lo, const float* ba,
+                             const void* Wc_hi, const void* Wc_lo, const float* bq2, const float* bkv1, float* a_s,
+                             float* a, float* q2, float* kv1, void* stream) {
   if (M <= 0) return 0;
   if (S % 32 || ldas % 8 || ((uintptr_t)aseq & 15)) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(xh_audio_fwd_kernel, dim3((M + 31) / 32), dim3(256), 0, (hipStream_t)stream, M, S,
-                     (const bf16_t*)aseq, ldas, SplitW{(const bf16_t*)Ws_hi, (const bf16_t*)Ws_lo}, bs,
-                     SplitW{(const bf16_t*)Wa_hi, (const bf16_t*)Wa_lo}, ba,
-                     SplitW{(const bf16_t*)Wc_hi, (const bf16_t*)Wc_lo}, bq2, bkv1, a_s, a, q2, kv1);
+  const SplitW ws{(const bf16_t*)Ws_hi, (const bf16_t*)Ws_lo}, wa{(const bf16_t*)Wa_hi, (const bf16_t*)Wa_lo},
+      wc{(const bf16_t*)Wc_hi, (const bf16_t*)Wc_lo};
+  if (aseq_dtype == MER_BF16)
+    hipLaunchKernelGGL(xh_audio_fwd_kernel<bf16_t>, dim3((M + 31) / 32), dim3(256), 0, (hipStream_t)stream, M, S,
+                       (const bf16_t*)aseq, ldas, ws, bs, wa, ba, wc, bq2, bkv1, a_s, a, q2, kv1);
+  else
+    hipLaunchKernelGGL(xh_audio_fwd_kernel<float>, dim3((M + 31) / 32), dim3(256), 0, (hipStream_t)stream, M, S,
+                       (const float*)aseq, ldas, ws, bs, wa, ba, wc, bq2, bkv1, a_s, a, q2, kv1);
   MER_LAUNCH_CHECK();
 }
 

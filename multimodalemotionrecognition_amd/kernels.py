@@ -836,10 +836,11 @@ def _f32c(*ts):
 
 def xh_audio_fwd(af, Ws, bs, Wa, ba, Wc, bq2, bkv1, a_s, a, q2, kv1):
     M, S = af.shape
-    if af.dtype != torch.bfloat16 or af.stride(1) != 1 or Ws[0].shape != (128, S) or Wc[0].shape != (384, 128):
+    if af.stride(1) != 1 or Ws[0].shape != (128, S) or Wc[0].shape != (384, 128):
         raise ValueError("xh_audio_fwd shapes")
     _f32c(a_s, a, q2, kv1)
-    _launch("xh_audio_fwd", (M, S), "mer_xh_audio_fwd", M, S, af.data_ptr(), af.stride(0), *_planes(Ws), bs.data_ptr(),
+    _launch("xh_audio_fwd", (M, S), "mer_xh_audio_fwd", M, S, af.data_ptr(), _dt(af), af.stride(0), *_planes(Ws),
+            bs.data_ptr(),
             *_planes(Wa), ba.data_ptr(), *_planes(Wc), bq2.data_ptr(), bkv1.data_ptr(), a_s.data_ptr(), a.data_ptr(),
             q2.data_ptr(), kv1.data_ptr(), stream_ptr())
 

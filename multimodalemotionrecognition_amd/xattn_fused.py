@@ -3,8 +3,8 @@
 launches of ``xattn_head.head_forward``.
 
 Scope of the fused path: d_model 128 with 4 heads (the reference's defaults, fusion.py:199-200), mean temporal
-pooling (the fusion default), concat or gated head, no emotion prior, bf16 audio features (the frozen WavLM's
-output), T <= 16 frames and Ta <= 160 audio frames (3 s clips: 8 and 149).  Everything else -- and INT8
+pooling (the fusion default), concat or gated head, no emotion prior, audio features that need no gradient
+(bf16 from the frozen WavLM, or fp32), T <= 16 frames and Ta <= 160 audio frames (3 s clips: 8 and 149).  Everything else -- and INT8
 inference -- runs the unfused schedule, which is the parity reference of this path.  The saved activations
 have the unfused schedule's names and layouts, so ``xattn_head.head_backward`` runs unchanged on them.
 """
@@ -39,7 +39,8 @@ def supported(cfg, p: Dict[str, torch.Tensor], v_feat: torch.Tensor, a_seq: torc
         return False
     B, T, vd = v_feat.shape
     _, Ta, sd = a_seq.shape
-    if a_seq.dtype != torch.bfloat16 or v_feat.dtype != torch.float32 or T > 16 or Ta > 160 or vd % 32 or sd % 32:
+    if a_seq.dtype not in (torch.bfloat16, torch.float32) or v_feat.dtype != torch.float32 or T > 16 or Ta > 160 \
+            or vd % 32 or sd % 32:
         return False
     if a_seq.requires_grad:  # the fused forward has no audio-feature gradient path (stage 2 runs unfused)
         return False

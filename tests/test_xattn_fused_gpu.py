@@ -32,12 +32,12 @@ def test_fused_forward_matches_unfused(head, training):
     v, a = feats(32, 8, 149, seed=7)
     a = a.to(torch.bfloat16)  # the frozen WavLM's features
     rng = torch.full((1,), 4242, dtype=torch.int64, device="cuda")
+    assert XF.supported(cfg, p, v, a, None)
     out = {}
     for fused in (False, True):
         XF.ENABLED = fused
         try:
             logits, ctx = XH.head_forward(p, cfg, v, a, training, rng)
-            assert XF.supported(cfg, p, v, a, None)
             dl = torch.from_numpy(np.random.default_rng(1).standard_normal(tuple(logits.shape)).astype(np.float32)).cuda()
             grads = _head_grads(p, set(XH.used_param_names(cfg)))
             grads = {n: torch.zeros_like(t) for n, t in grads.items()}
