@@ -475,8 +475,9 @@ int mer_concat_prior_rows(int B, int L, int d, int pd, int ldo, const float* tok
  * sample, MLP dropout row*H1 + col -- the conventions of mer_mha_fwd / mer_add_ln_fwd / mer_dropout_inplace,
  * so mer_mha_bwd / mer_add_ln_bwd and the rest of the unfused backward regenerate the same masks. */
 
-/* Split n fp32 weights into bf16 hi / lo planes for each descriptor row (src, hi, lo, n) of the device int64
- * table desc[n_items][4]. */
+/* Split fp32 weights into bf16 hi / lo planes, one descriptor row (src, hi, lo, rows, cols, trans, dst_ld) of
+ * the device int64 table desc[n_items][7] per [rows][cols] weight: trans 0 writes the planes in the source layout,
+ * trans 1 transposed (dst[c * dst_ld + r], the [in][out] planes the fused backward's data-gradient products read). */
 int mer_xh_split(int n_items, const long long* desc, void* stream);
 
 /* F1: a_s = aseq Ws^T + bs (aseq [M][S] bf16 -- the WavLM features, exact -- or fp32), a = a_s Wa^T + ba,
@@ -514,6 +515,47 @@ int mer_xh_mlp_fwd(int B, int Ta, int gated, int H1, int C, const float* part, f
                    const float* b0, const float* W3, const float* b3, const float* Wc, const float* bc, float mlp_p,
                    const unsigned long long* seed, unsigned long long site, float* hsave, float* gsave, float* fsave,
                    float* logits, void* stream);
+
+/* ---- fused xattn head backward (csrc/xattn_fused_bwd.hip; the unfused schedule is xattn_head.head_backward,
+ * xattn_head.py:191-315).  W*T_hi / _lo are the TRANSPOSED split planes ([in][out]).  Gradient buffers are
+ * accumulated into (+=); data gradients are written. ---- */
+
+/* G4: the classifier head (concat: h W3 / gated: gate + classifier) -> demb [B][256]; dW0 db0 dW3 db3 (+ dWc dbc
+ * gated) accumulated.  Exact fp32 FMA; one launch of 8 workgroups. */
+int mer_xh_mlp_bwd(int B, int C, int H1, int gated, const float* dlogits, const float* emb, const float* h,
+                   const float* g, const float* fused, const float* W0, const float* W3, const float* Wc, float mlp_p,
+                   const unsigned long long* seed, unsigned long long site, float* dW0, float* db0, float* dW3,
+                   float* db3, float* dWc, float* dbc, float* demb, void* stream);
+
+/* G3 (one workgroup per (sample, 16 query rows)): a-pool + LayerNorm backward -> da (the residual part, [B*Ta][128])
+ * and da2 = keep_b * ds; do2 = da2 Wo2; attention backward -> dq2 into dqkv[:, 0:128] ([B*Ta][384]), per-tile
+ * dK2 dV2 partials dkv2_part [B][ceil(Ta/16)][16][256], LayerNorm dgamma / dbeta partials ln_part [B*tiles][256]. */
+int mer_xh_a2v_bwd(int B, int T, int Ta, const float* demb, const float* s_a, const float* mean_a, const float* rstd_a,
+                   const float* gamma, const float* P2, const float* kv2, const float* q2, const void* WoT2_hi,
+                   const void* WoT2_lo, float attn_p, float path_p, const unsigned long long* seed,
+                   unsigned long long site_attn, unsigned long long site_path, float scale, float* da, float* da2,
+                   float* dqkv, float* dkv2_part, float* ln_part, void* stream);
+
+/* G2 (one workgroup per sample, T <= 16, Ta <= 160): dkv2 = fold(dkv2_part) [B*T][256], dv1 = demb_v / T +
+ * dkv2 Wkv2, LayerNorm backward (dv2, ln_part [B][256]), do1 = dv2 Wo1, attention backward -> dq1 [B*T][128],
+ * dK1 dV1 into dqkv[:, 128:384], dv = ds + dq1 Wq1 [B*T][128], dvfeat = dv Wv [B*T][vdim] (NULL: skipped). */
+int mer_xh_v2a_bwd(int B, int T, int Ta, int vdim, const float* dkv2_part, const void* WkvT2_hi, const void* WkvT2_lo,
+                   const float* demb, const float* s_v, const float* mean_v, const float* rstd_v, const float* gamma,
+                   const void* WoT1_hi, const void* WoT1_lo, const float* P1, const float* kv1, const float* q1,
+                   const void* WqT1_hi, const void* WqT1_lo, const void* WvT_hi, const void* WvT_lo, float attn_p,
+                   float path_p, const unsigned long long* seed, unsigned long long site_attn,
+                   unsigned long long site_path, float scale, float* dkv2, float* dv2, float* dq1, float* dv,
+                   float* dvfeat, float* dqkv, float* ln_part, void* stream);
+
+/* G1 (32 rows per workgroup): da += dqkv [Wq2 ; Wkv1] (in place), da_s = da Wa. */
+int mer_xh_audio_bwd(int M, const float* dqkv, const void* WcT_hi, const void* WcT_lo, const void* WaT_hi,
+                     const void* WaT_lo, float* da, float* da_s, void* stream);
+
+/* Grouped weight gradients: host table [nprob <= 16][11] rows {dY, ldy, X, ldx, x_dtype, M, N, K, splits, dW, db}:
+ * dW [N][K] += dY^T X and db [N] += column sums of dY (K = 0: column sums only).  Row splits write partials to ws
+ * (mer_xh_wgrad_ws_floats floats), added in split order by a second launch -- deterministic, no atomics. */
+int mer_xh_wgrad_ws_floats(int nprob, const long long* table, long long* out);
+int mer_xh_wgrad(int nprob, const long long* table, float* ws, long long ws_floats, void* stream);
 
 /* ============================ CLIP-style alignment (concat / gated, fusion_align_mode="clip") ============
  * ClipStyleAlignment.forward after its two projections (fusion.py:137-150): a_n / v_n = F.normalize rows,

@@ -818,8 +818,8 @@ def mha_bwd_lds_bytes(Lq: int, Lk: int, dh: int) -> int:
 # ---------------------------------------------------------------------------------------------------
 # fused xattn head forward (csrc/xattn_fused.hip)
 def xh_split(desc):
-    if desc.dtype != torch.int64 or desc.dim() != 2 or desc.shape[1] != 4 or not desc.is_cuda:
-        raise ValueError("split descriptor table must be a device int64 [n, 4] tensor")
+    if desc.dtype != torch.int64 or desc.dim() != 2 or desc.shape[1] != 7 or not desc.is_cuda:
+        raise ValueError("split descriptor table must be a device int64 [n, 7] tensor")
     LIB("mer_xh_split", desc.shape[0], desc.data_ptr(), stream_ptr())
 
 
@@ -878,3 +878,107 @@ def xh_mlp_fwd(B, Ta, gated, part, emb, W0, b0, W3, b3, Wc, bc, mlp_p, rng, site
     LIB("mer_xh_mlp_fwd", B, Ta, int(bool(gated)), H1, C, part.data_ptr(), emb.data_ptr(), W0.data_ptr(), b0.data_ptr(),
         W3.data_ptr(), b3.data_ptr(), _ptr(Wc), _ptr(bc), float(mlp_p), rng_ptr(rng) if mlp_p > 0 else 0, int(site),
         h.data_ptr(), _ptr(g), _ptr(fused), logits.data_ptr(), stream_ptr())
+
+
+# ---------------------------------------------------------------------------------------------------
+# fused xattn head backward (csrc/xattn_fused_bwd.hip); W*T arguments are transposed (hi, lo) planes
+def xh_mlp_bwd(B, gated, dlogits, emb, h, g, fused, W0, W3, Wc, mlp_p, rng, site, dW0, db0, dW3, db3, dWc, dbc, demb):
+    H1, C = W0.shape[0], dlogits.shape[1]
+    if W0.shape[1] != 256 or tuple(emb.shape) != (B, 256) or tuple(demb.shape) != (B, 256) or tuple(h.shape) != (B, H1):
+        raise ValueError("xh_mlp_bwd shapes")
+    _f32c(dlogits, emb, h, g, fused, W0, W3, Wc, dW0, db0, dW3, db3, dWc, dbc, demb)
+    _launch("xh_mlp_bwd", (B,), "mer_xh_mlp_bwd", B, C, H1, int(bool(gated)), dlogits.data_ptr(), emb.data_ptr(),
+            h.data_ptr(), _ptr(g), _ptr(fused), W0.data_ptr(), W3.data_ptr(), _ptr(Wc), float(mlp_p),
+            rng_ptr(rng) if mlp_p > 0 else 0, int(site), dW0.data_ptr(), db0.data_ptr(), dW3.data_ptr(),
+            db3.data_ptr(), _ptr(dWc), _ptr(dbc), demb.data_ptr(), stream_ptr())
+
+
+def xh_a2v_bwd(B, T, Ta, demb, s_a, mu_a, rs_a, gamma, P2, kv2, q2, WoT2, attn_p, path_p, rng, site_attn, site_path,
+               scale, da, da2, dqkv, dkv2_part, ln_part):
+    nt = (Ta + 15) // 16
+    if tuple(q2.shape) != (B * Ta, 128) or tuple(kv2.shape) != (B * T, 256) or tuple(dqkv.shape) != (B * Ta, 384) \
+            or dkv2_part.numel() != B * nt * 16 * 256 or ln_part.numel() != B * nt * 256 or WoT2[0].shape != (128, 128):
+        raise ValueError("xh_a2v_bwd shapes")
+    _f32c(demb, s_a, mu_a, rs_a, gamma, P2, kv2, q2, da, da2, dqkv, dkv2_part, ln_part)
+    _launch("xh_a2v_bwd", (B, T, Ta), "mer_xh_a2v_bwd", B, T, Ta, demb.data_ptr(), s_a.data_ptr(), mu_a.data_ptr(),
+            rs_a.data_ptr(), gamma.data_ptr(), P2.data_ptr(), kv2.data_ptr(), q2.data_ptr(), *_planes(WoT2),
+            float(attn_p), float(path_p), rng_ptr(rng) if (attn_p > 0 or path_p > 0) else 0, int(site_attn),
+            int(site_path), float(scale), da.data_ptr(), da2.data_ptr(), dqkv.data_ptr(), dkv2_part.data_ptr(),
+            ln_part.data_ptr(), stream_ptr())
+
+
+def xh_v2a_bwd(B, T, Ta, dkv2_part, WkvT2, demb, s_v, mu_v, rs_v, gamma, WoT1, P1, kv1, q1, WqT1, WvT, attn_p, path_p,
+               rng, site_attn, site_path, scale, dkv2, dv2, dq1, dv, dvfeat, dqkv, ln_part):
+    vdim = WvT[0].shape[0]
+    if tuple(kv1.shape) != (B * Ta, 256) or tuple(q1.shape) != (B * T, 128) or tuple(dkv2.shape) != (B * T, 256) \
+            or WkvT2[0].shape != (128, 256) or WvT[0].shape != (vdim, 128) or ln_part.numel() != B * 256 \
+            or (dvfeat is not None and tuple(dvfeat.shape) != (B * T, vdim)):
+        raise ValueError("xh_v2a_bwd shapes")
+    _f32c(dkv2_part, demb, s_v, mu_v, rs_v, gamma, P1, kv1, q1, dkv2, dv2, dq1, dv, dvfeat, dqkv, ln_part)
+    _launch("xh_v2a_bwd", (B, T, Ta), "mer_xh_v2a_bwd", B, T, Ta, vdim, dkv2_part.data_ptr(), *_planes(WkvT2),
+            demb.data_ptr(), s_v.data_ptr(), mu_v.data_ptr(), rs_v.data_ptr(), gamma.data_ptr(), *_planes(WoT1),
+            P1.data_ptr(), kv1.data_ptr(), q1.data_ptr(), *_planes(WqT1), *_planes(WvT), float(attn_p), float(path_p),
+            rng_ptr(rng) if (attn_p > 0 or path_p > 0) else 0, int(site_attn), int(site_path), float(scale),
+            dkv2.data_ptr(), dv2.data_ptr(), dq1.data_ptr(), dv.data_ptr(), _ptr(dvfeat), dqkv.data_ptr(),
+            ln_part.data_ptr(), stream_ptr())
+
+
+def xh_audio_bwd(dqkv, WcT, WaT, da, da_s):
+    M = dqkv.shape[0]
+    if tuple(dqkv.shape) != (M, 384) or WcT[0].shape != (128, 384) or WaT[0].shape != (128, 128) \
+            or tuple(da.shape) != (M, 128) or tuple(da_s.shape) != (M, 128):
+        raise ValueError("xh_audio_bwd shapes")
+    _f32c(dqkv, da, da_s)
+    _launch("xh_audio_bwd", (M,), "mer_xh_audio_bwd", M, dqkv.data_ptr(), *_planes(WcT), *_planes(WaT), da.data_ptr(),
+            da_s.data_ptr(), stream_ptr())
+
+
+class WGradTable:
+    """Problem table of mer_xh_wgrad (grouped weight gradients): add(dY, X, dW, db, splits) per Linear, then
+    ``ws_floats()`` for the workspace and ``run(ws)``.  Rows live in a host int64 array (the launch copies them
+    into its kernel arguments, so a captured graph keeps them)."""
+
+    COLS = 11
+
+    def __init__(self):
+        self.rows = []
+        self.keep = []  # the tensors whose addresses the rows hold
+
+    def add(self, dY, X, dW, db, splits=1):
+        M, N = dY.shape
+        if dY.dtype != torch.float32 or dY.stride(1) != 1:
+            raise ValueError("wgrad dY: fp32 rows with unit column stride")
+        if X is not None and (X.shape[0] != M or X.stride(1) != 1 or tuple(dW.shape) != (N, X.shape[1])):
+            raise ValueError("wgrad X / dW shapes")
+        for t in (dW, db):
+            if t is not None and (t.dtype != torch.float32 or not t.is_contiguous()):
+                raise ValueError("wgrad outputs: contiguous fp32")
+        if db is not None and db.numel() != N:
+            raise ValueError("wgrad db shape")
+        K = 0 if X is None else X.shape[1]
+        splits = max(1, min(int(splits), M))
+        self.rows.append([dY.data_ptr(), dY.stride(0), _ptr(X), 0 if X is None else X.stride(0),
+                          BF16 if (X is not None and X.dtype == torch.bfloat16) else F32, M, N, K, splits, _ptr(dW),
+                          _ptr(db)])
+        self.keep += [dY, X, dW, db]
+        return self
+
+    def _table(self):
+        import numpy as np
+        if len(self.rows) > 16:
+            raise ValueError("mer_xh_wgrad takes at most 16 problems")
+        return np.ascontiguousarray(np.array(self.rows, dtype=np.int64))
+
+    def ws_floats(self) -> int:
+        import ctypes
+        tab = self._table()
+        out = ctypes.c_longlong(0)
+        LIB("mer_xh_wgrad_ws_floats", len(self.rows), tab.ctypes.data, ctypes.addressof(out))
+        return int(out.value)
+
+    def run(self, ws):
+        tab = self._table()
+        if ws.dtype != torch.float32 or not ws.is_cuda:
+            raise ValueError("wgrad workspace: fp32 device tensor")
+        _launch("xh_wgrad", (len(self.rows),), "mer_xh_wgrad", len(self.rows), tab.ctypes.data, ws.data_ptr(),
+                ws.numel(), stream_ptr())

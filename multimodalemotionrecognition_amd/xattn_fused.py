@@ -18,6 +18,8 @@ import torch
 from . import kernels as K
 
 ENABLED = os.environ.get("MER_XATTN_FUSED", "1") != "0"
+BWD_ENABLED = os.environ.get("MER_XATTN_FUSED_BWD", "1") != "0"
+WGRAD_TARGET_BLOCKS = 96  # workgroups per weight-gradient problem (row splits = this / output tiles)
 
 # (weight name, row slice) for each split plane; rows are contiguous slices of the reference's parameters
 _PLANES = {
@@ -47,38 +49,72 @@ def supported(cfg, p: Dict[str, torch.Tensor], v_feat: torch.Tensor, a_seq: torc
     return p["audio_seq_proj.weight"].shape == (128, sd) and p["v_in_proj.weight"].shape == (128, vd)
 
 
+# transposed ([in][out]) planes of the backward's data-gradient products: (weight name, row slice) parts laid
+# side by side as column blocks of the transposed plane
+_TPLANES = {
+    "WcT": _PLANES["Wc"],  # [128][384]: da += [dq2 | dK1 dV1] . [Wq2 ; Wkv1]
+    "WaT": _PLANES["Wa"],
+    "WoT2": _PLANES["Wo2"],
+    "WkvT2": _PLANES["Wkv2"],  # [128][256]
+    "WoT1": _PLANES["Wo1"],
+    "WqT1": _PLANES["Wq1"],
+    "WvT": _PLANES["Wv"],  # [vdim][128]
+}
+
+
+def _parts(p, parts):
+    srcs = []
+    for name, sl in parts:
+        w = p[name]
+        if sl is not None:  # rows [sl0 * d, sl1 * d) of a packed [3d, d] in_proj weight
+            w = w[sl[0] * w.shape[1]:sl[1] * w.shape[1]]
+        if not w.is_contiguous():
+            raise ValueError("split planes need contiguous weight rows")
+        srcs.append(w)
+    return srcs
+
+
 class SplitPlanes:
     """bf16 hi / lo planes of the head weights the fused kernels read, refreshed by ONE mer_xh_split launch per
-    forward (inside the captured head graph, so every replay splits the current Adam-updated weights)."""
+    forward (inside the captured head graph, so every replay splits the current Adam-updated weights) and, for
+    the transposed planes of the backward, one more per backward."""
 
     def __init__(self, p: Dict[str, torch.Tensor]):
         dev = p["v_in_proj.weight"].device
-        rows = []
         self.planes = {}
+        rows = []
         for key, parts in _PLANES.items():
-            srcs = []
-            for name, sl in parts:
-                w = p[name]
-                if sl is not None:  # rows [sl0 * d, sl1 * d) of a packed [3d, d] in_proj weight
-                    w = w[sl[0] * w.shape[1]:sl[1] * w.shape[1]]
-                srcs.append(w)
-            n_rows = sum(s.shape[0] for s in srcs)
-            k = srcs[0].shape[1]
+            srcs = _parts(p, parts)
+            n_rows, k = sum(s.shape[0] for s in srcs), srcs[0].shape[1]
             hi = torch.empty(n_rows, k, device=dev, dtype=torch.bfloat16)
             lo = torch.empty(n_rows, k, device=dev, dtype=torch.bfloat16)
             off = 0
             for s in srcs:
-                if not s.is_contiguous():
-                    raise ValueError("split planes need contiguous weight rows")
-                n = s.numel()
-                rows.append([s.data_ptr(), hi.data_ptr() + 2 * off, lo.data_ptr() + 2 * off, n])
-                off += n
+                rows.append([s.data_ptr(), hi.data_ptr() + 2 * off, lo.data_ptr() + 2 * off, s.shape[0], s.shape[1], 0,
+                             s.shape[1]])
+                off += s.numel()
+            self.planes[key] = (hi, lo)
+        trows = []
+        for key, parts in _TPLANES.items():
+            srcs = _parts(p, parts)
+            n_rows, k = sum(s.shape[0] for s in srcs), srcs[0].shape[1]
+            hi = torch.empty(k, n_rows, device=dev, dtype=torch.bfloat16)
+            lo = torch.empty(k, n_rows, device=dev, dtype=torch.bfloat16)
+            col = 0
+            for s in srcs:
+                trows.append([s.data_ptr(), hi.data_ptr() + 2 * col, lo.data_ptr() + 2 * col, s.shape[0], s.shape[1], 1,
+                              n_rows])
+                col += s.shape[0]
             self.planes[key] = (hi, lo)
         self.desc = torch.tensor(rows, dtype=torch.int64).to(dev)
+        self.desc_t = torch.tensor(trows, dtype=torch.int64).to(dev)
         self.key = tuple(r[0] for r in rows)
 
     def refresh(self):
         K.xh_split(self.desc)
+
+    def refresh_transposed(self):
+        K.xh_split(self.desc_t)
 
     def __getitem__(self, key):
         return self.planes[key]
@@ -155,4 +191,84 @@ def fused_forward(p, cfg, v_feat, a_seq, training, rng, ctx, sites):
         sv.update(h=h, g=g, fused=fused)
     ctx.cfg = cfg
     ctx.drops = (dp_attn, dp_path, dp_mlp, 0.0)
+    ctx.fused = True
     return logits
+
+
+def backward_supported(ctx, p, need_da_seq: bool) -> bool:
+    """The fused backward runs on a context the fused forward filled, unless the audio features need a gradient
+    (stage 2 -- which the fused forward already excludes)."""
+    if not BWD_ENABLED or not getattr(ctx, "fused", False) or need_da_seq:
+        return False
+    C = (p["xattn_mlp.3.weight"] if ctx.cfg.xattn_head == "concat" else p["xattn_classifier.weight"]).shape[0]
+    return C <= 256
+
+
+def _splits(M: int, N: int, K: int, target: int = WGRAD_TARGET_BLOCKS) -> int:
+    """Row splits of one weight-gradient problem: about ``target`` workgroups each, at least 64 rows per split."""
+    tiles = -(-N // 64) * (-(-K // 64) if K else 1)
+    return max(1, min(-(-target // tiles), M // 64))
+
+
+def fused_backward(p, ctx, dlogits, grads, need_dv_feat=True):
+    """The fused backward (csrc/xattn_fused_bwd.hip) of a fused-forward context: the gradients head_backward
+    would write (accumulated into ``grads``), returns dv_feat [B, T, vd] (or None)."""
+    cfg = ctx.cfg
+    sv = ctx.saved
+    B, T, Ta, d, H = ctx.dims
+    rng = ctx.rng
+    dp_attn, dp_path, dp_mlp, _ = ctx.drops
+    dev = dlogits.device
+    f32 = torch.float32
+    e = lambda *shape: torch.empty(shape, device=dev, dtype=f32)  # noqa: E731
+    from .xattn_head import SITE_A2V, SITE_APATH, SITE_MLP, SITE_V2A, SITE_VPATH
+    sp = planes_for(p)
+    sp.refresh_transposed()
+    dlogits = dlogits.contiguous()
+    demb = e(B, 2 * d)
+    if cfg.xattn_head == "concat":
+        n0, n3 = "xattn_mlp.0.", "xattn_mlp.3."
+        K.xh_mlp_bwd(B, False, dlogits, sv["emb"], sv["h"], None, None, p[n0 + "weight"], p[n3 + "weight"], None,
+                     dp_mlp, rng, SITE_MLP, grads[n0 + "weight"], grads[n0 + "bias"], grads[n3 + "weight"],
+                     grads[n3 + "bias"], None, None, demb)
+    else:
+        n0, n3, nc = "xattn_gate.0.", "xattn_gate.3.", "xattn_classifier."
+        K.xh_mlp_bwd(B, True, dlogits, sv["emb"], sv["h"], sv["g"], sv["fused"], p[n0 + "weight"], p[n3 + "weight"],
+                     p[nc + "weight"], dp_mlp, rng, SITE_MLP, grads[n0 + "weight"], grads[n0 + "bias"],
+                     grads[n3 + "weight"], grads[n3 + "bias"], grads[nc + "weight"], grads[nc + "bias"], demb)
+    nt = (Ta + 15) // 16
+    scale = (d // H) ** -0.5
+    da, da2, dqkv = e(B * Ta, d), e(B * Ta, d), e(B * Ta, 3 * d)
+    dkv2_part, lnp_a = e(B, nt, 16, 2 * d), e(B * nt, 2 * d)
+    K.xh_a2v_bwd(B, T, Ta, demb, sv["s_a"], sv["mu_a"], sv["rs_a"], p["a_norm.weight"], sv["P2"], sv["kv2"], sv["q2"],
+                 sp["WoT2"], dp_attn, dp_path, rng, SITE_A2V, SITE_APATH, scale, da, da2, dqkv, dkv2_part, lnp_a)
+    vf = sv["vf"]
+    dkv2, dv2, dq1, dv = e(B * T, 2 * d), e(B * T, d), e(B * T, d), e(B * T, d)
+    dvfeat = e(B * T, vf.shape[1]) if need_dv_feat else None
+    lnp_v = e(B, 2 * d)
+    K.xh_v2a_bwd(B, T, Ta, dkv2_part, sp["WkvT2"], demb, sv["s_v"], sv["mu_v"], sv["rs_v"], p["v_norm.weight"],
+                 sp["WoT1"], sv["P1"], sv["kv1"], sv["q1"], sp["WqT1"], sp["WvT"], dp_attn, dp_path, rng, SITE_V2A,
+                 SITE_VPATH, scale, dkv2, dv2, dq1, dv, dvfeat, dqkv, lnp_v)
+    da_s = e(B * Ta, d)
+    K.xh_audio_bwd(dqkv, sp["WcT"], sp["WaT"], da, da_s)
+    gw1, gb1 = grads["v2a_attn.in_proj_weight"], grads["v2a_attn.in_proj_bias"]
+    gw2, gb2 = grads["a2v_attn.in_proj_weight"], grads["a2v_attn.in_proj_bias"]
+    Ma, Mv, af = B * Ta, B * T, sv["af"]
+    W = K.WGradTable()
+    for dY, X, dW, db in ((da_s, af, grads["audio_seq_proj.weight"], grads["audio_seq_proj.bias"]),
+                          (da, sv["a_s"], grads["a_in_proj.weight"], grads["a_in_proj.bias"]),
+                          (dqkv[:, :d], sv["a"], gw2[:d], gb2[:d]),
+                          (dqkv[:, d:], sv["a"], gw1[d:], gb1[d:]),
+                          (da2, sv["o2"], grads["a2v_attn.out_proj.weight"], grads["a2v_attn.out_proj.bias"]),
+                          (dkv2, sv["v1"], gw2[d:], gb2[d:]),
+                          (dv2, sv["o1"], grads["v2a_attn.out_proj.weight"], grads["v2a_attn.out_proj.bias"]),
+                          (dq1, sv["v"], gw1[:d], gb1[:d]),
+                          (dv, vf, grads["v_in_proj.weight"], grads["v_in_proj.bias"]),
+                          (lnp_a[:, :d], None, None, grads["a_norm.weight"]),
+                          (lnp_a[:, d:], None, None, grads["a_norm.bias"]),
+                          (lnp_v[:, :d], None, None, grads["v_norm.weight"]),
+                          (lnp_v[:, d:], None, None, grads["v_norm.bias"])):
+        W.add(dY, X, dW, db, _splits(dY.shape[0], dY.shape[1], 0 if X is None else X.shape[1]))
+    ws = e(W.ws_floats())
+    W.run(ws)
+    return dvfeat.view(B, T, -1) if dvfeat is not None else None

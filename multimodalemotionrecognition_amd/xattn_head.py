@@ -189,11 +189,15 @@ def head_forward(p: Dict[str, torch.Tensor], cfg: HeadConfig, v_feat: torch.Tens
 
 
 def head_backward(p: Dict[str, torch.Tensor], ctx: HeadCtx, dlogits: torch.Tensor, grads: Dict[str, torch.Tensor],
-                  need_dv_feat: bool = True, need_da_seq: bool = False):
+                  need_dv_feat: bool = True, need_da_seq: bool = False, fused: Optional[bool] = None):
     """Reverse schedule.  ``grads[name]`` must be zero-initialised fp32 buffers (accumulated into).
 
+    A context from the fused forward takes the fused backward (xattn_fused.fused_backward) unless ``fused`` is
+    False; the unfused schedule below reads the same saved activations.
     Returns (dv_feat [B,T,vd] fp32 or None, da_seq or None).
     """
+    if fused is not False and XF.backward_supported(ctx, p, need_da_seq):
+        return XF.fused_backward(p, ctx, dlogits, grads, need_dv_feat), None
     cfg: HeadConfig = ctx.cfg
     sv = ctx.saved
     B, T, Ta, d, H = ctx.dims
