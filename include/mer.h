@@ -482,22 +482,24 @@ int mer_xh_split(int n_items, const long long* desc, void* stream);
 
 /* F1: a_s = aseq Ws^T + bs (aseq [M][S] bf16 -- the WavLM features, exact -- or fp32), a = a_s Wa^T + ba,
  * [q2 | kv1] = a Wc^T + [bq2 | bkv1] (Wc = [a2v in_proj q rows; v2a in_proj k, v rows], 384 x 128).  Outputs
- * fp32: a_s, a, q2 [M][128], kv1 [M][256].  S % 32 == 0. */
+ * fp32: a_s, a, q2 [M][128], kv1 [M][256].  S % 32 == 0.  The same launch projects the Mv video rows:
+ * v = vfeat Wv^T + bv, q1 = v Wq1^T + bq1 ([Mv][128]; vdim % 32 == 0). */
 int mer_xh_audio_fwd(int M, int S, const void* aseq, int aseq_dtype, long ldas, const void* Ws_hi, const void* Ws_lo,
                      const float* bs, const void* Wa_hi, const void* Wa_lo, const float* ba, const void* Wc_hi,
                      const void* Wc_lo, const float* bq2, const float* bkv1, float* a_s, float* a, float* q2,
-                     float* kv1, void* stream);
+                     float* kv1, int Mv, int vdim, const float* vfeat, const void* Wv_hi, const void* Wv_lo,
+                     const float* bv, const void* Wq1_hi, const void* Wq1_lo, const float* bq1, float* v, float* q1,
+                     void* stream);
 
-/* F2 (one workgroup per sample, T <= 16, Ta <= 160): v = vfeat Wv^T + bv, q1 = v Wq1^T + bq1, v2a attention over
- * kv1, o1 Wo1^T + bo1, v1 = LayerNorm(v + keep_b * v2) (saving the pre-LN sum, mean, rstd), kv2 = v1 Wkv2^T + bkv2,
+/* F2 (one workgroup per sample, T <= 16, Ta <= 160): v2a attention of q1 over kv1, o1 Wo1^T + bo1,
+ * v1 = LayerNorm(v + keep_b * v2) (saving the pre-LN sum, mean, rstd), kv2 = v1 Wkv2^T + bkv2,
  * emb[b][0:128] = mean_t v1.  P1 [B][4][T][Ta] receives the pre-dropout probabilities. */
-int mer_xh_v2a_fwd(int B, int T, int Ta, int vdim, const float* vfeat, const void* Wv_hi, const void* Wv_lo,
-                   const float* bv, const void* Wq1_hi, const void* Wq1_lo, const float* bq1, const float* kv1,
-                   const void* Wo1_hi, const void* Wo1_lo, const float* bo1, const float* gamma, const float* beta,
-                   const void* Wkv2_hi, const void* Wkv2_lo, const float* bkv2, float attn_p, float path_p,
-                   const unsigned long long* seed, unsigned long long site_attn, unsigned long long site_path,
-                   float scale, float* v, float* q1, float* P1, float* o1, float* s_v, float* mean_v, float* rstd_v,
-                   float* v1, float* kv2, float* emb, long ld_emb, void* stream);
+int mer_xh_v2a_fwd(int B, int T, int Ta, const float* v, const float* q1, const float* kv1, const void* Wo1_hi,
+                   const void* Wo1_lo, const float* bo1, const float* gamma, const float* beta, const void* Wkv2_hi,
+                   const void* Wkv2_lo, const float* bkv2, float attn_p, float path_p, const unsigned long long* seed,
+                   unsigned long long site_attn, unsigned long long site_path, float scale, float* P1, float* o1,
+                   float* s_v, float* mean_v, float* rstd_v, float* v1, float* kv2, float* emb, long ld_emb,
+                   void* stream);
 
 /* F3 (one workgroup per (sample, 16 query rows)): a2v attention of q2 over kv2 (T keys), o2 Wo2^T + bo2,
  * a1 = LayerNorm(a + keep_b * a2) (pre-LN sum / mean / rstd saved), part[b][tile][128] = column sums of a1 over the
@@ -538,18 +540,20 @@ int mer_xh_a2v_bwd(int B, int T, int Ta, const float* demb, const float* s_a, co
 
 /* G2 (one workgroup per sample, T <= 16, Ta <= 160): dkv2 = fold(dkv2_part) [B*T][256], dv1 = demb_v / T +
  * dkv2 Wkv2, LayerNorm backward (dv2, ln_part [B][256]), do1 = dv2 Wo1, attention backward -> dq1 [B*T][128],
- * dK1 dV1 into dqkv[:, 128:384], dv = ds + dq1 Wq1 [B*T][128], dvfeat = dv Wv [B*T][vdim] (NULL: skipped). */
-int mer_xh_v2a_bwd(int B, int T, int Ta, int vdim, const float* dkv2_part, const void* WkvT2_hi, const void* WkvT2_lo,
+ * dK1 dV1 into dqkv[:, 128:384], dv [B*T][128] = the LayerNorm-residual part of dv (G1 adds dq1 Wq1). */
+int mer_xh_v2a_bwd(int B, int T, int Ta, const float* dkv2_part, const void* WkvT2_hi, const void* WkvT2_lo,
                    const float* demb, const float* s_v, const float* mean_v, const float* rstd_v, const float* gamma,
                    const void* WoT1_hi, const void* WoT1_lo, const float* P1, const float* kv1, const float* q1,
-                   const void* WqT1_hi, const void* WqT1_lo, const void* WvT_hi, const void* WvT_lo, float attn_p,
-                   float path_p, const unsigned long long* seed, unsigned long long site_attn,
+                   float attn_p, float path_p, const unsigned long long* seed, unsigned long long site_attn,
                    unsigned long long site_path, float scale, float* dkv2, float* dv2, float* dq1, float* dv,
-                   float* dvfeat, float* dqkv, float* ln_part, void* stream);
+                   float* dqkv, float* ln_part, void* stream);
 
-/* G1 (32 rows per workgroup): da += dqkv [Wq2 ; Wkv1] (in place), da_s = da Wa. */
+/* G1 (32 rows per workgroup): da += dqkv [Wq2 ; Wkv1] (in place), da_s = da Wa; the trailing ceil(Mv/32)
+ * workgroups: dv += dq1 Wq1 (in place), dvfeat = dv Wv [Mv][vdim] (NULL: not wanted). */
 int mer_xh_audio_bwd(int M, const float* dqkv, const void* WcT_hi, const void* WcT_lo, const void* WaT_hi,
-                     const void* WaT_lo, float* da, float* da_s, void* stream);
+                     const void* WaT_lo, float* da, float* da_s, int Mv, int vdim, const float* dq1,
+                     const void* WqT1_hi, const void* WqT1_lo, const void* WvT_hi, const void* WvT_lo, float* dv,
+                     float* dvfeat, void* stream);
 
 /* Grouped weight gradients: host table [nprob <= 16][11] rows {dY, ldy, X, ldx, x_dtype, M, N, K, splits, dW, db}:
  * dW [N][K] += dY^T X and db [N] += column sums of dY (K = 0: column sums only).  Row splits write partials to ws

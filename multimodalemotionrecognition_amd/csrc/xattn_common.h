@@ -3,6 +3,21 @@
 #pragma once
 #include "common.h"
 
+// Phase timestamps for kernel tuning (tools/xt_phases.py builds a separate library with -DMER_XH_TIMING; the
+// production library compiles these to nothing): XT(slot, k) stores wall_clock64() of workgroup blockIdx.x's
+// thread 0 at phase k into the slot's table.
+#ifdef MER_XH_TIMING
+static __device__ long long mer_xt_buf[4][512 * 16];  // one table per translation unit
+#define XT(slot, k) \
+  do { \
+    if (threadIdx.x == 0 && blockIdx.x < 512) mer_xt_buf[slot][blockIdx.x * 16 + (k)] = wall_clock64(); \
+  } while (0)
+#else
+#define XT(slot, k) \
+  do { \
+  } while (0)
+#endif
+
 namespace xh {
 
 constexpr int XD = 128;      // d_model
@@ -22,38 +37,38 @@ __device__ __forceinline__ f32x4 mma(bf16x8 a, bf16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
-// 8 fp32 -> (hi, lo) bf16 fragments
+typedef __attribute__((ext_vector_type(8))) float f32x8;
+
+// 8 fp32 -> (hi, lo) bf16 fragments: hi = RNE(x), lo = RNE(x - hi), both by the packed hardware conversion
 __device__ __forceinline__ void split8(const float (&x)[8], bf16x8& hi, bf16x8& lo) {
-  Frag H, L;
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const uint16_t hb = f2bf(x[e]);
-    H.h[e] = hb;
-    L.h[e] = f2bf(x[e] - bf2f(hb));
-  }
-  hi = H.v;
-  lo = L.v;
+  const f32x8 v = {x[0], x[1], x[2], x[3], x[4], x[5], x[6], x[7]};
+  hi = __builtin_convertvector(v, bf16x8);
+  lo = __builtin_convertvector(v - __builtin_convertvector(hi, f32x8), bf16x8);
 }
 
-// fp32 fragment: 8 consecutive k (stride 1) of one row; zero when !valid
+// Loads in these helpers are UNCONDITIONAL, and the caller passes an address that is always dereferenceable
+// (a clamped row): a load under a per-lane condition compiles to a branch around the load followed by a wait,
+// which serialises every load of a loop on the memory latency.  Invalid elements are zeroed by a select.
+
+// fp32 fragment: 8 consecutive k (stride 1) of one row; zero when !valid (p must still be dereferenceable)
 __device__ __forceinline__ void frag_row(const float* p, bool valid, bf16x8& hi, bf16x8& lo) {
-  float x[8];
-  if (valid) {
-    const f32x4 a = *reinterpret_cast<const f32x4*>(p), b = *reinterpret_cast<const f32x4*>(p + 4);
-    x[0] = a[0]; x[1] = a[1]; x[2] = a[2]; x[3] = a[3]; x[4] = b[0]; x[5] = b[1]; x[6] = b[2]; x[7] = b[3];
-  } else {
+  const f32x4 a = *reinterpret_cast<const f32x4*>(p), b = *reinterpret_cast<const f32x4*>(p + 4);
+  float x[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
 #pragma unroll
-    for (int e = 0; e < 8; ++e) x[e] = 0.f;
-  }
+  for (int e = 0; e < 8; ++e) x[e] = valid ? x[e] : 0.f;
   split8(x, hi, lo);
 }
 
-// fp32 fragment gathered with a k stride (transposed operand); element e valid while k0 + e < kmax
-__device__ __forceinline__ void frag_col(const float* p, long ks, int k0, int kmax, bool valid, bf16x8& hi,
-                                         bf16x8& lo) {
+// fp32 fragment gathered with a k stride (transposed operand) from p = &row k0; element e is row k0 + e, zero
+// for rows >= kmax (read from row kmax - 1 instead, so kmax >= 1 and row kmax - 1 must exist)
+__device__ __forceinline__ void frag_col(const float* p, long ks, int k0, int kmax, bf16x8& hi, bf16x8& lo) {
   float x[8];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) x[e] = (valid && k0 + e < kmax) ? p[(long)e * ks] : 0.f;
+  for (int e = 0; e < 8; ++e) {
+    const int kk = k0 + e < kmax ? k0 + e : kmax - 1;
+    const float v = p[(long)(kk - k0) * ks];
+    x[e] = k0 + e < kmax ? v : 0.f;
+  }
   split8(x, hi, lo);
 }
 
@@ -89,26 +104,76 @@ struct SplitW {  // one weight's pre-split planes [N][K]
   const bf16_t* lo;
 };
 
-// acc[i][j] (+)= A[rows 16i..][0:K] . W[cols c0 + 16j..][0:K]^T with A fp32 rows (row stride lda, 16-byte aligned),
-// rows >= rmax read as zero; W pre-split [N][K] (ldw elements)
+// acc[i][j] (+)= A[rows 16i..][0:K] . W[cols c0 + 16j..][0:K]^T with A fp32 rows (row stride lda, 16-byte aligned);
+// accumulator rows >= rmax hold junk (a copy of row rmax - 1's product) that callers must not store; W pre-split [N][K] (ldw elements).  Software-pipelined: the A rows and weight
+// fragments of the next D 32-wide k steps are in flight while a step's MFMAs run, so a K-long product costs
+// ~K / 32 / D memory latencies instead of K / 32 (these kernels are latency-bound: few workgroups, short chains).
 template <int TI, int TJ>
+struct MmStage {
+  f32x4 a0[TI], a1[TI];
+  u4 bh[TJ], bl[TJ];
+};
+
+template <int TI, int TJ>
+__device__ __forceinline__ void mm_load(MmStage<TI, TJ>& st, const float* A, long lda, int rmax, SplitW W, long ldw,
+                                        int c0, int k) {
+  const int lane = threadIdx.x & 63, fr = lane & 15, fk = (lane >> 4) * 8;
+#pragma unroll
+  for (int j = 0; j < TJ; ++j) {
+    const long off = (long)(c0 + 16 * j + fr) * ldw + k + fk;
+    st.bh[j] = *reinterpret_cast<const u4*>(W.hi + off);
+    st.bl[j] = *reinterpret_cast<const u4*>(W.lo + off);
+  }
+#pragma unroll
+  for (int i = 0; i < TI; ++i) {  // rows >= rmax read row rmax - 1: finite junk rows the epilogues never store
+    const int r = 16 * i + fr;
+    const float* p = A + (long)(r < rmax ? r : rmax - 1) * lda + k + fk;
+    st.a0[i] = *reinterpret_cast<const f32x4*>(p);  // no select here: it would wait for the load at issue
+    st.a1[i] = *reinterpret_cast<const f32x4*>(p + 4);
+  }
+}
+
+template <int TI, int TJ>
+__device__ __forceinline__ void mm_step(f32x4 (&acc)[TI][TJ], const MmStage<TI, TJ>& st, bool live) {
+  bf16x8 bh[TJ], bl[TJ];
+#pragma unroll
+  for (int j = 0; j < TJ; ++j) {
+    Frag H, L;
+    H.u = st.bh[j];
+    L.u = st.bl[j];
+    bh[j] = H.v;
+    bl[j] = L.v;
+  }
+#pragma unroll
+  for (int i = 0; i < TI; ++i) {
+    const f32x4 z = f32x4{0.f, 0.f, 0.f, 0.f};
+    const f32x4 a0 = live ? st.a0[i] : z, a1 = live ? st.a1[i] : z;  // a select, not a branch
+    const float x[8] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+    bf16x8 ah, al;
+    split8(x, ah, al);
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) acc[i][j] = mma3(ah, al, bh[j], bl[j], acc[i][j]);
+  }
+}
+
+// D k steps in flight: the stage consumed at step s was loaded D steps earlier (one workgroup per CU is common
+// here, so there are no other waves to hide a memory latency behind; the depth has to).  The loop body is
+// branch-free -- a conditional step or load would make the wait-count pass assume the worst at the merge and
+// wait for every load in flight (vmcnt(0)) -- so the tail steps past K load a clamped (valid) k slice and are
+// accumulated as zeros.
+template <int TI, int TJ, int D = 3>
 __device__ __forceinline__ void mm_aw(f32x4 (&acc)[TI][TJ], const float* A, long lda, int rmax, int K, SplitW W,
                                       long ldw, int c0) {
-  const int lane = threadIdx.x & 63, fr = lane & 15, fk = (lane >> 4) * 8;
-  for (int k = 0; k < K; k += 32) {
-    bf16x8 bh[TJ], bl[TJ];
+  const int nsteps = K / 32;
+  MmStage<TI, TJ> st[D];
 #pragma unroll
-    for (int j = 0; j < TJ; ++j) {
-      const long off = (long)(c0 + 16 * j + fr) * ldw + k + fk;
-      frag_w(W.hi + off, W.lo + off, bh[j], bl[j]);
-    }
+  for (int d = 0; d < D; ++d) mm_load(st[d], A, lda, rmax, W, ldw, c0, 32 * (d < nsteps ? d : nsteps - 1));
+  for (int s0 = 0; s0 < nsteps; s0 += D) {
 #pragma unroll
-    for (int i = 0; i < TI; ++i) {
-      const int r = 16 * i + fr;
-      bf16x8 ah, al;
-      frag_row(A + (long)r * lda + k + fk, r < rmax, ah, al);
-#pragma unroll
-      for (int j = 0; j < TJ; ++j) acc[i][j] = mma3(ah, al, bh[j], bl[j], acc[i][j]);
+    for (int d = 0; d < D; ++d) {
+      mm_step(acc, st[d], s0 + d < nsteps);
+      const int nx = s0 + d + D;
+      mm_load(st[d], A, lda, rmax, W, ldw, c0, 32 * (nx < nsteps ? nx : nsteps - 1));
     }
   }
 }

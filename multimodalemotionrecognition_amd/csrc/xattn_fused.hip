@@ -8,9 +8,10 @@
 // mer_xh_split (they change every Adam step); activations are split in registers as fragments are built.
 //
 // Four launches replace the ~40-launch schedule of xattn_head.py (mean temporal pooling; concat / gated):
-//   F1 xh_audio_fwd (grid B*Ta/32): a_seq(bf16) -> a_s = audio_seq_proj -> a = a_in_proj -> [q2 | k1 v1]
-//      (the a2v query projection and the v2a key/value projections share the input a)
-//   F2 xh_v2a_fwd (grid B): v = v_in_proj(v_feat) -> q1 -> MHA over the sample's Ta keys -> out-proj ->
+//   F1 xh_audio_fwd (grid B*Ta/32 + B*T/32): a_seq(bf16) -> a_s = audio_seq_proj -> a = a_in_proj -> [q2 | k1 v1]
+//      (the a2v query projection and the v2a key/value projections share the input a); the trailing blocks
+//      project the video rows: v = v_in_proj(v_feat), q1
+//   F2 xh_v2a_fwd (grid B): MHA of q1 over the sample's Ta keys -> out-proj ->
 //      drop-path + residual + LayerNorm -> v1 -> [k2 v2] (the a2v key/value projections) + mean-pool of v1
 //   F3 xh_a2v_fwd (grid B * ceil(Ta/16)): MHA of 16 query rows over the sample's T keys -> out-proj ->
 //      drop-path + residual + LayerNorm -> a1, per-tile column sums of a1 (the a-side mean pool)
@@ -45,6 +46,13 @@ __global__ void xh_split_kernel(const long long* __restrict__ desc) {
   }
 }
 
+#ifdef MER_XH_TIMING
+MER_API int mer_xt_read_fwd(long long* host) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(mer_xt_buf), sizeof(long long) * 4 * 512 * 16, 0,
+                                  hipMemcpyDeviceToHost);
+}
+#endif
+
 MER_API int mer_xh_split(int n_items, const long long* desc, void* stream) {
   if (n_items <= 0) return 0;
   hipLaunchKernelGGL(xh_split_kernel, dim3(64, n_items), dim3(256), 0, (hipStream_t)stream, desc);
@@ -52,54 +60,102 @@ MER_API int mer_xh_split(int n_items, const long long* desc, void* stream) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// F1: audio token chain.  32 rows per block, 4 waves.
+// F1: audio token chain, 32 rows per block, 4 waves; the trailing ceil(B*T/32) blocks run the video rows'
+// input and query projections (v, q1), which depend on nothing the audio chain makes.
 // ---------------------------------------------------------------------------------------------
+struct XhVideo {
+  int M, vdim;
+  const float* vfeat;
+  SplitW Wv;
+  const float* bv;
+  SplitW Wq1;
+  const float* bq1;
+  float* v;
+  float* q1;
+};
+
 template <typename TA>  // bf16: the WavLM features (exact, two passes); float: fp32 features (split, three passes)
 __global__ __launch_bounds__(256) void xh_audio_fwd_kernel(int M, int S, const TA* __restrict__ aseq, long ldas,
                                                            SplitW Ws, const float* __restrict__ bs, SplitW Wa,
                                                            const float* __restrict__ ba, SplitW Wc,
                                                            const float* __restrict__ bq2, const float* __restrict__ bkv1,
                                                            float* __restrict__ a_s, float* __restrict__ a,
-                                                           float* __restrict__ q2, float* __restrict__ kv1) {
+                                                           float* __restrict__ q2, float* __restrict__ kv1, XhVideo vid) {
   __shared__ __attribute__((aligned(16))) float asL[32 * LDA];
   __shared__ __attribute__((aligned(16))) float aL[32 * LDA];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, fr = lane & 15, fk = (lane >> 4) * 8;
+  const int na = (M + 31) / 32;
+  if ((int)blockIdx.x >= na) {  // video rows: v = v_feat Wv^T + bv, q1 = v Wq1^T + bq1
+    const long v0 = (long)(blockIdx.x - na) * 32;
+    const int vmax = (int)(vid.M - v0 < 32 ? vid.M - v0 : 32);
+    {
+      f32x4 acc[2][2];
+      zero(acc);
+      mm_aw(acc, vid.vfeat + v0 * vid.vdim, vid.vdim, vmax, vid.vdim, vid.Wv, vid.vdim, 32 * w);
+      store_acc(acc, 32 * w, vid.bv, asL, LDA, vid.v, XD, v0, vmax);
+    }
+    __syncthreads();
+    f32x4 acc[2][2];
+    zero(acc);
+    mm_aw(acc, asL, LDA, 32, XD, vid.Wq1, XD, 32 * w);
+    store_acc(acc, 32 * w, vid.bq1, nullptr, 0, vid.q1, XD, v0, vmax);
+    return;
+  }
+  XT(2, 0);
   const long r0 = (long)blockIdx.x * 32;
   const int rmax = (int)(M - r0 < 32 ? M - r0 : 32);
-  // a_s = a_seq Ws^T + bs  (A exact bf16: two passes)
+  // a_s = a_seq Ws^T + bs  (bf16 A is exact: two passes; fp32 A: split, three passes)
   {
     f32x4 acc[2][2];
     zero(acc);
     const int c0 = 32 * w;
-    for (int k = 0; k < S; k += 32) {
-      bf16x8 bh[2], bl[2];
+    if constexpr (sizeof(TA) == 2) {  // pipelined like mm_aw, F1_D k steps in flight
+      constexpr int F1_D = 4;
+      u4 sa[F1_D][2], sb[F1_D][2][2];
+      auto load = [&](int k, u4 (&ra)[2], u4 (&rb)[2][2]) {
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const long off = (long)(c0 + 16 * j + fr) * S + k + fk;
-        frag_w(Ws.hi + off, Ws.lo + off, bh[j], bl[j]);
-      }
+        for (int j = 0; j < 2; ++j) {
+          const long off = (long)(c0 + 16 * j + fr) * S + k + fk;
+          rb[j][0] = *reinterpret_cast<const u4*>(Ws.hi + off);
+          rb[j][1] = *reinterpret_cast<const u4*>(Ws.lo + off);
+        }
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int r = 16 * i + fr;
-        if constexpr (sizeof(TA) == 2) {
-          Frag A;
-          A.u = r < rmax ? *reinterpret_cast<const u4*>(aseq + (r0 + r) * ldas + k + fk) : u4{0u, 0u, 0u, 0u};
+        for (int i = 0; i < 2; ++i) {
+          const int r = 16 * i + fr;
+          ra[i] = *reinterpret_cast<const u4*>(aseq + (r0 + (r < rmax ? r : rmax - 1)) * ldas + k + fk);
+        }
+      };
+      const int nsteps = S / 32;  // branch-free pipeline, as mm_aw
 #pragma unroll
-          for (int j = 0; j < 2; ++j) {
-            acc[i][j] = mma(A.v, bh[j], acc[i][j]);
-            acc[i][j] = mma(A.v, bl[j], acc[i][j]);
+      for (int d = 0; d < F1_D; ++d) load(32 * (d < nsteps ? d : nsteps - 1), sa[d], sb[d]);
+      for (int s0 = 0; s0 < nsteps; s0 += F1_D) {
+#pragma unroll
+        for (int d = 0; d < F1_D; ++d) {
+          const bool live = s0 + d < nsteps;
+#pragma unroll
+          for (int i = 0; i < 2; ++i) {
+            Frag A;
+            A.u = live ? sa[d][i] : u4{0u, 0u, 0u, 0u};
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+              Frag H, L;
+              H.u = sb[d][j][0];
+              L.u = sb[d][j][1];
+              acc[i][j] = mma(A.v, H.v, acc[i][j]);
+              acc[i][j] = mma(A.v, L.v, acc[i][j]);
+            }
           }
-        } else {
-          bf16x8 ah, al;
-          frag_row(reinterpret_cast<const float*>(aseq) + (r0 + r) * ldas + k + fk, r < rmax, ah, al);
-#pragma unroll
-          for (int j = 0; j < 2; ++j) acc[i][j] = mma3(ah, al, bh[j], bl[j], acc[i][j]);
+          const int nx = s0 + d + F1_D;
+          load(32 * (nx < nsteps ? nx : nsteps - 1), sa[d], sb[d]);
         }
       }
+    } else {
+      mm_aw(acc, reinterpret_cast<const float*>(aseq) + r0 * ldas, ldas, rmax, S, Ws, S, c0);
     }
     store_acc(acc, c0, bs, asL, LDA, a_s, XD, r0, rmax);
   }
   __syncthreads();
+  XT(2, 1);
   {  // a = a_s Wa^T + ba
     f32x4 acc[2][2];
     zero(acc);
@@ -107,6 +163,7 @@ __global__ __launch_bounds__(256) void xh_audio_fwd_kernel(int M, int S, const T
     store_acc(acc, 32 * w, ba, aL, LDA, a, XD, r0, rmax);
   }
   __syncthreads();
+  XT(2, 2);
   {  // [q2 | k1 v1] = a Wc^T + [bq2 | bkv1]: 384 columns, 96 per wave
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
@@ -132,22 +189,28 @@ __global__ __launch_bounds__(256) void xh_audio_fwd_kernel(int M, int S, const T
       }
     }
   }
+  XT(2, 3);
 }
 
 MER_API int mer_xh_audio_fwd(int M, int S, const void* aseq, int aseq_dtype, long ldas, const void* Ws_hi,
                              const void* Ws_lo, const float* bs, const void* Wa_hi, const void* Wa_lo, const float* ba,
                              const void* Wc_hi, const void* Wc_lo, const float* bq2, const float* bkv1, float* a_s,
-                             float* a, float* q2, float* kv1, void* stream) {
-  if (M <= 0) return 0;
-  if (S % 32 || ldas % 8 || ((uintptr_t)aseq & 15)) return (int)hipErrorInvalidValue;
+                             float* a, float* q2, float* kv1, int Mv, int vdim, const float* vfeat, const void* Wv_hi,
+                             const void* Wv_lo, const float* bv, const void* Wq1_hi, const void* Wq1_lo,
+                             const float* bq1, float* v, float* q1, void* stream) {
+  if (M <= 0 || Mv < 0) return (int)hipErrorInvalidValue;
+  if (S % 32 || ldas % 8 || ((uintptr_t)aseq & 15) || (Mv > 0 && (vdim <= 0 || vdim % 32))) return (int)hipErrorInvalidValue;
   const SplitW ws{(const bf16_t*)Ws_hi, (const bf16_t*)Ws_lo}, wa{(const bf16_t*)Wa_hi, (const bf16_t*)Wa_lo},
       wc{(const bf16_t*)Wc_hi, (const bf16_t*)Wc_lo};
+  const XhVideo vid{Mv, vdim, vfeat, SplitW{(const bf16_t*)Wv_hi, (const bf16_t*)Wv_lo}, bv,
+                    SplitW{(const bf16_t*)Wq1_hi, (const bf16_t*)Wq1_lo}, bq1, v, q1};
+  const dim3 grid((M + 31) / 32 + (Mv + 31) / 32);
   if (aseq_dtype == MER_BF16)
-    hipLaunchKernelGGL(xh_audio_fwd_kernel<bf16_t>, dim3((M + 31) / 32), dim3(256), 0, (hipStream_t)stream, M, S,
-                       (const bf16_t*)aseq, ldas, ws, bs, wa, ba, wc, bq2, bkv1, a_s, a, q2, kv1);
+    hipLaunchKernelGGL(xh_audio_fwd_kernel<bf16_t>, grid, dim3(256), 0, (hipStream_t)stream, M, S,
+                       (const bf16_t*)aseq, ldas, ws, bs, wa, ba, wc, bq2, bkv1, a_s, a, q2, kv1, vid);
   else
-    hipLaunchKernelGGL(xh_audio_fwd_kernel<float>, dim3((M + 31) / 32), dim3(256), 0, (hipStream_t)stream, M, S,
-                       (const float*)aseq, ldas, ws, bs, wa, ba, wc, bq2, bkv1, a_s, a, q2, kv1);
+    hipLaunchKernelGGL(xh_audio_fwd_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, M, S,
+                       (const float*)aseq, ldas, ws, bs, wa, ba, wc, bq2, bkv1, a_s, a, q2, kv1, vid);
   MER_LAUNCH_CHECK();
 }
 
@@ -168,12 +231,12 @@ __device__ __forceinline__ void head_attention(int b, int h, int i0, int Lq, int
   for (int t = 0; t < NT; ++t) s[t] = f32x4{0.f, 0.f, 0.f, 0.f};
   {
     bf16x8 ah, al;
-    frag_row(Qrows + (long)fr * ldq + h * XDH + fk, i0 + fr < Lq, ah, al);
+    frag_row(Qrows + (long)(i0 + fr < Lq ? fr : Lq - 1 - i0) * ldq + h * XDH + fk, i0 + fr < Lq, ah, al);
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       const int j = 16 * t + fr;
       bf16x8 bh, bl;
-      frag_row(Krows + (long)j * ldkv + h * XDH + fk, j < Lk, bh, bl);
+      frag_row(Krows + (long)(j < Lk ? j : Lk - 1) * ldkv + h * XDH + fk, j < Lk, bh, bl);
       s[t] = mma3(ah, al, bh, bl, s[t]);
     }
   }
@@ -206,7 +269,7 @@ __device__ __forceinline__ void head_attention(int b, int h, int i0, int Lq, int
   for (int r = 0; r < 4; ++r)
 #pragma unroll
     for (int o = 1; o < 16; o <<= 1) sum[r] += __shfl_xor(sum[r], o, 64);
-  const int KP = 16 * NT;  // keys padded to the tile; PV contracts over KP rounded up to 32
+  constexpr int KP = 16 * NT;  // keys padded to the tile; PV contracts over KP rounded up to 32
 #pragma unroll
   for (int t = 0; t < NT; ++t)
 #pragma unroll
@@ -226,15 +289,16 @@ __device__ __forceinline__ void head_attention(int b, int h, int i0, int Lq, int
   }
   wave_sync_lds();
   // O_h = P' V_h: A = P' (16 x KP32), B[n = head dim][k = key] = V rows (gathered with stride ldkv)
-  const int KC = (KP + 31) / 32 * 32;
+  constexpr int KC = (KP + 31) / 32 * 32;
   f32x4 o[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
   for (int k = 0; k < KC; k += 32) {
     bf16x8 ah, al;
     frag_row(PL + fr * pld + k + fk, true, ah, al);
 #pragma unroll
     for (int jt = 0; jt < 2; ++jt) {
       bf16x8 bh, bl;
-      frag_col(Vrows + (long)(k + fk) * ldkv + h * XDH + 16 * jt + fr, ldkv, k + fk, Lk, true, bh, bl);
+      frag_col(Vrows + (long)(k + fk) * ldkv + h * XDH + 16 * jt + fr, ldkv, k + fk, Lk, bh, bl);
       o[jt] = mma3(ah, al, bh, bl, o[jt]);
     }
   }
@@ -274,10 +338,9 @@ constexpr int F2_KT = 10;                 // Ta <= 160 keys
 constexpr int F2_PLD = 16 * F2_KT + 20;   // P' tile stride (>= 32-padded keys)
 
 __global__ __launch_bounds__(256) void xh_v2a_fwd_kernel(
-    int T, int Ta, int vdim, const float* __restrict__ vfeat, SplitW Wv, const float* __restrict__ bv, SplitW Wq1,
-    const float* __restrict__ bq1, const float* __restrict__ kv1, SplitW Wo1, const float* __restrict__ bo1,
-    const float* __restrict__ gamma, const float* __restrict__ beta, SplitW Wkv2, const float* __restrict__ bkv2,
-    XhDrop dr, float scale, float* __restrict__ v, float* __restrict__ q1, float* __restrict__ P1,
+    int T, int Ta, const float* __restrict__ v, const float* __restrict__ q1, const float* __restrict__ kv1,
+    SplitW Wo1, const float* __restrict__ bo1, const float* __restrict__ gamma, const float* __restrict__ beta,
+    SplitW Wkv2, const float* __restrict__ bkv2, XhDrop dr, float scale, float* __restrict__ P1,
     float* __restrict__ o1, float* __restrict__ s_v, float* __restrict__ mean_v, float* __restrict__ rstd_v,
     float* __restrict__ v1, float* __restrict__ kv2, float* __restrict__ emb, long ld_emb) {
   extern __shared__ __attribute__((aligned(16))) float f2smem[];  // F2_LDS_BYTES
@@ -290,24 +353,22 @@ __global__ __launch_bounds__(256) void xh_v2a_fwd_kernel(
   const long row0 = (long)b * T;
   const unsigned long long seed_attn = mer_site_seed(dr.seed, dr.site_attn);
   const unsigned long long seed_path = mer_site_seed(dr.seed, dr.site_path);
-  {  // v = v_feat Wv^T + bv
-    f32x4 acc[1][2];
-    zero(acc);
-    mm_aw(acc, vfeat + row0 * vdim, vdim, T, vdim, Wv, vdim, 32 * w);
-    store_acc(acc, 32 * w, bv, vL, LDA, v, XD, row0, T);
+#pragma unroll
+  for (int e = threadIdx.x; e < 16 * XD; e += 256) {  // v, q1 (F1's video blocks)
+    const int r = e / XD, c = e - r * XD;
+    const long rc = row0 + (r < T ? r : T - 1);
+    const float xv = v[rc * XD + c], xq = q1[rc * XD + c];
+    vL[r * LDA + c] = r < T ? xv : 0.f;
+    qL[r * LDA + c] = r < T ? xq : 0.f;
   }
+  XT(3, 0);
   __syncthreads();
-  {  // q1 = v Wq1^T + bq1
-    f32x4 acc[1][2];
-    zero(acc);
-    mm_aw(acc, vL, LDA, 16, XD, Wq1, XD, 32 * w);
-    store_acc(acc, 32 * w, bq1, qL, LDA, q1, XD, row0, T);
-  }
-  __syncthreads();
+  XT(3, 1);
   // attention: wave w = head w, keys = this sample's Ta rows of kv1 (k | v)
   head_attention<F2_KT>(b, w, 0, T, Ta, qL, LDA, kv1 + (long)b * Ta * 2 * XD, kv1 + (long)b * Ta * 2 * XD + XD, 2 * XD,
                         scale, P1, dr.attn, seed_attn, PL + w * 16 * F2_PLD, F2_PLD, oL);
   __syncthreads();
+  XT(3, 2);
   for (int e = threadIdx.x; e < T * XD; e += 256) o1[row0 * XD + e] = oL[(e / XD) * LDA + e % XD];
   {  // v2 = o Wo1^T + bo1
     f32x4 acc[1][2];
@@ -316,6 +377,7 @@ __global__ __launch_bounds__(256) void xh_v2a_fwd_kernel(
     store_acc(acc, 32 * w, bo1, tL, LDA, nullptr, 0, 0, 16);
   }
   __syncthreads();
+  XT(3, 3);
   // v1 = LN(v + keep_b * v2)  (StochasticDepth: one keep draw per sample, fusion.py:11-26)
   add_ln_rows(T, vL, tL, dropout_scale(seed_path, b, dr.path), gamma, beta, qL, s_v, mean_v, rstd_v, row0);
   __syncthreads();
@@ -333,31 +395,28 @@ __global__ __launch_bounds__(256) void xh_v2a_fwd_kernel(
     mm_aw(acc, qL, LDA, 16, XD, Wkv2, XD, 64 * w);
     store_acc(acc, 64 * w, bkv2, nullptr, 0, kv2, 2 * XD, row0, T);
   }
+  XT(3, 4);
 }
 
 constexpr size_t F2_LDS_BYTES = sizeof(float) * (3 * 16 * LDA + XH * 16 * F2_PLD);
 
-MER_API int mer_xh_v2a_fwd(int B, int T, int Ta, int vdim, const float* vfeat, const void* Wv_hi, const void* Wv_lo,
-                           const float* bv, const void* Wq1_hi, const void* Wq1_lo, const float* bq1, const float* kv1,
-                           const void* Wo1_hi, const void* Wo1_lo, const float* bo1, const float* gamma,
-                           const float* beta, const void* Wkv2_hi, const void* Wkv2_lo, const float* bkv2,
-                           float attn_p, float path_p, const unsigned long long* seed, unsigned long long site_attn,
-                           unsigned long long site_path, float scale, float* v, float* q1, float* P1, float* o1,
-                           float* s_v, float* mean_v, float* rstd_v, float* v1, float* kv2, float* emb, long ld_emb,
-                           void* stream) {
+MER_API int mer_xh_v2a_fwd(int B, int T, int Ta, const float* v, const float* q1, const float* kv1, const void* Wo1_hi,
+                           const void* Wo1_lo, const float* bo1, const float* gamma, const float* beta,
+                           const void* Wkv2_hi, const void* Wkv2_lo, const float* bkv2, float attn_p, float path_p,
+                           const unsigned long long* seed, unsigned long long site_attn, unsigned long long site_path,
+                           float scale, float* P1, float* o1, float* s_v, float* mean_v, float* rstd_v, float* v1,
+                           float* kv2, float* emb, long ld_emb, void* stream) {
   if (B <= 0) return 0;
-  if (T <= 0 || T > 16 || Ta <= 0 || Ta > 16 * F2_KT || vdim % 32) return (int)hipErrorInvalidValue;
+  if (T <= 0 || T > 16 || Ta <= 0 || Ta > 16 * F2_KT) return (int)hipErrorInvalidValue;
   if ((attn_p > 0.f || path_p > 0.f) && !seed) return (int)hipErrorInvalidValue;
   XhDrop dr{attn_p, path_p, seed, site_attn, site_path};
   if (hipFuncSetAttribute(reinterpret_cast<const void*>(&xh_v2a_fwd_kernel),
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)F2_LDS_BYTES) != hipSuccess)
     return (int)hipErrorInvalidConfiguration;
-  hipLaunchKernelGGL(xh_v2a_fwd_kernel, dim3(B), dim3(256), F2_LDS_BYTES, (hipStream_t)stream, T, Ta, vdim, vfeat,
-                     SplitW{(const bf16_t*)Wv_hi, (const bf16_t*)Wv_lo}, bv,
-                     SplitW{(const bf16_t*)Wq1_hi, (const bf16_t*)Wq1_lo}, bq1, kv1,
+  hipLaunchKernelGGL(xh_v2a_fwd_kernel, dim3(B), dim3(256), F2_LDS_BYTES, (hipStream_t)stream, T, Ta, v, q1, kv1,
                      SplitW{(const bf16_t*)Wo1_hi, (const bf16_t*)Wo1_lo}, bo1, gamma, beta,
-                     SplitW{(const bf16_t*)Wkv2_hi, (const bf16_t*)Wkv2_lo}, bkv2, dr, scale, v, q1, P1, o1, s_v,
-                     mean_v, rstd_v, v1, kv2, emb, ld_emb);
+                     SplitW{(const bf16_t*)Wkv2_hi, (const bf16_t*)Wkv2_lo}, bkv2, dr, scale, P1, o1, s_v, mean_v,
+                     rstd_v, v1, kv2, emb, ld_emb);
   MER_LAUNCH_CHECK();
 }
 
@@ -386,9 +445,11 @@ __global__ __launch_bounds__(256) void xh_a2v_fwd_kernel(int T, int Ta, int ntil
   const unsigned long long seed_path = mer_site_seed(dr.seed, dr.site_path);
   head_attention<1>(b, w, i0, Ta, T, q2 + row0 * XD, XD, kv2 + (long)b * T * 2 * XD, kv2 + (long)b * T * 2 * XD + XD,
                     2 * XD, scale, P2, dr.attn, seed_attn, PL + w * 16 * F3_PLD, F3_PLD, oL);
+#pragma unroll
   for (int e = threadIdx.x; e < 16 * XD; e += 256) {
     const int r = e / XD, c = e - r * XD;
-    aL[r * LDA + c] = r < nr ? a[(row0 + r) * XD + c] : 0.f;
+    const float x = a[(row0 + (r < nr ? r : nr - 1)) * XD + c];
+    aL[r * LDA + c] = r < nr ? x : 0.f;
   }
   __syncthreads();
   for (int e = threadIdx.x; e < nr * XD; e += 256) o2[row0 * XD + e] = oL[(e / XD) * LDA + e % XD];
@@ -430,6 +491,8 @@ MER_API int mer_xh_a2v_fwd(int B, int T, int Ta, const float* q2, const float* k
 //   gated:  h = dropout(relu(emb Wg0^T + b)), z = h Wg3^T + b, g = sigmoid(z),
 //           fused = g v_emb + (1 - g) a_emb, logits = fused Wc^T + bc
 // ---------------------------------------------------------------------------------------------
+constexpr int F4_KC = 32;  // W0 k-chunk staged in LDS
+
 __global__ __launch_bounds__(256) void xh_mlp_fwd_kernel(int B, int Ta, int ntiles, int gated, int H1, int C,
                                                          const float* __restrict__ part, float* __restrict__ emb,
                                                          const float* __restrict__ W0, const float* __restrict__ b0,
@@ -441,9 +504,11 @@ __global__ __launch_bounds__(256) void xh_mlp_fwd_kernel(int B, int Ta, int ntil
                                                          float* __restrict__ logits) {
   __shared__ float eL[4][2 * XD];
   __shared__ float hL[4][256];
+  __shared__ float wL[256 * (F4_KC + 1)];  // W0[:, k0 : k0 + 32], row stride 33 (conflict-free column reads)
   __shared__ float zL[4];
-  const int t = threadIdx.x, s0 = blockIdx.x * 4;
+  const int t = threadIdx.x, s0 = blockIdx.x * 4, w = t >> 6, lane = t & 63;
   const unsigned long long seed = mer_site_seed(seed_ptr, site);
+#pragma unroll
   for (int e = t; e < 4 * 2 * XD; e += 256) {
     const int s = e / (2 * XD), c = e - s * 2 * XD, bb = s0 + s;
     float val = 0.f;
@@ -452,22 +517,51 @@ __global__ __launch_bounds__(256) void xh_mlp_fwd_kernel(int B, int Ta, int ntil
         val = emb[(long)bb * 2 * XD + c];
       } else {
         float acc = 0.f;
-        for (int q = 0; q < ntiles; ++q) acc += part[((long)bb * ntiles + q) * XD + c - XD];
+#pragma unroll
+        for (int q = 0; q < F2_KT; ++q) {
+          const float x = part[((long)bb * ntiles + (q < ntiles ? q : ntiles - 1)) * XD + c - XD];
+          acc += q < ntiles ? x : 0.f;
+        }
         val = acc / Ta;
         emb[(long)bb * 2 * XD + c] = val;
       }
     }
     eL[s][c] = val;
   }
-  __syncthreads();
+  // h = relu(emb W0^T + b0): thread t = output t for the 4 samples, W0 staged 32 columns at a time; the next
+  // chunk's loads (thread t: column t & 31 of rows t / 32 + 8 i) are in flight while this chunk is consumed
+  float acc[4];
+  for (int s = 0; s < 4; ++s) acc[s] = t < H1 ? b0[t] : 0.f;
+  float pre[256 / 8];
+  auto load = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < 256 / 8; ++i) {
+      const int r = (t >> 5) + 8 * i;
+      const float x = W0[(long)(r < H1 ? r : H1 - 1) * 2 * XD + k0 + (t & 31)];
+      pre[i] = r < H1 ? x : 0.f;
+    }
+  };
+  load(0);
+  for (int k0 = 0; k0 < 2 * XD; k0 += F4_KC) {
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 256 / 8; ++i) wL[((t >> 5) + 8 * i) * (F4_KC + 1) + (t & 31)] = pre[i];
+    __syncthreads();
+    if (k0 + F4_KC < 2 * XD) load(k0 + F4_KC);
+    if (t < H1) {
+#pragma unroll 8
+      for (int kk = 0; kk < F4_KC; ++kk) {
+        const float wv = wL[t * (F4_KC + 1) + kk];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) acc[s] = fmaf(eL[s][k0 + kk], wv, acc[s]);
+      }
+    }
+  }
   if (t < H1) {
-    const float* wr = W0 + (long)t * 2 * XD;
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       const int bb = s0 + s;
-      float acc = b0[t];
-      for (int k = 0; k < 2 * XD; ++k) acc = fmaf(eL[s][k], wr[k], acc);
-      float hv = acc > 0.f ? acc : 0.f;
+      float hv = acc[s] > 0.f ? acc[s] : 0.f;
       if (bb < B) {
         hv *= dropout_scale(seed, (uint64_t)((long)bb * H1 + t), mlp_p);
         hsave[(long)bb * H1 + t] = hv;
@@ -476,24 +570,26 @@ __global__ __launch_bounds__(256) void xh_mlp_fwd_kernel(int B, int Ta, int ntil
     }
   }
   __syncthreads();
-  if (!gated) {
-    if (t < 4 * C) {
-      const int s = t / C, c = t - s * C, bb = s0 + s;
-      if (bb < B) {
-        float acc = b3[c];
-        for (int k = 0; k < H1; ++k) acc = fmaf(hL[s][k], W3[(long)c * H1 + k], acc);
-        logits[(long)bb * C + c] = acc;
-      }
+  if (!gated) {  // logits: one wave per (sample, class) dot over H1
+    for (int o = w; o < 4 * C; o += 4) {
+      const int s = o / C, c = o - s * C, bb = s0 + s;
+      float a = 0.f;
+      for (int k = lane; k < H1; k += 64) a = fmaf(hL[s][k], W3[(long)c * H1 + k], a);
+      a = wave_sum(a);
+      if (lane == 0 && bb < B) logits[(long)bb * C + c] = a + b3[c];
     }
     return;
   }
-  if (t < 4) {  // z = h Wg3^T + b (one output), g = sigmoid(z)
-    const int bb = s0 + t;
-    float acc = b3[0];
-    for (int k = 0; k < H1; ++k) acc = fmaf(hL[t][k], W3[k], acc);
-    const float g = 1.f / (1.f + expf(-acc));
-    zL[t] = g;
-    if (bb < B) gsave[bb] = g;
+  {  // z = h Wg3^T + b (one output per sample, wave s), g = sigmoid(z)
+    const int s = w, bb = s0 + s;
+    float a = 0.f;
+    for (int k = lane; k < H1; k += 64) a = fmaf(hL[s][k], W3[k], a);
+    a = wave_sum(a) + b3[0];
+    const float g = 1.f / (1.f + expf(-a));
+    if (lane == 0) {
+      zL[s] = g;
+      if (bb < B) gsave[bb] = g;
+    }
   }
   __syncthreads();
   for (int e = t; e < 4 * XD; e += 256) {
@@ -504,13 +600,12 @@ __global__ __launch_bounds__(256) void xh_mlp_fwd_kernel(int B, int Ta, int ntil
     if (bb < B) fsave[(long)bb * XD + c] = f;
   }
   __syncthreads();
-  if (t < 4 * C) {
-    const int s = t / C, c = t - s * C, bb = s0 + s;
-    if (bb < B) {
-      float acc = bc[c];
-      for (int k = 0; k < XD; ++k) acc = fmaf(hL[s][k], Wc[(long)c * XD + k], acc);
-      logits[(long)bb * C + c] = acc;
-    }
+  for (int o = w; o < 4 * C; o += 4) {
+    const int s = o / C, c = o - s * C, bb = s0 + s;
+    float a = 0.f;
+    for (int k = lane; k < XD; k += 64) a = fmaf(hL[s][k], Wc[(long)c * XD + k], a);
+    a = wave_sum(a);
+    if (lane == 0 && bb < B) logits[(long)bb * C + c] = a + bc[c];
   }
 }
 
@@ -519,7 +614,8 @@ MER_API int mer_xh_mlp_fwd(int B, int Ta, int gated, int H1, int C, const float*
                            float mlp_p, const unsigned long long* seed, unsigned long long site, float* hsave,
                            float* gsave, float* fsave, float* logits, void* stream) {
   if (B <= 0) return 0;
-  if (H1 <= 0 || H1 > 256 || C <= 0 || 4 * C > 256 || (mlp_p > 0.f && !seed)) return (int)hipErrorInvalidValue;
+  if (H1 <= 0 || H1 > 256 || C <= 0 || 4 * C > 256 || Ta > 16 * F2_KT || (mlp_p > 0.f && !seed))
+    return (int)hipErrorInvalidValue;
   if (gated && (!Wc || !bc || !gsave || !fsave || H1 > 256)) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(xh_mlp_fwd_kernel, dim3((B + 3) / 4), dim3(256), 0, (hipStream_t)stream, B, Ta, (Ta + 15) / 16,
                      gated, H1, C, part, emb, W0, b0, W3, b3, Wc, bc, mlp_p, seed, site, hsave, gsave, fsave, logits);

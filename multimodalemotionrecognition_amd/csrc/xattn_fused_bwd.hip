@@ -1,12 +1,13 @@
 // Fused xattn head backward: the reverse of xattn_fused.hip (fusion.py:366-411 + the two nn.MultiheadAttention
 // blocks, TORCH:6576-6606) on split-bf16 MFMA.  Four data-gradient launches plus one grouped weight-gradient
 // launch and its fixed-order fold replace the ~25 backward launches of xattn_head.head_backward:
-//   G4 xh_mlp_bwd   (grid 8): classifier head -> demb; the head's own weight gradients (exact fp32 FMA)
+//   G4 xh_mlp_bwd   (grid 16): classifier head -> demb; the head's own weight gradients (exact fp32 FMA)
 //   G3 xh_a2v_bwd   (grid B * ceil(Ta/16)): a-pool / LayerNorm / out-proj / attention backward of 16 query rows
 //                   -> da (LN residual part), da2, dq2, per-tile partials of dK2 dV2 and of dgamma / dbeta
 //   G2 xh_v2a_bwd   (grid B): dK2 dV2 fold -> dv1 -> LayerNorm / out-proj / attention backward over the
-//                   sample's Ta keys -> dq1, dK1 dV1, dv and dv_feat (the ResNet18 trunk's input gradient)
-//   G1 xh_audio_bwd (grid B * Ta / 32): da += [dq2 | dK1 dV1] . [Wq2 ; Wkv1], da_s = da . Wa
+//                   sample's Ta keys -> dq1, dK1 dV1 and the residual part of dv
+//   G1 xh_audio_bwd (grid B*Ta/32 + B*T/32): da += [dq2 | dK1 dV1] . [Wq2 ; Wkv1], da_s = da . Wa; the trailing
+//                   blocks: dv += dq1 . Wq1, dv_feat = dv . Wv (the ResNet18 trunk's input gradient)
 //   W  xh_wgrad + xh_wfold: every dW = dY^T X and bias / LayerNorm-affine gradient as ONE grouped launch of
 //      (problem, 64 x 64 tile, row split) blocks writing partials, folded in split order (deterministic, no
 //      atomics) and added into the caller's gradient buffers
@@ -56,12 +57,18 @@ __device__ __forceinline__ void ln_part_store(float g0, float g1, float b0, floa
 }  // namespace
 
 // ---------------------------------------------------------------------------------------------
-// G4: classifier head backward, chunks of 32 samples.  Every block recomputes the chunk's dh (B x H1, cheap);
-// block k owns dW0 rows [k * H1 / 8, (k + 1) * H1 / 8) and demb of samples b = k (mod 8); block 0 the small
-// weights and the biases.  The unfused schedule: xattn_head.py:207-225.
+// G4: classifier head backward, chunks of 32 samples, 16 workgroups.  Every workgroup stages the chunk's emb,
+// h and dlogits in LDS and recomputes dh (B x H1, cheap); workgroup k owns the 16 emb columns
+// [16k, 16k + 16): dW0[:, slice] and demb[:, slice]; the small weights and the biases are spread over all
+// 4096 threads (one owner per output, so the += is race-free).  Unfused: xattn_head.py:207-225.
 // ---------------------------------------------------------------------------------------------
-constexpr int G4_BLOCKS = 8;
+constexpr int G4_SLICE = 16;
+constexpr int G4_BLOCKS = 2 * XD / G4_SLICE;
 constexpr int G4_CHUNK = 32;
+constexpr int G4_MAXH = 256, G4_MAXC = 32;
+constexpr int G4_DHLD = G4_MAXH + 1;
+constexpr size_t G4_LDS_FLOATS = G4_CHUNK * 2 * XD + G4_CHUNK * G4_MAXH + G4_CHUNK * G4_DHLD + G4_MAXH * G4_SLICE +
+                                 G4_CHUNK * (XD + 1) + G4_CHUNK * G4_MAXC + G4_MAXC * XD;
 
 __global__ __launch_bounds__(256) void xh_mlp_bwd_kernel(int B, int C, int H1, int gated, const float* __restrict__ dl,
                                                          const float* __restrict__ emb, const float* __restrict__ h,
@@ -73,97 +80,183 @@ __global__ __launch_bounds__(256) void xh_mlp_bwd_kernel(int B, int C, int H1, i
                                                          float* __restrict__ db0, float* __restrict__ dW3,
                                                          float* __restrict__ db3, float* __restrict__ dWc,
                                                          float* __restrict__ dbc, float* __restrict__ demb) {
-  __shared__ float dh[G4_CHUNK][256];
-  __shared__ float dfz[G4_CHUNK][XD + 1];  // gated: dfused (cols 0..127) and dz (col 128)
-  const int t = threadIdx.x, k = blockIdx.x;
+  extern __shared__ float g4smem[];
+  float* eL = g4smem;                     // [32][256]  emb chunk
+  float* hL = eL + G4_CHUNK * 2 * XD;     // [32][H1]   h chunk (post-dropout)
+  float* dhL = hL + G4_CHUNK * G4_MAXH;   // [32][G4_DHLD]
+  float* w0s = dhL + G4_CHUNK * G4_DHLD;  // [H1][16]   W0[:, slice]
+  float* dfz = w0s + G4_MAXH * G4_SLICE;  // [32][129]  gated: dfused, dz (col 128)
+  float* dlL = dfz + G4_CHUNK * (XD + 1); // [32][C]
+  float* wcL = dlL + G4_CHUNK * G4_MAXC;  // [C][128]   gated: Wc
+  const int t = threadIdx.x, k = blockIdx.x, j0 = k * G4_SLICE, w = t >> 6, lane = t & 63;
+  const int gt = k * 256 + t, nthreads = G4_BLOCKS * 256;
   const unsigned long long seed = mer_site_seed(seed_ptr, site);
-  const int rows_per = (H1 + G4_BLOCKS - 1) / G4_BLOCKS;
-  for (int c0 = 0; c0 < B; c0 += G4_CHUNK) {
-    const int nb = B - c0 < G4_CHUNK ? B - c0 : G4_CHUNK;
-    const float* dlc = dl + (long)c0 * C;
-    const float* embc = emb + (long)c0 * 2 * XD;
-    __syncthreads();
-    if (gated) {
-      for (int e = t; e < nb * XD; e += 256) {
-        const int b = e / XD, c = e - b * XD;
-        float acc = 0.f;
-        for (int q = 0; q < C; ++q) acc = fmaf(dlc[b * C + q], Wc[q * XD + c], acc);
-        dfz[b][c] = acc;
-      }
-      __syncthreads();
-      if (t < nb) {  // dz = sum_c dfused (v - a) g (1 - g)
-        float acc = 0.f;
-        for (int c = 0; c < XD; ++c) acc += dfz[t][c] * (embc[(long)t * 2 * XD + c] - embc[(long)t * 2 * XD + XD + c]);
-        const float g = gsave[c0 + t];
-        dfz[t][XD] = acc * g * (1.f - g);
-      }
-      __syncthreads();
-    }
-    for (int e = t; e < nb * H1; e += 256) {
-      const int b = e / H1, c = e - b * H1;
-      float acc;
-      if (gated) {
-        acc = dfz[b][XD] * W3[c];
-      } else {
-        acc = 0.f;
-        for (int q = 0; q < C; ++q) acc = fmaf(dlc[b * C + q], W3[q * H1 + c], acc);
-      }
-      const float hv = h[(long)(c0 + b) * H1 + c];  // post-dropout activation: relu' * keep / (1 - p)
-      dh[b][c] = hv > 0.f ? acc * dropout_scale(seed, (uint64_t)((long)(c0 + b) * H1 + c), mlp_p) : 0.f;
-    }
-    __syncthreads();
-    for (int r = k * rows_per; r < (k + 1) * rows_per && r < H1; ++r) {  // dW0[r][j] += sum_b dh[b][r] emb[b][j]
-      float acc = 0.f;
-      for (int b = 0; b < nb; ++b) acc = fmaf(dh[b][r], embc[(long)b * 2 * XD + t], acc);
-      dW0[(long)r * 2 * XD + t] += acc;
-    }
-    if (k == 0) {
-      if (t < H1) {
-        float acc = 0.f;
-        for (int b = 0; b < nb; ++b) acc += dh[b][t];
-        db0[t] += acc;
-      }
-      if (!gated) {
-        for (int e = t; e < C * H1; e += 256) {
-          const int q = e / H1, c = e - q * H1;
-          float acc = 0.f;
-          for (int b = 0; b < nb; ++b) acc = fmaf(dlc[b * C + q], h[(long)(c0 + b) * H1 + c], acc);
-          dW3[e] += acc;
-        }
-      } else {
-        if (t < H1) {
-          float acc = 0.f;
-          for (int b = 0; b < nb; ++b) acc = fmaf(dfz[b][XD], h[(long)(c0 + b) * H1 + t], acc);
-          dW3[t] += acc;
-        }
-        if (t == 0) {
-          float acc = 0.f;
-          for (int b = 0; b < nb; ++b) acc += dfz[b][XD];
-          db3[0] += acc;
-        }
-        for (int e = t; e < C * XD; e += 256) {
-          const int q = e / XD, c = e - q * XD;
-          float acc = 0.f;
-          for (int b = 0; b < nb; ++b) acc = fmaf(dlc[b * C + q], fsave[(long)(c0 + b) * XD + c], acc);
-          dWc[e] += acc;
-        }
-      }
-      if (t < C) {  // the classifier bias: xattn_mlp.3 (concat) or xattn_classifier (gated)
-        float acc = 0.f;
-        for (int b = 0; b < nb; ++b) acc += dlc[b * C + t];
-        (gated ? dbc : db3)[t] += acc;
-      }
-    }
-    for (int b = k; b < nb; b += G4_BLOCKS) {  // demb[b][j] = sum_r dh[b][r] W0[r][j] (+ the gate mix)
-      float acc = 0.f;
-      for (int r = 0; r < H1; ++r) acc = fmaf(dh[b][r], W0[(long)r * 2 * XD + t], acc);
-      if (gated) {
-        const float g = gsave[c0 + b];
-        acc += t < XD ? dfz[b][t] * g : dfz[b][t - XD] * (1.f - g);
-      }
-      demb[(long)(c0 + b) * 2 * XD + t] = acc;
+  XT(0, 0);
+  // Staging copies: float4, clamped loads and UNCONDITIONAL LDS stores (the arrays have room for whole
+  // 256-vector rounds), so no load is sunk into a per-lane branch and each round's loads are in flight together.
+  // (One workgroup per CU: nothing else hides a latency, so every phase keeps many independent loads / FMAs
+  // in flight per thread.)
+  {
+    const int n4 = H1 * G4_SLICE / 4;  // W0[:, slice]: 4 float4 per row
+#pragma unroll
+    for (int i = 0; i < G4_MAXH * G4_SLICE / 4 / 256; ++i) {
+      const int e = t + 256 * i, ec = e < n4 ? e : n4 - 1;
+      reinterpret_cast<f32x4*>(w0s)[e] = *reinterpret_cast<const f32x4*>(W0 + (long)(ec / 4) * 2 * XD + j0 + 4 * (ec % 4));
     }
   }
+  if (gated) {
+#pragma unroll 8
+    for (int i = 0; i < (C * XD + 255) / 256; ++i) {
+      const int e = t + 256 * i;
+      wcL[e] = Wc[e < C * XD ? e : C * XD - 1];
+    }
+  }
+  float w3r[G4_MAXC];  // concat: column t of W3 (W3[q][t], q < C, zero beyond); gated: W3[0][t]
+#pragma unroll
+  for (int q = 0; q < G4_MAXC; ++q) {
+    const int qc = q < C ? q : C - 1, cc = t < H1 ? t : H1 - 1;
+    const float x = gated ? W3[cc] : W3[(long)qc * H1 + cc];
+    w3r[q] = q < C ? x : 0.f;
+  }
+#pragma unroll
+  for (int i = 0; i < G4_CHUNK * G4_MAXC / 256; ++i) dlL[t + 256 * i] = 0.f;  // classes >= C stay zero
+  for (int c0 = 0; c0 < B; c0 += G4_CHUNK) {
+    const int nb = B - c0 < G4_CHUNK ? B - c0 : G4_CHUNK;
+    __syncthreads();
+    {
+      const int ne = nb * 2 * XD / 4, nh = nb * H1 / 4;
+#pragma unroll
+      for (int i = 0; i < G4_CHUNK * 2 * XD / 4 / 256; ++i) {
+        const int e = t + 256 * i;
+        reinterpret_cast<f32x4*>(eL)[e] = *reinterpret_cast<const f32x4*>(emb + (long)c0 * 2 * XD + 4 * (e < ne ? e : ne - 1));
+      }
+#pragma unroll
+      for (int i = 0; i < G4_CHUNK * G4_MAXH / 4 / 256; ++i) {
+        const int e = t + 256 * i;
+        reinterpret_cast<f32x4*>(hL)[e] = *reinterpret_cast<const f32x4*>(h + (long)c0 * H1 + 4 * (e < nh ? e : nh - 1));
+      }
+    }
+    for (int e = t; e < nb * C; e += 256) dlL[(e / C) * G4_MAXC + e % C] = dl[(long)c0 * C + e];
+    __syncthreads();
+    XT(0, 1);
+    if (gated) {
+      for (int e = t; e < nb * XD; e += 256) {  // dfused = dlogits Wc
+        const int b = e / XD, c = e - b * XD;
+        float acc = 0.f;
+        for (int q = 0; q < C; ++q) acc = fmaf(dlL[b * G4_MAXC + q], wcL[q * XD + c], acc);
+        dfz[b * (XD + 1) + c] = acc;
+      }
+      __syncthreads();
+      for (int b = w; b < nb; b += 4) {  // dz = sum_c dfused (v - a) g (1 - g)
+        const float* er = eL + b * 2 * XD;
+        const float* dr = dfz + b * (XD + 1);
+        const float s = wave_sum(dr[lane] * (er[lane] - er[XD + lane]) + dr[64 + lane] * (er[64 + lane] - er[XD + 64 + lane]));
+        const float g = gsave[c0 + b];
+        if (lane == 0) dfz[b * (XD + 1) + XD] = s * g * (1.f - g);
+      }
+      __syncthreads();
+    }
+    if (t < H1) {  // dh[b][t] = relu' . dropout' . (dlogits W3 | dz W3), thread = column
+      for (int b = 0; b < nb; ++b) {
+        float acc = 0.f;
+        if (gated) {
+          acc = dfz[b * (XD + 1) + XD] * w3r[0];
+        } else {  // all G4_MAXC classes, branch-free (zero beyond C on both sides)
+          const f32x4* d4 = reinterpret_cast<const f32x4*>(dlL + b * G4_MAXC);
+#pragma unroll
+          for (int q4 = 0; q4 < G4_MAXC / 4; ++q4) {
+            const f32x4 dv = d4[q4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) acc = fmaf(dv[u], w3r[4 * q4 + u], acc);
+          }
+        }
+        dhL[b * G4_DHLD + t] =
+            hL[b * H1 + t] > 0.f ? acc * dropout_scale(seed, (uint64_t)((long)(c0 + b) * H1 + t), mlp_p) : 0.f;
+      }
+    }
+    __syncthreads();
+    XT(0, 2);
+    {  // dW0[r][j0 + c] += sum_b dh[b][r] emb[b][j0 + c]: c = t & 15, rows r = t / 16 + 16 u (16 accumulators)
+      const int c = t & 15, rb = t >> 4;
+      float acc[G4_MAXH / 16];
+#pragma unroll
+      for (int u = 0; u < G4_MAXH / 16; ++u) acc[u] = 0.f;
+      for (int b = 0; b < nb; ++b) {
+        const float ev = eL[b * 2 * XD + j0 + c];
+#pragma unroll
+        for (int u = 0; u < G4_MAXH / 16; ++u) acc[u] = fmaf(dhL[b * G4_DHLD + rb + 16 * u], ev, acc[u]);
+      }
+      float old[G4_MAXH / 16];
+#pragma unroll
+      for (int u = 0; u < G4_MAXH / 16; ++u) {
+        const int r = rb + 16 * u;
+        old[u] = dW0[(long)(r < H1 ? r : H1 - 1) * 2 * XD + j0 + c];
+      }
+#pragma unroll
+      for (int u = 0; u < G4_MAXH / 16; ++u) {
+        const int r = rb + 16 * u;
+        if (r < H1) dW0[(long)r * 2 * XD + j0 + c] = old[u] + acc[u];
+      }
+    }
+    XT(0, 3);
+    {  // demb[b][j] = sum_r dh[b][r] W0[r][j] (+ the gate mix): c = t & 15, samples t / 16 and t / 16 + 16
+      const int c = t & 15, b0 = t >> 4, b1 = b0 + 16, j = j0 + c;
+      float a0[4] = {0.f, 0.f, 0.f, 0.f}, a1[4] = {0.f, 0.f, 0.f, 0.f};
+      for (int r = 0; r < H1; r += 4) {
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const float wv = w0s[(r + v) * G4_SLICE + c];
+          a0[v] = fmaf(dhL[b0 * G4_DHLD + r + v], wv, a0[v]);
+          a1[v] = fmaf(dhL[b1 * G4_DHLD + r + v], wv, a1[v]);
+        }
+      }
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        const int b = half ? b1 : b0;
+        const float* av = half ? a1 : a0;
+        float acc = (av[0] + av[1]) + (av[2] + av[3]);
+        if (b < nb) {
+          if (gated) {
+            const float g = gsave[c0 + b];
+            acc += j < XD ? dfz[b * (XD + 1) + j] * g : dfz[b * (XD + 1) + j - XD] * (1.f - g);
+          }
+          demb[(long)(c0 + b) * 2 * XD + j] = acc;
+        }
+      }
+    }
+    XT(0, 4);
+    // the small weights and biases, spread over the grid: [db0 | db3 or dbc | dW3 | dWc (gated) | db3 (gated)]
+    const int n_w3 = gated ? H1 : C * H1, n_wc = gated ? C * XD : 0;
+    const int total = H1 + C + n_w3 + n_wc + (gated ? 1 : 0);
+    for (int e = gt; e < total; e += nthreads) {
+      float acc = 0.f;
+      if (e < H1) {
+        for (int b = 0; b < nb; ++b) acc += dhL[b * G4_DHLD + e];
+        db0[e] += acc;
+      } else if (e < H1 + C) {
+        const int q = e - H1;
+        for (int b = 0; b < nb; ++b) acc += dlL[b * G4_MAXC + q];
+        (gated ? dbc : db3)[q] += acc;
+      } else if (e < H1 + C + n_w3) {
+        const int i = e - H1 - C;
+        if (gated) {
+          for (int b = 0; b < nb; ++b) acc = fmaf(dfz[b * (XD + 1) + XD], hL[b * H1 + i], acc);
+        } else {
+          const int q = i / H1, c = i - q * H1;
+          for (int b = 0; b < nb; ++b) acc = fmaf(dlL[b * G4_MAXC + q], hL[b * H1 + c], acc);
+        }
+        dW3[i] += acc;
+      } else if (e < H1 + C + n_w3 + n_wc) {
+        const int i = e - H1 - C - n_w3, q = i / XD, c = i - q * XD;
+        for (int b = 0; b < nb; ++b) acc = fmaf(dlL[b * G4_MAXC + q], fsave[(long)(c0 + b) * XD + c], acc);
+        dWc[i] += acc;
+      } else {
+        for (int b = 0; b < nb; ++b) acc += dfz[b * (XD + 1) + XD];
+        db3[0] += acc;
+      }
+    }
+  }
+  XT(0, 5);
 }
 
 MER_API int mer_xh_mlp_bwd(int B, int C, int H1, int gated, const float* dlogits, const float* emb, const float* h,
@@ -171,11 +264,15 @@ MER_API int mer_xh_mlp_bwd(int B, int C, int H1, int gated, const float* dlogits
                            float mlp_p, const unsigned long long* seed, unsigned long long site, float* dW0, float* db0,
                            float* dW3, float* db3, float* dWc, float* dbc, float* demb, void* stream) {
   if (B <= 0) return 0;
-  if (H1 <= 0 || H1 > 256 || C <= 0 || C > 256 || (mlp_p > 0.f && !seed) ||
+  if (H1 <= 0 || H1 > G4_MAXH || H1 % 4 || C <= 0 || C > G4_MAXC || (mlp_p > 0.f && !seed) ||
       (gated && (!Wc || !dWc || !dbc || !g || !fused)))
     return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(xh_mlp_bwd_kernel, dim3(G4_BLOCKS), dim3(256), 0, (hipStream_t)stream, B, C, H1, gated, dlogits,
-                     emb, h, g, fused, W0, W3, Wc, mlp_p, seed, site, dW0, db0, dW3, db3, dWc, dbc, demb);
+  const size_t lds = sizeof(float) * G4_LDS_FLOATS;
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&xh_mlp_bwd_kernel),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+    return (int)hipErrorInvalidConfiguration;
+  hipLaunchKernelGGL(xh_mlp_bwd_kernel, dim3(G4_BLOCKS), dim3(256), lds, (hipStream_t)stream, B, C, H1, gated,
+                     dlogits, emb, h, g, fused, W0, W3, Wc, mlp_p, seed, site, dW0, db0, dW3, db3, dWc, dbc, demb);
   MER_LAUNCH_CHECK();
 }
 
@@ -236,7 +333,7 @@ __global__ __launch_bounds__(256) void xh_a2v_bwd_kernel(
   {  // dP' = do2_h . V2_h^T
     bf16x8 ah, al, bh, bl;
     frag_row(oL + fr * LDA + h * XDH + fk, true, ah, al);
-    frag_row(kb + (long)fr * 2 * XD + XD + h * XDH + fk, fr < T, bh, bl);
+    frag_row(kb + (long)(fr < T ? fr : T - 1) * 2 * XD + XD + h * XDH + fk, fr < T, bh, bl);
     dp = mma3(ah, al, bh, bl, dp);
   }
   float pv[4], rs[4];
@@ -245,8 +342,10 @@ __global__ __launch_bounds__(256) void xh_a2v_bwd_kernel(
     const int i = i0 + 4 * fq + r, j = fr;
     const bool ok = (4 * fq + r) < nr && j < T;
     const long pi = (((long)b * XH + h) * Ta + i) * T + j;
+    const long pc = (((long)b * XH + h) * Ta + (ok ? i : i0)) * T + (ok ? j : 0);  // always in range
     const float m = ok ? dropout_scale(seed_attn, pi, dr.attn) : 0.f;
-    pv[r] = ok ? P2[pi] : 0.f;
+    const float pl = P2[pc];
+    pv[r] = ok ? pl : 0.f;
     dp[r] *= m;  // dP
     Pdt[(4 * fq + r) * G3_TLD + j] = pv[r] * m;
     rs[r] = pv[r] * dp[r];
@@ -268,7 +367,7 @@ __global__ __launch_bounds__(256) void xh_a2v_bwd_kernel(
 #pragma unroll
     for (int jt = 0; jt < 2; ++jt) {
       bf16x8 bh, bl;
-      frag_col(kb + (long)fk * 2 * XD + h * XDH + 16 * jt + fr, 2 * XD, fk, T, true, bh, bl);
+      frag_col(kb + (long)fk * 2 * XD + h * XDH + 16 * jt + fr, 2 * XD, fk, T, bh, bl);
       o[jt] = mma3(ah, al, bh, bl, o[jt]);
     }
 #pragma unroll
@@ -283,13 +382,13 @@ __global__ __launch_bounds__(256) void xh_a2v_bwd_kernel(
     f32x4 dk[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
     f32x4 dv[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
     bf16x8 sh, sl, ph, pl;
-    frag_col(dSt + (long)fk * G3_TLD + fr, G3_TLD, fk, 16, true, sh, sl);
-    frag_col(Pdt + (long)fk * G3_TLD + fr, G3_TLD, fk, 16, true, ph, pl);
+    frag_col(dSt + (long)fk * G3_TLD + fr, G3_TLD, fk, 16, sh, sl);
+    frag_col(Pdt + (long)fk * G3_TLD + fr, G3_TLD, fk, 16, ph, pl);
 #pragma unroll
     for (int jt = 0; jt < 2; ++jt) {
       bf16x8 qh, ql, gh, gl;
-      frag_col(q2 + (row0 + fk) * XD + h * XDH + 16 * jt + fr, XD, fk, nr, true, qh, ql);
-      frag_col(oL + fk * LDA + h * XDH + 16 * jt + fr, LDA, fk, 16, true, gh, gl);
+      frag_col(q2 + (row0 + fk) * XD + h * XDH + 16 * jt + fr, XD, fk, nr, qh, ql);
+      frag_col(oL + fk * LDA + h * XDH + 16 * jt + fr, LDA, fk, 16, gh, gl);
       dk[jt] = mma3(sh, sl, qh, ql, dk[jt]);
       dv[jt] = mma3(ph, pl, gh, gl, dv[jt]);
     }
@@ -330,12 +429,11 @@ constexpr int G2_SLD = 16 * G2_KT + 4;  // dS / P' tile row stride
 constexpr int G2_KVLD = 2 * XD + 4;
 
 __global__ __launch_bounds__(256) void xh_v2a_bwd_kernel(
-    int T, int Ta, int ntiles, int vdim, const float* __restrict__ dkv2_part, SplitW WkvT2,
-    const float* __restrict__ demb, const float* __restrict__ s_v, const float* __restrict__ mean_v,
-    const float* __restrict__ rstd_v, const float* __restrict__ gamma, SplitW WoT1, const float* __restrict__ P1,
-    const float* __restrict__ kv1, const float* __restrict__ q1, SplitW WqT1, SplitW WvT, XhDrop dr, float scale,
-    float* __restrict__ dkv2, float* __restrict__ dv2, float* __restrict__ dq1, float* __restrict__ dv,
-    float* __restrict__ dvfeat, float* __restrict__ dqkv, float* __restrict__ ln_part) {
+    int T, int Ta, int ntiles, const float* __restrict__ dkv2_part, SplitW WkvT2, const float* __restrict__ demb,
+    const float* __restrict__ s_v, const float* __restrict__ mean_v, const float* __restrict__ rstd_v,
+    const float* __restrict__ gamma, SplitW WoT1, const float* __restrict__ P1, const float* __restrict__ kv1,
+    const float* __restrict__ q1, XhDrop dr, float scale, float* __restrict__ dkv2, float* __restrict__ dv2,
+    float* __restrict__ dq1, float* __restrict__ dv, float* __restrict__ dqkv, float* __restrict__ ln_part) {
   extern __shared__ __attribute__((aligned(16))) float g2smem[];
   float* kvL = g2smem;                        // [16][G2_KVLD]  dK2 dV2
   float* t1 = kvL + 16 * G2_KVLD;             // [16][LDA]  dv1, then ds (the residual part of dv)
@@ -350,17 +448,24 @@ __global__ __launch_bounds__(256) void xh_v2a_bwd_kernel(
   const unsigned long long seed_attn = mer_site_seed(dr.seed, dr.site_attn);
   const unsigned long long seed_path = mer_site_seed(dr.seed, dr.site_path);
   const float keep = dropout_scale(seed_path, b, dr.path);
+  XT(1, 0);
   // dK2 dV2 of this sample: the a2v tiles' partials summed in tile order
+#pragma unroll 4
   for (int e = threadIdx.x; e < 16 * 2 * XD; e += 256) {
     const int r = e / (2 * XD), c = e - r * 2 * XD;
     float s = 0.f;
     if (r < T) {
-      for (int q = 0; q < ntiles; ++q) s += dkv2_part[(((long)b * ntiles + q) * 16 + r) * 2 * XD + c];
+#pragma unroll
+      for (int q = 0; q < G2_KT; ++q) {
+        const float x = dkv2_part[(((long)b * ntiles + (q < ntiles ? q : ntiles - 1)) * 16 + r) * 2 * XD + c];
+        s += q < ntiles ? x : 0.f;
+      }
       dkv2[(row0 + r) * 2 * XD + c] = s;
     }
     kvL[r * G2_KVLD + c] = s;
   }
   __syncthreads();
+  XT(1, 1);
   {  // dv1 (kv2 path) = [dK2 dV2] . Wkv2
     f32x4 acc[1][2];
     zero(acc);
@@ -368,6 +473,7 @@ __global__ __launch_bounds__(256) void xh_v2a_bwd_kernel(
     store_acc(acc, 32 * w, nullptr, t1, LDA, nullptr, 0, 0, 16);
   }
   __syncthreads();
+  XT(1, 2);
   {  // + v-pool (mean over T); LayerNorm backward; t1 = ds (dv residual), dv2 = keep * ds
     float g0 = 0.f, g1 = 0.f, b0 = 0.f, b1 = 0.f;
     const float pv0 = demb[(long)b * 2 * XD + lane] / T, pv1 = demb[(long)b * 2 * XD + 64 + lane] / T;
@@ -388,6 +494,7 @@ __global__ __launch_bounds__(256) void xh_v2a_bwd_kernel(
     ln_part_store(g0, g1, b0, b1, red, ln_part + (long)b * 256);
   }
   __syncthreads();
+  XT(1, 3);
   {  // do1 = dv2 . Wo1
     f32x4 acc[1][2];
     zero(acc);
@@ -395,6 +502,7 @@ __global__ __launch_bounds__(256) void xh_v2a_bwd_kernel(
     store_acc(acc, 32 * w, nullptr, oL, LDA, nullptr, 0, 0, 16);
   }
   __syncthreads();
+  XT(1, 4);
   // attention backward, head h = w, keys = the sample's Ta rows of kv1
   const int h = w;
   float* dSt = tiles + (h * 2) * 16 * G2_SLD;
@@ -410,7 +518,7 @@ __global__ __launch_bounds__(256) void xh_v2a_bwd_kernel(
     for (int t = 0; t < G2_KT; ++t) {  // dP' = do1_h . V1_h^T
       const int j = 16 * t + fr;
       bf16x8 bh, bl;
-      frag_row(kb + (long)j * 2 * XD + XD + h * XDH + fk, j < Ta, bh, bl);
+      frag_row(kb + (long)(j < Ta ? j : Ta - 1) * 2 * XD + XD + h * XDH + fk, j < Ta, bh, bl);
       dp[t] = mma3(ah, al, bh, bl, dp[t]);
     }
     float pv[G2_KT][4];
@@ -422,8 +530,10 @@ __global__ __launch_bounds__(256) void xh_v2a_bwd_kernel(
         const int i = 4 * fq + r, j = 16 * t + fr;
         const bool ok = i < T && j < Ta;
         const long pi = (((long)b * XH + h) * T + i) * Ta + j;
+        const long pc = (((long)b * XH + h) * T + (ok ? i : 0)) * Ta + (ok ? j : 0);  // always in range
         const float m = ok ? dropout_scale(seed_attn, pi, dr.attn) : 0.f;
-        const float p = ok ? P1[pi] : 0.f;
+        const float pl = P1[pc];
+        const float p = ok ? pl : 0.f;
         pv[t][r] = p;
         dp[t][r] *= m;  // dP
         Pdt[i * G2_SLD + j] = p * m;
@@ -439,15 +549,17 @@ __global__ __launch_bounds__(256) void xh_v2a_bwd_kernel(
       for (int r = 0; r < 4; ++r) dSt[(4 * fq + r) * G2_SLD + 16 * t + fr] = pv[t][r] * (dp[t][r] - rs[r]);
   }
   wave_sync_lds();
+  XT(1, 5);
   {  // dq1_h = dS . K1_h * scale  (keys >= Ta are zero in dS and read as zero from K1)
     f32x4 o[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
     for (int k = 0; k < 16 * G2_KT; k += 32) {
       bf16x8 ah, al;
       frag_row(dSt + fr * G2_SLD + k + fk, true, ah, al);
 #pragma unroll
       for (int jt = 0; jt < 2; ++jt) {
         bf16x8 bh, bl;
-        frag_col(kb + (long)(k + fk) * 2 * XD + h * XDH + 16 * jt + fr, 2 * XD, k + fk, Ta, true, bh, bl);
+        frag_col(kb + (long)(k + fk) * 2 * XD + h * XDH + 16 * jt + fr, 2 * XD, k + fk, Ta, bh, bl);
         o[jt] = mma3(ah, al, bh, bl, o[jt]);
       }
     }
@@ -456,19 +568,20 @@ __global__ __launch_bounds__(256) void xh_v2a_bwd_kernel(
 #pragma unroll
       for (int r = 0; r < 4; ++r) dqL[(4 * fq + r) * LDA + h * XDH + 16 * jt + fr] = o[jt][r] * scale;
   }
+  XT(1, 6);
   {  // dK1_h = dS^T . q1_h * scale, dV1_h = P'^T . do1_h: rows = keys, contraction over the T query rows
     bf16x8 qh[2], ql[2], gh[2], gl[2];
 #pragma unroll
     for (int jt = 0; jt < 2; ++jt) {
-      frag_col(q1 + (row0 + fk) * XD + h * XDH + 16 * jt + fr, XD, fk, T, true, qh[jt], ql[jt]);
-      frag_col(oL + fk * LDA + h * XDH + 16 * jt + fr, LDA, fk, 16, true, gh[jt], gl[jt]);
+      frag_col(q1 + (row0 + fk) * XD + h * XDH + 16 * jt + fr, XD, fk, T, qh[jt], ql[jt]);
+      frag_col(oL + fk * LDA + h * XDH + 16 * jt + fr, LDA, fk, 16, gh[jt], gl[jt]);
     }
 #pragma unroll
     for (int t = 0; t < G2_KT; ++t) {
       if (16 * t >= Ta) break;
       bf16x8 sh, sl, ph, pl;
-      frag_col(dSt + (long)fk * G2_SLD + 16 * t + fr, G2_SLD, fk, 16, true, sh, sl);
-      frag_col(Pdt + (long)fk * G2_SLD + 16 * t + fr, G2_SLD, fk, 16, true, ph, pl);
+      frag_col(dSt + (long)fk * G2_SLD + 16 * t + fr, G2_SLD, fk, 16, sh, sl);
+      frag_col(Pdt + (long)fk * G2_SLD + 16 * t + fr, G2_SLD, fk, 16, ph, pl);
 #pragma unroll
       for (int jt = 0; jt < 2; ++jt) {
         const f32x4 dk = mma3(sh, sl, qh[jt], ql[jt], f32x4{0.f, 0.f, 0.f, 0.f});
@@ -486,56 +599,33 @@ __global__ __launch_bounds__(256) void xh_v2a_bwd_kernel(
     }
   }
   __syncthreads();
-  for (int e = threadIdx.x; e < T * XD; e += 256) dq1[row0 * XD + e] = dqL[(e / XD) * LDA + e % XD];
-  {  // dv = ds + dq1 . Wq1  (rows >= T of dqL are zero: dS is zero there)
-    f32x4 acc[1][2];
-    zero(acc);
-    mm_aw(acc, dqL, LDA, 16, XD, WqT1, XD, 32 * w);
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = 4 * fq + r, col = 32 * w + 16 * j + fr;
-        const float val = row < T ? acc[0][j][r] + t1[row * LDA + col] : 0.f;
-        oL[row * LDA + col] = val;
-        if (row < T) dv[(row0 + row) * XD + col] = val;
-      }
+  for (int e = threadIdx.x; e < T * XD; e += 256) {  // dq1 and the residual part of dv (G1 adds dq1 . Wq1)
+    const int r = e / XD, c = e - r * XD;
+    dq1[row0 * XD + e] = dqL[r * LDA + c];
+    dv[row0 * XD + e] = t1[r * LDA + c];
   }
-  __syncthreads();
-  if (dvfeat) {  // dv_feat = dv . Wv  (16-column tiles round-robin over the waves)
-    for (int c0 = 16 * w; c0 < vdim; c0 += 64) {
-      f32x4 acc[1][1];
-      zero(acc);
-      mm_aw(acc, oL, LDA, 16, XD, WvT, XD, c0);
-      store_acc(acc, c0, nullptr, nullptr, 0, dvfeat, vdim, row0, T);
-    }
-  }
+  XT(1, 7);
 }
 
 constexpr size_t G2_LDS_BYTES = sizeof(float) * (16 * G2_KVLD + 4 * 16 * LDA + XH * 2 * 16 * G2_SLD + 4 * 256);
 
-MER_API int mer_xh_v2a_bwd(int B, int T, int Ta, int vdim, const float* dkv2_part, const void* WkvT2_hi,
-                           const void* WkvT2_lo, const float* demb, const float* s_v, const float* mean_v,
-                           const float* rstd_v, const float* gamma, const void* WoT1_hi, const void* WoT1_lo,
-                           const float* P1, const float* kv1, const float* q1, const void* WqT1_hi, const void* WqT1_lo,
-                           const void* WvT_hi, const void* WvT_lo, float attn_p, float path_p,
-                           const unsigned long long* seed, unsigned long long site_attn, unsigned long long site_path,
-                           float scale, float* dkv2, float* dv2, float* dq1, float* dv, float* dvfeat, float* dqkv,
-                           float* ln_part, void* stream) {
+MER_API int mer_xh_v2a_bwd(int B, int T, int Ta, const float* dkv2_part, const void* WkvT2_hi, const void* WkvT2_lo,
+                           const float* demb, const float* s_v, const float* mean_v, const float* rstd_v,
+                           const float* gamma, const void* WoT1_hi, const void* WoT1_lo, const float* P1,
+                           const float* kv1, const float* q1, float attn_p, float path_p, const unsigned long long* seed,
+                           unsigned long long site_attn, unsigned long long site_path, float scale, float* dkv2,
+                           float* dv2, float* dq1, float* dv, float* dqkv, float* ln_part, void* stream) {
   if (B <= 0) return 0;
-  if (T <= 0 || T > 16 || Ta <= 0 || Ta > 16 * G2_KT || vdim <= 0 || vdim % 16 ||
-      ((attn_p > 0.f || path_p > 0.f) && !seed))
+  if (T <= 0 || T > 16 || Ta <= 0 || Ta > 16 * G2_KT || ((attn_p > 0.f || path_p > 0.f) && !seed))
     return (int)hipErrorInvalidValue;
   XhDrop dr{attn_p, path_p, seed, site_attn, site_path};
   if (hipFuncSetAttribute(reinterpret_cast<const void*>(&xh_v2a_bwd_kernel),
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)G2_LDS_BYTES) != hipSuccess)
     return (int)hipErrorInvalidConfiguration;
   hipLaunchKernelGGL(xh_v2a_bwd_kernel, dim3(B), dim3(256), G2_LDS_BYTES, (hipStream_t)stream, T, Ta, (Ta + 15) / 16,
-                     vdim, dkv2_part, SplitW{(const bf16_t*)WkvT2_hi, (const bf16_t*)WkvT2_lo}, demb, s_v, mean_v,
-                     rstd_v, gamma, SplitW{(const bf16_t*)WoT1_hi, (const bf16_t*)WoT1_lo}, P1, kv1, q1,
-                     SplitW{(const bf16_t*)WqT1_hi, (const bf16_t*)WqT1_lo},
-                     SplitW{(const bf16_t*)WvT_hi, (const bf16_t*)WvT_lo}, dr, scale, dkv2, dv2, dq1, dv, dvfeat, dqkv,
-                     ln_part);
+                     dkv2_part, SplitW{(const bf16_t*)WkvT2_hi, (const bf16_t*)WkvT2_lo}, demb, s_v, mean_v, rstd_v,
+                     gamma, SplitW{(const bf16_t*)WoT1_hi, (const bf16_t*)WoT1_lo}, P1, kv1, q1, dr, scale, dkv2, dv2,
+                     dq1, dv, dqkv, ln_part);
   MER_LAUNCH_CHECK();
 }
 
@@ -543,16 +633,33 @@ MER_API int mer_xh_v2a_bwd(int B, int T, int Ta, int vdim, const float* dkv2_par
 // G1: audio chain backward, 32 rows per block: da += [dq2 | dK1 dV1] . [Wq2 ; Wkv1], da_s = da . Wa
 // Unfused: the dx halves of xattn_head.py:251, 269 and 303-304.
 // ---------------------------------------------------------------------------------------------
+struct XhVideoBwd {  // G1's video rows: dv += dq1 Wq1 (in place), dvfeat = dv Wv (NULL: not wanted)
+  int M, vdim;
+  const float* dq1;
+  SplitW WqT1, WvT;
+  float* dv;
+  float* dvfeat;
+};
+
 __global__ __launch_bounds__(256) void xh_audio_bwd_kernel(int M, const float* __restrict__ dqkv, SplitW WcT,
-                                                           SplitW WaT, float* __restrict__ da, float* __restrict__ da_s) {
+                                                           SplitW WaT, float* __restrict__ da, float* __restrict__ da_s,
+                                                           XhVideoBwd vid) {
   __shared__ __attribute__((aligned(16))) float daL[32 * LDA];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, fr = lane & 15, fq = lane >> 4;
-  const long r0 = (long)blockIdx.x * 32;
-  const int rmax = (int)(M - r0 < 32 ? M - r0 : 32);
-  {
+  const int na = (M + 31) / 32;
+  const bool video = (int)blockIdx.x >= na;
+  const long r0 = video ? (long)(blockIdx.x - na) * 32 : (long)blockIdx.x * 32;
+  const int rows = video ? vid.M : M;
+  const int rmax = (int)(rows - r0 < 32 ? rows - r0 : 32);
+  float* dst = video ? vid.dv : da;
+  {  // audio: da += [dq2 | dK1 dV1] . [Wq2 ; Wkv1];  video: dv += dq1 . Wq1
     f32x4 acc[2][2];
     zero(acc);
-    mm_aw(acc, dqkv + r0 * 3 * XD, 3 * XD, rmax, 3 * XD, WcT, 3 * XD, 32 * w);
+    if (video)
+      mm_aw(acc, vid.dq1 + r0 * XD, XD, rmax, XD, vid.WqT1, XD, 32 * w);
+    else
+      mm_aw(acc, dqkv + r0 * 3 * XD, 3 * XD, rmax, 3 * XD, WcT, 3 * XD, 32 * w);
+    float res[2][2][4];  // all residual loads first: the in-place stores below may alias them
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
@@ -560,27 +667,47 @@ __global__ __launch_bounds__(256) void xh_audio_bwd_kernel(int M, const float* _
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int row = 16 * i + 4 * fq + r, col = 32 * w + 16 * j + fr;
-          float v = 0.f;
-          if (row < rmax) {
-            v = acc[i][j][r] + da[(r0 + row) * XD + col];
-            da[(r0 + row) * XD + col] = v;
-          }
+          res[j][i][r] = dst[(r0 + (row < rmax ? row : rmax - 1)) * XD + col];
+        }
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = 16 * i + 4 * fq + r, col = 32 * w + 16 * j + fr;
+          const float v = row < rmax ? acc[i][j][r] + res[j][i][r] : 0.f;
+          if (row < rmax) dst[(r0 + row) * XD + col] = v;
           daL[row * LDA + col] = v;
         }
   }
   __syncthreads();
-  f32x4 acc[2][2];
-  zero(acc);
-  mm_aw(acc, daL, LDA, 32, XD, WaT, XD, 32 * w);
-  store_acc(acc, 32 * w, nullptr, nullptr, 0, da_s, XD, r0, rmax);
+  if (!video) {  // da_s = da . Wa
+    f32x4 acc[2][2];
+    zero(acc);
+    mm_aw(acc, daL, LDA, 32, XD, WaT, XD, 32 * w);
+    store_acc(acc, 32 * w, nullptr, nullptr, 0, da_s, XD, r0, rmax);
+  } else if (vid.dvfeat) {  // dv_feat = dv . Wv, 32-column passes per wave
+    for (int c0 = 32 * w; c0 < vid.vdim; c0 += 128) {
+      f32x4 acc[2][2];
+      zero(acc);
+      mm_aw(acc, daL, LDA, 32, XD, vid.WvT, XD, c0);
+      store_acc(acc, c0, nullptr, nullptr, 0, vid.dvfeat, vid.vdim, r0, rmax);
+    }
+  }
 }
 
 MER_API int mer_xh_audio_bwd(int M, const float* dqkv, const void* WcT_hi, const void* WcT_lo, const void* WaT_hi,
-                             const void* WaT_lo, float* da, float* da_s, void* stream) {
-  if (M <= 0) return 0;
-  hipLaunchKernelGGL(xh_audio_bwd_kernel, dim3((M + 31) / 32), dim3(256), 0, (hipStream_t)stream, M, dqkv,
-                     SplitW{(const bf16_t*)WcT_hi, (const bf16_t*)WcT_lo},
-                     SplitW{(const bf16_t*)WaT_hi, (const bf16_t*)WaT_lo}, da, da_s);
+                             const void* WaT_lo, float* da, float* da_s, int Mv, int vdim, const float* dq1,
+                             const void* WqT1_hi, const void* WqT1_lo, const void* WvT_hi, const void* WvT_lo, float* dv,
+                             float* dvfeat, void* stream) {
+  if (M <= 0 || Mv < 0 || (Mv > 0 && (!dq1 || !dv || (dvfeat && (vdim <= 0 || vdim % 32)))))
+    return (int)hipErrorInvalidValue;
+  const XhVideoBwd vid{Mv, vdim, dq1, SplitW{(const bf16_t*)WqT1_hi, (const bf16_t*)WqT1_lo},
+                       SplitW{(const bf16_t*)WvT_hi, (const bf16_t*)WvT_lo}, dv, dvfeat};
+  hipLaunchKernelGGL(xh_audio_bwd_kernel, dim3((M + 31) / 32 + (Mv + 31) / 32), dim3(256), 0, (hipStream_t)stream, M,
+                     dqkv, SplitW{(const bf16_t*)WcT_hi, (const bf16_t*)WcT_lo},
+                     SplitW{(const bf16_t*)WaT_hi, (const bf16_t*)WaT_lo}, da, da_s, vid);
   MER_LAUNCH_CHECK();
 }
 
@@ -592,7 +719,6 @@ MER_API int mer_xh_audio_bwd(int M, const float* dqkv, const void* WcT_hi, const
 // captured graph holds it (no device table to upload).
 // ---------------------------------------------------------------------------------------------
 constexpr int WG_MAXP = 16;
-constexpr int WG_LD = 64 + 4;
 constexpr int WG_HOST_COLS = 11;  // dY ldy X ldx x_dtype M N K splits dW db
 
 struct WgProb {
@@ -609,9 +735,43 @@ struct WgTab {
   int nprob;
 };
 
+// Staging: thread t owns column (t & 63) of the 64-wide dY / X tile and 8 consecutive rows (t >> 6) * 8 .. + 7 of
+// the 32-row chunk: 8 wave-coalesced loads each, split into bf16 hi / lo once and stored as ONE 16-byte LDS
+// vector per plane in [column][row] layout, which is exactly the MFMA fragment (8 consecutive m of one n / k).
+// The next chunk's loads are issued before the current chunk's MFMAs.
+constexpr int WG_LDM = 32 + 8;  // bf16 row stride of the [64][32] planes (80 bytes: 16-byte aligned)
+
+struct WgChunk {
+  float y[8], x[8];
+};
+
+__device__ __forceinline__ void wg_load(const WgProb& d, long mc, long m1, int n0, int k0, WgChunk& c) {
+  // Branch-free (see mm_aw): unconditional loads from clamped addresses (row m1 - 1, column N - 1 / K - 1),
+  // zeroed by selects; X is read as 32-bit words whatever its dtype (a bf16 element is one half of its word),
+  // and a K = 0 problem reads a valid dummy X (the host points X at dY).
+  const int col = threadIdx.x & 63, m8 = (threadIdx.x >> 6) * 8;
+  const bool okn = n0 + col < d.N, okk = k0 + col < d.K;
+  const int nc = okn ? n0 + col : d.N - 1, kc = okk ? k0 + col : (d.K > 0 ? d.K - 1 : 0);
+  const int esz = d.xbf ? 2 : 4;
+  const char* Xb = reinterpret_cast<const char*>(d.X);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const long m = mc + m8 + e;
+    const bool okm = m < m1;
+    const long mm = okm ? m : m1 - 1;
+    const float y = d.dY[mm * d.ldy + nc];
+    const long ie = mm * d.ldx + kc;
+    const uintptr_t addr = reinterpret_cast<uintptr_t>(Xb + ie * esz);
+    const uint32_t wv = *reinterpret_cast<const uint32_t*>(addr & ~(uintptr_t)3);
+    const uint32_t bits = d.xbf ? ((addr & 2) ? (wv & 0xffff0000u) : (wv << 16)) : wv;
+    c.y[e] = (okm && okn) ? y : 0.f;
+    c.x[e] = (okm && okk) ? __uint_as_float(bits) : 0.f;
+  }
+}
+
 __global__ __launch_bounds__(256) void xh_wgrad_kernel(const WgTab tab, float* __restrict__ ws) {
-  __shared__ __attribute__((aligned(16))) float yT[32 * WG_LD];
-  __shared__ __attribute__((aligned(16))) float xT[32 * WG_LD];
+  __shared__ __attribute__((aligned(16))) bf16_t yh[64 * WG_LDM], yl[64 * WG_LDM], xh_[64 * WG_LDM], xl[64 * WG_LDM];
+  __shared__ float bred[4][64];
   int pi = 0;
   while (pi + 1 < tab.nprob && tab.p[pi + 1].first_block <= (int)blockIdx.x) ++pi;
   const WgProb& d = tab.p[pi];
@@ -622,36 +782,53 @@ __global__ __launch_bounds__(256) void xh_wgrad_kernel(const WgTab tab, float* _
   const int tn = tile / ntk, tk = tile - tn * ntk;
   const int n0 = tn * 64, k0 = tk * 64;
   const long per = (d.M + splits - 1) / splits, m0 = split * per, m1 = m0 + per < d.M ? m0 + per : d.M;
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, fr = lane & 15, fq = lane >> 4, fk = fq * 8;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, fr = lane & 15, fk = (lane >> 4) * 8;
+  const int col = lane, m8 = w * 8;
   const bool bias = d.db != nullptr && tk == 0;
   f32x4 acc[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float bsum = 0.f;  // threads 0..63: column n0 + t of dY summed over the block's rows
+  float bsum = 0.f;  // column n0 + col, this thread's rows
+  WgChunk cur;
+  wg_load(d, m0, m1, n0, k0, cur);
   for (long mc = m0; mc < m1; mc += 32) {
-    __syncthreads();
-    for (int e = threadIdx.x; e < 32 * 64; e += 256) {
-      const int r = e >> 6, c = e & 63;
-      const long m = mc + r;
-      const bool okm = m < m1;
-      yT[r * WG_LD + c] = (okm && n0 + c < N) ? d.dY[m * d.ldy + n0 + c] : 0.f;
-      float xv = 0.f;
-      if (okm && k0 + c < K)
-        xv = d.xbf ? bf2f(reinterpret_cast<const bf16_t*>(d.X)[m * d.ldx + k0 + c])
-                   : reinterpret_cast<const float*>(d.X)[m * d.ldx + k0 + c];
-      xT[r * WG_LD + c] = xv;
+    __syncthreads();  // the previous chunk's fragments are read
+    {
+      Frag H, L;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        bsum += cur.y[e];
+        const uint16_t hb = f2bf(cur.y[e]);
+        H.h[e] = hb;
+        L.h[e] = f2bf(cur.y[e] - bf2f(hb));
+      }
+      *reinterpret_cast<u4*>(yh + col * WG_LDM + m8) = H.u;
+      *reinterpret_cast<u4*>(yl + col * WG_LDM + m8) = L.u;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const uint16_t hb = f2bf(cur.x[e]);
+        H.h[e] = hb;
+        L.h[e] = f2bf(cur.x[e] - bf2f(hb));
+      }
+      *reinterpret_cast<u4*>(xh_ + col * WG_LDM + m8) = H.u;
+      *reinterpret_cast<u4*>(xl + col * WG_LDM + m8) = L.u;
     }
     __syncthreads();
-    if (bias && threadIdx.x < 64)
-      for (int r = 0; r < 32; ++r) bsum += yT[r * WG_LD + threadIdx.x];
-    if (K > 0) {
-      bf16x8 ah, al;
-      frag_col(yT + fk * WG_LD + 16 * w + fr, WG_LD, 0, 32, true, ah, al);  // A[n][m] = dY[m][n]
+    // the next chunk's loads are in flight during the MFMAs (unconditional: past the end it re-reads the last
+    // chunk, unused); the MFMAs also run for K = 0 problems (their accumulators are never stored)
+    wg_load(d, mc + 32 < m1 ? mc + 32 : mc, m1, n0, k0, cur);
+    {
+      Frag AH, AL;
+      AH.u = *reinterpret_cast<const u4*>(yh + (16 * w + fr) * WG_LDM + fk);  // A[n][m] = dY[m][n]
+      AL.u = *reinterpret_cast<const u4*>(yl + (16 * w + fr) * WG_LDM + fk);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        bf16x8 bh, bl;
-        frag_col(xT + fk * WG_LD + 16 * j + fr, WG_LD, 0, 32, true, bh, bl);  // B[k][m] = X[m][k]
-        acc[j] = d.xbf ? mma(al, bh, mma(ah, bh, acc[j])) : mma3(ah, al, bh, bl, acc[j]);
+        Frag BH, BL;  // B[k][m] = X[m][k]; the lo plane of bf16 X is zero
+        BH.u = *reinterpret_cast<const u4*>(xh_ + (16 * j + fr) * WG_LDM + fk);
+        BL.u = *reinterpret_cast<const u4*>(xl + (16 * j + fr) * WG_LDM + fk);
+        acc[j] = mma(AH.v, BH.v, acc[j]);
+        acc[j] = mma(AL.v, BH.v, acc[j]);
+        acc[j] = mma(AH.v, BL.v, acc[j]);
       }
     }
   }
@@ -661,26 +838,42 @@ __global__ __launch_bounds__(256) void xh_wgrad_kernel(const WgTab tab, float* _
     for (int j = 0; j < 4; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int n = n0 + 16 * w + 4 * fq + r, k = k0 + 16 * j + fr;
+        const int n = n0 + 16 * w + 4 * (lane >> 4) + r, k = k0 + 16 * j + fr;
         if (n < N && k < K) out[(long)n * K + k] = acc[j][r];
       }
   }
-  if (bias && threadIdx.x < 64 && n0 + (int)threadIdx.x < N) ws[d.ws_b_off + (long)split * N + n0 + threadIdx.x] = bsum;
+  if (bias) {
+    bred[w][col] = bsum;
+    __syncthreads();
+    if (threadIdx.x < 64 && n0 + (int)threadIdx.x < N)
+      ws[d.ws_b_off + (long)split * N + n0 + threadIdx.x] =
+          ((bred[0][threadIdx.x] + bred[1][threadIdx.x]) + bred[2][threadIdx.x]) + bred[3][threadIdx.x];
+  }
 }
 
 __global__ __launch_bounds__(256) void xh_wfold_kernel(const WgTab tab, const float* __restrict__ ws) {
   const WgProb& d = tab.p[blockIdx.y];
   const long nk = (long)d.N * d.K, tot = nk + (d.db ? d.N : 0);
   for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < tot; e += (long)gridDim.x * blockDim.x) {
+    // partials in split order, loaded 8 at a time (the sum order stays fixed)
+    const bool wpart = e < nk;
+    const float* src = wpart ? ws + d.ws_off + e : ws + d.ws_b_off + (e - nk);
+    const long stride = wpart ? nk : (long)d.N;
     float s = 0.f;
-    if (e < nk) {
-      for (int q = 0; q < d.splits; ++q) s += ws[d.ws_off + q * nk + e];
-      d.dW[e] += s;
-    } else {
-      const long n = e - nk;
-      for (int q = 0; q < d.splits; ++q) s += ws[d.ws_b_off + (long)q * d.N + n];
-      d.db[n] += s;
+    for (int q0 = 0; q0 < d.splits; q0 += 8) {
+      float v[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float x = src[(long)(q0 + q < d.splits ? q0 + q : d.splits - 1) * stride];
+        v[q] = q0 + q < d.splits ? x : 0.f;
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q) s += v[q];
     }
+    if (wpart)
+      d.dW[e] += s;
+    else
+      d.db[e - nk] += s;
   }
 }
 
@@ -704,6 +897,11 @@ static long long wg_layout(int nprob, const long long* t, WgTab* tab, int* block
     p.dW = reinterpret_cast<float*>(r[9]);
     p.db = reinterpret_cast<float*>(r[10]);
     p.pad = 0;
+    if (p.K == 0) {  // column sums only: the loader still reads a (valid) X word
+      p.X = p.dY;
+      p.ldx = 0;
+      p.xbf = 0;
+    }
     if (p.M <= 0 || p.N <= 0 || p.K < 0 || p.splits <= 0 || p.splits > p.M || !p.dY ||
         (p.K > 0 && (!p.X || !p.dW)) || (p.K == 0 && !p.db))
       return -1;
@@ -718,6 +916,13 @@ static long long wg_layout(int nprob, const long long* t, WgTab* tab, int* block
   *blocks = fb;
   return off;
 }
+
+#ifdef MER_XH_TIMING
+MER_API int mer_xt_read_bwd(long long* host) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(mer_xt_buf), sizeof(long long) * 4 * 512 * 16, 0,
+                                  hipMemcpyDeviceToHost);
+}
+#endif
 
 MER_API int mer_xh_wgrad_ws_floats(int nprob, const long long* table, long long* out) {
   if (nprob <= 0 || nprob > WG_MAXP || !out) return (int)hipErrorInvalidValue;
@@ -737,6 +942,6 @@ MER_API int mer_xh_wgrad(int nprob, const long long* table, float* ws, long long
   const long long need = wg_layout(nprob, table, &tab, &blocks);
   if (need < 0 || need > ws_floats) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(xh_wgrad_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, tab, ws);
-  hipLaunchKernelGGL(xh_wfold_kernel, dim3(32, nprob), dim3(256), 0, (hipStream_t)stream, tab, ws);
+  hipLaunchKernelGGL(xh_wfold_kernel, dim3(64, nprob), dim3(256), 0, (hipStream_t)stream, tab, ws);
   MER_LAUNCH_CHECK();
 }

@@ -834,29 +834,29 @@ def _f32c(*ts):
             raise ValueError("fused head: contiguous fp32 device tensors expected")
 
 
-def xh_audio_fwd(af, Ws, bs, Wa, ba, Wc, bq2, bkv1, a_s, a, q2, kv1):
+def xh_audio_fwd(af, Ws, bs, Wa, ba, Wc, bq2, bkv1, a_s, a, q2, kv1, vf, Wv, bv, Wq1, bq1, v, q1):
     M, S = af.shape
-    if af.stride(1) != 1 or Ws[0].shape != (128, S) or Wc[0].shape != (384, 128):
+    Mv, vdim = vf.shape
+    if af.stride(1) != 1 or Ws[0].shape != (128, S) or Wc[0].shape != (384, 128) or Wv[0].shape != (128, vdim) \
+            or tuple(v.shape) != (Mv, 128) or tuple(q1.shape) != (Mv, 128):
         raise ValueError("xh_audio_fwd shapes")
-    _f32c(a_s, a, q2, kv1)
+    _f32c(a_s, a, q2, kv1, vf, v, q1)
     _launch("xh_audio_fwd", (M, S), "mer_xh_audio_fwd", M, S, af.data_ptr(), _dt(af), af.stride(0), *_planes(Ws),
-            bs.data_ptr(),
-            *_planes(Wa), ba.data_ptr(), *_planes(Wc), bq2.data_ptr(), bkv1.data_ptr(), a_s.data_ptr(), a.data_ptr(),
-            q2.data_ptr(), kv1.data_ptr(), stream_ptr())
+            bs.data_ptr(), *_planes(Wa), ba.data_ptr(), *_planes(Wc), bq2.data_ptr(), bkv1.data_ptr(), a_s.data_ptr(),
+            a.data_ptr(), q2.data_ptr(), kv1.data_ptr(), Mv, vdim, vf.data_ptr(), *_planes(Wv), bv.data_ptr(),
+            *_planes(Wq1), bq1.data_ptr(), v.data_ptr(), q1.data_ptr(), stream_ptr())
 
 
-def xh_v2a_fwd(B, T, Ta, vf, Wv, bv, Wq1, bq1, kv1, Wo1, bo1, gamma, beta, Wkv2, bkv2, attn_p, path_p, rng, site_attn,
-               site_path, scale, v, q1, P1, o1, s_v, mu_v, rs_v, v1, kv2, emb):
-    vdim = vf.shape[1]
-    if tuple(vf.shape) != (B * T, vdim) or Wv[0].shape != (128, vdim) or tuple(kv1.shape) != (B * Ta, 256):
+def xh_v2a_fwd(B, T, Ta, v, q1, kv1, Wo1, bo1, gamma, beta, Wkv2, bkv2, attn_p, path_p, rng, site_attn, site_path,
+               scale, P1, o1, s_v, mu_v, rs_v, v1, kv2, emb):
+    if tuple(v.shape) != (B * T, 128) or tuple(q1.shape) != (B * T, 128) or tuple(kv1.shape) != (B * Ta, 256):
         raise ValueError("xh_v2a_fwd shapes")
-    _f32c(vf, kv1, v, q1, P1, o1, s_v, mu_v, rs_v, v1, kv2, emb)
-    _launch("xh_v2a_fwd", (B, T, Ta), "mer_xh_v2a_fwd", B, T, Ta, vdim, vf.data_ptr(), *_planes(Wv), bv.data_ptr(),
-            *_planes(Wq1), bq1.data_ptr(), kv1.data_ptr(), *_planes(Wo1), bo1.data_ptr(), gamma.data_ptr(),
-            beta.data_ptr(), *_planes(Wkv2), bkv2.data_ptr(), float(attn_p), float(path_p), rng_ptr(rng),
-            int(site_attn), int(site_path), float(scale), v.data_ptr(), q1.data_ptr(), P1.data_ptr(), o1.data_ptr(),
-            s_v.data_ptr(), mu_v.data_ptr(), rs_v.data_ptr(), v1.data_ptr(), kv2.data_ptr(), emb.data_ptr(),
-            emb.stride(0), stream_ptr())
+    _f32c(v, q1, kv1, P1, o1, s_v, mu_v, rs_v, v1, kv2, emb)
+    _launch("xh_v2a_fwd", (B, T, Ta), "mer_xh_v2a_fwd", B, T, Ta, v.data_ptr(), q1.data_ptr(), kv1.data_ptr(),
+            *_planes(Wo1), bo1.data_ptr(), gamma.data_ptr(), beta.data_ptr(), *_planes(Wkv2), bkv2.data_ptr(),
+            float(attn_p), float(path_p), rng_ptr(rng), int(site_attn), int(site_path), float(scale), P1.data_ptr(),
+            o1.data_ptr(), s_v.data_ptr(), mu_v.data_ptr(), rs_v.data_ptr(), v1.data_ptr(), kv2.data_ptr(),
+            emb.data_ptr(), emb.stride(0), stream_ptr())
 
 
 def xh_a2v_fwd(B, T, Ta, q2, kv2, a, Wo2, bo2, gamma, beta, attn_p, path_p, rng, site_attn, site_path, scale, P2, o2,
@@ -907,30 +907,33 @@ def xh_a2v_bwd(B, T, Ta, demb, s_a, mu_a, rs_a, gamma, P2, kv2, q2, WoT2, attn_p
             ln_part.data_ptr(), stream_ptr())
 
 
-def xh_v2a_bwd(B, T, Ta, dkv2_part, WkvT2, demb, s_v, mu_v, rs_v, gamma, WoT1, P1, kv1, q1, WqT1, WvT, attn_p, path_p,
-               rng, site_attn, site_path, scale, dkv2, dv2, dq1, dv, dvfeat, dqkv, ln_part):
-    vdim = WvT[0].shape[0]
+def xh_v2a_bwd(B, T, Ta, dkv2_part, WkvT2, demb, s_v, mu_v, rs_v, gamma, WoT1, P1, kv1, q1, attn_p, path_p, rng,
+               site_attn, site_path, scale, dkv2, dv2, dq1, dv, dqkv, ln_part):
     if tuple(kv1.shape) != (B * Ta, 256) or tuple(q1.shape) != (B * T, 128) or tuple(dkv2.shape) != (B * T, 256) \
-            or WkvT2[0].shape != (128, 256) or WvT[0].shape != (vdim, 128) or ln_part.numel() != B * 256 \
-            or (dvfeat is not None and tuple(dvfeat.shape) != (B * T, vdim)):
+            or WkvT2[0].shape != (128, 256) or ln_part.numel() != B * 256 or tuple(dv.shape) != (B * T, 128) \
+            or dkv2_part.numel() != B * ((Ta + 15) // 16) * 16 * 256:
         raise ValueError("xh_v2a_bwd shapes")
-    _f32c(dkv2_part, demb, s_v, mu_v, rs_v, gamma, P1, kv1, q1, dkv2, dv2, dq1, dv, dvfeat, dqkv, ln_part)
-    _launch("xh_v2a_bwd", (B, T, Ta), "mer_xh_v2a_bwd", B, T, Ta, vdim, dkv2_part.data_ptr(), *_planes(WkvT2),
+    _f32c(dkv2_part, demb, s_v, mu_v, rs_v, gamma, P1, kv1, q1, dkv2, dv2, dq1, dv, dqkv, ln_part)
+    _launch("xh_v2a_bwd", (B, T, Ta), "mer_xh_v2a_bwd", B, T, Ta, dkv2_part.data_ptr(), *_planes(WkvT2),
             demb.data_ptr(), s_v.data_ptr(), mu_v.data_ptr(), rs_v.data_ptr(), gamma.data_ptr(), *_planes(WoT1),
-            P1.data_ptr(), kv1.data_ptr(), q1.data_ptr(), *_planes(WqT1), *_planes(WvT), float(attn_p), float(path_p),
+            P1.data_ptr(), kv1.data_ptr(), q1.data_ptr(), float(attn_p), float(path_p),
             rng_ptr(rng) if (attn_p > 0 or path_p > 0) else 0, int(site_attn), int(site_path), float(scale),
-            dkv2.data_ptr(), dv2.data_ptr(), dq1.data_ptr(), dv.data_ptr(), _ptr(dvfeat), dqkv.data_ptr(),
-            ln_part.data_ptr(), stream_ptr())
+            dkv2.data_ptr(), dv2.data_ptr(), dq1.data_ptr(), dv.data_ptr(), dqkv.data_ptr(), ln_part.data_ptr(),
+            stream_ptr())
 
 
-def xh_audio_bwd(dqkv, WcT, WaT, da, da_s):
-    M = dqkv.shape[0]
+def xh_audio_bwd(dqkv, WcT, WaT, da, da_s, dq1, WqT1, WvT, dv, dvfeat):
+    M, Mv = dqkv.shape[0], dq1.shape[0]
+    vdim = WvT[0].shape[0]
     if tuple(dqkv.shape) != (M, 384) or WcT[0].shape != (128, 384) or WaT[0].shape != (128, 128) \
-            or tuple(da.shape) != (M, 128) or tuple(da_s.shape) != (M, 128):
+            or tuple(da.shape) != (M, 128) or tuple(da_s.shape) != (M, 128) or tuple(dq1.shape) != (Mv, 128) \
+            or tuple(dv.shape) != (Mv, 128) or WqT1[0].shape != (128, 128) or WvT[0].shape != (vdim, 128) \
+            or (dvfeat is not None and tuple(dvfeat.shape) != (Mv, vdim)):
         raise ValueError("xh_audio_bwd shapes")
-    _f32c(dqkv, da, da_s)
+    _f32c(dqkv, da, da_s, dq1, dv, dvfeat)
     _launch("xh_audio_bwd", (M,), "mer_xh_audio_bwd", M, dqkv.data_ptr(), *_planes(WcT), *_planes(WaT), da.data_ptr(),
-            da_s.data_ptr(), stream_ptr())
+            da_s.data_ptr(), Mv, vdim, dq1.data_ptr(), *_planes(WqT1), *_planes(WvT), dv.data_ptr(), _ptr(dvfeat),
+            stream_ptr())
 
 
 class WGradTable:

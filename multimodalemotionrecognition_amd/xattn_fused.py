@@ -19,7 +19,7 @@ from . import kernels as K
 
 ENABLED = os.environ.get("MER_XATTN_FUSED", "1") != "0"
 BWD_ENABLED = os.environ.get("MER_XATTN_FUSED_BWD", "1") != "0"
-WGRAD_TARGET_BLOCKS = 96  # workgroups per weight-gradient problem (row splits = this / output tiles)
+WGRAD_ROWS = 256  # rows of dY / X per weight-gradient workgroup (the rest of M is split over the grid)
 
 # (weight name, row slice) for each split plane; rows are contiguous slices of the reference's parameters
 _PLANES = {
@@ -108,13 +108,21 @@ class SplitPlanes:
             self.planes[key] = (hi, lo)
         self.desc = torch.tensor(rows, dtype=torch.int64).to(dev)
         self.desc_t = torch.tensor(trows, dtype=torch.int64).to(dev)
+        self.desc_both = torch.tensor(rows + trows, dtype=torch.int64).to(dev)
         self.key = tuple(r[0] for r in rows)
+        self.gen = 0  # forward refreshes so far (host-side; frozen into a captured graph like the launches)
+        self.t_gen = -1  # the refresh that last wrote the transposed planes
 
-    def refresh(self):
-        K.xh_split(self.desc)
+    def refresh(self, transposed: bool = False):
+        """One launch: the forward planes, plus the backward's transposed planes when a backward will follow."""
+        self.gen += 1
+        K.xh_split(self.desc_both if transposed else self.desc)
+        if transposed:
+            self.t_gen = self.gen
 
     def refresh_transposed(self):
         K.xh_split(self.desc_t)
+        self.t_gen = self.gen
 
     def __getitem__(self, key):
         return self.planes[key]
@@ -151,21 +159,22 @@ def fused_forward(p, cfg, v_feat, a_seq, training, rng, ctx, sites):
     if training and (dp_attn > 0 or dp_path > 0 or dp_mlp > 0) and seed is None:
         raise ValueError("train-mode dropout needs the step's RNG base")
     sp = planes_for(p)
-    sp.refresh()
+    sp.refresh(transposed=training)  # a training forward is followed by the fused backward
+    ctx.planes_gen = sp.gen
     vf = v_feat.reshape(B * T, vd).contiguous()
     af = a_seq.reshape(B * Ta, sd).contiguous()
     a_s, a, q2, kv1 = e(B * Ta, d), e(B * Ta, d), e(B * Ta, d), e(B * Ta, 2 * d)
-    K.xh_audio_fwd(af, sp["Ws"], p["audio_seq_proj.bias"], sp["Wa"], p["a_in_proj.bias"], sp["Wc"],
-                   p["a2v_attn.in_proj_bias"][:d], p["v2a_attn.in_proj_bias"][d:], a_s, a, q2, kv1)
     v, q1, o1 = e(B * T, d), e(B * T, d), e(B * T, d)
+    K.xh_audio_fwd(af, sp["Ws"], p["audio_seq_proj.bias"], sp["Wa"], p["a_in_proj.bias"], sp["Wc"],
+                   p["a2v_attn.in_proj_bias"][:d], p["v2a_attn.in_proj_bias"][d:], a_s, a, q2, kv1, vf, sp["Wv"],
+                   p["v_in_proj.bias"], sp["Wq1"], p["v2a_attn.in_proj_bias"][:d], v, q1)
     P1 = e(B, H, T, Ta)
     s_v, mu_v, rs_v, v1, kv2 = e(B * T, d), e(B * T), e(B * T), e(B * T, d), e(B * T, 2 * d)
     emb = e(B, 2 * d)
     scale = (d // H) ** -0.5
-    K.xh_v2a_fwd(B, T, Ta, vf, sp["Wv"], p["v_in_proj.bias"], sp["Wq1"], p["v2a_attn.in_proj_bias"][:d], kv1,
-                 sp["Wo1"], p["v2a_attn.out_proj.bias"], p["v_norm.weight"], p["v_norm.bias"], sp["Wkv2"],
-                 p["a2v_attn.in_proj_bias"][d:], dp_attn, dp_path, seed, site_v2a, site_vpath, scale, v, q1, P1, o1,
-                 s_v, mu_v, rs_v, v1, kv2, emb)
+    K.xh_v2a_fwd(B, T, Ta, v, q1, kv1, sp["Wo1"], p["v2a_attn.out_proj.bias"], p["v_norm.weight"], p["v_norm.bias"],
+                 sp["Wkv2"], p["a2v_attn.in_proj_bias"][d:], dp_attn, dp_path, seed, site_v2a, site_vpath, scale, P1,
+                 o1, s_v, mu_v, rs_v, v1, kv2, emb)
     o2, P2 = e(B * Ta, d), e(B, H, Ta, T)
     s_a, mu_a, rs_a = e(B * Ta, d), e(B * Ta), e(B * Ta)
     part = e(B, (Ta + 15) // 16, d)
@@ -200,14 +209,14 @@ def backward_supported(ctx, p, need_da_seq: bool) -> bool:
     (stage 2 -- which the fused forward already excludes)."""
     if not BWD_ENABLED or not getattr(ctx, "fused", False) or need_da_seq:
         return False
+    n0 = "xattn_mlp.0.weight" if ctx.cfg.xattn_head == "concat" else "xattn_gate.0.weight"
     C = (p["xattn_mlp.3.weight"] if ctx.cfg.xattn_head == "concat" else p["xattn_classifier.weight"]).shape[0]
-    return C <= 256
+    return C <= 32 and p[n0].shape[0] <= 256  # mer_xh_mlp_bwd's LDS staging bounds
 
 
-def _splits(M: int, N: int, K: int, target: int = WGRAD_TARGET_BLOCKS) -> int:
-    """Row splits of one weight-gradient problem: about ``target`` workgroups each, at least 64 rows per split."""
-    tiles = -(-N // 64) * (-(-K // 64) if K else 1)
-    return max(1, min(-(-target // tiles), M // 64))
+def _splits(M: int) -> int:
+    """Row splits of one weight-gradient problem: WGRAD_ROWS rows (WGRAD_ROWS / 32 pipelined chunks) per workgroup."""
+    return max(1, min(-(-M // WGRAD_ROWS), 64))
 
 
 def fused_backward(p, ctx, dlogits, grads, need_dv_feat=True):
@@ -223,7 +232,8 @@ def fused_backward(p, ctx, dlogits, grads, need_dv_feat=True):
     e = lambda *shape: torch.empty(shape, device=dev, dtype=f32)  # noqa: E731
     from .xattn_head import SITE_A2V, SITE_APATH, SITE_MLP, SITE_V2A, SITE_VPATH
     sp = planes_for(p)
-    sp.refresh_transposed()
+    if sp.t_gen != getattr(ctx, "planes_gen", None):  # the forward did not split them (eval-mode forward)
+        sp.refresh_transposed()
     dlogits = dlogits.contiguous()
     demb = e(B, 2 * d)
     if cfg.xattn_head == "concat":
@@ -247,10 +257,10 @@ def fused_backward(p, ctx, dlogits, grads, need_dv_feat=True):
     dvfeat = e(B * T, vf.shape[1]) if need_dv_feat else None
     lnp_v = e(B, 2 * d)
     K.xh_v2a_bwd(B, T, Ta, dkv2_part, sp["WkvT2"], demb, sv["s_v"], sv["mu_v"], sv["rs_v"], p["v_norm.weight"],
-                 sp["WoT1"], sv["P1"], sv["kv1"], sv["q1"], sp["WqT1"], sp["WvT"], dp_attn, dp_path, rng, SITE_V2A,
-                 SITE_VPATH, scale, dkv2, dv2, dq1, dv, dvfeat, dqkv, lnp_v)
+                 sp["WoT1"], sv["P1"], sv["kv1"], sv["q1"], dp_attn, dp_path, rng, SITE_V2A, SITE_VPATH, scale, dkv2,
+                 dv2, dq1, dv, dqkv, lnp_v)
     da_s = e(B * Ta, d)
-    K.xh_audio_bwd(dqkv, sp["WcT"], sp["WaT"], da, da_s)
+    K.xh_audio_bwd(dqkv, sp["WcT"], sp["WaT"], da, da_s, dq1, sp["WqT1"], sp["WvT"], dv, dvfeat)
     gw1, gb1 = grads["v2a_attn.in_proj_weight"], grads["v2a_attn.in_proj_bias"]
     gw2, gb2 = grads["a2v_attn.in_proj_weight"], grads["a2v_attn.in_proj_bias"]
     Ma, Mv, af = B * Ta, B * T, sv["af"]
@@ -268,7 +278,7 @@ def fused_backward(p, ctx, dlogits, grads, need_dv_feat=True):
                           (lnp_a[:, d:], None, None, grads["a_norm.bias"]),
                           (lnp_v[:, :d], None, None, grads["v_norm.weight"]),
                           (lnp_v[:, d:], None, None, grads["v_norm.bias"])):
-        W.add(dY, X, dW, db, _splits(dY.shape[0], dY.shape[1], 0 if X is None else X.shape[1]))
+        W.add(dY, X, dW, db, _splits(dY.shape[0]))
     ws = e(W.ws_floats())
     W.run(ws)
     return dvfeat.view(B, T, -1) if dvfeat is not None else None
