@@ -35,6 +35,7 @@ import torch.distributed as dist
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
+from multimodalemotionrecognition_amd import fusion as F  # noqa: E402
 from multimodalemotionrecognition_amd import kernels as K  # noqa: E402
 from multimodalemotionrecognition_amd.dist import GradAllReduce, init_distributed, is_dist  # noqa: E402
 from multimodalemotionrecognition_amd.train import (TrainStep, apply_two_stage_freeze_policy,  # noqa: E402
@@ -56,6 +57,17 @@ PMC_FILE = ROOT / "profiles" / "pmc_traffic.json"
 # (projections 0.703 + FFN 1.406 + attention 0.068; LayerDrop skips ~1.1 of 12 in train mode).
 STEP_GFLOP_PER_CLIP_FIXED = 22.8 + 0.141 + 14.72 + 1.42 + 0.12
 WAVLM_LAYER_GFLOP_PER_CLIP = 0.703 + 1.406 + 0.068
+# the fused xattn head's arithmetic (csrc/xattn_fused*.hip): fp32-class products as three bf16 MFMA passes
+PEAK_SPLIT_TFLOPS = PEAK_BF16_TFLOPS / 3
+
+
+def head_flop(B=BATCH, T=FRAMES, Ta=149, sd=768, vd=512, d=128, h1=256, c=CLASSES):
+    """Algorithmic FLOPs of the xattn head forward + backward (fusion.py:366-411): every Linear 2MNK forward,
+    dX + dW backward (no dX for audio_seq_proj: the frozen WavLM needs none), the two attentions' QK^T and PV."""
+    lin = [(B * Ta, d, sd), (B * Ta, d, d), (B * T, d, vd), (B * T, d, d), (B * Ta, 2 * d, d), (B * T, d, d),
+           (B * Ta, d, d), (B * T, 2 * d, d), (B * Ta, d, d), (B, h1, 2 * d), (B, c, h1)]
+    fwd = sum(2.0 * m * n * k for m, n, k in lin) + 2 * 2 * (2.0 * B * T * Ta * d)
+    return fwd + 2 * fwd - 2.0 * B * Ta * d * sd
 
 
 def pmc_traffic():
@@ -200,15 +212,19 @@ def main():
 
     # probe steps (after the timed region): the dominant kernel bracketed by HIP events on its stream
     probe = K.KernelProbe(PROBE[0], PROBE[1], units=2.0 * PROBE[1][0] * PROBE[1][1] * PROBE[1][2])
+    hprobe = F.HeadProbe()
     if args.probe_steps > 0:
         probe.active = True
         K.PROBE = probe
+        F.HEAD_PROBE = hprobe
         for _ in range(args.probe_steps + 2):  # the first two build the instrumented (split) WavLM graphs
             step(video, audio, labels, next_audio=nxt)
         torch.cuda.synchronize()
         probe.pairs = probe.pairs[-args.probe_steps:]
+        hprobe.fwd, hprobe.bwd = hprobe.fwd[-args.probe_steps:], hprobe.bwd[-args.probe_steps:]
         probe.active = False
         K.PROBE = None
+        F.HEAD_PROBE = None
 
     kms = probe.avg_ms()
     roof = None
@@ -220,6 +236,29 @@ def main():
                 "avg_ms": round(kms, 4), "launches": len(probe.pairs),
                 "measured": f"HIP events on the launching stream in {len(probe.pairs)} probe steps after the timed "
                             "region"}
+    roof_head = None
+    hms = hprobe.avg_ms()
+    if hms and args.wavlm_unfreeze == 0 and not args.emotion_prior:
+        # the fused head's forward + backward graph replays in production (with the next batch's WavLM running
+        # beside them on the prefetch stream); bytes = the saved activations (inputs included) written once and
+        # read once + the used head parameters read twice and their gradients written once + dv_feat
+        fwd_ms, bwd_ms = hms
+        hparams = sum(t.numel() for n, t in zip(*model.head_params()) if t.requires_grad)
+        hbytes = 2 * hprobe.saved_bytes + 3 * 4 * hparams + 4 * BATCH * FRAMES * 512
+        hflop = head_flop()
+        ai = hflop / hbytes
+        attain = min(PEAK_SPLIT_TFLOPS, ai * PEAK_HBM_GBS / 1e3)
+        ach = hflop / ((fwd_ms + bwd_ms) * 1e-3) / 1e12
+        roof_head = {"bound": "mfma" if PEAK_SPLIT_TFLOPS < ai * PEAK_HBM_GBS / 1e3 else "hbm",
+                     "achieved": round(ach, 2), "peak": round(attain, 1), "unit": "TFLOP/s",
+                     "frac": round(ach / attain, 4), "traffic": None,
+                     "kernel": "fused xattn head fwd+bwd (csrc/xattn_fused.hip F1-F4, xattn_fused_bwd.hip G1-G4 + W)",
+                     "algorithmic_flop": hflop, "algorithmic_bytes": hbytes, "intensity_flop_per_byte": round(ai, 2),
+                     "fwd_ms": round(fwd_ms, 4), "bwd_ms": round(bwd_ms, 4), "ms_per_step": round(fwd_ms + bwd_ms, 4),
+                     "hbm_gbs_achieved": round(hbytes / ((fwd_ms + bwd_ms) * 1e-3) / 1e9, 1),
+                     "peak_basis": "min(split-bf16 fp32-class MFMA peak = 2.5 PF / 3, intensity x 8 TB/s)",
+                     "measured": f"HIP events around the head's forward / backward graph replays in "
+                                 f"{len(hprobe.fwd)} probe steps"}
     step_gflop = BATCH * (STEP_GFLOP_PER_CLIP_FIXED + WAVLM_LAYER_GFLOP_PER_CLIP * layers)
     out = {
         "metric": "3s-clip train steps/sec (B=32, xattn fusion) at 1/2/4/8 MI355X",
@@ -248,6 +287,7 @@ def main():
         "step_tflop": round(step_gflop / 1e3, 4),
         "step_tflops_achieved": round(step_gflop / 1e3 / (median_ms * 1e-3), 1),
         "roofline": roof,
+        "roofline_head": roof_head,
         "cpu_baseline": None,
     }
     if world == 1 and not args.no_cpu_baseline:

@@ -241,40 +241,49 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void wgrad_kernel(WgradGeom g) {
   const bool b_colok = b_nn < Ntot;
   const float inv_C = 1.f / g.C, inv_S = 1.f / g.S, inv_HoWo = 1.f / (g.Ho * g.Wo), inv_Wo = 1.f / g.Wo;
   const int b_tap = b_colok ? fdiv(b_nn, inv_C) : 0;
-  const int b_c = b_nn - b_tap * g.C;
+  const int b_c = b_colok ? b_nn - b_tap * g.C : 0;
   const int b_r = fdiv(b_tap, inv_S), b_s = b_tap - fdiv(b_tap, inv_S) * g.S;
   const int HoWo = g.Ho * g.Wo;
+  // Branch-free staging: every load is unconditional from a clamped (valid) address, its validity kept in a
+  // bit of `okm`; the zeroing select happens at the LDS store, after this K-step's MFMAs.  (A per-lane
+  // condition around a load compiles to a branch and a wait for that load: the staging loads of a K-step
+  // were serialised on the memory latency.)
+  unsigned okm = 0u;
   auto gload = [&](int p0) {
+    okm = 0u;
 #pragma unroll
     for (int i = 0; i < ACH; ++i) {
       const int p = p0 + a_pr0 + i * (NT / ACPR), k = m0 + a_cc * 8;
-      ra[i] = (p < p_end && k < g.K) ? *reinterpret_cast<const u32x4*>(g.dY + (long)p * g.ldy + k) : u32x4{0u, 0u, 0u, 0u};
+      const bool ok = p < p_end && k < g.K;
+      ra[i] = *reinterpret_cast<const u32x4*>(g.dY + (long)(p < p_end ? p : p_beg) * g.ldy + (k < g.K ? k : 0));
+      okm |= (ok ? 1u : 0u) << i;
     }
 #pragma unroll
     for (int i = 0; i < BCH; ++i) {
       const int p = p0 + b_pr0 + i * (NT / BCPR);
-      u32x4 v = {0u, 0u, 0u, 0u};
-      if (p < p_end && b_colok) {
-        const int n = fdiv(p, inv_HoWo);
-        const int rem = p - n * HoWo;
-        const int oh = fdiv(rem, inv_Wo), ow = rem - oh * g.Wo;
-        const int ih = oh * g.st - g.pad + b_r, iw = ow * g.st - g.pad + b_s;
-        if (ih >= 0 && ih < g.H && iw >= 0 && iw < g.W)
-          v = *reinterpret_cast<const u32x4*>(g.X + (((long)n * g.H + ih) * g.W + iw) * g.C + b_c);
-      }
-      rb[i] = v;
+      const int pc = p < p_end ? p : p_beg;
+      const int n = fdiv(pc, inv_HoWo);
+      const int rem = pc - n * HoWo;
+      const int oh = fdiv(rem, inv_Wo), ow = rem - oh * g.Wo;
+      const int ih = oh * g.st - g.pad + b_r, iw = ow * g.st - g.pad + b_s;
+      const bool ok = p < p_end && b_colok && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W;
+      const int ihc = ih < 0 ? 0 : (ih >= g.H ? g.H - 1 : ih), iwc = iw < 0 ? 0 : (iw >= g.W ? g.W - 1 : iw);
+      rb[i] = *reinterpret_cast<const u32x4*>(g.X + (((long)n * g.H + ihc) * g.W + iwc) * g.C + b_c);
+      okm |= (ok ? 1u : 0u) << (ACH + i);
     }
   };
   auto lstore = [&](int buf) {
+    const u32x4 z = {0u, 0u, 0u, 0u};
 #pragma unroll
     for (int i = 0; i < ACH; ++i) {
       const int ch = t + NT * i;
-      *reinterpret_cast<u32x4*>(&lds[buf][(ch / ACPR) * LDM + (ch % ACPR) * 8]) = ra[i];
+      *reinterpret_cast<u32x4*>(&lds[buf][(ch / ACPR) * LDM + (ch % ACPR) * 8]) = ((okm >> i) & 1u) ? ra[i] : z;
     }
 #pragma unroll
     for (int i = 0; i < BCH; ++i) {
       const int ch = t + NT * i;
-      *reinterpret_cast<u32x4*>(&lds[buf][64 * LDM + (ch / BCPR) * LDN + (ch % BCPR) * 8]) = rb[i];
+      *reinterpret_cast<u32x4*>(&lds[buf][64 * LDM + (ch / BCPR) * LDN + (ch % BCPR) * 8]) =
+          ((okm >> (ACH + i)) & 1u) ? rb[i] : z;
     }
   };
   // transposed fragment: elements j=0..7 = Img[k0 + 8*(lane>>4) + j][c0 + (lane&15)]
@@ -303,7 +312,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void wgrad_kernel(WgradGeom g) {
   __syncthreads();
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
-    if (kt + 1 < nk) gload(p_beg + (kt + 1) * 64);
+    gload(p_beg + (kt + 1 < nk ? kt + 1 : kt) * 64);  // unconditional (the last one re-reads, unused)
     const bf16_t* Aimg = &lds[cur][0];
     const bf16_t* Bimg = &lds[cur][64 * LDM];
 #pragma unroll
@@ -364,6 +373,39 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(int K, int C, int Cre
   float s = 0.f;
   for (int q = 0; q < SG; ++q) s += part[q * E + e];
   ws[idx] = s;  // slab 0 (only this block ever reads element idx)
+}
+
+// dw[k][c][r][s] += sum_z ws[z][k][(r*S+s)*C + c] for c < Creal, in split order: one pass replacing the
+// reduce + scatter pair.  Block (channel group of 32, k): each thread sums its (tap, channel) elements over
+// the splits (8 loads in flight, clamped, branch-free) into an LDS [tap][32] tile, written back in the
+// PyTorch order (c, r, s) -- a contiguous run of 32*R*S floats.
+__global__ __launch_bounds__(256) void wgrad_fold_scatter_kernel(int K, int C, int Creal, int RS, int splits,
+                                                                 const float* __restrict__ ws, float* __restrict__ dw) {
+  __shared__ float tile[49 * 32];  // R*S <= 49 (7x7 stem)
+  const int k = blockIdx.y, c0 = blockIdx.x * 32;
+  const long slab = (long)K * RS * C;
+  const float* src = ws + (long)k * RS * C;
+  for (int i = threadIdx.x; i < RS * 32; i += 256) {
+    const int tap = i >> 5, c = c0 + (i & 31);
+    const float* e = src + tap * C + (c < Creal ? c : 0);
+    float s = 0.f;
+    for (int z0 = 0; z0 < splits; z0 += 8) {
+      float v[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] = e[(long)(z0 + q < splits ? z0 + q : splits - 1) * slab];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) s += z0 + q < splits ? v[q] : 0.f;
+    }
+    tile[i] = c < Creal ? s : 0.f;
+  }
+  __syncthreads();
+  const int ncl = min(32, Creal - c0);
+  const float inv_RS = 1.f / RS;
+  float* dst = dw + ((long)k * Creal + c0) * RS;
+  for (int i = threadIdx.x; i < ncl * RS; i += 256) {  // i = cl*RS + tap
+    const int cl = fdiv(i, inv_RS), tap = i - cl * RS;
+    dst[i] += tile[tap * 32 + cl];
+  }
 }
 
 // dw[k][c][r][s] += slab0[k][(r*S+s)*C + c] for c < Creal.  Block (channel group of 32, k): reads coalesced
@@ -910,14 +952,18 @@ static int conv_wgrad_impl(int N, int H, int W, int C, int Creal, int K, int R, 
     else
       hipLaunchKernelGGL((wgrad_kernel<128, 128, 2, 4>), grid, dim3(512), 0, st, g);
   }
-  if (splits > 1) {
-    const int SG = splits >= 64 ? 16 : splits >= 16 ? 8 : 4;
+  if (splits > 16) {  // many partial slabs: a wide reduce first (one serial chain per element was latency-bound)
+    const int SG = splits >= 64 ? 16 : 8;
     const long total = (long)K * R * S * C;
     const int E = 256 / SG;
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((total + E - 1) / E)), dim3(256), 0, st, K, C, Creal, R * S,
                        splits, SG, workspace);
+    hipLaunchKernelGGL(wgrad_scatter_kernel, dim3((Creal + 31) / 32, K), dim3(256), 0, st, C, Creal, R * S, workspace,
+                       dw);
+  } else {  // few slabs: fold and scatter in one pass
+    hipLaunchKernelGGL(wgrad_fold_scatter_kernel, dim3((Creal + 31) / 32, K), dim3(256), 0, st, K, C, Creal, R * S,
+                       splits, workspace, dw);
   }
-  hipLaunchKernelGGL(wgrad_scatter_kernel, dim3((Creal + 31) / 32, K), dim3(256), 0, st, C, Creal, R * S, workspace, dw);
   MER_LAUNCH_CHECK();
 }
 

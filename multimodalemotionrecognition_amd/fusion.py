@@ -189,6 +189,30 @@ class _XattnHeadFn(torch.autograd.Function):
         return (dv, da, None, None, None, None, None, *out_grads)
 
 
+class HeadProbe:
+    """bench.py's second roofline entry: HIP events around the xattn head's forward / backward graph replays
+    (on the stream they replay on), collected while ``fusion.HEAD_PROBE`` is set."""
+
+    def __init__(self):
+        self.fwd, self.bwd = [], []
+        self.saved_bytes = 0
+
+    def mark(self):
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        return e
+
+    def avg_ms(self):
+        f = [a.elapsed_time(b) for a, b in self.fwd]
+        b = [a.elapsed_time(c) for a, c in self.bwd]
+        if not f or not b:
+            return None
+        return sum(f) / len(f), sum(b) / len(b)
+
+
+HEAD_PROBE = None
+
+
 class _HeadGraphs(G.PendingGuard):
     """Captured forward / backward hipGraphs of the xattn head for one input shape (graphs.py).
 
@@ -217,7 +241,12 @@ class _HeadGraphs(G.PendingGuard):
                                      [v_feat, a_seq])
         if self.training:  # this step's host-drawn RNG base, stream-ordered before the replay reads it
             self.rng.fill_(_next_seed())
+        probe = HEAD_PROBE
+        e0 = probe.mark() if probe is not None else None
         logits, hctx = self.fwd.replay(v_feat, a_seq)
+        if probe is not None:
+            probe.fwd.append((e0, probe.mark()))
+            probe.saved_bytes = sum(t.numel() * t.element_size() for t in hctx.saved.values())
         return logits.clone(), hctx
 
     def backward_graphable(self, p, used, need_v, need_a) -> bool:
@@ -236,7 +265,11 @@ class _HeadGraphs(G.PendingGuard):
                 return dv
 
             self.bwd = G.StaticGraph(run, [dlogits])
+        probe = HEAD_PROBE
+        e0 = probe.mark() if probe is not None else None
         dv = self.bwd.replay(dlogits)
+        if probe is not None:
+            probe.bwd.append((e0, probe.mark()))
         return dv.clone(), {n: grad_buffer(t) for n, t in params.items() if n in used and t.requires_grad}
 
 

@@ -505,8 +505,8 @@ def conv_wgrad(x, dy, dw, R, S, stride, pad, creal=None, variant=-1, splits=None
         raise ValueError("conv_wgrad shapes")
     P = N * Ho * Wo
     tiles = ((Kc + 127) // 128) * ((R * S * C + 127) // 128)
-    if splits is None:
-        splits = int(max(1, min(-(-512 // tiles), P // 2048)))
+    if splits is None:  # ~768 workgroups (3 per CU), >= 1024 pixels each
+        splits = int(max(1, min(-(-768 // tiles), P // 1024)))
     ws = torch.empty(splits * Kc * R * S * C, device=x.device, dtype=torch.float32)
     _launch("conv_wgrad", (N, H, W, C, Kc, R, stride), "mer_conv_wgrad_ex", N, H, W, C, creal, Kc, R, S, stride, pad,
             x.data_ptr(), dy.data_ptr(), dw.data_ptr(), int(splits), ws.data_ptr(), int(variant), stream_ptr())

@@ -1,6 +1,8 @@
 """Steady-state per-step kernel time from a rocprofv3 kernel_trace.csv of bench.py: steps are delimited
-by the optimizer's last adam_kernel launch (3 per step), setup/warm-up windows are dropped.
-    python tools/kstats_trace.py <run_kernel_trace.csv> [top]"""
+by the optimizer's last adam_kernel launch of each step, setup/warm-up windows are dropped.
+    python tools/kstats_trace.py <run_kernel_trace.csv> [top] [train_steps_in_trace]
+(train_steps_in_trace = warmup + steps + probe steps + 2 of the bench run; it sets the adam launches per step,
+default 1 -- FusedAdam launches one adam_kernel per run of equal step counts, one per step in the bench)"""
 import csv
 import sys
 from collections import defaultdict
@@ -8,7 +10,8 @@ from collections import defaultdict
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
 top = int(sys.argv[2]) if len(sys.argv) > 2 else 30
 adam = [i for i, r in enumerate(rows) if r["Kernel_Name"].startswith("adam_kernel")]
-ends = adam[2::3]
+per = max(1, round(len(adam) / int(sys.argv[3]))) if len(sys.argv) > 3 else 1
+ends = adam[per - 1::per]
 wins = list(zip(ends[1:-1], ends[2:]))  # skip the first (warm-up) window
 tot, cnt = defaultdict(float), defaultdict(int)
 span = 0.0

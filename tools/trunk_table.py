@@ -1,0 +1,90 @@
+"""Per-layer table of the ResNet18 trunk (fwd conv, dgrad, wgrad) from a rocprofv3 kernel trace of bench.py:
+layer, GEMM shape (M x N x K), us per launch, TF/s -- one steady-state step, launches labelled by the trunk's
+fixed launch order (video.py: forward stem + per block conv1, conv2, [downsample]; backward per block in
+reverse: wgrad conv2, dgrad conv2, wgrad conv1, [wgrad ds, dgrad ds], dgrad conv1; stem wgrad last).
+    python tools/trunk_table.py <run_kernel_trace.csv> [train_steps_in_trace] > profiles/<round>/trunk_table.txt"""
+import csv
+import sys
+
+NIMG, H = 256, 112  # B=32 clips x 8 frames, 112x112
+
+
+def trunk_convs():
+    """(name, M, N, K) of every conv in forward order (torchvision ResNet18 at 112x112; the stem as 7x7/s2)."""
+    convs = [("stem 7x7/2", NIMG * 56 * 56, 64, 3 * 49)]
+    hw, cin = 28, 64
+    for li, cout in enumerate((64, 128, 256, 512)):
+        for bi in range(2):
+            s = 2 if (bi == 0 and li > 0) else 1
+            ho = (hw + 2 - 3) // s + 1
+            convs.append((f"layer{li + 1}.{bi}.conv1", NIMG * ho * ho, cout, cin * 9))
+            convs.append((f"layer{li + 1}.{bi}.conv2", NIMG * ho * ho, cout, cout * 9))
+            if bi == 0 and li > 0:
+                convs.append((f"layer{li + 1}.{bi}.downsample", NIMG * ho * ho, cout, cin))
+            hw, cin = ho, cout
+    return convs
+
+
+def backward_order(convs):
+    """(kind, conv) in the backward launch order."""
+    blocks = {}
+    for c in convs[1:]:
+        blocks.setdefault(c[0].rsplit(".", 1)[0], {})[c[0].rsplit(".", 1)[1]] = c
+    order = []
+    for name in reversed(list(blocks)):
+        b = blocks[name]
+        order += [("wgrad", b["conv2"]), ("dgrad", b["conv2"]), ("wgrad", b["conv1"])]
+        if "downsample" in b:
+            order += [("wgrad", b["downsample"]), ("dgrad", b["downsample"])]
+        order.append(("dgrad", b["conv1"]))
+    order.append(("wgrad", convs[0]))
+    return order
+
+
+def main():
+    rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
+    adam = [i for i, r in enumerate(rows) if r["Kernel_Name"].startswith("adam_kernel")]
+    per = max(1, round(len(adam) / int(sys.argv[2]))) if len(sys.argv) > 2 else 1
+    ends = adam[per - 1::per]
+    a, b = ends[-3], ends[-2]  # one steady-state step
+    win = rows[a + 1:b + 1]
+    convs = trunk_convs()
+    fwd = [r for r in win if "conv_pipe_kernel<false" in r["Kernel_Name"].replace(" ", "")]
+    bwd = [r for r in win if "conv_pipe_kernel<true" in r["Kernel_Name"].replace(" ", "")
+           or r["Kernel_Name"].replace(" ", "").startswith("(anonymousnamespace)::wgrad_kernel")
+           or r["Kernel_Name"].replace(" ", "").startswith("void(anonymousnamespace)::wgrad_kernel")]
+    dur = lambda r: (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3  # noqa: E731
+    print(f"{'layer':26s} {'pass':6s} {'M x N x K':>22s} {'us':>8s} {'TF/s':>7s}  kernel")
+    tot = {"fwd": 0.0, "dgrad": 0.0, "wgrad": 0.0}
+    flops = {"fwd": 0.0, "dgrad": 0.0, "wgrad": 0.0}
+    for c, r in zip(convs, fwd):
+        us = dur(r)
+        f = 2.0 * c[1] * c[2] * c[3]
+        tot["fwd"] += us
+        flops["fwd"] += f
+        print(f"{c[0]:26s} {'fwd':6s} {c[1]:>9d}x{c[2]:>4d}x{c[3]:>5d} {us:8.1f} {f / us / 1e6:7.1f}  {r['Kernel_Name'][:60]}")
+    for (kind, c), r in zip(backward_order(convs), bwd):
+        us = dur(r)
+        f = 2.0 * c[1] * c[2] * c[3]
+        tot[kind] += us
+        flops[kind] += f
+        print(f"{c[0]:26s} {kind:6s} {c[1]:>9d}x{c[2]:>4d}x{c[3]:>5d} {us:8.1f} {f / us / 1e6:7.1f}  {r['Kernel_Name'][:60]}")
+    if len(fwd) != len(convs) or len(bwd) != len(backward_order(convs)):
+        print(f"# WARNING: matched {len(fwd)} fwd / {len(bwd)} bwd launches, expected {len(convs)} / "
+              f"{len(backward_order(convs))}")
+    for k in tot:
+        print(f"# {k}: {tot[k]:.1f} us, {flops[k] / 1e9:.1f} GFLOP, {flops[k] / tot[k] / 1e6:.1f} TF/s")
+    other = {}
+    for r in win:
+        n = r["Kernel_Name"]
+        if any(s in n for s in ("bn_", "wgrad_reduce", "wgrad_scatter", "pack_w", "pack_input", "stem_", "maxpool",
+                                "avgpool", "partials_sum")):
+            key = n.split("(")[0][:60]
+            other[key] = other.get(key, 0.0) + dur(r)
+    print(f"# conv total {sum(tot.values()):.1f} us; BN / pack / reduce / pool kernels {sum(other.values()):.1f} us:")
+    for k, v in sorted(other.items(), key=lambda kv: -kv[1]):
+        print(f"#   {v:8.1f} us  {k}")
+
+
+if __name__ == "__main__":
+    main()
