@@ -15,6 +15,8 @@
 // Tile 128x128x64, 256 threads = 4 waves (2x2), each wave 64x64 = 4x4 v_mfma_f32_16x16x32_bf16.
 // Register-staged double-buffered LDS (one barrier per K step); LDS rows padded to 72 elements
 // (144 B) so the 16 rows read by one ds_read_b128 lane group land on distinct banks.
+#include <cstdlib>
+
 #include "common.h"
 #include "mer.h"
 
@@ -46,7 +48,18 @@ struct GemmArgs {
   unsigned long long drop_site;
   const long long* skip_mask;
   int skip_bit;
+  // K-step order of overlapping-rows (convolution) A operands: K = kp_taps taps x kp_c channels; K-tile u reads
+  // tap u % kp_taps of channel block u / kp_taps, so the taps that re-read the same input rows (stride < taps)
+  // run back to back and hit L2 instead of re-fetching from HBM.  kp_taps = 0: natural order.
+  int kp_taps, kp_c;
 };
+
+// element offset of K-tile u (64 wide) in the K dimension
+__device__ __forceinline__ int ktile_off(const GemmArgs& g, int u) {
+  if (g.kp_taps <= 1) return u * 64;
+  const int cb = u / g.kp_taps, tap = u - cb * g.kp_taps;
+  return tap * g.kp_c + cb * 64;
+}
 
 __device__ __forceinline__ bool layer_skipped(const long long* mask, int bit) {
   return mask != nullptr && ((*mask >> bit) & 1ll);
@@ -284,14 +297,14 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_pipe_kernel(GemmArgs g) {
   // the tile kt+S-1 DMA then reuses.  Raw s_barrier: __syncthreads() would drain vmcnt to 0.
 #pragma unroll
   for (int p = 0; p < S - 1; ++p)
-    if (p < nk) stage(p, p * 64);
+    if (p < nk) stage(p, ktile_off(g, p));
   for (int kt = 0; kt < nk; ++kt) {
     const int ahead = (nk - 1 - kt) < (S - 2) ? (nk - 1 - kt) : (S - 2);
     wait_tiles_in_flight<G>(ahead);
     __builtin_amdgcn_s_waitcnt((15) | (7 << 4) | (0 << 8) | (3 << 14));  // lgkmcnt(0) only
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    if (kt + S - 1 < nk) stage((kt + S - 1) % S, (kt + S - 1) * 64);
+    if (kt + S - 1 < nk) stage((kt + S - 1) % S, ktile_off(g, kt + S - 1));
     const bf16_t* la = smem + (kt % S) * CF::BUF;
     const bf16_t* lb = la + CF::BM * 64;
 #pragma unroll
@@ -464,8 +477,8 @@ __global__ __launch_bounds__(PH_NT, 1) void gemm_phase_kernel(GemmArgs g) {
   auto stage = [&](int pc, int u) {
     if (u >= nk) return;
     bf16_t* dst = smem + ((u & 1) * 4 + pc) * PH_PIECE + w * 1024;
-    glds16(src[pc][0] + u * 64, dst);
-    glds16(src[pc][1] + u * 64, dst + 512);
+    glds16(src[pc][0] + ktile_off(g, u), dst);
+    glds16(src[pc][1] + ktile_off(g, u), dst + 512);
   };
 
   f32x4 acc[8][4];
@@ -684,6 +697,18 @@ MER_API int mer_gemm_bf16_tr(int M, int N, int K, const void* A, long a_gstride,
   g.bias = bias; g.R = (const bf16_t*)R; g.ldr = ldr; g.act = act;
   g.vec_epi = vec_epilogue_ok(N, C, ldc, R, ldr, 0);
   g.drop_p = drop_p; g.drop_seed = drop_seed; g.drop_site = drop_site; g.skip_mask = skip_mask; g.skip_bit = skip_bit;
+  static const bool kperm_on = [] {
+    const char* e = getenv("MER_GEMM_KPERM");  // A/B switch for tools/bench_gemm.py (default on)
+    return !(e && e[0] == '0');
+  }();
+  if (kperm_on && a_rstride > 0 && a_rstride < K) {  // overlapping rows = a strided conv: taps of gcd(stride, K) channels
+    long a = a_rstride, b = K;
+    while (b) { const long t = a % b; a = b; b = t; }
+    if (a % 64 == 0 && K / a > 1) {
+      g.kp_taps = (int)(K / a);
+      g.kp_c = (int)a;
+    }
+  }
   const hipStream_t st = (hipStream_t)stream;
   if (K % 64 != 0) variant = 0;
   if (variant == -1) variant = pick_variant(M, N, K);
