@@ -29,6 +29,24 @@ def test_library_exports_every_header_symbol():
     assert sorted(LIB.symbols()) == sorted(sigs)
 
 
+def test_io_library_exports_every_header_symbol():
+    """libmer_io.so (host input pipeline) exports every entry point of include/mer_io.h."""
+    import ctypes
+    import re
+    from pathlib import Path
+
+    root = Path(__file__).resolve().parents[1]
+    lib = root / "multimodalemotionrecognition_amd" / "libmer_io.so"
+    if not lib.exists():
+        pytest.skip("libmer_io.so not built")
+    text = re.sub(r"/\*.*?\*/", " ", (root / "include" / "mer_io.h").read_text(), flags=re.S)
+    names = re.findall(r"\b(mer_\w+)\s*\(", text)
+    assert len(names) >= 7
+    dll = ctypes.CDLL(str(lib))
+    for n in names:
+        assert hasattr(dll, n), f"{n} declared in include/mer_io.h but not exported"
+
+
 def test_hip_sources_include_the_header():
     for src in (ROOT / "multimodalemotionrecognition_amd" / "csrc").glob("*.hip"):
         assert '#include "mer.h"' in src.read_text(), src.name
