@@ -306,10 +306,12 @@ int mer_gelu_bwd(int rows, int cols, const float* df, const void* z, void* dz, f
 int mer_linear_wgrad(int M, int N, int K, const void* x, const void* dy, long ldy, float* dw, int splits,
                      float* workspace, void* stream);
 
-/* Backward of mer_wavlm_attention (tbl form: per-head bias table [H][2L-1]), L <= 192.  dout fp32 [B*L][>=H*64]
- * (gradient of the attention output; fp32 because dp_ij - sum_j p_ij dp_ij cancels for peaked rows), qkv / x as in the forward.  Writes dqkv bf16 [B*L][3*H*64] (dq | dk | dv),
+/* Backward of mer_wavlm_attention (tbl form: per-head bias table [H][2L-1]), L <= 192, on bf16 MFMA (fp32
+ * operands split hi + lo).  dout fp32 [B*L][>=H*64] (gradient of the attention output; fp32 because
+ * dp_ij - sum_j p_ij dp_ij cancels for peaked rows), qkv / x as in the forward (ldqkv, ldx multiples of 8, ldo of 4).
+ * Writes dqkv bf16 [B*L][3*H*64] (dq | dk | dv),
  * dx_gate fp32 (the gate path's gradient of the layer input x; may be NULL), P and dS scratch float[B*H][L][L],
- * gate_part float[B*H*ceil(L/32)][8*64 + 8 + H] per-block partials of (d gru_rel_pos_linear.weight [8][64],
+ * gate_part float[B*H*ceil(L/64)][8*64 + 8 + H] per-block partials of (d gru_rel_pos_linear.weight [8][64],
  * .bias [8], d gru_rel_pos_const [H]) -- fold with mer_fold_rows. */
 int mer_wavlm_attention_bwd(int B, int L, int H, const void* qkv, long ldqkv, const void* x, long ldx,
                             const void* dout, long ldo, const float* gate_w, const float* gate_b,

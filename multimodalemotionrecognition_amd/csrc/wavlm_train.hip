@@ -18,13 +18,6 @@ typedef __attribute__((ext_vector_type(2))) float f32x2;
 
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }
 
-// make this wave's LDS writes visible to all of its lanes (per-wave row buffers)
-__device__ __forceinline__ void wave_lds_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
 // ---------------------------------------------------------------------------------------------
 // LayerNorm backward over rows of d (d % 256 == 0, d <= 1024).  g = dy_a (+ dy_b) (+ dy_c), recomputes
 // (mean, rstd) from the saved pre-LN fp32 input.  dx = rstd * (g*gamma - mean(g*gamma) - xhat *
@@ -203,222 +196,412 @@ __global__ __launch_bounds__(256) void gelu_bwd_kernel(int rows, int cols, const
 //   dp_ij = do_i.v_j,  ds_ij = p_ij (dp_ij - sum_j p_ij dp_ij)
 //   dq_i = scale sum_j ds_ij k_j, dk_j = scale sum_i ds_ij q_i, dv_j = sum_i p_ij do_i
 //   dgate_i = sum_j ds_ij tbl[h][j - i + L - 1] -> gate (gru_rel_pos_linear / const) gradients + dx_gate.
-// Rows kernel: one wave per query row (4 rows per wave, 16 per block); K, V of the (b,h) staged in LDS
-// (bf16, 66-element row pitch: odd dword stride, conflict-free per-lane row reads); writes P and dS rows
-// (fp32 scratch [B*H][L][L]) for the cols kernel, dq into dqkv, dx_gate, per-block gate-grad partials.
-constexpr int AB_LMAX = 192;  // 3 key columns per lane; 2 blocks per CU in LDS (3 s clips: L = 149)
-constexpr int AB_PITCH = 68;  // bf16 row pitch: 8-byte aligned rows, 17j mod 32 banks -> conflict-free b64 reads
-constexpr int AB_ROWS = 32;  // query rows per block (8 per wave): K/V staged once per 32 rows
+// Both kernels run their products on v_mfma_f32_16x16x32_bf16.  bf16 operands (q, k, v, x) are exact; fp32
+// operands (dO in dp, dS in dq / dk, P in dv, the gate weight) are split into bf16 hi + lo fragments, so every
+// product is fp32-accurate -- dp_ij - sum_j p_ij dp_ij cancels, and the gate-path gradients are held to 1e-4.
+// Fragment maps (16x16x32): A lane = (row l & 15, k 8 (l >> 4) .. +7), B lane = (col l & 15, same k),
+// C lane = (rows 4 (l >> 4) + r, col l & 15).
+constexpr int AB_LMAX = 192;
+constexpr int AB_ROWS = 64;       // query rows per rows-kernel block (16 per wave)
+constexpr int AB_COLS = 32;       // key columns per cols-kernel block (16 per wave pair)
+constexpr int AB_KP = 72;         // bf16 row pitch of K / V in LDS (144 B: 16-byte aligned fragment reads)
 constexpr int GATE_PART = 8 * 64 + 8;  // + H (gate const) per partial row
 
+__device__ __forceinline__ f32x4 mma16(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;
+union AbFrag {
+  bf16x8 v;
+  u32x4 u;
+  uint16_t h[8];
+};
+typedef __attribute__((ext_vector_type(8))) float f32x8;
+__device__ __forceinline__ void ab_split(f32x4 a, f32x4 b, bf16x8& hi, bf16x8& lo) {
+  const f32x8 v = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+  hi = __builtin_convertvector(v, bf16x8);
+  lo = __builtin_convertvector(v - __builtin_convertvector(hi, f32x8), bf16x8);
+}
+// sum / max over the 16 lanes of a fragment row group (lanes sharing l >> 4)
+__device__ __forceinline__ float grp_sum(float v) {
+  v += __shfl_xor(v, 1);
+  v += __shfl_xor(v, 2);
+  v += __shfl_xor(v, 4);
+  return v + __shfl_xor(v, 8);
+}
+__device__ __forceinline__ float grp_max(float v) {
+  v = fmaxf(v, __shfl_xor(v, 1));
+  v = fmaxf(v, __shfl_xor(v, 2));
+  v = fmaxf(v, __shfl_xor(v, 4));
+  return fmaxf(v, __shfl_xor(v, 8));
+}
+
+// LDS plan of the rows kernel for NT 16-key tiles (KP = 16 NT padded keys)
+template <int NT>
+struct RowsLds {
+  static constexpr int KP = 16 * NT, KTP = KP + 8, DSP = KP + 4;
+  static constexpr int ks = 0;                                   // K [KP][AB_KP] bf16
+  static constexpr int vs = ks + KP * AB_KP * 2;                 // V [KP][AB_KP] bf16
+  static constexpr int kt = vs + KP * AB_KP * 2;                 // K^T [64][KTP] bf16
+  static constexpr int ds = kt + 64 * KTP * 2;                   // per-wave dS tiles [4][16][DSP] fp32
+  static constexpr int tb = ds + 4 * 16 * DSP * 4;               // bias row tbl[h] [2 KP] fp32
+  static constexpr int bytes = tb + 2 * KP * 4;
+  static_assert(16 * DSP >= GATE_PART + 1, "gate partial reduction reuses the dS tiles");
+};
+
+// Rows kernel: block = 64 query rows of one (b, h), 4 waves x 16 rows.  Stages K, V (row-major, the B operands of
+// S = Q K^T and dP = dO V^T) and K^T (the B operand of dQ = dS K) in LDS with zero rows past L; each wave
+// keeps its 16 x KP score / dP tiles in registers (softmax, dS, dgate by 16-lane shuffles), writes P and dS rows
+// (fp32 scratch [B*H][L][L]) for the cols kernel, stages its dS tile in LDS for dQ, and folds the gate backward
+// into the per-block partial row [8][64] weight, [8] bias, [H] const (this head's entry only).
+template <int NT>
 __global__ __launch_bounds__(256) void wavlm_attn_bwd_rows_kernel(
     int L, int H, const bf16_t* __restrict__ qkv, long ldqkv, const bf16_t* __restrict__ x, long ldx,
     const float* __restrict__ dout, long ldo, const float* __restrict__ gate_w, const float* __restrict__ gate_b,
     const float* __restrict__ gate_c, const float* __restrict__ tbl, float scale, float* __restrict__ Pbuf,
     float* __restrict__ dSbuf, bf16_t* __restrict__ dqkv, long lddq, float* __restrict__ dxg, long lddxg,
     float* __restrict__ gpart) {
-  __shared__ __attribute__((aligned(16))) bf16_t Ks[AB_LMAX * AB_PITCH];
-  __shared__ __attribute__((aligned(16))) bf16_t Vs[AB_LMAX * AB_PITCH];
-  __shared__ __attribute__((aligned(16))) float qrow[4][64];
-  __shared__ __attribute__((aligned(16))) float dorow[4][64];
-  __shared__ __attribute__((aligned(16))) float dsrow[4][AB_LMAX];
-  __shared__ float gw[8][64];
-  __shared__ float red[4][GATE_PART + 1];
+  typedef RowsLds<NT> Ly;
+  constexpr int KP = Ly::KP, KTP = Ly::KTP, DSP = Ly::DSP;
+  extern __shared__ __attribute__((aligned(16))) unsigned char ab_smem[];
+  bf16_t* Ks = reinterpret_cast<bf16_t*>(ab_smem + Ly::ks);
+  bf16_t* Vs = reinterpret_cast<bf16_t*>(ab_smem + Ly::vs);
+  bf16_t* KsT = reinterpret_cast<bf16_t*>(ab_smem + Ly::kt);
+  float* dSw = reinterpret_cast<float*>(ab_smem + Ly::ds);
+  float* tbs = reinterpret_cast<float*>(ab_smem + Ly::tb);
   const int bh = blockIdx.y, b = bh / H, h = bh - b * H;
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, fr = lane & 15, fq = lane >> 4, fk = 8 * fq;
   const int D = H * 64;
-  for (int i = t; i < 8 * 64; i += 256) gw[i >> 6][i & 63] = gate_w[i];
-  // stage K and V rows of this (b, h): 8 bf16 per 16-byte chunk, 8 chunks per row
-  for (int ch = t; ch < L * 8; ch += 256) {
+  // stage K, V (16-byte chunks) and K^T; rows L..KP-1 are zero (their products must be finite zeros)
+  for (int ch = t; ch < KP * 8; ch += 256) {
     const int j = ch >> 3, c8 = (ch & 7) * 8;
-    const long g = (long)(b * L + j) * ldqkv + h * 64 + c8;
-    const uint4 kv = *reinterpret_cast<const uint4*>(qkv + g + D);
-    const uint4 vv = *reinterpret_cast<const uint4*>(qkv + g + 2 * D);
-    uint32_t* kd = reinterpret_cast<uint32_t*>(Ks + j * AB_PITCH + c8);
-    uint32_t* vd = reinterpret_cast<uint32_t*>(Vs + j * AB_PITCH + c8);
-    kd[0] = kv.x; kd[1] = kv.y; kd[2] = kv.z; kd[3] = kv.w;
-    vd[0] = vv.x; vd[1] = vv.y; vd[2] = vv.z; vd[3] = vv.w;
+    const long g = (long)(b * L + (j < L ? j : L - 1)) * ldqkv + h * 64 + c8;
+    u32x4 kv = *reinterpret_cast<const u32x4*>(qkv + g + D);
+    u32x4 vv = *reinterpret_cast<const u32x4*>(qkv + g + 2 * D);
+    if (j >= L) kv = vv = u32x4{0u, 0u, 0u, 0u};
+    *reinterpret_cast<u32x4*>(Ks + j * AB_KP + c8) = kv;
+    *reinterpret_cast<u32x4*>(Vs + j * AB_KP + c8) = vv;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      KsT[(c8 + 2 * e) * KTP + j] = (bf16_t)(kv[e] & 0xffff);
+      KsT[(c8 + 2 * e + 1) * KTP + j] = (bf16_t)(kv[e] >> 16);
+    }
+  }
+  const float* th = tbl + (long)h * (2 * L - 1);
+  for (int k = t; k < 2 * L - 1; k += 256) tbs[k] = th[k];
+
+  // this wave's operand fragments: q, x (bf16, exact), dO split, gate weight split (cols 0..7 valid)
+  const int i0 = blockIdx.x * AB_ROWS + w * 16;
+  const long rowa = (long)(b * L + (i0 + fr < L ? i0 + fr : L - 1));
+  AbFrag qa[2], xa[2];
+  bf16x8 oh[2], ol[2], gh[2], gl[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const int c = h * 64 + 32 * s + fk;
+    qa[s].u = *reinterpret_cast<const u32x4*>(qkv + rowa * ldqkv + c);
+    xa[s].u = *reinterpret_cast<const u32x4*>(x + rowa * ldx + c);
+    const float* po = dout + rowa * ldo + c;
+    ab_split(*reinterpret_cast<const f32x4*>(po), *reinterpret_cast<const f32x4*>(po + 4), oh[s], ol[s]);
+    const float* pw = gate_w + (fr & 7) * 64 + 32 * s + fk;
+    f32x4 w0 = *reinterpret_cast<const f32x4*>(pw), w1 = *reinterpret_cast<const f32x4*>(pw + 4);
+    if (fr >= 8) w0 = w1 = f32x4{0.f, 0.f, 0.f, 0.f};
+    ab_split(w0, w1, gh[s], gl[s]);
+  }
+  // gate (TF:167-177): z[row][n] = x_h . gate_w[n] + gate_b[n]; pa = sum n<4, pb = sum 4<=n<8
+  f32x4 z = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    z = mma16(xa[s].v, gh[s], z);
+    z = mma16(xa[s].v, gl[s], z);
+  }
+  const float gbn = fr < 8 ? gate_b[fr & 7] : 0.f, gc = gate_c[h];
+  float ga[4], gb[4], gate[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    float v = fr < 8 ? z[r] + gbn : 0.f;
+    v += __shfl_xor(v, 1);
+    v += __shfl_xor(v, 2);
+    ga[r] = sigmoidf_(__shfl(v, fq * 16));
+    gb[r] = sigmoidf_(__shfl(v, fq * 16 + 4));
+    gate[r] = ga[r] * (gb[r] * gc - 1.f) + 2.f;
   }
   __syncthreads();
-  const float* th = tbl + (long)h * (2 * L - 1);
-  float wsa = 0.f, wsb = 0.f;  // column sums of the gate weight halves (d(pa)/dx, d(pb)/dx)
-  for (int r = 0; r < 4; ++r) { wsa += gw[r][lane]; wsb += gw[r + 4][lane]; }
-  float gacc[8], gbacc[8], gcacc = 0.f;
-  for (int r = 0; r < 8; ++r) gacc[r] = gbacc[r] = 0.f;
-  const float gc = gate_c[h];
-  constexpr int NJ = AB_LMAX / 64;
-  for (int rr = w; rr < AB_ROWS; rr += 4) {
-    const int i = blockIdx.x * AB_ROWS + rr;
-    if (i >= L) break;
-    const long row = (long)(b * L + i);
-    const float qd = bf2f(qkv[row * ldqkv + h * 64 + lane]) * scale;
-    const float dod = dout[row * ldo + h * 64 + lane];
-    const float xd = bf2f(x[row * ldx + h * 64 + lane]);
-    qrow[w][lane] = qd;
-    dorow[w][lane] = dod;
-    // gate (TF:167-177): 8 projections, pair sums of 4
-    float pa = 0.f, pb = 0.f;
-    for (int r = 0; r < 4; ++r) pa += wave_sum(xd * gw[r][lane]) + gate_b[r];
-    for (int r = 4; r < 8; ++r) pb += wave_sum(xd * gw[r][lane]) + gate_b[r];
-    const float ga = sigmoidf_(pa), gb = sigmoidf_(pb);
-    const float gate = ga * (gb * gc - 1.f) + 2.f;
-    wave_lds_sync();
-    float s[NJ], dp[NJ];
-    float mx = -INFINITY;
+
+  // S = Q K^T (exact), dP = dO V^T (split dO): 16 x KP per wave in registers
+  f32x4 s[NT], dp[NT];
 #pragma unroll
-    for (int jj = 0; jj < NJ; ++jj) {
-      const int j = jj * 64 + lane;
-      s[jj] = -INFINITY;
-      dp[jj] = 0.f;
-      if (j < L) {
-        // 4 dims per step: one b64 K read, one b64 V read (per lane), one broadcast b128 read each of q and dO
-        const uint2* kr = reinterpret_cast<const uint2*>(Ks + j * AB_PITCH);
-        const uint2* vr = reinterpret_cast<const uint2*>(Vs + j * AB_PITCH);
-        const f32x4* q4 = reinterpret_cast<const f32x4*>(qrow[w]);
-        const f32x4* o4 = reinterpret_cast<const f32x4*>(dorow[w]);
-        // packed fp32 FMAs (v_pk_fma_f32): two dims per instruction
-        f32x2 a = {0.f, 0.f}, c = {0.f, 0.f};
-#pragma unroll 4
-        for (int e = 0; e < 16; ++e) {
-          const uint2 kk = kr[e], vv = vr[e];
-          const f32x4 qq = q4[e], oo = o4[e];
-          const f32x2 k01 = {__uint_as_float(kk.x << 16), __uint_as_float(kk.x & 0xffff0000u)};
-          const f32x2 k23 = {__uint_as_float(kk.y << 16), __uint_as_float(kk.y & 0xffff0000u)};
-          const f32x2 v01 = {__uint_as_float(vv.x << 16), __uint_as_float(vv.x & 0xffff0000u)};
-          const f32x2 v23 = {__uint_as_float(vv.y << 16), __uint_as_float(vv.y & 0xffff0000u)};
-          a = __builtin_elementwise_fma(f32x2{qq[0], qq[1]}, k01, a);
-          a = __builtin_elementwise_fma(f32x2{qq[2], qq[3]}, k23, a);
-          c = __builtin_elementwise_fma(f32x2{oo[0], oo[1]}, v01, c);
-          c = __builtin_elementwise_fma(f32x2{oo[2], oo[3]}, v23, c);
-        }
-        s[jj] = a[0] + a[1] + gate * th[j - i + L - 1];
-        dp[jj] = c[0] + c[1];
-      }
-      mx = fmaxf(mx, s[jj]);
+  for (int tt = 0; tt < NT; ++tt) {
+    const bf16_t* kr = Ks + (16 * tt + fr) * AB_KP + fk;
+    const bf16_t* vr = Vs + (16 * tt + fr) * AB_KP + fk;
+    AbFrag k0, k1, v0, v1;
+    k0.u = *reinterpret_cast<const u32x4*>(kr);
+    k1.u = *reinterpret_cast<const u32x4*>(kr + 32);
+    v0.u = *reinterpret_cast<const u32x4*>(vr);
+    v1.u = *reinterpret_cast<const u32x4*>(vr + 32);
+    const f32x4 zz = f32x4{0.f, 0.f, 0.f, 0.f};
+    s[tt] = mma16(qa[1].v, k1.v, mma16(qa[0].v, k0.v, zz));
+    f32x4 d = mma16(oh[0], v0.v, zz);
+    d = mma16(ol[0], v0.v, d);
+    d = mma16(oh[1], v1.v, d);
+    dp[tt] = mma16(ol[1], v1.v, d);
+  }
+  const int ib = i0 + 4 * fq;  // this lane's rows ib + r
+  const int tmax = 2 * L - 2;
+  float mx[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+#pragma unroll
+  for (int tt = 0; tt < NT; ++tt) {
+    const int j = 16 * tt + fr;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int k = min(max(j - (ib + r) + L - 1, 0), tmax);
+      const float v = j < L ? s[tt][r] * scale + gate[r] * tbs[k] : -INFINITY;
+      s[tt][r] = v;
+      mx[r] = fmaxf(mx[r], v);
     }
-    mx = wave_max(mx);
-    float sum = 0.f;
+  }
+  float sum[4], Dr[4], dg[4];
 #pragma unroll
-    for (int jj = 0; jj < NJ; ++jj) {
-      s[jj] = (jj * 64 + lane < L) ? __expf(s[jj] - mx) : 0.f;
-      sum += s[jj];
+  for (int r = 0; r < 4; ++r) {
+    mx[r] = grp_max(mx[r]);
+    sum[r] = 0.f;
+  }
+#pragma unroll
+  for (int tt = 0; tt < NT; ++tt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      s[tt][r] = __expf(s[tt][r] - mx[r]);
+      sum[r] += s[tt][r];
     }
-    const float inv = 1.f / wave_sum(sum);
-    float pd = 0.f;
 #pragma unroll
-    for (int jj = 0; jj < NJ; ++jj) { s[jj] *= inv; pd += s[jj] * dp[jj]; }
-    const float Dsum = wave_sum(pd);
-    float dgl = 0.f;
-    float* prow = Pbuf + ((long)bh * L + i) * L;
-    float* drow = dSbuf + ((long)bh * L + i) * L;
+  for (int r = 0; r < 4; ++r) {
+    sum[r] = 1.f / grp_sum(sum[r]);
+    Dr[r] = 0.f;
+  }
 #pragma unroll
-    for (int jj = 0; jj < NJ; ++jj) {
-      const int j = jj * 64 + lane;
-      if (j < L) {
-        const float ds = s[jj] * (dp[jj] - Dsum);
-        dgl += ds * th[j - i + L - 1];
-        prow[j] = s[jj];
-        drow[j] = ds;
-        dsrow[w][j] = ds;
+  for (int tt = 0; tt < NT; ++tt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      s[tt][r] *= sum[r];
+      Dr[r] += s[tt][r] * dp[tt][r];
+    }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    Dr[r] = grp_sum(Dr[r]);
+    dg[r] = 0.f;
+  }
+  float* dsw = dSw + w * 16 * DSP;
+#pragma unroll
+  for (int tt = 0; tt < NT; ++tt) {
+    const int j = 16 * tt + fr;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = ib + r;
+      const float ds = s[tt][r] * (dp[tt][r] - Dr[r]);  // 0 for keys past L (p = 0, dp = 0)
+      dg[r] += ds * tbs[min(max(j - i + L - 1, 0), tmax)];
+      dsw[(4 * fq + r) * DSP + j] = ds;
+      if (i < L && j < L) {
+        const long o = ((long)bh * L + i) * L + j;
+        Pbuf[o] = s[tt][r];
+        dSbuf[o] = ds;
       }
     }
-    const float dgate = wave_sum(dgl);
-    wave_lds_sync();
-    // dq_i[d] = scale * sum_j ds_ij k_j[d]   (lane = d)
-    float q0 = 0.f, q1 = 0.f;
-    int j = 0;
-    for (; j + 4 <= L; j += 4) {
-      const f32x4 d4 = *reinterpret_cast<const f32x4*>(&dsrow[w][j]);
-      q0 += d4[0] * bf2f(Ks[j * AB_PITCH + lane]);
-      q1 += d4[1] * bf2f(Ks[(j + 1) * AB_PITCH + lane]);
-      q0 += d4[2] * bf2f(Ks[(j + 2) * AB_PITCH + lane]);
-      q1 += d4[3] * bf2f(Ks[(j + 3) * AB_PITCH + lane]);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+
+  // dQ = scale dS K: A = this wave's dS tile (split), B = K^T rows (exact); 4 tiles of 16 dims
+  f32x4 dq[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) dq[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < KP / 32; ++ks) {
+    const float* ap = dsw + fr * DSP + 32 * ks + fk;
+    bf16x8 ah, al;
+    ab_split(*reinterpret_cast<const f32x4*>(ap), *reinterpret_cast<const f32x4*>(ap + 4), ah, al);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      AbFrag kb;
+      kb.u = *reinterpret_cast<const u32x4*>(KsT + (16 * c + fr) * KTP + 32 * ks + fk);
+      dq[c] = mma16(ah, kb.v, dq[c]);
+      dq[c] = mma16(al, kb.v, dq[c]);
     }
-    for (; j < L; ++j) q0 += dsrow[w][j] * bf2f(Ks[j * AB_PITCH + lane]);
-    dqkv[row * lddq + h * 64 + lane] = f2bf((q0 + q1) * scale);
-    // gate backward: gate = ga (gb c - 1) + 2
-    const float dpa = dgate * (gb * gc - 1.f) * ga * (1.f - ga);
-    const float dpb = dgate * ga * gc * gb * (1.f - gb);
-    gcacc += dgate * ga * gb;
-    for (int r = 0; r < 4; ++r) { gacc[r] += dpa * xd; gacc[r + 4] += dpb * xd; }
-    gbacc[0] += dpa;
-    gbacc[4] += dpb;
-    if (dxg) dxg[row * lddxg + h * 64 + lane] = dpa * wsa + dpb * wsb;
-    wave_lds_sync();
   }
-  // per-block gate-gradient partial row: [8][64] weight, [8] bias, [H] const (this head only)
-  for (int r = 0; r < 8; ++r) red[w][r * 64 + lane] = gacc[r];
-  if (lane == 0) {
-    for (int r = 0; r < 8; ++r) red[w][512 + r] = gbacc[r < 4 ? 0 : 4];
-    red[w][GATE_PART] = gcacc;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int i = ib + r;
+    if (i < L) {
+      bf16_t* o = dqkv + (long)(b * L + i) * lddq + h * 64 + fr;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) o[16 * c] = f2bf(dq[c][r] * scale);
+    }
   }
+
+  // gate backward: gate = ga (gb c - 1) + 2, pa / pb = sums of 4 projections each
+  float dpa[4], dpb[4], gcl = 0.f, gal = 0.f, gbl = 0.f;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const float g = ib + r < L ? grp_sum(dg[r]) : 0.f;
+    dpa[r] = g * (gb[r] * gc - 1.f) * ga[r] * (1.f - ga[r]);
+    dpb[r] = g * ga[r] * gc * gb[r] * (1.f - gb[r]);
+    gcl += g * ga[r] * gb[r];
+    gal += dpa[r];
+    gbl += dpb[r];
+  }
+  // lane = d: dW[n][d] += dp{a,b} x[row][d] over the wave's 16 rows, dx_gate = dpa wsa + dpb wsb
+  float wsa = 0.f, wsb = 0.f;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    wsa += gate_w[r * 64 + lane];
+    wsb += gate_w[(r + 4) * 64 + lane];
+  }
+  float xd[16];
+#pragma unroll
+  for (int rr = 0; rr < 16; ++rr) xd[rr] = bf2f(x[(long)(b * L + min(i0 + rr, L - 1)) * ldx + h * 64 + lane]);
+  float wa = 0.f, wb = 0.f;
+#pragma unroll
+  for (int rr = 0; rr < 16; ++rr) {
+    const float a = __shfl(dpa[rr & 3], (rr >> 2) * 16), c = __shfl(dpb[rr & 3], (rr >> 2) * 16);
+    wa += a * xd[rr];
+    wb += c * xd[rr];
+    if (dxg && i0 + rr < L) dxg[(long)(b * L + i0 + rr) * lddxg + h * 64 + lane] = a * wsa + c * wsb;
+  }
+  // one copy per 16-lane group of the row-replicated sums
+  gal = __shfl(gal, 0) + __shfl(gal, 16) + __shfl(gal, 32) + __shfl(gal, 48);
+  gbl = __shfl(gbl, 0) + __shfl(gbl, 16) + __shfl(gbl, 32) + __shfl(gbl, 48);
+  gcl = __shfl(gcl, 0) + __shfl(gcl, 16) + __shfl(gcl, 32) + __shfl(gcl, 48);
+  __syncthreads();  // every wave is done with its dS tile: reuse them for the block reduction
+  float* red = dSw;  // [4][GATE_PART + 1]
+  constexpr int RP = GATE_PART + 1;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    red[w * RP + r * 64 + lane] = wa;
+    red[w * RP + (r + 4) * 64 + lane] = wb;
+  }
+  if (lane < 8) red[w * RP + 512 + lane] = lane < 4 ? gal : gbl;
+  if (lane == 0) red[w * RP + GATE_PART] = gcl;
   __syncthreads();
   float* pr = gpart + ((long)bh * gridDim.x + blockIdx.x) * (GATE_PART + H);
   for (int k = t; k < GATE_PART + H; k += 256) {
     float v;
-    if (k < GATE_PART) v = ((red[0][k] + red[1][k]) + red[2][k]) + red[3][k];
-    else v = (k - GATE_PART == h) ? ((red[0][GATE_PART] + red[1][GATE_PART]) + red[2][GATE_PART]) + red[3][GATE_PART] : 0.f;
+    if (k < GATE_PART) v = ((red[k] + red[RP + k]) + red[2 * RP + k]) + red[3 * RP + k];
+    else
+      v = (k - GATE_PART == h)
+              ? ((red[GATE_PART] + red[RP + GATE_PART]) + red[2 * RP + GATE_PART]) + red[3 * RP + GATE_PART]
+              : 0.f;
     pr[k] = v;
   }
 }
 
-// Cols kernel: one wave per 4 key columns j (16 per block): dk_j = scale sum_i ds_ij q_i, dv_j = sum_i p_ij do_i
-// (lane = d).  Q and dO rows of the (b, h) are staged in LDS (bf16), the block's P / dS column strips [L][16]
-// in fp32.
+// LDS plan of the cols kernel for NI 32-row query steps (IP = 32 NI padded query rows)
+template <int NI>
+struct ColsLds {
+  static constexpr int IP = 32 * NI, TP = IP + 4, BP = IP + 8;
+  static constexpr int ps = 0;                      // P^T strip [32][TP] fp32
+  static constexpr int ds = ps + 32 * TP * 4;       // dS^T strip [32][TP] fp32
+  static constexpr int qt = ds + 32 * TP * 4;       // Q^T [64][BP] bf16
+  static constexpr int ot = qt + 64 * BP * 2;       // dO^T [64][BP] bf16
+  static constexpr int bytes = ot + 64 * BP * 2;
+};
+
+// Cols kernel: block = 32 keys of one (b, h); wave w = (key half w & 1, dim half w >> 1).
+//   dK = scale dS^T Q (split dS, exact q), dV = P^T dO (split P; dO rounded to bf16 -- dv has no cancellation).
+// The P / dS column strips are staged transposed (contiguous A fragments), Q / dO transposed (contiguous B).
+template <int NI>
 __global__ __launch_bounds__(256) void wavlm_attn_bwd_cols_kernel(int L, int H, const bf16_t* __restrict__ qkv,
                                                                   long ldqkv, const float* __restrict__ dout, long ldo,
                                                                   const float* __restrict__ Pbuf,
                                                                   const float* __restrict__ dSbuf, float scale,
                                                                   bf16_t* __restrict__ dqkv, long lddq) {
-  __shared__ __attribute__((aligned(16))) bf16_t Qs[AB_LMAX * AB_PITCH];
-  __shared__ __attribute__((aligned(16))) bf16_t Os[AB_LMAX * AB_PITCH];
-  __shared__ float Pc[AB_LMAX][17], Dc[AB_LMAX][17];  // 17: keeps the block at 2 per CU in LDS
+  typedef ColsLds<NI> Ly;
+  constexpr int IP = Ly::IP, TP = Ly::TP, BP = Ly::BP;
+  extern __shared__ __attribute__((aligned(16))) unsigned char ab_smem[];
+  float* PsT = reinterpret_cast<float*>(ab_smem + Ly::ps);
+  float* DsT = reinterpret_cast<float*>(ab_smem + Ly::ds);
+  bf16_t* QT = reinterpret_cast<bf16_t*>(ab_smem + Ly::qt);
+  bf16_t* OT = reinterpret_cast<bf16_t*>(ab_smem + Ly::ot);
   const int bh = blockIdx.y, b = bh / H, h = bh - b * H;
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, fr = lane & 15, fq = lane >> 4, fk = 8 * fq;
   const int D = H * 64;
-  const int j0 = blockIdx.x * 16;
-  for (int ch = t; ch < L * 8; ch += 256) {
+  const int j0 = blockIdx.x * AB_COLS;
+  for (int ch = t; ch < IP * 8; ch += 256) {
     const int i = ch >> 3, c8 = (ch & 7) * 8;
-    const long row = (long)(b * L + i);
-    const uint4 qv = *reinterpret_cast<const uint4*>(qkv + row * ldqkv + h * 64 + c8);
+    const long row = (long)(b * L + (i < L ? i : L - 1));
+    const u32x4 qv = *reinterpret_cast<const u32x4*>(qkv + row * ldqkv + h * 64 + c8);
     const f32x4 o0 = *reinterpret_cast<const f32x4*>(dout + row * ldo + h * 64 + c8);
     const f32x4 o1 = *reinterpret_cast<const f32x4*>(dout + row * ldo + h * 64 + c8 + 4);
-    uint32_t* qd = reinterpret_cast<uint32_t*>(Qs + i * AB_PITCH + c8);
-    uint32_t* od = reinterpret_cast<uint32_t*>(Os + i * AB_PITCH + c8);
-    qd[0] = qv.x; qd[1] = qv.y; qd[2] = qv.z; qd[3] = qv.w;
-    // dv = sum_i p_ij do_i has no cancellation: dO is staged as bf16 here (it stays fp32 in the rows
-    // kernel, where dp_ij - sum_j p_ij dp_ij cancels)
-    od[0] = (uint32_t)f2bf(o0[0]) | ((uint32_t)f2bf(o0[1]) << 16);
-    od[1] = (uint32_t)f2bf(o0[2]) | ((uint32_t)f2bf(o0[3]) << 16);
-    od[2] = (uint32_t)f2bf(o1[0]) | ((uint32_t)f2bf(o1[1]) << 16);
-    od[3] = (uint32_t)f2bf(o1[2]) | ((uint32_t)f2bf(o1[3]) << 16);
+    const bool ok = i < L;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      QT[(c8 + 2 * e) * BP + i] = ok ? (bf16_t)(qv[e] & 0xffff) : (bf16_t)0;
+      QT[(c8 + 2 * e + 1) * BP + i] = ok ? (bf16_t)(qv[e] >> 16) : (bf16_t)0;
+      OT[(c8 + e) * BP + i] = ok ? f2bf(o0[e]) : (bf16_t)0;
+      OT[(c8 + 4 + e) * BP + i] = ok ? f2bf(o1[e]) : (bf16_t)0;
+    }
   }
-  for (int e = t; e < L * 16; e += 256) {
-    const int i = e >> 4, jc = e & 15, j = j0 + jc;
-    const long o = ((long)bh * L + i) * L + j;
-    Pc[i][jc] = j < L ? Pbuf[o] : 0.f;
-    Dc[i][jc] = j < L ? dSbuf[o] : 0.f;
+  for (int e = t; e < IP * AB_COLS; e += 256) {
+    const int i = e >> 5, jc = e & 31, j = j0 + jc;
+    const long o = ((long)bh * L + (i < L ? i : L - 1)) * L + (j < L ? j : L - 1);
+    const float pv = Pbuf[o], dv = dSbuf[o];
+    const bool ok = i < L && j < L;
+    PsT[jc * TP + i] = ok ? pv : 0.f;
+    DsT[jc * TP + i] = ok ? dv : 0.f;
   }
   __syncthreads();
-  float dk[4] = {0.f, 0.f, 0.f, 0.f}, dv[4] = {0.f, 0.f, 0.f, 0.f};
-  const int jc0 = w * 4;
-  for (int i = 0; i < L; ++i) {
-    const float qd = bf2f(Qs[i * AB_PITCH + lane]), od = bf2f(Os[i * AB_PITCH + lane]);
+  const int kt = w & 1, dd = w >> 1;
+  f32x4 dk[2], dv[2];
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      dk[c] += Dc[i][jc0 + c] * qd;
-      dv[c] += Pc[i][jc0 + c] * od;
+  for (int c = 0; c < 2; ++c) dk[c] = dv[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < NI; ++ks) {
+    const int a = (16 * kt + fr) * TP + 32 * ks + fk;
+    bf16x8 dh, dl, ph, pl;
+    ab_split(*reinterpret_cast<const f32x4*>(DsT + a), *reinterpret_cast<const f32x4*>(DsT + a + 4), dh, dl);
+    ab_split(*reinterpret_cast<const f32x4*>(PsT + a), *reinterpret_cast<const f32x4*>(PsT + a + 4), ph, pl);
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int n = 32 * dd + 16 * c + fr;
+      AbFrag qb, ob;
+      qb.u = *reinterpret_cast<const u32x4*>(QT + n * BP + 32 * ks + fk);
+      ob.u = *reinterpret_cast<const u32x4*>(OT + n * BP + 32 * ks + fk);
+      dk[c] = mma16(dh, qb.v, dk[c]);
+      dk[c] = mma16(dl, qb.v, dk[c]);
+      dv[c] = mma16(ph, ob.v, dv[c]);
+      dv[c] = mma16(pl, ob.v, dv[c]);
     }
   }
 #pragma unroll
-  for (int c = 0; c < 4; ++c) {
-    const int j = j0 + jc0 + c;
+  for (int r = 0; r < 4; ++r) {
+    const int j = j0 + 16 * kt + 4 * fq + r;
     if (j < L) {
-      const long row = (long)(b * L + j);
-      dqkv[row * lddq + D + h * 64 + lane] = f2bf(dk[c] * scale);
-      dqkv[row * lddq + 2 * D + h * 64 + lane] = f2bf(dv[c]);
+      bf16_t* o = dqkv + (long)(b * L + j) * lddq + h * 64 + 32 * dd + fr;
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        o[D + 16 * c] = f2bf(dk[c][r] * scale);
+        o[2 * D + 16 * c] = f2bf(dv[c][r]);
+      }
     }
   }
+}
+
+template <int NT>
+int wavlm_attention_bwd_launch(int B, int L, int H, const bf16_t* qkv, long ldqkv, const bf16_t* x, long ldx,
+                               const float* dout, long ldo, const float* gate_w, const float* gate_b,
+                               const float* gate_c, const float* tbl, float scale, float* P, float* dS, bf16_t* dqkv,
+                               long lddq, float* dxg, long lddxg, float* gpart, hipStream_t st) {
+  constexpr int rb = RowsLds<NT>::bytes, cb = ColsLds<NT / 2>::bytes;
+  static_assert(rb <= 160 * 1024 && cb <= 160 * 1024, "LDS");
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&wavlm_attn_bwd_rows_kernel<NT>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, rb) != hipSuccess ||
+      hipFuncSetAttribute(reinterpret_cast<const void*>(&wavlm_attn_bwd_cols_kernel<NT / 2>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, cb) != hipSuccess)
+    return (int)hipErrorInvalidConfiguration;
+  hipLaunchKernelGGL(wavlm_attn_bwd_rows_kernel<NT>, dim3((L + AB_ROWS - 1) / AB_ROWS, B * H), dim3(256), rb, st, L, H,
+                     qkv, ldqkv, x, ldx, dout, ldo, gate_w, gate_b, gate_c, tbl, scale, P, dS, dqkv, lddq, dxg, lddxg,
+                     gpart);
+  hipLaunchKernelGGL(wavlm_attn_bwd_cols_kernel<NT / 2>, dim3((L + AB_COLS - 1) / AB_COLS, B * H), dim3(256), cb, st,
+                     L, H, qkv, ldqkv, dout, ldo, P, dS, scale, dqkv, lddq);
+  return (int)hipGetLastError();
 }
 
 }  // namespace
@@ -478,15 +661,16 @@ MER_API int mer_wavlm_attention_bwd(int B, int L, int H, const void* qkv, long l
                                     const float* gate_const, const float* tbl, float scale, float* P, float* dS,
                                     void* dqkv, long lddq, float* dx_gate, long lddxg, float* gate_part,
                                     void* stream) {
-  if (L <= 0 || L > AB_LMAX || ldqkv % 8 || ldo % 4 || B <= 0 || H <= 0) return (int)hipErrorInvalidValue;
+  if (L <= 0 || L > AB_LMAX || ldqkv % 8 || ldx % 8 || ldo % 4 || B <= 0 || H <= 0) return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
-  const int nrb = (L + AB_ROWS - 1) / AB_ROWS;
-  hipLaunchKernelGGL(wavlm_attn_bwd_rows_kernel, dim3(nrb, B * H), dim3(256), 0, st, L, H, (const bf16_t*)qkv, ldqkv,
-                     (const bf16_t*)x, ldx, (const float*)dout, ldo, gate_w, gate_b, gate_const, tbl, scale, P, dS,
-                     (bf16_t*)dqkv, lddq, dx_gate, lddxg, gate_part);
-  hipLaunchKernelGGL(wavlm_attn_bwd_cols_kernel, dim3((L + 15) / 16, B * H), dim3(256), 0, st, L, H,
-                     (const bf16_t*)qkv, ldqkv, (const float*)dout, ldo, P, dS, scale, (bf16_t*)dqkv, lddq);
-  MER_LAUNCH_CHECK();
+  const int nt = (L + 15) / 16;  // 16-key tiles; the kernels are built for 4 / 8 / 10 / 12 (L <= 64 / 128 / 160 / 192)
+#define MER_AB_LAUNCH(NT)                                                                                             \
+  wavlm_attention_bwd_launch<NT>(B, L, H, (const bf16_t*)qkv, ldqkv, (const bf16_t*)x, ldx, (const float*)dout, ldo, \
+                                 gate_w, gate_b, gate_const, tbl, scale, P, dS, (bf16_t*)dqkv, lddq, dx_gate, lddxg,  \
+                                 gate_part, st)
+  const int rc = nt <= 4 ? MER_AB_LAUNCH(4) : nt <= 8 ? MER_AB_LAUNCH(8) : nt <= 10 ? MER_AB_LAUNCH(10) : MER_AB_LAUNCH(12);
+#undef MER_AB_LAUNCH
+  return rc;
 }
 
 namespace {

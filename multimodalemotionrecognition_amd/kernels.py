@@ -737,7 +737,7 @@ def linear_wgrad(x, dy, dw, col0=0):
 
 def wavlm_attention_bwd(qkv, x, dout, gate_w, gate_b, gate_const, tbl, B, L, H, scale, dqkv, dx_gate=None):
     """Backward of wavlm_attention (per-head table form).  Returns the gate partial rows
-    [B*H*ceil(L/32)][8*64 + 8 + H] for fold_rows."""
+    [B*H*ceil(L/64)][8*64 + 8 + H] for fold_rows."""
     M = B * L
     if L > 192 or tuple(qkv.shape) != (M, 3 * H * 64) or tuple(dqkv.shape) != (M, 3 * H * 64) or dout.shape[0] != M:
         raise ValueError("wavlm_attention_bwd shapes")
@@ -747,7 +747,7 @@ def wavlm_attention_bwd(qkv, x, dout, gate_w, gate_b, gate_const, tbl, B, L, H, 
         raise ValueError("wavlm_attention_bwd: bias table [H, 2L-1] fp32")
     P = torch.empty(B * H * L * L, device=qkv.device, dtype=torch.float32)
     dS = torch.empty_like(P)
-    nrb = (L + 31) // 32  # AB_ROWS query rows per block (csrc/wavlm_train.hip)
+    nrb = (L + 63) // 64  # AB_ROWS query rows per block (csrc/wavlm_train.hip)
     gpart = _workspace(B * H * nrb * (8 * 64 + 8 + H), qkv.device)
     LIB("mer_wavlm_attention_bwd", B, L, H, qkv.data_ptr(), qkv.stride(0), x.data_ptr(), x.stride(0), dout.data_ptr(),
         dout.stride(0), gate_w.data_ptr(), gate_b.data_ptr(), gate_const.data_ptr(), tbl.data_ptr(), float(scale),
