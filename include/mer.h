@@ -308,15 +308,19 @@ int mer_linear_wgrad(int M, int N, int K, const void* x, const void* dy, long ld
 
 /* Backward of mer_wavlm_attention (tbl form: per-head bias table [H][2L-1]), L <= 192, on bf16 MFMA (fp32
  * operands split hi + lo).  dout fp32 [B*L][>=H*64] (gradient of the attention output; fp32 because
- * dp_ij - sum_j p_ij dp_ij cancels for peaked rows), qkv / x as in the forward (ldqkv, ldx multiples of 8, ldo of 4).
- * Writes dqkv bf16 [B*L][3*H*64] (dq | dk | dv),
- * dx_gate fp32 (the gate path's gradient of the layer input x; may be NULL), P and dS scratch float[B*H][L][L],
- * gate_part float[B*H*ceil(L/64)][8*64 + 8 + H] per-block partials of (d gru_rel_pos_linear.weight [8][64],
- * .bias [8], d gru_rel_pos_const [H]) -- fold with mer_fold_rows. */
+ * dp_ij - sum_j p_ij dp_ij cancels for peaked rows), qkv / x as in the forward (ldqkv, ldx multiples of 8, ldo and
+ * lddq of 4).  Writes dqkv bf16 [B*L][3*H*64] (dq | dk | dv), dx_gate fp32 (the gate path's gradient of the layer
+ * input x; may be NULL), gate_part float[B*H*ceil(L/64)][8*64 + 8 + H] per-block partials of
+ * (d gru_rel_pos_linear.weight [8][64], .bias [8], d gru_rel_pos_const [H]) -- fold with mer_fold_rows.
+ * scratch: B*H * KP * (3 KP + 64) bf16 (P, dS hi, dS lo, bf16 dO between the two kernels),
+ * KP = mer_wavlm_attention_bwd_kp(L). */
 int mer_wavlm_attention_bwd(int B, int L, int H, const void* qkv, long ldqkv, const void* x, long ldx,
                             const void* dout, long ldo, const float* gate_w, const float* gate_b,
-                            const float* gate_const, const float* tbl, float scale, float* P, float* dS,
+                            const float* gate_const, const float* tbl, float scale, void* scratch,
                             void* dqkv, long lddq, float* dx_gate, long lddxg, float* gate_part, void* stream);
+/* Padded key / query count of mer_wavlm_attention_bwd's scratch (16 * 4 / 8 / 10 / 12 for L <= 64 / 128 / 160 /
+ * 192; 0 when L is out of range). */
+int mer_wavlm_attention_bwd_kp(int L);
 
 /* dst[c][r] = src[r][c], bf16 (the transposed weight operands of the stage-2 data-gradient GEMMs). */
 int mer_transpose_bf16(int rows, int cols, const void* src, long lds, void* dst, long ldd, void* stream);

@@ -197,109 +197,122 @@ __global__ __launch_bounds__(256) void gelu_bwd_kernel(int rows, int cols, const
 //   dq_i = scale sum_j ds_ij k_j, dk_j = scale sum_i ds_ij q_i, dv_j = sum_i p_ij do_i
 //   dgate_i = sum_j ds_ij tbl[h][j - i + L - 1] -> gate (gru_rel_pos_linear / const) gradients + dx_gate.
 // Both kernels run their products on v_mfma_f32_16x16x32_bf16.  bf16 operands (q, k, v, x) are exact; fp32
-// operands (dO in dp, dS in dq / dk, P in dv, the gate weight) are split into bf16 hi + lo fragments, so every
-// product is fp32-accurate -- dp_ij - sum_j p_ij dp_ij cancels, and the gate-path gradients are held to 1e-4.
+// operands (dO in dp, dS in dq / dk, the gate weight) are split into bf16 hi + lo fragments, so those products
+// are fp32-accurate -- dp_ij - sum_j p_ij dp_ij cancels, and the gate-path gradients are held to 1e-4.  Only
+// dv = P^T dO runs on single bf16 P and dO (no cancellation there).
 // Fragment maps (16x16x32): A lane = (row l & 15, k 8 (l >> 4) .. +7), B lane = (col l & 15, same k),
-// C lane = (rows 4 (l >> 4) + r, col l & 15).
+// C lane = (rows 4 (l >> 4) + r, col l & 15).  Transposed operands come from row-major LDS images through
+// ds_read_b64_tr_b16 (lane 4q + p of a 16-lane group addresses row q, columns 4p..4p+3 of a 4-row block and
+// receives column (lane & 15) of the 4 rows).
+// Scratch between the two kernels (KP = key / query count padded to 16 NT): P, dS hi, dS lo as bf16
+// [B*H][KP query rows][KP keys] (rows / keys past L zero), then dO rounded to bf16 [B*H][KP][64].
 constexpr int AB_LMAX = 192;
 constexpr int AB_ROWS = 64;       // query rows per rows-kernel block (16 per wave)
-constexpr int AB_COLS = 32;       // key columns per cols-kernel block (16 per wave pair)
-constexpr int AB_KP = 72;         // bf16 row pitch of K / V in LDS (144 B: 16-byte aligned fragment reads)
+constexpr int AB_COLS = 32;       // keys per cols-kernel block (16 per wave pair)
+constexpr int AB_KP = 72;         // bf16 row pitch of K / V / Q / dO images in LDS (144 B)
+constexpr int AB_SP = 40;         // bf16 row pitch of the P / dS strips in LDS (80 B)
 constexpr int GATE_PART = 8 * 64 + 8;  // + H (gate const) per partial row
 
 __device__ __forceinline__ f32x4 mma16(bf16x8 a, bf16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;
+typedef __attribute__((ext_vector_type(2))) uint32_t u32x2;
+typedef __attribute__((ext_vector_type(4))) short s16x4;
 union AbFrag {
   bf16x8 v;
   u32x4 u;
-  uint16_t h[8];
 };
 typedef __attribute__((ext_vector_type(8))) float f32x8;
-__device__ __forceinline__ void ab_split(f32x4 a, f32x4 b, bf16x8& hi, bf16x8& lo) {
-  const f32x8 v = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+__device__ __forceinline__ void ab_split8(const f32x8 v, bf16x8& hi, bf16x8& lo) {
   hi = __builtin_convertvector(v, bf16x8);
   lo = __builtin_convertvector(v - __builtin_convertvector(hi, f32x8), bf16x8);
 }
-// sum / max over the 16 lanes of a fragment row group (lanes sharing l >> 4)
-__device__ __forceinline__ float grp_sum(float v) {
-  v += __shfl_xor(v, 1);
-  v += __shfl_xor(v, 2);
-  v += __shfl_xor(v, 4);
-  return v + __shfl_xor(v, 8);
+__device__ __forceinline__ void ab_split(f32x4 a, f32x4 b, bf16x8& hi, bf16x8& lo) {
+  ab_split8(f32x8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]}, hi, lo);
 }
-__device__ __forceinline__ float grp_max(float v) {
-  v = fmaxf(v, __shfl_xor(v, 1));
-  v = fmaxf(v, __shfl_xor(v, 2));
-  v = fmaxf(v, __shfl_xor(v, 4));
-  return fmaxf(v, __shfl_xor(v, 8));
+// 4 bf16 of a 4-row block, transposed (see above); p must be 8-byte aligned, every lane active
+__device__ __forceinline__ u32x2 tr_read(const bf16_t* p) {
+  const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p));
+  return __builtin_bit_cast(u32x2, v);
+}
+__device__ __forceinline__ bf16x8 tr_frag(const bf16_t* p0, const bf16_t* p1) {
+  const u32x2 a = tr_read(p0), b = tr_read(p1);
+  AbFrag f;
+  f.u = u32x4{a[0], a[1], b[0], b[1]};
+  return f.v;
+}
+__device__ __forceinline__ uint32_t pack2(float a, float b) {
+  return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
 }
 
-// LDS plan of the rows kernel for NT 16-key tiles (KP = 16 NT padded keys)
 template <int NT>
 struct RowsLds {
-  static constexpr int KP = 16 * NT, KTP = KP + 8, DSP = KP + 4;
-  static constexpr int ks = 0;                                   // K [KP][AB_KP] bf16
-  static constexpr int vs = ks + KP * AB_KP * 2;                 // V [KP][AB_KP] bf16
-  static constexpr int kt = vs + KP * AB_KP * 2;                 // K^T [64][KTP] bf16
-  static constexpr int ds = kt + 64 * KTP * 2;                   // per-wave dS tiles [4][16][DSP] fp32
-  static constexpr int tb = ds + 4 * 16 * DSP * 4;               // bias row tbl[h] [2 KP] fp32
-  static constexpr int bytes = tb + 2 * KP * 4;
-  static_assert(16 * DSP >= GATE_PART + 1, "gate partial reduction reuses the dS tiles");
+  static constexpr int KP = 16 * NT;
+  static constexpr int ks = 0;                    // K [KP][AB_KP] bf16
+  static constexpr int vs = ks + KP * AB_KP * 2;  // V [KP][AB_KP] bf16; the gate partial reduction reuses it
+  static constexpr int tb = vs + KP * AB_KP * 2;  // bias row tbl[h] [512] fp32 (2L - 1 used)
+  static constexpr int bytes = tb + 512 * 4;
+  static_assert(KP * AB_KP * 2 >= 4 * (GATE_PART + 1) * 4, "gate partial reduction reuses the V image");
 };
 
-// Rows kernel: block = 64 query rows of one (b, h), 4 waves x 16 rows.  Stages K, V (row-major, the B operands of
-// S = Q K^T and dP = dO V^T) and K^T (the B operand of dQ = dS K) in LDS with zero rows past L; each wave
-// keeps its 16 x KP score / dP tiles in registers (softmax, dS, dgate by 16-lane shuffles), writes P and dS rows
-// (fp32 scratch [B*H][L][L]) for the cols kernel, stages its dS tile in LDS for dQ, and folds the gate backward
-// into the per-block partial row [8][64] weight, [8] bias, [H] const (this head's entry only).
+// Rows kernel (one-dimensional grid, XCD-aware block -> (row block, b*h)): block = 64 query rows of one (b, h), 4 waves x 16 rows, query row on the lane (l & 15).  Stages K,
+// V row-major in LDS (zero rows past L).  Per wave, in registers: S^T = K Q^T and dP^T = V dO^T tiles (keys on
+// the accumulator rows), softmax / dS / dgate by register sums + 2 shuffles, dQ^T = K^T dS^T with dS^T taken
+// straight from the accumulators (tile pair -> one k step, K^T by transposed LDS reads in the matching k order).
+// Writes P / dS hi / dS lo scratch rows, dq, dx_gate and the per-block gate partial row
+// [8][64] weight, [8] bias, [H] const (this head's entry only).
 template <int NT>
 __global__ __launch_bounds__(256) void wavlm_attn_bwd_rows_kernel(
     int L, int H, const bf16_t* __restrict__ qkv, long ldqkv, const bf16_t* __restrict__ x, long ldx,
     const float* __restrict__ dout, long ldo, const float* __restrict__ gate_w, const float* __restrict__ gate_b,
-    const float* __restrict__ gate_c, const float* __restrict__ tbl, float scale, float* __restrict__ Pbuf,
-    float* __restrict__ dSbuf, bf16_t* __restrict__ dqkv, long lddq, float* __restrict__ dxg, long lddxg,
-    float* __restrict__ gpart) {
+    const float* __restrict__ gate_c, const float* __restrict__ tbl, float scale, int nbh, bf16_t* __restrict__ scr,
+    bf16_t* __restrict__ dqkv, long lddq, float* __restrict__ dxg, long lddxg, float* __restrict__ gpart) {
   typedef RowsLds<NT> Ly;
-  constexpr int KP = Ly::KP, KTP = Ly::KTP, DSP = Ly::DSP;
+  constexpr int KP = Ly::KP;
   extern __shared__ __attribute__((aligned(16))) unsigned char ab_smem[];
   bf16_t* Ks = reinterpret_cast<bf16_t*>(ab_smem + Ly::ks);
   bf16_t* Vs = reinterpret_cast<bf16_t*>(ab_smem + Ly::vs);
-  bf16_t* KsT = reinterpret_cast<bf16_t*>(ab_smem + Ly::kt);
-  float* dSw = reinterpret_cast<float*>(ab_smem + Ly::ds);
   float* tbs = reinterpret_cast<float*>(ab_smem + Ly::tb);
-  const int bh = blockIdx.y, b = bh / H, h = bh - b * H;
+  const int nrb = (L + AB_ROWS - 1) / AB_ROWS;
+  int rb, bh;  // the row blocks of one (b, h) share its K / V: keep them on one XCD (one L2)
+  xcd_tile(blockIdx.x, nrb, nrb * nbh, rb, bh);
+  const int b = bh / H, h = bh - b * H;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6, fr = lane & 15, fq = lane >> 4, fk = 8 * fq;
   const int D = H * 64;
-  // stage K, V (16-byte chunks) and K^T; rows L..KP-1 are zero (their products must be finite zeros)
-  for (int ch = t; ch < KP * 8; ch += 256) {
-    const int j = ch >> 3, c8 = (ch & 7) * 8;
-    const long g = (long)(b * L + (j < L ? j : L - 1)) * ldqkv + h * 64 + c8;
-    u32x4 kv = *reinterpret_cast<const u32x4*>(qkv + g + D);
-    u32x4 vv = *reinterpret_cast<const u32x4*>(qkv + g + 2 * D);
-    if (j >= L) kv = vv = u32x4{0u, 0u, 0u, 0u};
-    *reinterpret_cast<u32x4*>(Ks + j * AB_KP + c8) = kv;
-    *reinterpret_cast<u32x4*>(Vs + j * AB_KP + c8) = vv;
+  // staging loads all issued before the first LDS store (KP * 8 16-byte chunks = NT / 2 per thread)
+  u32x4 kv[NT / 2], vv[NT / 2];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      KsT[(c8 + 2 * e) * KTP + j] = (bf16_t)(kv[e] & 0xffff);
-      KsT[(c8 + 2 * e + 1) * KTP + j] = (bf16_t)(kv[e] >> 16);
-    }
+  for (int it = 0; it < NT / 2; ++it) {
+    const int ch = t + 256 * it, j = ch >> 3, c8 = (ch & 7) * 8;
+    const long g = (long)(b * L + (j < L ? j : L - 1)) * ldqkv + h * 64 + c8;
+    kv[it] = *reinterpret_cast<const u32x4*>(qkv + g + D);
+    vv[it] = *reinterpret_cast<const u32x4*>(qkv + g + 2 * D);
   }
   const float* th = tbl + (long)h * (2 * L - 1);
-  for (int k = t; k < 2 * L - 1; k += 256) tbs[k] = th[k];
+  const float tb_a = th[min(t, 2 * L - 2)], tb_b = th[min(t + 256, 2 * L - 2)];
 
-  // this wave's operand fragments: q, x (bf16, exact), dO split, gate weight split (cols 0..7 valid)
-  const int i0 = blockIdx.x * AB_ROWS + w * 16;
-  const long rowa = (long)(b * L + (i0 + fr < L ? i0 + fr : L - 1));
-  AbFrag qa[2], xa[2];
+  // B operands (query row i = i0 + (l & 15) on the lane): q, x exact, dO split; A operand: gate weight rows split
+  const int i0 = rb * AB_ROWS + w * 16, i = i0 + fr;
+  // gate-backward operands, loaded now so their latency hides behind the staging (lane = d): the wave's 16 x
+  // rows, column sums of the gate weight halves
+  bf16_t xr[16];
+#pragma unroll
+  for (int rr = 0; rr < 16; ++rr) xr[rr] = x[(long)(b * L + min(i0 + rr, L - 1)) * ldx + h * 64 + lane];
+  float wsa = 0.f, wsb = 0.f;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    wsa += gate_w[r * 64 + lane];
+    wsb += gate_w[(r + 4) * 64 + lane];
+  }
+  const long rowa = (long)(b * L + (i < L ? i : L - 1));
+  AbFrag qb[2], xb[2];
   bf16x8 oh[2], ol[2], gh[2], gl[2];
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
     const int c = h * 64 + 32 * s + fk;
-    qa[s].u = *reinterpret_cast<const u32x4*>(qkv + rowa * ldqkv + c);
-    xa[s].u = *reinterpret_cast<const u32x4*>(x + rowa * ldx + c);
+    qb[s].u = *reinterpret_cast<const u32x4*>(qkv + rowa * ldqkv + c);
+    xb[s].u = *reinterpret_cast<const u32x4*>(x + rowa * ldx + c);
     const float* po = dout + rowa * ldo + c;
     ab_split(*reinterpret_cast<const f32x4*>(po), *reinterpret_cast<const f32x4*>(po + 4), oh[s], ol[s]);
     const float* pw = gate_w + (fr & 7) * 64 + 32 * s + fk;
@@ -307,27 +320,37 @@ __global__ __launch_bounds__(256) void wavlm_attn_bwd_rows_kernel(
     if (fr >= 8) w0 = w1 = f32x4{0.f, 0.f, 0.f, 0.f};
     ab_split(w0, w1, gh[s], gl[s]);
   }
-  // gate (TF:167-177): z[row][n] = x_h . gate_w[n] + gate_b[n]; pa = sum n<4, pb = sum 4<=n<8
+#pragma unroll
+  for (int it = 0; it < NT / 2; ++it) {
+    const int ch = t + 256 * it, j = ch >> 3, c8 = (ch & 7) * 8;
+    const bool jv = j < L;
+    *reinterpret_cast<u32x4*>(Ks + j * AB_KP + c8) = jv ? kv[it] : u32x4{0u, 0u, 0u, 0u};
+    *reinterpret_cast<u32x4*>(Vs + j * AB_KP + c8) = jv ? vv[it] : u32x4{0u, 0u, 0u, 0u};
+  }
+  tbs[t] = tb_a;
+  tbs[t + 256] = tb_b;
+  // dO rounded to bf16 for the cols kernel's dV (scratch plane 3, [B*H][KP][64])
+  if (i < KP) {
+    bf16_t* od = scr + 3 * (long)nbh * KP * KP + ((long)bh * KP + i) * 64 + fk;
+    *reinterpret_cast<bf16x8*>(od) = oh[0];
+    *reinterpret_cast<bf16x8*>(od + 32) = oh[1];
+  }
+  // gate (TF:167-177): z^T[n][i] = gate_w[n] . x_h[i]; pa = sum_{n<4} (z + b), pb = sum_{4<=n<8} (z + b)
   f32x4 z = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
-    z = mma16(xa[s].v, gh[s], z);
-    z = mma16(xa[s].v, gl[s], z);
+    z = mma16(gh[s], xb[s].v, z);
+    z = mma16(gl[s], xb[s].v, z);
   }
-  const float gbn = fr < 8 ? gate_b[fr & 7] : 0.f, gc = gate_c[h];
-  float ga[4], gb[4], gate[4];
+  float zs = 0.f;
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    float v = fr < 8 ? z[r] + gbn : 0.f;
-    v += __shfl_xor(v, 1);
-    v += __shfl_xor(v, 2);
-    ga[r] = sigmoidf_(__shfl(v, fq * 16));
-    gb[r] = sigmoidf_(__shfl(v, fq * 16 + 4));
-    gate[r] = ga[r] * (gb[r] * gc - 1.f) + 2.f;
-  }
+  for (int r = 0; r < 4; ++r) zs += z[r] + gate_b[(4 * fq + r) & 7];
+  const float ga = sigmoidf_(__shfl(zs, fr)), gb = sigmoidf_(__shfl(zs, 16 + fr));
+  const float gc = gate_c[h];
+  const float gate = ga * (gb * gc - 1.f) + 2.f;
   __syncthreads();
 
-  // S = Q K^T (exact), dP = dO V^T (split dO): 16 x KP per wave in registers
+  // S^T = K Q^T (exact), dP^T = V dO^T (split dO): key rows 16 tt + 4 fq + r in the registers
   f32x4 s[NT], dp[NT];
 #pragma unroll
   for (int tt = 0; tt < NT; ++tt) {
@@ -339,139 +362,120 @@ __global__ __launch_bounds__(256) void wavlm_attn_bwd_rows_kernel(
     v0.u = *reinterpret_cast<const u32x4*>(vr);
     v1.u = *reinterpret_cast<const u32x4*>(vr + 32);
     const f32x4 zz = f32x4{0.f, 0.f, 0.f, 0.f};
-    s[tt] = mma16(qa[1].v, k1.v, mma16(qa[0].v, k0.v, zz));
-    f32x4 d = mma16(oh[0], v0.v, zz);
-    d = mma16(ol[0], v0.v, d);
-    d = mma16(oh[1], v1.v, d);
-    dp[tt] = mma16(ol[1], v1.v, d);
+    s[tt] = mma16(k1.v, qb[1].v, mma16(k0.v, qb[0].v, zz));
+    f32x4 d = mma16(v0.v, oh[0], zz);
+    d = mma16(v0.v, ol[0], d);
+    d = mma16(v1.v, oh[1], d);
+    dp[tt] = mma16(v1.v, ol[1], d);
   }
-  const int ib = i0 + 4 * fq;  // this lane's rows ib + r
   const int tmax = 2 * L - 2;
-  float mx[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+  const int tb0 = L - 1 - i + 4 * fq;  // tbl index of key 4 fq (+ 16 tt + r)
+  float mx = -INFINITY;
 #pragma unroll
-  for (int tt = 0; tt < NT; ++tt) {
-    const int j = 16 * tt + fr;
+  for (int tt = 0; tt < NT; ++tt)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int k = min(max(j - (ib + r) + L - 1, 0), tmax);
-      const float v = j < L ? s[tt][r] * scale + gate[r] * tbs[k] : -INFINITY;
+      const int j = 16 * tt + 4 * fq + r;
+      const float v = j < L ? s[tt][r] * scale + gate * tbs[min(max(tb0 + 16 * tt + r, 0), tmax)] : -INFINITY;
       s[tt][r] = v;
-      mx[r] = fmaxf(mx[r], v);
+      mx = fmaxf(mx, v);
     }
-  }
-  float sum[4], Dr[4], dg[4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    mx[r] = grp_max(mx[r]);
-    sum[r] = 0.f;
-  }
+  mx = fmaxf(mx, __shfl_xor(mx, 16));
+  mx = fmaxf(mx, __shfl_xor(mx, 32));
+  float sum = 0.f;
 #pragma unroll
   for (int tt = 0; tt < NT; ++tt)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      s[tt][r] = __expf(s[tt][r] - mx[r]);
-      sum[r] += s[tt][r];
+      s[tt][r] = __expf(s[tt][r] - mx);
+      sum += s[tt][r];
     }
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    sum[r] = 1.f / grp_sum(sum[r]);
-    Dr[r] = 0.f;
-  }
+  sum += __shfl_xor(sum, 16);
+  sum += __shfl_xor(sum, 32);
+  const float inv = 1.f / sum;
+  float Dr = 0.f;
 #pragma unroll
   for (int tt = 0; tt < NT; ++tt)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      s[tt][r] *= sum[r];
-      Dr[r] += s[tt][r] * dp[tt][r];
+      s[tt][r] *= inv;
+      Dr += s[tt][r] * dp[tt][r];
     }
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    Dr[r] = grp_sum(Dr[r]);
-    dg[r] = 0.f;
-  }
-  float* dsw = dSw + w * 16 * DSP;
+  Dr += __shfl_xor(Dr, 16);
+  Dr += __shfl_xor(Dr, 32);
+  // dS (0 for keys past L: p = 0, dp = 0), dgate, scratch rows (zero for query rows past L)
+  const bool iv = i < L;
+  const long so = ((long)bh * KP + i) * KP + 4 * fq;
+  const long plane = (long)nbh * KP * KP;
+  float dg = 0.f;
 #pragma unroll
   for (int tt = 0; tt < NT; ++tt) {
-    const int j = 16 * tt + fr;
+    float hv[4], lv[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int i = ib + r;
-      const float ds = s[tt][r] * (dp[tt][r] - Dr[r]);  // 0 for keys past L (p = 0, dp = 0)
-      dg[r] += ds * tbs[min(max(j - i + L - 1, 0), tmax)];
-      dsw[(4 * fq + r) * DSP + j] = ds;
-      if (i < L && j < L) {
-        const long o = ((long)bh * L + i) * L + j;
-        Pbuf[o] = s[tt][r];
-        dSbuf[o] = ds;
-      }
+      const float ds = s[tt][r] * (dp[tt][r] - Dr);
+      dg += ds * tbs[min(max(tb0 + 16 * tt + r, 0), tmax)];
+      dp[tt][r] = ds;
+      const float hi = __builtin_bit_cast(float, (uint32_t)f2bf(ds) << 16);
+      hv[r] = iv ? hi : 0.f;
+      lv[r] = iv ? ds - hi : 0.f;
+    }
+    if (i < KP) {
+      const u32x2 pv = iv ? u32x2{pack2(s[tt][0], s[tt][1]), pack2(s[tt][2], s[tt][3])} : u32x2{0u, 0u};
+      *reinterpret_cast<u32x2*>(scr + so + 16 * tt) = pv;
+      *reinterpret_cast<u32x2*>(scr + plane + so + 16 * tt) = u32x2{pack2(hv[0], hv[1]), pack2(hv[2], hv[3])};
+      *reinterpret_cast<u32x2*>(scr + 2 * plane + so + 16 * tt) = u32x2{pack2(lv[0], lv[1]), pack2(lv[2], lv[3])};
     }
   }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  dg += __shfl_xor(dg, 16);
+  dg += __shfl_xor(dg, 32);
 
-  // dQ = scale dS K: A = this wave's dS tile (split), B = K^T rows (exact); 4 tiles of 16 dims
+  // dQ^T = K^T dS^T: k step ks = key tiles 2ks (elements 0..3) and 2ks + 1 (elements 4..7), split dS; the K^T
+  // fragment reads the same keys: rows 32 ks + 4 fq + q (+ 16), columns 16 c + 4 p
   f32x4 dq[4];
 #pragma unroll
   for (int c = 0; c < 4; ++c) dq[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int tq = fr >> 2, tp = fr & 3;
 #pragma unroll
-  for (int ks = 0; ks < KP / 32; ++ks) {
-    const float* ap = dsw + fr * DSP + 32 * ks + fk;
+  for (int ks = 0; ks < NT / 2; ++ks) {
     bf16x8 ah, al;
-    ab_split(*reinterpret_cast<const f32x4*>(ap), *reinterpret_cast<const f32x4*>(ap + 4), ah, al);
+    ab_split8(f32x8{dp[2 * ks][0], dp[2 * ks][1], dp[2 * ks][2], dp[2 * ks][3], dp[2 * ks + 1][0],
+                    dp[2 * ks + 1][1], dp[2 * ks + 1][2], dp[2 * ks + 1][3]},
+              ah, al);
+    const bf16_t* kp = Ks + (32 * ks + 4 * fq + tq) * AB_KP + 4 * tp;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-      AbFrag kb;
-      kb.u = *reinterpret_cast<const u32x4*>(KsT + (16 * c + fr) * KTP + 32 * ks + fk);
-      dq[c] = mma16(ah, kb.v, dq[c]);
-      dq[c] = mma16(al, kb.v, dq[c]);
+      const bf16x8 kt = tr_frag(kp + 16 * c, kp + 16 * AB_KP + 16 * c);
+      dq[c] = mma16(kt, ah, dq[c]);
+      dq[c] = mma16(kt, al, dq[c]);
     }
   }
+  if (iv) {
+    bf16_t* o = dqkv + (long)(b * L + i) * lddq + h * 64 + 4 * fq;
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int i = ib + r;
-    if (i < L) {
-      bf16_t* o = dqkv + (long)(b * L + i) * lddq + h * 64 + fr;
-#pragma unroll
-      for (int c = 0; c < 4; ++c) o[16 * c] = f2bf(dq[c][r] * scale);
-    }
+    for (int c = 0; c < 4; ++c)
+      *reinterpret_cast<u32x2*>(o + 16 * c) =
+          u32x2{pack2(dq[c][0] * scale, dq[c][1] * scale), pack2(dq[c][2] * scale, dq[c][3] * scale)};
   }
 
-  // gate backward: gate = ga (gb c - 1) + 2, pa / pb = sums of 4 projections each
-  float dpa[4], dpb[4], gcl = 0.f, gal = 0.f, gbl = 0.f;
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const float g = ib + r < L ? grp_sum(dg[r]) : 0.f;
-    dpa[r] = g * (gb[r] * gc - 1.f) * ga[r] * (1.f - ga[r]);
-    dpb[r] = g * ga[r] * gc * gb[r] * (1.f - gb[r]);
-    gcl += g * ga[r] * gb[r];
-    gal += dpa[r];
-    gbl += dpb[r];
-  }
-  // lane = d: dW[n][d] += dp{a,b} x[row][d] over the wave's 16 rows, dx_gate = dpa wsa + dpb wsb
-  float wsa = 0.f, wsb = 0.f;
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    wsa += gate_w[r * 64 + lane];
-    wsb += gate_w[(r + 4) * 64 + lane];
-  }
-  float xd[16];
-#pragma unroll
-  for (int rr = 0; rr < 16; ++rr) xd[rr] = bf2f(x[(long)(b * L + min(i0 + rr, L - 1)) * ldx + h * 64 + lane]);
+  // gate backward: gate = ga (gb c - 1) + 2, pa / pb sums of 4 projections each (query row i on lane l & 15)
+  const float g = iv ? dg : 0.f;
+  const float dpa = g * (gb * gc - 1.f) * ga * (1.f - ga);
+  const float dpb = g * ga * gc * gb * (1.f - gb);
+  // lane = d: dW[n][d] += dp{a,b}(i) x[i][d] over the wave's 16 rows, dx_gate = dpa wsa + dpb wsb
   float wa = 0.f, wb = 0.f;
 #pragma unroll
   for (int rr = 0; rr < 16; ++rr) {
-    const float a = __shfl(dpa[rr & 3], (rr >> 2) * 16), c = __shfl(dpb[rr & 3], (rr >> 2) * 16);
-    wa += a * xd[rr];
-    wb += c * xd[rr];
+    const float a = __shfl(dpa, rr), c = __shfl(dpb, rr);
+    wa += a * bf2f(xr[rr]);
+    wb += c * bf2f(xr[rr]);
     if (dxg && i0 + rr < L) dxg[(long)(b * L + i0 + rr) * lddxg + h * 64 + lane] = a * wsa + c * wsb;
   }
-  // one copy per 16-lane group of the row-replicated sums
-  gal = __shfl(gal, 0) + __shfl(gal, 16) + __shfl(gal, 32) + __shfl(gal, 48);
-  gbl = __shfl(gbl, 0) + __shfl(gbl, 16) + __shfl(gbl, 32) + __shfl(gbl, 48);
-  gcl = __shfl(gcl, 0) + __shfl(gcl, 16) + __shfl(gcl, 32) + __shfl(gcl, 48);
-  __syncthreads();  // every wave is done with its dS tile: reuse them for the block reduction
-  float* red = dSw;  // [4][GATE_PART + 1]
+  // row sums over the wave's 16 rows (lanes 0..15 hold one copy each)
+  const float gal = wave_sum(fq == 0 ? dpa : 0.f), gbl = wave_sum(fq == 0 ? dpb : 0.f);
+  const float gcl = wave_sum(fq == 0 ? g * ga * gb : 0.f);
+  __syncthreads();  // every wave is past dP: the V image becomes the block reduction buffer
+  float* red = reinterpret_cast<float*>(Vs);  // [4][GATE_PART + 1]
   constexpr int RP = GATE_PART + 1;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
@@ -481,7 +485,7 @@ __global__ __launch_bounds__(256) void wavlm_attn_bwd_rows_kernel(
   if (lane < 8) red[w * RP + 512 + lane] = lane < 4 ? gal : gbl;
   if (lane == 0) red[w * RP + GATE_PART] = gcl;
   __syncthreads();
-  float* pr = gpart + ((long)bh * gridDim.x + blockIdx.x) * (GATE_PART + H);
+  float* pr = gpart + ((long)bh * nrb + rb) * (GATE_PART + H);
   for (int k = t; k < GATE_PART + H; k += 256) {
     float v;
     if (k < GATE_PART) v = ((red[k] + red[RP + k]) + red[2 * RP + k]) + red[3 * RP + k];
@@ -493,93 +497,96 @@ __global__ __launch_bounds__(256) void wavlm_attn_bwd_rows_kernel(
   }
 }
 
-// LDS plan of the cols kernel for NI 32-row query steps (IP = 32 NI padded query rows)
-template <int NI>
+template <int NT>
 struct ColsLds {
-  static constexpr int IP = 32 * NI, TP = IP + 4, BP = IP + 8;
-  static constexpr int ps = 0;                      // P^T strip [32][TP] fp32
-  static constexpr int ds = ps + 32 * TP * 4;       // dS^T strip [32][TP] fp32
-  static constexpr int qt = ds + 32 * TP * 4;       // Q^T [64][BP] bf16
-  static constexpr int ot = qt + 64 * BP * 2;       // dO^T [64][BP] bf16
-  static constexpr int bytes = ot + 64 * BP * 2;
+  static constexpr int KP = 16 * NT;
+  static constexpr int qs = 0;                          // Q [KP][AB_KP] bf16
+  static constexpr int os = qs + KP * AB_KP * 2;        // dO (bf16) [KP][AB_KP]
+  static constexpr int ps = os + KP * AB_KP * 2;        // P, dS hi, dS lo strips [3][KP][AB_SP] bf16
+  static constexpr int bytes = ps + 3 * KP * AB_SP * 2;
 };
 
 // Cols kernel: block = 32 keys of one (b, h); wave w = (key half w & 1, dim half w >> 1).
-//   dK = scale dS^T Q (split dS, exact q), dV = P^T dO (split P; dO rounded to bf16 -- dv has no cancellation).
-// The P / dS column strips are staged transposed (contiguous A fragments), Q / dO transposed (contiguous B).
-template <int NI>
+//   dK^T = scale Q^T dS (split dS), dV^T = dO^T P (bf16 dO, P).  Q, dO and the block's P / dS column strips are
+// staged row-major (query rows); every fragment (k = query row) is a transposed LDS read.  One-dimensional grid,
+// XCD-aware (xcd_tile): block -> (key block, b*h).
+template <int NT>
 __global__ __launch_bounds__(256) void wavlm_attn_bwd_cols_kernel(int L, int H, const bf16_t* __restrict__ qkv,
-                                                                  long ldqkv, const float* __restrict__ dout, long ldo,
-                                                                  const float* __restrict__ Pbuf,
-                                                                  const float* __restrict__ dSbuf, float scale,
-                                                                  bf16_t* __restrict__ dqkv, long lddq) {
-  typedef ColsLds<NI> Ly;
-  constexpr int IP = Ly::IP, TP = Ly::TP, BP = Ly::BP;
+                                                                  long ldqkv, int nbh, const bf16_t* __restrict__ scr,
+                                                                  float scale, bf16_t* __restrict__ dqkv, long lddq) {
+  typedef ColsLds<NT> Ly;
+  constexpr int KP = Ly::KP;
   extern __shared__ __attribute__((aligned(16))) unsigned char ab_smem[];
-  float* PsT = reinterpret_cast<float*>(ab_smem + Ly::ps);
-  float* DsT = reinterpret_cast<float*>(ab_smem + Ly::ds);
-  bf16_t* QT = reinterpret_cast<bf16_t*>(ab_smem + Ly::qt);
-  bf16_t* OT = reinterpret_cast<bf16_t*>(ab_smem + Ly::ot);
-  const int bh = blockIdx.y, b = bh / H, h = bh - b * H;
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6, fr = lane & 15, fq = lane >> 4, fk = 8 * fq;
+  bf16_t* Qs = reinterpret_cast<bf16_t*>(ab_smem + Ly::qs);
+  bf16_t* Os = reinterpret_cast<bf16_t*>(ab_smem + Ly::os);
+  bf16_t* Ss = reinterpret_cast<bf16_t*>(ab_smem + Ly::ps);
+  constexpr int NKB = KP / AB_COLS;
+  int kb, bh;  // the key blocks of one (b, h) share its Q / dO: keep them on one XCD
+  xcd_tile(blockIdx.x, NKB, NKB * nbh, kb, bh);
+  const int b = bh / H, h = bh - b * H;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, fr = lane & 15, fq = lane >> 4;
   const int D = H * 64;
-  const int j0 = blockIdx.x * AB_COLS;
-  for (int ch = t; ch < IP * 8; ch += 256) {
-    const int i = ch >> 3, c8 = (ch & 7) * 8;
-    const long row = (long)(b * L + (i < L ? i : L - 1));
-    const u32x4 qv = *reinterpret_cast<const u32x4*>(qkv + row * ldqkv + h * 64 + c8);
-    const f32x4 o0 = *reinterpret_cast<const f32x4*>(dout + row * ldo + h * 64 + c8);
-    const f32x4 o1 = *reinterpret_cast<const f32x4*>(dout + row * ldo + h * 64 + c8 + 4);
-    const bool ok = i < L;
+  const int j0 = kb * AB_COLS;
+  const long plane = (long)nbh * KP * KP;
+  // all staging loads in flight before the first LDS store.  Query rows past L: any finite values (their P / dS
+  // rows are zero).  Q from qkv, dO as the rows kernel's bf16 copy, 4 16-byte chunks per strip row and plane.
+  constexpr int NS = (3 * KP * 4 + 255) / 256;
+  u32x4 qv[NT / 2], ov[NT / 2], sv[NS];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      QT[(c8 + 2 * e) * BP + i] = ok ? (bf16_t)(qv[e] & 0xffff) : (bf16_t)0;
-      QT[(c8 + 2 * e + 1) * BP + i] = ok ? (bf16_t)(qv[e] >> 16) : (bf16_t)0;
-      OT[(c8 + e) * BP + i] = ok ? f2bf(o0[e]) : (bf16_t)0;
-      OT[(c8 + 4 + e) * BP + i] = ok ? f2bf(o1[e]) : (bf16_t)0;
-    }
+  for (int it = 0; it < NT / 2; ++it) {
+    const int ch = t + 256 * it, i = ch >> 3, c8 = (ch & 7) * 8;
+    qv[it] = *reinterpret_cast<const u32x4*>(qkv + (long)(b * L + (i < L ? i : L - 1)) * ldqkv + h * 64 + c8);
+    ov[it] = *reinterpret_cast<const u32x4*>(scr + 3 * plane + ((long)bh * KP + i) * 64 + c8);
   }
-  for (int e = t; e < IP * AB_COLS; e += 256) {
-    const int i = e >> 5, jc = e & 31, j = j0 + jc;
-    const long o = ((long)bh * L + (i < L ? i : L - 1)) * L + (j < L ? j : L - 1);
-    const float pv = Pbuf[o], dv = dSbuf[o];
-    const bool ok = i < L && j < L;
-    PsT[jc * TP + i] = ok ? pv : 0.f;
-    DsT[jc * TP + i] = ok ? dv : 0.f;
+#pragma unroll
+  for (int it = 0; it < NS; ++it) {
+    const int ch = min(t + 256 * it, 3 * KP * 4 - 1);
+    const int pl = ch / (KP * 4), rem = ch - pl * KP * 4, i = rem >> 2, c8 = (rem & 3) * 8;
+    sv[it] = *reinterpret_cast<const u32x4*>(scr + pl * plane + ((long)bh * KP + i) * KP + j0 + c8);
+  }
+#pragma unroll
+  for (int it = 0; it < NT / 2; ++it) {
+    const int ch = t + 256 * it, i = ch >> 3, c8 = (ch & 7) * 8;
+    *reinterpret_cast<u32x4*>(Qs + i * AB_KP + c8) = qv[it];
+    *reinterpret_cast<u32x4*>(Os + i * AB_KP + c8) = ov[it];
+  }
+#pragma unroll
+  for (int it = 0; it < NS; ++it) {
+    const int ch = t + 256 * it;
+    const int pl = ch / (KP * 4), rem = ch - pl * KP * 4, i = rem >> 2, c8 = (rem & 3) * 8;
+    if (ch < 3 * KP * 4) *reinterpret_cast<u32x4*>(Ss + (pl * KP + i) * AB_SP + c8) = sv[it];
   }
   __syncthreads();
-  const int kt = w & 1, dd = w >> 1;
+  const int kt = w & 1, dd = w >> 1, tq = fr >> 2, tp = fr & 3;
   f32x4 dk[2], dv[2];
 #pragma unroll
   for (int c = 0; c < 2; ++c) dk[c] = dv[c] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int ks = 0; ks < NI; ++ks) {
-    const int a = (16 * kt + fr) * TP + 32 * ks + fk;
-    bf16x8 dh, dl, ph, pl;
-    ab_split(*reinterpret_cast<const f32x4*>(DsT + a), *reinterpret_cast<const f32x4*>(DsT + a + 4), dh, dl);
-    ab_split(*reinterpret_cast<const f32x4*>(PsT + a), *reinterpret_cast<const f32x4*>(PsT + a + 4), ph, pl);
+  for (int ks = 0; ks < NT / 2; ++ks) {
+    const int r0 = 32 * ks + 8 * fq + tq;  // rows r0 and r0 + 4 feed elements 0..3 / 4..7
+    const bf16_t* sp = Ss + r0 * AB_SP + 16 * kt + 4 * tp;
+    const bf16x8 pf = tr_frag(sp, sp + 4 * AB_SP);
+    const bf16x8 dh = tr_frag(sp + KP * AB_SP, sp + (KP + 4) * AB_SP);
+    const bf16x8 dl = tr_frag(sp + 2 * KP * AB_SP, sp + (2 * KP + 4) * AB_SP);
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
-      const int n = 32 * dd + 16 * c + fr;
-      AbFrag qb, ob;
-      qb.u = *reinterpret_cast<const u32x4*>(QT + n * BP + 32 * ks + fk);
-      ob.u = *reinterpret_cast<const u32x4*>(OT + n * BP + 32 * ks + fk);
-      dk[c] = mma16(dh, qb.v, dk[c]);
-      dk[c] = mma16(dl, qb.v, dk[c]);
-      dv[c] = mma16(ph, ob.v, dv[c]);
-      dv[c] = mma16(pl, ob.v, dv[c]);
+      const int n0 = 32 * dd + 16 * c + 4 * tp;
+      const bf16x8 qf = tr_frag(Qs + r0 * AB_KP + n0, Qs + (r0 + 4) * AB_KP + n0);
+      const bf16x8 of = tr_frag(Os + r0 * AB_KP + n0, Os + (r0 + 4) * AB_KP + n0);
+      dk[c] = mma16(qf, dh, dk[c]);
+      dk[c] = mma16(qf, dl, dk[c]);
+      dv[c] = mma16(of, pf, dv[c]);
     }
   }
+  // C: rows d = 32 dd + 16 c + 4 fq + r, column key j0 + 16 kt + (l & 15)
+  const int j = j0 + 16 * kt + fr;
+  if (j < L) {
+    bf16_t* o = dqkv + (long)(b * L + j) * lddq + h * 64 + 32 * dd + 4 * fq;
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int j = j0 + 16 * kt + 4 * fq + r;
-    if (j < L) {
-      bf16_t* o = dqkv + (long)(b * L + j) * lddq + h * 64 + 32 * dd + fr;
-#pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        o[D + 16 * c] = f2bf(dk[c][r] * scale);
-        o[2 * D + 16 * c] = f2bf(dv[c][r]);
-      }
+    for (int c = 0; c < 2; ++c) {
+      *reinterpret_cast<u32x2*>(o + D + 16 * c) =
+          u32x2{pack2(dk[c][0] * scale, dk[c][1] * scale), pack2(dk[c][2] * scale, dk[c][3] * scale)};
+      *reinterpret_cast<u32x2*>(o + 2 * D + 16 * c) = u32x2{pack2(dv[c][0], dv[c][1]), pack2(dv[c][2], dv[c][3])};
     }
   }
 }
@@ -587,21 +594,26 @@ __global__ __launch_bounds__(256) void wavlm_attn_bwd_cols_kernel(int L, int H, 
 template <int NT>
 int wavlm_attention_bwd_launch(int B, int L, int H, const bf16_t* qkv, long ldqkv, const bf16_t* x, long ldx,
                                const float* dout, long ldo, const float* gate_w, const float* gate_b,
-                               const float* gate_c, const float* tbl, float scale, float* P, float* dS, bf16_t* dqkv,
+                               const float* gate_c, const float* tbl, float scale, bf16_t* scr, bf16_t* dqkv,
                                long lddq, float* dxg, long lddxg, float* gpart, hipStream_t st) {
-  constexpr int rb = RowsLds<NT>::bytes, cb = ColsLds<NT / 2>::bytes;
+  constexpr int rb = RowsLds<NT>::bytes, cb = ColsLds<NT>::bytes;
   static_assert(rb <= 160 * 1024 && cb <= 160 * 1024, "LDS");
   if (hipFuncSetAttribute(reinterpret_cast<const void*>(&wavlm_attn_bwd_rows_kernel<NT>),
                           hipFuncAttributeMaxDynamicSharedMemorySize, rb) != hipSuccess ||
-      hipFuncSetAttribute(reinterpret_cast<const void*>(&wavlm_attn_bwd_cols_kernel<NT / 2>),
+      hipFuncSetAttribute(reinterpret_cast<const void*>(&wavlm_attn_bwd_cols_kernel<NT>),
                           hipFuncAttributeMaxDynamicSharedMemorySize, cb) != hipSuccess)
     return (int)hipErrorInvalidConfiguration;
-  hipLaunchKernelGGL(wavlm_attn_bwd_rows_kernel<NT>, dim3((L + AB_ROWS - 1) / AB_ROWS, B * H), dim3(256), rb, st, L, H,
-                     qkv, ldqkv, x, ldx, dout, ldo, gate_w, gate_b, gate_c, tbl, scale, P, dS, dqkv, lddq, dxg, lddxg,
-                     gpart);
-  hipLaunchKernelGGL(wavlm_attn_bwd_cols_kernel<NT / 2>, dim3((L + AB_COLS - 1) / AB_COLS, B * H), dim3(256), cb, st,
-                     L, H, qkv, ldqkv, dout, ldo, P, dS, scale, dqkv, lddq);
+  hipLaunchKernelGGL(wavlm_attn_bwd_rows_kernel<NT>, dim3((L + AB_ROWS - 1) / AB_ROWS * B * H), dim3(256), rb, st, L,
+                     H, qkv, ldqkv, x, ldx, dout, ldo, gate_w, gate_b, gate_c, tbl, scale, B * H, scr, dqkv, lddq, dxg,
+                     lddxg, gpart);
+  hipLaunchKernelGGL(wavlm_attn_bwd_cols_kernel<NT>, dim3(16 * NT / AB_COLS * B * H), dim3(256), cb, st, L, H, qkv,
+                     ldqkv, B * H, scr, scale, dqkv, lddq);
   return (int)hipGetLastError();
+}
+
+int ab_tiles(int L) {  // 16-key tiles the kernels are built for: 4 / 8 / 10 / 12 (L <= 64 / 128 / 160 / 192)
+  const int nt = (L + 15) / 16;
+  return nt <= 4 ? 4 : nt <= 8 ? 8 : nt <= 10 ? 10 : 12;
 }
 
 }  // namespace
@@ -656,19 +668,22 @@ MER_API int mer_gelu_bwd(int rows, int cols, const float* df, const void* z, voi
   MER_LAUNCH_CHECK();
 }
 
+MER_API int mer_wavlm_attention_bwd_kp(int L) { return (L <= 0 || L > AB_LMAX) ? 0 : 16 * ab_tiles(L); }
+
 MER_API int mer_wavlm_attention_bwd(int B, int L, int H, const void* qkv, long ldqkv, const void* x, long ldx,
                                     const void* dout, long ldo, const float* gate_w, const float* gate_b,
-                                    const float* gate_const, const float* tbl, float scale, float* P, float* dS,
+                                    const float* gate_const, const float* tbl, float scale, void* scratch,
                                     void* dqkv, long lddq, float* dx_gate, long lddxg, float* gate_part,
                                     void* stream) {
-  if (L <= 0 || L > AB_LMAX || ldqkv % 8 || ldx % 8 || ldo % 4 || B <= 0 || H <= 0) return (int)hipErrorInvalidValue;
+  if (L <= 0 || L > AB_LMAX || ldqkv % 8 || ldx % 8 || ldo % 4 || lddq % 4 || B <= 0 || H <= 0)
+    return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
-  const int nt = (L + 15) / 16;  // 16-key tiles; the kernels are built for 4 / 8 / 10 / 12 (L <= 64 / 128 / 160 / 192)
 #define MER_AB_LAUNCH(NT)                                                                                             \
   wavlm_attention_bwd_launch<NT>(B, L, H, (const bf16_t*)qkv, ldqkv, (const bf16_t*)x, ldx, (const float*)dout, ldo, \
-                                 gate_w, gate_b, gate_const, tbl, scale, P, dS, (bf16_t*)dqkv, lddq, dx_gate, lddxg,  \
-                                 gate_part, st)
-  const int rc = nt <= 4 ? MER_AB_LAUNCH(4) : nt <= 8 ? MER_AB_LAUNCH(8) : nt <= 10 ? MER_AB_LAUNCH(10) : MER_AB_LAUNCH(12);
+                                 gate_w, gate_b, gate_const, tbl, scale, (bf16_t*)scratch, (bf16_t*)dqkv, lddq,       \
+                                 dx_gate, lddxg, gate_part, st)
+  const int nt = ab_tiles(L);
+  const int rc = nt == 4 ? MER_AB_LAUNCH(4) : nt == 8 ? MER_AB_LAUNCH(8) : nt == 10 ? MER_AB_LAUNCH(10) : MER_AB_LAUNCH(12);
 #undef MER_AB_LAUNCH
   return rc;
 }

@@ -735,6 +735,12 @@ def linear_wgrad(x, dy, dw, col0=0):
         ws.data_ptr(), stream_ptr())
 
 
+def _attn_bwd_kp(L):
+    """mer_wavlm_attention_bwd_kp: padded key count of the attention-backward scratch (16 * 4/8/10/12)."""
+    nt = -(-L // 16)
+    return 16 * (4 if nt <= 4 else 8 if nt <= 8 else 10 if nt <= 10 else 12)
+
+
 def wavlm_attention_bwd(qkv, x, dout, gate_w, gate_b, gate_const, tbl, B, L, H, scale, dqkv, dx_gate=None):
     """Backward of wavlm_attention (per-head table form).  Returns the gate partial rows
     [B*H*ceil(L/64)][8*64 + 8 + H] for fold_rows."""
@@ -745,13 +751,13 @@ def wavlm_attention_bwd(qkv, x, dout, gate_w, gate_b, gate_const, tbl, B, L, H, 
         raise ValueError("wavlm_attention_bwd expects bf16 qkv / dqkv and fp32 dout")
     if tuple(tbl.shape) != (H, 2 * L - 1) or tbl.dtype != torch.float32:
         raise ValueError("wavlm_attention_bwd: bias table [H, 2L-1] fp32")
-    P = torch.empty(B * H * L * L, device=qkv.device, dtype=torch.float32)
-    dS = torch.empty_like(P)
+    kp = _attn_bwd_kp(L)
+    scratch = torch.empty(B * H * kp * (3 * kp + 64), device=qkv.device, dtype=torch.bfloat16)
     nrb = (L + 63) // 64  # AB_ROWS query rows per block (csrc/wavlm_train.hip)
     gpart = _workspace(B * H * nrb * (8 * 64 + 8 + H), qkv.device)
     LIB("mer_wavlm_attention_bwd", B, L, H, qkv.data_ptr(), qkv.stride(0), x.data_ptr(), x.stride(0), dout.data_ptr(),
         dout.stride(0), gate_w.data_ptr(), gate_b.data_ptr(), gate_const.data_ptr(), tbl.data_ptr(), float(scale),
-        P.data_ptr(), dS.data_ptr(), dqkv.data_ptr(), dqkv.stride(0), _ptr0(dx_gate),
+        scratch.data_ptr(), dqkv.data_ptr(), dqkv.stride(0), _ptr0(dx_gate),
         dx_gate.stride(0) if dx_gate is not None else 0, gpart.data_ptr(), stream_ptr())
     return gpart, B * H * nrb
 

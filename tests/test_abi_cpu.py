@@ -97,3 +97,18 @@ def test_bn_stat_parts_matches_header():
 
     m = re.search(r"#define\s+MER_BN_STAT_PARTS\s+(\d+)", _HEADER.read_text())
     assert m and int(m.group(1)) == K.BN_STAT_PARTS
+
+
+def test_attention_bwd_scratch_kp_matches_library():
+    """kernels.wavlm_attention_bwd sizes its scratch with the library's padded key count (host-only call)."""
+    _ensure_built()
+    import ctypes
+
+    from multimodalemotionrecognition_amd import kernels as K
+    from multimodalemotionrecognition_amd._lib import lib_path
+
+    fn = ctypes.CDLL(str(lib_path())).mer_wavlm_attention_bwd_kp
+    fn.argtypes, fn.restype = [ctypes.c_int], ctypes.c_int
+    for L in range(1, 193):
+        assert fn(L) == K._attn_bwd_kp(L) >= L, L
+    assert fn(0) == 0 and fn(193) == 0
