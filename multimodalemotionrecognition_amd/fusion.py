@@ -270,7 +270,9 @@ class _HeadGraphs(G.PendingGuard):
         dv = self.bwd.replay(dlogits)
         if probe is not None:
             probe.bwd.append((e0, probe.mark()))
-        return dv.clone(), {n: grad_buffer(t) for n, t in params.items() if n in used and t.requires_grad}
+        # dv goes straight back through autograd into the trunk backward of this same pass, before the next
+        # replay of this graph: the static tensor itself, no copy
+        return dv, {n: grad_buffer(t) for n, t in params.items() if n in used and t.requires_grad}
 
 
 class FusionModel(nn.Module):
@@ -411,8 +413,9 @@ class FusionModel(nn.Module):
             # gated: the fp32 hidden states their encode() / forward() pool (the pooling and classifier train)
             if stage2:
                 kind, out = "prefix", self.audio_model.encode_prefix(audio)
-            elif xattn:
-                kind, out = "seq", self.audio_model.encode_sequence(audio)
+            elif xattn:  # consumed by the next step's head forward, before the encoder graph's next replay
+                with G.borrow_outputs():
+                    kind, out = "seq", self.audio_model.encode_sequence(audio)
             else:
                 kind, out = "hidden", self.audio_model.encode_sequence(audio, out_dtype=torch.float32)
         # the tensor itself (not its address) identifies the batch: a recycled address cannot match
@@ -520,6 +523,9 @@ class FusionModel(nn.Module):
         cfg = self.head_config()
         v_feat, a_seq = v_feat.contiguous(), a_seq.contiguous()
         runner = self._head_runner(names, params, cfg, v_feat, a_seq)
+        if runner is None:  # the eager head keeps its inputs for the backward: own copies of borrowed outputs
+            v_feat = v_feat.clone() if G.is_borrowed(v_feat) else v_feat
+            a_seq = a_seq.clone() if G.is_borrowed(a_seq) else a_seq
         rng = self.step_rng(v_feat.device) if (self.training and runner is None) else None
         return _XattnHeadFn.apply(v_feat, a_seq, cfg, self.training, rng, names, runner, *params)
 
@@ -563,24 +569,28 @@ class FusionModel(nn.Module):
             # backward), its result is taken over instead.
             kind = "seq" if self.audio_encoder_frozen() else "prefix"
             if self._prefetch_matches(audio, kind):
-                v_feat = self.video_model.backbone(v_in).view(b, t, self.v_dim)
+                with G.borrow_outputs():
+                    v_feat = self.video_model.backbone(v_in).view(b, t, self.v_dim)
                 got = self._take_prefetched(audio, kind)
                 # stage 2: prefetched frozen prefix -> trainable tail now
                 a_seq = self.audio_model.encode_sequence(audio, prefix=got) if kind == "prefix" else got
                 return self.xattn_from_features(v_feat, a_seq)
             self._prefetched = None
             side = _side_stream(video.device) if _OVERLAP_ENCODERS else None
-            if side is not None:
-                cur = torch.cuda.current_stream(video.device)
-                side.wait_stream(cur)
-                with torch.cuda.stream(side):
+            # the encoders' graph outputs go to the head without a copy (graphs.borrow_outputs; the head's
+            # graph copies them into its static inputs, an eager head takes its own copy)
+            with G.borrow_outputs():
+                if side is not None:
+                    cur = torch.cuda.current_stream(video.device)
+                    side.wait_stream(cur)
+                    with torch.cuda.stream(side):
+                        a_seq = self.audio_model.encode_sequence(audio)
+                    v_feat = self.video_model.backbone(v_in).view(b, t, self.v_dim)
+                    cur.wait_stream(side)
+                    a_seq.record_stream(cur)
+                else:
                     a_seq = self.audio_model.encode_sequence(audio)
-                v_feat = self.video_model.backbone(v_in).view(b, t, self.v_dim)
-                cur.wait_stream(side)
-                a_seq.record_stream(cur)
-            else:
-                a_seq = self.audio_model.encode_sequence(audio)
-                v_feat = self.video_model.backbone(v_in).view(b, t, self.v_dim)
+                    v_feat = self.video_model.backbone(v_in).view(b, t, self.v_dim)
             return self.xattn_from_features(v_feat, a_seq)
 
         if self.mode not in {"concat", "gated"}:

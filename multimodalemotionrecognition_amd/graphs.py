@@ -13,6 +13,7 @@ Set ``MER_GRAPHS=0`` to run every launch eagerly (A/B and debugging).
 """
 from __future__ import annotations
 
+import contextlib
 import gc
 import os
 from typing import Callable, Dict, Optional
@@ -58,6 +59,38 @@ class StaticGraph:
                     st.copy_(x)
         self.graph.replay()
         return self.out
+
+
+_BORROW = [0]
+_BORROWED = set()  # storage addresses of static outputs handed out without a copy
+
+
+@contextlib.contextmanager
+def borrow_outputs():
+    """Inside this context, graph outputs are handed out as the graph's static tensors themselves (no copy).
+    For a caller that consumes them before the graph's next replay -- FusionModel feeding the encoders' outputs
+    to the head graph, which copies them into its own static inputs -- this removes one device copy per output
+    per step.  Outside it every output is a fresh copy (a caller may hold it across replays)."""
+    _BORROW[0] += 1
+    try:
+        yield
+    finally:
+        _BORROW[0] -= 1
+
+
+def hand_out(t: torch.Tensor) -> torch.Tensor:
+    """A captured graph's static output for the caller: the tensor itself inside ``borrow_outputs()``, else a
+    copy."""
+    if _BORROW[0]:
+        _BORROWED.add(t.untyped_storage().data_ptr())
+        return t
+    return t.clone()
+
+
+def is_borrowed(t: torch.Tensor) -> bool:
+    """True when ``t`` shares storage with a graph output handed out by ``hand_out`` without a copy (it is
+    overwritten by that graph's next replay)."""
+    return t.is_cuda and t.untyped_storage().data_ptr() in _BORROWED
 
 
 class GraphCache:

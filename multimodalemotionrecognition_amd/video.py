@@ -114,7 +114,7 @@ class _TrunkGraphs(G.PendingGuard):
         if self.fwd is None:
             self.fwd = G.StaticGraph(lambda xx: trunk_forward(self.trunk, xx, self.training, force_pack=True), [x])
         feats, saved = self.fwd.replay(x)
-        return feats.clone(), saved
+        return G.hand_out(feats), saved
 
     @staticmethod
     def backward_graphable(params) -> bool:

@@ -360,8 +360,8 @@ class WavLMBackbone(nn.Module):
             ga, y1, gb = graph
             x = ga.replay(wav)
             self._conv_layer(x, 1, x.shape[1], out=y1)
-            return gb.replay().clone()
-        return graph.replay(wav).clone()
+            return G.hand_out(gb.replay())
+        return G.hand_out(graph.replay(wav))
 
     def _stage_a(self, wav):
         """conv0 -> GroupNorm + GELU (one fused deterministic kernel pair): [B, S] -> [B, L0, 512] bf16."""
