@@ -12,7 +12,8 @@ import os
 import re
 from pathlib import Path
 
-_LIB_PATH = Path(__file__).resolve().parent / "libmer_hip.so"
+# MER_HIP_LIB: load another build of the same ABI instead (A/B timing of a kernel change in one process tree)
+_LIB_PATH = Path(os.environ.get("MER_HIP_LIB") or Path(__file__).resolve().parent / "libmer_hip.so")
 
 _HEADER = Path(__file__).resolve().parents[1] / "include" / "mer.h"
 

@@ -63,14 +63,19 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
-// Counter-based RNG (splitmix64 finaliser over (seed, stream, index)): the same mask is
-// regenerated in backward from the same (seed, index) -- no mask tensor is stored.
+// Counter-based RNG over (seed, index): the same mask is regenerated in backward from the same (seed, index) --
+// no mask tensor is stored.  32-bit arithmetic only (a 64-bit multiply is four quarter-rate VALU ops on CDNA, and
+// the attention / activation dropouts hash every element): the 64-bit seed and index are folded to 32 bits, and
+// the word is finalised by the "lowbias32" xorshift-multiply mixer (three 32-bit multiplies).
 __device__ __forceinline__ uint32_t mer_hash(uint64_t seed, uint64_t idx) {
-  uint64_t z = seed + 0x9E3779B97F4A7C15ull * (idx + 1);
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  z ^= z >> 31;
-  return (uint32_t)z;
+  const uint32_t s = (uint32_t)seed ^ ((uint32_t)(seed >> 32) * 0x85EBCA6Bu);
+  uint32_t x = ((uint32_t)idx ^ ((uint32_t)(idx >> 32) * 0xC2B2AE35u)) * 0x9E3779B9u + s;
+  x ^= x >> 16;
+  x *= 0x7FEB352Du;
+  x ^= x >> 15;
+  x *= 0x846CA68Bu;
+  x ^= x >> 16;
+  return x;
 }
 // Per-call-site dropout seed: the step's RNG base lives in DEVICE memory (so a captured hipGraph replays
 // with a fresh base every step, advanced in-graph by mer_rng_advance) and is mixed with a constant site

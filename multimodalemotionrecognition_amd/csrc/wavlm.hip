@@ -280,20 +280,26 @@ __global__ __launch_bounds__(256, 3) void wavlm_attn_kernel(int L, int H, const 
   float* gate = reinterpret_cast<float*>(Vt + ADH * VTP);  // [4][16]
   float* gws = gate + 64;                              // [8][64] gru_rel_pos_linear weight
   float* tbl = gws + 512;                              // [2L-1]
-  const int b = blockIdx.x / H, h = blockIdx.x % H;
+  // one-dimensional grid, XCD-aware: the row blocks of one (b, h) run on one XCD and share its K / V in L2
+  const int nrb = (LP / 16 + 3) / 4;
+  int rbk, bh;
+  xcd_tile(blockIdx.x, nrb, gridDim.x, rbk, bh);  // gridDim.x = nrb * B * H
+  const int b = bh / H, h = bh % H;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int D = H * ADH;
-  const int rb = blockIdx.y * 4 + w;  // this wave's 16-row query tile
-  const bool active = rb * 16 < L;    // wave-uniform
+  const int rb = rbk * 4 + w;       // this wave's 16-row query tile
+  const bool active = rb * 16 < L;  // wave-uniform
 
-  // this wave's Q fragments first (B operand of S^T = K Q^T: Q[i = lane&15][d = kk*32 + 8*(lane>>4) ..])
-  bf16x8 qb[2] = {bf16x8{0, 0, 0, 0, 0, 0, 0, 0}, bf16x8{0, 0, 0, 0, 0, 0, 0, 0}};
+  // Loads are unconditional from clamped (valid) rows, zeroed by a select at the LDS store: a load under a
+  // per-lane condition compiles to a branch around it and a wait for it, serialising the prologue's loads.
+  // This wave's Q fragments first (B operand of S^T = K Q^T: Q[i = lane&15][d = kk*32 + 8*(lane>>4) ..]); rows
+  // past L read row L - 1 (their outputs are never stored)
+  bf16x8 qb[2];
   {
-    const int qrow = rb * 16 + (lane & 15);
-    if (qrow < L)
+    const int qrow = min(rb * 16 + (lane & 15), L - 1);
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
-        qb[kk] = *reinterpret_cast<const bf16x8*>(qkv + ((long)b * L + qrow) * ldqkv + h * ADH + kk * 32 + (lane >> 4) * 8);
+    for (int kk = 0; kk < 2; ++kk)
+      qb[kk] = *reinterpret_cast<const bf16x8*>(qkv + ((long)b * L + qrow) * ldqkv + h * ADH + kk * 32 + (lane >> 4) * 8);
   }
   // Every global load of the prologue is issued before the first LDS store: K (row-major 16-byte chunks),
   // V (4-row groups for the V^T image), the relative-position bias row of this head (precomputed table
@@ -303,26 +309,22 @@ __global__ __launch_bounds__(256, 3) void wavlm_attn_kernel(int L, int H, const 
   u32x4 xg[2];
 #pragma unroll
   for (int it = 0; it < 2; ++it) {
-    const int i = rb * 16 + it * 8 + sub;
-    xg[it] = u32x4{0u, 0u, 0u, 0u};
-    if (active && i < L) xg[it] = *reinterpret_cast<const u32x4*>(x + ((long)b * L + i) * ldx + h * ADH + cl * 8);
+    const int i = min(rb * 16 + it * 8 + sub, L - 1);
+    xg[it] = *reinterpret_cast<const u32x4*>(x + ((long)b * L + i) * ldx + h * ADH + cl * 8);
   }
   float tb[2], gwv[2];
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
-    const int r = t + 256 * k;
-    tb[k] = 0.f;
-    if (r < 2 * L - 1) tb[k] = bucket ? rel_emb[(long)bucket[r] * H + h] : rel_emb[(long)h * (2 * L - 1) + r];
-    gwv[k] = gw[r];  // 512 = 8 x 64 weights
+    const int r = min(t + 256 * k, 2 * L - 2);
+    tb[k] = bucket ? rel_emb[(long)bucket[r] * H + h] : rel_emb[(long)h * (2 * L - 1) + r];
+    gwv[k] = gw[t + 256 * k];  // 512 = 8 x 64 weights
   }
   {
     u32x4 kr[8];
 #pragma unroll
     for (int it = 0; it < 8; ++it) {
-      const int c = t + it * 256, row = c >> 3, ch = c & 7;
-      kr[it] = u32x4{0u, 0u, 0u, 0u};
-      if (c < LP * 8 && row < L)
-        kr[it] = *reinterpret_cast<const u32x4*>(qkv + ((long)b * L + row) * ldqkv + D + h * ADH + ch * 8);
+      const int c = t + it * 256, row = min(c >> 3, L - 1), ch = c & 7;
+      kr[it] = *reinterpret_cast<const u32x4*>(qkv + ((long)b * L + row) * ldqkv + D + h * ADH + ch * 8);
     }
     u32x4 vr[2][4];
 #pragma unroll
@@ -330,10 +332,8 @@ __global__ __launch_bounds__(256, 3) void wavlm_attn_kernel(int L, int H, const 
       const int q = t + it * 256, rq = q >> 3, ch = q & 7;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const int row = rq * 4 + e;
-        vr[it][e] = u32x4{0u, 0u, 0u, 0u};
-        if (q < LP * 2 && row < L)
-          vr[it][e] = *reinterpret_cast<const u32x4*>(qkv + ((long)b * L + row) * ldqkv + 2 * D + h * ADH + ch * 8);
+        const int row = min(rq * 4 + e, L - 1);
+        vr[it][e] = *reinterpret_cast<const u32x4*>(qkv + ((long)b * L + row) * ldqkv + 2 * D + h * ADH + ch * 8);
       }
     }
 #pragma unroll
@@ -345,12 +345,15 @@ __global__ __launch_bounds__(256, 3) void wavlm_attn_kernel(int L, int H, const 
 #pragma unroll
     for (int it = 0; it < 8; ++it) {
       const int c = t + it * 256, row = c >> 3, ch = c & 7;
-      if (c < LP * 8) *reinterpret_cast<u32x4*>(&Ks[row * APAD + ch * 8]) = kr[it];
+      if (c < LP * 8) *reinterpret_cast<u32x4*>(&Ks[row * APAD + ch * 8]) = row < L ? kr[it] : u32x4{0u, 0u, 0u, 0u};
     }
 #pragma unroll
     for (int it = 0; it < 2; ++it) {
       const int q = t + it * 256, rq = q >> 3, ch = q & 7;
       if (q < LP * 2) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (rq * 4 + e >= L) vr[it][e] = u32x4{0u, 0u, 0u, 0u};
 #pragma unroll
         for (int i = 0; i < 8; ++i) {  // channel d = ch*8 + i: (V[4rq][d], .., V[4rq+3][d])
           const int sh = (i & 1) * 16, wd = i >> 1;
@@ -504,7 +507,7 @@ MER_API int mer_wavlm_attention_tr(int B, int L, int H, const void* qkv, long ld
     return (int)hipErrorInvalidValue;
   const int LP = (L + 15) / 16 * 16;
   const size_t lds = sizeof(bf16_t) * ((size_t)LP * APAD + (size_t)ADH * (LP + 8)) + sizeof(float) * (64 + 512 + 2 * L);
-  hipLaunchKernelGGL(wavlm_attn_kernel, dim3(B * H, (LP / 16 + 3) / 4), dim3(256), lds, (hipStream_t)stream, L, H,
+  hipLaunchKernelGGL(wavlm_attn_kernel, dim3(B * H * ((LP / 16 + 3) / 4)), dim3(256), lds, (hipStream_t)stream, L, H,
                      (const bf16_t*)qkv, ldqkv, (const bf16_t*)x, ldx, gate_w, gate_b, gate_const, rel_emb, bucket,
                      (bf16_t*)out, ldo, scale, drop_p, seed, site, skip_mask, skip_bit);
   MER_LAUNCH_CHECK();

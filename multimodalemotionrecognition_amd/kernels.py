@@ -7,6 +7,8 @@ exception), then pass raw pointers and the current stream.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from ._lib import LIB
@@ -496,6 +498,19 @@ def partials_sum(parts_buf, out):
     return out
 
 
+# Pixels per wgrad split, at least (tools/bench_conv.py on the ResNet18 layers, MI355X): 1024 in general -- more,
+# shorter splits lose to the fold of their partial slabs -- but 256 for the tiny 1x1 downsample outputs (a K loop of
+# 16 64-pixel steps per split was the whole time: 26 -> 19 us) and 512 where the output has so many tiles that
+# 1024 leaves only 4 splits (layer4 3x3: 65 -> 58 us).  MER_WGRAD_MIN_PIX overrides (A/B).
+_WGRAD_MIN_PIX = int(os.environ.get("MER_WGRAD_MIN_PIX", "0"))
+
+
+def _wgrad_min_pix(out_elems, tiles):
+    if _WGRAD_MIN_PIX > 0:
+        return _WGRAD_MIN_PIX
+    return 256 if out_elems <= 65536 else (512 if tiles >= 96 else 1024)
+
+
 def conv_wgrad(x, dy, dw, R, S, stride, pad, creal=None, variant=-1, splits=None):
     N, H, W, C = x.shape
     Kc = dy.shape[-1]
@@ -505,8 +520,8 @@ def conv_wgrad(x, dy, dw, R, S, stride, pad, creal=None, variant=-1, splits=None
         raise ValueError("conv_wgrad shapes")
     P = N * Ho * Wo
     tiles = ((Kc + 127) // 128) * ((R * S * C + 127) // 128)
-    if splits is None:  # ~768 workgroups (3 per CU), >= 1024 pixels each
-        splits = int(max(1, min(-(-768 // tiles), P // 1024)))
+    if splits is None:  # ~768 workgroups (3 per CU), >= _wgrad_min_pix pixels each
+        splits = int(max(1, min(-(-768 // tiles), P // _wgrad_min_pix(Kc * R * S * C, tiles))))
     ws = torch.empty(splits * Kc * R * S * C, device=x.device, dtype=torch.float32)
     _launch("conv_wgrad", (N, H, W, C, Kc, R, stride), "mer_conv_wgrad_ex", N, H, W, C, creal, Kc, R, S, stride, pad,
             x.data_ptr(), dy.data_ptr(), dw.data_ptr(), int(splits), ws.data_ptr(), int(variant), stream_ptr())

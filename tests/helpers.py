@@ -73,12 +73,18 @@ def site_seed(base: int, site: int) -> int:
 
 def hash_u32(seed: int, idx: np.ndarray) -> np.ndarray:
     idx = np.asarray(idx, dtype=np.uint64)
+    u32 = np.uint32
     with np.errstate(over="ignore"):
-        z = np.uint64(seed) + np.uint64(0x9E3779B97F4A7C15) * (idx + np.uint64(1))
-        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
-        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
-        z ^= z >> np.uint64(31)
-    return (z & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+        s = u32(seed & 0xFFFFFFFF) ^ (u32(seed >> 32) * u32(0x85EBCA6B))
+        lo = (idx & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+        hi = (idx >> np.uint64(32)).astype(np.uint32)
+        x = (lo ^ (hi * u32(0xC2B2AE35))) * u32(0x9E3779B9) + s
+        x ^= x >> u32(16)
+        x *= u32(0x7FEB352D)
+        x ^= x >> u32(15)
+        x *= u32(0x846CA68B)
+        x ^= x >> u32(16)
+    return x.astype(np.uint32)
 
 
 def dropout_keep(base: int, site: int, idx: np.ndarray, p: float) -> np.ndarray:

@@ -15,7 +15,9 @@ LAYERS = [("stem s2d 4x4", 59, 16, 64, 4, 1, 0), ("layer1 3x3", 28, 64, 64, 3, 1
           ("layer3.0 3x3 s2", 14, 128, 256, 3, 2, 1), ("layer3 3x3", 7, 256, 256, 3, 1, 1),
           ("layer4.0 3x3 s2", 7, 256, 512, 3, 2, 1), ("layer4 3x3", 4, 512, 512, 3, 1, 1),
           ("ds2 1x1 s2", 28, 64, 128, 1, 2, 0)]
-VARIANTS = [int(v) for v in next((a.split("=")[1] for a in sys.argv if a.startswith("--variants=")), "2,4").split(",")]
+VARIANTS = [int(v) for v in next((a.split("=")[1] for a in sys.argv if a.startswith("--variants=")), "2,4").split(",") if v]
+WGRAD_V = [int(v) for v in next((a.split("=")[1] for a in sys.argv if a.startswith("--wgrad-variants=")), "1,2").split(",")
+           if v]
 WGRAD = "--no-wgrad" not in sys.argv
 
 
@@ -49,7 +51,7 @@ def main():
         flop = 2.0 * NF * Ho * Ho * Kc * R * R * C
         dw = torch.zeros(Kc, C, R, R, device="cuda")
         line = f"{name:16s}"
-        for v in ((1, 2) if WGRAD else ()):
+        for v in (WGRAD_V if WGRAD else ()):
             tw = timeit(lambda: K.conv_wgrad(x, dy, dw, R, R, st, pad, variant=v))
             line += f" | wgrad v{v} {tw*1e3:7.1f}us {flop/tw/1e9:6.1f}TF"
         ref_y = ref_dx = None
