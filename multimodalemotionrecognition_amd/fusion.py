@@ -240,7 +240,7 @@ class _HeadGraphs(G.PendingGuard):
                                                                   self.rng if self.training else None),
                                      [v_feat, a_seq])
         if self.training:  # this step's host-drawn RNG base, stream-ordered before the replay reads it
-            self.rng.fill_(_next_seed())
+            self.rng.fill_(self.model.take_head_seed())
         probe = HEAD_PROBE
         e0 = probe.mark() if probe is not None else None
         logits, hctx = self.fwd.replay(v_feat, a_seq)
@@ -314,6 +314,8 @@ class FusionModel(nn.Module):
         self.xattn_use_emotion_prior = xattn_use_emotion_prior
         self.num_classes = num_classes
         self._prefetched = None  # (audio key, encoder output, stream) from prefetch_audio()
+        self._queued_audio = None  # the NEXT batch's waveform for an early prefetch (queue_next_audio)
+        self._head_seed = None  # this forward's head dropout seed, drawn ahead of an early prefetch
         self._head_graphs = G.GraphCache()
 
         if mode in {"concat", "gated"}:
@@ -383,7 +385,14 @@ class FusionModel(nn.Module):
         """This step's dropout RNG base: a fresh device int64 [1] tensor drawn from the host generator each
         training forward (so ``torch.manual_seed`` reproduces the masks, train.py:951 set_seed); the
         autograd context keeps it, so masks are regenerated correctly even with several forwards in flight."""
-        return torch.full((1,), _next_seed(), dtype=torch.int64, device=device)
+        return torch.full((1,), self.take_head_seed(), dtype=torch.int64, device=device)
+
+    def take_head_seed(self) -> int:
+        """The head's dropout seed of this forward: pre-drawn by an early prefetch (``_issue_queued``, which keeps
+        the host draw order of the inline schedule -- this step's head, then the next batch's encoder), else drawn
+        now."""
+        s, self._head_seed = self._head_seed, None
+        return _next_seed() if s is None else s
 
     def audio_encoder_frozen(self) -> bool:
         enc = getattr(self.audio_model, "wavlm", None)
@@ -421,6 +430,34 @@ class FusionModel(nn.Module):
         # the tensor itself (not its address) identifies the batch: a recycled address cannot match
         self._prefetched = (audio, audio._version, out, side, kind)
         return True
+
+    def queue_next_audio(self, audio: torch.Tensor) -> None:
+        """Early prefetch: the next xattn ``forward`` starts the audio encoder on ``audio`` (the NEXT batch) on the
+        side stream as soon as it has taken its own batch's encoder output -- before the frame trunk -- so the
+        encoder overlaps the whole step (forward and backward) instead of the backward only.  A forward that
+        cannot use it leaves it queued: ``take_queued_audio`` hands it back (TrainStep then prefetches the old
+        way, before the backward)."""
+        self._queued_audio = audio
+
+    def take_queued_audio(self):
+        a, self._queued_audio = self._queued_audio, None
+        return a
+
+    def _issue_queued(self, kind: str, a_out: torch.Tensor) -> torch.Tensor:
+        """Start the queued early prefetch now; returns ``a_out`` made safe against it (a borrowed encoder-graph
+        output is rewritten by that replay: this step keeps its own copy, ordered before the side stream)."""
+        nxt = self._queued_audio
+        if nxt is None or not torch.is_grad_enabled():
+            return a_out
+        self._queued_audio = None
+        if G.is_borrowed(a_out):
+            a_out = a_out.clone()
+        # host draws in the inline order: this step's head seed before the next batch's encoder draws
+        if self.training:
+            self._head_seed = _next_seed()
+        if not self.prefetch_audio(nxt):
+            self._queued_audio = nxt
+        return a_out
 
     def _prefetch_matches(self, audio: torch.Tensor, kind: str) -> bool:
         pf = self._prefetched
@@ -569,9 +606,9 @@ class FusionModel(nn.Module):
             # backward), its result is taken over instead.
             kind = "seq" if self.audio_encoder_frozen() else "prefix"
             if self._prefetch_matches(audio, kind):
+                got = self._issue_queued(kind, self._take_prefetched(audio, kind))
                 with G.borrow_outputs():
                     v_feat = self.video_model.backbone(v_in).view(b, t, self.v_dim)
-                got = self._take_prefetched(audio, kind)
                 # stage 2: prefetched frozen prefix -> trainable tail now
                 a_seq = self.audio_model.encode_sequence(audio, prefix=got) if kind == "prefix" else got
                 return self.xattn_from_features(v_feat, a_seq)
@@ -591,6 +628,8 @@ class FusionModel(nn.Module):
                 else:
                     a_seq = self.audio_model.encode_sequence(audio)
                     v_feat = self.video_model.backbone(v_in).view(b, t, self.v_dim)
+            if kind == "seq":  # (the first step of an early-prefetch run: nothing was prefetched for it yet)
+                a_seq = self._issue_queued(kind, a_seq)
             return self.xattn_from_features(v_feat, a_seq)
 
         if self.mode not in {"concat", "gated"}:

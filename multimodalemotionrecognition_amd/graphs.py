@@ -90,7 +90,7 @@ def hand_out(t: torch.Tensor) -> torch.Tensor:
 def is_borrowed(t: torch.Tensor) -> bool:
     """True when ``t`` shares storage with a graph output handed out by ``hand_out`` without a copy (it is
     overwritten by that graph's next replay)."""
-    return t.is_cuda and t.untyped_storage().data_ptr() in _BORROWED
+    return isinstance(t, torch.Tensor) and t.is_cuda and t.untyped_storage().data_ptr() in _BORROWED
 
 
 class GraphCache:

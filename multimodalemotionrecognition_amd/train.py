@@ -9,6 +9,7 @@
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, Optional
 
 import torch
@@ -178,6 +179,11 @@ def make_loss(fusion_mode: str, label_smoothing: float = 0.0) -> nn.Module:
     return LateNLLLoss() if fusion_mode == "late" else CrossEntropyLoss(label_smoothing=label_smoothing)
 
 
+# Early prefetch (FusionModel.queue_next_audio): the next batch's frozen audio encoder starts at the top of the
+# step instead of before its backward.  MER_EARLY_PREFETCH=0 restores the backward-only overlap (A/B).
+EARLY_PREFETCH = os.environ.get("MER_EARLY_PREFETCH", "1") != "0"
+
+
 class TrainStep:
     """One training step of train.py:200-228 on the HIP path: returns (loss, preds) as device tensors."""
 
@@ -191,11 +197,15 @@ class TrainStep:
     def __call__(self, video: torch.Tensor, audio: torch.Tensor, labels: torch.Tensor,
                  next_audio: Optional[torch.Tensor] = None):
         """``next_audio``: the NEXT step's waveform batch, already on the device.  With a frozen audio
-        encoder its forward is started on a side stream right after this step's forward, so it overlaps
-        this step's backward (``FusionModel.prefetch_audio``); results are identical either way."""
+        encoder its forward is started on a side stream -- at the top of this step's xattn forward (early
+        prefetch), else right after the forward -- so it overlaps this step's work
+        (``FusionModel.prefetch_audio``); results are identical either way."""
         if not self.model.training:  # (a full module-tree walk; skipped when already in train mode)
             self.model.train()
         self.opt.zero_grad()
+        early = EARLY_PREFETCH and next_audio is not None and hasattr(self.model, "queue_next_audio")
+        if early:  # the forward starts it right after taking this batch's encoder output (overlaps the whole step)
+            self.model.queue_next_audio(next_audio)
         if self.mode in {"audio", "video"}:
             outputs = self.model(audio if self.mode == "audio" else video)
         else:
@@ -207,6 +217,8 @@ class TrainStep:
             if align is not None:
                 loss = add_scaled(cls_loss, align, self.fusion_align_weight)
         self.last_losses = (cls_loss.detach(), align.detach() if align is not None else None)
+        if early:
+            next_audio = self.model.take_queued_audio()  # None when the forward issued it
         if next_audio is not None and hasattr(self.model, "prefetch_audio"):
             self.model.prefetch_audio(next_audio)
         loss.backward()

@@ -105,10 +105,16 @@ def test_train_step_graphs_match_eager():
         G.ENABLED = prev
 
 
-def test_audio_prefetch_matches_inline():
-    """TrainStep(next_audio=...) runs the frozen WavLM of the next batch during this step's backward.
-    The WavLM path is deterministic, so the prefetched features must be bit-identical to an inline
-    encode of the same waveform; a prefetch is used only for the very tensor it was computed from."""
+@pytest.mark.parametrize("early", [False, True])
+def test_audio_prefetch_matches_inline(early, monkeypatch):
+    """TrainStep(next_audio=...) runs the frozen WavLM of the next batch on a side stream: from the top of this
+    step's forward (early prefetch, FusionModel.queue_next_audio: this step keeps a copy of its own borrowed
+    encoder output first) or during this step's backward.  The WavLM path is deterministic, so the prefetched
+    features must be bit-identical to an inline encode of the same waveform; a prefetch is used only for the
+    very tensor it was computed from."""
+    from multimodalemotionrecognition_amd import train as T
+
+    monkeypatch.setattr(T, "EARLY_PREFETCH", early)
     prev = G.ENABLED
     try:
         G.ENABLED = True
