@@ -14,9 +14,10 @@ WavLM runs with the reference's train-mode semantics (the reference keeps the fr
 under no_grad, train.py:194): SpecAugment, dropout and LayerDrop -- so the algorithmic FLOPs of a step count
 only the encoder layers actually executed; `wavlm_layers_per_step` reports them.
 
-Extra fields: `roofline` for the dominant kernel (HIP events around its launches, on the side stream it runs
-on, in `--probe-steps` instrumented steps that follow the timed region: the production WavLM forward is ONE
-captured graph, so the probe steps alone run it as two graphs around an eagerly launched conv1 GEMM) and
+Extra fields: `roofline` for the dominant kernel (after the timed region: HIP events around `--probe-launches`
+standalone launches of that kernel on its production shape, weights and stream, with nothing else in flight --
+the figure a rocprofv3 kernel trace of the same command reports for it; the timed schedule is never altered),
+`roofline_head` for the fused xattn head (HIP events around its graph replays in `--probe-steps` steps) and
 `cpu_baseline` (the fp32 CPU oracle of the same step, rank 0, N=1: BASELINE.md section 3 -- warm-up steps,
 then the median of timed steps, on the threads of this process's CPU share, CPU model recorded).
 """
@@ -148,13 +149,42 @@ def cpu_baseline(threads: int, steps: int = 10, warmup: int = 10):
                       f"B=32 ({dt:.2f} s/step, {BATCH / dt:.2f} clips/s), torch CPU eager, {threads} threads"}
 
 
+def time_dominant(model, dev, probe, launches: int):
+    """HIP events around standalone launches of the WavLM conv1 implicit GEMM (wavlm_audio._conv_layer, i = 1) on
+    its production shape, bf16 weight pack and stream, operands resident in HBM, nothing else in flight."""
+    wav = model.audio_model.wavlm
+    L0 = (SAMPLES - 10) // 5 + 1          # conv0 output frames (kernel 10, stride 5)
+    L1 = (L0 - 3) // 2 + 1                # conv1 output frames (kernel 3, stride 2)
+    M, N, Kd = PROBE[1]
+    assert M == BATCH * L1 and N == 512 and Kd == 3 * 512
+    x = (torch.rand(BATCH, L0, 512, device=dev) * 2 - 1).bfloat16()
+    y = torch.empty(BATCH, L1, 512, device=dev, dtype=torch.bfloat16)
+    w = wav.packed_weights()["conv"][0]
+
+    def launch():
+        K.gemm_bf16(x, w, y, M=M, K=Kd, rows=(L1, 2 * 512, L0 * 512), act="gelu")
+
+    with torch.cuda.stream(F._side_stream(dev)):  # the stream the production WavLM forward runs on
+        for _ in range(3):
+            launch()
+        probe.active = True
+        K.PROBE = probe
+        for _ in range(launches):
+            launch()
+        K.PROBE = None
+        probe.active = False
+    torch.cuda.synchronize()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--probe-steps", type=int, default=10,
-                    help="instrumented steps after the timed region in which the dominant kernel is timed")
+                    help="instrumented steps after the timed region in which the fused head's graphs are timed")
+    ap.add_argument("--probe-launches", type=int, default=20,
+                    help="standalone launches of the dominant kernel timed after the timed region")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: this process's CPU share (cpu_share_threads)")
     ap.add_argument("--cpu-steps", type=int, default=10)
@@ -210,22 +240,19 @@ def main():
                                                                            step_ms[len(step_ms) // 2])
     layers = (wav.executed_layers - lay0) / max(1, wav.train_forwards - fwd0)
 
-    # probe steps (after the timed region): the dominant kernel bracketed by HIP events on its stream
-    probe = K.KernelProbe(PROBE[0], PROBE[1], units=2.0 * PROBE[1][0] * PROBE[1][1] * PROBE[1][2])
+    # probe steps (after the timed region): the fused head's forward / backward graph replays bracketed by HIP
+    # events on their stream
     hprobe = F.HeadProbe()
     if args.probe_steps > 0:
-        probe.active = True
-        K.PROBE = probe
         F.HEAD_PROBE = hprobe
-        for _ in range(args.probe_steps + 2):  # the first two build the instrumented (split) WavLM graphs
+        for _ in range(args.probe_steps):
             step(video, audio, labels, next_audio=nxt)
         torch.cuda.synchronize()
-        probe.pairs = probe.pairs[-args.probe_steps:]
-        hprobe.fwd, hprobe.bwd = hprobe.fwd[-args.probe_steps:], hprobe.bwd[-args.probe_steps:]
-        probe.active = False
-        K.PROBE = None
         F.HEAD_PROBE = None
-
+    # the dominant kernel: standalone launches on the production conv1 shape / weight pack / WavLM stream
+    probe = K.KernelProbe(PROBE[0], PROBE[1], units=2.0 * PROBE[1][0] * PROBE[1][1] * PROBE[1][2])
+    if args.probe_launches > 0:
+        time_dominant(model, dev, probe, args.probe_launches)
     kms = probe.avg_ms()
     roof = None
     if kms:
@@ -234,8 +261,8 @@ def main():
                 "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": pmc_traffic(),
                 "kernel": f"{PROBE_KERNEL} (WavLM conv1 implicit GEMM {PROBE[1][0]}x{PROBE[1][1]}x{PROBE[1][2]})",
                 "avg_ms": round(kms, 4), "launches": len(probe.pairs),
-                "measured": f"HIP events on the launching stream in {len(probe.pairs)} probe steps after the timed "
-                            "region"}
+                "measured": f"HIP events around {len(probe.pairs)} standalone launches after the timed region "
+                            "(production shape, weight pack and stream)"}
     roof_head = None
     hms = hprobe.avg_ms()
     if hms and args.wavlm_unfreeze == 0 and not args.emotion_prior:

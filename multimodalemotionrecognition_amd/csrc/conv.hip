@@ -45,7 +45,15 @@ struct ConvGeom {
   const bf16_t* bnr_x2;
   const float* bnr_ms2;
   float* bnr_red2;
+  int vec;                // 16-byte epilogue (Ncols, ldy multiples of 8, every operand 16-byte aligned)
 };
+
+__host__ __device__ inline bool conv_vec_ok(const ConvGeom& g) {
+  const uintptr_t a = (uintptr_t)g.Y | (uintptr_t)g.R_ | (uintptr_t)g.Rmask | (uintptr_t)g.bnr_mask |
+                      (uintptr_t)g.bnr_x | (uintptr_t)g.bnr_x2 | (uintptr_t)g.stats | (uintptr_t)g.bnr_red |
+                      (uintptr_t)g.bnr_red2;
+  return g.Ncols % 8 == 0 && g.ldy % 8 == 0 && (a & 15) == 0;
+}
 
 template <bool DGRAD>
 __device__ __forceinline__ u32x4 conv_a_chunk(const ConvGeom& g, int n, int oh, int ow, bool rowok, int kk, int tap,
@@ -213,7 +221,7 @@ struct WgradGeom {
   long ldy;               // dY row stride (elements; K for a conv, a column slice of a wider matrix for a Linear)
 };
 
-template <int BM_, int BN_, int WM = 2, int WN = 2>
+template <int BM_, int BN_, int WM = 2, int WN = 2, int PF = 1>
 __global__ __launch_bounds__(64 * WM * WN, 2) void wgrad_kernel(WgradGeom g) {
   constexpr int NT = 64 * WM * WN;
   constexpr int LDM = BM_ + 16, LDN = BN_ + 16;
@@ -232,7 +240,11 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void wgrad_kernel(WgradGeom g) {
   const int wm = (w / WN) * (BM_ / WM), wn = (w % WN) * (BN_ / WN);
   constexpr int ACPR = BM_ / 8, BCPR = BN_ / 8;  // chunks per LDS row
 
-  u32x4 ra[ACH], rb[BCH];
+  // PF = 1: one register set, the next K-step's loads in flight during this one's MFMAs, __syncthreads per step.
+  // PF = 2: two register sets, K-steps kt+1 and kt+2 in flight; the per-step barrier is a raw s_barrier after
+  // lgkmcnt(0) (this wave's LDS traffic), so the younger register loads stay in flight across it (a
+  // __syncthreads would drain vmcnt to 0 and leave one step of latency hiding).
+  u32x4 ra[ACH], rb[BCH], ra2[ACH], rb2[BCH];
   // Per-thread constants: a thread always stages the same 16-byte column chunk, so its (tap, c) and the
   // row offsets of its chunks are fixed; only the pixel base moves (by 64) per K step.
   const int a_cc = t % ACPR, a_pr0 = t / ACPR;
@@ -248,8 +260,8 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void wgrad_kernel(WgradGeom g) {
   // bit of `okm`; the zeroing select happens at the LDS store, after this K-step's MFMAs.  (A per-lane
   // condition around a load compiles to a branch and a wait for that load: the staging loads of a K-step
   // were serialised on the memory latency.)
-  unsigned okm = 0u;
-  auto gload = [&](int p0) {
+  unsigned okm = 0u, okm2 = 0u;
+  auto gload = [&](u32x4* ra, u32x4* rb, unsigned& okm, int p0) {
     okm = 0u;
 #pragma unroll
     for (int i = 0; i < ACH; ++i) {
@@ -272,7 +284,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void wgrad_kernel(WgradGeom g) {
       okm |= (ok ? 1u : 0u) << (ACH + i);
     }
   };
-  auto lstore = [&](int buf) {
+  auto lstore = [&](int buf, const u32x4* ra, const u32x4* rb, unsigned okm) {
     const u32x4 z = {0u, 0u, 0u, 0u};
 #pragma unroll
     for (int i = 0; i < ACH; ++i) {
@@ -305,14 +317,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void wgrad_kernel(WgradGeom g) {
     for (int j = 0; j < JT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nk = (p_end - p_beg + 63) / 64;
-  if (nk > 0) {
-    gload(p_beg);
-    lstore(0);
-  }
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    gload(p_beg + (kt + 1 < nk ? kt + 1 : kt) * 64);  // unconditional (the last one re-reads, unused)
+  auto compute = [&](int cur) {
     const bf16_t* Aimg = &lds[cur][0];
     const bf16_t* Bimg = &lds[cur][64 * LDM];
 #pragma unroll
@@ -327,8 +332,40 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void wgrad_kernel(WgradGeom g) {
 #pragma unroll
         for (int j = 0; j < JT; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
-    if (kt + 1 < nk) lstore(cur ^ 1);
+  };
+  if (PF == 1) {
+    if (nk > 0) {
+      gload(ra, rb, okm, p_beg);
+      lstore(0, ra, rb, okm);
+    }
     __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      const int cur = kt & 1;
+      gload(ra, rb, okm, p_beg + (kt + 1 < nk ? kt + 1 : kt) * 64);  // unconditional (the last one re-reads, unused)
+      compute(cur);
+      if (kt + 1 < nk) lstore(cur ^ 1, ra, rb, okm);
+      __syncthreads();
+    }
+  } else {
+    // set 1 (ra, rb) carries the even K-steps, set 2 the odd ones; loads past the end re-read step nk-1, unused
+    auto kstep = [&](int k) { return p_beg + (k < nk ? k : nk - 1) * 64; };
+    if (nk > 0) {
+      gload(ra, rb, okm, p_beg);
+      gload(ra2, rb2, okm2, kstep(1));
+      lstore(0, ra, rb, okm);
+    }
+    lds_barrier();
+    for (int kt = 0; kt < nk; kt += 2) {
+      gload(ra, rb, okm, kstep(kt + 2));  // set 1 was stored into LDS by the previous step
+      compute(0);
+      if (kt + 1 < nk) lstore(1, ra2, rb2, okm2);
+      lds_barrier();
+      if (kt + 1 >= nk) break;
+      gload(ra2, rb2, okm2, kstep(kt + 3));
+      compute(1);
+      if (kt + 2 < nk) lstore(0, ra, rb, okm);
+      lds_barrier();
+    }
   }
   // partial tile -> this split's fp32 slab [K][R*S*C] (plain coalesced stores; summed by wgrad_reduce)
   float* slab = g.ws + (long)blockIdx.z * g.K * Ntot;
@@ -636,6 +673,161 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_pipe_kernel(ConvGeom g) 
     const int hh = rem / pc.Wc, ww = rem - hh * pc.Wc;
     return ((long)n * g.OH + 2 * hh + pc.ph) * g.OW + 2 * ww + pc.pw;
   };
+  // partial-row index of this tile for the fused reductions: ty, after the row tiles of the preceding parity
+  // classes in the PAR (stride-2) form
+  auto red_row = [&]() -> long {
+    long row_id = ty;
+    if (PAR)
+      for (int c2 = 0; c2 < (int)blockIdx.y; ++c2) {
+        const ParClass q = par_class(g, c2);
+        row_id += (g.N * q.Hc * q.Wc + BM_ - 1) / BM_;
+      }
+    return row_id;
+  };
+  if (g.vec) {
+    // 16-byte epilogue: each wave stages fp32 accumulators of 16-row groups of its TM x TN sub-tile in its own
+    // slice of the idle LDS ring, then every lane owns 8 consecutive columns of one row per pass: 16-byte
+    // residual / mask / BN-operand loads and one 16-byte bf16 store instead of 2-byte accesses per element.
+    // The fused column reductions (forward BN statistics of the stored bf16 values; the dgrad's BN-backward
+    // sums) accumulate per lane over its rows, then meet across the lanes sharing the columns (xor tree) and
+    // across the WM waves of a column (LDS, wave order): one writer per partial-row element, fixed order.
+    constexpr int LDT = TN + 4;
+    constexpr int WAVE_FLOATS = STAGES * BUF / 2 / WAVES;
+    constexpr int GI0 = WAVE_FLOATS / (16 * LDT);
+    constexpr int GI = GI0 < FM ? GI0 : FM;
+    static_assert(GI >= 1, "epilogue staging slice too small");
+    constexpr int LPR = TN / 8, RPP = 64 / LPR;
+    float* wl = reinterpret_cast<float*>(smem) + w * WAVE_FLOATS;
+    const int lr = lane / LPR, lc = (lane % LPR) * 8;
+    const int colv = n0 + wc * TN + lc;
+    const bool cok = colv < g.Ncols;
+    const bool do_bnr = DGRAD && g.bnr_red != nullptr;
+    const bool has_x2 = do_bnr && g.bnr_x2 != nullptr;
+    float mu[8], rs[8], mu2[8], rs2[8];
+    float sA[8], sB[8], sC[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int col = cok ? colv + e : 0;
+      mu[e] = do_bnr ? g.bnr_ms[2 * col] : 0.f;
+      rs[e] = do_bnr ? g.bnr_ms[2 * col + 1] : 0.f;
+      mu2[e] = has_x2 ? g.bnr_ms2[2 * col] : 0.f;
+      rs2[e] = has_x2 ? g.bnr_ms2[2 * col + 1] : 0.f;
+      sA[e] = sB[e] = sC[e] = 0.f;
+    }
+#pragma unroll
+    for (int i0 = 0; i0 < FM; i0 += GI) {
+#pragma unroll
+      for (int ii = 0; ii < GI; ++ii) {
+        if (i0 + ii >= FM) break;
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) wl[(ii * 16 + fq * 4 + r) * LDT + j * 16 + fr] = acc[i0 + ii][j][r];
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const int nrows = (FM - i0 < GI ? FM - i0 : GI) * 16;
+#pragma unroll
+      for (int rr = 0; rr < GI * 16; rr += RPP) {
+        const int rl = rr + lr;
+        const int row = m0 + wr * TM + i0 * 16 + rl;
+        if (rl < nrows && row < M && cok) {
+          const f32x4 lo = *reinterpret_cast<const f32x4*>(&wl[rl * LDT + lc]);
+          const f32x4 hi = *reinterpret_cast<const f32x4*>(&wl[rl * LDT + lc + 4]);
+          float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          const long e0 = out_row(row) * g.ldy + colv;
+          if (DGRAD && g.R_) {
+            const u32x4 rv = *reinterpret_cast<const u32x4*>(g.R_ + e0);
+            const u32x4 mv = g.Rmask ? *reinterpret_cast<const u32x4*>(g.Rmask + e0) : u32x4{1u, 1u, 1u, 1u};
+            const bf16_t* rh = reinterpret_cast<const bf16_t*>(&rv);
+            const bf16_t* mh = reinterpret_cast<const bf16_t*>(&mv);
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+              if (!g.Rmask || bf2f(mh[e]) > 0.f) v[e] += bf2f(rh[e]);
+          }
+          u32x4 ov;
+          bf16_t* oh = reinterpret_cast<bf16_t*>(&ov);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            oh[e] = f2bf(v[e]);
+            v[e] = bf2f(oh[e]);  // the stored value feeds the reductions
+          }
+          *reinterpret_cast<u32x4*>(g.Y + e0) = ov;
+          if (do_bnr) {
+            const u32x4 mv = *reinterpret_cast<const u32x4*>(g.bnr_mask + e0);
+            const u32x4 xv = *reinterpret_cast<const u32x4*>(g.bnr_x + e0);
+            const u32x4 x2v = has_x2 ? *reinterpret_cast<const u32x4*>(g.bnr_x2 + e0) : u32x4{0u, 0u, 0u, 0u};
+            const bf16_t* mh = reinterpret_cast<const bf16_t*>(&mv);
+            const bf16_t* xh = reinterpret_cast<const bf16_t*>(&xv);
+            const bf16_t* x2h = reinterpret_cast<const bf16_t*>(&x2v);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const float gv = bf2f(mh[e]) > 0.f ? v[e] : 0.f;
+              sA[e] += gv;
+              sB[e] += gv * (bf2f(xh[e]) - mu[e]) * rs[e];
+              if (has_x2) sC[e] += gv * (bf2f(x2h[e]) - mu2[e]) * rs2[e];
+            }
+          }
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    if (do_bnr) {
+    // lanes sharing this lane's 8 columns: lane % LPR equal -> xor over the row bits of the lane index
+#pragma unroll
+    for (int o = LPR; o < 64; o <<= 1)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        sA[e] += __shfl_xor(sA[e], o, 64);
+        sB[e] += __shfl_xor(sB[e], o, 64);
+        if (has_x2) sC[e] += __shfl_xor(sC[e], o, 64);
+      }
+    // the WM waves of a column range meet in LDS: red[(wr*WN + wc)][TN][3]
+    float* red = reinterpret_cast<float*>(smem);
+    __syncthreads();  // every wave is past its staging slice
+    if (wr > 0 && lane < LPR)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float* o = red + ((wr * WN + wc) * TN + lc + e) * 3;
+        o[0] = sA[e];
+        o[1] = sB[e];
+        o[2] = sC[e];
+      }
+    __syncthreads();
+    if (wr != 0 || lane >= LPR || !cok) return;
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+#pragma unroll
+      for (int q = 1; q < WM; ++q) {
+        const float* o = red + ((q * WN + wc) * TN + lc + e) * 3;
+        sA[e] += o[0];
+        sB[e] += o[1];
+        sC[e] += o[2];
+      }
+    {
+      const long slab = red_row() * g.Ncols * 2 + 2 * colv;
+#pragma unroll
+      for (int e = 0; e < 8; e += 2) {
+        *reinterpret_cast<f32x4*>(g.bnr_red + slab + 2 * e) = f32x4{sA[e], sB[e], sA[e + 1], sB[e + 1]};
+        if (g.bnr_red2)
+          *reinterpret_cast<f32x4*>(g.bnr_red2 + slab + 2 * e) = f32x4{sA[e], sC[e], sA[e + 1], sC[e + 1]};
+      }
+    }
+    return;
+    }  // do_bnr
+    if (!g.stats) return;
+    // forward BN statistics from the accumulator layout (column = lane & 15: two shuffles per value, cheaper than
+    // the 8-column lane reduction) over the stored, bf16-rounded values
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[i][j][r] = bf2f(f2bf(acc[i][j][r]));
+  } else {
 #pragma unroll
   for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -732,6 +924,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_pipe_kernel(ConvGeom g) 
       }
     }
   }
+  }  // !g.vec
   if (g.stats) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
@@ -861,6 +1054,26 @@ int launch_conv(ConvGeom& g, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
+// MER_WGRAD_VARIANT overrides the default weight-gradient variant (A/B switch for tools/bench_conv.py)
+// (tools/bench_conv.py: the 2-deep register prefetch wins on the 64-column tiles -- stem, layer1 -- and loses on
+// 128 x 128, where its 160 VGPRs leave one 8-wave block per CU)
+int wgrad_default_variant(int K) {
+  static const int v = [] {
+    const char* e = getenv("MER_WGRAD_VARIANT");
+    return e ? atoi(e) : 0;
+  }();
+  return v > 0 ? v : (K <= 64 ? 3 : 2);
+}
+
+// MER_CONV_VEC=0 keeps the 2-byte epilogue (A/B switch for tools/bench_conv.py)
+bool vec_epilogue_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("MER_CONV_VEC");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 }  // namespace
 
 MER_API int mer_conv_fwd(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, const void* x,
@@ -878,6 +1091,7 @@ MER_API int mer_conv_fwd_ex(int N, int H, int W, int C, int K, int R, int S, int
   g.R = R; g.S = S; g.st = stride; g.pad = pad;
   g.Ncols = K; g.Kred = R * S * C;
   g.X = (const bf16_t*)x; g.Wt = (const bf16_t*)w_packed; g.Y = (bf16_t*)y; g.ldy = K; g.stats = stats;
+  g.vec = vec_epilogue_enabled() && conv_vec_ok(g);
   if (variant == 0) return launch_conv<false>(g, (hipStream_t)stream);
   return launch_conv_pipe<false, false>(g, (hipStream_t)stream, variant);
 }
@@ -912,6 +1126,7 @@ MER_API int mer_conv_dgrad_bnr(int N, int H, int W, int C, int K, int R, int S, 
   g.R_ = (const bf16_t*)residual; g.Rmask = (const bf16_t*)residual_mask;
   g.bnr_mask = (const bf16_t*)bn_mask; g.bnr_x = (const bf16_t*)bn_x; g.bnr_ms = bn_ms; g.bnr_red = bn_red;
   g.bnr_x2 = (const bf16_t*)bn_x2; g.bnr_ms2 = bn_ms2; g.bnr_red2 = bn_red2;
+  g.vec = vec_epilogue_enabled() && conv_vec_ok(g);
   if (variant == 0 || stride > 2) return launch_conv<true>(g, (hipStream_t)stream);
   if (stride == 2) return launch_conv_pipe<true, true>(g, (hipStream_t)stream, variant);
   return launch_conv_pipe<true, false>(g, (hipStream_t)stream, variant);
@@ -925,8 +1140,8 @@ MER_API int mer_conv_wgrad(int N, int H, int W, int C, int Creal, int K, int R, 
 static int conv_wgrad_impl(int N, int H, int W, int C, int Creal, int K, int R, int S, int stride, int pad,
                            const void* x, const void* dy, long ldy, float* dw, int splits, float* workspace,
                            int variant, void* stream) {
-  if (C % 8 || K % 8 || variant < -1 || variant > 2 || R * S > 49) return (int)hipErrorInvalidValue;
-  if (variant == -1) variant = 2;
+  if (C % 8 || K % 8 || variant < -1 || variant > 3 || R * S > 49) return (int)hipErrorInvalidValue;
+  if (variant == -1) variant = wgrad_default_variant(K);
   WgradGeom g{};
   g.N = N; g.H = H; g.W = W; g.C = C; g.Creal = Creal;
   g.Ho = (H + 2 * pad - R) / stride + 1; g.Wo = (W + 2 * pad - S) / stride + 1; g.K = K;
@@ -943,12 +1158,16 @@ static int conv_wgrad_impl(int N, int H, int W, int C, int Creal, int K, int R, 
     dim3 grid(((Ntot + 127) / 128) * ((K + 63) / 64), 1, splits);
     if (variant == 1)
       hipLaunchKernelGGL((wgrad_kernel<64, 128>), grid, dim3(256), 0, st, g);
+    else if (variant == 3)
+      hipLaunchKernelGGL((wgrad_kernel<64, 128, 2, 4, 2>), grid, dim3(512), 0, st, g);
     else
       hipLaunchKernelGGL((wgrad_kernel<64, 128, 2, 4>), grid, dim3(512), 0, st, g);
   } else {
     dim3 grid(((Ntot + 127) / 128) * ((K + 127) / 128), 1, splits);
     if (variant == 1)
       hipLaunchKernelGGL((wgrad_kernel<128, 128>), grid, dim3(256), 0, st, g);
+    else if (variant == 3)
+      hipLaunchKernelGGL((wgrad_kernel<128, 128, 2, 4, 2>), grid, dim3(512), 0, st, g);
     else
       hipLaunchKernelGGL((wgrad_kernel<128, 128, 2, 4>), grid, dim3(512), 0, st, g);
   }
@@ -1095,27 +1314,54 @@ __global__ __launch_bounds__(256) void pack_w_batched_kernel(const long long* __
     const int k = blockIdx.x;
     if (k >= K) return;
     const float* src = w + (long)k * C * RS;
-    for (int i = threadIdx.x; i < C * RS; i += 256) tile[i] = src[i];  // [c][rs]
+    const int n = C * RS;
+    if ((n & 3) == 0 && (((uintptr_t)src) & 15) == 0) {
+      for (int i = threadIdx.x; i < n / 4; i += 256)
+        reinterpret_cast<f32x4*>(tile)[i] = reinterpret_cast<const f32x4*>(src)[i];  // [c][rs]
+    } else {
+      for (int i = threadIdx.x; i < n; i += 256) tile[i] = src[i];
+    }
     __syncthreads();
     bf16_t* dst = out + (long)k * RS * Cp;
-    for (int i = threadIdx.x; i < RS * Cp; i += 256) {  // i = rs*Cp + c
-      const int rs = i / Cp, c = i - rs * Cp;
-      dst[i] = c < C ? f2bf(tile[c * RS + rs]) : (bf16_t)0;
+    // 8 consecutive channels of one tap per thread, one 16-byte store (Cp % 8 == 0); i / Cp by reciprocal
+    const float inv_Cp = 1.f / Cp;
+    for (int i = threadIdx.x; i < RS * Cp / 8; i += 256) {  // i*8 = rs*Cp + c0
+      const int rs = fdiv(i * 8, inv_Cp), c0 = i * 8 - rs * Cp;
+      uint32_t pk[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int c = c0 + 2 * e;
+        const uint32_t lo = c < C ? f2bf(tile[c * RS + rs]) : 0u, hi = c + 1 < C ? f2bf(tile[(c + 1) * RS + rs]) : 0u;
+        pk[e] = lo | (hi << 16);
+      }
+      *reinterpret_cast<uint4*>(dst + (long)i * 8) = uint4{pk[0], pk[1], pk[2], pk[3]};
     }
   } else {
     const int kb = (K + 63) / 64;
     const int c = blockIdx.x / kb, k0 = (blockIdx.x - c * kb) * 64;
     if (c >= Cp) return;
     const int nk = min(64, K - k0);
+    const float inv_RS = 1.f / RS;
     for (int i = threadIdx.x; i < nk * RS; i += 256) {  // [kk][rs]
-      const int kk = i / RS, rs = i - kk * RS;
+      const int kk = fdiv(i, inv_RS), rs = i - kk * RS;
       tile[i] = c < C ? w[((long)(k0 + kk) * C + c) * RS + rs] : 0.f;
     }
     __syncthreads();
     bf16_t* dst = out + (long)c * RS * K + k0;
-    for (int i = threadIdx.x; i < RS * nk; i += 256) {  // i = rs*nk + kk
-      const int rs = i / nk, kk = i - rs * nk;
-      dst[(long)rs * K + kk] = f2bf(tile[kk * RS + rs]);
+    if (nk == 64 && (K & 7) == 0) {  // 8 consecutive output channels per thread, one 16-byte store
+      for (int i = threadIdx.x; i < RS * 8; i += 256) {  // i = rs*8 + kk0/8
+        const int rs = i >> 3, kk0 = (i & 7) * 8;
+        uint32_t pk[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          pk[e] = (uint32_t)f2bf(tile[(kk0 + 2 * e) * RS + rs]) | ((uint32_t)f2bf(tile[(kk0 + 2 * e + 1) * RS + rs]) << 16);
+        *reinterpret_cast<uint4*>(dst + (long)rs * K + kk0) = uint4{pk[0], pk[1], pk[2], pk[3]};
+      }
+    } else {
+      for (int i = threadIdx.x; i < RS * nk; i += 256) {  // i = rs*nk + kk
+        const int rs = i / nk, kk = i - rs * nk;
+        dst[(long)rs * K + kk] = f2bf(tile[kk * RS + rs]);
+      }
     }
   }
 }

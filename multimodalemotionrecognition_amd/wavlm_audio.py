@@ -318,49 +318,33 @@ class WavLMBackbone(nn.Module):
         if capture is None and not G.capturing():
             # a prefix run (stage 2) is keyed on the prefix's weights only: the trainable tail changes every step
             wkey = self._weights_key()
-            split = K.PROBE is not None and K.PROBE.active and K.PROBE.name == "gemm_bf16"
-            key = (tuple(wav.shape), out_dtype, wav.device.index, nl, draw is not None, split,
+            key = (tuple(wav.shape), out_dtype, wav.device.index, nl, draw is not None,
                    wkey if nl is None else wkey[:self._prefix_param_count(nl)])
             if self._graphs.ready(key):
-                return self._forward_graphed(wav, out_dtype, key, nl, draw, split)
+                return self._forward_graphed(wav, out_dtype, key, nl, draw)
         ctl = self.train_ctl(draw, wav.device)
         x, L = self._stage_a(wav)
         y = self._conv_layer(x, 1, L)
         return self._stage_b(y, L, out_dtype, nl, capture, ctl)
 
-    def _forward_graphed(self, wav, out_dtype, key, nl=None, draw=None, split=False):
-        """One captured graph per key.  ``split`` (bench.py's kernel probe only, never the timed schedule): two
-        graphs around an eager launch of the feature-extractor conv1 GEMM, which the probe brackets with HIP
-        events on its stream."""
+    def _forward_graphed(self, wav, out_dtype, key, nl=None, draw=None):
+        """One captured graph per key (the whole forward, conv0 .. final LayerNorm)."""
         g = self._graphs.get(key)
         if g is None:
             ctl = None
             if draw is not None:  # static RNG-base / LayerDrop-mask scalars the graph reads
                 ctl = self.train_ctl(draw, wav.device)
-            if split:
-                ga = G.StaticGraph(lambda w: self._stage_a(w)[0], [wav])
-                B, L0 = wav.shape[0], ga.out.shape[1]
-                L1 = (L0 - CONV_KERNEL[1]) // CONV_STRIDE[1] + 1
-                y1 = torch.empty(B, L1, CONV_DIM, device=wav.device, dtype=torch.bfloat16)
-                gb = G.StaticGraph(lambda: self._stage_b(y1, L0, out_dtype, nl, None, ctl), [])
-                graph = (ga, y1, gb)
-            else:
-                def run(w):
-                    x, L0 = self._stage_a(w)
-                    return self._stage_b(self._conv_layer(x, 1, L0), L0, out_dtype, nl, None, ctl)
+            def run(w):
+                x, L0 = self._stage_a(w)
+                return self._stage_b(self._conv_layer(x, 1, L0), L0, out_dtype, nl, None, ctl)
 
-                graph = G.StaticGraph(run, [wav])
+            graph = G.StaticGraph(run, [wav])
             # the graph reads the packed weights captured with it: keep that pack alive (a later full repack,
             # e.g. after the stage-2 tail moved, replaces self._packed while a prefix key still matches)
             g = self._graphs.put(key, (graph, ctl, self._packed))
         graph, ctl, _ = g
         if draw is not None:
             self.train_ctl(draw, wav.device, ctl.rng, ctl.skip)
-        if split:
-            ga, y1, gb = graph
-            x = ga.replay(wav)
-            self._conv_layer(x, 1, x.shape[1], out=y1)
-            return G.hand_out(gb.replay())
         return G.hand_out(graph.replay(wav))
 
     def _stage_a(self, wav):

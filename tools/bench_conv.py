@@ -19,6 +19,7 @@ VARIANTS = [int(v) for v in next((a.split("=")[1] for a in sys.argv if a.startsw
 WGRAD_V = [int(v) for v in next((a.split("=")[1] for a in sys.argv if a.startswith("--wgrad-variants=")), "1,2").split(",")
            if v]
 WGRAD = "--no-wgrad" not in sys.argv
+FUSED = "--fused" in sys.argv  # dgrad as in the train step: residual under a ReLU mask + the fused BN-backward sums
 
 
 def timeit(fn, reps=20):
@@ -45,7 +46,7 @@ def main():
         wt = torch.empty(C, R * R * Kc, device="cuda", dtype=torch.bfloat16)
         K.pack_conv_weight(w, wt, C, True)
         y = torch.empty(NF, Ho, Ho, Kc, device="cuda", dtype=torch.bfloat16)
-        stats = K.bn_stats_buffer(Kc, "cuda")
+        stats = K.bn_stats_buffer(Kc, "cuda", NF * Ho * Ho)
         dy = (torch.rand(NF, Ho, Ho, Kc, device="cuda") * 2 - 1).bfloat16()
         dx = torch.empty(NF, H, H, C, device="cuda", dtype=torch.bfloat16)
         flop = 2.0 * NF * Ho * Ho * Kc * R * R * C
@@ -55,9 +56,17 @@ def main():
             tw = timeit(lambda: K.conv_wgrad(x, dy, dw, R, R, st, pad, variant=v))
             line += f" | wgrad v{v} {tw*1e3:7.1f}us {flop/tw/1e9:6.1f}TF"
         ref_y = ref_dx = None
+        fk = {}
+        if FUSED and H != 59:
+            res = (torch.rand_like(dx.float()) * 2 - 1).bfloat16()
+            msk = (torch.rand_like(dx.float()) - 0.5).relu().bfloat16()
+            xb = (torch.rand_like(dx.float()) * 2 - 1).bfloat16()
+            ms = torch.stack([torch.zeros(C, device="cuda"), torch.ones(C, device="cuda")], 1).contiguous()
+            red = torch.zeros(K.bn_red_rows(NF * H * H), C, 2, device="cuda")
+            fk = dict(residual=res, mask=msk, bnr=(msk, xb, ms, red))
         for v in VARIANTS:
             tf = timeit(lambda: K.conv_fwd(x, wp, y, stats, R, R, st, pad, variant=v))
-            tb = timeit(lambda: K.conv_dgrad(dy, wt, dx, R, R, st, pad, variant=v)) if H != 59 else float("nan")
+            tb = timeit(lambda: K.conv_dgrad(dy, wt, dx, R, R, st, pad, variant=v, **fk)) if H != 59 else float("nan")
             if ref_y is None:
                 ref_y, ref_dx = y.clone(), dx.clone()
             elif not (torch.equal(ref_y, y) and (H == 59 or torch.equal(ref_dx, dx))):

@@ -63,6 +63,20 @@ def main():
                 d = float((outs[v] - outs[ref_v]).abs().max()) if v != ref_v else 0.0
                 print(f"{name:14s} M={M:6d} N={N:5d} K={Kd:5d} v{v}: {ms*1e3:8.1f} us {2*M*N*Kd/ms/1e9:7.1f} TF/s  maxdiff_vs_first={d:.3g}",
                       flush=True)
+        if "--blas" in sys.argv and not rows:  # calibration only: the vendor library (hipBLASLt) on the same shape
+            wt = w.t()
+            for _ in range(3):
+                torch.matmul(a, wt)
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(20):
+                torch.matmul(a, wt)
+            e1.record()
+            torch.cuda.synchronize()
+            ms = e0.elapsed_time(e1) / 20
+            print(f"{name:14s} M={M:6d} N={N:5d} K={Kd:5d} torch.matmul (hipBLASLt): {ms*1e3:8.1f} us "
+                  f"{2*M*N*Kd/ms/1e9:7.1f} TF/s", flush=True)
 
 
 if __name__ == "__main__":
