@@ -383,6 +383,156 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void wgrad_kernel(WgradGeom g) {
     }
 }
 
+// wgrad on a global_load_lds ring (the conv_pipe_kernel structure): no staging registers, STAGES-1 K-steps of
+// 64 pixels in flight across each barrier (counted vmcnt + raw s_barrier).  LDS images [64 pixels][BM | BN]
+// are dense rows of 16-byte chunks, chunk c of row r stored at c ^ wswz(r) (the DMA writes lane-linear, so the
+// XOR is applied to each lane's SOURCE chunk and to the transposed fragment read): the 4 rows one
+// ds_read_b64_tr_b16 lane group reads land on distinct bank groups.  Spatial padding, pixels past the split
+// and channels past K / R*S*C read a 16-byte zero chunk in global memory.  Same partial slabs as wgrad_kernel.
+__device__ __attribute__((aligned(16))) uint32_t mer_conv_zero16[4] = {0u, 0u, 0u, 0u};
+
+__device__ __forceinline__ int wswz(int row, int nchunks) { return ((row & 7) << 1) & (nchunks - 1); }
+
+template <int BM_, int BN_, int WM, int WN, int STAGES>
+__global__ __launch_bounds__(64 * WM * WN, 2) void wgrad_pipe_kernel(WgradGeom g) {
+  constexpr int WAVES = WM * WN;
+  constexpr int ACW = BM_ / 8, BCW = BN_ / 8;           // 16-byte chunks per LDS row
+  constexpr int ARI = 64 / ACW, BRI = 64 / BCW;         // rows per glds instruction
+  constexpr int IA = 64 / ARI / WAVES, IB = 64 / BRI / WAVES;  // glds per wave per K-step
+  static_assert(IA * ARI * WAVES == 64 && IB * BRI * WAVES == 64, "64-pixel K-step must split into glds rows");
+  constexpr int IT = BM_ / WM / 16, JT = BN_ / WN / 16;
+  constexpr int BUF = 64 * (BM_ + BN_);                 // bf16 elements per ring slot
+  extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int Ntot = g.R * g.S * g.C;
+  const int P = g.N * g.Ho * g.Wo;
+  const int wnx = (Ntot + BN_ - 1) / BN_, wny = (g.K + BM_ - 1) / BM_;
+  int wtx, wty;
+  xcd_tile(blockIdx.x, wnx, wnx * wny, wtx, wty);
+  const int m0 = wty * BM_, n0 = wtx * BN_;
+  const int p_beg = blockIdx.z * g.pix_per_split, p_end = min(P, p_beg + g.pix_per_split);
+  const int wm = (w / WN) * (BM_ / WM), wn = (w % WN) * (BN_ / WN);
+  const bf16_t* zero = reinterpret_cast<const bf16_t*>(mer_conv_zero16);
+
+  // per-lane constants of each glds: its LDS row inside the K-step and its (logical) column chunk
+  int arow[IA], acol[IA];
+  bool acok[IA];
+#pragma unroll
+  for (int j = 0; j < IA; ++j) {
+    const int row = (w * IA + j) * ARI + lane / ACW;
+    arow[j] = row;
+    acol[j] = m0 + ((lane % ACW) ^ wswz(row, ACW)) * 8;
+    acok[j] = acol[j] < g.K;
+  }
+  int brow[IB], bc[IB], br[IB], bs[IB];
+  bool bcok[IB];
+  const float inv_C = 1.f / g.C, inv_S = 1.f / g.S, inv_HoWo = 1.f / (g.Ho * g.Wo), inv_Wo = 1.f / g.Wo;
+#pragma unroll
+  for (int j = 0; j < IB; ++j) {
+    const int row = (w * IB + j) * BRI + lane / BCW;
+    brow[j] = row;
+    const int col = n0 + ((lane % BCW) ^ wswz(row, BCW)) * 8;
+    bcok[j] = col < Ntot;
+    const int cc = bcok[j] ? col : 0;
+    const int tap = fdiv(cc, inv_C);
+    bc[j] = cc - tap * g.C;
+    br[j] = fdiv(tap, inv_S);
+    bs[j] = tap - br[j] * g.S;
+  }
+  const int HoWo = g.Ho * g.Wo;
+  auto stage = [&](int slot, int p0) {
+    bf16_t* la = smem + slot * BUF;
+    bf16_t* lb = la + 64 * BM_;
+#pragma unroll
+    for (int j = 0; j < IA; ++j) {
+      const int p = p0 + arow[j];
+      glds16(p < p_end && acok[j] ? g.dY + (long)p * g.ldy + acol[j] : zero, la + (w * IA + j) * 512);
+    }
+#pragma unroll
+    for (int j = 0; j < IB; ++j) {
+      const int p = p0 + brow[j];
+      const int pc = p < p_end ? p : p_beg;
+      const int n = fdiv(pc, inv_HoWo);
+      const int rem = pc - n * HoWo;
+      const int oh = fdiv(rem, inv_Wo), ow = rem - oh * g.Wo;
+      const int ih = oh * g.st - g.pad + br[j], iw = ow * g.st - g.pad + bs[j];
+      const bool ok = p < p_end && bcok[j] && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W;
+      glds16(ok ? g.X + (((long)n * g.H + ih) * g.W + iw) * g.C + bc[j] : zero, lb + (w * IB + j) * 512);
+    }
+  };
+  // transposed fragment from a swizzled image with CW chunks per row: elements j = 0..7 =
+  // Img[k0 + 8*(lane>>4) + j][c0 + (lane&15)]
+  auto tr_frag = [&](const bf16_t* img, int CW, int k0, int c0) -> bf16x8 {
+    const int q = (lane & 15) >> 2, p4 = (lane & 3) * 4;
+    const int kr = k0 + 8 * (lane >> 4);
+    const int lc = (c0 + p4) >> 3, sub = (c0 + p4) & 7;
+    typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+    const int r0 = kr + q, r1 = kr + 4 + q;
+    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (lds_s16x4*)(img + r0 * CW * 8 + ((lc ^ wswz(r0, CW)) << 3) + sub));
+    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (lds_s16x4*)(img + r1 * CW * 8 + ((lc ^ wswz(r1, CW)) << 3) + sub));
+    typedef __attribute__((ext_vector_type(8))) short s16x8;
+    s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8, v);
+  };
+
+  f32x4 acc[IT][JT];
+#pragma unroll
+  for (int i = 0; i < IT; ++i)
+#pragma unroll
+    for (int j = 0; j < JT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nk = (p_end - p_beg + 63) / 64;
+  constexpr int G = IA + IB;
+#pragma unroll
+  for (int s = 0; s < STAGES - 1; ++s)
+    if (s < nk) stage(s, p_beg + s * 64);
+  for (int kt = 0; kt < nk; ++kt) {
+    const int ahead = (nk - 1 - kt) < (STAGES - 2) ? (nk - 1 - kt) : (STAGES - 2);
+    wait_tiles_in_flight<G>(ahead);
+    lds_barrier();
+    if (kt + STAGES - 1 < nk) stage((kt + STAGES - 1) % STAGES, p_beg + (kt + STAGES - 1) * 64);
+    const bf16_t* Aimg = smem + (kt % STAGES) * BUF;
+    const bf16_t* Bimg = Aimg + 64 * BM_;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8 af[IT], bfr[JT];
+#pragma unroll
+      for (int i = 0; i < IT; ++i) af[i] = tr_frag(Aimg, ACW, s * 32, wm + i * 16);
+#pragma unroll
+      for (int j = 0; j < JT; ++j) bfr[j] = tr_frag(Bimg, BCW, s * 32, wn + j * 16);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < IT; ++i)
+#pragma unroll
+        for (int j = 0; j < JT; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+  }
+  float* slab = g.ws + (long)blockIdx.z * g.K * Ntot;
+#pragma unroll
+  for (int i = 0; i < IT; ++i)
+#pragma unroll
+    for (int j = 0; j < JT; ++j) {
+      const int nn = n0 + wn + j * 16 + (lane & 15);
+      if (nn >= Ntot) continue;
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int k = m0 + wm + i * 16 + (lane >> 4) * 4 + rr;
+        if (k < g.K) slab[(long)k * Ntot + nn] = acc[i][j][rr];
+      }
+    }
+}
+
+template <int BM_, int BN_, int WM, int WN, int STAGES>
+void launch_wgrad_pipe(const WgradGeom& g, dim3 grid, hipStream_t st) {
+  const size_t lds = (size_t)STAGES * 64 * (BM_ + BN_) * sizeof(bf16_t);
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_pipe_kernel<BM_, BN_, WM, WN, STAGES>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+    return;
+  hipLaunchKernelGGL((wgrad_pipe_kernel<BM_, BN_, WM, WN, STAGES>), grid, dim3(64 * WM * WN), lds, st, g);
+}
+
 // slab0[i] = sum_z ws[z][i] over the flat [K][R*S*C] index.  A block owns E = 256/SG consecutive elements
 // and SG split-groups: thread (sg, e) sums splits sg, sg+SG, ... with 4 independent loads in flight (the
 // split count reaches ~100 on the stem / layer1, where one serial chain per element was latency-bound),
@@ -475,7 +625,6 @@ __global__ __launch_bounds__(256) void wgrad_scatter_kernel(int C, int Creal, in
 // gemm_bf16.hip's pipelined kernel.  Zero padding (spatial borders, dgrad's stride holes, K tail,
 // rows past M / N) is served by pointing the lane at a 16-byte zero chunk in global memory.
 // ---------------------------------------------------------------------------------------
-__device__ __attribute__((aligned(16))) uint32_t mer_conv_zero16[4] = {0u, 0u, 0u, 0u};
 
 __device__ __forceinline__ int cswz(int row, int c) { return c ^ ((row >> 1) & 7); }
 
@@ -1055,14 +1204,16 @@ int launch_conv(ConvGeom& g, hipStream_t st) {
 }
 
 // MER_WGRAD_VARIANT overrides the default weight-gradient variant (A/B switch for tools/bench_conv.py)
-// (tools/bench_conv.py: the 2-deep register prefetch wins on the 64-column tiles -- stem, layer1 -- and loses on
-// 128 x 128, where its 160 VGPRs leave one 8-wave block per CU)
+// (tools/bench_conv.py, ResNet18 layers at 256 frames: the global_load_lds ring, variant 4, is 1.1-1.25x the
+// register-staged kernel on the stem, layer1, layer3 and layer4 and within 4% elsewhere; its 3-stage form, at one
+// block per CU, is slower)
 int wgrad_default_variant(int K) {
   static const int v = [] {
     const char* e = getenv("MER_WGRAD_VARIANT");
     return e ? atoi(e) : 0;
   }();
-  return v > 0 ? v : (K <= 64 ? 3 : 2);
+  (void)K;
+  return v > 0 ? v : 4;
 }
 
 // MER_CONV_VEC=0 keeps the 2-byte epilogue (A/B switch for tools/bench_conv.py)
@@ -1140,7 +1291,7 @@ MER_API int mer_conv_wgrad(int N, int H, int W, int C, int Creal, int K, int R, 
 static int conv_wgrad_impl(int N, int H, int W, int C, int Creal, int K, int R, int S, int stride, int pad,
                            const void* x, const void* dy, long ldy, float* dw, int splits, float* workspace,
                            int variant, void* stream) {
-  if (C % 8 || K % 8 || variant < -1 || variant > 3 || R * S > 49) return (int)hipErrorInvalidValue;
+  if (C % 8 || K % 8 || variant < -1 || variant > 5 || R * S > 49) return (int)hipErrorInvalidValue;
   if (variant == -1) variant = wgrad_default_variant(K);
   WgradGeom g{};
   g.N = N; g.H = H; g.W = W; g.C = C; g.Creal = Creal;
@@ -1158,6 +1309,10 @@ static int conv_wgrad_impl(int N, int H, int W, int C, int Creal, int K, int R, 
     dim3 grid(((Ntot + 127) / 128) * ((K + 63) / 64), 1, splits);
     if (variant == 1)
       hipLaunchKernelGGL((wgrad_kernel<64, 128>), grid, dim3(256), 0, st, g);
+    else if (variant == 4)
+      launch_wgrad_pipe<64, 128, 2, 4, 2>(g, grid, st);
+    else if (variant == 5)
+      launch_wgrad_pipe<64, 128, 2, 4, 3>(g, grid, st);
     else if (variant == 3)
       hipLaunchKernelGGL((wgrad_kernel<64, 128, 2, 4, 2>), grid, dim3(512), 0, st, g);
     else
@@ -1166,6 +1321,10 @@ static int conv_wgrad_impl(int N, int H, int W, int C, int Creal, int K, int R, 
     dim3 grid(((Ntot + 127) / 128) * ((K + 127) / 128), 1, splits);
     if (variant == 1)
       hipLaunchKernelGGL((wgrad_kernel<128, 128>), grid, dim3(256), 0, st, g);
+    else if (variant == 4)
+      launch_wgrad_pipe<128, 128, 2, 4, 2>(g, grid, st);
+    else if (variant == 5)
+      launch_wgrad_pipe<128, 128, 2, 4, 3>(g, grid, st);
     else if (variant == 3)
       hipLaunchKernelGGL((wgrad_kernel<128, 128, 2, 4, 2>), grid, dim3(512), 0, st, g);
     else

@@ -284,9 +284,12 @@ def test_dgrad_fused_bn_reduce_matches_standalone(stride, ds):
 
 
 @pytest.mark.parametrize("N,H,C,Kc,R,stride,pad", [(2, 28, 64, 64, 3, 1, 1), (2, 14, 128, 256, 3, 2, 1),
-                                                   (2, 30, 8, 64, 7, 2, 3), (4, 7, 512, 512, 3, 1, 1)])
+                                                   (2, 30, 8, 64, 7, 2, 3), (4, 7, 512, 512, 3, 1, 1),
+                                                   (32, 28, 64, 64, 3, 1, 1), (32, 28, 64, 128, 3, 2, 1),
+                                                   (64, 14, 128, 256, 3, 1, 1), (64, 7, 256, 512, 1, 2, 0)])
 def test_wgrad_variants_bit_identical(N, H, C, Kc, R, stride, pad):
-    """8-wave wgrad (default) == 4-wave wgrad: same pixel order per split, same split sum order."""
+    """Every wgrad variant gives the same bits: 4- / 8-wave register-staged (1, 2), 2-deep register prefetch (3),
+    global_load_lds ring with 2 / 3 stages (4, 5) -- same pixel order per split, same split sum order."""
     from multimodalemotionrecognition_amd import kernels as K
 
     torch.manual_seed(4)
@@ -295,11 +298,15 @@ def test_wgrad_variants_bit_identical(N, H, C, Kc, R, stride, pad):
     dy = torch.randn(N, Ho, Ho, Kc, device="cuda").bfloat16()
     creal = 3 if C == 8 else C
     out = []
-    for v in (1, 2):
+    for v in (1, 2, 3, 4, 5):
         dw = torch.zeros(Kc, creal, R, R, device="cuda")
         K.conv_wgrad(x, dy, dw, R, R, stride, pad, creal=creal, variant=v)
         out.append(dw)
-    assert torch.equal(out[0], out[1])
+    ref = (x.float().permute(0, 3, 1, 2)[:, :creal], dy.float().permute(0, 3, 1, 2))
+    dw_ref = torch.nn.grad.conv2d_weight(ref[0], (Kc, creal, R, R), ref[1], stride=stride, padding=pad)
+    assert (out[0] - dw_ref).abs().max() <= 5e-3 * dw_ref.abs().max() + 1e-3
+    for v, o in zip((2, 3, 4, 5), out[1:]):
+        assert torch.equal(out[0], o), f"variant {v} differs"
 
 
 @pytest.mark.parametrize("H", [112, 32])
