@@ -140,6 +140,7 @@ __device__ __forceinline__ void xcd_tile_grouped(int pid, int nx, int ny, int G,
   const int ntiles = nx * ny;
   const int q = ntiles / 8, r = ntiles % 8, xcd = pid % 8, loc = pid / 8;
   const int tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+  G = G < 1 ? 1 : G;
   const int band = G * nx, gid = tile / band, first = gid * G;
   const int gsz = ny - first < G ? ny - first : G;
   const int in = tile - gid * band;

@@ -52,6 +52,9 @@ struct GemmArgs {
   // tap u % kp_taps of channel block u / kp_taps, so the taps that re-read the same input rows (stride < taps)
   // run back to back and hit L2 instead of re-fetching from HBM.  kp_taps = 0: natural order.
   int kp_taps, kp_c;
+  // row bands of the XCD-grouped tile order (xcd_tile_grouped); 1 = plain row-major chunks, so the N-tiles of one
+  // row panel run back to back on one XCD and share the A panel through its L2
+  int tgroup;
 };
 
 // element offset of K-tile u (64 wide) in the K dimension
@@ -228,7 +231,7 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_pipe_kernel(GemmArgs g) {
   const int z = blockIdx.z;
   const int nx = (g.N + CF::BN - 1) / CF::BN, ny = (g.M + CF::BM - 1) / CF::BM;
   int tx, ty;
-  xcd_tile_grouped(blockIdx.x, nx, ny, 8, tx, ty);
+  xcd_tile_grouped(blockIdx.x, nx, ny, g.tgroup, tx, ty);
   const int m0 = ty * CF::BM, n0 = tx * CF::BN;
   const int wr = w / CF::WN, wc = w % CF::WN;
 
@@ -451,7 +454,7 @@ __global__ __launch_bounds__(PH_NT, 1) void gemm_phase_kernel(GemmArgs g) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int nx = (g.N + 255) / 256, ny = (g.M + 255) / 256;
   int tx, ty;
-  xcd_tile_grouped(blockIdx.x, nx, ny, 8, tx, ty);
+  xcd_tile_grouped(blockIdx.x, nx, ny, g.tgroup, tx, ty);
   const int m0 = ty * 256, n0 = tx * 256;
   const int wr = w >> 2, wc = w & 3;
   const int lrow = lane >> 3, lchunk = lane & 7;
@@ -655,6 +658,19 @@ int launch(const GemmArgs& g, int out_dtype, int groups, hipStream_t st) {
 }  // namespace
 
 namespace {
+// Tile order: with at most 4 column tiles of 256 (conv1..6: N = 512) the B operand is a few hundred KB and always
+// L2-resident, while the A row panel is the stream: keep a panel's N-tiles adjacent (group 1) so they run in lockstep
+// on one XCD and fetch the panel once.  Wider outputs (QKV, FFN-up) walk 8-row bands (the B panels dominate).
+// MER_GEMM_GROUP overrides (A/B).
+int tile_group(int N) {
+  static const int env = [] {
+    const char* e = getenv("MER_GEMM_GROUP");
+    return e ? atoi(e) : 0;
+  }();
+  if (env > 0) return env;
+  return (N + 255) / 256 <= 4 ? 1 : 8;
+}
+
 // 16-byte epilogue accesses: 8-column runs never straddle N, and every row start is 16-byte aligned
 bool vec_epilogue_ok(int N, const void* C, long ldc, const void* R, long ldr, long c_zoff) {
   if (N % 8 || ldc % 8 || c_zoff % 8 || (((uintptr_t)C) & 15)) return false;
@@ -696,6 +712,7 @@ MER_API int mer_gemm_bf16_tr(int M, int N, int K, const void* A, long a_gstride,
   g.C = C; g.ldc = ldc; g.c_zoff = 0;
   g.bias = bias; g.R = (const bf16_t*)R; g.ldr = ldr; g.act = act;
   g.vec_epi = vec_epilogue_ok(N, C, ldc, R, ldr, 0);
+  g.tgroup = tile_group(N);
   g.drop_p = drop_p; g.drop_seed = drop_seed; g.drop_site = drop_site; g.skip_mask = skip_mask; g.skip_bit = skip_bit;
   static const bool kperm_on = [] {
     const char* e = getenv("MER_GEMM_KPERM");  // A/B switch for tools/bench_gemm.py (default on)
@@ -743,6 +760,7 @@ MER_API int mer_posconv_gemm_bf16(int B, int L, int C_total, int groups, int tap
   g.C = out; g.ldc = ldo; g.c_zoff = cg;
   g.bias = bias; g.R = (const bf16_t*)R; g.ldr = ldr; g.act = act;
   g.vec_epi = vec_epilogue_ok(cg, out, ldo, R, ldr, g.c_zoff);
+  g.tgroup = 8;
   if (g.K % 64 == 0 && (((uintptr_t)X | (uintptr_t)Wp) & 15) == 0)
     return launch_pipe<CfgP, 1>(g, out_dtype, (hipStream_t)stream, groups);
   return launch<1>(g, out_dtype, groups, (hipStream_t)stream);

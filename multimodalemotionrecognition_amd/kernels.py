@@ -503,6 +503,7 @@ def partials_sum(parts_buf, out):
 # 16 64-pixel steps per split was the whole time: 26 -> 19 us) and 512 where the output has so many tiles that
 # 1024 leaves only 4 splits (layer4 3x3: 65 -> 58 us).  MER_WGRAD_MIN_PIX overrides (A/B).
 _WGRAD_MIN_PIX = int(os.environ.get("MER_WGRAD_MIN_PIX", "0"))
+_WGRAD_WGS = int(os.environ.get("MER_WGRAD_WGS", "768"))  # target workgroups per wgrad launch (A/B)
 
 
 def _wgrad_min_pix(out_elems, tiles):
@@ -521,7 +522,7 @@ def conv_wgrad(x, dy, dw, R, S, stride, pad, creal=None, variant=-1, splits=None
     P = N * Ho * Wo
     tiles = ((Kc + 127) // 128) * ((R * S * C + 127) // 128)
     if splits is None:  # ~768 workgroups (3 per CU), >= _wgrad_min_pix pixels each
-        splits = int(max(1, min(-(-768 // tiles), P // _wgrad_min_pix(Kc * R * S * C, tiles))))
+        splits = int(max(1, min(-(-_WGRAD_WGS // tiles), P // _wgrad_min_pix(Kc * R * S * C, tiles))))
     ws = torch.empty(splits * Kc * R * S * C, device=x.device, dtype=torch.float32)
     _launch("conv_wgrad", (N, H, W, C, Kc, R, stride), "mer_conv_wgrad_ex", N, H, W, C, creal, Kc, R, S, stride, pad,
             x.data_ptr(), dy.data_ptr(), dw.data_ptr(), int(splits), ws.data_ptr(), int(variant), stream_ptr())
