@@ -318,6 +318,22 @@ int mer_wavlm_attention_bwd(int B, int L, int H, const void* qkv, long ldqkv, co
                             const void* dout, long ldo, const float* gate_w, const float* gate_b,
                             const float* gate_const, const float* tbl, float scale, void* scratch,
                             void* dqkv, long lddq, float* dx_gate, long lddxg, float* gate_part, void* stream);
+/* Train mode (stage-2 fine-tuning with the reference's attention dropout, TF:206-228): the same backward for a forward
+ * run with mer_wavlm_attention_tr(drop_p, seed, site): the probability mask (index ((b*H+h)*L + i)*L + j) is
+ * regenerated, dP = (dO V^T) o M and dV = (P o M)^T dO.  drop_p = 0 is mer_wavlm_attention_bwd.
+ * Replaces: the backward of F.multi_head_attention_forward's dropout_p inside WavLMAttention (TF:206-228). */
+int mer_wavlm_attention_bwd_tr(int B, int L, int H, const void* qkv, long ldqkv, const void* x, long ldx,
+                               const void* dout, long ldo, const float* gate_w, const float* gate_b,
+                               const float* gate_const, const float* tbl, float scale, void* scratch,
+                               void* dqkv, long lddq, float* dx_gate, long lddxg, float* gate_part, float drop_p,
+                               const unsigned long long* seed, unsigned long long site, void* stream);
+/* y = x o M / (1 - p) for the dropout call site `site` (mask index row * cols + col, the index of the GEMM-epilogue
+ * dropout of mer_gemm_bf16_tr), regenerated from the step's RNG base: x fp32 or bf16 [rows][ldx], y32 (fp32) and /
+ * or y16 (bf16) outputs (either may be NULL).  cols and the strides multiples of 8 (ldy32 of 4).  Stage-2 uses: the
+ * FFN activation dropout in the forward, and every dropout's backward (the same mask on the gradient).
+ * Replaces: nn.Dropout / F.dropout of WavLMFeedForward and WavLMAttention's output (TF:286-294, 323) in backward. */
+int mer_dropout_rows(int rows, int cols, const void* x, int x_dtype, long ldx, float* y32, long ldy32, void* y16,
+                     long ldy16, float p, const unsigned long long* seed, unsigned long long site, void* stream);
 /* Padded key / query count of mer_wavlm_attention_bwd's scratch (16 * 4 / 8 / 10 / 12 for L <= 64 / 128 / 160 /
  * 192; 0 when L is out of range). */
 int mer_wavlm_attention_bwd_kp(int L);

@@ -267,7 +267,8 @@ __global__ __launch_bounds__(256) void wavlm_attn_bwd_rows_kernel(
     int L, int H, const bf16_t* __restrict__ qkv, long ldqkv, const bf16_t* __restrict__ x, long ldx,
     const float* __restrict__ dout, long ldo, const float* __restrict__ gate_w, const float* __restrict__ gate_b,
     const float* __restrict__ gate_c, const float* __restrict__ tbl, float scale, int nbh, bf16_t* __restrict__ scr,
-    bf16_t* __restrict__ dqkv, long lddq, float* __restrict__ dxg, long lddxg, float* __restrict__ gpart) {
+    bf16_t* __restrict__ dqkv, long lddq, float* __restrict__ dxg, long lddxg, float* __restrict__ gpart,
+    float drop_p, const unsigned long long* __restrict__ seed_ptr, unsigned long long site) {
   typedef RowsLds<NT> Ly;
   constexpr int KP = Ly::KP;
   extern __shared__ __attribute__((aligned(16))) unsigned char ab_smem[];
@@ -393,12 +394,18 @@ __global__ __launch_bounds__(256) void wavlm_attn_bwd_rows_kernel(
   sum += __shfl_xor(sum, 16);
   sum += __shfl_xor(sum, 32);
   const float inv = 1.f / sum;
+  // train mode: attention-probability dropout of the forward (wavlm_attn_kernel, mask index ((b*H+h)*L + i)*L + j):
+  // O = (P o M) V, so dP = (dO V^T) o M and the cols kernel's dV reads P o M; dS keeps the undropped P
+  const unsigned long long dseed = mer_site_seed(seed_ptr, site);
+  const long mrow = (((long)b * H + h) * L + (i < L ? i : L - 1)) * L;
+  auto keep = [&](int j) -> float { return dropout_scale(dseed, (uint64_t)(mrow + j), drop_p); };
   float Dr = 0.f;
 #pragma unroll
   for (int tt = 0; tt < NT; ++tt)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       s[tt][r] *= inv;
+      if (drop_p > 0.f) dp[tt][r] *= keep(16 * tt + 4 * fq + r);
       Dr += s[tt][r] * dp[tt][r];
     }
   Dr += __shfl_xor(Dr, 16);
@@ -421,7 +428,10 @@ __global__ __launch_bounds__(256) void wavlm_attn_bwd_rows_kernel(
       lv[r] = iv ? ds - hi : 0.f;
     }
     if (i < KP) {
-      const u32x2 pv = iv ? u32x2{pack2(s[tt][0], s[tt][1]), pack2(s[tt][2], s[tt][3])} : u32x2{0u, 0u};
+      float pm[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) pm[r] = drop_p > 0.f ? s[tt][r] * keep(16 * tt + 4 * fq + r) : s[tt][r];
+      const u32x2 pv = iv ? u32x2{pack2(pm[0], pm[1]), pack2(pm[2], pm[3])} : u32x2{0u, 0u};
       *reinterpret_cast<u32x2*>(scr + so + 16 * tt) = pv;
       *reinterpret_cast<u32x2*>(scr + plane + so + 16 * tt) = u32x2{pack2(hv[0], hv[1]), pack2(hv[2], hv[3])};
       *reinterpret_cast<u32x2*>(scr + 2 * plane + so + 16 * tt) = u32x2{pack2(lv[0], lv[1]), pack2(lv[2], lv[3])};
@@ -595,7 +605,8 @@ template <int NT>
 int wavlm_attention_bwd_launch(int B, int L, int H, const bf16_t* qkv, long ldqkv, const bf16_t* x, long ldx,
                                const float* dout, long ldo, const float* gate_w, const float* gate_b,
                                const float* gate_c, const float* tbl, float scale, bf16_t* scr, bf16_t* dqkv,
-                               long lddq, float* dxg, long lddxg, float* gpart, hipStream_t st) {
+                               long lddq, float* dxg, long lddxg, float* gpart, float drop_p,
+                               const unsigned long long* seed, unsigned long long site, hipStream_t st) {
   constexpr int rb = RowsLds<NT>::bytes, cb = ColsLds<NT>::bytes;
   static_assert(rb <= 160 * 1024 && cb <= 160 * 1024, "LDS");
   if (hipFuncSetAttribute(reinterpret_cast<const void*>(&wavlm_attn_bwd_rows_kernel<NT>),
@@ -605,7 +616,7 @@ int wavlm_attention_bwd_launch(int B, int L, int H, const bf16_t* qkv, long ldqk
     return (int)hipErrorInvalidConfiguration;
   hipLaunchKernelGGL(wavlm_attn_bwd_rows_kernel<NT>, dim3((L + AB_ROWS - 1) / AB_ROWS * B * H), dim3(256), rb, st, L,
                      H, qkv, ldqkv, x, ldx, dout, ldo, gate_w, gate_b, gate_c, tbl, scale, B * H, scr, dqkv, lddq, dxg,
-                     lddxg, gpart);
+                     lddxg, gpart, drop_p, seed, site);
   hipLaunchKernelGGL(wavlm_attn_bwd_cols_kernel<NT>, dim3(16 * NT / AB_COLS * B * H), dim3(256), cb, st, L, H, qkv,
                      ldqkv, B * H, scr, scale, dqkv, lddq);
   return (int)hipGetLastError();
@@ -668,6 +679,52 @@ MER_API int mer_gelu_bwd(int rows, int cols, const float* df, const void* z, voi
   MER_LAUNCH_CHECK();
 }
 
+namespace {
+// y = x * dropout_scale(seed(site), row * cols + col, p): the mask of one dropout call site (the same index as the
+// GEMM-epilogue dropout of mer_gemm_bf16_tr), regenerated; 8 columns per thread
+template <typename TI>
+__global__ __launch_bounds__(256) void dropout_rows_kernel(int rows, int cols, const TI* __restrict__ x, long ldx,
+                                                           float* __restrict__ y32, long ldy32, bf16_t* __restrict__ y16,
+                                                           long ldy16, float p, const unsigned long long* seed_ptr,
+                                                           unsigned long long site) {
+  const unsigned long long seed = mer_site_seed(seed_ptr, site);
+  const int c8 = cols / 8;
+  const long n = (long)rows * c8;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < n; e += (long)gridDim.x * blockDim.x) {
+    const int r = (int)(e / c8), c0 = (int)(e - (long)r * c8) * 8;
+    float v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = ldf<TI>(x, (long)r * ldx + c0 + k) * dropout_scale(seed, (uint64_t)((long)r * cols + c0 + k), p);
+    if (y32) {
+      float* o = y32 + (long)r * ldy32 + c0;
+      *reinterpret_cast<f32x4*>(o) = f32x4{v[0], v[1], v[2], v[3]};
+      *reinterpret_cast<f32x4*>(o + 4) = f32x4{v[4], v[5], v[6], v[7]};
+    }
+    if (y16) {
+      *reinterpret_cast<u32x4*>(y16 + (long)r * ldy16 + c0) =
+          u32x4{pack2(v[0], v[1]), pack2(v[2], v[3]), pack2(v[4], v[5]), pack2(v[6], v[7])};
+    }
+  }
+}
+}  // namespace
+
+MER_API int mer_dropout_rows(int rows, int cols, const void* x, int x_dtype, long ldx, float* y32, long ldy32,
+                             void* y16, long ldy16, float p, const unsigned long long* seed, unsigned long long site,
+                             void* stream) {
+  if (rows <= 0 || cols <= 0) return 0;
+  if (cols % 8 || ldx % 8 || (y32 && ldy32 % 4) || (y16 && ldy16 % 8) || p < 0.f || p >= 1.f || (p > 0.f && !seed))
+    return (int)hipErrorInvalidValue;
+  const long n = (long)rows * (cols / 8);
+  const unsigned grid = (unsigned)((n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096);
+  if (x_dtype == MER_BF16)
+    hipLaunchKernelGGL(dropout_rows_kernel<bf16_t>, dim3(grid), dim3(256), 0, (hipStream_t)stream, rows, cols,
+                       (const bf16_t*)x, ldx, y32, ldy32, (bf16_t*)y16, ldy16, p, seed, site);
+  else
+    hipLaunchKernelGGL(dropout_rows_kernel<float>, dim3(grid), dim3(256), 0, (hipStream_t)stream, rows, cols,
+                       (const float*)x, ldx, y32, ldy32, (bf16_t*)y16, ldy16, p, seed, site);
+  MER_LAUNCH_CHECK();
+}
+
 MER_API int mer_wavlm_attention_bwd_kp(int L) { return (L <= 0 || L > AB_LMAX) ? 0 : 16 * ab_tiles(L); }
 
 MER_API int mer_wavlm_attention_bwd(int B, int L, int H, const void* qkv, long ldqkv, const void* x, long ldx,
@@ -675,13 +732,24 @@ MER_API int mer_wavlm_attention_bwd(int B, int L, int H, const void* qkv, long l
                                     const float* gate_const, const float* tbl, float scale, void* scratch,
                                     void* dqkv, long lddq, float* dx_gate, long lddxg, float* gate_part,
                                     void* stream) {
+  return mer_wavlm_attention_bwd_tr(B, L, H, qkv, ldqkv, x, ldx, dout, ldo, gate_w, gate_b, gate_const, tbl, scale,
+                                    scratch, dqkv, lddq, dx_gate, lddxg, gate_part, 0.f, nullptr, 0ull, stream);
+}
+
+MER_API int mer_wavlm_attention_bwd_tr(int B, int L, int H, const void* qkv, long ldqkv, const void* x, long ldx,
+                                       const void* dout, long ldo, const float* gate_w, const float* gate_b,
+                                       const float* gate_const, const float* tbl, float scale, void* scratch,
+                                       void* dqkv, long lddq, float* dx_gate, long lddxg, float* gate_part,
+                                       float drop_p, const unsigned long long* seed, unsigned long long site,
+                                       void* stream) {
   if (L <= 0 || L > AB_LMAX || ldqkv % 8 || ldx % 8 || ldo % 4 || lddq % 4 || B <= 0 || H <= 0)
     return (int)hipErrorInvalidValue;
+  if (drop_p < 0.f || drop_p >= 1.f || (drop_p > 0.f && !seed)) return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
 #define MER_AB_LAUNCH(NT)                                                                                             \
   wavlm_attention_bwd_launch<NT>(B, L, H, (const bf16_t*)qkv, ldqkv, (const bf16_t*)x, ldx, (const float*)dout, ldo, \
                                  gate_w, gate_b, gate_const, tbl, scale, (bf16_t*)scratch, (bf16_t*)dqkv, lddq,       \
-                                 dx_gate, lddxg, gate_part, st)
+                                 dx_gate, lddxg, gate_part, drop_p, seed, site, st)
   const int nt = ab_tiles(L);
   const int rc = nt == 4 ? MER_AB_LAUNCH(4) : nt == 8 ? MER_AB_LAUNCH(8) : nt == 10 ? MER_AB_LAUNCH(10) : MER_AB_LAUNCH(12);
 #undef MER_AB_LAUNCH

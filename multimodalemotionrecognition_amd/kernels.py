@@ -757,9 +757,11 @@ def _attn_bwd_kp(L):
     return 16 * (4 if nt <= 4 else 8 if nt <= 8 else 10 if nt <= 10 else 12)
 
 
-def wavlm_attention_bwd(qkv, x, dout, gate_w, gate_b, gate_const, tbl, B, L, H, scale, dqkv, dx_gate=None):
-    """Backward of wavlm_attention (per-head table form).  Returns the gate partial rows
-    [B*H*ceil(L/64)][8*64 + 8 + H] for fold_rows."""
+def wavlm_attention_bwd(qkv, x, dout, gate_w, gate_b, gate_const, tbl, B, L, H, scale, dqkv, dx_gate=None,
+                        drop_p=0.0, rng=None, site=0):
+    """Backward of wavlm_attention (per-head table form; ``drop_p`` / ``rng`` / ``site``: the forward's attention-
+    probability dropout, its mask regenerated).  Returns the gate partial rows [B*H*ceil(L/64)][8*64 + 8 + H] for
+    fold_rows."""
     M = B * L
     if L > 192 or tuple(qkv.shape) != (M, 3 * H * 64) or tuple(dqkv.shape) != (M, 3 * H * 64) or dout.shape[0] != M:
         raise ValueError("wavlm_attention_bwd shapes")
@@ -771,11 +773,26 @@ def wavlm_attention_bwd(qkv, x, dout, gate_w, gate_b, gate_const, tbl, B, L, H, 
     scratch = torch.empty(B * H * kp * (3 * kp + 64), device=qkv.device, dtype=torch.bfloat16)
     nrb = (L + 63) // 64  # AB_ROWS query rows per block (csrc/wavlm_train.hip)
     gpart = _workspace(B * H * nrb * (8 * 64 + 8 + H), qkv.device)
-    LIB("mer_wavlm_attention_bwd", B, L, H, qkv.data_ptr(), qkv.stride(0), x.data_ptr(), x.stride(0), dout.data_ptr(),
-        dout.stride(0), gate_w.data_ptr(), gate_b.data_ptr(), gate_const.data_ptr(), tbl.data_ptr(), float(scale),
-        scratch.data_ptr(), dqkv.data_ptr(), dqkv.stride(0), _ptr0(dx_gate),
-        dx_gate.stride(0) if dx_gate is not None else 0, gpart.data_ptr(), stream_ptr())
+    tr = _train_args(drop_p, rng, site, None, 0)[:3]
+    LIB("mer_wavlm_attention_bwd_tr", B, L, H, qkv.data_ptr(), qkv.stride(0), x.data_ptr(), x.stride(0),
+        dout.data_ptr(), dout.stride(0), gate_w.data_ptr(), gate_b.data_ptr(), gate_const.data_ptr(), tbl.data_ptr(),
+        float(scale), scratch.data_ptr(), dqkv.data_ptr(), dqkv.stride(0), _ptr0(dx_gate),
+        dx_gate.stride(0) if dx_gate is not None else 0, gpart.data_ptr(), *tr, stream_ptr())
     return gpart, B * H * nrb
+
+
+def dropout_rows(x, drop_p, rng, site, y32=None, y16=None):
+    """y = x * mask / (1 - p) for dropout call site ``site`` (mask index row * cols + col, as the GEMM-epilogue
+    dropout), fp32 and / or bf16 outputs (in place allowed when the dtypes match)."""
+    rows, cols = x.shape
+    for y in (y32, y16):
+        if y is not None and tuple(y.shape) != (rows, cols):
+            raise ValueError("dropout_rows output shape")
+    if (y32 is not None and y32.dtype != torch.float32) or (y16 is not None and y16.dtype != torch.bfloat16):
+        raise ValueError("dropout_rows: y32 fp32, y16 bf16")
+    tr = _train_args(drop_p, rng, site, None, 0)[:3]
+    LIB("mer_dropout_rows", rows, cols, x.data_ptr(), _dt(x), x.stride(0), _ptr0(y32),
+        y32.stride(0) if y32 is not None else 0, _ptr0(y16), y16.stride(0) if y16 is not None else 0, *tr, stream_ptr())
 
 
 def transpose_bf16(src, dst):

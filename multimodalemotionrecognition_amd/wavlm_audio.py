@@ -477,25 +477,28 @@ class WavLMBackbone(nn.Module):
             self.__dict__["_pack_limit"] = None
         if draw is not None:  # the trainable layers' executions (the prefix counted its own)
             self.executed_layers += sum(1 for i in range(first, len(self.encoder.layers)) if not (draw[1] >> i) & 1)
-        return x, tbl, (draw[1] if draw is not None else 0)
+        return x, tbl, (draw[1] if draw is not None else 0), (draw[0] if draw is not None else None)
 
     def forward_train(self, wav: torch.Tensor, prefix=None) -> torch.Tensor:
         """Stage-2 forward: frozen conv stack + layers [0, first) on the inference schedule (or ``prefix``, a
         ``forward_prefix`` result computed ahead), then layers [first, 12) saving their activations.  Returns
         fp32 [B, L, 768] tracked by autograd."""
         first = self.first_trainable_layer()
-        x, tbl, mask = prefix if prefix is not None else self.forward_prefix(wav)
+        x, tbl, mask, seed = prefix if prefix is not None else self.forward_prefix(wav)
         names, params = [], []
         for li in range(first, len(self.encoder.layers)):
             for n, q in self.encoder.layers[li].named_parameters():
                 names.append((li, n))
                 params.append(q)
-        return _WavLMTailFn.apply(x, tbl, self, first, mask, tuple(names), *params)
+        return _WavLMTailFn.apply(x, tbl, self, first, (mask, seed), tuple(names), *params)
 
-    def tail_forward(self, x, tbl, first, mask: int = 0):
+    def tail_forward(self, x, tbl, first, mask: int = 0, seed: Optional[int] = None):
         """Layers [first, 12) on bf16 x [B, L, D]; returns (fp32 output [B*L, D], saved activations).  Layers
         whose bit is set in the LayerDrop ``mask`` (train mode, TF:417-419) are skipped: no activations are saved
-        and their parameters get no gradient (torch Adam then leaves them alone, as in the reference)."""
+        and their parameters get no gradient (torch Adam then leaves them alone, as in the reference).  ``seed``
+        (train mode: the forward's RNG base, the prefix's draw) applies the reference's dropouts inside the layers
+        -- attention probabilities, attention output, FFN activation, FFN output (TF:206-228, 286-294, 323), the
+        same call sites and masks as the frozen train-mode forward -- and tail_backward regenerates them."""
         cfg = self.config
         B, L, D = x.shape
         H = cfg.num_attention_heads
@@ -505,6 +508,9 @@ class WavLMBackbone(nn.Module):
         scale = (D // H) ** -0.5
         nl = len(self.encoder.layers)
         h = x.reshape(M, D)
+        rng = torch.full((1,), int(seed), dtype=torch.int64, device=dev) if seed is not None else None
+        hd, ad, acd = ((cfg.hidden_dropout, cfg.attention_dropout, cfg.activation_dropout) if rng is not None
+                       else (0.0, 0.0, 0.0))
         saved = []
         for li in range(first, nl):
             if (mask >> li) & 1:
@@ -513,22 +519,26 @@ class WavLMBackbone(nn.Module):
             layer = self.encoder.layers[li]
             at = layer.attention
             lw = _pack_layer(layer, dev)
-            sv = dict(x=h, pack=lw)
+            s_att, s_out, s_act, s_ffn = _layer_sites(li)
+            sv = dict(x=h, pack=lw, rng=rng, drop=(hd, ad, acd))
             qkv = torch.empty(M, 3 * D, device=dev, dtype=bf)
             K.gemm_bf16(h, lw["qkv_w"], qkv, bias=lw["qkv_b"])
             att = torch.empty(M, D, device=dev, dtype=bf)
             K.wavlm_attention(qkv, h, at.gru_rel_pos_linear.weight, at.gru_rel_pos_linear.bias, lw["gate_c"], tbl, None,
-                              att, B, L, H, scale)
+                              att, B, L, H, scale, drop_p=ad, rng=rng, site=s_att)
             y1 = torch.empty(M, D, device=dev, dtype=torch.float32)
-            K.gemm_bf16(att, lw["out_w"], y1, bias=at.out_proj.bias, residual=h)
+            K.gemm_bf16(att, lw["out_w"], y1, bias=at.out_proj.bias, residual=h, drop_p=hd, rng=rng, site=s_out)
             x1 = torch.empty(M, D, device=dev, dtype=bf)
             K.layernorm(y1, layer.layer_norm.weight, layer.layer_norm.bias, x1, eps=cfg.layer_norm_eps)
             z = torch.empty(M, cfg.intermediate_size, device=dev, dtype=bf)
             K.gemm_bf16(x1, lw["ff1_w"], z, bias=layer.feed_forward.intermediate_dense.bias)
             f = torch.empty_like(z)
             K.gelu_bf16(z, f)
+            if acd > 0:  # the frozen forward's act="gelu" GEMM epilogue dropout: same site, index row * FF + col
+                K.dropout_rows(f, acd, rng, s_act, y16=f)
             y2 = torch.empty(M, D, device=dev, dtype=torch.float32)
-            K.gemm_bf16(f, lw["ff2_w"], y2, bias=layer.feed_forward.output_dense.bias, residual=x1)
+            K.gemm_bf16(f, lw["ff2_w"], y2, bias=layer.feed_forward.output_dense.bias, residual=x1, drop_p=hd, rng=rng,
+                        site=s_ffn)
             last = li == nl - 1
             out = torch.empty(M, D, device=dev, dtype=torch.float32 if last else bf)
             K.layernorm(y2, layer.final_layer_norm.weight, layer.final_layer_norm.bias, out, eps=cfg.layer_norm_eps)
@@ -560,15 +570,24 @@ class WavLMBackbone(nn.Module):
             at, ff = layer.attention, layer.feed_forward
             lw = sv["pack"]
             g = grads
+            rng, (hd, ad, acd) = sv["rng"], sv["drop"]
+            s_att, s_out, s_act, s_ffn = _layer_sites(li)
             # final LayerNorm; its sum-of-dx partials are the FFN output bias gradient (residual: dy2 -> x1 too)
             dy2, dy2h = torch.empty(M, D, device=dev, dtype=f32), torch.empty(M, D, device=dev, dtype=bf)
             part = K.ln_bwd(addends[0], sv["y2"], layer.final_layer_norm.weight, eps, dy_b=addends[1],
                             dy_c=addends[2], dx32=dy2, dx16=dy2h)
             K.ln_bwd_fold(part, M, D, g[layer.final_layer_norm.weight], g[layer.final_layer_norm.bias],
-                          g[ff.output_dense.bias])
-            K.linear_wgrad(sv["f"], dy2h, g[ff.output_dense.weight])
+                          g[ff.output_dense.bias] if hd == 0 else None)
+            gf = dy2h  # gradient of the FFN output branch: the residual keeps dy2, the branch sees its dropout mask
+            if hd > 0:
+                gf32, gf = torch.empty(M, D, device=dev, dtype=f32), torch.empty(M, D, device=dev, dtype=bf)
+                K.dropout_rows(dy2, hd, rng, s_ffn, y32=gf32, y16=gf)
+                K.colsum_into(gf32, g[ff.output_dense.bias])
+            K.linear_wgrad(sv["f"], gf, g[ff.output_dense.weight])
             df = torch.empty(M, FF, device=dev, dtype=f32)
-            K.gemm_bf16(dy2h, _transposed(lw, "ff2_w", dev), df)
+            K.gemm_bf16(gf, _transposed(lw, "ff2_w", dev), df)
+            if acd > 0:
+                K.dropout_rows(df, acd, rng, s_act, y32=df)
             dz = torch.empty(M, FF, device=dev, dtype=bf)
             K.gelu_bwd(df, sv["z"], dz, g[ff.intermediate_dense.bias])
             K.linear_wgrad(sv["x1"], dz, g[ff.intermediate_dense.weight])
@@ -577,22 +596,28 @@ class WavLMBackbone(nn.Module):
             # attention LayerNorm (input y1 = x + out_proj(att)); residual gradient dy2 joins here
             dy1, dy1h = torch.empty(M, D, device=dev, dtype=f32), torch.empty(M, D, device=dev, dtype=bf)
             part = K.ln_bwd(dx1, sv["y1"], layer.layer_norm.weight, eps, dy_b=dy2, dx32=dy1, dx16=dy1h)
-            K.ln_bwd_fold(part, M, D, g[layer.layer_norm.weight], g[layer.layer_norm.bias], g[at.out_proj.bias])
-            K.linear_wgrad(sv["att"], dy1h, g[at.out_proj.weight])
+            K.ln_bwd_fold(part, M, D, g[layer.layer_norm.weight], g[layer.layer_norm.bias],
+                          g[at.out_proj.bias] if hd == 0 else None)
+            go, goh = dy1, dy1h  # gradient of the attention-output branch (dropout mask in train mode)
+            if hd > 0:
+                go, goh = torch.empty(M, D, device=dev, dtype=f32), torch.empty(M, D, device=dev, dtype=bf)
+                K.dropout_rows(dy1, hd, rng, s_out, y32=go, y16=goh)
+                K.colsum_into(go, g[at.out_proj.bias])
+            K.linear_wgrad(sv["att"], goh, g[at.out_proj.weight])
             # gradient of the attention output in fp32 from fp32 operands (exact-f32 MFMA GEMM): the softmax
             # backward's dp_ij - sum_j p_ij dp_ij cancels for peaked rows, so bf16 operands here would cost
             # the score-path gradients (q/k/gate) ~10% (tests/test_wavlm_stage2_gpu.py)
             datt = torch.empty(M, D, device=dev, dtype=f32)
             if _DATT_F32:
-                K.gemm(dy1, at.out_proj.weight.detach(), datt)
+                K.gemm(go, at.out_proj.weight.detach(), datt)
             else:
-                K.gemm_bf16(dy1h, _transposed(lw, "out_w", dev), datt)
+                K.gemm_bf16(goh, _transposed(lw, "out_w", dev), datt)
             need_dx = k > 0
             dqkv = torch.empty(M, 3 * D, device=dev, dtype=bf)
             dxg = torch.empty(M, D, device=dev, dtype=f32) if need_dx else None
             gpart, nparts = K.wavlm_attention_bwd(sv["qkv"], sv["x"], datt, at.gru_rel_pos_linear.weight,
                                                   at.gru_rel_pos_linear.bias, lw["gate_c"], tbl, B, L, H, scale,
-                                                  dqkv, dxg)
+                                                  dqkv, dxg, drop_p=ad, rng=rng, site=s_att)
             ldp = 8 * 64 + 8 + H
             K.fold_rows(gpart, nparts, 8 * 64, ldp, g[at.gru_rel_pos_linear.weight], offset=0)
             K.fold_rows(gpart, nparts, 8, ldp, g[at.gru_rel_pos_linear.bias], offset=8 * 64)
@@ -640,8 +665,8 @@ class _WavLMTailFn(torch.autograd.Function):
     tail_backward writing each parameter gradient straight into its ``grad_buffer`` slot."""
 
     @staticmethod
-    def forward(ctx, x, tbl, enc, first, mask, names, *params):
-        out, saved = enc.tail_forward(x, tbl, first, mask)
+    def forward(ctx, x, tbl, enc, first, draw, names, *params):
+        out, saved = enc.tail_forward(x, tbl, first, draw[0], draw[1])
         B, L, D = x.shape
         ctx.enc, ctx.first, ctx.saved, ctx.tbl, ctx.shape = enc, first, saved, tbl, (B, L)
         ctx.params, ctx.names = params, names

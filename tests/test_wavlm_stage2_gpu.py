@@ -39,8 +39,20 @@ def _rt(t):
     return t + (t.to(torch.bfloat16).float() - t).detach()
 
 
-def _layer_matched(p, x, pb, li, last):
-    """wavlm_ref.encoder_layer / attention (TF:147-186, 314-336) with the HIP path's bf16 storage points."""
+def _mask(base, site, p, shape, idx=None):
+    """The kernels' dropout multiplier (0 or 1/(1-p), float32) for call site ``site``, element index = flat
+    position (row * cols + col) unless ``idx`` is given."""
+    from tests.helpers import dropout_keep
+
+    n = int(np.prod(shape))
+    keep = dropout_keep(base, site, np.arange(n, dtype=np.uint64) if idx is None else idx, p)
+    return torch.from_numpy(keep.reshape(shape).astype(np.float32) * np.float32(1.0 / (1.0 - np.float32(p))))
+
+
+def _layer_matched(p, x, pb, li, last, drop=None):
+    """wavlm_ref.encoder_layer / attention (TF:147-186, 314-336) with the HIP path's bf16 storage points.
+    ``drop`` = (rng base, attention p, hidden p, activation p): train mode, the kernels' masks at the four call
+    sites of layer li (wavlm_audio._layer_sites)."""
     import math
     import torch.nn.functional as F
 
@@ -58,12 +70,23 @@ def _layer_matched(p, x, pb, li, last):
     k = _rt(lin(x, a + "k_proj")).view(B, L, H, dh).transpose(1, 2)
     v = _rt(lin(x, a + "v_proj")).view(B, L, H, dh).transpose(1, 2)
     sc = (q * (1.0 / math.sqrt(dh))) @ k.transpose(-1, -2) + gate * pb[None]
-    o = _rt((torch.softmax(sc, dim=-1) @ v).transpose(1, 2).reshape(B, L, D))
-    y1 = x + lin(o, a + "out_proj")
+    prob = torch.softmax(sc, dim=-1)
+    m_out = m_act = m_ffn = 1.0
+    if drop is not None:
+        from multimodalemotionrecognition_amd.wavlm_audio import _layer_sites
+
+        base, pa, ph, pc = drop
+        s_att, s_out, s_act, s_ffn = _layer_sites(li)
+        prob = prob * _mask(base, s_att, pa, (B, H, L, L))  # index ((b*H + h)*L + i)*L + j
+        m_out = _mask(base, s_out, ph, (B, L, D))
+        m_act = _mask(base, s_act, pc, (B, L, 4 * D))
+        m_ffn = _mask(base, s_ffn, ph, (B, L, D))
+    o = _rt((prob @ v).transpose(1, 2).reshape(B, L, D))
+    y1 = x + lin(o, a + "out_proj") * m_out
     x1 = _rt(F.layer_norm(y1, (D,), p[n + "layer_norm.weight"], p[n + "layer_norm.bias"], 1e-5))
     z = _rt(lin(x1, n + "feed_forward.intermediate_dense"))
-    f = _rt(F.gelu(z))
-    y2 = x1 + lin(f, n + "feed_forward.output_dense")
+    f = _rt(_rt(F.gelu(z)) * m_act)
+    y2 = x1 + lin(f, n + "feed_forward.output_dense") * m_ffn
     out = F.layer_norm(y2, (D,), p[n + "final_layer_norm.weight"], p[n + "final_layer_norm.bias"], 1e-5)
     return out if last else _rt(out)
 
@@ -153,10 +176,14 @@ def _compare(named, out, ref_out, ref_grads, matched, floor):
     return bad
 
 
-def test_wavlm_tail_per_layer_teacher_forced():
+@pytest.mark.parametrize("train", [False, True])
+def test_wavlm_tail_per_layer_teacher_forced(train):
     """Each of 4 trainable layers on its own: the matched-precision oracle layer gets the HIP forward's exact bf16
     layer input AND the exact upstream gradient the HIP backward delivered to that layer's output, so nothing but
-    the layer's own backward differs -- every parameter gradient within 2e-2 rel-RMS (score path 5e-2)."""
+    the layer's own backward differs -- every parameter gradient within 2e-2 rel-RMS (score path 5e-2).
+    ``train``: the reference's dropouts inside the trainable layers (attention probabilities 0.1, attention output
+    0.1, FFN activation 0.1, FFN output 0.1; TF:206-228, 286-294, 323) with the kernels' masks restated on the host
+    (tests/helpers.py dropout_keep) in the oracle, so the same bars hold."""
     m = build_backbone()
     _unfreeze(m, 4)
     first = m.first_trainable_layer()
@@ -164,9 +191,10 @@ def test_wavlm_tail_per_layer_teacher_forced():
     wav = torch.from_numpy(audio).squeeze(1).cuda()
     cap = {}
     m.__dict__["_capture_upstream"] = cap
-    x_in, tbl, mask = m.forward_prefix(wav)
-    assert mask == 0  # eval semantics in this test (train_semantics off): no layer dropped
-    out, saved = m.tail_forward(x_in, tbl, first)
+    x_in, tbl, mask, _ = m.forward_prefix(wav)
+    assert mask == 0  # eval semantics for the prefix in this test (train_semantics off): no layer dropped
+    base = 0x5EED1234 if train else None
+    out, saved = m.tail_forward(x_in, tbl, first, 0, base)
     G = torch.from_numpy(np.random.default_rng(9).standard_normal((2 * 149, 768)).astype(np.float32)).cuda()
     grads = {q: torch.zeros_like(q) for li in range(first, 12) for q in m.encoder.layers[li].parameters()}
     m.tail_backward(G, saved, tbl, first, 2, 149, grads)
@@ -174,12 +202,18 @@ def test_wavlm_tail_per_layer_teacher_forced():
     m.__dict__.pop("_capture_upstream")
     p = {k: v.detach().float().cpu().clone() for k, v in m.state_dict().items()}
     pb = wavlm_ref.position_bias(p, 149)
+    cfg = m.config
+    drop = (base, cfg.attention_dropout, cfg.hidden_dropout, cfg.activation_dropout) if train else None
     bad, worst = [], {}
     for k, li in enumerate(range(first, 12)):
         x = saved[k]["x"].float().cpu().view(2, 149, 768)
         up = sum(a.float().cpu() for a in cap[li] if a is not None).view(2, 149, 768)
         lp = {n: t.requires_grad_(True) for n, t in p.items() if n.startswith(f"encoder.layers.{li}.")}
-        y = _layer_matched(p, x, pb, li, li == 11)
+        y = _layer_matched(p, x, pb, li, li == 11, drop)
+        if li < 11:  # the forward itself, teacher-forced: the next layer's saved input is this layer's output
+            e = rel_rms(saved[k + 1]["x"].float().view(2, 149, 768), y.detach().numpy())
+            print(f"  layer {li} output rel-rms {e:.2e}")
+            assert e < 1e-2, (li, e)
         (y * up).sum().backward()
         for n, t in lp.items():
             if n.endswith("k_proj.bias"):  # exactly zero in exact arithmetic (softmax shift invariance)
@@ -245,10 +279,12 @@ def test_fusion_stage2_train_step_updates_wavlm_tail():
     print("stage-2 losses", losses)
 
 
-def test_attention_backward_kernel_vs_fp64():
+@pytest.mark.parametrize("drop_p", [0.0, 0.1])
+def test_attention_backward_kernel_vs_fp64(drop_p):
     """mer_wavlm_attention_bwd alone: identical bf16 q/k/v, layer input x (gate source) and fp32 output
     gradient on both sides; reference = fp64 autograd of TF:163-186 (gated relative position bias attention).
-    Bars: dq/dk/dv (bf16 outputs) 1e-2 rel-RMS; gate-path gradients (fp32 outputs) 1e-4."""
+    Bars: dq/dk/dv (bf16 outputs) 1e-2 rel-RMS; gate-path gradients (fp32 outputs) 1e-4.  drop_p > 0: the
+    train-mode attention-probability dropout (mask regenerated by the kernel, restated on the host here)."""
     import math
 
     from multimodalemotionrecognition_amd import kernels as K
@@ -267,8 +303,10 @@ def test_attention_backward_kernel_vs_fp64():
     scale = dh ** -0.5
     dqkv = torch.empty(B * L, 3 * D, dtype=torch.bfloat16, device="cuda")
     dxg = torch.empty(B * L, D, dtype=torch.float32, device="cuda")
+    base, site = 987654321, 1100 + 8 * 10
+    rngt = torch.full((1,), base, dtype=torch.int64, device="cuda")
     gpart, nparts = K.wavlm_attention_bwd(qkv.cuda(), x.cuda(), dout.cuda(), gw.cuda(), gb.cuda(), gc.cuda(), tbl.cuda(),
-                                          B, L, H, scale, dqkv, dxg)
+                                          B, L, H, scale, dqkv, dxg, drop_p=drop_p, rng=rngt, site=site)
     dgw, dgb, dgc = (torch.zeros(n, device="cuda") for n in (8 * dh, 8, H))
     ldp = 8 * dh + 8 + H
     K.fold_rows(gpart, nparts, 8 * dh, ldp, dgw, offset=0)
@@ -288,7 +326,10 @@ def test_attention_backward_kernel_vs_fp64():
     idx = torch.arange(L)[None, :] - torch.arange(L)[:, None] + L - 1
     pb = tbl.double()[:, idx]  # [H, L, L]
     sc = (q64 * scale) @ k64.transpose(-1, -2) + gate * pb[None]
-    o = (torch.softmax(sc, -1) @ v64).transpose(1, 2).reshape(B * L, D)
+    prob = torch.softmax(sc, -1)
+    if drop_p > 0:
+        prob = prob * _mask(base, site, drop_p, (B, H, L, L)).double()
+    o = (prob @ v64).transpose(1, 2).reshape(B * L, D)
     (o * dout.double()).sum().backward()
     ref = {"dq": q64.grad.transpose(1, 2).reshape(B * L, D), "dk": k64.grad.transpose(1, 2).reshape(B * L, D),
            "dv": v64.grad.transpose(1, 2).reshape(B * L, D)}
