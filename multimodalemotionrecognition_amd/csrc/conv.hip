@@ -393,15 +393,16 @@ __device__ __attribute__((aligned(16))) uint32_t mer_conv_zero16[4] = {0u, 0u, 0
 
 __device__ __forceinline__ int wswz(int row, int nchunks) { return ((row & 7) << 1) & (nchunks - 1); }
 
-template <int BM_, int BN_, int WM, int WN, int STAGES>
+template <int BM_, int BN_, int WM, int WN, int STAGES, int KS = 64>
 __global__ __launch_bounds__(64 * WM * WN, 2) void wgrad_pipe_kernel(WgradGeom g) {
   constexpr int WAVES = WM * WN;
   constexpr int ACW = BM_ / 8, BCW = BN_ / 8;           // 16-byte chunks per LDS row
   constexpr int ARI = 64 / ACW, BRI = 64 / BCW;         // rows per glds instruction
-  constexpr int IA = 64 / ARI / WAVES, IB = 64 / BRI / WAVES;  // glds per wave per K-step
-  static_assert(IA * ARI * WAVES == 64 && IB * BRI * WAVES == 64, "64-pixel K-step must split into glds rows");
+  constexpr int IA = KS / ARI / WAVES, IB = KS / BRI / WAVES;  // glds per wave per K-step of KS pixels
+  static_assert(IA * ARI * WAVES == KS && IB * BRI * WAVES == KS, "the K-step must split into whole glds rows");
+  static_assert(KS % 32 == 0, "MFMA k = 32 pixels");
   constexpr int IT = BM_ / WM / 16, JT = BN_ / WN / 16;
-  constexpr int BUF = 64 * (BM_ + BN_);                 // bf16 elements per ring slot
+  constexpr int BUF = KS * (BM_ + BN_);                 // bf16 elements per ring slot
   extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int Ntot = g.R * g.S * g.C;
@@ -442,7 +443,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void wgrad_pipe_kernel(WgradGeom g
   const int HoWo = g.Ho * g.Wo;
   auto stage = [&](int slot, int p0) {
     bf16_t* la = smem + slot * BUF;
-    bf16_t* lb = la + 64 * BM_;
+    bf16_t* lb = la + KS * BM_;
 #pragma unroll
     for (int j = 0; j < IA; ++j) {
       const int p = p0 + arow[j];
@@ -482,20 +483,20 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void wgrad_pipe_kernel(WgradGeom g
   for (int i = 0; i < IT; ++i)
 #pragma unroll
     for (int j = 0; j < JT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int nk = (p_end - p_beg + 63) / 64;
+  const int nk = (p_end - p_beg + KS - 1) / KS;
   constexpr int G = IA + IB;
 #pragma unroll
   for (int s = 0; s < STAGES - 1; ++s)
-    if (s < nk) stage(s, p_beg + s * 64);
+    if (s < nk) stage(s, p_beg + s * KS);
   for (int kt = 0; kt < nk; ++kt) {
     const int ahead = (nk - 1 - kt) < (STAGES - 2) ? (nk - 1 - kt) : (STAGES - 2);
     wait_tiles_in_flight<G>(ahead);
     lds_barrier();
-    if (kt + STAGES - 1 < nk) stage((kt + STAGES - 1) % STAGES, p_beg + (kt + STAGES - 1) * 64);
+    if (kt + STAGES - 1 < nk) stage((kt + STAGES - 1) % STAGES, p_beg + (kt + STAGES - 1) * KS);
     const bf16_t* Aimg = smem + (kt % STAGES) * BUF;
-    const bf16_t* Bimg = Aimg + 64 * BM_;
+    const bf16_t* Bimg = Aimg + KS * BM_;
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
+    for (int s = 0; s < KS / 32; ++s) {
       bf16x8 af[IT], bfr[JT];
 #pragma unroll
       for (int i = 0; i < IT; ++i) af[i] = tr_frag(Aimg, ACW, s * 32, wm + i * 16);
@@ -524,13 +525,13 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void wgrad_pipe_kernel(WgradGeom g
     }
 }
 
-template <int BM_, int BN_, int WM, int WN, int STAGES>
+template <int BM_, int BN_, int WM, int WN, int STAGES, int KS = 64>
 void launch_wgrad_pipe(const WgradGeom& g, dim3 grid, hipStream_t st) {
-  const size_t lds = (size_t)STAGES * 64 * (BM_ + BN_) * sizeof(bf16_t);
-  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_pipe_kernel<BM_, BN_, WM, WN, STAGES>),
+  const size_t lds = (size_t)STAGES * KS * (BM_ + BN_) * sizeof(bf16_t);
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_pipe_kernel<BM_, BN_, WM, WN, STAGES, KS>),
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return;
-  hipLaunchKernelGGL((wgrad_pipe_kernel<BM_, BN_, WM, WN, STAGES>), grid, dim3(64 * WM * WN), lds, st, g);
+  hipLaunchKernelGGL((wgrad_pipe_kernel<BM_, BN_, WM, WN, STAGES, KS>), grid, dim3(64 * WM * WN), lds, st, g);
 }
 
 // slab0[i] = sum_z ws[z][i] over the flat [K][R*S*C] index.  A block owns E = 256/SG consecutive elements
@@ -1291,7 +1292,7 @@ MER_API int mer_conv_wgrad(int N, int H, int W, int C, int Creal, int K, int R, 
 static int conv_wgrad_impl(int N, int H, int W, int C, int Creal, int K, int R, int S, int stride, int pad,
                            const void* x, const void* dy, long ldy, float* dw, int splits, float* workspace,
                            int variant, void* stream) {
-  if (C % 8 || K % 8 || variant < -1 || variant > 5 || R * S > 49) return (int)hipErrorInvalidValue;
+  if (C % 8 || K % 8 || variant < -1 || variant > 7 || R * S > 49) return (int)hipErrorInvalidValue;
   if (variant == -1) variant = wgrad_default_variant(K);
   WgradGeom g{};
   g.N = N; g.H = H; g.W = W; g.C = C; g.Creal = Creal;
@@ -1311,7 +1312,7 @@ static int conv_wgrad_impl(int N, int H, int W, int C, int Creal, int K, int R, 
       hipLaunchKernelGGL((wgrad_kernel<64, 128>), grid, dim3(256), 0, st, g);
     else if (variant == 4)
       launch_wgrad_pipe<64, 128, 2, 4, 2>(g, grid, st);
-    else if (variant == 5)
+    else if (variant == 5 || variant == 6)
       launch_wgrad_pipe<64, 128, 2, 4, 3>(g, grid, st);
     else if (variant == 3)
       hipLaunchKernelGGL((wgrad_kernel<64, 128, 2, 4, 2>), grid, dim3(512), 0, st, g);
@@ -1325,6 +1326,10 @@ static int conv_wgrad_impl(int N, int H, int W, int C, int Creal, int K, int R, 
       launch_wgrad_pipe<128, 128, 2, 4, 2>(g, grid, st);
     else if (variant == 5)
       launch_wgrad_pipe<128, 128, 2, 4, 3>(g, grid, st);
+    else if (variant == 6)
+      launch_wgrad_pipe<128, 128, 2, 4, 4, 32>(g, grid, st);
+    else if (variant == 7)
+      launch_wgrad_pipe<128, 128, 2, 4, 3, 32>(g, grid, st);
     else if (variant == 3)
       hipLaunchKernelGGL((wgrad_kernel<128, 128, 2, 4, 2>), grid, dim3(512), 0, st, g);
     else

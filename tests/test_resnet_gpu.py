@@ -298,14 +298,14 @@ def test_wgrad_variants_bit_identical(N, H, C, Kc, R, stride, pad):
     dy = torch.randn(N, Ho, Ho, Kc, device="cuda").bfloat16()
     creal = 3 if C == 8 else C
     out = []
-    for v in (1, 2, 3, 4, 5):
+    for v in (1, 2, 3, 4, 5, 6, 7):
         dw = torch.zeros(Kc, creal, R, R, device="cuda")
         K.conv_wgrad(x, dy, dw, R, R, stride, pad, creal=creal, variant=v)
         out.append(dw)
     ref = (x.float().permute(0, 3, 1, 2)[:, :creal], dy.float().permute(0, 3, 1, 2))
     dw_ref = torch.nn.grad.conv2d_weight(ref[0], (Kc, creal, R, R), ref[1], stride=stride, padding=pad)
     assert (out[0] - dw_ref).abs().max() <= 5e-3 * dw_ref.abs().max() + 1e-3
-    for v, o in zip((2, 3, 4, 5), out[1:]):
+    for v, o in zip((2, 3, 4, 5, 6, 7), out[1:]):
         assert torch.equal(out[0], o), f"variant {v} differs"
 
 
