@@ -261,7 +261,8 @@ constexpr int ADH = 64, APAD = ADH + 8;
 typedef __attribute__((ext_vector_type(4))) short s16x4;
 }
 
-__global__ __launch_bounds__(256, 3) void wavlm_attn_kernel(int L, int H, const bf16_t* __restrict__ qkv, long ldqkv,
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void wavlm_attn_kernel(int L, int H, const bf16_t* __restrict__ qkv, long ldqkv,
                                                          const bf16_t* __restrict__ x, long ldx,
                                                          const float* __restrict__ gw, const float* __restrict__ gb,
                                                          const float* __restrict__ gconst,
@@ -277,17 +278,19 @@ __global__ __launch_bounds__(256, 3) void wavlm_attn_kernel(int L, int H, const 
   const int VTP = LP + 8;
   bf16_t* Ks = reinterpret_cast<bf16_t*>(smem_raw);   // [LP][APAD]
   bf16_t* Vt = Ks + LP * APAD;                        // [ADH][VTP]
-  float* gate = reinterpret_cast<float*>(Vt + ADH * VTP);  // [4][16]
-  float* gws = gate + 64;                              // [8][64] gru_rel_pos_linear weight
+  float* gate = reinterpret_cast<float*>(Vt + ADH * VTP);  // [NW][16]
+  float* gws = gate + 16 * NW;                         // [8][64] gru_rel_pos_linear weight
   float* tbl = gws + 512;                              // [2L-1]
   // one-dimensional grid, XCD-aware: the row blocks of one (b, h) run on one XCD and share its K / V in L2
-  const int nrb = (LP / 16 + 3) / 4;
+  constexpr int NTH = 64 * NW;
+  constexpr int KIT = (256 * 8 + NTH - 1) / NTH, VIT = (512 + NTH - 1) / NTH, TIT = (512 + NTH - 1) / NTH;
+  const int nrb = (LP / 16 + NW - 1) / NW;
   int rbk, bh;
   xcd_tile(blockIdx.x, nrb, gridDim.x, rbk, bh);  // gridDim.x = nrb * B * H
   const int b = bh / H, h = bh % H;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int D = H * ADH;
-  const int rb = rbk * 4 + w;       // this wave's 16-row query tile
+  const int rb = rbk * NW + w;      // this wave's 16-row query tile
   const bool active = rb * 16 < L;  // wave-uniform
 
   // Loads are unconditional from clamped (valid) rows, zeroed by a select at the LDS store: a load under a
@@ -312,24 +315,24 @@ __global__ __launch_bounds__(256, 3) void wavlm_attn_kernel(int L, int H, const 
     const int i = min(rb * 16 + it * 8 + sub, L - 1);
     xg[it] = *reinterpret_cast<const u32x4*>(x + ((long)b * L + i) * ldx + h * ADH + cl * 8);
   }
-  float tb[2], gwv[2];
+  float tb[TIT], gwv[TIT];
 #pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const int r = min(t + 256 * k, 2 * L - 2);
+  for (int k = 0; k < TIT; ++k) {
+    const int r = min(t + NTH * k, 2 * L - 2);
     tb[k] = bucket ? rel_emb[(long)bucket[r] * H + h] : rel_emb[(long)h * (2 * L - 1) + r];
-    gwv[k] = gw[t + 256 * k];  // 512 = 8 x 64 weights
+    gwv[k] = gw[min(t + NTH * k, 511)];  // 512 = 8 x 64 weights
   }
   {
-    u32x4 kr[8];
+    u32x4 kr[KIT];
 #pragma unroll
-    for (int it = 0; it < 8; ++it) {
-      const int c = t + it * 256, row = min(c >> 3, L - 1), ch = c & 7;
+    for (int it = 0; it < KIT; ++it) {
+      const int c = t + it * NTH, row = min(c >> 3, L - 1), ch = c & 7;
       kr[it] = *reinterpret_cast<const u32x4*>(qkv + ((long)b * L + row) * ldqkv + D + h * ADH + ch * 8);
     }
-    u32x4 vr[2][4];
+    u32x4 vr[VIT][4];
 #pragma unroll
-    for (int it = 0; it < 2; ++it) {
-      const int q = t + it * 256, rq = q >> 3, ch = q & 7;
+    for (int it = 0; it < VIT; ++it) {
+      const int q = t + it * NTH, rq = q >> 3, ch = q & 7;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int row = min(rq * 4 + e, L - 1);
@@ -337,19 +340,19 @@ __global__ __launch_bounds__(256, 3) void wavlm_attn_kernel(int L, int H, const 
       }
     }
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int r = t + 256 * k;
+    for (int k = 0; k < TIT; ++k) {
+      const int r = t + NTH * k;
       if (r < 2 * L - 1) tbl[r] = tb[k];
-      gws[r] = gwv[k];
+      if (r < 512) gws[r] = gwv[k];
     }
 #pragma unroll
-    for (int it = 0; it < 8; ++it) {
-      const int c = t + it * 256, row = c >> 3, ch = c & 7;
+    for (int it = 0; it < KIT; ++it) {
+      const int c = t + it * NTH, row = c >> 3, ch = c & 7;
       if (c < LP * 8) *reinterpret_cast<u32x4*>(&Ks[row * APAD + ch * 8]) = row < L ? kr[it] : u32x4{0u, 0u, 0u, 0u};
     }
 #pragma unroll
-    for (int it = 0; it < 2; ++it) {
-      const int q = t + it * 256, rq = q >> 3, ch = q & 7;
+    for (int it = 0; it < VIT; ++it) {
+      const int q = t + it * NTH, rq = q >> 3, ch = q & 7;
       if (q < LP * 2) {
 #pragma unroll
         for (int e = 0; e < 4; ++e)
@@ -506,10 +509,24 @@ MER_API int mer_wavlm_attention_tr(int B, int L, int H, const void* qkv, long ld
   if ((ldqkv % 8) || (ldx % 8) || (ldo % 4) || ((((uintptr_t)qkv) | ((uintptr_t)x)) & 15) || (((uintptr_t)out) & 7))
     return (int)hipErrorInvalidValue;
   const int LP = (L + 15) / 16 * 16;
-  const size_t lds = sizeof(bf16_t) * ((size_t)LP * APAD + (size_t)ADH * (LP + 8)) + sizeof(float) * (64 + 512 + 2 * L);
-  hipLaunchKernelGGL(wavlm_attn_kernel, dim3(B * H * ((LP / 16 + 3) / 4)), dim3(256), lds, (hipStream_t)stream, L, H,
-                     (const bf16_t*)qkv, ldqkv, (const bf16_t*)x, ldx, gate_w, gate_b, gate_const, rel_emb, bucket,
-                     (bf16_t*)out, ldo, scale, drop_p, seed, site, skip_mask, skip_bit);
+  static const int nw_env = [] {  // MER_ATTN_NW: waves (16-row query tiles) per block, A/B switch
+    const char* e = getenv("MER_ATTN_NW");
+    return e ? atoi(e) : 0;
+  }();
+  const int NWsel = nw_env == 5 || nw_env == 10 || nw_env == 4 ? nw_env : 4;
+#define MER_ATTN_LAUNCH(NW)                                                                                       \
+  do {                                                                                                           \
+    const size_t lds = sizeof(bf16_t) * ((size_t)LP * APAD + (size_t)ADH * (LP + 8)) +                           \
+                       sizeof(float) * (16 * NW + 512 + 2 * L);                                                   \
+    hipLaunchKernelGGL(wavlm_attn_kernel<NW>, dim3(B * H * ((LP / 16 + NW - 1) / NW)), dim3(64 * NW), lds,         \
+                       (hipStream_t)stream, L, H, (const bf16_t*)qkv, ldqkv, (const bf16_t*)x, ldx, gate_w, gate_b, \
+                       gate_const, rel_emb, bucket, (bf16_t*)out, ldo, scale, drop_p, seed, site, skip_mask,      \
+                       skip_bit);                                                                                 \
+  } while (0)
+  if (NWsel == 10) MER_ATTN_LAUNCH(10);
+  else if (NWsel == 5) MER_ATTN_LAUNCH(5);
+  else MER_ATTN_LAUNCH(4);
+#undef MER_ATTN_LAUNCH
   MER_LAUNCH_CHECK();
 }
 
