@@ -628,6 +628,13 @@ __global__ __launch_bounds__(256) void wgrad_scatter_kernel(int C, int Creal, in
 // ---------------------------------------------------------------------------------------
 
 __device__ __forceinline__ int cswz(int row, int c) { return c ^ ((row >> 1) & 7); }
+// K-step of CW 16-byte chunks per LDS row: 8 (64-wide, 128-byte rows) or 4 (32-wide, 64-byte rows; four rows share
+// a 256-byte bank row, so the XOR takes row bits 2-3 -- the 16 rows one ds_read_b128 lane group reads then cover
+// all 16 bank slots)
+template <int CW>
+__device__ __forceinline__ int cswz_k(int row, int c) {
+  return CW == 8 ? (c ^ ((row >> 1) & 7)) : (c ^ ((row >> 2) & 3));
+}
 
 template <bool DGRAD>
 __device__ __forceinline__ const bf16_t* conv_a_src(const ConvGeom& g, int n, int oh, int ow, bool rowok, int kk,
@@ -683,13 +690,15 @@ __device__ __forceinline__ ParClass par_class(const ConvGeom& g, int cls) {
 // STAGES-deep LDS ring (cdna_hip_programming.md "Pipelining across barriers"): tiles kt+1 .. kt+STAGES-2 stay
 // in flight across the barrier that publishes tile kt (counted vmcnt, raw s_barrier); the barrier also retires
 // every wave's reads of tile kt-1, whose buffer the DMA of tile kt+STAGES-1 then reuses.
-template <bool DGRAD, bool PAR, int BM_, int BN_, int WM = 2, int WN = 2, int STAGES = 2>
+template <bool DGRAD, bool PAR, int BM_, int BN_, int WM = 2, int WN = 2, int STAGES = 2, int KS = 64>
 __global__ __launch_bounds__(64 * WM * WN, 2) void conv_pipe_kernel(ConvGeom g) {
   constexpr int WAVES = WM * WN;
-  constexpr int IA = BM_ / 8 / WAVES, IB = BN_ / 8 / WAVES;  // glds per wave per K-tile (8 rows each)
-  static_assert(IA * 8 * WAVES == BM_ && IB * 8 * WAVES == BN_, "tile rows must split into 8-row glds pieces");
+  constexpr int CW = KS / 8, RPG = 64 / CW;  // 16-byte chunks per LDS row, rows per glds instruction
+  constexpr int IA = BM_ / RPG / WAVES, IB = BN_ / RPG / WAVES;  // glds per wave per K-tile
+  static_assert(IA * RPG * WAVES == BM_ && IB * RPG * WAVES == BN_, "tile rows must split into whole glds pieces");
+  static_assert(KS == 64 || KS == 32, "K-tile");
   constexpr int TM = BM_ / WM, TN = BN_ / WN, FM = TM / 16, FN = TN / 16;
-  constexpr int BUF = (BM_ + BN_) * 64;
+  constexpr int BUF = (BM_ + BN_) * KS;
   extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   ParClass pc{};
@@ -717,7 +726,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_pipe_kernel(ConvGeom g) 
   bool aok[IA];
 #pragma unroll
   for (int j = 0; j < IA; ++j) {
-    const int r = (w * IA + j) * 8 + (lane >> 3);
+    const int r = (w * IA + j) * RPG + lane / CW;
     const int m = m0 + r;
     aok[j] = m < M;
     const int mm = aok[j] ? m : 0;
@@ -725,18 +734,18 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_pipe_kernel(ConvGeom g) 
     const int rem = mm - an[j] * rowsH * rowsW;
     aoh[j] = rem / rowsW;
     aow[j] = rem - aoh[j] * rowsW;
-    acl[j] = cswz(r, lane & 7) * 8;
+    acl[j] = cswz_k<CW>(r, lane % CW) * 8;
   }
   const bf16_t* pb[IB];
   int bcl[IB];
   bool bok[IB];
 #pragma unroll
   for (int j = 0; j < IB; ++j) {
-    const int r = (w * IB + j) * 8 + (lane >> 3);
+    const int r = (w * IB + j) * RPG + lane / CW;
     const int n = n0 + r;
     bok[j] = n < g.Ncols;
     pb[j] = g.Wt + (long)(bok[j] ? n : 0) * g.Kred;
-    bcl[j] = cswz(r, lane & 7) * 8;
+    bcl[j] = cswz_k<CW>(r, lane % CW) * 8;
   }
   const float inv_IC = 1.f / g.IC, inv_S = 1.f / g.S, inv_ns = PAR ? 1.f / pc.ns : 1.f;
   const bf16_t* zero = reinterpret_cast<const bf16_t*>(mer_conv_zero16);
@@ -756,7 +765,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_pipe_kernel(ConvGeom g) 
   };
   auto stage = [&](int buf, int k0) {
     bf16_t* la = smem + buf * BUF;
-    bf16_t* lb = la + BM_ * 64;
+    bf16_t* lb = la + BM_ * KS;
 #pragma unroll
     for (int j = 0; j < IA; ++j) {
       const bf16_t* src = PAR ? par_a_src(an[j], aoh[j], aow[j], aok[j], k0 + acl[j])
@@ -778,32 +787,32 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_pipe_kernel(ConvGeom g) 
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int fr = lane & 15, fq = lane >> 4;
-  const int nk = (Kr + CBK - 1) / CBK;
+  const int nk = (Kr + KS - 1) / KS;
   float part[FN][2];
   constexpr int G = IA + IB;
   static_assert(STAGES >= 2 && STAGES <= 4, "ring depth");
 #pragma unroll
   for (int p = 0; p < STAGES - 1; ++p)
-    if (p < nk) stage(p, p * CBK);
+    if (p < nk) stage(p, p * KS);
   for (int kt = 0; kt < nk; ++kt) {
     const int ahead = (nk - 1 - kt) < (STAGES - 2) ? (nk - 1 - kt) : (STAGES - 2);
     wait_tiles_in_flight<G>(ahead);
     lds_barrier();
-    if (kt + STAGES - 1 < nk) stage((kt + STAGES - 1) % STAGES, (kt + STAGES - 1) * CBK);
+    if (kt + STAGES - 1 < nk) stage((kt + STAGES - 1) % STAGES, (kt + STAGES - 1) * KS);
     const bf16_t* la = smem + (kt % STAGES) * BUF;
-    const bf16_t* lb = la + BM_ * 64;
+    const bf16_t* lb = la + BM_ * KS;
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
+    for (int s = 0; s < KS / 32; ++s) {
       bf16x8 af[FM], bfr[FN];
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
         const int r = wr * TM + i * 16 + fr;
-        af[i] = *reinterpret_cast<const bf16x8*>(la + r * 64 + cswz(r, s * 4 + fq) * 8);
+        af[i] = *reinterpret_cast<const bf16x8*>(la + r * KS + cswz_k<CW>(r, s * 4 + fq) * 8);
       }
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
         const int r = wc * TN + j * 16 + fr;
-        bfr[j] = *reinterpret_cast<const bf16x8*>(lb + r * 64 + cswz(r, s * 4 + fq) * 8);
+        bfr[j] = *reinterpret_cast<const bf16x8*>(lb + r * KS + cswz_k<CW>(r, s * 4 + fq) * 8);
       }
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -1130,16 +1139,16 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_pipe_kernel(ConvGeom g) 
   }
 }
 
-template <bool DGRAD, bool PAR, int BM_, int BN_, int WM = 2, int WN = 2, int STAGES = 2>
+template <bool DGRAD, bool PAR, int BM_, int BN_, int WM = 2, int WN = 2, int STAGES = 2, int KS = 64>
 int launch_conv_pipe_t(ConvGeom& g, hipStream_t st) {
   // PAR: grid.x covers the largest parity class (ph = pw = 0), grid.y = the 4 classes
   const int Mg = PAR ? g.N * ((g.OH + 1) / 2) * ((g.OW + 1) / 2) : g.N * g.OH * g.OW;
   const long tiles = (long)((Mg + BM_ - 1) / BM_) * ((g.Ncols + BN_ - 1) / BN_);
-  const size_t lds = STAGES * (BM_ + BN_) * 64 * sizeof(bf16_t);
-  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_pipe_kernel<DGRAD, PAR, BM_, BN_, WM, WN, STAGES>),
+  const size_t lds = STAGES * (BM_ + BN_) * KS * sizeof(bf16_t);
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_pipe_kernel<DGRAD, PAR, BM_, BN_, WM, WN, STAGES, KS>),
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return (int)hipErrorInvalidConfiguration;
-  hipLaunchKernelGGL((conv_pipe_kernel<DGRAD, PAR, BM_, BN_, WM, WN, STAGES>), dim3((unsigned)tiles, PAR ? 4 : 1),
+  hipLaunchKernelGGL((conv_pipe_kernel<DGRAD, PAR, BM_, BN_, WM, WN, STAGES, KS>), dim3((unsigned)tiles, PAR ? 4 : 1),
                      dim3(64 * WM * WN), lds, st, g);
   return (int)hipGetLastError();
 }
@@ -1156,6 +1165,13 @@ int launch_conv_pipe(ConvGeom& g, hipStream_t st, int variant) {
   if (variant == 3 && !small_m) {  // 256-row tiles (8 / 16 waves) for the large-M layers
     if (bn == 64) return launch_conv_pipe_t<DGRAD, PAR, 256, 64, 4, 2>(g, st);
     return launch_conv_pipe_t<DGRAD, PAR, 256, 128, 4, 4>(g, st);
+  }
+  if (variant == 5) {  // 32-wide K-tiles on a 4-deep ring (three K-tiles in flight), 4-wave tiles
+    if (bn == 64)
+      return small_m ? launch_conv_pipe_t<DGRAD, PAR, 64, 64, 2, 2, 4, 32>(g, st)
+                     : launch_conv_pipe_t<DGRAD, PAR, 128, 64, 2, 2, 4, 32>(g, st);
+    return small_m ? launch_conv_pipe_t<DGRAD, PAR, 64, 128, 2, 2, 4, 32>(g, st)
+                   : launch_conv_pipe_t<DGRAD, PAR, 128, 128, 2, 4, 4, 32>(g, st);
   }
   if (variant == 4) {  // variant-2 tiles on a 3-deep ring (two K-tiles in flight across each barrier)
     if (bn == 64)
@@ -1235,7 +1251,7 @@ MER_API int mer_conv_fwd(int N, int H, int W, int C, int K, int R, int S, int st
 
 MER_API int mer_conv_fwd_ex(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, const void* x,
                             const void* w_packed, void* y, float* stats, int variant, void* stream) {
-  if (C % 8 || variant < -1 || variant > 4) return (int)hipErrorInvalidValue;
+  if (C % 8 || variant < -1 || variant > 5) return (int)hipErrorInvalidValue;
   if (variant == -1) variant = 2;
   ConvGeom g{};
   g.N = N; g.IH = H; g.IW = W; g.IC = C;
@@ -1265,8 +1281,11 @@ MER_API int mer_conv_dgrad_bnr(int N, int H, int W, int C, int K, int R, int S, 
                                const void* wt_packed, void* dx, const void* residual, const void* residual_mask,
                                const void* bn_mask, const void* bn_x, const float* bn_ms, float* bn_red,
                                const void* bn_x2, const float* bn_ms2, float* bn_red2, int variant, void* stream) {
-  if (K % 8 || C % 8 || variant < -1 || variant > 4) return (int)hipErrorInvalidValue;
-  if (variant == -1) variant = 2;
+  if (K % 8 || C % 8 || variant < -1 || variant > 5) return (int)hipErrorInvalidValue;
+  // 64-channel outputs (layer1, the layer2.0 input gradients): 32-wide K-tiles on a 4-deep ring with 4-wave tiles
+  // (tools/bench_conv.py --fused: layer1 101 -> 65 us, layer2.0 s2 74 -> 51, downsample 48 -> 31); wider outputs
+  // keep the 64-wide 2-deep ring (the deep ring loses 10-50% there)
+  if (variant == -1) variant = C <= 64 ? 5 : 2;
   if (bn_red && (!bn_mask || !bn_x || !bn_ms || (bn_x2 && (!bn_ms2 || !bn_red2)))) return (int)hipErrorInvalidValue;
   if (bn_red && (variant == 0 || stride > 2)) return (int)hipErrorInvalidValue;  // fused only in the pipelined kernel
   ConvGeom g{};

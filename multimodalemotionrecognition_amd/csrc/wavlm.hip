@@ -249,8 +249,8 @@ MER_API int mer_layernorm_tr(int rows, int d, const void* x, int x_dtype, long l
 //   S_ij   = scale * q_i.k_j + gate_i * emb[bucket(j - i), h]                 (TF:243-271)
 //   O_i    = softmax_j(S_i) V
 // Q/K/V come from one fused projection [B*L, 3*768] (q | k | v).  L <= 256, dh = 64.
-// Grid (B*H, ceil(L/64)): a workgroup stages K (row-major) and V^T of its (b, h) in LDS, and each
-// of its 4 waves owns 16 query rows.  The scores are computed TRANSPOSED, S^T = K Q^T
+// Grid (B*H, ceil(L/(16 NW))): a workgroup stages K (row-major) and V^T of its (b, h) in LDS, and each
+// of its NW waves (default 5) owns 16 query rows.  The scores are computed TRANSPOSED, S^T = K Q^T
 // (v_mfma_f32_16x16x32_bf16, key j on the accumulator rows, query i = lane & 15), so every lane holds
 // whole key columns of one query: the softmax reduces in-lane plus two xor-shuffles, the gate is one
 // register per lane, and the accumulator tiles ARE the B operand of O^T = V^T P^T on
@@ -513,7 +513,9 @@ MER_API int mer_wavlm_attention_tr(int B, int L, int H, const void* qkv, long ld
     const char* e = getenv("MER_ATTN_NW");
     return e ? atoi(e) : 0;
   }();
-  const int NWsel = nw_env == 5 || nw_env == 10 || nw_env == 4 ? nw_env : 4;
+  // 5 waves (80 query rows) per block: 2 blocks per (b, h) at L = 149, 3 blocks per CU -> the B*H*2 blocks run in
+  // one round (4 waves: 3 blocks per (b, h), 1.5 rounds; 10 waves: one block per CU); bench.py A/B +1.5% / +1%
+  const int NWsel = nw_env == 5 || nw_env == 10 || nw_env == 4 ? nw_env : 5;
 #define MER_ATTN_LAUNCH(NW)                                                                                       \
   do {                                                                                                           \
     const size_t lds = sizeof(bf16_t) * ((size_t)LP * APAD + (size_t)ADH * (LP + 8)) +                           \

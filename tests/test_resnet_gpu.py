@@ -226,7 +226,7 @@ def test_conv_variants_bit_identical(N, H, C, Kc, R, stride, pad):
     wt = torch.empty(C, R * R * Kc, device="cuda", dtype=torch.bfloat16)
     K.pack_conv_weight(w, wt, C, True)
     ys, sts = [], []
-    for v in (0, 1, 2, 3):
+    for v in (0, 1, 2, 3, 4, 5):
         y = torch.empty(N, Ho, Ho, Kc, device="cuda", dtype=torch.bfloat16)
         st = K.bn_stats_buffer(Kc, "cuda", N * Ho * Ho)
         K.conv_fwd(x, wp, y, st, R, R, stride, pad, variant=v)
@@ -238,7 +238,7 @@ def test_conv_variants_bit_identical(N, H, C, Kc, R, stride, pad):
     res = torch.randn(N, H, H, C, device="cuda").bfloat16()
     mask = torch.randn(N, H, H, C, device="cuda").bfloat16()
     dxs = []
-    for v in (0, 1, 2, 3):
+    for v in (0, 1, 2, 3, 4, 5):
         dx = torch.empty(N, H, H, C, device="cuda", dtype=torch.bfloat16)
         K.conv_dgrad(dy, wt, dx, R, R, stride, pad, residual=res, mask=mask, variant=v)
         dxs.append(dx)
