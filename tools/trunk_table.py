@@ -51,8 +51,8 @@ def main():
     convs = trunk_convs()
     fwd = [r for r in win if "conv_pipe_kernel<false" in r["Kernel_Name"].replace(" ", "")]
     bwd = [r for r in win if "conv_pipe_kernel<true" in r["Kernel_Name"].replace(" ", "")
-           or r["Kernel_Name"].replace(" ", "").startswith("(anonymousnamespace)::wgrad_kernel")
-           or r["Kernel_Name"].replace(" ", "").startswith("void(anonymousnamespace)::wgrad_kernel")]
+           or "(anonymousnamespace)::wgrad_kernel<" in r["Kernel_Name"].replace(" ", "")
+           or "(anonymousnamespace)::wgrad_pipe_kernel<" in r["Kernel_Name"].replace(" ", "")]
     dur = lambda r: (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3  # noqa: E731
     print(f"{'layer':26s} {'pass':6s} {'M x N x K':>22s} {'us':>8s} {'TF/s':>7s}  kernel")
     tot = {"fwd": 0.0, "dgrad": 0.0, "wgrad": 0.0}
