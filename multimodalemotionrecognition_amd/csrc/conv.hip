@@ -672,6 +672,10 @@ struct ParClass {
   int ph, pw, Hc, Wc, r0, s0, nr, ns, dh0, dw0;
 };
 
+// Parity class of this block: grid.y walks the classes longest first (3 = odd/odd: 4 taps of a 3x3, then 2, 2, 1)
+// -- blocks dispatch y-major, so the long class-3 tiles start first and the short ones fill the tail.
+__device__ __forceinline__ int par_cls() { return 3 - (int)blockIdx.y; }
+
 __device__ __forceinline__ ParClass par_class(const ConvGeom& g, int cls) {
   ParClass c;
   c.ph = cls >> 1;
@@ -704,7 +708,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_pipe_kernel(ConvGeom g) 
   ParClass pc{};
   int M, Kr, rowsH, rowsW;  // this launch's GEMM rows / reduction length, row -> (n, a, b) grid
   if (PAR) {
-    pc = par_class(g, blockIdx.y);
+    pc = par_class(g, par_cls());
     M = g.N * pc.Hc * pc.Wc;
     Kr = pc.nr * pc.ns * g.IC;
     rowsH = pc.Hc;
@@ -837,7 +841,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_pipe_kernel(ConvGeom g) 
   auto red_row = [&]() -> long {
     long row_id = ty;
     if (PAR)
-      for (int c2 = 0; c2 < (int)blockIdx.y; ++c2) {
+      for (int c2 = 0; c2 < par_cls(); ++c2) {
         const ParClass q = par_class(g, c2);
         row_id += (g.N * q.Hc * q.Wc + BM_ - 1) / BM_;
       }
@@ -1056,7 +1060,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_pipe_kernel(ConvGeom g) 
       // row = ty, after the row tiles of the preceding parity classes in the PAR (stride-2) form
       long row_id = ty;
       if (PAR)
-        for (int c2 = 0; c2 < (int)blockIdx.y; ++c2) {
+        for (int c2 = 0; c2 < par_cls(); ++c2) {
           const ParClass q = par_class(g, c2);
           row_id += (g.N * q.Hc * q.Wc + BM_ - 1) / BM_;
         }
