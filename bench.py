@@ -189,6 +189,9 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: this process's CPU share (cpu_share_threads)")
     ap.add_argument("--cpu-steps", type=int, default=10)
     ap.add_argument("--cpu-warmup", type=int, default=10)
+    ap.add_argument("--stream-priority", choices=("normal", "high"), default="normal",
+                    help="run the training loop on a stream of this priority (the prefetched WavLM forward stays on its "
+                         "normal-priority side stream)")
     ap.add_argument("--no-prefetch", action="store_true",
                     help="run the frozen WavLM inline in every step instead of overlapping the next batch's "
                          "WavLM forward with this step's backward")
@@ -200,6 +203,14 @@ def main():
     args = ap.parse_args()
 
     world, rank, local = init_distributed()
+    if args.stream_priority == "high":
+        hi = torch.cuda.Stream(device=local, priority=torch.cuda.Stream.priority_range()[1])
+        with torch.cuda.stream(hi):
+            return _bench(args, world, rank, local)
+    return _bench(args, world, rank, local)
+
+
+def _bench(args, world, rank, local):
     dev = torch.device("cuda", local)
     torch.manual_seed(1234)  # identical init on every rank
     prior = dict(xattn_use_emotion_prior=True, forward_emotion_prior_flags=True) if args.emotion_prior else {}

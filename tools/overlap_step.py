@@ -1,0 +1,81 @@
+"""Unprofiled timeline of the bench train step (TrainStep with the early next-batch WavLM prefetch) from HIP events:
+when the prefetched WavLM forward starts / ends on the side stream relative to the step's start on the main stream,
+and where the main stream's forward ends.  python tools/overlap_step.py"""
+import sys
+from pathlib import Path
+
+import torch
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+import bench  # noqa: E402
+from multimodalemotionrecognition_amd import fusion as F  # noqa: E402
+from multimodalemotionrecognition_amd.train import TrainStep, build_model, build_optimizer, make_loss  # noqa: E402
+
+
+def main():
+    prio = int(sys.argv[1]) if len(sys.argv) > 1 else None  # run the steps on a main stream of this priority
+    if prio is not None:
+        print("stream priority range (least, greatest):", torch.cuda.Stream.priority_range())
+        with torch.cuda.stream(torch.cuda.Stream(device=0, priority=prio)):
+            return run()
+    return run()
+
+
+def run():
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(1234)
+    model = build_model(8, "xattn", pretrained_video=False, use_wavlm=True).to(dev)
+    opt = build_optimizer(model, lr=1e-3, weight_decay=1e-4)
+    step = TrainStep(model, opt, make_loss("xattn"), "xattn", None)
+    video, audio, labels = bench.synthetic_batch(dev, 20261015)
+    ev = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
+    marks = []
+    orig = model.prefetch_audio
+
+    def prefetch(a):  # events on the side stream around the prefetched encoder forward
+        side = F._side_stream(a.device)
+        side.wait_stream(torch.cuda.current_stream(a.device))
+        s0 = ev()
+        s0.record(side)
+        ok = orig(a)
+        s1 = ev()
+        s1.record(side)
+        marks.append((s0, s1))
+        return ok
+
+    model.prefetch_audio = prefetch
+    orig_head = model.xattn_from_features
+
+    def head(v, a):  # main-stream event when the trunk forward is done (the head starts)
+        e = ev()
+        e.record()
+        heads.append(e)
+        return orig_head(v, a)
+
+    heads = []
+    model.xattn_from_features = head
+    for _ in range(10):
+        step(video, audio, labels, next_audio=audio)
+    torch.cuda.synchronize()
+    marks.clear()
+    heads.clear()
+    starts, ends = [], []
+    for _ in range(10):
+        t0 = ev()
+        t0.record()
+        step(video, audio, labels, next_audio=audio)
+        t1 = ev()
+        t1.record()
+        starts.append(t0)
+        ends.append(t1)
+    torch.cuda.synchronize()
+    n = len(starts)
+    for i in range(n):
+        s0, s1 = marks[i]
+        print(f"step {i}: step {starts[i].elapsed_time(ends[i]):.3f} ms | WavLM(next) on side: start "
+              f"{starts[i].elapsed_time(s0):+.3f} end {starts[i].elapsed_time(s1):+.3f} ms | head starts at "
+              f"{starts[i].elapsed_time(heads[i]):.3f} ms")
+
+
+if __name__ == "__main__":
+    main()
