@@ -204,19 +204,32 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs g) {
 // glds writes lane-linear (base + 16*lane), so the XOR goes on each lane's SOURCE address and on
 // the fragment read (rule 21: both sides).  Rows past M/N are clamped to the last valid row (their
 // outputs are discarded); K is a multiple of 64, so no K tail.
-template <int BM_, int BN_, int WM_, int WN_, int STAGES_ = 2>
+template <int BM_, int BN_, int WM_, int WN_, int STAGES_ = 2, int KS_ = 64>
 struct PipeCfg {
   static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_;       // tile, waves along M / N
   static constexpr int STAGES = STAGES_;                            // LDS ring depth (K-tiles)
+  static constexpr int KS = KS_;                                    // K-tile width (64, or 32 for deep rings)
+  static constexpr int CW = KS / 8, RPG = 64 / CW;                  // 16-byte chunks per LDS row, rows per glds
   static constexpr int WAVES = WM * WN, NT = 64 * WAVES;
   static constexpr int TM = BM / WM, TN = BN / WN;                  // per-wave output
   static constexpr int FM = TM / 16, FN = TN / 16;                  // 16x16 fragments per wave
-  static constexpr int IA = BM / 8 / WAVES, IB = BN / 8 / WAVES;    // glds per wave per K-tile
-  static constexpr int BUF = (BM + BN) * 64;                        // bf16 elements per LDS buffer
-  static_assert(IA * 8 * WAVES == BM && IB * 8 * WAVES == BN, "tile rows must split into 8-row glds pieces");
+  static constexpr int IA = BM / RPG / WAVES, IB = BN / RPG / WAVES;  // glds per wave per K-tile
+  static constexpr int BUF = (BM + BN) * KS;                        // bf16 elements per LDS buffer
+  static_assert(IA * RPG * WAVES == BM && IB * RPG * WAVES == BN, "tile rows must split into whole glds pieces");
+  static_assert(KS == 64 || KS == 32, "K-tile");
 };
 
 __device__ __forceinline__ int swz_chunk(int row, int c) { return c ^ ((row >> 1) & 7); }
+// CW chunks per row: 8 (128-byte rows) or 4 (64-byte rows: four rows share a 256-byte bank row, XOR by row bits 2-3)
+template <int CW>
+__device__ __forceinline__ int swz_k(int row, int c) {
+  return CW == 8 ? (c ^ ((row >> 1) & 7)) : (c ^ ((row >> 2) & 3));
+}
+// element offset of K-tile u of width KS (the 32-wide tiles walk the 64-wide order in halves)
+template <int KS>
+__device__ __forceinline__ int ktile_off_k(const GemmArgs& g, int u) {
+  return KS == 64 ? ktile_off(g, u) : ktile_off(g, u >> 1) + (u & 1) * 32;
+}
 
 
 __device__ __attribute__((aligned(16))) uint32_t mer_gemm_zero16[4] = {0u, 0u, 0u, 0u};
@@ -239,33 +252,33 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_pipe_kernel(GemmArgs g) {
   const bf16_t* pa[CF::IA];
   const bf16_t* pb[CF::IB];
   int at[CF::IA], acl[CF::IA];  // AMODE 1: the row's time index and logical chunk
-  const int lrow = lane >> 3, lchunk = lane & 7;
+  const int lrow = lane / CF::CW, lchunk = lane % CF::CW;
 #pragma unroll
   for (int j = 0; j < CF::IA; ++j) {
-    const int r = (w * CF::IA + j) * 8 + lrow;
+    const int r = (w * CF::IA + j) * CF::RPG + lrow;
     int m = m0 + r;
     m = m < g.M ? m : g.M - 1;
     if (AMODE == 0) {
-      pa[j] = g.A + (long)(m / g.a_rpg) * g.a_gstride + (long)(m % g.a_rpg) * g.a_rstride + swz_chunk(r, lchunk) * 8;
+      pa[j] = g.A + (long)(m / g.a_rpg) * g.a_gstride + (long)(m % g.a_rpg) * g.a_rstride + swz_k<CF::CW>(r, lchunk) * 8;
     } else {
       const int b = m / g.pc_L;
       at[j] = m - b * g.pc_L;
-      acl[j] = swz_chunk(r, lchunk) * 8;
+      acl[j] = swz_k<CF::CW>(r, lchunk) * 8;
       pa[j] = g.A + (long)b * g.pc_L * g.pc_ldx + (long)z * g.pc_cg;
     }
   }
   const bf16_t* Bz = g.B + (long)z * g.b_zstride;
 #pragma unroll
   for (int j = 0; j < CF::IB; ++j) {
-    const int r = (w * CF::IB + j) * 8 + lrow;
+    const int r = (w * CF::IB + j) * CF::RPG + lrow;
     int n = n0 + r;
     n = n < g.N ? n : g.N - 1;
-    pb[j] = Bz + (long)n * g.ldb + swz_chunk(r, lchunk) * 8;
+    pb[j] = Bz + (long)n * g.ldb + swz_k<CF::CW>(r, lchunk) * 8;
   }
   const float inv_cg = AMODE == 1 ? 1.f / g.pc_cg : 0.f;
   auto stage = [&](int buf, int k0) {
     bf16_t* la = smem + buf * CF::BUF;
-    bf16_t* lb = la + CF::BM * 64;
+    bf16_t* lb = la + CF::BM * CF::KS;
 #pragma unroll
     for (int j = 0; j < CF::IA; ++j) {
       if (AMODE == 0) {
@@ -292,7 +305,7 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_pipe_kernel(GemmArgs g) {
 
   // fragment read offsets (elements) inside one operand image, per k-step s: row*64 + phys_chunk*8
   const int fr = lane & 15, fq = lane >> 4;
-  const int nk = g.K / 64;
+  const int nk = g.K / CF::KS;
   constexpr int S = CF::STAGES, G = CF::IA + CF::IB;
   static_assert(S >= 2 && S <= 4 && (S - 2) * G < 64, "ring depth");
   // Ring of S LDS buffers: tiles kt+1 .. kt+S-2 stay in flight (counted vmcnt) across the barrier
@@ -300,28 +313,28 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_pipe_kernel(GemmArgs g) {
   // the tile kt+S-1 DMA then reuses.  Raw s_barrier: __syncthreads() would drain vmcnt to 0.
 #pragma unroll
   for (int p = 0; p < S - 1; ++p)
-    if (p < nk) stage(p, ktile_off(g, p));
+    if (p < nk) stage(p, ktile_off_k<CF::KS>(g, p));
   for (int kt = 0; kt < nk; ++kt) {
     const int ahead = (nk - 1 - kt) < (S - 2) ? (nk - 1 - kt) : (S - 2);
     wait_tiles_in_flight<G>(ahead);
     __builtin_amdgcn_s_waitcnt((15) | (7 << 4) | (0 << 8) | (3 << 14));  // lgkmcnt(0) only
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    if (kt + S - 1 < nk) stage((kt + S - 1) % S, ktile_off(g, kt + S - 1));
+    if (kt + S - 1 < nk) stage((kt + S - 1) % S, ktile_off_k<CF::KS>(g, kt + S - 1));
     const bf16_t* la = smem + (kt % S) * CF::BUF;
-    const bf16_t* lb = la + CF::BM * 64;
+    const bf16_t* lb = la + CF::BM * CF::KS;
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
+    for (int s = 0; s < CF::KS / 32; ++s) {
       bf16x8 af[CF::FM], bfr[CF::FN];
 #pragma unroll
       for (int i = 0; i < CF::FM; ++i) {
         const int r = wr * CF::TM + i * 16 + fr;
-        af[i] = *reinterpret_cast<const bf16x8*>(la + r * 64 + swz_chunk(r, s * 4 + fq) * 8);
+        af[i] = *reinterpret_cast<const bf16x8*>(la + r * CF::KS + swz_k<CF::CW>(r, s * 4 + fq) * 8);
       }
 #pragma unroll
       for (int j = 0; j < CF::FN; ++j) {
         const int r = wc * CF::TN + j * 16 + fr;
-        bfr[j] = *reinterpret_cast<const bf16x8*>(lb + r * 64 + swz_chunk(r, s * 4 + fq) * 8);
+        bfr[j] = *reinterpret_cast<const bf16x8*>(lb + r * CF::KS + swz_k<CF::CW>(r, s * 4 + fq) * 8);
       }
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -616,6 +629,9 @@ using CfgW3 = PipeCfg<128, 128, 2, 4, 3>;  // 8 waves, 3-deep, 96 KiB LDS
 using CfgV3 = PipeCfg<128, 64, 4, 1, 3>;   // 4 waves as 4x1 (32x64 each), 3-deep, 72 KiB LDS
 using CfgX2 = PipeCfg<256, 128, 4, 4, 2>;  // 16 waves (64x32 each), 2-deep, 96 KiB LDS (1 block / CU)
 using CfgY2 = PipeCfg<256, 256, 4, 4, 2>;  // 16 waves (64x64 each), 2-deep, 128 KiB LDS
+using CfgY4 = PipeCfg<256, 256, 4, 4, 4, 32>;  // 16 waves, 32-wide K-tiles on a 4-deep ring, 128 KiB LDS
+using CfgT4 = PipeCfg<128, 64, 2, 2, 4, 32>;   // 128x64 tiles, 32-wide K on a 4-deep ring, 48 KiB LDS
+using CfgW4 = PipeCfg<128, 128, 2, 4, 4, 32>;  // 8 waves, 32-wide K on a 4-deep ring, 64 KiB LDS
 
 template <class CF, typename TOUT, int AMODE>
 int launch_pipe_t(const GemmArgs& g, int groups, hipStream_t st) {
@@ -701,7 +717,7 @@ MER_API int mer_gemm_bf16_tr(int M, int N, int K, const void* A, long a_gstride,
   if (M <= 0 || N <= 0) return 0;
   if (drop_p < 0.f || drop_p >= 1.f || (drop_p > 0.f && !drop_seed) || skip_bit < 0 || skip_bit > 62)
     return (int)hipErrorInvalidValue;
-  if (variant < -1 || variant > 14) return (int)hipErrorInvalidValue;
+  if (variant < -1 || variant > 17) return (int)hipErrorInvalidValue;
   if (K % 8 != 0 || a_rpg <= 0 || (a_rstride % 8) != 0 || (a_gstride % 8) != 0 || (ldw % 8) != 0)
     return (int)hipErrorInvalidValue;
   if ((((uintptr_t)A) | ((uintptr_t)W)) & 15) return (int)hipErrorInvalidValue;
@@ -744,6 +760,9 @@ MER_API int mer_gemm_bf16_tr(int M, int N, int K, const void* A, long a_gstride,
     case 12: return launch_pipe<CfgX2>(g, c_dtype, st);
     case 13: return launch_pipe<CfgY2>(g, c_dtype, st);
     case 14: return c_dtype == MER_BF16 ? launch_phase_t<bf16_t>(g, st) : launch_phase_t<float>(g, st);
+    case 15: return launch_pipe<CfgY4>(g, c_dtype, st);
+    case 16: return launch_pipe<CfgT4>(g, c_dtype, st);
+    case 17: return launch_pipe<CfgW4>(g, c_dtype, st);
     default: return launch<0>(g, c_dtype, 1, st);
   }
 }
