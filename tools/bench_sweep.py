@@ -1,7 +1,7 @@
 """C4 (BASELINE.json configs[3]): the fusion-head sweep under one HIP backend -- full train steps (ResNet18 +
 WavLM-base frozen + head, B=32 synthetic 3 s clips, fwd+bwd+Adam) for late / concat / gated / xattn /
 xattn + emotion-prior bias, steps/s each.
-    python tools/bench_sweep.py [--steps 10] [--warmup 3]"""
+    python tools/bench_sweep.py [--steps 30] [--warmup 10]"""
 import argparse
 import json
 import sys
@@ -16,8 +16,8 @@ from oracle import params  # noqa: E402  (synthetic clip generator only)
 from multimodalemotionrecognition_amd.train import TrainStep, build_model, build_optimizer, make_loss  # noqa: E402
 
 ap = argparse.ArgumentParser()
-ap.add_argument("--steps", type=int, default=10)
-ap.add_argument("--warmup", type=int, default=3)
+ap.add_argument("--steps", type=int, default=30)
+ap.add_argument("--warmup", type=int, default=10)  # graphs are captured during the first steps
 ap.add_argument("--batch", type=int, default=32)
 args = ap.parse_args()
 video, audio, labels = params.clip_inputs(args.batch, seed=20261015)
