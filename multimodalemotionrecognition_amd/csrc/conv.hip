@@ -1358,7 +1358,11 @@ static int conv_wgrad_impl(int N, int H, int W, int C, int Creal, int K, int R, 
     else
       hipLaunchKernelGGL((wgrad_kernel<128, 128, 2, 4>), grid, dim3(512), 0, st, g);
   }
-  if (splits > 16) {  // many partial slabs: a wide reduce first (one serial chain per element was latency-bound)
+  static const int fold_max = [] {  // MER_WGRAD_FOLD_MAX: most slabs folded in the single fold+scatter pass (A/B)
+    const char* e = getenv("MER_WGRAD_FOLD_MAX");
+    return e ? atoi(e) : 16;
+  }();
+  if (splits > fold_max) {  // many partial slabs: a wide reduce first (one serial chain per element was latency-bound)
     const int SG = splits >= 64 ? 16 : 8;
     const long total = (long)K * R * S * C;
     const int E = 256 / SG;
