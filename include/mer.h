@@ -418,6 +418,10 @@ int mer_pack_conv_weight(int K, int C, int R, int S, int Cp, int transpose, cons
  * layout [K][(R+2)/2][(S+2)/2][Cp], see mer_pack_input_s2d), records in output order, first
  * elements the prefix sums of K*R*S*Cp; total = the sum. */
 int mer_pack_conv_weights(int n, const long long* desc, long total, void* stream);
+/* The same packs on a 1-D grid with no idle blocks: column 8 of each record is instead its first block, a record
+ * taking K blocks (transpose 0 / 2) or Cp * ceil(K / 64) blocks (transpose 1); total_blocks = the sum.  Output is
+ * bit-identical to mer_pack_conv_weights (the per-step re-pack in video.py uses this form). */
+int mer_pack_conv_weights_flat(int n, const long long* desc, long total_blocks, void* stream);
 
 /* BatchNorm2d finalize: ms[c] = (mean, rstd) from the MER_BN_STAT_ROWS(M) stats rows of a conv forward (summed in a
  * fixed order, through the buffer's 64 scratch rows) over M values and, when non-NULL, updates

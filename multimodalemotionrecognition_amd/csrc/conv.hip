@@ -1480,14 +1480,49 @@ MER_API int mer_pack_conv_weight(int K, int C, int R, int S, int Cp, int transpo
 //   transpose 0: block = one output channel k: w[k][c][rs] (C*RS contiguous floats) -> out[k][rs][c<Cp];
 //   transpose 1: block = (input channel c, 64 output channels k0..): w[k][c][rs] (runs of RS) ->
 //                out[c][rs][k0..k0+63].
-__global__ __launch_bounds__(256) void pack_w_batched_kernel(const long long* __restrict__ desc) {
+// FLAT: one-dimensional grid over every record's blocks (column 8 = the record's first block): no idle blocks (the
+// 2-D form launches 4,096 blocks per record, most of which only exit -- that dispatch was most of its time)
+template <bool FLAT>
+__global__ __launch_bounds__(256) void pack_w_batched_kernel(const long long* __restrict__ desc, int n) {
   __shared__ float tile[4608];  // max C*RS (512 * 9) or 64 * RS (RS <= 49 -> 3136)
-  const long long* r = desc + blockIdx.y * 9;
+  int rec = FLAT ? 0 : (int)blockIdx.y;
+  if (FLAT)
+    for (int i = 1; i < n; ++i)
+      if (desc[i * 9 + 8] <= (long long)blockIdx.x) rec = i;
+  const long long* r = desc + rec * 9;
+  const int bx = FLAT ? (int)(blockIdx.x - r[8]) : (int)blockIdx.x;
   const float* w = reinterpret_cast<const float*>(r[0]);
   bf16_t* out = reinterpret_cast<bf16_t*>(r[1]);
   const int K = (int)r[2], C = (int)r[3], RS = (int)(r[4] * r[5]), Cp = (int)r[6];
+  if (r[7] == 3) {  // transposed pack from the forward bf16 pack: src [K][RS][C] -> out [C][RS][K] (C, K % 64 == 0)
+    // block = (tap, 64-channel tile, 64-output tile): 16-byte loads of 64 k-rows into LDS, 16-byte stores of 64 c-rows
+    const uint16_t* src = reinterpret_cast<const uint16_t*>(r[0]);
+    uint16_t* lds = reinterpret_cast<uint16_t*>(tile);  // [64 k][72] (row pad spreads the column gathers)
+    const int kbn = K >> 6, cbn = C >> 6;
+    const int rs = bx / (kbn * cbn), rem = bx - rs * kbn * cbn, cb = rem / kbn, kb = rem - cb * kbn;
+    if (rs >= RS) return;
+    const int k0 = kb * 64, c0 = cb * 64;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int i = threadIdx.x + 256 * j, kk = i >> 3, ch = (i & 7) * 8;
+      const uint4 v = *reinterpret_cast<const uint4*>(src + ((long)(k0 + kk) * RS + rs) * C + c0 + ch);
+      *reinterpret_cast<uint4*>(lds + kk * 72 + ch) = v;
+    }
+    __syncthreads();
+    uint16_t* ob = reinterpret_cast<uint16_t*>(out);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int i = threadIdx.x + 256 * j, cc = i >> 3, kc = (i & 7) * 8;
+      uint32_t pk[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        pk[e] = (uint32_t)lds[(kc + 2 * e) * 72 + cc] | ((uint32_t)lds[(kc + 2 * e + 1) * 72 + cc] << 16);
+      *reinterpret_cast<uint4*>(ob + ((long)(c0 + cc) * RS + rs) * K + k0 + kc) = uint4{pk[0], pk[1], pk[2], pk[3]};
+    }
+    return;
+  }
   if (r[7] == 2) {  // space-to-depth stem: out[k][ry][rx][ch], tap (r, s) = (2ry+dy-1, 2rx+dx-1), ch = (dy*2+dx)*C + c
-    const int k = blockIdx.x;
+    const int k = bx;
     const int R = (int)r[4], S = (int)r[5], Ro = (R + 2) / 2, So = (S + 2) / 2;
     if (k >= K) return;
     const float* src = w + (long)k * C * RS;
@@ -1502,7 +1537,7 @@ __global__ __launch_bounds__(256) void pack_w_batched_kernel(const long long* __
       dst[i] = ok ? f2bf(tile[c * RS + rr * S + ss]) : (bf16_t)0;
     }
   } else if (!r[7]) {
-    const int k = blockIdx.x;
+    const int k = bx;
     if (k >= K) return;
     const float* src = w + (long)k * C * RS;
     const int n = C * RS;
@@ -1529,7 +1564,7 @@ __global__ __launch_bounds__(256) void pack_w_batched_kernel(const long long* __
     }
   } else {
     const int kb = (K + 63) / 64;
-    const int c = blockIdx.x / kb, k0 = (blockIdx.x - c * kb) * 64;
+    const int c = bx / kb, k0 = (bx - c * kb) * 64;
     if (c >= Cp) return;
     const int nk = min(64, K - k0);
     const float inv_RS = 1.f / RS;
@@ -1560,7 +1595,13 @@ MER_API int mer_pack_conv_weights(int n, const long long* desc, long total, void
   (void)total;
   if (n <= 0 || n > 64) return (int)hipErrorInvalidValue;
   // grid.x covers the largest record: 512 output channels (layout 0) or 512 x 8 (c, k-block) tiles
-  hipLaunchKernelGGL(pack_w_batched_kernel, dim3(512 * 8, n), dim3(256), 0, (hipStream_t)stream, desc);
+  hipLaunchKernelGGL(pack_w_batched_kernel<false>, dim3(512 * 8, n), dim3(256), 0, (hipStream_t)stream, desc, n);
+  MER_LAUNCH_CHECK();
+}
+MER_API int mer_pack_conv_weights_flat(int n, const long long* desc, long total_blocks, void* stream) {
+  if (n <= 0 || n > 64 || total_blocks <= 0 || total_blocks > (1L << 30)) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(pack_w_batched_kernel<true>, dim3((unsigned)total_blocks), dim3(256), 0, (hipStream_t)stream, desc,
+                     n);
   MER_LAUNCH_CHECK();
 }
 

@@ -546,11 +546,14 @@ def pack_conv_weight(w, out, cp, transpose):
     LIB("mer_pack_conv_weight", Kc, C, R, S, cp, int(transpose), w.data_ptr(), out.data_ptr(), stream_ptr())
 
 
-def pack_conv_weights(desc, total):
-    """Batched weight packing from a device int64 descriptor table [n, 9] (see mer_pack_conv_weights)."""
+def pack_conv_weights(desc, blocks, flat=True):
+    """Batched weight packing from a device int64 descriptor table [n, 9].  flat: one 1-D grid of ``blocks``
+    blocks, column 8 of each record its first block (mer_pack_conv_weights_flat); otherwise the 2-D grid of
+    mer_pack_conv_weights (``blocks`` is then the total element count and column 8 is ignored)."""
     if desc.dtype != torch.int64 or desc.dim() != 2 or desc.shape[1] != 9 or not desc.is_cuda:
         raise ValueError("pack descriptor table must be a device int64 [n, 9] tensor")
-    LIB("mer_pack_conv_weights", desc.shape[0], desc.data_ptr(), int(total), stream_ptr())
+    name = "mer_pack_conv_weights_flat" if flat else "mer_pack_conv_weights"
+    LIB(name, desc.shape[0], desc.data_ptr(), int(blocks), stream_ptr())
 
 
 def bn_finalize(stats, M, eps, momentum, ms, rmean=None, rvar=None, nbt=None):

@@ -223,18 +223,22 @@ class ResNet18Trunk(nn.Sequential):
     def _pack_plan(self, transpose: bool):
         """Persistent packed-weight buffers + the device descriptor table of one batched pack launch.
         Forward packs [K][R][S][Cp] for every conv (the stem in its space-to-depth 4x4 form); transposed packs
-        [Cp][R][S][K] for every conv but the stem (the frames need no data gradient)."""
+        [Cp][R][S][K] for every conv but the stem (the frames need no data gradient), as 64x64 tile transposes of
+        the forward bf16 packs (mode 3: half the bytes of re-reading the fp32 weights; pack_all(True) refreshes
+        the forward packs first if they are stale)."""
         convs = self.__dict__.get("_mer_convs")
         if convs is None:
             convs = self.__dict__["_mer_convs"] = [m for m in self.modules() if isinstance(m, nn.Conv2d)]
+        fwd = None
         if transpose:
             convs = convs[1:]
-        ptrs = tuple(c.weight.data_ptr() for c in convs)
+            fwd = self._pack_plan(False)
+        ptrs = tuple(c.weight.data_ptr() for c in convs) + ((id(fwd),) if fwd is not None else ())
         plan = self._plans.get(transpose)
         if plan is not None and plan["ptrs"] == ptrs:
             return plan
         dev = convs[0].weight.device
-        outs, rows, first = {}, [], 0
+        outs, rows, first, blocks = {}, [], 0, 0
         for c in convs:
             Kc, C, R, S = c.weight.shape
             if C * R * S > 4608 or Kc > 512 or C > 512:  # the batched kernel's LDS tile / grid bounds
@@ -248,9 +252,15 @@ class ResNet18Trunk(nn.Sequential):
                 shape = (cp, R * S * Kc) if transpose else (Kc, R * S * cp)
             buf = torch.empty(shape, device=dev, dtype=torch.bfloat16)
             outs[id(c)] = buf
-            rows.append([c.weight.data_ptr(), buf.data_ptr(), Kc, C, R, S, cp, mode, first])
+            src = c.weight.data_ptr()
+            if transpose and C % 64 == 0 and Kc % 64 == 0:
+                mode, src = 3, fwd["outs"][id(c)].data_ptr()
+            rows.append([src, buf.data_ptr(), Kc, C, R, S, cp, mode, blocks])
             first += buf.numel()
-        plan = dict(convs=convs, ptrs=ptrs, outs=outs, total=first, vers=None,
+            # blocks: (tap, c tile, k tile) | (c, 64-k tile) | one per k
+            blocks += (R * S * (C // 64) * (Kc // 64) if mode == 3 else cp * ((Kc + 63) // 64) if mode == 1
+                       else Kc)
+        plan = dict(convs=convs, ptrs=ptrs, outs=outs, total=first, blocks=blocks, vers=None, fwd=fwd,
                     desc=torch.tensor(rows, dtype=torch.int64).to(dev))
         self._plans[transpose] = plan
         return plan
@@ -259,8 +269,11 @@ class ResNet18Trunk(nn.Sequential):
         """(Re-)pack every conv weight in one launch when any weight changed (always inside a capture)."""
         plan = self._pack_plan(transpose)
         vers = tuple(weight_version(c.weight) for c in plan["convs"])
+        if plan["fwd"] is not None and plan["fwd"]["vers"] != tuple(weight_version(c.weight)
+                                                                    for c in plan["fwd"]["convs"]):
+            self.pack_all(False)  # the transposed packs read the forward packs
         if self._force_pack or vers != plan["vers"]:
-            K.pack_conv_weights(plan["desc"], plan["total"])
+            K.pack_conv_weights(plan["desc"], plan["blocks"])
             plan["vers"] = vers
 
     def packed(self, conv: nn.Conv2d, cp: int, transpose: bool):

@@ -325,7 +325,7 @@ def test_space_to_depth_stem_vs_torch(H):
     wd = w.cuda()
     wp = torch.empty(64, 4 * 4 * S2D_CH, device="cuda", dtype=torch.bfloat16)
     desc = torch.tensor([[wd.data_ptr(), wp.data_ptr(), 64, 3, 7, 7, S2D_CH, 2, 0]], dtype=torch.int64).cuda()
-    K.pack_conv_weights(desc, wp.numel())
+    K.pack_conv_weights(desc, 64)  # one block per output channel
     y = torch.empty(N, H // 2, H // 2, 64, device="cuda", dtype=torch.bfloat16)
     K.conv_fwd(xs, wp, y, None, 4, 4, 1, 0)
     wr = w.clone().requires_grad_(True)
@@ -400,3 +400,54 @@ def test_trunk_forward_backward_deterministic():
         a, b = grads[0].get(id(q)), grads[1].get(id(q))
         if a is not None:
             assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("transpose", [False, True])
+def test_flat_pack_matches_2d_pack(transpose):
+    """mer_pack_conv_weights_flat (the per-step re-pack: 1-D grid, column 8 = first block) == the 2-D-grid
+    mer_pack_conv_weights bit for bit, for every ResNet18 conv (forward + s2d stem, or transposed)."""
+    from multimodalemotionrecognition_amd import kernels as K
+    from multimodalemotionrecognition_amd.video import ResNet18Trunk
+
+    torch.manual_seed(7)
+    trunk = ResNet18Trunk().cuda()
+    trunk.pack_all(False)  # the transposed (mode 3) records read the forward packs
+    plan = trunk._pack_plan(transpose)
+    bufs = [plan["outs"][id(c)] for c in plan["convs"]]
+    for b in bufs:
+        b.fill_(1.0)
+    K.pack_conv_weights(plan["desc"], plan["total"], flat=False)
+    ref = [b.clone() for b in bufs]
+    for b in bufs:
+        b.fill_(-3.0)
+    K.pack_conv_weights(plan["desc"], plan["blocks"])
+    torch.cuda.synchronize()
+    for c, b, r in zip(plan["convs"], bufs, ref):
+        assert torch.equal(b, r), f"conv {tuple(c.weight.shape)} differs"
+
+
+def test_transposed_pack_from_forward_pack():
+    """Mode 3 (64x64 tile transpose of the forward bf16 pack, the per-step path) == mode 1 (the fp32 weights
+    re-read and rounded) bit for bit for every non-stem ResNet18 conv, and == torch's own layout."""
+    from multimodalemotionrecognition_amd import kernels as K
+    from multimodalemotionrecognition_amd.video import ResNet18Trunk
+
+    torch.manual_seed(11)
+    trunk = ResNet18Trunk().cuda()
+    trunk.pack_all(True)
+    plan = trunk._pack_plan(True)
+    assert all(int(m) == 3 for m in plan["desc"][:, 7].tolist())
+    got = [plan["outs"][id(c)].clone() for c in plan["convs"]]
+    rows, blocks = [], 0
+    for c, r in zip(plan["convs"], plan["desc"].tolist()):
+        Kc, C = r[2], r[3]
+        rows.append([c.weight.data_ptr(), r[1], Kc, C, r[4], r[5], r[6], 1, blocks])
+        blocks += r[6] * ((Kc + 63) // 64)
+    K.pack_conv_weights(torch.tensor(rows, dtype=torch.int64).cuda(), blocks)
+    torch.cuda.synchronize()
+    for c, g in zip(plan["convs"], got):
+        ref = plan["outs"][id(c)]
+        assert torch.equal(g, ref), f"conv {tuple(c.weight.shape)} differs"
+        Kc, C, R, S = c.weight.shape
+        want = c.weight.detach().bfloat16().permute(1, 2, 3, 0).reshape(C, R * S * Kc)
+        assert torch.equal(g, want)
