@@ -531,8 +531,10 @@ def conv_wgrad(x, dy, dw, R, S, stride, pad, creal=None, variant=-1, splits=None
 def pack_input_s2d(x, y):
     """fp32 NCHW frames -> space-to-depth bf16 [N][H/2+3][W/2+3][16] (the 4x4 stride-1 form of the stem conv)."""
     N, C, H, W = x.shape
-    if tuple(y.shape) != (N, H // 2 + 3, W // 2 + 3, 16) or y.dtype != torch.bfloat16:
+    if tuple(y.shape) != (N, H // 2 + 3, W // 2 + 3, 16) or y.dtype != torch.bfloat16 or not y.is_contiguous():
         raise ValueError("pack_input_s2d shapes")
+    if x.dtype != torch.float32 or not x.is_contiguous():
+        raise ValueError("pack_input_s2d reads contiguous fp32 NCHW frames")
     LIB("mer_pack_input_s2d", N, C, H, W, x.data_ptr(), y.data_ptr(), stream_ptr())
 
 

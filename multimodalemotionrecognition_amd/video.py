@@ -95,7 +95,8 @@ class _TrunkFn(torch.autograd.Function):
 class _TrunkGraphs(G.PendingGuard):
     """Captured forward / backward hipGraphs of one (input shape, mode) of the trunk (graphs.py).
 
-    Forward graph: pack input -> ... -> avgpool, with the per-step weight packing and the BatchNorm
+    Forward graph: (space-to-depth frames, packed just before the replay) -> ... -> avgpool, with the per-step
+    weight packing and the BatchNorm
     running-stat updates inside it; its saved activations are graph-owned static tensors.  Backward:
     the whole reverse schedule, writing every parameter gradient straight into the optimizer's flat
     gradient buffer (``FusedAdam`` slots, fixed addresses); returned to autograd as fresh views.  With a
@@ -111,9 +112,14 @@ class _TrunkGraphs(G.PendingGuard):
         self.cur_gen = 0
 
     def forward(self, x):
+        # the frames are packed to space-to-depth bf16 straight into the graph's static input (one launch before
+        # the replay), not copied as fp32 into a static buffer and packed inside the graph
         if self.fwd is None:
-            self.fwd = G.StaticGraph(lambda xx: trunk_forward(self.trunk, xx, self.training, force_pack=True), [x])
-        feats, saved = self.fwd.replay(x)
+            self.fwd = G.StaticGraph(lambda s: trunk_forward(self.trunk, x, self.training, force_pack=True, s2d=s),
+                                     [s2d_input(x)])
+        s2d = self.fwd.static_in[0]
+        s2d_input(x, s2d)
+        feats, saved = self.fwd.replay(s2d)
         return G.hand_out(feats), saved
 
     @staticmethod
@@ -410,12 +416,25 @@ class _ForcePack:
 
 
 @torch.no_grad()
-def trunk_forward(trunk: ResNet18Trunk, video: torch.Tensor, training: bool, force_pack: bool = False):
+def trunk_forward(trunk: ResNet18Trunk, video: torch.Tensor, training: bool, force_pack: bool = False,
+                  s2d: torch.Tensor = None):
+    """``s2d``: the frames already packed by ``s2d_input`` (``video`` then only gives the shape) -- the captured
+    forward graph takes the packed frames as its static input, so the per-step fp32 frame copy is not needed."""
     with _ForcePack(trunk, force_pack):
-        return _trunk_forward(trunk, video, training)
+        return _trunk_forward(trunk, video, training, s2d)
 
 
-def _trunk_forward(trunk: ResNet18Trunk, video: torch.Tensor, training: bool):
+def s2d_input(video: torch.Tensor, out: torch.Tensor = None) -> torch.Tensor:
+    """fp32 NCHW frames -> the stem's bf16 space-to-depth input [N][H/2+3][W/2+3][S2D_CH] (mer_pack_input_s2d)."""
+    N, C, H, W = video.shape
+    video = video.float().contiguous()
+    if out is None:
+        out = torch.empty(N, H // 2 + 3, W // 2 + 3, S2D_CH, device=video.device, dtype=torch.bfloat16)
+    K.pack_input_s2d(video, out)
+    return out
+
+
+def _trunk_forward(trunk: ResNet18Trunk, video: torch.Tensor, training: bool, s2d: torch.Tensor = None):
     trunk.pack_all(transpose=False)
     N, C, H, W = video.shape
     dev = video.device
@@ -423,8 +442,12 @@ def _trunk_forward(trunk: ResNet18Trunk, video: torch.Tensor, training: bool):
     conv1, bn1 = trunk[0], trunk[1]
     _check_stem(conv1, C, H, W)
     # stem conv 7x7/s2/p3 as a 4x4/s1/p0 conv on the 2x2 space-to-depth frames (K = 256, not 7*7*8)
-    x0 = torch.empty(N, H // 2 + 3, W // 2 + 3, S2D_CH, device=dev, dtype=bf)
-    K.pack_input_s2d(video, x0)
+    if s2d is None:
+        x0 = s2d_input(video)
+    else:
+        if tuple(s2d.shape) != (N, H // 2 + 3, W // 2 + 3, S2D_CH) or s2d.dtype != bf:
+            raise ValueError(f"packed frames {tuple(s2d.shape)} do not match video {tuple(video.shape)}")
+        x0 = s2d
     arena = _StatsArena(trunk, dev, floats=_fwd_stat_floats(trunk, N, H, W)) if training else None
     c1, ms1 = _conv_bn(trunk, conv1, bn1, x0, 1, 0, training, arena, rs=(4, 4))
     Hp, Wp = (c1.shape[1] - 1) // 2 + 1, (c1.shape[2] - 1) // 2 + 1
