@@ -168,3 +168,32 @@ def test_wavlm_attention_vs_torch(L):
     ref = (torch.softmax(s, -1) @ v).transpose(1, 2).reshape(B * L, D)
     err = max_abs(out.float(), ref)
     assert err < 2e-2 * float(ref.abs().max()), err
+
+
+@pytest.mark.parametrize("case", ["noise", "dc_highpass"])
+def test_conv0_groupnorm_moments_vs_torch(case):
+    """conv0 -> GroupNorm(512, 512) -> GELU (statistics from fp64 waveform moments, modeling_wavlm.py
+    feature-extractor layer 0) vs torch fp32 conv1d + group_norm + gelu.  ``dc_highpass``: a large DC offset
+    under zero-sum (high-pass) filters, where E[y^2] - mean^2 cancels -- the case an fp32 Gram would get wrong."""
+    from multimodalemotionrecognition_amd import kernels as K
+    import torch.nn.functional as F
+
+    g = torch.Generator().manual_seed(5)
+    B, S = 3, 16000
+    wav = torch.randn(B, S, generator=g)
+    w = torch.randn(512, 1, 10, generator=g) * 0.3
+    if case == "dc_highpass":
+        wav = wav * 0.01 + 40.0
+        w = w - w.mean(dim=2, keepdim=True)
+    gamma = 1 + 0.1 * torch.randn(512, generator=g)
+    beta = 0.1 * torch.randn(512, generator=g)
+    ref = F.gelu(F.group_norm(F.conv1d(wav[:, None].double(), w.double(), stride=5), 512, gamma.double(),
+                              beta.double(), eps=1e-5)).float().transpose(1, 2)
+    out = torch.empty(B, (S - 10) // 5 + 1, 512, device="cuda", dtype=torch.bfloat16)
+    K.wavlm_conv0_gn_gelu(wav.cuda(), w.reshape(512, 10).contiguous().cuda(), gamma.cuda(), beta.cuda(), out)
+    err = (out.float().cpu() - ref).abs()
+    assert err.max() <= 0.02 * ref.abs().max(), float(err.max())
+    assert rel_rms(out, ref.numpy()) < 4e-3
+    out2 = torch.empty_like(out)
+    K.wavlm_conv0_gn_gelu(wav.cuda(), w.reshape(512, 10).contiguous().cuda(), gamma.cuda(), beta.cuda(), out2)
+    assert torch.equal(out, out2)  # deterministic
