@@ -11,6 +11,10 @@ B = 32
 SHAPES = {
     "conv1 (rows)": (B * 4799, 512, 1536, (4799, 1024, 9599 * 512), B * 9599 * 512),
     "conv2 (rows)": (B * 2399, 512, 1536, (2399, 1024, 4799 * 512), B * 4799 * 512),
+    "conv3 (rows)": (B * 1199, 512, 1536, (1199, 1024, 2399 * 512), B * 2399 * 512),
+    "conv4 (rows)": (B * 599, 512, 1536, (599, 1024, 1199 * 512), B * 1199 * 512),
+    "conv5 (rows)": (B * 299, 512, 1024, (299, 1024, 599 * 512), B * 599 * 512),
+    "conv6 (rows)": (B * 149, 512, 1024, (149, 1024, 299 * 512), B * 299 * 512),
     "qkv": (B * 149, 2304, 768, None, None),
     "ffn1": (B * 149, 3072, 768, None, None),
     "ffn2": (B * 149, 768, 3072, None, None),
@@ -63,7 +67,23 @@ def main():
                 d = float((outs[v] - outs[ref_v]).abs().max()) if v != ref_v else 0.0
                 print(f"{name:14s} M={M:6d} N={N:5d} K={Kd:5d} v{v}: {ms*1e3:8.1f} us {2*M*N*Kd/ms/1e9:7.1f} TF/s  maxdiff_vs_first={d:.3g}",
                       flush=True)
-        if "--blas" in sys.argv and not rows:  # calibration only: the vendor library (hipBLASLt) on the same shape
+        if "--blas" in sys.argv:  # calibration only: the vendor library (hipBLASLt) on the same shape
+            if rows:  # the implicit-GEMM conv shapes: the library on a dense [M, K] operand (its best case)
+                a = (torch.rand(M, Kd, device="cuda") * 2 - 1).bfloat16()
+                out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+                for v in VARIANTS:  # ours on the same dense operand
+                    for _ in range(3):
+                        K.gemm_bf16(a, w, out, variant=v)
+                    torch.cuda.synchronize()
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record()
+                    for _ in range(20):
+                        K.gemm_bf16(a, w, out, variant=v)
+                    e1.record()
+                    torch.cuda.synchronize()
+                    ms = e0.elapsed_time(e1) / 20
+                    print(f"{name:14s} M={M:6d} N={N:5d} K={Kd:5d} v{v} dense: {ms*1e3:8.1f} us "
+                          f"{2*M*N*Kd/ms/1e9:7.1f} TF/s", flush=True)
             wt = w.t()
             for _ in range(3):
                 torch.matmul(a, wt)
