@@ -654,10 +654,12 @@ int launch_pipe(const GemmArgs& g, int out_dtype, hipStream_t st, int groups = 1
 // hides the DMA latency of this 2-deep pipeline, so the 16-wave 256x256 tile wins wherever its grid covers
 // most of the 256 CUs (conv1/conv2 as GEMMs, QKV, FFN-up: 0.80 / 0.82 / 0.49 / 0.64 PF); the 768-column
 // GEMMs have too few such tiles: FFN-down (K = 3072) runs 128x64 tiles with a 3-deep ring, the output
-// projection 128x128 tiles with 8 waves.
+// projection 128x128 tiles with 8 waves.  The 512-column feature-extractor convs below conv1 (300-600 such tiles,
+// 1.2-2.3 rounds of the 256 CUs) run faster on 128x128 tiles: conv2 134 -> 130 us, conv3 79 -> 69 us
+// (profiles/r02f/bench_gemm_convs.log; all variants bit-identical).
 int pick_variant(int M, int N, int K) {
   const long tl = (long)((M + 255) / 256) * ((N + 255) / 256);
-  if (tl >= 160) return 13;
+  if (tl >= 160 && !(N <= 512 && tl < 1200)) return 13;
   return K >= 2048 ? 7 : 9;
 }
 
