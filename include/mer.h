@@ -127,9 +127,10 @@ int mer_softmax_dropout_fwd(int B, int H, int h, int Lq, int Lk, const float* S,
                             float p, const unsigned long long* seed, unsigned long long site, void* stream);
 
 /* nn.CrossEntropyLoss(label_smoothing) (train.py:1033) or, late=1, NLLLoss(log(p+1e-8)) (train.py:212-214),
- * mean over the batch, fused with dloss/dlogits (for dloss = 1).  labels are int64. */
+ * mean over the batch, fused with dloss/dlogits (for dloss = 1).  labels are int64.  preds (nullable): the
+ * per-row top-1 index, first maximum as torch.argmax (train.py:216,220 ``outputs.argmax(dim=1)``). */
 int mer_cross_entropy(int B, int C, const float* logits, const long long* labels, float label_smoothing, int late,
-                      float* loss, float* dlogits, void* stream);
+                      float* loss, float* dlogits, long long* preds, void* stream);
 
 /* state = splitmix64(state + golden): the next step's RNG base, computed on the device (graph-capturable). */
 int mer_rng_advance(unsigned long long* state, void* stream);

@@ -450,15 +450,36 @@ MER_API int mer_mean_pool_bwd(int B, int L, int D, const float* dy, long lddy, f
 // loss = mean_b [(1-eps) * nll_b + eps * mean_c(-logp_bc)];  dlogits = (softmax - q) / B.
 // late mode (train.py:212-214): inputs are probabilities p, loss = NLL(log(p + 1e-8)).
 // ---------------------------------------------------------------------------------------
+__device__ __forceinline__ bool argmax_better(float v, int i, float bv, int bi, int C) {
+  if (i >= C) return false;
+  if (bi >= C) return true;
+  const bool vn = v != v, bn = bv != bv;
+  if (vn != bn) return vn;
+  if (vn) return i < bi;
+  return v > bv || (v == bv && i < bi);
+}
 __global__ __launch_bounds__(256) void ce_kernel(int B, int C, const float* __restrict__ logits,
                                                  const long long* __restrict__ labels, float eps_ls, int late,
-                                                 float* __restrict__ loss, float* __restrict__ dlogits) {
+                                                 float* __restrict__ loss, float* __restrict__ dlogits,
+                                                 long long* __restrict__ preds) {
   __shared__ float part[4];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   float acc = 0.f;
   for (int b = w; b < B; b += 4) {
     const float* z = logits + (long)b * C;
     const long long y = labels[b];
+    if (preds) {  // top-1 as torch.argmax: NaN counts as the maximum, the lowest index wins among equals
+      float bv = 0.f;
+      int bi = C;  // C = no candidate yet
+      for (int c = lane; c < C; c += 64)
+        if (argmax_better(z[c], c, bv, bi, C)) { bv = z[c]; bi = c; }
+      for (int off = 32; off > 0; off >>= 1) {
+        const float ov = __shfl_xor(bv, off);
+        const int oi = __shfl_xor(bi, off);
+        if (argmax_better(ov, oi, bv, bi, C)) { bv = ov; bi = oi; }
+      }
+      if (lane == 0) preds[b] = bi < C ? bi : 0;
+    }
     if (late) {
       for (int c = lane; c < C; c += 64) {
         const float pc = z[c];
@@ -488,9 +509,9 @@ __global__ __launch_bounds__(256) void ce_kernel(int B, int C, const float* __re
   if (threadIdx.x == 0) *loss = (part[0] + part[1] + part[2] + part[3]) / B;
 }
 MER_API int mer_cross_entropy(int B, int C, const float* logits, const long long* labels, float label_smoothing,
-                              int late, float* loss, float* dlogits, void* stream) {
+                              int late, float* loss, float* dlogits, long long* preds, void* stream) {
   hipLaunchKernelGGL(ce_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, B, C, logits, labels, label_smoothing, late,
-                     loss, dlogits);
+                     loss, dlogits, preds);
   MER_LAUNCH_CHECK();
 }
 

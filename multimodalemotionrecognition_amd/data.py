@@ -191,48 +191,87 @@ def load_video_frames(src: FrameSource, num_frames: int = 8, size: int = 112, bb
     return clips.preprocess_frames(dev_frames, size)
 
 
-class ClipLoader:
-    """Batches of (video [B, 8, 3, 112, 112], audio [B, 1, 48000], labels [B]) assembled on the GPU.
+def _collate_meta(metas: List[dict]) -> dict:
+    """default_collate of the reference's per-clip meta dicts (ravdess.py:608-615): one list per key (ints as a
+    tensor, as torch's collate does)."""
+    keys = []
+    for m in metas:
+        keys += [k for k in m if k not in keys]
+    out = {}
+    for k in keys:
+        vals = [m.get(k) for m in metas]
+        out[k] = torch.tensor(vals) if all(isinstance(v, int) and not isinstance(v, bool) for v in vals) else vals
+    return out
 
-    ``items``: (frames source, wav path, label, bbox-or-None) per clip.  Rank ``rank`` of ``world`` takes items
-    ``rank::world`` (disjoint shards, SURVEY 8(e)); ``workers`` threads decode ahead (``prefetch`` batches)."""
+
+def shard_indices(n: int, rank: int, world: int, shuffle: bool, seed: int, epoch: int) -> np.ndarray:
+    """``torch.utils.data.DistributedSampler`` order (drop_last=False): one permutation of ALL items drawn from
+    (seed + epoch) on every rank, padded by wrapping to a multiple of ``world``, then every ``world``-th index from
+    ``rank`` -- every rank sees the same number of items and, across epochs, different clips."""
+    order = np.arange(n)
+    if shuffle:
+        np.random.default_rng(seed + epoch).shuffle(order)
+    total = -(-n // world) * world if n else 0
+    if total > n:
+        reps = -(-(total - n) // n)
+        order = np.concatenate([order] + [order] * reps)[:total]
+    return order[rank:total:world]
+
+
+class ClipLoader:
+    """Batches of ``(video [B, 8, 3, 112, 112], audio [B, 1, 48000], labels [B], meta)`` assembled on the GPU --
+    the 4-tuples of the reference's datasets (ravdess.py:616, 654) that ``train_one_epoch`` unpacks
+    (train.py:200).
+
+    ``items``: ``(frames source, wav path, label[, bbox-or-None[, meta dict]])`` per clip.  Data parallelism:
+    rank ``rank`` of ``world`` takes a ``DistributedSampler``-style shard of one global permutation
+    (``shard_indices``), so all ranks run the same number of steps (a rank with an extra step would block in the
+    gradient all-reduce).  ``workers`` threads decode ahead (``prefetch`` batches).  ``augment``: the reference's
+    train-split audio augmentation (ravdess.py:519-578, bar noise at a drawn SNR; ``bar_noise`` is the 16 kHz
+    track, else Gaussian noise), drawn from a generator seeded per (seed, epoch, item) so the draws do not depend
+    on thread scheduling.  The reference's video augmentation (cv2.GaussianBlur + darken + noise, ravdess.py:
+    366-384) needs cv2, which this image lacks: not applied."""
 
     def __init__(self, items: Sequence[Tuple], batch_size: int = 32, num_frames: int = 8, size: int = 112,
                  sample_rate: int = 16000, duration_sec: float = 3.0, rank: int = 0, world: int = 1,
                  workers: int = 8, prefetch: int = 2, device="cuda", shuffle: bool = False, seed: int = 0,
-                 drop_last: bool = True):
-        self.items = list(items)[rank::world]
+                 drop_last: bool = True, augment: bool = False, bar_noise: Optional[np.ndarray] = None):
+        self.all_items = list(items)
+        self.rank, self.world = int(rank), max(1, int(world))
+        if not 0 <= self.rank < self.world:
+            raise ValueError(f"rank {rank} outside world {world}")
         self.B, self.T, self.size = batch_size, num_frames, size
         self.sr, self.dur = sample_rate, duration_sec
         self.workers, self.prefetch = max(1, workers), max(1, prefetch)
         self.device = torch.device(device)
         self.shuffle, self.seed, self.drop_last = shuffle, seed, drop_last
+        self.augment, self.bar_noise = bool(augment), bar_noise
         self.epoch = 0
 
-    def __len__(self):
-        n = len(self.items)
-        return n // self.B if self.drop_last else -(-n // self.B)
+    @property
+    def items(self):
+        """This rank's items in epoch-0 order."""
+        return [self.all_items[i] for i in shard_indices(len(self.all_items), self.rank, self.world, False, 0, 0)]
 
-    def _decode(self, item):
-        src, wav_path, label = item[0], item[1], item[2]
-        bbox = item[3] if len(item) > 3 else None
-        frames = select_frames(_frames(src), self.T, bbox)
-        wav = load_audio_wav(wav_path, self.sr, self.dur)[0].numpy()
-        return frames, wav, int(label)
+    def num_samples(self) -> int:
+        return -(-len(self.all_items) // self.world) if self.all_items else 0
+
+    def __len__(self):
+        n = self.num_samples()
+        return n // self.B if self.drop_last else -(-n // self.B)
 
     def _assemble(self, decoded):
         # frames of one batch may differ in size (per-clip crops): resize each clip's frames on the device
-        vids = [clips.preprocess_frames(torch.from_numpy(f).to(self.device), self.size) for f, _, _ in decoded]
+        vids = [clips.preprocess_frames(torch.from_numpy(f).to(self.device), self.size) for f, _, _, _ in decoded]
         video = torch.stack(vids).contiguous()
-        audio = clips.pad_crop_waveforms([torch.from_numpy(w) for _, w, _ in decoded], self.sr, self.dur,
+        audio = clips.pad_crop_waveforms([torch.from_numpy(w) for _, w, _, _ in decoded], self.sr, self.dur,
                                          device=self.device)
-        labels = torch.tensor([lab for _, _, lab in decoded], dtype=torch.long).to(self.device)
-        return video, audio, labels
+        labels = torch.tensor([lab for _, _, lab, _ in decoded], dtype=torch.long).to(self.device)
+        return video, audio, labels, _collate_meta([m for _, _, _, m in decoded])
 
     def __iter__(self):
-        order = np.arange(len(self.items))
-        if self.shuffle:
-            np.random.default_rng(self.seed + self.epoch).shuffle(order)
+        order = shard_indices(len(self.all_items), self.rank, self.world, self.shuffle, self.seed, self.epoch)
+        epoch = self.epoch
         self.epoch += 1
         nb = len(self)
         batches = [order[i * self.B:(i + 1) * self.B] for i in range(nb)]
@@ -246,7 +285,7 @@ class ClipLoader:
                     for b in batches:
                         if stop.is_set():
                             return
-                        decoded = list(ex.map(self._decode, [self.items[i] for i in b]))
+                        decoded = list(ex.map(self._decode_epoch(epoch), [(int(i), self.all_items[i]) for i in b]))
                         out_q.put(("ok", decoded))
             except BaseException as e:  # surfaced to the consumer
                 out_q.put(("err", e))
@@ -264,3 +303,17 @@ class ClipLoader:
                 yield self._assemble(val)
         finally:
             stop.set()
+
+    def _decode_epoch(self, epoch):
+        def fn(job):
+            gi, item = job
+            src, wav_path, label = item[0], item[1], item[2]
+            bbox = item[3] if len(item) > 3 else None
+            meta = dict(item[4]) if len(item) > 4 and item[4] is not None else {}
+            meta.setdefault("index", int(gi))
+            frames = select_frames(_frames(src), self.T, bbox)
+            rng = np.random.default_rng([self.seed, epoch, int(gi)]) if self.augment else None
+            wav = load_audio_wav(wav_path, self.sr, self.dur, augment=self.augment, bar_noise=self.bar_noise,
+                                 rng=rng)[0].numpy()
+            return frames, wav, int(label), meta
+        return fn

@@ -51,10 +51,13 @@ def is_dist() -> bool:
 
 
 def cpu_group():
-    """A gloo group over the same ranks for small host-side collectives (created once)."""
+    """A gloo group over the same ranks for small host-side collectives (created once, by every rank at the
+    same point: GradAllReduce's constructor).  Always a group of its OWN, even under a gloo default backend:
+    collectives on one group are matched by issue order, and the early gradient bucket may be issued before
+    (hook fired) or after (hook did not fire) the flag all-reduce on different ranks."""
     global _CPU_GROUP
     if _CPU_GROUP is None:
-        _CPU_GROUP = dist.group.WORLD if dist.get_backend() == "gloo" else dist.new_group(backend="gloo")
+        _CPU_GROUP = dist.new_group(backend="gloo")
     return _CPU_GROUP
 
 
@@ -74,48 +77,77 @@ class GradAllReduce:
     before step 0), and the model's early-gradient hook (``register_grad_ready_hook``) is used to start
     the head + layer4 bucket while the rest of the backward runs.  ``mask_sync``: union the per-parameter
     "has a gradient" flags over ranks (default: ask the model whether some step can leave a trainable
-    parameter without a gradient)."""
+    parameter without a gradient).
+
+    Bucket boundaries never depend on the rank or the step: the early prefix ``[0, E)`` of each flat buffer is
+    fixed at construction from the STATIC set of parameters the hook announces (``model.early_grad_params()``
+    or ``early_params``).  A rank whose hook did not fire this step (gated ModalityDropout dropping the video
+    branch detaches it, so the trunk backward never runs) launches ``[0, E)`` at ``__call__`` with the same
+    chunking, before ``[E, N)``: every rank issues the same sequence of collectives."""
 
     def __init__(self, optimizer, bucket_bytes: int = BUCKET_BYTES, model: Optional[torch.nn.Module] = None,
-                 mask_sync: Optional[bool] = None):
+                 mask_sync: Optional[bool] = None, early_params=None):
         self.opt = optimizer
         self.bucket_bytes = bucket_bytes
         self.world = dist.get_world_size() if is_dist() else 1
         optimizer.grad_scale = 1.0 / self.world
         self._pending = []      # async works launched this step
-        self._done = {}         # group index -> flat elements already launched (prefix)
+        self._done = {}         # group index -> flat elements already launched (the early prefix)
         if mask_sync is None:
             mask_sync = bool(getattr(model, "may_skip_grads", lambda: True)()) if model is not None else True
         self.mask_sync = mask_sync
+        if mask_sync and self.world > 1:
+            cpu_group()
         if model is not None and self.world > 1:
             broadcast_module(model)
             with torch.no_grad():  # re-homed trainables: one broadcast per flat buffer
                 for f in optimizer.flat_params():
                     dist.broadcast(f, 0)
-        if model is not None and hasattr(model, "register_grad_ready_hook"):
+        if early_params is None and model is not None and hasattr(model, "early_grad_params"):
+            early_params = model.early_grad_params()
+        self._early_ids = {id(p) for p in (early_params or [])}
+        self._early_end = self._prefix_ends(self._early_ids)
+        if self._early_end and model is not None and hasattr(model, "register_grad_ready_hook"):
             model.register_grad_ready_hook(self.grads_ready)
+
+    def _prefix_ends(self, ids) -> dict:
+        """Per flat buffer: the end of the longest prefix made of parameters in ``ids`` (0 entries dropped)."""
+        ends, stopped = {}, set()
+        for gi, p, o, n in self.opt.param_slices():
+            if gi in stopped:
+                continue
+            if id(p) in ids:
+                ends[gi] = o + (n + 3) // 4 * 4
+            else:
+                stopped.add(gi)
+        return {gi: e for gi, e in ends.items() if e > 0}
 
     def _launch(self, gi: int, flat: torch.Tensor, lo: int, hi: int) -> None:
         n = max(1, self.bucket_bytes // flat.element_size())
         for a, b in _ranges(lo, hi, n):
             self._pending.append(dist.all_reduce(flat[a:b], op=dist.ReduceOp.SUM, async_op=True))
 
-    def grads_ready(self, params) -> None:
-        """Early hook: ``params`` have their final local gradients in the flat buffers (enqueued on the current
-        stream).  Launches the longest flat-buffer PREFIX made of ready parameters."""
+    @torch.no_grad()
+    def _home_prefix(self) -> None:
+        """Copy any early-prefix gradient autograd produced OUTSIDE the flat buffer into its slot (enqueued before
+        the collective on the same stream), so the early bucket never ships a stale slot that ``gather_grads``
+        would overwrite while RCCL still reads it."""
+        for gi, p, o, n in self.opt.param_slices():
+            if id(p) not in self._early_ids or p.grad is None:
+                continue
+            flat = self.opt.flat_grads()[gi]
+            if p.grad.data_ptr() != flat[o:].data_ptr():
+                flat[o:o + n].view_as(p).copy_(p.grad)
+                p.grad = flat[o:o + n].view_as(p)
+
+    def grads_ready(self, params=None) -> None:
+        """Early hook: the static early prefix has its final local gradients (enqueued on the current stream).
+        Launches ``[0, E)`` of every flat buffer (once per step)."""
         if self.world == 1:
             return
-        ready = {id(p) for p in params}
-        ends, stopped = {}, set()
-        for gi, p, o, n in self.opt.param_slices():
-            if gi in stopped:
-                continue
-            if id(p) in ready:
-                ends[gi] = o + (n + 3) // 4 * 4
-            else:
-                stopped.add(gi)
+        self._home_prefix()
         for gi, flat in enumerate(self.opt.flat_grads()):
-            end, start = ends.get(gi, 0), self._done.get(gi, 0)
+            end, start = self._early_end.get(gi, 0), self._done.get(gi, 0)
             if end > start:
                 self._launch(gi, flat, start, end)
                 self._done[gi] = end
@@ -131,9 +163,11 @@ class GradAllReduce:
             it = iter(flags.tolist())
             self.opt.set_used([[bool(next(it)) for _ in g] for g in used])
         for gi, flat in enumerate(self.opt.flat_grads()):
-            start = self._done.get(gi, 0)
-            if start < flat.numel():
-                self._launch(gi, flat, start, flat.numel())
+            end, start = self._early_end.get(gi, 0), self._done.get(gi, 0)
+            if end > start:  # the hook did not fire on this rank this step: same prefix, same chunking
+                self._launch(gi, flat, start, end)
+            if max(end, start) < flat.numel():
+                self._launch(gi, flat, max(end, start), flat.numel())
         for w in self._pending:
             w.wait()
         self._pending, self._done = [], {}

@@ -509,13 +509,25 @@ class FusionModel(nn.Module):
         wav = getattr(self.audio_model, "wavlm", None)
         return self.mode == "gated" or (wav is not None and wav.trainable())
 
-    def register_grad_ready_hook(self, fn) -> None:
-        """``fn(params)`` is called from the backward as soon as the head's and the ResNet18 layer4 gradients are
-        final (enqueued): the early all-reduce bucket (dist.GradAllReduce)."""
+    def early_grad_params(self):
+        """The parameters whose gradients are final once the ResNet18 backward has enqueued blocks >=
+        ``video.SPLIT_BLOCK``: the fusion head, the video encoder's head and those trunk blocks (a STATIC list:
+        dist.GradAllReduce fixes its early-bucket boundaries from it, identically on every rank)."""
+        from .video import SPLIT_BLOCK
+
         trunk = self.video_model.backbone
+        if not hasattr(trunk, "split_params"):
+            return []
         head = [q for n, q in self.named_parameters() if not n.startswith(("audio_model.", "video_model."))]
         vid_head = [q for n, q in self.video_model.named_parameters() if not n.startswith("backbone.")]
-        trunk.grad_ready_hook = lambda ps: fn(head + vid_head + list(ps))
+        return head + vid_head + list(trunk.split_params(SPLIT_BLOCK))
+
+    def register_grad_ready_hook(self, fn) -> None:
+        """``fn(params)`` is called from the backward as soon as the ``early_grad_params()`` gradients are final
+        (enqueued): the early all-reduce bucket (dist.GradAllReduce)."""
+        trunk = self.video_model.backbone
+        early = self.early_grad_params()
+        trunk.grad_ready_hook = lambda ps: fn(early)
 
     def pop_alignment_loss(self) -> Optional[torch.Tensor]:
         loss = self.alignment_loss

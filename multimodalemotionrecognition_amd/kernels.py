@@ -251,12 +251,14 @@ def gemm_batched(a, b, out, *, M, N, K, sam, sak, bsa, sbk, sbn, bsb, ldc, bsc, 
     return out
 
 
-def cross_entropy(logits, labels, loss, dlogits, label_smoothing=0.0, late=False):
+def cross_entropy(logits, labels, loss, dlogits, label_smoothing=0.0, late=False, preds=None):
     B, C = logits.shape
     if labels.dtype != torch.int64 or labels.numel() != B:
         raise ValueError("labels must be int64 [B]")
+    if preds is not None and (preds.dtype != torch.int64 or preds.numel() != B):
+        raise ValueError("preds must be int64 [B]")
     LIB("mer_cross_entropy", B, C, logits.data_ptr(), labels.data_ptr(), float(label_smoothing), int(late),
-        loss.data_ptr(), _ptr(dlogits), stream_ptr())
+        loss.data_ptr(), _ptr(dlogits), _ptr(preds), stream_ptr())
 
 
 def scale_dev(x, s, y):

@@ -13,12 +13,14 @@ class _CEFn(torch.autograd.Function):
         logits = logits.contiguous().float()
         loss = torch.empty((), device=logits.device, dtype=torch.float32)
         dlogits = torch.empty_like(logits)
-        K.cross_entropy(logits, labels.contiguous(), loss, dlogits, label_smoothing, late)
+        preds = torch.empty(logits.shape[0], device=logits.device, dtype=torch.int64)
+        K.cross_entropy(logits, labels.contiguous(), loss, dlogits, label_smoothing, late, preds=preds)
         ctx.save_for_backward(dlogits)
-        return loss
+        ctx.mark_non_differentiable(preds)
+        return loss, preds
 
     @staticmethod
-    def backward(ctx, gloss):
+    def backward(ctx, gloss, gpreds=None):
         (dlogits,) = ctx.saved_tensors
         out = torch.empty_like(dlogits)
         K.scale_dev(dlogits, gloss.contiguous().float().reshape(1), out)
@@ -26,21 +28,30 @@ class _CEFn(torch.autograd.Function):
 
 
 class CrossEntropyLoss(nn.Module):
-    """``nn.CrossEntropyLoss(label_smoothing=...)`` with mean reduction (train.py:1033)."""
+    """``nn.CrossEntropyLoss(label_smoothing=...)`` with mean reduction (train.py:1033).  The same kernel writes
+    the rows' top-1 indices (``outputs.argmax(dim=1)``, train.py:220) to ``last_preds``."""
 
     def __init__(self, label_smoothing: float = 0.0) -> None:
         super().__init__()
         self.label_smoothing = float(label_smoothing)
+        self.last_preds = None
 
     def forward(self, logits: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
-        return _CEFn.apply(logits, labels, self.label_smoothing, False)
+        loss, self.last_preds = _CEFn.apply(logits, labels, self.label_smoothing, False)
+        return loss
 
 
 class LateNLLLoss(nn.Module):
-    """late-mode loss ``NLLLoss()(log(probs + 1e-8), labels)`` (train.py:1031, 212-214), given probabilities."""
+    """late-mode loss ``NLLLoss()(log(probs + 1e-8), labels)`` (train.py:1031, 212-214), given probabilities;
+    ``last_preds`` = ``outputs.argmax(dim=1)`` (train.py:216)."""
+
+    def __init__(self) -> None:
+        super().__init__()
+        self.last_preds = None
 
     def forward(self, probs: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
-        return _CEFn.apply(probs, labels, 0.0, True)
+        loss, self.last_preds = _CEFn.apply(probs, labels, 0.0, True)
+        return loss
 
 
 class _AddScaledFn(torch.autograd.Function):

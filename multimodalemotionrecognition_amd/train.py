@@ -260,26 +260,39 @@ class TrainStep:
         if self.grad_sync is not None:
             self.grad_sync()
         self.opt.step()
-        return loss.detach(), outputs.detach().argmax(dim=1)
+        preds = getattr(self.loss_fn, "last_preds", None)  # the CE kernel's top-1 (train.py:216,220)
+        if preds is None:
+            raise RuntimeError("TrainStep needs a loss from losses.py (it writes the top-1 predictions)")
+        return loss.detach(), preds
 
 
 def train_one_epoch(model: nn.Module, loader, optimizer: FusedAdam, device: torch.device, loss_fn: nn.Module,
                     fusion_mode: str, fusion_align_weight: float = 0.0,
                     grad_sync: Optional[GradAllReduce] = None) -> Dict[str, float]:
-    """train.py:185-244 (accuracy / macro-F1 computed once at the end, on the host)."""
+    """train.py:185-244 (accuracy / macro-F1 computed once at the end, on the host).
+
+    ``loader`` yields the reference's ``(video, audio, labels, meta)`` batches (ravdess.py:616, 654 through a
+    DataLoader; ``data.ClipLoader`` yields the same); ``(video, audio, labels)`` is accepted too.  One batch of
+    lookahead: the next batch's waveform starts its frozen-encoder forward during this step (TrainStep
+    ``next_audio``), which changes no result."""
     step = TrainStep(model, optimizer, loss_fn, fusion_mode, grad_sync, fusion_align_weight=fusion_align_weight)
     losses, cls_losses, con_losses, preds, targets = [], [], [], [], []
     n = 0
+
+    def unpack(batch):
+        if not isinstance(batch, (tuple, list)) or len(batch) not in (3, 4):
+            raise ValueError("loader batches must be (video, audio, labels[, meta])")
+        return batch[0], batch[1].to(device), batch[2]
+
     it = iter(loader)
     nxt = next(it, None)
+    nxt = unpack(nxt) if nxt is not None else None
     while nxt is not None:
-        video, audio, labels, _ = nxt
-        video, audio, labels = video.to(device), audio.to(device), labels.to(device)
+        video, audio, labels = nxt
+        video, labels = video.to(device), labels.to(device)
         nxt = next(it, None)  # one batch of lookahead: its audio feeds the encoder prefetch
-        nxt_audio = None
-        if nxt is not None:
-            nxt = (nxt[0], nxt[1].to(device), nxt[2], nxt[3])
-            nxt_audio = nxt[1]
+        nxt = unpack(nxt) if nxt is not None else None
+        nxt_audio = nxt[1] if nxt is not None else None
         loss, pred = step(video, audio, labels, next_audio=nxt_audio)
         losses.append(loss * labels.numel())
         cls_l, con_l = step.last_losses

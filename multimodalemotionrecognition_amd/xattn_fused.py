@@ -46,6 +46,12 @@ def supported(cfg, p: Dict[str, torch.Tensor], v_feat: torch.Tensor, a_seq: torc
         return False
     if a_seq.requires_grad:  # the fused forward has no audio-feature gradient path (stage 2 runs unfused)
         return False
+    # the classifier kernels' staging bounds (xh_mlp_fwd: H1 <= 256 hidden units, 4 * C <= 256 class rows;
+    # xh_mlp_bwd: C <= 32): wider heads take the unfused schedule instead of failing the launch
+    n0 = "xattn_mlp.0.weight" if cfg.xattn_head == "concat" else "xattn_gate.0.weight"
+    C = (p["xattn_mlp.3.weight"] if cfg.xattn_head == "concat" else p["xattn_classifier.weight"]).shape[0]
+    if p[n0].shape[0] > 256 or C > 32:
+        return False
     return p["audio_seq_proj.weight"].shape == (128, sd) and p["v_in_proj.weight"].shape == (128, vd)
 
 

@@ -71,3 +71,61 @@ def train_step(p: Dict[str, Tensor], trainable: List[str], opt: AdamRef, video: 
     loss.backward()
     opt.step()
     return float(loss.detach())
+
+
+def encoders_forward(p: Dict[str, Tensor], video: Tensor, audio: Tensor, bn_training: bool = True):
+    """The two encoders' outputs: ResNet18 frame features ``[B, T, 512]`` (video.py:21-23 via ``backbone``) and the
+    frozen WavLM hidden states ``[B, Ta, 768]`` (wavlm_audio.py:165-183, eval semantics, no grad)."""
+    b, t, c, h, w = video.shape
+    vf = resnet18_ref.resnet18_trunk(p, video.reshape(b * t, c, h, w), bn_training,
+                                     prefix="video_model.backbone.").reshape(b, t, -1)
+    with torch.no_grad():
+        hidden = wavlm_ref.wavlm_forward(p, audio, prefix="audio_model.wavlm.")
+    return vf, hidden
+
+
+def audio_encode(p: Dict[str, Tensor], hidden: Tensor, embedding_dim: int = 768) -> Tensor:
+    """``WavLMAudioEncoder.encode`` after ``encode_sequence`` (wavlm_audio.py:146-163): mean temporal pooling, then
+    ``classifier[0]`` only when the pooled width differs from ``embedding_dim`` (not for WavLM-base: 768)."""
+    a_emb = hidden.mean(dim=1)
+    if a_emb.shape[-1] != embedding_dim:
+        a_emb = fusion_ref.linear(a_emb, p, "audio_model.classifier.0")
+    return a_emb
+
+
+def video_encode(vf: Tensor) -> Tensor:
+    """``VideoNet.encode`` after the backbone (video.py:34-40): mean temporal pooling of the frame features."""
+    return vf.mean(dim=1)
+
+
+def embedding_model_forward(p: Dict[str, Tensor], mode: str, video: Tensor, audio: Tensor,
+                            bn_training: bool = True, return_embeddings: bool = False):
+    """``FusionModel.forward`` for the non-xattn modes with the real encoders:
+
+    * ``late`` (fusion.py:358-363): mean of the softmaxes of ``WavLMAudioEncoder.forward`` (wavlm_audio.py:121-144:
+      pool, classifier Linear-ReLU-Dropout-Linear) and ``VideoNet.forward`` (video.py:42-44: encode, Linear) --
+      probabilities;
+    * ``concat`` / ``gated`` (fusion.py:413-435): ``encode`` of both encoders, then the projection + MLP / gate head
+      (dropouts and ModalityDropout identity: the deterministic variant)."""
+    vf, hidden = encoders_forward(p, video, audio, bn_training)
+    a_emb, v_emb = audio_encode(p, hidden), video_encode(vf)
+    if mode == "late":
+        h = torch.relu(fusion_ref.linear(hidden.mean(dim=1), p, "audio_model.classifier.0"))
+        a_logits = fusion_ref.linear(h, p, "audio_model.classifier.3")
+        v_logits = fusion_ref.linear(v_emb, p, "video_model.classifier")
+        out = fusion_ref.late_forward(a_logits, v_logits)
+    else:
+        out = fusion_ref.embedding_fusion_forward(p, mode, a_emb, v_emb)
+    return (out, a_emb, v_emb) if return_embeddings else out
+
+
+def train_step_mode(p: Dict[str, Tensor], trainable: List[str], opt: AdamRef, mode: str, video: Tensor,
+                    audio: Tensor, labels: Tensor) -> float:
+    """One train step (train.py:200-228) of a non-xattn model: CE, or late NLL(log(p + 1e-8))."""
+    for n in trainable:
+        p[n].grad = None
+    out = embedding_model_forward(p, mode, video, audio)
+    loss = fusion_ref.late_nll(out, labels) if mode == "late" else fusion_ref.cross_entropy(out, labels)
+    loss.backward()
+    opt.step()
+    return float(loss.detach())

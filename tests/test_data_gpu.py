@@ -33,8 +33,9 @@ def test_clip_loader_batches_match_oracle(tmp_path):
     loader = D.ClipLoader(items, batch_size=3, workers=3)
     batches = list(loader)
     assert len(batches) == 2
-    for bi, (video, audio, labels) in enumerate(batches):
+    for bi, (video, audio, labels, meta) in enumerate(batches):
         assert tuple(video.shape) == (3, 8, 3, 112, 112) and tuple(audio.shape) == (3, 1, 48000)
+        assert meta["index"].tolist() == list(range(3 * bi, 3 * bi + 3))
         assert video.is_cuda and audio.is_cuda and labels.tolist() == [it[2] for it in items[3 * bi:3 * bi + 3]]
         for j in range(3):
             fp, wp, _, bbox = items[3 * bi + j]
@@ -50,7 +51,7 @@ def test_clip_loader_rank_shards(tmp_path):
     items = _items(tmp_path, 4)
     seen = []
     for rank in range(2):
-        for _, _, labels in D.ClipLoader(items, batch_size=2, rank=rank, world=2, workers=2):
+        for _, _, labels, _ in D.ClipLoader(items, batch_size=2, rank=rank, world=2, workers=2):
             seen += labels.tolist()
     assert sorted(seen) == sorted(it[2] for it in items)
 

@@ -84,10 +84,12 @@ def test_grad_allreduce_world2_gloo():
         assert tmax == 2.0
 
 
-def _worker_early_bucket(rank, world, port, q):
+def _worker_early_bucket(rank, world, port, q, hook_ranks=(0, 1)):
     """A real (CPU autograd) backward: the first layer's grads are announced early through grads_ready (the
-    trunk hook's role), the rest go at __call__; autograd produced every .grad OUTSIDE the flat buffer, so
-    gather_grads must bring them home first.  Every element must be reduced exactly once."""
+    trunk hook's role), the rest go at __call__; autograd produced every .grad OUTSIDE the flat buffer, so the
+    hook itself must bring the prefix home before launching (then gather_grads the rest).  Ranks not in
+    ``hook_ranks`` never see the hook (gated ModalityDropout detaching the video branch): they must issue the
+    same prefix bucket at __call__ -- same boundaries, no hang.  Every element must be reduced exactly once."""
     _env(rank, world, port)
     from multimodalemotionrecognition_amd.dist import GradAllReduce, init_distributed
     from multimodalemotionrecognition_amd.optim import FusedAdam
@@ -97,31 +99,35 @@ def _worker_early_bucket(rank, world, port, q):
         m = _two_layer(0)
         head, tail = list(m[1].parameters()), list(m[0].parameters())
         opt = FusedAdam(head + tail)  # backward order: the last layer first (the early bucket's prefix)
-        ar = GradAllReduce(opt, bucket_bytes=256, mask_sync=True)
-        x = torch.randn(8, 64, generator=torch.Generator().manual_seed(rank))
-        m(x).square().sum().backward()
-        local = [p.grad.clone() for p in head + tail]
-        opt.gather_grads()            # the hook runs mid-backward; here the grads already exist
-        ar.grads_ready(head)          # early bucket: exactly the head prefix
-        early = dict(ar._done)
-        ar()
-        # reference: sum over ranks of the local gradients
-        tot = [t.clone() for t in local]
-        for t in tot:
-            dist.all_reduce(t)
-        ok = all(torch.allclose(p.grad, t, rtol=0, atol=1e-6) for p, t in zip(head + tail, tot))
-        (g,) = opt.flat_grads()
-        ok_flat = all(p.grad.data_ptr() == g[o:].data_ptr() for _, p, o, _ in opt.param_slices())
-        q.put((rank, ok, ok_flat, early.get(0, 0), None))
+        ar = GradAllReduce(opt, bucket_bytes=256, mask_sync=True, early_params=head)
+        early_end = dict(ar._early_end)
+        for it in range(2):
+            opt.zero_grad()
+            x = torch.randn(8, 64, generator=torch.Generator().manual_seed(rank + 10 * it))
+            m(x).square().sum().backward()
+            local = [p.grad.clone() for p in head + tail]
+            if rank in hook_ranks:
+                ar.grads_ready()      # BEFORE gather_grads: the hook homes the prefix itself
+            ar()
+            tot = [t.clone() for t in local]
+            for t in tot:
+                dist.all_reduce(t)
+            ok = all(torch.allclose(p.grad, t, rtol=0, atol=1e-6) for p, t in zip(head + tail, tot))
+            (g,) = opt.flat_grads()
+            ok_flat = all(p.grad.data_ptr() == g[o:].data_ptr() for _, p, o, _ in opt.param_slices())
+            if not (ok and ok_flat):
+                break
+        q.put((rank, ok, ok_flat, early_end.get(0, 0), None))
     finally:
         if dist.is_initialized():
             dist.destroy_process_group()
 
 
-def test_early_bucket_and_gather_world2_gloo():
-    for rank, ok, ok_flat, early, _ in _run(_worker_early_bucket):
+@pytest.mark.parametrize("hook_ranks", [(0, 1), (0,), ()])
+def test_early_bucket_and_gather_world2_gloo(hook_ranks):
+    for rank, ok, ok_flat, early, _ in _run(_worker_early_bucket, 2, hook_ranks):
         assert ok and ok_flat, (rank, ok, ok_flat)
-        # head = Linear(32, 5): weight 160 + bias 5 (padded to 8) = 168 flat elements announced early
+        # head = Linear(32, 5): weight 160 + bias 5 (padded to 8) = 168 flat elements in the early prefix
         assert early == 168, early
 
 

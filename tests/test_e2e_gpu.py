@@ -149,3 +149,51 @@ def test_non_xattn_prefetch_matches_inline(fusion):
         torch.manual_seed(1)
         runs.append([float(step(video, audio, labels, next_audio=audio if prefetch else None)[0]) for _ in range(4)])
     assert runs[0] == runs[1], runs
+
+
+@pytest.fixture(scope="module")
+def c5_oracle():
+    """The C5 workload (BASELINE.json configs[4]): one B=64 batch of 3 s clips through the fp32 oracle in eval
+    mode, fp32 and with the head Linears quantized as quantize_dynamic({nn.Linear}) does (int8_ref)."""
+    p = _oracle_state()
+    video, audio, _ = OP.clip_inputs(64, seed=20261015)
+    video, audio = torch.from_numpy(video), torch.from_numpy(audio)
+    out = {}
+    with torch.no_grad():
+        vf, hidden = train_ref.encoders_forward(p, video, audio, bn_training=False)
+        for int8 in (False, True):
+            q = int8_ref.quantize_params(p, int8_ref.XATTN_INT8["concat"]) if int8 else p
+            logits, _ = fusion_ref.xattn_forward(q, vf, hidden)
+            out[int8] = torch.softmax(logits, dim=1)
+    return p, video, audio, out
+
+
+@pytest.mark.parametrize("int8", [False, True])
+def test_runner_c5_b64_full_clips_vs_oracle(int8, c5_oracle, tmp_path):
+    """C5 at its own workload: inference_worker.py:131-147 -> TorchModelRunner.predict_probs
+    (optimized_runtime.py:95-108) on a [64,8,3,112,112] + [64,1,48000] batch, bf16 encoders and fp32 / INT8 head
+    vs the oracle's forward.  Bars: probabilities 5e-3 (bf16) / 1e-2 (INT8) max-abs; top-1 agreement >= 0.95 of
+    rows (random init gives near-uniform probabilities, so a row whose top-2 gap is below the probability error
+    may flip; rows with a top-2 gap >= 2x the bar must all agree)."""
+    from multimodalemotionrecognition_amd.optimized_runtime import TorchModelRunner, process_batch
+
+    p, video, audio, ref = c5_oracle
+    m = _model(p)
+    ck = {"model": {k: v.cpu() for k, v in m.state_dict().items()}, "val_f1": 0.5,
+          "config": {"fusion": "xattn", "xattn_head": "concat", "use_wavlm": True, "num_classes": 8}}
+    del m
+    r = TorchModelRunner(checkpoint=ck, device="cuda", enable_dynamic_quant=int8)
+    probs = r.predict_probs(video, audio)
+    ref = ref[int8]
+    assert tuple(probs.shape) == (64, 8) and torch.allclose(probs.sum(1), torch.ones(64), atol=1e-5)
+    d = float((probs - ref).abs().max())
+    bar = 1e-2 if int8 else 5e-3
+    agree = float((probs.argmax(1) == ref.argmax(1)).float().mean())
+    top2 = ref.topk(2, dim=1).values
+    clear = (top2[:, 0] - top2[:, 1]) >= 2 * bar
+    print("C5", "int8" if int8 else "bf16", "max|dprob|", d, "top-1 agreement", agree, "clear rows", int(clear.sum()))
+    assert d < bar
+    assert agree >= 0.95
+    assert bool((probs.argmax(1) == ref.argmax(1))[clear].all())
+    rows = process_batch(r, list(video), list(audio))
+    assert [row["top1"]["label"] for row in rows] == [r.labels[i] for i in probs.argmax(1).tolist()]

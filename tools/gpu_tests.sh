@@ -12,7 +12,7 @@ if [ -n "$FILES" ]; then
   echo "FOCUS_EXIT $rc" >> $OUT/focus.log
   grep -E "PASSED|FAILED|ERROR|passed|failed" $OUT/focus.log | tail -30
 fi
-if [ "$3" == "--all" ] && [ $rc -ne 124 ] && [ $rc -ne 137 ]; then
+if [ "$3" == "--all" ] && { [ $rc -eq 0 ] || [ $rc -eq 1 ]; }; then
   timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread > $OUT/all.log 2>&1
   echo "ALL_EXIT $?" >> $OUT/all.log
   tail -15 $OUT/all.log
