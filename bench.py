@@ -58,8 +58,8 @@ PMC_FILE = ROOT / "profiles" / "pmc_traffic.json"
 # (projections 0.703 + FFN 1.406 + attention 0.068; LayerDrop skips ~1.1 of 12 in train mode).
 STEP_GFLOP_PER_CLIP_FIXED = 22.8 + 0.141 + 14.72 + 1.42 + 0.12
 WAVLM_LAYER_GFLOP_PER_CLIP = 0.703 + 1.406 + 0.068
-# the fused xattn head's arithmetic (csrc/xattn_fused*.hip): fp32-class products as three bf16 MFMA passes
-PEAK_SPLIT_TFLOPS = PEAK_BF16_TFLOPS / 3
+# the fused xattn head's arithmetic (csrc/xattn_fused*.hip): fp32-class products as three bf16 MFMA passes, so its
+# MFMA peak is the box's dense bf16 peak / 3 (box_peaks)
 
 
 def head_flop(B=BATCH, T=FRAMES, Ta=149, sd=768, vd=512, d=128, h1=256, c=CLASSES):
@@ -93,6 +93,44 @@ def synthetic_batch(device, seed):
     audio = (0.1 * torch.randn(BATCH, 1, SAMPLES, device=device, generator=g)).clamp_(-1, 1)
     labels = torch.randint(0, CLASSES, (BATCH,), device=device, generator=g)
     return video.contiguous(), audio.contiguous(), labels
+
+
+def box_peaks():
+    """The MI355X's dense MFMA and HBM peaks, from the box itself: compute units and the
+    peak engine clock from rocminfo / the device properties; dense bf16 = CUs x 4 SIMDs x 1,024 FLOP/clk (the
+    v_mfma_f32_32x32x16_bf16 rate, MI355X_MICROARCH.md) x clock.  HBM bandwidth is not reported by the runtime:
+    the 8 TB/s HBM3E spec is used and labelled as such."""
+    import subprocess
+
+    cus, mhz, src = 0, 0.0, []
+    try:
+        prop = torch.cuda.get_device_properties(0)
+        cus = int(prop.multi_processor_count)
+        src.append("torch device properties (CUs)")
+    except Exception:  # noqa: BLE001
+        pass
+    try:
+        txt = subprocess.run(["rocminfo"], capture_output=True, text=True, timeout=30).stdout
+        agent = None
+        for line in txt.splitlines():
+            t = line.strip()
+            if t.startswith("Name:") and "gfx" in t:
+                agent = t.split(":", 1)[1].strip()
+            if agent and t.startswith("Max Clock Freq. (MHz):"):
+                mhz = float(t.split(":", 1)[1].split()[0])
+            if agent and t.startswith("Compute Unit:") and not cus:
+                cus = int(t.split(":", 1)[1].split()[0])
+            if agent and mhz:
+                break
+        if mhz:
+            src.append(f"rocminfo ({agent}: max clock)")
+    except Exception:  # noqa: BLE001
+        pass
+    out = {"cus": cus or None, "max_sclk_mhz": mhz or None, "source": ", ".join(src) or "spec",
+           "bf16_dense_tflops": PEAK_BF16_TFLOPS, "hbm_gbs": PEAK_HBM_GBS, "hbm_source": "HBM3E spec (8 TB/s)"}
+    if cus and mhz:
+        out["bf16_dense_tflops"] = round(cus * 4 * 1024 * mhz * 1e6 / 1e12, 1)
+    return out
 
 
 def cpu_model() -> str:
@@ -197,17 +235,115 @@ def main():
                          "WavLM forward with this step's backward")
     ap.add_argument("--emotion-prior", action="store_true",
                     help="xattn with the emotion-prior attention bias (C4 variant, not the headline config)")
+    ap.add_argument("--c5", action="store_true",
+                    help="BASELINE.json configs[4] instead: the inference_worker batch path (TorchModelRunner."
+                         "predict_probs, B=64 3 s clips) bf16 vs INT8, clips/s, top-1 agreement, B=64 CPU baseline")
     ap.add_argument("--wavlm-unfreeze", type=int, default=0,
                     help="stage-2 fine-tuning step instead (train.py:798-872 two-stage policy): unfreeze the last N "
                          "WavLM layers and the last video block, stage optimizer groups (not the headline config)")
     args = ap.parse_args()
 
     world, rank, local = init_distributed()
+    if args.c5:
+        return _bench_c5(args, world, rank, local)
     if args.stream_priority == "high":
         hi = torch.cuda.Stream(device=local, priority=torch.cuda.Stream.priority_range()[1])
         with torch.cuda.stream(hi):
             return _bench(args, world, rank, local)
     return _bench(args, world, rank, local)
+
+
+def cpu_baseline_c5(threads: int, batch: int = 64, steps: int = 2, warmup: int = 1):
+    """The fp32 CPU oracle of the C5 batch (encoders in eval mode + xattn head + softmax) at B=64."""
+    import statistics
+
+    from oracle import params as OP
+    from oracle import fusion_ref, resnet18_ref, train_ref, wavlm_ref
+
+    torch.set_num_threads(threads)
+    shapes = [("video_model." + n, s) for n, s in resnet18_ref.param_shapes()]
+    shapes += [("audio_model.wavlm." + n, s) for n, s in wavlm_ref.wavlm_param_shapes()]
+    shapes += fusion_ref.xattn_head_param_shapes()
+    p = {k: torch.from_numpy(v) for k, v in OP.init_state(shapes).items()}
+    video, audio, _ = OP.clip_inputs(batch)
+    video, audio = torch.from_numpy(video), torch.from_numpy(audio)
+
+    def run():
+        with torch.no_grad():
+            return torch.softmax(train_ref.model_forward(p, video, audio, bn_training=False), dim=1)
+
+    for _ in range(warmup):
+        run()
+    times = []
+    for _ in range(steps):
+        t = time.perf_counter()
+        run()
+        times.append(time.perf_counter() - t)
+    dt = statistics.median(times)
+    return {"value": round(batch / dt, 3), "unit": "clips/s", "cores": threads, "kind": "port",
+            "cpu_model": cpu_model(), "os_cpu_count": os.cpu_count(),
+            "sample": f"median of {steps} B={batch} fp32 oracle forwards (eval) after {warmup} warm-up "
+                      f"({dt:.2f} s/batch), torch CPU eager, {threads} threads"}
+
+
+def _bench_c5(args, world, rank, local):
+    """BASELINE.json configs[4]: inference_worker.py:131-147 -> TorchModelRunner.predict_probs
+    (optimized_runtime.py:95-108) on B=64 synthetic 3 s clips resident on the GPU; bf16 encoders with the fp32 head
+    vs the INT8 dynamic-quantised Linears; the probabilities' D2H copy (the reference's .cpu()) is inside the
+    timed region.  Replicas only (no collective on the inference path): value = clips of all ranks / max time."""
+    from multimodalemotionrecognition_amd.optimized_runtime import TorchModelRunner
+
+    dev = torch.device("cuda", local)
+    B = 64
+    torch.manual_seed(0)
+    model = build_model(CLASSES, "xattn", pretrained_video=False, use_wavlm=True)
+    ck = {"model": {k: v.detach().cpu() for k, v in model.state_dict().items()}, "val_f1": 0.0,
+          "config": {"fusion": "xattn", "use_wavlm": True, "num_classes": CLASSES}}
+    del model
+    g = torch.Generator(device=dev).manual_seed(20261015 + rank)
+    mean = torch.tensor([0.485, 0.456, 0.406], device=dev).view(1, 1, 3, 1, 1)
+    std = torch.tensor([0.229, 0.224, 0.225], device=dev).view(1, 1, 3, 1, 1)
+    video = ((torch.rand(B, FRAMES, 3, SIZE, SIZE, device=dev, generator=g) - mean) / std).contiguous()
+    audio = (0.1 * torch.randn(B, 1, SAMPLES, device=dev, generator=g)).clamp_(-1, 1).contiguous()
+    res, probs = {}, {}
+    for name, q in (("bf16", False), ("int8", True)):
+        runner = TorchModelRunner(checkpoint=ck, device=str(dev), enable_dynamic_quant=q)
+        for _ in range(args.warmup):
+            runner.predict_probs(video, audio)
+        torch.cuda.synchronize()
+        if is_dist():
+            dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            pr = runner.predict_probs(video, audio)
+        torch.cuda.synchronize()
+        el = torch.tensor([time.perf_counter() - t0], device=dev)
+        if is_dist():
+            dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        el = float(el)
+        probs[name] = pr
+        res[name] = {"clips_per_s": round(world * B * args.steps / el, 1), "ms_per_batch": round(el / args.steps * 1e3, 3)}
+        del runner
+    agree = float((probs["int8"].argmax(1) == probs["bf16"].argmax(1)).float().mean())
+    out = {
+        "metric": "inference_worker batch clips/s (B=64, xattn, bf16 and INT8 Linears)",
+        "value": res["bf16"]["clips_per_s"], "unit": "clips/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": res["bf16"]["ms_per_batch"], "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+        "data": "synthetic (seeded B=64 3 s clips resident in HBM; random-init weights)",
+        "config": {"workload": "TorchModelRunner.predict_probs, ResNet18 + WavLM-base + xattn head (eval)",
+                   "per_gpu_batch": B, "parallelism": f"replicas{world}"},
+        "bf16": res["bf16"], "int8": res["int8"], "top1_agreement_int8_vs_bf16": agree,
+        "max_abs_prob_diff_int8_vs_bf16": round(float((probs["int8"] - probs["bf16"]).abs().max()), 6),
+        "peaks": box_peaks(), "cpu_baseline": None,
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        threads = args.cpu_threads if args.cpu_threads > 0 else cpu_share_threads()
+        out["cpu_baseline"] = cpu_baseline_c5(threads)
+    print(json.dumps(out), flush=True)
+    if is_dist():
+        dist.barrier()
+        dist.destroy_process_group()
 
 
 def _bench(args, world, rank, local):
@@ -265,11 +401,14 @@ def _bench(args, world, rank, local):
     if args.probe_launches > 0:
         time_dominant(model, dev, probe, args.probe_launches)
     kms = probe.avg_ms()
+    peaks = box_peaks()
+    peak_bf16 = peaks["bf16_dense_tflops"]
+    peak_split = peak_bf16 / 3
     roof = None
     if kms:
         achieved = probe.units / (kms * 1e-3) / 1e12
-        roof = {"bound": "mfma", "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": pmc_traffic(),
+        roof = {"bound": "mfma", "achieved": round(achieved, 1), "peak": peak_bf16, "unit": "TFLOP/s",
+                "frac": round(achieved / peak_bf16, 4), "traffic": pmc_traffic(),
                 "kernel": f"{PROBE_KERNEL} (WavLM conv1 implicit GEMM {PROBE[1][0]}x{PROBE[1][1]}x{PROBE[1][2]})",
                 "avg_ms": round(kms, 4), "launches": len(probe.pairs),
                 "measured": f"HIP events around {len(probe.pairs)} standalone launches after the timed region "
@@ -285,9 +424,9 @@ def _bench(args, world, rank, local):
         hbytes = 2 * hprobe.saved_bytes + 3 * 4 * hparams + 4 * BATCH * FRAMES * 512
         hflop = head_flop()
         ai = hflop / hbytes
-        attain = min(PEAK_SPLIT_TFLOPS, ai * PEAK_HBM_GBS / 1e3)
+        attain = min(peak_split, ai * PEAK_HBM_GBS / 1e3)
         ach = hflop / ((fwd_ms + bwd_ms) * 1e-3) / 1e12
-        roof_head = {"bound": "mfma" if PEAK_SPLIT_TFLOPS < ai * PEAK_HBM_GBS / 1e3 else "hbm",
+        roof_head = {"bound": "mfma" if peak_split < ai * PEAK_HBM_GBS / 1e3 else "hbm",
                      "achieved": round(ach, 2), "peak": round(attain, 1), "unit": "TFLOP/s",
                      "frac": round(ach / attain, 4), "traffic": None,
                      "kernel": "fused xattn head fwd+bwd (csrc/xattn_fused.hip F1-F4, xattn_fused_bwd.hip G1-G4 + W)",
@@ -326,6 +465,7 @@ def _bench(args, world, rank, local):
         "step_tflops_achieved": round(step_gflop / 1e3 / (median_ms * 1e-3), 1),
         "roofline": roof,
         "roofline_head": roof_head,
+        "peaks": peaks,
         "cpu_baseline": None,
     }
     if world == 1 and not args.no_cpu_baseline:

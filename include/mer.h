@@ -520,22 +520,23 @@ int mer_xh_audio_fwd(int M, int S, const void* aseq, int aseq_dtype, long ldas, 
 
 /* F2 (one workgroup per sample, T <= 16, Ta <= 160): v2a attention of q1 over kv1, o1 Wo1^T + bo1,
  * v1 = LayerNorm(v + keep_b * v2) (saving the pre-LN sum, mean, rstd), kv2 = v1 Wkv2^T + bkv2,
- * emb[b][0:128] = mean_t v1.  P1 [B][4][T][Ta] receives the pre-dropout probabilities. */
+ * emb[b][0:128] = mean_t v1.  P1 [B][4][T][Ta] receives the pre-dropout probabilities.  bias (nullable): the
+ * emotion-prior attention bias [B][T][Ta] added to every head's scaled scores (fusion.py:390-394 attn_mask). */
 int mer_xh_v2a_fwd(int B, int T, int Ta, const float* v, const float* q1, const float* kv1, const void* Wo1_hi,
                    const void* Wo1_lo, const float* bo1, const float* gamma, const float* beta, const void* Wkv2_hi,
                    const void* Wkv2_lo, const float* bkv2, float attn_p, float path_p, const unsigned long long* seed,
                    unsigned long long site_attn, unsigned long long site_path, float scale, float* P1, float* o1,
                    float* s_v, float* mean_v, float* rstd_v, float* v1, float* kv2, float* emb, long ld_emb,
-                   void* stream);
+                   const float* bias, void* stream);
 
 /* F3 (one workgroup per (sample, 16 query rows)): a2v attention of q2 over kv2 (T keys), o2 Wo2^T + bo2,
  * a1 = LayerNorm(a + keep_b * a2) (pre-LN sum / mean / rstd saved), part[b][tile][128] = column sums of a1 over the
- * tile's rows.  P2 [B][4][Ta][T]. */
+ * tile's rows.  P2 [B][4][Ta][T].  bias (nullable): the emotion-prior a2v bias [B][Ta][T] (fusion.py:391,398). */
 int mer_xh_a2v_fwd(int B, int T, int Ta, const float* q2, const float* kv2, const float* a, const void* Wo2_hi,
                    const void* Wo2_lo, const float* bo2, const float* gamma, const float* beta, float attn_p,
                    float path_p, const unsigned long long* seed, unsigned long long site_attn,
                    unsigned long long site_path, float scale, float* P2, float* o2, float* s_a, float* mean_a,
-                   float* rstd_a, float* part, void* stream);
+                   float* rstd_a, float* part, const float* bias, void* stream);
 
 /* F4: emb[b][128:256] = sum_tiles part / Ta (tile order), then the classifier: concat (gated = 0):
  * h = dropout(relu(emb W0^T + b0)) [B][H1], logits = h W3^T + b3; gated: h [B][H1 = 128], g = sigmoid(h W3^T + b3),
@@ -549,31 +550,35 @@ int mer_xh_mlp_fwd(int B, int Ta, int gated, int H1, int C, const float* part, f
  * xattn_head.py:191-315).  W*T_hi / _lo are the TRANSPOSED split planes ([in][out]).  Gradient buffers are
  * accumulated into (+=); data gradients are written. ---- */
 
-/* G4: the classifier head (concat: h W3 / gated: gate + classifier) -> demb [B][256]; dW0 db0 dW3 db3 (+ dWc dbc
- * gated) accumulated.  Exact fp32 FMA; one launch of 8 workgroups. */
+/* G4: the classifier head's data gradients (fusion.py:404-411 backward; concat: h W3 / gated: gate + classifier),
+ * one workgroup per sample: dh [B][H1] (the gradient at the hidden pre-activation), dz [B] (gated: at the gate
+ * logit) and demb [B][256].  The head's weight / bias gradients (dW0 = dh^T emb, dW3 = dl^T h; gated
+ * dWg3 = dz^T h, dWc = dl^T fused) are problems of mer_xh_wgrad.  Exact fp32 FMA. */
 int mer_xh_mlp_bwd(int B, int C, int H1, int gated, const float* dlogits, const float* emb, const float* h,
-                   const float* g, const float* fused, const float* W0, const float* W3, const float* Wc, float mlp_p,
-                   const unsigned long long* seed, unsigned long long site, float* dW0, float* db0, float* dW3,
-                   float* db3, float* dWc, float* dbc, float* demb, void* stream);
+                   const float* g, const float* W0, const float* W3, const float* Wc, float mlp_p,
+                   const unsigned long long* seed, unsigned long long site, float* dh, float* dz, float* demb,
+                   void* stream);
 
 /* G3 (one workgroup per (sample, 16 query rows)): a-pool + LayerNorm backward -> da (the residual part, [B*Ta][128])
  * and da2 = keep_b * ds; do2 = da2 Wo2; attention backward -> dq2 into dqkv[:, 0:128] ([B*Ta][384]), per-tile
- * dK2 dV2 partials dkv2_part [B][ceil(Ta/16)][16][256], LayerNorm dgamma / dbeta partials ln_part [B*tiles][256]. */
+ * dK2 dV2 partials dkv2_part [B][ceil(Ta/16)][16][256], LayerNorm dgamma / dbeta partials ln_part [B*tiles][256].
+ * dbias (nullable): the prior bias gradient [B][Ta][T] = sum over heads of dS (head order). */
 int mer_xh_a2v_bwd(int B, int T, int Ta, const float* demb, const float* s_a, const float* mean_a, const float* rstd_a,
                    const float* gamma, const float* P2, const float* kv2, const float* q2, const void* WoT2_hi,
                    const void* WoT2_lo, float attn_p, float path_p, const unsigned long long* seed,
                    unsigned long long site_attn, unsigned long long site_path, float scale, float* da, float* da2,
-                   float* dqkv, float* dkv2_part, float* ln_part, void* stream);
+                   float* dqkv, float* dkv2_part, float* ln_part, float* dbias, void* stream);
 
 /* G2 (one workgroup per sample, T <= 16, Ta <= 160): dkv2 = fold(dkv2_part) [B*T][256], dv1 = demb_v / T +
  * dkv2 Wkv2, LayerNorm backward (dv2, ln_part [B][256]), do1 = dv2 Wo1, attention backward -> dq1 [B*T][128],
- * dK1 dV1 into dqkv[:, 128:384], dv [B*T][128] = the LayerNorm-residual part of dv (G1 adds dq1 Wq1). */
+ * dK1 dV1 into dqkv[:, 128:384], dv [B*T][128] = the LayerNorm-residual part of dv (G1 adds dq1 Wq1).
+ * dbias (nullable): the prior bias gradient [B][T][Ta] = sum over heads of dS (head order). */
 int mer_xh_v2a_bwd(int B, int T, int Ta, const float* dkv2_part, const void* WkvT2_hi, const void* WkvT2_lo,
                    const float* demb, const float* s_v, const float* mean_v, const float* rstd_v, const float* gamma,
                    const void* WoT1_hi, const void* WoT1_lo, const float* P1, const float* kv1, const float* q1,
                    float attn_p, float path_p, const unsigned long long* seed, unsigned long long site_attn,
                    unsigned long long site_path, float scale, float* dkv2, float* dv2, float* dq1, float* dv,
-                   float* dqkv, float* ln_part, void* stream);
+                   float* dqkv, float* ln_part, float* dbias, void* stream);
 
 /* G1 (32 rows per workgroup): da += dqkv [Wq2 ; Wkv1] (in place), da_s = da Wa; the trailing ceil(Mv/32)
  * workgroups: dv += dq1 Wq1 (in place), dvfeat = dv Wv [Mv][vdim] (NULL: not wanted). */

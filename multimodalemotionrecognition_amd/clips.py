@@ -43,6 +43,13 @@ def video_clip_batch(frames: torch.Tensor, size: int = 112) -> torch.Tensor:
     return preprocess_frames(frames.reshape(B * T, *frames.shape[2:]), size).view(B, T, 3, size, size)
 
 
+def _h2d(t: torch.Tensor, dev) -> torch.Tensor:
+    """Asynchronous host-to-device copy from a PINNED staging copy: the caching host allocator keeps the pinned
+    block alive until the copy has executed.  (An asynchronous copy straight from a pageable temporary may still be
+    in flight when the temporary is freed and its memory reused -- the device then reads whatever is there.)"""
+    return t.pin_memory().to(dev, non_blocking=True)
+
+
 def pad_crop_waveforms(wavs: Sequence[torch.Tensor], sample_rate: int = 16000, duration_sec: float = 3.0,
                        device=None) -> torch.Tensor:
     """Ragged mono waveforms (1-D fp32, host or device) -> ``[B, 1, target]`` on the GPU, zero-padded at the end or
@@ -60,11 +67,11 @@ def pad_crop_waveforms(wavs: Sequence[torch.Tensor], sample_rate: int = 16000, d
         offsets.append(offsets[-1] + n)
     if not sum(lengths):
         packed = torch.zeros(1, device=dev)
-    elif all(not w.is_cuda for w in flat):  # decoded on the host: one contiguous host buffer, one H2D copy
-        packed = torch.cat(flat).to(dev, non_blocking=True)
+    elif all(not w.is_cuda for w in flat):  # decoded on the host: one contiguous PINNED host buffer, one H2D copy
+        packed = _h2d(torch.cat(flat), dev)
     else:
-        packed = torch.cat([w.to(dev, non_blocking=True) for w in flat])
-    meta = torch.tensor([offsets, lengths], dtype=torch.int64).to(dev, non_blocking=True)
+        packed = torch.cat([w.to(dev) if w.is_cuda else _h2d(w, dev) for w in flat])
+    meta = _h2d(torch.tensor([offsets, lengths], dtype=torch.int64), dev)
     out = torch.empty(len(flat), 1, target, device=dev, dtype=torch.float32)
     K.LIB("mer_wav_pad_crop", len(flat), target, packed.data_ptr(), meta[0].data_ptr(), meta[1].data_ptr(),
           out.data_ptr(), K.stream_ptr())

@@ -15,7 +15,7 @@
 //      drop-path + residual + LayerNorm -> v1 -> [k2 v2] (the a2v key/value projections) + mean-pool of v1
 //   F3 xh_a2v_fwd (grid B * ceil(Ta/16)): MHA of 16 query rows over the sample's T keys -> out-proj ->
 //      drop-path + residual + LayerNorm -> a1, per-tile column sums of a1 (the a-side mean pool)
-//   F4 xh_mlp_fwd (grid ceil(B/4)): a-pool fold, concat MLP (or gated head) -> logits, exact fp32 FMA
+//   F4 xh_mlp_fwd (grid B): a-pool fold, concat MLP (or gated head) -> logits, exact fp32 FMA
 // Every tensor the backward (xattn_head.head_backward) reads is written out with the same layout as the
 // unfused schedule.  Fragment maps (v_mfma_f32_16x16x32_bf16): A lane l = row l&15, k = 8*(l>>4)..+7;
 // B lane l = col l&15, same k; C/D col = l&15, row = 4*(l>>4) + r.
@@ -110,7 +110,7 @@ __global__ __launch_bounds__(256) void xh_audio_fwd_kernel(int M, int S, const T
     zero(acc);
     const int c0 = 32 * w;
     if constexpr (sizeof(TA) == 2) {  // pipelined like mm_aw, F1_D k steps in flight
-      constexpr int F1_D = 4;
+      constexpr int F1_D = 6;
       u4 sa[F1_D][2], sb[F1_D][2][2];
       auto load = [&](int k, u4 (&ra)[2], u4 (&rb)[2][2]) {
 #pragma unroll
@@ -164,29 +164,26 @@ __global__ __launch_bounds__(256) void xh_audio_fwd_kernel(int M, int S, const T
   }
   __syncthreads();
   XT(2, 2);
-  {  // [q2 | k1 v1] = a Wc^T + [bq2 | bkv1]: 384 columns, 96 per wave
+  {  // [q2 | k1 v1] = a Wc^T + [bq2 | bkv1]: 384 columns, 96 per wave in ONE pipelined pass (K = 128: 4 steps)
+    f32x4 acc[2][6];
+    zero(acc);
+    const int c0 = 96 * w;
+    mm_aw<2, 6, 2>(acc, aL, LDA, 32, XD, Wc, XD, c0);
 #pragma unroll
-    for (int half = 0; half < 2; ++half) {
-      f32x4 acc[2][3];
-      zero(acc);
-      const int c0 = 96 * w + 48 * half;
-      mm_aw(acc, aL, LDA, 32, XD, Wc, XD, c0);
+    for (int j = 0; j < 6; ++j) {
+      const int col = c0 + 16 * j + fr;
+      const bool isq = col < XD;
+      const float bv = isq ? bq2[col] : bkv1[col - XD];
 #pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        const int col = c0 + 16 * j + fr;
-        const bool isq = col < XD;
-        const float bv = isq ? bq2[col] : bkv1[col - XD];
+      for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int row = 16 * i + 4 * (lane >> 4) + r;
-            if (row >= rmax) continue;
-            const float v = acc[i][j][r] + bv;
-            if (isq) q2[(r0 + row) * XD + col] = v;
-            else kv1[(r0 + row) * 2 * XD + col - XD] = v;
-          }
-      }
+        for (int r = 0; r < 4; ++r) {
+          const int row = 16 * i + 4 * (lane >> 4) + r;
+          if (row >= rmax) continue;
+          const float v = acc[i][j][r] + bv;
+          if (isq) q2[(r0 + row) * XD + col] = v;
+          else kv1[(r0 + row) * 2 * XD + col - XD] = v;
+        }
     }
   }
   XT(2, 3);
@@ -223,8 +220,41 @@ template <int NT>
 __device__ __forceinline__ void head_attention(int b, int h, int i0, int Lq, int Lk, const float* Qrows, long ldq,
                                                const float* Krows, const float* Vrows, long ldkv, float scale,
                                                float* P, float drop_p, unsigned long long dseed, float* PL, int pld,
-                                               float* oL) {
+                                               float* oL, const float* __restrict__ bias) {
   const int lane = threadIdx.x & 63, fr = lane & 15, fq = lane >> 4, fk = fq * 8;
+  constexpr int KP = 16 * NT;               // keys padded to the tile
+  constexpr int KC = (KP + 31) / 32 * 32;   // PV contracts over KP rounded up to 32
+  // Every global load of the head is issued up front, so the whole attention waits on ONE memory latency: the
+  // K fragments of the NT key tiles and the V column gathers of the PV contraction (raw fp32, split at use).
+  f32x4 kraw[NT][2];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int j = 16 * t + fr;
+    const float* kp = Krows + (long)(j < Lk ? j : Lk - 1) * ldkv + h * XDH + fk;
+    kraw[t][0] = *reinterpret_cast<const f32x4*>(kp);
+    kraw[t][1] = *reinterpret_cast<const f32x4*>(kp + 4);
+  }
+  float vraw[KC / 32][2][8];
+#pragma unroll
+  for (int k = 0; k < KC / 32; ++k)
+#pragma unroll
+    for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int kk = 32 * k + fk + e;
+        vraw[k][jt][e] = Vrows[(long)(kk < Lk ? kk : Lk - 1) * ldkv + h * XDH + 16 * jt + fr];
+      }
+  // the emotion-prior attention bias of this sample (fusion.py:390-398 attn_mask, added after the scaling):
+  // bias[b][i][j], the same for every head
+  float bv[NT][4];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = i0 + 4 * fq + r, j = 16 * t + fr;
+      const long bi = ((long)b * Lq + (i < Lq ? i : Lq - 1)) * Lk + (j < Lk ? j : Lk - 1);
+      bv[t][r] = bias ? bias[bi] : 0.f;
+    }
   // S = Q_h K_h^T: A = Q rows (k = head dims), B[n = key][k] = K rows
   f32x4 s[NT];
 #pragma unroll
@@ -234,9 +264,13 @@ __device__ __forceinline__ void head_attention(int b, int h, int i0, int Lq, int
     frag_row(Qrows + (long)(i0 + fr < Lq ? fr : Lq - 1 - i0) * ldq + h * XDH + fk, i0 + fr < Lq, ah, al);
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
-      const int j = 16 * t + fr;
+      const bool ok = 16 * t + fr < Lk;
+      float x[8] = {kraw[t][0][0], kraw[t][0][1], kraw[t][0][2], kraw[t][0][3],
+                    kraw[t][1][0], kraw[t][1][1], kraw[t][1][2], kraw[t][1][3]};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) x[e] = ok ? x[e] : 0.f;
       bf16x8 bh, bl;
-      frag_row(Krows + (long)(j < Lk ? j : Lk - 1) * ldkv + h * XDH + fk, j < Lk, bh, bl);
+      split8(x, bh, bl);
       s[t] = mma3(ah, al, bh, bl, s[t]);
     }
   }
@@ -248,7 +282,7 @@ __device__ __forceinline__ void head_attention(int b, int h, int i0, int Lq, int
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int j = 16 * t + fr;
-      s[t][r] = j < Lk ? s[t][r] * scale : -INFINITY;
+      s[t][r] = j < Lk ? s[t][r] * scale + bv[t][r] : -INFINITY;
       mx[r] = fmaxf(mx[r], s[t][r]);
     }
 #pragma unroll
@@ -269,7 +303,6 @@ __device__ __forceinline__ void head_attention(int b, int h, int i0, int Lq, int
   for (int r = 0; r < 4; ++r)
 #pragma unroll
     for (int o = 1; o < 16; o <<= 1) sum[r] += __shfl_xor(sum[r], o, 64);
-  constexpr int KP = 16 * NT;  // keys padded to the tile; PV contracts over KP rounded up to 32
 #pragma unroll
   for (int t = 0; t < NT; ++t)
 #pragma unroll
@@ -288,17 +321,19 @@ __device__ __forceinline__ void head_attention(int b, int h, int i0, int Lq, int
     for (int e = lane; e < 16 * 16; e += 64) PL[(e >> 4) * pld + KP + (e & 15)] = 0.f;
   }
   wave_sync_lds();
-  // O_h = P' V_h: A = P' (16 x KP32), B[n = head dim][k = key] = V rows (gathered with stride ldkv)
-  constexpr int KC = (KP + 31) / 32 * 32;
+  // O_h = P' V_h: A = P' (16 x KC), B[n = head dim][k = key] = the preloaded V gathers
   f32x4 o[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
-  for (int k = 0; k < KC; k += 32) {
+  for (int k = 0; k < KC / 32; ++k) {
     bf16x8 ah, al;
-    frag_row(PL + fr * pld + k + fk, true, ah, al);
+    frag_row(PL + fr * pld + 32 * k + fk, true, ah, al);
 #pragma unroll
     for (int jt = 0; jt < 2; ++jt) {
+      float x[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) x[e] = 32 * k + fk + e < Lk ? vraw[k][jt][e] : 0.f;
       bf16x8 bh, bl;
-      frag_col(Vrows + (long)(k + fk) * ldkv + h * XDH + 16 * jt + fr, ldkv, k + fk, Lk, bh, bl);
+      split8(x, bh, bl);
       o[jt] = mma3(ah, al, bh, bl, o[jt]);
     }
   }
@@ -342,7 +377,8 @@ __global__ __launch_bounds__(256) void xh_v2a_fwd_kernel(
     SplitW Wo1, const float* __restrict__ bo1, const float* __restrict__ gamma, const float* __restrict__ beta,
     SplitW Wkv2, const float* __restrict__ bkv2, XhDrop dr, float scale, float* __restrict__ P1,
     float* __restrict__ o1, float* __restrict__ s_v, float* __restrict__ mean_v, float* __restrict__ rstd_v,
-    float* __restrict__ v1, float* __restrict__ kv2, float* __restrict__ emb, long ld_emb) {
+    float* __restrict__ v1, float* __restrict__ kv2, float* __restrict__ emb, long ld_emb,
+    const float* __restrict__ bias) {
   extern __shared__ __attribute__((aligned(16))) float f2smem[];  // F2_LDS_BYTES
   float* vL = f2smem;
   float* qL = vL + 16 * LDA;
@@ -366,7 +402,7 @@ __global__ __launch_bounds__(256) void xh_v2a_fwd_kernel(
   XT(3, 1);
   // attention: wave w = head w, keys = this sample's Ta rows of kv1 (k | v)
   head_attention<F2_KT>(b, w, 0, T, Ta, qL, LDA, kv1 + (long)b * Ta * 2 * XD, kv1 + (long)b * Ta * 2 * XD + XD, 2 * XD,
-                        scale, P1, dr.attn, seed_attn, PL + w * 16 * F2_PLD, F2_PLD, oL);
+                        scale, P1, dr.attn, seed_attn, PL + w * 16 * F2_PLD, F2_PLD, oL, bias);
   __syncthreads();
   XT(3, 2);
   for (int e = threadIdx.x; e < T * XD; e += 256) o1[row0 * XD + e] = oL[(e / XD) * LDA + e % XD];
@@ -405,7 +441,7 @@ MER_API int mer_xh_v2a_fwd(int B, int T, int Ta, const float* v, const float* q1
                            const void* Wkv2_hi, const void* Wkv2_lo, const float* bkv2, float attn_p, float path_p,
                            const unsigned long long* seed, unsigned long long site_attn, unsigned long long site_path,
                            float scale, float* P1, float* o1, float* s_v, float* mean_v, float* rstd_v, float* v1,
-                           float* kv2, float* emb, long ld_emb, void* stream) {
+                           float* kv2, float* emb, long ld_emb, const float* bias, void* stream) {
   if (B <= 0) return 0;
   if (T <= 0 || T > 16 || Ta <= 0 || Ta > 16 * F2_KT) return (int)hipErrorInvalidValue;
   if ((attn_p > 0.f || path_p > 0.f) && !seed) return (int)hipErrorInvalidValue;
@@ -416,7 +452,7 @@ MER_API int mer_xh_v2a_fwd(int B, int T, int Ta, const float* v, const float* q1
   hipLaunchKernelGGL(xh_v2a_fwd_kernel, dim3(B), dim3(256), F2_LDS_BYTES, (hipStream_t)stream, T, Ta, v, q1, kv1,
                      SplitW{(const bf16_t*)Wo1_hi, (const bf16_t*)Wo1_lo}, bo1, gamma, beta,
                      SplitW{(const bf16_t*)Wkv2_hi, (const bf16_t*)Wkv2_lo}, bkv2, dr, scale, P1, o1, s_v, mean_v,
-                     rstd_v, v1, kv2, emb, ld_emb);
+                     rstd_v, v1, kv2, emb, ld_emb, bias);
   MER_LAUNCH_CHECK();
 }
 
@@ -432,7 +468,7 @@ __global__ __launch_bounds__(256) void xh_a2v_fwd_kernel(int T, int Ta, int ntil
                                                          XhDrop dr, float scale, float* __restrict__ P2,
                                                          float* __restrict__ o2, float* __restrict__ s_a,
                                                          float* __restrict__ mean_a, float* __restrict__ rstd_a,
-                                                         float* __restrict__ part) {
+                                                         float* __restrict__ part, const float* __restrict__ bias) {
   __shared__ __attribute__((aligned(16))) float aL[16 * LDA];
   __shared__ __attribute__((aligned(16))) float oL[16 * LDA];
   __shared__ __attribute__((aligned(16))) float tL[16 * LDA];
@@ -444,7 +480,7 @@ __global__ __launch_bounds__(256) void xh_a2v_fwd_kernel(int T, int Ta, int ntil
   const unsigned long long seed_attn = mer_site_seed(dr.seed, dr.site_attn);
   const unsigned long long seed_path = mer_site_seed(dr.seed, dr.site_path);
   head_attention<1>(b, w, i0, Ta, T, q2 + row0 * XD, XD, kv2 + (long)b * T * 2 * XD, kv2 + (long)b * T * 2 * XD + XD,
-                    2 * XD, scale, P2, dr.attn, seed_attn, PL + w * 16 * F3_PLD, F3_PLD, oL);
+                    2 * XD, scale, P2, dr.attn, seed_attn, PL + w * 16 * F3_PLD, F3_PLD, oL, bias);
 #pragma unroll
   for (int e = threadIdx.x; e < 16 * XD; e += 256) {
     const int r = e / XD, c = e - r * XD;
@@ -473,7 +509,7 @@ MER_API int mer_xh_a2v_fwd(int B, int T, int Ta, const float* q2, const float* k
                            const void* Wo2_lo, const float* bo2, const float* gamma, const float* beta, float attn_p,
                            float path_p, const unsigned long long* seed, unsigned long long site_attn,
                            unsigned long long site_path, float scale, float* P2, float* o2, float* s_a, float* mean_a,
-                           float* rstd_a, float* part, void* stream) {
+                           float* rstd_a, float* part, const float* bias, void* stream) {
   if (B <= 0) return 0;
   if (T <= 0 || T > 16 || Ta <= 0) return (int)hipErrorInvalidValue;
   if ((attn_p > 0.f || path_p > 0.f) && !seed) return (int)hipErrorInvalidValue;
@@ -481,19 +517,73 @@ MER_API int mer_xh_a2v_fwd(int B, int T, int Ta, const float* q2, const float* k
   XhDrop dr{attn_p, path_p, seed, site_attn, site_path};
   hipLaunchKernelGGL(xh_a2v_fwd_kernel, dim3(B * ntiles), dim3(256), 0, (hipStream_t)stream, T, Ta, ntiles, q2, kv2,
                      a, SplitW{(const bf16_t*)Wo2_hi, (const bf16_t*)Wo2_lo}, bo2, gamma, beta, dr, scale, P2, o2, s_a,
-                     mean_a, rstd_a, part);
+                     mean_a, rstd_a, part, bias);
   MER_LAUNCH_CHECK();
 }
 
 // ---------------------------------------------------------------------------------------------
-// F4: a-pool fold + classifier head (fusion.py:404-411), 4 samples per workgroup, exact fp32 FMA.
+// F4: a-pool fold + classifier head (fusion.py:404-411), ONE sample per workgroup, exact fp32 FMA.
 //   concat: h = dropout(relu(emb W0^T + b0)), logits = h W3^T + b3
 //   gated:  h = dropout(relu(emb Wg0^T + b)), z = h Wg3^T + b, g = sigmoid(z),
 //           fused = g v_emb + (1 - g) a_emb, logits = fused Wc^T + bc
+// Every product is rows . vector with k across the 64 lanes (each weight row is one coalesced 512 B / 1 KB
+// load per wave, 8 rows in flight per wave), the 8 per-lane partials of a row group reduced by a transposing
+// butterfly (dot_rows8).  The per-sample chain is a handful of dependent L2 round trips; B workgroups.
 // ---------------------------------------------------------------------------------------------
-constexpr int F4_KC = 32;  // W0 k-chunk staged in LDS
 
-__global__ __launch_bounds__(256) void xh_mlp_fwd_kernel(int B, int Ta, int ntiles, int gated, int H1, int C,
+// v[j] (j < 8: partial sums of 8 rows) -> every lane holds the full sum of row 4*b5 + 2*b4 + b3 (lane bits)
+__device__ __forceinline__ float xpose_sum8(float (&v)[8]) {
+  const int lane = threadIdx.x & 63;
+  const bool h5 = lane & 32, h4 = lane & 16, h3 = lane & 8;
+  float u[4], q[2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float send = h5 ? v[i] : v[4 + i];
+    u[i] = (h5 ? v[4 + i] : v[i]) + __shfl_xor(send, 32, 64);
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const float send = h4 ? u[i] : u[2 + i];
+    q[i] = (h4 ? u[2 + i] : u[i]) + __shfl_xor(send, 16, 64);
+  }
+  float r = (h3 ? q[1] : q[0]) + __shfl_xor(h3 ? q[0] : q[1], 8, 64);
+  r += __shfl_xor(r, 4, 64);
+  r += __shfl_xor(r, 2, 64);
+  r += __shfl_xor(r, 1, 64);
+  return r;
+}
+
+// rows [r0, r0 + 8) of W ([nrows][K], row stride ldw) dotted with x (LDS, K floats): returns the sum of row
+// r0 + ((lane >> 3) & 7) in every lane (rows >= nrows read row nrows - 1: callers drop them).  K = 64 * KL.
+template <int KL>
+__device__ __forceinline__ float dot_rows8(const float* __restrict__ W, long ldw, int nrows, int r0, const float* xL) {
+  const int lane = threadIdx.x & 63;
+  float xv[KL];
+#pragma unroll
+  for (int e = 0; e < KL; ++e) xv[e] = xL[KL * lane + e];
+  float v[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int r = r0 + j < nrows ? r0 + j : nrows - 1;
+    const float* wr = W + (long)r * ldw + KL * lane;
+    float wv[KL];
+    if constexpr (KL == 4) {
+      const f32x4 q = *reinterpret_cast<const f32x4*>(wr);
+      wv[0] = q[0]; wv[1] = q[1]; wv[2] = q[2]; wv[3] = q[3];
+    } else {
+#pragma unroll
+      for (int e = 0; e < KL; ++e) wv[e] = wr[e];
+    }
+    float acc = 0.f;
+#pragma unroll
+    for (int e = 0; e < KL; ++e) acc = fmaf(wv[e], xv[e], acc);
+    v[j] = acc;
+  }
+  return xpose_sum8(v);
+}
+
+template <bool GATED>
+__global__ __launch_bounds__(256) void xh_mlp_fwd_kernel(int Ta, int ntiles, int H1, int C,
                                                          const float* __restrict__ part, float* __restrict__ emb,
                                                          const float* __restrict__ W0, const float* __restrict__ b0,
                                                          const float* __restrict__ W3, const float* __restrict__ b3,
@@ -502,110 +592,73 @@ __global__ __launch_bounds__(256) void xh_mlp_fwd_kernel(int B, int Ta, int ntil
                                                          unsigned long long site, float* __restrict__ hsave,
                                                          float* __restrict__ gsave, float* __restrict__ fsave,
                                                          float* __restrict__ logits) {
-  __shared__ float eL[4][2 * XD];
-  __shared__ float hL[4][256];
-  __shared__ float wL[256 * (F4_KC + 1)];  // W0[:, k0 : k0 + 32], row stride 33 (conflict-free column reads)
-  __shared__ float zL[4];
-  const int t = threadIdx.x, s0 = blockIdx.x * 4, w = t >> 6, lane = t & 63;
+  __shared__ __attribute__((aligned(16))) float eL[2 * XD];
+  __shared__ __attribute__((aligned(16))) float hL[256];
+  __shared__ __attribute__((aligned(16))) float fL[XD];
+  __shared__ float zL;
+  const int t = threadIdx.x, b = blockIdx.x, w = t >> 6, lane = t & 63, sub = (lane >> 3) & 7;
   const unsigned long long seed = mer_site_seed(seed_ptr, site);
+  {  // emb = [v-pool (F2) | a-pool = the F3 tile partials folded in tile order / Ta]
+    float val;
+    if (t < XD) {
+      val = emb[(long)b * 2 * XD + t];
+    } else {
+      float acc = 0.f;
 #pragma unroll
-  for (int e = t; e < 4 * 2 * XD; e += 256) {
-    const int s = e / (2 * XD), c = e - s * 2 * XD, bb = s0 + s;
-    float val = 0.f;
-    if (bb < B) {
-      if (c < XD) {
-        val = emb[(long)bb * 2 * XD + c];
-      } else {
-        float acc = 0.f;
-#pragma unroll
-        for (int q = 0; q < F2_KT; ++q) {
-          const float x = part[((long)bb * ntiles + (q < ntiles ? q : ntiles - 1)) * XD + c - XD];
-          acc += q < ntiles ? x : 0.f;
-        }
-        val = acc / Ta;
-        emb[(long)bb * 2 * XD + c] = val;
+      for (int q = 0; q < F2_KT; ++q) {
+        const float x = part[((long)b * ntiles + (q < ntiles ? q : ntiles - 1)) * XD + t - XD];
+        acc += q < ntiles ? x : 0.f;
       }
+      val = acc / Ta;
+      emb[(long)b * 2 * XD + t] = val;
     }
-    eL[s][c] = val;
-  }
-  // h = relu(emb W0^T + b0): thread t = output t for the 4 samples, W0 staged 32 columns at a time; the next
-  // chunk's loads (thread t: column t & 31 of rows t / 32 + 8 i) are in flight while this chunk is consumed
-  float acc[4];
-  for (int s = 0; s < 4; ++s) acc[s] = t < H1 ? b0[t] : 0.f;
-  float pre[256 / 8];
-  auto load = [&](int k0) {
-#pragma unroll
-    for (int i = 0; i < 256 / 8; ++i) {
-      const int r = (t >> 5) + 8 * i;
-      const float x = W0[(long)(r < H1 ? r : H1 - 1) * 2 * XD + k0 + (t & 31)];
-      pre[i] = r < H1 ? x : 0.f;
-    }
-  };
-  load(0);
-  for (int k0 = 0; k0 < 2 * XD; k0 += F4_KC) {
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < 256 / 8; ++i) wL[((t >> 5) + 8 * i) * (F4_KC + 1) + (t & 31)] = pre[i];
-    __syncthreads();
-    if (k0 + F4_KC < 2 * XD) load(k0 + F4_KC);
-    if (t < H1) {
-#pragma unroll 8
-      for (int kk = 0; kk < F4_KC; ++kk) {
-        const float wv = wL[t * (F4_KC + 1) + kk];
-#pragma unroll
-        for (int s = 0; s < 4; ++s) acc[s] = fmaf(eL[s][k0 + kk], wv, acc[s]);
-      }
-    }
-  }
-  if (t < H1) {
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const int bb = s0 + s;
-      float hv = acc[s] > 0.f ? acc[s] : 0.f;
-      if (bb < B) {
-        hv *= dropout_scale(seed, (uint64_t)((long)bb * H1 + t), mlp_p);
-        hsave[(long)bb * H1 + t] = hv;
-      }
-      hL[s][t] = hv;
-    }
+    eL[t] = val;
   }
   __syncthreads();
-  if (!gated) {  // logits: one wave per (sample, class) dot over H1
-    for (int o = w; o < 4 * C; o += 4) {
-      const int s = o / C, c = o - s * C, bb = s0 + s;
-      float a = 0.f;
-      for (int k = lane; k < H1; k += 64) a = fmaf(hL[s][k], W3[(long)c * H1 + k], a);
-      a = wave_sum(a);
-      if (lane == 0 && bb < B) logits[(long)bb * C + c] = a + b3[c];
+  // h = dropout(relu(emb W0^T + b0)): wave w takes the 8-row groups w, w + 4, ...
+  for (int g = w; 8 * g < H1; g += 4) {
+    const float s = dot_rows8<4>(W0, 2 * XD, H1, 8 * g, eL);
+    const int r = 8 * g + sub;
+    if ((lane & 7) == 0 && r < H1) {
+      float hv = s + b0[r];
+      hv = (hv > 0.f ? hv : 0.f) * dropout_scale(seed, (uint64_t)((long)b * H1 + r), mlp_p);
+      hL[r] = hv;
+      hsave[(long)b * H1 + r] = hv;
+    }
+  }
+  for (int r = H1 + t; r < 256; r += 256) hL[r] = 0.f;  // (H1 % 4 == 0: the k-split reads whole float4)
+  __syncthreads();
+  if constexpr (!GATED) {  // logits = h W3^T + b3
+    for (int g = w; 8 * g < C; g += 4) {
+      const float s = dot_rows8<4>(W3, H1, C, 8 * g, hL);
+      const int c = 8 * g + sub;
+      if ((lane & 7) == 0 && c < C) logits[(long)b * C + c] = s + b3[c];
     }
     return;
-  }
-  {  // z = h Wg3^T + b (one output per sample, wave s), g = sigmoid(z)
-    const int s = w, bb = s0 + s;
-    float a = 0.f;
-    for (int k = lane; k < H1; k += 64) a = fmaf(hL[s][k], W3[k], a);
-    a = wave_sum(a) + b3[0];
-    const float g = 1.f / (1.f + expf(-a));
-    if (lane == 0) {
-      zL[s] = g;
-      if (bb < B) gsave[bb] = g;
+  } else {
+    if (w == 0) {  // z = h Wg3^T + b, g = sigmoid(z)
+      float a = 0.f;
+      for (int k = lane; k < H1; k += 64) a = fmaf(hL[k], W3[k], a);
+      a = wave_sum(a) + b3[0];
+      if (lane == 0) {
+        const float gv = 1.f / (1.f + expf(-a));
+        zL = gv;
+        gsave[b] = gv;
+      }
     }
-  }
-  __syncthreads();
-  for (int e = t; e < 4 * XD; e += 256) {
-    const int s = e / XD, c = e - s * XD, bb = s0 + s;
-    const float g = zL[s];
-    const float f = g * eL[s][c] + (1.f - g) * eL[s][XD + c];
-    hL[s][c] = f;  // h no longer needed
-    if (bb < B) fsave[(long)bb * XD + c] = f;
-  }
-  __syncthreads();
-  for (int o = w; o < 4 * C; o += 4) {
-    const int s = o / C, c = o - s * C, bb = s0 + s;
-    float a = 0.f;
-    for (int k = lane; k < XD; k += 64) a = fmaf(hL[s][k], Wc[(long)c * XD + k], a);
-    a = wave_sum(a);
-    if (lane == 0 && bb < B) logits[(long)bb * C + c] = a + bc[c];
+    __syncthreads();
+    if (t < XD) {
+      const float gv = zL;
+      const float f = gv * eL[t] + (1.f - gv) * eL[XD + t];
+      fL[t] = f;
+      fsave[(long)b * XD + t] = f;
+    }
+    __syncthreads();
+    for (int g = w; 8 * g < C; g += 4) {  // logits = fused Wc^T + bc
+      const float s = dot_rows8<2>(Wc, XD, C, 8 * g, fL);
+      const int c = 8 * g + sub;
+      if ((lane & 7) == 0 && c < C) logits[(long)b * C + c] = s + bc[c];
+    }
   }
 }
 
@@ -614,10 +667,15 @@ MER_API int mer_xh_mlp_fwd(int B, int Ta, int gated, int H1, int C, const float*
                            float mlp_p, const unsigned long long* seed, unsigned long long site, float* hsave,
                            float* gsave, float* fsave, float* logits, void* stream) {
   if (B <= 0) return 0;
-  if (H1 <= 0 || H1 > 256 || C <= 0 || 4 * C > 256 || Ta > 16 * F2_KT || (mlp_p > 0.f && !seed))
+  if (H1 <= 0 || H1 > 256 || H1 % 4 || C <= 0 || C > 32 || Ta > 16 * F2_KT || (mlp_p > 0.f && !seed))
     return (int)hipErrorInvalidValue;
-  if (gated && (!Wc || !bc || !gsave || !fsave || H1 > 256)) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(xh_mlp_fwd_kernel, dim3((B + 3) / 4), dim3(256), 0, (hipStream_t)stream, B, Ta, (Ta + 15) / 16,
-                     gated, H1, C, part, emb, W0, b0, W3, b3, Wc, bc, mlp_p, seed, site, hsave, gsave, fsave, logits);
+  if (gated && (!Wc || !bc || !gsave || !fsave)) return (int)hipErrorInvalidValue;
+  const int ntiles = (Ta + 15) / 16;
+  if (gated)
+    hipLaunchKernelGGL(xh_mlp_fwd_kernel<true>, dim3(B), dim3(256), 0, (hipStream_t)stream, Ta, ntiles, H1, C, part,
+                       emb, W0, b0, W3, b3, Wc, bc, mlp_p, seed, site, hsave, gsave, fsave, logits);
+  else
+    hipLaunchKernelGGL(xh_mlp_fwd_kernel<false>, dim3(B), dim3(256), 0, (hipStream_t)stream, Ta, ntiles, H1, C, part,
+                       emb, W0, b0, W3, b3, Wc, bc, mlp_p, seed, site, hsave, gsave, fsave, logits);
   MER_LAUNCH_CHECK();
 }

@@ -1,7 +1,7 @@
 // Fused xattn head backward: the reverse of xattn_fused.hip (fusion.py:366-411 + the two nn.MultiheadAttention
 // blocks, TORCH:6576-6606) on split-bf16 MFMA.  Four data-gradient launches plus one grouped weight-gradient
 // launch and its fixed-order fold replace the ~25 backward launches of xattn_head.head_backward:
-//   G4 xh_mlp_bwd   (grid 16): classifier head -> demb; the head's own weight gradients (exact fp32 FMA)
+//   G4 xh_mlp_bwd   (grid B): classifier head -> dh (dz), demb (exact fp32 FMA); its weight gradients go to W
 //   G3 xh_a2v_bwd   (grid B * ceil(Ta/16)): a-pool / LayerNorm / out-proj / attention backward of 16 query rows
 //                   -> da (LN residual part), da2, dq2, per-tile partials of dK2 dV2 and of dgamma / dbeta
 //   G2 xh_v2a_bwd   (grid B): dK2 dV2 fold -> dv1 -> LayerNorm / out-proj / attention backward over the
@@ -57,222 +57,117 @@ __device__ __forceinline__ void ln_part_store(float g0, float g1, float b0, floa
 }  // namespace
 
 // ---------------------------------------------------------------------------------------------
-// G4: classifier head backward, chunks of 32 samples, 16 workgroups.  Every workgroup stages the chunk's emb,
-// h and dlogits in LDS and recomputes dh (B x H1, cheap); workgroup k owns the 16 emb columns
-// [16k, 16k + 16): dW0[:, slice] and demb[:, slice]; the small weights and the biases are spread over all
-// 4096 threads (one owner per output, so the += is race-free).  Unfused: xattn_head.py:207-225.
+// G4: classifier head backward, ONE sample per workgroup (the data gradients only; the head's weight and bias
+// gradients dW0 = dh^T emb, dW3 = dl^T h (gated: dWg3 = dz^T h, dWc = dl^T fused) are problems of the grouped
+// W launch, which runs after G1).  Unfused: xattn_head.py:207-225.
+//   concat: dh = relu' . dropout' . (dl W3),                   demb = dh W0
+//   gated:  dfused = dl Wc, dz = sum_c dfused (v - a) g (1 - g), dh = relu' . dropout' . dz Wg3,
+//           demb = dh Wg0 + [g dfused | (1 - g) dfused]
+// demb = W0^T dh runs with the 256 emb columns across the lanes (one coalesced 1 KB row load per wave and row,
+// 16 rows in flight) and the rows split over the 4 waves, folded in wave order.  Exact fp32 FMA.
 // ---------------------------------------------------------------------------------------------
-constexpr int G4_SLICE = 16;
-constexpr int G4_BLOCKS = 2 * XD / G4_SLICE;
-constexpr int G4_CHUNK = 32;
-constexpr int G4_MAXH = 256, G4_MAXC = 32;
-constexpr int G4_DHLD = G4_MAXH + 1;
-constexpr size_t G4_LDS_FLOATS = G4_CHUNK * 2 * XD + G4_CHUNK * G4_MAXH + G4_CHUNK * G4_DHLD + G4_MAXH * G4_SLICE +
-                                 G4_CHUNK * (XD + 1) + G4_CHUNK * G4_MAXC + G4_MAXC * XD;
-
-__global__ __launch_bounds__(256) void xh_mlp_bwd_kernel(int B, int C, int H1, int gated, const float* __restrict__ dl,
+template <bool GATED>
+__global__ __launch_bounds__(256) void xh_mlp_bwd_kernel(int C, int H1, const float* __restrict__ dl,
                                                          const float* __restrict__ emb, const float* __restrict__ h,
-                                                         const float* __restrict__ gsave,
-                                                         const float* __restrict__ fsave, const float* __restrict__ W0,
+                                                         const float* __restrict__ gsave, const float* __restrict__ W0,
                                                          const float* __restrict__ W3, const float* __restrict__ Wc,
                                                          float mlp_p, const unsigned long long* __restrict__ seed_ptr,
-                                                         unsigned long long site, float* __restrict__ dW0,
-                                                         float* __restrict__ db0, float* __restrict__ dW3,
-                                                         float* __restrict__ db3, float* __restrict__ dWc,
-                                                         float* __restrict__ dbc, float* __restrict__ demb) {
-  extern __shared__ float g4smem[];
-  float* eL = g4smem;                     // [32][256]  emb chunk
-  float* hL = eL + G4_CHUNK * 2 * XD;     // [32][H1]   h chunk (post-dropout)
-  float* dhL = hL + G4_CHUNK * G4_MAXH;   // [32][G4_DHLD]
-  float* w0s = dhL + G4_CHUNK * G4_DHLD;  // [H1][16]   W0[:, slice]
-  float* dfz = w0s + G4_MAXH * G4_SLICE;  // [32][129]  gated: dfused, dz (col 128)
-  float* dlL = dfz + G4_CHUNK * (XD + 1); // [32][C]
-  float* wcL = dlL + G4_CHUNK * G4_MAXC;  // [C][128]   gated: Wc
-  const int t = threadIdx.x, k = blockIdx.x, j0 = k * G4_SLICE, w = t >> 6, lane = t & 63;
-  const int gt = k * 256 + t, nthreads = G4_BLOCKS * 256;
+                                                         unsigned long long site, float* __restrict__ dh_out,
+                                                         float* __restrict__ dz_out, float* __restrict__ demb) {
+  __shared__ float dlL[32];
+  __shared__ __attribute__((aligned(16))) float dhL[256];
+  __shared__ float dfL[XD];
+  __shared__ float red[4][2 * XD];
+  __shared__ float dzL;
+  const int t = threadIdx.x, b = blockIdx.x, w = t >> 6, lane = t & 63;
   const unsigned long long seed = mer_site_seed(seed_ptr, site);
-  XT(0, 0);
-  // Staging copies: float4, clamped loads and UNCONDITIONAL LDS stores (the arrays have room for whole
-  // 256-vector rounds), so no load is sunk into a per-lane branch and each round's loads are in flight together.
-  // (One workgroup per CU: nothing else hides a latency, so every phase keeps many independent loads / FMAs
-  // in flight per thread.)
-  {
-    const int n4 = H1 * G4_SLICE / 4;  // W0[:, slice]: 4 float4 per row
-#pragma unroll
-    for (int i = 0; i < G4_MAXH * G4_SLICE / 4 / 256; ++i) {
-      const int e = t + 256 * i, ec = e < n4 ? e : n4 - 1;
-      reinterpret_cast<f32x4*>(w0s)[e] = *reinterpret_cast<const f32x4*>(W0 + (long)(ec / 4) * 2 * XD + j0 + 4 * (ec % 4));
-    }
-  }
-  if (gated) {
-#pragma unroll 8
-    for (int i = 0; i < (C * XD + 255) / 256; ++i) {
-      const int e = t + 256 * i;
-      wcL[e] = Wc[e < C * XD ? e : C * XD - 1];
-    }
-  }
-  float w3r[G4_MAXC];  // concat: column t of W3 (W3[q][t], q < C, zero beyond); gated: W3[0][t]
-#pragma unroll
-  for (int q = 0; q < G4_MAXC; ++q) {
-    const int qc = q < C ? q : C - 1, cc = t < H1 ? t : H1 - 1;
-    const float x = gated ? W3[cc] : W3[(long)qc * H1 + cc];
-    w3r[q] = q < C ? x : 0.f;
-  }
-#pragma unroll
-  for (int i = 0; i < G4_CHUNK * G4_MAXC / 256; ++i) dlL[t + 256 * i] = 0.f;  // classes >= C stay zero
-  for (int c0 = 0; c0 < B; c0 += G4_CHUNK) {
-    const int nb = B - c0 < G4_CHUNK ? B - c0 : G4_CHUNK;
-    __syncthreads();
-    {
-      const int ne = nb * 2 * XD / 4, nh = nb * H1 / 4;
-#pragma unroll
-      for (int i = 0; i < G4_CHUNK * 2 * XD / 4 / 256; ++i) {
-        const int e = t + 256 * i;
-        reinterpret_cast<f32x4*>(eL)[e] = *reinterpret_cast<const f32x4*>(emb + (long)c0 * 2 * XD + 4 * (e < ne ? e : ne - 1));
-      }
-#pragma unroll
-      for (int i = 0; i < G4_CHUNK * G4_MAXH / 4 / 256; ++i) {
-        const int e = t + 256 * i;
-        reinterpret_cast<f32x4*>(hL)[e] = *reinterpret_cast<const f32x4*>(h + (long)c0 * H1 + 4 * (e < nh ? e : nh - 1));
-      }
-    }
-    for (int e = t; e < nb * C; e += 256) dlL[(e / C) * G4_MAXC + e % C] = dl[(long)c0 * C + e];
-    __syncthreads();
-    XT(0, 1);
-    if (gated) {
-      for (int e = t; e < nb * XD; e += 256) {  // dfused = dlogits Wc
-        const int b = e / XD, c = e - b * XD;
-        float acc = 0.f;
-        for (int q = 0; q < C; ++q) acc = fmaf(dlL[b * G4_MAXC + q], wcL[q * XD + c], acc);
-        dfz[b * (XD + 1) + c] = acc;
-      }
-      __syncthreads();
-      for (int b = w; b < nb; b += 4) {  // dz = sum_c dfused (v - a) g (1 - g)
-        const float* er = eL + b * 2 * XD;
-        const float* dr = dfz + b * (XD + 1);
-        const float s = wave_sum(dr[lane] * (er[lane] - er[XD + lane]) + dr[64 + lane] * (er[64 + lane] - er[XD + 64 + lane]));
-        const float g = gsave[c0 + b];
-        if (lane == 0) dfz[b * (XD + 1) + XD] = s * g * (1.f - g);
-      }
-      __syncthreads();
-    }
-    if (t < H1) {  // dh[b][t] = relu' . dropout' . (dlogits W3 | dz W3), thread = column
-      for (int b = 0; b < nb; ++b) {
-        float acc = 0.f;
-        if (gated) {
-          acc = dfz[b * (XD + 1) + XD] * w3r[0];
-        } else {  // all G4_MAXC classes, branch-free (zero beyond C on both sides)
-          const f32x4* d4 = reinterpret_cast<const f32x4*>(dlL + b * G4_MAXC);
-#pragma unroll
-          for (int q4 = 0; q4 < G4_MAXC / 4; ++q4) {
-            const f32x4 dv = d4[q4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) acc = fmaf(dv[u], w3r[4 * q4 + u], acc);
-          }
-        }
-        dhL[b * G4_DHLD + t] =
-            hL[b * H1 + t] > 0.f ? acc * dropout_scale(seed, (uint64_t)((long)(c0 + b) * H1 + t), mlp_p) : 0.f;
-      }
-    }
-    __syncthreads();
-    XT(0, 2);
-    {  // dW0[r][j0 + c] += sum_b dh[b][r] emb[b][j0 + c]: c = t & 15, rows r = t / 16 + 16 u (16 accumulators)
-      const int c = t & 15, rb = t >> 4;
-      float acc[G4_MAXH / 16];
-#pragma unroll
-      for (int u = 0; u < G4_MAXH / 16; ++u) acc[u] = 0.f;
-      for (int b = 0; b < nb; ++b) {
-        const float ev = eL[b * 2 * XD + j0 + c];
-#pragma unroll
-        for (int u = 0; u < G4_MAXH / 16; ++u) acc[u] = fmaf(dhL[b * G4_DHLD + rb + 16 * u], ev, acc[u]);
-      }
-      float old[G4_MAXH / 16];
-#pragma unroll
-      for (int u = 0; u < G4_MAXH / 16; ++u) {
-        const int r = rb + 16 * u;
-        old[u] = dW0[(long)(r < H1 ? r : H1 - 1) * 2 * XD + j0 + c];
-      }
-#pragma unroll
-      for (int u = 0; u < G4_MAXH / 16; ++u) {
-        const int r = rb + 16 * u;
-        if (r < H1) dW0[(long)r * 2 * XD + j0 + c] = old[u] + acc[u];
-      }
-    }
-    XT(0, 3);
-    {  // demb[b][j] = sum_r dh[b][r] W0[r][j] (+ the gate mix): c = t & 15, samples t / 16 and t / 16 + 16
-      const int c = t & 15, b0 = t >> 4, b1 = b0 + 16, j = j0 + c;
-      float a0[4] = {0.f, 0.f, 0.f, 0.f}, a1[4] = {0.f, 0.f, 0.f, 0.f};
-      for (int r = 0; r < H1; r += 4) {
-#pragma unroll
-        for (int v = 0; v < 4; ++v) {
-          const float wv = w0s[(r + v) * G4_SLICE + c];
-          a0[v] = fmaf(dhL[b0 * G4_DHLD + r + v], wv, a0[v]);
-          a1[v] = fmaf(dhL[b1 * G4_DHLD + r + v], wv, a1[v]);
-        }
-      }
-#pragma unroll
-      for (int half = 0; half < 2; ++half) {
-        const int b = half ? b1 : b0;
-        const float* av = half ? a1 : a0;
-        float acc = (av[0] + av[1]) + (av[2] + av[3]);
-        if (b < nb) {
-          if (gated) {
-            const float g = gsave[c0 + b];
-            acc += j < XD ? dfz[b * (XD + 1) + j] * g : dfz[b * (XD + 1) + j - XD] * (1.f - g);
-          }
-          demb[(long)(c0 + b) * 2 * XD + j] = acc;
-        }
-      }
-    }
-    XT(0, 4);
-    // the small weights and biases, spread over the grid: [db0 | db3 or dbc | dW3 | dWc (gated) | db3 (gated)]
-    const int n_w3 = gated ? H1 : C * H1, n_wc = gated ? C * XD : 0;
-    const int total = H1 + C + n_w3 + n_wc + (gated ? 1 : 0);
-    for (int e = gt; e < total; e += nthreads) {
+  if (t < C) dlL[t] = dl[(long)b * C + t];
+  __syncthreads();
+  float gv = 0.f;
+  if constexpr (GATED) {
+    gv = gsave[b];
+    if (t < XD) {  // dfused = dl Wc  ([C][128])
       float acc = 0.f;
-      if (e < H1) {
-        for (int b = 0; b < nb; ++b) acc += dhL[b * G4_DHLD + e];
-        db0[e] += acc;
-      } else if (e < H1 + C) {
-        const int q = e - H1;
-        for (int b = 0; b < nb; ++b) acc += dlL[b * G4_MAXC + q];
-        (gated ? dbc : db3)[q] += acc;
-      } else if (e < H1 + C + n_w3) {
-        const int i = e - H1 - C;
-        if (gated) {
-          for (int b = 0; b < nb; ++b) acc = fmaf(dfz[b * (XD + 1) + XD], hL[b * H1 + i], acc);
-        } else {
-          const int q = i / H1, c = i - q * H1;
-          for (int b = 0; b < nb; ++b) acc = fmaf(dlL[b * G4_MAXC + q], hL[b * H1 + c], acc);
-        }
-        dW3[i] += acc;
-      } else if (e < H1 + C + n_w3 + n_wc) {
-        const int i = e - H1 - C - n_w3, q = i / XD, c = i - q * XD;
-        for (int b = 0; b < nb; ++b) acc = fmaf(dlL[b * G4_MAXC + q], fsave[(long)(c0 + b) * XD + c], acc);
-        dWc[i] += acc;
+      for (int q = 0; q < C; ++q) acc = fmaf(dlL[q], Wc[(long)q * XD + t], acc);
+      dfL[t] = acc;
+    }
+    __syncthreads();
+    if (w < 2) {  // dz over the 128 columns (waves 0, 1), folded in wave order
+      const int c = 64 * w + lane;
+      const float x = dfL[c] * (emb[(long)b * 2 * XD + c] - emb[(long)b * 2 * XD + XD + c]);
+      const float s = wave_sum(x);
+      if (lane == 0) red[0][w] = s;
+    }
+    __syncthreads();
+    if (t == 0) {
+      const float dz = (red[0][0] + red[0][1]) * gv * (1.f - gv);
+      dzL = dz;
+      dz_out[b] = dz;
+    }
+    __syncthreads();
+  }
+  // dh (thread = hidden unit); h is the saved post-dropout activation: relu' . dropout' = (h > 0) * mask scale
+  for (int r = t; r < 256; r += 256) {
+    float dhv = 0.f;
+    if (r < H1) {
+      float acc;
+      if constexpr (GATED) {
+        acc = dzL * W3[r];
       } else {
-        for (int b = 0; b < nb; ++b) acc += dfz[b * (XD + 1) + XD];
-        db3[0] += acc;
+        acc = 0.f;
+        for (int q = 0; q < C; ++q) acc = fmaf(dlL[q], W3[(long)q * H1 + r], acc);
+      }
+      const float hv = h[(long)b * H1 + r];
+      dhv = hv > 0.f ? acc * dropout_scale(seed, (uint64_t)((long)b * H1 + r), mlp_p) : 0.f;
+      dh_out[(long)b * H1 + r] = dhv;
+    }
+    dhL[r] = dhv;
+  }
+  __syncthreads();
+  {  // demb partial of this wave's rows: column 4 * lane .. + 3
+    const int per = (H1 + 3) / 4, r0 = w * per, r1 = r0 + per < H1 ? r0 + per : H1;
+    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+    constexpr int U = 16;
+    for (int rb = r0; rb < r1; rb += U) {
+      f32x4 wv[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int r = rb + u < r1 ? rb + u : r1 - 1;
+        wv[u] = *reinterpret_cast<const f32x4*>(W0 + (long)r * 2 * XD + 4 * lane);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const float d = rb + u < r1 ? dhL[rb + u] : 0.f;
+        acc[0] = fmaf(d, wv[u][0], acc[0]);
+        acc[1] = fmaf(d, wv[u][1], acc[1]);
+        acc[2] = fmaf(d, wv[u][2], acc[2]);
+        acc[3] = fmaf(d, wv[u][3], acc[3]);
       }
     }
+    *reinterpret_cast<f32x4*>(&red[w][4 * lane]) = acc;
   }
-  XT(0, 5);
+  __syncthreads();
+  {
+    float s = ((red[0][t] + red[1][t]) + red[2][t]) + red[3][t];
+    if constexpr (GATED) s += t < XD ? dfL[t] * gv : dfL[t - XD] * (1.f - gv);
+    demb[(long)b * 2 * XD + t] = s;
+  }
 }
 
 MER_API int mer_xh_mlp_bwd(int B, int C, int H1, int gated, const float* dlogits, const float* emb, const float* h,
-                           const float* g, const float* fused, const float* W0, const float* W3, const float* Wc,
-                           float mlp_p, const unsigned long long* seed, unsigned long long site, float* dW0, float* db0,
-                           float* dW3, float* db3, float* dWc, float* dbc, float* demb, void* stream) {
+                           const float* g, const float* W0, const float* W3, const float* Wc, float mlp_p,
+                           const unsigned long long* seed, unsigned long long site, float* dh, float* dz, float* demb,
+                           void* stream) {
   if (B <= 0) return 0;
-  if (H1 <= 0 || H1 > G4_MAXH || H1 % 4 || C <= 0 || C > G4_MAXC || (mlp_p > 0.f && !seed) ||
-      (gated && (!Wc || !dWc || !dbc || !g || !fused)))
+  if (H1 <= 0 || H1 > 256 || C <= 0 || C > 32 || (mlp_p > 0.f && !seed) || !dh || !demb ||
+      (gated && (!Wc || !g || !dz)))
     return (int)hipErrorInvalidValue;
-  const size_t lds = sizeof(float) * G4_LDS_FLOATS;
-  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&xh_mlp_bwd_kernel),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
-    return (int)hipErrorInvalidConfiguration;
-  hipLaunchKernelGGL(xh_mlp_bwd_kernel, dim3(G4_BLOCKS), dim3(256), lds, (hipStream_t)stream, B, C, H1, gated,
-                     dlogits, emb, h, g, fused, W0, W3, Wc, mlp_p, seed, site, dW0, db0, dW3, db3, dWc, dbc, demb);
+  if (gated)
+    hipLaunchKernelGGL(xh_mlp_bwd_kernel<true>, dim3(B), dim3(256), 0, (hipStream_t)stream, C, H1, dlogits, emb, h, g,
+                       W0, W3, Wc, mlp_p, seed, site, dh, dz, demb);
+  else
+    hipLaunchKernelGGL(xh_mlp_bwd_kernel<false>, dim3(B), dim3(256), 0, (hipStream_t)stream, C, H1, dlogits, emb, h, g,
+                       W0, W3, Wc, mlp_p, seed, site, dh, dz, demb);
   MER_LAUNCH_CHECK();
 }
 
@@ -286,7 +181,7 @@ __global__ __launch_bounds__(256) void xh_a2v_bwd_kernel(
     const float* __restrict__ mean_a, const float* __restrict__ rstd_a, const float* __restrict__ gamma,
     const float* __restrict__ P2, const float* __restrict__ kv2, const float* __restrict__ q2, SplitW WoT2, XhDrop dr,
     float scale, float* __restrict__ da, float* __restrict__ da2, float* __restrict__ dqkv,
-    float* __restrict__ dkv2_part, float* __restrict__ ln_part) {
+    float* __restrict__ dkv2_part, float* __restrict__ ln_part, float* __restrict__ dbias) {
   __shared__ __attribute__((aligned(16))) float d2L[16 * LDA];
   __shared__ __attribute__((aligned(16))) float oL[16 * LDA];
   __shared__ __attribute__((aligned(16))) float tiles[XH * 2 * 16 * G3_TLD];
@@ -402,6 +297,16 @@ __global__ __launch_bounds__(256) void xh_a2v_bwd_kernel(
         pt[j * 2 * XD + XD + h * XDH + 16 * jt + fr] = dv[jt][r];
       }
   }
+  if (dbias) {  // the prior bias gradient: dS summed over the heads in head order (mha_dbias_kernel's order)
+    __syncthreads();
+    for (int e = threadIdx.x; e < nr * T; e += 256) {
+      const int i = e / T, j = e - i * T;
+      float s = 0.f;
+#pragma unroll
+      for (int q = 0; q < XH; ++q) s += tiles[(q * 2) * 16 * G3_TLD + i * G3_TLD + j];
+      dbias[((long)b * Ta + i0 + i) * T + j] = s;
+    }
+  }
 }
 
 MER_API int mer_xh_a2v_bwd(int B, int T, int Ta, const float* demb, const float* s_a, const float* mean_a,
@@ -409,14 +314,14 @@ MER_API int mer_xh_a2v_bwd(int B, int T, int Ta, const float* demb, const float*
                            const void* WoT2_hi, const void* WoT2_lo, float attn_p, float path_p,
                            const unsigned long long* seed, unsigned long long site_attn, unsigned long long site_path,
                            float scale, float* da, float* da2, float* dqkv, float* dkv2_part, float* ln_part,
-                           void* stream) {
+                           float* dbias, void* stream) {
   if (B <= 0) return 0;
   if (T <= 0 || T > 16 || Ta <= 0 || ((attn_p > 0.f || path_p > 0.f) && !seed)) return (int)hipErrorInvalidValue;
   const int ntiles = (Ta + 15) / 16;
   XhDrop dr{attn_p, path_p, seed, site_attn, site_path};
   hipLaunchKernelGGL(xh_a2v_bwd_kernel, dim3(B * ntiles), dim3(256), 0, (hipStream_t)stream, T, Ta, ntiles, demb, s_a,
                      mean_a, rstd_a, gamma, P2, kv2, q2, SplitW{(const bf16_t*)WoT2_hi, (const bf16_t*)WoT2_lo}, dr,
-                     scale, da, da2, dqkv, dkv2_part, ln_part);
+                     scale, da, da2, dqkv, dkv2_part, ln_part, dbias);
   MER_LAUNCH_CHECK();
 }
 
@@ -433,7 +338,8 @@ __global__ __launch_bounds__(256) void xh_v2a_bwd_kernel(
     const float* __restrict__ s_v, const float* __restrict__ mean_v, const float* __restrict__ rstd_v,
     const float* __restrict__ gamma, SplitW WoT1, const float* __restrict__ P1, const float* __restrict__ kv1,
     const float* __restrict__ q1, XhDrop dr, float scale, float* __restrict__ dkv2, float* __restrict__ dv2,
-    float* __restrict__ dq1, float* __restrict__ dv, float* __restrict__ dqkv, float* __restrict__ ln_part) {
+    float* __restrict__ dq1, float* __restrict__ dv, float* __restrict__ dqkv, float* __restrict__ ln_part,
+    float* __restrict__ dbias) {
   extern __shared__ __attribute__((aligned(16))) float g2smem[];
   float* kvL = g2smem;                        // [16][G2_KVLD]  dK2 dV2
   float* t1 = kvL + 16 * G2_KVLD;             // [16][LDA]  dv1, then ds (the residual part of dv)
@@ -604,6 +510,15 @@ __global__ __launch_bounds__(256) void xh_v2a_bwd_kernel(
     dq1[row0 * XD + e] = dqL[r * LDA + c];
     dv[row0 * XD + e] = t1[r * LDA + c];
   }
+  if (dbias) {  // the prior bias gradient: dS summed over the heads in head order (mha_dbias_kernel's order)
+    for (int e = threadIdx.x; e < T * Ta; e += 256) {
+      const int i = e / Ta, j = e - i * Ta;
+      float s = 0.f;
+#pragma unroll
+      for (int q = 0; q < XH; ++q) s += tiles[(q * 2) * 16 * G2_SLD + i * G2_SLD + j];
+      dbias[((long)b * T + i) * Ta + j] = s;
+    }
+  }
   XT(1, 7);
 }
 
@@ -614,7 +529,8 @@ MER_API int mer_xh_v2a_bwd(int B, int T, int Ta, const float* dkv2_part, const v
                            const float* gamma, const void* WoT1_hi, const void* WoT1_lo, const float* P1,
                            const float* kv1, const float* q1, float attn_p, float path_p, const unsigned long long* seed,
                            unsigned long long site_attn, unsigned long long site_path, float scale, float* dkv2,
-                           float* dv2, float* dq1, float* dv, float* dqkv, float* ln_part, void* stream) {
+                           float* dv2, float* dq1, float* dv, float* dqkv, float* ln_part, float* dbias,
+                           void* stream) {
   if (B <= 0) return 0;
   if (T <= 0 || T > 16 || Ta <= 0 || Ta > 16 * G2_KT || ((attn_p > 0.f || path_p > 0.f) && !seed))
     return (int)hipErrorInvalidValue;
@@ -625,7 +541,7 @@ MER_API int mer_xh_v2a_bwd(int B, int T, int Ta, const float* dkv2_part, const v
   hipLaunchKernelGGL(xh_v2a_bwd_kernel, dim3(B), dim3(256), G2_LDS_BYTES, (hipStream_t)stream, T, Ta, (Ta + 15) / 16,
                      dkv2_part, SplitW{(const bf16_t*)WkvT2_hi, (const bf16_t*)WkvT2_lo}, demb, s_v, mean_v, rstd_v,
                      gamma, SplitW{(const bf16_t*)WoT1_hi, (const bf16_t*)WoT1_lo}, P1, kv1, q1, dr, scale, dkv2, dv2,
-                     dq1, dv, dqkv, ln_part);
+                     dq1, dv, dqkv, ln_part, dbias);
   MER_LAUNCH_CHECK();
 }
 
@@ -718,7 +634,7 @@ MER_API int mer_xh_audio_bwd(int M, const float* dqkv, const void* WcT_hi, const
 // xh_wfold adds the partials in split order.  The table travels by value in the kernel arguments, so a
 // captured graph holds it (no device table to upload).
 // ---------------------------------------------------------------------------------------------
-constexpr int WG_MAXP = 16;
+constexpr int WG_MAXP = 20;
 constexpr int WG_HOST_COLS = 11;  // dY ldy X ldx x_dtype M N K splits dW db
 
 struct WgProb {
@@ -860,15 +776,15 @@ __global__ __launch_bounds__(256) void xh_wfold_kernel(const WgTab tab, const fl
     const float* src = wpart ? ws + d.ws_off + e : ws + d.ws_b_off + (e - nk);
     const long stride = wpart ? nk : (long)d.N;
     float s = 0.f;
-    for (int q0 = 0; q0 < d.splits; q0 += 8) {
-      float v[8];
+    for (int q0 = 0; q0 < d.splits; q0 += 32) {  // 32 partials in flight, summed in split order
+      float v[32];
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
+      for (int q = 0; q < 32; ++q) {
         const float x = src[(long)(q0 + q < d.splits ? q0 + q : d.splits - 1) * stride];
         v[q] = q0 + q < d.splits ? x : 0.f;
       }
 #pragma unroll
-      for (int q = 0; q < 8; ++q) s += v[q];
+      for (int q = 0; q < 32; ++q) s += v[q];
     }
     if (wpart)
       d.dW[e] += s;
@@ -942,6 +858,14 @@ MER_API int mer_xh_wgrad(int nprob, const long long* table, float* ws, long long
   const long long need = wg_layout(nprob, table, &tab, &blocks);
   if (need < 0 || need > ws_floats) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(xh_wgrad_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, tab, ws);
-  hipLaunchKernelGGL(xh_wfold_kernel, dim3(64, nprob), dim3(256), 0, (hipStream_t)stream, tab, ws);
+  // fold: one element per thread for the largest problem (each thread's split loads are one latency round, not
+  // one per element it would otherwise loop over)
+  long long most = 0;
+  for (int i = 0; i < nprob; ++i) {
+    const long long tot = (long long)tab.p[i].N * tab.p[i].K + (tab.p[i].db ? tab.p[i].N : 0);
+    most = tot > most ? tot : most;
+  }
+  const unsigned fold_x = (unsigned)((most + 255) / 256 < 1024 ? (most + 255) / 256 : 1024);
+  hipLaunchKernelGGL(xh_wfold_kernel, dim3(fold_x, nprob), dim3(256), 0, (hipStream_t)stream, tab, ws);
   MER_LAUNCH_CHECK();
 }

@@ -894,26 +894,28 @@ def xh_audio_fwd(af, Ws, bs, Wa, ba, Wc, bq2, bkv1, a_s, a, q2, kv1, vf, Wv, bv,
 
 
 def xh_v2a_fwd(B, T, Ta, v, q1, kv1, Wo1, bo1, gamma, beta, Wkv2, bkv2, attn_p, path_p, rng, site_attn, site_path,
-               scale, P1, o1, s_v, mu_v, rs_v, v1, kv2, emb):
-    if tuple(v.shape) != (B * T, 128) or tuple(q1.shape) != (B * T, 128) or tuple(kv1.shape) != (B * Ta, 256):
+               scale, P1, o1, s_v, mu_v, rs_v, v1, kv2, emb, bias=None):
+    if tuple(v.shape) != (B * T, 128) or tuple(q1.shape) != (B * T, 128) or tuple(kv1.shape) != (B * Ta, 256) \
+            or (bias is not None and bias.numel() != B * T * Ta):
         raise ValueError("xh_v2a_fwd shapes")
-    _f32c(v, q1, kv1, P1, o1, s_v, mu_v, rs_v, v1, kv2, emb)
+    _f32c(v, q1, kv1, P1, o1, s_v, mu_v, rs_v, v1, kv2, emb, bias)
     _launch("xh_v2a_fwd", (B, T, Ta), "mer_xh_v2a_fwd", B, T, Ta, v.data_ptr(), q1.data_ptr(), kv1.data_ptr(),
             *_planes(Wo1), bo1.data_ptr(), gamma.data_ptr(), beta.data_ptr(), *_planes(Wkv2), bkv2.data_ptr(),
             float(attn_p), float(path_p), rng_ptr(rng), int(site_attn), int(site_path), float(scale), P1.data_ptr(),
             o1.data_ptr(), s_v.data_ptr(), mu_v.data_ptr(), rs_v.data_ptr(), v1.data_ptr(), kv2.data_ptr(),
-            emb.data_ptr(), emb.stride(0), stream_ptr())
+            emb.data_ptr(), emb.stride(0), _ptr(bias), stream_ptr())
 
 
 def xh_a2v_fwd(B, T, Ta, q2, kv2, a, Wo2, bo2, gamma, beta, attn_p, path_p, rng, site_attn, site_path, scale, P2, o2,
-               s_a, mu_a, rs_a, part):
-    if tuple(q2.shape) != (B * Ta, 128) or tuple(kv2.shape) != (B * T, 256) or part.numel() != B * ((Ta + 15) // 16) * 128:
+               s_a, mu_a, rs_a, part, bias=None):
+    if tuple(q2.shape) != (B * Ta, 128) or tuple(kv2.shape) != (B * T, 256) or part.numel() != B * ((Ta + 15) // 16) * 128 \
+            or (bias is not None and bias.numel() != B * T * Ta):
         raise ValueError("xh_a2v_fwd shapes")
-    _f32c(q2, kv2, a, P2, o2, s_a, mu_a, rs_a, part)
+    _f32c(q2, kv2, a, P2, o2, s_a, mu_a, rs_a, part, bias)
     _launch("xh_a2v_fwd", (B, T, Ta), "mer_xh_a2v_fwd", B, T, Ta, q2.data_ptr(), kv2.data_ptr(), a.data_ptr(),
             *_planes(Wo2), bo2.data_ptr(), gamma.data_ptr(), beta.data_ptr(), float(attn_p), float(path_p),
             rng_ptr(rng), int(site_attn), int(site_path), float(scale), P2.data_ptr(), o2.data_ptr(), s_a.data_ptr(),
-            mu_a.data_ptr(), rs_a.data_ptr(), part.data_ptr(), stream_ptr())
+            mu_a.data_ptr(), rs_a.data_ptr(), part.data_ptr(), _ptr(bias), stream_ptr())
 
 
 def xh_mlp_fwd(B, Ta, gated, part, emb, W0, b0, W3, b3, Wc, bc, mlp_p, rng, site, h, g, fused, logits):
@@ -928,44 +930,49 @@ def xh_mlp_fwd(B, Ta, gated, part, emb, W0, b0, W3, b3, Wc, bc, mlp_p, rng, site
 
 # ---------------------------------------------------------------------------------------------------
 # fused xattn head backward (csrc/xattn_fused_bwd.hip); W*T arguments are transposed (hi, lo) planes
-def xh_mlp_bwd(B, gated, dlogits, emb, h, g, fused, W0, W3, Wc, mlp_p, rng, site, dW0, db0, dW3, db3, dWc, dbc, demb):
+def xh_mlp_bwd(B, gated, dlogits, emb, h, g, W0, W3, Wc, mlp_p, rng, site, dh, dz, demb):
+    """G4: the classifier head's data gradients -> dh [B, H1], dz [B] (gated), demb [B, 256]."""
     H1, C = W0.shape[0], dlogits.shape[1]
-    if W0.shape[1] != 256 or tuple(emb.shape) != (B, 256) or tuple(demb.shape) != (B, 256) or tuple(h.shape) != (B, H1):
+    if W0.shape[1] != 256 or tuple(emb.shape) != (B, 256) or tuple(demb.shape) != (B, 256) or tuple(h.shape) != (B, H1) \
+            or tuple(dh.shape) != (B, H1) or (gated and (dz is None or dz.numel() != B)):
         raise ValueError("xh_mlp_bwd shapes")
-    _f32c(dlogits, emb, h, g, fused, W0, W3, Wc, dW0, db0, dW3, db3, dWc, dbc, demb)
+    _f32c(dlogits, emb, h, g, W0, W3, Wc, dh, dz, demb)
     _launch("xh_mlp_bwd", (B,), "mer_xh_mlp_bwd", B, C, H1, int(bool(gated)), dlogits.data_ptr(), emb.data_ptr(),
-            h.data_ptr(), _ptr(g), _ptr(fused), W0.data_ptr(), W3.data_ptr(), _ptr(Wc), float(mlp_p),
-            rng_ptr(rng) if mlp_p > 0 else 0, int(site), dW0.data_ptr(), db0.data_ptr(), dW3.data_ptr(),
-            db3.data_ptr(), _ptr(dWc), _ptr(dbc), demb.data_ptr(), stream_ptr())
+            h.data_ptr(), _ptr(g), W0.data_ptr(), W3.data_ptr(), _ptr(Wc), float(mlp_p),
+            rng_ptr(rng) if mlp_p > 0 else 0, int(site), dh.data_ptr(), _ptr(dz), demb.data_ptr(), stream_ptr())
 
 
 def xh_a2v_bwd(B, T, Ta, demb, s_a, mu_a, rs_a, gamma, P2, kv2, q2, WoT2, attn_p, path_p, rng, site_attn, site_path,
-               scale, da, da2, dqkv, dkv2_part, ln_part):
+               scale, da, da2, dqkv, dkv2_part, ln_part, dbias=None):
     nt = (Ta + 15) // 16
     if tuple(q2.shape) != (B * Ta, 128) or tuple(kv2.shape) != (B * T, 256) or tuple(dqkv.shape) != (B * Ta, 384) \
             or dkv2_part.numel() != B * nt * 16 * 256 or ln_part.numel() != B * nt * 256 or WoT2[0].shape != (128, 128):
         raise ValueError("xh_a2v_bwd shapes")
-    _f32c(demb, s_a, mu_a, rs_a, gamma, P2, kv2, q2, da, da2, dqkv, dkv2_part, ln_part)
+    _f32c(demb, s_a, mu_a, rs_a, gamma, P2, kv2, q2, da, da2, dqkv, dkv2_part, ln_part, dbias)
+    if dbias is not None and dbias.numel() != B * Ta * T:
+        raise ValueError("xh_a2v_bwd dbias shape")
     _launch("xh_a2v_bwd", (B, T, Ta), "mer_xh_a2v_bwd", B, T, Ta, demb.data_ptr(), s_a.data_ptr(), mu_a.data_ptr(),
             rs_a.data_ptr(), gamma.data_ptr(), P2.data_ptr(), kv2.data_ptr(), q2.data_ptr(), *_planes(WoT2),
             float(attn_p), float(path_p), rng_ptr(rng) if (attn_p > 0 or path_p > 0) else 0, int(site_attn),
             int(site_path), float(scale), da.data_ptr(), da2.data_ptr(), dqkv.data_ptr(), dkv2_part.data_ptr(),
-            ln_part.data_ptr(), stream_ptr())
+            ln_part.data_ptr(), _ptr(dbias), stream_ptr())
 
 
 def xh_v2a_bwd(B, T, Ta, dkv2_part, WkvT2, demb, s_v, mu_v, rs_v, gamma, WoT1, P1, kv1, q1, attn_p, path_p, rng,
-               site_attn, site_path, scale, dkv2, dv2, dq1, dv, dqkv, ln_part):
+               site_attn, site_path, scale, dkv2, dv2, dq1, dv, dqkv, ln_part, dbias=None):
     if tuple(kv1.shape) != (B * Ta, 256) or tuple(q1.shape) != (B * T, 128) or tuple(dkv2.shape) != (B * T, 256) \
             or WkvT2[0].shape != (128, 256) or ln_part.numel() != B * 256 or tuple(dv.shape) != (B * T, 128) \
             or dkv2_part.numel() != B * ((Ta + 15) // 16) * 16 * 256:
         raise ValueError("xh_v2a_bwd shapes")
-    _f32c(dkv2_part, demb, s_v, mu_v, rs_v, gamma, P1, kv1, q1, dkv2, dv2, dq1, dv, dqkv, ln_part)
+    _f32c(dkv2_part, demb, s_v, mu_v, rs_v, gamma, P1, kv1, q1, dkv2, dv2, dq1, dv, dqkv, ln_part, dbias)
+    if dbias is not None and dbias.numel() != B * T * Ta:
+        raise ValueError("xh_v2a_bwd dbias shape")
     _launch("xh_v2a_bwd", (B, T, Ta), "mer_xh_v2a_bwd", B, T, Ta, dkv2_part.data_ptr(), *_planes(WkvT2),
             demb.data_ptr(), s_v.data_ptr(), mu_v.data_ptr(), rs_v.data_ptr(), gamma.data_ptr(), *_planes(WoT1),
             P1.data_ptr(), kv1.data_ptr(), q1.data_ptr(), float(attn_p), float(path_p),
             rng_ptr(rng) if (attn_p > 0 or path_p > 0) else 0, int(site_attn), int(site_path), float(scale),
             dkv2.data_ptr(), dv2.data_ptr(), dq1.data_ptr(), dv.data_ptr(), dqkv.data_ptr(), ln_part.data_ptr(),
-            stream_ptr())
+            _ptr(dbias), stream_ptr())
 
 
 def xh_audio_bwd(dqkv, WcT, WaT, da, da_s, dq1, WqT1, WvT, dv, dvfeat):
@@ -1014,8 +1021,8 @@ class WGradTable:
 
     def _table(self):
         import numpy as np
-        if len(self.rows) > 16:
-            raise ValueError("mer_xh_wgrad takes at most 16 problems")
+        if len(self.rows) > 20:
+            raise ValueError("mer_xh_wgrad takes at most 20 problems")
         return np.ascontiguousarray(np.array(self.rows, dtype=np.int64))
 
     def ws_floats(self) -> int:

@@ -58,5 +58,5 @@ def hip_dropout(x: torch.Tensor, p: float, training: bool) -> torch.Tensor:
     if not training or p <= 0:
         return x
     seed = int(torch.randint(0, 2 ** 62, (1,)).item())  # host draw: torch.manual_seed reproduces it
-    rng = torch.tensor([seed], dtype=torch.int64).to(x.device, non_blocking=True)
+    rng = torch.full((1,), seed, dtype=torch.int64, device=x.device)  # a fill kernel: no host buffer in flight
     return _DropoutFn.apply(x, p, rng)

@@ -35,7 +35,7 @@ _PLANES = {
 
 
 def supported(cfg, p: Dict[str, torch.Tensor], v_feat: torch.Tensor, a_seq: torch.Tensor, qlin) -> bool:
-    if not ENABLED or qlin is not None or cfg.use_prior or cfg.temporal_pooling != "mean":
+    if not ENABLED or qlin is not None or cfg.temporal_pooling != "mean":
         return False
     if cfg.num_heads != 4 or p["v_in_proj.weight"].shape[0] != 128 or cfg.xattn_head not in ("concat", "gated"):
         return False
@@ -174,19 +174,25 @@ def fused_forward(p, cfg, v_feat, a_seq, training, rng, ctx, sites):
     K.xh_audio_fwd(af, sp["Ws"], p["audio_seq_proj.bias"], sp["Wa"], p["a_in_proj.bias"], sp["Wc"],
                    p["a2v_attn.in_proj_bias"][:d], p["v2a_attn.in_proj_bias"][d:], a_s, a, q2, kv1, vf, sp["Wv"],
                    p["v_in_proj.bias"], sp["Wq1"], p["v2a_attn.in_proj_bias"][:d], v, q1)
+    sv = ctx.saved
+    v2a_bias = a2v_bias = None
+    dp_prior = cfg.prior_dropout if training else 0.0
+    if cfg.use_prior:  # the emotion-prior attention biases from the pre-attention tokens (fusion.py:390-391)
+        from .xattn_head import linear_runner, prior_forward
+        sv.update(v=v, a=a)
+        v2a_bias, a2v_bias = prior_forward(p, v, a, B, T, Ta, dp_prior, seed, sv, linear_runner(p))
     P1 = e(B, H, T, Ta)
     s_v, mu_v, rs_v, v1, kv2 = e(B * T, d), e(B * T), e(B * T), e(B * T, d), e(B * T, 2 * d)
     emb = e(B, 2 * d)
     scale = (d // H) ** -0.5
     K.xh_v2a_fwd(B, T, Ta, v, q1, kv1, sp["Wo1"], p["v2a_attn.out_proj.bias"], p["v_norm.weight"], p["v_norm.bias"],
                  sp["Wkv2"], p["a2v_attn.in_proj_bias"][d:], dp_attn, dp_path, seed, site_v2a, site_vpath, scale, P1,
-                 o1, s_v, mu_v, rs_v, v1, kv2, emb)
+                 o1, s_v, mu_v, rs_v, v1, kv2, emb, bias=v2a_bias)
     o2, P2 = e(B * Ta, d), e(B, H, Ta, T)
     s_a, mu_a, rs_a = e(B * Ta, d), e(B * Ta), e(B * Ta)
     part = e(B, (Ta + 15) // 16, d)
     K.xh_a2v_fwd(B, T, Ta, q2, kv2, a, sp["Wo2"], p["a2v_attn.out_proj.bias"], p["a_norm.weight"], p["a_norm.bias"],
-                 dp_attn, dp_path, seed, site_a2v, site_apath, scale, P2, o2, s_a, mu_a, rs_a, part)
-    sv = ctx.saved
+                 dp_attn, dp_path, seed, site_a2v, site_apath, scale, P2, o2, s_a, mu_a, rs_a, part, bias=a2v_bias)
     sv.update(vf=vf, af=af, v=v, a_s=a_s, a=a, q1=q1, kv1=kv1, o1=o1, P1=P1, v1=v1, s_v=s_v, mu_v=mu_v, rs_v=rs_v,
               q2=q2, kv2=kv2, o2=o2, P2=P2, s_a=s_a, mu_a=mu_a, rs_a=rs_a, emb=emb)
     if cfg.xattn_head == "concat":
@@ -205,7 +211,7 @@ def fused_forward(p, cfg, v_feat, a_seq, training, rng, ctx, sites):
         K.xh_mlp_fwd(B, Ta, True, part, emb, W0, b0, W3, b3, Wc, bc, dp_mlp, seed, site_mlp, h, g, fused, logits)
         sv.update(h=h, g=g, fused=fused)
     ctx.cfg = cfg
-    ctx.drops = (dp_attn, dp_path, dp_mlp, 0.0)
+    ctx.drops = (dp_attn, dp_path, dp_mlp, dp_prior)
     ctx.fused = True
     return logits
 
@@ -217,7 +223,7 @@ def backward_supported(ctx, p, need_da_seq: bool) -> bool:
         return False
     n0 = "xattn_mlp.0.weight" if ctx.cfg.xattn_head == "concat" else "xattn_gate.0.weight"
     C = (p["xattn_mlp.3.weight"] if ctx.cfg.xattn_head == "concat" else p["xattn_classifier.weight"]).shape[0]
-    return C <= 32 and p[n0].shape[0] <= 256  # mer_xh_mlp_bwd's LDS staging bounds
+    return C <= 32 and p[n0].shape[0] <= 256  # mer_xh_mlp_bwd's bounds
 
 
 def _splits(M: int) -> int:
@@ -244,27 +250,39 @@ def fused_backward(p, ctx, dlogits, grads, need_dv_feat=True):
     demb = e(B, 2 * d)
     if cfg.xattn_head == "concat":
         n0, n3 = "xattn_mlp.0.", "xattn_mlp.3."
-        K.xh_mlp_bwd(B, False, dlogits, sv["emb"], sv["h"], None, None, p[n0 + "weight"], p[n3 + "weight"], None,
-                     dp_mlp, rng, SITE_MLP, grads[n0 + "weight"], grads[n0 + "bias"], grads[n3 + "weight"],
-                     grads[n3 + "bias"], None, None, demb)
+        dh, dz = e(B, p[n0 + "weight"].shape[0]), None
+        K.xh_mlp_bwd(B, False, dlogits, sv["emb"], sv["h"], None, p[n0 + "weight"], p[n3 + "weight"], None, dp_mlp,
+                     rng, SITE_MLP, dh, None, demb)
+        # the classifier's weight gradients: problems of the grouped W launch below
+        head_w = ((dh, sv["emb"], grads[n0 + "weight"], grads[n0 + "bias"]),
+                  (dlogits, sv["h"], grads[n3 + "weight"], grads[n3 + "bias"]))
     else:
         n0, n3, nc = "xattn_gate.0.", "xattn_gate.3.", "xattn_classifier."
-        K.xh_mlp_bwd(B, True, dlogits, sv["emb"], sv["h"], sv["g"], sv["fused"], p[n0 + "weight"], p[n3 + "weight"],
-                     p[nc + "weight"], dp_mlp, rng, SITE_MLP, grads[n0 + "weight"], grads[n0 + "bias"],
-                     grads[n3 + "weight"], grads[n3 + "bias"], grads[nc + "weight"], grads[nc + "bias"], demb)
+        dh, dz = e(B, p[n0 + "weight"].shape[0]), e(B, 1)
+        K.xh_mlp_bwd(B, True, dlogits, sv["emb"], sv["h"], sv["g"], p[n0 + "weight"], p[n3 + "weight"],
+                     p[nc + "weight"], dp_mlp, rng, SITE_MLP, dh, dz, demb)
+        head_w = ((dh, sv["emb"], grads[n0 + "weight"], grads[n0 + "bias"]),
+                  (dz, sv["h"], grads[n3 + "weight"], grads[n3 + "bias"]),
+                  (dlogits, sv["fused"], grads[nc + "weight"], grads[nc + "bias"]))
     nt = (Ta + 15) // 16
     scale = (d // H) ** -0.5
     da, da2, dqkv = e(B * Ta, d), e(B * Ta, d), e(B * Ta, 3 * d)
     dkv2_part, lnp_a = e(B, nt, 16, 2 * d), e(B * nt, 2 * d)
+    prior = cfg.use_prior
+    dbias_a2v, dbias_v2a = (e(B, Ta, T), e(B, T, Ta)) if prior else (None, None)
     K.xh_a2v_bwd(B, T, Ta, demb, sv["s_a"], sv["mu_a"], sv["rs_a"], p["a_norm.weight"], sv["P2"], sv["kv2"], sv["q2"],
-                 sp["WoT2"], dp_attn, dp_path, rng, SITE_A2V, SITE_APATH, scale, da, da2, dqkv, dkv2_part, lnp_a)
+                 sp["WoT2"], dp_attn, dp_path, rng, SITE_A2V, SITE_APATH, scale, da, da2, dqkv, dkv2_part, lnp_a,
+                 dbias=dbias_a2v)
     vf = sv["vf"]
     dkv2, dv2, dq1, dv = e(B * T, 2 * d), e(B * T, d), e(B * T, d), e(B * T, d)
     dvfeat = e(B * T, vf.shape[1]) if need_dv_feat else None
     lnp_v = e(B, 2 * d)
     K.xh_v2a_bwd(B, T, Ta, dkv2_part, sp["WkvT2"], demb, sv["s_v"], sv["mu_v"], sv["rs_v"], p["v_norm.weight"],
                  sp["WoT1"], sv["P1"], sv["kv1"], sv["q1"], dp_attn, dp_path, rng, SITE_V2A, SITE_VPATH, scale, dkv2,
-                 dv2, dq1, dv, dqkv, lnp_v)
+                 dv2, dq1, dv, dqkv, lnp_v, dbias=dbias_v2a)
+    if prior:  # the prior's weight gradients; its token gradients join da / dv before G1 reads them
+        from .xattn_head import prior_backward
+        prior_backward(p, sv, dbias_v2a, dbias_a2v, dv, da, grads, B, T, Ta, ctx.drops[3], rng)
     da_s = e(B * Ta, d)
     K.xh_audio_bwd(dqkv, sp["WcT"], sp["WaT"], da, da_s, dq1, sp["WqT1"], sp["WvT"], dv, dvfeat)
     gw1, gb1 = grads["v2a_attn.in_proj_weight"], grads["v2a_attn.in_proj_bias"]
@@ -283,7 +301,7 @@ def fused_backward(p, ctx, dlogits, grads, need_dv_feat=True):
                           (lnp_a[:, :d], None, None, grads["a_norm.weight"]),
                           (lnp_a[:, d:], None, None, grads["a_norm.bias"]),
                           (lnp_v[:, :d], None, None, grads["v_norm.weight"]),
-                          (lnp_v[:, d:], None, None, grads["v_norm.bias"])):
+                          (lnp_v[:, d:], None, None, grads["v_norm.bias"])) + head_w:
         W.add(dY, X, dW, db, _splits(dY.shape[0]))
     ws = e(W.ws_floats())
     W.run(ws)

@@ -97,34 +97,7 @@ def head_forward(p: Dict[str, torch.Tensor], cfg: HeadConfig, v_feat: torch.Tens
 
     v2a_bias = a2v_bias = None
     if cfg.use_prior:
-        n = "emotion_prior_bias."
-        pg = _e((B, 2 * d), v)
-        K.mean_pool_fwd(v.view(B, T, d), pg[:, :d], ldy=2 * d)
-        K.mean_pool_fwd(a.view(B, Ta, d), pg[:, d:], ldy=2 * d)
-        h1 = lin(n + "prior_net.0", pg, _e((B, p[n + "prior_net.0.weight"].shape[0]), v), act="relu")
-        K.dropout_(h1, dp_prior, rng, SITE_PRIOR)
-        prior = lin(n + "prior_net.3", h1, _e((B, p[n + "prior_net.3.weight"].shape[0]), v))
-        sv["pg"], sv["h1"], sv["prior"] = pg, h1, prior
-        tok = {}
-        for head, toks, L in (("v_query_bias", v, T), ("a_key_bias", a, Ta), ("a_query_bias", a, Ta), ("v_key_bias", v, T)):
-            w = p[n + head + ".weight"]  # [1, d + pd]
-            if qlin is not None and n + head in qlin:
-                # INT8 (inference): the Linear sees cat([token, prior]) (fusion.py:171-174), quantized as ONE tensor
-                ql = qlin[n + head]
-                rows = K.concat_prior_rows(toks, prior, _e((toks.shape[0], ql.in_padded), v), L)
-                tt = ql(rows, _e((toks.shape[0], 1), v))
-                tp = torch.zeros(B, 1, device=v.device, dtype=torch.float32)
-            else:
-                tt = K.gemm(toks, w[:, :d], _e((toks.shape[0], 1), v), trans_b=True)
-                tp = K.gemm(prior, w[:, d:], _e((B, 1), v), trans_b=True, bias=p[n + head + ".bias"])
-            tok[head] = (tt, tp)
-            sv["tt_" + head], sv["tp_" + head] = tt, tp
-        v2a_bias = _e((B, T, Ta), v)
-        K.token_bias_fwd(tok["v_query_bias"][0], tok["v_query_bias"][1], tok["a_key_bias"][0], tok["a_key_bias"][1],
-                         p[n + "bias_scale"], v2a_bias)
-        a2v_bias = _e((B, Ta, T), v)
-        K.token_bias_fwd(tok["a_query_bias"][0], tok["a_query_bias"][1], tok["v_key_bias"][0], tok["v_key_bias"][1],
-                         p[n + "bias_scale"], a2v_bias)
+        v2a_bias, a2v_bias = prior_forward(p, v, a, B, T, Ta, dp_prior, rng, sv, lin, qlin)
 
     # ---- v2a: v2 = MHA(q=v, k=a, v=a)  (fusion.py:394) ----
     w1, b1 = p["v2a_attn.in_proj_weight"], p["v2a_attn.in_proj_bias"]
@@ -274,34 +247,7 @@ def head_backward(p: Dict[str, torch.Tensor], ctx: HeadCtx, dlogits: torch.Tenso
 
     # ---- emotion prior backward (fusion.py:170-184) ----
     if cfg.use_prior:
-        n = "emotion_prior_bias."
-        prior = sv["prior"]
-        pd_ = prior.shape[1]
-        dprior = z(B, pd_)
-        dscale_part = e(2, B)
-        spec = ((dbias_v2a, "v_query_bias", "a_key_bias", T, Ta, sv["v"], sv["a"], 0),
-                (dbias_a2v, "a_query_bias", "v_key_bias", Ta, T, sv["a"], sv["v"], 1))
-        for dbias, qh, kh, Lq, Lk, qtok, ktok, idx in spec:
-            dqt, dkt, dqp, dkp = e(B * Lq, 1), e(B * Lk, 1), e(B, 1), e(B, 1)
-            K.token_bias_bwd(sv["tt_" + qh], sv["tp_" + qh], sv["tt_" + kh], sv["tp_" + kh], p[n + "bias_scale"],
-                             dbias, dqt, dkt, dqp, dkp, dscale_part[idx])
-            for head, dtt, dtp, toks, dtoks in ((qh, dqt, dqp, qtok, dv if qtok is sv["v"] else da),
-                                                (kh, dkt, dkp, ktok, dv if ktok is sv["v"] else da)):
-                w = p[n + head + ".weight"]
-                gw = grads[n + head + ".weight"]
-                # tt = toks @ w[:, :d]^T  ;  tp = prior @ w[:, d:]^T + b
-                K.linear_bwd(toks, w[:, :d], dtt, dx=dtoks, dw=gw[:, :d], dx_beta=1)
-                K.linear_bwd(prior, w[:, d:], dtp, dx=dprior, dw=gw[:, d:], db=grads[n + head + ".bias"], dx_beta=1)
-        K.vec_sum(dscale_part, grads[n + "bias_scale"], accumulate=True)
-        dh1 = e(B, sv["h1"].shape[1])
-        K.linear_bwd(sv["h1"], p[n + "prior_net.3.weight"], dprior, dx=dh1, dw=grads[n + "prior_net.3.weight"],
-                     db=grads[n + "prior_net.3.bias"])
-        K.relu_dropout_bwd_(dh1, sv["h1"], dp_prior, rng, SITE_PRIOR)
-        dpg = e(B, 2 * d)
-        K.linear_bwd(sv["pg"], p[n + "prior_net.0.weight"], dh1, dx=dpg, dw=grads[n + "prior_net.0.weight"],
-                     db=grads[n + "prior_net.0.bias"])
-        K.mean_pool_bwd(dpg[:, :d], dv.view(B, T, d), accumulate=True)
-        K.mean_pool_bwd(dpg[:, d:], da.view(B, Ta, d), accumulate=True)
+        prior_backward(p, sv, dbias_v2a, dbias_a2v, dv, da, grads, B, T, Ta, dp_prior, rng)
 
     # ---- input projections ----
     da_s = e(B * Ta, d)
@@ -317,6 +263,78 @@ def head_backward(p: Dict[str, torch.Tensor], ctx: HeadCtx, dlogits: torch.Tenso
     K.linear_bwd(sv["vf"], p["v_in_proj.weight"], dv, dx=dv_feat, dw=grads["v_in_proj.weight"], db=grads["v_in_proj.bias"])
     return (dv_feat.view(B, T, -1) if dv_feat is not None else None,
             da_seq.view(B, Ta, -1) if da_seq is not None else None)
+
+
+def prior_forward(p, v, a, B, T, Ta, dp_prior, rng, sv, lin, qlin=None):
+    """``EmotionPriorBiasAdapter.forward`` (fusion.py:178-184) on the pre-attention tokens v [B*T, d], a [B*Ta, d]:
+    pooled means -> prior_net (256 -> 64 ReLU Dropout -> 8) -> the four token-bias Linears over cat([token, prior])
+    -> (v2a_bias [B, T, Ta], a2v_bias [B, Ta, T]) = tanh(q + k) * bias_scale.  Saves what prior_backward reads."""
+    n = "emotion_prior_bias."
+    d = v.shape[1]
+    pg = _e((B, 2 * d), v)
+    K.mean_pool_fwd(v.view(B, T, d), pg[:, :d], ldy=2 * d)
+    K.mean_pool_fwd(a.view(B, Ta, d), pg[:, d:], ldy=2 * d)
+    h1 = lin(n + "prior_net.0", pg, _e((B, p[n + "prior_net.0.weight"].shape[0]), v), act="relu")
+    K.dropout_(h1, dp_prior, rng, SITE_PRIOR)
+    prior = lin(n + "prior_net.3", h1, _e((B, p[n + "prior_net.3.weight"].shape[0]), v))
+    sv["pg"], sv["h1"], sv["prior"] = pg, h1, prior
+    tok = {}
+    for head, toks, L in (("v_query_bias", v, T), ("a_key_bias", a, Ta), ("a_query_bias", a, Ta), ("v_key_bias", v, T)):
+        w = p[n + head + ".weight"]  # [1, d + pd]
+        if qlin is not None and n + head in qlin:
+            # INT8 (inference): the Linear sees cat([token, prior]) (fusion.py:171-174), quantized as ONE tensor
+            ql = qlin[n + head]
+            rows = K.concat_prior_rows(toks, prior, _e((toks.shape[0], ql.in_padded), v), L)
+            tt = ql(rows, _e((toks.shape[0], 1), v))
+            tp = torch.zeros(B, 1, device=v.device, dtype=torch.float32)
+        else:
+            tt = K.gemm(toks, w[:, :d], _e((toks.shape[0], 1), v), trans_b=True)
+            tp = K.gemm(prior, w[:, d:], _e((B, 1), v), trans_b=True, bias=p[n + head + ".bias"])
+        tok[head] = (tt, tp)
+        sv["tt_" + head], sv["tp_" + head] = tt, tp
+    v2a_bias = _e((B, T, Ta), v)
+    K.token_bias_fwd(tok["v_query_bias"][0], tok["v_query_bias"][1], tok["a_key_bias"][0], tok["a_key_bias"][1],
+                     p[n + "bias_scale"], v2a_bias)
+    a2v_bias = _e((B, Ta, T), v)
+    K.token_bias_fwd(tok["a_query_bias"][0], tok["a_query_bias"][1], tok["v_key_bias"][0], tok["v_key_bias"][1],
+                     p[n + "bias_scale"], a2v_bias)
+    return v2a_bias, a2v_bias
+
+
+def prior_backward(p, sv, dbias_v2a, dbias_a2v, dv, da, grads, B, T, Ta, dp_prior, rng):
+    """Backward of prior_forward (fusion.py:170-184): the prior weights' gradients (accumulated into ``grads``) and the
+    token gradients ADDED into dv [B*T, d] and da [B*Ta, d] (token-bias Linears + the pooled means)."""
+    n = "emotion_prior_bias."
+    d = dv.shape[1]
+    prior = sv["prior"]
+    pd_ = prior.shape[1]
+    dev = dv.device
+    e = lambda *shape: torch.empty(shape, device=dev, dtype=torch.float32)  # noqa: E731
+    dprior = torch.zeros(B, pd_, device=dev, dtype=torch.float32)
+    dscale_part = e(2, B)
+    spec = ((dbias_v2a, "v_query_bias", "a_key_bias", T, Ta, sv["v"], sv["a"], 0),
+            (dbias_a2v, "a_query_bias", "v_key_bias", Ta, T, sv["a"], sv["v"], 1))
+    for dbias, qh, kh, Lq, Lk, qtok, ktok, idx in spec:
+        dqt, dkt, dqp, dkp = e(B * Lq, 1), e(B * Lk, 1), e(B, 1), e(B, 1)
+        K.token_bias_bwd(sv["tt_" + qh], sv["tp_" + qh], sv["tt_" + kh], sv["tp_" + kh], p[n + "bias_scale"],
+                         dbias, dqt, dkt, dqp, dkp, dscale_part[idx])
+        for head, dtt, dtp, toks, dtoks in ((qh, dqt, dqp, qtok, dv if qtok is sv["v"] else da),
+                                            (kh, dkt, dkp, ktok, dv if ktok is sv["v"] else da)):
+            w = p[n + head + ".weight"]
+            gw = grads[n + head + ".weight"]
+            # tt = toks @ w[:, :d]^T  ;  tp = prior @ w[:, d:]^T + b
+            K.linear_bwd(toks, w[:, :d], dtt, dx=dtoks, dw=gw[:, :d], dx_beta=1)
+            K.linear_bwd(prior, w[:, d:], dtp, dx=dprior, dw=gw[:, d:], db=grads[n + head + ".bias"], dx_beta=1)
+    K.vec_sum(dscale_part, grads[n + "bias_scale"], accumulate=True)
+    dh1 = e(B, sv["h1"].shape[1])
+    K.linear_bwd(sv["h1"], p[n + "prior_net.3.weight"], dprior, dx=dh1, dw=grads[n + "prior_net.3.weight"],
+                 db=grads[n + "prior_net.3.bias"])
+    K.relu_dropout_bwd_(dh1, sv["h1"], dp_prior, rng, SITE_PRIOR)
+    dpg = e(B, 2 * d)
+    K.linear_bwd(sv["pg"], p[n + "prior_net.0.weight"], dh1, dx=dpg, dw=grads[n + "prior_net.0.weight"],
+                 db=grads[n + "prior_net.0.bias"])
+    K.mean_pool_bwd(dpg[:, :d], dv.view(B, T, d), accumulate=True)
+    K.mean_pool_bwd(dpg[:, d:], da.view(B, Ta, d), accumulate=True)
 
 
 def used_param_names(cfg: HeadConfig):

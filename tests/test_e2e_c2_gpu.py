@@ -92,7 +92,7 @@ def test_c2_train_step_b32_vs_oracle():
     dlog = float((logits.detach().cpu() - rlogits.detach()).abs().max())
     dloss = abs(float(loss.detach()) - float(rloss.detach()))
     print(f"B=32 logits max|d| {dlog:.3e}  loss hip {float(loss):.5f} oracle {float(rloss):.5f}")
-    assert dlog < 5e-2 and dloss < 1e-2
+    assert dlog < 3e-2 and dloss < 3e-3  # measured 1.1e-2 / 5e-4 (r3a)
 
     # ---- BatchNorm running statistics ----
     worst = 0.0
@@ -100,7 +100,7 @@ def test_c2_train_step_b32_vs_oracle():
         if k.startswith("video_model.") and k.endswith(("running_mean", "running_var")):
             worst = max(worst, _rel(after[k], p[k]))
     print("BN running stats worst rel", worst)
-    assert worst < 2e-2
+    assert worst < 5e-3  # measured 1.5e-3 (r3a)
     assert int(after["video_model.backbone.1.num_batches_tracked"]) == 1
 
     # ---- fp32 head teacher-forced on the HIP encoders' features ----
@@ -110,7 +110,7 @@ def test_c2_train_step_b32_vs_oracle():
     fusion_ref.cross_entropy(tlogits, labels).backward()
     dl_t = float((logits.detach().cpu() - tlogits.detach()).abs().max())
     print("teacher-forced head logits max|d|", dl_t)
-    assert dl_t < 1e-4
+    assert dl_t < 3e-5  # measured 7.4e-6 (r3a)
     for k, q in hp.items():
         r = _rel(hip_grads[k], q.grad)
         assert r < 1e-3, (k, r)
@@ -129,7 +129,7 @@ def test_c2_train_step_b32_vs_oracle():
         agree = float(((dh > 0) == (dr > 0)).float().mean())
         if k.startswith("video_model."):
             agree_trunk.append(agree)
-            assert agree >= 0.70, (k, agree)
+            assert agree >= 0.75, (k, agree)  # measured min 0.81 (r3a)
             assert cosines[k] >= 0.85, (k, cosines[k])
         else:  # vs the FULL oracle: the head sees the bf16 encoders' features (its own math: teacher-forced above)
             assert agree >= 0.9, (k, agree)

@@ -1,0 +1,9 @@
+#!/bin/bash
+OUT=$PWD/gpurun_out/r3f
+mkdir -p $OUT
+timeout -k 10 300 python -u tools/diag_grads.py 0 > $OUT/grads_late.log 2>&1
+rc=$?; echo "EXIT $rc" >> $OUT/grads_late.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 600 python -u -m pytest tests/test_xattn_fused_gpu.py tests/test_head_gpu.py tests/test_train_epoch_gpu.py tests/test_round2_features_gpu.py -m gpu -q -x --timeout 300 --timeout-method thread > $OUT/tests.log 2>&1
+rc=$?; echo "EXIT $rc" >> $OUT/tests.log; [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
+timeout -k 10 200 python -u tools/bench_head.py > $OUT/head.log 2>&1
+echo "EXIT $?" >> $OUT/head.log
