@@ -695,7 +695,7 @@ __device__ __forceinline__ ParClass par_class(const ConvGeom& g, int cls) {
 // in flight across the barrier that publishes tile kt (counted vmcnt, raw s_barrier); the barrier also retires
 // every wave's reads of tile kt-1, whose buffer the DMA of tile kt+STAGES-1 then reuses.
 template <bool DGRAD, bool PAR, int BM_, int BN_, int WM = 2, int WN = 2, int STAGES = 2, int KS = 64>
-__global__ __launch_bounds__(64 * WM * WN, 2) void conv_pipe_kernel(ConvGeom g) {
+__global__ __launch_bounds__(64 * WM * WN, WM * WN >= 16 ? 1 : 2) void conv_pipe_kernel(ConvGeom g) {  // 16 waves: 1 block / CU (2 would spill to scratch)
   constexpr int WAVES = WM * WN;
   constexpr int CW = KS / 8, RPG = 64 / CW;  // 16-byte chunks per LDS row, rows per glds instruction
   constexpr int IA = BM_ / RPG / WAVES, IB = BN_ / RPG / WAVES;  // glds per wave per K-tile
@@ -1167,8 +1167,14 @@ int launch_conv_pipe(ConvGeom& g, hipStream_t st, int variant) {
   const long tiles128 = (long)((M + 127) / 128) * ((g.Ncols + bn - 1) / bn) * (PAR ? 4 : 1);
   const bool small_m = tiles128 < 384;
   if (variant == 3 && !small_m) {  // 256-row tiles (8 / 16 waves) for the large-M layers
-    if (bn == 64) return launch_conv_pipe_t<DGRAD, PAR, 256, 64, 4, 2>(g, st);
-    return launch_conv_pipe_t<DGRAD, PAR, 256, 128, 4, 4>(g, st);
+    // (the 16-wave dgrad tile needs more than 128 VGPRs and would spill to scratch: 8-wave 256 x 64 tiles instead;
+    // tools/check_scratch.py keeps every kernel of the library scratch-free)
+    if constexpr (DGRAD) {
+      return launch_conv_pipe_t<DGRAD, PAR, 256, 64, 4, 2>(g, st);
+    } else {
+      if (bn == 64) return launch_conv_pipe_t<DGRAD, PAR, 256, 64, 4, 2>(g, st);
+      return launch_conv_pipe_t<DGRAD, PAR, 256, 128, 4, 4>(g, st);
+    }
   }
   if (variant == 5) {  // 32-wide K-tiles on a 4-deep ring (three K-tiles in flight), 4-wave tiles
     if (bn == 64)

@@ -50,13 +50,19 @@ __device__ __forceinline__ void split8(const float (&x)[8], bf16x8& hi, bf16x8& 
 // (a clamped row): a load under a per-lane condition compiles to a branch around the load followed by a wait,
 // which serialises every load of a loop on the memory latency.  Invalid elements are zeroed by a select.
 
+// the same split from two 4-vectors (no float array in between: an array the compiler does not promote to
+// registers ends up in scratch memory)
+__device__ __forceinline__ void split8v(f32x4 a, f32x4 b, bf16x8& hi, bf16x8& lo) {
+  const f32x8 v = __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
+  hi = __builtin_convertvector(v, bf16x8);
+  lo = __builtin_convertvector(v - __builtin_convertvector(hi, f32x8), bf16x8);
+}
+
 // fp32 fragment: 8 consecutive k (stride 1) of one row; zero when !valid (p must still be dereferenceable)
 __device__ __forceinline__ void frag_row(const float* p, bool valid, bf16x8& hi, bf16x8& lo) {
+  const f32x4 z = f32x4{0.f, 0.f, 0.f, 0.f};
   const f32x4 a = *reinterpret_cast<const f32x4*>(p), b = *reinterpret_cast<const f32x4*>(p + 4);
-  float x[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
-#pragma unroll
-  for (int e = 0; e < 8; ++e) x[e] = valid ? x[e] : 0.f;
-  split8(x, hi, lo);
+  split8v(valid ? a : z, valid ? b : z, hi, lo);
 }
 
 // fp32 fragment gathered with a k stride (transposed operand) from p = &row k0; element e is row k0 + e, zero
@@ -148,9 +154,8 @@ __device__ __forceinline__ void mm_step(f32x4 (&acc)[TI][TJ], const MmStage<TI, 
   for (int i = 0; i < TI; ++i) {
     const f32x4 z = f32x4{0.f, 0.f, 0.f, 0.f};
     const f32x4 a0 = live ? st.a0[i] : z, a1 = live ? st.a1[i] : z;  // a select, not a branch
-    const float x[8] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
     bf16x8 ah, al;
-    split8(x, ah, al);
+    split8v(a0, a1, ah, al);
 #pragma unroll
     for (int j = 0; j < TJ; ++j) acc[i][j] = mma3(ah, al, bh[j], bl[j], acc[i][j]);
   }
@@ -161,13 +166,16 @@ __device__ __forceinline__ void mm_step(f32x4 (&acc)[TI][TJ], const MmStage<TI, 
 // branch-free -- a conditional step or load would make the wait-count pass assume the worst at the merge and
 // wait for every load in flight (vmcnt(0)) -- so the tail steps past K load a clamped (valid) k slice and are
 // accumulated as zeros.
-template <int TI, int TJ, int D = 3>
+template <int TI, int TJ, int D = 3, int KS = 0>
 __device__ __forceinline__ void mm_aw(f32x4 (&acc)[TI][TJ], const float* A, long lda, int rmax, int K, SplitW W,
                                       long ldw, int c0) {
-  const int nsteps = K / 32;
+  // KS > 0: the depth is a compile-time constant (K == KS): the step loop unrolls completely and the stage ring
+  // stays in registers (with a run-time trip count the compiler keeps the ring in scratch memory)
+  const int nsteps = KS > 0 ? KS / 32 : K / 32;
   MmStage<TI, TJ> st[D];
 #pragma unroll
   for (int d = 0; d < D; ++d) mm_load(st[d], A, lda, rmax, W, ldw, c0, 32 * (d < nsteps ? d : nsteps - 1));
+#pragma unroll
   for (int s0 = 0; s0 < nsteps; s0 += D) {
 #pragma unroll
     for (int d = 0; d < D; ++d) {

@@ -97,7 +97,7 @@ __global__ __launch_bounds__(256) void xh_audio_fwd_kernel(int M, int S, const T
     __syncthreads();
     f32x4 acc[2][2];
     zero(acc);
-    mm_aw(acc, asL, LDA, 32, XD, vid.Wq1, XD, 32 * w);
+    mm_aw<2, 2, 3, XD>(acc, asL, LDA, 32, XD, vid.Wq1, XD, 32 * w);
     store_acc(acc, 32 * w, vid.bq1, nullptr, 0, vid.q1, XD, v0, vmax);
     return;
   }
@@ -159,7 +159,7 @@ __global__ __launch_bounds__(256) void xh_audio_fwd_kernel(int M, int S, const T
   {  // a = a_s Wa^T + ba
     f32x4 acc[2][2];
     zero(acc);
-    mm_aw(acc, asL, LDA, 32, XD, Wa, XD, 32 * w);
+    mm_aw<2, 2, 3, XD>(acc, asL, LDA, 32, XD, Wa, XD, 32 * w);
     store_acc(acc, 32 * w, ba, aL, LDA, a, XD, r0, rmax);
   }
   __syncthreads();
@@ -168,7 +168,7 @@ __global__ __launch_bounds__(256) void xh_audio_fwd_kernel(int M, int S, const T
     f32x4 acc[2][6];
     zero(acc);
     const int c0 = 96 * w;
-    mm_aw<2, 6, 2>(acc, aL, LDA, 32, XD, Wc, XD, c0);
+    mm_aw<2, 6, 2, XD>(acc, aL, LDA, 32, XD, Wc, XD, c0);
 #pragma unroll
     for (int j = 0; j < 6; ++j) {
       const int col = c0 + 16 * j + fr;
@@ -409,7 +409,7 @@ __global__ __launch_bounds__(256) void xh_v2a_fwd_kernel(
   {  // v2 = o Wo1^T + bo1
     f32x4 acc[1][2];
     zero(acc);
-    mm_aw(acc, oL, LDA, 16, XD, Wo1, XD, 32 * w);
+    mm_aw<1, 2, 3, XD>(acc, oL, LDA, 16, XD, Wo1, XD, 32 * w);
     store_acc(acc, 32 * w, bo1, tL, LDA, nullptr, 0, 0, 16);
   }
   __syncthreads();
@@ -428,7 +428,7 @@ __global__ __launch_bounds__(256) void xh_v2a_fwd_kernel(
   {  // [k2 v2] = v1 Wkv2^T + bkv2: 256 columns, 64 per wave
     f32x4 acc[1][4];
     zero(acc);
-    mm_aw(acc, qL, LDA, 16, XD, Wkv2, XD, 64 * w);
+    mm_aw<1, 4, 3, XD>(acc, qL, LDA, 16, XD, Wkv2, XD, 64 * w);
     store_acc(acc, 64 * w, bkv2, nullptr, 0, kv2, 2 * XD, row0, T);
   }
   XT(3, 4);
@@ -492,7 +492,7 @@ __global__ __launch_bounds__(256) void xh_a2v_fwd_kernel(int T, int Ta, int ntil
   {  // a2 = o Wo2^T + bo2
     f32x4 acc[1][2];
     zero(acc);
-    mm_aw(acc, oL, LDA, 16, XD, Wo2, XD, 32 * w);
+    mm_aw<1, 2, 3, XD>(acc, oL, LDA, 16, XD, Wo2, XD, 32 * w);
     store_acc(acc, 32 * w, bo2, tL, LDA, nullptr, 0, 0, 16);
   }
   __syncthreads();

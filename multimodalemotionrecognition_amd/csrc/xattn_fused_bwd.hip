@@ -215,7 +215,7 @@ __global__ __launch_bounds__(256) void xh_a2v_bwd_kernel(
   {  // do2 = da2 . Wo2
     f32x4 acc[1][2];
     zero(acc);
-    mm_aw(acc, d2L, LDA, 16, XD, WoT2, XD, 32 * w);
+    mm_aw<1, 2, 3, XD>(acc, d2L, LDA, 16, XD, WoT2, XD, 32 * w);
     store_acc(acc, 32 * w, nullptr, oL, LDA, nullptr, 0, 0, 16);
   }
   __syncthreads();
@@ -375,7 +375,7 @@ __global__ __launch_bounds__(256) void xh_v2a_bwd_kernel(
   {  // dv1 (kv2 path) = [dK2 dV2] . Wkv2
     f32x4 acc[1][2];
     zero(acc);
-    mm_aw(acc, kvL, G2_KVLD, 16, 2 * XD, WkvT2, 2 * XD, 32 * w);
+    mm_aw<1, 2, 3, 2 * XD>(acc, kvL, G2_KVLD, 16, 2 * XD, WkvT2, 2 * XD, 32 * w);
     store_acc(acc, 32 * w, nullptr, t1, LDA, nullptr, 0, 0, 16);
   }
   __syncthreads();
@@ -404,7 +404,7 @@ __global__ __launch_bounds__(256) void xh_v2a_bwd_kernel(
   {  // do1 = dv2 . Wo1
     f32x4 acc[1][2];
     zero(acc);
-    mm_aw(acc, d2L, LDA, 16, XD, WoT1, XD, 32 * w);
+    mm_aw<1, 2, 3, XD>(acc, d2L, LDA, 16, XD, WoT1, XD, 32 * w);
     store_acc(acc, 32 * w, nullptr, oL, LDA, nullptr, 0, 0, 16);
   }
   __syncthreads();
@@ -414,7 +414,25 @@ __global__ __launch_bounds__(256) void xh_v2a_bwd_kernel(
   float* dSt = tiles + (h * 2) * 16 * G2_SLD;
   float* Pdt = dSt + 16 * G2_SLD;
   const float* kb = kv1 + (long)b * Ta * 2 * XD;
+  float kraw[G2_KT / 2][2][8];
   {
+    // every global load of the attention backward first (one memory latency): the V1 key-tile fragments and the
+    // saved probabilities of this head (raw fp32, split / masked at use)
+    f32x4 vraw[G2_KT][2];
+    float praw[G2_KT][4];
+#pragma unroll
+    for (int t = 0; t < G2_KT; ++t) {
+      const int j = 16 * t + fr;
+      const float* vp = kb + (long)(j < Ta ? j : Ta - 1) * 2 * XD + XD + h * XDH + fk;
+      vraw[t][0] = *reinterpret_cast<const f32x4*>(vp);
+      vraw[t][1] = *reinterpret_cast<const f32x4*>(vp + 4);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = 4 * fq + r;
+        const bool ok = i < T && j < Ta;
+        praw[t][r] = P1[(((long)b * XH + h) * T + (ok ? i : 0)) * Ta + (ok ? j : 0)];  // always in range
+      }
+    }
     f32x4 dp[G2_KT];
 #pragma unroll
     for (int t = 0; t < G2_KT; ++t) dp[t] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -422,11 +440,25 @@ __global__ __launch_bounds__(256) void xh_v2a_bwd_kernel(
     frag_row(oL + fr * LDA + h * XDH + fk, true, ah, al);
 #pragma unroll
     for (int t = 0; t < G2_KT; ++t) {  // dP' = do1_h . V1_h^T
-      const int j = 16 * t + fr;
+      const bool ok = 16 * t + fr < Ta;
+      float x[8] = {vraw[t][0][0], vraw[t][0][1], vraw[t][0][2], vraw[t][0][3],
+                    vraw[t][1][0], vraw[t][1][1], vraw[t][1][2], vraw[t][1][3]};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) x[e] = ok ? x[e] : 0.f;
       bf16x8 bh, bl;
-      frag_row(kb + (long)(j < Ta ? j : Ta - 1) * 2 * XD + XD + h * XDH + fk, j < Ta, bh, bl);
+      split8(x, bh, bl);
       dp[t] = mma3(ah, al, bh, bl, dp[t]);
     }
+    // the K1 gathers of dq1 = dS K1 (next phase) go out now, behind the dS arithmetic
+#pragma unroll
+    for (int k = 0; k < G2_KT / 2; ++k)
+#pragma unroll
+      for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int kk = 32 * k + fk + e;
+          kraw[k][jt][e] = kb[(long)(kk < Ta ? kk : Ta - 1) * 2 * XD + h * XDH + 16 * jt + fr];
+        }
     float pv[G2_KT][4];
     float rs[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -436,10 +468,8 @@ __global__ __launch_bounds__(256) void xh_v2a_bwd_kernel(
         const int i = 4 * fq + r, j = 16 * t + fr;
         const bool ok = i < T && j < Ta;
         const long pi = (((long)b * XH + h) * T + i) * Ta + j;
-        const long pc = (((long)b * XH + h) * T + (ok ? i : 0)) * Ta + (ok ? j : 0);  // always in range
         const float m = ok ? dropout_scale(seed_attn, pi, dr.attn) : 0.f;
-        const float pl = P1[pc];
-        const float p = ok ? pl : 0.f;
+        const float p = ok ? praw[t][r] : 0.f;
         pv[t][r] = p;
         dp[t][r] *= m;  // dP
         Pdt[i * G2_SLD + j] = p * m;
@@ -459,13 +489,16 @@ __global__ __launch_bounds__(256) void xh_v2a_bwd_kernel(
   {  // dq1_h = dS . K1_h * scale  (keys >= Ta are zero in dS and read as zero from K1)
     f32x4 o[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
-    for (int k = 0; k < 16 * G2_KT; k += 32) {
+    for (int k = 0; k < G2_KT / 2; ++k) {
       bf16x8 ah, al;
-      frag_row(dSt + fr * G2_SLD + k + fk, true, ah, al);
+      frag_row(dSt + fr * G2_SLD + 32 * k + fk, true, ah, al);
 #pragma unroll
       for (int jt = 0; jt < 2; ++jt) {
+        float x[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) x[e] = 32 * k + fk + e < Ta ? kraw[k][jt][e] : 0.f;
         bf16x8 bh, bl;
-        frag_col(kb + (long)(k + fk) * 2 * XD + h * XDH + 16 * jt + fr, 2 * XD, k + fk, Ta, bh, bl);
+        split8(x, bh, bl);
         o[jt] = mma3(ah, al, bh, bl, o[jt]);
       }
     }
@@ -568,13 +601,9 @@ __global__ __launch_bounds__(256) void xh_audio_bwd_kernel(int M, const float* _
   const int rows = video ? vid.M : M;
   const int rmax = (int)(rows - r0 < 32 ? rows - r0 : 32);
   float* dst = video ? vid.dv : da;
-  {  // audio: da += [dq2 | dK1 dV1] . [Wq2 ; Wkv1];  video: dv += dq1 . Wq1
-    f32x4 acc[2][2];
-    zero(acc);
-    if (video)
-      mm_aw(acc, vid.dq1 + r0 * XD, XD, rmax, XD, vid.WqT1, XD, 32 * w);
-    else
-      mm_aw(acc, dqkv + r0 * 3 * XD, 3 * XD, rmax, 3 * XD, WcT, 3 * XD, 32 * w);
+  // audio: da += [dq2 | dK1 dV1] . [Wq2 ; Wkv1];  video: dv += dq1 . Wq1.  Each arm owns its accumulators (one
+  // array shared by both arms of the branch is a phi of arrays the compiler puts in scratch memory)
+  auto finish = [&](const f32x4 (&acc)[2][2]) {
     float res[2][2][4];  // all residual loads first: the in-place stores below may alias them
 #pragma unroll
     for (int j = 0; j < 2; ++j)
@@ -596,18 +625,29 @@ __global__ __launch_bounds__(256) void xh_audio_bwd_kernel(int M, const float* _
           if (row < rmax) dst[(r0 + row) * XD + col] = v;
           daL[row * LDA + col] = v;
         }
+  };
+  if (video) {
+    f32x4 acc[2][2];
+    zero(acc);
+    mm_aw<2, 2, 3, XD>(acc, vid.dq1 + r0 * XD, XD, rmax, XD, vid.WqT1, XD, 32 * w);
+    finish(acc);
+  } else {
+    f32x4 acc[2][2];
+    zero(acc);
+    mm_aw<2, 2, 3, 3 * XD>(acc, dqkv + r0 * 3 * XD, 3 * XD, rmax, 3 * XD, WcT, 3 * XD, 32 * w);
+    finish(acc);
   }
   __syncthreads();
   if (!video) {  // da_s = da . Wa
     f32x4 acc[2][2];
     zero(acc);
-    mm_aw(acc, daL, LDA, 32, XD, WaT, XD, 32 * w);
+    mm_aw<2, 2, 3, XD>(acc, daL, LDA, 32, XD, WaT, XD, 32 * w);
     store_acc(acc, 32 * w, nullptr, nullptr, 0, da_s, XD, r0, rmax);
   } else if (vid.dvfeat) {  // dv_feat = dv . Wv, 32-column passes per wave
     for (int c0 = 32 * w; c0 < vid.vdim; c0 += 128) {
       f32x4 acc[2][2];
       zero(acc);
-      mm_aw(acc, daL, LDA, 32, XD, vid.WvT, XD, c0);
+      mm_aw<2, 2, 3, XD>(acc, daL, LDA, 32, XD, vid.WvT, XD, c0);
       store_acc(acc, c0, nullptr, nullptr, 0, vid.dvfeat, vid.vdim, r0, rmax);
     }
   }

@@ -86,19 +86,22 @@ class GradAllReduce:
     chunking, before ``[E, N)``: every rank issues the same sequence of collectives."""
 
     def __init__(self, optimizer, bucket_bytes: int = BUCKET_BYTES, model: Optional[torch.nn.Module] = None,
-                 mask_sync: Optional[bool] = None, early_params=None):
+                 mask_sync: Optional[bool] = None, early_params=None, force: bool = False):
+        """``force``: run the bucket / hook / collective path even in a world of one process (an initialised
+        1-rank group: the RCCL wiring test on a single GPU; the sums are identities)."""
         self.opt = optimizer
         self.bucket_bytes = bucket_bytes
         self.world = dist.get_world_size() if is_dist() else 1
+        self.active = self.world > 1 or (force and dist.is_available() and dist.is_initialized())
         optimizer.grad_scale = 1.0 / self.world
         self._pending = []      # async works launched this step
         self._done = {}         # group index -> flat elements already launched (the early prefix)
         if mask_sync is None:
             mask_sync = bool(getattr(model, "may_skip_grads", lambda: True)()) if model is not None else True
         self.mask_sync = mask_sync
-        if mask_sync and self.world > 1:
+        if mask_sync and self.active:
             cpu_group()
-        if model is not None and self.world > 1:
+        if model is not None and self.active:
             broadcast_module(model)
             with torch.no_grad():  # re-homed trainables: one broadcast per flat buffer
                 for f in optimizer.flat_params():
@@ -143,7 +146,7 @@ class GradAllReduce:
     def grads_ready(self, params=None) -> None:
         """Early hook: the static early prefix has its final local gradients (enqueued on the current stream).
         Launches ``[0, E)`` of every flat buffer (once per step)."""
-        if self.world == 1:
+        if not self.active:
             return
         self._home_prefix()
         for gi, flat in enumerate(self.opt.flat_grads()):
@@ -154,7 +157,7 @@ class GradAllReduce:
 
     def __call__(self) -> None:
         used = self.opt.gather_grads()
-        if self.world == 1:
+        if not self.active:
             self._done = {}
             return
         if self.mask_sync:

@@ -112,3 +112,23 @@ def test_attention_bwd_scratch_kp_matches_library():
     for L in range(1, 193):
         assert fn(L) == K._attn_bwd_kp(L) >= L, L
     assert fn(0) == 0 and fn(193) == 0
+
+
+def test_no_kernel_uses_scratch_memory():
+    """Every gfx950 kernel of libmer_hip.so keeps its private segment at 0 bytes (no register spills or stack arrays
+    in scratch).  A scratch-using kernel on one stream beside a captured graph on another corrupted that graph's
+    results on the GPU box (the xattn head's F1 / G1 beside the prefetched WavLM forward: DESIGN.md section 4b),
+    so scratch-free code is a property of the library, checked from the code objects' metadata."""
+    import importlib.util
+    import shutil
+
+    import pytest
+
+    if not shutil.which("objcopy") or not Path("/opt/rocm/llvm/bin/clang-offload-bundler").exists():
+        pytest.skip("needs objcopy and the ROCm LLVM tools")
+    spec = importlib.util.spec_from_file_location("check_scratch", ROOT / "tools" / "check_scratch.py")
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    ks = mod.kernel_scratch(ROOT / "multimodalemotionrecognition_amd" / "libmer_hip.so")
+    assert len(ks) > 200, len(ks)
+    assert {k: v for k, v in ks.items() if v} == {}

@@ -107,3 +107,47 @@ def test_dp_world2_bit_identical_and_equal_to_mean_gradient_step(tmp_path):
     for a, b in zip(opt.flat_params(), r0["flat"]):
         d = float((a.cpu() - b).abs().max())
         assert torch.equal(a.cpu(), b), f"DP step != mean-gradient step (max|d| {d})"
+
+
+def _worker_rccl1(port, out_dir, use_dp):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1", LOCAL_RANK="0",
+                      HSA_ENABLE_IPC_MODE_LEGACY="0")
+    import torch.distributed as dist
+
+    from multimodalemotionrecognition_amd.dist import GradAllReduce
+    from multimodalemotionrecognition_amd.train import TrainStep, make_loss
+
+    try:
+        torch.cuda.set_device(0)
+        if use_dp:
+            dist.init_process_group(backend="nccl", rank=0, world_size=1)
+        m, opt = _build()
+        sync = None
+        if use_dp:
+            sync = GradAllReduce(opt, model=m, force=True, bucket_bytes=8 << 20)
+            assert sync.active and sync._early_end, "the early head+layer4 bucket must be armed"
+        step = TrainStep(m, opt, make_loss("xattn"), "xattn", sync)
+        for s in range(3):  # eager, capture, replay of the split trunk-backward graphs
+            step(*_batch(0, s))
+        torch.cuda.synchronize()
+        torch.save({"flat": [f.cpu() for f in opt.flat_params()]}, os.path.join(out_dir, f"dp{int(use_dp)}.pt"))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def test_rccl_world1_bucket_path_bitwise(tmp_path):
+    """The RCCL wiring on the device: a world-1 'nccl' (RCCL) group with GradAllReduce forced onto
+    its collective path -- broadcast, the early head+layer4 bucket launched from the trunk-backward hook between the
+    two backward graphs, the remaining buckets, the async works waited on the compute stream -- must leave the
+    training bit-identical to the step without data parallelism (a 1-rank SUM is the identity)."""
+    ctx = mp.get_context("spawn")
+    for use_dp in (False, True):
+        p = ctx.Process(target=_worker_rccl1, args=(_free_port(), str(tmp_path), use_dp))
+        p.start()
+        p.join(timeout=600)
+        assert p.exitcode == 0
+    a = torch.load(tmp_path / "dp0.pt", weights_only=True)["flat"]
+    b = torch.load(tmp_path / "dp1.pt", weights_only=True)["flat"]
+    for x, y in zip(a, b):
+        assert torch.equal(x, y), float((x - y).abs().max())
