@@ -760,5 +760,5 @@ class WavLMAudioEncoder(nn.Module):
         hidden = self.encode_sequence(x, out_dtype=torch.float32) if hidden is None else hidden
         a_emb = self.temporal_pool(hidden)
         h = hip_linear(a_emb, self.classifier[0], act="relu")
-        h = hip_dropout(h, 0.2, self.training)
+        h = hip_dropout(h, float(self.classifier[2].p), self.training)  # the nn.Dropout(0.2) of wavlm_audio.py:58
         return hip_linear(h, self.classifier[3])

@@ -136,9 +136,9 @@ def test_full_model_and_train_step_vs_oracle(mode):
     ref = train_ref.embedding_model_forward(p, mode, video, audio, bn_training=True).detach()
     d = float((out.cpu() - ref).abs().max())
     print(mode, "full-model max|d out|", d, "scale", float(ref.abs().max()))
-    # bf16 encoders vs fp32 oracle (the head is fp32): late = probabilities (measured 3.9e-2: the audio classifier
-    # amplifies the ~1% WavLM embedding error into its logits), concat / gated = logits (measured 9.8e-3 / 9.5e-3)
-    assert d < (1e-1 if mode == "late" else 3e-2), d
+    # bf16 encoders vs fp32 oracle (the head is fp32): late = probabilities (measured 1.75e-3), concat / gated =
+    # logits (measured 9.8e-3 / 9.5e-3)
+    assert d < (5e-3 if mode == "late" else 3e-2), d
 
     m, p = _model_and_oracle(mode)  # fresh running statistics for the step
     opt = build_optimizer(m, lr=1e-3, weight_decay=1e-4)
@@ -152,7 +152,7 @@ def test_full_model_and_train_step_vs_oracle(mode):
     ropt = train_ref.AdamRef([p[n] for n in trainable], lr=1e-3, weight_decay=1e-4)
     rloss = train_ref.train_step_mode(p, trainable, ropt, mode, video, audio, labels)
     print(mode, "train-step loss hip/oracle", float(loss), rloss)
-    assert abs(float(loss) - rloss) < 1e-2  # measured 2.3e-3 / 3.6e-3 (concat / gated, r3a)
+    assert abs(float(loss) - rloss) < 1e-2  # measured 1.7e-3 / 2.3e-3 / 3.6e-3 (late / concat / gated)
     assert pred.shape == (B,) and pred.dtype == torch.int64
     sd = m.state_dict()
     for k in ("video_model.backbone.1.running_mean", "video_model.backbone.7.1.bn2.running_var"):
