@@ -138,9 +138,9 @@ _CACHE: Dict[tuple, SplitPlanes] = {}
 
 
 def planes_for(p: Dict[str, torch.Tensor]) -> SplitPlanes:
-    key = tuple(p[n].data_ptr() for n in ("audio_seq_proj.weight", "a_in_proj.weight", "a2v_attn.in_proj_weight",
-                                          "v2a_attn.in_proj_weight", "v_in_proj.weight", "v2a_attn.out_proj.weight",
-                                          "a2v_attn.out_proj.weight"))
+    key = tuple((p[n].data_ptr(), tuple(p[n].shape)) for n in (
+        "audio_seq_proj.weight", "a_in_proj.weight", "a2v_attn.in_proj_weight", "v2a_attn.in_proj_weight",
+        "v_in_proj.weight", "v2a_attn.out_proj.weight", "a2v_attn.out_proj.weight"))
     sp = _CACHE.get(key)
     if sp is None:
         if len(_CACHE) > 8:
@@ -167,6 +167,7 @@ def fused_forward(p, cfg, v_feat, a_seq, training, rng, ctx, sites):
     sp = planes_for(p)
     sp.refresh(transposed=training)  # a training forward is followed by the fused backward
     ctx.planes_gen = sp.gen
+    ctx.planes = sp  # a captured graph writes through sp's descriptors: keep them alive as long as the context
     vf = v_feat.reshape(B * T, vd).contiguous()
     af = a_seq.reshape(B * Ta, sd).contiguous()
     a_s, a, q2, kv1 = e(B * Ta, d), e(B * Ta, d), e(B * Ta, d), e(B * Ta, 2 * d)
@@ -243,7 +244,7 @@ def fused_backward(p, ctx, dlogits, grads, need_dv_feat=True):
     f32 = torch.float32
     e = lambda *shape: torch.empty(shape, device=dev, dtype=f32)  # noqa: E731
     from .xattn_head import SITE_A2V, SITE_APATH, SITE_MLP, SITE_V2A, SITE_VPATH
-    sp = planes_for(p)
+    sp = getattr(ctx, "planes", None) or planes_for(p)
     if sp.t_gen != getattr(ctx, "planes_gen", None):  # the forward did not split them (eval-mode forward)
         sp.refresh_transposed()
     dlogits = dlogits.contiguous()
