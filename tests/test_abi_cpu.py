@@ -114,11 +114,7 @@ def test_attention_bwd_scratch_kp_matches_library():
     assert fn(0) == 0 and fn(193) == 0
 
 
-def test_no_kernel_uses_scratch_memory():
-    """Every gfx950 kernel of libmer_hip.so keeps its private segment at 0 bytes (no register spills or stack arrays
-    in scratch).  A scratch-using kernel on one stream beside a captured graph on another corrupted that graph's
-    results on the GPU box (the xattn head's F1 / G1 beside the prefetched WavLM forward: DESIGN.md section 4b),
-    so scratch-free code is a property of the library, checked from the code objects' metadata."""
+def _codeobj_tool():
     import importlib.util
     import shutil
 
@@ -126,9 +122,24 @@ def test_no_kernel_uses_scratch_memory():
 
     if not shutil.which("objcopy") or not Path("/opt/rocm/llvm/bin/clang-offload-bundler").exists():
         pytest.skip("needs objcopy and the ROCm LLVM tools")
-    spec = importlib.util.spec_from_file_location("check_scratch", ROOT / "tools" / "check_scratch.py")
+    _ensure_built()
+    spec = importlib.util.spec_from_file_location("check_codeobj", ROOT / "tools" / "check_codeobj.py")
     mod = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mod)
-    ks = mod.kernel_scratch(ROOT / "multimodalemotionrecognition_amd" / "libmer_hip.so")
+    return mod
+
+
+def test_no_kernel_uses_scratch_memory():
+    """Every gfx950 kernel of libmer_hip.so keeps its private segment at 0 bytes (no register spills or stack arrays
+    in scratch), checked from the code objects' metadata."""
+    ks = _codeobj_tool().kernel_scratch(ROOT / "multimodalemotionrecognition_amd" / "libmer_hip.so")
     assert len(ks) > 200, len(ks)
     assert {k: v for k, v in ks.items() if v} == {}
+
+
+def test_no_packed_fp32_instructions():
+    """No v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32 in any gfx950 kernel (the Makefile turns the feature off): on the
+    MI355X boxes kernels using them returned different results while the fused head's kernels ran on the same CUs
+    from another stream (the GPU regression is tests/test_concurrency_gpu.py)."""
+    pk = _codeobj_tool().packed_fp32_sites(ROOT / "multimodalemotionrecognition_amd" / "libmer_hip.so")
+    assert pk == {}, sorted(pk.items(), key=lambda kv: -kv[1])[:10]
