@@ -4,6 +4,7 @@
 #include "mer.h"
 
 typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;
+typedef __attribute__((ext_vector_type(8))) float f32x8;
 
 // ---------------------------------------------------------------------------------------
 // Feature-extractor layer 0 (TF:723-745): conv0 = Conv1d(1, 512, k=10, s=5, bias=False) on the raw
@@ -256,13 +257,34 @@ MER_API int mer_layernorm_tr(int rows, int d, const void* x, int x_dtype, long l
 // register per lane, and the accumulator tiles ARE the B operand of O^T = V^T P^T on
 // v_mfma_f32_16x16x16_bf16 (k = 4*(lane>>4) + e) -- P never goes through LDS.
 // ---------------------------------------------------------------------------------------
+// Phase timestamps for tuning (tools/attn_phases.py builds a separate library with -DMER_ATTN_TIMING; the production
+// library compiles AT() to nothing): wall_clock64() of each block's thread 0 at phase k.
+#ifdef MER_ATTN_TIMING
+static __device__ long long mer_at_buf[2048 * 8];
+#define AT(k) \
+  do { \
+    if (threadIdx.x == 0 && blockIdx.x < 2048) mer_at_buf[blockIdx.x * 8 + (k)] = wall_clock64(); \
+  } while (0)
+MER_API int mer_at_read(long long* host) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(mer_at_buf), sizeof(long long) * 2048 * 8, 0, hipMemcpyDeviceToHost);
+}
+#else
+#define AT(k) \
+  do { \
+  } while (0)
+#endif
+
 namespace {
 constexpr int ADH = 64, APAD = ADH + 8;
 typedef __attribute__((ext_vector_type(4))) short s16x4;
 }
 
-template <int NW>
-__global__ __launch_bounds__(64 * NW) void wavlm_attn_kernel(int L, int H, const bf16_t* __restrict__ qkv, long ldqkv,
+// KT: key tiles held in registers (compile time, >= ceil(L / 16)): 10 for L <= 160 (the 3 s clips: L = 149), 16 up to
+// L = 256.  NW waves per block, one 16-row query tile each.  (Waves owning 2 tiles so that one 8-wave block stages
+// K / V once per (b, h) need > 128 VGPRs -- 3 waves per SIMD, one such block per CU -- or spill: measured no gain.)
+template <int NW, int KT>
+__global__ __launch_bounds__(64 * NW) void wavlm_attn_kernel(
+    int L, int H, const bf16_t* __restrict__ qkv, long ldqkv,
                                                          const bf16_t* __restrict__ x, long ldx,
                                                          const float* __restrict__ gw, const float* __restrict__ gb,
                                                          const float* __restrict__ gconst,
@@ -273,54 +295,54 @@ __global__ __launch_bounds__(64 * NW) void wavlm_attn_kernel(int L, int H, const
                                                          unsigned long long site, const long long* __restrict__ skip,
                                                          int skip_bit) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  AT(0);
+#ifdef MER_ATTN_TIMING
+  if (threadIdx.x == 0 && blockIdx.x < 2048)  // HW_ID (wave / SIMD / CU / SE) and XCC_ID of wave 0
+    mer_at_buf[blockIdx.x * 8 + 7] = ((long long)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32) |
+                                     (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);
+#endif
   if (skip && ((*skip >> skip_bit) & 1ll)) return;
-  const int LP = (L + 15) / 16 * 16;
-  const int VTP = LP + 8;
-  bf16_t* Ks = reinterpret_cast<bf16_t*>(smem_raw);   // [LP][APAD]
-  bf16_t* Vt = Ks + LP * APAD;                        // [ADH][VTP]
-  float* gate = reinterpret_cast<float*>(Vt + ADH * VTP);  // [NW][16]
-  float* gws = gate + 16 * NW;                         // [8][64] gru_rel_pos_linear weight
-  float* tbl = gws + 512;                              // [2L-1]
-  // one-dimensional grid, XCD-aware: the row blocks of one (b, h) run on one XCD and share its K / V in L2
+  constexpr int KP = 16 * KT;  // keys held (zero rows / columns past L)
+  constexpr int VTP = KP + 8;
+  const int NTL = (L + 15) / 16;  // query tiles
+  bf16_t* Ks = reinterpret_cast<bf16_t*>(smem_raw);   // [KP][APAD]
+  bf16_t* Vt = Ks + KP * APAD;                        // [ADH][VTP]
+  // this head's relative-position bias row, tbl[16 + r] = bias(r - (L - 1)) for r in [0, 2L-1), zero padding of 16
+  // entries before and KP - L after: every (i < 16 NTL, j < KP) reads tbl[16 + j - i + L - 1] without clamping
+  // (padding values only reach masked scores)
+  float* tbl = reinterpret_cast<float*>(Vt + ADH * VTP);
   constexpr int NTH = 64 * NW;
-  constexpr int KIT = (256 * 8 + NTH - 1) / NTH, VIT = (512 + NTH - 1) / NTH, TIT = (512 + NTH - 1) / NTH;
-  const int nrb = (LP / 16 + NW - 1) / NW;
+  constexpr int KIT = (KP * 8 + NTH - 1) / NTH, VIT = (KP * 2 + NTH - 1) / NTH;
+  constexpr int TIT = (16 + 2 * 256 + KP + NTH - 1) / NTH;  // table entries (L <= 256) per thread
+  // one-dimensional grid, XCD-aware: the row blocks of one (b, h) run on one XCD and share its K / V in L2
+  const int nrb = (NTL + NW - 1) / NW;
   int rbk, bh;
   xcd_tile(blockIdx.x, nrb, gridDim.x, rbk, bh);  // gridDim.x = nrb * B * H
   const int b = bh / H, h = bh % H;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int D = H * ADH;
-  const int rb = rbk * NW + w;      // this wave's 16-row query tile
-  const bool active = rb * 16 < L;  // wave-uniform
+  const int rb = rbk * NW + w;  // this wave's 16-row query tile
 
   // Loads are unconditional from clamped (valid) rows, zeroed by a select at the LDS store: a load under a
   // per-lane condition compiles to a branch around it and a wait for it, serialising the prologue's loads.
-  // This wave's Q fragments first (B operand of S^T = K Q^T: Q[i = lane&15][d = kk*32 + 8*(lane>>4) ..]); rows
-  // past L read row L - 1 (their outputs are never stored)
-  bf16x8 qb[2];
-  {
-    const int qrow = min(rb * 16 + (lane & 15), L - 1);
+  // Prologue: the 8 gru_rel_pos_linear weight rows as MFMA A fragments (row n = lane&15 < 8, zero above; split
+  // into bf16 hi + lo at use), the relative-position bias row of this head (precomputed table [H][2L-1] when
+  // bucket == nullptr, else gathered through the bucket index), K (row-major 16-byte chunks) and V (4-row groups
+  // for the V^T image); rows >= L are zero.
+  const int gn = lane & 15;
+  f32x4 gwr[2][2];
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-      qb[kk] = *reinterpret_cast<const bf16x8*>(qkv + ((long)b * L + qrow) * ldqkv + h * ADH + kk * 32 + (lane >> 4) * 8);
+  for (int kk = 0; kk < 2; ++kk) {
+    const float* wp = gw + (gn < 8 ? gn : 7) * ADH + kk * 32 + (lane >> 4) * 8;
+    gwr[kk][0] = *reinterpret_cast<const f32x4*>(wp);
+    gwr[kk][1] = *reinterpret_cast<const f32x4*>(wp + 4);
   }
-  // Every global load of the prologue is issued before the first LDS store: K (row-major 16-byte chunks),
-  // V (4-row groups for the V^T image), the relative-position bias row of this head (precomputed table
-  // [H][2L-1] when bucket == nullptr, else gathered through the bucket index), gru_rel_pos_linear's weight
-  // and the x slices of this wave's 16 gate rows.  Rows >= L are zero.
-  const int sub = lane >> 3, cl = lane & 7;
-  u32x4 xg[2];
-#pragma unroll
-  for (int it = 0; it < 2; ++it) {
-    const int i = min(rb * 16 + it * 8 + sub, L - 1);
-    xg[it] = *reinterpret_cast<const u32x4*>(x + ((long)b * L + i) * ldx + h * ADH + cl * 8);
-  }
-  float tb[TIT], gwv[TIT];
+  const int ntbl = 16 + 2 * L - 1 + (KP - L);
+  float tb[TIT];
 #pragma unroll
   for (int k = 0; k < TIT; ++k) {
-    const int r = min(t + NTH * k, 2 * L - 2);
+    const int r = min(max(t + NTH * k - 16, 0), 2 * L - 2);
     tb[k] = bucket ? rel_emb[(long)bucket[r] * H + h] : rel_emb[(long)h * (2 * L - 1) + r];
-    gwv[k] = gw[min(t + NTH * k, 511)];  // 512 = 8 x 64 weights
   }
   {
     u32x4 kr[KIT];
@@ -339,21 +361,21 @@ __global__ __launch_bounds__(64 * NW) void wavlm_attn_kernel(int L, int H, const
         vr[it][e] = *reinterpret_cast<const u32x4*>(qkv + ((long)b * L + row) * ldqkv + 2 * D + h * ADH + ch * 8);
       }
     }
+    AT(1);
 #pragma unroll
     for (int k = 0; k < TIT; ++k) {
       const int r = t + NTH * k;
-      if (r < 2 * L - 1) tbl[r] = tb[k];
-      if (r < 512) gws[r] = gwv[k];
+      if (r < ntbl) tbl[r] = (r >= 16 && r < 16 + 2 * L - 1) ? tb[k] : 0.f;
     }
 #pragma unroll
     for (int it = 0; it < KIT; ++it) {
       const int c = t + it * NTH, row = c >> 3, ch = c & 7;
-      if (c < LP * 8) *reinterpret_cast<u32x4*>(&Ks[row * APAD + ch * 8]) = row < L ? kr[it] : u32x4{0u, 0u, 0u, 0u};
+      if (c < KP * 8) *reinterpret_cast<u32x4*>(&Ks[row * APAD + ch * 8]) = row < L ? kr[it] : u32x4{0u, 0u, 0u, 0u};
     }
 #pragma unroll
     for (int it = 0; it < VIT; ++it) {
       const int q = t + it * NTH, rq = q >> 3, ch = q & 7;
-      if (q < LP * 2) {
+      if (q < KP * 2) {
 #pragma unroll
         for (int e = 0; e < 4; ++e)
           if (rq * 4 + e >= L) vr[it][e] = u32x4{0u, 0u, 0u, 0u};
@@ -367,127 +389,152 @@ __global__ __launch_bounds__(64 * NW) void wavlm_attn_kernel(int L, int H, const
       }
     }
   }
-  __syncthreads();
-  if (!active) return;
-  // gate of this wave's 16 rows (fp32): 8 lanes per row, each lane one 16-byte chunk (8 channels) of x and
-  // the matching 8x8 block of the weight (from LDS); the 8 projections are summed over the row's lanes
-  {
-    float gwr[8][8];
+  // the gate weights as split bf16 A fragments (kept for every tile of this wave)
+  bf16x8 whi[2], wlo[2];
 #pragma unroll
-    for (int o = 0; o < 8; ++o) {
-      const f32x4 lo = *reinterpret_cast<const f32x4*>(&gws[o * ADH + cl * 8]);
-      const f32x4 hi = *reinterpret_cast<const f32x4*>(&gws[o * ADH + cl * 8 + 4]);
-      gwr[o][0] = lo[0]; gwr[o][1] = lo[1]; gwr[o][2] = lo[2]; gwr[o][3] = lo[3];
-      gwr[o][4] = hi[0]; gwr[o][5] = hi[1]; gwr[o][6] = hi[2]; gwr[o][7] = hi[3];
-    }
-    const float gbs0 = gb[0] + gb[1] + gb[2] + gb[3], gbs1 = gb[4] + gb[5] + gb[6] + gb[7];
-    const float gc = gconst[h];
-#pragma unroll
-    for (int it = 0; it < 2; ++it) {
-      const int ri = it * 8 + sub, i = rb * 16 + ri;
-      float pr[8];
-#pragma unroll
-      for (int o = 0; o < 8; ++o) pr[o] = 0.f;
-      const bf16_t* xh = reinterpret_cast<const bf16_t*>(&xg[it]);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float xe = bf2f(xh[e]);
-#pragma unroll
-        for (int o = 0; o < 8; ++o) pr[o] += xe * gwr[o][e];
-      }
-#pragma unroll
-      for (int o = 0; o < 8; ++o) {
-        pr[o] += __shfl_xor(pr[o], 1, 64);
-        pr[o] += __shfl_xor(pr[o], 2, 64);
-        pr[o] += __shfl_xor(pr[o], 4, 64);
-      }
-      if (cl == 0) {
-        float gsum = 1.f;
-        if (i < L) {
-          const float ga = 1.f / (1.f + __expf(-(pr[0] + pr[1] + pr[2] + pr[3] + gbs0)));
-          const float gbv = 1.f / (1.f + __expf(-(pr[4] + pr[5] + pr[6] + pr[7] + gbs1)));
-          gsum = ga * (gbv * gc - 1.f) + 2.f;
-        }
-        gate[w * 16 + ri] = gsum;
-      }
-    }
+  for (int kk = 0; kk < 2; ++kk) {
+    const f32x4 z = f32x4{0.f, 0.f, 0.f, 0.f};
+    const f32x8 wv = __builtin_shufflevector(gn < 8 ? gwr[kk][0] : z, gn < 8 ? gwr[kk][1] : z, 0, 1, 2, 3, 4, 5, 6, 7);
+    whi[kk] = __builtin_convertvector(wv, bf16x8);
+    wlo[kk] = __builtin_convertvector(wv - __builtin_convertvector(whi[kk], f32x8), bf16x8);
   }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const float gc = gconst[h];
+  const unsigned long long dseed = mer_site_seed(seed_ptr, site);
+  // the dropout mask's seed mix (mer_hash), the keep threshold on the hash's top 24 bits (u = (h >> 8) / 2^24 >= p
+  // exactly when (h >> 8) >= ceil(p 2^24)) and whether every mask index ((b*H+h)*L + i)*L + j fits 32 bits
+  const uint32_t hseed = (uint32_t)dseed ^ ((uint32_t)(dseed >> 32) * 0x85EBCA6Bu);
+  const uint32_t keep_thr = (uint32_t)ceilf(drop_p * 16777216.0f);
+  const bool idx32 = (unsigned long long)(gridDim.x / nrb) * (unsigned long long)L * (unsigned long long)L < (1ull << 32);
+  __syncthreads();
+  AT(2);
 
-  const int NT = LP / 16;  // key tiles
-  const int i = rb * 16 + (lane & 15);
-  const float gi = gate[w * 16 + (lane & 15)];
-  // S^T tiles: s[ct][r] = S[i][j = ct*16 + 4*(lane>>4) + r]
-  f32x4 s[16];
+  if (rb < NTL) {  // wave-uniform
+    // this tile's Q (B operand of S^T = K Q^T) and x rows (B operand of the gate product): Q[i = lane&15][d =
+    // kk*32 + 8*(lane>>4) ..]; rows past L read row L - 1 (their outputs are never stored)
+    const int qrow = min(rb * 16 + (lane & 15), L - 1);
+    bf16x8 qb[2], xb[2];
 #pragma unroll
-  for (int ct = 0; ct < 16; ++ct) s[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int kk = 0; kk < 2; ++kk) {
+      qb[kk] = *reinterpret_cast<const bf16x8*>(qkv + ((long)b * L + qrow) * ldqkv + h * ADH + kk * 32 + (lane >> 4) * 8);
+      xb[kk] = *reinterpret_cast<const bf16x8*>(x + ((long)b * L + qrow) * ldx + h * ADH + kk * 32 + (lane >> 4) * 8);
+    }
+    // gate of the tile's 16 rows: the 8 gru_rel_pos_linear outputs G^T[n][i] = sum_k W[n][k] x[i][k] on MFMA (the
+    // fp32 weight split into bf16 hi + lo; x is exact bf16).  Lane (i = lane&15, group q = lane>>4) holds outputs
+    // n = 4q .. 4q+3 of row i: group 0 sums a_i (TF:163-177 .view(.., 2, 4).sum(-1)), group 1 b_i.
+    const int i = rb * 16 + (lane & 15);
+    float gi;
+    {
+      f32x4 g = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int kk = 0; kk < 2; ++kk)
+      for (int kk = 0; kk < 2; ++kk) {
+        g = __builtin_amdgcn_mfma_f32_16x16x32_bf16(whi[kk], xb[kk], g, 0, 0, 0);
+        g = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wlo[kk], xb[kk], g, 0, 0, 0);
+      }
+      // sum_{r} (z + b) in the order of the stage-2 backward's recompute (wavlm_train.hip), so a trainable layer's
+      // backward differentiates exactly the gate its forward applied
+      float zs = 0.f;
 #pragma unroll
-    for (int ct = 0; ct < 16; ++ct)
-      if (ct < NT) {
+      for (int r = 0; r < 4; ++r) zs += g[r] + gb[(4 * (lane >> 4) + r) & 7];
+      const float ga = 1.f / (1.f + __expf(-__shfl(zs, lane & 15, 64)));
+      const float gbv = 1.f / (1.f + __expf(-__shfl(zs, 16 + (lane & 15), 64)));
+      gi = i < L ? ga * (gbv * gc - 1.f) + 2.f : 1.f;
+    }
+    AT(3);
+    // S^T tiles: s[ct][r] = S[i][j = ct*16 + 4*(lane>>4) + r]; key tiles past L are zero rows of Ks (LDS sized for
+    // KT tiles), masked to -inf below
+    f32x4 s[KT];
+#pragma unroll
+    for (int ct = 0; ct < KT; ++ct) s[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int ct = 0; ct < KT; ++ct) {
         const bf16x8 ka = *reinterpret_cast<const bf16x8*>(&Ks[(ct * 16 + (lane & 15)) * APAD + kk * 32 + (lane >> 4) * 8]);
         s[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka, qb[kk], s[ct], 0, 0, 0);
       }
-  float mx = -INFINITY;
+    float mx = -INFINITY;
+    const float* trow = tbl + 16 + (lane >> 4) * 4 - i + L - 1;  // + j - 4*(lane>>4) = ct*16 + r
 #pragma unroll
-  for (int ct = 0; ct < 16; ++ct)
-    if (ct < NT)
+    for (int ct = 0; ct < KT; ++ct) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int j = ct * 16 + (lane >> 4) * 4 + r;
-        int rel = j - i + L - 1;
-        rel = rel < 0 ? 0 : (rel > 2 * L - 2 ? 2 * L - 2 : rel);
-        const float v = j < L ? s[ct][r] * scale + gi * tbl[rel] : -INFINITY;
-        s[ct][r] = v;
-        mx = fmaxf(mx, v);
+      for (int r = 0; r < 4; ++r) s[ct][r] = s[ct][r] * scale + gi * trow[ct * 16 + r];
+      if (ct * 16 + 15 >= L) {  // (wave-uniform) the tile holds keys past L
+#pragma unroll
+        for (int r = 0; r < 4; ++r) s[ct][r] = ct * 16 + (lane >> 4) * 4 + r < L ? s[ct][r] : -INFINITY;
       }
-  mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-  // P^T = exp(S^T - max) rounded to bf16 (the weights that enter PV also form the normaliser).  Train mode:
-  // attention-probability dropout (F.multi_head_attention_forward dropout_p, TF:206-228): dropped weights do
-  // not enter PV, the kept ones are rescaled by 1/(1-p) with the normaliser (mask index ((b*H+h)*L + i)*L + j)
-  const unsigned long long dseed = mer_site_seed(seed_ptr, site);
-  const long mrow = (((long)b * H + h) * L + i) * L;
-  float sum = 0.f;
-  s16x4 pb[16];
 #pragma unroll
-  for (int ct = 0; ct < 16; ++ct)
-    if (ct < NT)
+      for (int r = 0; r < 4; ++r) mx = fmaxf(mx, s[ct][r]);
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    AT(4);
+    // P^T = exp(S^T - max) rounded to bf16 (the weights that enter PV also form the normaliser).  Train mode:
+    // attention-probability dropout (F.multi_head_attention_forward dropout_p, TF:206-228): dropped weights do
+    // not enter PV, the kept ones are rescaled by 1/(1-p) with the normaliser (mask index ((b*H+h)*L + i)*L + j)
+    const long mrow = (((long)b * H + h) * L + i) * L;
+    float sum = 0.f;
+    s16x4 pb[KT];
+#pragma unroll
+    for (int ct = 0; ct < KT; ++ct)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const bf16_t p = f2bf(__expf(s[ct][r] - mx));
         sum += bf2f(p);
-        const int j = ct * 16 + (lane >> 4) * 4 + r;
-        const bool keep = drop_p <= 0.f || dropout_scale(dseed, (uint64_t)(mrow + j), drop_p) != 0.f;
-        pb[ct][r] = keep ? (short)p : (short)0;
+        pb[ct][r] = (short)p;
       }
-  sum += __shfl_xor(sum, 16, 64);
-  sum += __shfl_xor(sum, 32, 64);
-  // O^T[d][i] = sum_j V^T[d][j] P^T[j][i]: A = V^T (d = lane&15, j = ct*16 + 4*(lane>>4) + e)
-  f32x4 o[4];
+    if (drop_p > 0.f) {  // (uniform) the keep mask: dropout_scale(dseed, mrow + j, p) != 0
+      if (idx32) {
+        // every mask index is < 2^32: mer_hash's first product distributes over mrow + j, so the per-element work
+        // is one add + the two-multiply finaliser and an integer threshold -- the same bits as dropout_scale
+        const uint32_t xb0 = (uint32_t)mrow * 0x9E3779B9u + hseed + (uint32_t)((lane >> 4) * 4) * 0x9E3779B9u;
 #pragma unroll
-  for (int dt = 0; dt < 4; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int ct = 0; ct < KT; ++ct)
 #pragma unroll
-  for (int ct = 0; ct < 16; ++ct)
-    if (ct < NT)
+          for (int r = 0; r < 4; ++r) {
+            uint32_t xh = xb0 + (uint32_t)(ct * 16 + r) * 0x9E3779B9u;
+            xh ^= xh >> 16;
+            xh *= 0x7FEB352Du;
+            xh ^= xh >> 15;
+            xh *= 0x846CA68Bu;
+            xh ^= xh >> 16;
+            if ((xh >> 8) < keep_thr) pb[ct][r] = 0;
+          }
+      } else {
+#pragma unroll
+        for (int ct = 0; ct < KT; ++ct)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int j = ct * 16 + (lane >> 4) * 4 + r;
+            if (dropout_scale(dseed, (uint64_t)(mrow + j), drop_p) == 0.f) pb[ct][r] = 0;
+          }
+      }
+    }
+    sum += __shfl_xor(sum, 16, 64);
+    sum += __shfl_xor(sum, 32, 64);
+    AT(5);
+    // O^T[d][i] = sum_j V^T[d][j] P^T[j][i]: A = V^T (d = lane&15, j = ct*16 + 4*(lane>>4) + e)
+    f32x4 o[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ct = 0; ct < KT; ++ct)
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
         const s16x4 va = *reinterpret_cast<const s16x4*>(&Vt[(dt * 16 + (lane & 15)) * VTP + ct * 16 + (lane >> 4) * 4]);
         o[dt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(va, pb[ct], o[dt], 0, 0, 0);
       }
-  if (i < L) {
-    const float inv = (drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f) / sum;
-    bf16_t* orow = out + ((long)b * L + i) * ldo + h * ADH + (lane >> 4) * 4;
+    if (i < L) {
+      const float inv = (drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f) / sum;
+      bf16_t* orow = out + ((long)b * L + i) * ldo + h * ADH + (lane >> 4) * 4;
 #pragma unroll
-    for (int dt = 0; dt < 4; ++dt) {
-      const uint32_t lo = (uint32_t)f2bf(o[dt][0] * inv) | ((uint32_t)f2bf(o[dt][1] * inv) << 16);
-      const uint32_t hi = (uint32_t)f2bf(o[dt][2] * inv) | ((uint32_t)f2bf(o[dt][3] * inv) << 16);
-      *reinterpret_cast<uint2*>(orow + dt * 16) = uint2{lo, hi};
+      for (int dt = 0; dt < 4; ++dt) {
+        const uint32_t lo = (uint32_t)f2bf(o[dt][0] * inv) | ((uint32_t)f2bf(o[dt][1] * inv) << 16);
+        const uint32_t hi = (uint32_t)f2bf(o[dt][2] * inv) | ((uint32_t)f2bf(o[dt][3] * inv) << 16);
+        *reinterpret_cast<uint2*>(orow + dt * 16) = uint2{lo, hi};
+      }
     }
   }
+  AT(6);
 }
 
 MER_API int mer_wavlm_attention(int B, int L, int H, const void* qkv, long ldqkv, const void* x, long ldx,
@@ -513,21 +560,28 @@ MER_API int mer_wavlm_attention_tr(int B, int L, int H, const void* qkv, long ld
     const char* e = getenv("MER_ATTN_NW");
     return e ? atoi(e) : 0;
   }();
-  // 5 waves (80 query rows) per block: 2 blocks per (b, h) at L = 149, 3 blocks per CU -> the B*H*2 blocks run in
-  // one round (4 waves: 3 blocks per (b, h), 1.5 rounds; 10 waves: one block per CU); bench.py A/B +1.5% / +1%
+  // 5 waves (80 query rows) per block: 2 blocks per (b, h) at L = 149.  The workgroup's waves land on SIMDs
+  // 0,1,2,3,0, so SIMD 0 holds 2 of every block: at <= 4 waves per SIMD 2 blocks run per CU (the 768 blocks of
+  // B = 32 in 2 rounds).  MER_ATTN_NW=4 / 10 are the A/B alternatives.
   const int NWsel = nw_env == 5 || nw_env == 10 || nw_env == 4 ? nw_env : 5;
-#define MER_ATTN_LAUNCH(NW)                                                                                       \
+#define MER_ATTN_LAUNCH(NW, KT)                                                                                   \
   do {                                                                                                           \
-    const size_t lds = sizeof(bf16_t) * ((size_t)LP * APAD + (size_t)ADH * (LP + 8)) +                           \
-                       sizeof(float) * (16 * NW + 512 + 2 * L);                                                   \
-    hipLaunchKernelGGL(wavlm_attn_kernel<NW>, dim3(B * H * ((LP / 16 + NW - 1) / NW)), dim3(64 * NW), lds,         \
+    const size_t lds = sizeof(bf16_t) * ((size_t)16 * KT * APAD + (size_t)ADH * (16 * KT + 8)) +                 \
+                       sizeof(float) * (16 + 2 * L + 16 * KT);                                                    \
+    hipLaunchKernelGGL((wavlm_attn_kernel<NW, KT>), dim3(B * H * ((LP / 16 + NW - 1) / NW)), dim3(64 * NW), lds,   \
                        (hipStream_t)stream, L, H, (const bf16_t*)qkv, ldqkv, (const bf16_t*)x, ldx, gate_w, gate_b, \
                        gate_const, rel_emb, bucket, (bf16_t*)out, ldo, scale, drop_p, seed, site, skip_mask,      \
                        skip_bit);                                                                                 \
   } while (0)
-  if (NWsel == 10) MER_ATTN_LAUNCH(10);
-  else if (NWsel == 5) MER_ATTN_LAUNCH(5);
-  else MER_ATTN_LAUNCH(4);
+  if (LP <= 160) {  // 10 key tiles in registers: the 3 s clip (L = 149)
+    if (NWsel == 10) MER_ATTN_LAUNCH(10, 10);
+    else if (NWsel == 5) MER_ATTN_LAUNCH(5, 10);
+    else MER_ATTN_LAUNCH(4, 10);
+  } else {
+    if (NWsel == 10) MER_ATTN_LAUNCH(10, 16);
+    else if (NWsel == 5) MER_ATTN_LAUNCH(5, 16);
+    else MER_ATTN_LAUNCH(4, 16);
+  }
 #undef MER_ATTN_LAUNCH
   MER_LAUNCH_CHECK();
 }

@@ -1,0 +1,60 @@
+"""Standalone timing of the WavLM gated-rel-pos attention kernel at the C2 shape (B=32, L=149, 12 heads): eval and
+train mode (p = 0.1 dropout), HIP events around a captured graph of back-to-back launches on an otherwise idle GPU.
+    MER_ATTN_NW=4|5|10 python tools/bench_attn.py [--iters 200] [--batch 32]"""
+import argparse
+import os
+import sys
+from pathlib import Path
+
+import torch
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=200)
+    ap.add_argument("--batch", type=int, default=32)
+    args = ap.parse_args()
+    from multimodalemotionrecognition_amd import kernels as K
+
+    B, L, H, D = args.batch, 149, 12, 768
+    g = torch.Generator(device="cuda").manual_seed(0)
+    qkv = (torch.randn(B * L, 3 * D, device="cuda", generator=g) * 0.5).to(torch.bfloat16)
+    x = torch.randn(B * L, D, device="cuda", generator=g).to(torch.bfloat16)
+    gw = torch.randn(8, 64, device="cuda", generator=g) * 0.1
+    gb = torch.zeros(8, device="cuda")
+    gc = torch.ones(H, device="cuda")
+    tbl = torch.randn(H, 2 * L - 1, device="cuda", generator=g)
+    out = torch.empty(B * L, D, device="cuda", dtype=torch.bfloat16)
+    rng = torch.full((1,), 77, dtype=torch.int64, device="cuda")
+    flop = 4.0 * B * H * L * L * 64
+    for mode, p in (("eval", 0.0), ("train", 0.1)):
+        run = lambda: K.wavlm_attention(qkv, x, gw, gb, gc, tbl, None, out, B, L, H, 0.125, drop_p=p,  # noqa: E731
+                                        rng=rng if p > 0 else None)
+        for _ in range(10):
+            run()
+        torch.cuda.synchronize()
+        # the launches are captured in one graph: from Python each ctypes launch costs ~20 us of host time, which
+        # would bound a plain loop
+        g = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.graph(g, stream=s):
+            for _ in range(args.iters):
+                run()
+        torch.cuda.current_stream().wait_stream(s)
+        g.replay()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        g.replay()
+        e1.record()
+        torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) / args.iters * 1e3
+        print(f"wavlm attention B={B} L={L} {mode} NW={os.environ.get('MER_ATTN_NW', 'default')}: {us:.1f} us "
+              f"({flop / us / 1e6:.1f} TF/s)", flush=True)
+
+
+if __name__ == "__main__":
+    main()
