@@ -14,7 +14,7 @@ run() {
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "STOP after $name"; exit $rc; fi
   return 0
 }
-run pytest 800 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread
+run pytest 900 python -u -m pytest tests -m gpu -q --timeout 200 --timeout-method thread
 run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('SMOKE_OK')"
 run bench 600 python -u bench.py
 cd /tmp && export TMPDIR=/tmp

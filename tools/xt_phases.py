@@ -18,7 +18,8 @@ def build():
     csrc = PKG / "csrc"
     out = csrc / "build" / "xt"
     out.mkdir(parents=True, exist_ok=True)
-    flags = ["--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17", "-DMER_XH_TIMING", f"-I{ROOT / 'include'}"]
+    flags = ["--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17", "-DMER_XH_TIMING", f"-I{ROOT / 'include'}",
+             "-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops"]
     xt_objs = []
     for name in ("xattn_fused", "xattn_fused_bwd"):
         o = out / f"{name}.o"
