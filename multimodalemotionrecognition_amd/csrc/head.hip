@@ -458,60 +458,95 @@ __device__ __forceinline__ bool argmax_better(float v, int i, float bv, int bi, 
   if (vn) return i < bi;
   return v > bv || (v == bv && i < bi);
 }
+// One group of G lanes (G = pow2 >= C, at most 64; a lane loops over classes g, g + G, .. past that) per row, 256 / G
+// rows in flight per pass: the rows' loads are issued together (one memory latency for B * C logits instead of B
+// serial ones).  Per-row loss terms are summed in row order by thread 0 (deterministic).
+template <int G>
 __global__ __launch_bounds__(256) void ce_kernel(int B, int C, const float* __restrict__ logits,
                                                  const long long* __restrict__ labels, float eps_ls, int late,
                                                  float* __restrict__ loss, float* __restrict__ dlogits,
                                                  long long* __restrict__ preds) {
-  __shared__ float part[4];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  float acc = 0.f;
-  for (int b = w; b < B; b += 4) {
-    const float* z = logits + (long)b * C;
-    const long long y = labels[b];
+  constexpr int RPB = 256 / G;  // rows per pass
+  __shared__ float rl[RPB];
+  __shared__ float total;
+  const int g = threadIdx.x % G, rg = threadIdx.x / G;
+  if (threadIdx.x == 0) total = 0.f;
+  for (int b0 = 0; b0 < B; b0 += RPB) {
+    const int b = b0 + rg;
+    const bool rv = b < B;
+    const float* z = logits + (long)(rv ? b : B - 1) * C;
+    const long long y = labels[rv ? b : B - 1];
+    float term = 0.f;
     if (preds) {  // top-1 as torch.argmax: NaN counts as the maximum, the lowest index wins among equals
       float bv = 0.f;
-      int bi = C;  // C = no candidate yet
-      for (int c = lane; c < C; c += 64)
+      int bi = C;  // C = no candidate
+      for (int c = g; c < C; c += G)
         if (argmax_better(z[c], c, bv, bi, C)) { bv = z[c]; bi = c; }
-      for (int off = 32; off > 0; off >>= 1) {
-        const float ov = __shfl_xor(bv, off);
-        const int oi = __shfl_xor(bi, off);
+#pragma unroll
+      for (int off = G / 2; off > 0; off >>= 1) {
+        const float ov = __shfl_xor(bv, off, G);
+        const int oi = __shfl_xor(bi, off, G);
         if (argmax_better(ov, oi, bv, bi, C)) { bv = ov; bi = oi; }
       }
-      if (lane == 0) preds[b] = bi < C ? bi : 0;
+      if (g == 0 && rv) preds[b] = bi < C ? bi : 0;
     }
     if (late) {
-      for (int c = lane; c < C; c += 64) {
+      for (int c = g; c < C; c += G) {
         const float pc = z[c];
-        if (c == y) acc += -logf(pc + 1e-8f);
-        if (dlogits) dlogits[(long)b * C + c] = (c == y) ? -1.0f / ((pc + 1e-8f) * B) : 0.f;
+        if (c == y) term += -logf(pc + 1e-8f);
+        if (dlogits && rv) dlogits[(long)b * C + c] = (c == y) ? -1.0f / ((pc + 1e-8f) * B) : 0.f;
       }
-      continue;
+#pragma unroll
+      for (int off = G / 2; off > 0; off >>= 1) term += __shfl_xor(term, off, G);
+    } else {
+      float mx = -INFINITY;
+      for (int c = g; c < C; c += G) mx = fmaxf(mx, z[c]);
+#pragma unroll
+      for (int off = G / 2; off > 0; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off, G));
+      float se = 0.f, sz = 0.f, zy = 0.f;
+      for (int c = g; c < C; c += G) {
+        se += __expf(z[c] - mx);
+        sz += z[c];
+        if (c == y) zy = z[c];
+      }
+#pragma unroll
+      for (int off = G / 2; off > 0; off >>= 1) {
+        se += __shfl_xor(se, off, G);
+        sz += __shfl_xor(sz, off, G);
+        zy += __shfl_xor(zy, off, G);
+      }
+      const float lse = mx + logf(se);
+      term = (1.f - eps_ls) * (lse - zy) + eps_ls * (lse - sz / C);
+      if (dlogits && rv) {
+        for (int c = g; c < C; c += G) {
+          const float sm = __expf(z[c] - lse);
+          const float q = (c == y ? 1.f - eps_ls : 0.f) + eps_ls / C;
+          dlogits[(long)b * C + c] = (sm - q) / B;
+        }
+      }
     }
-    float mx = -INFINITY;
-    for (int c = lane; c < C; c += 64) mx = fmaxf(mx, z[c]);
-    mx = wave_max(mx);
-    float se = 0.f, sz = 0.f;
-    for (int c = lane; c < C; c += 64) { se += __expf(z[c] - mx); sz += z[c]; }
-    se = wave_sum(se);
-    sz = wave_sum(sz);
-    const float lse = mx + logf(se);
-    if (lane == 0) acc += (1.f - eps_ls) * (lse - z[y]) + eps_ls * (lse - sz / C);
-    for (int c = lane; c < C; c += 64) {
-      const float sm = __expf(z[c] - lse);
-      const float q = (c == y ? 1.f - eps_ls : 0.f) + eps_ls / C;
-      if (dlogits) dlogits[(long)b * C + c] = (sm - q) / B;
+    if (g == 0) rl[rg] = rv ? term : 0.f;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float acc = total;
+      for (int r = 0; r < RPB && b0 + r < B; ++r) acc += rl[r];
+      total = acc;
     }
+    __syncthreads();
   }
-  acc = wave_sum(acc);
-  if (lane == 0) part[w] = acc;
-  __syncthreads();
-  if (threadIdx.x == 0) *loss = (part[0] + part[1] + part[2] + part[3]) / B;
+  if (threadIdx.x == 0) *loss = total / B;
 }
 MER_API int mer_cross_entropy(int B, int C, const float* logits, const long long* labels, float label_smoothing,
                               int late, float* loss, float* dlogits, long long* preds, void* stream) {
-  hipLaunchKernelGGL(ce_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, B, C, logits, labels, label_smoothing, late,
-                     loss, dlogits, preds);
+  if (B <= 0 || C <= 0) return (int)hipErrorInvalidValue;
+  hipStream_t st = (hipStream_t)stream;
+#define MER_CE(G) hipLaunchKernelGGL(ce_kernel<G>, dim3(1), dim3(256), 0, st, B, C, logits, labels, label_smoothing, \
+                                     late, loss, dlogits, preds)
+  if (C <= 8) MER_CE(8);
+  else if (C <= 16) MER_CE(16);
+  else if (C <= 32) MER_CE(32);
+  else MER_CE(64);
+#undef MER_CE
   MER_LAUNCH_CHECK();
 }
 

@@ -207,6 +207,28 @@ def test_late_and_ce_kernels():
     assert max_abs(zd.grad, z.grad) < 1e-6
 
 
+@pytest.mark.parametrize("B,C", [(1, 8), (32, 8), (100, 8), (33, 3), (40, 13), (7, 64), (9, 70)])
+def test_ce_kernel_shapes_and_top1(B, C):
+    """ce_kernel<G> (one lane group per row, several passes when B > 256 / G, a lane looping over classes when
+    C > 64): loss, logits gradient and top-1 vs torch (label smoothing 0.1), ties resolved to the lowest index."""
+    from multimodalemotionrecognition_amd import kernels as K
+
+    g = torch.Generator().manual_seed(B * 100 + C)
+    z = torch.randn(B, C, generator=g)
+    z[0, : min(C, 3)] = 2.5  # a tie for the top-1
+    y = torch.randint(0, C, (B,), generator=g)
+    loss = torch.empty((), device="cuda")
+    dl = torch.empty(B, C, device="cuda")
+    pred = torch.empty(B, dtype=torch.int64, device="cuda")
+    K.cross_entropy(z.cuda(), y.cuda(), loss, dl, label_smoothing=0.1, preds=pred)
+    zr = z.clone().requires_grad_(True)
+    lr = torch.nn.functional.cross_entropy(zr, y, label_smoothing=0.1)
+    lr.backward()
+    assert abs(float(loss) - float(lr)) < 1e-5 * max(1.0, float(lr))
+    assert max_abs(dl, zr.grad) < 1e-6
+    assert torch.equal(pred.cpu(), z.argmax(dim=1))
+
+
 @pytest.mark.parametrize("mode", ["concat", "gated", "late"])
 def test_c4_embedding_heads(mode):
     """late / concat / gated heads at feature level vs the reference goldens (fusion.py:358-363,413-435)."""
