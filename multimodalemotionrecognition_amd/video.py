@@ -11,6 +11,7 @@ trunk starts from random init (``pretrained`` is accepted and ignored with a war
 """
 from __future__ import annotations
 
+import os
 import warnings
 from typing import List
 
@@ -506,9 +507,47 @@ def _bnr_target(blk_sv, blk, arena):
     return (out, bc2, bms2, red2, cd, msd, redd), (red2, redd)
 
 
+# Weight gradients on a second stream (MER_WGRAD_STREAM=1; default inline): a block's wgrad and dgrad read the same
+# upstream gradient and write disjoint buffers, so the wgrad can fork off the current stream and run beside the
+# dgrad and BatchNorm passes, one join per backward (graph) segment.  Deterministic, tested equal -- but measured
+# SLOWER in the train step (175.4 / 176.4 vs 188.3 / 188.4 steps/s, same box, alternating runs): beside the
+# prefetched WavLM stream a third stream only adds contention and graph-branch overhead.
+WGRAD_STREAM = os.environ.get("MER_WGRAD_STREAM", "0") != "0"
+_WGRAD_STREAMS = {}
+
+
+class _WgradLane:
+    """Fork / join of the weight-gradient stream.  Tensors the forked work reads are kept referenced until the
+    join, so the caching allocator cannot hand their blocks to the current stream while the lane still reads them
+    (the same holds inside a graph capture, where the fork and join are graph edges)."""
+
+    def __init__(self, device):
+        self.enabled = WGRAD_STREAM and device.type == "cuda"
+        self.keep = []
+        if self.enabled:
+            idx = device.index if device.index is not None else torch.cuda.current_device()
+            self.stream = _WGRAD_STREAMS.get(idx)
+            if self.stream is None:
+                self.stream = _WGRAD_STREAMS[idx] = torch.cuda.Stream(device=idx)
+
+    def run(self, fn, *reads):
+        if not self.enabled:
+            fn()
+            return
+        self.stream.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(self.stream):
+            fn()
+        self.keep.extend(reads)
+
+    def join(self):
+        if self.enabled and self.keep:
+            torch.cuda.current_stream().wait_stream(self.stream)
+        self.keep = []
+
+
 @torch.no_grad()
 def block_backward(trunk, blk: BasicBlock, sv, dx: torch.Tensor, grads, training: bool = True, pre=None,
-                   prev=None, arena=None):
+                   prev=None, arena=None, lane=None):
     """Reverse of block_forward given dx = dL/d(block output); returns dL/d(block input).
 
     ``pre``: this block's bn2 / downsample-BN reductions already accumulated by the producer of ``dx``
@@ -519,6 +558,9 @@ def block_backward(trunk, blk: BasicBlock, sv, dx: torch.Tensor, grads, training
     xin, bc1, bms1, ba1, bc2, bms2, cd, msd, out = sv
     if arena is None:  # standalone call: room for this block's own reductions and one upstream target
         arena = _StatsArena(trunk, dev, floats=_block_bwd_floats(sv))
+    own_lane = lane is None
+    if own_lane:
+        lane = _WgradLane(dev)
     g_out = dx
     s = blk.stride
     C2 = bc2.shape[-1]
@@ -537,7 +579,7 @@ def block_backward(trunk, blk: BasicBlock, sv, dx: torch.Tensor, grads, training
     # conv2 (its dgrad also reduces bn1's backward sums: g = da1 * (ba1 > 0))
     w2 = _grad(blk.conv2.weight, grads)
     if w2 is not None:
-        K.conv_wgrad(ba1, dc2, w2, 3, 3, 1, 1)
+        lane.run(lambda: K.conv_wgrad(ba1, dc2, w2, 3, 3, 1, 1), ba1, dc2, w2)
     da1 = torch.empty_like(ba1)
     C1 = bc1.shape[-1]
     red1p = arena.take(C1, parts=K.bn_red_rows(ba1.numel() // C1))
@@ -547,19 +589,21 @@ def block_backward(trunk, blk: BasicBlock, sv, dx: torch.Tensor, grads, training
     # conv1 (+ downsample) -> dx of the block input (+ the preceding block's bn2 / downsample reductions)
     w1 = _grad(blk.conv1.weight, grads)
     if w1 is not None:
-        K.conv_wgrad(xin, dc1, w1, 3, 3, s, 1)
+        lane.run(lambda: K.conv_wgrad(xin, dc1, w1, 3, 3, s, 1), xin, dc1, w1)
     dxin = torch.empty_like(xin)
     Cin = xin.shape[-1]
     bnr, nxt = _bnr_target(prev[0], prev[1], arena) if prev is not None else (None, None)
     if cd is not None:
         wd = _grad(blk.downsample[0].weight, grads)
         if wd is not None:
-            K.conv_wgrad(xin, dcd, wd, 1, 1, s, 0)
+            lane.run(lambda: K.conv_wgrad(xin, dcd, wd, 1, 1, s, 0), xin, dcd, wd)
         dxd = torch.empty_like(xin)
         K.conv_dgrad(dcd, trunk.packed(blk.downsample[0], Cin, True), dxd, 1, 1, s, 0)
         K.conv_dgrad(dc1, trunk.packed(blk.conv1, Cin, True), dxin, 3, 3, s, 1, residual=dxd, bnr=bnr)
     else:
         K.conv_dgrad(dc1, trunk.packed(blk.conv1, Cin, True), dxin, 3, 3, s, 1, residual=g_out, mask=out, bnr=bnr)
+    if own_lane:
+        lane.join()
     return dxin, nxt
 
 
@@ -587,8 +631,9 @@ def trunk_backward_start(trunk, saved, dfeat, training, split, force_pack=False)
         svs = saved["blocks"]
         # every backward BatchNorm reduction buffer of this pass: one memset
         arena = _StatsArena(trunk, dev, floats=sum(_block_bwd_floats(sv) for sv in svs) + 2 * K.BN_RED_WS_ROWS * 64 * 2)
-        state = dict(dx=dx, pre=None, grads={}, arena=arena, i=len(svs) - 1)
+        state = dict(dx=dx, pre=None, grads={}, arena=arena, i=len(svs) - 1, lane=_WgradLane(dev))
         _backward_blocks(trunk, saved, state, max(split, trunk.backward_stop(), 0), training)
+        state["lane"].join()  # the early-bucket hook (or the next graph segment) sees final layer4 gradients
         return state
 
 
@@ -598,7 +643,8 @@ def _backward_blocks(trunk, saved, state, lo, training):
         i = state["i"]
         prev = (svs[i - 1], blocks[i - 1]) if i > 0 else None
         state["dx"], state["pre"] = block_backward(trunk, blocks[i], svs[i], state["dx"], state["grads"], training,
-                                                   pre=state["pre"], prev=prev, arena=state["arena"])
+                                                   pre=state["pre"], prev=prev, arena=state["arena"],
+                                                   lane=state["lane"])
         state["i"] = i - 1
 
 
@@ -610,6 +656,7 @@ def trunk_backward_finish(trunk, saved, state, training, force_pack=False):
         _backward_blocks(trunk, saved, state, max(stop, 0), training)
         grads, arena, dx = state["grads"], state["arena"], state["dx"]
         if stop >= 0:  # stem and the blocks below `stop` frozen (stage-2 video tail): nothing more is needed
+            state["lane"].join()
             return grads
         dev = dx.device
         # stem: maxpool -> bn1/relu -> conv1 (no data gradient for the frames)
@@ -629,6 +676,7 @@ def trunk_backward_finish(trunk, saved, state, training, force_pack=False):
             if idx is None or idx.device != dev:
                 idx = trunk.__dict__["_mer_stem_idx"] = _stem_wgrad_index(R, S, Cin, dev)
             w.add_(ws2d.view(Kc, -1).index_select(1, idx).view_as(w))
+        state["lane"].join()
         return grads
 
 

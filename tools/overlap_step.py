@@ -54,11 +54,33 @@ def run():
 
     heads = []
     model.xattn_from_features = head
+    losses, adams = [], []
+    orig_loss = step.loss_fn.forward
+
+    def loss_fn(o, y):  # main-stream event after the loss (head forward + CE done: the backward starts)
+        r = orig_loss(o, y)
+        e = ev()
+        e.record()
+        losses.append(e)
+        return r
+
+    step.loss_fn.forward = loss_fn
+    orig_step = opt.step
+
+    def opt_step(*a, **k):  # main-stream event when the backward is done (Adam starts)
+        e = ev()
+        e.record()
+        adams.append(e)
+        return orig_step(*a, **k)
+
+    opt.step = opt_step
     for _ in range(10):
         step(video, audio, labels, next_audio=audio)
     torch.cuda.synchronize()
     marks.clear()
     heads.clear()
+    losses.clear()
+    adams.clear()
     starts, ends = [], []
     for _ in range(10):
         t0 = ev()
@@ -74,7 +96,8 @@ def run():
         s0, s1 = marks[i]
         print(f"step {i}: step {starts[i].elapsed_time(ends[i]):.3f} ms | WavLM(next) on side: start "
               f"{starts[i].elapsed_time(s0):+.3f} end {starts[i].elapsed_time(s1):+.3f} ms | head starts at "
-              f"{starts[i].elapsed_time(heads[i]):.3f} ms")
+              f"{starts[i].elapsed_time(heads[i]):.3f} | backward starts {starts[i].elapsed_time(losses[i]):.3f} | "
+              f"Adam starts {starts[i].elapsed_time(adams[i]):.3f} ms")
 
 
 if __name__ == "__main__":
