@@ -60,9 +60,15 @@ MER_API int mer_xh_split(int n_items, const long long* desc, void* stream) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// F1: audio token chain, 32 rows per block, 4 waves; the trailing ceil(B*T/32) blocks run the video rows'
-// input and query projections (v, q1), which depend on nothing the audio chain makes.
+// F1: audio token chain, 32 rows per block, 8 waves; the trailing ceil(B*T/32) blocks run the video rows'
+// input and query projections (v, q1), which depend on nothing the audio chain makes.  The 768-deep first
+// product is split over the wave halves (waves 4..7 take the upper half of K and hand their partial sums over
+// LDS); the two short products use all 8 waves on 16 / 48 columns each (35 -> 31.7 us at B = 32: the first
+// product itself is bound by L2 traffic -- every block re-reads the whole 393 KB split weight with half-used
+// 128-byte lines -- not by the k-step chain; a fully register-pipelined version of it measured slower).
 // ---------------------------------------------------------------------------------------------
+constexpr int F1_WAVES = 8;
+
 struct XhVideo {
   int M, vdim;
   const float* vfeat;
@@ -75,57 +81,60 @@ struct XhVideo {
 };
 
 template <typename TA>  // bf16: the WavLM features (exact, two passes); float: fp32 features (split, three passes)
-__global__ __launch_bounds__(256) void xh_audio_fwd_kernel(int M, int S, const TA* __restrict__ aseq, long ldas,
-                                                           SplitW Ws, const float* __restrict__ bs, SplitW Wa,
-                                                           const float* __restrict__ ba, SplitW Wc,
-                                                           const float* __restrict__ bq2, const float* __restrict__ bkv1,
-                                                           float* __restrict__ a_s, float* __restrict__ a,
-                                                           float* __restrict__ q2, float* __restrict__ kv1, XhVideo vid) {
+__global__ __launch_bounds__(64 * F1_WAVES) void xh_audio_fwd_kernel(int M, int S, const TA* __restrict__ aseq,
+                                                                     long ldas, SplitW Ws, const float* __restrict__ bs,
+                                                                     SplitW Wa, const float* __restrict__ ba, SplitW Wc,
+                                                                     const float* __restrict__ bq2,
+                                                                     const float* __restrict__ bkv1,
+                                                                     float* __restrict__ a_s, float* __restrict__ a,
+                                                                     float* __restrict__ q2, float* __restrict__ kv1,
+                                                                     XhVideo vid) {
   __shared__ __attribute__((aligned(16))) float asL[32 * LDA];
   __shared__ __attribute__((aligned(16))) float aL[32 * LDA];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, fr = lane & 15, fk = (lane >> 4) * 8;
   const int na = (M + 31) / 32;
-  if ((int)blockIdx.x >= na) {  // video rows: v = v_feat Wv^T + bv, q1 = v Wq1^T + bq1
+  if ((int)blockIdx.x >= na) {  // video rows: v = v_feat Wv^T + bv, q1 = v Wq1^T + bq1 (16 columns per wave)
     const long v0 = (long)(blockIdx.x - na) * 32;
     const int vmax = (int)(vid.M - v0 < 32 ? vid.M - v0 : 32);
     {
-      f32x4 acc[2][2];
+      f32x4 acc[2][1];
       zero(acc);
-      mm_aw(acc, vid.vfeat + v0 * vid.vdim, vid.vdim, vmax, vid.vdim, vid.Wv, vid.vdim, 32 * w);
-      store_acc(acc, 32 * w, vid.bv, asL, LDA, vid.v, XD, v0, vmax);
+      mm_aw(acc, vid.vfeat + v0 * vid.vdim, vid.vdim, vmax, vid.vdim, vid.Wv, vid.vdim, 16 * w);
+      store_acc(acc, 16 * w, vid.bv, asL, LDA, vid.v, XD, v0, vmax);
     }
     __syncthreads();
-    f32x4 acc[2][2];
+    f32x4 acc[2][1];
     zero(acc);
-    mm_aw<2, 2, 3, XD>(acc, asL, LDA, 32, XD, vid.Wq1, XD, 32 * w);
-    store_acc(acc, 32 * w, vid.bq1, nullptr, 0, vid.q1, XD, v0, vmax);
+    mm_aw<2, 1, 3, XD>(acc, asL, LDA, 32, XD, vid.Wq1, XD, 16 * w);
+    store_acc(acc, 16 * w, vid.bq1, nullptr, 0, vid.q1, XD, v0, vmax);
     return;
   }
   XT(2, 0);
   const long r0 = (long)blockIdx.x * 32;
   const int rmax = (int)(M - r0 < 32 ? M - r0 : 32);
-  // a_s = a_seq Ws^T + bs  (bf16 A is exact: two passes; fp32 A: split, three passes)
+  // a_s = a_seq Ws^T + bs  (bf16 A is exact: two passes; fp32 A: split, three passes); wave (w & 3) owns 32
+  // columns, wave half (w >> 2) one half of K
   {
     f32x4 acc[2][2];
     zero(acc);
-    const int c0 = 32 * w;
+    const int c0 = 32 * (w & 3), kh = w >> 2, Kh = S / 2, kbase = kh * Kh;
     if constexpr (sizeof(TA) == 2) {  // pipelined like mm_aw, F1_D k steps in flight
       constexpr int F1_D = 6;
       u4 sa[F1_D][2], sb[F1_D][2][2];
       auto load = [&](int k, u4 (&ra)[2], u4 (&rb)[2][2]) {
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
-          const long off = (long)(c0 + 16 * j + fr) * S + k + fk;
+          const long off = (long)(c0 + 16 * j + fr) * S + kbase + k + fk;
           rb[j][0] = *reinterpret_cast<const u4*>(Ws.hi + off);
           rb[j][1] = *reinterpret_cast<const u4*>(Ws.lo + off);
         }
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
           const int r = 16 * i + fr;
-          ra[i] = *reinterpret_cast<const u4*>(aseq + (r0 + (r < rmax ? r : rmax - 1)) * ldas + k + fk);
+          ra[i] = *reinterpret_cast<const u4*>(aseq + (r0 + (r < rmax ? r : rmax - 1)) * ldas + kbase + k + fk);
         }
       };
-      const int nsteps = S / 32;  // branch-free pipeline, as mm_aw
+      const int nsteps = Kh / 32;  // branch-free pipeline, as mm_aw
 #pragma unroll
       for (int d = 0; d < F1_D; ++d) load(32 * (d < nsteps ? d : nsteps - 1), sa[d], sb[d]);
       for (int s0 = 0; s0 < nsteps; s0 += F1_D) {
@@ -150,27 +159,39 @@ __global__ __launch_bounds__(256) void xh_audio_fwd_kernel(int M, int S, const T
         }
       }
     } else {
-      mm_aw(acc, reinterpret_cast<const float*>(aseq) + r0 * ldas, ldas, rmax, S, Ws, S, c0);
+      mm_aw(acc, reinterpret_cast<const float*>(aseq) + r0 * ldas + kbase, ldas, rmax, Kh,
+            SplitW{Ws.hi + kbase, Ws.lo + kbase}, S, c0);
     }
-    store_acc(acc, c0, bs, asL, LDA, a_s, XD, r0, rmax);
+    // the upper K half's partial sums through aL (free until the second product), added in a fixed order
+    if (kh == 1) store_acc(acc, c0, nullptr, aL, LDA, nullptr, 0, 0, 32);
+    __syncthreads();
+    if (kh == 0) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[i][j][r] += aL[(16 * i + 4 * (lane >> 4) + r) * LDA + c0 + 16 * j + fr];
+      store_acc(acc, c0, bs, asL, LDA, a_s, XD, r0, rmax);
+    }
   }
   __syncthreads();
   XT(2, 1);
-  {  // a = a_s Wa^T + ba
-    f32x4 acc[2][2];
+  {  // a = a_s Wa^T + ba (16 columns per wave)
+    f32x4 acc[2][1];
     zero(acc);
-    mm_aw<2, 2, 3, XD>(acc, asL, LDA, 32, XD, Wa, XD, 32 * w);
-    store_acc(acc, 32 * w, ba, aL, LDA, a, XD, r0, rmax);
+    mm_aw<2, 1, 3, XD>(acc, asL, LDA, 32, XD, Wa, XD, 16 * w);
+    store_acc(acc, 16 * w, ba, aL, LDA, a, XD, r0, rmax);
   }
   __syncthreads();
   XT(2, 2);
-  {  // [q2 | k1 v1] = a Wc^T + [bq2 | bkv1]: 384 columns, 96 per wave in ONE pipelined pass (K = 128: 4 steps)
-    f32x4 acc[2][6];
+  {  // [q2 | k1 v1] = a Wc^T + [bq2 | bkv1]: 384 columns, 48 per wave in ONE pipelined pass (K = 128: 4 steps)
+    f32x4 acc[2][3];
     zero(acc);
-    const int c0 = 96 * w;
-    mm_aw<2, 6, 2, XD>(acc, aL, LDA, 32, XD, Wc, XD, c0);
+    const int c0 = 48 * w;
+    mm_aw<2, 3, 2, XD>(acc, aL, LDA, 32, XD, Wc, XD, c0);
 #pragma unroll
-    for (int j = 0; j < 6; ++j) {
+    for (int j = 0; j < 3; ++j) {
       const int col = c0 + 16 * j + fr;
       const bool isq = col < XD;
       const float bv = isq ? bq2[col] : bkv1[col - XD];
@@ -196,17 +217,17 @@ MER_API int mer_xh_audio_fwd(int M, int S, const void* aseq, int aseq_dtype, lon
                              const void* Wv_lo, const float* bv, const void* Wq1_hi, const void* Wq1_lo,
                              const float* bq1, float* v, float* q1, void* stream) {
   if (M <= 0 || Mv < 0) return (int)hipErrorInvalidValue;
-  if (S % 32 || ldas % 8 || ((uintptr_t)aseq & 15) || (Mv > 0 && (vdim <= 0 || vdim % 32))) return (int)hipErrorInvalidValue;
+  if (S % 64 || ldas % 8 || ((uintptr_t)aseq & 15) || (Mv > 0 && (vdim <= 0 || vdim % 32))) return (int)hipErrorInvalidValue;
   const SplitW ws{(const bf16_t*)Ws_hi, (const bf16_t*)Ws_lo}, wa{(const bf16_t*)Wa_hi, (const bf16_t*)Wa_lo},
       wc{(const bf16_t*)Wc_hi, (const bf16_t*)Wc_lo};
   const XhVideo vid{Mv, vdim, vfeat, SplitW{(const bf16_t*)Wv_hi, (const bf16_t*)Wv_lo}, bv,
                     SplitW{(const bf16_t*)Wq1_hi, (const bf16_t*)Wq1_lo}, bq1, v, q1};
   const dim3 grid((M + 31) / 32 + (Mv + 31) / 32);
   if (aseq_dtype == MER_BF16)
-    hipLaunchKernelGGL(xh_audio_fwd_kernel<bf16_t>, grid, dim3(256), 0, (hipStream_t)stream, M, S,
+    hipLaunchKernelGGL(xh_audio_fwd_kernel<bf16_t>, grid, dim3(64 * F1_WAVES), 0, (hipStream_t)stream, M, S,
                        (const bf16_t*)aseq, ldas, ws, bs, wa, ba, wc, bq2, bkv1, a_s, a, q2, kv1, vid);
   else
-    hipLaunchKernelGGL(xh_audio_fwd_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, M, S,
+    hipLaunchKernelGGL(xh_audio_fwd_kernel<float>, grid, dim3(64 * F1_WAVES), 0, (hipStream_t)stream, M, S,
                        (const float*)aseq, ldas, ws, bs, wa, ba, wc, bq2, bkv1, a_s, a, q2, kv1, vid);
   MER_LAUNCH_CHECK();
 }

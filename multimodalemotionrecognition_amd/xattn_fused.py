@@ -42,7 +42,7 @@ def supported(cfg, p: Dict[str, torch.Tensor], v_feat: torch.Tensor, a_seq: torc
     B, T, vd = v_feat.shape
     _, Ta, sd = a_seq.shape
     if a_seq.dtype not in (torch.bfloat16, torch.float32) or v_feat.dtype != torch.float32 or T > 16 or Ta > 160 \
-            or vd % 32 or sd % 32:
+            or vd % 32 or sd % 64:
         return False
     if a_seq.requires_grad:  # the fused forward has no audio-feature gradient path (stage 2 runs unfused)
         return False
