@@ -512,7 +512,7 @@ def _bnr_target(blk_sv, blk, arena):
 # dgrad and BatchNorm passes, one join per backward (graph) segment.  Deterministic, tested equal -- but measured
 # SLOWER in the train step (175.4 / 176.4 vs 188.3 / 188.4 steps/s, same box, alternating runs): beside the
 # prefetched WavLM stream a third stream only adds contention and graph-branch overhead.
-WGRAD_STREAM = os.environ.get("MER_WGRAD_STREAM", "0") != "0"
+WGRAD_STREAM = int(os.environ.get("MER_WGRAD_STREAM", "0"))  # 1: every block, 2: layer1 blocks only (A/B)
 _WGRAD_STREAMS = {}
 
 
@@ -522,7 +522,8 @@ class _WgradLane:
     (the same holds inside a graph capture, where the fork and join are graph edges)."""
 
     def __init__(self, device):
-        self.enabled = WGRAD_STREAM and device.type == "cuda"
+        self.enabled = WGRAD_STREAM > 0 and device.type == "cuda"
+        self.only_below = 2 if WGRAD_STREAM == 2 else None  # block index bound for the fork (layer1 = blocks 0, 1)
         self.keep = []
         if self.enabled:
             idx = device.index if device.index is not None else torch.cuda.current_device()
@@ -530,8 +531,8 @@ class _WgradLane:
             if self.stream is None:
                 self.stream = _WGRAD_STREAMS[idx] = torch.cuda.Stream(device=idx)
 
-    def run(self, fn, *reads):
-        if not self.enabled:
+    def run(self, fn, *reads, block=None):
+        if not self.enabled or (self.only_below is not None and (block is None or block >= self.only_below)):
             fn()
             return
         self.stream.wait_stream(torch.cuda.current_stream())
@@ -547,7 +548,7 @@ class _WgradLane:
 
 @torch.no_grad()
 def block_backward(trunk, blk: BasicBlock, sv, dx: torch.Tensor, grads, training: bool = True, pre=None,
-                   prev=None, arena=None, lane=None):
+                   prev=None, arena=None, lane=None, bidx=None):
     """Reverse of block_forward given dx = dL/d(block output); returns dL/d(block input).
 
     ``pre``: this block's bn2 / downsample-BN reductions already accumulated by the producer of ``dx``
@@ -579,7 +580,7 @@ def block_backward(trunk, blk: BasicBlock, sv, dx: torch.Tensor, grads, training
     # conv2 (its dgrad also reduces bn1's backward sums: g = da1 * (ba1 > 0))
     w2 = _grad(blk.conv2.weight, grads)
     if w2 is not None:
-        lane.run(lambda: K.conv_wgrad(ba1, dc2, w2, 3, 3, 1, 1), ba1, dc2, w2)
+        lane.run(lambda: K.conv_wgrad(ba1, dc2, w2, 3, 3, 1, 1), ba1, dc2, w2, block=bidx)
     da1 = torch.empty_like(ba1)
     C1 = bc1.shape[-1]
     red1p = arena.take(C1, parts=K.bn_red_rows(ba1.numel() // C1))
@@ -589,14 +590,14 @@ def block_backward(trunk, blk: BasicBlock, sv, dx: torch.Tensor, grads, training
     # conv1 (+ downsample) -> dx of the block input (+ the preceding block's bn2 / downsample reductions)
     w1 = _grad(blk.conv1.weight, grads)
     if w1 is not None:
-        lane.run(lambda: K.conv_wgrad(xin, dc1, w1, 3, 3, s, 1), xin, dc1, w1)
+        lane.run(lambda: K.conv_wgrad(xin, dc1, w1, 3, 3, s, 1), xin, dc1, w1, block=bidx)
     dxin = torch.empty_like(xin)
     Cin = xin.shape[-1]
     bnr, nxt = _bnr_target(prev[0], prev[1], arena) if prev is not None else (None, None)
     if cd is not None:
         wd = _grad(blk.downsample[0].weight, grads)
         if wd is not None:
-            lane.run(lambda: K.conv_wgrad(xin, dcd, wd, 1, 1, s, 0), xin, dcd, wd)
+            lane.run(lambda: K.conv_wgrad(xin, dcd, wd, 1, 1, s, 0), xin, dcd, wd, block=bidx)
         dxd = torch.empty_like(xin)
         K.conv_dgrad(dcd, trunk.packed(blk.downsample[0], Cin, True), dxd, 1, 1, s, 0)
         K.conv_dgrad(dc1, trunk.packed(blk.conv1, Cin, True), dxin, 3, 3, s, 1, residual=dxd, bnr=bnr)
@@ -644,7 +645,7 @@ def _backward_blocks(trunk, saved, state, lo, training):
         prev = (svs[i - 1], blocks[i - 1]) if i > 0 else None
         state["dx"], state["pre"] = block_backward(trunk, blocks[i], svs[i], state["dx"], state["grads"], training,
                                                    pre=state["pre"], prev=prev, arena=state["arena"],
-                                                   lane=state["lane"])
+                                                   lane=state["lane"], bidx=i)
         state["i"] = i - 1
 
 
