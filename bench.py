@@ -53,6 +53,7 @@ PROBE = ("gemm_bf16", (BATCH * 4799, 512, 1536))
 # 16 waves each)
 PROBE_KERNEL = "gemm_pipe_kernel<PipeCfg<256,256,4,4,2,64>, bf16>"
 PMC_FILE = ROOT / "profiles" / "pmc_traffic.json"
+PMC_HEAD_FILE = ROOT / "profiles" / "pmc_traffic_head.json"  # tools/pmc_head.py summarize (fused head fwd + bwd)
 # Algorithmic work per clip: ResNet18 fwd+bwd over 8 frames 22.8 GFLOP, head fwd+bwd 0.141, WavLM
 # feature extractor 14.72 + pos-conv 1.42 + projection 0.12, and 2.177 GFLOP per EXECUTED encoder layer
 # (projections 0.703 + FFN 1.406 + attention 0.068; LayerDrop skips ~1.1 of 12 in train mode).
@@ -82,6 +83,14 @@ def pmc_traffic():
     if d.get("kernel_match") not in PROBE_KERNEL.replace(" ", "") or tuple(d.get("shape", ())) != PROBE[1]:
         return None
     return d.get("traffic_bytes_per_launch")
+
+
+def pmc_traffic_head():
+    """HBM bytes of one fused-head forward + backward from the committed PMC passes (tools/pmc_head.py), or None."""
+    try:
+        return json.loads(PMC_HEAD_FILE.read_text()).get("traffic_bytes_per_step")
+    except (OSError, ValueError):
+        return None
 
 
 def synthetic_batch(device, seed):
@@ -428,7 +437,7 @@ def _bench(args, world, rank, local):
         ach = hflop / ((fwd_ms + bwd_ms) * 1e-3) / 1e12
         roof_head = {"bound": "mfma" if peak_split < ai * PEAK_HBM_GBS / 1e3 else "hbm",
                      "achieved": round(ach, 2), "peak": round(attain, 1), "unit": "TFLOP/s",
-                     "frac": round(ach / attain, 4), "traffic": None,
+                     "frac": round(ach / attain, 4), "traffic": pmc_traffic_head(),
                      "kernel": "fused xattn head fwd+bwd (csrc/xattn_fused.hip F1-F4, xattn_fused_bwd.hip G1-G4 + W)",
                      "algorithmic_flop": hflop, "algorithmic_bytes": hbytes, "intensity_flop_per_byte": round(ai, 2),
                      "fwd_ms": round(fwd_ms, 4), "bwd_ms": round(bwd_ms, 4), "ms_per_step": round(fwd_ms + bwd_ms, 4),
