@@ -56,9 +56,19 @@ def main():
                 torch.cuda.synchronize()
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 reps = 5 if quick else 20
+                # the reps as one captured graph: a ctypes launch costs ~20-27 us of host time, which would
+                # bound the small WavLM encoder shapes (a plain loop timed QKV at 27.3 us whatever the variant)
+                gph = torch.cuda.CUDAGraph()
+                cs = torch.cuda.Stream()
+                cs.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.graph(gph, stream=cs):
+                    for _ in range(reps):
+                        K.gemm_bf16(a, w, out, variant=v, **kw)
+                torch.cuda.current_stream().wait_stream(cs)
+                gph.replay()
+                torch.cuda.synchronize()
                 e0.record()
-                for _ in range(reps):
-                    K.gemm_bf16(a, w, out, variant=v, **kw)
+                gph.replay()
                 e1.record()
                 torch.cuda.synchronize()
                 ms = e0.elapsed_time(e1) / reps
