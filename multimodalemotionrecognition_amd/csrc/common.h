@@ -91,6 +91,32 @@ __device__ __forceinline__ float dropout_scale(uint64_t seed, uint64_t idx, floa
   return u >= p ? 1.0f / (1.0f - p) : 0.0f;
 }
 
+// Paired-index dropout (the WavLM encoder's sites: GEMM epilogues, encoder LayerNorm, attention probabilities,
+// mer_dropout_rows): one mer_hash word serves two adjacent mask indices -- its low 16 bits decide index 2q, its
+// high 16 bits index 2q + 1 -- and an index is kept when its half is >= ceil(p 2^16) (keep rate 1 - 6554 / 65536
+// at p = 0.1).  Callers holding adjacent indices hash once per pair: half the VALU work of dropout_scale, which
+// was ~40% of a train-mode attention launch.
+__device__ __forceinline__ uint32_t drop_thr16(float p) { return (uint32_t)ceilf(p * 65536.0f); }
+__device__ __forceinline__ bool pair_keep(uint32_t h, uint64_t idx, uint32_t thr) {
+  return ((idx & 1ull) ? (h >> 16) : (h & 0xFFFFu)) >= thr;
+}
+__device__ __forceinline__ float dropout_scale_pair(uint64_t seed, uint64_t idx, float p) {  // one index
+  if (p <= 0.f) return 1.f;
+  return pair_keep(mer_hash(seed, idx >> 1), idx, drop_thr16(p)) ? 1.0f / (1.0f - p) : 0.0f;
+}
+// v[e] *= keep scale of index i0 + e, e < N (N even, i0 even): one hash per pair
+template <int N>
+__device__ __forceinline__ void dropout_pairs(float* v, uint64_t seed, uint64_t i0, float p) {
+  const uint32_t thr = drop_thr16(p);
+  const float ks = 1.0f / (1.0f - p);
+#pragma unroll
+  for (int e = 0; e < N; e += 2) {
+    const uint32_t h = mer_hash(seed, (i0 + e) >> 1);
+    v[e] *= (h & 0xFFFFu) >= thr ? ks : 0.f;
+    v[e + 1] *= (h >> 16) >= thr ? ks : 0.f;
+  }
+}
+
 // a / d for 0 <= a < 2^22 with inv_d = 1.0f / d (d >= 1): exact, ~3 VALU ops instead of an
 // integer-division sequence.  (a + 0.5) / d sits >= 0.5/d away from any integer, far more than the
 // float rounding error at these magnitudes.

@@ -70,7 +70,7 @@ __device__ __forceinline__ bool layer_skipped(const long long* mask, int bit) {
 // act -> dropout (train mode) of one epilogue element
 __device__ __forceinline__ float epi_act_drop(float v, int act, float p, unsigned long long seed, long idx) {
   v = apply_act(v, act);
-  return p > 0.f ? v * dropout_scale(seed, (uint64_t)idx, p) : v;
+  return p > 0.f ? v * dropout_scale_pair(seed, (uint64_t)idx, p) : v;
 }
 
 typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;
@@ -394,10 +394,8 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_pipe_kernel(GemmArgs g) {
           const f32x4 lo = *reinterpret_cast<const f32x4*>(&wl[rl * LDT + lc]);
           const f32x4 hi = *reinterpret_cast<const f32x4*>(&wl[rl * LDT + lc + 4]);
           float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-          if (g.drop_p > 0.f) {
-#pragma unroll
-            for (int e = 0; e < 8; ++e) v[e] *= dropout_scale(dseed, (uint64_t)((long)row * g.N + colv + e), g.drop_p);
-          }
+          if (g.drop_p > 0.f)  // N % 8 == 0 on this path: the 8 indices start even
+            dropout_pairs<8>(v, dseed, (uint64_t)((long)row * g.N + colv), g.drop_p);
           if (g.R) {
             const u32x4 rv = *reinterpret_cast<const u32x4*>(g.R + (long)row * g.ldr + (long)z * g.c_zoff + colv);
 #pragma unroll

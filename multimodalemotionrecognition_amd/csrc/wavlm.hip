@@ -182,9 +182,11 @@ __global__ __launch_bounds__(256) void layernorm_kernel(int rows, int d, const T
       const f32x4 g = *reinterpret_cast<const f32x4*>(gamma + c), b = *reinterpret_cast<const f32x4*>(beta + c);
       f32x4 o;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        o[e] = (vals[4 * i + e] - mean) * rstd * g[e] + b[e];
-        if (drop_p > 0.f) o[e] *= dropout_scale(seed, (uint64_t)((long)row * d + c + e), drop_p);
+      for (int e = 0; e < 4; ++e) o[e] = (vals[4 * i + e] - mean) * rstd * g[e] + b[e];
+      if (drop_p > 0.f) {  // d % 256 == 0: the 4 indices start even
+        float ov[4] = {o[0], o[1], o[2], o[3]};
+        dropout_pairs<4>(ov, seed, (uint64_t)((long)row * d + c), drop_p);
+        o = f32x4{ov[0], ov[1], ov[2], ov[3]};
       }
       st4<TO>(yr + c, o);
     }
@@ -202,7 +204,7 @@ __global__ __launch_bounds__(256) void layernorm_kernel(int rows, int d, const T
   n = 0;
   for (int c = lane; c < d; c += 64, ++n) {
     float o = (vals[n] - mean) * rstd * gamma[c] + beta[c];
-    if (drop_p > 0.f) o *= dropout_scale(seed, (uint64_t)((long)row * d + c), drop_p);
+    if (drop_p > 0.f) o *= dropout_scale_pair(seed, (uint64_t)((long)row * d + c), drop_p);
     stf<TO>(yr, c, o);
   }
 }
@@ -400,11 +402,13 @@ __global__ __launch_bounds__(64 * NW) void wavlm_attn_kernel(
   }
   const float gc = gconst[h];
   const unsigned long long dseed = mer_site_seed(seed_ptr, site);
-  // the dropout mask's seed mix (mer_hash), the keep threshold on the hash's top 24 bits (u = (h >> 8) / 2^24 >= p
-  // exactly when (h >> 8) >= ceil(p 2^24)) and whether every mask index ((b*H+h)*L + i)*L + j fits 32 bits
+  // the paired dropout mask (common.h dropout_scale_pair) over index ((b*H+h)*L + i)*LE + j, LE = L rounded up to
+  // even: the seed mix of mer_hash, the 16-bit keep threshold, and whether every index fits 32 bits
+  const int LE = L + (L & 1);
   const uint32_t hseed = (uint32_t)dseed ^ ((uint32_t)(dseed >> 32) * 0x85EBCA6Bu);
-  const uint32_t keep_thr = (uint32_t)ceilf(drop_p * 16777216.0f);
-  const bool idx32 = (unsigned long long)(gridDim.x / nrb) * (unsigned long long)L * (unsigned long long)L < (1ull << 32);
+  const uint32_t keep_thr = drop_thr16(drop_p);
+  const bool idx32 = (unsigned long long)(gridDim.x / nrb) * (unsigned long long)(L + 1) * (unsigned long long)LE <
+                     (1ull << 32);
   __syncthreads();
   AT(2);
 
@@ -470,8 +474,8 @@ __global__ __launch_bounds__(64 * NW) void wavlm_attn_kernel(
     AT(4);
     // P^T = exp(S^T - max) rounded to bf16 (the weights that enter PV also form the normaliser).  Train mode:
     // attention-probability dropout (F.multi_head_attention_forward dropout_p, TF:206-228): dropped weights do
-    // not enter PV, the kept ones are rescaled by 1/(1-p) with the normaliser (mask index ((b*H+h)*L + i)*L + j)
-    const long mrow = (((long)b * H + h) * L + i) * L;
+    // not enter PV, the kept ones are rescaled by 1/(1-p) with the normaliser
+    const long mrow = (((long)b * H + h) * L + i) * LE;  // even: the lane's keys pair up as (r0, r1), (r2, r3)
     float sum = 0.f;
     s16x4 pb[KT];
 #pragma unroll
@@ -482,22 +486,23 @@ __global__ __launch_bounds__(64 * NW) void wavlm_attn_kernel(
         sum += bf2f(p);
         pb[ct][r] = (short)p;
       }
-    if (drop_p > 0.f) {  // (uniform) the keep mask: dropout_scale(dseed, mrow + j, p) != 0
+    if (drop_p > 0.f) {  // (uniform) the keep mask, dropout_scale_pair(dseed, mrow + j, p) != 0
       if (idx32) {
-        // every mask index is < 2^32: mer_hash's first product distributes over mrow + j, so the per-element work
-        // is one add + the two-multiply finaliser and an integer threshold -- the same bits as dropout_scale
-        const uint32_t xb0 = (uint32_t)mrow * 0x9E3779B9u + hseed + (uint32_t)((lane >> 4) * 4) * 0x9E3779B9u;
+        // every mask index is < 2^32: mer_hash's first product distributes over the pair index (mrow + j) / 2 =
+        // mrow / 2 + 8 ct + 2 (lane >> 4) + r / 2, so each pair costs one add + the two-multiply finaliser
+        const uint32_t qb0 = (uint32_t)(mrow >> 1) * 0x9E3779B9u + hseed + (uint32_t)(2 * (lane >> 4)) * 0x9E3779B9u;
 #pragma unroll
         for (int ct = 0; ct < KT; ++ct)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            uint32_t xh = xb0 + (uint32_t)(ct * 16 + r) * 0x9E3779B9u;
+          for (int rp = 0; rp < 2; ++rp) {
+            uint32_t xh = qb0 + (uint32_t)(ct * 8 + rp) * 0x9E3779B9u;
             xh ^= xh >> 16;
             xh *= 0x7FEB352Du;
             xh ^= xh >> 15;
             xh *= 0x846CA68Bu;
             xh ^= xh >> 16;
-            if ((xh >> 8) < keep_thr) pb[ct][r] = 0;
+            if ((xh & 0xFFFFu) < keep_thr) pb[ct][2 * rp] = 0;
+            if ((xh >> 16) < keep_thr) pb[ct][2 * rp + 1] = 0;
           }
       } else {
 #pragma unroll
@@ -505,7 +510,7 @@ __global__ __launch_bounds__(64 * NW) void wavlm_attn_kernel(
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int j = ct * 16 + (lane >> 4) * 4 + r;
-            if (dropout_scale(dseed, (uint64_t)(mrow + j), drop_p) == 0.f) pb[ct][r] = 0;
+            if (dropout_scale_pair(dseed, (uint64_t)(mrow + j), drop_p) == 0.f) pb[ct][r] = 0;
           }
       }
     }

@@ -394,11 +394,12 @@ __global__ __launch_bounds__(256) void wavlm_attn_bwd_rows_kernel(
   sum += __shfl_xor(sum, 16);
   sum += __shfl_xor(sum, 32);
   const float inv = 1.f / sum;
-  // train mode: attention-probability dropout of the forward (wavlm_attn_kernel, mask index ((b*H+h)*L + i)*L + j):
+  // train mode: attention-probability dropout of the forward (wavlm_attn_kernel, paired mask index
+  // ((b*H+h)*L + i)*LE + j, LE = L rounded up to even):
   // O = (P o M) V, so dP = (dO V^T) o M and the cols kernel's dV reads P o M; dS keeps the undropped P
   const unsigned long long dseed = mer_site_seed(seed_ptr, site);
-  const long mrow = (((long)b * H + h) * L + (i < L ? i : L - 1)) * L;
-  auto keep = [&](int j) -> float { return dropout_scale(dseed, (uint64_t)(mrow + j), drop_p); };
+  const long mrow = (((long)b * H + h) * L + (i < L ? i : L - 1)) * (long)(L + (L & 1));
+  auto keep = [&](int j) -> float { return dropout_scale_pair(dseed, (uint64_t)(mrow + j), drop_p); };
   float Dr = 0.f;
 #pragma unroll
   for (int tt = 0; tt < NT; ++tt)
@@ -680,8 +681,8 @@ MER_API int mer_gelu_bwd(int rows, int cols, const float* df, const void* z, voi
 }
 
 namespace {
-// y = x * dropout_scale(seed(site), row * cols + col, p): the mask of one dropout call site (the same index as the
-// GEMM-epilogue dropout of mer_gemm_bf16_tr), regenerated; 8 columns per thread
+// y = x * dropout_scale_pair(seed(site), row * cols + col, p): the mask of one dropout call site (the same index as
+// the GEMM-epilogue dropout of mer_gemm_bf16_tr), regenerated; 8 columns per thread
 template <typename TI>
 __global__ __launch_bounds__(256) void dropout_rows_kernel(int rows, int cols, const TI* __restrict__ x, long ldx,
                                                            float* __restrict__ y32, long ldy32, bf16_t* __restrict__ y16,
@@ -694,7 +695,8 @@ __global__ __launch_bounds__(256) void dropout_rows_kernel(int rows, int cols, c
     const int r = (int)(e / c8), c0 = (int)(e - (long)r * c8) * 8;
     float v[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] = ldf<TI>(x, (long)r * ldx + c0 + k) * dropout_scale(seed, (uint64_t)((long)r * cols + c0 + k), p);
+    for (int k = 0; k < 8; ++k) v[k] = ldf<TI>(x, (long)r * ldx + c0 + k);
+    dropout_pairs<8>(v, seed, (uint64_t)((long)r * cols + c0), p);  // cols % 8 == 0: the indices start even
     if (y32) {
       float* o = y32 + (long)r * ldy32 + c0;
       *reinterpret_cast<f32x4*>(o) = f32x4{v[0], v[1], v[2], v[3]};

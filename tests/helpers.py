@@ -88,6 +88,24 @@ def hash_u32(seed: int, idx: np.ndarray) -> np.ndarray:
 
 
 def dropout_keep(base: int, site: int, idx: np.ndarray, p: float) -> np.ndarray:
-    """Boolean keep mask of the kernels' dropout for element indices ``idx``."""
+    """Boolean keep mask of the kernels' dropout_scale for element indices ``idx`` (the xattn head's sites)."""
     u = (hash_u32(site_seed(base, site), idx) >> np.uint32(8)).astype(np.float32) * np.float32(1.0 / 16777216.0)
     return u >= np.float32(p)
+
+
+def dropout_keep_pair(base: int, site: int, idx: np.ndarray, p: float) -> np.ndarray:
+    """Boolean keep mask of dropout_scale_pair (csrc/common.h; the WavLM encoder's sites): one hash word per index
+    pair idx >> 1, its low 16 bits for the even index and the high 16 bits for the odd one, kept when >= ceil(p 2^16)."""
+    idx = np.asarray(idx, dtype=np.uint64)
+    h = hash_u32(site_seed(base, site), idx >> np.uint64(1))
+    half = np.where((idx & np.uint64(1)) == 1, h >> np.uint32(16), h & np.uint32(0xFFFF))
+    thr = np.uint32(np.ceil(np.float32(p) * np.float32(65536.0)))
+    return half >= thr
+
+
+def attention_mask_index(B: int, H: int, L: int) -> np.ndarray:
+    """Mask indices of the WavLM attention-probability dropout for [B, H, L, L]: ((b*H + h)*L + i)*LE + j with the
+    row stride LE = L rounded up to even (so a row's keys pair up)."""
+    le = L + (L & 1)
+    rows = np.arange(B * H * L, dtype=np.uint64)[:, None] * np.uint64(le)
+    return (rows + np.arange(L, dtype=np.uint64)[None, :]).reshape(-1)

@@ -19,6 +19,7 @@ import pytest
 import torch
 
 from oracle import params, wavlm_ref
+from tests.helpers import attention_mask_index
 from tests.test_wavlm_gpu import build_backbone, rel_rms
 
 pytestmark = pytest.mark.gpu
@@ -41,11 +42,11 @@ def _rt(t):
 
 def _mask(base, site, p, shape, idx=None):
     """The kernels' dropout multiplier (0 or 1/(1-p), float32) for call site ``site``, element index = flat
-    position (row * cols + col) unless ``idx`` is given."""
-    from tests.helpers import dropout_keep
+    position (row * cols + col) unless ``idx`` is given (the WavLM sites' paired mask, dropout_keep_pair)."""
+    from tests.helpers import dropout_keep_pair
 
     n = int(np.prod(shape))
-    keep = dropout_keep(base, site, np.arange(n, dtype=np.uint64) if idx is None else idx, p)
+    keep = dropout_keep_pair(base, site, np.arange(n, dtype=np.uint64) if idx is None else idx, p)
     return torch.from_numpy(keep.reshape(shape).astype(np.float32) * np.float32(1.0 / (1.0 - np.float32(p))))
 
 
@@ -77,7 +78,7 @@ def _layer_matched(p, x, pb, li, last, drop=None):
 
         base, pa, ph, pc = drop
         s_att, s_out, s_act, s_ffn = _layer_sites(li)
-        prob = prob * _mask(base, s_att, pa, (B, H, L, L))  # index ((b*H + h)*L + i)*L + j
+        prob = prob * _mask(base, s_att, pa, (B, H, L, L), idx=attention_mask_index(B, H, L))
         m_out = _mask(base, s_out, ph, (B, L, D))
         m_act = _mask(base, s_act, pc, (B, L, 4 * D))
         m_ffn = _mask(base, s_ffn, ph, (B, L, D))
@@ -328,7 +329,7 @@ def test_attention_backward_kernel_vs_fp64(drop_p):
     sc = (q64 * scale) @ k64.transpose(-1, -2) + gate * pb[None]
     prob = torch.softmax(sc, -1)
     if drop_p > 0:
-        prob = prob * _mask(base, site, drop_p, (B, H, L, L)).double()
+        prob = prob * _mask(base, site, drop_p, (B, H, L, L), idx=attention_mask_index(B, H, L)).double()
     o = (prob @ v64).transpose(1, 2).reshape(B * L, D)
     (o * dout.double()).sum().backward()
     ref = {"dq": q64.grad.transpose(1, 2).reshape(B * L, D), "dk": k64.grad.transpose(1, 2).reshape(B * L, D),
