@@ -402,6 +402,14 @@ int mer_conv_wgrad(int N, int H, int W, int C, int Creal, int K, int R, int S, i
 /* mer_conv_wgrad with an explicit kernel: -1 auto, 1 4-wave tiles, 2 8-wave tiles (the default). */
 int mer_conv_wgrad_ex(int N, int H, int W, int C, int Creal, int K, int R, int S, int stride, int pad, const void* x,
                       const void* dy, float* dw, int splits, float* workspace, int variant, void* stream);
+/* The split-K pass of mer_conv_wgrad alone: workspace = splits x [K][R*S*C] fp32 partial slabs, folded later by
+ * mer_wgrad_fold_batch (one launch for all weight gradients of a backward segment). */
+int mer_conv_wgrad_partials(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, const void* x,
+                            const void* dy, int splits, float* workspace, int variant, void* stream);
+/* Fold n <= 32 deferred slab sets in one launch.  rows: n x 8 int64 {ws, dw, map, K, C, Creal, R*S, splits}:
+ * dw[k][c][r][s] += sum_z ws[z][k][(r*S+s)*C + c] for c < Creal (fixed split order), or, with map != NULL
+ * (int32 [R*S*C], -1 = dropped), dw[k][map[j]] += sum_z ws[z][k][j] with Creal = dw floats per k. */
+int mer_wgrad_fold_batch(int n, const long long* rows, void* stream);
 
 /* NCHW fp32 frames -> NHWC bf16 with channels zero-padded to Cp (<= 16). */
 int mer_pack_input_nhwc(int N, int C, int H, int W, int Cp, const float* x, void* y, void* stream);

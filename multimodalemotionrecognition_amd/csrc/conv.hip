@@ -618,6 +618,63 @@ __global__ __launch_bounds__(256) void wgrad_scatter_kernel(int C, int Creal, in
   }
 }
 
+// Batched fold of deferred split-K partial slabs: every weight gradient of one backward segment in ONE launch
+// instead of one or two per convolution (the folds were ~30 launches of 5-12 us each on the critical stream).
+// Record r: dw_r[k][c][tap] += sum_z ws_r[z][k][tap*C + c] (c < Creal), or with a scatter map
+// dw_r[k][map[j]] for source column j = tap*C + c (-1: dropped) -- the stem's 4x4 space-to-depth form
+// gathered back to 7x7x3.  Threads walk the SOURCE order (coalesced slab reads, the bulk of the bytes);
+// a block owns E = 256/SG source elements and SG split-groups (thread (sg, e) sums splits sg, sg+SG, ...
+// with 4 loads in flight, the SG partials meet in LDS in order) -- fixed order, deterministic.
+struct FoldRec {
+  const float* ws;
+  float* dw;
+  const int* map;
+  int K, C, Creal, RS, splits, SG, blk0, nblk;
+};
+constexpr int kFoldMaxRecs = 32;
+struct FoldTable {
+  int n;
+  FoldRec r[kFoldMaxRecs];
+};
+
+__global__ __launch_bounds__(256) void wgrad_fold_batch_kernel(FoldTable t) {
+  __shared__ float part[256];
+  int ri = 0;
+  while (ri + 1 < t.n && (int)blockIdx.x >= t.r[ri + 1].blk0) ++ri;
+  const FoldRec& R = t.r[ri];
+  const int SG = R.SG, E = 256 / SG, e = threadIdx.x % E, sg = threadIdx.x / E;
+  const long row = (long)R.RS * R.C, total = (long)R.K * row;
+  const long idx = (long)((int)blockIdx.x - R.blk0) * E + e;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  if (idx < total) {
+    const float* src = R.ws + idx;
+    int z = sg;
+    for (; z + 3 * SG < R.splits; z += 4 * SG) {
+      a0 += src[(long)z * total];
+      a1 += src[(long)(z + SG) * total];
+      a2 += src[(long)(z + 2 * SG) * total];
+      a3 += src[(long)(z + 3 * SG) * total];
+    }
+    for (; z < R.splits; z += SG) a0 += src[(long)z * total];
+  }
+  part[threadIdx.x] = (a0 + a1) + (a2 + a3);
+  __syncthreads();
+  if (sg != 0 || idx >= total) return;
+  float s = 0.f;
+  for (int q = 0; q < SG; ++q) s += part[q * E + e];
+  const int k = (int)(idx / row), j = (int)(idx - (long)k * row);
+  int o;
+  if (R.map) {
+    o = R.map[j];
+  } else {
+    const int tap = j / R.C, c = j - tap * R.C;
+    o = c < R.Creal ? c * R.RS + tap : -1;
+  }
+  if (o < 0) return;
+  const long per_k = R.map ? (long)R.Creal : (long)R.Creal * R.RS;  // map records: Creal = output floats per k
+  R.dw[(long)k * per_k + o] += s;
+}
+
 
 // ---------------------------------------------------------------------------------------
 // Pipelined fwd / dgrad implicit GEMM: the im2col A tile and the weight tile are DMA'd straight into
@@ -1320,7 +1377,7 @@ MER_API int mer_conv_wgrad(int N, int H, int W, int C, int Creal, int K, int R, 
 
 static int conv_wgrad_impl(int N, int H, int W, int C, int Creal, int K, int R, int S, int stride, int pad,
                            const void* x, const void* dy, long ldy, float* dw, int splits, float* workspace,
-                           int variant, void* stream) {
+                           int variant, void* stream, bool fold = true) {
   if (C % 8 || K % 8 || variant < -1 || variant > 7 || R * S > 49) return (int)hipErrorInvalidValue;
   if (variant == -1) variant = wgrad_default_variant(K);
   WgradGeom g{};
@@ -1364,6 +1421,7 @@ static int conv_wgrad_impl(int N, int H, int W, int C, int Creal, int K, int R, 
     else
       hipLaunchKernelGGL((wgrad_kernel<128, 128, 2, 4>), grid, dim3(512), 0, st, g);
   }
+  if (!fold) MER_LAUNCH_CHECK();  // partial slabs left for mer_wgrad_fold_batch
   static const int fold_max = [] {  // MER_WGRAD_FOLD_MAX: most slabs folded in the single fold+scatter pass (A/B)
     const char* e = getenv("MER_WGRAD_FOLD_MAX");
     return e ? atoi(e) : 16;
@@ -1387,6 +1445,37 @@ MER_API int mer_conv_wgrad_ex(int N, int H, int W, int C, int Creal, int K, int 
                               const void* x, const void* dy, float* dw, int splits, float* workspace, int variant,
                               void* stream) {
   return conv_wgrad_impl(N, H, W, C, Creal, K, R, S, stride, pad, x, dy, K, dw, splits, workspace, variant, stream);
+}
+
+MER_API int mer_conv_wgrad_partials(int N, int H, int W, int C, int K, int R, int S, int stride, int pad,
+                                    const void* x, const void* dy, int splits, float* workspace, int variant,
+                                    void* stream) {
+  return conv_wgrad_impl(N, H, W, C, C, K, R, S, stride, pad, x, dy, K, nullptr, splits, workspace, variant, stream,
+                         false);
+}
+
+// rows: n x 8 int64 {ws, dw, map, K, C, Creal (map records: output floats per k), R*S, splits}
+MER_API int mer_wgrad_fold_batch(int n, const long long* rows, void* stream) {
+  if (n < 1 || n > kFoldMaxRecs) return (int)hipErrorInvalidValue;
+  FoldTable t{};
+  t.n = n;
+  int blk = 0;
+  for (int i = 0; i < n; ++i) {
+    const long long* q = rows + 8 * i;
+    FoldRec& r = t.r[i];
+    r.ws = (const float*)q[0]; r.dw = (float*)q[1]; r.map = (const int*)q[2];
+    r.K = (int)q[3]; r.C = (int)q[4]; r.Creal = (int)q[5]; r.RS = (int)q[6]; r.splits = (int)q[7];
+    if (!r.ws || !r.dw || r.K < 1 || r.C < 1 || r.RS < 1 || r.splits < 1 || r.Creal < 1 ||
+        (!r.map && r.Creal > r.C))
+      return (int)hipErrorInvalidValue;
+    r.SG = r.splits > 48 ? 16 : (r.splits > 12 ? 4 : 1);
+    const long total = (long)r.K * r.RS * r.C;
+    r.blk0 = blk;
+    r.nblk = (int)((total + 256 / r.SG - 1) / (256 / r.SG));
+    blk += r.nblk;
+  }
+  hipLaunchKernelGGL(wgrad_fold_batch_kernel, dim3(blk), dim3(256), 0, (hipStream_t)stream, t);
+  MER_LAUNCH_CHECK();
 }
 
 // Linear weight gradient as a 1x1 convolution over M "pixels": dw[n][k] += sum_m dy[m][n] x[m][k].

@@ -514,18 +514,57 @@ def _wgrad_min_pix(out_elems, tiles):
     return 256 if out_elems <= 65536 else (512 if tiles >= 96 else 1024)
 
 
-def conv_wgrad(x, dy, dw, R, S, stride, pad, creal=None, variant=-1, splits=None):
+class WgradFolds:
+    """Deferred split-K folds of one backward segment: conv_wgrad(..., defer=self) launches only the partial-slab
+    pass and records (slabs, dw); flush() folds every record in ONE mer_wgrad_fold_batch launch on the current
+    stream.  The slab tensors stay referenced until the flush is enqueued (stream order then protects them)."""
+
+    MAX = 32
+
+    def __init__(self):
+        self.rows, self.keep = [], []
+
+    def add(self, ws, dw, Kc, C, creal, RS, splits, map_=None):
+        self.rows.append([ws.data_ptr(), dw.data_ptr(), _ptr(map_), Kc, C, creal, RS, splits])
+        self.keep += [ws, dw, map_]
+
+    def flush(self):
+        import numpy as np
+        for i in range(0, len(self.rows), self.MAX):
+            tab = np.ascontiguousarray(np.array(self.rows[i:i + self.MAX], dtype=np.int64))
+            _launch("wgrad_fold_batch", (len(tab),), "mer_wgrad_fold_batch", len(tab), tab.ctypes.data, stream_ptr())
+        self.rows, self.keep = [], []
+
+
+def conv_wgrad(x, dy, dw, R, S, stride, pad, creal=None, variant=-1, splits=None, defer=None, dw_map=None):
+    """dw += weight gradient.  ``defer`` (a WgradFolds): leave the split-K slabs for its batched fold.  ``dw_map``
+    (deferred only; int32 [R*S*C], -1 dropped): dw is any fp32 tensor, slab column j folds into dw[k].flat[map[j]]
+    (the stem's space-to-depth gradient gathered straight into the 7x7 weight)."""
     N, H, W, C = x.shape
     Kc = dy.shape[-1]
     Ho, Wo = (H + 2 * pad - R) // stride + 1, (W + 2 * pad - S) // stride + 1
     creal = C if creal is None else creal
-    if tuple(dy.shape) != (N, Ho, Wo, Kc) or tuple(dw.shape) != (Kc, creal, R, S) or dw.dtype != torch.float32:
+    if dw_map is not None:
+        if defer is None or dw_map.dtype != torch.int32 or dw_map.numel() != R * S * C or not dw.is_contiguous():
+            raise ValueError("conv_wgrad dw_map: deferred fold, int32 [R*S*C], contiguous dw")
+        if dw.shape[0] != Kc or dw.dtype != torch.float32:
+            raise ValueError("conv_wgrad shapes")
+    elif tuple(dy.shape) != (N, Ho, Wo, Kc) or tuple(dw.shape) != (Kc, creal, R, S) or dw.dtype != torch.float32:
+        raise ValueError("conv_wgrad shapes")
+    if tuple(dy.shape) != (N, Ho, Wo, Kc):
         raise ValueError("conv_wgrad shapes")
     P = N * Ho * Wo
     tiles = ((Kc + 127) // 128) * ((R * S * C + 127) // 128)
     if splits is None:  # ~768 workgroups (3 per CU), >= _wgrad_min_pix pixels each
         splits = int(max(1, min(-(-_WGRAD_WGS // tiles), P // _wgrad_min_pix(Kc * R * S * C, tiles))))
     ws = torch.empty(splits * Kc * R * S * C, device=x.device, dtype=torch.float32)
+    if defer is not None:
+        _launch("conv_wgrad", (N, H, W, C, Kc, R, stride), "mer_conv_wgrad_partials", N, H, W, C, Kc, R, S, stride,
+                pad, x.data_ptr(), dy.data_ptr(), int(splits), ws.data_ptr(), int(variant), stream_ptr())
+        pps = (-(-P // splits) + 63) // 64 * 64  # conv_wgrad_impl: every split non-empty, 64-pixel granules
+        eff = -(-P // pps)
+        defer.add(ws, dw, Kc, C, dw.numel() // Kc if dw_map is not None else creal, R * S, eff, dw_map)
+        return
     _launch("conv_wgrad", (N, H, W, C, Kc, R, stride), "mer_conv_wgrad_ex", N, H, W, C, creal, Kc, R, S, stride, pad,
             x.data_ptr(), dy.data_ptr(), dw.data_ptr(), int(splits), ws.data_ptr(), int(variant), stream_ptr())
 

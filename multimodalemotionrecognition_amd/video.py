@@ -365,6 +365,20 @@ def _stem_wgrad_index(R: int, S: int, C: int, device) -> torch.Tensor:
     return idx.view(-1).to(device)
 
 
+def _stem_wgrad_map(R: int, S: int, C: int, device) -> torch.Tensor:
+    """int32 [Ro*So*16]: for each column (tap, s2d channel) of the stem's wgrad slabs, the flat (c, r, s) index of
+    the 7x7 weight it is, or -1 (the zero-padded taps / channels); the inverse of _stem_wgrad_index."""
+    So, Ro = (S + 2) // 2, (R + 2) // 2
+    m = torch.full((Ro * So * S2D_CH,), -1, dtype=torch.int32)
+    for c in range(C):
+        for r in range(R):
+            for s_ in range(S):
+                ry, dy = divmod(r + 1, 2)
+                rx, dx = divmod(s_ + 1, 2)
+                m[(ry * So + rx) * S2D_CH + (dy * 2 + dx) * C + c] = (c * R + r) * S + s_
+    return m.to(device)
+
+
 def _conv_bn(trunk, conv, bn, x, stride, pad, training, arena=None, rs=None):
     """conv (+ fused batch stats) -> (conv output, (mean, rstd))."""
     Kc, _, R, S = conv.weight.shape
@@ -514,6 +528,10 @@ def _bnr_target(blk_sv, blk, arena):
 # prefetched WavLM stream a third stream only adds contention and graph-branch overhead.
 WGRAD_STREAM = int(os.environ.get("MER_WGRAD_STREAM", "0"))  # 1: every block, 2: layer1 blocks only (A/B)
 _WGRAD_STREAMS = {}
+# Deferred weight-gradient folds (default on; MER_WGRAD_DEFER=0 folds after every wgrad, A/B): the wgrad launches
+# leave their split-K slabs and the segment's join folds them all in one mer_wgrad_fold_batch launch -- ~30 launches
+# of 5-12 us each off the critical stream per step (the stem's zero / gather / add included).
+WGRAD_DEFER = os.environ.get("MER_WGRAD_DEFER", "1") != "0"
 
 
 class _WgradLane:
@@ -525,6 +543,7 @@ class _WgradLane:
         self.enabled = WGRAD_STREAM > 0 and device.type == "cuda"
         self.only_below = 2 if WGRAD_STREAM == 2 else None  # block index bound for the fork (layer1 = blocks 0, 1)
         self.keep = []
+        self.folds = K.WgradFolds() if WGRAD_DEFER and not self.enabled else None
         if self.enabled:
             idx = device.index if device.index is not None else torch.cuda.current_device()
             self.stream = _WGRAD_STREAMS.get(idx)
@@ -541,6 +560,8 @@ class _WgradLane:
         self.keep.extend(reads)
 
     def join(self):
+        if self.folds is not None:
+            self.folds.flush()
         if self.enabled and self.keep:
             torch.cuda.current_stream().wait_stream(self.stream)
         self.keep = []
@@ -580,7 +601,7 @@ def block_backward(trunk, blk: BasicBlock, sv, dx: torch.Tensor, grads, training
     # conv2 (its dgrad also reduces bn1's backward sums: g = da1 * (ba1 > 0))
     w2 = _grad(blk.conv2.weight, grads)
     if w2 is not None:
-        lane.run(lambda: K.conv_wgrad(ba1, dc2, w2, 3, 3, 1, 1), ba1, dc2, w2, block=bidx)
+        lane.run(lambda: K.conv_wgrad(ba1, dc2, w2, 3, 3, 1, 1, defer=lane.folds), ba1, dc2, w2, block=bidx)
     da1 = torch.empty_like(ba1)
     C1 = bc1.shape[-1]
     red1p = arena.take(C1, parts=K.bn_red_rows(ba1.numel() // C1))
@@ -590,14 +611,14 @@ def block_backward(trunk, blk: BasicBlock, sv, dx: torch.Tensor, grads, training
     # conv1 (+ downsample) -> dx of the block input (+ the preceding block's bn2 / downsample reductions)
     w1 = _grad(blk.conv1.weight, grads)
     if w1 is not None:
-        lane.run(lambda: K.conv_wgrad(xin, dc1, w1, 3, 3, s, 1), xin, dc1, w1, block=bidx)
+        lane.run(lambda: K.conv_wgrad(xin, dc1, w1, 3, 3, s, 1, defer=lane.folds), xin, dc1, w1, block=bidx)
     dxin = torch.empty_like(xin)
     Cin = xin.shape[-1]
     bnr, nxt = _bnr_target(prev[0], prev[1], arena) if prev is not None else (None, None)
     if cd is not None:
         wd = _grad(blk.downsample[0].weight, grads)
         if wd is not None:
-            lane.run(lambda: K.conv_wgrad(xin, dcd, wd, 1, 1, s, 0), xin, dcd, wd, block=bidx)
+            lane.run(lambda: K.conv_wgrad(xin, dcd, wd, 1, 1, s, 0, defer=lane.folds), xin, dcd, wd, block=bidx)
         dxd = torch.empty_like(xin)
         K.conv_dgrad(dcd, trunk.packed(blk.downsample[0], Cin, True), dxd, 1, 1, s, 0)
         K.conv_dgrad(dc1, trunk.packed(blk.conv1, Cin, True), dxin, 3, 3, s, 1, residual=dxd, bnr=bnr)
@@ -670,13 +691,21 @@ def trunk_backward_finish(trunk, saved, state, training, force_pack=False):
         w = _grad(trunk[0].weight, grads)
         if w is not None:  # wgrad of the 4x4 space-to-depth form, then gathered back to [64][3][7][7]
             Kc, Cin, R, S = trunk[0].weight.shape
-            ws2d = torch.empty(Kc, S2D_CH, (R + 2) // 2, (S + 2) // 2, device=dev, dtype=torch.float32)
-            ws2d.zero_()
-            K.conv_wgrad(x0, dc1, ws2d, ws2d.shape[2], ws2d.shape[3], 1, 0)
-            idx = trunk.__dict__.get("_mer_stem_idx")
-            if idx is None or idx.device != dev:
-                idx = trunk.__dict__["_mer_stem_idx"] = _stem_wgrad_index(R, S, Cin, dev)
-            w.add_(ws2d.view(Kc, -1).index_select(1, idx).view_as(w))
+            Ro, So = (R + 2) // 2, (S + 2) // 2
+            folds = state["lane"].folds
+            if folds is not None:  # slab column (tap, s2d channel) folds straight into the 7x7 weight
+                m = trunk.__dict__.get("_mer_stem_map")
+                if m is None or m.device != dev:
+                    m = trunk.__dict__["_mer_stem_map"] = _stem_wgrad_map(R, S, Cin, dev)
+                K.conv_wgrad(x0, dc1, w, Ro, So, 1, 0, defer=folds, dw_map=m)
+            else:
+                ws2d = torch.empty(Kc, S2D_CH, Ro, So, device=dev, dtype=torch.float32)
+                ws2d.zero_()
+                K.conv_wgrad(x0, dc1, ws2d, Ro, So, 1, 0)
+                idx = trunk.__dict__.get("_mer_stem_idx")
+                if idx is None or idx.device != dev:
+                    idx = trunk.__dict__["_mer_stem_idx"] = _stem_wgrad_index(R, S, Cin, dev)
+                w.add_(ws2d.view(Kc, -1).index_select(1, idx).view_as(w))
         state["lane"].join()
         return grads
 

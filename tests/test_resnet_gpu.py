@@ -309,6 +309,72 @@ def test_wgrad_variants_bit_identical(N, H, C, Kc, R, stride, pad):
         assert torch.equal(out[0], o), f"variant {v} differs"
 
 
+def test_wgrad_fold_batch_matches_immediate_fold():
+    """Deferred slabs folded by ONE mer_wgrad_fold_batch launch == the per-conv fold (fold+scatter below 17 slabs,
+    reduce + scatter above), for records of 1-12, 13-48 and > 48 slabs, Creal < C, and the stem's map record
+    (space-to-depth slabs gathered into the 7x7x3 weight); dw accumulates (+=) like the immediate path."""
+    from multimodalemotionrecognition_amd import kernels as K
+    from multimodalemotionrecognition_amd.video import S2D_CH, _stem_wgrad_index, _stem_wgrad_map
+
+    torch.manual_seed(6)
+    cases = [(2, 28, 64, 64, 3, 1, 1, None, 4), (4, 14, 128, 256, 3, 2, 1, None, 20),
+             (32, 28, 64, 64, 3, 1, 1, None, 150), (2, 30, 8, 64, 7, 2, 3, 3, None), (8, 7, 256, 512, 1, 2, 0, None, None)]
+    folds = K.WgradFolds()
+    refs, outs, inits = [], [], []
+    for N, H, C, Kc, R, stride, pad, creal, splits in cases:
+        Ho = (H + 2 * pad - R) // stride + 1
+        x = torch.randn(N, H, H, C, device="cuda").bfloat16()
+        dy = torch.randn(N, Ho, Ho, Kc, device="cuda").bfloat16()
+        cr = creal or C
+        init = torch.randn(Kc, cr, R, R, device="cuda")
+        ref, out = init.clone(), init.clone()
+        K.conv_wgrad(x, dy, ref, R, R, stride, pad, creal=cr, splits=splits)
+        K.conv_wgrad(x, dy, out, R, R, stride, pad, creal=cr, splits=splits, defer=folds)
+        refs.append(ref)
+        outs.append(out)
+        inits.append(init)
+    # stem: 4x4 stride-1 wgrad on 16 space-to-depth channels, gathered to [64][3][7][7]
+    xs = torch.randn(4, 31, 31, S2D_CH, device="cuda").bfloat16()
+    dys = torch.randn(4, 28, 28, 64, device="cuda").bfloat16()
+    ws = torch.zeros(64, S2D_CH, 4, 4, device="cuda")
+    K.conv_wgrad(xs, dys, ws, 4, 4, 1, 0)
+    w0 = torch.randn(64, 3, 7, 7, device="cuda")
+    refs.append(w0 + ws.view(64, -1).index_select(1, _stem_wgrad_index(7, 7, 3, ws.device)).view(64, 3, 7, 7))
+    out = w0.clone()
+    K.conv_wgrad(xs, dys, out, 4, 4, 1, 0, defer=folds, dw_map=_stem_wgrad_map(7, 7, 3, out.device))
+    outs.append(out)
+    inits.append(w0)
+    torch.cuda.synchronize()
+    assert all(torch.equal(o, i) for o, i in zip(outs, inits))  # nothing folded before the flush
+    folds.flush()
+    for i, (r, o) in enumerate(zip(refs, outs)):
+        assert (o - r).abs().max() <= 1e-5 * r.abs().max(), i
+
+
+def test_trunk_backward_deferred_folds_match(monkeypatch):
+    """The train step's trunk backward with deferred batched folds == with a fold after every wgrad (fp32
+    summation order only), and bit-reproducible run to run."""
+    from multimodalemotionrecognition_amd import video as V
+
+    m, _ = build_trunk()
+    m.train(True)
+    video, _, _ = params.clip_inputs(1, frames=8, seed=44)
+    x = torch.from_numpy(video[0]).cuda()
+    res = []
+    for defer in (False, True, True):
+        monkeypatch.setattr(V, "WGRAD_DEFER", defer)
+        f, saved = V.trunk_forward(m, x, True)
+        g = V.trunk_backward(m, saved, torch.ones_like(f), True)
+        res.append({k: v.clone() for k, v in g.items()})
+        for q in m.parameters():
+            q.grad = None
+    for q in m.parameters():
+        a, b, c = (r.get(id(q)) for r in res)
+        if a is not None:
+            assert torch.equal(b, c)
+            assert (a - b).abs().max() <= 1e-5 * a.abs().max() + 1e-12
+
+
 @pytest.mark.parametrize("H", [112, 32])
 def test_space_to_depth_stem_vs_torch(H):
     """The stem conv (7x7, stride 2, pad 3) run as a 4x4 stride-1 conv on 2x2 space-to-depth frames:
