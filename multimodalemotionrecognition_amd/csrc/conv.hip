@@ -2181,8 +2181,9 @@ MER_API int mer_maxpool_bwd(int N, int H, int W, int C, const void* dy, const vo
 // ---------------------------------------------------------------------------------------
 // Fused ResNet stem tail (video.py:21-23 -> torchvision conv1/bn1/relu/maxpool), channel-last, C = 64:
 //   forward:  p = maxpool3x3s2p1( a ),  a = bf16(relu(x * scale + shift))  -- a is never stored;
-//   backward: g = bf16(maxpool gather of dp) * (a > 0), recomputed from (dp, argmax, x, BN) in both the
-//             BatchNorm reduction pass and the apply pass, so neither a nor da goes through HBM.
+//   backward: da = maxpool gather of dp (materialised once by maxpool_bwd), g = da * (a > 0) with the ReLU
+//             mask recomputed from (x, BN) in the BatchNorm reduction and apply passes, so a is never stored
+//             (gathering dp inside both passes instead was measured 2x slower: DESIGN.md section 4e).
 // Same roundings, tap order and tie rule as bn_apply -> maxpool_fwd / maxpool_bwd -> bn_bwd_*.
 // ---------------------------------------------------------------------------------------
 
