@@ -1454,6 +1454,15 @@ MER_API int mer_conv_wgrad_partials(int N, int H, int W, int C, int K, int R, in
                          false);
 }
 
+static int fold_sg_max() {  // MER_FOLD_SG: split groups per block for many-slab records (A/B), 8 default
+  static const int v = [] {
+    const char* e = getenv("MER_FOLD_SG");
+    const int x = e ? atoi(e) : 8;
+    return (x == 4 || x == 8 || x == 16) ? x : 8;
+  }();
+  return v;
+}
+
 // rows: n x 8 int64 {ws, dw, map, K, C, Creal (map records: output floats per k), R*S, splits}
 MER_API int mer_wgrad_fold_batch(int n, const long long* rows, void* stream) {
   if (n < 1 || n > kFoldMaxRecs) return (int)hipErrorInvalidValue;
@@ -1468,7 +1477,9 @@ MER_API int mer_wgrad_fold_batch(int n, const long long* rows, void* stream) {
     if (!r.ws || !r.dw || r.K < 1 || r.C < 1 || r.RS < 1 || r.splits < 1 || r.Creal < 1 ||
         (!r.map && r.Creal > r.C))
       return (int)hipErrorInvalidValue;
-    r.SG = r.splits > 48 ? 16 : (r.splits > 12 ? 4 : 1);
+    // SG <= 8: E >= 32 consecutive floats per split group, i.e. whole 128-byte lines (SG 16 read half lines: the
+    // slabs are cold by the time the segment folds, so half-used lines cost HBM bytes)
+    r.SG = r.splits > 48 ? fold_sg_max() : (r.splits > 12 ? 4 : 1);
     const long total = (long)r.K * r.RS * r.C;
     r.blk0 = blk;
     r.nblk = (int)((total + 256 / r.SG - 1) / (256 / r.SG));

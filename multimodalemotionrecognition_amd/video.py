@@ -532,6 +532,7 @@ _WGRAD_STREAMS = {}
 # leave their split-K slabs and the segment's join folds them all in one mer_wgrad_fold_batch launch -- ~30 launches
 # of 5-12 us each off the critical stream per step (the stem's zero / gather / add included).
 WGRAD_DEFER = os.environ.get("MER_WGRAD_DEFER", "1") != "0"
+WGRAD_FLUSH_EVERY = int(os.environ.get("MER_WGRAD_FLUSH_EVERY", "0"))  # >0: fold after every N blocks (A/B)
 
 
 class _WgradLane:
@@ -668,6 +669,9 @@ def _backward_blocks(trunk, saved, state, lo, training):
                                                    pre=state["pre"], prev=prev, arena=state["arena"],
                                                    lane=state["lane"], bidx=i)
         state["i"] = i - 1
+        folds = state["lane"].folds
+        if WGRAD_FLUSH_EVERY > 0 and folds is not None and i % WGRAD_FLUSH_EVERY == 0:
+            folds.flush()
 
 
 @torch.no_grad()
