@@ -514,6 +514,14 @@ def _wgrad_min_pix(out_elems, tiles):
     return 256 if out_elems <= 65536 else (512 if tiles >= 96 else 1024)
 
 
+def wgrad_split_count(P: int, splits: int) -> int:
+    """The split count a wgrad launch asked for ``splits`` over P output pixels really uses (conv.hip
+    conv_wgrad_impl): 64-pixel granules per split, every split non-empty."""
+    splits = max(1, int(splits))
+    pps = (-(-P // splits) + 63) // 64 * 64
+    return -(-P // pps)
+
+
 class WgradFolds:
     """Deferred split-K folds of one backward segment: conv_wgrad(..., defer=self) launches only the partial-slab
     pass and records (slabs, dw); flush() folds every record in ONE mer_wgrad_fold_batch launch on the current
@@ -561,9 +569,8 @@ def conv_wgrad(x, dy, dw, R, S, stride, pad, creal=None, variant=-1, splits=None
     if defer is not None:
         _launch("conv_wgrad", (N, H, W, C, Kc, R, stride), "mer_conv_wgrad_partials", N, H, W, C, Kc, R, S, stride,
                 pad, x.data_ptr(), dy.data_ptr(), int(splits), ws.data_ptr(), int(variant), stream_ptr())
-        pps = (-(-P // splits) + 63) // 64 * 64  # conv_wgrad_impl: every split non-empty, 64-pixel granules
-        eff = -(-P // pps)
-        defer.add(ws, dw, Kc, C, dw.numel() // Kc if dw_map is not None else creal, R * S, eff, dw_map)
+        defer.add(ws, dw, Kc, C, dw.numel() // Kc if dw_map is not None else creal, R * S,
+                  wgrad_split_count(P, splits), dw_map)
         return
     _launch("conv_wgrad", (N, H, W, C, Kc, R, stride), "mer_conv_wgrad_ex", N, H, W, C, creal, Kc, R, S, stride, pad,
             x.data_ptr(), dy.data_ptr(), dw.data_ptr(), int(splits), ws.data_ptr(), int(variant), stream_ptr())
