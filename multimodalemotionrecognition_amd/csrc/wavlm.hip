@@ -279,6 +279,7 @@ MER_API int mer_at_read(long long* host) {
 namespace {
 constexpr int ADH = 64, APAD = ADH + 8;
 typedef __attribute__((ext_vector_type(4))) short s16x4;
+typedef __attribute__((ext_vector_type(2))) uint32_t u32x2;
 }
 
 // KT: key tiles held in registers (compile time, >= ceil(L / 16)): 10 for L <= 160 (the 3 s clips: L = 149), 16 up to
@@ -477,14 +478,18 @@ __global__ __launch_bounds__(64 * NW) void wavlm_attn_kernel(
     // not enter PV, the kept ones are rescaled by 1/(1-p) with the normaliser
     const long mrow = (((long)b * H + h) * L + i) * LE;  // even: the lane's keys pair up as (r0, r1), (r2, r3)
     float sum = 0.f;
-    s16x4 pb[KT];
+    // P^T as packed bf16 pairs: word pw[ct][rp] = keys (2 rp, 2 rp + 1) of the tile (low half first), the layout of
+    // the PV A operand -- the dropout mask then clears whole 16-bit halves with one AND per pair (per-element
+    // inserts into a short vector compiled to ~25 permutes + an exec-mask branch each)
+    uint32_t pw[KT][2];
 #pragma unroll
     for (int ct = 0; ct < KT; ++ct)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const bf16_t p = f2bf(__expf(s[ct][r] - mx));
-        sum += bf2f(p);
-        pb[ct][r] = (short)p;
+      for (int rp = 0; rp < 2; ++rp) {
+        const bf16_t p0 = f2bf(__expf(s[ct][2 * rp] - mx)), p1 = f2bf(__expf(s[ct][2 * rp + 1] - mx));
+        sum += bf2f(p0);
+        sum += bf2f(p1);
+        pw[ct][rp] = (uint32_t)p0 | ((uint32_t)p1 << 16);
       }
     if (drop_p > 0.f) {  // (uniform) the keep mask, dropout_scale_pair(dseed, mrow + j, p) != 0
       if (idx32) {
@@ -501,16 +506,18 @@ __global__ __launch_bounds__(64 * NW) void wavlm_attn_kernel(
             xh ^= xh >> 15;
             xh *= 0x846CA68Bu;
             xh ^= xh >> 16;
-            if ((xh & 0xFFFFu) < keep_thr) pb[ct][2 * rp] = 0;
-            if ((xh >> 16) < keep_thr) pb[ct][2 * rp + 1] = 0;
+            const uint32_t keep = ((xh & 0xFFFFu) < keep_thr ? 0u : 0x0000FFFFu) | ((xh >> 16) < keep_thr ? 0u : 0xFFFF0000u);
+            pw[ct][rp] &= keep;
           }
       } else {
 #pragma unroll
         for (int ct = 0; ct < KT; ++ct)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int j = ct * 16 + (lane >> 4) * 4 + r;
-            if (dropout_scale_pair(dseed, (uint64_t)(mrow + j), drop_p) == 0.f) pb[ct][r] = 0;
+          for (int rp = 0; rp < 2; ++rp) {
+            const int j = ct * 16 + (lane >> 4) * 4 + 2 * rp;
+            const bool k0 = dropout_scale_pair(dseed, (uint64_t)(mrow + j), drop_p) != 0.f;
+            const bool k1 = dropout_scale_pair(dseed, (uint64_t)(mrow + j + 1), drop_p) != 0.f;
+            pw[ct][rp] &= (k0 ? 0x0000FFFFu : 0u) | (k1 ? 0xFFFF0000u : 0u);
           }
       }
     }
@@ -526,7 +533,8 @@ __global__ __launch_bounds__(64 * NW) void wavlm_attn_kernel(
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
         const s16x4 va = *reinterpret_cast<const s16x4*>(&Vt[(dt * 16 + (lane & 15)) * VTP + ct * 16 + (lane >> 4) * 4]);
-        o[dt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(va, pb[ct], o[dt], 0, 0, 0);
+        o[dt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(va, __builtin_bit_cast(s16x4, u32x2{pw[ct][0], pw[ct][1]}),
+                                                          o[dt], 0, 0, 0);
       }
     if (i < L) {
       const float inv = (drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f) / sum;

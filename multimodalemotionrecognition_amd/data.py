@@ -205,12 +205,14 @@ def _collate_meta(metas: List[dict]) -> dict:
 
 
 def shard_indices(n: int, rank: int, world: int, shuffle: bool, seed: int, epoch: int) -> np.ndarray:
-    """``torch.utils.data.DistributedSampler`` order (drop_last=False): one permutation of ALL items drawn from
-    (seed + epoch) on every rank, padded by wrapping to a multiple of ``world``, then every ``world``-th index from
-    ``rank`` -- every rank sees the same number of items and, across epochs, different clips."""
-    order = np.arange(n)
+    """``torch.utils.data.DistributedSampler`` order (drop_last=False): one permutation of ALL items drawn by
+    ``torch.randperm`` from a CPU generator seeded with (seed + epoch) on every rank -- the sampler's own draw, so
+    the shuffled order is the reference pipeline's --, padded by wrapping to a multiple of ``world``, then every
+    ``world``-th index from ``rank``: every rank sees the same number of items and, across epochs, different clips."""
     if shuffle:
-        np.random.default_rng(seed + epoch).shuffle(order)
+        order = torch.randperm(n, generator=torch.Generator().manual_seed(int(seed) + int(epoch))).numpy()
+    else:
+        order = np.arange(n)
     total = -(-n // world) * world if n else 0
     if total > n:
         reps = -(-(total - n) // n)

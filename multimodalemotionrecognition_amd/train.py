@@ -184,22 +184,6 @@ def make_loss(fusion_mode: str, label_smoothing: float = 0.0) -> nn.Module:
 EARLY_PREFETCH = os.environ.get("MER_EARLY_PREFETCH", "1") != "0"
 
 
-_HIPRIO = os.environ.get("MER_HIPRIO", "0") != "0"
-_COMPUTE_STREAMS = {}
-
-
-def _compute_stream(t: torch.Tensor):
-    """The high-priority stream TrainStep runs on for t's device (None: CPU tensors or MER_HIPRIO=0)."""
-    if not _HIPRIO or not t.is_cuda:
-        return None
-    idx = t.device.index if t.device.index is not None else torch.cuda.current_device()
-    s = _COMPUTE_STREAMS.get(idx)
-    if s is None:
-        hi = torch.cuda.Stream.priority_range()[1]  # the greatest priority (numerically lowest)
-        s = _COMPUTE_STREAMS[idx] = torch.cuda.Stream(device=idx, priority=hi)
-    return s
-
-
 class TrainStep:
     """One training step of train.py:200-228 on the HIP path: returns (loss, preds) as device tensors."""
 
@@ -215,26 +199,8 @@ class TrainStep:
         """``next_audio``: the NEXT step's waveform batch, already on the device.  With a frozen audio
         encoder its forward is started on a side stream -- at the top of this step's xattn forward (early
         prefetch), else right after the forward -- so it overlaps this step's work
-        (``FusionModel.prefetch_audio``); results are identical either way.
-
-        MER_HIPRIO=1 runs the step on a HIGH-priority stream (ordered after the caller's stream on entry, the
-        caller's stream ordered after it on return), so the dispatcher hands free CUs to the step's kernels first
-        and the prefetched encoder fills what they leave idle.  Off by default: with the per-step stream hops it
-        measured 5.50 vs 5.43 ms in bench.py (profiles/r02c/ab_hiprio_*.json); a training loop that runs
-        entirely on a high-priority stream (bench.py --stream-priority high) needs no hops."""
-        s = _compute_stream(video)
-        if s is None:
-            return self._step(video, audio, labels, next_audio)
-        cur = torch.cuda.current_stream(video.device)
-        s.wait_stream(cur)
-        with torch.cuda.stream(s):
-            out = self._step(video, audio, labels, next_audio)
-        cur.wait_stream(s)
-        for t in (*out, *(x for x in (self.last_losses or ()) if x is not None)):
-            t.record_stream(cur)
-        return out
-
-    def _step(self, video, audio, labels, next_audio):
+        (``FusionModel.prefetch_audio``); results are identical either way.  (A high-priority step stream was
+        measured in round 2 and dropped: 5.50 vs 5.43 ms, profiles/r02c/ab_hiprio_*.json.)"""
         if not self.model.training:  # (a full module-tree walk; skipped when already in train mode)
             self.model.train()
         self.opt.zero_grad()

@@ -174,10 +174,20 @@ class ResNet18Trunk(nn.Sequential):
         and the stem's space-to-depth weight-gradient index (a gradient-cut first step -- gated ModalityDropout
         -- can reach the first backward capture with neither built by an eager backward)."""
         self._pack_plan(True)
-        idx = self.__dict__.get("_mer_stem_idx")
-        if idx is None or idx.device != device:
+        self.stem_wgrad_table(device, WGRAD_DEFER)
+
+    def stem_wgrad_table(self, device, deferred: bool) -> torch.Tensor:
+        """The stem's space-to-depth weight-gradient table on ``device``: the slab-column -> 7x7-weight map of the
+        deferred fold (``deferred``) or the gather index of the immediate one.  Built once (a pageable H2D copy
+        that must not run inside a graph capture, hence prepare_backward)."""
+        key = "_mer_stem_map" if deferred else "_mer_stem_idx"
+        t = self.__dict__.get(key)
+        if t is None or t.device != device:
+            if G.capturing():
+                raise RuntimeError("stem weight-gradient table built inside a graph capture; call prepare_backward")
             Kc, Cin, R, S = self[0].weight.shape
-            self.__dict__["_mer_stem_idx"] = _stem_wgrad_index(R, S, Cin, device)
+            t = self.__dict__[key] = (_stem_wgrad_map if deferred else _stem_wgrad_index)(R, S, Cin, device)
+        return t
 
     def split_params(self, split: int):
         """Parameters whose gradients are final once the backward has passed BasicBlock ``split``."""
@@ -521,51 +531,25 @@ def _bnr_target(blk_sv, blk, arena):
     return (out, bc2, bms2, red2, cd, msd, redd), (red2, redd)
 
 
-# Weight gradients on a second stream (MER_WGRAD_STREAM=1; default inline): a block's wgrad and dgrad read the same
-# upstream gradient and write disjoint buffers, so the wgrad can fork off the current stream and run beside the
-# dgrad and BatchNorm passes, one join per backward (graph) segment.  Deterministic, tested equal -- but measured
-# SLOWER in the train step (175.4 / 176.4 vs 188.3 / 188.4 steps/s, same box, alternating runs): beside the
-# prefetched WavLM stream a third stream only adds contention and graph-branch overhead.
-WGRAD_STREAM = int(os.environ.get("MER_WGRAD_STREAM", "0"))  # 1: every block, 2: layer1 blocks only (A/B)
-_WGRAD_STREAMS = {}
-# Deferred weight-gradient folds (default on; MER_WGRAD_DEFER=0 folds after every wgrad, A/B): the wgrad launches
-# leave their split-K slabs and the segment's join folds them all in one mer_wgrad_fold_batch launch -- ~30 launches
-# of 5-12 us each off the critical stream per step (the stem's zero / gather / add included).
+# Deferred weight-gradient folds (default on; MER_WGRAD_DEFER=0 folds after every wgrad): the wgrad launches leave
+# their split-K slabs and the segment's join folds them all in one mer_wgrad_fold_batch launch -- ~30 launches of
+# 5-12 us each off the critical stream per step (the stem's zero / gather / add included).  (Round 3 also measured
+# the weight gradients on a third stream and folding after every N blocks: both slower or inside the noise, removed.)
 WGRAD_DEFER = os.environ.get("MER_WGRAD_DEFER", "1") != "0"
-WGRAD_FLUSH_EVERY = int(os.environ.get("MER_WGRAD_FLUSH_EVERY", "0"))  # >0: fold after every N blocks (A/B)
 
 
 class _WgradLane:
-    """Fork / join of the weight-gradient stream.  Tensors the forked work reads are kept referenced until the
-    join, so the caching allocator cannot hand their blocks to the current stream while the lane still reads them
-    (the same holds inside a graph capture, where the fork and join are graph edges)."""
+    """The weight-gradient launches of one backward (graph) segment and their deferred folds, flushed at join()."""
 
     def __init__(self, device):
-        self.enabled = WGRAD_STREAM > 0 and device.type == "cuda"
-        self.only_below = 2 if WGRAD_STREAM == 2 else None  # block index bound for the fork (layer1 = blocks 0, 1)
-        self.keep = []
-        self.folds = K.WgradFolds() if WGRAD_DEFER and not self.enabled else None
-        if self.enabled:
-            idx = device.index if device.index is not None else torch.cuda.current_device()
-            self.stream = _WGRAD_STREAMS.get(idx)
-            if self.stream is None:
-                self.stream = _WGRAD_STREAMS[idx] = torch.cuda.Stream(device=idx)
+        self.folds = K.WgradFolds() if WGRAD_DEFER else None
 
     def run(self, fn, *reads, block=None):
-        if not self.enabled or (self.only_below is not None and (block is None or block >= self.only_below)):
-            fn()
-            return
-        self.stream.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(self.stream):
-            fn()
-        self.keep.extend(reads)
+        fn()
 
     def join(self):
         if self.folds is not None:
             self.folds.flush()
-        if self.enabled and self.keep:
-            torch.cuda.current_stream().wait_stream(self.stream)
-        self.keep = []
 
 
 @torch.no_grad()
@@ -669,9 +653,6 @@ def _backward_blocks(trunk, saved, state, lo, training):
                                                    pre=state["pre"], prev=prev, arena=state["arena"],
                                                    lane=state["lane"], bidx=i)
         state["i"] = i - 1
-        folds = state["lane"].folds
-        if WGRAD_FLUSH_EVERY > 0 and folds is not None and i % WGRAD_FLUSH_EVERY == 0:
-            folds.flush()
 
 
 @torch.no_grad()
@@ -698,17 +679,12 @@ def trunk_backward_finish(trunk, saved, state, training, force_pack=False):
             Ro, So = (R + 2) // 2, (S + 2) // 2
             folds = state["lane"].folds
             if folds is not None:  # slab column (tap, s2d channel) folds straight into the 7x7 weight
-                m = trunk.__dict__.get("_mer_stem_map")
-                if m is None or m.device != dev:
-                    m = trunk.__dict__["_mer_stem_map"] = _stem_wgrad_map(R, S, Cin, dev)
-                K.conv_wgrad(x0, dc1, w, Ro, So, 1, 0, defer=folds, dw_map=m)
+                K.conv_wgrad(x0, dc1, w, Ro, So, 1, 0, defer=folds, dw_map=trunk.stem_wgrad_table(dev, True))
             else:
                 ws2d = torch.empty(Kc, S2D_CH, Ro, So, device=dev, dtype=torch.float32)
                 ws2d.zero_()
                 K.conv_wgrad(x0, dc1, ws2d, Ro, So, 1, 0)
-                idx = trunk.__dict__.get("_mer_stem_idx")
-                if idx is None or idx.device != dev:
-                    idx = trunk.__dict__["_mer_stem_idx"] = _stem_wgrad_index(R, S, Cin, dev)
+                idx = trunk.stem_wgrad_table(dev, False)
                 w.add_(ws2d.view(Kc, -1).index_select(1, idx).view_as(w))
         state["lane"].join()
         return grads

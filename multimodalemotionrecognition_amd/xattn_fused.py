@@ -3,9 +3,10 @@
 launches of ``xattn_head.head_forward``.
 
 Scope of the fused path: d_model 128 with 4 heads (the reference's defaults, fusion.py:199-200), mean temporal
-pooling (the fusion default), concat or gated head, no emotion prior, audio features that need no gradient
-(bf16 from the frozen WavLM, or fp32), T <= 16 frames and Ta <= 160 audio frames (3 s clips: 8 and 149).  Everything else -- and INT8
-inference -- runs the unfused schedule, which is the parity reference of this path.  The saved activations
+pooling (the fusion default), concat or gated head, with or without the emotion-prior attention bias (the bias
+enters F2 / F3 / G2 / G3; the prior's own small Linears run beside them, fusion.py:153-184,390-394), audio features
+that need no gradient (bf16 from the frozen WavLM, or fp32), T <= 16 frames and Ta <= 160 audio frames (3 s clips: 8
+and 149).  Everything else -- and INT8 inference -- runs the unfused schedule, which is the parity reference of this path.  The saved activations
 have the unfused schedule's names and layouts, so ``xattn_head.head_backward`` runs unchanged on them.
 """
 from __future__ import annotations
@@ -161,8 +162,9 @@ def fused_forward(p, cfg, v_feat, a_seq, training, rng, ctx, sites):
     dp_path = cfg.drop_path if training else 0.0
     dp_mlp = cfg.mlp_dropout if training else 0.0
     site_prior, site_v2a, site_vpath, site_a2v, site_apath, site_mlp = sites
+    dp_prior = cfg.prior_dropout if (training and cfg.use_prior) else 0.0
     seed = rng if (training and rng is not None) else None
-    if training and (dp_attn > 0 or dp_path > 0 or dp_mlp > 0) and seed is None:
+    if training and (dp_attn > 0 or dp_path > 0 or dp_mlp > 0 or dp_prior > 0) and seed is None:
         raise ValueError("train-mode dropout needs the step's RNG base")
     sp = planes_for(p)
     sp.refresh(transposed=training)  # a training forward is followed by the fused backward
@@ -177,7 +179,6 @@ def fused_forward(p, cfg, v_feat, a_seq, training, rng, ctx, sites):
                    p["v_in_proj.bias"], sp["Wq1"], p["v2a_attn.in_proj_bias"][:d], v, q1)
     sv = ctx.saved
     v2a_bias = a2v_bias = None
-    dp_prior = cfg.prior_dropout if training else 0.0
     if cfg.use_prior:  # the emotion-prior attention biases from the pre-attention tokens (fusion.py:390-391)
         from .xattn_head import linear_runner, prior_forward
         sv.update(v=v, a=a)
