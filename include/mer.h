@@ -351,6 +351,18 @@ int mer_transpose_bf16(int rows, int cols, const void* src, long lds, void* dst,
 int mer_frames_resize_normalize(int N, int H0, int W0, const void* frames, long frame_stride, int S, float mean0,
                                 float mean1, float mean2, float std0, float std1, float std2, float* out, void* stream);
 
+/* cv2.resize(frame, (S, S), INTER_LINEAR) alone (ravdess.py:352): out uint8 [N][S][S][3] (the augmentation's input). */
+int mer_frames_resize_u8(int N, int H0, int W0, const void* frames, long frame_stride, int S, void* out, void* stream);
+/* Train-split video augmentation + normalisation of load_video_frames (ravdess.py:363-389) on resized frames
+ * frames_u8 [N][S][S][3] (N = clips * T): per clip c, clip_params[c] = (factor, noise_scale, ksize) and a noise seed
+ * clip_seeds[c] (DEVICE arrays): uint8 round trip, cv2.GaussianBlur(k, sigma 0) in OpenCV's exact 8U fixed-point form
+ * (BORDER_REFLECT_101), /255, * factor, + noise_scale * ztable[hash(seed, element) >> 16] (ztable: DEVICE fp32
+ * [65536], the inverse normal CDF at (i + 0.5) / 65536), clip to [0, 1], (x - mean) / std -> out fp32 [N][3][S][S].
+ * Replaces: the `if augment:` block of ravdess.py:366-384. */
+int mer_frames_augment_normalize(int N, int S, int T, const void* frames_u8, const float* clip_params,
+                                 const unsigned long long* clip_seeds, const float* ztable, float mean0, float mean1,
+                                 float mean2, float std0, float std1, float std2, float* out, void* stream);
+
 /* load_audio_wav pad / crop (ravdess.py:505-513): out[b][t] = t < lengths[b] ? packed[offsets[b] + t] : 0,
  * out fp32 [B][target]; offsets / lengths are DEVICE int64 arrays (a ragged batch of decoded waveforms). */
 int mer_wav_pad_crop(int B, int target, const float* packed, const long long* offsets, const long long* lengths,

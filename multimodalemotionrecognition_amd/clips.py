@@ -5,11 +5,14 @@ decoded uint8 frames / raw waveforms cross PCIe and the batch is assembled in HB
 * ``preprocess_frames`` -- decoded RGB uint8 frames ``[N, H, W, 3]`` -> ``[N, 3, size, size]`` fp32:
   ``cv2.resize(..., INTER_LINEAR)`` (ravdess.py:352), ``/ 255`` (:363), ImageNet normalisation (:386-389).
 * ``video_clip_batch`` -- ``B`` clips of ``T`` such frames -> the model's ``[B, T, 3, size, size]`` input.
+* ``augment_clips`` -- the train-split video augmentation (ravdess.py:366-384: uint8 round trip,
+  ``cv2.GaussianBlur(k, 0)``, darken, Gaussian noise, clip) + normalisation of ``B`` clips, per-clip draws from
+  ``draw_video_augment``.
 * ``pad_crop_waveforms`` -- a ragged list of mono waveforms -> ``[B, 1, sample_rate * duration]``
   (ravdess.py:505-513).
 
-Decoding (cv2.VideoCapture / librosa), face detection / crop and the augmentations stay on the host
-(DESIGN.md section 7).  Kernels: ``csrc/clips.hip``; CPU restatement: ``oracle/clips_ref.py``.
+Decoding (cv2.VideoCapture / librosa), face detection / crop and the audio augmentation stay on the host
+(DESIGN.md section 4c).  Kernels: ``csrc/clips.hip``; CPU restatement: ``oracle/clips_ref.py``.
 """
 from __future__ import annotations
 
@@ -41,6 +44,73 @@ def video_clip_batch(frames: torch.Tensor, size: int = 112) -> torch.Tensor:
     """``[B, T, H, W, 3]`` uint8 -> ``[B, T, 3, size, size]`` fp32 (the FusionModel video input)."""
     B, T = frames.shape[:2]
     return preprocess_frames(frames.reshape(B * T, *frames.shape[2:]), size).view(B, T, 3, size, size)
+
+
+NORMAL_TABLE_BITS = 16
+
+
+def normal_table() -> torch.Tensor:
+    """fp32 [65536]: the standard normal inverse CDF at (i + 0.5) / 65536 (float64, then rounded) -- the
+    augmentation noise draws z = table[hash >> 16] (a 16-bit-resolution Gaussian, |z| <= 4.17)."""
+    n = 1 << NORMAL_TABLE_BITS
+    u = (torch.arange(n, dtype=torch.float64) + 0.5) / n
+    return torch.special.ndtri(u).to(torch.float32)
+
+
+_ZTABLES = {}
+
+
+def _ztable(dev) -> torch.Tensor:
+    t = _ZTABLES.get(dev)
+    if t is None:
+        t = _ZTABLES[dev] = normal_table().to(dev)
+    return t
+
+
+def draw_video_augment(rng) -> tuple:
+    """One clip's draws of ravdess.py:368-372 from a numpy Generator, in the reference's order: brightness factor
+    U(0.2, 0.6), noise scale U(0, 5e-4), blur ksize from {3, 5, 7} -- plus the 63-bit seed of the clip's noise."""
+    factor = float(rng.uniform(0.2, 0.6))
+    noise_scale = float(rng.uniform(0.0, 0.0005))
+    ksize = int(rng.choice([3, 5, 7]))
+    if ksize % 2 == 0:
+        ksize += 1
+    return factor, noise_scale, ksize, int(rng.integers(0, 2 ** 63 - 1))
+
+
+def resize_frames_u8(frames: torch.Tensor, size: int = 112, out: torch.Tensor = None) -> torch.Tensor:
+    """``[N, H, W, 3]`` uint8 on the GPU -> ``[N, size, size, 3]`` uint8 (cv2.resize INTER_LINEAR, ravdess.py:352)."""
+    if not frames.is_cuda or frames.dtype != torch.uint8 or frames.dim() != 4 or frames.shape[-1] != 3:
+        raise ValueError("frames must be uint8 [N, H, W, 3] (RGB) on the GPU")
+    frames = frames.contiguous()
+    N, H, W, _ = frames.shape
+    if out is None:
+        out = torch.empty(N, size, size, 3, device=frames.device, dtype=torch.uint8)
+    K.LIB("mer_frames_resize_u8", N, H, W, frames.data_ptr(), H * W * 3, size, out.data_ptr(), K.stream_ptr())
+    return out
+
+
+def augment_clips(frames_u8: torch.Tensor, params: Sequence[tuple]) -> torch.Tensor:
+    """Resized clips ``[B, T, S, S, 3]`` uint8 on the GPU + one ``draw_video_augment`` tuple per clip ->
+    ``[B, T, 3, S, S]`` fp32: the augmentation of ravdess.py:366-384 then the ImageNet normalisation (:386-389)."""
+    if not frames_u8.is_cuda:
+        raise RuntimeError("augment_clips runs on the MI355X kernels; move the frames to the GPU")
+    if frames_u8.dtype != torch.uint8 or frames_u8.dim() != 5 or frames_u8.shape[-1] != 3 \
+            or frames_u8.shape[2] != frames_u8.shape[3]:
+        raise ValueError("frames must be uint8 [B, T, S, S, 3]")
+    B, T, S = frames_u8.shape[:3]
+    if len(params) != B:
+        raise ValueError(f"{len(params)} augmentation draws for {B} clips")
+    for _, _, k, _ in params:
+        if k not in (1, 3, 5, 7):
+            raise ValueError(f"blur ksize {k}: the device blur implements cv2's sigma-0 kernels of size <= 7")
+    dev = frames_u8.device
+    fp = _h2d(torch.tensor([[f, n, float(k)] for f, n, k, _ in params], dtype=torch.float32), dev)
+    seeds = _h2d(torch.tensor([sd for _, _, _, sd in params], dtype=torch.int64), dev)
+    out = torch.empty(B, T, 3, S, S, device=dev, dtype=torch.float32)
+    K.LIB("mer_frames_augment_normalize", B * T, S, T, frames_u8.contiguous().data_ptr(), fp.data_ptr(),
+          seeds.data_ptr(), _ztable(dev).data_ptr(), *IMAGENET_MEAN, *IMAGENET_STD, out.data_ptr(), K.stream_ptr())
+    return out
 
 
 def _h2d(t: torch.Tensor, dev) -> torch.Tensor:

@@ -264,12 +264,18 @@ class ClipLoader:
 
     def _assemble(self, decoded):
         # frames of one batch may differ in size (per-clip crops): resize each clip's frames on the device
-        vids = [clips.preprocess_frames(torch.from_numpy(f).to(self.device), self.size) for f, _, _, _ in decoded]
-        video = torch.stack(vids).contiguous()
-        audio = clips.pad_crop_waveforms([torch.from_numpy(w) for _, w, _, _ in decoded], self.sr, self.dur,
+        if self.augment:  # resized uint8 clips, then ONE augmentation + normalisation launch with per-clip draws
+            u8 = torch.empty(len(decoded), self.T, self.size, self.size, 3, device=self.device, dtype=torch.uint8)
+            for i, (f, _, _, _, _) in enumerate(decoded):
+                clips.resize_frames_u8(torch.from_numpy(f).to(self.device), self.size, out=u8[i])
+            video = clips.augment_clips(u8, [va for _, _, _, _, va in decoded])
+        else:
+            vids = [clips.preprocess_frames(torch.from_numpy(f).to(self.device), self.size) for f, _, _, _, _ in decoded]
+            video = torch.stack(vids).contiguous()
+        audio = clips.pad_crop_waveforms([torch.from_numpy(w) for _, w, _, _, _ in decoded], self.sr, self.dur,
                                          device=self.device)
-        labels = torch.tensor([lab for _, _, lab, _ in decoded], dtype=torch.long).to(self.device)
-        return video, audio, labels, _collate_meta([m for _, _, _, m in decoded])
+        labels = torch.tensor([lab for _, _, lab, _, _ in decoded], dtype=torch.long).to(self.device)
+        return video, audio, labels, _collate_meta([m for _, _, _, m, _ in decoded])
 
     def __iter__(self):
         order = shard_indices(len(self.all_items), self.rank, self.world, self.shuffle, self.seed, self.epoch)
@@ -315,7 +321,9 @@ class ClipLoader:
             meta.setdefault("index", int(gi))
             frames = select_frames(_frames(src), self.T, bbox)
             rng = np.random.default_rng([self.seed, epoch, int(gi)]) if self.augment else None
+            # the reference loads (and augments) the video before the audio (ravdess.py:639-645): same draw order
+            vaug = clips.draw_video_augment(rng) if self.augment else None
             wav = load_audio_wav(wav_path, self.sr, self.dur, augment=self.augment, bar_noise=self.bar_noise,
                                  rng=rng)[0].numpy()
-            return frames, wav, int(label), meta
+            return frames, wav, int(label), meta, vaug
         return fn

@@ -42,3 +42,77 @@ def test_pad_crop_matches_reference_semantics():
         ref = torch.from_numpy(w)[None]
         ref = F.pad(ref, (0, 48000 - n)) if n < 48000 else ref[:, :48000]
         assert np.array_equal(clips_ref.pad_crop_wav(w, 48000), ref.numpy())
+
+
+# ---- train-split video augmentation (ravdess.py:366-384), oracle side ----
+
+def test_uint8_round_trip_is_identity():
+    """(u8 / 255 in fp32 * 255).astype(uint8) == u8 for every value: the device blur reads the frames directly."""
+    u = np.arange(256, dtype=np.uint8)
+    assert np.array_equal((u.astype(np.float32) / np.float32(255.0) * np.float32(255.0)).astype(np.uint8), u)
+
+
+def test_blur_tables_are_opencv_sigma0_kernels():
+    """getGaussianKernel(k, sigma<=0) for k <= 7 is OpenCV's fixed small_gaussian_tab, not the sigma formula."""
+    tab = {3: [0.25, 0.5, 0.25], 5: [0.0625, 0.25, 0.375, 0.25, 0.0625],
+           7: [0.03125, 0.109375, 0.21875, 0.28125, 0.21875, 0.109375, 0.03125]}
+    for k, ref in tab.items():
+        w, m = clips_ref._BLUR[k]
+        assert np.array_equal(np.array(w, np.float64) / (1 << m), np.array(ref))
+
+
+@pytest.mark.parametrize("k", [1, 3, 5, 7])
+@pytest.mark.parametrize("shape", [(112, 112), (9, 13), (2, 5)])
+def test_blur_u8_equals_exact_separable_convolution(k, shape):
+    """blur_u8 vs an independent float64 2-D convolution (scipy 'mirror' = BORDER_REFLECT_101) rounded half up:
+    the integer sums are exact in float64, so the two must agree bit for bit."""
+    from scipy import ndimage
+
+    rng = np.random.default_rng(k * 100 + shape[0])
+    img = rng.integers(0, 256, size=(*shape, 3), dtype=np.uint8)
+    w, m = clips_ref._BLUR[k]
+    w1 = np.array(w, np.float64) / (1 << m)
+    ker = np.outer(w1, w1)
+    ref = np.stack([np.floor(ndimage.convolve(img[..., c].astype(np.float64), ker, mode="mirror") + 0.5)
+                    for c in range(3)], -1)
+    assert np.array_equal(clips_ref.blur_u8(img, k).astype(np.float64), ref)
+
+
+def test_oracle_hash_matches_helpers_restatement():
+    from tests.helpers import hash_u32
+
+    idx = np.arange(0, 1 << 20, 997, dtype=np.uint64)
+    for seed in (0, 12345, (1 << 63) - 1, 0xDEADBEEFCAFEF00D):
+        assert np.array_equal(clips_ref._mer_hash(seed, idx).astype(np.uint32), hash_u32(seed, idx))
+
+
+def test_normal_table_and_draws():
+    from multimodalemotionrecognition_amd import clips
+
+    z = clips.normal_table().numpy()
+    assert z.shape == (65536,) and np.all(np.diff(z) > 0) and np.array_equal(z, -z[::-1])
+    assert abs(z.mean()) < 1e-6 and abs(z.std() - 1) < 2e-3
+    rng = np.random.default_rng(0)
+    d = [clips.draw_video_augment(rng) for _ in range(3000)]
+    f, n, k, s = (np.array(x) for x in zip(*d))
+    assert f.min() >= 0.2 and f.max() < 0.6 and n.min() >= 0 and n.max() < 5e-4
+    assert set(k.tolist()) == {3, 5, 7} and all(abs((k == v).mean() - 1 / 3) < 0.04 for v in (3, 5, 7))
+    assert len(set(s.tolist())) == 3000
+
+
+def test_augment_clip_statistics():
+    """Darkening scales the mean by the factor; the noise is N(0, noise_scale); output clipped to [0, 1]."""
+    from multimodalemotionrecognition_amd import clips
+
+    zt = clips.normal_table().numpy()
+    rng = np.random.default_rng(1)
+    fr = rng.integers(0, 256, size=(2, 112, 112, 3), dtype=np.uint8)
+    flat = np.full((2, 112, 112, 3), 128, np.uint8)  # blur of a constant image is the constant
+    out = clips_ref.augment_clip(flat, 0.4, 0.0, 5, 7, zt)
+    raw = out.transpose(0, 2, 3, 1) * clips_ref.STD + clips_ref.MEAN
+    assert np.allclose(raw, np.float32(128 / 255.0) * np.float32(0.4), atol=1e-6)
+    noisy = clips_ref.augment_clip(flat, 0.4, 0.01, 5, 7, zt).transpose(0, 2, 3, 1) * clips_ref.STD + clips_ref.MEAN
+    dn = (noisy - raw).ravel()
+    assert abs(dn.mean()) < 2e-4 and abs(dn.std() - 0.01) < 3e-4
+    o = clips_ref.augment_clip(fr, 0.6, 4e-4, 7, 3, zt).transpose(0, 2, 3, 1) * clips_ref.STD + clips_ref.MEAN
+    assert o.min() >= -1e-6 and o.max() <= 0.6 + 5e-3
