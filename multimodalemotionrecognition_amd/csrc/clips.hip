@@ -103,6 +103,7 @@ __global__ __launch_bounds__(256) void frames_augment_normalize_kernel(int S, in
                                                                        const float* __restrict__ ztable, float m0,
                                                                        float m1, float m2, float sd0, float sd1, float sd2,
                                                                        float* __restrict__ dst) {
+#pragma clang fp contract(off)  // the noise term is fl(fl(x * factor) + fl(sigma * z)), never an fma (numpy order)
   const int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y, n = blockIdx.z;
   if (x >= S) return;
   const int clip = n / T;
@@ -132,8 +133,8 @@ __global__ __launch_bounds__(256) void frames_augment_normalize_kernel(int S, in
   const long e0 = (((long)(n - clip * T) * S + y) * S + x) * 3;  // element index inside the clip, HWC order
   for (int c = 0; c < 3; ++c) {
     const int b = m ? (acc[c] + (1 << (2 * m - 1))) >> (2 * m) : acc[c];
-    float v = __fmul_rn((float)b / 255.f, factor);
-    if (sigma > 0.f) v = __fadd_rn(v, __fmul_rn(sigma, ztable[mer_hash(seed, (uint64_t)(e0 + c)) >> 16]));
+    float v = (float)b / 255.f * factor;
+    if (sigma > 0.f) v = v + sigma * ztable[mer_hash(seed, (uint64_t)(e0 + c)) >> 16];
     v = fminf(fmaxf(v, 0.f), 1.f);
     dst[o + c * plane] = (v - mean[c]) / sd[c];
   }
