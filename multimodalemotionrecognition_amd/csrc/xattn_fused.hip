@@ -216,8 +216,11 @@ MER_API int mer_xh_audio_fwd(int M, int S, const void* aseq, int aseq_dtype, lon
                              float* a, float* q2, float* kv1, int Mv, int vdim, const float* vfeat, const void* Wv_hi,
                              const void* Wv_lo, const float* bv, const void* Wq1_hi, const void* Wq1_lo,
                              const float* bq1, float* v, float* q1, void* stream) {
-  if (M <= 0 || Mv < 0) return (int)hipErrorInvalidValue;
-  if (S % 64 || ldas % 8 || ((uintptr_t)aseq & 15) || (Mv > 0 && (vdim <= 0 || vdim % 32))) return (int)hipErrorInvalidValue;
+  // M = 0: the video rows alone; Mv = 0: the audio chain alone (the head's audio-first schedule launches them
+  // separately, the audio chain on a side stream beside the frame trunk)
+  if (M < 0 || Mv < 0 || M + Mv == 0) return (int)hipErrorInvalidValue;
+  if ((M > 0 && (S % 64 || ldas % 8 || ((uintptr_t)aseq & 15))) || (Mv > 0 && (vdim <= 0 || vdim % 32)))
+    return (int)hipErrorInvalidValue;
   const SplitW ws{(const bf16_t*)Ws_hi, (const bf16_t*)Ws_lo}, wa{(const bf16_t*)Wa_hi, (const bf16_t*)Wa_lo},
       wc{(const bf16_t*)Wc_hi, (const bf16_t*)Wc_lo};
   const XhVideo vid{Mv, vdim, vfeat, SplitW{(const bf16_t*)Wv_hi, (const bf16_t*)Wv_lo}, bv,

@@ -657,7 +657,8 @@ MER_API int mer_xh_audio_bwd(int M, const float* dqkv, const void* WcT_hi, const
                              const void* WaT_lo, float* da, float* da_s, int Mv, int vdim, const float* dq1,
                              const void* WqT1_hi, const void* WqT1_lo, const void* WvT_hi, const void* WvT_lo, float* dv,
                              float* dvfeat, void* stream) {
-  if (M <= 0 || Mv < 0 || (Mv > 0 && (!dq1 || !dv || (dvfeat && (vdim <= 0 || vdim % 32)))))
+  // M = 0: the video rows alone (the critical path into the trunk backward); Mv = 0: the audio chain alone
+  if (M < 0 || Mv < 0 || M + Mv == 0 || (Mv > 0 && (!dq1 || !dv || (dvfeat && (vdim <= 0 || vdim % 32)))))
     return (int)hipErrorInvalidValue;
   const XhVideoBwd vid{Mv, vdim, dq1, SplitW{(const bf16_t*)WqT1_hi, (const bf16_t*)WqT1_lo},
                        SplitW{(const bf16_t*)WvT_hi, (const bf16_t*)WvT_lo}, dv, dvfeat};
