@@ -223,6 +223,76 @@ def time_dominant(model, dev, probe, launches: int):
     torch.cuda.synchronize()
 
 
+CORE_KERNELS = ("xh_v2a_fwd", "xh_a2v_fwd", "xh_v2a_bwd", "xh_a2v_bwd")
+
+
+def core_attention(B=BATCH, T=FRAMES, Ta=149, d=128, H=4):
+    """(FLOP, bytes) of the xattn attention cores (fusion.py:394,398: v2a and a2v nn.MultiheadAttention) per train
+    step: forward QK^T + PV per direction, backward dP, dV, dQ, dK (2x); bytes = Q, K, V read and P, O written in
+    the forward, Q, K, V, P, dO read and dQ, dK, dV written in the backward, fp32."""
+    flop = 3 * 2 * (2 * 2.0 * B * T * Ta * d)  # two directions x (fwd 2 products + bwd 4)
+    byt = 0
+    for lq, lk in ((T, Ta), (Ta, T)):
+        q, kv, p, o = B * lq * d * 4, B * lk * 2 * d * 4, B * H * lq * lk * 4, B * lq * d * 4
+        byt += (q + kv + p + o) + (q + kv + p + o) + (q + kv)
+    return flop, byt
+
+
+def roof_core(core_ms, peak_split):
+    """The ``roofline_head.core`` entry: the attention cores' FLOPs over the summed standalone durations of the
+    four kernels that run them, against min(split-bf16 peak, intensity x HBM bandwidth)."""
+    if not core_ms or any(v is None for v in core_ms.values()):
+        return None
+    flop, byt = core_attention()
+    ms = sum(core_ms.values())
+    ai = flop / byt
+    attain = min(peak_split, ai * PEAK_HBM_GBS / 1e3)
+    ach = flop / (ms * 1e-3) / 1e12
+    return {"bound": "mfma" if peak_split < ai * PEAK_HBM_GBS / 1e3 else "hbm", "achieved": round(ach, 3),
+            "peak": round(attain, 2), "unit": "TFLOP/s", "frac": round(ach / attain, 4), "algorithmic_flop": flop,
+            "algorithmic_bytes": byt, "intensity_flop_per_byte": round(ai, 2), "kernel_ms": {
+                k: round(v, 4) for k, v in core_ms.items()}, "ms": round(ms, 4),
+            "measured": "HIP events around 20 eager train-mode head fwd+bwd passes per kernel (each kernel also "
+                        "runs its out-projection, residual + LayerNorm; the whole duration is charged to the core)"}
+
+
+def time_head_core(model, dev, reps: int):
+    """HIP events around every launch of the fused head's four attention kernels (F2 / F3 forward, G2 / G3 backward:
+    each fuses its attention with the out-projection, drop-path + residual + LayerNorm and, F2 / G2, the next
+    projection) in eager train-mode head forward + backward passes on the production shapes, nothing else in
+    flight.  Returns {kernel: avg ms}."""
+    from multimodalemotionrecognition_amd import xattn_head as XH
+
+    names, params = model.head_params()
+    p = dict(zip(names, params))
+    cfg = model.head_config()
+    g = torch.Generator(device=dev).manual_seed(7)
+    v = torch.randn(BATCH, FRAMES, 512, device=dev, generator=g)
+    a = torch.randn(BATCH, 149, 768, device=dev, generator=g).to(torch.bfloat16)
+    rng = torch.full((1,), 4242, dtype=torch.int64, device=dev)
+    used = set(XH.used_param_names(cfg))
+    grads = {n: torch.zeros_like(t) for n, t in p.items() if n in used}
+    dl = torch.randn(BATCH, CLASSES, device=dev, generator=g)
+    probe = K.MultiProbe(CORE_KERNELS)
+
+    def one():
+        _, ctx = XH.head_forward(p, cfg, v, a, True, rng)
+        XH.head_backward(p, ctx, dl, grads, need_dv_feat=True)
+
+    with torch.no_grad():
+        for _ in range(3):
+            one()
+        torch.cuda.synchronize()
+        probe.active = True
+        K.PROBE = probe
+        for _ in range(reps):
+            one()
+        K.PROBE = None
+        probe.active = False
+    torch.cuda.synchronize()
+    return {n: probe.avg_ms(n) for n in CORE_KERNELS}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -422,6 +492,8 @@ def _bench(args, world, rank, local):
                 "avg_ms": round(kms, 4), "launches": len(probe.pairs),
                 "measured": f"HIP events around {len(probe.pairs)} standalone launches after the timed region "
                             "(production shape, weight pack and stream)"}
+    core_ms = time_head_core(model, dev, 20) if (args.probe_launches > 0 and args.wavlm_unfreeze == 0
+                                                 and not args.emotion_prior) else None
     roof_head = None
     hms = hprobe.avg_ms()
     if hms and args.wavlm_unfreeze == 0 and not args.emotion_prior:
@@ -449,6 +521,7 @@ def _bench(args, world, rank, local):
                      "ms_per_step": round(head_ms, 4), "critical_path_ms": round(fwd_ms + bwd_ms, 4),
                      "hbm_gbs_achieved": round(hbytes / (head_ms * 1e-3) / 1e9, 1),
                      "peak_basis": "min(split-bf16 fp32-class MFMA peak = 2.5 PF / 3, intensity x 8 TB/s)",
+                     "core": roof_core(core_ms, peak_split),
                      "measured": f"HIP events around the head's forward / backward graph replays (main stream; "
                                  f"audio phase and deferred backward on the head stream) in {len(hprobe.fwd)} "
                                  "probe steps"}

@@ -38,6 +38,29 @@ class KernelProbe:
             return None
         return sum(a.elapsed_time(b) for a, b in self.pairs) / len(self.pairs)
 
+    def record(self, name, pair):
+        self.pairs.append(pair)
+
+
+class MultiProbe:
+    """Brackets every launch of the named kernels (any shape) with HIP events: per-kernel average device time
+    (bench.py's head-core roofline entry)."""
+
+    def __init__(self, names):
+        self.names = tuple(names)
+        self.by_name = {n: [] for n in self.names}
+        self.active = False
+
+    def matches(self, name, key):
+        return self.active and name in self.by_name
+
+    def record(self, name, pair):
+        self.by_name[name].append(pair)
+
+    def avg_ms(self, name):
+        p = self.by_name.get(name) or []
+        return sum(a.elapsed_time(b) for a, b in p) / len(p) if p else None
+
 
 PROBE = None
 
@@ -49,7 +72,7 @@ def _launch(name, key, fn, *args):
         a.record(s)
         LIB(fn, *args)
         b.record(s)
-        PROBE.pairs.append((a, b))
+        PROBE.record(name, (a, b))
     else:
         LIB(fn, *args)
 

@@ -124,11 +124,22 @@ def test_audio_prefetch_matches_inline(early, monkeypatch):
         v2, a2, y2 = video[4:8], audio[4:8].clone(), labels[4:8]
         seen = []
         orig = mb.xattn_from_features
-        mb.xattn_from_features = lambda v, a, **kw: (seen.append(a.detach().clone()), orig(v, a, **kw))[1]
+
+        def spy(v, a, runner=False):
+            # the audio-first head (fusion._HeadGraphs) took its own copy of the features on the head stream --
+            # the borrowed encoder output may already be rewritten by the next batch's prefetch: read that copy
+            # once the step is done; otherwise the features passed in are the head's input
+            took = runner not in (None, False) and runner.audio_issued
+            seen.append(runner.fwd_a.static_in[0] if took else a.detach().clone())
+            return orig(v, a, runner=runner)
+
+        mb.xattn_from_features = spy
         seq = [(v1, a1, y1), (v2, a2, y2), (v1, a1, y1)]
         for i, (v, a, y) in enumerate(seq):
             nxt = seq[i + 1][1] if i + 1 < len(seq) else None
             sb(v, a, y, next_audio=nxt)
+            torch.cuda.synchronize()
+            seen[-1] = seen[-1].clone()  # (a head-stream static copy is rewritten by the next step)
         assert mb._prefetched is None  # consumed
         for (v, a, y), feats in zip(seq, seen):
             with torch.no_grad():
