@@ -538,7 +538,8 @@ int mer_xh_audio_fwd(int M, int S, const void* aseq, int aseq_dtype, long ldas, 
                      const float* bv, const void* Wq1_hi, const void* Wq1_lo, const float* bq1, float* v, float* q1,
                      void* stream);
 
-/* F2 (one workgroup per sample, T <= 16, Ta <= 160): v2a attention of q1 over kv1, o1 Wo1^T + bo1,
+/* F2 (two launches: the attention per (sample, head), then the rest per sample; T <= 16, Ta <= 256): v2a attention
+ * of q1 over kv1, o1 Wo1^T + bo1,
  * v1 = LayerNorm(v + keep_b * v2) (saving the pre-LN sum, mean, rstd), kv2 = v1 Wkv2^T + bkv2,
  * emb[b][0:128] = mean_t v1.  P1 [B][4][T][Ta] receives the pre-dropout probabilities.  bias (nullable): the
  * emotion-prior attention bias [B][T][Ta] added to every head's scaled scores (fusion.py:390-394 attn_mask). */
@@ -589,16 +590,17 @@ int mer_xh_a2v_bwd(int B, int T, int Ta, const float* demb, const float* s_a, co
                    unsigned long long site_attn, unsigned long long site_path, float scale, float* da, float* da2,
                    float* dqkv, float* dkv2_part, float* ln_part, float* dbias, void* stream);
 
-/* G2 (one workgroup per sample, T <= 16, Ta <= 160): dkv2 = fold(dkv2_part) [B*T][256], dv1 = demb_v / T +
- * dkv2 Wkv2, LayerNorm backward (dv2, ln_part [B][256]), do1 = dv2 Wo1, attention backward -> dq1 [B*T][128],
- * dK1 dV1 into dqkv[:, 128:384], dv [B*T][128] = the LayerNorm-residual part of dv (G1 adds dq1 Wq1).
- * dbias (nullable): the prior bias gradient [B][T][Ta] = sum over heads of dS (head order). */
+/* G2 (two launches: one workgroup per sample, then the attention backward per (sample, head); T <= 16,
+ * Ta <= 160): dkv2 = fold(dkv2_part) [B*T][256], dv1 = demb_v / T + dkv2 Wkv2, LayerNorm backward (dv2, ln_part
+ * [B][256]), do1 = dv2 Wo1 ([B*T][128] scratch), attention backward -> dq1 [B*T][128], dK1 dV1 into
+ * dqkv[:, 128:384], dv [B*T][128] = the LayerNorm-residual part of dv (G1 adds dq1 Wq1).  dbias (nullable): the
+ * prior bias gradient [B][T][Ta] = sum over heads of dS (head order), through the dS_heads scratch [B][4][T][Ta]. */
 int mer_xh_v2a_bwd(int B, int T, int Ta, const float* dkv2_part, const void* WkvT2_hi, const void* WkvT2_lo,
                    const float* demb, const float* s_v, const float* mean_v, const float* rstd_v, const float* gamma,
                    const void* WoT1_hi, const void* WoT1_lo, const float* P1, const float* kv1, const float* q1,
                    float attn_p, float path_p, const unsigned long long* seed, unsigned long long site_attn,
                    unsigned long long site_path, float scale, float* dkv2, float* dv2, float* dq1, float* dv,
-                   float* dqkv, float* ln_part, float* dbias, void* stream);
+                   float* dqkv, float* ln_part, float* do1, float* dS_heads, float* dbias, void* stream);
 
 /* G1 (32 rows per workgroup): da += dqkv [Wq2 ; Wkv1] (in place), da_s = da Wa; the trailing ceil(Mv/32)
  * workgroups: dv += dq1 Wq1 (in place), dvfeat = dv Wv [Mv][vdim] (NULL: not wanted). */

@@ -390,46 +390,190 @@ __device__ __forceinline__ void add_ln_rows(int nrows, const float* xL, const fl
   }
 }
 
-// ---------------------------------------------------------------------------------------------
-// F2: v2a block, one workgroup per sample (T <= 16 query rows).
-// ---------------------------------------------------------------------------------------------
-constexpr int F2_KT = 10;                 // Ta <= 160 keys
-constexpr int F2_PLD = 16 * F2_KT + 20;   // P' tile stride (>= 32-padded keys)
+constexpr int F2_KT = 10;  // 16-key tiles of the v2a attention (Ta <= 160: F4 folds up to this many F3 tiles)
 
-__global__ __launch_bounds__(256) void xh_v2a_fwd_kernel(
-    int T, int Ta, const float* __restrict__ v, const float* __restrict__ q1, const float* __restrict__ kv1,
-    SplitW Wo1, const float* __restrict__ bo1, const float* __restrict__ gamma, const float* __restrict__ beta,
-    SplitW Wkv2, const float* __restrict__ bkv2, XhDrop dr, float scale, float* __restrict__ P1,
-    float* __restrict__ o1, float* __restrict__ s_v, float* __restrict__ mean_v, float* __restrict__ rstd_v,
-    float* __restrict__ v1, float* __restrict__ kv2, float* __restrict__ emb, long ld_emb,
-    const float* __restrict__ bias) {
-  extern __shared__ __attribute__((aligned(16))) float f2smem[];  // F2_LDS_BYTES
-  float* vL = f2smem;
-  float* qL = vL + 16 * LDA;
-  float* oL = qL + 16 * LDA;
-  float* PL = oL + 16 * LDA;  // [XH][16][F2_PLD]
-  float* tL = PL;             // the out-projection tile reuses P' once the attention is done
+// ---------------------------------------------------------------------------------------------
+// F2: the v2a block as two launches.  F2a = the v2a attention, one workgroup per (sample, head) -- 128 workgroups
+// at B = 32 (the one-workgroup-per-sample version, a wave per head, ran 32), each wave walking a quarter of the
+// keys --; F2b = its out-projection, drop-path + residual + LayerNorm, v-pool and [k2 v2] projection, one
+// workgroup per sample.
+//
+// F2a: wave w owns the 32-key chunks c = w, w + 4, ... of the sample's Ta keys.  Scores S = Q_h K^T (+ the
+// emotion-prior bias), the row max and then the row sum of exp(S - max) meet across the 4 waves in LDS (wave
+// order), P = exp / sum is saved (pre-dropout, as the unfused schedule saves it), and each wave's P' V_h partial
+// is summed in wave order into o1's 32 columns of head h.  Loads are issued up front (one memory latency).
+// ---------------------------------------------------------------------------------------------
+constexpr int F2A_MAXC = 2;               // 32-key chunks per wave: Ta <= 4 * 2 * 32 = 256
+constexpr int F2A_PLD = 36;               // P' chunk stride
+
+__global__ __launch_bounds__(256) void xh_v2a_attn_kernel(int T, int Ta, const float* __restrict__ q1,
+                                                          const float* __restrict__ kv1, XhDrop dr, float scale,
+                                                          float* __restrict__ P1, float* __restrict__ o1,
+                                                          const float* __restrict__ bias) {
+  __shared__ float red[2][4][16];                                   // per-wave row max / row sum
+  __shared__ __attribute__((aligned(16))) float PL[4][16 * F2A_PLD];  // per-wave P' chunk (PV A operand)
+  __shared__ float oP[4][16][33];                                   // per-wave P' V partials
+  const int b = blockIdx.x >> 2, h = blockIdx.x & 3;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, fr = lane & 15, fq = lane >> 4, fk = fq * 8;
+  const long ldkv = 2 * XD;
+  const float* Kr = kv1 + (long)b * Ta * ldkv + h * XDH;       // key j: Kr[j * ldkv + d]
+  const float* Vr = Kr + XD;                                   // value j: Vr[j * ldkv + d]
+  const int nch = (Ta + 31) / 32;
+  const unsigned long long dseed = mer_site_seed(dr.seed, dr.site_attn);
+  // every global load first: K fragments and V gathers of this wave's chunks (clamped rows), the prior bias
+  f32x4 kraw[F2A_MAXC][2][2];
+  float vraw[F2A_MAXC][2][8];
+  float bv[F2A_MAXC][2][4];
+#pragma unroll
+  for (int ci = 0; ci < F2A_MAXC; ++ci) {
+    const int c = w + 4 * ci;
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt) {
+      const int j = 32 * c + 16 * tt + fr, jc = j < Ta ? j : Ta - 1;
+      kraw[ci][tt][0] = *reinterpret_cast<const f32x4*>(Kr + (long)jc * ldkv + fk);
+      kraw[ci][tt][1] = *reinterpret_cast<const f32x4*>(Kr + (long)jc * ldkv + fk + 4);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = 4 * fq + r;
+        const long bi = ((long)b * T + (i < T ? i : T - 1)) * Ta + jc;
+        bv[ci][tt][r] = bias ? bias[bi] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int kk = 32 * c + fk + e;
+        vraw[ci][jt][e] = Vr[(long)(kk < Ta ? kk : Ta - 1) * ldkv + 16 * jt + fr];
+      }
+  }
+  bf16x8 qh, ql;
+  frag_row(q1 + ((long)b * T + (fr < T ? fr : T - 1)) * XD + h * XDH + fk, fr < T, qh, ql);
+  f32x4 s[F2A_MAXC][2];
+  float mx[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+#pragma unroll
+  for (int ci = 0; ci < F2A_MAXC; ++ci)
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt) {
+      const int j = 32 * (w + 4 * ci) + 16 * tt + fr;
+      float x[8] = {kraw[ci][tt][0][0], kraw[ci][tt][0][1], kraw[ci][tt][0][2], kraw[ci][tt][0][3],
+                    kraw[ci][tt][1][0], kraw[ci][tt][1][1], kraw[ci][tt][1][2], kraw[ci][tt][1][3]};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) x[e] = j < Ta ? x[e] : 0.f;
+      bf16x8 bh, bl;
+      split8(x, bh, bl);
+      s[ci][tt] = mma3(qh, ql, bh, bl, f32x4{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        s[ci][tt][r] = j < Ta ? s[ci][tt][r] * scale + bv[ci][tt][r] : -INFINITY;
+        mx[r] = fmaxf(mx[r], s[ci][tt][r]);
+      }
+    }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) mx[r] = fmaxf(mx[r], __shfl_xor(mx[r], o, 64));
+    if (fr == 0) red[0][w][4 * fq + r] = mx[r];
+  }
+  __syncthreads();
+  float sum[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int i = 4 * fq + r;
+    mx[r] = fmaxf(fmaxf(red[0][0][i], red[0][1][i]), fmaxf(red[0][2][i], red[0][3][i]));
+    sum[r] = 0.f;
+  }
+#pragma unroll
+  for (int ci = 0; ci < F2A_MAXC; ++ci)
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int j = 32 * (w + 4 * ci) + 16 * tt + fr;
+        const float e = j < Ta ? __expf(s[ci][tt][r] - mx[r]) : 0.f;
+        s[ci][tt][r] = e;
+        sum[r] += e;
+      }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) sum[r] += __shfl_xor(sum[r], o, 64);
+    if (fr == 0) red[1][w][4 * fq + r] = sum[r];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int i = 4 * fq + r;
+    sum[r] = (red[1][0][i] + red[1][1][i]) + (red[1][2][i] + red[1][3][i]);
+  }
+  // P (saved, pre-dropout), P' = dropout(P) through LDS into O_w = P'_w V_w
+  f32x4 o[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+  float* pl = PL[w];
+#pragma unroll
+  for (int ci = 0; ci < F2A_MAXC; ++ci) {
+    const int c = w + 4 * ci;
+    if (c >= nch) break;  // (wave-uniform)
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = 4 * fq + r, j = 32 * c + 16 * tt + fr;
+        float pd = 0.f;
+        if (i < T && j < Ta) {
+          const float pr = s[ci][tt][r] / sum[r];
+          const long pi = (((long)b * XH + h) * T + i) * Ta + j;
+          P1[pi] = pr;
+          pd = pr * dropout_scale(dseed, pi, dr.attn);
+        }
+        pl[i * F2A_PLD + 16 * tt + fr] = pd;
+      }
+    wave_sync_lds();
+    bf16x8 ah, al;
+    frag_row(pl + fr * F2A_PLD + fk, true, ah, al);
+#pragma unroll
+    for (int jt = 0; jt < 2; ++jt) {
+      float x[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) x[e] = 32 * c + fk + e < Ta ? vraw[ci][jt][e] : 0.f;
+      bf16x8 bh, bl;
+      split8(x, bh, bl);
+      o[jt] = mma3(ah, al, bh, bl, o[jt]);
+    }
+    wave_sync_lds();  // the next chunk overwrites pl
+  }
+#pragma unroll
+  for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) oP[w][4 * fq + r][16 * jt + fr] = o[jt][r];
+  __syncthreads();
+  for (int e = threadIdx.x; e < T * XDH; e += 256) {
+    const int i = e / XDH, d = e - i * XDH;
+    o1[((long)b * T + i) * XD + h * XDH + d] = (oP[0][i][d] + oP[1][i][d]) + (oP[2][i][d] + oP[3][i][d]);
+  }
+}
+
+// F2b: F2's second half on o1 (one workgroup per sample): v2 = o1 Wo1^T + bo1, v1 = LN(v + keep_b v2), v-pool,
+// [k2 v2] = v1 Wkv2^T + bkv2
+__global__ __launch_bounds__(256) void xh_v2a_post_kernel(
+    int T, const float* __restrict__ v, const float* __restrict__ o1, SplitW Wo1, const float* __restrict__ bo1,
+    const float* __restrict__ gamma, const float* __restrict__ beta, SplitW Wkv2, const float* __restrict__ bkv2,
+    XhDrop dr, float* __restrict__ s_v, float* __restrict__ mean_v, float* __restrict__ rstd_v, float* __restrict__ v1,
+    float* __restrict__ kv2, float* __restrict__ emb, long ld_emb) {
+  __shared__ __attribute__((aligned(16))) float vL[16 * LDA];
+  __shared__ __attribute__((aligned(16))) float oL[16 * LDA];
+  __shared__ __attribute__((aligned(16))) float tL[16 * LDA];
   const int b = blockIdx.x, w = threadIdx.x >> 6;
   const long row0 = (long)b * T;
-  const unsigned long long seed_attn = mer_site_seed(dr.seed, dr.site_attn);
   const unsigned long long seed_path = mer_site_seed(dr.seed, dr.site_path);
 #pragma unroll
-  for (int e = threadIdx.x; e < 16 * XD; e += 256) {  // v, q1 (F1's video blocks)
+  for (int e = threadIdx.x; e < 16 * XD; e += 256) {
     const int r = e / XD, c = e - r * XD;
     const long rc = row0 + (r < T ? r : T - 1);
-    const float xv = v[rc * XD + c], xq = q1[rc * XD + c];
+    const float xv = v[rc * XD + c], xo = o1[rc * XD + c];
     vL[r * LDA + c] = r < T ? xv : 0.f;
-    qL[r * LDA + c] = r < T ? xq : 0.f;
+    oL[r * LDA + c] = r < T ? xo : 0.f;
   }
-  XT(3, 0);
   __syncthreads();
-  XT(3, 1);
-  // attention: wave w = head w, keys = this sample's Ta rows of kv1 (k | v)
-  head_attention<F2_KT>(b, w, 0, T, Ta, qL, LDA, kv1 + (long)b * Ta * 2 * XD, kv1 + (long)b * Ta * 2 * XD + XD, 2 * XD,
-                        scale, P1, dr.attn, seed_attn, PL + w * 16 * F2_PLD, F2_PLD, oL, bias);
-  __syncthreads();
-  XT(3, 2);
-  for (int e = threadIdx.x; e < T * XD; e += 256) o1[row0 * XD + e] = oL[(e / XD) * LDA + e % XD];
   {  // v2 = o Wo1^T + bo1
     f32x4 acc[1][2];
     zero(acc);
@@ -437,46 +581,41 @@ __global__ __launch_bounds__(256) void xh_v2a_fwd_kernel(
     store_acc(acc, 32 * w, bo1, tL, LDA, nullptr, 0, 0, 16);
   }
   __syncthreads();
-  XT(3, 3);
   // v1 = LN(v + keep_b * v2)  (StochasticDepth: one keep draw per sample, fusion.py:11-26)
-  add_ln_rows(T, vL, tL, dropout_scale(seed_path, b, dr.path), gamma, beta, qL, s_v, mean_v, rstd_v, row0);
+  add_ln_rows(T, vL, tL, dropout_scale(seed_path, b, dr.path), gamma, beta, oL, s_v, mean_v, rstd_v, row0);
   __syncthreads();
-  for (int e = threadIdx.x; e < T * XD; e += 256) v1[row0 * XD + e] = qL[(e / XD) * LDA + e % XD];
-  for (int e = threadIdx.x; e < (16 - T) * XD; e += 256) qL[(T + e / XD) * LDA + e % XD] = 0.f;
+  for (int e = threadIdx.x; e < T * XD; e += 256) v1[row0 * XD + e] = oL[(e / XD) * LDA + e % XD];
+  for (int e = threadIdx.x; e < (16 - T) * XD; e += 256) oL[(T + e / XD) * LDA + e % XD] = 0.f;
   if (threadIdx.x < XD) {  // mean temporal pool of v1 (temporal.py:108-109) -> emb[b, 0:d]
     float s = 0.f;
-    for (int r = 0; r < T; ++r) s += qL[r * LDA + threadIdx.x];
+    for (int r = 0; r < T; ++r) s += oL[r * LDA + threadIdx.x];
     emb[(long)b * ld_emb + threadIdx.x] = s / T;
   }
   __syncthreads();
   {  // [k2 v2] = v1 Wkv2^T + bkv2: 256 columns, 64 per wave
     f32x4 acc[1][4];
     zero(acc);
-    mm_aw<1, 4, 3, XD>(acc, qL, LDA, 16, XD, Wkv2, XD, 64 * w);
+    mm_aw<1, 4, 3, XD>(acc, oL, LDA, 16, XD, Wkv2, XD, 64 * w);
     store_acc(acc, 64 * w, bkv2, nullptr, 0, kv2, 2 * XD, row0, T);
   }
-  XT(3, 4);
 }
 
-constexpr size_t F2_LDS_BYTES = sizeof(float) * (3 * 16 * LDA + XH * 16 * F2_PLD);
-
 MER_API int mer_xh_v2a_fwd(int B, int T, int Ta, const float* v, const float* q1, const float* kv1, const void* Wo1_hi,
-                           const void* Wo1_lo, const float* bo1, const float* gamma, const float* beta,
-                           const void* Wkv2_hi, const void* Wkv2_lo, const float* bkv2, float attn_p, float path_p,
-                           const unsigned long long* seed, unsigned long long site_attn, unsigned long long site_path,
-                           float scale, float* P1, float* o1, float* s_v, float* mean_v, float* rstd_v, float* v1,
-                           float* kv2, float* emb, long ld_emb, const float* bias, void* stream) {
+                            const void* Wo1_lo, const float* bo1, const float* gamma, const float* beta,
+                            const void* Wkv2_hi, const void* Wkv2_lo, const float* bkv2, float attn_p, float path_p,
+                            const unsigned long long* seed, unsigned long long site_attn, unsigned long long site_path,
+                            float scale, float* P1, float* o1, float* s_v, float* mean_v, float* rstd_v, float* v1,
+                            float* kv2, float* emb, long ld_emb, const float* bias, void* stream) {
   if (B <= 0) return 0;
-  if (T <= 0 || T > 16 || Ta <= 0 || Ta > 16 * F2_KT) return (int)hipErrorInvalidValue;
+  if (T <= 0 || T > 16 || Ta <= 0 || Ta > 4 * F2A_MAXC * 32) return (int)hipErrorInvalidValue;
   if ((attn_p > 0.f || path_p > 0.f) && !seed) return (int)hipErrorInvalidValue;
   XhDrop dr{attn_p, path_p, seed, site_attn, site_path};
-  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&xh_v2a_fwd_kernel),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)F2_LDS_BYTES) != hipSuccess)
-    return (int)hipErrorInvalidConfiguration;
-  hipLaunchKernelGGL(xh_v2a_fwd_kernel, dim3(B), dim3(256), F2_LDS_BYTES, (hipStream_t)stream, T, Ta, v, q1, kv1,
+  hipLaunchKernelGGL(xh_v2a_attn_kernel, dim3(B * XH), dim3(256), 0, (hipStream_t)stream, T, Ta, q1, kv1, dr, scale,
+                     P1, o1, bias);
+  hipLaunchKernelGGL(xh_v2a_post_kernel, dim3(B), dim3(256), 0, (hipStream_t)stream, T, v, o1,
                      SplitW{(const bf16_t*)Wo1_hi, (const bf16_t*)Wo1_lo}, bo1, gamma, beta,
-                     SplitW{(const bf16_t*)Wkv2_hi, (const bf16_t*)Wkv2_lo}, bkv2, dr, scale, P1, o1, s_v, mean_v,
-                     rstd_v, v1, kv2, emb, ld_emb, bias);
+                     SplitW{(const bf16_t*)Wkv2_hi, (const bf16_t*)Wkv2_lo}, bkv2, dr, s_v, mean_v, rstd_v, v1, kv2,
+                     emb, ld_emb);
   MER_LAUNCH_CHECK();
 }
 

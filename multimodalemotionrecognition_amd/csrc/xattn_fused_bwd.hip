@@ -326,35 +326,33 @@ MER_API int mer_xh_a2v_bwd(int B, int T, int Ta, const float* demb, const float*
 }
 
 // ---------------------------------------------------------------------------------------------
-// G2: v2a block backward, one workgroup per sample (T <= 16 query rows, Ta <= 160 keys), wave = head.
-// Unfused: xattn_head.py:252-269 + the v-pool half of 229-231.
+// G2: v2a block backward as two launches (xattn_head.py:252-269 + the v-pool half of 229-231).
+// G2a, one workgroup per sample: dkv2 = the a2v tiles' dK2 dV2 partials summed in tile order, dv1 = dkv2 Wkv2 +
+// v-pool gradient, LayerNorm backward (dv = its residual part, dv2 = keep * ds, dgamma / dbeta partials),
+// do1 = dv2 Wo1 (to global: G2b reads it).
+// G2b, one workgroup per (sample, head) (128 at B = 32; the one-workgroup-per-sample version ran 32): the
+// attention backward of head h, wave w owning the 32-key chunks c = w, w + 4, ...: dP' = do1_h V_h^T, the row sums
+// sum_j P dP meet in LDS (wave order), dS = P (dP - rowsum), dq1_h = dS K_h (per-wave partials summed in wave
+// order), dK1 / dV1 rows of the wave's keys into dqkv[:, 128:384].
 // ---------------------------------------------------------------------------------------------
-constexpr int G2_KT = 10;               // 16-key tiles (Ta <= 160)
-constexpr int G2_SLD = 16 * G2_KT + 4;  // dS / P' tile row stride
+constexpr int G2_KT = 10;  // 16-key tiles of one sample's keys the dkv2 fold reads (Ta <= 160 in G2a's fold)
 constexpr int G2_KVLD = 2 * XD + 4;
+constexpr int G2B_MAXC = 2;  // 32-key chunks per wave (Ta <= 256)
+constexpr int G2B_TLD = 36;
 
-__global__ __launch_bounds__(256) void xh_v2a_bwd_kernel(
-    int T, int Ta, int ntiles, const float* __restrict__ dkv2_part, SplitW WkvT2, const float* __restrict__ demb,
+__global__ __launch_bounds__(256) void xh_v2a_pre_bwd_kernel(
+    int T, int ntiles, const float* __restrict__ dkv2_part, SplitW WkvT2, const float* __restrict__ demb,
     const float* __restrict__ s_v, const float* __restrict__ mean_v, const float* __restrict__ rstd_v,
-    const float* __restrict__ gamma, SplitW WoT1, const float* __restrict__ P1, const float* __restrict__ kv1,
-    const float* __restrict__ q1, XhDrop dr, float scale, float* __restrict__ dkv2, float* __restrict__ dv2,
-    float* __restrict__ dq1, float* __restrict__ dv, float* __restrict__ dqkv, float* __restrict__ ln_part,
-    float* __restrict__ dbias) {
-  extern __shared__ __attribute__((aligned(16))) float g2smem[];
-  float* kvL = g2smem;                        // [16][G2_KVLD]  dK2 dV2
-  float* t1 = kvL + 16 * G2_KVLD;             // [16][LDA]  dv1, then ds (the residual part of dv)
-  float* d2L = t1 + 16 * LDA;                 // [16][LDA]  dv2
-  float* oL = d2L + 16 * LDA;                 // [16][LDA]  do1, then dv
-  float* dqL = oL + 16 * LDA;                 // [16][LDA]  dq1
-  float* tiles = dqL + 16 * LDA;              // [XH][2][16][G2_SLD]  dS, P'
-  float* red = tiles + XH * 2 * 16 * G2_SLD;  // [4][256]
+    const float* __restrict__ gamma, SplitW WoT1, XhDrop dr, float* __restrict__ dkv2, float* __restrict__ dv2,
+    float* __restrict__ dv, float* __restrict__ do1, float* __restrict__ ln_part) {
+  __shared__ __attribute__((aligned(16))) float kvL[16 * G2_KVLD];  // dK2 dV2
+  __shared__ __attribute__((aligned(16))) float t1[16 * LDA];       // dv1, then ds
+  __shared__ __attribute__((aligned(16))) float d2L[16 * LDA];      // dv2
+  __shared__ float red[4 * 256];
   const int b = blockIdx.x, w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int fr = lane & 15, fq = lane >> 4, fk = fq * 8;
   const long row0 = (long)b * T;
-  const unsigned long long seed_attn = mer_site_seed(dr.seed, dr.site_attn);
   const unsigned long long seed_path = mer_site_seed(dr.seed, dr.site_path);
   const float keep = dropout_scale(seed_path, b, dr.path);
-  XT(1, 0);
   // dK2 dV2 of this sample: the a2v tiles' partials summed in tile order
 #pragma unroll 4
   for (int e = threadIdx.x; e < 16 * 2 * XD; e += 256) {
@@ -371,7 +369,6 @@ __global__ __launch_bounds__(256) void xh_v2a_bwd_kernel(
     kvL[r * G2_KVLD + c] = s;
   }
   __syncthreads();
-  XT(1, 1);
   {  // dv1 (kv2 path) = [dK2 dV2] . Wkv2
     f32x4 acc[1][2];
     zero(acc);
@@ -379,7 +376,6 @@ __global__ __launch_bounds__(256) void xh_v2a_bwd_kernel(
     store_acc(acc, 32 * w, nullptr, t1, LDA, nullptr, 0, 0, 16);
   }
   __syncthreads();
-  XT(1, 2);
   {  // + v-pool (mean over T); LayerNorm backward; t1 = ds (dv residual), dv2 = keep * ds
     float g0 = 0.f, g1 = 0.f, b0 = 0.f, b1 = 0.f;
     const float pv0 = demb[(long)b * 2 * XD + lane] / T, pv1 = demb[(long)b * 2 * XD + 64 + lane] / T;
@@ -391,143 +387,156 @@ __global__ __launch_bounds__(256) void xh_v2a_bwd_kernel(
                    gamma, ds0, ds1, g0, g1, b0, b1);
         dv2[gr * XD + lane] = keep * ds0;
         dv2[gr * XD + 64 + lane] = keep * ds1;
+        dv[gr * XD + lane] = ds0;  // the residual part of dv (G1 adds dq1 . Wq1)
+        dv[gr * XD + 64 + lane] = ds1;
       }
-      t1[r * LDA + lane] = ds0;
-      t1[r * LDA + 64 + lane] = ds1;
       d2L[r * LDA + lane] = keep * ds0;
       d2L[r * LDA + 64 + lane] = keep * ds1;
     }
     ln_part_store(g0, g1, b0, b1, red, ln_part + (long)b * 256);
   }
   __syncthreads();
-  XT(1, 3);
   {  // do1 = dv2 . Wo1
     f32x4 acc[1][2];
     zero(acc);
     mm_aw<1, 2, 3, XD>(acc, d2L, LDA, 16, XD, WoT1, XD, 32 * w);
-    store_acc(acc, 32 * w, nullptr, oL, LDA, nullptr, 0, 0, 16);
+    store_acc(acc, 32 * w, nullptr, nullptr, 0, do1, XD, row0, T);
   }
-  __syncthreads();
-  XT(1, 4);
-  // attention backward, head h = w, keys = the sample's Ta rows of kv1
-  const int h = w;
-  float* dSt = tiles + (h * 2) * 16 * G2_SLD;
-  float* Pdt = dSt + 16 * G2_SLD;
-  const float* kb = kv1 + (long)b * Ta * 2 * XD;
-  float kraw[G2_KT / 2][2][8];
-  {
-    // every global load of the attention backward first (one memory latency): the V1 key-tile fragments and the
-    // saved probabilities of this head (raw fp32, split / masked at use)
-    f32x4 vraw[G2_KT][2];
-    float praw[G2_KT][4];
+}
+
+__global__ __launch_bounds__(256) void xh_v2a_attn_bwd_kernel(
+    int T, int Ta, const float* __restrict__ do1, const float* __restrict__ P1, const float* __restrict__ kv1,
+    const float* __restrict__ q1, XhDrop dr, float scale, float* __restrict__ dq1, float* __restrict__ dqkv,
+    float* __restrict__ dS_heads) {
+  __shared__ float red[4][16];
+  __shared__ __attribute__((aligned(16))) float dSt[4][16 * G2B_TLD];  // per-wave dS chunk [query][key]
+  __shared__ __attribute__((aligned(16))) float Pdt[4][16 * G2B_TLD];  // per-wave P' chunk
+  __shared__ float oP[4][16][33];
+  const int b = blockIdx.x >> 2, h = blockIdx.x & 3;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, fr = lane & 15, fq = lane >> 4, fk = fq * 8;
+  const long ldkv = 2 * XD, row0 = (long)b * T;
+  const float* Kr = kv1 + (long)b * Ta * ldkv + h * XDH;
+  const float* Vr = Kr + XD;
+  const int nch = (Ta + 31) / 32;
+  const unsigned long long seed_attn = mer_site_seed(dr.seed, dr.site_attn);
+  // every global load first: V fragments (dP), the saved probabilities, K gathers (dq1), the q1 / do1 fragments
+  f32x4 vraw[G2B_MAXC][2][2];
+  float praw[G2B_MAXC][2][4];
+  float kraw[G2B_MAXC][2][8];
 #pragma unroll
-    for (int t = 0; t < G2_KT; ++t) {
-      const int j = 16 * t + fr;
-      const float* vp = kb + (long)(j < Ta ? j : Ta - 1) * 2 * XD + XD + h * XDH + fk;
-      vraw[t][0] = *reinterpret_cast<const f32x4*>(vp);
-      vraw[t][1] = *reinterpret_cast<const f32x4*>(vp + 4);
+  for (int ci = 0; ci < G2B_MAXC; ++ci) {
+    const int c = w + 4 * ci;
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt) {
+      const int j = 32 * c + 16 * tt + fr, jc = j < Ta ? j : Ta - 1;
+      vraw[ci][tt][0] = *reinterpret_cast<const f32x4*>(Vr + (long)jc * ldkv + fk);
+      vraw[ci][tt][1] = *reinterpret_cast<const f32x4*>(Vr + (long)jc * ldkv + fk + 4);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int i = 4 * fq + r;
-        const bool ok = i < T && j < Ta;
-        praw[t][r] = P1[(((long)b * XH + h) * T + (ok ? i : 0)) * Ta + (ok ? j : 0)];  // always in range
-      }
-    }
-    f32x4 dp[G2_KT];
-#pragma unroll
-    for (int t = 0; t < G2_KT; ++t) dp[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-    bf16x8 ah, al;
-    frag_row(oL + fr * LDA + h * XDH + fk, true, ah, al);
-#pragma unroll
-    for (int t = 0; t < G2_KT; ++t) {  // dP' = do1_h . V1_h^T
-      const bool ok = 16 * t + fr < Ta;
-      float x[8] = {vraw[t][0][0], vraw[t][0][1], vraw[t][0][2], vraw[t][0][3],
-                    vraw[t][1][0], vraw[t][1][1], vraw[t][1][2], vraw[t][1][3]};
-#pragma unroll
-      for (int e = 0; e < 8; ++e) x[e] = ok ? x[e] : 0.f;
-      bf16x8 bh, bl;
-      split8(x, bh, bl);
-      dp[t] = mma3(ah, al, bh, bl, dp[t]);
-    }
-    // the K1 gathers of dq1 = dS K1 (next phase) go out now, behind the dS arithmetic
-#pragma unroll
-    for (int k = 0; k < G2_KT / 2; ++k)
-#pragma unroll
-      for (int jt = 0; jt < 2; ++jt)
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const int kk = 32 * k + fk + e;
-          kraw[k][jt][e] = kb[(long)(kk < Ta ? kk : Ta - 1) * 2 * XD + h * XDH + 16 * jt + fr];
-        }
-    float pv[G2_KT][4];
-    float rs[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int t = 0; t < G2_KT; ++t)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int i = 4 * fq + r, j = 16 * t + fr;
-        const bool ok = i < T && j < Ta;
-        const long pi = (((long)b * XH + h) * T + i) * Ta + j;
-        const float m = ok ? dropout_scale(seed_attn, pi, dr.attn) : 0.f;
-        const float p = ok ? praw[t][r] : 0.f;
-        pv[t][r] = p;
-        dp[t][r] *= m;  // dP
-        Pdt[i * G2_SLD + j] = p * m;
-        rs[r] += p * dp[t][r];
-      }
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-#pragma unroll
-      for (int o = 1; o < 16; o <<= 1) rs[r] += __shfl_xor(rs[r], o, 64);
-#pragma unroll
-    for (int t = 0; t < G2_KT; ++t)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) dSt[(4 * fq + r) * G2_SLD + 16 * t + fr] = pv[t][r] * (dp[t][r] - rs[r]);
-  }
-  wave_sync_lds();
-  XT(1, 5);
-  {  // dq1_h = dS . K1_h * scale  (keys >= Ta are zero in dS and read as zero from K1)
-    f32x4 o[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
-#pragma unroll
-    for (int k = 0; k < G2_KT / 2; ++k) {
-      bf16x8 ah, al;
-      frag_row(dSt + fr * G2_SLD + 32 * k + fk, true, ah, al);
-#pragma unroll
-      for (int jt = 0; jt < 2; ++jt) {
-        float x[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) x[e] = 32 * k + fk + e < Ta ? kraw[k][jt][e] : 0.f;
-        bf16x8 bh, bl;
-        split8(x, bh, bl);
-        o[jt] = mma3(ah, al, bh, bl, o[jt]);
+        praw[ci][tt][r] = P1[(((long)b * XH + h) * T + (i < T ? i : T - 1)) * Ta + jc];  // always in range
       }
     }
 #pragma unroll
     for (int jt = 0; jt < 2; ++jt)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) dqL[(4 * fq + r) * LDA + h * XDH + 16 * jt + fr] = o[jt][r] * scale;
+      for (int e = 0; e < 8; ++e) {
+        const int kk = 32 * c + fk + e;
+        kraw[ci][jt][e] = Kr[(long)(kk < Ta ? kk : Ta - 1) * ldkv + 16 * jt + fr];
+      }
   }
-  XT(1, 6);
-  {  // dK1_h = dS^T . q1_h * scale, dV1_h = P'^T . do1_h: rows = keys, contraction over the T query rows
-    bf16x8 qh[2], ql[2], gh[2], gl[2];
+  bf16x8 gh, gl;  // do1_h rows (A of dP)
+  frag_row(do1 + (row0 + (fr < T ? fr : T - 1)) * XD + h * XDH + fk, fr < T, gh, gl);
+  bf16x8 qch[2], qcl[2], gch[2], gcl[2];  // q1_h / do1_h as [dim][query] B operands of dK / dV
 #pragma unroll
-    for (int jt = 0; jt < 2; ++jt) {
-      frag_col(q1 + (row0 + fk) * XD + h * XDH + 16 * jt + fr, XD, fk, T, qh[jt], ql[jt]);
-      frag_col(oL + fk * LDA + h * XDH + 16 * jt + fr, LDA, fk, 16, gh[jt], gl[jt]);
+  for (int jt = 0; jt < 2; ++jt) {
+    frag_col(q1 + (row0 + fk) * XD + h * XDH + 16 * jt + fr, XD, fk, T, qch[jt], qcl[jt]);
+    frag_col(do1 + (row0 + fk) * XD + h * XDH + 16 * jt + fr, XD, fk, T, gch[jt], gcl[jt]);
+  }
+  f32x4 dp[G2B_MAXC][2];
+  float pv[G2B_MAXC][2][4], mk[G2B_MAXC][2][4];
+  float rs[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ci = 0; ci < G2B_MAXC; ++ci)
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt) {  // dP' = do1_h . V_h^T, dP = dP' * mask, rowsum partials of P dP
+      const int j = 32 * (w + 4 * ci) + 16 * tt + fr;
+      float x[8] = {vraw[ci][tt][0][0], vraw[ci][tt][0][1], vraw[ci][tt][0][2], vraw[ci][tt][0][3],
+                    vraw[ci][tt][1][0], vraw[ci][tt][1][1], vraw[ci][tt][1][2], vraw[ci][tt][1][3]};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) x[e] = j < Ta ? x[e] : 0.f;
+      bf16x8 bh, bl;
+      split8(x, bh, bl);
+      dp[ci][tt] = mma3(gh, gl, bh, bl, f32x4{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = 4 * fq + r;
+        const bool ok = i < T && j < Ta;
+        const long pi = (((long)b * XH + h) * T + i) * Ta + j;
+        const float m = ok ? dropout_scale(seed_attn, pi, dr.attn) : 0.f;
+        const float p = ok ? praw[ci][tt][r] : 0.f;
+        pv[ci][tt][r] = p;
+        mk[ci][tt][r] = m;
+        dp[ci][tt][r] *= m;
+        rs[r] += p * dp[ci][tt][r];
+      }
     }
 #pragma unroll
-    for (int t = 0; t < G2_KT; ++t) {
-      if (16 * t >= Ta) break;
-      bf16x8 sh, sl, ph, pl;
-      frag_col(dSt + (long)fk * G2_SLD + 16 * t + fr, G2_SLD, fk, 16, sh, sl);
-      frag_col(Pdt + (long)fk * G2_SLD + 16 * t + fr, G2_SLD, fk, 16, ph, pl);
+  for (int r = 0; r < 4; ++r) {
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) rs[r] += __shfl_xor(rs[r], o, 64);
+    if (fr == 0) red[w][4 * fq + r] = rs[r];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int i = 4 * fq + r;
+    rs[r] = (red[0][i] + red[1][i]) + (red[2][i] + red[3][i]);
+  }
+  f32x4 oq[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+  float* st = dSt[w];
+  float* pt = Pdt[w];
+#pragma unroll
+  for (int ci = 0; ci < G2B_MAXC; ++ci) {
+    const int c = w + 4 * ci;
+    if (c >= nch) break;  // (wave-uniform)
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = 4 * fq + r, jj = 16 * tt + fr, j = 32 * c + jj;
+        const float ds = pv[ci][tt][r] * (dp[ci][tt][r] - rs[r]);
+        st[i * G2B_TLD + jj] = ds;
+        pt[i * G2B_TLD + jj] = pv[ci][tt][r] * mk[ci][tt][r];  // P' (zero outside the T x Ta block)
+        if (dS_heads && i < T && j < Ta) dS_heads[(((long)b * XH + h) * T + i) * Ta + j] = ds;
+      }
+    wave_sync_lds();
+    {  // dq1_h partial = dS . K_h over this chunk's keys
+      bf16x8 ah, al;
+      frag_row(st + fr * G2B_TLD + fk, true, ah, al);
 #pragma unroll
       for (int jt = 0; jt < 2; ++jt) {
-        const f32x4 dk = mma3(sh, sl, qh[jt], ql[jt], f32x4{0.f, 0.f, 0.f, 0.f});
-        const f32x4 dvv = mma3(ph, pl, gh[jt], gl[jt], f32x4{0.f, 0.f, 0.f, 0.f});
+        float x[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) x[e] = 32 * c + fk + e < Ta ? kraw[ci][jt][e] : 0.f;
+        bf16x8 bh, bl;
+        split8(x, bh, bl);
+        oq[jt] = mma3(ah, al, bh, bl, oq[jt]);
+      }
+    }
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt) {  // dK1_h = dS^T q1_h * scale, dV1_h = P'^T do1_h for the chunk's 2 key tiles
+      if (32 * c + 16 * tt >= Ta) break;
+      bf16x8 sh, sl, ph, pl;
+      frag_col(st + (long)fk * G2B_TLD + 16 * tt + fr, G2B_TLD, fk, 16, sh, sl);
+      frag_col(pt + (long)fk * G2B_TLD + 16 * tt + fr, G2B_TLD, fk, 16, ph, pl);
+#pragma unroll
+      for (int jt = 0; jt < 2; ++jt) {
+        const f32x4 dk = mma3(sh, sl, qch[jt], qcl[jt], f32x4{0.f, 0.f, 0.f, 0.f});
+        const f32x4 dvv = mma3(ph, pl, gch[jt], gcl[jt], f32x4{0.f, 0.f, 0.f, 0.f});
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int j = 16 * t + 4 * fq + r;
+          const int j = 32 * c + 16 * tt + 4 * fq + r;
           if (j < Ta) {
             float* drow = dqkv + ((long)b * Ta + j) * 3 * XD;
             drow[XD + h * XDH + 16 * jt + fr] = dk[r] * scale;
@@ -536,45 +545,52 @@ __global__ __launch_bounds__(256) void xh_v2a_bwd_kernel(
         }
       }
     }
+    wave_sync_lds();  // the next chunk overwrites st / pt
   }
-  __syncthreads();
-  for (int e = threadIdx.x; e < T * XD; e += 256) {  // dq1 and the residual part of dv (G1 adds dq1 . Wq1)
-    const int r = e / XD, c = e - r * XD;
-    dq1[row0 * XD + e] = dqL[r * LDA + c];
-    dv[row0 * XD + e] = t1[r * LDA + c];
-  }
-  if (dbias) {  // the prior bias gradient: dS summed over the heads in head order (mha_dbias_kernel's order)
-    for (int e = threadIdx.x; e < T * Ta; e += 256) {
-      const int i = e / Ta, j = e - i * Ta;
-      float s = 0.f;
 #pragma unroll
-      for (int q = 0; q < XH; ++q) s += tiles[(q * 2) * 16 * G2_SLD + i * G2_SLD + j];
-      dbias[((long)b * T + i) * Ta + j] = s;
-    }
+  for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) oP[w][4 * fq + r][16 * jt + fr] = oq[jt][r];
+  __syncthreads();
+  for (int e = threadIdx.x; e < T * XDH; e += 256) {
+    const int i = e / XDH, d = e - i * XDH;
+    dq1[(row0 + i) * XD + h * XDH + d] = ((oP[0][i][d] + oP[1][i][d]) + (oP[2][i][d] + oP[3][i][d])) * scale;
   }
-  XT(1, 7);
 }
 
-constexpr size_t G2_LDS_BYTES = sizeof(float) * (16 * G2_KVLD + 4 * 16 * LDA + XH * 2 * 16 * G2_SLD + 4 * 256);
+// the prior bias gradient: dbias[b][i][j] = sum over heads of dS (head order, mha_dbias_kernel's order)
+__global__ __launch_bounds__(256) void xh_dbias_heads_kernel(long n_per_b, long n, const float* __restrict__ dS_heads,
+                                                             float* __restrict__ dbias) {
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < n; e += (long)gridDim.x * 256) {
+    const long b = e / n_per_b, k = e - b * n_per_b;
+    const float* p = dS_heads + b * XH * n_per_b + k;
+    dbias[e] = ((p[0] + p[n_per_b]) + p[2 * n_per_b]) + p[3 * n_per_b];
+  }
+}
 
 MER_API int mer_xh_v2a_bwd(int B, int T, int Ta, const float* dkv2_part, const void* WkvT2_hi, const void* WkvT2_lo,
                            const float* demb, const float* s_v, const float* mean_v, const float* rstd_v,
                            const float* gamma, const void* WoT1_hi, const void* WoT1_lo, const float* P1,
                            const float* kv1, const float* q1, float attn_p, float path_p, const unsigned long long* seed,
                            unsigned long long site_attn, unsigned long long site_path, float scale, float* dkv2,
-                           float* dv2, float* dq1, float* dv, float* dqkv, float* ln_part, float* dbias,
-                           void* stream) {
+                           float* dv2, float* dq1, float* dv, float* dqkv, float* ln_part, float* do1,
+                           float* dS_heads, float* dbias, void* stream) {
   if (B <= 0) return 0;
-  if (T <= 0 || T > 16 || Ta <= 0 || Ta > 16 * G2_KT || ((attn_p > 0.f || path_p > 0.f) && !seed))
+  if (T <= 0 || T > 16 || Ta <= 0 || Ta > 16 * G2_KT || ((attn_p > 0.f || path_p > 0.f) && !seed) || !do1 ||
+      (dbias && !dS_heads))
     return (int)hipErrorInvalidValue;
   XhDrop dr{attn_p, path_p, seed, site_attn, site_path};
-  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&xh_v2a_bwd_kernel),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)G2_LDS_BYTES) != hipSuccess)
-    return (int)hipErrorInvalidConfiguration;
-  hipLaunchKernelGGL(xh_v2a_bwd_kernel, dim3(B), dim3(256), G2_LDS_BYTES, (hipStream_t)stream, T, Ta, (Ta + 15) / 16,
-                     dkv2_part, SplitW{(const bf16_t*)WkvT2_hi, (const bf16_t*)WkvT2_lo}, demb, s_v, mean_v, rstd_v,
-                     gamma, SplitW{(const bf16_t*)WoT1_hi, (const bf16_t*)WoT1_lo}, P1, kv1, q1, dr, scale, dkv2, dv2,
-                     dq1, dv, dqkv, ln_part, dbias);
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(xh_v2a_pre_bwd_kernel, dim3(B), dim3(256), 0, st, T, (Ta + 15) / 16, dkv2_part,
+                     SplitW{(const bf16_t*)WkvT2_hi, (const bf16_t*)WkvT2_lo}, demb, s_v, mean_v, rstd_v, gamma,
+                     SplitW{(const bf16_t*)WoT1_hi, (const bf16_t*)WoT1_lo}, dr, dkv2, dv2, dv, do1, ln_part);
+  hipLaunchKernelGGL(xh_v2a_attn_bwd_kernel, dim3(B * XH), dim3(256), 0, st, T, Ta, do1, P1, kv1, q1, dr, scale, dq1,
+                     dqkv, dbias ? dS_heads : nullptr);
+  if (dbias) {
+    const long n = (long)B * T * Ta;
+    hipLaunchKernelGGL(xh_dbias_heads_kernel, dim3((unsigned)((n + 255) / 256 < 1024 ? (n + 255) / 256 : 1024)),
+                       dim3(256), 0, st, (long)T * Ta, n, dS_heads, dbias);
+  }
   MER_LAUNCH_CHECK();
 }
 

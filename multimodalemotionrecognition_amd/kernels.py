@@ -1036,12 +1036,15 @@ def xh_v2a_bwd(B, T, Ta, dkv2_part, WkvT2, demb, s_v, mu_v, rs_v, gamma, WoT1, P
     _f32c(dkv2_part, demb, s_v, mu_v, rs_v, gamma, P1, kv1, q1, dkv2, dv2, dq1, dv, dqkv, ln_part, dbias)
     if dbias is not None and dbias.numel() != B * T * Ta:
         raise ValueError("xh_v2a_bwd dbias shape")
+    dev = dv.device
+    do1 = torch.empty(B * T, 128, device=dev, dtype=torch.float32)  # G2a -> G2b hand-off
+    dsh = torch.empty(B, 4, T, Ta, device=dev, dtype=torch.float32) if dbias is not None else None
     _launch("xh_v2a_bwd", (B, T, Ta), "mer_xh_v2a_bwd", B, T, Ta, dkv2_part.data_ptr(), *_planes(WkvT2),
             demb.data_ptr(), s_v.data_ptr(), mu_v.data_ptr(), rs_v.data_ptr(), gamma.data_ptr(), *_planes(WoT1),
             P1.data_ptr(), kv1.data_ptr(), q1.data_ptr(), float(attn_p), float(path_p),
             rng_ptr(rng) if (attn_p > 0 or path_p > 0) else 0, int(site_attn), int(site_path), float(scale),
             dkv2.data_ptr(), dv2.data_ptr(), dq1.data_ptr(), dv.data_ptr(), dqkv.data_ptr(), ln_part.data_ptr(),
-            _ptr(dbias), stream_ptr())
+            do1.data_ptr(), _ptr(dsh), _ptr(dbias), stream_ptr())
 
 
 def xh_audio_bwd(dqkv, WcT, WaT, da, da_s, dq1, WqT1, WvT, dv, dvfeat):
