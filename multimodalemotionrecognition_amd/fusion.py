@@ -53,7 +53,14 @@ _HEAD_SPLIT = os.environ.get("MER_HEAD_SPLIT", "1") != "0"
 _HEAD_STREAMS = {}
 
 
+_HEAD_OWN_STREAM = os.environ.get("MER_HEAD_STREAM", "side") == "own"
+
+
 def _head_stream(device: torch.device):
+    """The audio-first head's stream: the audio encoder's side stream (the head's audio phase queues ahead of the
+    next batch's encoder, its deferred backward behind it), or its own (MER_HEAD_STREAM=own, A/B)."""
+    if not _HEAD_OWN_STREAM:
+        return _side_stream(device)
     idx = device.index if device.index is not None else torch.cuda.current_device()
     s = _HEAD_STREAMS.get(idx)
     if s is None:
