@@ -500,11 +500,8 @@ def _bench(args, world, rank, local):
         # the fused head's forward + backward graph replays in production (with the next batch's WavLM running
         # beside them on the prefetch stream); bytes = the saved activations (inputs included) written once and
         # read once + the used head parameters read twice and their gradients written once + dv_feat
-        # audio-first schedule: the forward's audio phase and the backward's deferred phase run on the head stream
-        # beside the frame trunk; the head's time is the sum of its four spans, its critical path the main-stream two
         fwd_ms, bwd_ms = hms
-        sfwd_ms, sbwd_ms = hprobe.avg_side_ms()
-        head_ms = fwd_ms + bwd_ms + sfwd_ms + sbwd_ms
+        head_ms = fwd_ms + bwd_ms
         hparams = sum(t.numel() for n, t in zip(*model.head_params()) if t.requires_grad)
         hbytes = 2 * hprobe.saved_bytes + 3 * 4 * hparams + 4 * BATCH * FRAMES * 512
         hflop = head_flop()
@@ -516,15 +513,12 @@ def _bench(args, world, rank, local):
                      "frac": round(ach / attain, 4), "traffic": pmc_traffic_head(),
                      "kernel": "fused xattn head fwd+bwd (csrc/xattn_fused.hip F1-F4, xattn_fused_bwd.hip G1-G4 + W)",
                      "algorithmic_flop": hflop, "algorithmic_bytes": hbytes, "intensity_flop_per_byte": round(ai, 2),
-                     "fwd_ms": round(fwd_ms, 4), "bwd_ms": round(bwd_ms, 4),
-                     "side_fwd_ms": round(sfwd_ms, 4), "side_bwd_ms": round(sbwd_ms, 4),
-                     "ms_per_step": round(head_ms, 4), "critical_path_ms": round(fwd_ms + bwd_ms, 4),
+                     "fwd_ms": round(fwd_ms, 4), "bwd_ms": round(bwd_ms, 4), "ms_per_step": round(head_ms, 4),
                      "hbm_gbs_achieved": round(hbytes / (head_ms * 1e-3) / 1e9, 1),
                      "peak_basis": "min(split-bf16 fp32-class MFMA peak = 2.5 PF / 3, intensity x 8 TB/s)",
                      "core": roof_core(core_ms, peak_split),
-                     "measured": f"HIP events around the head's forward / backward graph replays (main stream; "
-                                 f"audio phase and deferred backward on the head stream) in {len(hprobe.fwd)} "
-                                 "probe steps"}
+                     "measured": f"HIP events around the head's forward / backward graph replays in "
+                                 f"{len(hprobe.fwd)} probe steps"}
     step_gflop = BATCH * (STEP_GFLOP_PER_CLIP_FIXED + WAVLM_LAYER_GFLOP_PER_CLIP * layers)
     out = {
         "metric": "3s-clip train steps/sec (B=32, xattn fusion) at 1/2/4/8 MI355X",

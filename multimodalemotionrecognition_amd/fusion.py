@@ -46,28 +46,6 @@ def _side_stream(device: torch.device):
     return s
 
 
-# The head's audio-first schedule (_HeadGraphs): its audio phase runs on a head stream beside the frame trunk and
-# its deferred backward (G1's audio rows, the grouped weight gradients) beside the trunk backward.
-# MER_HEAD_SPLIT=0 keeps the whole head on the main stream (A/B).
-_HEAD_SPLIT = os.environ.get("MER_HEAD_SPLIT", "1") != "0"
-_HEAD_STREAMS = {}
-
-
-_HEAD_OWN_STREAM = os.environ.get("MER_HEAD_STREAM", "side") == "own"
-
-
-def _head_stream(device: torch.device):
-    """The audio-first head's stream: the audio encoder's side stream (the head's audio phase queues ahead of the
-    next batch's encoder, its deferred backward behind it), or its own (MER_HEAD_STREAM=own, A/B)."""
-    if not _HEAD_OWN_STREAM:
-        return _side_stream(device)
-    idx = device.index if device.index is not None else torch.cuda.current_device()
-    s = _HEAD_STREAMS.get(idx)
-    if s is None:
-        s = _HEAD_STREAMS[idx] = torch.cuda.Stream(device=idx)
-    return s
-
-
 def _next_seed() -> int:
     # host-side draw so that torch.manual_seed() makes runs reproducible (train.py:951 set_seed)
     return int(torch.randint(0, 2 ** 62, (1,)).item())
@@ -216,28 +194,20 @@ class HeadProbe:
     (on the stream they replay on), collected while ``fusion.HEAD_PROBE`` is set."""
 
     def __init__(self):
-        self.fwd, self.bwd = [], []  # the main-stream (critical-path) replays
-        self.fwd_side, self.bwd_side = [], []  # the audio-first schedule's head-stream replays
+        self.fwd, self.bwd = [], []
         self.saved_bytes = 0
 
-    def mark(self, stream=None):
+    def mark(self):
         e = torch.cuda.Event(enable_timing=True)
-        e.record(stream)
+        e.record()
         return e
 
-    @staticmethod
-    def _avg(pairs):
-        return sum(a.elapsed_time(b) for a, b in pairs) / len(pairs) if pairs else 0.0
-
     def avg_ms(self):
-        """(forward, backward) ms on the main stream, or None."""
-        if not self.fwd or not self.bwd:
+        f = [a.elapsed_time(b) for a, b in self.fwd]
+        b = [a.elapsed_time(c) for a, c in self.bwd]
+        if not f or not b:
             return None
-        return self._avg(self.fwd), self._avg(self.bwd)
-
-    def avg_side_ms(self):
-        """(forward, backward) ms of the head-stream replays (0 without the audio-first schedule)."""
-        return self._avg(self.fwd_side), self._avg(self.bwd_side)
+        return sum(f) / len(f), sum(b) / len(b)
 
 
 HEAD_PROBE = None
@@ -251,67 +221,17 @@ class _HeadGraphs(G.PendingGuard):
     the masks exactly as in eager mode), and the backward graph regenerates the same masks from it.
     ``pending`` marks a forward whose backward has not run yet: a second forward in between (gradient
     accumulation) runs eagerly instead of overwriting the saved static activations.
-
-    Audio-first schedule (the fused head, ``split``): the forward is two graphs -- ``fwd_a``, the weight split +
-    F1's audio chain, which needs only the audio features and is issued on the head stream as soon as they are
-    known (FusionModel.forward does so before the frame trunk, which it then overlaps), and ``fwd_v``, the rest,
-    on the main stream after the trunk -- and so is the backward: ``bwd`` (G4, G3, G2, G1's video rows: what the
-    trunk backward waits for) on the main stream, then ``bwd_d`` (G1's audio rows + the grouped weight gradients)
-    on the head stream beside the trunk backward.  The main stream waits for ``bwd_d`` at the end of the backward
-    pass (an autograd engine callback) and before the data-parallel early bucket.
     """
 
     def __init__(self, model, names, cfg, training):
         super().__init__()
         self.model, self.names, self.cfg, self.training = model, names, cfg, training
         self.fwd = self.bwd = None
-        self.fwd_a = self.fwd_v = self.bwd_d = None
-        self.split = None  # decided on the first forward
-        self.audio_issued = False
-        self.ev_a = self.ev_d = None
         self.cur_gen = 0
         self.rng = None
 
-    def _params(self):
-        return dict(zip(self.names, self.model.head_params()[1]))
-
-    def _decide(self, params, v_like, a_seq) -> bool:
-        if self.split is None:
-            self.split = bool(_HEAD_SPLIT and XF.supported(self.cfg, params, v_like, a_seq, None))
-            if self.split:
-                self.ev_a, self.ev_d = torch.cuda.Event(), torch.cuda.Event()
-        return self.split
-
-    def issue_audio(self, a_seq, T: int) -> bool:
-        """Start the audio phase on the head stream now (ordered after the main stream's work so far); False when
-        this head does not take the audio-first schedule."""
-        params = self._params()
-        v_like = torch.empty((a_seq.shape[0], T, params["v_in_proj.weight"].shape[1]), device="meta")
-        if not self._decide(params, v_like, a_seq):
-            return False
-        main = torch.cuda.current_stream(a_seq.device)
-        hs = _head_stream(a_seq.device)
-        hs.wait_stream(main)
-        if not G.is_borrowed(a_seq):  # an eager encoder output: keep its block from the allocator while hs reads it
-            a_seq.record_stream(hs)
-        with torch.cuda.stream(hs):
-            if self.fwd_a is None:
-                XF.planes_for(params)  # host-side setup (an H2D descriptor copy) outside the capture
-                self.fwd_a = G.StaticGraph(lambda a: XH.head_forward_audio(params, self.cfg, a, self.training, T),
-                                           [a_seq])
-            probe = HEAD_PROBE
-            e0 = probe.mark(hs) if probe is not None else None
-            self.fwd_a.replay(a_seq)  # copies a_seq into its static input first: the caller may reuse a_seq after
-            if probe is not None:
-                probe.fwd_side.append((e0, probe.mark(hs)))
-            self.ev_a.record(hs)
-        self.audio_issued = True
-        return True
-
     def forward(self, v_feat, a_seq):
-        params = self._params()
-        if self._decide(params, v_feat, a_seq):
-            return self._forward_split(params, v_feat, a_seq)
+        params = dict(zip(self.names, self.model.head_params()[1]))
         if self.fwd is None:
             if XF.supported(self.cfg, params, v_feat, a_seq, None):
                 XF.planes_for(params)  # host-side setup (an H2D descriptor copy) outside the capture
@@ -329,70 +249,27 @@ class _HeadGraphs(G.PendingGuard):
             probe.saved_bytes = sum(t.numel() * t.element_size() for t in hctx.saved.values())
         return logits.clone(), hctx
 
-    def _forward_split(self, params, v_feat, a_seq):
-        if not self.audio_issued:  # (not issued ahead by FusionModel.forward: no prefetched features)
-            self.issue_audio(a_seq, v_feat.shape[1])
-        self.audio_issued = False
-        main = torch.cuda.current_stream(v_feat.device)
-        if self.fwd_v is None:
-            self.rng = torch.zeros(1, dtype=torch.int64, device=v_feat.device)
-            hctx_a = self.fwd_a.out
-            self.fwd_v = G.StaticGraph(
-                lambda v: XH.head_forward_video(params, self.cfg, v, self.fwd_a.static_in[0], self.training,
-                                                self.rng if self.training else None, hctx_a), [v_feat])
-        if self.training:
-            self.rng.fill_(self.model.take_head_seed())
-        main.wait_event(self.ev_a)
-        probe = HEAD_PROBE
-        e0 = probe.mark() if probe is not None else None
-        logits = self.fwd_v.replay(v_feat)
-        hctx = self.fwd_a.out
-        if probe is not None:
-            probe.fwd.append((e0, probe.mark()))
-            probe.saved_bytes = sum(t.numel() * t.element_size() for t in hctx.saved.values())
-        return logits.clone(), hctx
-
     def backward_graphable(self, p, used, need_v, need_a) -> bool:
         return (not need_a) and all(t.grad is None and getattr(t, "_mer_grad_slot", None) is not None
                                     for n, t in p.items() if n in used and t.requires_grad)
 
     def backward(self, dlogits):
-        params = self._params()
+        params = dict(zip(self.names, self.model.head_params()[1]))
         used = set(XH.used_param_names(self.cfg))
-        split = bool(self.split)
         if self.bwd is None:
-            hctx = self.fwd_a.out if split else self.fwd.out[1]
+            _, hctx = self.fwd.out
 
             def run(dl):
                 grads = _head_grads(params, used)
-                dv, _ = XH.head_backward(params, hctx, dl, grads, need_dv_feat=True, need_da_seq=False,
-                                         phase="critical" if split else "all")
+                dv, _ = XH.head_backward(params, hctx, dl, grads, need_dv_feat=True, need_da_seq=False)
                 return dv
 
             self.bwd = G.StaticGraph(run, [dlogits])
-            if split:  # captured after bwd: it reads the intermediates bwd's capture left in hctx.bwd_state
-                self.bwd_d = G.StaticGraph(
-                    lambda: XH.head_backward(params, hctx, None, _head_grads(params, used), phase="deferred"), [],
-                    stream=_head_stream(dlogits.device))
         probe = HEAD_PROBE
         e0 = probe.mark() if probe is not None else None
         dv = self.bwd.replay(dlogits)
         if probe is not None:
             probe.bwd.append((e0, probe.mark()))
-        if split:
-            main = torch.cuda.current_stream(dlogits.device)
-            hs = _head_stream(dlogits.device)
-            hs.wait_stream(main)
-            with torch.cuda.stream(hs):
-                e0 = probe.mark(hs) if probe is not None else None
-                self.bwd_d.replay()
-                if probe is not None:
-                    probe.bwd_side.append((e0, probe.mark(hs)))
-                self.ev_d.record(hs)
-            self.model._head_join = (main, self.ev_d)
-            # the gradients are complete for whatever runs after this backward pass (the optimizer step, a caller's
-            # own loop): the main stream waits for the deferred phase at the end of the pass
-            torch.autograd.Variable._execution_engine.queue_callback(self.model.join_head)
         # dv goes straight back through autograd into the trunk backward of this same pass, before the next
         # replay of this graph: the static tensor itself, no copy
         return dv, {n: grad_buffer(t) for n, t in params.items() if n in used and t.requires_grad}
@@ -566,18 +443,14 @@ class FusionModel(nn.Module):
         a, self._queued_audio = self._queued_audio, None
         return a
 
-    def _issue_queued(self, kind: str, a_out: torch.Tensor, head=None) -> torch.Tensor:
+    def _issue_queued(self, kind: str, a_out: torch.Tensor) -> torch.Tensor:
         """Start the queued early prefetch now; returns ``a_out`` made safe against it (a borrowed encoder-graph
-        output is rewritten by that replay: this step keeps its own copy, ordered before the side stream).
-        ``head``: a head runner whose audio phase already took ``a_out`` on the head stream (into its own static
-        input): the prefetch is ordered after that instead, and no copy is needed."""
+        output is rewritten by that replay: this step keeps its own copy, ordered before the side stream)."""
         nxt = self._queued_audio
         if nxt is None or not torch.is_grad_enabled():
             return a_out
         self._queued_audio = None
-        if head is not None and head.audio_issued:
-            _side_stream(a_out.device).wait_event(head.ev_a)
-        elif G.is_borrowed(a_out):
+        if G.is_borrowed(a_out):
             a_out = a_out.clone()
         # host draws in the inline order: this step's head seed before the next batch's encoder draws
         if self.training:
@@ -651,23 +524,10 @@ class FusionModel(nn.Module):
 
     def register_grad_ready_hook(self, fn) -> None:
         """``fn(params)`` is called from the backward as soon as the ``early_grad_params()`` gradients are final
-        (enqueued): the early all-reduce bucket (dist.GradAllReduce).  The head's deferred weight gradients (audio-
-        first schedule) are joined onto the current stream first."""
+        (enqueued): the early all-reduce bucket (dist.GradAllReduce)."""
         trunk = self.video_model.backbone
         early = self.early_grad_params()
-
-        def hook(ps):
-            self.join_head()
-            fn(early)
-
-        trunk.grad_ready_hook = hook
-
-    def join_head(self) -> None:
-        """Order the current (main) stream after the head's deferred backward phase, if one is in flight."""
-        j = self.__dict__.get("_head_join")
-        if j is not None:
-            self.__dict__["_head_join"] = None
-            j[0].wait_event(j[1])
+        trunk.grad_ready_hook = lambda ps: fn(early)
 
     def pop_alignment_loss(self) -> Optional[torch.Tensor]:
         loss = self.alignment_loss
@@ -700,23 +560,8 @@ class FusionModel(nn.Module):
             hp = self.__dict__["_mer_head_params"] = (tuple(names), params)
         return hp
 
-    def _head_audio_first(self, T: int, a_seq: torch.Tensor):
-        """Audio-first schedule: claim the head's graph runner for this step now and start its audio phase on the
-        head stream (before the frame trunk).  Returns the runner (or None: eager head this step) for
-        ``xattn_from_features``; the runner's ``audio_issued`` says whether the phase was started."""
-        if EH.int8_images(self) is not None or a_seq.requires_grad:
-            return None
-        names, params = self.head_params()
-        cfg = self.head_config()
-        v_like = torch.empty((a_seq.shape[0], T, self.v_dim), device="meta")
-        runner = self._head_runner(names, params, cfg, v_like, a_seq.contiguous())
-        if runner is not None:
-            runner.issue_audio(a_seq.contiguous(), T)
-        return runner
-
-    def xattn_from_features(self, v_feat: torch.Tensor, a_seq: torch.Tensor, runner=False) -> torch.Tensor:
-        """xattn head on encoder features: v_feat [B,T,v_dim] (backbone output), a_seq [B,Ta,seq_dim].
-        ``runner``: the head runner ``_head_audio_first`` already claimed for this step (None: eager)."""
+    def xattn_from_features(self, v_feat: torch.Tensor, a_seq: torch.Tensor) -> torch.Tensor:
+        """xattn head on encoder features: v_feat [B,T,v_dim] (backbone output), a_seq [B,Ta,seq_dim]."""
         _require_device(v_feat, a_seq)
         names, params = self.head_params()
         qlin = EH.int8_images(self)
@@ -726,8 +571,7 @@ class FusionModel(nn.Module):
                                        a_seq.contiguous(), False, None, qlin=qlin)[0]
         cfg = self.head_config()
         v_feat, a_seq = v_feat.contiguous(), a_seq.contiguous()
-        if runner is False:
-            runner = self._head_runner(names, params, cfg, v_feat, a_seq)
+        runner = self._head_runner(names, params, cfg, v_feat, a_seq)
         if runner is None:  # the eager head keeps its inputs for the backward: own copies of borrowed outputs
             v_feat = v_feat.clone() if G.is_borrowed(v_feat) else v_feat
             a_seq = a_seq.clone() if G.is_borrowed(a_seq) else a_seq
@@ -740,7 +584,7 @@ class FusionModel(nn.Module):
         for the audio features (graphs.py)."""
         if G.capturing() or a_seq.requires_grad:
             return None
-        key = (tuple(v_feat.shape), tuple(a_seq.shape), a_seq.dtype, a_seq.device.index, self.training,
+        key = (tuple(v_feat.shape), tuple(a_seq.shape), a_seq.dtype, v_feat.device.index, self.training,
                dataclasses.astuple(cfg), tuple(q.data_ptr() for q in params))
         if not self._head_graphs.ready(key):
             return None
@@ -774,15 +618,12 @@ class FusionModel(nn.Module):
             # backward), its result is taken over instead.
             kind = "seq" if self.audio_encoder_frozen() else "prefix"
             if self._prefetch_matches(audio, kind):
-                got = self._take_prefetched(audio, kind)
-                # the head's audio phase starts now, beside the frame trunk (audio-first schedule)
-                head = self._head_audio_first(t, got) if kind == "seq" else False
-                got = self._issue_queued(kind, got, head=head or None)
+                got = self._issue_queued(kind, self._take_prefetched(audio, kind))
                 with G.borrow_outputs():
                     v_feat = self.video_model.backbone(v_in).view(b, t, self.v_dim)
                 # stage 2: prefetched frozen prefix -> trainable tail now
                 a_seq = self.audio_model.encode_sequence(audio, prefix=got) if kind == "prefix" else got
-                return self.xattn_from_features(v_feat, a_seq, runner=head)
+                return self.xattn_from_features(v_feat, a_seq)
             self._prefetched = None
             side = _side_stream(video.device) if _OVERLAP_ENCODERS else None
             # the encoders' graph outputs go to the head without a copy (graphs.borrow_outputs; the head's

@@ -150,52 +150,34 @@ def planes_for(p: Dict[str, torch.Tensor]) -> SplitPlanes:
     return sp
 
 
-def fused_forward(p, cfg, v_feat, a_seq, training, rng, ctx, sites, phase: str = "all"):
-    """Fill ``ctx`` (xattn_head.HeadCtx) exactly as head_forward does and return the logits.
-
-    ``phase``: "all" -- the whole forward; "audio" -- the weight split and F1's audio chain alone (a_seq ->
-    a_s, a, [q2 | k1 v1]: no dropout, nothing from the frame trunk), returns None; "video" -- the rest, on a
-    context whose audio phase has run.  The audio-first schedule (fusion._HeadGraphs) runs the audio phase on a
-    side stream beside the frame trunk, so only the video phase sits on the critical path."""
-    B, Ta, sd = a_seq.shape
-    vd = p["v_in_proj.weight"].shape[1]
-    T = v_feat.shape[1] if v_feat is not None else 0  # (the audio phase runs without the frame features)
+def fused_forward(p, cfg, v_feat, a_seq, training, rng, ctx, sites):
+    """Fill ``ctx`` (xattn_head.HeadCtx) exactly as head_forward does and return the logits."""
+    B, T, vd = v_feat.shape
+    _, Ta, sd = a_seq.shape
     d, H = 128, 4
-    dev = a_seq.device
+    dev = v_feat.device
     f32 = torch.float32
     e = lambda *shape: torch.empty(shape, device=dev, dtype=f32)  # noqa: E731
-    sv = ctx.saved
-    if phase in ("all", "audio"):
-        sp = planes_for(p)
-        sp.refresh(transposed=training)  # a training forward is followed by the fused backward
-        ctx.planes_gen = sp.gen
-        ctx.planes = sp  # a captured graph writes through sp's descriptors: keep them alive as long as the context
-        af = a_seq.reshape(B * Ta, sd).contiguous()
-        a_s, a, q2, kv1 = e(B * Ta, d), e(B * Ta, d), e(B * Ta, d), e(B * Ta, 2 * d)
-        sv.update(af=af, a_s=a_s, a=a, q2=q2, kv1=kv1)
-    if phase == "audio":
-        K.xh_audio_fwd(af, sp["Ws"], p["audio_seq_proj.bias"], sp["Wa"], p["a_in_proj.bias"], sp["Wc"],
-                       p["a2v_attn.in_proj_bias"][:d], p["v2a_attn.in_proj_bias"][d:], a_s, a, q2, kv1, e(0, vd),
-                       sp["Wv"], p["v_in_proj.bias"], sp["Wq1"], p["v2a_attn.in_proj_bias"][:d], e(0, d), e(0, d))
-        return None
-    sp = ctx.planes
-    af, a_s, a, q2, kv1 = sv["af"], sv["a_s"], sv["a"], sv["q2"], sv["kv1"]
     dp_attn = cfg.attn_dropout if training else 0.0
     dp_path = cfg.drop_path if training else 0.0
     dp_mlp = cfg.mlp_dropout if training else 0.0
-    dp_prior = cfg.prior_dropout if (training and cfg.use_prior) else 0.0
     site_prior, site_v2a, site_vpath, site_a2v, site_apath, site_mlp = sites
+    dp_prior = cfg.prior_dropout if (training and cfg.use_prior) else 0.0
     seed = rng if (training and rng is not None) else None
     if training and (dp_attn > 0 or dp_path > 0 or dp_mlp > 0 or dp_prior > 0) and seed is None:
         raise ValueError("train-mode dropout needs the step's RNG base")
+    sp = planes_for(p)
+    sp.refresh(transposed=training)  # a training forward is followed by the fused backward
+    ctx.planes_gen = sp.gen
+    ctx.planes = sp  # a captured graph writes through sp's descriptors: keep them alive as long as the context
     vf = v_feat.reshape(B * T, vd).contiguous()
+    af = a_seq.reshape(B * Ta, sd).contiguous()
+    a_s, a, q2, kv1 = e(B * Ta, d), e(B * Ta, d), e(B * Ta, d), e(B * Ta, 2 * d)
     v, q1, o1 = e(B * T, d), e(B * T, d), e(B * T, d)
-    # "all": ONE F1 launch (audio blocks + trailing video blocks); "video": the video blocks alone
-    aud = af if phase == "all" else af[:0]
-    K.xh_audio_fwd(aud, sp["Ws"], p["audio_seq_proj.bias"], sp["Wa"], p["a_in_proj.bias"], sp["Wc"],
-                   p["a2v_attn.in_proj_bias"][:d], p["v2a_attn.in_proj_bias"][d:], a_s[:aud.shape[0]],
-                   a[:aud.shape[0]], q2[:aud.shape[0]], kv1[:aud.shape[0]], vf, sp["Wv"], p["v_in_proj.bias"],
-                   sp["Wq1"], p["v2a_attn.in_proj_bias"][:d], v, q1)
+    K.xh_audio_fwd(af, sp["Ws"], p["audio_seq_proj.bias"], sp["Wa"], p["a_in_proj.bias"], sp["Wc"],
+                   p["a2v_attn.in_proj_bias"][:d], p["v2a_attn.in_proj_bias"][d:], a_s, a, q2, kv1, vf, sp["Wv"],
+                   p["v_in_proj.bias"], sp["Wq1"], p["v2a_attn.in_proj_bias"][:d], v, q1)
+    sv = ctx.saved
     v2a_bias = a2v_bias = None
     if cfg.use_prior:  # the emotion-prior attention biases from the pre-attention tokens (fusion.py:390-391)
         from .xattn_head import linear_runner, prior_forward
@@ -251,17 +233,9 @@ def _splits(M: int) -> int:
     return max(1, min(-(-M // WGRAD_ROWS), 64))
 
 
-def fused_backward(p, ctx, dlogits, grads, need_dv_feat=True, phase: str = "all"):
+def fused_backward(p, ctx, dlogits, grads, need_dv_feat=True):
     """The fused backward (csrc/xattn_fused_bwd.hip) of a fused-forward context: the gradients head_backward
-    would write (accumulated into ``grads``), returns dv_feat [B, T, vd] (or None).
-
-    ``phase``: "all"; "critical" -- G4, G3, G2 (+ the prior's backward) and G1's video rows: everything the
-    frame trunk's backward waits for, returns dv_feat; "deferred" -- G1's audio chain and the grouped weight
-    gradients of every head Linear / LayerNorm, on a context whose critical phase has run (its intermediates
-    are kept in ``ctx.bwd_state``), returns None.  The audio-first schedule runs the deferred phase on a side
-    stream beside the trunk backward.  Same kernels, same arithmetic: the split changes no result."""
-    if phase == "deferred":
-        return _backward_deferred(ctx, grads, **ctx.bwd_state)
+    would write (accumulated into ``grads``), returns dv_feat [B, T, vd] (or None)."""
     cfg = ctx.cfg
     sv = ctx.saved
     B, T, Ta, d, H = ctx.dims
@@ -312,27 +286,7 @@ def fused_backward(p, ctx, dlogits, grads, need_dv_feat=True, phase: str = "all"
         from .xattn_head import prior_backward
         prior_backward(p, sv, dbias_v2a, dbias_a2v, dv, da, grads, B, T, Ta, ctx.drops[3], rng)
     da_s = e(B * Ta, d)
-    if phase == "all":
-        K.xh_audio_bwd(dqkv, sp["WcT"], sp["WaT"], da, da_s, dq1, sp["WqT1"], sp["WvT"], dv, dvfeat)
-    else:  # the video rows alone (the audio blocks of the same kernel run in the deferred phase)
-        K.xh_audio_bwd(dqkv[:0], sp["WcT"], sp["WaT"], da[:0], da_s[:0], dq1, sp["WqT1"], sp["WvT"], dv, dvfeat)
-    st = dict(sp=sp, da=da, da_s=da_s, dqkv=dqkv, da2=da2, dkv2=dkv2, dv2=dv2, dq1=dq1, dv=dv, lnp_a=lnp_a,
-              lnp_v=lnp_v, head_w=head_w)
-    if phase == "critical":
-        ctx.bwd_state = st
-    else:
-        _backward_deferred(ctx, grads, audio_rows=False, **st)
-    return dvfeat.view(B, T, -1) if dvfeat is not None else None
-
-
-def _backward_deferred(ctx, grads, sp, da, da_s, dqkv, da2, dkv2, dv2, dq1, dv, lnp_a, lnp_v, head_w,
-                       audio_rows=True):
-    """G1's audio rows (``audio_rows``) and the grouped weight-gradient launch + fold."""
-    sv = ctx.saved
-    B, T, Ta, d, H = ctx.dims
-    if audio_rows:
-        K.xh_audio_bwd(dqkv, sp["WcT"], sp["WaT"], da, da_s, dq1[:0], sp["WqT1"], sp["WvT"], dv[:0], None)
-    vf = sv["vf"]
+    K.xh_audio_bwd(dqkv, sp["WcT"], sp["WaT"], da, da_s, dq1, sp["WqT1"], sp["WvT"], dv, dvfeat)
     gw1, gb1 = grads["v2a_attn.in_proj_weight"], grads["v2a_attn.in_proj_bias"]
     gw2, gb2 = grads["a2v_attn.in_proj_weight"], grads["a2v_attn.in_proj_bias"]
     Ma, Mv, af = B * Ta, B * T, sv["af"]
@@ -351,5 +305,6 @@ def _backward_deferred(ctx, grads, sp, da, da_s, dqkv, da2, dkv2, dv2, dq1, dv, 
                           (lnp_v[:, :d], None, None, grads["v_norm.weight"]),
                           (lnp_v[:, d:], None, None, grads["v_norm.bias"])) + head_w:
         W.add(dY, X, dW, db, _splits(dY.shape[0]))
-    ws = torch.empty(W.ws_floats(), device=da.device, dtype=torch.float32)
+    ws = e(W.ws_floats())
     W.run(ws)
+    return dvfeat.view(B, T, -1) if dvfeat is not None else None

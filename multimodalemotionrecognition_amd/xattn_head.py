@@ -71,14 +71,15 @@ def head_forward(p: Dict[str, torch.Tensor], cfg: HeadConfig, v_feat: torch.Tens
                  training: bool, rng: Optional[torch.Tensor] = None, qlin: Optional[dict] = None):
     """Returns (logits [B, C], ctx).  ``rng``: the step's device RNG base (training dropout), ``qlin``: INT8
     images of the plain Linears (inference only)."""
-    if XF.supported(cfg, p, v_feat, a_seq, qlin):  # four fused launches (csrc/xattn_fused.hip)
-        ctx = head_forward_audio(p, cfg, a_seq, training, v_feat.shape[1], phase="all")
-        return head_forward_video(p, cfg, v_feat, a_seq, training, rng, ctx, phase="all"), ctx
     B, T, vd = v_feat.shape
     _, Ta, sd = a_seq.shape
     d = p["v_in_proj.weight"].shape[0]
     H = cfg.num_heads
     ctx = HeadCtx(dims=(B, T, Ta, d, H), rng=rng, training=training)
+    if XF.supported(cfg, p, v_feat, a_seq, qlin):  # four fused launches (csrc/xattn_fused.hip)
+        logits = XF.fused_forward(p, cfg, v_feat, a_seq, training, rng, ctx,
+                                  (SITE_PRIOR, SITE_V2A, SITE_VPATH, SITE_A2V, SITE_APATH, SITE_MLP))
+        return logits, ctx
     sv = ctx.saved
     dp_attn = cfg.attn_dropout if training else 0.0
     dp_path = cfg.drop_path if training else 0.0
@@ -160,41 +161,16 @@ def head_forward(p: Dict[str, torch.Tensor], cfg: HeadConfig, v_feat: torch.Tens
     return logits, ctx
 
 
-def head_forward_audio(p: Dict[str, torch.Tensor], cfg: HeadConfig, a_seq: torch.Tensor, training: bool, T: int,
-                       phase: str = "audio") -> HeadCtx:
-    """The fused head's audio phase (xattn_fused.fused_forward phase "audio": the weight split + F1's audio
-    chain) on a fresh context; ``phase="all"`` only creates the context (head_forward runs both phases in one)."""
-    B, Ta, _ = a_seq.shape
-    ctx = HeadCtx(dims=(B, T, Ta, p["v_in_proj.weight"].shape[0], cfg.num_heads), rng=None, training=training)
-    if phase == "audio":
-        XF.fused_forward(p, cfg, None, a_seq, training, None, ctx, _SITES, phase="audio")
-    return ctx
-
-
-def head_forward_video(p: Dict[str, torch.Tensor], cfg: HeadConfig, v_feat: torch.Tensor, a_seq: torch.Tensor,
-                       training: bool, rng: Optional[torch.Tensor], ctx: HeadCtx, phase: str = "video"):
-    """The rest of the fused forward on ``ctx`` (phase "video" after head_forward_audio, or "all"): logits."""
-    ctx.rng = rng
-    return XF.fused_forward(p, cfg, v_feat, a_seq, training, rng, ctx, _SITES, phase=phase)
-
-
-_SITES = (SITE_PRIOR, SITE_V2A, SITE_VPATH, SITE_A2V, SITE_APATH, SITE_MLP)
-
-
 def head_backward(p: Dict[str, torch.Tensor], ctx: HeadCtx, dlogits: torch.Tensor, grads: Dict[str, torch.Tensor],
-                  need_dv_feat: bool = True, need_da_seq: bool = False, fused: Optional[bool] = None,
-                  phase: str = "all"):
+                  need_dv_feat: bool = True, need_da_seq: bool = False, fused: Optional[bool] = None):
     """Reverse schedule.  ``grads[name]`` must be zero-initialised fp32 buffers (accumulated into).
 
     A context from the fused forward takes the fused backward (xattn_fused.fused_backward) unless ``fused`` is
-    False; the unfused schedule below reads the same saved activations.  ``phase`` ("critical" / "deferred",
-    fused backward only): the two halves of the audio-first schedule (xattn_fused.fused_backward).
+    False; the unfused schedule below reads the same saved activations.
     Returns (dv_feat [B,T,vd] fp32 or None, da_seq or None).
     """
     if fused is not False and XF.backward_supported(ctx, p, need_da_seq):
-        return XF.fused_backward(p, ctx, dlogits, grads, need_dv_feat, phase=phase), None
-    if phase != "all":
-        raise ValueError("the critical / deferred backward phases exist for the fused head only")
+        return XF.fused_backward(p, ctx, dlogits, grads, need_dv_feat), None
     cfg: HeadConfig = ctx.cfg
     sv = ctx.saved
     B, T, Ta, d, H = ctx.dims

@@ -18,5 +18,5 @@ grep '^{' $OUT/bench.log | python -c "
 import json,sys
 for l in sys.stdin:
     d=json.loads(l); h=d.get('roofline_head') or {}
-    print('BENCH', d['value'], d['ms_per_step'], d.get('ms_per_step_median'), 'head', {k: h.get(k) for k in ('frac','fwd_ms','bwd_ms','side_fwd_ms','side_bwd_ms','ms_per_step')})"
+    print('BENCH', d['value'], d['ms_per_step'], d.get('ms_per_step_median'), 'head', {k: h.get(k) for k in ('frac','fwd_ms','bwd_ms','ms_per_step')}, 'core', (h.get('core') or {}).get('kernel_ms'), (h.get('core') or {}).get('frac'))"
 exit $rc
