@@ -51,7 +51,7 @@ PEAK_HBM_GBS = 8000.0       # HBM3E spec
 PROBE = ("gemm_bf16", (BATCH * 4799, 512, 1536))
 # the kernel mer_gemm_bf16 dispatches for that shape (gemm_bf16.hip pick_variant: 1,200 tiles of 256x256,
 # 16 waves each)
-PROBE_KERNEL = "gemm_pipe_kernel<PipeCfg<256,256,4,4,2,64>, bf16>"
+PROBE_KERNEL = "gemm_pipe_kernel<PipeCfg<256,256,4,4,2,64,3>, bf16>"
 PMC_FILE = ROOT / "profiles" / "pmc_traffic.json"
 PMC_HEAD_FILE = ROOT / "profiles" / "pmc_traffic_head.json"  # tools/pmc_head.py summarize (fused head fwd + bwd)
 # Algorithmic work per clip: ResNet18 fwd+bwd over 8 frames 22.8 GFLOP, head fwd+bwd 0.141, WavLM

@@ -191,7 +191,8 @@ int mer_gemm_bf16(int M, int N, int K, const void* A, long a_gstride, long a_rst
  * register-staged kernel (any K % 8 == 0), 1/2/3 the global_load_lds pipelined kernel with 256x256 /
  * 256x128 / 128x128 tiles and a 2-deep LDS ring, 4/5 128x128 with a 3/4-deep ring, 6 256x128 3-deep,
  * 7 128x64 3-deep, 8 128x64 2-deep, 9/10 128x128 with 8 waves 2/3-deep, 11 128x64 as 4x1 waves 3-deep,
- * 12 256x128 with 16 waves, 13 256x256 with 16 waves
+ * 12 256x128 with 16 waves, 13 256x256 with 16 waves, 14 256x256 phase-interleaved, 15/16/17 32-wide K-tiles on
+ * 4-deep rings (256x256 / 128x64 / 128x128), 18/19 256x256 with 16 / 8 waves on split rings (A 3-deep, B 2-deep)
  * (K % 64 == 0; otherwise variant 0 runs). */
 int mer_gemm_bf16_ex(int M, int N, int K, const void* A, long a_gstride, long a_rstride, int a_rpg, const void* W,
                      long ldw, void* C, int c_dtype, long ldc, const float* bias, const void* R, long ldr, int act,

@@ -204,10 +204,14 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs g) {
 // glds writes lane-linear (base + 16*lane), so the XOR goes on each lane's SOURCE address and on
 // the fragment read (rule 21: both sides).  Rows past M/N are clamped to the last valid row (their
 // outputs are discarded); K is a multiple of 64, so no K tail.
-template <int BM_, int BN_, int WM_, int WN_, int STAGES_ = 2, int KS_ = 64>
+template <int BM_, int BN_, int WM_, int WN_, int STAGES_ = 2, int KS_ = 64, int SA_ = 0>
 struct PipeCfg {
   static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_;       // tile, waves along M / N
   static constexpr int STAGES = STAGES_;                            // LDS ring depth (K-tiles)
+  // SA > 0: the A operand gets its own, deeper ring (SA = 3 with a 2-deep B ring): A is the HBM stream of the
+  // conv-as-GEMMs (B, the weights, stays L2-resident), so A tiles are issued two K-steps ahead, B tiles one
+  static constexpr int SA = SA_ > 0 ? SA_ : STAGES_, SB = STAGES_;
+  static constexpr int LDS_ELEMS = SA * BM * KS_ + SB * BN * KS_;   // bf16 elements of the whole ring
   static constexpr int KS = KS_;                                    // K-tile width (64, or 32 for deep rings)
   static constexpr int CW = KS / 8, RPG = 64 / CW;                  // 16-byte chunks per LDS row, rows per glds
   static constexpr int WAVES = WM * WN, NT = 64 * WAVES;
@@ -276,9 +280,7 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_pipe_kernel(GemmArgs g) {
     pb[j] = Bz + (long)n * g.ldb + swz_k<CF::CW>(r, lchunk) * 8;
   }
   const float inv_cg = AMODE == 1 ? 1.f / g.pc_cg : 0.f;
-  auto stage = [&](int buf, int k0) {
-    bf16_t* la = smem + buf * CF::BUF;
-    bf16_t* lb = la + CF::BM * CF::KS;
+  auto stage_a = [&](bf16_t* la, int k0) {
 #pragma unroll
     for (int j = 0; j < CF::IA; ++j) {
       if (AMODE == 0) {
@@ -292,9 +294,16 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_pipe_kernel(GemmArgs g) {
                la + (w * CF::IA + j) * 512);
       }
     }
+  };
+  auto stage_b = [&](bf16_t* lb, int k0) {
 #pragma unroll
     for (int j = 0; j < CF::IB; ++j)
       glds16(pb[j] + k0, lb + (w * CF::IB + j) * 512);
+  };
+  auto stage = [&](int buf, int k0) {
+    bf16_t* la = smem + buf * CF::BUF;
+    stage_a(la, k0);
+    stage_b(la + CF::BM * CF::KS, k0);
   };
 
   f32x4 acc[CF::FM][CF::FN];
@@ -311,18 +320,44 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_pipe_kernel(GemmArgs g) {
   // Ring of S LDS buffers: tiles kt+1 .. kt+S-2 stay in flight (counted vmcnt) across the barrier
   // that publishes tile kt; the barrier also retires every wave's reads of tile kt-1, whose buffer
   // the tile kt+S-1 DMA then reuses.  Raw s_barrier: __syncthreads() would drain vmcnt to 0.
+  // split rings (SA = 3, SB = 2): A tiles at smem + (k % 3) * BM*KS, B tiles after the A ring at (k % 2) * BN*KS.
+  // Issue order: prologue A(0) B(0) A(1); step kt issues B(kt+1) then A(kt+2), so when step kt starts the
+  // youngest group is A(kt+1), issued after B(kt): vmcnt(IA) leaves exactly it in flight.  A(kt+2) reuses the
+  // buffer of A(kt-1) and B(kt+1) that of B(kt-1), both read in step kt-1, before this step's barrier.
+  constexpr bool SPLIT = CF::SA != CF::SB;
+  static_assert(!SPLIT || (CF::SA == 3 && CF::SB == 2), "split ring: SA = 3, SB = 2");
+  bf16_t* const ring_b = smem + CF::SA * CF::BM * CF::KS;
+  if constexpr (SPLIT) {
+    stage_a(smem, ktile_off_k<CF::KS>(g, 0));
+    stage_b(ring_b, ktile_off_k<CF::KS>(g, 0));
+    if (nk > 1) stage_a(smem + CF::BM * CF::KS, ktile_off_k<CF::KS>(g, 1));
+  } else {
 #pragma unroll
-  for (int p = 0; p < S - 1; ++p)
-    if (p < nk) stage(p, ktile_off_k<CF::KS>(g, p));
+    for (int p = 0; p < S - 1; ++p)
+      if (p < nk) stage(p, ktile_off_k<CF::KS>(g, p));
+  }
   for (int kt = 0; kt < nk; ++kt) {
-    const int ahead = (nk - 1 - kt) < (S - 2) ? (nk - 1 - kt) : (S - 2);
-    wait_tiles_in_flight<G>(ahead);
+    if constexpr (SPLIT) {
+      if (kt + 1 < nk) wait_vmcnt<CF::IA>(); else wait_vmcnt<0>();
+    } else {
+      const int ahead = (nk - 1 - kt) < (S - 2) ? (nk - 1 - kt) : (S - 2);
+      wait_tiles_in_flight<G>(ahead);
+    }
     __builtin_amdgcn_s_waitcnt((15) | (7 << 4) | (0 << 8) | (3 << 14));  // lgkmcnt(0) only
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    if (kt + S - 1 < nk) stage((kt + S - 1) % S, ktile_off_k<CF::KS>(g, kt + S - 1));
-    const bf16_t* la = smem + (kt % S) * CF::BUF;
-    const bf16_t* lb = la + CF::BM * CF::KS;
+    const bf16_t* la;
+    const bf16_t* lb;
+    if constexpr (SPLIT) {
+      if (kt + 1 < nk) stage_b(ring_b + ((kt + 1) & 1) * CF::BN * CF::KS, ktile_off_k<CF::KS>(g, kt + 1));
+      if (kt + 2 < nk) stage_a(smem + ((kt + 2) % 3) * CF::BM * CF::KS, ktile_off_k<CF::KS>(g, kt + 2));
+      la = smem + (kt % 3) * CF::BM * CF::KS;
+      lb = ring_b + (kt & 1) * CF::BN * CF::KS;
+    } else {
+      if (kt + S - 1 < nk) stage((kt + S - 1) % S, ktile_off_k<CF::KS>(g, kt + S - 1));
+      la = smem + (kt % S) * CF::BUF;
+      lb = la + CF::BM * CF::KS;
+    }
 #pragma unroll
     for (int s = 0; s < CF::KS / 32; ++s) {
       bf16x8 af[CF::FM], bfr[CF::FN];
@@ -356,7 +391,7 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_pipe_kernel(GemmArgs g) {
     // stores instead of one 2- or 4-byte access per accumulator element.  Same arithmetic and rounding as
     // the direct path below.
     constexpr int LDT = CF::TN + 4;
-    constexpr int WAVE_FLOATS = CF::STAGES * CF::BUF / 2 / CF::WAVES;  // bf16 ring elements / 2 = floats
+    constexpr int WAVE_FLOATS = CF::LDS_ELEMS / 2 / CF::WAVES;  // bf16 ring elements / 2 = floats
     constexpr int GI0 = WAVE_FLOATS / (16 * LDT);
     constexpr int GI = GI0 < CF::FM ? GI0 : CF::FM;
     static_assert(GI >= 1, "epilogue staging slice too small");
@@ -630,11 +665,13 @@ using CfgY2 = PipeCfg<256, 256, 4, 4, 2>;  // 16 waves (64x64 each), 2-deep, 128
 using CfgY4 = PipeCfg<256, 256, 4, 4, 4, 32>;  // 16 waves, 32-wide K-tiles on a 4-deep ring, 128 KiB LDS
 using CfgT4 = PipeCfg<128, 64, 2, 2, 4, 32>;   // 128x64 tiles, 32-wide K on a 4-deep ring, 48 KiB LDS
 using CfgW4 = PipeCfg<128, 128, 2, 4, 4, 32>;  // 8 waves, 32-wide K on a 4-deep ring, 64 KiB LDS
+using CfgY32 = PipeCfg<256, 256, 4, 4, 2, 64, 3>;  // 16 waves, A 3-deep + B 2-deep rings, 160 KiB LDS
+using CfgL32 = PipeCfg<256, 256, 2, 4, 2, 64, 3>;  // 8 waves (128x64 each), A 3-deep + B 2-deep, 160 KiB LDS
 
 template <class CF, typename TOUT, int AMODE>
 int launch_pipe_t(const GemmArgs& g, int groups, hipStream_t st) {
   const long tiles = (long)((g.N + CF::BN - 1) / CF::BN) * ((g.M + CF::BM - 1) / CF::BM);
-  const size_t lds = CF::STAGES * CF::BUF * sizeof(bf16_t);
+  const size_t lds = CF::LDS_ELEMS * sizeof(bf16_t);
   if (hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_pipe_kernel<CF, TOUT, AMODE>),
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return (int)hipErrorInvalidConfiguration;
@@ -655,8 +692,12 @@ int launch_pipe(const GemmArgs& g, int out_dtype, hipStream_t st, int groups = 1
 // projection 128x128 tiles with 8 waves.  The 512-column feature-extractor convs below conv1 (300-600 such tiles,
 // 1.2-2.3 rounds of the 256 CUs) run faster on 128x128 tiles: conv2 134 -> 130 us, conv3 79 -> 69 us
 // (profiles/r02f/bench_gemm_convs.log; all variants bit-identical).
+// conv1 (1,200 tiles streaming a 314 MB A operand) takes the split ring (A three K-tiles deep, B two):
+// 278.6 -> 271.4 us; the same ring is 2-7 % slower on conv2 / conv3 / QKV / FFN-up / 4096^3
+// (profiles/r04/gemm_split_ring.log, all bit-identical).
 int pick_variant(int M, int N, int K) {
   const long tl = (long)((M + 255) / 256) * ((N + 255) / 256);
+  if (tl >= 1200 && N <= 512) return 18;
   if (tl >= 160 && !(N <= 512 && tl < 1200)) return 13;
   return K >= 2048 ? 7 : 9;
 }
@@ -717,7 +758,7 @@ MER_API int mer_gemm_bf16_tr(int M, int N, int K, const void* A, long a_gstride,
   if (M <= 0 || N <= 0) return 0;
   if (drop_p < 0.f || drop_p >= 1.f || (drop_p > 0.f && !drop_seed) || skip_bit < 0 || skip_bit > 62)
     return (int)hipErrorInvalidValue;
-  if (variant < -1 || variant > 17) return (int)hipErrorInvalidValue;
+  if (variant < -1 || variant > 19) return (int)hipErrorInvalidValue;
   if (K % 8 != 0 || a_rpg <= 0 || (a_rstride % 8) != 0 || (a_gstride % 8) != 0 || (ldw % 8) != 0)
     return (int)hipErrorInvalidValue;
   if ((((uintptr_t)A) | ((uintptr_t)W)) & 15) return (int)hipErrorInvalidValue;
@@ -763,6 +804,8 @@ MER_API int mer_gemm_bf16_tr(int M, int N, int K, const void* A, long a_gstride,
     case 15: return launch_pipe<CfgY4>(g, c_dtype, st);
     case 16: return launch_pipe<CfgT4>(g, c_dtype, st);
     case 17: return launch_pipe<CfgW4>(g, c_dtype, st);
+    case 18: return launch_pipe<CfgY32>(g, c_dtype, st);
+    case 19: return launch_pipe<CfgL32>(g, c_dtype, st);
     default: return launch<0>(g, c_dtype, 1, st);
   }
 }
