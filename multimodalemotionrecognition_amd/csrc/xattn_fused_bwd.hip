@@ -686,13 +686,16 @@ MER_API int mer_xh_audio_bwd(int M, const float* dqkv, const void* WcT_hi, const
 
 // ---------------------------------------------------------------------------------------------
 // W: grouped weight gradients.  Problem p: dW[n][k] (+)= sum_m dY[m][n] X[m][k] and db[n] (+)= sum_m dY[m][n]
-// (K = 0: a column-sum-only problem, the LayerNorm dgamma / dbeta partials).  Blocks = (problem, 64 x 64
+// (K = 0: a column-sum-only problem, the LayerNorm dgamma / dbeta partials).  Blocks = (problem, 128 x 128
 // output tile, row split); each writes its partial tile to ws, the bias partials (k-tile 0 blocks) after it;
 // xh_wfold adds the partials in split order.  The table travels by value in the kernel arguments, so a
-// captured graph holds it (no device table to upload).
+// captured graph holds it (no device table to upload).  128 x 128 tiles cover the head's 128 / 256-wide
+// Linears with one or two tiles, so each dY / X column block is read once per tile instead of once per 64-wide
+// tile of the other operand (the 64 x 64 version re-read dY 12x for audio_seq_proj: 97 MB per step).
 // ---------------------------------------------------------------------------------------------
 constexpr int WG_MAXP = 20;
 constexpr int WG_HOST_COLS = 11;  // dY ldy X ldx x_dtype M N K splits dW db
+constexpr int WG_T = 128;         // output tile (n and k)
 
 struct WgProb {
   const float* dY;
@@ -708,28 +711,28 @@ struct WgTab {
   int nprob;
 };
 
-// Staging: thread t owns column (t & 63) of the 64-wide dY / X tile and 8 consecutive rows (t >> 6) * 8 .. + 7 of
-// the 32-row chunk: 8 wave-coalesced loads each, split into bf16 hi / lo once and stored as ONE 16-byte LDS
-// vector per plane in [column][row] layout, which is exactly the MFMA fragment (8 consecutive m of one n / k).
-// The next chunk's loads are issued before the current chunk's MFMAs.
-constexpr int WG_LDM = 32 + 8;  // bf16 row stride of the [64][32] planes (80 bytes: 16-byte aligned)
+// Staging: thread t owns column (t & 127) of the 128-wide dY / X tile and 16 consecutive rows (t >> 7) * 16 ..
+// + 15 of the 32-row chunk: 16 wave-coalesced loads per operand, split into bf16 hi / lo once and stored as two
+// 16-byte LDS vectors per plane in [column][row] layout, which is exactly the MFMA fragment (8 consecutive m of
+// one n / k).  The next chunk's loads are issued before the current chunk's MFMAs.
+constexpr int WG_LDM = 32 + 8;  // bf16 row stride of the [128][32] planes (80 bytes: 16-byte aligned)
 
 struct WgChunk {
-  float y[8], x[8];
+  float y[16], x[16];
 };
 
 __device__ __forceinline__ void wg_load(const WgProb& d, long mc, long m1, int n0, int k0, WgChunk& c) {
   // Branch-free (see mm_aw): unconditional loads from clamped addresses (row m1 - 1, column N - 1 / K - 1),
   // zeroed by selects; X is read as 32-bit words whatever its dtype (a bf16 element is one half of its word),
   // and a K = 0 problem reads a valid dummy X (the host points X at dY).
-  const int col = threadIdx.x & 63, m8 = (threadIdx.x >> 6) * 8;
+  const int col = threadIdx.x & 127, m16 = (threadIdx.x >> 7) * 16;
   const bool okn = n0 + col < d.N, okk = k0 + col < d.K;
   const int nc = okn ? n0 + col : d.N - 1, kc = okk ? k0 + col : (d.K > 0 ? d.K - 1 : 0);
   const int esz = d.xbf ? 2 : 4;
   const char* Xb = reinterpret_cast<const char*>(d.X);
 #pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const long m = mc + m8 + e;
+  for (int e = 0; e < 16; ++e) {
+    const long m = mc + m16 + e;
     const bool okm = m < m1;
     const long mm = okm ? m : m1 - 1;
     const float y = d.dY[mm * d.ldy + nc];
@@ -742,85 +745,93 @@ __device__ __forceinline__ void wg_load(const WgProb& d, long mc, long m1, int n
   }
 }
 
+__device__ __forceinline__ void wg_store_planes(const float (&v)[16], bf16_t* hi, bf16_t* lo) {
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    Frag H, L;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const uint16_t hb = f2bf(v[8 * half + e]);
+      H.h[e] = hb;
+      L.h[e] = f2bf(v[8 * half + e] - bf2f(hb));
+    }
+    *reinterpret_cast<u4*>(hi + 8 * half) = H.u;
+    *reinterpret_cast<u4*>(lo + 8 * half) = L.u;
+  }
+}
+
 __global__ __launch_bounds__(256) void xh_wgrad_kernel(const WgTab tab, float* __restrict__ ws) {
-  __shared__ __attribute__((aligned(16))) bf16_t yh[64 * WG_LDM], yl[64 * WG_LDM], xh_[64 * WG_LDM], xl[64 * WG_LDM];
-  __shared__ float bred[4][64];
+  __shared__ __attribute__((aligned(16))) bf16_t yh[WG_T * WG_LDM], yl[WG_T * WG_LDM], xh_[WG_T * WG_LDM],
+      xl[WG_T * WG_LDM];
+  __shared__ float bred[2][WG_T];
   int pi = 0;
   while (pi + 1 < tab.nprob && tab.p[pi + 1].first_block <= (int)blockIdx.x) ++pi;
   const WgProb& d = tab.p[pi];
   const int N = d.N, K = d.K, splits = d.splits;
-  const int ntk = K > 0 ? (K + 63) / 64 : 1;
+  const int ntk = K > 0 ? (K + WG_T - 1) / WG_T : 1;
   const int local = blockIdx.x - d.first_block;
   const int split = local % splits, tile = local / splits;
   const int tn = tile / ntk, tk = tile - tn * ntk;
-  const int n0 = tn * 64, k0 = tk * 64;
+  const int n0 = tn * WG_T, k0 = tk * WG_T;
   const long per = (d.M + splits - 1) / splits, m0 = split * per, m1 = m0 + per < d.M ? m0 + per : d.M;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, fr = lane & 15, fk = (lane >> 4) * 8;
-  const int col = lane, m8 = w * 8;
+  const int wn = w >> 1, wk = w & 1;  // this wave's 64 x 64 quadrant of the tile
+  const int col = threadIdx.x & 127, m16 = (threadIdx.x >> 7) * 16;
   const bool bias = d.db != nullptr && tk == 0;
-  f32x4 acc[4];
+  f32x4 acc[4][4];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   float bsum = 0.f;  // column n0 + col, this thread's rows
   WgChunk cur;
   wg_load(d, m0, m1, n0, k0, cur);
   for (long mc = m0; mc < m1; mc += 32) {
     __syncthreads();  // the previous chunk's fragments are read
-    {
-      Frag H, L;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        bsum += cur.y[e];
-        const uint16_t hb = f2bf(cur.y[e]);
-        H.h[e] = hb;
-        L.h[e] = f2bf(cur.y[e] - bf2f(hb));
-      }
-      *reinterpret_cast<u4*>(yh + col * WG_LDM + m8) = H.u;
-      *reinterpret_cast<u4*>(yl + col * WG_LDM + m8) = L.u;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const uint16_t hb = f2bf(cur.x[e]);
-        H.h[e] = hb;
-        L.h[e] = f2bf(cur.x[e] - bf2f(hb));
-      }
-      *reinterpret_cast<u4*>(xh_ + col * WG_LDM + m8) = H.u;
-      *reinterpret_cast<u4*>(xl + col * WG_LDM + m8) = L.u;
-    }
+    for (int e = 0; e < 16; ++e) bsum += cur.y[e];
+    wg_store_planes(cur.y, yh + col * WG_LDM + m16, yl + col * WG_LDM + m16);
+    wg_store_planes(cur.x, xh_ + col * WG_LDM + m16, xl + col * WG_LDM + m16);
     __syncthreads();
     // the next chunk's loads are in flight during the MFMAs (unconditional: past the end it re-reads the last
     // chunk, unused); the MFMAs also run for K = 0 problems (their accumulators are never stored)
     wg_load(d, mc + 32 < m1 ? mc + 32 : mc, m1, n0, k0, cur);
-    {
-      Frag AH, AL;
-      AH.u = *reinterpret_cast<const u4*>(yh + (16 * w + fr) * WG_LDM + fk);  // A[n][m] = dY[m][n]
-      AL.u = *reinterpret_cast<const u4*>(yl + (16 * w + fr) * WG_LDM + fk);
+    Frag BH[4], BL[4];  // B[k][m] = X[m][k]; the lo plane of bf16 X is zero
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      BH[j].u = *reinterpret_cast<const u4*>(xh_ + (64 * wk + 16 * j + fr) * WG_LDM + fk);
+      BL[j].u = *reinterpret_cast<const u4*>(xl + (64 * wk + 16 * j + fr) * WG_LDM + fk);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      Frag AH, AL;  // A[n][m] = dY[m][n]
+      AH.u = *reinterpret_cast<const u4*>(yh + (64 * wn + 16 * i + fr) * WG_LDM + fk);
+      AL.u = *reinterpret_cast<const u4*>(yl + (64 * wn + 16 * i + fr) * WG_LDM + fk);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        Frag BH, BL;  // B[k][m] = X[m][k]; the lo plane of bf16 X is zero
-        BH.u = *reinterpret_cast<const u4*>(xh_ + (16 * j + fr) * WG_LDM + fk);
-        BL.u = *reinterpret_cast<const u4*>(xl + (16 * j + fr) * WG_LDM + fk);
-        acc[j] = mma(AH.v, BH.v, acc[j]);
-        acc[j] = mma(AL.v, BH.v, acc[j]);
-        acc[j] = mma(AH.v, BL.v, acc[j]);
+        acc[i][j] = mma(AH.v, BH[j].v, acc[i][j]);
+        acc[i][j] = mma(AL.v, BH[j].v, acc[i][j]);
+        acc[i][j] = mma(AH.v, BL[j].v, acc[i][j]);
       }
     }
   }
   if (K > 0) {
     float* out = ws + d.ws_off + (long)split * N * K;
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int n = n0 + 16 * w + 4 * (lane >> 4) + r, k = k0 + 16 * j + fr;
-        if (n < N && k < K) out[(long)n * K + k] = acc[j][r];
-      }
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int n = n0 + 64 * wn + 16 * i + 4 * (lane >> 4) + r, k = k0 + 64 * wk + 16 * j + fr;
+          if (n < N && k < K) out[(long)n * K + k] = acc[i][j][r];
+        }
   }
   if (bias) {
-    bred[w][col] = bsum;
+    bred[threadIdx.x >> 7][col] = bsum;
     __syncthreads();
-    if (threadIdx.x < 64 && n0 + (int)threadIdx.x < N)
-      ws[d.ws_b_off + (long)split * N + n0 + threadIdx.x] =
-          ((bred[0][threadIdx.x] + bred[1][threadIdx.x]) + bred[2][threadIdx.x]) + bred[3][threadIdx.x];
+    if (threadIdx.x < WG_T && n0 + (int)threadIdx.x < N)
+      ws[d.ws_b_off + (long)split * N + n0 + threadIdx.x] = bred[0][threadIdx.x] + bred[1][threadIdx.x];
   }
 }
 
@@ -883,7 +894,7 @@ static long long wg_layout(int nprob, const long long* t, WgTab* tab, int* block
     p.ws_b_off = off;
     if (p.db) off += (long long)p.splits * p.N;
     p.first_block = fb;
-    fb += p.splits * ((p.N + 63) / 64) * (p.K > 0 ? (p.K + 63) / 64 : 1);
+    fb += p.splits * ((p.N + WG_T - 1) / WG_T) * (p.K > 0 ? (p.K + WG_T - 1) / WG_T : 1);
   }
   tab->nprob = nprob;
   *blocks = fb;
