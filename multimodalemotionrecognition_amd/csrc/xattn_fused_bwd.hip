@@ -760,10 +760,14 @@ __device__ __forceinline__ void wg_store_planes(const float (&v)[16], bf16_t* hi
   }
 }
 
-__global__ __launch_bounds__(256) void xh_wgrad_kernel(const WgTab tab, float* __restrict__ ws) {
-  __shared__ __attribute__((aligned(16))) bf16_t yh[WG_T * WG_LDM], yl[WG_T * WG_LDM], xh_[WG_T * WG_LDM],
-      xl[WG_T * WG_LDM];
-  __shared__ float bred[2][WG_T];
+// 512 threads = two groups of 4 waves; group g takes the 32-row chunks 2i + g of the block's row range into its own
+// LDS planes and accumulators (2 waves per SIMD: twice the loads in flight of a 4-wave block), then group 1 hands
+// its 128 x 128 partial to group 0 through LDS, which adds it (fixed order) and writes the block's slab.
+constexpr int WG_PLANE = WG_T * WG_LDM;  // bf16 elements per plane
+
+__global__ __launch_bounds__(512) void xh_wgrad_kernel(const WgTab tab, float* __restrict__ ws) {
+  __shared__ __attribute__((aligned(16))) bf16_t planes[2][4][WG_PLANE];  // [group][yh, yl, xh, xl]
+  __shared__ float bred[4][WG_T];
   int pi = 0;
   while (pi + 1 < tab.nprob && tab.p[pi + 1].first_block <= (int)blockIdx.x) ++pi;
   const WgProb& d = tab.p[pi];
@@ -774,9 +778,14 @@ __global__ __launch_bounds__(256) void xh_wgrad_kernel(const WgTab tab, float* _
   const int tn = tile / ntk, tk = tile - tn * ntk;
   const int n0 = tn * WG_T, k0 = tk * WG_T;
   const long per = (d.M + splits - 1) / splits, m0 = split * per, m1 = m0 + per < d.M ? m0 + per : d.M;
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, fr = lane & 15, fk = (lane >> 4) * 8;
+  const int grp = threadIdx.x >> 8, t = threadIdx.x & 255;
+  const int w = t >> 6, lane = threadIdx.x & 63, fr = lane & 15, fk = (lane >> 4) * 8;
   const int wn = w >> 1, wk = w & 1;  // this wave's 64 x 64 quadrant of the tile
-  const int col = threadIdx.x & 127, m16 = (threadIdx.x >> 7) * 16;
+  const int col = t & 127, m16 = (t >> 7) * 16;
+  bf16_t* yh = planes[grp][0];
+  bf16_t* yl = planes[grp][1];
+  bf16_t* xh_ = planes[grp][2];
+  bf16_t* xl = planes[grp][3];
   const bool bias = d.db != nullptr && tk == 0;
   f32x4 acc[4][4];
 #pragma unroll
@@ -784,18 +793,21 @@ __global__ __launch_bounds__(256) void xh_wgrad_kernel(const WgTab tab, float* _
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   float bsum = 0.f;  // column n0 + col, this thread's rows
+  const long nchunk = (m1 - m0 + 31) / 32, iters = (nchunk + 1) / 2;
+  // chunk i of this group starts at row m0 + 32 * (2i + grp); a group past the range loads an empty range
+  // (m >= m1 everywhere: zeros), so both groups run the same iterations and barriers
+  auto chunk_row = [&](long i) { return m0 + 32 * (2 * i + grp); };
   WgChunk cur;
-  wg_load(d, m0, m1, n0, k0, cur);
-  for (long mc = m0; mc < m1; mc += 32) {
+  wg_load(d, chunk_row(0), m1, n0, k0, cur);
+  for (long it = 0; it < iters; ++it) {
     __syncthreads();  // the previous chunk's fragments are read
 #pragma unroll
     for (int e = 0; e < 16; ++e) bsum += cur.y[e];
     wg_store_planes(cur.y, yh + col * WG_LDM + m16, yl + col * WG_LDM + m16);
     wg_store_planes(cur.x, xh_ + col * WG_LDM + m16, xl + col * WG_LDM + m16);
     __syncthreads();
-    // the next chunk's loads are in flight during the MFMAs (unconditional: past the end it re-reads the last
-    // chunk, unused); the MFMAs also run for K = 0 problems (their accumulators are never stored)
-    wg_load(d, mc + 32 < m1 ? mc + 32 : mc, m1, n0, k0, cur);
+    // the next chunk's loads are in flight during the MFMAs (past the end: the current chunk again, unused)
+    wg_load(d, it + 1 < iters ? chunk_row(it + 1) : chunk_row(it), m1, n0, k0, cur);
     Frag BH[4], BL[4];  // B[k][m] = X[m][k]; the lo plane of bf16 X is zero
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -815,23 +827,34 @@ __global__ __launch_bounds__(256) void xh_wgrad_kernel(const WgTab tab, float* _
       }
     }
   }
-  if (K > 0) {
-    float* out = ws + d.ws_off + (long)split * N * K;
+  bred[grp * 2 + (t >> 7)][col] = bsum;
+  __syncthreads();  // every group is past its last fragment read: the planes take group 1's partial
+  float* xch = reinterpret_cast<float*>(&planes[0][0][0]);  // [256 lanes][64] fp32 = 64 KiB of the 80 KiB
+  if (grp == 1) {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int n = n0 + 64 * wn + 16 * i + 4 * (lane >> 4) + r, k = k0 + 64 * wk + 16 * j + fr;
-          if (n < N && k < K) out[(long)n * K + k] = acc[i][j][r];
-        }
+        *reinterpret_cast<f32x4*>(xch + ((i * 4 + j) * 256 + t) * 4) = acc[i][j];
   }
-  if (bias) {
-    bred[threadIdx.x >> 7][col] = bsum;
-    __syncthreads();
-    if (threadIdx.x < WG_T && n0 + (int)threadIdx.x < N)
-      ws[d.ws_b_off + (long)split * N + n0 + threadIdx.x] = bred[0][threadIdx.x] + bred[1][threadIdx.x];
+  __syncthreads();
+  if (grp == 0) {
+    if (K > 0) {
+      float* out = ws + d.ws_off + (long)split * N * K;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const f32x4 o = *reinterpret_cast<const f32x4*>(xch + ((i * 4 + j) * 256 + t) * 4);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int n = n0 + 64 * wn + 16 * i + 4 * (lane >> 4) + r, k = k0 + 64 * wk + 16 * j + fr;
+            if (n < N && k < K) out[(long)n * K + k] = acc[i][j][r] + o[r];
+          }
+        }
+    }
+    if (bias && t < WG_T && n0 + t < N)
+      ws[d.ws_b_off + (long)split * N + n0 + t] = (bred[0][t] + bred[1][t]) + (bred[2][t] + bred[3][t]);
   }
 }
 
@@ -925,7 +948,7 @@ MER_API int mer_xh_wgrad(int nprob, const long long* table, float* ws, long long
   int blocks = 0;
   const long long need = wg_layout(nprob, table, &tab, &blocks);
   if (need < 0 || need > ws_floats) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(xh_wgrad_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, tab, ws);
+  hipLaunchKernelGGL(xh_wgrad_kernel, dim3(blocks), dim3(512), 0, (hipStream_t)stream, tab, ws);
   // fold: one element per thread for the largest problem (each thread's split loads are one latency round, not
   // one per element it would otherwise loop over)
   long long most = 0;

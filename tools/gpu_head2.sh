@@ -6,7 +6,7 @@ OUT=$R/gpurun_out/$TAG
 mkdir -p $OUT
 timeout -k 10 600 python -u -m pytest tests/test_xattn_fused_gpu.py tests/test_head_gpu.py tests/test_graphs_gpu.py -m gpu -q -x --timeout 200 --timeout-method thread > $OUT/tests.log 2>&1 || { tail -20 $OUT/tests.log; exit 1; }
 tail -2 $OUT/tests.log
-for rows in 512 256; do
+for rows in 256 512 128; do
   MER_XH_WGRAD_ROWS=$rows timeout -k 10 200 python -u tools/bench_head.py > $OUT/head_$rows.log 2>&1 || { tail $OUT/head_$rows.log; exit 1; }
   echo "rows $rows: $(grep fused $OUT/head_$rows.log)"
 done
