@@ -725,7 +725,7 @@ __device__ __forceinline__ void wg_load(const WgProb& d, long mc, long m1, int n
   // Branch-free (see mm_aw): unconditional loads from clamped addresses (row m1 - 1, column N - 1 / K - 1),
   // zeroed by selects; X is read as 32-bit words whatever its dtype (a bf16 element is one half of its word),
   // and a K = 0 problem reads a valid dummy X (the host points X at dY).
-  const int col = threadIdx.x & 127, m16 = (threadIdx.x >> 7) * 16;
+  const int col = threadIdx.x & 127, m16 = ((threadIdx.x >> 7) & 1) * 16;  // (each 256-thread group stages a chunk)
   const bool okn = n0 + col < d.N, okk = k0 + col < d.K;
   const int nc = okn ? n0 + col : d.N - 1, kc = okk ? k0 + col : (d.K > 0 ? d.K - 1 : 0);
   const int esz = d.xbf ? 2 : 4;
