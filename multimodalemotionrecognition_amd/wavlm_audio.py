@@ -412,7 +412,10 @@ class WavLMBackbone(nn.Module):
         nl = cfg.num_hidden_layers if num_layers is None else num_layers
         qkv = torch.empty(B * L, 3 * D, device=dev, dtype=bf)
         att = torch.empty(B * L, D, device=dev, dtype=bf)
-        y32 = torch.empty(B * L, D, device=dev, dtype=torch.float32)
+        # the residual sums each post-LayerNorm normalises (x + out_proj(att), x1 + ffn): bf16, like every other
+        # activation of the encoder -- half the bytes of the fp32 sums the two GEMM epilogues used to write and the
+        # LayerNorms to read back (the statistics are taken in fp32 over the stored values)
+        y32 = torch.empty(B * L, D, device=dev, dtype=bf)
         x1 = torch.empty(B * L, D, device=dev, dtype=bf)
         ff = torch.empty(B * L, cfg.intermediate_size, device=dev, dtype=bf)
         ad, acd = (cfg.attention_dropout, cfg.activation_dropout) if tr else (0.0, 0.0)
