@@ -1535,11 +1535,23 @@ __global__ void pack_input_s2d_kernel(int N, int C, int H, int W, const float* _
     uint32_t o[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
     const int jj = j - 2, ii = i - 2;
     if (jj >= 0 && jj < H / 2 && ii >= 0 && ii < W / 2) {
-      const float* xn = x + (long)n * C * H * W;
+      // the 2x2 block's two rows of each channel as float2 loads (adjacent lanes read adjacent 8-byte pairs: one
+      // coalesced 512-byte run per wave instruction; the per-element scalar gathers ran at 1/6 of HBM speed)
+      const float* xn = x + (long)n * C * H * W + (long)(2 * jj) * W + 2 * ii;
+      float v[4][4];  // [c][dydx]
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        if (c >= C) break;
+#pragma unroll
+        for (int dy = 0; dy < 2; ++dy) {
+          const float2 q = *reinterpret_cast<const float2*>(xn + (long)c * H * W + dy * W);
+          v[c][2 * dy] = q.x;
+          v[c][2 * dy + 1] = q.y;
+        }
+      }
       for (int ch = 0; ch < 4 * C; ++ch) {
         const int dydx = ch / C, c = ch - dydx * C;
-        const float v = xn[((long)c * H + 2 * jj + (dydx >> 1)) * W + 2 * ii + (dydx & 1)];
-        o[ch >> 1] |= (uint32_t)f2bf(v) << ((ch & 1) * 16);
+        o[ch >> 1] |= (uint32_t)f2bf(v[c][dydx]) << ((ch & 1) * 16);
       }
     }
     u32x4* dst = reinterpret_cast<u32x4*>(y + p * 16);
@@ -1548,7 +1560,7 @@ __global__ void pack_input_s2d_kernel(int N, int C, int H, int W, const float* _
   }
 }
 MER_API int mer_pack_input_s2d(int N, int C, int H, int W, const float* x, void* y, void* stream) {
-  if (C < 1 || C > 4 || (H & 1) || (W & 1)) return (int)hipErrorInvalidValue;
+  if (C < 1 || C > 4 || (H & 1) || (W & 1) || ((uintptr_t)x & 7)) return (int)hipErrorInvalidValue;
   const long total = (long)N * (H / 2 + 3) * (W / 2 + 3);
   const int grid = (int)((total + 255) / 256 < 16384 ? (total + 255) / 256 : 16384);
   hipLaunchKernelGGL(pack_input_s2d_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, N, C, H, W, x, (bf16_t*)y);
@@ -1914,22 +1926,36 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(long M, int C, const
       rstd[i] = ms[2 * (tc * 8 + i) + 1];
       if (BNMASK) stem_bn_coef(tc * 8 + i, ms, mgamma, mbeta, msc[i], msh[i]);
     }
-    for (long r = r0 + tr; r < r1; r += rows_per_iter) {
-      const long off = r * C + tc * 8;
-      const u32x4 gv = *reinterpret_cast<const u32x4*>(dy + off);
-      const u32x4 xv = *reinterpret_cast<const u32x4*>(x + off);
-      u32x4 mv = {1u, 1u, 1u, 1u};
-      if (!BNMASK && mask) mv = *reinterpret_cast<const u32x4*>(mask + off);
-      const bf16_t* gh = reinterpret_cast<const bf16_t*>(&gv);
-      const bf16_t* xh = reinterpret_cast<const bf16_t*>(&xv);
-      const bf16_t* mh = reinterpret_cast<const bf16_t*>(&mv);
+    // 4 rows per iteration with every load issued first (unconditional, from clamped rows; a row past r1
+    // contributes exact zeros), so a thread has 8-12 loads in flight instead of one row's 2-3: the same rows
+    // in the same order as a one-row loop, bit-identical sums
+    for (long rb = r0 + tr; rb < r1; rb += 4 * rows_per_iter) {
+      u32x4 gv[4], xv[4], mv[4];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const bool live = BNMASK ? bf2f(f2bf(fmaxf(bf2f(xh[i]) * msc[i] + msh[i], 0.f))) > 0.f
-                                 : (!mask || bf2f(mh[i]) > 0.f);
-        const float g = live ? bf2f(gh[i]) : 0.f;
-        s1[i] += g;
-        s2[i] += g * (bf2f(xh[i]) - mean[i]) * rstd[i];
+      for (int u = 0; u < 4; ++u) {
+        const long r = rb + u * rows_per_iter;
+        const long off = (r < r1 ? r : r1 - 1) * C + tc * 8;
+        gv[u] = *reinterpret_cast<const u32x4*>(dy + off);
+        xv[u] = *reinterpret_cast<const u32x4*>(x + off);
+        mv[u] = u32x4{1u, 1u, 1u, 1u};
+        if (!BNMASK && mask) mv[u] = *reinterpret_cast<const u32x4*>(mask + off);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const bool rowok = rb + u * rows_per_iter < r1;
+        const bf16_t* gh = reinterpret_cast<const bf16_t*>(&gv[u]);
+        const bf16_t* xh = reinterpret_cast<const bf16_t*>(&xv[u]);
+        const bf16_t* mh = reinterpret_cast<const bf16_t*>(&mv[u]);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const bool live = BNMASK ? bf2f(f2bf(fmaxf(bf2f(xh[i]) * msc[i] + msh[i], 0.f))) > 0.f
+                                   : (!mask || bf2f(mh[i]) > 0.f);
+          const float g = (live && rowok) ? bf2f(gh[i]) : 0.f;
+          if (rowok) {  // (a select: the loads above are unconditional)
+            s1[i] += g;
+            s2[i] += g * (bf2f(xh[i]) - mean[i]) * rstd[i];
+          }
+        }
       }
     }
 #pragma unroll
@@ -2154,24 +2180,34 @@ __global__ void maxpool_bwd_kernel(int N, int H, int W, int C, int Ho, int Wo, c
     const int n = fdiv(q2, inv_H);
     const int h = q2 - n * H;
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    for (int oh = (h + 1) / 2 - 1; oh <= (h + 1) / 2; ++oh) {
-      if (oh < 0 || oh >= Ho) continue;
-      const int r = h - (oh * 2 - 1);
-      if (r < 0 || r > 2) continue;
-      for (int ow = (w + 1) / 2 - 1; ow <= (w + 1) / 2; ++ow) {
-        if (ow < 0 || ow >= Wo) continue;
-        const int s = w - (ow * 2 - 1);
-        if (s < 0 || s > 2) continue;
-        const long oi = (((long)n * Ho + oh) * Wo + ow) * C + c0;
-        const u32x4 g = *reinterpret_cast<const u32x4*>(dy + oi);
-        const uint2 a = *reinterpret_cast<const uint2*>(arg + oi);
-        const bf16_t* gh = reinterpret_cast<const bf16_t*>(&g);
-        const uint8_t* a8 = reinterpret_cast<const uint8_t*>(&a);
+    // the (<= 4) candidate windows: every load unconditional from a clamped window, invalid ones masked by the
+    // tap test (a load under a per-lane branch waits for itself: 4 dependent round trips per thread)
+    u32x4 gq[2][2];
+    uint2 aq[2][2];
+    int tap[2][2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const int oh = (h + 1) / 2 - 1 + a, ow = (w + 1) / 2 - 1 + b;
+        const int r = h - (oh * 2 - 1), s = w - (ow * 2 - 1);
+        const bool ok = oh >= 0 && oh < Ho && ow >= 0 && ow < Wo && r >= 0 && r <= 2 && s >= 0 && s <= 2;
+        const int ohc = oh < 0 ? 0 : (oh >= Ho ? Ho - 1 : oh), owc = ow < 0 ? 0 : (ow >= Wo ? Wo - 1 : ow);
+        const long oi = (((long)n * Ho + ohc) * Wo + owc) * C + c0;
+        gq[a][b] = *reinterpret_cast<const u32x4*>(dy + oi);
+        aq[a][b] = *reinterpret_cast<const uint2*>(arg + oi);
+        tap[a][b] = ok ? r * 3 + s : -1;  // -1 matches no argmax
+      }
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const bf16_t* gh = reinterpret_cast<const bf16_t*>(&gq[a][b]);
+        const uint8_t* a8 = reinterpret_cast<const uint8_t*>(&aq[a][b]);
 #pragma unroll
         for (int i = 0; i < 8; ++i)
-          if (a8[i] == r * 3 + s) acc[i] += bf2f(gh[i]);
+          if ((int)a8[i] == tap[a][b]) acc[i] += bf2f(gh[i]);
       }
-    }
     u32x4 o;
     bf16_t* oh8 = reinterpret_cast<bf16_t*>(&o);
 #pragma unroll
@@ -2220,18 +2256,26 @@ __global__ void stem_bnrelu_maxpool_kernel(int N, int H, int W, int C, int Ho, i
       best[i] = -INFINITY;
       bi[i] = 0;
     }
-    for (int r = 0; r < 3; ++r)
-      for (int s = 0; s < 3; ++s) {
-        const int ih = oh * 2 - 1 + r, iw = ow * 2 - 1 + s;
-        if (ih < 0 || ih >= H || iw < 0 || iw >= W) continue;
-        const u32x4 v = *reinterpret_cast<const u32x4*>(x + (((long)n * H + ih) * W + iw) * C + c0);
-        const bf16_t* vh = reinterpret_cast<const bf16_t*>(&v);
+    // all 9 taps loaded first, unconditionally from clamped pixels (branch-free: the loads are in flight
+    // together), out-of-frame taps masked to -inf so they never win; same tap order and first-max tie rule
+    u32x4 v[9];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const float f = bf2f(f2bf(fmaxf(bf2f(vh[i]) * sc[i] + sh[i], 0.f)));
-          if (f > best[i]) { best[i] = f; bi[i] = r * 3 + s; }
-        }
+    for (int t = 0; t < 9; ++t) {
+      const int ih = oh * 2 - 1 + t / 3, iw = ow * 2 - 1 + t % 3;
+      const int ihc = ih < 0 ? 0 : (ih >= H ? H - 1 : ih), iwc = iw < 0 ? 0 : (iw >= W ? W - 1 : iw);
+      v[t] = *reinterpret_cast<const u32x4*>(x + (((long)n * H + ihc) * W + iwc) * C + c0);
+    }
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int ih = oh * 2 - 1 + t / 3, iw = ow * 2 - 1 + t % 3;
+      const bool ok = ih >= 0 && ih < H && iw >= 0 && iw < W;
+      const bf16_t* vh = reinterpret_cast<const bf16_t*>(&v[t]);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float f = ok ? bf2f(f2bf(fmaxf(bf2f(vh[i]) * sc[i] + sh[i], 0.f))) : -INFINITY;
+        if (f > best[i]) { best[i] = f; bi[i] = t; }
       }
+    }
     u32x4 o;
     bf16_t* oh8 = reinterpret_cast<bf16_t*>(&o);
     uint2 a;
