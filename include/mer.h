@@ -402,6 +402,17 @@ int mer_conv_dgrad_bnr(int N, int H, int W, int C, int K, int R, int S, int stri
                        const void* wt_packed, void* dx, const void* residual, const void* residual_mask,
                        const void* bn_mask, const void* bn_x, const float* bn_ms, float* bn_red, const void* bn_x2,
                        const float* bn_ms2, float* bn_red2, int variant, void* stream);
+/* mer_conv_dgrad_bnr of a 3x3 / stride-2 / pad-1 conv with the input gradient of a 1x1 / stride-2 / pad-0
+ * downsample of the SAME input fused in (the first BasicBlock of layers 2-4, video.py:21-23 -> torchvision
+ * BasicBlock.downsample): dx += conv-transpose(ds_dy [N][Ho][Wo][ds_K], ds_wt_packed [C][ds_K]) as an extra
+ * reduction segment of parity class (0, 0), the only pixels its taps reach -- one launch and one fp32 accumulator
+ * instead of a separate dgrad whose bf16 output the 3x3 dgrad read back as its residual.  ds_K, K multiples of
+ * 64; ds_dy NULL = mer_conv_dgrad_bnr. */
+int mer_conv_dgrad_ds(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, const void* dy,
+                      const void* wt_packed, void* dx, const void* residual, const void* residual_mask,
+                      const void* bn_mask, const void* bn_x, const float* bn_ms, float* bn_red, const void* bn_x2,
+                      const float* bn_ms2, float* bn_red2, const void* ds_dy, const void* ds_wt_packed, int ds_K,
+                      int variant, void* stream);
 
 /* out[c][0:2] = sum_p in[p][c][0:2] over `parts` partial rows, in a fixed order.  parts > 64 needs 64 more
  * rows after them in `in` (fold scratch, overwritten). */

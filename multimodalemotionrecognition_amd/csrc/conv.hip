@@ -46,6 +46,11 @@ struct ConvGeom {
   const float* bnr_ms2;
   float* bnr_red2;
   int vec;                // 16-byte epilogue (Ncols, ldy multiples of 8, every operand 16-byte aligned)
+  // stride-2 dgrad only: a 1x1 / stride-2 / pad-0 downsample of the same input fused as an extra K segment of parity
+  // class (0, 0) -- the only class its taps reach: dx[2i, 2j] += sum_k dY2[i, j, k] W2t[c][k] (NULL X2 = off)
+  const bf16_t* X2;       // [N][IH][IW][K2], the downsample branch's output gradient
+  const bf16_t* Wt2;      // [Ncols][K2]
+  int K2;
 };
 
 __host__ __device__ inline bool conv_vec_ok(const ConvGeom& g) {
@@ -764,10 +769,12 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN >= 16 ? 1 : 2) void conv_pipe
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   ParClass pc{};
   int M, Kr, rowsH, rowsW;  // this launch's GEMM rows / reduction length, row -> (n, a, b) grid
+  int Kr0 = 0;              // PAR: the 3x3 taps' share of Kr (the fused downsample segment follows it in class 0)
   if (PAR) {
     pc = par_class(g, par_cls());
     M = g.N * pc.Hc * pc.Wc;
-    Kr = pc.nr * pc.ns * g.IC;
+    Kr0 = pc.nr * pc.ns * g.IC;
+    Kr = Kr0 + ((g.X2 && pc.ph == 0 && pc.pw == 0) ? g.K2 : 0);
     rowsH = pc.Hc;
     rowsW = pc.Wc;
   } else {
@@ -798,6 +805,7 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN >= 16 ? 1 : 2) void conv_pipe
     acl[j] = cswz_k<CW>(r, lane % CW) * 8;
   }
   const bf16_t* pb[IB];
+  const bf16_t* pb2[IB];
   int bcl[IB];
   bool bok[IB];
 #pragma unroll
@@ -806,6 +814,7 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN >= 16 ? 1 : 2) void conv_pipe
     const int n = n0 + r;
     bok[j] = n < g.Ncols;
     pb[j] = g.Wt + (long)(bok[j] ? n : 0) * g.Kred;
+    pb2[j] = g.Wt2 + (long)(bok[j] ? n : 0) * g.K2;  // (unused unless the downsample segment is fused)
     bcl[j] = cswz_k<CW>(r, lane % CW) * 8;
   }
   const float inv_IC = 1.f / g.IC, inv_S = 1.f / g.S, inv_ns = PAR ? 1.f / pc.ns : 1.f;
@@ -813,6 +822,8 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN >= 16 ? 1 : 2) void conv_pipe
   // class-local reduction index kk -> (ri, si, c) -> source; the weight operand's offset of the same kk
   auto par_a_src = [&](int n, int hh, int ww, bool rowok, int kk) -> const bf16_t* {
     if (!rowok || kk >= Kr) return zero;
+    if (kk >= Kr0)  // the fused downsample segment (class 0): its output pixel (hh, ww) is the input pixel (2hh, 2ww)
+      return g.X2 + (((long)n * g.IH + hh) * g.IW + ww) * g.K2 + (kk - Kr0);
     const int tap = fdiv(kk, inv_IC), c = kk - tap * g.IC;
     const int ri = fdiv(tap, inv_ns), si = tap - ri * pc.ns;
     const int ih = hh + pc.dh0 - ri, iw = ww + pc.dw0 - si;
@@ -837,7 +848,8 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN >= 16 ? 1 : 2) void conv_pipe
     for (int j = 0; j < IB; ++j) {
       const int kk = k0 + bcl[j];
       const bool ok = bok[j] && kk < Kr;
-      glds16(ok ? pb[j] + (PAR ? par_b_off(kk) : kk) : zero, lb + (w * IB + j) * 512);
+      const bf16_t* src = !PAR ? pb[j] + kk : (kk >= Kr0 ? pb2[j] + (kk - Kr0) : pb[j] + par_b_off(kk));
+      glds16(ok ? src : zero, lb + (w * IB + j) * 512);
     }
   };
 
@@ -1348,7 +1360,21 @@ MER_API int mer_conv_dgrad_bnr(int N, int H, int W, int C, int K, int R, int S, 
                                const void* wt_packed, void* dx, const void* residual, const void* residual_mask,
                                const void* bn_mask, const void* bn_x, const float* bn_ms, float* bn_red,
                                const void* bn_x2, const float* bn_ms2, float* bn_red2, int variant, void* stream) {
+  return mer_conv_dgrad_ds(N, H, W, C, K, R, S, stride, pad, dy, wt_packed, dx, residual, residual_mask, bn_mask, bn_x,
+                           bn_ms, bn_red, bn_x2, bn_ms2, bn_red2, nullptr, nullptr, 0, variant, stream);
+}
+
+MER_API int mer_conv_dgrad_ds(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, const void* dy,
+                              const void* wt_packed, void* dx, const void* residual, const void* residual_mask,
+                              const void* bn_mask, const void* bn_x, const float* bn_ms, float* bn_red,
+                              const void* bn_x2, const float* bn_ms2, float* bn_red2, const void* ds_dy,
+                              const void* ds_wt_packed, int ds_K, int variant, void* stream) {
   if (K % 8 || C % 8 || variant < -1 || variant > 5) return (int)hipErrorInvalidValue;
+  // the fused downsample: a 1x1 / stride-2 / pad-0 conv of the same input with ds_K output channels, beside a
+  // 3x3 / stride-2 / pad-1 conv (its taps land in parity class (0, 0) only, at pixel (2i, 2j)); K-tile aligned
+  if (ds_dy && (stride != 2 || R != 3 || S != 3 || pad != 1 || !ds_wt_packed || ds_K <= 0 || ds_K % 64 || K % 64 ||
+                variant == 0))
+    return (int)hipErrorInvalidValue;
   // 64-channel outputs (layer1, the layer2.0 input gradients): 32-wide K-tiles on a 4-deep ring with 4-wave tiles
   // (tools/bench_conv.py --fused: layer1 101 -> 65 us, layer2.0 s2 74 -> 51, downsample 48 -> 31); wider outputs
   // keep the 64-wide 2-deep ring (the deep ring loses 10-50% there)
@@ -1364,6 +1390,7 @@ MER_API int mer_conv_dgrad_bnr(int N, int H, int W, int C, int K, int R, int S, 
   g.R_ = (const bf16_t*)residual; g.Rmask = (const bf16_t*)residual_mask;
   g.bnr_mask = (const bf16_t*)bn_mask; g.bnr_x = (const bf16_t*)bn_x; g.bnr_ms = bn_ms; g.bnr_red = bn_red;
   g.bnr_x2 = (const bf16_t*)bn_x2; g.bnr_ms2 = bn_ms2; g.bnr_red2 = bn_red2;
+  g.X2 = (const bf16_t*)ds_dy; g.Wt2 = (const bf16_t*)ds_wt_packed; g.K2 = ds_dy ? ds_K : 0;
   g.vec = vec_epilogue_enabled() && conv_vec_ok(g);
   if (variant == 0 || stride > 2) return launch_conv<true>(g, (hipStream_t)stream);
   if (stride == 2) return launch_conv_pipe<true, true>(g, (hipStream_t)stream, variant);

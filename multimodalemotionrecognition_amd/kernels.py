@@ -492,10 +492,11 @@ def conv_fwd(x, wp, y, stats, R, S, stride, pad, variant=-1):
             wp.data_ptr(), y.data_ptr(), _ptr(stats), int(variant), stream_ptr())
 
 
-def conv_dgrad(dy, wt, dx, R, S, stride, pad, residual=None, mask=None, variant=-1, bnr=None):
+def conv_dgrad(dy, wt, dx, R, S, stride, pad, residual=None, mask=None, variant=-1, bnr=None, ds=None):
     """dx = conv-transpose(dy) (+ residual where mask > 0).  ``bnr``: optional fused BatchNorm-backward
     reduction of the BN the gradient flows into, ``(mask, x, ms, red[, x2, ms2, red2])`` with red(2)
-    zeroed [BN_STAT_PARTS, C, 2] buffers (see mer_conv_dgrad_bnr)."""
+    zeroed [BN_STAT_PARTS, C, 2] buffers (see mer_conv_dgrad_bnr).  ``ds``: ``(ds_dy, ds_wt)`` -- the input gradient
+    of a 1x1 / stride-2 downsample of the same input, fused in (mer_conv_dgrad_ds)."""
     N, H, W, C = dx.shape
     Kc = dy.shape[-1]
     Ho, Wo = (H + 2 * pad - R) // stride + 1, (W + 2 * pad - S) // stride + 1
@@ -508,6 +509,15 @@ def conv_dgrad(dy, wt, dx, R, S, stride, pad, residual=None, mask=None, variant=
     for t in (b[3], b[6]):
         if t is not None and t.numel() != bn_red_rows(N * H * W) * C * 2:
             raise ValueError("conv_dgrad bnr red buffers must be zeroed [bn_red_rows(N*H*W), C, 2]")
+    if ds is not None:
+        ddy, dwt = ds
+        Kd = ddy.shape[-1]
+        if tuple(ddy.shape) != (N, Ho, Wo, Kd) or tuple(dwt.shape) != (C, Kd) or stride != 2 or R != 3 or pad != 1:
+            raise ValueError("conv_dgrad ds: a 1x1 / stride-2 downsample gradient beside a 3x3 / stride-2 / pad-1 conv")
+        _launch("conv_dgrad", (N, H, W, C, Kc, R, stride), "mer_conv_dgrad_ds", N, H, W, C, Kc, R, S, stride, pad,
+                dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), _ptr(residual), _ptr(mask), *[_ptr(t) for t in b],
+                ddy.data_ptr(), dwt.data_ptr(), Kd, int(variant), stream_ptr())
+        return
     _launch("conv_dgrad", (N, H, W, C, Kc, R, stride), "mer_conv_dgrad_bnr", N, H, W, C, Kc, R, S, stride, pad,
             dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), _ptr(residual), _ptr(mask), *[_ptr(t) for t in b],
             int(variant), stream_ptr())

@@ -536,6 +536,9 @@ def _bnr_target(blk_sv, blk, arena):
 # 5-12 us each off the critical stream per step (the stem's zero / gather / add included).  (Round 3 also measured
 # the weight gradients on a third stream and folding after every N blocks: both slower or inside the noise, removed.)
 WGRAD_DEFER = os.environ.get("MER_WGRAD_DEFER", "1") != "0"
+# The downsample's input gradient fused into conv1's stride-2 dgrad (mer_conv_dgrad_ds; MER_FUSED_DS_DGRAD=0: the
+# separate 1x1 dgrad + residual read, A/B)
+FUSED_DS_DGRAD = os.environ.get("MER_FUSED_DS_DGRAD", "1") != "0"
 
 
 class _WgradLane:
@@ -604,9 +607,13 @@ def block_backward(trunk, blk: BasicBlock, sv, dx: torch.Tensor, grads, training
         wd = _grad(blk.downsample[0].weight, grads)
         if wd is not None:
             lane.run(lambda: K.conv_wgrad(xin, dcd, wd, 1, 1, s, 0, defer=lane.folds), xin, dcd, wd, block=bidx)
-        dxd = torch.empty_like(xin)
-        K.conv_dgrad(dcd, trunk.packed(blk.downsample[0], Cin, True), dxd, 1, 1, s, 0)
-        K.conv_dgrad(dc1, trunk.packed(blk.conv1, Cin, True), dxin, 3, 3, s, 1, residual=dxd, bnr=bnr)
+        if FUSED_DS_DGRAD and s == 2:  # the downsample's input gradient as an extra K segment of conv1's dgrad
+            K.conv_dgrad(dc1, trunk.packed(blk.conv1, Cin, True), dxin, 3, 3, s, 1, bnr=bnr,
+                         ds=(dcd, trunk.packed(blk.downsample[0], Cin, True)))
+        else:
+            dxd = torch.empty_like(xin)
+            K.conv_dgrad(dcd, trunk.packed(blk.downsample[0], Cin, True), dxd, 1, 1, s, 0)
+            K.conv_dgrad(dc1, trunk.packed(blk.conv1, Cin, True), dxin, 3, 3, s, 1, residual=dxd, bnr=bnr)
     else:
         K.conv_dgrad(dc1, trunk.packed(blk.conv1, Cin, True), dxin, 3, 3, s, 1, residual=g_out, mask=out, bnr=bnr)
     if own_lane:

@@ -517,3 +517,35 @@ def test_transposed_pack_from_forward_pack():
         Kc, C, R, S = c.weight.shape
         want = c.weight.detach().bfloat16().permute(1, 2, 3, 0).reshape(C, R * S * Kc)
         assert torch.equal(g, want)
+
+
+@pytest.mark.parametrize("C,Kc,H", [(64, 128, 28), (128, 256, 14), (256, 512, 8)])
+def test_dgrad_fused_downsample_vs_torch(C, Kc, H):
+    """mer_conv_dgrad_ds: the 3x3/s2/p1 conv1 dgrad with the 1x1/s2 downsample's input gradient fused in as an extra
+    K segment of parity class (0, 0) == torch's conv_transpose sum of the two branches on the same bf16 operands
+    (one fp32 accumulator, one bf16 rounding), and within a bf16 rounding of the two-launch form."""
+    from multimodalemotionrecognition_amd import kernels as K
+
+    torch.manual_seed(C)
+    N = 2
+    Ho = (H + 2 - 3) // 2 + 1
+    dy = torch.randn(N, Kc, Ho, Ho).bfloat16().float()
+    dyd = torch.randn(N, Kc, Ho, Ho).bfloat16().float()
+    w = (torch.randn(Kc, C, 3, 3) / (9 * C) ** 0.5).bfloat16().float()
+    wd = (torch.randn(Kc, C, 1, 1) / C ** 0.5).bfloat16().float()
+    ref = F.conv_transpose2d(dy, w, stride=2, padding=1, output_padding=1) + \
+        F.conv_transpose2d(dyd, wd, stride=2, output_padding=1)
+    ref = ref[:, :, :H, :H]
+    wt = w.permute(1, 2, 3, 0).reshape(C, 9 * Kc).contiguous().cuda().bfloat16()  # [C][r][s][k]
+    wdt = wd.reshape(Kc, C).t().contiguous().cuda().bfloat16()                   # [C][k]
+    dyh = dy.permute(0, 2, 3, 1).contiguous().cuda().bfloat16()
+    dydh = dyd.permute(0, 2, 3, 1).contiguous().cuda().bfloat16()
+    dx = torch.empty(N, H, H, C, device="cuda", dtype=torch.bfloat16)
+    K.conv_dgrad(dyh, wt, dx, 3, 3, 2, 1, ds=(dydh, wdt))
+    got = dx.float().permute(0, 3, 1, 2).cpu()
+    assert rel_rms(got, ref) < 4e-3, rel_rms(got, ref)
+    dxd = torch.empty_like(dx)
+    K.conv_dgrad(dydh, wdt, dxd, 1, 1, 2, 0)
+    dx2 = torch.empty_like(dx)
+    K.conv_dgrad(dyh, wt, dx2, 3, 3, 2, 1, residual=dxd)
+    assert rel_rms(got, dx2.float().permute(0, 3, 1, 2).cpu()) < 6e-3
