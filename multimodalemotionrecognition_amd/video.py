@@ -536,9 +536,9 @@ def _bnr_target(blk_sv, blk, arena):
 # 5-12 us each off the critical stream per step (the stem's zero / gather / add included).  (Round 3 also measured
 # the weight gradients on a third stream and folding after every N blocks: both slower or inside the noise, removed.)
 WGRAD_DEFER = os.environ.get("MER_WGRAD_DEFER", "1") != "0"
-# The downsample's input gradient fused into conv1's stride-2 dgrad (mer_conv_dgrad_ds; MER_FUSED_DS_DGRAD=0: the
-# separate 1x1 dgrad + residual read, A/B)
-FUSED_DS_DGRAD = os.environ.get("MER_FUSED_DS_DGRAD", "1") != "0"
+# The downsample's input gradient fused into conv1's stride-2 dgrad (mer_conv_dgrad_ds): +1.2 % same-box vs the
+# separate 1x1 dgrad whose bf16 output the 3x3 dgrad read back as its residual (profiles/r04/ab_runs.txt)
+FUSED_DS_DGRAD = True
 
 
 class _WgradLane:
