@@ -19,12 +19,16 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--steps", type=int, default=30)
 ap.add_argument("--warmup", type=int, default=10)  # graphs are captured during the first steps
 ap.add_argument("--batch", type=int, default=32)
+ap.add_argument("--modes", default="late,concat,gated,xattn,xattn+prior")
 args = ap.parse_args()
+MODES = args.modes.split(",")
 video, audio, labels = params.clip_inputs(args.batch, seed=20261015)
 video, audio, labels = torch.from_numpy(video).cuda(), torch.from_numpy(audio).cuda(), torch.from_numpy(labels).cuda()
 res = {}
 for name, fusion, kw in (("late", "late", {}), ("concat", "concat", {}), ("gated", "gated", {}),
                          ("xattn", "xattn", {}), ("xattn+prior", "xattn", {"xattn_use_emotion_prior": True, "forward_emotion_prior_flags": True})):
+    if name not in MODES:
+        continue
     torch.manual_seed(0)
     model = build_model(8, fusion, pretrained_video=False, use_wavlm=True, **kw).cuda()
     if kw:  # the reference never forwards the prior flags (train.py:454-469); set the module up explicitly
