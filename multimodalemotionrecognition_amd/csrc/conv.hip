@@ -1552,36 +1552,37 @@ MER_API int mer_pack_input_nhwc(int N, int C, int H, int W, int Cp, const float*
 // with channel (dy*2 + dx)*C + c (zero for the 2 leading / 1 trailing border rows and columns and for
 // channels >= 4C).  The stride-2 7x7 conv then is a stride-1 4x4 conv with no padding on 16 channels
 // (K = 256 instead of 7*7*8 = 392 for the 8-channel-padded direct form); weights: pack mode 2 below.
-__global__ void pack_input_s2d_kernel(int N, int C, int H, int W, const float* __restrict__ x, bf16_t* __restrict__ y) {
+template <int C>  // compile-time channel count: the (dy, dx, c) -> s2d channel map unrolls to fixed registers
+__global__ void pack_input_s2d_kernel(int N, int H, int W, const float* __restrict__ x, bf16_t* __restrict__ y) {
   const int Hs = H / 2 + 3, Ws = W / 2 + 3;
-  const long total = (long)N * Hs * Ws;
-  for (long p = blockIdx.x * (long)blockDim.x + threadIdx.x; p < total; p += (long)gridDim.x * blockDim.x) {
-    const int i = (int)(p % Ws);
-    const long q = p / Ws;
-    const int j = (int)(q % Hs), n = (int)(q / Hs);
+  const int total = N * Hs * Ws;  // (< 2^22, checked on the host: 32-bit index math, exact float-reciprocal divides --
+                                  // the 64-bit divisions of a long index were most of this kernel's time)
+  const float inv_Ws = 1.f / Ws, inv_Hs = 1.f / Hs;
+  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < total; p += gridDim.x * blockDim.x) {
+    const int q = fdiv(p, inv_Ws);
+    const int i = p - q * Ws;
+    const int n = fdiv(q, inv_Hs);
+    const int j = q - n * Hs;
     uint32_t o[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
     const int jj = j - 2, ii = i - 2;
     if (jj >= 0 && jj < H / 2 && ii >= 0 && ii < W / 2) {
       // the 2x2 block's two rows of each channel as float2 loads (adjacent lanes read adjacent 8-byte pairs: one
-      // coalesced 512-byte run per wave instruction; the per-element scalar gathers ran at 1/6 of HBM speed)
+      // coalesced 512-byte run per wave instruction)
       const float* xn = x + (long)n * C * H * W + (long)(2 * jj) * W + 2 * ii;
-      float v[4][4];  // [c][dydx]
+      float v[C][4];  // [c][dydx]
 #pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        if (c >= C) break;
+      for (int c = 0; c < C; ++c)
 #pragma unroll
         for (int dy = 0; dy < 2; ++dy) {
-          const float2 q = *reinterpret_cast<const float2*>(xn + (long)c * H * W + dy * W);
-          v[c][2 * dy] = q.x;
-          v[c][2 * dy + 1] = q.y;
+          const float2 q2 = *reinterpret_cast<const float2*>(xn + (long)c * H * W + dy * W);
+          v[c][2 * dy] = q2.x;
+          v[c][2 * dy + 1] = q2.y;
         }
-      }
-      for (int ch = 0; ch < 4 * C; ++ch) {
-        const int dydx = ch / C, c = ch - dydx * C;
-        o[ch >> 1] |= (uint32_t)f2bf(v[c][dydx]) << ((ch & 1) * 16);
-      }
+#pragma unroll
+      for (int ch = 0; ch < 4 * C; ++ch)
+        o[ch >> 1] |= (uint32_t)f2bf(v[ch % C][ch / C]) << ((ch & 1) * 16);
     }
-    u32x4* dst = reinterpret_cast<u32x4*>(y + p * 16);
+    u32x4* dst = reinterpret_cast<u32x4*>(y + (long)p * 16);
     dst[0] = u32x4{o[0], o[1], o[2], o[3]};
     dst[1] = u32x4{o[4], o[5], o[6], o[7]};
   }
@@ -1589,8 +1590,13 @@ __global__ void pack_input_s2d_kernel(int N, int C, int H, int W, const float* _
 MER_API int mer_pack_input_s2d(int N, int C, int H, int W, const float* x, void* y, void* stream) {
   if (C < 1 || C > 4 || (H & 1) || (W & 1) || ((uintptr_t)x & 7)) return (int)hipErrorInvalidValue;
   const long total = (long)N * (H / 2 + 3) * (W / 2 + 3);
+  if (total >= (1L << 22)) return (int)hipErrorInvalidValue;  // fdiv range
   const int grid = (int)((total + 255) / 256 < 16384 ? (total + 255) / 256 : 16384);
-  hipLaunchKernelGGL(pack_input_s2d_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, N, C, H, W, x, (bf16_t*)y);
+  const hipStream_t st = (hipStream_t)stream;
+  if (C == 3) hipLaunchKernelGGL(pack_input_s2d_kernel<3>, dim3(grid), dim3(256), 0, st, N, H, W, x, (bf16_t*)y);
+  else if (C == 1) hipLaunchKernelGGL(pack_input_s2d_kernel<1>, dim3(grid), dim3(256), 0, st, N, H, W, x, (bf16_t*)y);
+  else if (C == 2) hipLaunchKernelGGL(pack_input_s2d_kernel<2>, dim3(grid), dim3(256), 0, st, N, H, W, x, (bf16_t*)y);
+  else hipLaunchKernelGGL(pack_input_s2d_kernel<4>, dim3(grid), dim3(256), 0, st, N, H, W, x, (bf16_t*)y);
   MER_LAUNCH_CHECK();
 }
 
