@@ -207,9 +207,10 @@ int mer_posconv_gemm_bf16(int B, int L, int C_total, int groups, int taps, int p
 
 /* WavLM feature-extractor layer 0 (TF:723-745): Conv1d(1,512,k=10,s=5,no bias) of wav [B,S] fp32 ->
  * GroupNorm(512,512) (per (clip, channel) statistics over time of the bf16-rounded conv output) -> GELU,
- * written once as bf16 [B,Lout,512].  Two passes over the (cheap: 10 taps) conv: statistics into per-tile
- * partial rows, reduced in a fixed order (deterministic, no atomics), then conv recompute + normalise +
- * GELU.  workspace: float[B * (ceil(Lout/128) + 1) * 1024]. */
+ * written once as bf16 [B,Lout,512].  Two passes over the (cheap: 10 taps, on split-bf16 MFMA at fp32-class
+ * accuracy) conv: statistics into per-tile partial rows, reduced in a fixed order (deterministic, no atomics),
+ * then conv recompute + normalise + GELU.  workspace (16-byte aligned): float[B * (ceil(Lout/128) + 1) * 1024
+ * + 16384] (the last 64 KB hold the split weight fragments). */
 int mer_wavlm_conv0_gn_gelu(int B, int S, int Lout, const float* wav, const float* w0, const float* gamma,
                             const float* beta, float eps, float* workspace, void* out, void* stream);
 

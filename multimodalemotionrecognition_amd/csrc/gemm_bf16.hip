@@ -637,6 +637,186 @@ __global__ __launch_bounds__(PH_NT, 1) void gemm_phase_kernel(GemmArgs g) {
   }
 }
 
+// Ping-pong form of the phase kernel (cdna_hip_programming.md §5 "256² 8-phase template": two barriers per
+// phase, the wave rows staggered by one barrier).  Same tile, waves, pieces and fragment maps as
+// gemm_phase_kernel; each phase is  R: [vmcnt wait] stage one piece, ds_read the phase's fragments | barrier |
+// M: lgkmcnt(0), 16 MFMAs | barrier.  Wave row 1 (waves 4-7, one per SIMD) runs one barrier behind row 0, so on
+// every SIMD one wave's R section (LDS reads, DMA issue) overlaps the other's MFMA cluster.
+// Global barrier k ends "interval" k: row 0 runs R(phi) in interval 2phi+1 and M(phi) in 2phi+2, row 1 one later.
+//   Reads, phase (u,p): p0 P0(u) Q0(u), p1 Q1(u), p2 P1(u), p3 none.
+//   Stages, phase (u,p): p0 Q1(u+1), p1 P1(u+1), p2 P0(u+2), p3 Q0(u+2)   (piece X(v) issued 4..6 phases early)
+//   RAW: at the top of R(phi) every wave waits (counted vmcnt) for its DMA of the pieces read in phase phi+1;
+//        a reader in R(phi+1) (interval >= 2phi+3) is past the barrier that follows both rows' waits.
+//   WAR: X(v+2) reuses X(v)'s buffer; row 1's last read of X(v) in phase r is retired (lgkmcnt(0) in its M(r))
+//        by barrier 2r+3, and X(v+2) is issued in phase >= r+2, i.e. interval >= 2r+5.
+// Steady state: 3 pieces (6 glds per wave) stay in flight across every wait.
+template <typename TOUT>
+__global__ __launch_bounds__(PH_NT, 1) void gemm_pp_kernel(GemmArgs g) {
+  extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
+  if (layer_skipped(g.skip_mask, g.skip_bit)) return;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int nx = (g.N + 255) / 256, ny = (g.M + 255) / 256;
+  int tx, ty;
+  xcd_tile_grouped(blockIdx.x, nx, ny, g.tgroup, tx, ty);
+  const int m0 = ty * 256, n0 = tx * 256;
+  const int wr = w >> 2, wc = w & 3;
+  const int lrow = lane >> 3, lchunk = lane & 7;
+
+  const bf16_t* src[4][2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int pr = (w * 2 + j) * 8 + lrow;
+    const int sw = swz_chunk(pr, lchunk) * 8;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      int m = m0 + (pr >> 6) * 128 + h * 64 + (pr & 63);
+      m = m < g.M ? m : g.M - 1;
+      src[h ? 3 : 0][j] = g.A + (long)(m / g.a_rpg) * g.a_gstride + (long)(m % g.a_rpg) * g.a_rstride + sw;
+      int n = n0 + (pr >> 5) * 64 + h * 32 + (pr & 31);
+      n = n < g.N ? n : g.N - 1;
+      src[1 + h][j] = g.B + (long)n * g.ldb + sw;
+    }
+  }
+  const int nk = g.K / 64;
+  auto stage = [&](int pc, int u) {
+    if (u >= nk) return;
+    bf16_t* dst = smem + ((u & 1) * 4 + pc) * PH_PIECE + w * 1024;
+    glds16(src[pc][0] + ktile_off(g, u), dst);
+    glds16(src[pc][1] + ktile_off(g, u), dst + 512);
+  };
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int fr = lane & 15, fq = lane >> 4;
+  auto read_frags = [&](const bf16_t* piece, int rbase, int n16, bf16x8 (*out)[2]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (i >= n16) break;
+      const int r = rbase + i * 16 + fr;
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+        out[i][s] = *reinterpret_cast<const bf16x8*>(piece + r * 64 + swz_chunk(r, s * 4 + fq) * 8);
+    }
+  };
+  auto barrier = [&]() {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto mfma_entry = [&]() {
+    __builtin_amdgcn_s_waitcnt((15) | (7 << 4) | (0 << 8) | (3 << 14));  // lgkmcnt(0) only
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  // prologue: the stages of phases -6 .. -1 = P0(0) Q0(0) Q1(0) P1(0) P0(1) Q0(1); wait for P0(0), Q0(0)
+  stage(0, 0); stage(1, 0); stage(2, 0); stage(3, 0); stage(0, 1); stage(1, 1);
+  wait_vm_even(nk > 1 ? 8 : 4);
+  barrier();
+  if (wr == 1) barrier();  // the stagger
+
+  bf16x8 af[4][2], bq0[2][2], bq1[2][2];
+  for (int u = 0; u < nk; ++u) {
+    const int e1 = u + 1 < nk, e2 = u + 2 < nk;
+    const bf16_t* buf = smem + (u & 1) * 4 * PH_PIECE;
+    // phase 0: reads P0(u), Q0(u); waits for Q1(u) (read in phase 1); stages Q1(u+1)
+    wait_vm_even(2 * (1 + 2 * e1));
+    stage(2, u + 1);
+    read_frags(buf + 0 * PH_PIECE, wr * 64, 4, af);
+    read_frags(buf + 1 * PH_PIECE, wc * 32, 2, bq0);
+    barrier();
+    mfma_entry();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][s], bq0[j][s], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    barrier();
+    // phase 1: reads Q1(u); waits for P1(u); stages P1(u+1)
+    wait_vm_even(2 * 3 * e1);
+    stage(3, u + 1);
+    read_frags(buf + 2 * PH_PIECE, wc * 32, 2, bq1);
+    barrier();
+    mfma_entry();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][s], bq1[j][s], acc[i][2 + j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    barrier();
+    // phase 2: reads P1(u); nothing to wait for (phase 3 reads nothing); stages P0(u+2)
+    stage(0, u + 2);
+    read_frags(buf + 3 * PH_PIECE, wr * 64, 4, af);
+    barrier();
+    mfma_entry();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][s], bq0[j][s], acc[4 + i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    barrier();
+    // phase 3: no reads; waits for P0(u+1), Q0(u+1) (read in phase (u+1,0)); stages Q0(u+2)
+    wait_vm_even(2 * (2 * e1 + e2));
+    stage(1, u + 2);
+    barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[4 + i][2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][s], bq1[j][s], acc[4 + i][2 + j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    barrier();
+  }
+  if (wr == 0) barrier();  // rows leave with equal barrier counts
+
+  TOUT* C = reinterpret_cast<TOUT*>(g.C);
+  const unsigned long long dseed = mer_site_seed(g.drop_seed, g.drop_site);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int col = n0 + wc * 64 + j * 16 + fr;
+    if (col >= g.N) continue;
+    const float bv = g.bias ? g.bias[col] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wr * 128 + i * 16 + fq * 4 + r;
+        if (row >= g.M) continue;
+        float v = epi_act_drop(acc[i][j][r] + bv, g.act, g.drop_p, dseed, (long)row * g.N + col);
+        if (g.R) v += bf2f(g.R[(long)row * g.ldr + col]);
+        stf<TOUT>(C, (long)row * g.ldc + col, v);
+      }
+  }
+}
+
+template <typename TOUT>
+int launch_pp_t(const GemmArgs& g, hipStream_t st) {
+  const long tiles = (long)((g.N + 255) / 256) * ((g.M + 255) / 256);
+  const size_t lds = 8 * PH_PIECE * sizeof(bf16_t);
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_pp_kernel<TOUT>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+    return (int)hipErrorInvalidConfiguration;
+  hipLaunchKernelGGL((gemm_pp_kernel<TOUT>), dim3((unsigned)tiles), dim3(PH_NT), lds, st, g);
+  return (int)hipGetLastError();
+}
+
 template <typename TOUT>
 int launch_phase_t(const GemmArgs& g, hipStream_t st) {
   const long tiles = (long)((g.N + 255) / 256) * ((g.M + 255) / 256);
@@ -758,7 +938,7 @@ MER_API int mer_gemm_bf16_tr(int M, int N, int K, const void* A, long a_gstride,
   if (M <= 0 || N <= 0) return 0;
   if (drop_p < 0.f || drop_p >= 1.f || (drop_p > 0.f && !drop_seed) || skip_bit < 0 || skip_bit > 62)
     return (int)hipErrorInvalidValue;
-  if (variant < -1 || variant > 19) return (int)hipErrorInvalidValue;
+  if (variant < -1 || variant > 20) return (int)hipErrorInvalidValue;
   if (K % 8 != 0 || a_rpg <= 0 || (a_rstride % 8) != 0 || (a_gstride % 8) != 0 || (ldw % 8) != 0)
     return (int)hipErrorInvalidValue;
   if ((((uintptr_t)A) | ((uintptr_t)W)) & 15) return (int)hipErrorInvalidValue;
@@ -806,6 +986,7 @@ MER_API int mer_gemm_bf16_tr(int M, int N, int K, const void* A, long a_gstride,
     case 17: return launch_pipe<CfgW4>(g, c_dtype, st);
     case 18: return launch_pipe<CfgY32>(g, c_dtype, st);
     case 19: return launch_pipe<CfgL32>(g, c_dtype, st);
+    case 20: return c_dtype == MER_BF16 ? launch_pp_t<bf16_t>(g, st) : launch_pp_t<float>(g, st);
     default: return launch<0>(g, c_dtype, 1, st);
   }
 }

@@ -14,71 +14,181 @@ typedef __attribute__((ext_vector_type(8))) float f32x8;
 // tile and keeps only per-tile partial (sum, sumsq) rows, a finalize reduces them in a fixed order
 // (deterministic), and pass 2 recomputes the conv, normalises, applies GELU and writes once.
 // Statistics are taken over the bf16-ROUNDED conv outputs, the values GroupNorm sees in the bf16 path.
-// Block = 128 output steps of one clip, 2 channels per thread (256 threads x 2 = 512 channels).
+//
+// The conv runs on v_mfma_f32_16x16x32_bf16 at fp32-class accuracy: waveform and weights are split exactly
+// into three bf16 planes (x = xh + xm + xl, 8 + 8 + 8 mantissa bits) and the six products down to 2^-24
+// relative (xh.wh, xh.wm, xm.wh, xh.wl, xm.wm, xl.wh) are stacked along K: 6 terms x 10 taps = 60 of the 64
+// K slots of two MFMAs per 16 channels x 16 time steps (the dropped xm.wl, xl.wm, xl.wl are below fp32's own
+// rounding; the high-pass / DC-offset case of tests/test_wavlm_gpu.py is the one that needs all six).  The
+// 10 VALU FMAs per output (plus their LDS sample reads) were half of both passes' VALU time; what is left is
+// GroupNorm + GELU.  Operand roles: A = weights (row = channel), B = samples (column = time step), so a lane's
+// accumulator holds 4 ADJACENT channels of one time step: one 8-byte store of the channel-last output.
+// Block = 128 output steps of one clip x 512 channels, 4 waves x 128 channels.
 // ---------------------------------------------------------------------------------------
 namespace {
 constexpr int C0_TS = 128, C0_KW = 10, C0_ST = 5;
+constexpr int C0_PL = C0_TS * C0_ST + C0_KW;  // samples per tile (one plane)
+constexpr int C0_ZERO = 3 * C0_PL;            // index of the zero slot after the three planes
+// term t (K slots 10t .. 10t+9) of the split product: sample plane and weight plane (0 = hi, 1 = mid, 2 = lo)
+__device__ __forceinline__ int c0_xplane(int t) { return (0x210100 >> (4 * t)) & 15; }  // h h m h m l
+__device__ __forceinline__ int c0_wplane(int t) { return (0x012010 >> (4 * t)) & 15; }  // h m h l m h
 
-__device__ __forceinline__ void conv0_tile_load(const float* __restrict__ x, int S, int t0, float* xs) {
-  for (int i = threadIdx.x; i < C0_TS * C0_ST + C0_KW; i += blockDim.x) {
+__device__ __forceinline__ void split3(float x, bf16_t& h, bf16_t& m, bf16_t& l) {
+  h = f2bf(x);
+  const float r1 = x - bf2f(h);  // exact
+  m = f2bf(r1);
+  l = f2bf(r1 - bf2f(m));        // exact remainder, <= 8 significant bits
+}
+
+// the tile's samples t0*5 .. t0*5 + 649 as three bf16 planes (zero past the clip), plus the zero slot
+__device__ __forceinline__ void conv0_tile_split(const float* __restrict__ x, int S, int t0, bf16_t* xs3) {
+  for (int i = threadIdx.x; i < C0_PL; i += blockDim.x) {
     const long si = (long)t0 * C0_ST + i;
-    xs[i] = si < S ? x[si] : 0.f;
+    bf16_t h, m, l;
+    split3(si < S ? x[si] : 0.f, h, m, l);
+    xs3[i] = h;
+    xs3[C0_PL + i] = m;
+    xs3[2 * C0_PL + i] = l;
   }
+  if (threadIdx.x == 0) xs3[C0_ZERO] = 0;
+}
+
+// B-fragment gather table of this lane (col = time l & 15, K slots 32m + 8(l>>4) + i): LDS index of slot i
+// at local time 0, and the per-time-step stride mask (samples advance 5 per step; the 4 empty slots 60..63
+// read the zero slot at stride 0)
+struct C0Gather {
+  int off[16], msk[16];
+  __device__ __forceinline__ void init(int lane) {
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const int k = 32 * (s >> 3) + 8 * (lane >> 4) + (s & 7), t = k / 10, j = k - 10 * t;
+      off[s] = t < 6 ? c0_xplane(t) * C0_PL + j : C0_ZERO;
+      msk[s] = t < 6 ? -1 : 0;
+    }
+  }
+  // the two B fragments (K 0..31, 32..63) of local time step tl
+  __device__ __forceinline__ void load(const bf16_t* xs3, int tl, bf16x8& b0, bf16x8& b1) const {
+    const int t5 = tl * C0_ST;
+    uint32_t u[8];
+#pragma unroll
+    for (int p = 0; p < 8; ++p)
+      u[p] = (uint32_t)xs3[off[2 * p] + (t5 & msk[2 * p])] | ((uint32_t)xs3[off[2 * p + 1] + (t5 & msk[2 * p + 1])] << 16);
+    b0 = __builtin_bit_cast(bf16x8, u32x4{u[0], u[1], u[2], u[3]});
+    b1 = __builtin_bit_cast(bf16x8, u32x4{u[4], u[5], u[6], u[7]});
+  }
+};
+
+__device__ __forceinline__ f32x4 c0_mfma(const bf16x8* a, bf16x8 b0, bf16x8 b1) {
+  f32x4 d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b0, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b1, d, 0, 0, 0);
 }
 }  // namespace
 
-typedef __attribute__((ext_vector_type(2))) float f32x2;
-
-// thread t owns the adjacent channels (2t, 2t+1): the two convolutions run as packed fp32 FMAs on one
-// broadcast sample, and the pair is stored as one 32-bit word
-__global__ __launch_bounds__(256) void wavlm_conv0_stats_kernel(int S, int Lout, const float* __restrict__ wav,
-                                                                const float* __restrict__ w,
-                                                                float* __restrict__ part) {
-  __shared__ float xs[C0_TS * C0_ST + C0_KW];
-  const int b = blockIdx.y, t0 = blockIdx.x * C0_TS;
-  conv0_tile_load(wav + (long)b * S, S, t0, xs);
-  const int c = 2 * threadIdx.x;
-  f32x2 wr[C0_KW];
+// A fragments of the split weights, once per call: wfrag[(g16 * 2 + m) * 64 + lane] = 8 bf16 of channel
+// 16 g16 + (lane & 15), K slots 32m + 8(lane>>4) .. +7.  Grid 32 (16-channel groups) x 128 threads.
+__global__ __launch_bounds__(128) void wavlm_conv0_wfrag_kernel(const float* __restrict__ w,
+                                                                bf16x8* __restrict__ wfrag) {
+  const int m = threadIdx.x >> 6, lane = threadIdx.x & 63, c = blockIdx.x * 16 + (lane & 15);
+  uint32_t u[4];
 #pragma unroll
-  for (int k = 0; k < C0_KW; ++k) wr[k] = f32x2{w[c * C0_KW + k], w[(c + 1) * C0_KW + k]};
-  __syncthreads();
-  // 4 time steps per iteration on 4 independent accumulator pairs (the sums are otherwise one serial chain);
-  // the partial sums are combined in a fixed order, so the statistics stay deterministic
-  f32x2 s[4], q[4];
+  for (int p = 0; p < 4; ++p) {
+    bf16_t v[2];
 #pragma unroll
-  for (int u = 0; u < 4; ++u) s[u] = q[u] = f32x2{0.f, 0.f};
-  const int tn = min(C0_TS, Lout - t0);
-  for (int tt = 0; tt < tn; tt += 4) {
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      if (tt + u < tn) {
-        f32x2 a = {0.f, 0.f};
-#pragma unroll
-        for (int k = 0; k < C0_KW; ++k) a += wr[k] * xs[(tt + u) * C0_ST + k];
-        const f32x2 r = {bf2f(f2bf(a[0])), bf2f(f2bf(a[1]))};
-        s[u] += r;
-        q[u] += r * r;
+    for (int e = 0; e < 2; ++e) {
+      const int k = 32 * m + 8 * (lane >> 4) + 2 * p + e, t = k / 10, j = k - 10 * t;
+      v[e] = 0;
+      if (t < 6) {
+        bf16_t pl[3];
+        split3(w[c * C0_KW + j], pl[0], pl[1], pl[2]);
+        v[e] = pl[c0_wplane(t)];
       }
     }
+    u[p] = (uint32_t)v[0] | ((uint32_t)v[1] << 16);
   }
-  const f32x2 st = (s[0] + s[1]) + (s[2] + s[3]), qt = (q[0] + q[1]) + (q[2] + q[3]);
-  float* pr = part + ((long)b * gridDim.x + blockIdx.x) * 1024;
-  *reinterpret_cast<f32x4*>(pr + c * 2) = f32x4{st[0], qt[0], st[1], qt[1]};
+  wfrag[(blockIdx.x * 2 + m) * 64 + lane] = __builtin_bit_cast(bf16x8, u32x4{u[0], u[1], u[2], u[3]});
 }
 
-// coef[b][c] = (scale, shift) of GroupNorm from the tile partials, summed in tile order
+// pass 1: per-tile (sum, sumsq) of the bf16-rounded conv outputs per channel.  Wave w, channel group cb
+// (16 channels) outer, the tile's 8 column blocks of 16 time steps inner; a lane sums its 4 channels over its
+// 8 time steps, then the 16 lanes of a channel quad meet in a fixed xor tree (deterministic)
+__global__ __launch_bounds__(256) void wavlm_conv0_stats_kernel(int S, int Lout, const float* __restrict__ wav,
+                                                                const bf16x8* __restrict__ wfrag,
+                                                                float* __restrict__ part) {
+  __shared__ bf16_t xs3[C0_ZERO + 2];
+  const int b = blockIdx.y, t0 = blockIdx.x * C0_TS, wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  conv0_tile_split(wav + (long)b * S, S, t0, xs3);
+  C0Gather gt;
+  gt.init(lane);
+  const int tn = min(C0_TS, Lout - t0);
+  __syncthreads();
+  bf16x8 bq[8][2];
+#pragma unroll
+  for (int tb = 0; tb < 8; ++tb) gt.load(xs3, 16 * tb + (lane & 15), bq[tb][0], bq[tb][1]);
+  float* pr = part + ((long)b * gridDim.x + blockIdx.x) * 1024;
+  const bf16x8* wf = wfrag + wv * 8 * 2 * 64 + lane;
+  bf16x8 an[2] = {wf[0], wf[64]};  // the next channel group's A fragments, one group ahead
+  for (int cb = 0; cb < 8; ++cb) {
+    const bf16x8 af[2] = {an[0], an[1]};
+    if (cb + 1 < 8) {
+      an[0] = wf[(cb + 1) * 128];
+      an[1] = wf[(cb + 1) * 128 + 64];
+    }
+    f32x4 s = {0.f, 0.f, 0.f, 0.f}, q = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int tb = 0; tb < 8; ++tb) {
+      const f32x4 d = c0_mfma(af, bq[tb][0], bq[tb][1]);
+      const float vm = 16 * tb + (lane & 15) < tn ? 1.f : 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float v = bf2f(f2bf(d[r])) * vm;
+        s[r] += v;
+        q[r] += v * v;
+      }
+    }
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        s[r] += __shfl_xor(s[r], o, 64);
+        q[r] += __shfl_xor(q[r], o, 64);
+      }
+    if ((lane & 15) == 0) {
+      const int c = wv * 128 + cb * 16 + 4 * (lane >> 4);
+      *reinterpret_cast<f32x4*>(pr + c * 2) = f32x4{s[0], q[0], s[1], q[1]};
+      *reinterpret_cast<f32x4*>(pr + c * 2 + 4) = f32x4{s[2], q[2], s[3], q[3]};
+    }
+  }
+}
+
+// coef[b][c] = (scale, shift) of GroupNorm from the tile partials.  Block = 64 channels of one clip; thread
+// (quarter qt, channel) sums tiles qt, qt+4, ... with 4 loads in flight, the quarters meet in LDS in order
+// (fixed order: deterministic)
 __global__ __launch_bounds__(256) void wavlm_gn_finalize_kernel(int ntiles, int Lout, const float* __restrict__ part,
                                                                 const float* __restrict__ gamma,
                                                                 const float* __restrict__ beta, float eps,
                                                                 float* __restrict__ coef) {
-  const int b = blockIdx.y, c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= 512) return;
-  const float* p = part + (long)b * ntiles * 1024 + c * 2;
-  float s = 0.f, q = 0.f;
-  for (int t = 0; t < ntiles; ++t) {
-    s += p[(long)t * 1024];
-    q += p[(long)t * 1024 + 1];
+  __shared__ float2 red[4][64];
+  const int b = blockIdx.y, cl = threadIdx.x & 63, qt = threadIdx.x >> 6, c = blockIdx.x * 64 + cl;
+  const float2* p = reinterpret_cast<const float2*>(part + (long)b * ntiles * 1024) + c;
+  float2 a[4] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};
+  int t = qt;
+  for (; t + 12 < ntiles; t += 16)
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const float2 v = p[(long)(t + 4 * u) * 512];
+      a[u].x += v.x;
+      a[u].y += v.y;
+    }
+  for (; t < ntiles; t += 4) {
+    const float2 v = p[(long)t * 512];
+    a[0].x += v.x;
+    a[0].y += v.y;
   }
+  red[qt][cl] = float2{(a[0].x + a[1].x) + (a[2].x + a[3].x), (a[0].y + a[1].y) + (a[2].y + a[3].y)};
+  __syncthreads();
+  if (qt != 0) return;
+  const float s = (red[0][cl].x + red[1][cl].x) + (red[2][cl].x + red[3][cl].x);
+  const float q = (red[0][cl].y + red[1][cl].y) + (red[2][cl].y + red[3][cl].y);
   const float mu = s / Lout;
   const float var = fmaxf(q / Lout - mu * mu, 0.f);
   const float sc = rsqrtf(var + eps) * gamma[c];
@@ -86,29 +196,44 @@ __global__ __launch_bounds__(256) void wavlm_gn_finalize_kernel(int ntiles, int 
   coef[((long)b * 512 + c) * 2 + 1] = beta[c] - mu * sc;
 }
 
+// pass 2: conv recompute, GroupNorm affine, GELU, one bf16 write.  Column block (16 time steps) outer so each
+// wave finishes its 256-byte row segments of 16 output rows back to back; the (scale, shift) table of the
+// clip's 512 channels sits in LDS
 __global__ __launch_bounds__(256) void wavlm_conv0_gn_gelu_kernel(int S, int Lout, const float* __restrict__ wav,
-                                                                  const float* __restrict__ w,
+                                                                  const bf16x8* __restrict__ wfrag,
                                                                   const float* __restrict__ coef,
                                                                   bf16_t* __restrict__ out) {
-  __shared__ float xs[C0_TS * C0_ST + C0_KW];
-  const int b = blockIdx.y, t0 = blockIdx.x * C0_TS;
-  conv0_tile_load(wav + (long)b * S, S, t0, xs);
-  const int c = 2 * threadIdx.x;
-  f32x2 wr[C0_KW];
+  __shared__ bf16_t xs3[C0_ZERO + 2];
+  __shared__ f32x4 cf[256];  // (scale, shift) of channels 2i, 2i+1
+  const int b = blockIdx.y, t0 = blockIdx.x * C0_TS, wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  conv0_tile_split(wav + (long)b * S, S, t0, xs3);
+  cf[threadIdx.x] = reinterpret_cast<const f32x4*>(coef + (long)b * 1024)[threadIdx.x];
+  C0Gather gt;
+  gt.init(lane);
+  bf16x8 af[8][2];
 #pragma unroll
-  for (int k = 0; k < C0_KW; ++k) wr[k] = f32x2{w[c * C0_KW + k], w[(c + 1) * C0_KW + k]};
-  const f32x4 cf = *reinterpret_cast<const f32x4*>(coef + (long)b * 1024 + c * 2);
-  const f32x2 sc = {cf[0], cf[2]}, sh = {cf[1], cf[3]};
-  __syncthreads();
+  for (int cb = 0; cb < 8; ++cb) {
+    af[cb][0] = wfrag[((wv * 8 + cb) * 2) * 64 + lane];
+    af[cb][1] = wfrag[((wv * 8 + cb) * 2 + 1) * 64 + lane];
+  }
   const int tn = min(C0_TS, Lout - t0);
-  uint32_t* o = reinterpret_cast<uint32_t*>(out + ((long)b * Lout + t0) * 512 + c);
-#pragma unroll 4
-  for (int tt = 0; tt < tn; ++tt) {
-    f32x2 a = {0.f, 0.f};
+  __syncthreads();
+  for (int tb = 0; tb < 8; ++tb) {
+    const int tl = 16 * tb + (lane & 15);
+    bf16x8 b0, b1;
+    gt.load(xs3, tl, b0, b1);
+    bf16_t* orow = out + ((long)b * Lout + t0 + tl) * 512 + wv * 128 + 4 * (lane >> 4);
 #pragma unroll
-    for (int k = 0; k < C0_KW; ++k) a += wr[k] * xs[tt * C0_ST + k];
-    const f32x2 z = f32x2{bf2f(f2bf(a[0])), bf2f(f2bf(a[1]))} * sc + sh;
-    o[(long)tt * 256] = (uint32_t)f2bf(gelu_erf(z[0])) | ((uint32_t)f2bf(gelu_erf(z[1])) << 16);
+    for (int cb = 0; cb < 8; ++cb) {
+      const f32x4 d = c0_mfma(af[cb], b0, b1);
+      const int c2 = (wv * 128 + cb * 16 + 4 * (lane >> 4)) >> 1;  // channel pair index
+      const f32x4 p0 = cf[c2], p1 = cf[c2 + 1];                    // sc0 sh0 sc1 sh1 | sc2 sh2 sc3 sh3
+      const float y0 = gelu_erf(bf2f(f2bf(d[0])) * p0[0] + p0[1]), y1 = gelu_erf(bf2f(f2bf(d[1])) * p0[2] + p0[3]);
+      const float y2 = gelu_erf(bf2f(f2bf(d[2])) * p1[0] + p1[1]), y3 = gelu_erf(bf2f(f2bf(d[3])) * p1[2] + p1[3]);
+      if (tl < tn)
+        *reinterpret_cast<uint2*>(orow + cb * 16) = uint2{(uint32_t)f2bf(y0) | ((uint32_t)f2bf(y1) << 16),
+                                                          (uint32_t)f2bf(y2) | ((uint32_t)f2bf(y3) << 16)};
+    }
   }
 }
 
@@ -118,10 +243,12 @@ MER_API int mer_wavlm_conv0_gn_gelu(int B, int S, int Lout, const float* wav, co
   const int ntiles = (Lout + C0_TS - 1) / C0_TS;
   float* part = workspace;                             // [B][ntiles][512][2]
   float* coef = workspace + (long)B * ntiles * 1024;   // [B][512][2]
+  bf16x8* wfrag = reinterpret_cast<bf16x8*>(coef + (long)B * 1024);  // [32][2][64] split weight fragments
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(wavlm_conv0_stats_kernel, dim3(ntiles, B), dim3(256), 0, st, S, Lout, wav, w0, part);
-  hipLaunchKernelGGL(wavlm_gn_finalize_kernel, dim3(2, B), dim3(256), 0, st, ntiles, Lout, part, gamma, beta, eps, coef);
-  hipLaunchKernelGGL(wavlm_conv0_gn_gelu_kernel, dim3(ntiles, B), dim3(256), 0, st, S, Lout, wav, w0, coef,
+  hipLaunchKernelGGL(wavlm_conv0_wfrag_kernel, dim3(32), dim3(128), 0, st, w0, wfrag);
+  hipLaunchKernelGGL(wavlm_conv0_stats_kernel, dim3(ntiles, B), dim3(256), 0, st, S, Lout, wav, wfrag, part);
+  hipLaunchKernelGGL(wavlm_gn_finalize_kernel, dim3(8, B), dim3(256), 0, st, ntiles, Lout, part, gamma, beta, eps, coef);
+  hipLaunchKernelGGL(wavlm_conv0_gn_gelu_kernel, dim3(ntiles, B), dim3(256), 0, st, S, Lout, wav, wfrag, coef,
                      (bf16_t*)out);
   MER_LAUNCH_CHECK();
 }

@@ -391,7 +391,7 @@ def wavlm_conv0_gn_gelu(wav, w0, gamma, beta, out, eps=1e-5):
     Lout = out.shape[1]
     if tuple(out.shape) != (B, (S - 10) // 5 + 1, 512) or out.dtype != torch.bfloat16:
         raise ValueError(f"wavlm_conv0_gn_gelu out {tuple(out.shape)}")
-    ws = torch.empty(B * ((Lout + 127) // 128 + 1) * 1024, device=wav.device, dtype=torch.float32)
+    ws = torch.empty(B * ((Lout + 127) // 128 + 1) * 1024 + 16384, device=wav.device, dtype=torch.float32)
     LIB("mer_wavlm_conv0_gn_gelu", B, S, Lout, wav.data_ptr(), w0.data_ptr(), gamma.data_ptr(), beta.data_ptr(),
         float(eps), ws.data_ptr(), out.data_ptr(), stream_ptr())
 

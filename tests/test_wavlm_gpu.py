@@ -79,9 +79,10 @@ def test_gemm_bf16_shapes_vs_fp32():
         assert err < 2e-2 * max(1.0, (Kd / 64) ** 0.5), (M, N, Kd, err)
 
 
-@pytest.mark.parametrize("variant", list(range(15)))
+@pytest.mark.parametrize("variant", list(range(21)))
 def test_gemm_bf16_variants(variant):
-    """Every GEMM kernel variant (register-staged 128^2, glds-pipelined 256^2 / 256x128 / 128^2) on ragged
+    """Every GEMM kernel variant (register-staged 128^2, glds-pipelined 256^2 / 256x128 / 128^2, split A/B rings,
+    the 4-phase and the ping-pong 256^2 kernels) on ragged
     shapes and in Conv1d 'rows' mode, vs fp32 torch on the same bf16 operands."""
     from multimodalemotionrecognition_amd import kernels as K
 

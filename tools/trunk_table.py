@@ -1,9 +1,11 @@
 """Per-layer table of the ResNet18 trunk (fwd conv, dgrad, wgrad) from a rocprofv3 kernel trace of bench.py:
 layer, GEMM shape (M x N x K), us per launch, TF/s -- one steady-state step, launches labelled by the trunk's
 fixed launch order (video.py: forward stem + per block conv1, conv2, [downsample]; backward per block in
-reverse: wgrad conv2, dgrad conv2, wgrad conv1, [wgrad ds, dgrad ds], dgrad conv1; stem wgrad last).
+reverse: wgrad conv2, dgrad conv2, wgrad conv1, [wgrad ds], dgrad conv1 (with the downsample's dgrad fused in,
+video.FUSED_DS_DGRAD; MER_TRUNK_UNFUSED_DS=1 for traces of the two-launch form); stem wgrad last).
     python tools/trunk_table.py <run_kernel_trace.csv> [train_steps_in_trace] > profiles/<round>/trunk_table.txt"""
 import csv
+import os
 import sys
 
 NIMG, H = 256, 112  # B=32 clips x 8 frames, 112x112
@@ -25,19 +27,27 @@ def trunk_convs():
     return convs
 
 
+FUSED_DS = os.environ.get("MER_TRUNK_UNFUSED_DS", "0") != "1"
+
+
 def backward_order(convs):
-    """(kind, conv) in the backward launch order."""
+    """(kind, conv, extra FLOPs) in the backward launch order."""
     blocks = {}
     for c in convs[1:]:
         blocks.setdefault(c[0].rsplit(".", 1)[0], {})[c[0].rsplit(".", 1)[1]] = c
     order = []
     for name in reversed(list(blocks)):
         b = blocks[name]
-        order += [("wgrad", b["conv2"]), ("dgrad", b["conv2"]), ("wgrad", b["conv1"])]
+        order += [("wgrad", b["conv2"], 0.0), ("dgrad", b["conv2"], 0.0), ("wgrad", b["conv1"], 0.0)]
         if "downsample" in b:
-            order += [("wgrad", b["downsample"]), ("dgrad", b["downsample"])]
-        order.append(("dgrad", b["conv1"]))
-    order.append(("wgrad", convs[0]))
+            ds, c1 = b["downsample"], b["conv1"]
+            order.append(("wgrad", ds, 0.0))
+            if FUSED_DS:  # one launch: conv1's dgrad with the downsample's as an extra K segment (FLOPs of both)
+                order.append(("dgrad", (c1[0] + "+ds",) + c1[1:], 2.0 * ds[1] * ds[2] * ds[3]))
+                continue
+            order.append(("dgrad", ds, 0.0))
+        order.append(("dgrad", b["conv1"], 0.0))
+    order.append(("wgrad", convs[0], 0.0))
     return order
 
 
@@ -63,9 +73,9 @@ def main():
         tot["fwd"] += us
         flops["fwd"] += f
         print(f"{c[0]:26s} {'fwd':6s} {c[1]:>9d}x{c[2]:>4d}x{c[3]:>5d} {us:8.1f} {f / us / 1e6:7.1f}  {r['Kernel_Name'][:60]}")
-    for (kind, c), r in zip(backward_order(convs), bwd):
+    for (kind, c, extra), r in zip(backward_order(convs), bwd):
         us = dur(r)
-        f = 2.0 * c[1] * c[2] * c[3]
+        f = 2.0 * c[1] * c[2] * c[3] + extra
         tot[kind] += us
         flops[kind] += f
         print(f"{c[0]:26s} {kind:6s} {c[1]:>9d}x{c[2]:>4d}x{c[3]:>5d} {us:8.1f} {f / us / 1e6:7.1f}  {r['Kernel_Name'][:60]}")
