@@ -224,6 +224,7 @@ struct WgradGeom {
   float* ws;              // [splits][K][R*S*C] fp32 partial slabs
   int pix_per_split;
   long ldy;               // dY row stride (elements; K for a conv, a column slice of a wider matrix for a Linear)
+  int flat;               // wgrad_pipe_kernel: 1-D grid of splits x tiles, a split's tiles on one XCD (see there)
 };
 
 template <int BM_, int BN_, int WM = 2, int WN = 2, int PF = 1>
@@ -413,10 +414,23 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void wgrad_pipe_kernel(WgradGeom g
   const int Ntot = g.R * g.S * g.C;
   const int P = g.N * g.Ho * g.Wo;
   const int wnx = (Ntot + BN_ - 1) / BN_, wny = (g.K + BM_ - 1) / BM_;
-  int wtx, wty;
-  xcd_tile(blockIdx.x, wnx, wnx * wny, wtx, wty);
+  int wtx, wty, zs;
+  if (g.flat) {
+    // Every tile of one split reads the same pixel range (dY rows and, for an R x S conv, R*S shifted windows of X
+    // rows).  Split-major over the bijective XCD chunks (xcd_tile on the flattened (split, tile) index): an XCD runs
+    // whole splits, so their tiles fetch the rows into ITS L2 once.  With the z grid the T tiles of a split went
+    // to T different XCDs (linear dispatch order round-robins XCDs) and each re-fetched the rows from HBM:
+    // layer1's 3x3 wgrad read 244 MB per launch for 51 MB of operands (gpurun_out/pmcstep).
+    int tile;
+    xcd_tile(blockIdx.x, wnx * wny, (int)gridDim.x, tile, zs);
+    wty = tile / wnx;
+    wtx = tile - wty * wnx;
+  } else {
+    xcd_tile(blockIdx.x, wnx, wnx * wny, wtx, wty);
+    zs = blockIdx.z;
+  }
   const int m0 = wty * BM_, n0 = wtx * BN_;
-  const int p_beg = blockIdx.z * g.pix_per_split, p_end = min(P, p_beg + g.pix_per_split);
+  const int p_beg = zs * g.pix_per_split, p_end = min(P, p_beg + g.pix_per_split);
   const int wm = (w / WN) * (BM_ / WM), wn = (w % WN) * (BN_ / WN);
   const bf16_t* zero = reinterpret_cast<const bf16_t*>(mer_conv_zero16);
 
@@ -515,7 +529,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void wgrad_pipe_kernel(WgradGeom g
       __builtin_amdgcn_s_setprio(0);
     }
   }
-  float* slab = g.ws + (long)blockIdx.z * g.K * Ntot;
+  float* slab = g.ws + (long)zs * g.K * Ntot;
 #pragma unroll
   for (int i = 0; i < IT; ++i)
 #pragma unroll
@@ -531,12 +545,19 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void wgrad_pipe_kernel(WgradGeom g
 }
 
 template <int BM_, int BN_, int WM, int WN, int STAGES, int KS = 64>
-void launch_wgrad_pipe(const WgradGeom& g, dim3 grid, hipStream_t st) {
+void launch_wgrad_pipe(const WgradGeom& g0, dim3 grid, hipStream_t st) {
   const size_t lds = (size_t)STAGES * KS * (BM_ + BN_) * sizeof(bf16_t);
   if (hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_pipe_kernel<BM_, BN_, WM, WN, STAGES, KS>),
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return;
-  hipLaunchKernelGGL((wgrad_pipe_kernel<BM_, BN_, WM, WN, STAGES, KS>), grid, dim3(64 * WM * WN), lds, st, g);
+  static const bool flat_on = [] {  // MER_WGRAD_XCD=0: the z grid (tiles of a split on different XCDs), A/B
+    const char* e = getenv("MER_WGRAD_XCD");
+    return !(e && e[0] == '0');
+  }();
+  WgradGeom g = g0;
+  g.flat = flat_on ? 1 : 0;
+  const dim3 gr = flat_on ? dim3(grid.x * grid.z, 1, 1) : grid;
+  hipLaunchKernelGGL((wgrad_pipe_kernel<BM_, BN_, WM, WN, STAGES, KS>), gr, dim3(64 * WM * WN), lds, st, g);
 }
 
 // slab0[i] = sum_z ws[z][i] over the flat [K][R*S*C] index.  A block owns E = 256/SG consecutive elements
@@ -644,12 +665,26 @@ struct FoldTable {
 
 __global__ __launch_bounds__(256) void wgrad_fold_batch_kernel(FoldTable t) {
   __shared__ float part[256];
+  // Blocks in XCD chunks (xcd_tile's bijective map: consecutive virtual ids v on one XCD), and inside a record the
+  // R*S taps of one (k, channel block) on consecutive v: the ~R*S blocks whose sums land in the same 128-byte lines
+  // of dw[k][c][r][s] (stride R*S between channels) run on one XCD, so a line is completed in ONE L2 instead of
+  // being written back partially from up to 8 (the slab-order grid wrote ~4x dw's bytes, gpurun_out/pmcstep).
+  int v, unused;
+  xcd_tile(blockIdx.x, 1 << 30, (int)gridDim.x, v, unused);
   int ri = 0;
-  while (ri + 1 < t.n && (int)blockIdx.x >= t.r[ri + 1].blk0) ++ri;
+  while (ri + 1 < t.n && v >= t.r[ri + 1].blk0) ++ri;
   const FoldRec& R = t.r[ri];
   const int SG = R.SG, E = 256 / SG, e = threadIdx.x % E, sg = threadIdx.x / E;
   const long row = (long)R.RS * R.C, total = (long)R.K * row;
-  const long idx = (long)((int)blockIdx.x - R.blk0) * E + e;
+  const int lb = v - R.blk0;
+  long idx;
+  if (!R.map && R.C % E == 0) {  // lb -> (k, channel block cb, tap), tap fastest
+    const int CB = R.C / E, per_k = R.RS * CB;
+    const int k = lb / per_k, rem = lb - k * per_k, cb = rem / R.RS, tap = rem - cb * R.RS;
+    idx = (long)k * row + (long)tap * R.C + cb * E + e;
+  } else {
+    idx = (long)lb * E + e;
+  }
   float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
   if (idx < total) {
     const float* src = R.ws + idx;

@@ -878,6 +878,14 @@ int launch_pipe(const GemmArgs& g, int out_dtype, hipStream_t st, int groups = 1
 int pick_variant(int M, int N, int K) {
   const long tl = (long)((M + 255) / 256) * ((N + 255) / 256);
   if (tl >= 1200 && N <= 512) return 18;
+  // the middle feature-extractor convs (conv2..conv4: 600 / 300 / 150 tiles of 256^2): the 16-wave 256^2 ring, not
+  // 128^2 tiles (tools/bench_gemm.py, gpurun_out/gsmall: conv2 163 -> 128 us, conv3 83 -> 80, conv4 45 -> 40).
+  // MER_GEMM_CONVMID=0 restores the 128^2 pick (A/B)
+  static const bool convmid = [] {
+    const char* e = getenv("MER_GEMM_CONVMID");
+    return !(e && e[0] == '0');
+  }();
+  if (convmid && N <= 512 && tl >= 150 && tl < 1200) return 13;
   if (tl >= 160 && !(N <= 512 && tl < 1200)) return 13;
   return K >= 2048 ? 7 : 9;
 }

@@ -160,35 +160,22 @@ __global__ __launch_bounds__(256) void wavlm_conv0_stats_kernel(int S, int Lout,
   }
 }
 
-// coef[b][c] = (scale, shift) of GroupNorm from the tile partials.  Block = 64 channels of one clip; thread
-// (quarter qt, channel) sums tiles qt, qt+4, ... with 4 loads in flight, the quarters meet in LDS in order
-// (fixed order: deterministic)
-__global__ __launch_bounds__(256) void wavlm_gn_finalize_kernel(int ntiles, int Lout, const float* __restrict__ part,
-                                                                const float* __restrict__ gamma,
-                                                                const float* __restrict__ beta, float eps,
-                                                                float* __restrict__ coef) {
-  __shared__ float2 red[4][64];
-  const int b = blockIdx.y, cl = threadIdx.x & 63, qt = threadIdx.x >> 6, c = blockIdx.x * 64 + cl;
+// coef[b][c] = (scale, shift) of GroupNorm from the tile partials, summed in tile order (one serial chain per
+// channel: the statistics feed a test whose score-path gradients are rounding-chaotic, so the order stays
+// fixed); one wave per 64 channels, the loads unrolled so a chain's operands are in flight together
+__global__ __launch_bounds__(64) void wavlm_gn_finalize_kernel(int ntiles, int Lout, const float* __restrict__ part,
+                                                               const float* __restrict__ gamma,
+                                                               const float* __restrict__ beta, float eps,
+                                                               float* __restrict__ coef) {
+  const int b = blockIdx.y, c = blockIdx.x * 64 + threadIdx.x;
   const float2* p = reinterpret_cast<const float2*>(part + (long)b * ntiles * 1024) + c;
-  float2 a[4] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};
-  int t = qt;
-  for (; t + 12 < ntiles; t += 16)
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const float2 v = p[(long)(t + 4 * u) * 512];
-      a[u].x += v.x;
-      a[u].y += v.y;
-    }
-  for (; t < ntiles; t += 4) {
+  float s = 0.f, q = 0.f;
+#pragma unroll 16
+  for (int t = 0; t < ntiles; ++t) {
     const float2 v = p[(long)t * 512];
-    a[0].x += v.x;
-    a[0].y += v.y;
+    s += v.x;
+    q += v.y;
   }
-  red[qt][cl] = float2{(a[0].x + a[1].x) + (a[2].x + a[3].x), (a[0].y + a[1].y) + (a[2].y + a[3].y)};
-  __syncthreads();
-  if (qt != 0) return;
-  const float s = (red[0][cl].x + red[1][cl].x) + (red[2][cl].x + red[3][cl].x);
-  const float q = (red[0][cl].y + red[1][cl].y) + (red[2][cl].y + red[3][cl].y);
   const float mu = s / Lout;
   const float var = fmaxf(q / Lout - mu * mu, 0.f);
   const float sc = rsqrtf(var + eps) * gamma[c];
@@ -247,7 +234,7 @@ MER_API int mer_wavlm_conv0_gn_gelu(int B, int S, int Lout, const float* wav, co
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(wavlm_conv0_wfrag_kernel, dim3(32), dim3(128), 0, st, w0, wfrag);
   hipLaunchKernelGGL(wavlm_conv0_stats_kernel, dim3(ntiles, B), dim3(256), 0, st, S, Lout, wav, wfrag, part);
-  hipLaunchKernelGGL(wavlm_gn_finalize_kernel, dim3(8, B), dim3(256), 0, st, ntiles, Lout, part, gamma, beta, eps, coef);
+  hipLaunchKernelGGL(wavlm_gn_finalize_kernel, dim3(8, B), dim3(64), 0, st, ntiles, Lout, part, gamma, beta, eps, coef);
   hipLaunchKernelGGL(wavlm_conv0_gn_gelu_kernel, dim3(ntiles, B), dim3(256), 0, st, S, Lout, wav, wfrag, coef,
                      (bf16_t*)out);
   MER_LAUNCH_CHECK();
@@ -291,6 +278,13 @@ __global__ __launch_bounds__(256) void layernorm_kernel(int rows, int d, const T
   float s = 0.f;
   if (VEC) {
     const int nv = d >> 8;
+    f32x4 gv[4], bv[4];  // issued with the row loads: their latency overlaps the row's, not the reductions'
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (i >= nv) break;
+      gv[i] = *reinterpret_cast<const f32x4*>(gamma + (i * 64 + lane) * 4);
+      bv[i] = *reinterpret_cast<const f32x4*>(beta + (i * 64 + lane) * 4);
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       if (i >= nv) break;
@@ -306,7 +300,7 @@ __global__ __launch_bounds__(256) void layernorm_kernel(int rows, int d, const T
     for (int i = 0; i < 4; ++i) {
       if (i >= nv) break;
       const int c = (i * 64 + lane) * 4;
-      const f32x4 g = *reinterpret_cast<const f32x4*>(gamma + c), b = *reinterpret_cast<const f32x4*>(beta + c);
+      const f32x4 g = gv[i], b = bv[i];
       f32x4 o;
 #pragma unroll
       for (int e = 0; e < 4; ++e) o[e] = (vals[4 * i + e] - mean) * rstd * g[e] + b[e];
