@@ -2240,7 +2240,11 @@ __global__ void maxpool_bwd_kernel(int N, int H, int W, int C, int Ho, int Wo, c
   const int cpr = C / 8;
   const int total = N * H * W * cpr;
   const float inv_cpr = 1.f / cpr, inv_W = 1.f / W, inv_H = 1.f / H;
-  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
+  // consecutive (virtual) blocks on one XCD: neighbouring output rows read the same pooled rows, so they should
+  // share an L2 (round-robin block placement fetched every pooled row ~4x, gpurun_out/pmcstep)
+  int vb, unused;
+  xcd_tile(blockIdx.x, 1 << 30, (int)gridDim.x, vb, unused);
+  for (int e = vb * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
     const int q = fdiv(e, inv_cpr);
     const int c0 = (e - q * cpr) * 8;
     const int q2 = fdiv(q, inv_W);
@@ -2309,7 +2313,9 @@ __global__ void stem_bnrelu_maxpool_kernel(int N, int H, int W, int C, int Ho, i
   const int cpr = C / 8;
   const int total = N * Ho * Wo * cpr;
   const float inv_cpr = 1.f / cpr, inv_Wo = 1.f / Wo, inv_Ho = 1.f / Ho;
-  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
+  int vb, unused;  // XCD-contiguous blocks: adjacent pooled rows share input rows (maxpool_bwd_kernel)
+  xcd_tile(blockIdx.x, 1 << 30, (int)gridDim.x, vb, unused);
+  for (int e = vb * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
     const int q = fdiv(e, inv_cpr);
     const int c0 = (e - q * cpr) * 8;
     const int q2 = fdiv(q, inv_Wo);
