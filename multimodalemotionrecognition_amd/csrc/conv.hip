@@ -665,26 +665,14 @@ struct FoldTable {
 
 __global__ __launch_bounds__(256) void wgrad_fold_batch_kernel(FoldTable t) {
   __shared__ float part[256];
-  // Blocks in XCD chunks (xcd_tile's bijective map: consecutive virtual ids v on one XCD), and inside a record the
-  // R*S taps of one (k, channel block) on consecutive v: the ~R*S blocks whose sums land in the same 128-byte lines
-  // of dw[k][c][r][s] (stride R*S between channels) run on one XCD, so a line is completed in ONE L2 instead of
-  // being written back partially from up to 8 (the slab-order grid wrote ~4x dw's bytes, gpurun_out/pmcstep).
-  int v, unused;
-  xcd_tile(blockIdx.x, 1 << 30, (int)gridDim.x, v, unused);
+  // (Slab order over round-robin blocks.  Tap-major blocks in XCD chunks -- the R*S blocks writing the same dw lines
+  // on one L2 -- cut the HBM writes 101 -> 21 MB per launch but ran 99 -> 107 us: DESIGN.md section 4e''.)
   int ri = 0;
-  while (ri + 1 < t.n && v >= t.r[ri + 1].blk0) ++ri;
+  while (ri + 1 < t.n && (int)blockIdx.x >= t.r[ri + 1].blk0) ++ri;
   const FoldRec& R = t.r[ri];
   const int SG = R.SG, E = 256 / SG, e = threadIdx.x % E, sg = threadIdx.x / E;
   const long row = (long)R.RS * R.C, total = (long)R.K * row;
-  const int lb = v - R.blk0;
-  long idx;
-  if (!R.map && R.C % E == 0) {  // lb -> (k, channel block cb, tap), tap fastest
-    const int CB = R.C / E, per_k = R.RS * CB;
-    const int k = lb / per_k, rem = lb - k * per_k, cb = rem / R.RS, tap = rem - cb * R.RS;
-    idx = (long)k * row + (long)tap * R.C + cb * E + e;
-  } else {
-    idx = (long)lb * E + e;
-  }
+  const long idx = (long)((int)blockIdx.x - R.blk0) * E + e;
   float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
   if (idx < total) {
     const float* src = R.ws + idx;
@@ -2240,11 +2228,9 @@ __global__ void maxpool_bwd_kernel(int N, int H, int W, int C, int Ho, int Wo, c
   const int cpr = C / 8;
   const int total = N * H * W * cpr;
   const float inv_cpr = 1.f / cpr, inv_W = 1.f / W, inv_H = 1.f / H;
-  // consecutive (virtual) blocks on one XCD: neighbouring output rows read the same pooled rows, so they should
-  // share an L2 (round-robin block placement fetched every pooled row ~4x, gpurun_out/pmcstep)
-  int vb, unused;
-  xcd_tile(blockIdx.x, 1 << 30, (int)gridDim.x, vb, unused);
-  for (int e = vb * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
+  // (XCD-contiguous blocks cut this kernel's HBM fetch 165 -> 37 MB but made it SLOWER, 49 -> 55 us: the
+  // round-robin placement keeps the whole chip on one sequential stream; DESIGN.md section 4e'')
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
     const int q = fdiv(e, inv_cpr);
     const int c0 = (e - q * cpr) * 8;
     const int q2 = fdiv(q, inv_W);
@@ -2313,9 +2299,7 @@ __global__ void stem_bnrelu_maxpool_kernel(int N, int H, int W, int C, int Ho, i
   const int cpr = C / 8;
   const int total = N * Ho * Wo * cpr;
   const float inv_cpr = 1.f / cpr, inv_Wo = 1.f / Wo, inv_Ho = 1.f / Ho;
-  int vb, unused;  // XCD-contiguous blocks: adjacent pooled rows share input rows (maxpool_bwd_kernel)
-  xcd_tile(blockIdx.x, 1 << 30, (int)gridDim.x, vb, unused);
-  for (int e = vb * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
     const int q = fdiv(e, inv_cpr);
     const int c0 = (e - q * cpr) * 8;
     const int q2 = fdiv(q, inv_Wo);
