@@ -869,9 +869,10 @@ int launch_pipe(const GemmArgs& g, int out_dtype, hipStream_t st, int groups = 1
 // hides the DMA latency of this 2-deep pipeline, so the 16-wave 256x256 tile wins wherever its grid covers
 // most of the 256 CUs (conv1/conv2 as GEMMs, QKV, FFN-up: 0.80 / 0.82 / 0.49 / 0.64 PF); the 768-column
 // GEMMs have too few such tiles: FFN-down (K = 3072) runs 128x64 tiles with a 3-deep ring, the output
-// projection 128x128 tiles with 8 waves.  The 512-column feature-extractor convs below conv1 (300-600 such tiles,
-// 1.2-2.3 rounds of the 256 CUs) run faster on 128x128 tiles: conv2 134 -> 130 us, conv3 79 -> 69 us
-// (profiles/r02f/bench_gemm_convs.log; all variants bit-identical).
+// projection 128x128 tiles with 8 waves.  The 512-column feature-extractor convs below conv1 measured faster on
+// 128x128 tiles in round 2 (conv2 134 -> 130 us, conv3 79 -> 69 us, profiles/r02f/bench_gemm_convs.log) and slower
+// in round 4 (conv2 163 vs 128 us on the 256^2 ring, conv3 83 vs 80, conv4 45 vs 40, profiles/r04h/
+// bench_gemm_small_shapes.log); in the step the two are within noise (all variants bit-identical).
 // conv1 (1,200 tiles streaming a 314 MB A operand) takes the split ring (A three K-tiles deep, B two):
 // 278.6 -> 271.4 us; the same ring is 2-7 % slower on conv2 / conv3 / QKV / FFN-up / 4096^3
 // (profiles/r04/gemm_split_ring.log, all bit-identical).
@@ -1012,7 +1013,14 @@ MER_API int mer_posconv_gemm_bf16(int B, int L, int C_total, int groups, int tap
   g.bias = bias; g.R = (const bf16_t*)R; g.ldr = ldr; g.act = act;
   g.vec_epi = vec_epilogue_ok(cg, out, ldo, R, ldr, g.c_zoff);
   g.tgroup = 8;
-  if (g.K % 64 == 0 && (((uintptr_t)X | (uintptr_t)Wp) & 15) == 0)
+  static const int pc_cfg = [] {  // MER_POSCONV_CFG (A/B): 0 = 2-deep 128x64, 1 = 3-deep, 2 = 32-wide K on a 4-deep ring
+    const char* e = getenv("MER_POSCONV_CFG");
+    return e ? atoi(e) : 0;
+  }();
+  if (g.K % 64 == 0 && (((uintptr_t)X | (uintptr_t)Wp) & 15) == 0) {
+    if (pc_cfg == 1) return launch_pipe<CfgT3, 1>(g, out_dtype, (hipStream_t)stream, groups);
+    if (pc_cfg == 2) return launch_pipe<CfgT4, 1>(g, out_dtype, (hipStream_t)stream, groups);
     return launch_pipe<CfgP, 1>(g, out_dtype, (hipStream_t)stream, groups);
+  }
   return launch<1>(g, out_dtype, groups, (hipStream_t)stream);
 }

@@ -709,6 +709,7 @@ struct WgProb {
 struct WgTab {
   WgProb p[WG_MAXP];
   int nprob;
+  int xcd;  // split-major blocks in XCD chunks (xh_wgrad_kernel)
 };
 
 // Staging: thread t owns column (t & 127) of the 128-wide dY / X tile and 16 consecutive rows (t >> 7) * 16 ..
@@ -768,13 +769,19 @@ constexpr int WG_PLANE = WG_T * WG_LDM;  // bf16 elements per plane
 __global__ __launch_bounds__(512) void xh_wgrad_kernel(const WgTab tab, float* __restrict__ ws) {
   __shared__ __attribute__((aligned(16))) bf16_t planes[2][4][WG_PLANE];  // [group][yh, yl, xh, xl]
   __shared__ float bred[4][WG_T];
+  // tab.xcd: the tiles of one row split (same dY rows: every tile of a column block tn reads the same dY slice)
+  // on consecutive virtual ids of one XCD chunk (xcd_tile's bijective map), so the slice is fetched into one L2
+  // once instead of once per XCD the round-robin placement spread them over
+  int vb = blockIdx.x, unused;
+  if (tab.xcd) xcd_tile(blockIdx.x, 1 << 30, (int)gridDim.x, vb, unused);
   int pi = 0;
-  while (pi + 1 < tab.nprob && tab.p[pi + 1].first_block <= (int)blockIdx.x) ++pi;
+  while (pi + 1 < tab.nprob && tab.p[pi + 1].first_block <= vb) ++pi;
   const WgProb& d = tab.p[pi];
   const int N = d.N, K = d.K, splits = d.splits;
   const int ntk = K > 0 ? (K + WG_T - 1) / WG_T : 1;
-  const int local = blockIdx.x - d.first_block;
-  const int split = local % splits, tile = local / splits;
+  const int local = vb - d.first_block;
+  const int ntiles = ((N + WG_T - 1) / WG_T) * ntk;
+  const int split = tab.xcd ? local / ntiles : local % splits, tile = tab.xcd ? local - split * ntiles : local / splits;
   const int tn = tile / ntk, tk = tile - tn * ntk;
   const int n0 = tn * WG_T, k0 = tk * WG_T;
   const long per = (d.M + splits - 1) / splits, m0 = split * per, m1 = m0 + per < d.M ? m0 + per : d.M;
@@ -948,6 +955,11 @@ MER_API int mer_xh_wgrad(int nprob, const long long* table, float* ws, long long
   int blocks = 0;
   const long long need = wg_layout(nprob, table, &tab, &blocks);
   if (need < 0 || need > ws_floats) return (int)hipErrorInvalidValue;
+  static const int xcd_on = [] {  // MER_XH_WGRAD_XCD=0: tile-major round-robin order (A/B)
+    const char* e = getenv("MER_XH_WGRAD_XCD");
+    return (e && e[0] == '0') ? 0 : 1;
+  }();
+  tab.xcd = xcd_on;
   hipLaunchKernelGGL(xh_wgrad_kernel, dim3(blocks), dim3(512), 0, (hipStream_t)stream, tab, ws);
   // fold: one element per thread for the largest problem (each thread's split loads are one latency round, not
   // one per element it would otherwise loop over)

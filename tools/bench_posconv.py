@@ -1,0 +1,46 @@
+"""Time the WavLM positional conv (grouped Conv1d(768, 768, k=128, pad=64, groups=16) + bias + GELU + residual, TF:82-90)
+as mer_posconv_gemm_bf16 at B=32, L=149, one captured graph of back-to-back launches; MER_POSCONV_CFG selects the
+tile / ring (A/B).  python tools/bench_posconv.py"""
+import sys
+from pathlib import Path
+
+import torch
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+from multimodalemotionrecognition_amd import kernels as K  # noqa: E402
+
+B, L, C, G, TAPS, PAD = 32, 149, 768, 16, 128, 64
+
+
+def main():
+    torch.manual_seed(0)
+    cg = C // G
+    x = (torch.randn(B, L, C, device="cuda") * 0.5).bfloat16()
+    wp = (torch.randn(G, cg, TAPS * cg, device="cuda") * 0.02).bfloat16()
+    bias = torch.randn(C, device="cuda") * 0.1
+    out = torch.empty(B, L, C, device="cuda", dtype=torch.bfloat16)
+    for _ in range(3):
+        K.posconv_gemm_bf16(x, wp, out, B, L, C, G, TAPS, PAD, bias, x)
+    torch.cuda.synchronize()
+    reps = 20
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.graph(g, stream=s):
+        for _ in range(reps):
+            K.posconv_gemm_bf16(x, wp, out, B, L, C, G, TAPS, PAD, bias, x)
+    torch.cuda.current_stream().wait_stream(s)
+    g.replay()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    g.replay()
+    e1.record()
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) / reps * 1e3
+    flop = 2.0 * B * L * C * cg * TAPS
+    print(f"posconv B={B} L={L}: {us:.1f} us  {flop / us / 1e6:.1f} TF/s  checksum {float(out.float().sum()):.6e}")
+
+
+if __name__ == "__main__":
+    main()
