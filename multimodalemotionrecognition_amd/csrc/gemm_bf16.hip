@@ -1000,6 +1000,122 @@ MER_API int mer_gemm_bf16_tr(int M, int N, int K, const void* A, long a_gstride,
   }
 }
 
+namespace {
+// ---------------------------------------------------------------------------------------------------------------
+// Positional conv (grouped Conv1d(768, 768, k=128, pad=64, groups=16), TF:82-90) as a Toeplitz product.  The
+// implicit GEMM above gathers its A operand per K-tile from x[b, t + tap - pad, c]: with 128 taps every x row is
+// fetched 128 times through L2 (~0.94 GB of operand loads per launch for a 7 MB input), which bounded it at ~115 us
+// (380 TF/s).  Here one block owns one (clip, group): the clip's rows of that group's 48 channels are loaded ONCE
+// into an LDS strip of L + taps - 1 rows (zero rows for the padding), and the A fragment of tap j, time t is strip
+// row t + j -- the same 16 bytes the gather produced.  The weights stream through a double-buffered LDS chunk of
+// PS_KC k-columns.  Every output element accumulates the same bf16 fragments in the same k-block order on the same
+// MFMA as gemm_pipe_kernel<CfgP, 1>, and the epilogue is the same arithmetic (act(acc + bias) rounded through a
+// register, then + residual, then bf16), so the result is bit-identical (tests/test_wavlm_gpu.py).
+// Limits: L <= PS_MAXL, taps <= PS_MAXT, cg = CG (a multiple of 16), taps * CG % PS_KC == 0.
+constexpr int PS_MAXL = 160, PS_MAXT = 128, PS_KC = 192;
+
+template <int CG, int NW>
+__global__ __launch_bounds__(64 * NW, 2) void posconv_strip_kernel(int L, int taps, int pad, const bf16_t* __restrict__ X,
+                                                               long ldx, const bf16_t* __restrict__ Wp,
+                                                               bf16_t* __restrict__ out, long ldo,
+                                                               const float* __restrict__ bias,
+                                                               const bf16_t* __restrict__ R, long ldr, int act) {
+  // wave w owns M fragments w, w + NW, ... (16 time steps each): MI per wave, computed for every wave whether or not
+  // the clip has that many rows (branch-free fragment loop; rows past L are discarded by the epilogue), so the strip
+  // covers NW * MI fragments
+  constexpr int MI = (PS_MAXL / 16 + NW - 1) / NW;
+  constexpr int NF = CG / 16, CH = CG / 8, WROW = PS_KC + 8, SROWS = NW * MI * 16 + PS_MAXT;
+  constexpr int NT = 64 * NW;
+  constexpr int WCH = PS_KC / 8;  // 16-byte chunks per weight row of one K-chunk
+  constexpr int WIT = (CG * WCH + NT - 1) / NT;
+  __shared__ __attribute__((aligned(16))) bf16_t strip[SROWS * CG];
+  __shared__ __attribute__((aligned(16))) bf16_t wbuf[2][CG * WROW];
+  // grid (groups, clips): linear block id = clip * groups + group, so with groups % 8 == 0 every block of a group
+  // lands on the same XCD (ids round-robin over the 8 XCDs) and that XCD's L2 holds only its 2 groups' weights
+  // (2 x 590 KB) instead of all 16 (9.4 MB, more than the 4 MB L2: every chunk re-fetched)
+  const int z = blockIdx.x, b = blockIdx.y, t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int K = taps * CG, nkc = K / PS_KC;
+  const bf16_t* Xb = X + (long)b * L * ldx + (long)z * CG;
+  const bf16_t* Wz = Wp + (long)z * CG * K;
+  const u32x4 zero4 = {0u, 0u, 0u, 0u};
+  // strip row u = input time u - pad (zero outside the clip; rows past L + taps - 1 are zero too)
+  for (int i = t; i < SROWS * CH; i += NT) {
+    const int u = i / CH, ch = i - u * CH, tt = u - pad;
+    const bool ok = tt >= 0 && tt < L;
+    const u32x4 v = *reinterpret_cast<const u32x4*>(ok ? Xb + (long)tt * ldx + ch * 8 : Xb);
+    *reinterpret_cast<u32x4*>(strip + u * CG + ch * 8) = ok ? v : zero4;
+  }
+  // the next weight chunk in registers, loaded at the top of a chunk and stored to the other buffer at its end (two
+  // register sets loading two chunks ahead measured no faster: 77.5 vs 75.8 us)
+  u32x4 wr[WIT];
+  auto wload = [&](int kc) {
+#pragma unroll
+    for (int j = 0; j < WIT; ++j) {
+      const int i = t + NT * j, n = i / WCH, ch = i - n * WCH;
+      wr[j] = i < CG * WCH ? *reinterpret_cast<const u32x4*>(Wz + (long)n * K + kc * PS_KC + ch * 8) : zero4;
+    }
+  };
+  auto wstore = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < WIT; ++j) {
+      const int i = t + NT * j, n = i / WCH, ch = i - n * WCH;
+      if (i < CG * WCH) *reinterpret_cast<u32x4*>(wbuf[buf] + n * WROW + ch * 8) = wr[j];
+    }
+  };
+  const int nmf = (L + 15) / 16;
+  f32x4 acc[MI][NF];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NF; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int fr = lane & 15, fq = lane >> 4;
+  wload(0);
+  wstore(0);
+  __syncthreads();
+  for (int kc = 0; kc < nkc; ++kc) {
+    if (kc + 1 < nkc) wload(kc + 1);  // in flight across this chunk's MFMAs
+    const bf16_t* wb = wbuf[kc & 1];
+#pragma unroll
+    for (int kb = 0; kb < PS_KC / 32; ++kb) {
+      const int kl = kb * 32 + fq * 8, kg = kc * PS_KC + kl;
+      const int tap = kg / CG, c0 = kg - tap * CG;
+      bf16x8 bq[NF], af[MI];
+#pragma unroll
+      for (int j = 0; j < NF; ++j) bq[j] = *reinterpret_cast<const bf16x8*>(wb + (j * 16 + fr) * WROW + kl);
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+        af[i] = *reinterpret_cast<const bf16x8*>(strip + ((w + NW * i) * 16 + fr + tap) * CG + c0);
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NF; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bq[j], acc[i][j], 0, 0, 0);
+    }
+    if (kc + 1 < nkc) wstore((kc + 1) & 1);  // the other buffer: its last reader (chunk kc - 1) passed the barrier
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < MI; ++i) {
+    const int mf = w + NW * i;
+    if (mf >= nmf) break;
+#pragma unroll
+    for (int j = 0; j < NF; ++j) {
+      const int n = j * 16 + fr;
+      const float bv = bias ? bias[z * CG + n] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int tt = mf * 16 + fq * 4 + r;
+        if (tt >= L) continue;
+        float v = apply_act(acc[i][j][r] + bv, act);
+        asm volatile("" : "+v"(v));  // round to fp32 here, as the LDS-staged epilogue does: no fma with the add
+        const long row = (long)b * L + tt;
+        if (R) v += bf2f(R[row * ldr + z * CG + n]);
+        out[row * ldo + z * CG + n] = f2bf(v);
+      }
+    }
+  }
+}
+}  // namespace
+
 MER_API int mer_posconv_gemm_bf16(int B, int L, int C_total, int groups, int taps, int pad, const void* X, long ldx,
                                   const void* Wp, void* out, int out_dtype, long ldo, const float* bias,
                                   const void* R, long ldr, int act, void* stream) {
@@ -1013,10 +1129,17 @@ MER_API int mer_posconv_gemm_bf16(int B, int L, int C_total, int groups, int tap
   g.bias = bias; g.R = (const bf16_t*)R; g.ldr = ldr; g.act = act;
   g.vec_epi = vec_epilogue_ok(cg, out, ldo, R, ldr, g.c_zoff);
   g.tgroup = 8;
-  static const int pc_cfg = [] {  // MER_POSCONV_CFG (A/B): 0 = 2-deep 128x64, 1 = 3-deep, 2 = 32-wide K on a 4-deep ring
-    const char* e = getenv("MER_POSCONV_CFG");
-    return e ? atoi(e) : 0;
-  }();
+  // MER_POSCONV_CFG (A/B, read per call so a test can compare the kernels): 0 = 2-deep 128x64, 1 = 3-deep, 2 = 32-wide
+  // K on a 4-deep ring; 3 = the Toeplitz strip kernel (default where it applies)
+  const char* pc_env = getenv("MER_POSCONV_CFG");
+  const int pc_cfg = pc_env ? atoi(pc_env) : 3;
+  if (pc_cfg == 3 && cg == 48 && L <= PS_MAXL && taps <= PS_MAXT && (taps * cg) % PS_KC == 0 && out_dtype == MER_BF16 &&
+      (ldx % 8) == 0 && (((uintptr_t)X | (uintptr_t)Wp) & 15) == 0) {
+    // 4 waves of 3 fragments each (8 or 10 waves per block measured 77-89 us vs 75)
+    hipLaunchKernelGGL((posconv_strip_kernel<48, 4>), dim3(groups, B), dim3(256), 0, (hipStream_t)stream, L, taps, pad,
+                       (const bf16_t*)X, ldx, (const bf16_t*)Wp, (bf16_t*)out, ldo, bias, (const bf16_t*)R, ldr, act);
+    return (int)hipGetLastError();
+  }
   if (g.K % 64 == 0 && (((uintptr_t)X | (uintptr_t)Wp) & 15) == 0) {
     if (pc_cfg == 1) return launch_pipe<CfgT3, 1>(g, out_dtype, (hipStream_t)stream, groups);
     if (pc_cfg == 2) return launch_pipe<CfgT4, 1>(g, out_dtype, (hipStream_t)stream, groups);
