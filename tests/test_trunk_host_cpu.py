@@ -1,6 +1,7 @@
 """Host-side logic of the trunk backward's deferred weight-gradient folds (no GPU): the stem's slab-column map and
 the fold table the batched launch receives."""
 import numpy as np
+import pytest
 import torch
 
 from multimodalemotionrecognition_amd import kernels as K
@@ -41,3 +42,20 @@ def test_wgrad_folds_table_and_split_count():
         assert 1 <= eff <= splits and pps % 64 == 0 and (eff - 1) * pps < P <= eff * pps  # none empty, all covered
     assert K.wgrad_split_count(1000, 64) == 16  # 64 asked, 16-pixel splits rounded up to 64: 16 non-empty
     assert np.array(f.rows, dtype=np.int64).shape == (1, 8)
+
+
+def test_stem_wgrad_table_built_outside_capture(monkeypatch):
+    """the deferred fold's stem map is a pageable H2D copy, so prepare_backward builds it before any
+    graph capture; inside a capture the prebuilt table is returned as is, and a missing one raises instead of
+    copying inside the capture."""
+    from multimodalemotionrecognition_amd import graphs as G
+    from multimodalemotionrecognition_amd import video
+
+    trunk = video.ResNet18Trunk()
+    dev = torch.device("cpu")
+    monkeypatch.setattr(G, "capturing", lambda: False)
+    built = trunk.stem_wgrad_table(dev, True)  # what prepare_backward does for the default (deferred) folds
+    monkeypatch.setattr(G, "capturing", lambda: True)
+    assert trunk.stem_wgrad_table(dev, True) is built
+    with pytest.raises(RuntimeError, match="prepare_backward"):
+        trunk.stem_wgrad_table(dev, False)  # the immediate-fold index was never built
