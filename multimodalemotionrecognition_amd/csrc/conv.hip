@@ -644,6 +644,19 @@ __global__ __launch_bounds__(256) void wgrad_scatter_kernel(int C, int Creal, in
   }
 }
 
+// XCD-contiguous block order for the streaming stem / pool / fold kernels (A/B switches, default off: their HBM
+// bytes drop -- DESIGN.md section 4e'' -- but a whole-step A/B decides): MER_POOL_XCD, MER_FOLD_XCD
+static int env_flag(const char* name) {
+  const char* e = getenv(name);
+  return (e && e[0] == '1') ? 1 : 0;
+}
+__device__ __forceinline__ int xcd_block(int xcd) {
+  if (!xcd) return blockIdx.x;
+  int v, unused;
+  xcd_tile(blockIdx.x, 1 << 30, (int)gridDim.x, v, unused);
+  return v;
+}
+
 // Batched fold of deferred split-K partial slabs: every weight gradient of one backward segment in ONE launch
 // instead of one or two per convolution (the folds were ~30 launches of 5-12 us each on the critical stream).
 // Record r: dw_r[k][c][tap] += sum_z ws_r[z][k][tap*C + c] (c < Creal), or with a scatter map
@@ -660,19 +673,27 @@ struct FoldRec {
 constexpr int kFoldMaxRecs = 32;
 struct FoldTable {
   int n;
+  int xcd;  // MER_FOLD_XCD: tap-major blocks in XCD chunks (the R*S blocks writing the same dw lines on one L2)
   FoldRec r[kFoldMaxRecs];
 };
 
 __global__ __launch_bounds__(256) void wgrad_fold_batch_kernel(FoldTable t) {
   __shared__ float part[256];
-  // (Slab order over round-robin blocks.  Tap-major blocks in XCD chunks -- the R*S blocks writing the same dw lines
-  // on one L2 -- cut the HBM writes 101 -> 21 MB per launch but ran 99 -> 107 us: DESIGN.md section 4e''.)
+  const int v = xcd_block(t.xcd);
   int ri = 0;
-  while (ri + 1 < t.n && (int)blockIdx.x >= t.r[ri + 1].blk0) ++ri;
+  while (ri + 1 < t.n && v >= t.r[ri + 1].blk0) ++ri;
   const FoldRec& R = t.r[ri];
   const int SG = R.SG, E = 256 / SG, e = threadIdx.x % E, sg = threadIdx.x / E;
   const long row = (long)R.RS * R.C, total = (long)R.K * row;
-  const long idx = (long)((int)blockIdx.x - R.blk0) * E + e;
+  const int lb = v - R.blk0;
+  long idx;
+  if (t.xcd && !R.map && R.C % E == 0) {  // lb -> (k, channel block cb, tap), tap fastest
+    const int CB = R.C / E, per_k = R.RS * CB;
+    const int k = lb / per_k, rem = lb - k * per_k, cb = rem / R.RS, tap = rem - cb * R.RS;
+    idx = (long)k * row + (long)tap * R.C + cb * E + e;
+  } else {
+    idx = (long)lb * E + e;
+  }
   float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
   if (idx < total) {
     const float* src = R.ws + idx;
@@ -1518,6 +1539,8 @@ MER_API int mer_wgrad_fold_batch(int n, const long long* rows, void* stream) {
   if (n < 1 || n > kFoldMaxRecs) return (int)hipErrorInvalidValue;
   FoldTable t{};
   t.n = n;
+  static const int fold_xcd = env_flag("MER_FOLD_XCD");
+  t.xcd = fold_xcd;
   int blk = 0;
   for (int i = 0; i < n; ++i) {
     const long long* q = rows + 8 * i;
@@ -2224,13 +2247,11 @@ MER_API int mer_maxpool_fwd(int N, int H, int W, int C, const void* x, void* y, 
 }
 // gather backward: dx[n,h,w,c] = sum of dy over the (<= 4) windows whose argmax is (h,w)
 __global__ void maxpool_bwd_kernel(int N, int H, int W, int C, int Ho, int Wo, const bf16_t* __restrict__ dy,
-                                   const uint8_t* __restrict__ arg, bf16_t* __restrict__ dx) {
+                                   const uint8_t* __restrict__ arg, bf16_t* __restrict__ dx, int xcd) {
   const int cpr = C / 8;
   const int total = N * H * W * cpr;
   const float inv_cpr = 1.f / cpr, inv_W = 1.f / W, inv_H = 1.f / H;
-  // (XCD-contiguous blocks cut this kernel's HBM fetch 165 -> 37 MB but made it SLOWER, 49 -> 55 us: the
-  // round-robin placement keeps the whole chip on one sequential stream; DESIGN.md section 4e'')
-  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
+  for (int e = xcd_block(xcd) * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
     const int q = fdiv(e, inv_cpr);
     const int c0 = (e - q * cpr) * 8;
     const int q2 = fdiv(q, inv_W);
@@ -2278,8 +2299,9 @@ MER_API int mer_maxpool_bwd(int N, int H, int W, int C, const void* dy, const vo
   if (C % 8 || (long)N * H * W >= (1L << 22)) return (int)hipErrorInvalidValue;
   const long total = (long)N * H * W * C / 8;
   const int grid = (int)((total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192);
+  static const int xcd = env_flag("MER_POOL_XCD");
   hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, N, H, W, C, Ho, Wo,
-                     (const bf16_t*)dy, (const uint8_t*)argmax, (bf16_t*)dx);
+                     (const bf16_t*)dy, (const uint8_t*)argmax, (bf16_t*)dx, xcd);
   MER_LAUNCH_CHECK();
 }
 
@@ -2295,11 +2317,11 @@ MER_API int mer_maxpool_bwd(int N, int H, int W, int C, const void* dy, const vo
 __global__ void stem_bnrelu_maxpool_kernel(int N, int H, int W, int C, int Ho, int Wo, const bf16_t* __restrict__ x,
                                            const float* __restrict__ ms, const float* __restrict__ gamma,
                                            const float* __restrict__ beta, bf16_t* __restrict__ y,
-                                           uint8_t* __restrict__ arg) {
+                                           uint8_t* __restrict__ arg, int xcd) {
   const int cpr = C / 8;
   const int total = N * Ho * Wo * cpr;
   const float inv_cpr = 1.f / cpr, inv_Wo = 1.f / Wo, inv_Ho = 1.f / Ho;
-  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
+  for (int e = xcd_block(xcd) * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
     const int q = fdiv(e, inv_cpr);
     const int c0 = (e - q * cpr) * 8;
     const int q2 = fdiv(q, inv_Wo);
@@ -2351,8 +2373,9 @@ MER_API int mer_stem_bnrelu_maxpool_fwd(int N, int H, int W, int C, const void* 
   if (C % 8 || C > 512 || (long)N * H * W >= (1L << 22)) return (int)hipErrorInvalidValue;
   const long total = (long)N * Ho * Wo * C / 8;
   const int grid = (int)((total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192);
+  static const int xcd = env_flag("MER_POOL_XCD");
   hipLaunchKernelGGL(stem_bnrelu_maxpool_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, N, H, W, C, Ho, Wo,
-                     (const bf16_t*)x, ms, gamma, beta, (bf16_t*)y, (uint8_t*)argmax);
+                     (const bf16_t*)x, ms, gamma, beta, (bf16_t*)y, (uint8_t*)argmax, xcd);
   MER_LAUNCH_CHECK();
 }
 
