@@ -1375,7 +1375,11 @@ MER_API int mer_conv_fwd(int N, int H, int W, int C, int K, int R, int S, int st
 MER_API int mer_conv_fwd_ex(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, const void* x,
                             const void* w_packed, void* y, float* stats, int variant, void* stream) {
   if (C % 8 || variant < -1 || variant > 5) return (int)hipErrorInvalidValue;
-  if (variant == -1) variant = 2;
+  static const int fwd_v = [] {  // MER_CONV_FWD_VARIANT (A/B): override the default tile / ring
+    const char* e = getenv("MER_CONV_FWD_VARIANT");
+    return e ? atoi(e) : 2;
+  }();
+  if (variant == -1) variant = fwd_v;
   ConvGeom g{};
   g.N = N; g.IH = H; g.IW = W; g.IC = C;
   g.OH = (H + 2 * pad - R) / stride + 1; g.OW = (W + 2 * pad - S) / stride + 1;
@@ -1422,7 +1426,11 @@ MER_API int mer_conv_dgrad_ds(int N, int H, int W, int C, int K, int R, int S, i
   // 64-channel outputs (layer1, the layer2.0 input gradients): 32-wide K-tiles on a 4-deep ring with 4-wave tiles
   // (tools/bench_conv.py --fused: layer1 101 -> 65 us, layer2.0 s2 74 -> 51, downsample 48 -> 31); wider outputs
   // keep the 64-wide 2-deep ring (the deep ring loses 10-50% there)
-  if (variant == -1) variant = C <= 64 ? 5 : 2;
+  static const int dg_v = [] {  // MER_CONV_DGRAD_VARIANT (A/B): override the default (5 for <= 64 channels, else 2)
+    const char* e = getenv("MER_CONV_DGRAD_VARIANT");
+    return e ? atoi(e) : -1;
+  }();
+  if (variant == -1) variant = dg_v >= 0 ? dg_v : (C <= 64 ? 5 : 2);
   if (bn_red && (!bn_mask || !bn_x || !bn_ms || (bn_x2 && (!bn_ms2 || !bn_red2)))) return (int)hipErrorInvalidValue;
   if (bn_red && (variant == 0 || stride > 2)) return (int)hipErrorInvalidValue;  // fused only in the pipelined kernel
   ConvGeom g{};

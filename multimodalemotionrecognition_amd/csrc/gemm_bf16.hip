@@ -887,6 +887,16 @@ int pick_variant(int M, int N, int K) {
     return !(e && e[0] == '0');
   }();
   if (convmid && N <= 512 && tl >= 150 && tl < 1200) return 13;
+  // Every other shape on the 256^2 16-wave ring too: fewer, fuller workgroups.  On the few-tile shapes (FFN-down,
+  // out-projection, conv5 / conv6: 57-76 tiles) that is LONGER wall time (FFN-down 33 -> 66 us on 57 CUs) but about
+  // half the CU-time (57 CUs x 66 us vs 228 x 33), and the two-stream step is bound by CU-time: the trunk stream
+  // fills the CUs the encoder leaves idle.  Same-box A/B +1.1 % (201.2 vs 199.1 steps/s, profiles/r04j/ab_wide.txt).
+  // MER_GEMM_WIDE=0 restores the per-shape wall-time picks (128^2 / 128x64 tiles).
+  static const bool wide = [] {
+    const char* e = getenv("MER_GEMM_WIDE");
+    return !(e && e[0] == '0');
+  }();
+  if (wide) return 13;
   if (tl >= 160 && !(N <= 512 && tl < 1200)) return 13;
   return K >= 2048 ? 7 : 9;
 }
