@@ -892,11 +892,11 @@ int pick_variant(int M, int N, int K) {
   // half the CU-time (57 CUs x 66 us vs 228 x 33), and the two-stream step is bound by CU-time: the trunk stream
   // fills the CUs the encoder leaves idle.  Same-box A/B +1.1 % (201.2 vs 199.1 steps/s, profiles/r04j/ab_wide.txt).
   // MER_GEMM_WIDE=0 restores the per-shape wall-time picks (128^2 / 128x64 tiles).
-  static const bool wide = [] {
+  static const int wide = [] {  // MER_GEMM_WIDE=<variant> (A/B) picks another wide variant, e.g. 18 (split ring)
     const char* e = getenv("MER_GEMM_WIDE");
-    return !(e && e[0] == '0');
+    return e ? atoi(e) : 13;
   }();
-  if (wide) return 13;
+  if (wide == 13 || wide == 18 || wide == 19 || wide == 20) return wide;
   if (tl >= 160 && !(N <= 512 && tl < 1200)) return 13;
   return K >= 2048 ? 7 : 9;
 }
