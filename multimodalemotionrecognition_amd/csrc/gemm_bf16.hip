@@ -892,9 +892,12 @@ int pick_variant(int M, int N, int K) {
   // half the CU-time (57 CUs x 66 us vs 228 x 33), and the two-stream step is bound by CU-time: the trunk stream
   // fills the CUs the encoder leaves idle.  Same-box A/B +1.1 % (201.2 vs 199.1 steps/s, profiles/r04j/ab_wide.txt).
   // MER_GEMM_WIDE=0 restores the per-shape wall-time picks (128^2 / 128x64 tiles).
-  static const int wide = [] {  // MER_GEMM_WIDE=<variant> (A/B) picks another wide variant, e.g. 18 (split ring)
+  // The split ring (v18: A three K-tiles deep) over the plain 16-wave ring: +0.3 % more, every one of 3 same-box
+  // rounds (201.6 / 201.7 / 202.1 vs 201.3 / 201.1 / 201.0, profiles/r04j/ab_wide_v18.txt).
+  // MER_GEMM_WIDE=<variant> (A/B) picks another wide variant (13, 18, 19, 20)
+  static const int wide = [] {
     const char* e = getenv("MER_GEMM_WIDE");
-    return e ? atoi(e) : 13;
+    return e ? atoi(e) : 18;
   }();
   if (wide == 13 || wide == 18 || wide == 19 || wide == 20) return wide;
   if (tl >= 160 && !(N <= 512 && tl < 1200)) return 13;
