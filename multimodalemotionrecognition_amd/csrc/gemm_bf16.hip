@@ -877,29 +877,19 @@ int launch_pipe(const GemmArgs& g, int out_dtype, hipStream_t st, int groups = 1
 // 278.6 -> 271.4 us; the same ring is 2-7 % slower on conv2 / conv3 / QKV / FFN-up / 4096^3
 // (profiles/r04/gemm_split_ring.log, all bit-identical).
 int pick_variant(int M, int N, int K) {
-  const long tl = (long)((M + 255) / 256) * ((N + 255) / 256);
-  if (tl >= 1200 && N <= 512) return 18;
-  // the middle feature-extractor convs (conv2..conv4: 600 / 300 / 150 tiles of 256^2): the 16-wave 256^2 ring, not
-  // 128^2 tiles (tools/bench_gemm.py, gpurun_out/gsmall: conv2 163 -> 128 us, conv3 83 -> 80, conv4 45 -> 40).
-  // MER_GEMM_CONVMID=0 restores the 128^2 pick (A/B)
-  static const bool convmid = [] {
-    const char* e = getenv("MER_GEMM_CONVMID");
-    return !(e && e[0] == '0');
-  }();
-  if (convmid && N <= 512 && tl >= 150 && tl < 1200) return 13;
-  // Every other shape on the 256^2 16-wave ring too: fewer, fuller workgroups.  On the few-tile shapes (FFN-down,
-  // out-projection, conv5 / conv6: 57-76 tiles) that is LONGER wall time (FFN-down 33 -> 66 us on 57 CUs) but about
-  // half the CU-time (57 CUs x 66 us vs 228 x 33), and the two-stream step is bound by CU-time: the trunk stream
-  // fills the CUs the encoder leaves idle.  Same-box A/B +1.1 % (201.2 vs 199.1 steps/s, profiles/r04j/ab_wide.txt).
-  // MER_GEMM_WIDE=0 restores the per-shape wall-time picks (128^2 / 128x64 tiles).
-  // The split ring (v18: A three K-tiles deep) over the plain 16-wave ring: +0.3 % more, every one of 3 same-box
-  // rounds (201.6 / 201.7 / 202.1 vs 201.3 / 201.1 / 201.0, profiles/r04j/ab_wide_v18.txt).
-  // MER_GEMM_WIDE=<variant> (A/B) picks another wide variant (13, 18, 19, 20)
+  // Every shape on the 16-wave 256^2 split ring (v18: A three K-tiles deep).  On the few-tile shapes (FFN-down, the
+  // out-projection, conv5 / conv6: 38-76 tiles) that is LONGER wall time than the 128^2 / 128x64 tiles they had
+  // (FFN-down 33 -> 66 us on 57 CUs) but about half the CU-time (57 CUs x 66 us vs 228 x 33): the two-stream step is
+  // bound by CU-time and the trunk stream fills the CUs the encoder leaves idle.  Same-box A/Bs (profiles/r04j):
+  // 256^2 ring for all +1.1 % (twice), split ring over the plain ring +0.3 %, conv2-4 on the split ring too +0.1 %.
+  // MER_GEMM_WIDE=<variant> picks another wide variant (13, 19, 20); MER_GEMM_WIDE=0 the round-3 wall-time picks.
   static const int wide = [] {
     const char* e = getenv("MER_GEMM_WIDE");
     return e ? atoi(e) : 18;
   }();
   if (wide == 13 || wide == 18 || wide == 19 || wide == 20) return wide;
+  const long tl = (long)((M + 255) / 256) * ((N + 255) / 256);
+  if (tl >= 1200 && N <= 512) return 18;
   if (tl >= 160 && !(N <= 512 && tl < 1200)) return 13;
   return K >= 2048 ? 7 : 9;
 }
