@@ -1278,7 +1278,11 @@ int launch_conv_pipe(ConvGeom& g, hipStream_t st, int variant) {
   const int M = PAR ? g.N * g.OH * g.OW / 4 : g.N * g.OH * g.OW;
   const int bn = g.Ncols <= 64 ? 64 : 128;
   const long tiles128 = (long)((M + 127) / 128) * ((g.Ncols + bn - 1) / bn) * (PAR ? 4 : 1);
-  const bool small_m = tiles128 < 384;
+  static const int small_m_tiles = [] {  // MER_CONV_SMALLM_TILES (A/B): below this many 128-row tiles, 64-row tiles
+    const char* e = getenv("MER_CONV_SMALLM_TILES");
+    return e ? atoi(e) : 384;
+  }();
+  const bool small_m = tiles128 < small_m_tiles;
   if (variant == 3 && !small_m) {  // 256-row tiles (8 / 16 waves) for the large-M layers
     // (the 16-wave dgrad tile needs more than 128 VGPRs and would spill to scratch: 8-wave 256 x 64 tiles instead;
     // tools/check_scratch.py keeps every kernel of the library scratch-free)
