@@ -220,3 +220,25 @@ def test_conv0_groupnorm_moments_vs_torch(case):
     out2 = torch.empty_like(out)
     K.wavlm_conv0_gn_gelu(wav.cuda(), w.reshape(512, 10).contiguous().cuda(), gamma.cuda(), beta.cuda(), out2)
     assert torch.equal(out, out2)  # deterministic
+
+
+@pytest.mark.parametrize("rows,drop", [(4768, 0.0), (4767, 0.1), (3, 0.1)])
+def test_layernorm_two_rows_per_wave_bit_identical(rows, drop, monkeypatch):
+    """The two-rows-per-wave LayerNorm (MER_LN_ROWS2=1) against the row-per-wave kernel: same per-row arithmetic
+    and order (and the same dropout mask indices) -> the same bits, odd row counts included."""
+    from multimodalemotionrecognition_amd import kernels as K
+
+    torch.manual_seed(4)
+    d = 768
+    x = (torch.randn(rows, d) * 3 + 1).bfloat16().cuda()
+    g = (1 + 0.1 * torch.randn(d)).cuda()
+    b = (0.1 * torch.randn(d)).cuda()
+    rng = torch.tensor([12345], dtype=torch.int64, device="cuda") if drop > 0 else None
+    outs = []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("MER_LN_ROWS2", flag)
+        y = torch.full((rows, d), float("nan"), device="cuda", dtype=torch.bfloat16)
+        K.layernorm(x, g, b, y, drop_p=drop, rng=rng, site=7)
+        torch.cuda.synchronize()
+        outs.append(y.cpu())
+    assert torch.equal(outs[0], outs[1])
