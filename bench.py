@@ -20,17 +20,46 @@ the figure a rocprofv3 kernel trace of the same command reports for it; the time
 `roofline_head` for the fused xattn head (HIP events around its graph replays in `--probe-steps` steps) and
 `cpu_baseline` (the fp32 CPU oracle of the same step, rank 0, N=1: BASELINE.md section 3 -- warm-up steps,
 then the median of timed steps, on the threads of this process's CPU share, CPU model recorded).
+
+Multi-GPU: ``python bench.py --gpus N`` (N > 1) outside torchrun starts the N ranks itself -- one
+``torch.distributed.run`` child job on 127.0.0.1, launched before this process imports torch or touches a GPU --
+and exits with that job's status; rank 0 prints the one JSON line.  Under torchrun (WORLD_SIZE set) it runs as the
+rank it was given and refuses to run when the group's size differs from ``--gpus``.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 from pathlib import Path
 
-import torch
+
+def _launch_ranks_if_needed(argv) -> None:
+    """``--gpus N`` with N > 1 and no torchrun environment: run this script as an N-rank single-node job
+    (python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1) and exit with its status.
+    Called before torch is imported, so the parent never initialises a GPU (no exec: a child process)."""
+    pre = argparse.ArgumentParser(add_help=False)
+    pre.add_argument("--gpus", type=int, default=1)
+    known, _ = pre.parse_known_args(argv)
+    if known.gpus <= 1 or "WORLD_SIZE" in os.environ:
+        return
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={known.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", str(Path(__file__).resolve()), *argv]
+    sys.exit(subprocess.run(cmd).returncode)
+
+
+if __name__ == "__main__":
+    _launch_ranks_if_needed(sys.argv[1:])
+
+import torch  # noqa: E402
 import torch.distributed as dist
 
 ROOT = Path(__file__).resolve().parent
@@ -320,9 +349,16 @@ def main():
     ap.add_argument("--wavlm-unfreeze", type=int, default=0,
                     help="stage-2 fine-tuning step instead (train.py:798-872 two-stage policy): unfreeze the last N "
                          "WavLM layers and the last video block, stage optimizer groups (not the headline config)")
+    ap.add_argument("--stub-step", action="store_true",
+                    help="test hook for the rank launcher: a CPU matmul + gloo all-reduce in place of the train step")
     args = ap.parse_args()
 
-    world, rank, local = init_distributed()
+    world, rank, local = init_distributed("gloo" if args.stub_step else None)
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but the process group has {world} rank(s)", file=sys.stderr, flush=True)
+        sys.exit(2)
+    if args.stub_step:
+        return _bench_stub(args, world, rank)
     if args.c5:
         return _bench_c5(args, world, rank, local)
     if args.stream_priority == "high":
@@ -330,6 +366,37 @@ def main():
         with torch.cuda.stream(hi):
             return _bench(args, world, rank, local)
     return _bench(args, world, rank, local)
+
+
+def _bench_stub(args, world, rank):
+    """The launcher's test hook (tests/test_bench_launch_cpu.py): the same warm-up / barrier / timed region /
+    max-over-ranks structure as ``_bench`` around a CPU matmul + gloo all-reduce, one JSON line from rank 0 that
+    says how many ranks took part."""
+    x = torch.full((64, 64), 1.0 / 64)
+    for _ in range(args.warmup):
+        x = x @ x
+    if is_dist():
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        x = x @ x
+        if is_dist():
+            dist.all_reduce(x)
+            x /= world
+    if is_dist():
+        dist.barrier()
+    el = torch.tensor([time.perf_counter() - t0])
+    ranks = torch.ones(1)
+    if is_dist():
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        dist.all_reduce(ranks)
+    if rank == 0:
+        print(json.dumps({"metric": "stub", "value": round(world * args.steps / float(el), 3), "unit": "steps/s",
+                          "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "ranks_reporting": int(ranks), "pid": os.getpid()}), flush=True)
+    if is_dist():
+        dist.barrier()
+        dist.destroy_process_group()
 
 
 def cpu_baseline_c5(threads: int, batch: int = 64, steps: int = 2, warmup: int = 1):

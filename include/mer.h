@@ -187,23 +187,23 @@ int mer_gemm_bf16(int M, int N, int K, const void* A, long a_gstride, long a_rst
                   long ldw, void* C, int c_dtype, long ldc, const float* bias, const void* R, long ldr, int act,
                   void* stream);
 
-/* mer_gemm_bf16 with an explicit kernel variant: -1 auto (what mer_gemm_bf16 does), 0 the 128x128
- * register-staged kernel (any K % 8 == 0), 1/2/3 the global_load_lds pipelined kernel with 256x256 /
- * 256x128 / 128x128 tiles and a 2-deep LDS ring, 4/5 128x128 with a 3/4-deep ring, 6 256x128 3-deep,
- * 7 128x64 3-deep, 8 128x64 2-deep, 9/10 128x128 with 8 waves 2/3-deep, 11 128x64 as 4x1 waves 3-deep,
- * 12 256x128 with 16 waves, 13 256x256 with 16 waves, 14 256x256 phase-interleaved, 15/16/17 32-wide K-tiles on
- * 4-deep rings (256x256 / 128x64 / 128x128), 18/19 256x256 with 16 / 8 waves on split rings (A 3-deep, B 2-deep)
- * (K % 64 == 0; otherwise variant 0 runs). */
+/* mer_gemm_bf16 with an explicit kernel variant: -1 the wall-time pick (what mer_gemm_bf16 does), -2 the
+ * CU-time pick (every shape on the 256x256 split ring: the train step's side-stream encoder forward), 0 the
+ * 128x128 register-staged kernel (any K % 8 == 0), and the global_load_lds pipelined kernel as 7 (128x64 tiles,
+ * 3-deep ring), 9 (128x128, 8 waves, 2-deep), 13 (256x256, 16 waves, 2-deep), 18 (256x256, 16 waves, split
+ * rings: A 3-deep, B 2-deep).  K % 64 == 0 for 7-18, otherwise variant 0 runs.  Every variant gives the same
+ * bits.  Other values: hipErrorInvalidValue. */
 int mer_gemm_bf16_ex(int M, int N, int K, const void* A, long a_gstride, long a_rstride, int a_rpg, const void* W,
                      long ldw, void* C, int c_dtype, long ldc, const float* bias, const void* R, long ldr, int act,
                      int variant, void* stream);
 
 /* Grouped positional Conv1d of WavLM (TF:48-90): out[b,t,g*Cg+n] = act(sum_{tap,c} X[b,t+tap-pad,g*Cg+c]
  * Wp[g][n][tap][c] + bias) (+ R), rows t in [0, L) (the SamePad crop).  Wp is the weight-normed, bf16
- * repacked kernel (mer_weightnorm_scale + mer_permute3_bf16). */
+ * repacked kernel (mer_weightnorm_scale + mer_permute3_bf16).  variant -1: the Toeplitz strip kernel where it
+ * applies (48 channels per group, L <= 160), else the gather GEMM; 0: the gather GEMM (bit-identical). */
 int mer_posconv_gemm_bf16(int B, int L, int C_total, int groups, int taps, int pad, const void* X, long ldx,
                           const void* Wp, void* out, int out_dtype, long ldo, const float* bias, const void* R,
-                          long ldr, int act, void* stream);
+                          long ldr, int act, int variant, void* stream);
 
 /* WavLM feature-extractor layer 0 (TF:723-745): Conv1d(1,512,k=10,s=5,no bias) of wav [B,S] fp32 ->
  * GroupNorm(512,512) (per (clip, channel) statistics over time of the bf16-rounded conv output) -> GELU,

@@ -550,13 +550,11 @@ void launch_wgrad_pipe(const WgradGeom& g0, dim3 grid, hipStream_t st) {
   if (hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_pipe_kernel<BM_, BN_, WM, WN, STAGES, KS>),
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return;
-  static const bool flat_on = [] {  // MER_WGRAD_XCD=0: the z grid (tiles of a split on different XCDs), A/B
-    const char* e = getenv("MER_WGRAD_XCD");
-    return !(e && e[0] == '0');
-  }();
+  // split-major 1-D grid over xcd_tile's XCD chunks: the tiles of one split (same dY rows, same shifted X windows)
+  // share an L2 (DESIGN.md section 4e'': layer1 / stem wgrad fetch 244 -> 67 MB per launch)
   WgradGeom g = g0;
-  g.flat = flat_on ? 1 : 0;
-  const dim3 gr = flat_on ? dim3(grid.x * grid.z, 1, 1) : grid;
+  g.flat = 1;
+  const dim3 gr(grid.x * grid.z, 1, 1);
   hipLaunchKernelGGL((wgrad_pipe_kernel<BM_, BN_, WM, WN, STAGES, KS>), gr, dim3(64 * WM * WN), lds, st, g);
 }
 
@@ -644,19 +642,6 @@ __global__ __launch_bounds__(256) void wgrad_scatter_kernel(int C, int Creal, in
   }
 }
 
-// XCD-contiguous block order for the streaming stem / pool / fold kernels (A/B switches, default off: their HBM
-// bytes drop -- DESIGN.md section 4e'' -- but a whole-step A/B decides): MER_POOL_XCD, MER_FOLD_XCD
-static int env_flag(const char* name) {
-  const char* e = getenv(name);
-  return (e && e[0] == '1') ? 1 : 0;
-}
-__device__ __forceinline__ int xcd_block(int xcd) {
-  if (!xcd) return blockIdx.x;
-  int v, unused;
-  xcd_tile(blockIdx.x, 1 << 30, (int)gridDim.x, v, unused);
-  return v;
-}
-
 // Batched fold of deferred split-K partial slabs: every weight gradient of one backward segment in ONE launch
 // instead of one or two per convolution (the folds were ~30 launches of 5-12 us each on the critical stream).
 // Record r: dw_r[k][c][tap] += sum_z ws_r[z][k][tap*C + c] (c < Creal), or with a scatter map
@@ -673,27 +658,19 @@ struct FoldRec {
 constexpr int kFoldMaxRecs = 32;
 struct FoldTable {
   int n;
-  int xcd;  // MER_FOLD_XCD: tap-major blocks in XCD chunks (the R*S blocks writing the same dw lines on one L2)
   FoldRec r[kFoldMaxRecs];
 };
 
 __global__ __launch_bounds__(256) void wgrad_fold_batch_kernel(FoldTable t) {
   __shared__ float part[256];
-  const int v = xcd_block(t.xcd);
+  const int v = blockIdx.x;
   int ri = 0;
   while (ri + 1 < t.n && v >= t.r[ri + 1].blk0) ++ri;
   const FoldRec& R = t.r[ri];
   const int SG = R.SG, E = 256 / SG, e = threadIdx.x % E, sg = threadIdx.x / E;
   const long row = (long)R.RS * R.C, total = (long)R.K * row;
   const int lb = v - R.blk0;
-  long idx;
-  if (t.xcd && !R.map && R.C % E == 0) {  // lb -> (k, channel block cb, tap), tap fastest
-    const int CB = R.C / E, per_k = R.RS * CB;
-    const int k = lb / per_k, rem = lb - k * per_k, cb = rem / R.RS, tap = rem - cb * R.RS;
-    idx = (long)k * row + (long)tap * R.C + cb * E + e;
-  } else {
-    idx = (long)lb * E + e;
-  }
+  const long idx = (long)lb * E + e;
   float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
   if (idx < total) {
     const float* src = R.ws + idx;
@@ -1278,11 +1255,8 @@ int launch_conv_pipe(ConvGeom& g, hipStream_t st, int variant) {
   const int M = PAR ? g.N * g.OH * g.OW / 4 : g.N * g.OH * g.OW;
   const int bn = g.Ncols <= 64 ? 64 : 128;
   const long tiles128 = (long)((M + 127) / 128) * ((g.Ncols + bn - 1) / bn) * (PAR ? 4 : 1);
-  static const int small_m_tiles = [] {  // MER_CONV_SMALLM_TILES (A/B): below this many 128-row tiles, 64-row tiles
-    const char* e = getenv("MER_CONV_SMALLM_TILES");
-    return e ? atoi(e) : 384;
-  }();
-  const bool small_m = tiles128 < small_m_tiles;
+  // below 384 128-row tiles, 64-row tiles (128-row tiles on the deep layers lose 3.5 % of the step)
+  const bool small_m = tiles128 < 384;
   if (variant == 3 && !small_m) {  // 256-row tiles (8 / 16 waves) for the large-M layers
     // (the 16-wave dgrad tile needs more than 128 VGPRs and would spill to scratch: 8-wave 256 x 64 tiles instead;
     // tools/check_scratch.py keeps every kernel of the library scratch-free)
@@ -1352,22 +1326,11 @@ int launch_conv(ConvGeom& g, hipStream_t st) {
 // register-staged kernel on the stem, layer1, layer3 and layer4 and within 4% elsewhere; its 3-stage form, at one
 // block per CU, is slower)
 int wgrad_default_variant(int K) {
-  static const int v = [] {
-    const char* e = getenv("MER_WGRAD_VARIANT");
-    return e ? atoi(e) : 0;
-  }();
   (void)K;
-  return v > 0 ? v : 4;
+  return 4;
 }
 
-// MER_CONV_VEC=0 keeps the 2-byte epilogue (A/B switch for tools/bench_conv.py)
-bool vec_epilogue_enabled() {
-  static const bool on = [] {
-    const char* e = getenv("MER_CONV_VEC");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
+bool vec_epilogue_enabled() { return true; }
 
 }  // namespace
 
@@ -1379,11 +1342,7 @@ MER_API int mer_conv_fwd(int N, int H, int W, int C, int K, int R, int S, int st
 MER_API int mer_conv_fwd_ex(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, const void* x,
                             const void* w_packed, void* y, float* stats, int variant, void* stream) {
   if (C % 8 || variant < -1 || variant > 5) return (int)hipErrorInvalidValue;
-  static const int fwd_v = [] {  // MER_CONV_FWD_VARIANT (A/B): override the default tile / ring
-    const char* e = getenv("MER_CONV_FWD_VARIANT");
-    return e ? atoi(e) : 2;
-  }();
-  if (variant == -1) variant = fwd_v;
+  if (variant == -1) variant = 2;
   ConvGeom g{};
   g.N = N; g.IH = H; g.IW = W; g.IC = C;
   g.OH = (H + 2 * pad - R) / stride + 1; g.OW = (W + 2 * pad - S) / stride + 1;
@@ -1422,19 +1381,16 @@ MER_API int mer_conv_dgrad_ds(int N, int H, int W, int C, int K, int R, int S, i
                               const void* bn_x2, const float* bn_ms2, float* bn_red2, const void* ds_dy,
                               const void* ds_wt_packed, int ds_K, int variant, void* stream) {
   if (K % 8 || C % 8 || variant < -1 || variant > 5) return (int)hipErrorInvalidValue;
-  // the fused downsample: a 1x1 / stride-2 / pad-0 conv of the same input with ds_K output channels, beside a
-  // 3x3 / stride-2 / pad-1 conv (its taps land in parity class (0, 0) only, at pixel (2i, 2j)); K-tile aligned
-  if (ds_dy && (stride != 2 || R != 3 || S != 3 || pad != 1 || !ds_wt_packed || ds_K <= 0 || ds_K % 64 || K % 64 ||
-                variant == 0))
-    return (int)hipErrorInvalidValue;
   // 64-channel outputs (layer1, the layer2.0 input gradients): 32-wide K-tiles on a 4-deep ring with 4-wave tiles
   // (tools/bench_conv.py --fused: layer1 101 -> 65 us, layer2.0 s2 74 -> 51, downsample 48 -> 31); wider outputs
   // keep the 64-wide 2-deep ring (the deep ring loses 10-50% there)
-  static const int dg_v = [] {  // MER_CONV_DGRAD_VARIANT (A/B): override the default (5 for <= 64 channels, else 2)
-    const char* e = getenv("MER_CONV_DGRAD_VARIANT");
-    return e ? atoi(e) : -1;
-  }();
-  if (variant == -1) variant = dg_v >= 0 ? dg_v : (C <= 64 ? 5 : 2);
+  if (variant == -1) variant = C <= 64 ? 5 : 2;
+  // the fused downsample: a 1x1 / stride-2 / pad-0 conv of the same input with ds_K output channels, beside a
+  // 3x3 / stride-2 / pad-1 conv (its taps land in parity class (0, 0) only, at pixel (2i, 2j)); K-tile aligned.
+  // Checked AFTER the variant is resolved: only the pipelined kernels (variants 1..5) read the second K segment.
+  if (ds_dy && (stride != 2 || R != 3 || S != 3 || pad != 1 || !ds_wt_packed || ds_K <= 0 || ds_K % 64 || K % 64 ||
+                variant < 1))
+    return (int)hipErrorInvalidValue;
   if (bn_red && (!bn_mask || !bn_x || !bn_ms || (bn_x2 && (!bn_ms2 || !bn_red2)))) return (int)hipErrorInvalidValue;
   if (bn_red && (variant == 0 || stride > 2)) return (int)hipErrorInvalidValue;  // fused only in the pipelined kernel
   ConvGeom g{};
@@ -1505,10 +1461,7 @@ static int conv_wgrad_impl(int N, int H, int W, int C, int Creal, int K, int R, 
       hipLaunchKernelGGL((wgrad_kernel<128, 128, 2, 4>), grid, dim3(512), 0, st, g);
   }
   if (!fold) MER_LAUNCH_CHECK();  // partial slabs left for mer_wgrad_fold_batch
-  static const int fold_max = [] {  // MER_WGRAD_FOLD_MAX: most slabs folded in the single fold+scatter pass (A/B)
-    const char* e = getenv("MER_WGRAD_FOLD_MAX");
-    return e ? atoi(e) : 16;
-  }();
+  constexpr int fold_max = 16;  // most slabs folded in the single fold+scatter pass
   if (splits > fold_max) {  // many partial slabs: a wide reduce first (one serial chain per element was latency-bound)
     const int SG = splits >= 64 ? 16 : 8;
     const long total = (long)K * R * S * C;
@@ -1537,22 +1490,13 @@ MER_API int mer_conv_wgrad_partials(int N, int H, int W, int C, int K, int R, in
                          false);
 }
 
-static int fold_sg_max() {  // MER_FOLD_SG: split groups per block for many-slab records (A/B), 8 default
-  static const int v = [] {
-    const char* e = getenv("MER_FOLD_SG");
-    const int x = e ? atoi(e) : 8;
-    return (x == 4 || x == 8 || x == 16) ? x : 8;
-  }();
-  return v;
-}
+static int fold_sg_max() { return 8; }  // split groups per block for many-slab records
 
 // rows: n x 8 int64 {ws, dw, map, K, C, Creal (map records: output floats per k), R*S, splits}
 MER_API int mer_wgrad_fold_batch(int n, const long long* rows, void* stream) {
   if (n < 1 || n > kFoldMaxRecs) return (int)hipErrorInvalidValue;
   FoldTable t{};
   t.n = n;
-  static const int fold_xcd = env_flag("MER_FOLD_XCD");
-  t.xcd = fold_xcd;
   int blk = 0;
   for (int i = 0; i < n; ++i) {
     const long long* q = rows + 8 * i;
@@ -2259,11 +2203,11 @@ MER_API int mer_maxpool_fwd(int N, int H, int W, int C, const void* x, void* y, 
 }
 // gather backward: dx[n,h,w,c] = sum of dy over the (<= 4) windows whose argmax is (h,w)
 __global__ void maxpool_bwd_kernel(int N, int H, int W, int C, int Ho, int Wo, const bf16_t* __restrict__ dy,
-                                   const uint8_t* __restrict__ arg, bf16_t* __restrict__ dx, int xcd) {
+                                   const uint8_t* __restrict__ arg, bf16_t* __restrict__ dx) {
   const int cpr = C / 8;
   const int total = N * H * W * cpr;
   const float inv_cpr = 1.f / cpr, inv_W = 1.f / W, inv_H = 1.f / H;
-  for (int e = xcd_block(xcd) * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
     const int q = fdiv(e, inv_cpr);
     const int c0 = (e - q * cpr) * 8;
     const int q2 = fdiv(q, inv_W);
@@ -2311,9 +2255,8 @@ MER_API int mer_maxpool_bwd(int N, int H, int W, int C, const void* dy, const vo
   if (C % 8 || (long)N * H * W >= (1L << 22)) return (int)hipErrorInvalidValue;
   const long total = (long)N * H * W * C / 8;
   const int grid = (int)((total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192);
-  static const int xcd = env_flag("MER_POOL_XCD");
   hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, N, H, W, C, Ho, Wo,
-                     (const bf16_t*)dy, (const uint8_t*)argmax, (bf16_t*)dx, xcd);
+                     (const bf16_t*)dy, (const uint8_t*)argmax, (bf16_t*)dx);
   MER_LAUNCH_CHECK();
 }
 
@@ -2329,11 +2272,11 @@ MER_API int mer_maxpool_bwd(int N, int H, int W, int C, const void* dy, const vo
 __global__ void stem_bnrelu_maxpool_kernel(int N, int H, int W, int C, int Ho, int Wo, const bf16_t* __restrict__ x,
                                            const float* __restrict__ ms, const float* __restrict__ gamma,
                                            const float* __restrict__ beta, bf16_t* __restrict__ y,
-                                           uint8_t* __restrict__ arg, int xcd) {
+                                           uint8_t* __restrict__ arg) {
   const int cpr = C / 8;
   const int total = N * Ho * Wo * cpr;
   const float inv_cpr = 1.f / cpr, inv_Wo = 1.f / Wo, inv_Ho = 1.f / Ho;
-  for (int e = xcd_block(xcd) * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
     const int q = fdiv(e, inv_cpr);
     const int c0 = (e - q * cpr) * 8;
     const int q2 = fdiv(q, inv_Wo);
@@ -2385,9 +2328,8 @@ MER_API int mer_stem_bnrelu_maxpool_fwd(int N, int H, int W, int C, const void* 
   if (C % 8 || C > 512 || (long)N * H * W >= (1L << 22)) return (int)hipErrorInvalidValue;
   const long total = (long)N * Ho * Wo * C / 8;
   const int grid = (int)((total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192);
-  static const int xcd = env_flag("MER_POOL_XCD");
   hipLaunchKernelGGL(stem_bnrelu_maxpool_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, N, H, W, C, Ho, Wo,
-                     (const bf16_t*)x, ms, gamma, beta, (bf16_t*)y, (uint8_t*)argmax, xcd);
+                     (const bf16_t*)x, ms, gamma, beta, (bf16_t*)y, (uint8_t*)argmax);
   MER_LAUNCH_CHECK();
 }
 

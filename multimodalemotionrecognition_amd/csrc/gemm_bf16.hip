@@ -15,8 +15,6 @@
 // Tile 128x128x64, 256 threads = 4 waves (2x2), each wave 64x64 = 4x4 v_mfma_f32_16x16x32_bf16.
 // Register-staged double-buffered LDS (one barrier per K step); LDS rows padded to 72 elements
 // (144 B) so the 16 rows read by one ds_read_b128 lane group land on distinct banks.
-#include <cstdlib>
-
 #include "common.h"
 #include "mer.h"
 
@@ -466,387 +464,11 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_pipe_kernel(GemmArgs g) {
   }
 }
 
-// Phase-interleaved 256x256 tile (cdna_hip_programming.md §5 "256² 8-phase template", T3+T4), rows mode.
-// 8 waves as 2 (M) x 4 (N), 128x64 outputs each.  A K-tile (64 deep) is consumed in four phases, one
-// 64x32 accumulator quadrant per phase, and its LDS image is cut into four 16 KiB pieces in the order
-// the phases first read them:
-//   piece 0 = P0: A rows wr*128 + [0,64)    read in phase 0   (quadrants (0,0), (0,1))
-//   piece 1 = Q0: B rows wc*64  + [0,32)    read in phase 0   (quadrants (0,0), (1,0))
-//   piece 2 = Q1: B rows wc*64  + [32,64)   read in phase 1
-//   piece 3 = P1: A rows wr*128 + [64,128)  read in phase 2
-// Two K-tile buffers (128 KiB).  A piece of tile u+2 overwrites the same piece of tile u as soon as
-// every wave has read it (the barrier of the following phase proves that), one piece (2 glds per
-// thread) per phase:  phase (u,0) stages P1(u+1), (u,1) P0(u+2), (u,2) Q0(u+2), (u,3) Q1(u+2).
-// So each piece is issued 6-7 phases before its first read and five pieces (10 glds) stay in flight
-// across every barrier: phase p in {0,1,2} waits vmcnt(#younger glds) for its own piece, then one raw
-// s_barrier makes every wave's DMA visible.  Phase 3 reads nothing and needs no barrier.
-constexpr int PH_NT = 512, PH_PIECE = 128 * 64;  // threads; bf16 elements per piece
-
-__device__ __forceinline__ void wait_vm_even(int n) {  // n in {0,2,...,10}, wave-uniform
-  switch (n) {
-    case 10: wait_vmcnt<10>(); break;
-    case 8: wait_vmcnt<8>(); break;
-    case 6: wait_vmcnt<6>(); break;
-    case 4: wait_vmcnt<4>(); break;
-    case 2: wait_vmcnt<2>(); break;
-    default: wait_vmcnt<0>(); break;
-  }
-}
-
-template <typename TOUT>
-__global__ __launch_bounds__(PH_NT, 1) void gemm_phase_kernel(GemmArgs g) {
-  extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
-  if (layer_skipped(g.skip_mask, g.skip_bit)) return;
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const int nx = (g.N + 255) / 256, ny = (g.M + 255) / 256;
-  int tx, ty;
-  xcd_tile_grouped(blockIdx.x, nx, ny, g.tgroup, tx, ty);
-  const int m0 = ty * 256, n0 = tx * 256;
-  const int wr = w >> 2, wc = w & 3;
-  const int lrow = lane >> 3, lchunk = lane & 7;
-
-  // per-lane source of each piece's two glds (piece row pr = (w*2 + j)*8 + lrow)
-  const bf16_t* src[4][2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int pr = (w * 2 + j) * 8 + lrow;
-    const int sw = swz_chunk(pr, lchunk) * 8;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {  // A pieces P0 (h=0) / P1 (h=1)
-      int m = m0 + (pr >> 6) * 128 + h * 64 + (pr & 63);
-      m = m < g.M ? m : g.M - 1;
-      src[h ? 3 : 0][j] = g.A + (long)(m / g.a_rpg) * g.a_gstride + (long)(m % g.a_rpg) * g.a_rstride + sw;
-      int n = n0 + (pr >> 5) * 64 + h * 32 + (pr & 31);  // B pieces Q0 (h=0) / Q1 (h=1)
-      n = n < g.N ? n : g.N - 1;
-      src[1 + h][j] = g.B + (long)n * g.ldb + sw;
-    }
-  }
-  const int nk = g.K / 64;
-  // stage piece pc of K-tile u (skipped past the end)
-  auto stage = [&](int pc, int u) {
-    if (u >= nk) return;
-    bf16_t* dst = smem + ((u & 1) * 4 + pc) * PH_PIECE + w * 1024;
-    glds16(src[pc][0] + ktile_off(g, u), dst);
-    glds16(src[pc][1] + ktile_off(g, u), dst + 512);
-  };
-
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int fr = lane & 15, fq = lane >> 4;
-  auto read_frags = [&](const bf16_t* piece, int rbase, int n16, bf16x8 (*out)[2]) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      if (i >= n16) break;
-      const int r = rbase + i * 16 + fr;
-#pragma unroll
-      for (int s = 0; s < 2; ++s)
-        out[i][s] = *reinterpret_cast<const bf16x8*>(piece + r * 64 + swz_chunk(r, s * 4 + fq) * 8);
-    }
-  };
-  auto sync = [&](int nyoung) {
-    wait_vm_even(nyoung);
-    __builtin_amdgcn_s_waitcnt((15) | (7 << 4) | (0 << 8) | (3 << 14));  // lgkmcnt(0) only
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-  };
-
-  // prologue = the issues of virtual phases (-2,1..3) and (-1,0..3)
-  stage(0, 0); stage(1, 0); stage(2, 0); stage(3, 0);
-  stage(0, 1); stage(1, 1); stage(2, 1);
-
-  bf16x8 af[4][2], bq0[2][2], bq1[2][2];
-  for (int u = 0; u < nk; ++u) {
-    const int e1 = u + 1 < nk, e2 = u + 2 < nk;
-    const bf16_t* buf = smem + (u & 1) * 4 * PH_PIECE;
-    // phase 0: P0, Q0 -> quadrant (0,0)
-    sync(2 * (2 + 3 * e1));
-    stage(3, u + 1);
-    read_frags(buf + 0 * PH_PIECE, wr * 64, 4, af);
-    read_frags(buf + 1 * PH_PIECE, wc * 32, 2, bq0);
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][s], bq0[j][s], acc[i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-    // phase 1: Q1 -> quadrant (0,1)
-    sync(2 * (1 + 4 * e1));
-    stage(0, u + 2);
-    read_frags(buf + 2 * PH_PIECE, wc * 32, 2, bq1);
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[i][2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][s], bq1[j][s], acc[i][2 + j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-    // phase 2: P1 -> quadrant (1,0)
-    sync(2 * (4 * e1 + e2));
-    stage(1, u + 2);
-    read_frags(buf + 3 * PH_PIECE, wr * 64, 4, af);
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][s], bq0[j][s], acc[4 + i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-    // phase 3: no reads -> quadrant (1,1); Q1(u) was retired by every wave before phase 2's barrier
-    __builtin_amdgcn_sched_barrier(0);
-    stage(2, u + 2);
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[4 + i][2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][s], bq1[j][s], acc[4 + i][2 + j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-  }
-
-  TOUT* C = reinterpret_cast<TOUT*>(g.C);
-  const unsigned long long dseed = mer_site_seed(g.drop_seed, g.drop_site);
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int col = n0 + wc * 64 + j * 16 + fr;
-    if (col >= g.N) continue;
-    const float bv = g.bias ? g.bias[col] : 0.f;
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = m0 + wr * 128 + i * 16 + fq * 4 + r;
-        if (row >= g.M) continue;
-        float v = epi_act_drop(acc[i][j][r] + bv, g.act, g.drop_p, dseed, (long)row * g.N + col);
-        if (g.R) v += bf2f(g.R[(long)row * g.ldr + col]);
-        stf<TOUT>(C, (long)row * g.ldc + col, v);
-      }
-  }
-}
-
-// Ping-pong form of the phase kernel (cdna_hip_programming.md §5 "256² 8-phase template": two barriers per
-// phase, the wave rows staggered by one barrier).  Same tile, waves, pieces and fragment maps as
-// gemm_phase_kernel; each phase is  R: [vmcnt wait] stage one piece, ds_read the phase's fragments | barrier |
-// M: lgkmcnt(0), 16 MFMAs | barrier.  Wave row 1 (waves 4-7, one per SIMD) runs one barrier behind row 0, so on
-// every SIMD one wave's R section (LDS reads, DMA issue) overlaps the other's MFMA cluster.
-// Global barrier k ends "interval" k: row 0 runs R(phi) in interval 2phi+1 and M(phi) in 2phi+2, row 1 one later.
-//   Reads, phase (u,p): p0 P0(u) Q0(u), p1 Q1(u), p2 P1(u), p3 none.
-//   Stages, phase (u,p): p0 Q1(u+1), p1 P1(u+1), p2 P0(u+2), p3 Q0(u+2)   (piece X(v) issued 4..6 phases early)
-//   RAW: at the top of R(phi) every wave waits (counted vmcnt) for its DMA of the pieces read in phase phi+1;
-//        a reader in R(phi+1) (interval >= 2phi+3) is past the barrier that follows both rows' waits.
-//   WAR: X(v+2) reuses X(v)'s buffer; row 1's last read of X(v) in phase r is retired (lgkmcnt(0) in its M(r))
-//        by barrier 2r+3, and X(v+2) is issued in phase >= r+2, i.e. interval >= 2r+5.
-// Steady state: 3 pieces (6 glds per wave) stay in flight across every wait.
-template <typename TOUT>
-__global__ __launch_bounds__(PH_NT, 1) void gemm_pp_kernel(GemmArgs g) {
-  extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
-  if (layer_skipped(g.skip_mask, g.skip_bit)) return;
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const int nx = (g.N + 255) / 256, ny = (g.M + 255) / 256;
-  int tx, ty;
-  xcd_tile_grouped(blockIdx.x, nx, ny, g.tgroup, tx, ty);
-  const int m0 = ty * 256, n0 = tx * 256;
-  const int wr = w >> 2, wc = w & 3;
-  const int lrow = lane >> 3, lchunk = lane & 7;
-
-  const bf16_t* src[4][2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int pr = (w * 2 + j) * 8 + lrow;
-    const int sw = swz_chunk(pr, lchunk) * 8;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      int m = m0 + (pr >> 6) * 128 + h * 64 + (pr & 63);
-      m = m < g.M ? m : g.M - 1;
-      src[h ? 3 : 0][j] = g.A + (long)(m / g.a_rpg) * g.a_gstride + (long)(m % g.a_rpg) * g.a_rstride + sw;
-      int n = n0 + (pr >> 5) * 64 + h * 32 + (pr & 31);
-      n = n < g.N ? n : g.N - 1;
-      src[1 + h][j] = g.B + (long)n * g.ldb + sw;
-    }
-  }
-  const int nk = g.K / 64;
-  auto stage = [&](int pc, int u) {
-    if (u >= nk) return;
-    bf16_t* dst = smem + ((u & 1) * 4 + pc) * PH_PIECE + w * 1024;
-    glds16(src[pc][0] + ktile_off(g, u), dst);
-    glds16(src[pc][1] + ktile_off(g, u), dst + 512);
-  };
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int fr = lane & 15, fq = lane >> 4;
-  auto read_frags = [&](const bf16_t* piece, int rbase, int n16, bf16x8 (*out)[2]) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      if (i >= n16) break;
-      const int r = rbase + i * 16 + fr;
-#pragma unroll
-      for (int s = 0; s < 2; ++s)
-        out[i][s] = *reinterpret_cast<const bf16x8*>(piece + r * 64 + swz_chunk(r, s * 4 + fq) * 8);
-    }
-  };
-  auto barrier = [&]() {
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-  };
-  auto mfma_entry = [&]() {
-    __builtin_amdgcn_s_waitcnt((15) | (7 << 4) | (0 << 8) | (3 << 14));  // lgkmcnt(0) only
-    __builtin_amdgcn_sched_barrier(0);
-  };
-
-  // prologue: the stages of phases -6 .. -1 = P0(0) Q0(0) Q1(0) P1(0) P0(1) Q0(1); wait for P0(0), Q0(0)
-  stage(0, 0); stage(1, 0); stage(2, 0); stage(3, 0); stage(0, 1); stage(1, 1);
-  wait_vm_even(nk > 1 ? 8 : 4);
-  barrier();
-  if (wr == 1) barrier();  // the stagger
-
-  bf16x8 af[4][2], bq0[2][2], bq1[2][2];
-  for (int u = 0; u < nk; ++u) {
-    const int e1 = u + 1 < nk, e2 = u + 2 < nk;
-    const bf16_t* buf = smem + (u & 1) * 4 * PH_PIECE;
-    // phase 0: reads P0(u), Q0(u); waits for Q1(u) (read in phase 1); stages Q1(u+1)
-    wait_vm_even(2 * (1 + 2 * e1));
-    stage(2, u + 1);
-    read_frags(buf + 0 * PH_PIECE, wr * 64, 4, af);
-    read_frags(buf + 1 * PH_PIECE, wc * 32, 2, bq0);
-    barrier();
-    mfma_entry();
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][s], bq0[j][s], acc[i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-    barrier();
-    // phase 1: reads Q1(u); waits for P1(u); stages P1(u+1)
-    wait_vm_even(2 * 3 * e1);
-    stage(3, u + 1);
-    read_frags(buf + 2 * PH_PIECE, wc * 32, 2, bq1);
-    barrier();
-    mfma_entry();
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[i][2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][s], bq1[j][s], acc[i][2 + j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-    barrier();
-    // phase 2: reads P1(u); nothing to wait for (phase 3 reads nothing); stages P0(u+2)
-    stage(0, u + 2);
-    read_frags(buf + 3 * PH_PIECE, wr * 64, 4, af);
-    barrier();
-    mfma_entry();
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][s], bq0[j][s], acc[4 + i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-    barrier();
-    // phase 3: no reads; waits for P0(u+1), Q0(u+1) (read in phase (u+1,0)); stages Q0(u+2)
-    wait_vm_even(2 * (2 * e1 + e2));
-    stage(1, u + 2);
-    barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[4 + i][2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][s], bq1[j][s], acc[4 + i][2 + j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-    barrier();
-  }
-  if (wr == 0) barrier();  // rows leave with equal barrier counts
-
-  TOUT* C = reinterpret_cast<TOUT*>(g.C);
-  const unsigned long long dseed = mer_site_seed(g.drop_seed, g.drop_site);
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int col = n0 + wc * 64 + j * 16 + fr;
-    if (col >= g.N) continue;
-    const float bv = g.bias ? g.bias[col] : 0.f;
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = m0 + wr * 128 + i * 16 + fq * 4 + r;
-        if (row >= g.M) continue;
-        float v = epi_act_drop(acc[i][j][r] + bv, g.act, g.drop_p, dseed, (long)row * g.N + col);
-        if (g.R) v += bf2f(g.R[(long)row * g.ldr + col]);
-        stf<TOUT>(C, (long)row * g.ldc + col, v);
-      }
-  }
-}
-
-template <typename TOUT>
-int launch_pp_t(const GemmArgs& g, hipStream_t st) {
-  const long tiles = (long)((g.N + 255) / 256) * ((g.M + 255) / 256);
-  const size_t lds = 8 * PH_PIECE * sizeof(bf16_t);
-  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_pp_kernel<TOUT>),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
-    return (int)hipErrorInvalidConfiguration;
-  hipLaunchKernelGGL((gemm_pp_kernel<TOUT>), dim3((unsigned)tiles), dim3(PH_NT), lds, st, g);
-  return (int)hipGetLastError();
-}
-
-template <typename TOUT>
-int launch_phase_t(const GemmArgs& g, hipStream_t st) {
-  const long tiles = (long)((g.N + 255) / 256) * ((g.M + 255) / 256);
-  const size_t lds = 8 * PH_PIECE * sizeof(bf16_t);
-  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_phase_kernel<TOUT>),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
-    return (int)hipErrorInvalidConfiguration;
-  hipLaunchKernelGGL((gemm_phase_kernel<TOUT>), dim3((unsigned)tiles), dim3(PH_NT), lds, st, g);
-  return (int)hipGetLastError();
-}
-
-using CfgL = PipeCfg<256, 256, 2, 4>;  // 8 waves, 128x64 per wave, 128 KiB LDS
-using CfgM = PipeCfg<256, 128, 4, 2>;  // 8 waves, 64x64 per wave, 96 KiB LDS
-using CfgS = PipeCfg<128, 128, 2, 2>;  // 4 waves, 64x64 per wave, 64 KiB LDS
-using CfgP = PipeCfg<128, 64, 2, 2>;   // 4 waves, 64x32 per wave, 48 KiB LDS (pos-conv: 48 columns per group)
-using CfgS3 = PipeCfg<128, 128, 2, 2, 3>;  // 3-deep ring, 96 KiB LDS (1 block / CU)
-using CfgS4 = PipeCfg<128, 128, 2, 2, 4>;  // 4-deep ring, 128 KiB LDS
-using CfgM3 = PipeCfg<256, 128, 4, 2, 3>;  // 8 waves, 3-deep ring, 144 KiB LDS
-using CfgT3 = PipeCfg<128, 64, 2, 2, 3>;   // 128x64 tiles, 3-deep ring, 72 KiB LDS (2 blocks / CU)
-using CfgT2 = PipeCfg<128, 64, 2, 2, 2>;   // 128x64 tiles, 2-deep ring, 48 KiB LDS (3 blocks / CU)
-using CfgW2 = PipeCfg<128, 128, 2, 4, 2>;  // 8 waves (64x32 each), 2-deep, 64 KiB LDS (2 blocks / CU)
-using CfgW3 = PipeCfg<128, 128, 2, 4, 3>;  // 8 waves, 3-deep, 96 KiB LDS
-using CfgV3 = PipeCfg<128, 64, 4, 1, 3>;   // 4 waves as 4x1 (32x64 each), 3-deep, 72 KiB LDS
-using CfgX2 = PipeCfg<256, 128, 4, 4, 2>;  // 16 waves (64x32 each), 2-deep, 96 KiB LDS (1 block / CU)
-using CfgY2 = PipeCfg<256, 256, 4, 4, 2>;  // 16 waves (64x64 each), 2-deep, 128 KiB LDS
-using CfgY4 = PipeCfg<256, 256, 4, 4, 4, 32>;  // 16 waves, 32-wide K-tiles on a 4-deep ring, 128 KiB LDS
-using CfgT4 = PipeCfg<128, 64, 2, 2, 4, 32>;   // 128x64 tiles, 32-wide K on a 4-deep ring, 48 KiB LDS
-using CfgW4 = PipeCfg<128, 128, 2, 4, 4, 32>;  // 8 waves, 32-wide K on a 4-deep ring, 64 KiB LDS
-using CfgY32 = PipeCfg<256, 256, 4, 4, 2, 64, 3>;  // 16 waves, A 3-deep + B 2-deep rings, 160 KiB LDS
-using CfgL32 = PipeCfg<256, 256, 2, 4, 2, 64, 3>;  // 8 waves (128x64 each), A 3-deep + B 2-deep, 160 KiB LDS
+using CfgP = PipeCfg<128, 64, 2, 2>;   // 4 waves, 64x32 per wave, 48 KiB LDS (pos-conv gather: 48 columns per group)
+using CfgT3 = PipeCfg<128, 64, 2, 2, 3>;   // v7: 128x64 tiles, 3-deep ring, 72 KiB LDS (2 blocks / CU)
+using CfgW2 = PipeCfg<128, 128, 2, 4, 2>;  // v9: 8 waves (64x32 each), 2-deep, 64 KiB LDS (2 blocks / CU)
+using CfgY2 = PipeCfg<256, 256, 4, 4, 2>;  // v13: 16 waves (64x64 each), 2-deep, 128 KiB LDS
+using CfgY32 = PipeCfg<256, 256, 4, 4, 2, 64, 3>;  // v18: 16 waves, A 3-deep + B 2-deep rings, 160 KiB LDS
 
 template <class CF, typename TOUT, int AMODE>
 int launch_pipe_t(const GemmArgs& g, int groups, hipStream_t st) {
@@ -865,32 +487,21 @@ int launch_pipe(const GemmArgs& g, int out_dtype, hipStream_t st, int groups = 1
                                : launch_pipe_t<CF, float, AMODE>(g, groups, st);
 }
 
-// Tile choice (tools/bench_gemm.py on the B=32 WavLM shapes, MI355X): occupancy (waves per CU) is what
-// hides the DMA latency of this 2-deep pipeline, so the 16-wave 256x256 tile wins wherever its grid covers
-// most of the 256 CUs (conv1/conv2 as GEMMs, QKV, FFN-up: 0.80 / 0.82 / 0.49 / 0.64 PF); the 768-column
-// GEMMs have too few such tiles: FFN-down (K = 3072) runs 128x64 tiles with a 3-deep ring, the output
-// projection 128x128 tiles with 8 waves.  The 512-column feature-extractor convs below conv1 measured faster on
-// 128x128 tiles in round 2 (conv2 134 -> 130 us, conv3 79 -> 69 us, profiles/r02f/bench_gemm_convs.log) and slower
-// in round 4 (conv2 163 vs 128 us on the 256^2 ring, conv3 83 vs 80, conv4 45 vs 40, profiles/r04h/
-// bench_gemm_small_shapes.log); in the step the two are within noise (all variants bit-identical).
-// conv1 (1,200 tiles streaming a 314 MB A operand) takes the split ring (A three K-tiles deep, B two):
-// 278.6 -> 271.4 us; the same ring is 2-7 % slower on conv2 / conv3 / QKV / FFN-up / 4096^3
-// (profiles/r04/gemm_split_ring.log, all bit-identical).
-int pick_variant(int M, int N, int K) {
-  // Every shape on the 16-wave 256^2 split ring (v18: A three K-tiles deep).  On the few-tile shapes (FFN-down, the
-  // out-projection, conv5 / conv6: 38-76 tiles) that is LONGER wall time than the 128^2 / 128x64 tiles they had
-  // (FFN-down 33 -> 66 us on 57 CUs) but about half the CU-time (57 CUs x 66 us vs 228 x 33): the two-stream step is
-  // bound by CU-time and the trunk stream fills the CUs the encoder leaves idle.  Same-box A/Bs (profiles/r04j):
-  // 256^2 ring for all +1.1 % (twice), split ring over the plain ring +0.3 %, conv2-4 on the split ring too +0.1 %.
-  // MER_GEMM_WIDE=<variant> picks another wide variant (13, 19, 20); MER_GEMM_WIDE=0 the round-3 wall-time picks.
-  static const int wide = [] {
-    const char* e = getenv("MER_GEMM_WIDE");
-    return e ? atoi(e) : 18;
-  }();
-  if (wide == 13 || wide == 18 || wide == 19 || wide == 20) return wide;
+// Tile choice.  variant -1 = the WALL-TIME pick (tools/bench_gemm.py on the B=32 WavLM shapes): occupancy (waves
+// per CU) hides the DMA latency of the 2-deep pipeline, so the 16-wave 256x256 tile (v13) wins wherever its grid
+// covers most of the 256 CUs (QKV, FFN-up: 0.49 / 0.64 PF); conv1 (1,200 tiles streaming a 314 MB A operand) takes
+// the split ring (v18, A three K-tiles deep: 278.6 -> 271.4 us); the 768-column GEMMs and the 512-column convs
+// below conv1 have too few such tiles: 128x64 tiles on a 3-deep ring for K >= 2048 (FFN-down), 128x128 8-wave
+// tiles otherwise.  variant -2 = the CU-TIME pick for the train step's frozen forward, which runs on a side stream
+// beside the trunk: every shape on the v18 split ring.  On the few-tile shapes that is LONGER wall time (FFN-down
+// 33 -> 66 us on 57 CUs) but about half the CU-time (57 CUs x 66 us vs 228 x 33), and the two-stream step is bound
+// by CU-time: same-box +1.1 % (twice), split ring over the plain ring +0.3 % (profiles/r04j).  All variants are
+// bit-identical (same fragments, same k order).
+int pick_variant(int M, int N, int K, int rule) {
+  if (rule == -2) return 18;
   const long tl = (long)((M + 255) / 256) * ((N + 255) / 256);
   if (tl >= 1200 && N <= 512) return 18;
-  if (tl >= 160 && !(N <= 512 && tl < 1200)) return 13;
+  if (tl >= 160 && N > 512) return 13;
   return K >= 2048 ? 7 : 9;
 }
 
@@ -910,15 +521,7 @@ namespace {
 // Tile order: with at most 4 column tiles of 256 (conv1..6: N = 512) the B operand is a few hundred KB and always
 // L2-resident, while the A row panel is the stream: keep a panel's N-tiles adjacent (group 1) so they run in lockstep
 // on one XCD and fetch the panel once.  Wider outputs (QKV, FFN-up) walk 8-row bands (the B panels dominate).
-// MER_GEMM_GROUP overrides (A/B).
-int tile_group(int N) {
-  static const int env = [] {
-    const char* e = getenv("MER_GEMM_GROUP");
-    return e ? atoi(e) : 0;
-  }();
-  if (env > 0) return env;
-  return (N + 255) / 256 <= 4 ? 1 : 8;
-}
+int tile_group(int N) { return (N + 255) / 256 <= 4 ? 1 : 8; }
 
 // 16-byte epilogue accesses: 8-column runs never straddle N, and every row start is 16-byte aligned
 bool vec_epilogue_ok(int N, const void* C, long ldc, const void* R, long ldr, long c_zoff) {
@@ -950,7 +553,9 @@ MER_API int mer_gemm_bf16_tr(int M, int N, int K, const void* A, long a_gstride,
   if (M <= 0 || N <= 0) return 0;
   if (drop_p < 0.f || drop_p >= 1.f || (drop_p > 0.f && !drop_seed) || skip_bit < 0 || skip_bit > 62)
     return (int)hipErrorInvalidValue;
-  if (variant < -1 || variant > 20) return (int)hipErrorInvalidValue;
+  if (!(variant == -2 || variant == -1 || variant == 0 || variant == 7 || variant == 9 || variant == 13 ||
+        variant == 18))
+    return (int)hipErrorInvalidValue;
   if (K % 8 != 0 || a_rpg <= 0 || (a_rstride % 8) != 0 || (a_gstride % 8) != 0 || (ldw % 8) != 0)
     return (int)hipErrorInvalidValue;
   if ((((uintptr_t)A) | ((uintptr_t)W)) & 15) return (int)hipErrorInvalidValue;
@@ -963,11 +568,7 @@ MER_API int mer_gemm_bf16_tr(int M, int N, int K, const void* A, long a_gstride,
   g.vec_epi = vec_epilogue_ok(N, C, ldc, R, ldr, 0);
   g.tgroup = tile_group(N);
   g.drop_p = drop_p; g.drop_seed = drop_seed; g.drop_site = drop_site; g.skip_mask = skip_mask; g.skip_bit = skip_bit;
-  static const bool kperm_on = [] {
-    const char* e = getenv("MER_GEMM_KPERM");  // A/B switch for tools/bench_gemm.py (default on)
-    return !(e && e[0] == '0');
-  }();
-  if (kperm_on && a_rstride > 0 && a_rstride < K) {  // overlapping rows = a strided conv: taps of gcd(stride, K) channels
+  if (a_rstride > 0 && a_rstride < K) {  // overlapping rows = a strided conv: taps of gcd(stride, K) channels
     long a = a_rstride, b = K;
     while (b) { const long t = a % b; a = b; b = t; }
     if (a % 64 == 0 && K / a > 1) {
@@ -976,29 +577,13 @@ MER_API int mer_gemm_bf16_tr(int M, int N, int K, const void* A, long a_gstride,
     }
   }
   const hipStream_t st = (hipStream_t)stream;
-  if (K % 64 != 0) variant = 0;
-  if (variant == -1) variant = pick_variant(M, N, K);
+  if (K % 64 != 0) variant = 0;  // the register-staged kernel takes any K (multiple of 8)
+  if (variant < 0) variant = pick_variant(M, N, K, variant);
   switch (variant) {
-    case 1: return launch_pipe<CfgL>(g, c_dtype, st);
-    case 2: return launch_pipe<CfgM>(g, c_dtype, st);
-    case 3: return launch_pipe<CfgS>(g, c_dtype, st);
-    case 4: return launch_pipe<CfgS3>(g, c_dtype, st);
-    case 5: return launch_pipe<CfgS4>(g, c_dtype, st);
-    case 6: return launch_pipe<CfgM3>(g, c_dtype, st);
     case 7: return launch_pipe<CfgT3>(g, c_dtype, st);
-    case 8: return launch_pipe<CfgT2>(g, c_dtype, st);
     case 9: return launch_pipe<CfgW2>(g, c_dtype, st);
-    case 10: return launch_pipe<CfgW3>(g, c_dtype, st);
-    case 11: return launch_pipe<CfgV3>(g, c_dtype, st);
-    case 12: return launch_pipe<CfgX2>(g, c_dtype, st);
     case 13: return launch_pipe<CfgY2>(g, c_dtype, st);
-    case 14: return c_dtype == MER_BF16 ? launch_phase_t<bf16_t>(g, st) : launch_phase_t<float>(g, st);
-    case 15: return launch_pipe<CfgY4>(g, c_dtype, st);
-    case 16: return launch_pipe<CfgT4>(g, c_dtype, st);
-    case 17: return launch_pipe<CfgW4>(g, c_dtype, st);
     case 18: return launch_pipe<CfgY32>(g, c_dtype, st);
-    case 19: return launch_pipe<CfgL32>(g, c_dtype, st);
-    case 20: return c_dtype == MER_BF16 ? launch_pp_t<bf16_t>(g, st) : launch_pp_t<float>(g, st);
     default: return launch<0>(g, c_dtype, 1, st);
   }
 }
@@ -1121,7 +706,7 @@ __global__ __launch_bounds__(64 * NW, 2) void posconv_strip_kernel(int L, int ta
 
 MER_API int mer_posconv_gemm_bf16(int B, int L, int C_total, int groups, int taps, int pad, const void* X, long ldx,
                                   const void* Wp, void* out, int out_dtype, long ldo, const float* bias,
-                                  const void* R, long ldr, int act, void* stream) {
+                                  const void* R, long ldr, int act, int variant, void* stream) {
   const int cg = C_total / groups;
   if (cg * groups != C_total || cg % 8 != 0 || (ldx % 8) != 0) return (int)hipErrorInvalidValue;
   GemmArgs g{};
@@ -1132,11 +717,10 @@ MER_API int mer_posconv_gemm_bf16(int B, int L, int C_total, int groups, int tap
   g.bias = bias; g.R = (const bf16_t*)R; g.ldr = ldr; g.act = act;
   g.vec_epi = vec_epilogue_ok(cg, out, ldo, R, ldr, g.c_zoff);
   g.tgroup = 8;
-  // MER_POSCONV_CFG (A/B, read per call so a test can compare the kernels): 0 = 2-deep 128x64, 1 = 3-deep, 2 = 32-wide
-  // K on a 4-deep ring; 3 = the Toeplitz strip kernel (default where it applies)
-  const char* pc_env = getenv("MER_POSCONV_CFG");
-  const int pc_cfg = pc_env ? atoi(pc_env) : 3;
-  if (pc_cfg == 3 && cg == 48 && L <= PS_MAXL && taps <= PS_MAXT && (taps * cg) % PS_KC == 0 && out_dtype == MER_BF16 &&
+  // variant -1: the Toeplitz strip kernel where it applies, else the gather GEMM; 0: the gather GEMM (the strip
+  // kernel's bit-exact reference, tests/test_wavlm_gpu.py)
+  if (variant < -1 || variant > 0) return (int)hipErrorInvalidValue;
+  if (variant == -1 && cg == 48 && L <= PS_MAXL && taps <= PS_MAXT && (taps * cg) % PS_KC == 0 && out_dtype == MER_BF16 &&
       (ldx % 8) == 0 && (((uintptr_t)X | (uintptr_t)Wp) & 15) == 0) {
     // 4 waves of 3 fragments each (8 or 10 waves per block measured 77-89 us vs 75)
     hipLaunchKernelGGL((posconv_strip_kernel<48, 4>), dim3(groups, B), dim3(256), 0, (hipStream_t)stream, L, taps, pad,
@@ -1144,8 +728,6 @@ MER_API int mer_posconv_gemm_bf16(int B, int L, int C_total, int groups, int tap
     return (int)hipGetLastError();
   }
   if (g.K % 64 == 0 && (((uintptr_t)X | (uintptr_t)Wp) & 15) == 0) {
-    if (pc_cfg == 1) return launch_pipe<CfgT3, 1>(g, out_dtype, (hipStream_t)stream, groups);
-    if (pc_cfg == 2) return launch_pipe<CfgT4, 1>(g, out_dtype, (hipStream_t)stream, groups);
     return launch_pipe<CfgP, 1>(g, out_dtype, (hipStream_t)stream, groups);
   }
   return launch<1>(g, out_dtype, groups, (hipStream_t)stream);

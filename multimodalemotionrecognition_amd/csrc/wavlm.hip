@@ -330,72 +330,6 @@ __global__ __launch_bounds__(256) void layernorm_kernel(int rows, int d, const T
   }
 }
 
-// Two rows per wave (VEC shapes only, A/B: MER_LN_ROWS2=1): the same per-row arithmetic in the same order as
-// layernorm_kernel (bit-identical), with both rows' loads in flight together -- half the waves for the same latency.
-template <typename TI, typename TO>
-__global__ __launch_bounds__(256) void layernorm2_kernel(int rows, int d, const TI* __restrict__ x, long ldx,
-                                                         const float* __restrict__ gamma, const float* __restrict__ beta,
-                                                         float eps, TO* __restrict__ y, long ldy, float drop_p,
-                                                         const unsigned long long* __restrict__ seed_ptr,
-                                                         unsigned long long site, const long long* __restrict__ skip,
-                                                         int skip_bit) {
-  if (skip && ((*skip >> skip_bit) & 1ll)) return;
-  const int row0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 2, lane = threadIdx.x & 63;
-  if (row0 >= rows) return;
-  const int nr = rows - row0 < 2 ? 1 : 2;
-  const unsigned long long seed = mer_site_seed(seed_ptr, site);
-  const int nv = d >> 8;
-  f32x4 gv[4], bv[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    if (i >= nv) break;
-    gv[i] = *reinterpret_cast<const f32x4*>(gamma + (i * 64 + lane) * 4);
-    bv[i] = *reinterpret_cast<const f32x4*>(beta + (i * 64 + lane) * 4);
-  }
-  float vals[2][16], s[2] = {0.f, 0.f};
-#pragma unroll
-  for (int r = 0; r < 2; ++r) {
-    const TI* xr = x + (long)(row0 + (r < nr ? r : 0)) * ldx;  // a missing second row re-reads the first
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      if (i >= nv) break;
-      const f32x4 v = ld4<TI>(xr + (i * 64 + lane) * 4);
-      vals[r][4 * i] = v[0]; vals[r][4 * i + 1] = v[1]; vals[r][4 * i + 2] = v[2]; vals[r][4 * i + 3] = v[3];
-      s[r] += (v[0] + v[1]) + (v[2] + v[3]);
-    }
-  }
-  float mean[2], rstd[2];
-#pragma unroll
-  for (int r = 0; r < 2; ++r) mean[r] = wave_sum(s[r]) / d;
-#pragma unroll
-  for (int r = 0; r < 2; ++r) {
-    float q = 0.f;
-    for (int i = 0; i < 4 * nv; ++i) { const float v = vals[r][i] - mean[r]; q += v * v; }
-    rstd[r] = rsqrtf(wave_sum(q) / d + eps);
-  }
-#pragma unroll
-  for (int r = 0; r < 2; ++r) {
-    if (r >= nr) break;
-    const long row = row0 + r;
-    TO* yr = y + row * ldy;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      if (i >= nv) break;
-      const int c = (i * 64 + lane) * 4;
-      const f32x4 g = gv[i], b = bv[i];
-      f32x4 o;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) o[e] = (vals[r][4 * i + e] - mean[r]) * rstd[r] * g[e] + b[e];
-      if (drop_p > 0.f) {
-        float ov[4] = {o[0], o[1], o[2], o[3]};
-        dropout_pairs<4>(ov, seed, (uint64_t)(row * d + c), drop_p);
-        o = f32x4{ov[0], ov[1], ov[2], ov[3]};
-      }
-      st4<TO>(yr + c, o);
-    }
-  }
-}
-
 MER_API int mer_layernorm(int rows, int d, const void* x, int x_dtype, long ldx, const float* gamma,
                           const float* beta, float eps, void* y, int y_dtype, long ldy, void* stream) {
   return mer_layernorm_tr(rows, d, x, x_dtype, ldx, gamma, beta, eps, y, y_dtype, ldy, 0.f, nullptr, 0ull, nullptr, 0,
@@ -415,15 +349,9 @@ MER_API int mer_layernorm_tr(int rows, int d, const void* x, int x_dtype, long l
                    (((uintptr_t)x) & (x_dtype == MER_F32 ? 15 : 7)) == 0 &&
                    (((uintptr_t)y) & (y_dtype == MER_F32 ? 15 : 7)) == 0 &&
                    ((((uintptr_t)gamma) | ((uintptr_t)beta)) & 15) == 0;
-  const char* rows2_env = getenv("MER_LN_ROWS2");  // per call, so a test can compare the two kernels
-  const bool rows2 = rows2_env && rows2_env[0] == '1';
-  const dim3 grid2((rows + 7) / 8);
 #define L(TI, TO)                                                                                              \
   do {                                                                                                         \
-    if (vec && rows2)                                                                                          \
-      hipLaunchKernelGGL((layernorm2_kernel<TI, TO>), grid2, dim3(256), 0, st, rows, d, (const TI*)x, ldx,    \
-                         gamma, beta, eps, (TO*)y, ldy, drop_p, seed, site, skip_mask, skip_bit);             \
-    else if (vec)                                                                                              \
+    if (vec)                                                                                                   \
       hipLaunchKernelGGL((layernorm_kernel<TI, TO, true>), grid, dim3(256), 0, st, rows, d, (const TI*)x, ldx, \
                          gamma, beta, eps, (TO*)y, ldy, drop_p, seed, site, skip_mask, skip_bit);             \
     else                                                                                                       \
@@ -762,14 +690,10 @@ MER_API int mer_wavlm_attention_tr(int B, int L, int H, const void* qkv, long ld
   if ((ldqkv % 8) || (ldx % 8) || (ldo % 4) || ((((uintptr_t)qkv) | ((uintptr_t)x)) & 15) || (((uintptr_t)out) & 7))
     return (int)hipErrorInvalidValue;
   const int LP = (L + 15) / 16 * 16;
-  static const int nw_env = [] {  // MER_ATTN_NW: waves (16-row query tiles) per block, A/B switch
-    const char* e = getenv("MER_ATTN_NW");
-    return e ? atoi(e) : 0;
-  }();
   // 5 waves (80 query rows) per block: 2 blocks per (b, h) at L = 149.  The workgroup's waves land on SIMDs
   // 0,1,2,3,0, so SIMD 0 holds 2 of every block: at <= 4 waves per SIMD 2 blocks run per CU (the 768 blocks of
-  // B = 32 in 2 rounds).  MER_ATTN_NW=4 / 10 are the A/B alternatives.
-  const int NWsel = nw_env == 5 || nw_env == 10 || nw_env == 4 ? nw_env : 5;
+  // B = 32 in 2 rounds).  4 waves (1.5 rounds) lost 1.5 %, one 10-wave block per (b, h) (K/V staged once) 0.5 %
+  // of the step.
 #define MER_ATTN_LAUNCH(NW, KT)                                                                                   \
   do {                                                                                                           \
     const size_t lds = sizeof(bf16_t) * ((size_t)16 * KT * APAD + (size_t)ADH * (16 * KT + 8)) +                 \
@@ -779,15 +703,10 @@ MER_API int mer_wavlm_attention_tr(int B, int L, int H, const void* qkv, long ld
                        gate_const, rel_emb, bucket, (bf16_t*)out, ldo, scale, drop_p, seed, site, skip_mask,      \
                        skip_bit);                                                                                 \
   } while (0)
-  if (LP <= 160) {  // 10 key tiles in registers: the 3 s clip (L = 149)
-    if (NWsel == 10) MER_ATTN_LAUNCH(10, 10);
-    else if (NWsel == 5) MER_ATTN_LAUNCH(5, 10);
-    else MER_ATTN_LAUNCH(4, 10);
-  } else {
-    if (NWsel == 10) MER_ATTN_LAUNCH(10, 16);
-    else if (NWsel == 5) MER_ATTN_LAUNCH(5, 16);
-    else MER_ATTN_LAUNCH(4, 16);
-  }
+  if (LP <= 160)  // 10 key tiles in registers: the 3 s clip (L = 149)
+    MER_ATTN_LAUNCH(5, 10);
+  else
+    MER_ATTN_LAUNCH(5, 16);
 #undef MER_ATTN_LAUNCH
   MER_LAUNCH_CHECK();
 }

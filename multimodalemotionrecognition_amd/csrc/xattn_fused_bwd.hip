@@ -955,11 +955,7 @@ MER_API int mer_xh_wgrad(int nprob, const long long* table, float* ws, long long
   int blocks = 0;
   const long long need = wg_layout(nprob, table, &tab, &blocks);
   if (need < 0 || need > ws_floats) return (int)hipErrorInvalidValue;
-  static const int xcd_on = [] {  // MER_XH_WGRAD_XCD=0: tile-major round-robin order (A/B)
-    const char* e = getenv("MER_XH_WGRAD_XCD");
-    return (e && e[0] == '0') ? 0 : 1;
-  }();
-  tab.xcd = xcd_on;
+  tab.xcd = 1;  // split-major per XCD: the tiles of one row split (same dY slice) share an L2
   hipLaunchKernelGGL(xh_wgrad_kernel, dim3(blocks), dim3(512), 0, (hipStream_t)stream, tab, ws);
   // fold: one element per thread for the largest problem (each thread's split loads are one latency round, not
   // one per element it would otherwise loop over)

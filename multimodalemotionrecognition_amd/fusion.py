@@ -33,7 +33,6 @@ def _require_device(*ts):
                                "inputs to a 'cuda' device (the CPU reference lives in oracle/, test-only)")
 
 
-_OVERLAP_ENCODERS = os.environ.get("MER_OVERLAP_ENCODERS", "1") != "0"
 _SIDE_STREAMS = {}
 
 
@@ -625,7 +624,7 @@ class FusionModel(nn.Module):
                 a_seq = self.audio_model.encode_sequence(audio, prefix=got) if kind == "prefix" else got
                 return self.xattn_from_features(v_feat, a_seq)
             self._prefetched = None
-            side = _side_stream(video.device) if _OVERLAP_ENCODERS else None
+            side = _side_stream(video.device)
             # the encoders' graph outputs go to the head without a copy (graphs.borrow_outputs; the head's
             # graph copies them into its static inputs, an eager head takes its own copy)
             with G.borrow_outputs():

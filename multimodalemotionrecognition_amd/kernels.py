@@ -379,10 +379,11 @@ def gemm_bf16(a, w, out, *, M=None, K=None, rows=None, bias=None, residual=None,
     return out
 
 
-def posconv_gemm_bf16(x, wp, out, B, L, C, groups, taps, pad, bias, residual, act="gelu"):
+def posconv_gemm_bf16(x, wp, out, B, L, C, groups, taps, pad, bias, residual, act="gelu", variant=-1):
+    """``variant`` -1: the Toeplitz strip kernel where it applies; 0: the gather GEMM (its bit-exact reference)."""
     LIB("mer_posconv_gemm_bf16", B, L, C, groups, taps, pad, x.data_ptr(), x.stride(-2), wp.data_ptr(), out.data_ptr(),
         _dt(out), out.stride(-2), _ptr(bias), _ptr(residual), 0 if residual is None else residual.stride(-2),
-        ACT[act], stream_ptr())
+        ACT[act], int(variant), stream_ptr())
 
 
 def wavlm_conv0_gn_gelu(wav, w0, gamma, beta, out, eps=1e-5):
@@ -536,14 +537,12 @@ def partials_sum(parts_buf, out):
 # Pixels per wgrad split, at least (tools/bench_conv.py on the ResNet18 layers, MI355X): 1024 in general -- more,
 # shorter splits lose to the fold of their partial slabs -- but 256 for the tiny 1x1 downsample outputs (a K loop of
 # 16 64-pixel steps per split was the whole time: 26 -> 19 us) and 512 where the output has so many tiles that
-# 1024 leaves only 4 splits (layer4 3x3: 65 -> 58 us).  MER_WGRAD_MIN_PIX overrides (A/B).
-_WGRAD_MIN_PIX = int(os.environ.get("MER_WGRAD_MIN_PIX", "0"))
-_WGRAD_WGS = int(os.environ.get("MER_WGRAD_WGS", "768"))  # target workgroups per wgrad launch (A/B)
+# 1024 leaves only 4 splits (layer4 3x3: 65 -> 58 us).
+# Target workgroups per wgrad launch: 768 (256 / 384 / 512 lose 3.1 / 1.3 / 0.3 % of the step, 1024 loses 0.4 %).
+_WGRAD_WGS = 768
 
 
 def _wgrad_min_pix(out_elems, tiles):
-    if _WGRAD_MIN_PIX > 0:
-        return _WGRAD_MIN_PIX
     return 256 if out_elems <= 65536 else (512 if tiles >= 96 else 1024)
 
 

@@ -180,8 +180,8 @@ def make_loss(fusion_mode: str, label_smoothing: float = 0.0) -> nn.Module:
 
 
 # Early prefetch (FusionModel.queue_next_audio): the next batch's frozen audio encoder starts at the top of the
-# step instead of before its backward.  MER_EARLY_PREFETCH=0 restores the backward-only overlap (A/B).
-EARLY_PREFETCH = os.environ.get("MER_EARLY_PREFETCH", "1") != "0"
+# step instead of before its backward (tests set EARLY_PREFETCH = False for the backward-only overlap).
+EARLY_PREFETCH = True
 
 
 class TrainStep:

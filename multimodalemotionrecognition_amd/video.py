@@ -531,11 +531,11 @@ def _bnr_target(blk_sv, blk, arena):
     return (out, bc2, bms2, red2, cd, msd, redd), (red2, redd)
 
 
-# Deferred weight-gradient folds (default on; MER_WGRAD_DEFER=0 folds after every wgrad): the wgrad launches leave
+# Deferred weight-gradient folds (tests set WGRAD_DEFER = False to fold after every wgrad): the wgrad launches leave
 # their split-K slabs and the segment's join folds them all in one mer_wgrad_fold_batch launch -- ~30 launches of
 # 5-12 us each off the critical stream per step (the stem's zero / gather / add included).  (Round 3 also measured
 # the weight gradients on a third stream and folding after every N blocks: both slower or inside the noise, removed.)
-WGRAD_DEFER = os.environ.get("MER_WGRAD_DEFER", "1") != "0"
+WGRAD_DEFER = True
 # The downsample's input gradient fused into conv1's stride-2 dgrad (mer_conv_dgrad_ds): +1.2 % same-box vs the
 # separate 1x1 dgrad whose bf16 output the 3x3 dgrad read back as its residual (profiles/r04/ab_runs.txt)
 FUSED_DS_DGRAD = True

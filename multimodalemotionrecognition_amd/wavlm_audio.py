@@ -64,6 +64,14 @@ class WavLMConfigLite:
 SITE_TIME_MASK, SITE_ENC_DROPOUT = 1000, 1001
 
 
+def _gemm_pick(ctl) -> int:
+    """GEMM tile rule of a frozen forward (csrc/gemm_bf16.hip pick_variant): the train-mode forward (``ctl`` set)
+    is the one the train step prefetches on its side stream beside the trunk, where the step is bound by the two
+    streams' summed CU-time, so its GEMMs take the CU-time pick (-2: every shape on the 256^2 split ring); eval /
+    inference and the stage-2 tail run alone and keep the wall-time pick (-1)."""
+    return -2 if ctl is not None else -1
+
+
 def _layer_sites(li: int):
     """(attention probs, attention output, FFN activation, FFN output) dropout sites of encoder layer li."""
     b = 1100 + 8 * li
@@ -324,7 +332,7 @@ class WavLMBackbone(nn.Module):
                 return self._forward_graphed(wav, out_dtype, key, nl, draw)
         ctl = self.train_ctl(draw, wav.device)
         x, L = self._stage_a(wav)
-        y = self._conv_layer(x, 1, L)
+        y = self._conv_layer(x, 1, L, pick=_gemm_pick(ctl))
         return self._stage_b(y, L, out_dtype, nl, capture, ctl)
 
     def _forward_graphed(self, wav, out_dtype, key, nl=None, draw=None):
@@ -336,7 +344,7 @@ class WavLMBackbone(nn.Module):
                 ctl = self.train_ctl(draw, wav.device)
             def run(w):
                 x, L0 = self._stage_a(w)
-                return self._stage_b(self._conv_layer(x, 1, L0), L0, out_dtype, nl, None, ctl)
+                return self._stage_b(self._conv_layer(x, 1, L0, pick=_gemm_pick(ctl)), L0, out_dtype, nl, None, ctl)
 
             graph = G.StaticGraph(run, [wav])
             # the graph reads the packed weights captured with it: keep that pack alive (a later full repack,
@@ -357,14 +365,15 @@ class WavLMBackbone(nn.Module):
         K.wavlm_conv0_gn_gelu(wav, pk["conv0_w"], gn.weight, gn.bias, xg, eps=gn.eps)
         return xg, L
 
-    def _conv_layer(self, x, i, L, out=None):
-        """Feature-extractor conv i >= 1 as an implicit GEMM with fused GELU (TF:723-782)."""
+    def _conv_layer(self, x, i, L, out=None, pick=-1):
+        """Feature-extractor conv i >= 1 as an implicit GEMM with fused GELU (TF:723-782).  ``pick``: the GEMM
+        tile rule (-1 wall time, -2 CU-time: see ``_gemm_pick``)."""
         k, s = CONV_KERNEL[i], CONV_STRIDE[i]
         B = x.shape[0]
         L_out = (L - k) // s + 1
         y = out if out is not None else torch.empty(B, L_out, CONV_DIM, device=x.device, dtype=torch.bfloat16)
         K.gemm_bf16(x, self.packed_weights()["conv"][i - 1], y, M=B * L_out, K=k * CONV_DIM,
-                    rows=(L_out, s * CONV_DIM, L * CONV_DIM), act="gelu")
+                    rows=(L_out, s * CONV_DIM, L * CONV_DIM), act="gelu", variant=pick)
         return y
 
     def _stage_b(self, x, L0, out_dtype, num_layers, capture, ctl: Optional[TrainCtl] = None):
@@ -376,8 +385,9 @@ class WavLMBackbone(nn.Module):
         dev = x.device
         bf = torch.bfloat16
         L = (L0 - CONV_KERNEL[1]) // CONV_STRIDE[1] + 1
+        pick = _gemm_pick(ctl)
         for i in range(2, len(CONV_KERNEL)):
-            x = self._conv_layer(x, i, L)
+            x = self._conv_layer(x, i, L, pick=pick)
             L = x.shape[1]
         D = cfg.hidden_size
         fp = self.feature_projection
@@ -386,7 +396,7 @@ class WavLMBackbone(nn.Module):
         if capture is not None:
             capture["extract_features"] = xn.view(B, L, CONV_DIM).clone()
         h = torch.empty(B * L, D, device=dev, dtype=bf)
-        K.gemm_bf16(xn, pk["proj_w"], h, bias=fp.projection.bias)  # feat_proj_dropout = 0 (TF:98-104)
+        K.gemm_bf16(xn, pk["proj_w"], h, bias=fp.projection.bias, variant=pick)  # feat_proj_dropout = 0 (TF:98-104)
         tr = ctl is not None
         if tr and cfg.mask_time_prob > 0:  # SpecAugment on the projected features (TF:1063 -> 1006-1015)
             K.wavlm_time_mask(h, B, L, self.masked_spec_embed, cfg.mask_time_prob, cfg.mask_time_length,
@@ -415,7 +425,7 @@ class WavLMBackbone(nn.Module):
         # the residual sums each post-LayerNorm normalises (x + out_proj(att), x1 + ffn): bf16, like every other
         # activation of the encoder -- half the bytes of the fp32 sums the two GEMM epilogues used to write and the
         # LayerNorms to read back (the statistics are taken in fp32 over the stored values)
-        y32 = torch.empty(B * L, D, device=dev, dtype=bf)
+        ysum = torch.empty(B * L, D, device=dev, dtype=bf)
         x1 = torch.empty(B * L, D, device=dev, dtype=bf)
         ff = torch.empty(B * L, cfg.intermediate_size, device=dev, dtype=bf)
         ad, acd = (cfg.attention_dropout, cfg.activation_dropout) if tr else (0.0, 0.0)
@@ -427,19 +437,20 @@ class WavLMBackbone(nn.Module):
             # LayerDrop (train): every launch of a skipped layer is a no-op, so x passes through unchanged
             sk = dict(skip=ctl.skip, skip_bit=li) if tr else {}
             s_att, s_out, s_act, s_ffn = _layer_sites(li)
-            K.gemm_bf16(x, lw["qkv_w"], qkv, bias=lw["qkv_b"], **sk)
+            K.gemm_bf16(x, lw["qkv_w"], qkv, bias=lw["qkv_b"], variant=pick, **sk)
             K.wavlm_attention(qkv, x, at.gru_rel_pos_linear.weight, at.gru_rel_pos_linear.bias, lw["gate_c"],
                               bias_tbl, None, att, B, L, H, scale, drop_p=ad, rng=rng, site=s_att, **sk)
-            K.gemm_bf16(att, lw["out_w"], y32, bias=at.out_proj.bias, residual=x, drop_p=hd, rng=rng, site=s_out, **sk)
-            K.layernorm(y32, layer.layer_norm.weight, layer.layer_norm.bias, x1, eps=cfg.layer_norm_eps, **sk)
+            K.gemm_bf16(att, lw["out_w"], ysum, bias=at.out_proj.bias, residual=x, drop_p=hd, rng=rng, site=s_out,
+                        variant=pick, **sk)
+            K.layernorm(ysum, layer.layer_norm.weight, layer.layer_norm.bias, x1, eps=cfg.layer_norm_eps, **sk)
             K.gemm_bf16(x1, lw["ff1_w"], ff, bias=layer.feed_forward.intermediate_dense.bias, act="gelu",
-                        drop_p=acd, rng=rng, site=s_act, **sk)
-            K.gemm_bf16(ff, lw["ff2_w"], y32, bias=layer.feed_forward.output_dense.bias, residual=x1, drop_p=hd,
-                        rng=rng, site=s_ffn, **sk)
+                        drop_p=acd, rng=rng, site=s_act, variant=pick, **sk)
+            K.gemm_bf16(ff, lw["ff2_w"], ysum, bias=layer.feed_forward.output_dense.bias, residual=x1, drop_p=hd,
+                        rng=rng, site=s_ffn, variant=pick, **sk)
             last = li == nl - 1
             # train mode writes every layer in place (a skipped last layer must leave x as the output)
             xo = torch.empty(B * L, D, device=dev, dtype=out_dtype) if (last and not tr) else x
-            K.layernorm(y32, layer.final_layer_norm.weight, layer.final_layer_norm.bias, xo, eps=cfg.layer_norm_eps,
+            K.layernorm(ysum, layer.final_layer_norm.weight, layer.final_layer_norm.bias, xo, eps=cfg.layer_norm_eps,
                         **sk)
             x = xo
             if capture is not None and li == 0:
@@ -611,10 +622,7 @@ class WavLMBackbone(nn.Module):
             # backward's dp_ij - sum_j p_ij dp_ij cancels for peaked rows, so bf16 operands here would cost
             # the score-path gradients (q/k/gate) ~10% (tests/test_wavlm_stage2_gpu.py)
             datt = torch.empty(M, D, device=dev, dtype=f32)
-            if _DATT_F32:
-                K.gemm(go, at.out_proj.weight.detach(), datt)
-            else:
-                K.gemm_bf16(goh, _transposed(lw, "out_w", dev), datt)
+            K.gemm(go, at.out_proj.weight.detach(), datt)
             need_dx = k > 0
             dqkv = torch.empty(M, 3 * D, device=dev, dtype=bf)
             dxg = torch.empty(M, D, device=dev, dtype=f32) if need_dx else None
@@ -634,9 +642,6 @@ class WavLMBackbone(nn.Module):
                 dxq = torch.empty(M, D, device=dev, dtype=f32)
                 K.gemm_bf16(dqkv, _transposed(lw, "qkv_w", dev), dxq)
                 addends = (dxq, dy1, dxg)
-
-
-_DATT_F32 = __import__("os").environ.get("MER_DATT_F32", "1") != "0"
 
 
 def _pack_layer(layer, dev):

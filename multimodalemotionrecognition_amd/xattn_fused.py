@@ -20,7 +20,7 @@ from . import kernels as K
 
 ENABLED = os.environ.get("MER_XATTN_FUSED", "1") != "0"
 BWD_ENABLED = os.environ.get("MER_XATTN_FUSED_BWD", "1") != "0"
-WGRAD_ROWS = int(os.environ.get("MER_XH_WGRAD_ROWS", "256"))  # rows of dY / X per weight-gradient workgroup (M is split over the grid)
+WGRAD_ROWS = 256  # rows of dY / X per weight-gradient workgroup (M is split over the grid)
 
 # (weight name, row slice) for each split plane; rows are contiguous slices of the reference's parameters
 _PLANES = {

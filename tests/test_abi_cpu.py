@@ -143,3 +143,27 @@ def test_no_packed_fp32_instructions():
     from another stream (the GPU regression is tests/test_concurrency_gpu.py)."""
     pk = _codeobj_tool().packed_fp32_sites(ROOT / "multimodalemotionrecognition_amd" / "libmer_hip.so")
     assert pk == {}, sorted(pk.items(), key=lambda kv: -kv[1])[:10]
+
+
+def test_argument_checks_reject_before_any_launch():
+    """Argument validation returns hipErrorInvalidValue (1) before any HIP call, so it runs without a GPU:
+    the fused downsample dgrad refuses the register-staged variant 0 (it never reads the second K segment --
+    ADVICE r4), and the GEMM / positional-conv dispatchers refuse variants they do not build."""
+    from multimodalemotionrecognition_amd._lib import LIB
+
+    LIB.load()
+    f = LIB._fns
+    fake = 1 << 20  # never dereferenced: every call below fails its checks first
+    # mer_conv_dgrad_ds(N,H,W,C,K,R,S,stride,pad, dy, wt, dx, res, rmask, bn_mask, bn_x, bn_ms, bn_red, bn_x2,
+    #                   bn_ms2, bn_red2, ds_dy, ds_wt, ds_K, variant, stream)
+    args = [2, 8, 8, 64, 128, 3, 3, 2, 1, fake, fake, fake, None, None, None, None, None, None, None, None, None,
+            fake, fake, 64]
+    assert f["mer_conv_dgrad_ds"](*args, 0, None) == 1
+    assert f["mer_conv_dgrad_ds"](*args, 6, None) == 1
+    # mer_gemm_bf16_ex(M,N,K, A, gs, rs, rpg, W, ldw, C, dt, ldc, bias, R, ldr, act, variant, stream)
+    g = [64, 64, 64, fake, 64, 64, 64, fake, 64, fake, 1, 64, None, None, 0, 0]
+    for v in (1, 14, 20, -3):
+        assert f["mer_gemm_bf16_ex"](*g, v, None) == 1, v
+    # mer_posconv_gemm_bf16(B, L, C, groups, taps, pad, X, ldx, Wp, out, dt, ldo, bias, R, ldr, act, variant, stream)
+    assert f["mer_posconv_gemm_bf16"](2, 37, 768, 16, 128, 64, fake, 768, fake, fake, 1, 768, None, None, 0, 1, 3,
+                                      None) == 1

@@ -1,6 +1,6 @@
 """Standalone timing of the WavLM gated-rel-pos attention kernel at the C2 shape (B=32, L=149, 12 heads): eval and
 train mode (p = 0.1 dropout), HIP events around a captured graph of back-to-back launches on an otherwise idle GPU.
-    MER_ATTN_NW=4|5|10 python tools/bench_attn.py [--iters 200] [--batch 32]"""
+    python tools/bench_attn.py [--iters 200] [--batch 32]"""
 import argparse
 import os
 import sys
@@ -52,7 +52,7 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         us = e0.elapsed_time(e1) / args.iters * 1e3
-        print(f"wavlm attention B={B} L={L} {mode} NW={os.environ.get('MER_ATTN_NW', 'default')}: {us:.1f} us "
+        print(f"wavlm attention B={B} L={L} {mode}: {us:.1f} us "
               f"({flop / us / 1e6:.1f} TF/s)", flush=True)
 
 

@@ -1,6 +1,6 @@
 """Time the WavLM positional conv (grouped Conv1d(768, 768, k=128, pad=64, groups=16) + bias + GELU + residual, TF:82-90)
-as mer_posconv_gemm_bf16 at B=32, L=149, one captured graph of back-to-back launches; MER_POSCONV_CFG selects the
-tile / ring (A/B).  python tools/bench_posconv.py"""
+as mer_posconv_gemm_bf16 at B=32, L=149, one captured graph of back-to-back launches; --variant 0 times the gather GEMM instead of the strip kernel.
+python tools/bench_posconv.py [--variant 0]"""
 import sys
 from pathlib import Path
 
@@ -10,6 +10,7 @@ sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 from multimodalemotionrecognition_amd import kernels as K  # noqa: E402
 
 B, L, C, G, TAPS, PAD = 32, 149, 768, 16, 128, 64
+VARIANT = int(sys.argv[sys.argv.index('--variant') + 1]) if '--variant' in sys.argv else -1
 
 
 def main():
@@ -20,7 +21,7 @@ def main():
     bias = torch.randn(C, device="cuda") * 0.1
     out = torch.empty(B, L, C, device="cuda", dtype=torch.bfloat16)
     for _ in range(3):
-        K.posconv_gemm_bf16(x, wp, out, B, L, C, G, TAPS, PAD, bias, x)
+        K.posconv_gemm_bf16(x, wp, out, B, L, C, G, TAPS, PAD, bias, x, variant=VARIANT)
     torch.cuda.synchronize()
     reps = 20
     g = torch.cuda.CUDAGraph()
@@ -28,7 +29,7 @@ def main():
     s.wait_stream(torch.cuda.current_stream())
     with torch.cuda.graph(g, stream=s):
         for _ in range(reps):
-            K.posconv_gemm_bf16(x, wp, out, B, L, C, G, TAPS, PAD, bias, x)
+            K.posconv_gemm_bf16(x, wp, out, B, L, C, G, TAPS, PAD, bias, x, variant=VARIANT)
     torch.cuda.current_stream().wait_stream(s)
     g.replay()
     torch.cuda.synchronize()
