@@ -572,6 +572,35 @@ int mer_xh_a2v_fwd(int B, int T, int Ta, const float* q2, const float* kv2, cons
                    unsigned long long site_path, float scale, float* P2, float* o2, float* s_a, float* mean_a,
                    float* rstd_a, float* part, const float* bias, void* stream);
 
+/* Emotion-prior attention bias forward (EmotionPriorBiasAdapter, fusion.py:153-184, used at fusion.py:390-391;
+ * replaces xattn_head.prior_forward's ~14 launches), one workgroup per sample, exact fp32: pg = [mean_t v | mean_j a]
+ * [B][2d], h1 = dropout(relu(pg W0^T + b0)) [B][H1] (mask index b*H1 + j at `site`), prior = h1 W3^T + b3 [B][PD];
+ * the four token-bias Linears (w_*: [d + PD] rows, b_*: [1]) as token halves tt_* = token . w[:d] ([B*T] for vq / vk,
+ * [B*Ta] for ak / aq) and prior halves tp_* = prior . w[d:] + b ([B]); v2a_bias[b][i][j] = tanh(tt_vq + tt_ak + tp_vq
+ * + tp_ak) * scale [B][T][Ta], a2v_bias[b][j][i] = tanh(tt_aq + tt_vk + tp_aq + tp_vk) * scale [B][Ta][T].
+ * v [B*T][d], a [B*Ta][d] fp32 pre-attention tokens; d = 128, T <= 16, Ta <= 160, H1 <= 256, PD <= 16. */
+int mer_xh_prior_fwd(int B, int T, int Ta, int d, int H1, int PD, const float* v, const float* a, const float* W0,
+                     const float* b0, const float* W3, const float* b3, const float* w_vq, const float* b_vq,
+                     const float* w_ak, const float* b_ak, const float* w_aq, const float* b_aq, const float* w_vk,
+                     const float* b_vk, const float* scale, float drop_p, const unsigned long long* seed,
+                     unsigned long long site, float* pg, float* h1, float* prior, float* tt_vq, float* tt_ak,
+                     float* tt_aq, float* tt_vk, float* tp_vq, float* tp_ak, float* tp_aq, float* tp_vk,
+                     float* v2a_bias, float* a2v_bias, void* stream);
+
+/* Its backward (xattn_head.prior_backward's ~20 launches), one workgroup per sample: from dbias_v2a [B][T][Ta] and
+ * dbias_a2v [B][Ta][T], the token-half gradients dtt_* (layouts of tt_*), the prior-half gradients dtp_* [B], dprior
+ * [B][PD], dh1 [B][H1] (through the ReLU / dropout mask of the saved h1), dscale_part [B] (this sample's sum of
+ * dbias * tanh over both biases), and the token gradients ADDED into dv [B*T][d] / da [B*Ta][d] (token-bias Linears
+ * + mean pools).  The weight gradients are products of these with the saved tensors (grouped wgrad problems). */
+int mer_xh_prior_bwd(int B, int T, int Ta, int d, int H1, int PD, const float* dbias_v2a, const float* dbias_a2v,
+                     const float* tt_vq, const float* tt_ak, const float* tt_aq, const float* tt_vk,
+                     const float* tp_vq, const float* tp_ak, const float* tp_aq, const float* tp_vk,
+                     const float* scale, const float* w_vq, const float* w_ak, const float* w_aq, const float* w_vk,
+                     const float* W0, const float* W3, const float* h1, float drop_p, const unsigned long long* seed,
+                     unsigned long long site, float* dtt_vq, float* dtt_ak, float* dtt_aq, float* dtt_vk,
+                     float* dtp_vq, float* dtp_ak, float* dtp_aq, float* dtp_vk, float* dprior, float* dh1,
+                     float* dscale_part, float* dv, float* da, void* stream);
+
 /* F4: emb[b][128:256] = sum_tiles part / Ta (tile order), then the classifier: concat (gated = 0):
  * h = dropout(relu(emb W0^T + b0)) [B][H1], logits = h W3^T + b3; gated: h [B][H1 = 128], g = sigmoid(h W3^T + b3),
  * fused = g emb_v + (1 - g) emb_a (gsave [B], fsave [B][128]), logits = fused Wc^T + bc.  Exact fp32 FMA. */

@@ -11,11 +11,30 @@
 // operands are staged [pixel][channel] and read with the gfx950 LDS transpose (ds_read_b64_tr_b16).
 // BatchNorm (train mode: batch statistics, running-stat update with momentum 0.1 / unbiased var)
 // is split into a stats reduction fused into the conv epilogue, a finalize, and an apply pass.
+#include <type_traits>
+
 #include "common.h"
 #include "mer.h"
 
 typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;
 typedef __attribute__((ext_vector_type(4))) short s16x4;
+
+// Phase timestamps of the halo conv (tools/halo_phases.py builds a separate library with -DMER_CONV_TIMING; the
+// production library compiles CT() to nothing): wall_clock64() of workgroup blockIdx.x's thread 0 at slot k.
+#ifdef MER_CONV_TIMING
+static __device__ long long mer_ct_buf[512 * 64];
+#define CT(k) \
+  do { \
+    if (threadIdx.x == 0 && blockIdx.x < 512 && (k) < 64) mer_ct_buf[blockIdx.x * 64 + (k)] = wall_clock64(); \
+  } while (0)
+MER_API int mer_ct_read(long long* host) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(mer_ct_buf), sizeof(long long) * 512 * 64, 0, hipMemcpyDeviceToHost);
+}
+#else
+#define CT(k) \
+  do { \
+  } while (0)
+#endif
 
 namespace {
 
@@ -774,6 +793,297 @@ __device__ __forceinline__ ParClass par_class(const ConvGeom& g, int cls) {
   return c;
 }
 
+// Forward BatchNorm statistics of one output tile from the accumulator layout (column = lane & 15: two shuffles per
+// value; acc holds the stored, bf16-rounded outputs).  The cross-wave exchanges here and in conv_epilogue_vec go
+// through LDS only, so they use lds_barrier() (lgkmcnt(0) + s_barrier): a __syncthreads() would also drain every
+// outstanding global store and DMA (vmcnt(0)), which the persistent halo kernel overlaps with its next tile.  The WM waves sharing a column meet in LDS (red: >= WM*WN*TN*2
+// idle floats) in wave order; the block then STORES its per-column (sum, sumsq) into stats row stat_row -- every (row
+// tile, column) has exactly one writer, so the statistics (and every BatchNorm output) are bitwise deterministic.
+template <int FM, int FN, int WM, int WN>
+__device__ __forceinline__ void conv_tile_stats(const ConvGeom& g, const f32x4 (&acc)[FM][FN], float* red, int w,
+                                                int lane, int m0, int n0, int M, long stat_row) {
+  constexpr int TM = FM * 16, TN = FN * 16;
+  const int wr = w / WN, wc = w % WN, fr = lane & 15, fq = lane >> 4;
+  float part[FN][2];
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int col = n0 + wc * TN + j * 16 + fr;
+    float csum = 0.f, csq = 0.f;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wr * TM + i * 16 + fq * 4 + r;
+        if (row < M && col < g.Ncols) {
+          const float hv = acc[i][j][r];
+          csum += hv;
+          csq += hv * hv;
+        }
+      }
+    csum += __shfl_xor(csum, 16, 64);
+    csum += __shfl_xor(csum, 32, 64);
+    csq += __shfl_xor(csq, 16, 64);
+    csq += __shfl_xor(csq, 32, 64);
+    part[j][0] = csum;
+    part[j][1] = csq;
+  }
+  lds_barrier();
+  if (wr > 0 && fq == 0)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      red[((wr * WN + wc) * FN * 16 + j * 16 + fr) * 2] = part[j][0];
+      red[((wr * WN + wc) * FN * 16 + j * 16 + fr) * 2 + 1] = part[j][1];
+    }
+  lds_barrier();
+  if (wr == 0 && fq == 0) {
+    float* slab = g.stats + stat_row * g.Ncols * 2;
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int col = n0 + wc * TN + j * 16 + fr;
+      float t0 = part[j][0], t1 = part[j][1];
+#pragma unroll
+      for (int q = 1; q < WM; ++q) {
+        t0 += red[((q * WN + wc) * FN * 16 + j * 16 + fr) * 2];
+        t1 += red[((q * WN + wc) * FN * 16 + j * 16 + fr) * 2 + 1];
+      }
+      if (col < g.Ncols) {
+        slab[2 * col] = t0;
+        slab[2 * col + 1] = t1;
+      }
+    }
+  }
+}
+
+// The 16-byte conv epilogue: each wave stages fp32 accumulators of 16-row groups of its TM x TN sub-tile in its own
+// slice (WAVE_FLOATS floats at smemf + w * WAVE_FLOATS, idle LDS), then every lane owns 8 consecutive columns of one
+// row per pass: 16-byte residual / mask / BN-operand loads and one 16-byte bf16 store instead of 2-byte accesses per
+// element.  The fused column reductions (forward BN statistics of the stored bf16 values into stats row stat_row; the
+// dgrad's BN-backward sums into bnr_red row red_row_id) accumulate per lane over its rows, then meet across the lanes
+// sharing the columns (xor tree) and across the WM waves of a column (LDS, wave order): one writer per partial-row
+// element, fixed order.  out_row(row) = the output pixel of GEMM row `row`.  Called by every wave of the workgroup.
+// The epilogue's pass geometry: each wave stages GI 16-row groups at a time; a pass moves RPP rows, one per lane
+// group of LPR lanes (8 columns each)
+template <int FM, int FN, int WAVE_FLOATS>
+struct EpiGeo {
+  static constexpr int TM = FM * 16, TN = FN * 16, LDT = TN + 4;
+  static constexpr int GI0 = WAVE_FLOATS / (16 * LDT);
+  static constexpr int GI = GI0 < FM ? GI0 : FM;
+  static constexpr int LPR = TN / 8, RPP = 64 / LPR;
+  static constexpr int PPG = (GI * 16 + RPP - 1) / RPP;  // passes per staged group
+  static constexpr int NP = ((FM + GI - 1) / GI) * PPG;  // passes per tile
+};
+
+// The dgrad epilogue's global operands (residual, residual mask, BN mask, BN input(s), BN (mean, rstd) of its 8
+// columns), loaded AHEAD of the epilogue -- conv3x3_halo_kernel issues them before its K loop, so their latency hides
+// under the MFMAs instead of stalling the epilogue's passes one after another.  Same addresses as the in-epilogue
+// loads (rows past M clamped to row M - 1; those passes discard them).
+template <int NP>
+struct EpiPre {
+  u32x4 r[NP], m[NP], bm[NP], x[NP], x2[NP];
+  float mu[8], rs[8], mu2[8], rs2[8];
+};
+struct EpiNone {};
+
+template <bool DGRAD, int FM, int FN, int WM, int WN, int WAVE_FLOATS, class OutRow, int NP>
+__device__ __forceinline__ void conv_epilogue_prefetch(const ConvGeom& g, EpiPre<NP>& pre, int w, int lane, int m0,
+                                                       int n0, int M, OutRow out_row) {
+  using E = EpiGeo<FM, FN, WAVE_FLOATS>;
+  static_assert(NP == E::NP, "prefetch pass count");
+  const int wr = w / WN, wc = w % WN;
+  const int lr = lane / E::LPR, lc = (lane % E::LPR) * 8;
+  const int colv = n0 + wc * E::TN + lc;
+  const bool cok = colv < g.Ncols;
+  const bool do_bnr = DGRAD && g.bnr_red != nullptr;
+  const bool has_x2 = do_bnr && g.bnr_x2 != nullptr;
+  const u32x4 z = {0u, 0u, 0u, 0u};
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int col = cok ? colv + e : 0;
+    pre.mu[e] = do_bnr ? g.bnr_ms[2 * col] : 0.f;
+    pre.rs[e] = do_bnr ? g.bnr_ms[2 * col + 1] : 0.f;
+    pre.mu2[e] = has_x2 ? g.bnr_ms2[2 * col] : 0.f;
+    pre.rs2[e] = has_x2 ? g.bnr_ms2[2 * col + 1] : 0.f;
+  }
+#pragma unroll
+  for (int q = 0; q < NP; ++q) {
+    const int i0 = (q / E::PPG) * E::GI, rr = (q % E::PPG) * E::RPP;
+    int row = m0 + wr * E::TM + i0 * 16 + rr + lr;
+    row = row < M ? row : M - 1;
+    const long e0 = out_row(row) * g.ldy + (cok ? colv : 0);
+    pre.r[q] = (DGRAD && g.R_) ? *reinterpret_cast<const u32x4*>(g.R_ + e0) : z;
+    pre.m[q] = (DGRAD && g.R_ && g.Rmask) ? *reinterpret_cast<const u32x4*>(g.Rmask + e0) : z;
+    pre.bm[q] = do_bnr ? *reinterpret_cast<const u32x4*>(g.bnr_mask + e0) : z;
+    pre.x[q] = do_bnr ? *reinterpret_cast<const u32x4*>(g.bnr_x + e0) : z;
+    pre.x2[q] = has_x2 ? *reinterpret_cast<const u32x4*>(g.bnr_x2 + e0) : z;
+  }
+}
+
+template <bool DGRAD, int FM, int FN, int WM, int WN, int WAVE_FLOATS, class OutRow, class Pre = EpiNone>
+__device__ __forceinline__ void conv_epilogue_vec(const ConvGeom& g, f32x4 (&acc)[FM][FN], float* smemf, int w,
+                                                  int lane, int m0, int n0, int M, long red_row_id, long stat_row,
+                                                  OutRow out_row, const Pre* pre = nullptr) {
+  constexpr bool PREF = !std::is_same<Pre, EpiNone>::value;
+  using E = EpiGeo<FM, FN, WAVE_FLOATS>;
+  constexpr int TM = FM * 16, TN = FN * 16;
+  const int wr = w / WN, wc = w % WN, fr = lane & 15, fq = lane >> 4;
+  constexpr int LDT = TN + 4;
+  constexpr int GI = E::GI;
+  static_assert(GI >= 1, "epilogue staging slice too small");
+  constexpr int LPR = TN / 8, RPP = 64 / LPR;
+  float* wl = smemf + w * WAVE_FLOATS;
+  const int lr = lane / LPR, lc = (lane % LPR) * 8;
+  const int colv = n0 + wc * TN + lc;
+  const bool cok = colv < g.Ncols;
+  const bool do_bnr = DGRAD && g.bnr_red != nullptr;
+  const bool has_x2 = do_bnr && g.bnr_x2 != nullptr;
+  float mu[8], rs[8], mu2[8], rs2[8];
+  float sA[8], sB[8], sC[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    if constexpr (PREF) {
+      mu[e] = pre->mu[e];
+      rs[e] = pre->rs[e];
+      mu2[e] = pre->mu2[e];
+      rs2[e] = pre->rs2[e];
+    } else {
+      const int col = cok ? colv + e : 0;
+      mu[e] = do_bnr ? g.bnr_ms[2 * col] : 0.f;
+      rs[e] = do_bnr ? g.bnr_ms[2 * col + 1] : 0.f;
+      mu2[e] = has_x2 ? g.bnr_ms2[2 * col] : 0.f;
+      rs2[e] = has_x2 ? g.bnr_ms2[2 * col + 1] : 0.f;
+    }
+    sA[e] = sB[e] = sC[e] = 0.f;
+  }
+#pragma unroll
+  for (int i0 = 0; i0 < FM; i0 += GI) {
+#pragma unroll
+    for (int ii = 0; ii < GI; ++ii) {
+      if (i0 + ii >= FM) break;
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) wl[(ii * 16 + fq * 4 + r) * LDT + j * 16 + fr] = acc[i0 + ii][j][r];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int nrows = (FM - i0 < GI ? FM - i0 : GI) * 16;
+#pragma unroll
+    for (int rr = 0; rr < GI * 16; rr += RPP) {
+      const int rl = rr + lr;
+      const int row = m0 + wr * TM + i0 * 16 + rl;
+      if (rl < nrows && row < M && cok) {
+        const f32x4 lo = *reinterpret_cast<const f32x4*>(&wl[rl * LDT + lc]);
+        const f32x4 hi = *reinterpret_cast<const f32x4*>(&wl[rl * LDT + lc + 4]);
+        float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        const long e0 = out_row(row) * g.ldy + colv;
+        const int q = (i0 / GI) * E::PPG + rr / RPP;  // this pass's prefetch slot (static once the loops unroll)
+        if (DGRAD && g.R_) {
+          u32x4 rv, mv;
+          if constexpr (PREF) {
+            rv = pre->r[q];
+            mv = g.Rmask ? pre->m[q] : u32x4{1u, 1u, 1u, 1u};
+          } else {
+            rv = *reinterpret_cast<const u32x4*>(g.R_ + e0);
+            mv = g.Rmask ? *reinterpret_cast<const u32x4*>(g.Rmask + e0) : u32x4{1u, 1u, 1u, 1u};
+          }
+          const bf16_t* rh = reinterpret_cast<const bf16_t*>(&rv);
+          const bf16_t* mh = reinterpret_cast<const bf16_t*>(&mv);
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            if (!g.Rmask || bf2f(mh[e]) > 0.f) v[e] += bf2f(rh[e]);
+        }
+        u32x4 ov;
+        bf16_t* oh = reinterpret_cast<bf16_t*>(&ov);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          oh[e] = f2bf(v[e]);
+          v[e] = bf2f(oh[e]);  // the stored value feeds the reductions
+        }
+        *reinterpret_cast<u32x4*>(g.Y + e0) = ov;
+        if (do_bnr) {
+          u32x4 mv, xv, x2v;
+          if constexpr (PREF) {
+            mv = pre->bm[q];
+            xv = pre->x[q];
+            x2v = pre->x2[q];
+          } else {
+            mv = *reinterpret_cast<const u32x4*>(g.bnr_mask + e0);
+            xv = *reinterpret_cast<const u32x4*>(g.bnr_x + e0);
+            x2v = has_x2 ? *reinterpret_cast<const u32x4*>(g.bnr_x2 + e0) : u32x4{0u, 0u, 0u, 0u};
+          }
+          const bf16_t* mh = reinterpret_cast<const bf16_t*>(&mv);
+          const bf16_t* xh = reinterpret_cast<const bf16_t*>(&xv);
+          const bf16_t* x2h = reinterpret_cast<const bf16_t*>(&x2v);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float gv = bf2f(mh[e]) > 0.f ? v[e] : 0.f;
+            sA[e] += gv;
+            sB[e] += gv * (bf2f(xh[e]) - mu[e]) * rs[e];
+            if (has_x2) sC[e] += gv * (bf2f(x2h[e]) - mu2[e]) * rs2[e];
+          }
+        }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  if (do_bnr) {
+  // lanes sharing this lane's 8 columns: lane % LPR equal -> xor over the row bits of the lane index
+#pragma unroll
+  for (int o = LPR; o < 64; o <<= 1)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      sA[e] += __shfl_xor(sA[e], o, 64);
+      sB[e] += __shfl_xor(sB[e], o, 64);
+      if (has_x2) sC[e] += __shfl_xor(sC[e], o, 64);
+    }
+  // the WM waves of a column range meet in LDS: red[(wr*WN + wc)][TN][3]
+  float* red = smemf;
+  lds_barrier();  // every wave is past its staging slice
+  if (wr > 0 && lane < LPR)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float* o = red + ((wr * WN + wc) * TN + lc + e) * 3;
+      o[0] = sA[e];
+      o[1] = sB[e];
+      o[2] = sC[e];
+    }
+  lds_barrier();
+  if (wr != 0 || lane >= LPR || !cok) return;
+#pragma unroll
+  for (int e = 0; e < 8; ++e)
+#pragma unroll
+    for (int q = 1; q < WM; ++q) {
+      const float* o = red + ((q * WN + wc) * TN + lc + e) * 3;
+      sA[e] += o[0];
+      sB[e] += o[1];
+      sC[e] += o[2];
+    }
+  {
+    const long slab = red_row_id * g.Ncols * 2 + 2 * colv;
+#pragma unroll
+    for (int e = 0; e < 8; e += 2) {
+      *reinterpret_cast<f32x4*>(g.bnr_red + slab + 2 * e) = f32x4{sA[e], sB[e], sA[e + 1], sB[e + 1]};
+      if (g.bnr_red2)
+        *reinterpret_cast<f32x4*>(g.bnr_red2 + slab + 2 * e) = f32x4{sA[e], sC[e], sA[e + 1], sC[e + 1]};
+    }
+  }
+  return;
+  }  // do_bnr
+  if (!g.stats) return;
+  // forward BN statistics from the accumulator layout (column = lane & 15: two shuffles per value, cheaper than
+  // the 8-column lane reduction) over the stored, bf16-rounded values
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[i][j][r] = bf2f(f2bf(acc[i][j][r]));
+  conv_tile_stats<FM, FN, WM, WN>(g, acc, smemf, w, lane, m0, n0, M, stat_row);
+}
+
 // STAGES-deep LDS ring (cdna_hip_programming.md "Pipelining across barriers"): tiles kt+1 .. kt+STAGES-2 stay
 // in flight across the barrier that publishes tile kt (counted vmcnt, raw s_barrier); the barrier also retires
 // every wave's reads of tile kt-1, whose buffer the DMA of tile kt+STAGES-1 then reuses.
@@ -882,7 +1192,6 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN >= 16 ? 1 : 2) void conv_pipe
 
   const int fr = lane & 15, fq = lane >> 4;
   const int nk = (Kr + KS - 1) / KS;
-  float part[FN][2];
   constexpr int G = IA + IB;
   static_assert(STAGES >= 2 && STAGES <= 4, "ring depth");
 #pragma unroll
@@ -938,148 +1247,9 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN >= 16 ? 1 : 2) void conv_pipe
     return row_id;
   };
   if (g.vec) {
-    // 16-byte epilogue: each wave stages fp32 accumulators of 16-row groups of its TM x TN sub-tile in its own
-    // slice of the idle LDS ring, then every lane owns 8 consecutive columns of one row per pass: 16-byte
-    // residual / mask / BN-operand loads and one 16-byte bf16 store instead of 2-byte accesses per element.
-    // The fused column reductions (forward BN statistics of the stored bf16 values; the dgrad's BN-backward
-    // sums) accumulate per lane over its rows, then meet across the lanes sharing the columns (xor tree) and
-    // across the WM waves of a column (LDS, wave order): one writer per partial-row element, fixed order.
-    constexpr int LDT = TN + 4;
-    constexpr int WAVE_FLOATS = STAGES * BUF / 2 / WAVES;
-    constexpr int GI0 = WAVE_FLOATS / (16 * LDT);
-    constexpr int GI = GI0 < FM ? GI0 : FM;
-    static_assert(GI >= 1, "epilogue staging slice too small");
-    constexpr int LPR = TN / 8, RPP = 64 / LPR;
-    float* wl = reinterpret_cast<float*>(smem) + w * WAVE_FLOATS;
-    const int lr = lane / LPR, lc = (lane % LPR) * 8;
-    const int colv = n0 + wc * TN + lc;
-    const bool cok = colv < g.Ncols;
-    const bool do_bnr = DGRAD && g.bnr_red != nullptr;
-    const bool has_x2 = do_bnr && g.bnr_x2 != nullptr;
-    float mu[8], rs[8], mu2[8], rs2[8];
-    float sA[8], sB[8], sC[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int col = cok ? colv + e : 0;
-      mu[e] = do_bnr ? g.bnr_ms[2 * col] : 0.f;
-      rs[e] = do_bnr ? g.bnr_ms[2 * col + 1] : 0.f;
-      mu2[e] = has_x2 ? g.bnr_ms2[2 * col] : 0.f;
-      rs2[e] = has_x2 ? g.bnr_ms2[2 * col + 1] : 0.f;
-      sA[e] = sB[e] = sC[e] = 0.f;
-    }
-#pragma unroll
-    for (int i0 = 0; i0 < FM; i0 += GI) {
-#pragma unroll
-      for (int ii = 0; ii < GI; ++ii) {
-        if (i0 + ii >= FM) break;
-#pragma unroll
-        for (int j = 0; j < FN; ++j)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) wl[(ii * 16 + fq * 4 + r) * LDT + j * 16 + fr] = acc[i0 + ii][j][r];
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      const int nrows = (FM - i0 < GI ? FM - i0 : GI) * 16;
-#pragma unroll
-      for (int rr = 0; rr < GI * 16; rr += RPP) {
-        const int rl = rr + lr;
-        const int row = m0 + wr * TM + i0 * 16 + rl;
-        if (rl < nrows && row < M && cok) {
-          const f32x4 lo = *reinterpret_cast<const f32x4*>(&wl[rl * LDT + lc]);
-          const f32x4 hi = *reinterpret_cast<const f32x4*>(&wl[rl * LDT + lc + 4]);
-          float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-          const long e0 = out_row(row) * g.ldy + colv;
-          if (DGRAD && g.R_) {
-            const u32x4 rv = *reinterpret_cast<const u32x4*>(g.R_ + e0);
-            const u32x4 mv = g.Rmask ? *reinterpret_cast<const u32x4*>(g.Rmask + e0) : u32x4{1u, 1u, 1u, 1u};
-            const bf16_t* rh = reinterpret_cast<const bf16_t*>(&rv);
-            const bf16_t* mh = reinterpret_cast<const bf16_t*>(&mv);
-#pragma unroll
-            for (int e = 0; e < 8; ++e)
-              if (!g.Rmask || bf2f(mh[e]) > 0.f) v[e] += bf2f(rh[e]);
-          }
-          u32x4 ov;
-          bf16_t* oh = reinterpret_cast<bf16_t*>(&ov);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            oh[e] = f2bf(v[e]);
-            v[e] = bf2f(oh[e]);  // the stored value feeds the reductions
-          }
-          *reinterpret_cast<u32x4*>(g.Y + e0) = ov;
-          if (do_bnr) {
-            const u32x4 mv = *reinterpret_cast<const u32x4*>(g.bnr_mask + e0);
-            const u32x4 xv = *reinterpret_cast<const u32x4*>(g.bnr_x + e0);
-            const u32x4 x2v = has_x2 ? *reinterpret_cast<const u32x4*>(g.bnr_x2 + e0) : u32x4{0u, 0u, 0u, 0u};
-            const bf16_t* mh = reinterpret_cast<const bf16_t*>(&mv);
-            const bf16_t* xh = reinterpret_cast<const bf16_t*>(&xv);
-            const bf16_t* x2h = reinterpret_cast<const bf16_t*>(&x2v);
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-              const float gv = bf2f(mh[e]) > 0.f ? v[e] : 0.f;
-              sA[e] += gv;
-              sB[e] += gv * (bf2f(xh[e]) - mu[e]) * rs[e];
-              if (has_x2) sC[e] += gv * (bf2f(x2h[e]) - mu2[e]) * rs2[e];
-            }
-          }
-        }
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    }
-    if (do_bnr) {
-    // lanes sharing this lane's 8 columns: lane % LPR equal -> xor over the row bits of the lane index
-#pragma unroll
-    for (int o = LPR; o < 64; o <<= 1)
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        sA[e] += __shfl_xor(sA[e], o, 64);
-        sB[e] += __shfl_xor(sB[e], o, 64);
-        if (has_x2) sC[e] += __shfl_xor(sC[e], o, 64);
-      }
-    // the WM waves of a column range meet in LDS: red[(wr*WN + wc)][TN][3]
-    float* red = reinterpret_cast<float*>(smem);
-    __syncthreads();  // every wave is past its staging slice
-    if (wr > 0 && lane < LPR)
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        float* o = red + ((wr * WN + wc) * TN + lc + e) * 3;
-        o[0] = sA[e];
-        o[1] = sB[e];
-        o[2] = sC[e];
-      }
-    __syncthreads();
-    if (wr != 0 || lane >= LPR || !cok) return;
-#pragma unroll
-    for (int e = 0; e < 8; ++e)
-#pragma unroll
-      for (int q = 1; q < WM; ++q) {
-        const float* o = red + ((q * WN + wc) * TN + lc + e) * 3;
-        sA[e] += o[0];
-        sB[e] += o[1];
-        sC[e] += o[2];
-      }
-    {
-      const long slab = red_row() * g.Ncols * 2 + 2 * colv;
-#pragma unroll
-      for (int e = 0; e < 8; e += 2) {
-        *reinterpret_cast<f32x4*>(g.bnr_red + slab + 2 * e) = f32x4{sA[e], sB[e], sA[e + 1], sB[e + 1]};
-        if (g.bnr_red2)
-          *reinterpret_cast<f32x4*>(g.bnr_red2 + slab + 2 * e) = f32x4{sA[e], sC[e], sA[e + 1], sC[e + 1]};
-      }
-    }
+    conv_epilogue_vec<DGRAD, FM, FN, WM, WN, STAGES * BUF / 2 / WAVES>(
+        g, acc, reinterpret_cast<float*>(smem), w, lane, m0, n0, M, (DGRAD && g.bnr_red) ? red_row() : 0l, ty, out_row);
     return;
-    }  // do_bnr
-    if (!g.stats) return;
-    // forward BN statistics from the accumulator layout (column = lane & 15: two shuffles per value, cheaper than
-    // the 8-column lane reduction) over the stored, bf16-rounded values
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) acc[i][j][r] = bf2f(f2bf(acc[i][j][r]));
   } else {
 #pragma unroll
   for (int i = 0; i < FM; ++i)
@@ -1178,59 +1348,7 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN >= 16 ? 1 : 2) void conv_pipe
     }
   }
   }  // !g.vec
-  if (g.stats) {
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      const int col = n0 + wc * TN + j * 16 + fr;
-      float csum = 0.f, csq = 0.f;
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = m0 + wr * TM + i * 16 + fq * 4 + r;
-          if (row < M && col < g.Ncols) {
-            const float hv = acc[i][j][r];
-            csum += hv;
-            csq += hv * hv;
-          }
-        }
-      csum += __shfl_xor(csum, 16, 64);
-      csum += __shfl_xor(csum, 32, 64);
-      csq += __shfl_xor(csq, 16, 64);
-      csq += __shfl_xor(csq, 32, 64);
-      part[j][0] = csum;
-      part[j][1] = csq;
-    }
-    // the WM waves sharing a column meet in LDS (the staging buffers are idle now), in wave order; the block
-    // then STORES its per-column (sum, sumsq) into stats row ty -- every (row tile, column) has exactly one
-    // writer, so the statistics (and with them every BatchNorm output) are bitwise deterministic
-    float* red = reinterpret_cast<float*>(smem);
-    __syncthreads();
-    if (wr > 0 && fq == 0)
-#pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        red[((wr * WN + wc) * FN * 16 + j * 16 + fr) * 2] = part[j][0];
-        red[((wr * WN + wc) * FN * 16 + j * 16 + fr) * 2 + 1] = part[j][1];
-      }
-    __syncthreads();
-    if (wr == 0 && fq == 0) {
-      float* slab = g.stats + (long)ty * g.Ncols * 2;
-#pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        const int col = n0 + wc * TN + j * 16 + fr;
-        float t0 = part[j][0], t1 = part[j][1];
-#pragma unroll
-        for (int q = 1; q < WM; ++q) {
-          t0 += red[((q * WN + wc) * FN * 16 + j * 16 + fr) * 2];
-          t1 += red[((q * WN + wc) * FN * 16 + j * 16 + fr) * 2 + 1];
-        }
-        if (col < g.Ncols) {
-          slab[2 * col] = t0;
-          slab[2 * col + 1] = t1;
-        }
-      }
-    }
-  }
+  if (g.stats) conv_tile_stats<FM, FN, WM, WN>(g, acc, reinterpret_cast<float*>(smem), w, lane, m0, n0, M, ty);
 }
 
 template <bool DGRAD, bool PAR, int BM_, int BN_, int WM = 2, int WN = 2, int STAGES = 2, int KS = 64>
@@ -1325,6 +1443,179 @@ int launch_conv(ConvGeom& g, hipStream_t st) {
 // (tools/bench_conv.py, ResNet18 layers at 256 frames: the global_load_lds ring, variant 4, is 1.1-1.25x the
 // register-staged kernel on the stem, layer1, layer3 and layer4 and within 4% elsewhere; its 3-stage form, at one
 // block per CU, is slower)
+// ---------------------------------------------------------------------------------------
+// Stride-1 3x3 convolutions with 64 input and 64 output channels on 28-wide maps (ResNet18 layer1 at 112^2 frames,
+// forward and input gradient).  conv_pipe_kernel re-fetches every input pixel from L2 once per tap (9x) and waits one
+// DMA round trip per 64-deep K-step with ~8 MFMAs per wave behind it: latency-bound, layer1 ran at 200-380 TF/s.
+// Here one persistent workgroup per CU keeps the whole packed weight [64][9*64] resident in LDS (73.7 KB) and stages,
+// per 128-pixel output tile, the HALO its 9 taps read -- (rows + 2) x (W + 2) pixels x 64 channels, zero border
+// columns -- double-buffered, so tile i+1's halo streams in while tile i computes.  The K loop is LDS -> MFMA only:
+// no global load, no barrier.  The A fragment of tap (dr, ds) for output pixel (y, x) is halo pixel (y + dr, x + 1 +
+// ds), the same 16 bytes conv_pipe_kernel gathers; K-steps run in the same (tap, channel) order on the same MFMA with
+// the same wave layout and the same epilogue (conv_epilogue_vec), so outputs, BN statistics and BN-backward sums are
+// bit-identical to conv_pipe_kernel's (tests/test_resnet_gpu.py).  Both LDS images are XOR-swizzled per 16-byte chunk
+// (chunk c of pixel / weight row r at c ^ ((r >> 1) & 7)), which spreads a fragment's 16 rows over all 16 bank slots.
+// ---------------------------------------------------------------------------------------
+namespace halo {
+constexpr int BM = 128, C = 64, KRED = 9 * C, WCH = KRED / 8;  // tile rows, channels, reduction, 16-B chunks per weight row
+template <int W>
+struct Geo {
+  static constexpr int HW = W + 2;                       // halo row width (pixels)
+  static constexpr int ROWS = (W + BM - 2) / W + 1 + 2;  // image rows 128 consecutive pixels span, + 2 halo rows
+  static constexpr int CH = (ROWS * HW * 8 + 63) / 64 * 64;  // 16-byte chunks per halo buffer (whole glds pieces)
+  static constexpr int ELEMS = CH * 8;                   // bf16 elements per halo buffer
+  static constexpr int LDS_ELEMS = 64 * KRED + 2 * ELEMS + 64;  // weights, two halo buffers, one zero pixel
+};
+}  // namespace halo
+
+template <bool DGRAD, int WM, int WN, int W_>
+__global__ __launch_bounds__(64 * WM * WN, 1) void conv3x3_halo_kernel(ConvGeom g) {
+  using GE = halo::Geo<W_>;
+  constexpr int WAVES = WM * WN;
+  constexpr int TM = halo::BM / WM, TN = 64 / WN, FM = TM / 16, FN = TN / 16;
+  constexpr int HW = GE::HW;
+  extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
+  bf16_t* const wlds = smem;
+  bf16_t* const hbuf = smem + 64 * halo::KRED;
+  bf16_t* const zpix = hbuf + 2 * GE::ELEMS;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int wr = w / WN, wc = w % WN, fr = lane & 15, fq = lane >> 4;
+  const int H = g.OH, M = g.N * g.OH * W_, rows_total = g.N * g.OH;
+  const int ntiles = (M + halo::BM - 1) / halo::BM;
+  const bf16_t* zero = reinterpret_cast<const bf16_t*>(mer_conv_zero16);
+  int tile = blockIdx.x;
+  CT(0);
+
+  // halo of `tl`: image rows gr0 .. gr0 + ROWS - 1 (global row = frame * H + y; gr0 = the tile's first row - 1),
+  // columns -1 .. W; chunk L of the buffer holds pixel L / 8, logical channel chunk (L % 8) ^ ((pixel >> 1) & 7)
+  auto stage_halo = [&](bf16_t* hb, int tl) {
+    const int gr0 = (tl * halo::BM) / W_ - 1;
+    for (int j = w; j < GE::CH / 64; j += WAVES) {
+      const int L = j * 64 + lane;
+      const int hp = L >> 3, c = (L & 7) ^ ((hp >> 1) & 7);
+      const int hr = hp / HW, x = hp - hr * HW - 1, gr = gr0 + hr;
+      const bool ok = hr < GE::ROWS && gr >= 0 && gr < rows_total && x >= 0 && x < W_;
+      glds16(ok ? g.X + ((long)gr * W_ + x) * halo::C + c * 8 : zero, hb + j * 512);
+    }
+  };
+  // resident weights: row n (output column) x 72 chunks, chunk c of row n at (c & ~7) | ((c & 7) ^ ((n >> 1) & 7))
+  for (int j = w; j < halo::WCH; j += WAVES) {  // 64 rows x 72 chunks = 72 glds pieces of 64 chunks
+    const int L = j * 64 + lane;
+    const int n = L / halo::WCH, pc = L - n * halo::WCH;
+    const int c = (pc & ~7) | ((pc & 7) ^ ((n >> 1) & 7));
+    glds16(g.Wt + (long)n * halo::KRED + c * 8, wlds + j * 512);
+  }
+  stage_halo(hbuf, tile);
+  if (t < 8) *reinterpret_cast<u32x4*>(zpix + t * 8) = u32x4{0u, 0u, 0u, 0u};
+  wait_vmcnt<0>();
+  __syncthreads();
+  CT(1);
+
+  // Per tile: issue the next tile's halo DMA, run the K loop on this one, wait for that DMA (and the previous tile's
+  // epilogue stores -- both had the whole K loop to land), then the epilogue (staged through this tile's halo buffer,
+  // now free).  No vmcnt wait follows the epilogue: its stores drain under the next K loop.
+  for (int cur = 0, it = 0; tile < ntiles; tile += gridDim.x, cur ^= 1, ++it) {
+    bf16_t* const hb = hbuf + cur * GE::ELEMS;
+    if (tile + (int)gridDim.x < ntiles) stage_halo(hbuf + (cur ^ 1) * GE::ELEMS, tile + gridDim.x);
+    CT(2 + 5 * it);
+    const int m0 = tile * halo::BM, gr0 = m0 / W_ - 1;
+    const auto out_row = [](int row) { return (long)row; };
+    constexpr int EWF = GE::ELEMS / 2 / WAVES;  // epilogue staging floats per wave (this tile's halo buffer)
+    EpiPre<EpiGeo<FM, FN, EWF>::NP> pre;
+    if constexpr (DGRAD) conv_epilogue_prefetch<DGRAD, FM, FN, WM, WN, EWF>(g, pre, w, lane, m0, 0, M, out_row);
+    int hpb[FM], yv[FM];  // per fragment row of this lane: halo pixel of the centre tap, image row y
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      int m = m0 + wr * TM + i * 16 + fr;
+      m = m < M ? m : M - 1;  // rows past M compute garbage that the epilogue discards
+      const int gr = m / W_, x = m - gr * W_;
+      yv[i] = gr - (gr / H) * H;
+      hpb[i] = (gr - gr0) * HW + x + 1;
+    }
+    f32x4 acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // 18 k-steps of 32 = (tap, channel half), tap-major: the fragments of step u + 1 are read while step u's MFMAs
+    // run (two register sets, static indices: the loop is fully unrolled)
+    bf16x8 af[2][FM], bfr[2][FN];
+    auto frags = [&](int u, bf16x8 (&a)[FM], bf16x8 (&b)[FN]) {
+      const int tap = u >> 1, sub = u & 1;
+      const int r = tap / 3, s = tap - 3 * (tap / 3);
+      const int dr = DGRAD ? 1 - r : r - 1, ds = DGRAD ? 1 - s : s - 1;  // source pixel offset of this tap
+      const int c = sub * 4 + fq;  // logical 16-byte chunk (8 channels) of this lane's k slice
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int hp = hpb[i] + dr * HW + ds;
+        const bool ok = (unsigned)(yv[i] + dr) < (unsigned)H;  // rows outside the frame read the zero pixel
+        a[i] = *reinterpret_cast<const bf16x8*>(ok ? hb + hp * 64 + ((c ^ ((hp >> 1) & 7)) << 3) : zpix);
+      }
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int n = wc * TN + j * 16 + fr, cb = tap * 8 + c;
+        b[j] = *reinterpret_cast<const bf16x8*>(wlds + n * halo::KRED + (((cb & ~7) | ((cb & 7) ^ ((n >> 1) & 7))) << 3));
+      }
+    };
+    frags(0, af[0], bfr[0]);
+#pragma unroll
+    for (int u = 0; u < 18; ++u) {
+      if (u + 1 < 18) frags(u + 1, af[(u + 1) & 1], bfr[(u + 1) & 1]);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[u & 1][i], bfr[u & 1][j], acc[i][j], 0, 0, 0);
+    }
+    CT(3 + 5 * it);
+    wait_vmcnt<0>();  // this wave's share of the next halo (and the previous epilogue's stores) has landed
+    lds_barrier();    // every wave's: the next halo is complete and no wave still reads hb
+    CT(4 + 5 * it);
+    if constexpr (DGRAD)
+      conv_epilogue_vec<DGRAD, FM, FN, WM, WN, EWF>(g, acc, reinterpret_cast<float*>(hb), w, lane, m0, 0, M, (long)tile,
+                                                    (long)tile, out_row, &pre);
+    else
+      conv_epilogue_vec<DGRAD, FM, FN, WM, WN, EWF>(g, acc, reinterpret_cast<float*>(hb), w, lane, m0, 0, M, (long)tile,
+                                                    (long)tile, out_row);
+    CT(5 + 5 * it);
+    lds_barrier();    // every wave is past its epilogue's use of hb before the DMA two tiles on refills it
+    CT(6 + 5 * it);
+  }
+}
+
+// conv3x3_halo_kernel applies: 3x3 / stride 1 / pad 1, 64 -> 64 channels, 28-wide maps, 16-byte epilogue, no fused
+// downsample segment
+bool halo_ok(const ConvGeom& g) {
+  return g.R == 3 && g.S == 3 && g.st == 1 && g.pad == 1 && g.IC == 64 && g.Ncols == 64 && g.IW == 28 && g.OW == 28 &&
+         g.IH == g.OH && g.Kred == 576 && g.ldy == 64 && g.vec && g.X2 == nullptr &&
+         ((((uintptr_t)g.X) | ((uintptr_t)g.Wt)) & 15) == 0;
+}
+
+int cu_count() {
+  static const int n = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                hipSuccess || v <= 0)
+      return 256;
+    return v;
+  }();
+  return n;
+}
+
+template <bool DGRAD>
+int launch_conv_halo(ConvGeom& g, hipStream_t st) {
+  constexpr int WM = 4, WN = 2;  // 8 waves, 32 x 32 each: conv_pipe_kernel's layer1 forward tile (variant 2)
+  using GE = halo::Geo<28>;
+  const size_t lds = GE::LDS_ELEMS * sizeof(bf16_t);
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_halo_kernel<DGRAD, WM, WN, 28>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+    return (int)hipErrorInvalidConfiguration;
+  const int M = g.N * g.OH * g.OW, ntiles = (M + halo::BM - 1) / halo::BM;
+  const int grid = ntiles < cu_count() ? ntiles : cu_count();
+  hipLaunchKernelGGL((conv3x3_halo_kernel<DGRAD, WM, WN, 28>), dim3(grid), dim3(64 * WM * WN), lds, st, g);
+  return (int)hipGetLastError();
+}
+
 int wgrad_default_variant(int K) {
   (void)K;
   return 4;
@@ -1341,8 +1632,7 @@ MER_API int mer_conv_fwd(int N, int H, int W, int C, int K, int R, int S, int st
 
 MER_API int mer_conv_fwd_ex(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, const void* x,
                             const void* w_packed, void* y, float* stats, int variant, void* stream) {
-  if (C % 8 || variant < -1 || variant > 5) return (int)hipErrorInvalidValue;
-  if (variant == -1) variant = 2;
+  if (C % 8 || variant < -1 || variant > 6) return (int)hipErrorInvalidValue;
   ConvGeom g{};
   g.N = N; g.IH = H; g.IW = W; g.IC = C;
   g.OH = (H + 2 * pad - R) / stride + 1; g.OW = (W + 2 * pad - S) / stride + 1;
@@ -1350,6 +1640,10 @@ MER_API int mer_conv_fwd_ex(int N, int H, int W, int C, int K, int R, int S, int
   g.Ncols = K; g.Kred = R * S * C;
   g.X = (const bf16_t*)x; g.Wt = (const bf16_t*)w_packed; g.Y = (bf16_t*)y; g.ldy = K; g.stats = stats;
   g.vec = vec_epilogue_enabled() && conv_vec_ok(g);
+  // default: the halo kernel where it applies (layer1), else the 8-wave pipelined tiles; variant 6 = halo or fail
+  if ((variant == -1 || variant == 6) && halo_ok(g)) return launch_conv_halo<false>(g, (hipStream_t)stream);
+  if (variant == 6) return (int)hipErrorInvalidValue;
+  if (variant == -1) variant = 2;
   if (variant == 0) return launch_conv<false>(g, (hipStream_t)stream);
   return launch_conv_pipe<false, false>(g, (hipStream_t)stream, variant);
 }
@@ -1380,10 +1674,11 @@ MER_API int mer_conv_dgrad_ds(int N, int H, int W, int C, int K, int R, int S, i
                               const void* bn_mask, const void* bn_x, const float* bn_ms, float* bn_red,
                               const void* bn_x2, const float* bn_ms2, float* bn_red2, const void* ds_dy,
                               const void* ds_wt_packed, int ds_K, int variant, void* stream) {
-  if (K % 8 || C % 8 || variant < -1 || variant > 5) return (int)hipErrorInvalidValue;
+  if (K % 8 || C % 8 || variant < -1 || variant > 6) return (int)hipErrorInvalidValue;
+  const bool auto_variant = variant == -1;
   // 64-channel outputs (layer1, the layer2.0 input gradients): 32-wide K-tiles on a 4-deep ring with 4-wave tiles
   // (tools/bench_conv.py --fused: layer1 101 -> 65 us, layer2.0 s2 74 -> 51, downsample 48 -> 31); wider outputs
-  // keep the 64-wide 2-deep ring (the deep ring loses 10-50% there)
+  // keep the 64-wide 2-deep ring (the deep ring loses 10-50% there).  The layer1 shapes take the halo kernel (6).
   if (variant == -1) variant = C <= 64 ? 5 : 2;
   // the fused downsample: a 1x1 / stride-2 / pad-0 conv of the same input with ds_K output channels, beside a
   // 3x3 / stride-2 / pad-1 conv (its taps land in parity class (0, 0) only, at pixel (2i, 2j)); K-tile aligned.
@@ -1404,6 +1699,8 @@ MER_API int mer_conv_dgrad_ds(int N, int H, int W, int C, int K, int R, int S, i
   g.bnr_x2 = (const bf16_t*)bn_x2; g.bnr_ms2 = bn_ms2; g.bnr_red2 = bn_red2;
   g.X2 = (const bf16_t*)ds_dy; g.Wt2 = (const bf16_t*)ds_wt_packed; g.K2 = ds_dy ? ds_K : 0;
   g.vec = vec_epilogue_enabled() && conv_vec_ok(g);
+  if ((auto_variant || variant == 6) && halo_ok(g)) return launch_conv_halo<true>(g, (hipStream_t)stream);
+  if (variant == 6) return (int)hipErrorInvalidValue;
   if (variant == 0 || stride > 2) return launch_conv<true>(g, (hipStream_t)stream);
   if (stride == 2) return launch_conv_pipe<true, true>(g, (hipStream_t)stream, variant);
   return launch_conv_pipe<true, false>(g, (hipStream_t)stream, variant);

@@ -693,7 +693,7 @@ MER_API int mer_xh_audio_bwd(int M, const float* dqkv, const void* WcT_hi, const
 // Linears with one or two tiles, so each dY / X column block is read once per tile instead of once per 64-wide
 // tile of the other operand (the 64 x 64 version re-read dY 12x for audio_seq_proj: 97 MB per step).
 // ---------------------------------------------------------------------------------------------
-constexpr int WG_MAXP = 20;
+constexpr int WG_MAXP = 32;  // the head's Linears + LayerNorms + classifier + the emotion prior's 10 products
 constexpr int WG_HOST_COLS = 11;  // dY ldy X ldx x_dtype M N K splits dW db
 constexpr int WG_T = 128;         // output tile (n and k)
 

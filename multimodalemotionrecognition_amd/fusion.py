@@ -646,11 +646,20 @@ class FusionModel(nn.Module):
         if self.mode not in {"concat", "gated"}:
             raise ValueError(f"Unknown fusion mode: {self.mode}")
         hidden = self._take_prefetched(audio, "hidden")
+        # gated: ModalityDropout (fusion.py:430) replaces a projection by zeros_like -- the dropped branch and
+        # everything feeding only it get NO gradient (torch's Adam then skips them), see embedding_head
+        gated = self.mode == "gated"
+        drops = None
+        if hidden is not None:
+            # early prefetch: the next batch's encoder starts now and overlaps this whole step (as in xattn mode).
+            # This step's own host draws (modality dropout here, the head's seed in _issue_queued) come first, as
+            # in the inline schedule, whose encoder draws all happen after them
+            drops = self.modality_dropout.draw() if gated else (False, False)
+            hidden = self._issue_queued("hidden", hidden)
         a_emb = self.audio_model.encode(audio) if hidden is None else self.audio_model.encode(audio, hidden=hidden)
         v_emb = self.video_model.encode(video)
         if self.semantic_alignment is not None:  # fusion.py:417-418
             a_emb, v_emb, self.alignment_loss = self.semantic_alignment(a_emb, v_emb)
-        # gated: ModalityDropout (fusion.py:430) replaces a projection by zeros_like -- the dropped branch and
-        # everything feeding only it get NO gradient (torch's Adam then skips them), see embedding_head
-        drop_a, drop_v = self.modality_dropout.draw() if self.mode == "gated" else (False, False)
-        return EH.embedding_head(self, a_emb, v_emb, drop_a, drop_v)
+        if drops is None:
+            drops = self.modality_dropout.draw() if gated else (False, False)
+        return EH.embedding_head(self, a_emb, v_emb, *drops)

@@ -1006,6 +1006,38 @@ def xh_mlp_fwd(B, Ta, gated, part, emb, W0, b0, W3, b3, Wc, bc, mlp_p, rng, site
         h.data_ptr(), _ptr(g), _ptr(fused), logits.data_ptr(), stream_ptr())
 
 
+def xh_prior_fwd(B, T, Ta, v, a, W0, b0, W3, b3, heads, scale, drop_p, rng, site, pg, h1, prior, tt, tp, v2a_bias,
+                 a2v_bias):
+    """The emotion-prior adapter forward in one launch (csrc/prior.hip): ``heads`` = [(weight [1, d + PD], bias [1])]
+    of the v_query, a_key, a_query, v_key token-bias Linears; ``tt`` / ``tp`` = their 4 token / prior halves."""
+    d, H1, PD = v.shape[1], W0.shape[0], W3.shape[0]
+    if tuple(v.shape) != (B * T, d) or tuple(a.shape) != (B * Ta, d) or W0.shape[1] != 2 * d or W3.shape[1] != H1 \
+            or any(w.numel() != d + PD or bb.numel() != 1 for w, bb in heads) or len(tt) != 4 or len(tp) != 4 \
+            or tuple(v2a_bias.shape) != (B, T, Ta) or tuple(a2v_bias.shape) != (B, Ta, T):
+        raise ValueError("xh_prior_fwd shapes")
+    _f32c(v, a, W0, b0, W3, b3, pg, h1, prior, v2a_bias, a2v_bias, *tt, *tp, *[w for w, _ in heads])
+    hw = [x.data_ptr() for wb in heads for x in wb]
+    LIB("mer_xh_prior_fwd", B, T, Ta, d, H1, PD, v.data_ptr(), a.data_ptr(), W0.data_ptr(), b0.data_ptr(), W3.data_ptr(),
+        b3.data_ptr(), *hw, scale.data_ptr(), float(drop_p), rng_ptr(rng) if drop_p > 0 else 0, int(site),
+        pg.data_ptr(), h1.data_ptr(), prior.data_ptr(), *[t.data_ptr() for t in tt], *[t.data_ptr() for t in tp],
+        v2a_bias.data_ptr(), a2v_bias.data_ptr(), stream_ptr())
+
+
+def xh_prior_bwd(B, T, Ta, dbias_v2a, dbias_a2v, tt, tp, scale, head_w, W0, W3, h1, drop_p, rng, site, dtt, dtp,
+                 dprior, dh1, dscale_part, dv, da):
+    """Its backward (csrc/prior.hip): dtt / dtp / dprior / dh1 / dscale_part out, token gradients ADDED into dv, da."""
+    d, H1, PD = dv.shape[1], W0.shape[0], W3.shape[0]
+    if tuple(dbias_v2a.shape) != (B, T, Ta) or tuple(dbias_a2v.shape) != (B, Ta, T) or tuple(dv.shape) != (B * T, d) \
+            or tuple(da.shape) != (B * Ta, d) or dscale_part.numel() != B or len(head_w) != 4:
+        raise ValueError("xh_prior_bwd shapes")
+    _f32c(dbias_v2a, dbias_a2v, W0, W3, h1, dprior, dh1, dscale_part, dv, da, *tt, *tp, *dtt, *dtp, *head_w)
+    LIB("mer_xh_prior_bwd", B, T, Ta, d, H1, PD, dbias_v2a.data_ptr(), dbias_a2v.data_ptr(),
+        *[t.data_ptr() for t in tt], *[t.data_ptr() for t in tp], scale.data_ptr(), *[w.data_ptr() for w in head_w],
+        W0.data_ptr(), W3.data_ptr(), h1.data_ptr(), float(drop_p), rng_ptr(rng) if drop_p > 0 else 0, int(site),
+        *[t.data_ptr() for t in dtt], *[t.data_ptr() for t in dtp], dprior.data_ptr(), dh1.data_ptr(),
+        dscale_part.data_ptr(), dv.data_ptr(), da.data_ptr(), stream_ptr())
+
+
 # ---------------------------------------------------------------------------------------------------
 # fused xattn head backward (csrc/xattn_fused_bwd.hip); W*T arguments are transposed (hi, lo) planes
 def xh_mlp_bwd(B, gated, dlogits, emb, h, g, W0, W3, Wc, mlp_p, rng, site, dh, dz, demb):
@@ -1102,8 +1134,8 @@ class WGradTable:
 
     def _table(self):
         import numpy as np
-        if len(self.rows) > 20:
-            raise ValueError("mer_xh_wgrad takes at most 20 problems")
+        if len(self.rows) > 32:
+            raise ValueError("mer_xh_wgrad takes at most 32 problems")
         return np.ascontiguousarray(np.array(self.rows, dtype=np.int64))
 
     def ws_floats(self) -> int:

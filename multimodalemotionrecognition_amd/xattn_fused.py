@@ -4,7 +4,8 @@ launches of ``xattn_head.head_forward``.
 
 Scope of the fused path: d_model 128 with 4 heads (the reference's defaults, fusion.py:199-200), mean temporal
 pooling (the fusion default), concat or gated head, with or without the emotion-prior attention bias (the bias
-enters F2 / F3 / G2 / G3; the prior's own small Linears run beside them, fusion.py:153-184,390-394), audio features
+enters F2 / F3 / G2 / G3; the adapter itself -- pooled means, prior_net, the four token-bias Linears -- is ONE launch
+each way, csrc/prior.hip, its weight gradients problems of the grouped W launch; fusion.py:153-184,390-394), audio features
 that need no gradient (bf16 from the frozen WavLM, or fp32), T <= 16 frames and Ta <= 160 audio frames (3 s clips: 8
 and 149).  Everything else -- and INT8 inference -- runs the unfused schedule, which is the parity reference of this path.  The saved activations
 have the unfused schedule's names and layouts, so ``xattn_head.head_backward`` runs unchanged on them.
@@ -21,6 +22,8 @@ from . import kernels as K
 ENABLED = os.environ.get("MER_XATTN_FUSED", "1") != "0"
 BWD_ENABLED = os.environ.get("MER_XATTN_FUSED_BWD", "1") != "0"
 WGRAD_ROWS = 256  # rows of dY / X per weight-gradient workgroup (M is split over the grid)
+PRIOR = "emotion_prior_bias."
+PRIOR_HEADS = ("v_query_bias", "a_key_bias", "a_query_bias", "v_key_bias")  # mer_xh_prior_fwd's head order
 
 # (weight name, row slice) for each split plane; rows are contiguous slices of the reference's parameters
 _PLANES = {
@@ -179,10 +182,20 @@ def fused_forward(p, cfg, v_feat, a_seq, training, rng, ctx, sites):
                    p["v_in_proj.bias"], sp["Wq1"], p["v2a_attn.in_proj_bias"][:d], v, q1)
     sv = ctx.saved
     v2a_bias = a2v_bias = None
-    if cfg.use_prior:  # the emotion-prior attention biases from the pre-attention tokens (fusion.py:390-391)
-        from .xattn_head import linear_runner, prior_forward
-        sv.update(v=v, a=a)
-        v2a_bias, a2v_bias = prior_forward(p, v, a, B, T, Ta, dp_prior, seed, sv, linear_runner(p))
+    if cfg.use_prior:  # the emotion-prior attention biases from the pre-attention tokens (fusion.py:390-391): one launch
+        n = PRIOR
+        H1, PD = p[n + "prior_net.0.weight"].shape[0], p[n + "prior_net.3.weight"].shape[0]
+        pg, h1, prior = e(B, 2 * d), e(B, H1), e(B, PD)
+        tt = [e(B * L, 1) for L in (T, Ta, Ta, T)]
+        tp = [e(B, 1) for _ in PRIOR_HEADS]
+        v2a_bias, a2v_bias = e(B, T, Ta), e(B, Ta, T)
+        K.xh_prior_fwd(B, T, Ta, v, a, p[n + "prior_net.0.weight"], p[n + "prior_net.0.bias"],
+                       p[n + "prior_net.3.weight"], p[n + "prior_net.3.bias"],
+                       [(p[n + h + ".weight"], p[n + h + ".bias"]) for h in PRIOR_HEADS], p[n + "bias_scale"],
+                       dp_prior, seed, site_prior, pg, h1, prior, tt, tp, v2a_bias, a2v_bias)
+        sv.update(v=v, a=a, pg=pg, h1=h1, prior=prior)  # the unfused schedule's names (prior_backward reads them)
+        for h, t_, p_ in zip(PRIOR_HEADS, tt, tp):
+            sv["tt_" + h], sv["tp_" + h] = t_, p_
     P1 = e(B, H, T, Ta)
     s_v, mu_v, rs_v, v1, kv2 = e(B * T, d), e(B * T), e(B * T), e(B * T, d), e(B * T, 2 * d)
     emb = e(B, 2 * d)
@@ -244,7 +257,7 @@ def fused_backward(p, ctx, dlogits, grads, need_dv_feat=True):
     dev = dlogits.device
     f32 = torch.float32
     e = lambda *shape: torch.empty(shape, device=dev, dtype=f32)  # noqa: E731
-    from .xattn_head import SITE_A2V, SITE_APATH, SITE_MLP, SITE_V2A, SITE_VPATH
+    from .xattn_head import SITE_A2V, SITE_APATH, SITE_MLP, SITE_PRIOR, SITE_V2A, SITE_VPATH
     sp = getattr(ctx, "planes", None) or planes_for(p)
     if sp.t_gen != getattr(ctx, "planes_gen", None):  # the forward did not split them (eval-mode forward)
         sp.refresh_transposed()
@@ -282,9 +295,23 @@ def fused_backward(p, ctx, dlogits, grads, need_dv_feat=True):
     K.xh_v2a_bwd(B, T, Ta, dkv2_part, sp["WkvT2"], demb, sv["s_v"], sv["mu_v"], sv["rs_v"], p["v_norm.weight"],
                  sp["WoT1"], sv["P1"], sv["kv1"], sv["q1"], dp_attn, dp_path, rng, SITE_V2A, SITE_VPATH, scale, dkv2,
                  dv2, dq1, dv, dqkv, lnp_v, dbias=dbias_v2a)
-    if prior:  # the prior's weight gradients; its token gradients join da / dv before G1 reads them
-        from .xattn_head import prior_backward
-        prior_backward(p, sv, dbias_v2a, dbias_a2v, dv, da, grads, B, T, Ta, ctx.drops[3], rng)
+    prior_w = ()
+    if prior:  # one launch: the prior's data gradients; its token gradients join da / dv before G1 reads them
+        n = PRIOR
+        dtt = [e(B * L, 1) for L in (T, Ta, Ta, T)]
+        dtp = [e(B, 1) for _ in PRIOR_HEADS]
+        dprior, dh1, dsc = e(B, sv["prior"].shape[1]), e(B, sv["h1"].shape[1]), e(B, 1)
+        K.xh_prior_bwd(B, T, Ta, dbias_v2a, dbias_a2v, [sv["tt_" + h] for h in PRIOR_HEADS],
+                       [sv["tp_" + h] for h in PRIOR_HEADS], p[n + "bias_scale"], [p[n + h + ".weight"] for h in PRIOR_HEADS],
+                       p[n + "prior_net.0.weight"], p[n + "prior_net.3.weight"], sv["h1"], ctx.drops[3], rng, SITE_PRIOR,
+                       dtt, dtp, dprior, dh1, dsc, dv, da)
+        # its weight gradients: problems of the grouped launch below (token-bias weights split [token | prior] columns)
+        prior_w = [(dh1, sv["pg"], grads[n + "prior_net.0.weight"], grads[n + "prior_net.0.bias"]),
+                   (dprior, sv["h1"], grads[n + "prior_net.3.weight"], grads[n + "prior_net.3.bias"]),
+                   (dsc, None, None, grads[n + "bias_scale"])]
+        for h, dt, dq, toks in zip(PRIOR_HEADS, dtt, dtp, (sv["v"], sv["a"], sv["a"], sv["v"])):
+            gw = grads[n + h + ".weight"]
+            prior_w += [(dt, toks, gw[:, :d], None), (dq, sv["prior"], gw[:, d:], grads[n + h + ".bias"])]
     da_s = e(B * Ta, d)
     K.xh_audio_bwd(dqkv, sp["WcT"], sp["WaT"], da, da_s, dq1, sp["WqT1"], sp["WvT"], dv, dvfeat)
     gw1, gb1 = grads["v2a_attn.in_proj_weight"], grads["v2a_attn.in_proj_bias"]
@@ -303,7 +330,7 @@ def fused_backward(p, ctx, dlogits, grads, need_dv_feat=True):
                           (lnp_a[:, :d], None, None, grads["a_norm.weight"]),
                           (lnp_a[:, d:], None, None, grads["a_norm.bias"]),
                           (lnp_v[:, :d], None, None, grads["v_norm.weight"]),
-                          (lnp_v[:, d:], None, None, grads["v_norm.bias"])) + head_w:
+                          (lnp_v[:, d:], None, None, grads["v_norm.bias"])) + head_w + tuple(prior_w):
         W.add(dY, X, dW, db, _splits(dY.shape[0]))
     ws = e(W.ws_floats())
     W.run(ws)

@@ -3,15 +3,15 @@ xattn head, CE, Adam) at B=32 x 8 frames x 48,000 samples on the HIP path vs the
 (train.py:200-228).  B=32 exercises the 256-frame conv tile picks and the M-dependent
 GEMM variants the bench runs.
 
-Bars (bf16 encoders, fp32 head):
-* logits max|d| < 5e-2 and |dloss| < 1e-2 against the full fp32 oracle step;
-* BatchNorm running statistics (every BN of the trunk) within 2e-2 relative;
-* the xattn head teacher-forced on the HIP encoders' own features: logits within 1e-4 and every head
+Bars (bf16 encoders, fp32 head; the values asserted below, with the round-3 measurements beside them):
+* logits max|d| < 3e-2 (measured 1.1e-2) and |dloss| < 3e-3 (5e-4) against the full fp32 oracle step;
+* BatchNorm running statistics (every BN of the trunk) within 5e-3 relative (1.5e-3);
+* the xattn head teacher-forced on the HIP encoders' own features: logits within 3e-5 (7.4e-6) and every head
   gradient within 1e-3 relative (max|d| / max|ref|) of the fp32 oracle head -- the head is fp32 end to end;
 * the first Adam update (~ -lr * sign(g)) against the FULL oracle step: per-parameter sign agreement >= 0.9
   for head parameters (they see the bf16 encoders' features; their own fp32 math is pinned teacher-forced
-  above) and >= 0.70 for every trunk parameter (bf16 trunk gradients; near-zero gradient elements flip),
-  >= 0.85 averaged over the trunk;
+  above) and >= 0.75 for every trunk parameter (measured min 0.81; bf16 trunk gradients, near-zero gradient
+  elements flip), >= 0.85 averaged over the trunk;
 * trunk gradient cosine >= 0.85 per parameter (the round-1 trunk bar: an fp32 forward flips ~1% of the
   near-zero ReLU decisions of a bf16 one, which alone moves masked gradients) and >= 0.93
   averaged over the trunk's parameters (measured 0.946, worst 0.891: layer1 BatchNorm biases).

@@ -245,6 +245,65 @@ def test_conv_variants_bit_identical(N, H, C, Kc, R, stride, pad):
     assert all(torch.equal(dxs[0], d) for d in dxs[1:])
 
 
+@pytest.mark.parametrize("N", [3, 40, 256])
+def test_halo_conv_bit_identical(N):
+    """The layer1 halo kernel (variant 6: resident weights, per-tile input halo in LDS, persistent workgroups) against
+    the pipelined implicit GEMM it replaces (fwd variant 2, dgrad variant 5): same fragments and K order -> identical
+    outputs; with the forward's wave layout and epilogue, identical BN-statistics rows; the BN-backward sums (residual
+    under a ReLU mask, two BNs) agree to fp32 rounding.  N = 3: a partial last tile; 40: fewer tiles than CUs; 256 (the B=32 step): ~6 tiles per
+    workgroup, the double-buffered halo in use.  The default (-1) takes variant 6 on this shape."""
+    from multimodalemotionrecognition_amd import kernels as K
+
+    torch.manual_seed(9)
+    H, C = 28, 64
+    x = torch.randn(N, H, H, C, device="cuda").bfloat16()
+    w = torch.randn(C, C, 3, 3, device="cuda") / 24.0
+    wp = torch.empty(C, 9 * C, device="cuda", dtype=torch.bfloat16)
+    K.pack_conv_weight(w, wp, C, False)
+    wt = torch.empty(C, 9 * C, device="cuda", dtype=torch.bfloat16)
+    K.pack_conv_weight(w, wt, C, True)
+    outs = {}
+    for v in (2, 6, -1):
+        y = torch.full((N, H, H, C), float("nan"), device="cuda", dtype=torch.bfloat16)
+        st = K.bn_stats_buffer(C, "cuda", N * H * H)
+        K.conv_fwd(x, wp, y, st, 3, 3, 1, 1, variant=v)
+        outs[v] = (y, st)
+    # the pipelined kernel takes 128-row tiles (the halo kernel's) from 384 tiles up; below, 64-row tiles group the
+    # partial rows differently, so only their sums can be compared
+    same_tiles = (N * H * H + 127) // 128 >= 384
+    for v in (6, -1):
+        assert torch.equal(outs[2][0], outs[v][0]), v
+        if same_tiles:
+            assert torch.equal(outs[2][1], outs[v][1]), v
+        else:
+            assert torch.allclose(outs[2][1].sum(0), outs[v][1].sum(0), rtol=1e-5, atol=1e-2), v
+    dy = torch.randn(N, H, H, C, device="cuda").bfloat16()
+    res = torch.randn(N, H, H, C, device="cuda").bfloat16()
+    mask = torch.randn(N, H, H, C, device="cuda").bfloat16()
+    xb = torch.randn(N, H, H, C, device="cuda").bfloat16()
+    xb2 = torch.randn(N, H, H, C, device="cuda").bfloat16()
+    ms = torch.stack([torch.randn(C), torch.rand(C) + 0.5], 1).cuda().contiguous()
+    ms2 = torch.stack([torch.randn(C), torch.rand(C) + 0.5], 1).cuda().contiguous()
+    rows = K.bn_red_rows(N * H * H)
+    douts = {}
+    for v in (5, 6, -1):
+        dx = torch.full((N, H, H, C), float("nan"), device="cuda", dtype=torch.bfloat16)
+        red = torch.zeros(rows, C, 2, device="cuda")
+        red2 = torch.zeros(rows, C, 2, device="cuda")
+        K.conv_dgrad(dy, wt, dx, 3, 3, 1, 1, residual=res, mask=mask, variant=v,
+                     bnr=(mask, xb, ms, red, xb2, ms2, red2))
+        douts[v] = (dx, red, red2)
+    # dgrad: the halo kernel runs the forward's 8-wave layout (variant 5 has 4 waves), so the BN-backward partial rows
+    # group their sums differently: dx bit-identical, the folded sums to fp32 rounding
+    for v in (6, -1):
+        assert torch.equal(douts[5][0], douts[v][0]), v
+        for a, b in zip(douts[5][1:], douts[v][1:]):
+            assert torch.allclose(a.sum(0), b.sum(0), rtol=1e-5, atol=1e-2), v
+    assert torch.equal(douts[6][1], douts[-1][1]) and torch.equal(douts[6][2], douts[-1][2])
+    ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.bfloat16().float(), padding=1).permute(0, 2, 3, 1)
+    assert rel_rms(outs[6][0], ref) < 1e-2
+
+
 @pytest.mark.parametrize("stride,ds", [(1, False), (2, True)])
 def test_dgrad_fused_bn_reduce_matches_standalone(stride, ds):
     """mer_conv_dgrad_bnr's epilogue reduction == mer_bn_bwd_reduce over the stored gradient (both BNs)."""

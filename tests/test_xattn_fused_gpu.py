@@ -61,8 +61,9 @@ def test_fused_forward_matches_unfused(head, training, prior):
         assert _rel(s1[k], s0[k]) < 3e-5, k
     for n in g0:
         # the prior's token-bias Linears: their bias gradient is ONE sum over every token's dS (positive and negative
-        # terms cancel), so the ~1e-5 forward-level differences reach it amplified (measured 1.2e-4)
-        bar = 5e-4 if n.startswith("emotion_prior_bias.") else 1e-4
+        # terms cancel), so the ~1e-5 forward-level differences reach it amplified (measured 1.2e-4); likewise any
+        # single-scalar gradient (the gate's output bias: one sum over the batch, 1.4e-4 with the fused prior)
+        bar = 5e-4 if (n.startswith("emotion_prior_bias.") or g0[n].numel() == 1) else 1e-4
         assert _rel(g1[n], g0[n]) < bar, (n, _rel(g1[n], g0[n]))
     assert _rel(dv1, dv0) < 1e-4
 

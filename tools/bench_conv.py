@@ -19,7 +19,8 @@ VARIANTS = [int(v) for v in next((a.split("=")[1] for a in sys.argv if a.startsw
 WGRAD_V = [int(v) for v in next((a.split("=")[1] for a in sys.argv if a.startswith("--wgrad-variants=")), "1,2").split(",")
            if v]
 WGRAD = "--no-wgrad" not in sys.argv
-FUSED = "--fused" in sys.argv  # dgrad as in the train step: residual under a ReLU mask + the fused BN-backward sums
+FUSED = "--fused" in sys.argv
+ONLY = next((a.split("=")[1] for a in sys.argv if a.startswith("--layers=")), None)  # substring filter, e.g. layer1  # dgrad as in the train step: residual under a ReLU mask + the fused BN-backward sums
 
 
 def timeit(fn, reps=20):
@@ -38,6 +39,8 @@ def timeit(fn, reps=20):
 def main():
     torch.manual_seed(0)
     for name, H, C, Kc, R, st, pad in LAYERS:
+        if ONLY is not None and ONLY not in name:
+            continue
         Ho = (H + 2 * pad - R) // st + 1
         x = (torch.rand(NF, H, H, C, device="cuda") * 2 - 1).bfloat16()
         w = torch.randn(Kc, C, R, R, device="cuda") * 0.05

@@ -1,22 +1,24 @@
 #!/bin/bash
-# One build -> measure iteration on the GPU box: focused tests, then the default bench line (no CPU baseline).
-#   bash tools/gpu_iter.sh TAG "tests/a.py tests/b.py" [extra bench args]
+# Iteration session: selected GPU tests (TESTS), optional tool commands (TOOLS, ';'-separated), the bench line.
+#   TESTS="tests/test_resnet_gpu.py -k halo" TOOLS="python tools/bench_conv.py --layers=layer1" bash tools/gpu_iter.sh TAG
 TAG=${1:-iter}
-FILES=$2
-shift 2
-OUT=$PWD/gpurun_out/$TAG
+R=$PWD
+OUT=$R/gpurun_out/$TAG
 mkdir -p $OUT
-if [ -n "$FILES" ]; then
-  timeout -k 10 600 python -u -m pytest $FILES -m gpu -q -x --timeout 200 --timeout-method thread > $OUT/focus.log 2>&1
-  rc=$?
-  tail -5 $OUT/focus.log
-  if [ $rc -ne 0 ]; then echo "FOCUS_EXIT $rc"; exit $rc; fi
-fi
-timeout -k 10 300 python -u bench.py --no-cpu-baseline "$@" > $OUT/bench.log 2>&1
-rc=$?
-grep '^{' $OUT/bench.log | python -c "
-import json,sys
-for l in sys.stdin:
-    d=json.loads(l); h=d.get('roofline_head') or {}
-    print('BENCH', d['value'], d['ms_per_step'], d.get('ms_per_step_median'), 'head', {k: h.get(k) for k in ('frac','fwd_ms','bwd_ms','ms_per_step')}, 'core', (h.get('core') or {}).get('kernel_ms'), (h.get('core') or {}).get('frac'))"
-exit $rc
+run() {
+  local name=$1 to=$2; shift 2
+  timeout -k 10 $to "$@" > $OUT/$name.log 2>&1
+  local rc=$?
+  echo "== $name rc=$rc"; grep -v amdgpu.ids $OUT/$name.log | tail -${TAILN:-6} | cut -c1-400
+  if [ $rc -ne 0 ]; then echo "STOP after $name"; exit $rc; fi
+  return 0
+}
+if [ -n "$TESTS" ]; then run pytest 600 python -u -m pytest $TESTS -x -q --timeout 200 --timeout-method thread; fi
+i=0
+IFS=';' read -ra CMDS <<< "$TOOLS"
+for c in "${CMDS[@]}"; do
+  [ -z "$c" ] && continue
+  i=$((i+1)); TAILN=30 run tool$i 300 bash -c "$c"
+done
+if [ "${BENCH:-1}" = 1 ]; then run bench 400 python -u bench.py --no-cpu-baseline; fi
+echo SESSION_DONE
