@@ -27,6 +27,10 @@ static __device__ long long mer_ct_buf[512 * 64];
   do { \
     if (threadIdx.x == 0 && blockIdx.x < 512 && (k) < 64) mer_ct_buf[blockIdx.x * 64 + (k)] = wall_clock64(); \
   } while (0)
+MER_API int mer_ct_reset() {
+  static long long zeros[512 * 64];
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(mer_ct_buf), zeros, sizeof(zeros), 0, hipMemcpyHostToDevice);
+}
 MER_API int mer_ct_read(long long* host) {
   return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(mer_ct_buf), sizeof(long long) * 512 * 64, 0, hipMemcpyDeviceToHost);
 }
@@ -874,7 +878,7 @@ struct EpiGeo {
 };
 
 // The dgrad epilogue's global operands (residual, residual mask, BN mask, BN input(s), BN (mean, rstd) of its 8
-// columns), loaded AHEAD of the epilogue -- conv3x3_halo_kernel issues them before its K loop, so their latency hides
+// columns), loaded AHEAD of the epilogue -- conv_halo_kernel issues them before its K loop, so their latency hides
 // under the MFMAs instead of stalling the epilogue's passes one after another.  Same addresses as the in-epilogue
 // loads (rows past M clamped to row M - 1; those passes discard them).
 template <int NP>
@@ -921,7 +925,7 @@ __device__ __forceinline__ void conv_epilogue_prefetch(const ConvGeom& g, EpiPre
 template <bool DGRAD, int FM, int FN, int WM, int WN, int WAVE_FLOATS, class OutRow, class Pre = EpiNone>
 __device__ __forceinline__ void conv_epilogue_vec(const ConvGeom& g, f32x4 (&acc)[FM][FN], float* smemf, int w,
                                                   int lane, int m0, int n0, int M, long red_row_id, long stat_row,
-                                                  OutRow out_row, const Pre* pre = nullptr) {
+                                                  OutRow out_row, const Pre* pre = nullptr, int ct_slot = -1) {
   constexpr bool PREF = !std::is_same<Pre, EpiNone>::value;
   using E = EpiGeo<FM, FN, WAVE_FLOATS>;
   constexpr int TM = FM * 16, TN = FN * 16;
@@ -938,6 +942,19 @@ __device__ __forceinline__ void conv_epilogue_vec(const ConvGeom& g, f32x4 (&acc
   const bool has_x2 = do_bnr && g.bnr_x2 != nullptr;
   float mu[8], rs[8], mu2[8], rs2[8];
   float sA[8], sB[8], sC[8];
+  // the 16-byte output stores are issued LAST, after the cross-wave reductions: a wave stalled issuing stores would
+  // otherwise hold every other wave at the reductions' barriers (the store queue drains ~16 B/clk per CU)
+  constexpr int NPS = E::NP;
+  u32x4 pend[NPS];
+  long pend_at[NPS];
+  bool pend_ok[NPS];
+#pragma unroll
+  for (int q = 0; q < NPS; ++q) pend_ok[q] = false;
+  auto flush = [&]() {
+#pragma unroll
+    for (int q = 0; q < NPS; ++q)
+      if (pend_ok[q]) *reinterpret_cast<u32x4*>(g.Y + pend_at[q]) = pend[q];
+  };
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     if constexpr (PREF) {
@@ -1000,7 +1017,9 @@ __device__ __forceinline__ void conv_epilogue_vec(const ConvGeom& g, f32x4 (&acc
           oh[e] = f2bf(v[e]);
           v[e] = bf2f(oh[e]);  // the stored value feeds the reductions
         }
-        *reinterpret_cast<u32x4*>(g.Y + e0) = ov;
+        pend[q] = ov;
+        pend_at[q] = e0;
+        pend_ok[q] = true;
         if (do_bnr) {
           u32x4 mv, xv, x2v;
           if constexpr (PREF) {
@@ -1029,6 +1048,7 @@ __device__ __forceinline__ void conv_epilogue_vec(const ConvGeom& g, f32x4 (&acc
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
+  if (ct_slot >= 0) CT(ct_slot);
   if (do_bnr) {
   // lanes sharing this lane's 8 columns: lane % LPR equal -> xor over the row bits of the lane index
 #pragma unroll
@@ -1051,7 +1071,10 @@ __device__ __forceinline__ void conv_epilogue_vec(const ConvGeom& g, f32x4 (&acc
       o[2] = sC[e];
     }
   lds_barrier();
-  if (wr != 0 || lane >= LPR || !cok) return;
+  if (wr != 0 || lane >= LPR || !cok) {
+    flush();
+    return;
+  }
 #pragma unroll
   for (int e = 0; e < 8; ++e)
 #pragma unroll
@@ -1070,9 +1093,15 @@ __device__ __forceinline__ void conv_epilogue_vec(const ConvGeom& g, f32x4 (&acc
         *reinterpret_cast<f32x4*>(g.bnr_red2 + slab + 2 * e) = f32x4{sA[e], sC[e], sA[e + 1], sC[e + 1]};
     }
   }
+  if (ct_slot >= 0) CT(ct_slot + 1);
+  flush();
+  if (ct_slot >= 0) CT(ct_slot + 2);
   return;
   }  // do_bnr
-  if (!g.stats) return;
+  if (!g.stats) {
+    flush();
+    return;
+  }
   // forward BN statistics from the accumulator layout (column = lane & 15: two shuffles per value, cheaper than
   // the 8-column lane reduction) over the stored, bf16-rounded values
 #pragma unroll
@@ -1082,6 +1111,9 @@ __device__ __forceinline__ void conv_epilogue_vec(const ConvGeom& g, f32x4 (&acc
 #pragma unroll
       for (int r = 0; r < 4; ++r) acc[i][j][r] = bf2f(f2bf(acc[i][j][r]));
   conv_tile_stats<FM, FN, WM, WN>(g, acc, smemf, w, lane, m0, n0, M, stat_row);
+  if (ct_slot >= 0) CT(ct_slot + 1);
+  flush();
+  if (ct_slot >= 0) CT(ct_slot + 2);
 }
 
 // STAGES-deep LDS ring (cdna_hip_programming.md "Pipelining across barriers"): tiles kt+1 .. kt+STAGES-2 stay
@@ -1439,74 +1471,89 @@ int launch_conv(ConvGeom& g, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
-// MER_WGRAD_VARIANT overrides the default weight-gradient variant (A/B switch for tools/bench_conv.py)
-// (tools/bench_conv.py, ResNet18 layers at 256 frames: the global_load_lds ring, variant 4, is 1.1-1.25x the
-// register-staged kernel on the stem, layer1, layer3 and layer4 and within 4% elsewhere; its 3-stage form, at one
-// block per CU, is slower)
 // ---------------------------------------------------------------------------------------
-// Stride-1 3x3 convolutions with 64 input and 64 output channels on 28-wide maps (ResNet18 layer1 at 112^2 frames,
-// forward and input gradient).  conv_pipe_kernel re-fetches every input pixel from L2 once per tap (9x) and waits one
-// DMA round trip per 64-deep K-step with ~8 MFMAs per wave behind it: latency-bound, layer1 ran at 200-380 TF/s.
-// Here one persistent workgroup per CU keeps the whole packed weight [64][9*64] resident in LDS (73.7 KB) and stages,
-// per 128-pixel output tile, the HALO its 9 taps read -- (rows + 2) x (W + 2) pixels x 64 channels, zero border
-// columns -- double-buffered, so tile i+1's halo streams in while tile i computes.  The K loop is LDS -> MFMA only:
-// no global load, no barrier.  The A fragment of tap (dr, ds) for output pixel (y, x) is halo pixel (y + dr, x + 1 +
-// ds), the same 16 bytes conv_pipe_kernel gathers; K-steps run in the same (tap, channel) order on the same MFMA with
-// the same wave layout and the same epilogue (conv_epilogue_vec), so outputs, BN statistics and BN-backward sums are
-// bit-identical to conv_pipe_kernel's (tests/test_resnet_gpu.py).  Both LDS images are XOR-swizzled per 16-byte chunk
-// (chunk c of pixel / weight row r at c ^ ((r >> 1) & 7)), which spreads a fragment's 16 rows over all 16 bank slots.
+// Stride-1 convolutions of 64 output channels with the whole weight resident in LDS: ResNet18 layer1 (3x3, pad 1,
+// 64 -> 64 channels on 28x28 maps at 112^2 frames; forward and input gradient) and the stem in its space-to-depth form
+// (4x4, pad 0, 16 -> 64 channels: 59x59 -> 56x56).  conv_pipe_kernel re-fetches every input pixel from L2 once per
+// tap and waits one DMA round trip per 64-deep K-step with ~8 MFMAs per wave behind it: latency-bound, layer1 ran at
+// 200-380 TF/s and the stem at ~195.  Here persistent workgroups keep the packed weight [64][R*S*C] resident in LDS
+// (layer1 73.7 KB, stem 32 KB) and stage, per 128-pixel output tile, the HALO its taps read -- the input rows the
+// tile's output rows need, (W + R - 1) pixels wide with zero border columns -- double-buffered, so tile i+1's halo
+// streams in while tile i computes.  The K loop is LDS -> MFMA only: no global load, no barrier.  The A fragment of
+// tap (r, s) for output pixel (n, y, x) is halo pixel (n*IH + y + r - pad - base, x + s), the same 16 bytes
+// conv_pipe_kernel gathers; K-steps run in the same (tap, channel) order on the same MFMA with the same wave layout
+// and epilogue (conv_epilogue_vec), so outputs and BN statistics are bit-identical to conv_pipe_kernel's
+// (tests/test_resnet_gpu.py).  Both LDS images are XOR-swizzled per 16-byte chunk so a fragment's 16 rows fall on 16
+// distinct bank slots.
 // ---------------------------------------------------------------------------------------
 namespace halo {
-constexpr int BM = 128, C = 64, KRED = 9 * C, WCH = KRED / 8;  // tile rows, channels, reduction, 16-B chunks per weight row
-template <int W>
+constexpr int BM = 128;  // output pixels per tile
+// C input channels, R x R taps, pad, W output width, IHX = IH - OH (input rows beyond the output rows: the stem's 3),
+// ROWS halo rows: the image rows 128 consecutive output pixels span + R - 1, + IHX when a tile may straddle frames
+template <int C_, int R_, int PAD_, int W_, int IHX_>
 struct Geo {
-  static constexpr int HW = W + 2;                       // halo row width (pixels)
-  static constexpr int ROWS = (W + BM - 2) / W + 1 + 2;  // image rows 128 consecutive pixels span, + 2 halo rows
-  static constexpr int CH = (ROWS * HW * 8 + 63) / 64 * 64;  // 16-byte chunks per halo buffer (whole glds pieces)
-  static constexpr int ELEMS = CH * 8;                   // bf16 elements per halo buffer
-  static constexpr int LDS_ELEMS = 64 * KRED + 2 * ELEMS + 64;  // weights, two halo buffers, one zero pixel
+  static constexpr int C = C_, R = R_, PAD = PAD_, W = W_, IHX = IHX_;
+  static constexpr int KRED = R * R * C, WCH = KRED / 8;    // reduction, 16-byte chunks per weight row
+  static constexpr int CPP = C / 8;                         // chunks per halo pixel
+  static constexpr int HW = W + R - 1;                      // halo row width (pixels)
+  static constexpr int ROWS = (W + BM - 2) / W + 1 + (R - 1) + IHX;
+  static constexpr int CH = (ROWS * HW * CPP + 63) / 64 * 64;  // 16-byte chunks per halo buffer (whole glds pieces)
+  static constexpr int ELEMS = CH * 8;                         // bf16 elements per halo buffer
+  static constexpr int LDS_ELEMS = 64 * KRED + 2 * ELEMS + C;  // weights, two halo buffers, one zero pixel
+  static constexpr int KSTEPS = KRED / 32;
+  static constexpr int HSHIFT = CPP == 8 ? 1 : 3;  // halo swizzle: chunk c of pixel p at c ^ ((p >> HSHIFT) & (CPP-1))
+  static_assert(CPP == 8 || CPP == 2, "halo layouts for 16 or 64 channels");
+  static_assert(WCH % 16 == 0 || WCH % 16 == 8, "weight-row swizzle");
 };
+// physical chunk of logical weight chunk c in row n (16 consecutive rows at one c cover all 16 bank slots)
+template <int WCH>
+__device__ __forceinline__ int wchunk(int n, int c) {
+  return WCH % 16 == 0 ? ((c & ~15) | ((c & 15) ^ (n & 15))) : ((c & ~7) | ((c & 7) ^ ((n >> 1) & 7)));
+}
 }  // namespace halo
 
-template <bool DGRAD, int WM, int WN, int W_>
-__global__ __launch_bounds__(64 * WM * WN, 1) void conv3x3_halo_kernel(ConvGeom g) {
-  using GE = halo::Geo<W_>;
+template <bool DGRAD, class GE, int WM, int WN, int OCC>
+__global__ __launch_bounds__(64 * WM * WN, OCC) void conv_halo_kernel(ConvGeom g) {
   constexpr int WAVES = WM * WN;
   constexpr int TM = halo::BM / WM, TN = 64 / WN, FM = TM / 16, FN = TN / 16;
-  constexpr int HW = GE::HW;
+  constexpr int HW = GE::HW, CPP = GE::CPP, C = GE::C, R = GE::R, PAD = GE::PAD, W_ = GE::W;
   extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
   bf16_t* const wlds = smem;
-  bf16_t* const hbuf = smem + 64 * halo::KRED;
+  bf16_t* const hbuf = smem + 64 * GE::KRED;
   bf16_t* const zpix = hbuf + 2 * GE::ELEMS;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int wr = w / WN, wc = w % WN, fr = lane & 15, fq = lane >> 4;
-  const int H = g.OH, M = g.N * g.OH * W_, rows_total = g.N * g.OH;
+  const int OH = g.OH, IH = g.IH, IW = g.IW, M = g.N * g.OH * W_, in_rows = g.N * g.IH;
   const int ntiles = (M + halo::BM - 1) / halo::BM;
   const bf16_t* zero = reinterpret_cast<const bf16_t*>(mer_conv_zero16);
   int tile = blockIdx.x;
   CT(0);
-
-  // halo of `tl`: image rows gr0 .. gr0 + ROWS - 1 (global row = frame * H + y; gr0 = the tile's first row - 1),
-  // columns -1 .. W; chunk L of the buffer holds pixel L / 8, logical channel chunk (L % 8) ^ ((pixel >> 1) & 7)
+  // global input row of output row (frame n, row y) at tap row 0: n * IH + y - pad
+  auto in_row0 = [&](int m) {
+    const int go = m / W_, n = go / OH;
+    return n * IH + (go - n * OH) - PAD;
+  };
+  // halo of tile `tl`: global input rows base .. base + ROWS - 1 (base = in_row0 of the tile's first pixel), input
+  // columns -pad .. W + R - 2 - pad; chunk L of the buffer holds halo pixel L / CPP, logical channel chunk
+  // (L % CPP) ^ ((pixel >> HSHIFT) & (CPP - 1))
   auto stage_halo = [&](bf16_t* hb, int tl) {
-    const int gr0 = (tl * halo::BM) / W_ - 1;
+    const int base = in_row0(tl * halo::BM);
     for (int j = w; j < GE::CH / 64; j += WAVES) {
       const int L = j * 64 + lane;
-      const int hp = L >> 3, c = (L & 7) ^ ((hp >> 1) & 7);
-      const int hr = hp / HW, x = hp - hr * HW - 1, gr = gr0 + hr;
-      const bool ok = hr < GE::ROWS && gr >= 0 && gr < rows_total && x >= 0 && x < W_;
-      glds16(ok ? g.X + ((long)gr * W_ + x) * halo::C + c * 8 : zero, hb + j * 512);
+      const int hp = L / CPP, c = (L % CPP) ^ ((hp >> GE::HSHIFT) & (CPP - 1));
+      const int hr = hp / HW, x = hp - hr * HW - PAD, gr = base + hr;
+      const bool ok = hr < GE::ROWS && gr >= 0 && gr < in_rows && x >= 0 && x < IW;
+      glds16(ok ? g.X + ((long)gr * IW + x) * C + c * 8 : zero, hb + j * 512);
     }
   };
-  // resident weights: row n (output column) x 72 chunks, chunk c of row n at (c & ~7) | ((c & 7) ^ ((n >> 1) & 7))
-  for (int j = w; j < halo::WCH; j += WAVES) {  // 64 rows x 72 chunks = 72 glds pieces of 64 chunks
+  // resident weights: row n (output column) x WCH chunks, swizzled by halo::wchunk
+  for (int j = w; j < GE::WCH; j += WAVES) {  // 64 rows x WCH chunks = WCH glds pieces of 64 chunks
     const int L = j * 64 + lane;
-    const int n = L / halo::WCH, pc = L - n * halo::WCH;
-    const int c = (pc & ~7) | ((pc & 7) ^ ((n >> 1) & 7));
-    glds16(g.Wt + (long)n * halo::KRED + c * 8, wlds + j * 512);
+    const int n = L / GE::WCH, pc = L - n * GE::WCH;
+    glds16(g.Wt + (long)n * GE::KRED + halo::wchunk<GE::WCH>(n, pc) * 8, wlds + j * 512);  // (an involution)
   }
   stage_halo(hbuf, tile);
-  if (t < 8) *reinterpret_cast<u32x4*>(zpix + t * 8) = u32x4{0u, 0u, 0u, 0u};
+  if (t < CPP) *reinterpret_cast<u32x4*>(zpix + t * 8) = u32x4{0u, 0u, 0u, 0u};
   wait_vmcnt<0>();
   __syncthreads();
   CT(1);
@@ -1517,78 +1564,91 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv3x3_halo_kernel(ConvGeom 
   for (int cur = 0, it = 0; tile < ntiles; tile += gridDim.x, cur ^= 1, ++it) {
     bf16_t* const hb = hbuf + cur * GE::ELEMS;
     if (tile + (int)gridDim.x < ntiles) stage_halo(hbuf + (cur ^ 1) * GE::ELEMS, tile + gridDim.x);
-    CT(2 + 5 * it);
-    const int m0 = tile * halo::BM, gr0 = m0 / W_ - 1;
+    CT(it < 11 ? 2 + 5 * it : 63);
+    const int m0 = tile * halo::BM, base = in_row0(m0);
     const auto out_row = [](int row) { return (long)row; };
     constexpr int EWF = GE::ELEMS / 2 / WAVES;  // epilogue staging floats per wave (this tile's halo buffer)
     EpiPre<EpiGeo<FM, FN, EWF>::NP> pre;
     if constexpr (DGRAD) conv_epilogue_prefetch<DGRAD, FM, FN, WM, WN, EWF>(g, pre, w, lane, m0, 0, M, out_row);
-    int hpb[FM], yv[FM];  // per fragment row of this lane: halo pixel of the centre tap, image row y
+    int hpb[FM], yv[FM];  // per fragment row of this lane: halo pixel of tap (0, 0), input row of tap row 0
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
       int m = m0 + wr * TM + i * 16 + fr;
       m = m < M ? m : M - 1;  // rows past M compute garbage that the epilogue discards
-      const int gr = m / W_, x = m - gr * W_;
-      yv[i] = gr - (gr / H) * H;
-      hpb[i] = (gr - gr0) * HW + x + 1;
+      const int go = m / W_, x = m - go * W_, n = go / OH, y = go - n * OH;
+      yv[i] = y - PAD;
+      hpb[i] = (n * IH + y - PAD - base) * HW + x;
     }
     f32x4 acc[FM][FN];
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    // 18 k-steps of 32 = (tap, channel half), tap-major: the fragments of step u + 1 are read while step u's MFMAs
-    // run (two register sets, static indices: the loop is fully unrolled)
+    // k-steps of 32 in the packed (tap, channel) order: the fragments of step u + 1 are read while step u's MFMAs run
+    // (two register sets, static indices: the loop is fully unrolled)
     bf16x8 af[2][FM], bfr[2][FN];
     auto frags = [&](int u, bf16x8 (&a)[FM], bf16x8 (&b)[FN]) {
-      const int tap = u >> 1, sub = u & 1;
-      const int r = tap / 3, s = tap - 3 * (tap / 3);
-      const int dr = DGRAD ? 1 - r : r - 1, ds = DGRAD ? 1 - s : s - 1;  // source pixel offset of this tap
-      const int c = sub * 4 + fq;  // logical 16-byte chunk (8 channels) of this lane's k slice
+      const int kk = u * 32 + fq * 8;       // this lane's 8 reduction indices start here
+      const int tap = kk / C, c = (kk % C) / 8;
+      const int r = tap / R, s = tap - R * (tap / R);
+      // dgrad: tap (r, s) of the packed transposed weight reads dy at (h + pad - r, w + pad - s): the halo row / col
+      // of output (y, x) then sits at offset (R - 1 - r, R - 1 - s) from (y - pad, x - pad) when pad = (R - 1) / 2
+      const int hr = DGRAD ? R - 1 - r : r, hs = DGRAD ? R - 1 - s : s;
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
-        const int hp = hpb[i] + dr * HW + ds;
-        const bool ok = (unsigned)(yv[i] + dr) < (unsigned)H;  // rows outside the frame read the zero pixel
-        a[i] = *reinterpret_cast<const bf16x8*>(ok ? hb + hp * 64 + ((c ^ ((hp >> 1) & 7)) << 3) : zpix);
+        const int hp = hpb[i] + hr * HW + hs;
+        const bool ok = (unsigned)(yv[i] + hr) < (unsigned)IH;  // rows outside the frame read the zero pixel
+        a[i] = *reinterpret_cast<const bf16x8*>(
+            ok ? hb + hp * C + ((c ^ ((hp >> GE::HSHIFT) & (CPP - 1))) << 3) : zpix);
       }
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
-        const int n = wc * TN + j * 16 + fr, cb = tap * 8 + c;
-        b[j] = *reinterpret_cast<const bf16x8*>(wlds + n * halo::KRED + (((cb & ~7) | ((cb & 7) ^ ((n >> 1) & 7))) << 3));
+        const int n = wc * TN + j * 16 + fr, cb = u * 4 + fq;
+        b[j] = *reinterpret_cast<const bf16x8*>(wlds + n * GE::KRED + (halo::wchunk<GE::WCH>(n, cb) << 3));
       }
     };
     frags(0, af[0], bfr[0]);
 #pragma unroll
-    for (int u = 0; u < 18; ++u) {
-      if (u + 1 < 18) frags(u + 1, af[(u + 1) & 1], bfr[(u + 1) & 1]);
+    for (int u = 0; u < GE::KSTEPS; ++u) {
+      if (u + 1 < GE::KSTEPS) frags(u + 1, af[(u + 1) & 1], bfr[(u + 1) & 1]);
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[u & 1][i], bfr[u & 1][j], acc[i][j], 0, 0, 0);
     }
-    CT(3 + 5 * it);
+    CT(it < 11 ? 3 + 5 * it : 63);
     wait_vmcnt<0>();  // this wave's share of the next halo (and the previous epilogue's stores) has landed
     lds_barrier();    // every wave's: the next halo is complete and no wave still reads hb
-    CT(4 + 5 * it);
+    CT(it < 11 ? 4 + 5 * it : 63);
+    const int ct_slot = it == 1 ? 60 : -1;  // (timing build: stamps inside the second tile's epilogue)
     if constexpr (DGRAD)
       conv_epilogue_vec<DGRAD, FM, FN, WM, WN, EWF>(g, acc, reinterpret_cast<float*>(hb), w, lane, m0, 0, M, (long)tile,
-                                                    (long)tile, out_row, &pre);
+                                                    (long)tile, out_row, &pre, ct_slot);
     else
       conv_epilogue_vec<DGRAD, FM, FN, WM, WN, EWF>(g, acc, reinterpret_cast<float*>(hb), w, lane, m0, 0, M, (long)tile,
-                                                    (long)tile, out_row);
-    CT(5 + 5 * it);
+                                                    (long)tile, out_row, static_cast<const EpiNone*>(nullptr), ct_slot);
+    CT(it < 11 ? 5 + 5 * it : 63);
     lds_barrier();    // every wave is past its epilogue's use of hb before the DMA two tiles on refills it
-    CT(6 + 5 * it);
+    CT(it < 11 ? 6 + 5 * it : 63);
   }
 }
 
-// conv3x3_halo_kernel applies: 3x3 / stride 1 / pad 1, 64 -> 64 channels, 28-wide maps, 16-byte epilogue, no fused
-// downsample segment
-bool halo_ok(const ConvGeom& g) {
-  return g.R == 3 && g.S == 3 && g.st == 1 && g.pad == 1 && g.IC == 64 && g.Ncols == 64 && g.IW == 28 && g.OW == 28 &&
-         g.IH == g.OH && g.Kred == 576 && g.ldy == 64 && g.vec && g.X2 == nullptr &&
-         ((((uintptr_t)g.X) | ((uintptr_t)g.Wt)) & 15) == 0;
+using HaloL1 = halo::Geo<64, 3, 1, 28, 0>;    // layer1: 3x3 / pad 1, 64 -> 64, 28x28
+using HaloStem = halo::Geo<16, 4, 0, 56, 3>;  // the stem's space-to-depth form: 4x4 / pad 0, 16 -> 64, 59x59 -> 56x56
+
+// which halo kernel applies (0: none): 3x3 / stride 1 / pad 1, 64 -> 64 channels on 28-wide maps (fwd and dgrad), or
+// 4x4 / stride 1 / pad 0, 16 -> 64 channels, 59 -> 56 (fwd); 64 output columns, 16-byte epilogue, no fused downsample
+int halo_kind(const ConvGeom& g, bool dgrad) {
+  if (g.st != 1 || g.Ncols != 64 || g.ldy != 64 || !g.vec || g.X2 != nullptr ||
+      ((((uintptr_t)g.X) | ((uintptr_t)g.Wt)) & 15) != 0)
+    return 0;
+  if (g.R == 3 && g.S == 3 && g.pad == 1 && g.IC == 64 && g.IW == 28 && g.OW == 28 && g.IH == g.OH && g.Kred == 576)
+    return 1;
+  if (!dgrad && g.R == 4 && g.S == 4 && g.pad == 0 && g.IC == 16 && g.IW == 59 && g.OW == 56 && g.IH == 59 &&
+      g.OH == 56 && g.Kred == 256)
+    return 2;
+  return 0;
 }
 
 int cu_count() {
@@ -1602,18 +1662,26 @@ int cu_count() {
   return n;
 }
 
-template <bool DGRAD>
-int launch_conv_halo(ConvGeom& g, hipStream_t st) {
-  constexpr int WM = 4, WN = 2;  // 8 waves, 32 x 32 each: conv_pipe_kernel's layer1 forward tile (variant 2)
-  using GE = halo::Geo<28>;
+template <bool DGRAD, class GE, int OCC>
+int launch_halo_t(ConvGeom& g, hipStream_t st) {
+  constexpr int WM = 4, WN = 2;  // 8 waves, 32 x 32 each: conv_pipe_kernel's 128 x 64 tile (variant 2)
   const size_t lds = GE::LDS_ELEMS * sizeof(bf16_t);
-  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_halo_kernel<DGRAD, WM, WN, 28>),
+  static_assert(GE::LDS_ELEMS * 2 * OCC <= 160 * 1024, "LDS per CU");
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_halo_kernel<DGRAD, GE, WM, WN, OCC>),
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return (int)hipErrorInvalidConfiguration;
   const int M = g.N * g.OH * g.OW, ntiles = (M + halo::BM - 1) / halo::BM;
-  const int grid = ntiles < cu_count() ? ntiles : cu_count();
-  hipLaunchKernelGGL((conv3x3_halo_kernel<DGRAD, WM, WN, 28>), dim3(grid), dim3(64 * WM * WN), lds, st, g);
+  const int slots = OCC * cu_count();
+  hipLaunchKernelGGL((conv_halo_kernel<DGRAD, GE, WM, WN, OCC>), dim3(ntiles < slots ? ntiles : slots),
+                     dim3(64 * WM * WN), lds, st, g);
   return (int)hipGetLastError();
+}
+
+template <bool DGRAD>
+int launch_conv_halo(ConvGeom& g, hipStream_t st, int kind) {
+  if (kind == 1) return launch_halo_t<DGRAD, HaloL1, 1>(g, st);
+  if constexpr (!DGRAD) return launch_halo_t<false, HaloStem, 2>(g, st);  // 71 KB of LDS: two workgroups per CU
+  return (int)hipErrorInvalidValue;
 }
 
 int wgrad_default_variant(int K) {
@@ -1641,7 +1709,10 @@ MER_API int mer_conv_fwd_ex(int N, int H, int W, int C, int K, int R, int S, int
   g.X = (const bf16_t*)x; g.Wt = (const bf16_t*)w_packed; g.Y = (bf16_t*)y; g.ldy = K; g.stats = stats;
   g.vec = vec_epilogue_enabled() && conv_vec_ok(g);
   // default: the halo kernel where it applies (layer1), else the 8-wave pipelined tiles; variant 6 = halo or fail
-  if ((variant == -1 || variant == 6) && halo_ok(g)) return launch_conv_halo<false>(g, (hipStream_t)stream);
+  if (variant == -1 || variant == 6) {
+    const int hk = halo_kind(g, false);
+    if (hk) return launch_conv_halo<false>(g, (hipStream_t)stream, hk);
+  }
   if (variant == 6) return (int)hipErrorInvalidValue;
   if (variant == -1) variant = 2;
   if (variant == 0) return launch_conv<false>(g, (hipStream_t)stream);
@@ -1699,7 +1770,10 @@ MER_API int mer_conv_dgrad_ds(int N, int H, int W, int C, int K, int R, int S, i
   g.bnr_x2 = (const bf16_t*)bn_x2; g.bnr_ms2 = bn_ms2; g.bnr_red2 = bn_red2;
   g.X2 = (const bf16_t*)ds_dy; g.Wt2 = (const bf16_t*)ds_wt_packed; g.K2 = ds_dy ? ds_K : 0;
   g.vec = vec_epilogue_enabled() && conv_vec_ok(g);
-  if ((auto_variant || variant == 6) && halo_ok(g)) return launch_conv_halo<true>(g, (hipStream_t)stream);
+  if (auto_variant || variant == 6) {
+    const int hk = halo_kind(g, true);
+    if (hk) return launch_conv_halo<true>(g, (hipStream_t)stream, hk);
+  }
   if (variant == 6) return (int)hipErrorInvalidValue;
   if (variant == 0 || stride > 2) return launch_conv<true>(g, (hipStream_t)stream);
   if (stride == 2) return launch_conv_pipe<true, true>(g, (hipStream_t)stream, variant);

@@ -304,6 +304,35 @@ def test_halo_conv_bit_identical(N):
     assert rel_rms(outs[6][0], ref) < 1e-2
 
 
+@pytest.mark.parametrize("N", [3, 64])
+def test_halo_stem_bit_identical(N):
+    """The stem's space-to-depth form (4x4 / stride 1 / pad 0, 16 -> 64 channels, 59x59 -> 56x56) on the halo kernel
+    (variant 6, two persistent workgroups per CU) against the pipelined implicit GEMM (variant 2): identical outputs
+    and identical BN-statistics rows (same 128 x 64 tiles, wave layout and epilogue); the default (-1) takes it."""
+    from multimodalemotionrecognition_amd import kernels as K
+
+    torch.manual_seed(10)
+    x = torch.randn(N, 59, 59, 16, device="cuda").bfloat16()
+    w = torch.randn(64, 16, 4, 4, device="cuda") / 16.0
+    wp = torch.empty(64, 256, device="cuda", dtype=torch.bfloat16)
+    K.pack_conv_weight(w, wp, 16, False)
+    outs = {}
+    for v in (2, 6, -1):
+        y = torch.full((N, 56, 56, 64), float("nan"), device="cuda", dtype=torch.bfloat16)
+        st = K.bn_stats_buffer(64, "cuda", N * 56 * 56)
+        K.conv_fwd(x, wp, y, st, 4, 4, 1, 0, variant=v)
+        outs[v] = (y, st)
+    same_tiles = (N * 56 * 56 + 127) // 128 >= 384
+    for v in (6, -1):
+        assert torch.equal(outs[2][0], outs[v][0]), v
+        if same_tiles:
+            assert torch.equal(outs[2][1], outs[v][1]), v
+        else:
+            assert torch.allclose(outs[2][1].sum(0), outs[v][1].sum(0), rtol=1e-5, atol=1e-2), v
+    ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.bfloat16().float()).permute(0, 2, 3, 1)
+    assert rel_rms(outs[6][0], ref) < 1e-2
+
+
 @pytest.mark.parametrize("stride,ds", [(1, False), (2, True)])
 def test_dgrad_fused_bn_reduce_matches_standalone(stride, ds):
     """mer_conv_dgrad_bnr's epilogue reduction == mer_bn_bwd_reduce over the stored gradient (both BNs)."""

@@ -3,12 +3,37 @@ layer, GEMM shape (M x N x K), us per launch, TF/s -- one steady-state step, lau
 fixed launch order (video.py: forward stem + per block conv1, conv2, [downsample]; backward per block in
 reverse: wgrad conv2, dgrad conv2, wgrad conv1, [wgrad ds], dgrad conv1 (with the downsample's dgrad fused in,
 video.FUSED_DS_DGRAD; MER_TRUNK_UNFUSED_DS=1 for traces of the two-launch form); stem wgrad last).
-    python tools/trunk_table.py <run_kernel_trace.csv> [train_steps_in_trace] > profiles/<round>/trunk_table.txt"""
+    python tools/trunk_table.py <run_kernel_trace.csv> [train_steps_in_trace] > profiles/<round>/trunk_table.txt
+Each launch also gets its roofline: attainable = min(dense bf16 MFMA peak, FLOPs / algorithmic bytes x 8 TB/s) with
+the algorithmic bytes = the bf16 A source read once + the bf16 weights + the bf16 output (wgrad: both activations +
+the fp32 weight gradient), and frac = achieved / attainable.  tools/trunk_serial.py makes a serialized
+(single-stream, trunk-only) trace for this table."""
 import csv
 import os
 import sys
 
 NIMG, H = 256, 112  # B=32 clips x 8 frames, 112x112
+PEAK_TF, HBM_TBS = 2500.0, 8.0  # MI355X dense bf16 MFMA, HBM3E (MI355X_MICROARCH.md)
+
+
+def conv_bytes(kind, c):
+    """Algorithmic HBM bytes of one launch: (name, M, N, K) with K = taps * Cin; bf16 activations."""
+    _, M, N, Kr = c
+    name = c[0]
+    taps = 49 if name.startswith("stem") else (1 if "downsample" in name else 9)
+    cin = Kr // taps
+    stride = 2 if ("downsample" in name or name.startswith("stem") or ".0.conv1" in name and not name.startswith(
+        "layer1")) else 1
+    m_in = M * stride * stride  # input pixels (the stem: 3 channels of 112^2 per output 56^2)
+    if kind == "wgrad":
+        return 2 * m_in * cin + 2 * M * N + 4 * N * Kr
+    return 2 * m_in * cin + 2 * N * Kr + 2 * M * N
+
+
+def roof(flop, byt, us):
+    ach = flop / us / 1e6
+    att = min(PEAK_TF, flop / byt * HBM_TBS)
+    return ach, att, ach / att
 
 
 def trunk_convs():
@@ -59,12 +84,14 @@ def main():
     a, b = ends[-3], ends[-2]  # one steady-state step
     win = rows[a + 1:b + 1]
     convs = trunk_convs()
-    fwd = [r for r in win if "conv_pipe_kernel<false" in r["Kernel_Name"].replace(" ", "")]
+    fwd = [r for r in win if "conv_pipe_kernel<false" in r["Kernel_Name"].replace(" ", "")
+           or "conv_halo_kernel<false" in r["Kernel_Name"].replace(" ", "")]
     bwd = [r for r in win if "conv_pipe_kernel<true" in r["Kernel_Name"].replace(" ", "")
+           or "conv_halo_kernel<true" in r["Kernel_Name"].replace(" ", "")
            or "(anonymousnamespace)::wgrad_kernel<" in r["Kernel_Name"].replace(" ", "")
            or "(anonymousnamespace)::wgrad_pipe_kernel<" in r["Kernel_Name"].replace(" ", "")]
     dur = lambda r: (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3  # noqa: E731
-    print(f"{'layer':26s} {'pass':6s} {'M x N x K':>22s} {'us':>8s} {'TF/s':>7s}  kernel")
+    print(f"{'layer':26s} {'pass':6s} {'M x N x K':>22s} {'us':>8s} {'TF/s':>7s} {'attain':>7s} {'frac':>6s}  kernel")
     tot = {"fwd": 0.0, "dgrad": 0.0, "wgrad": 0.0}
     flops = {"fwd": 0.0, "dgrad": 0.0, "wgrad": 0.0}
     for c, r in zip(convs, fwd):
@@ -72,13 +99,17 @@ def main():
         f = 2.0 * c[1] * c[2] * c[3]
         tot["fwd"] += us
         flops["fwd"] += f
-        print(f"{c[0]:26s} {'fwd':6s} {c[1]:>9d}x{c[2]:>4d}x{c[3]:>5d} {us:8.1f} {f / us / 1e6:7.1f}  {r['Kernel_Name'][:60]}")
+        _, att, fr = roof(f, conv_bytes("fwd", c), us)
+        print(f"{c[0]:26s} {'fwd':6s} {c[1]:>9d}x{c[2]:>4d}x{c[3]:>5d} {us:8.1f} {f / us / 1e6:7.1f} {att:7.0f} {fr:6.3f}  "
+              f"{r['Kernel_Name'][:60]}")
     for (kind, c, extra), r in zip(backward_order(convs), bwd):
         us = dur(r)
         f = 2.0 * c[1] * c[2] * c[3] + extra
         tot[kind] += us
         flops[kind] += f
-        print(f"{c[0]:26s} {kind:6s} {c[1]:>9d}x{c[2]:>4d}x{c[3]:>5d} {us:8.1f} {f / us / 1e6:7.1f}  {r['Kernel_Name'][:60]}")
+        _, att, fr = roof(f, conv_bytes(kind, c), us)
+        print(f"{c[0]:26s} {kind:6s} {c[1]:>9d}x{c[2]:>4d}x{c[3]:>5d} {us:8.1f} {f / us / 1e6:7.1f} {att:7.0f} {fr:6.3f}  "
+              f"{r['Kernel_Name'][:60]}")
     if len(fwd) != len(convs) or len(bwd) != len(backward_order(convs)):
         print(f"# WARNING: matched {len(fwd)} fwd / {len(bwd)} bwd launches, expected {len(convs)} / "
               f"{len(backward_order(convs))}")
