@@ -540,6 +540,15 @@ int mer_concat_prior_rows(int B, int L, int d, int pd, int ldo, const float* tok
  * trans 1 transposed (dst[c * dst_ld + r], the [in][out] planes the fused backward's data-gradient products read). */
 int mer_xh_split(int n_items, const long long* desc, void* stream);
 
+/* F1 from a precomputed first product: pair [M][ldp] fp32 holds aseq Ws_hi^T in columns 0..127 and aseq Ws_lo^T in
+ * 128..255 (one mer_gemm_bf16 of the bf16 WavLM features with the stacked [hi; lo] planes of audio_seq_proj);
+ * a_s = pair[:, :128] + pair[:, 128:] + bs, then a, q2, kv1 and the video rows exactly as mer_xh_audio_fwd. */
+int mer_xh_audio_fwd_pair(int M, const float* pair, long ldp, const float* bs, const void* Wa_hi, const void* Wa_lo,
+                          const float* ba, const void* Wc_hi, const void* Wc_lo, const float* bq2, const float* bkv1,
+                          float* a_s, float* a, float* q2, float* kv1, int Mv, int vdim, const float* vfeat,
+                          const void* Wv_hi, const void* Wv_lo, const float* bv, const void* Wq1_hi, const void* Wq1_lo,
+                          const float* bq1, float* v, float* q1, void* stream);
+
 /* F1: a_s = aseq Ws^T + bs (aseq [M][S] bf16 -- the WavLM features, exact -- or fp32), a = a_s Wa^T + ba,
  * [q2 | kv1] = a Wc^T + [bq2 | bkv1] (Wc = [a2v in_proj q rows; v2a in_proj k, v rows], 384 x 128).  Outputs
  * fp32: a_s, a, q2 [M][128], kv1 [M][256].  S % 32 == 0.  The same launch projects the Mv video rows:

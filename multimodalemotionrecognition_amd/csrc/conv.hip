@@ -1962,15 +1962,25 @@ __global__ void pack_input_s2d_kernel(int N, int H, int W, const float* __restri
 }
 MER_API int mer_pack_input_s2d(int N, int C, int H, int W, const float* x, void* y, void* stream) {
   if (C < 1 || C > 4 || (H & 1) || (W & 1) || ((uintptr_t)x & 7)) return (int)hipErrorInvalidValue;
-  const long total = (long)N * (H / 2 + 3) * (W / 2 + 3);
-  if (total >= (1L << 22)) return (int)hipErrorInvalidValue;  // fdiv range
-  const int grid = (int)((total + 255) / 256 < 16384 ? (total + 255) / 256 : 16384);
+  const long per_frame = (long)(H / 2 + 3) * (W / 2 + 3);
+  if (N < 0 || per_frame >= (1L << 22)) return (int)hipErrorInvalidValue;
+  // the kernel's fdiv index math holds below 2^22 pixels per launch: larger batches go in frame chunks
+  const int chunk = (int)(((1L << 22) - 1) / per_frame);
   const hipStream_t st = (hipStream_t)stream;
-  if (C == 3) hipLaunchKernelGGL(pack_input_s2d_kernel<3>, dim3(grid), dim3(256), 0, st, N, H, W, x, (bf16_t*)y);
-  else if (C == 1) hipLaunchKernelGGL(pack_input_s2d_kernel<1>, dim3(grid), dim3(256), 0, st, N, H, W, x, (bf16_t*)y);
-  else if (C == 2) hipLaunchKernelGGL(pack_input_s2d_kernel<2>, dim3(grid), dim3(256), 0, st, N, H, W, x, (bf16_t*)y);
-  else hipLaunchKernelGGL(pack_input_s2d_kernel<4>, dim3(grid), dim3(256), 0, st, N, H, W, x, (bf16_t*)y);
-  MER_LAUNCH_CHECK();
+  for (int n0 = 0; n0 < N; n0 += chunk) {
+    const int nc = N - n0 < chunk ? N - n0 : chunk;
+    const long total = (long)nc * per_frame;
+    const int grid = (int)((total + 255) / 256 < 16384 ? (total + 255) / 256 : 16384);
+    const float* xc = x + (long)n0 * C * H * W;
+    bf16_t* yc = (bf16_t*)y + n0 * per_frame * 16;
+    if (C == 3) hipLaunchKernelGGL(pack_input_s2d_kernel<3>, dim3(grid), dim3(256), 0, st, nc, H, W, xc, yc);
+    else if (C == 1) hipLaunchKernelGGL(pack_input_s2d_kernel<1>, dim3(grid), dim3(256), 0, st, nc, H, W, xc, yc);
+    else if (C == 2) hipLaunchKernelGGL(pack_input_s2d_kernel<2>, dim3(grid), dim3(256), 0, st, nc, H, W, xc, yc);
+    else hipLaunchKernelGGL(pack_input_s2d_kernel<4>, dim3(grid), dim3(256), 0, st, nc, H, W, xc, yc);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return (int)e;
+  }
+  return 0;
 }
 
 // PyTorch conv weight [K][C][R][S] fp32 -> fwd [K][R][S][Cp] (transpose=0) or dgrad [Cp][R][S][Kp] (transpose=1)

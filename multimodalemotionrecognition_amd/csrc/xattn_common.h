@@ -99,6 +99,16 @@ __device__ __forceinline__ void wave_sync_lds() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
+// workgroup barrier for LDS traffic only: LDS stores / loads before it have retired, global loads and stores
+// stay in flight (__syncthreads' release fence waits for every outstanding global access as well).  The empty
+// asm statements keep the compiler from moving memory accesses across it.
+__device__ __forceinline__ void lds_sync() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  lds_barrier();
+  asm volatile("" ::: "memory");
+}
+
 struct XhDrop {  // dropout / drop-path of the head (train mode), sites as xattn_head.py
   float attn, path;
   const unsigned long long* seed;

@@ -60,14 +60,18 @@ MER_API int mer_xh_split(int n_items, const long long* desc, void* stream) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// F1: audio token chain, 32 rows per block, 8 waves; the trailing ceil(B*T/32) blocks run the video rows'
-// input and query projections (v, q1), which depend on nothing the audio chain makes.  The 768-deep first
-// product is split over the wave halves (waves 4..7 take the upper half of K and hand their partial sums over
-// LDS); the two short products use all 8 waves on 16 / 48 columns each (35 -> 31.7 us at B = 32: the first
-// product itself is bound by L2 traffic -- every block re-reads the whole 393 KB split weight with half-used
-// 128-byte lines -- not by the k-step chain; a fully register-pipelined version of it measured slower).
+// F1: audio token chain, 32 rows per block, 8 waves; the trailing ceil(B*T/16) blocks run the video rows'
+// input and query projections (v, q1), which depend on nothing the audio chain makes.
+// These blocks are latency chains (one block per CU, three dependent products): every weight fragment a wave
+// needs for the short products is loaded into registers at block entry (WRegs), so its L2 latency overlaps
+// the first phase instead of recurring at each k step of each product (phase stamps, B = 32: the video
+// blocks' 512-deep product 25.3 us with a 3-deep k-step pipeline from L2; the a / [q2 | k1 v1] products
+// 3.0 / 9.2 us).  The video rows' fp32 features are staged once into LDS (zero past vdim).
 // ---------------------------------------------------------------------------------------------
 constexpr int F1_WAVES = 8;
+constexpr int F1_VROWS = 16;     // video rows per block
+constexpr int F1_VK = 512;       // video feature depth bound (ResNet18: 512)
+constexpr int F1_VLD = F1_VK + 4;  // LDS row stride of the staged video features
 
 struct XhVideo {
   int M, vdim;
@@ -80,7 +84,52 @@ struct XhVideo {
   float* q1;
 };
 
-template <typename TA>  // bf16: the WavLM features (exact, two passes); float: fp32 features (split, three passes)
+// pre-split weight fragments of NS 32-wide k steps x TJ 16-column tiles, held in registers
+template <int NS, int TJ>
+struct WRegs {
+  u4 h[NS][TJ], l[NS][TJ];
+};
+
+// steps >= nvalid load step nvalid - 1 (a valid address; the A operand is zero there)
+template <int NS, int TJ>
+__device__ __forceinline__ void wregs_load(WRegs<NS, TJ>& r, SplitW W, long ldw, int c0, int nvalid) {
+  const int lane = threadIdx.x & 63, fr = lane & 15, fk = (lane >> 4) * 8;
+#pragma unroll
+  for (int s = 0; s < NS; ++s)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const long off = (long)(c0 + 16 * j + fr) * ldw + 32 * (s < nvalid ? s : nvalid - 1) + fk;
+      r.h[s][j] = *reinterpret_cast<const u4*>(W.hi + off);
+      r.l[s][j] = *reinterpret_cast<const u4*>(W.lo + off);
+    }
+}
+
+// acc[i][j] += A[rows 16i..][0 : 32 NS] . W^T: A fp32 rows in LDS (split on the fly), W from registers; the same
+// per-step order as mm_aw (hi.hi, hi.lo, lo.hi per k step)
+template <int TI, int TJ, int NS>
+__device__ __forceinline__ void mm_lw(f32x4 (&acc)[TI][TJ], const float* A, int lda, const WRegs<NS, TJ>& w) {
+  const int lane = threadIdx.x & 63, fr = lane & 15, fk = (lane >> 4) * 8;
+#pragma unroll
+  for (int s = 0; s < NS; ++s)
+#pragma unroll
+    for (int i = 0; i < TI; ++i) {
+      bf16x8 ah, al;
+      frag_row(A + (16 * i + fr) * lda + 32 * s + fk, true, ah, al);
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {
+        Frag H, L;
+        H.u = w.h[s][j];
+        L.u = w.l[s][j];
+        acc[i][j] = mma3(ah, al, H.v, L.v, acc[i][j]);
+      }
+    }
+}
+
+// TA bf16: the WavLM features (exact, two passes); float: fp32 features (split, three passes).  PAIR: the first
+// product was computed beforehand as ONE bf16 GEMM of the WavLM features with the stacked [hi; lo] planes of
+// audio_seq_proj (mer_gemm_bf16: 256 output columns, a well-pipelined 768-deep product) and aseq is that fp32
+// [M][256] pair; a_s = pair[:, :128] + pair[:, 128:] + bs.
+template <typename TA, bool PAIR = false>
 __global__ __launch_bounds__(64 * F1_WAVES) void xh_audio_fwd_kernel(int M, int S, const TA* __restrict__ aseq,
                                                                      long ldas, SplitW Ws, const float* __restrict__ bs,
                                                                      SplitW Wa, const float* __restrict__ ba, SplitW Wc,
@@ -89,32 +138,83 @@ __global__ __launch_bounds__(64 * F1_WAVES) void xh_audio_fwd_kernel(int M, int 
                                                                      float* __restrict__ a_s, float* __restrict__ a,
                                                                      float* __restrict__ q2, float* __restrict__ kv1,
                                                                      XhVideo vid) {
-  __shared__ __attribute__((aligned(16))) float asL[32 * LDA];
-  __shared__ __attribute__((aligned(16))) float aL[32 * LDA];
+  __shared__ __attribute__((aligned(16))) float smem[64 * LDA];  // asL | aL; the video blocks: [16][F1_VLD]
+  float* asL = smem;
+  float* aL = smem + 32 * LDA;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, fr = lane & 15, fk = (lane >> 4) * 8;
   const int na = (M + 31) / 32;
   if ((int)blockIdx.x >= na) {  // video rows: v = v_feat Wv^T + bv, q1 = v Wq1^T + bq1 (16 columns per wave)
-    const long v0 = (long)(blockIdx.x - na) * 32;
-    const int vmax = (int)(vid.M - v0 < 32 ? vid.M - v0 : 32);
-    {
-      f32x4 acc[2][1];
-      zero(acc);
-      mm_aw(acc, vid.vfeat + v0 * vid.vdim, vid.vdim, vmax, vid.vdim, vid.Wv, vid.vdim, 16 * w);
-      store_acc(acc, 16 * w, vid.bv, asL, LDA, vid.v, XD, v0, vmax);
+    XT(2, 8);
+    const long v0 = (long)(blockIdx.x - na) * F1_VROWS;
+    const int vmax = (int)(vid.M - v0 < F1_VROWS ? vid.M - v0 : F1_VROWS), vd = vid.vdim;
+    f32x4 x[F1_VROWS * F1_VK / 4 / (64 * F1_WAVES)];
+#pragma unroll
+    for (int q = 0; q < F1_VROWS * F1_VK / 4 / (64 * F1_WAVES); ++q) {  // the rows first (clamped addresses)
+      const int e = threadIdx.x + 64 * F1_WAVES * q, r = e / (F1_VK / 4), k = 4 * (e % (F1_VK / 4));
+      x[q] = *reinterpret_cast<const f32x4*>(vid.vfeat + (v0 + (r < vmax ? r : vmax - 1)) * vd + (k < vd ? k : vd - 4));
     }
-    __syncthreads();
-    f32x4 acc[2][1];
+    WRegs<F1_VK / 32, 1> wv;  // then every weight fragment: their latency overlaps the staging
+    wregs_load(wv, vid.Wv, vd, 16 * w, vd / 32);
+    WRegs<XD / 32, 1> wq;
+    wregs_load(wq, vid.Wq1, XD, 16 * w, XD / 32);
+#pragma unroll
+    for (int q = 0; q < F1_VROWS * F1_VK / 4 / (64 * F1_WAVES); ++q) {  // zero past vmax / vdim
+      const int e = threadIdx.x + 64 * F1_WAVES * q, r = e / (F1_VK / 4), k = 4 * (e % (F1_VK / 4));
+      *reinterpret_cast<f32x4*>(smem + r * F1_VLD + k) = (r < vmax && k < vd) ? x[q] : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    lds_sync();  // LDS only: the weight loads stay in flight
+    f32x4 acc[1][1];
+    {  // two accumulator chains (even / odd k steps) so consecutive MFMAs do not wait on each other
+      f32x4 c2[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+      for (int s = 0; s < F1_VK / 32; ++s) {
+        bf16x8 ah, al;
+        frag_row(smem + fr * F1_VLD + 32 * s + fk, true, ah, al);
+        Frag H, L;
+        H.u = wv.h[s][0];
+        L.u = wv.l[s][0];
+        c2[s & 1] = mma3(ah, al, H.v, L.v, c2[s & 1]);
+      }
+      acc[0][0] = c2[0] + c2[1];
+    }
+    lds_sync();  // the staged features are dead: v goes to LDS rows 0..15
+    store_acc(acc, 16 * w, vid.bv, smem, LDA, vid.v, XD, v0, vmax);
+    lds_sync();
+    XT(2, 9);
     zero(acc);
-    mm_aw<2, 1, 3, XD>(acc, asL, LDA, 32, XD, vid.Wq1, XD, 16 * w);
+    mm_lw<1, 1, XD / 32>(acc, smem, LDA, wq);
     store_acc(acc, 16 * w, vid.bq1, nullptr, 0, vid.q1, XD, v0, vmax);
+    XT(2, 10);
     return;
   }
   XT(2, 0);
   const long r0 = (long)blockIdx.x * 32;
   const int rmax = (int)(M - r0 < 32 ? M - r0 : 32);
+  WRegs<XD / 32, 1> wa;
+  WRegs<XD / 32, 3> wc;
   // a_s = a_seq Ws^T + bs  (bf16 A is exact: two passes; fp32 A: split, three passes); wave (w & 3) owns 32
   // columns, wave half (w >> 2) one half of K
-  {
+  if constexpr (PAIR) {
+    const float* pr = reinterpret_cast<const float*>(aseq);
+    f32x4 x0[2], x1[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {  // 32 rows x 32 float4 per half, two per thread
+      const int e = threadIdx.x + 64 * F1_WAVES * q, r = e >> 5, c = 4 * (e & 31);
+      const long rc = r0 + (r < rmax ? r : rmax - 1);
+      x0[q] = *reinterpret_cast<const f32x4*>(pr + rc * ldas + c);
+      x1[q] = *reinterpret_cast<const f32x4*>(pr + rc * ldas + XD + c);
+    }
+    wregs_load(wa, Wa, XD, 16 * w, XD / 32);  // issued after the pair loads: their latency overlaps the sum
+    wregs_load(wc, Wc, XD, 48 * w, XD / 32);
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int e = threadIdx.x + 64 * F1_WAVES * q, r = e >> 5, c = 4 * (e & 31);
+      const f32x4 v = (x0[q] + x1[q]) + *reinterpret_cast<const f32x4*>(bs + c);
+      *reinterpret_cast<f32x4*>(asL + r * LDA + c) = r < rmax ? v : f32x4{0.f, 0.f, 0.f, 0.f};
+      if (r < rmax) *reinterpret_cast<f32x4*>(a_s + (r0 + r) * XD + c) = v;
+    }
+    XT(2, 1);
+  } else {
     f32x4 acc[2][2];
     zero(acc);
     const int c0 = 32 * (w & 3), kh = w >> 2, Kh = S / 2, kbase = kh * Kh;
@@ -162,6 +262,8 @@ __global__ __launch_bounds__(64 * F1_WAVES) void xh_audio_fwd_kernel(int M, int 
       mm_aw(acc, reinterpret_cast<const float*>(aseq) + r0 * ldas + kbase, ldas, rmax, Kh,
             SplitW{Ws.hi + kbase, Ws.lo + kbase}, S, c0);
     }
+    wregs_load(wa, Wa, XD, 16 * w, XD / 32);
+    wregs_load(wc, Wc, XD, 48 * w, XD / 32);
     // the upper K half's partial sums through aL (free until the second product), added in a fixed order
     if (kh == 1) store_acc(acc, c0, nullptr, aL, LDA, nullptr, 0, 0, 32);
     __syncthreads();
@@ -175,21 +277,21 @@ __global__ __launch_bounds__(64 * F1_WAVES) void xh_audio_fwd_kernel(int M, int 
       store_acc(acc, c0, bs, asL, LDA, a_s, XD, r0, rmax);
     }
   }
-  __syncthreads();
-  XT(2, 1);
+  lds_sync();  // LDS only: the weight loads and the a_s stores stay in flight
+  XT(2, 2);
   {  // a = a_s Wa^T + ba (16 columns per wave)
     f32x4 acc[2][1];
     zero(acc);
-    mm_aw<2, 1, 3, XD>(acc, asL, LDA, 32, XD, Wa, XD, 16 * w);
+    mm_lw<2, 1, XD / 32>(acc, asL, LDA, wa);
     store_acc(acc, 16 * w, ba, aL, LDA, a, XD, r0, rmax);
   }
-  __syncthreads();
-  XT(2, 2);
+  lds_sync();
+  XT(2, 3);
   {  // [q2 | k1 v1] = a Wc^T + [bq2 | bkv1]: 384 columns, 48 per wave in ONE pipelined pass (K = 128: 4 steps)
     f32x4 acc[2][3];
     zero(acc);
     const int c0 = 48 * w;
-    mm_aw<2, 3, 2, XD>(acc, aL, LDA, 32, XD, Wc, XD, c0);
+    mm_lw<2, 3, XD / 32>(acc, aL, LDA, wc);
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
       const int col = c0 + 16 * j + fr;
@@ -207,7 +309,25 @@ __global__ __launch_bounds__(64 * F1_WAVES) void xh_audio_fwd_kernel(int M, int 
         }
     }
   }
-  XT(2, 3);
+  XT(2, 4);
+}
+
+MER_API int mer_xh_audio_fwd_pair(int M, const float* pair, long ldp, const float* bs, const void* Wa_hi,
+                                  const void* Wa_lo, const float* ba, const void* Wc_hi, const void* Wc_lo,
+                                  const float* bq2, const float* bkv1, float* a_s, float* a, float* q2, float* kv1, int Mv,
+                                  int vdim, const float* vfeat, const void* Wv_hi, const void* Wv_lo, const float* bv,
+                                  const void* Wq1_hi, const void* Wq1_lo, const float* bq1, float* v, float* q1,
+                                  void* stream) {
+  if (M <= 0 || Mv < 0 || ldp < 2 * XD || ldp % 4 || ((uintptr_t)pair & 15) ||
+      (Mv > 0 && (vdim <= 0 || vdim % 32 || vdim > F1_VK || ((uintptr_t)vfeat & 15))))
+    return (int)hipErrorInvalidValue;
+  const SplitW wa{(const bf16_t*)Wa_hi, (const bf16_t*)Wa_lo}, wc{(const bf16_t*)Wc_hi, (const bf16_t*)Wc_lo};
+  const XhVideo vid{Mv, vdim, vfeat, SplitW{(const bf16_t*)Wv_hi, (const bf16_t*)Wv_lo}, bv,
+                    SplitW{(const bf16_t*)Wq1_hi, (const bf16_t*)Wq1_lo}, bq1, v, q1};
+  const dim3 grid((M + 31) / 32 + (Mv + F1_VROWS - 1) / F1_VROWS);
+  hipLaunchKernelGGL((xh_audio_fwd_kernel<float, true>), grid, dim3(64 * F1_WAVES), 0, (hipStream_t)stream, M, 2 * XD,
+                     pair, ldp, SplitW{nullptr, nullptr}, bs, wa, ba, wc, bq2, bkv1, a_s, a, q2, kv1, vid);
+  MER_LAUNCH_CHECK();
 }
 
 MER_API int mer_xh_audio_fwd(int M, int S, const void* aseq, int aseq_dtype, long ldas, const void* Ws_hi,
@@ -219,13 +339,14 @@ MER_API int mer_xh_audio_fwd(int M, int S, const void* aseq, int aseq_dtype, lon
   // M = 0: the video rows alone; Mv = 0: the audio chain alone (the head's audio-first schedule launches them
   // separately, the audio chain on a side stream beside the frame trunk)
   if (M < 0 || Mv < 0 || M + Mv == 0) return (int)hipErrorInvalidValue;
-  if ((M > 0 && (S % 64 || ldas % 8 || ((uintptr_t)aseq & 15))) || (Mv > 0 && (vdim <= 0 || vdim % 32)))
+  if ((M > 0 && (S % 64 || ldas % 8 || ((uintptr_t)aseq & 15))) ||
+      (Mv > 0 && (vdim <= 0 || vdim % 32 || vdim > F1_VK || ((uintptr_t)vfeat & 15))))
     return (int)hipErrorInvalidValue;
   const SplitW ws{(const bf16_t*)Ws_hi, (const bf16_t*)Ws_lo}, wa{(const bf16_t*)Wa_hi, (const bf16_t*)Wa_lo},
       wc{(const bf16_t*)Wc_hi, (const bf16_t*)Wc_lo};
   const XhVideo vid{Mv, vdim, vfeat, SplitW{(const bf16_t*)Wv_hi, (const bf16_t*)Wv_lo}, bv,
                     SplitW{(const bf16_t*)Wq1_hi, (const bf16_t*)Wq1_lo}, bq1, v, q1};
-  const dim3 grid((M + 31) / 32 + (Mv + 31) / 32);
+  const dim3 grid((M + 31) / 32 + (Mv + F1_VROWS - 1) / F1_VROWS);
   if (aseq_dtype == MER_BF16)
     hipLaunchKernelGGL(xh_audio_fwd_kernel<bf16_t>, grid, dim3(64 * F1_WAVES), 0, (hipStream_t)stream, M, S,
                        (const bf16_t*)aseq, ldas, ws, bs, wa, ba, wc, bq2, bkv1, a_s, a, q2, kv1, vid);

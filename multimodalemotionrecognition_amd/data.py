@@ -231,8 +231,10 @@ class ClipLoader:
     gradient all-reduce).  ``workers`` threads decode ahead (``prefetch`` batches).  ``augment``: the reference's
     train-split audio augmentation (ravdess.py:519-578, bar noise at a drawn SNR; ``bar_noise`` is the 16 kHz
     track, else Gaussian noise), drawn from a generator seeded per (seed, epoch, item) so the draws do not depend
-    on thread scheduling.  The reference's video augmentation (cv2.GaussianBlur + darken + noise, ravdess.py:
-    366-384) needs cv2, which this image lacks: not applied."""
+    on thread scheduling.  ``augment`` also applies the reference's train-split video augmentation
+    (cv2.GaussianBlur(k, 0) + darken + Gaussian noise on the uint8 frames, ravdess.py:366-384) on the device, one
+    ``clips.augment_clips`` launch per batch with per-clip draws from the same generator; it is bit-exact against
+    the restatement in ``oracle/clips_ref.py``, and parity against cv2 itself is unpinned (cv2 is absent here)."""
 
     def __init__(self, items: Sequence[Tuple], batch_size: int = 32, num_frames: int = 8, size: int = 112,
                  sample_rate: int = 16000, duration_sec: float = 3.0, rank: int = 0, world: int = 1,

@@ -971,6 +971,20 @@ def xh_audio_fwd(af, Ws, bs, Wa, ba, Wc, bq2, bkv1, a_s, a, q2, kv1, vf, Wv, bv,
             *_planes(Wq1), bq1.data_ptr(), v.data_ptr(), q1.data_ptr(), stream_ptr())
 
 
+def xh_audio_fwd_pair(pair, bs, Wa, ba, Wc, bq2, bkv1, a_s, a, q2, kv1, vf, Wv, bv, Wq1, bq1, v, q1):
+    """F1 after the first product ran as one bf16 GEMM: ``pair`` = [aseq Ws_hi^T | aseq Ws_lo^T] fp32 [M, 256]."""
+    M = pair.shape[0]
+    Mv, vdim = vf.shape
+    if pair.shape[1] != 256 or pair.stride(1) != 1 or Wc[0].shape != (384, 128) or Wv[0].shape != (128, vdim) \
+            or tuple(v.shape) != (Mv, 128) or tuple(q1.shape) != (Mv, 128):
+        raise ValueError("xh_audio_fwd_pair shapes")
+    _f32c(pair, a_s, a, q2, kv1, vf, v, q1)
+    _launch("xh_audio_fwd", (M, 256), "mer_xh_audio_fwd_pair", M, pair.data_ptr(), pair.stride(0), bs.data_ptr(),
+            *_planes(Wa), ba.data_ptr(), *_planes(Wc), bq2.data_ptr(), bkv1.data_ptr(), a_s.data_ptr(), a.data_ptr(),
+            q2.data_ptr(), kv1.data_ptr(), Mv, vdim, vf.data_ptr(), *_planes(Wv), bv.data_ptr(), *_planes(Wq1),
+            bq1.data_ptr(), v.data_ptr(), q1.data_ptr(), stream_ptr())
+
+
 def xh_v2a_fwd(B, T, Ta, v, q1, kv1, Wo1, bo1, gamma, beta, Wkv2, bkv2, attn_p, path_p, rng, site_attn, site_path,
                scale, P1, o1, s_v, mu_v, rs_v, v1, kv2, emb, bias=None):
     if tuple(v.shape) != (B * T, 128) or tuple(q1.shape) != (B * T, 128) or tuple(kv1.shape) != (B * Ta, 256) \

@@ -24,6 +24,7 @@ BWD_ENABLED = os.environ.get("MER_XATTN_FUSED_BWD", "1") != "0"
 WGRAD_ROWS = 256  # rows of dY / X per weight-gradient workgroup (M is split over the grid)
 PRIOR = "emotion_prior_bias."
 PRIOR_HEADS = ("v_query_bias", "a_key_bias", "a_query_bias", "v_key_bias")  # mer_xh_prior_fwd's head order
+F1_PAIR = True  # bf16 features: the first product as a bf16 GEMM + mer_xh_audio_fwd_pair (tools A/B only)
 
 # (weight name, row slice) for each split plane; rows are contiguous slices of the reference's parameters
 _PLANES = {
@@ -46,7 +47,7 @@ def supported(cfg, p: Dict[str, torch.Tensor], v_feat: torch.Tensor, a_seq: torc
     B, T, vd = v_feat.shape
     _, Ta, sd = a_seq.shape
     if a_seq.dtype not in (torch.bfloat16, torch.float32) or v_feat.dtype != torch.float32 or T > 16 or Ta > 160 \
-            or vd % 32 or sd % 64:
+            or vd % 32 or vd > 512 or sd % 64:
         return False
     if a_seq.requires_grad:  # the fused forward has no audio-feature gradient path (stage 2 runs unfused)
         return False
@@ -93,11 +94,13 @@ class SplitPlanes:
         dev = p["v_in_proj.weight"].device
         self.planes = {}
         rows = []
+        self.stacked = {}  # key -> [hi; lo] as one [2 * rows][k] bf16 matrix (the GEMM operand of F1's first product)
         for key, parts in _PLANES.items():
             srcs = _parts(p, parts)
             n_rows, k = sum(s.shape[0] for s in srcs), srcs[0].shape[1]
-            hi = torch.empty(n_rows, k, device=dev, dtype=torch.bfloat16)
-            lo = torch.empty(n_rows, k, device=dev, dtype=torch.bfloat16)
+            both = torch.empty(2, n_rows, k, device=dev, dtype=torch.bfloat16)
+            hi, lo = both[0], both[1]
+            self.stacked[key] = both.view(2 * n_rows, k)
             off = 0
             for s in srcs:
                 rows.append([s.data_ptr(), hi.data_ptr() + 2 * off, lo.data_ptr() + 2 * off, s.shape[0], s.shape[1], 0,
@@ -177,9 +180,18 @@ def fused_forward(p, cfg, v_feat, a_seq, training, rng, ctx, sites):
     af = a_seq.reshape(B * Ta, sd).contiguous()
     a_s, a, q2, kv1 = e(B * Ta, d), e(B * Ta, d), e(B * Ta, d), e(B * Ta, 2 * d)
     v, q1, o1 = e(B * T, d), e(B * T, d), e(B * T, d)
-    K.xh_audio_fwd(af, sp["Ws"], p["audio_seq_proj.bias"], sp["Wa"], p["a_in_proj.bias"], sp["Wc"],
-                   p["a2v_attn.in_proj_bias"][:d], p["v2a_attn.in_proj_bias"][d:], a_s, a, q2, kv1, vf, sp["Wv"],
-                   p["v_in_proj.bias"], sp["Wq1"], p["v2a_attn.in_proj_bias"][:d], v, q1)
+    if af.dtype == torch.bfloat16 and F1_PAIR:
+        # the 768-deep first product as ONE pipelined bf16 GEMM against the stacked [hi; lo] planes (128 x 64 tiles:
+        # 152 workgroups), F1 then sums the two halves: the product inside F1 was L2-latency-bound (~34 us)
+        pair = e(B * Ta, 2 * d)
+        K.gemm_bf16(af, sp.stacked["Ws"], pair, variant=7)
+        K.xh_audio_fwd_pair(pair, p["audio_seq_proj.bias"], sp["Wa"], p["a_in_proj.bias"], sp["Wc"],
+                            p["a2v_attn.in_proj_bias"][:d], p["v2a_attn.in_proj_bias"][d:], a_s, a, q2, kv1, vf, sp["Wv"],
+                            p["v_in_proj.bias"], sp["Wq1"], p["v2a_attn.in_proj_bias"][:d], v, q1)
+    else:
+        K.xh_audio_fwd(af, sp["Ws"], p["audio_seq_proj.bias"], sp["Wa"], p["a_in_proj.bias"], sp["Wc"],
+                       p["a2v_attn.in_proj_bias"][:d], p["v2a_attn.in_proj_bias"][d:], a_s, a, q2, kv1, vf, sp["Wv"],
+                       p["v_in_proj.bias"], sp["Wq1"], p["v2a_attn.in_proj_bias"][:d], v, q1)
     sv = ctx.saved
     v2a_bias = a2v_bias = None
     if cfg.use_prior:  # the emotion-prior attention biases from the pre-attention tokens (fusion.py:390-391): one launch

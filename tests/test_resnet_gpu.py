@@ -493,6 +493,24 @@ def test_space_to_depth_stem_vs_torch(H):
     assert rel_rms(dw, wr.grad) < 1e-2
 
 
+def test_space_to_depth_pack_frame_chunks():
+    """Above 2^22 packed pixels per launch (1204 frames at 112x112) the pack runs in frame chunks: the result
+    equals per-frame-slice packs bit for bit (no batch-size ceiling from the index math)."""
+    from multimodalemotionrecognition_amd import kernels as K
+    from multimodalemotionrecognition_amd.video import S2D_CH
+
+    N, H = 1300, 112
+    g = torch.Generator(device="cuda").manual_seed(5)
+    x = torch.randn(N, 3, H, H, device="cuda", generator=g)
+    whole = torch.empty(N, H // 2 + 3, H // 2 + 3, S2D_CH, device="cuda", dtype=torch.bfloat16)
+    K.pack_input_s2d(x, whole)
+    part = torch.empty_like(whole)
+    for n0 in range(0, N, 400):
+        K.pack_input_s2d(x[n0:n0 + 400], part[n0:n0 + 400])
+    torch.cuda.synchronize()
+    assert torch.equal(whole.view(torch.int16), part.view(torch.int16))
+
+
 @pytest.mark.parametrize("training", [True, False])
 def test_fused_stem_tail_matches_unfused(training):
     """stem_bnrelu_maxpool == bn_apply(relu) -> maxpool_fwd bit for bit; stem_pool_bn_bwd == maxpool_bwd ->

@@ -18,11 +18,13 @@ def main():
     ap.add_argument("--iters", type=int, default=200)
     ap.add_argument("--head", default="concat")
     ap.add_argument("--train", type=int, default=1)
+    ap.add_argument("--f1-pair", type=int, default=1)
     args = ap.parse_args()
     from multimodalemotionrecognition_amd import xattn_fused as XF
     from multimodalemotionrecognition_amd import xattn_head as XH
     from multimodalemotionrecognition_amd.fusion import _head_grads
     from tests.gpu_helpers import feats, head_model
+    XF.F1_PAIR = bool(args.f1_pair)
 
     m = head_model(args.head, False).train(bool(args.train))
     names, params = m.head_params()

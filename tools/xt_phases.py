@@ -40,6 +40,8 @@ def run():
     from multimodalemotionrecognition_amd import xattn_head as XH
     from multimodalemotionrecognition_amd.fusion import _head_grads
     from tests.gpu_helpers import feats, head_model
+    from multimodalemotionrecognition_amd import xattn_fused as XF
+    XF.F1_PAIR = "nopair" not in sys.argv[2:]
     m = head_model("concat", False).train(True)
     names, params = m.head_params()
     p = dict(zip(names, params))
@@ -62,18 +64,19 @@ def run():
     tick_us = 0.01  # wall_clock64: 100 MHz
     for slot, name in NAMES.items():
         t = buf[slot]
-        used = [b for b in range(512) if t[b, 0] != 0]
-        if not used:
-            continue
-        nph = max(k for k in range(16) if t[used[0], k] != 0)
-        rows = []
-        for k in range(1, nph + 1):
-            d = [(t[b, k] - t[b, k - 1]) * tick_us for b in used if t[b, k] and t[b, k - 1]]
-            rows.append(f"p{k} {np.median(d):6.2f}")
-        tot = [(t[b, nph] - t[b, 0]) * tick_us for b in used]
-        span = (max(t[b, nph] for b in used) - min(t[b, 0] for b in used)) * tick_us
-        print(f"{name:14s} blocks {len(used):4d}  " + "  ".join(rows) + f"  | block total {np.median(tot):6.2f}  kernel span {span:6.2f} us")
-
+        for k0, sub in ((0, ""), (8, " (k 8+)")):  # F1: audio blocks stamp 0-3, video blocks 8-10
+            used = [b for b in range(512) if t[b, k0] != 0]
+            if not used:
+                continue
+            nph = max(k for k in range(k0, 16) if t[used[0], k] != 0)
+            rows = []
+            for k in range(k0 + 1, nph + 1):
+                d = [(t[b, k] - t[b, k - 1]) * tick_us for b in used if t[b, k] and t[b, k - 1]]
+                rows.append(f"p{k} {np.median(d):6.2f}")
+            tot = [(t[b, nph] - t[b, k0]) * tick_us for b in used]
+            span = (max(t[b, nph] for b in used) - min(t[b, k0] for b in used)) * tick_us
+            print(f"{name + sub:22s} blocks {len(used):4d}  " + "  ".join(rows)
+                  + f"  | block total {np.median(tot):6.2f} max {np.max(tot):6.2f}  span {span:6.2f} us")
 
 if __name__ == "__main__":
     {"build": build, "run": run}[sys.argv[1]]()
