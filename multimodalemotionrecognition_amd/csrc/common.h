@@ -150,6 +150,18 @@ __device__ __forceinline__ void wait_tiles_in_flight(int n) {
   else if (n == 2) wait_vmcnt<2 * G>();
   else wait_vmcnt<3 * G>();
 }
+// Record of block v in a kernel-argument table sorted by first block (first(0) = 0, non-decreasing, n <= 64):
+// each lane loads one record's first block and a ballot counts the records at or before v -- one load latency
+// instead of a serial scan whose every step is a dependent scalar load of the argument segment (~0.8 us each,
+// paid by every block before its first useful instruction).
+template <typename F>
+__device__ __forceinline__ int table_find(int n, int v, F first) {
+  const int lane = threadIdx.x & 63;
+  const int f = lane < n ? first(lane) : 0x7fffffff;
+  const unsigned long long m = __ballot(f <= v);
+  return __builtin_amdgcn_readfirstlane(__popcll(m) - 1);
+}
+
 // lgkmcnt(0) only (LDS reads retired), then a raw s_barrier: glds DMAs stay in flight across it
 __device__ __forceinline__ void lds_barrier() {
   __builtin_amdgcn_s_waitcnt((15) | (7 << 4) | (0 << 8) | (3 << 14));

@@ -687,8 +687,7 @@ struct FoldTable {
 __global__ __launch_bounds__(256) void wgrad_fold_batch_kernel(FoldTable t) {
   __shared__ float part[256];
   const int v = blockIdx.x;
-  int ri = 0;
-  while (ri + 1 < t.n && v >= t.r[ri + 1].blk0) ++ri;
+  const int ri = table_find(t.n, v, [&](int i) { return t.r[i].blk0; });
   const FoldRec& R = t.r[ri];
   const int SG = R.SG, E = 256 / SG, e = threadIdx.x % E, sg = threadIdx.x / E;
   const long row = (long)R.RS * R.C, total = (long)R.K * row;

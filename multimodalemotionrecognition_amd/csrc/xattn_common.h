@@ -196,6 +196,50 @@ __device__ __forceinline__ void mm_aw(f32x4 (&acc)[TI][TJ], const float* A, long
   }
 }
 
+// pre-split weight fragments of NS 32-wide k steps x TJ 16-column tiles, held in registers
+template <int NS, int TJ>
+struct WRegs {
+  u4 h[NS][TJ], l[NS][TJ];
+};
+
+// steps >= nvalid load step nvalid - 1 and columns >= nrows row nrows - 1 (valid addresses; the A operand is
+// zero past the valid steps, the extra columns are never stored)
+template <int NS, int TJ>
+__device__ __forceinline__ void wregs_load(WRegs<NS, TJ>& r, SplitW W, long ldw, int c0, int nvalid,
+                                           int nrows = 1 << 30) {
+  const int lane = threadIdx.x & 63, fr = lane & 15, fk = (lane >> 4) * 8;
+#pragma unroll
+  for (int s = 0; s < NS; ++s)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const int n = c0 + 16 * j + fr;
+      const long off = (long)(n < nrows ? n : nrows - 1) * ldw + 32 * (s < nvalid ? s : nvalid - 1) + fk;
+      r.h[s][j] = *reinterpret_cast<const u4*>(W.hi + off);
+      r.l[s][j] = *reinterpret_cast<const u4*>(W.lo + off);
+    }
+}
+
+// acc[i][j] += A[rows 16i..][0 : 32 NS] . W^T: A fp32 rows in LDS (split on the fly), W from registers; the same
+// per-step order as mm_aw (hi.hi, hi.lo, lo.hi per k step)
+template <int TI, int TJ, int NS>
+__device__ __forceinline__ void mm_lw(f32x4 (&acc)[TI][TJ], const float* A, int lda, const WRegs<NS, TJ>& w) {
+  const int lane = threadIdx.x & 63, fr = lane & 15, fk = (lane >> 4) * 8;
+#pragma unroll
+  for (int s = 0; s < NS; ++s)
+#pragma unroll
+    for (int i = 0; i < TI; ++i) {
+      bf16x8 ah, al;
+      frag_row(A + (16 * i + fr) * lda + 32 * s + fk, true, ah, al);
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {
+        Frag H, L;
+        H.u = w.h[s][j];
+        L.u = w.l[s][j];
+        acc[i][j] = mma3(ah, al, H.v, L.v, acc[i][j]);
+      }
+    }
+}
+
 template <int TI, int TJ>
 __device__ __forceinline__ void zero(f32x4 (&acc)[TI][TJ]) {
 #pragma unroll

@@ -8,7 +8,7 @@
 // mer_xh_split (they change every Adam step); activations are split in registers as fragments are built.
 //
 // Four launches replace the ~40-launch schedule of xattn_head.py (mean temporal pooling; concat / gated):
-//   F1 xh_audio_fwd (grid B*Ta/32 + B*T/32): a_seq(bf16) -> a_s = audio_seq_proj -> a = a_in_proj -> [q2 | k1 v1]
+//   F1 xh_audio_fwd (grid B*Ta/32 + B*T/16): a_seq(bf16) -> a_s = audio_seq_proj -> a = a_in_proj -> [q2 | k1 v1]
 //      (the a2v query projection and the v2a key/value projections share the input a); the trailing blocks
 //      project the video rows: v = v_in_proj(v_feat), q1
 //   F2 xh_v2a_fwd (grid B): MHA of q1 over the sample's Ta keys -> out-proj ->
@@ -35,12 +35,15 @@ __global__ void xh_split_kernel(const long long* __restrict__ desc) {
   const float* src = reinterpret_cast<const float*>(d[0]);
   bf16_t* hi = reinterpret_cast<bf16_t*>(d[1]);
   bf16_t* lo = reinterpret_cast<bf16_t*>(d[2]);
-  const long rows = d[3], cols = d[4], n = rows * cols, dld = d[6];
+  // 32-bit index math (the head's weights: well below 2^31 elements): a 64-bit division per
+  // element was most of this kernel's time
+  const unsigned rows = (unsigned)d[3], cols = (unsigned)d[4], n = rows * cols, dld = (unsigned)d[6];
   const bool trans = d[5] != 0;
-  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < n; e += (long)gridDim.x * blockDim.x) {
+  for (unsigned e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
     const float x = src[e];
     const bf16_t h = f2bf(x);
-    const long o = trans ? (e % cols) * dld + e / cols : e;
+    const unsigned q = e / cols;
+    const unsigned o = trans ? (e - q * cols) * dld + q : e;
     hi[o] = h;
     lo[o] = f2bf(x - bf2f(h));
   }
@@ -83,47 +86,6 @@ struct XhVideo {
   float* v;
   float* q1;
 };
-
-// pre-split weight fragments of NS 32-wide k steps x TJ 16-column tiles, held in registers
-template <int NS, int TJ>
-struct WRegs {
-  u4 h[NS][TJ], l[NS][TJ];
-};
-
-// steps >= nvalid load step nvalid - 1 (a valid address; the A operand is zero there)
-template <int NS, int TJ>
-__device__ __forceinline__ void wregs_load(WRegs<NS, TJ>& r, SplitW W, long ldw, int c0, int nvalid) {
-  const int lane = threadIdx.x & 63, fr = lane & 15, fk = (lane >> 4) * 8;
-#pragma unroll
-  for (int s = 0; s < NS; ++s)
-#pragma unroll
-    for (int j = 0; j < TJ; ++j) {
-      const long off = (long)(c0 + 16 * j + fr) * ldw + 32 * (s < nvalid ? s : nvalid - 1) + fk;
-      r.h[s][j] = *reinterpret_cast<const u4*>(W.hi + off);
-      r.l[s][j] = *reinterpret_cast<const u4*>(W.lo + off);
-    }
-}
-
-// acc[i][j] += A[rows 16i..][0 : 32 NS] . W^T: A fp32 rows in LDS (split on the fly), W from registers; the same
-// per-step order as mm_aw (hi.hi, hi.lo, lo.hi per k step)
-template <int TI, int TJ, int NS>
-__device__ __forceinline__ void mm_lw(f32x4 (&acc)[TI][TJ], const float* A, int lda, const WRegs<NS, TJ>& w) {
-  const int lane = threadIdx.x & 63, fr = lane & 15, fk = (lane >> 4) * 8;
-#pragma unroll
-  for (int s = 0; s < NS; ++s)
-#pragma unroll
-    for (int i = 0; i < TI; ++i) {
-      bf16x8 ah, al;
-      frag_row(A + (16 * i + fr) * lda + 32 * s + fk, true, ah, al);
-#pragma unroll
-      for (int j = 0; j < TJ; ++j) {
-        Frag H, L;
-        H.u = w.h[s][j];
-        L.u = w.l[s][j];
-        acc[i][j] = mma3(ah, al, H.v, L.v, acc[i][j]);
-      }
-    }
-}
 
 // TA bf16: the WavLM features (exact, two passes); float: fp32 features (split, three passes).  PAIR: the first
 // product was computed beforehand as ONE bf16 GEMM of the WavLM features with the stacked [hi; lo] planes of

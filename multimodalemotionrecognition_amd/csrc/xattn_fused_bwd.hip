@@ -596,7 +596,11 @@ MER_API int mer_xh_v2a_bwd(int B, int T, int Ta, const float* dkv2_part, const v
 
 // ---------------------------------------------------------------------------------------------
 // G1: audio chain backward, 32 rows per block: da += [dq2 | dK1 dV1] . [Wq2 ; Wkv1], da_s = da . Wa
-// Unfused: the dx halves of xattn_head.py:251, 269 and 303-304.
+// Unfused: the dx halves of xattn_head.py:251, 269 and 303-304.  The trailing ceil(B*T/16) blocks: dv += dq1 Wq1,
+// dv_feat = dv Wv.  Latency chains like F1: the block's input rows are staged into LDS with one load per
+// thread-slot and every weight fragment a wave needs is loaded into registers at block entry (WRegs), so one
+// memory latency precedes the products instead of one per k step (phase stamps, B = 32: the 384-deep first
+// product took 14.9 us, the video blocks' four 32-column dv_feat passes 12.5 us).
 // ---------------------------------------------------------------------------------------------
 struct XhVideoBwd {  // G1's video rows: dv += dq1 Wq1 (in place), dvfeat = dv Wv (NULL: not wanted)
   int M, vdim;
@@ -606,67 +610,126 @@ struct XhVideoBwd {  // G1's video rows: dv += dq1 Wq1 (in place), dvfeat = dv W
   float* dvfeat;
 };
 
-__global__ __launch_bounds__(256) void xh_audio_bwd_kernel(int M, const float* __restrict__ dqkv, SplitW WcT,
-                                                           SplitW WaT, float* __restrict__ da, float* __restrict__ da_s,
-                                                           XhVideoBwd vid) {
+constexpr int G1_WAVES = 8;
+constexpr int G1_ALD = 3 * XD + 4;  // LDS row stride of the staged [dq2 | dK1 dV1] rows
+constexpr int G1_VROWS = 16;        // video rows per block
+constexpr int G1_VK = 512;          // dv_feat width bound (ResNet18: 512)
+
+__global__ __launch_bounds__(64 * G1_WAVES) void xh_audio_bwd_kernel(int M, const float* __restrict__ dqkv,
+                                                                     SplitW WcT, SplitW WaT, float* __restrict__ da,
+                                                                     float* __restrict__ da_s, XhVideoBwd vid) {
+  __shared__ __attribute__((aligned(16))) float inL[32 * G1_ALD];
   __shared__ __attribute__((aligned(16))) float daL[32 * LDA];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, fr = lane & 15, fq = lane >> 4;
   const int na = (M + 31) / 32;
-  const bool video = (int)blockIdx.x >= na;
-  const long r0 = video ? (long)(blockIdx.x - na) * 32 : (long)blockIdx.x * 32;
-  const int rows = video ? vid.M : M;
-  const int rmax = (int)(rows - r0 < 32 ? rows - r0 : 32);
-  float* dst = video ? vid.dv : da;
-  // audio: da += [dq2 | dK1 dV1] . [Wq2 ; Wkv1];  video: dv += dq1 . Wq1.  Each arm owns its accumulators (one
-  // array shared by both arms of the branch is a phi of arrays the compiler puts in scratch memory)
-  auto finish = [&](const f32x4 (&acc)[2][2]) {
-    float res[2][2][4];  // all residual loads first: the in-place stores below may alias them
+  constexpr int NT = 64 * G1_WAVES;
+  if ((int)blockIdx.x < na) {
+    XT(0, 0);
+    const long r0 = (long)blockIdx.x * 32;
+    const int rmax = (int)(M - r0 < 32 ? M - r0 : 32);
+    constexpr int NX = 32 * 3 * XD / 4 / NT;  // float4 slots per thread
+    f32x4 x[NX];
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int q = 0; q < NX; ++q) {
+      const int e = threadIdx.x + NT * q, r = e / (3 * XD / 4), c = 4 * (e % (3 * XD / 4));
+      x[q] = *reinterpret_cast<const f32x4*>(dqkv + (r0 + (r < rmax ? r : rmax - 1)) * 3 * XD + c);
+    }
+    WRegs<3 * XD / 32, 1> wc;
+    wregs_load(wc, WcT, 3 * XD, 16 * w, 3 * XD / 32);
+    WRegs<XD / 32, 1> wa;
+    wregs_load(wa, WaT, XD, 16 * w, XD / 32);
+    float res[2][4];  // the residual (G3's LayerNorm-backward da), loaded before any store of this block
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = 16 * i + 4 * fq + r;
+        res[i][r] = da[(r0 + (row < rmax ? row : rmax - 1)) * XD + 16 * w + fr];
+      }
+#pragma unroll
+    for (int q = 0; q < NX; ++q) {
+      const int e = threadIdx.x + NT * q, r = e / (3 * XD / 4), c = 4 * (e % (3 * XD / 4));
+      *reinterpret_cast<f32x4*>(inL + r * G1_ALD + c) = r < rmax ? x[q] : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    lds_sync();
+    {
+      f32x4 acc[2][1];
+      zero(acc);
+      mm_lw<2, 1, 3 * XD / 32>(acc, inL, G1_ALD, wc);
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int row = 16 * i + 4 * fq + r, col = 32 * w + 16 * j + fr;
-          res[j][i][r] = dst[(r0 + (row < rmax ? row : rmax - 1)) * XD + col];
-        }
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = 16 * i + 4 * fq + r, col = 32 * w + 16 * j + fr;
-          const float v = row < rmax ? acc[i][j][r] + res[j][i][r] : 0.f;
-          if (row < rmax) dst[(r0 + row) * XD + col] = v;
+          const int row = 16 * i + 4 * fq + r, col = 16 * w + fr;
+          const float v = row < rmax ? acc[i][0][r] + res[i][r] : 0.f;
+          if (row < rmax) da[(r0 + row) * XD + col] = v;
           daL[row * LDA + col] = v;
         }
-  };
-  if (video) {
-    f32x4 acc[2][2];
+    }
+    lds_sync();
+    XT(0, 1);
+    f32x4 acc[2][1];  // da_s = da . Wa
     zero(acc);
-    mm_aw<2, 2, 3, XD>(acc, vid.dq1 + r0 * XD, XD, rmax, XD, vid.WqT1, XD, 32 * w);
-    finish(acc);
-  } else {
-    f32x4 acc[2][2];
-    zero(acc);
-    mm_aw<2, 2, 3, 3 * XD>(acc, dqkv + r0 * 3 * XD, 3 * XD, rmax, 3 * XD, WcT, 3 * XD, 32 * w);
-    finish(acc);
+    mm_lw<2, 1, XD / 32>(acc, daL, LDA, wa);
+    store_acc(acc, 16 * w, nullptr, nullptr, 0, da_s, XD, r0, rmax);
+    XT(0, 2);
+    return;
   }
-  __syncthreads();
-  if (!video) {  // da_s = da . Wa
-    f32x4 acc[2][2];
+  XT(0, 8);
+  const long v0 = (long)(blockIdx.x - na) * G1_VROWS;
+  const int vmax = (int)(vid.M - v0 < G1_VROWS ? vid.M - v0 : G1_VROWS), vd = vid.vdim;
+  constexpr int NX = G1_VROWS * XD / 4;  // = NT: one float4 per thread
+  static_assert(NX == NT, "one staged float4 per thread");
+  f32x4 x;
+  {
+    const int r = threadIdx.x / (XD / 4), c = 4 * (threadIdx.x % (XD / 4));
+    x = *reinterpret_cast<const f32x4*>(vid.dq1 + (v0 + (r < vmax ? r : vmax - 1)) * XD + c);
+  }
+  WRegs<XD / 32, 1> wq;
+  wregs_load(wq, vid.WqT1, XD, 16 * w, XD / 32);
+  WRegs<XD / 32, G1_VK / 16 / G1_WAVES> wv;  // 64 dv_feat columns per wave
+  if (vid.dvfeat) wregs_load(wv, vid.WvT, XD, (G1_VK / G1_WAVES) * w, XD / 32, vd);
+  float res[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int row = 4 * fq + r;
+    res[r] = vid.dv[(v0 + (row < vmax ? row : vmax - 1)) * XD + 16 * w + fr];
+  }
+  {
+    const int r = threadIdx.x / (XD / 4), c = 4 * (threadIdx.x % (XD / 4));
+    *reinterpret_cast<f32x4*>(inL + r * LDA + c) = r < vmax ? x : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  lds_sync();
+  {
+    f32x4 acc[1][1];
     zero(acc);
-    mm_aw<2, 2, 3, XD>(acc, daL, LDA, 32, XD, WaT, XD, 32 * w);
-    store_acc(acc, 32 * w, nullptr, nullptr, 0, da_s, XD, r0, rmax);
-  } else if (vid.dvfeat) {  // dv_feat = dv . Wv, 32-column passes per wave
-    for (int c0 = 32 * w; c0 < vid.vdim; c0 += 128) {
-      f32x4 acc[2][2];
-      zero(acc);
-      mm_aw<2, 2, 3, XD>(acc, daL, LDA, 32, XD, vid.WvT, XD, c0);
-      store_acc(acc, c0, nullptr, nullptr, 0, vid.dvfeat, vid.vdim, r0, rmax);
+    mm_lw<1, 1, XD / 32>(acc, inL, LDA, wq);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = 4 * fq + r, col = 16 * w + fr;
+      const float v = row < vmax ? acc[0][0][r] + res[r] : 0.f;
+      if (row < vmax) vid.dv[(v0 + row) * XD + col] = v;
+      daL[row * LDA + col] = v;
     }
   }
+  lds_sync();
+  XT(0, 9);
+  if (vid.dvfeat) {  // dv_feat = dv . Wv
+    constexpr int TJ = G1_VK / 16 / G1_WAVES;
+    f32x4 acc[1][TJ];
+    zero(acc);
+    mm_lw<1, TJ, XD / 32>(acc, daL, LDA, wv);
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const int col = (G1_VK / G1_WAVES) * w + 16 * j + fr;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = 4 * fq + r;
+        if (row < vmax && col < vd) vid.dvfeat[(v0 + row) * vd + col] = acc[0][j][r];
+      }
+    }
+  }
+  XT(0, 10);
 }
 
 MER_API int mer_xh_audio_bwd(int M, const float* dqkv, const void* WcT_hi, const void* WcT_lo, const void* WaT_hi,
@@ -674,11 +737,13 @@ MER_API int mer_xh_audio_bwd(int M, const float* dqkv, const void* WcT_hi, const
                              const void* WqT1_hi, const void* WqT1_lo, const void* WvT_hi, const void* WvT_lo, float* dv,
                              float* dvfeat, void* stream) {
   // M = 0: the video rows alone (the critical path into the trunk backward); Mv = 0: the audio chain alone
-  if (M < 0 || Mv < 0 || M + Mv == 0 || (Mv > 0 && (!dq1 || !dv || (dvfeat && (vdim <= 0 || vdim % 32)))))
+  if (M < 0 || Mv < 0 || M + Mv == 0 ||
+      (Mv > 0 && (!dq1 || !dv || (dvfeat && (vdim <= 0 || vdim % 32 || vdim > G1_VK)))))
     return (int)hipErrorInvalidValue;
   const XhVideoBwd vid{Mv, vdim, dq1, SplitW{(const bf16_t*)WqT1_hi, (const bf16_t*)WqT1_lo},
                        SplitW{(const bf16_t*)WvT_hi, (const bf16_t*)WvT_lo}, dv, dvfeat};
-  hipLaunchKernelGGL(xh_audio_bwd_kernel, dim3((M + 31) / 32 + (Mv + 31) / 32), dim3(256), 0, (hipStream_t)stream, M,
+  hipLaunchKernelGGL(xh_audio_bwd_kernel, dim3((M + 31) / 32 + (Mv + G1_VROWS - 1) / G1_VROWS), dim3(64 * G1_WAVES), 0,
+                     (hipStream_t)stream, M,
                      dqkv, SplitW{(const bf16_t*)WcT_hi, (const bf16_t*)WcT_lo},
                      SplitW{(const bf16_t*)WaT_hi, (const bf16_t*)WaT_lo}, da, da_s, vid);
   MER_LAUNCH_CHECK();
@@ -774,8 +839,7 @@ __global__ __launch_bounds__(512) void xh_wgrad_kernel(const WgTab tab, float* _
   // once instead of once per XCD the round-robin placement spread them over
   int vb = blockIdx.x, unused;
   if (tab.xcd) xcd_tile(blockIdx.x, 1 << 30, (int)gridDim.x, vb, unused);
-  int pi = 0;
-  while (pi + 1 < tab.nprob && tab.p[pi + 1].first_block <= vb) ++pi;
+  const int pi = table_find(tab.nprob, vb, [&](int i) { return tab.p[i].first_block; });
   const WgProb& d = tab.p[pi];
   const int N = d.N, K = d.K, splits = d.splits;
   const int ntk = K > 0 ? (K + WG_T - 1) / WG_T : 1;
@@ -804,6 +868,7 @@ __global__ __launch_bounds__(512) void xh_wgrad_kernel(const WgTab tab, float* _
   // chunk i of this group starts at row m0 + 32 * (2i + grp); a group past the range loads an empty range
   // (m >= m1 everywhere: zeros), so both groups run the same iterations and barriers
   auto chunk_row = [&](long i) { return m0 + 32 * (2 * i + grp); };
+  XT(1, 0);
   WgChunk cur;
   wg_load(d, chunk_row(0), m1, n0, k0, cur);
   for (long it = 0; it < iters; ++it) {
@@ -833,6 +898,7 @@ __global__ __launch_bounds__(512) void xh_wgrad_kernel(const WgTab tab, float* _
         acc[i][j] = mma(AH.v, BL[j].v, acc[i][j]);
       }
     }
+    if (it < 4) XT(1, 1 + it);
   }
   bred[grp * 2 + (t >> 7)][col] = bsum;
   __syncthreads();  // every group is past its last fragment read: the planes take group 1's partial
@@ -845,6 +911,7 @@ __global__ __launch_bounds__(512) void xh_wgrad_kernel(const WgTab tab, float* _
         *reinterpret_cast<f32x4*>(xch + ((i * 4 + j) * 256 + t) * 4) = acc[i][j];
   }
   __syncthreads();
+  XT(1, 5);
   if (grp == 0) {
     if (K > 0) {
       float* out = ws + d.ws_off + (long)split * N * K;
@@ -863,6 +930,7 @@ __global__ __launch_bounds__(512) void xh_wgrad_kernel(const WgTab tab, float* _
     if (bias && t < WG_T && n0 + t < N)
       ws[d.ws_b_off + (long)split * N + n0 + t] = (bred[0][t] + bred[1][t]) + (bred[2][t] + bred[3][t]);
   }
+  XT(1, 6);
 }
 
 __global__ __launch_bounds__(256) void xh_wfold_kernel(const WgTab tab, const float* __restrict__ ws) {

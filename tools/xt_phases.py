@@ -11,7 +11,7 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parents[1]
 PKG = ROOT / "multimodalemotionrecognition_amd"
 XT_LIB = PKG / "libmer_hip_xt.so"
-NAMES = {0: "G4 mlp_bwd", 1: "G2 v2a_bwd", 2: "F1 audio_fwd", 3: "F2 v2a_fwd"}
+NAMES = {0: "G1 audio_bwd", 1: "W wgrad", 2: "F1 audio_fwd", 3: "F2 v2a_fwd"}
 
 
 def build():
