@@ -285,6 +285,27 @@ def roof_core(core_ms, peak_split):
                         "runs its out-projection, residual + LayerNorm; the whole duration is charged to the core)"}
 
 
+CORE_ATTN_FILE = Path(__file__).resolve().parent / "profiles" / "r05" / "core_attn.json"
+
+
+def roof_core_attn(peak_split):
+    """The ``roofline_head.core_attn`` entry: the attention cores' FLOPs over the QK^T / softmax / PV phases alone
+    (their backward too) -- phase stamps of the timing build (tools/xt_phases.py ... core), committed as
+    profiles/r05/core_attn.json; the four kernels' out-projection / residual / LayerNorm phases are excluded."""
+    if not CORE_ATTN_FILE.exists():
+        return None
+    rec = json.loads(CORE_ATTN_FILE.read_text())
+    flop, byt = core_attention()
+    ms = rec["core_attn_us"] / 1e3
+    ai = flop / byt
+    attain = min(peak_split, ai * PEAK_HBM_GBS / 1e3)
+    ach = flop / (ms * 1e-3) / 1e12
+    return {"bound": "mfma" if peak_split < ai * PEAK_HBM_GBS / 1e3 else "hbm", "achieved": round(ach, 3),
+            "peak": round(attain, 2), "unit": "TFLOP/s", "frac": round(ach / attain, 4), "ms": round(ms, 4),
+            "kernel_us": {k: v["core_us"] for k, v in rec["kernels"].items()},
+            "source": "profiles/r05/core_attn.json (" + rec["method"] + ")"}
+
+
 def time_head_core(model, dev, reps: int):
     """HIP events around every launch of the fused head's four attention kernels (F2 / F3 forward, G2 / G3 backward:
     each fuses its attention with the out-projection, drop-path + residual + LayerNorm and, F2 / G2, the next
@@ -584,6 +605,7 @@ def _bench(args, world, rank, local):
                      "hbm_gbs_achieved": round(hbytes / (head_ms * 1e-3) / 1e9, 1),
                      "peak_basis": "min(split-bf16 fp32-class MFMA peak = 2.5 PF / 3, intensity x 8 TB/s)",
                      "core": roof_core(core_ms, peak_split),
+                     "core_attn": roof_core_attn(peak_split),
                      "measured": f"HIP events around the head's forward / backward graph replays in "
                                  f"{len(hprobe.fwd)} probe steps"}
     step_gflop = BATCH * (STEP_GFLOP_PER_CLIP_FIXED + WAVLM_LAYER_GFLOP_PER_CLIP * layers)

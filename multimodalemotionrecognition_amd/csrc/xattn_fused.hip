@@ -496,6 +496,7 @@ __global__ __launch_bounds__(256) void xh_v2a_attn_kernel(int T, int Ta, const f
   __shared__ float red[2][4][16];                                   // per-wave row max / row sum
   __shared__ __attribute__((aligned(16))) float PL[4][16 * F2A_PLD];  // per-wave P' chunk (PV A operand)
   __shared__ float oP[4][16][33];                                   // per-wave P' V partials
+  XT(3, 0);
   const int b = blockIdx.x >> 2, h = blockIdx.x & 3;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, fr = lane & 15, fq = lane >> 4, fk = fq * 8;
   const long ldkv = 2 * XD;
@@ -633,6 +634,7 @@ __global__ __launch_bounds__(256) void xh_v2a_attn_kernel(int T, int Ta, const f
     const int i = e / XDH, d = e - i * XDH;
     o1[((long)b * T + i) * XD + h * XDH + d] = (oP[0][i][d] + oP[1][i][d]) + (oP[2][i][d] + oP[3][i][d]);
   }
+  XT(3, 1);
 }
 
 // F2b: F2's second half on o1 (one workgroup per sample): v2 = o1 Wo1^T + bo1, v1 = LN(v + keep_b v2), v-pool,
@@ -725,20 +727,31 @@ __global__ __launch_bounds__(256) void xh_a2v_fwd_kernel(int T, int Ta, int ntil
   const long row0 = (long)b * Ta + i0;
   const unsigned long long seed_attn = mer_site_seed(dr.seed, dr.site_attn);
   const unsigned long long seed_path = mer_site_seed(dr.seed, dr.site_path);
+  XT(1, 0);
+  // the residual rows and the out-projection's weight fragments are loaded before the attention (their latency
+  // overlaps it)
+  f32x4 ar[16 * XD / 4 / 256];
+#pragma unroll
+  for (int q = 0; q < 16 * XD / 4 / 256; ++q) {
+    const int e = threadIdx.x + 256 * q, r = e / (XD / 4), c = 4 * (e % (XD / 4));
+    ar[q] = *reinterpret_cast<const f32x4*>(a + (row0 + (r < nr ? r : nr - 1)) * XD + c);
+  }
+  WRegs<XD / 32, 2> wo;
+  wregs_load(wo, Wo2, XD, 32 * w, XD / 32);
   head_attention<1>(b, w, i0, Ta, T, q2 + row0 * XD, XD, kv2 + (long)b * T * 2 * XD, kv2 + (long)b * T * 2 * XD + XD,
                     2 * XD, scale, P2, dr.attn, seed_attn, PL + w * 16 * F3_PLD, F3_PLD, oL, bias);
+  XT(1, 1);
 #pragma unroll
-  for (int e = threadIdx.x; e < 16 * XD; e += 256) {
-    const int r = e / XD, c = e - r * XD;
-    const float x = a[(row0 + (r < nr ? r : nr - 1)) * XD + c];
-    aL[r * LDA + c] = r < nr ? x : 0.f;
+  for (int q = 0; q < 16 * XD / 4 / 256; ++q) {
+    const int e = threadIdx.x + 256 * q, r = e / (XD / 4), c = 4 * (e % (XD / 4));
+    *reinterpret_cast<f32x4*>(aL + r * LDA + c) = r < nr ? ar[q] : f32x4{0.f, 0.f, 0.f, 0.f};
   }
   __syncthreads();
   for (int e = threadIdx.x; e < nr * XD; e += 256) o2[row0 * XD + e] = oL[(e / XD) * LDA + e % XD];
   {  // a2 = o Wo2^T + bo2
     f32x4 acc[1][2];
     zero(acc);
-    mm_aw<1, 2, 3, XD>(acc, oL, LDA, 16, XD, Wo2, XD, 32 * w);
+    mm_lw<1, 2, XD / 32>(acc, oL, LDA, wo);
     store_acc(acc, 32 * w, bo2, tL, LDA, nullptr, 0, 0, 16);
   }
   __syncthreads();
@@ -749,6 +762,7 @@ __global__ __launch_bounds__(256) void xh_a2v_fwd_kernel(int T, int Ta, int ntil
     for (int r = 0; r < nr; ++r) s += oL[r * LDA + threadIdx.x];
     part[((long)b * ntiles + tile) * XD + threadIdx.x] = s;
   }
+  XT(1, 2);
 }
 
 MER_API int mer_xh_a2v_fwd(int B, int T, int Ta, const float* q2, const float* kv2, const float* a, const void* Wo2_hi,

@@ -186,6 +186,7 @@ __global__ __launch_bounds__(256) void xh_a2v_bwd_kernel(
   __shared__ __attribute__((aligned(16))) float oL[16 * LDA];
   __shared__ __attribute__((aligned(16))) float tiles[XH * 2 * 16 * G3_TLD];
   __shared__ float red[4 * 256];
+  XT(3, 0);
   const int b = blockIdx.x / ntiles, tile = blockIdx.x - b * ntiles, w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int fr = lane & 15, fq = lane >> 4, fk = fq * 8;
   const int i0 = tile * 16, nr = Ta - i0 < 16 ? Ta - i0 : 16;
@@ -219,6 +220,7 @@ __global__ __launch_bounds__(256) void xh_a2v_bwd_kernel(
     store_acc(acc, 32 * w, nullptr, oL, LDA, nullptr, 0, 0, 16);
   }
   __syncthreads();
+  XT(3, 1);
   // attention backward of head h = w over the sample's T keys
   const int h = w;
   float* dSt = tiles + (h * 2) * 16 * G3_TLD;
@@ -297,6 +299,7 @@ __global__ __launch_bounds__(256) void xh_a2v_bwd_kernel(
         pt[j * 2 * XD + XD + h * XDH + 16 * jt + fr] = dv[jt][r];
       }
   }
+  XT(3, 2);
   if (dbias) {  // the prior bias gradient: dS summed over the heads in head order (mha_dbias_kernel's order)
     __syncthreads();
     for (int e = threadIdx.x; e < nr * T; e += 256) {
@@ -307,6 +310,7 @@ __global__ __launch_bounds__(256) void xh_a2v_bwd_kernel(
       dbias[((long)b * Ta + i0 + i) * T + j] = s;
     }
   }
+  XT(3, 3);
 }
 
 MER_API int mer_xh_a2v_bwd(int B, int T, int Ta, const float* demb, const float* s_a, const float* mean_a,
@@ -412,6 +416,7 @@ __global__ __launch_bounds__(256) void xh_v2a_attn_bwd_kernel(
   __shared__ __attribute__((aligned(16))) float dSt[4][16 * G2B_TLD];  // per-wave dS chunk [query][key]
   __shared__ __attribute__((aligned(16))) float Pdt[4][16 * G2B_TLD];  // per-wave P' chunk
   __shared__ float oP[4][16][33];
+  XT(2, 0);
   const int b = blockIdx.x >> 2, h = blockIdx.x & 3;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, fr = lane & 15, fq = lane >> 4, fk = fq * 8;
   const long ldkv = 2 * XD, row0 = (long)b * T;
@@ -556,6 +561,7 @@ __global__ __launch_bounds__(256) void xh_v2a_attn_bwd_kernel(
     const int i = e / XDH, d = e - i * XDH;
     dq1[(row0 + i) * XD + h * XDH + d] = ((oP[0][i][d] + oP[1][i][d]) + (oP[2][i][d] + oP[3][i][d])) * scale;
   }
+  XT(2, 1);
 }
 
 // the prior bias gradient: dbias[b][i][j] = sum over heads of dS (head order, mha_dbias_kernel's order)
@@ -864,22 +870,22 @@ __global__ __launch_bounds__(512) void xh_wgrad_kernel(const WgTab tab, float* _
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   float bsum = 0.f;  // column n0 + col, this thread's rows
-  const long nchunk = (m1 - m0 + 31) / 32, iters = (nchunk + 1) / 2;
-  // chunk i of this group starts at row m0 + 32 * (2i + grp); a group past the range loads an empty range
-  // (m >= m1 everywhere: zeros), so both groups run the same iterations and barriers
+  const long nchunk = (m1 - m0 + 31) / 32, iters = ((nchunk + 1) / 2 + 1) / 2 * 2;  // even: two buffers
+  // chunk i of this group starts at row m0 + 32 * (2i + grp); a chunk past the range loads an empty range
+  // (m >= m1 everywhere: zeros), so both groups run the same iterations and barriers.  Two chunks are in
+  // flight (buffers c0 / c1, loop unrolled by two so no register copy waits on a load), and the barriers are
+  // LDS-only: __syncthreads' release fence would wait for the prefetch at every iteration.
   auto chunk_row = [&](long i) { return m0 + 32 * (2 * i + grp); };
   XT(1, 0);
-  WgChunk cur;
-  wg_load(d, chunk_row(0), m1, n0, k0, cur);
-  for (long it = 0; it < iters; ++it) {
-    __syncthreads();  // the previous chunk's fragments are read
+  auto step = [&](WgChunk& c, long it) {
+    lds_sync();  // the previous chunk's fragments are read
 #pragma unroll
-    for (int e = 0; e < 16; ++e) bsum += cur.y[e];
-    wg_store_planes(cur.y, yh + col * WG_LDM + m16, yl + col * WG_LDM + m16);
-    wg_store_planes(cur.x, xh_ + col * WG_LDM + m16, xl + col * WG_LDM + m16);
-    __syncthreads();
-    // the next chunk's loads are in flight during the MFMAs (past the end: the current chunk again, unused)
-    wg_load(d, it + 1 < iters ? chunk_row(it + 1) : chunk_row(it), m1, n0, k0, cur);
+    for (int e = 0; e < 16; ++e) bsum += c.y[e];
+    wg_store_planes(c.y, yh + col * WG_LDM + m16, yl + col * WG_LDM + m16);
+    wg_store_planes(c.x, xh_ + col * WG_LDM + m16, xl + col * WG_LDM + m16);
+    lds_sync();
+    // chunk it + 2 into the buffer just consumed (past the end: an empty range, unused)
+    wg_load(d, chunk_row(it + 2 < iters ? it + 2 : iters), m1, n0, k0, c);
     Frag BH[4], BL[4];  // B[k][m] = X[m][k]; the lo plane of bf16 X is zero
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -899,6 +905,13 @@ __global__ __launch_bounds__(512) void xh_wgrad_kernel(const WgTab tab, float* _
       }
     }
     if (it < 4) XT(1, 1 + it);
+  };
+  WgChunk c0, c1;
+  wg_load(d, chunk_row(0), m1, n0, k0, c0);
+  wg_load(d, chunk_row(1), m1, n0, k0, c1);
+  for (long it = 0; it < iters; it += 2) {
+    step(c0, it);
+    step(c1, it + 1);
   }
   bred[grp * 2 + (t >> 7)][col] = bsum;
   __syncthreads();  // every group is past its last fragment read: the planes take group 1's partial
@@ -912,23 +925,52 @@ __global__ __launch_bounds__(512) void xh_wgrad_kernel(const WgTab tab, float* _
   }
   __syncthreads();
   XT(1, 5);
+  // group 0 adds group 1's partial (fixed order) and the sum goes back through LDS as a row-major tile, so the
+  // slab is written with 16-byte stores of whole row segments: the MFMA-layout stores (4 rows x 64 bytes per
+  // instruction) drained at ~1.2 TB/s after the blocks' last phase (~13 us of a 37 us launch at B = 32)
+  constexpr int TLD = WG_T + 4;  // [128][132] fp32 = 66 KiB of the 80 KiB planes
+  float* tileL = xch;
+  f32x4 sum[4][4];
   if (grp == 0) {
-    if (K > 0) {
-      float* out = ws + d.ws_off + (long)split * N * K;
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const f32x4 o = *reinterpret_cast<const f32x4*>(xch + ((i * 4 + j) * 256 + t) * 4);
+      for (int j = 0; j < 4; ++j) {
+        const f32x4 o = *reinterpret_cast<const f32x4*>(xch + ((i * 4 + j) * 256 + t) * 4);
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int n = n0 + 64 * wn + 16 * i + 4 * (lane >> 4) + r, k = k0 + 64 * wk + 16 * j + fr;
-            if (n < N && k < K) out[(long)n * K + k] = acc[i][j][r] + o[r];
-          }
-        }
+        for (int r = 0; r < 4; ++r) sum[i][j][r] = acc[i][j][r] + o[r];
+      }
+  }
+  __syncthreads();  // the exchange is read: the tile overwrites it
+  if (grp == 0 && K > 0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          tileL[(64 * wn + 16 * i + 4 * (lane >> 4) + r) * TLD + 64 * wk + 16 * j + fr] = sum[i][j][r];
+  }
+  if (grp == 0 && bias && t < WG_T && n0 + t < N)
+    ws[d.ws_b_off + (long)split * N + n0 + t] = (bred[0][t] + bred[1][t]) + (bred[2][t] + bred[3][t]);
+  __syncthreads();
+  if (K > 0) {
+    float* out = ws + d.ws_off + (long)split * N * K;
+    const int c4 = 4 * (threadIdx.x & 31), k = k0 + c4;
+#pragma unroll
+    for (int q = 0; q < WG_T / 16; ++q) {
+      const int rl = (threadIdx.x >> 5) + 16 * q, n = n0 + rl;
+      if (n >= N || k >= K) continue;
+      const f32x4 v = *reinterpret_cast<const f32x4*>(tileL + rl * TLD + c4);
+      float* dst = out + (long)n * K + k;
+      if (k + 3 < K && ((uintptr_t)dst & 15) == 0) {
+        *reinterpret_cast<f32x4*>(dst) = v;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (k + e < K) dst[e] = v[e];
+      }
     }
-    if (bias && t < WG_T && n0 + t < N)
-      ws[d.ws_b_off + (long)split * N + n0 + t] = (bred[0][t] + bred[1][t]) + (bred[2][t] + bred[3][t]);
   }
   XT(1, 6);
 }

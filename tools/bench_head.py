@@ -19,12 +19,16 @@ def main():
     ap.add_argument("--head", default="concat")
     ap.add_argument("--train", type=int, default=1)
     ap.add_argument("--f1-pair", type=int, default=1)
+    ap.add_argument("--wgrad-rows", type=int, default=0)
+    ap.add_argument("--fused-only", type=int, default=0)
     args = ap.parse_args()
     from multimodalemotionrecognition_amd import xattn_fused as XF
     from multimodalemotionrecognition_amd import xattn_head as XH
     from multimodalemotionrecognition_amd.fusion import _head_grads
     from tests.gpu_helpers import feats, head_model
     XF.F1_PAIR = bool(args.f1_pair)
+    if args.wgrad_rows:
+        XF.WGRAD_ROWS = args.wgrad_rows
 
     m = head_model(args.head, False).train(bool(args.train))
     names, params = m.head_params()
@@ -36,7 +40,7 @@ def main():
     grads = {n: torch.zeros_like(t) for n, t in _head_grads(p, set(XH.used_param_names(cfg))).items()}
     dl = torch.from_numpy(np.random.default_rng(1).standard_normal((32, 8)).astype(np.float32)).cuda()
     res = {}
-    for fused in (False, True):
+    for fused in ((True,) if args.fused_only else (False, True)):
         XF.ENABLED = fused
 
         def step():
