@@ -650,25 +650,39 @@ __global__ __launch_bounds__(256) void xh_v2a_post_kernel(
   const int b = blockIdx.x, w = threadIdx.x >> 6;
   const long row0 = (long)b * T;
   const unsigned long long seed_path = mer_site_seed(dr.seed, dr.site_path);
+  // every weight fragment of both products first (registers), then the rows: one memory latency for all
+  WRegs<XD / 32, 2> wo;
+  wregs_load(wo, Wo1, XD, 32 * w, XD / 32);
+  WRegs<XD / 32, 4> wkv;
+  wregs_load(wkv, Wkv2, XD, 64 * w, XD / 32);
+  {
+    f32x4 xv[16 * XD / 4 / 256], xo[16 * XD / 4 / 256];
 #pragma unroll
-  for (int e = threadIdx.x; e < 16 * XD; e += 256) {
-    const int r = e / XD, c = e - r * XD;
-    const long rc = row0 + (r < T ? r : T - 1);
-    const float xv = v[rc * XD + c], xo = o1[rc * XD + c];
-    vL[r * LDA + c] = r < T ? xv : 0.f;
-    oL[r * LDA + c] = r < T ? xo : 0.f;
+    for (int q = 0; q < 16 * XD / 4 / 256; ++q) {
+      const int e = threadIdx.x + 256 * q, r = e / (XD / 4), c = 4 * (e % (XD / 4));
+      const long rc = row0 + (r < T ? r : T - 1);
+      xv[q] = *reinterpret_cast<const f32x4*>(v + rc * XD + c);
+      xo[q] = *reinterpret_cast<const f32x4*>(o1 + rc * XD + c);
+    }
+#pragma unroll
+    for (int q = 0; q < 16 * XD / 4 / 256; ++q) {
+      const int e = threadIdx.x + 256 * q, r = e / (XD / 4), c = 4 * (e % (XD / 4));
+      const f32x4 z = f32x4{0.f, 0.f, 0.f, 0.f};
+      *reinterpret_cast<f32x4*>(vL + r * LDA + c) = r < T ? xv[q] : z;
+      *reinterpret_cast<f32x4*>(oL + r * LDA + c) = r < T ? xo[q] : z;
+    }
   }
-  __syncthreads();
+  lds_sync();
   {  // v2 = o Wo1^T + bo1
     f32x4 acc[1][2];
     zero(acc);
-    mm_aw<1, 2, 3, XD>(acc, oL, LDA, 16, XD, Wo1, XD, 32 * w);
+    mm_lw<1, 2, XD / 32>(acc, oL, LDA, wo);
     store_acc(acc, 32 * w, bo1, tL, LDA, nullptr, 0, 0, 16);
   }
-  __syncthreads();
+  lds_sync();
   // v1 = LN(v + keep_b * v2)  (StochasticDepth: one keep draw per sample, fusion.py:11-26)
   add_ln_rows(T, vL, tL, dropout_scale(seed_path, b, dr.path), gamma, beta, oL, s_v, mean_v, rstd_v, row0);
-  __syncthreads();
+  lds_sync();
   for (int e = threadIdx.x; e < T * XD; e += 256) v1[row0 * XD + e] = oL[(e / XD) * LDA + e % XD];
   for (int e = threadIdx.x; e < (16 - T) * XD; e += 256) oL[(T + e / XD) * LDA + e % XD] = 0.f;
   if (threadIdx.x < XD) {  // mean temporal pool of v1 (temporal.py:108-109) -> emb[b, 0:d]
@@ -676,11 +690,11 @@ __global__ __launch_bounds__(256) void xh_v2a_post_kernel(
     for (int r = 0; r < T; ++r) s += oL[r * LDA + threadIdx.x];
     emb[(long)b * ld_emb + threadIdx.x] = s / T;
   }
-  __syncthreads();
+  lds_sync();
   {  // [k2 v2] = v1 Wkv2^T + bkv2: 256 columns, 64 per wave
     f32x4 acc[1][4];
     zero(acc);
-    mm_aw<1, 4, 3, XD>(acc, oL, LDA, 16, XD, Wkv2, XD, 64 * w);
+    mm_lw<1, 4, XD / 32>(acc, oL, LDA, wkv);
     store_acc(acc, 64 * w, bkv2, nullptr, 0, kv2, 2 * XD, row0, T);
   }
 }
@@ -746,7 +760,7 @@ __global__ __launch_bounds__(256) void xh_a2v_fwd_kernel(int T, int Ta, int ntil
     const int e = threadIdx.x + 256 * q, r = e / (XD / 4), c = 4 * (e % (XD / 4));
     *reinterpret_cast<f32x4*>(aL + r * LDA + c) = r < nr ? ar[q] : f32x4{0.f, 0.f, 0.f, 0.f};
   }
-  __syncthreads();
+  lds_sync();
   for (int e = threadIdx.x; e < nr * XD; e += 256) o2[row0 * XD + e] = oL[(e / XD) * LDA + e % XD];
   {  // a2 = o Wo2^T + bo2
     f32x4 acc[1][2];
@@ -754,9 +768,9 @@ __global__ __launch_bounds__(256) void xh_a2v_fwd_kernel(int T, int Ta, int ntil
     mm_lw<1, 2, XD / 32>(acc, oL, LDA, wo);
     store_acc(acc, 32 * w, bo2, tL, LDA, nullptr, 0, 0, 16);
   }
-  __syncthreads();
+  lds_sync();
   add_ln_rows(nr, aL, tL, dropout_scale(seed_path, b, dr.path), gamma, beta, oL, s_a, mean_a, rstd_a, row0);
-  __syncthreads();
+  lds_sync();
   if (threadIdx.x < XD) {  // this tile's column sums of a1 (the a-side mean pool, folded in tile order by F4)
     float s = 0.f;
     for (int r = 0; r < nr; ++r) s += oL[r * LDA + threadIdx.x];

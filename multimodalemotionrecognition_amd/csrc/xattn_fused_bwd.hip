@@ -46,7 +46,7 @@ __device__ __forceinline__ void ln_part_store(float g0, float g1, float b0, floa
   red[w * 256 + 64 + lane] = g1;
   red[w * 256 + 128 + lane] = b0;
   red[w * 256 + 192 + lane] = b1;
-  __syncthreads();
+  lds_sync();
   if (threadIdx.x < 256) {
     float s = 0.f;
     for (int q = 0; q < 4; ++q) s += red[q * 256 + threadIdx.x];
@@ -194,6 +194,8 @@ __global__ __launch_bounds__(256) void xh_a2v_bwd_kernel(
   const unsigned long long seed_attn = mer_site_seed(dr.seed, dr.site_attn);
   const unsigned long long seed_path = mer_site_seed(dr.seed, dr.site_path);
   const float keep = dropout_scale(seed_path, b, dr.path);
+  WRegs<XD / 32, 2> wo;  // do2's weight fragments first: their latency overlaps the LayerNorm backward
+  wregs_load(wo, WoT2, XD, 32 * w, XD / 32);
   {  // a-pool (mean over Ta) + LayerNorm backward; da = ds (residual), da2 = keep * ds
     float g0 = 0.f, g1 = 0.f, b0 = 0.f, b1 = 0.f;
     const float dy0 = demb[(long)b * 2 * XD + XD + lane] / Ta, dy1 = demb[(long)b * 2 * XD + XD + 64 + lane] / Ta;
@@ -212,14 +214,14 @@ __global__ __launch_bounds__(256) void xh_a2v_bwd_kernel(
     }
     ln_part_store(g0, g1, b0, b1, red, ln_part + (long)blockIdx.x * 256);
   }
-  __syncthreads();
+  lds_sync();
   {  // do2 = da2 . Wo2
     f32x4 acc[1][2];
     zero(acc);
-    mm_aw<1, 2, 3, XD>(acc, d2L, LDA, 16, XD, WoT2, XD, 32 * w);
+    mm_lw<1, 2, XD / 32>(acc, d2L, LDA, wo);
     store_acc(acc, 32 * w, nullptr, oL, LDA, nullptr, 0, 0, 16);
   }
-  __syncthreads();
+  lds_sync();
   XT(3, 1);
   // attention backward of head h = w over the sample's T keys
   const int h = w;
@@ -357,29 +359,50 @@ __global__ __launch_bounds__(256) void xh_v2a_pre_bwd_kernel(
   const long row0 = (long)b * T;
   const unsigned long long seed_path = mer_site_seed(dr.seed, dr.site_path);
   const float keep = dropout_scale(seed_path, b, dr.path);
-  // dK2 dV2 of this sample: the a2v tiles' partials summed in tile order
-#pragma unroll 4
-  for (int e = threadIdx.x; e < 16 * 2 * XD; e += 256) {
-    const int r = e / (2 * XD), c = e - r * 2 * XD;
-    float s = 0.f;
-    if (r < T) {
+  // both products' weight fragments first (registers): their latency overlaps the fold below
+  WRegs<2 * XD / 32, 2> wkv;
+  wregs_load(wkv, WkvT2, 2 * XD, 32 * w, 2 * XD / 32);
+  WRegs<XD / 32, 2> wo;
+  wregs_load(wo, WoT1, XD, 32 * w, XD / 32);
+  // dK2 dV2 of this sample: the a2v tiles' partials summed in tile order; thread = one of the 256 columns, rows
+  // in groups of 8 with every load of a group in flight at once (T is block-uniform: whole groups are skipped)
+  {
+    const int c = threadIdx.x;
 #pragma unroll
-      for (int q = 0; q < G2_KT; ++q) {
-        const float x = dkv2_part[(((long)b * ntiles + (q < ntiles ? q : ntiles - 1)) * 16 + r) * 2 * XD + c];
-        s += q < ntiles ? x : 0.f;
+    for (int rb = 0; rb < 16; rb += 8) {
+      if (rb < T) {
+        float x[8][G2_KT];
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+          for (int q = 0; q < G2_KT; ++q) {
+            const int rc = rb + i < T ? rb + i : T - 1, qc = q < ntiles ? q : ntiles - 1;
+            x[i][q] = dkv2_part[(((long)b * ntiles + qc) * 16 + rc) * 2 * XD + c];
+          }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int r = rb + i;
+          float sum = 0.f;
+#pragma unroll
+          for (int q = 0; q < G2_KT; ++q) sum += q < ntiles ? x[i][q] : 0.f;
+          sum = r < T ? sum : 0.f;
+          if (r < T) dkv2[(row0 + r) * 2 * XD + c] = sum;
+          kvL[r * G2_KVLD + c] = sum;
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) kvL[(rb + i) * G2_KVLD + c] = 0.f;
       }
-      dkv2[(row0 + r) * 2 * XD + c] = s;
     }
-    kvL[r * G2_KVLD + c] = s;
   }
-  __syncthreads();
+  lds_sync();
   {  // dv1 (kv2 path) = [dK2 dV2] . Wkv2
     f32x4 acc[1][2];
     zero(acc);
-    mm_aw<1, 2, 3, 2 * XD>(acc, kvL, G2_KVLD, 16, 2 * XD, WkvT2, 2 * XD, 32 * w);
+    mm_lw<1, 2, 2 * XD / 32>(acc, kvL, G2_KVLD, wkv);
     store_acc(acc, 32 * w, nullptr, t1, LDA, nullptr, 0, 0, 16);
   }
-  __syncthreads();
+  lds_sync();
   {  // + v-pool (mean over T); LayerNorm backward; t1 = ds (dv residual), dv2 = keep * ds
     float g0 = 0.f, g1 = 0.f, b0 = 0.f, b1 = 0.f;
     const float pv0 = demb[(long)b * 2 * XD + lane] / T, pv1 = demb[(long)b * 2 * XD + 64 + lane] / T;
@@ -399,11 +422,11 @@ __global__ __launch_bounds__(256) void xh_v2a_pre_bwd_kernel(
     }
     ln_part_store(g0, g1, b0, b1, red, ln_part + (long)b * 256);
   }
-  __syncthreads();
+  lds_sync();
   {  // do1 = dv2 . Wo1
     f32x4 acc[1][2];
     zero(acc);
-    mm_aw<1, 2, 3, XD>(acc, d2L, LDA, 16, XD, WoT1, XD, 32 * w);
+    mm_lw<1, 2, XD / 32>(acc, d2L, LDA, wo);
     store_acc(acc, 32 * w, nullptr, nullptr, 0, do1, XD, row0, T);
   }
 }
