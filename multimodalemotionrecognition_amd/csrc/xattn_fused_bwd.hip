@@ -812,31 +812,48 @@ struct WgTab {
 // one n / k).  The next chunk's loads are issued before the current chunk's MFMAs.
 constexpr int WG_LDM = 32 + 8;  // bf16 row stride of the [128][32] planes (80 bytes: 16-byte aligned)
 
-struct WgChunk {
-  float y[16], x[16];
+struct WgChunk {  // raw loads: decoded (dtype, bounds) only when the chunk is consumed
+  float y[16];
+  uint32_t xw[16];
 };
 
+// Branch-free (see mm_aw): unconditional loads from clamped addresses (row m1 - 1, column N - 1 / K - 1); X is
+// read as 32-bit words whatever its dtype (a bf16 element is one half of its word), and a K = 0 problem reads a
+// valid dummy X (the host points X at dY).  Nothing here uses the loaded values, so the loads stay in flight
+// until wg_decode (decoding at load time made every load wait for itself).
 __device__ __forceinline__ void wg_load(const WgProb& d, long mc, long m1, int n0, int k0, WgChunk& c) {
-  // Branch-free (see mm_aw): unconditional loads from clamped addresses (row m1 - 1, column N - 1 / K - 1),
-  // zeroed by selects; X is read as 32-bit words whatever its dtype (a bf16 element is one half of its word),
-  // and a K = 0 problem reads a valid dummy X (the host points X at dY).
   const int col = threadIdx.x & 127, m16 = ((threadIdx.x >> 7) & 1) * 16;  // (each 256-thread group stages a chunk)
-  const bool okn = n0 + col < d.N, okk = k0 + col < d.K;
-  const int nc = okn ? n0 + col : d.N - 1, kc = okk ? k0 + col : (d.K > 0 ? d.K - 1 : 0);
+  const int nc = n0 + col < d.N ? n0 + col : d.N - 1, kc = k0 + col < d.K ? k0 + col : (d.K > 0 ? d.K - 1 : 0);
   const int esz = d.xbf ? 2 : 4;
   const char* Xb = reinterpret_cast<const char*>(d.X);
 #pragma unroll
   for (int e = 0; e < 16; ++e) {
-    const long m = mc + m16 + e;
+    const long m = mc + m16 + e, mm = m < m1 ? m : m1 - 1;
+    c.y[e] = d.dY[mm * d.ldy + nc];
+    const uintptr_t addr = reinterpret_cast<uintptr_t>(Xb + (mm * d.ldx + kc) * esz);
+    // an integer-derived pointer would be a FLAT access (LDS or global: every flat load waits for itself and
+    // for LDS traffic); the global address space keeps these ordinary pipelined loads
+    c.xw[e] = *(const __attribute__((address_space(1))) uint32_t*)(addr & ~(uintptr_t)3);
+  }
+}
+
+// zero the out-of-range elements, take the bf16 half of X's words
+__device__ __forceinline__ void wg_decode(const WgProb& d, long mc, long m1, int n0, int k0, WgChunk& c,
+                                          float (&x)[16]) {
+  const int col = threadIdx.x & 127, m16 = ((threadIdx.x >> 7) & 1) * 16;
+  const bool okn = n0 + col < d.N, okk = k0 + col < d.K;
+  const int kc = okk ? k0 + col : (d.K > 0 ? d.K - 1 : 0);
+  const int esz = d.xbf ? 2 : 4;
+  const uintptr_t xb = reinterpret_cast<uintptr_t>(d.X);
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const long m = mc + m16 + e, mm = m < m1 ? m : m1 - 1;
     const bool okm = m < m1;
-    const long mm = okm ? m : m1 - 1;
-    const float y = d.dY[mm * d.ldy + nc];
-    const long ie = mm * d.ldx + kc;
-    const uintptr_t addr = reinterpret_cast<uintptr_t>(Xb + ie * esz);
-    const uint32_t wv = *reinterpret_cast<const uint32_t*>(addr & ~(uintptr_t)3);
+    const uintptr_t addr = xb + (mm * d.ldx + kc) * esz;
+    const uint32_t wv = c.xw[e];
     const uint32_t bits = d.xbf ? ((addr & 2) ? (wv & 0xffff0000u) : (wv << 16)) : wv;
-    c.y[e] = (okm && okn) ? y : 0.f;
-    c.x[e] = (okm && okk) ? __uint_as_float(bits) : 0.f;
+    c.y[e] = (okm && okn) ? c.y[e] : 0.f;
+    x[e] = (okm && okk) ? __uint_as_float(bits) : 0.f;
   }
 }
 
@@ -902,10 +919,12 @@ __global__ __launch_bounds__(512) void xh_wgrad_kernel(const WgTab tab, float* _
   XT(1, 0);
   auto step = [&](WgChunk& c, long it) {
     lds_sync();  // the previous chunk's fragments are read
+    float xv[16];
+    wg_decode(d, chunk_row(it), m1, n0, k0, c, xv);
 #pragma unroll
     for (int e = 0; e < 16; ++e) bsum += c.y[e];
     wg_store_planes(c.y, yh + col * WG_LDM + m16, yl + col * WG_LDM + m16);
-    wg_store_planes(c.x, xh_ + col * WG_LDM + m16, xl + col * WG_LDM + m16);
+    wg_store_planes(xv, xh_ + col * WG_LDM + m16, xl + col * WG_LDM + m16);
     lds_sync();
     // chunk it + 2 into the buffer just consumed (past the end: an empty range, unused)
     wg_load(d, chunk_row(it + 2 < iters ? it + 2 : iters), m1, n0, k0, c);
