@@ -2147,20 +2147,31 @@ MER_API int mer_pack_conv_weights_flat(int n, const long long* desc, long total_
 // rows, unused rows zero) followed by 64 scratch rows.  Rows are summed in a fixed order: stage 1 (when
 // there are more than 64 rows) folds contiguous row groups into the 64 scratch rows, stage 2 folds <= 64
 // rows per channel -- deterministic whatever the tile size and block schedule were.
+// Latency: a block here is a short chain (one wave-row of loads, a sum, an LDS meet), so every load of a
+// thread's rows is issued before the first add (batches of 16 from clamped addresses, zero-selected) -- the
+// loop that added as it loaded waited one memory latency per two rows.  The sum order is unchanged: a0 takes
+// the thread's rows 0, 2, 4, ... and a1 rows 1, 3, 5, ... (rows r0 + pg + 4 i).
 __global__ __launch_bounds__(256) void bn_stat_rows_fold_kernel(int C2, int rows, int per, const float* __restrict__ in,
                                                                 float* __restrict__ out) {
   __shared__ float part[4][64];
   const int el = threadIdx.x & 63, pg = threadIdx.x >> 6;
   const int e = blockIdx.x * 64 + el, grp = blockIdx.y;
   const int r0 = grp * per, r1 = min(rows, r0 + per);
+  const int ec = e < C2 ? e : C2 - 1;
+  const int n = r1 - (r0 + pg) > 0 ? (r1 - (r0 + pg) + 3) / 4 : 0;  // this thread's rows
   float a0 = 0.f, a1 = 0.f;
-  if (e < C2) {
-    int r = r0 + pg;
-    for (; r + 4 < r1; r += 8) {
-      a0 += in[(long)r * C2 + e];
-      a1 += in[(long)(r + 4) * C2 + e];
+  for (int i0 = 0; i0 < n; i0 += 16) {
+    float x[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int r = r0 + pg + 4 * (i0 + i);
+      x[i] = in[(long)(r < r1 ? r : r1 - 1) * C2 + ec];
     }
-    if (r < r1) a0 += in[(long)r * C2 + e];
+#pragma unroll
+    for (int i = 0; i < 16; i += 2) {
+      if (i0 + i < n) a0 += x[i];
+      if (i0 + i + 1 < n) a1 += x[i + 1];
+    }
   }
   part[pg][el] = a0 + a1;
   __syncthreads();
@@ -2183,12 +2194,21 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(int C, long M, int row
     return;
   }
   float sum = 0.f, sq = 0.f;
-  if (c < C) {
-#pragma unroll 4
-    for (int p = pg; p < rows; p += 4) {
-      sum += stats[(long)p * 2 * C + 2 * c];
-      sq += stats[(long)p * 2 * C + 2 * c + 1];
+  {  // rows <= 64: this wave's <= 16 rows all in flight before the first add (same order)
+    const int cc = c < C ? c : C - 1;
+    float xs[16], xq[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int p = pg + 4 * i, pc = p < rows ? p : rows - 1;
+      xs[i] = stats[(long)pc * 2 * C + 2 * cc];
+      xq[i] = stats[(long)pc * 2 * C + 2 * cc + 1];
     }
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      if (pg + 4 * i < rows) {
+        sum += xs[i];
+        sq += xq[i];
+      }
   }
   part[pg][cl][0] = sum;
   part[pg][cl][1] = sq;
@@ -2414,9 +2434,17 @@ __global__ __launch_bounds__(256) void partials_sum_kernel(int C, int parts, con
   const int el = threadIdx.x & 63, pg = threadIdx.x >> 6;
   const int e = blockIdx.x * 64 + el;
   float acc = 0.f;
-  if (e < 2 * C) {
-#pragma unroll 4
-    for (int p = pg; p < parts; p += 4) acc += in[(long)p * 2 * C + e];
+  {  // parts <= 64: this wave's <= 16 rows all in flight before the first add (same order)
+    const int ec = e < 2 * C ? e : 2 * C - 1;
+    float x[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int p = pg + 4 * i;
+      x[i] = in[(long)(p < parts ? p : parts - 1) * 2 * C + ec];
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      if (pg + 4 * i < parts) acc += x[i];
   }
   part[pg][el] = acc;
   __syncthreads();
