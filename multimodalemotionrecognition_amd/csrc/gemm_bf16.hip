@@ -234,6 +234,29 @@ __device__ __forceinline__ int ktile_off_k(const GemmArgs& g, int u) {
 }
 
 
+// Phase timestamps of the pipelined GEMM (tools/gemm_phases.py builds a separate library with
+// -DMER_GEMM_TIMING; the production library compiles GT() to nothing): wall_clock64() of workgroup blockIdx.x's
+// thread 0 at phase k.
+#ifdef MER_GEMM_TIMING
+static __device__ long long mer_gt_buf[1024 * 8];
+#define GT(k) \
+  do { \
+    if (threadIdx.x == 0 && blockIdx.x < 1024 && blockIdx.z == 0) mer_gt_buf[blockIdx.x * 8 + (k)] = wall_clock64(); \
+  } while (0)
+MER_API int mer_gt_reset() {
+  static long long zeros[1024 * 8];
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(mer_gt_buf), zeros, sizeof(zeros), 0, hipMemcpyHostToDevice);
+}
+MER_API int mer_gt_read(long long* host) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(mer_gt_buf), sizeof(long long) * 1024 * 8, 0,
+                                  hipMemcpyDeviceToHost);
+}
+#else
+#define GT(k) \
+  do { \
+  } while (0)
+#endif
+
 __device__ __attribute__((aligned(16))) uint32_t mer_gemm_zero16[4] = {0u, 0u, 0u, 0u};
 
 // AMODE 0: rows mode; AMODE 1: grouped positional conv (group = blockIdx.z), A chunks gathered per
@@ -242,6 +265,7 @@ template <class CF, typename TOUT, int AMODE>
 __global__ __launch_bounds__(CF::NT, 1) void gemm_pipe_kernel(GemmArgs g) {
   extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
   if (layer_skipped(g.skip_mask, g.skip_bit)) return;
+  GT(0);
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int z = blockIdx.z;
   const int nx = (g.N + CF::BN - 1) / CF::BN, ny = (g.M + CF::BM - 1) / CF::BM;
@@ -344,6 +368,7 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_pipe_kernel(GemmArgs g) {
     __builtin_amdgcn_s_waitcnt((15) | (7 << 4) | (0 << 8) | (3 << 14));  // lgkmcnt(0) only
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
+    if (kt == 0) GT(1);
     const bf16_t* la;
     const bf16_t* lb;
     if constexpr (SPLIT) {
@@ -379,6 +404,7 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_pipe_kernel(GemmArgs g) {
     }
   }
 
+  GT(2);
   TOUT* C = reinterpret_cast<TOUT*>(g.C) + (long)z * g.c_zoff;
   const unsigned long long dseed = mer_site_seed(g.drop_seed, g.drop_site);
   if (g.vec_epi) {
@@ -406,6 +432,18 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_pipe_kernel(GemmArgs g) {
     const int colv = n0 + wc * CF::TN + lc;
 #pragma unroll
     for (int i0 = 0; i0 < CF::FM; i0 += GI) {
+      // this pass's residual vectors first: their latency overlaps the staging writes (a load inside the store
+      // loop exposed it once per row group)
+      constexpr int NRR = (GI * 16 + RPP - 1) / RPP;
+      u32x4 rres[NRR];
+      if (g.R) {
+#pragma unroll
+        for (int q = 0; q < NRR; ++q) {
+          const int row = m0 + wr * CF::TM + i0 * 16 + q * RPP + lr;
+          const long rr = row < g.M ? row : g.M - 1;
+          rres[q] = *reinterpret_cast<const u32x4*>(g.R + rr * g.ldr + (long)z * g.c_zoff + (colv < g.N ? colv : 0));
+        }
+      }
 #pragma unroll
       for (int ii = 0; ii < GI; ++ii) {
         if (i0 + ii >= CF::FM) break;
@@ -430,7 +468,7 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_pipe_kernel(GemmArgs g) {
           if (g.drop_p > 0.f)  // N % 8 == 0 on this path: the 8 indices start even
             dropout_pairs<8>(v, dseed, (uint64_t)((long)row * g.N + colv), g.drop_p);
           if (g.R) {
-            const u32x4 rv = *reinterpret_cast<const u32x4*>(g.R + (long)row * g.ldr + (long)z * g.c_zoff + colv);
+            const u32x4 rv = rres[rr / RPP];
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
               v[2 * e] += __uint_as_float(rv[e] << 16);
@@ -444,6 +482,7 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_pipe_kernel(GemmArgs g) {
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
+    GT(3);
     return;
   }
 #pragma unroll
