@@ -30,22 +30,54 @@ using namespace xh;
 // hi / lo (bf16) = split(src) in the same layout (trans 0, dst contiguous) or transposed (trans 1:
 // dst[c * dst_ld + r], the [in][out] planes the backward's data-gradient products read)
 // ---------------------------------------------------------------------------------------------
-__global__ void xh_split_kernel(const long long* __restrict__ desc) {
+__global__ __launch_bounds__(256) void xh_split_kernel(const long long* __restrict__ desc) {
+  __shared__ float tileL[32][33];
   const long long* d = desc + 7 * blockIdx.y;
-  const float* src = reinterpret_cast<const float*>(d[0]);
-  bf16_t* hi = reinterpret_cast<bf16_t*>(d[1]);
-  bf16_t* lo = reinterpret_cast<bf16_t*>(d[2]);
-  // 32-bit index math (the head's weights: well below 2^31 elements): a 64-bit division per
-  // element was most of this kernel's time
+  // pointers read from a table are FLAT accesses unless typed global (a flat access also waits for LDS traffic)
+  typedef __attribute__((address_space(1))) const float gcf;
+  typedef __attribute__((address_space(1))) bf16_t gbf;
+  gcf* src = (gcf*)(d[0]);
+  gbf* hi = (gbf*)(d[1]);
+  gbf* lo = (gbf*)(d[2]);
+  // 32-bit index math (the head's weights: well below 2^31 elements)
   const unsigned rows = (unsigned)d[3], cols = (unsigned)d[4], n = rows * cols, dld = (unsigned)d[6];
-  const bool trans = d[5] != 0;
-  for (unsigned e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
-    const float x = src[e];
-    const bf16_t h = f2bf(x);
-    const unsigned q = e / cols;
-    const unsigned o = trans ? (e - q * cols) * dld + q : e;
-    hi[o] = h;
-    lo[o] = f2bf(x - bf2f(h));
+  auto split1 = [](float x, bf16_t& h, bf16_t& l) {
+    h = f2bf(x);
+    l = f2bf(x - bf2f(h));
+  };
+  if (d[5] == 0) {  // same layout: element e
+    for (unsigned e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
+      bf16_t h, l;
+      split1(src[e], h, l);
+      hi[e] = h;
+      lo[e] = l;
+    }
+    return;
+  }
+  // transposed (dst[c * dld + r]): 32 x 32 tiles through LDS, so both the source rows and the destination rows
+  // are read / written contiguously (the element-wise form wrote 2 bytes per lane to 64 different rows)
+  const unsigned tr = (rows + 31) / 32, tc = (cols + 31) / 32;
+  const int t = threadIdx.x, ty = t >> 3, tx = (t & 7) * 4;
+  for (unsigned tile = blockIdx.x; tile < tr * tc; tile += gridDim.x) {
+    const unsigned r0 = (tile / tc) * 32, c0 = (tile % tc) * 32;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const unsigned r = r0 + ty, c = c0 + tx + e;
+      tileL[ty][tx + e] = (r < rows && c < cols) ? src[r * cols + c] : 0.f;
+    }
+    __syncthreads();
+    const unsigned c = c0 + ty;  // destination row
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const unsigned r = r0 + tx + e;
+      if (c < cols && r < rows) {
+        bf16_t h, l;
+        split1(tileL[tx + e][ty], h, l);
+        hi[c * dld + r] = h;
+        lo[c * dld + r] = l;
+      }
+    }
+    __syncthreads();
   }
 }
 
@@ -889,15 +921,24 @@ __global__ __launch_bounds__(256) void xh_mlp_fwd_kernel(int Ta, int ntiles, int
     eL[t] = val;
   }
   __syncthreads();
-  // h = dropout(relu(emb W0^T + b0)): wave w takes the 8-row groups w, w + 4, ...
-  for (int g = w; 8 * g < H1; g += 4) {
-    const float s = dot_rows8<4>(W0, 2 * XD, H1, 8 * g, eL);
-    const int r = 8 * g + sub;
-    if ((lane & 7) == 0 && r < H1) {
-      float hv = s + b0[r];
-      hv = (hv > 0.f ? hv : 0.f) * dropout_scale(seed, (uint64_t)((long)b * H1 + r), mlp_p);
-      hL[r] = hv;
-      hsave[(long)b * H1 + r] = hv;
+  // h = dropout(relu(emb W0^T + b0)): wave w takes the 8-row groups w, w + 4, ..., four groups' weight rows in
+  // flight at once (a group at a time waited one L2 round trip per 8 rows: 8 per wave at H1 = 256)
+  for (int g0 = w; 8 * g0 < H1; g0 += 16) {
+    float sv[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int g = g0 + 4 * q;
+      sv[q] = dot_rows8<4>(W0, 2 * XD, H1, 8 * (8 * g < H1 ? g : g0), eL);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int g = g0 + 4 * q, r = 8 * g + sub;
+      if ((lane & 7) == 0 && 8 * g < H1 && r < H1) {
+        float hv = sv[q] + b0[r];
+        hv = (hv > 0.f ? hv : 0.f) * dropout_scale(seed, (uint64_t)((long)b * H1 + r), mlp_p);
+        hL[r] = hv;
+        hsave[(long)b * H1 + r] = hv;
+      }
     }
   }
   for (int r = H1 + t; r < 256; r += 256) hL[r] = 0.f;  // (H1 % 4 == 0: the k-split reads whole float4)
