@@ -921,7 +921,8 @@ __device__ __forceinline__ void conv_epilogue_prefetch(const ConvGeom& g, EpiPre
   }
 }
 
-template <bool DGRAD, int FM, int FN, int WM, int WN, int WAVE_FLOATS, class OutRow, class Pre = EpiNone>
+template <bool DGRAD, int FM, int FN, int WM, int WN, int WAVE_FLOATS, class OutRow, class Pre = EpiNone,
+          bool DEFER = false, bool X2 = true>
 __device__ __forceinline__ void conv_epilogue_vec(const ConvGeom& g, f32x4 (&acc)[FM][FN], float* smemf, int w,
                                                   int lane, int m0, int n0, int M, long red_row_id, long stat_row,
                                                   OutRow out_row, const Pre* pre = nullptr, int ct_slot = -1) {
@@ -938,12 +939,14 @@ __device__ __forceinline__ void conv_epilogue_vec(const ConvGeom& g, f32x4 (&acc
   const int colv = n0 + wc * TN + lc;
   const bool cok = colv < g.Ncols;
   const bool do_bnr = DGRAD && g.bnr_red != nullptr;
-  const bool has_x2 = do_bnr && g.bnr_x2 != nullptr;
+  const bool has_x2 = X2 && do_bnr && g.bnr_x2 != nullptr;  // X2 = false: compiled out (24 VGPRs)
   float mu[8], rs[8], mu2[8], rs2[8];
   float sA[8], sB[8], sC[8];
-  // the 16-byte output stores are issued LAST, after the cross-wave reductions: a wave stalled issuing stores would
-  // otherwise hold every other wave at the reductions' barriers (the store queue drains ~16 B/clk per CU)
-  constexpr int NPS = E::NP;
+  // DEFER (the halo kernel): the 16-byte output stores are issued LAST, after the cross-wave reductions -- a wave
+  // stalled issuing stores would otherwise hold every other wave at the reductions' barriers (the store queue
+  // drains ~16 B/clk per CU).  The deferred stores hold ~40 VGPRs, which cost conv_pipe_kernel's 8-wave dgrad
+  // tiles their second block per CU (127 -> 150 VGPRs: layer2's dgrads 37 -> 56 us), so it stores per pass.
+  constexpr int NPS = DEFER ? E::NP : 1;
   u32x4 pend[NPS];
   long pend_at[NPS];
   bool pend_ok[NPS];
@@ -1016,9 +1019,13 @@ __device__ __forceinline__ void conv_epilogue_vec(const ConvGeom& g, f32x4 (&acc
           oh[e] = f2bf(v[e]);
           v[e] = bf2f(oh[e]);  // the stored value feeds the reductions
         }
-        pend[q] = ov;
-        pend_at[q] = e0;
-        pend_ok[q] = true;
+        if constexpr (DEFER) {
+          pend[q] = ov;
+          pend_at[q] = e0;
+          pend_ok[q] = true;
+        } else {
+          *reinterpret_cast<u32x4*>(g.Y + e0) = ov;
+        }
         if (do_bnr) {
           u32x4 mv, xv, x2v;
           if constexpr (PREF) {
@@ -1118,7 +1125,7 @@ __device__ __forceinline__ void conv_epilogue_vec(const ConvGeom& g, f32x4 (&acc
 // STAGES-deep LDS ring (cdna_hip_programming.md "Pipelining across barriers"): tiles kt+1 .. kt+STAGES-2 stay
 // in flight across the barrier that publishes tile kt (counted vmcnt, raw s_barrier); the barrier also retires
 // every wave's reads of tile kt-1, whose buffer the DMA of tile kt+STAGES-1 then reuses.
-template <bool DGRAD, bool PAR, int BM_, int BN_, int WM = 2, int WN = 2, int STAGES = 2, int KS = 64>
+template <bool DGRAD, bool PAR, int BM_, int BN_, int WM = 2, int WN = 2, int STAGES = 2, int KS = 64, bool X2 = true>
 __global__ __launch_bounds__(64 * WM * WN, WM * WN >= 16 ? 1 : 2) void conv_pipe_kernel(ConvGeom g) {  // 16 waves: 1 block / CU (2 would spill to scratch)
   constexpr int WAVES = WM * WN;
   constexpr int CW = KS / 8, RPG = 64 / CW;  // 16-byte chunks per LDS row, rows per glds instruction
@@ -1278,7 +1285,7 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN >= 16 ? 1 : 2) void conv_pipe
     return row_id;
   };
   if (g.vec) {
-    conv_epilogue_vec<DGRAD, FM, FN, WM, WN, STAGES * BUF / 2 / WAVES>(
+    conv_epilogue_vec<DGRAD, FM, FN, WM, WN, STAGES * BUF / 2 / WAVES, decltype(out_row), EpiNone, false, X2>(
         g, acc, reinterpret_cast<float*>(smem), w, lane, m0, n0, M, (DGRAD && g.bnr_red) ? red_row() : 0l, ty, out_row);
     return;
   } else {
@@ -1388,6 +1395,19 @@ int launch_conv_pipe_t(ConvGeom& g, hipStream_t st) {
   const int Mg = PAR ? g.N * ((g.OH + 1) / 2) * ((g.OW + 1) / 2) : g.N * g.OH * g.OW;
   const long tiles = (long)((Mg + BM_ - 1) / BM_) * ((g.Ncols + BN_ - 1) / BN_);
   const size_t lds = STAGES * (BM_ + BN_) * KS * sizeof(bf16_t);
+  // a stride-1 input gradient whose BN-backward target has no second (downsample) branch runs the instantiation
+  // without the x2 terms: 24 fewer VGPRs, which keeps the 8-wave tiles at 2 blocks per CU
+  if constexpr (DGRAD && !PAR) {
+    if (!g.bnr_x2) {
+      if (hipFuncSetAttribute(
+              reinterpret_cast<const void*>(&conv_pipe_kernel<DGRAD, PAR, BM_, BN_, WM, WN, STAGES, KS, false>),
+              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+        return (int)hipErrorInvalidConfiguration;
+      hipLaunchKernelGGL((conv_pipe_kernel<DGRAD, PAR, BM_, BN_, WM, WN, STAGES, KS, false>), dim3((unsigned)tiles, 1),
+                         dim3(64 * WM * WN), lds, st, g);
+      return (int)hipGetLastError();
+    }
+  }
   if (hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_pipe_kernel<DGRAD, PAR, BM_, BN_, WM, WN, STAGES, KS>),
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return (int)hipErrorInvalidConfiguration;
@@ -1438,9 +1458,12 @@ int launch_conv_pipe(ConvGeom& g, hipStream_t st, int variant) {
       return small_m ? (PAR ? launch_conv_pipe_t<DGRAD, PAR, 64, 64, 2, 2>(g, st)
                             : launch_conv_pipe_t<DGRAD, PAR, 64, 64, 2, 2, 3>(g, st))
                      : launch_conv_pipe_t<DGRAD, PAR, 128, 64, 4, 2>(g, st);
-    return small_m ? (PAR ? launch_conv_pipe_t<DGRAD, PAR, 64, 128, 2, 4>(g, st)
-                          : launch_conv_pipe_t<DGRAD, PAR, 64, 128, 2, 4, 3>(g, st))
-                   : launch_conv_pipe_t<DGRAD, PAR, 128, 128, 2, 4>(g, st);
+    // a stride-1 input gradient with a second BN-backward branch (x2: the block-0 output of layers 2-4) needs 138
+    // VGPRs on the 128 x 128 tile (1 block per CU): it takes the 64 x 128 tile (115 VGPRs, 2 blocks per CU)
+    const bool x2_tile = DGRAD && !PAR && g.bnr_x2 != nullptr;
+    return (small_m || x2_tile) ? (PAR ? launch_conv_pipe_t<DGRAD, PAR, 64, 128, 2, 4>(g, st)
+                                       : launch_conv_pipe_t<DGRAD, PAR, 64, 128, 2, 4, 3>(g, st))
+                                : launch_conv_pipe_t<DGRAD, PAR, 128, 128, 2, 4>(g, st);
   }
   if (bn == 64)
     return small_m ? launch_conv_pipe_t<DGRAD, PAR, 64, 64>(g, st) : launch_conv_pipe_t<DGRAD, PAR, 128, 64>(g, st);
@@ -1622,11 +1645,12 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void conv_halo_kernel(ConvGeom g
     CT(it < 11 ? 4 + 5 * it : 63);
     const int ct_slot = it == 1 ? 60 : -1;  // (timing build: stamps inside the second tile's epilogue)
     if constexpr (DGRAD)
-      conv_epilogue_vec<DGRAD, FM, FN, WM, WN, EWF>(g, acc, reinterpret_cast<float*>(hb), w, lane, m0, 0, M, (long)tile,
-                                                    (long)tile, out_row, &pre, ct_slot);
+      conv_epilogue_vec<DGRAD, FM, FN, WM, WN, EWF, decltype(out_row), decltype(pre), true>(
+          g, acc, reinterpret_cast<float*>(hb), w, lane, m0, 0, M, (long)tile, (long)tile, out_row, &pre, ct_slot);
     else
-      conv_epilogue_vec<DGRAD, FM, FN, WM, WN, EWF>(g, acc, reinterpret_cast<float*>(hb), w, lane, m0, 0, M, (long)tile,
-                                                    (long)tile, out_row, static_cast<const EpiNone*>(nullptr), ct_slot);
+      conv_epilogue_vec<DGRAD, FM, FN, WM, WN, EWF, decltype(out_row), EpiNone, true>(
+          g, acc, reinterpret_cast<float*>(hb), w, lane, m0, 0, M, (long)tile, (long)tile, out_row,
+          static_cast<const EpiNone*>(nullptr), ct_slot);
     CT(it < 11 ? 5 + 5 * it : 63);
     lds_barrier();    // every wave is past its epilogue's use of hb before the DMA two tiles on refills it
     CT(it < 11 ? 6 + 5 * it : 63);

@@ -23,4 +23,10 @@ echo "== prof rc=$?"
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc/fetch -o run -- python $R/tools/bench_gemm.py --shapes=conv1 --variants=18 > $OUT/pmc_fetch.log 2>&1 || { echo "pmc fetch failed"; exit 1; }
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc/write -o run -- python $R/tools/bench_gemm.py --shapes=conv1 --variants=18 > $OUT/pmc_write.log 2>&1 || { echo "pmc write failed"; exit 1; }
 cd $R && python tools/pmc_traffic.py $OUT/pmc > $OUT/pmc_traffic.json && cat $OUT/pmc_traffic.json
+cd /tmp
+# the fused head's HBM traffic and MFMA busy fraction (tools/pmc_head.py): one counter group per pass
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmch/fetch -o run -- python $R/tools/pmc_head.py run > $OUT/pmch_fetch.log 2>&1 || { echo "head pmc fetch failed"; exit 1; }
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmch/write -o run -- python $R/tools/pmc_head.py run > $OUT/pmch_write.log 2>&1 || { echo "head pmc write failed"; exit 1; }
+timeout -s KILL 120 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d $OUT/pmch/mfma -o run -- python $R/tools/pmc_head.py run > $OUT/pmch_mfma.log 2>&1 || { echo "head pmc mfma failed"; exit 1; }
+cd $R && python tools/pmc_head.py summarize $OUT/pmch > $OUT/pmc_traffic_head.json && grep traffic_bytes $OUT/pmc_traffic_head.json
 echo SESSION_DONE
