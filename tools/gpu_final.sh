@@ -29,4 +29,6 @@ timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmch/
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmch/write -o run -- python $R/tools/pmc_head.py run > $OUT/pmch_write.log 2>&1 || { echo "head pmc write failed"; exit 1; }
 timeout -s KILL 120 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d $OUT/pmch/mfma -o run -- python $R/tools/pmc_head.py run > $OUT/pmch_mfma.log 2>&1 || { echo "head pmc mfma failed"; exit 1; }
 cd $R && python tools/pmc_head.py summarize $OUT/pmch > $OUT/pmc_traffic_head.json && grep traffic_bytes $OUT/pmc_traffic_head.json
+# the serialized per-conv roofline table of the same tree
+bash tools/gpu_trunk_serial.sh ${TAG}_trunk > $OUT/trunk.log 2>&1 && grep "^# " $R/gpurun_out/${TAG}_trunk/trunk_table_serial.txt | head -4
 echo SESSION_DONE
