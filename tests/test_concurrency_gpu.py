@@ -15,14 +15,14 @@ pytestmark = pytest.mark.gpu
 
 
 def _head_calls(m, B=4):
-    """(fn, args, kwargs) of the fused head forward's xh_audio_fwd / xh_v2a_fwd / xh_a2v_fwd launches."""
+    """(fn, args, kwargs) of the fused head forward's F1 / F2 / F3 launches (xh_audio_fwd[_pair], xh_v2a_fwd, xh_a2v_fwd)."""
     from multimodalemotionrecognition_amd import kernels as K
     from multimodalemotionrecognition_amd import xattn_head as XH
 
     names, params = m.head_params()
     p = dict(zip(names, params))
     rec, orig = [], {}
-    for n in ("xh_audio_fwd", "xh_v2a_fwd", "xh_a2v_fwd"):
+    for n in ("xh_audio_fwd", "xh_audio_fwd_pair", "xh_v2a_fwd", "xh_a2v_fwd"):
         orig[n] = fn = getattr(K, n)
 
         def wrapped(*a, _fn=fn, **kw):

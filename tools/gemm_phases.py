@@ -39,19 +39,28 @@ def run():
     resid = "--resid" in sys.argv
     M = 32 * 149
     shapes = {"qkv": (2304, 768), "ffn1": (3072, 768), "ffn2": (768, 3072), "out_proj": (768, 768)}
+    if "--conv1" in sys.argv:  # the feature extractor's conv1 as an implicit GEMM (rows mode, tools/bench_gemm.py)
+        shapes = {"conv1": (512, 1536)}
     tick_us = 0.01
     for name, (N, Kd) in shapes.items():
-        a = (torch.rand(M, Kd, device="cuda") * 2 - 1).bfloat16()
+        kw = {}
+        if name == "conv1":
+            Mr = 32 * 4799
+            a = (torch.rand(32 * 9599 * 512, device="cuda") * 2 - 1).bfloat16()
+            kw = dict(M=Mr, K=Kd, rows=(4799, 1024, 9599 * 512))
+        else:
+            Mr = M
+            a = (torch.rand(M, Kd, device="cuda") * 2 - 1).bfloat16()
         w = (torch.rand(N, Kd, device="cuda") * 2 - 1).bfloat16()
-        out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
-        r = (torch.rand(M, N, device="cuda") * 2 - 1).bfloat16() if resid else None
+        out = torch.empty(Mr, N, device="cuda", dtype=torch.bfloat16)
+        r = (torch.rand(Mr, N, device="cuda") * 2 - 1).bfloat16() if resid else None
         bias = torch.rand(N, device="cuda")
         for v in variants:
             for _ in range(3):
-                K.gemm_bf16(a, w, out, bias=bias, residual=r, variant=v)
+                K.gemm_bf16(a, w, out, bias=bias, residual=r, variant=v, **kw)
             torch.cuda.synchronize()
             assert _lib.LIB._dll.mer_gt_reset() == 0
-            K.gemm_bf16(a, w, out, bias=bias, residual=r, variant=v)
+            K.gemm_bf16(a, w, out, bias=bias, residual=r, variant=v, **kw)
             torch.cuda.synchronize()
             t = np.zeros((1024, 8), dtype=np.int64)
             assert _lib.LIB._dll.mer_gt_read(ctypes.c_void_p(t.ctypes.data)) == 0
