@@ -202,9 +202,15 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs g) {
 // glds writes lane-linear (base + 16*lane), so the XOR goes on each lane's SOURCE address and on
 // the fragment read (rule 21: both sides).  Rows past M/N are clamped to the last valid row (their
 // outputs are discarded); K is a multiple of 64, so no K tail.
-template <int BM_, int BN_, int WM_, int WN_, int STAGES_ = 2, int KS_ = 64, int SA_ = 0>
+template <int BM_, int BN_, int WM_, int WN_, int STAGES_ = 2, int KS_ = 64, int SA_ = 0, int SW_ = 0, int IL_ = 0>
 struct PipeCfg {
+  // IL (split ring only): the K-step's LDS-DMA issue goes between the first substep's MFMA rows instead of ahead of
+  // the fragment reads, so its issue cost runs under the SIMD's MFMAs rather than in front of them
+  static constexpr bool IL = IL_ != 0;
   static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_;       // tile, waves along M / N
+  // SW: operand-swapped MFMA (W fragment as the A operand): a lane's accumulator quad is then 4 consecutive COLUMNS
+  // of one row, which the staged epilogue writes to LDS as one 16-byte fp32 or 8-byte bf16 vector
+  static constexpr bool SW = SW_ != 0;
   static constexpr int STAGES = STAGES_;                            // LDS ring depth (K-tiles)
   // SA > 0: the A operand gets its own, deeper ring (SA = 3 with a 2-deep B ring): A is the HBM stream of the
   // conv-as-GEMMs (B, the weights, stays L2-resident), so A tiles are issued two K-steps ahead, B tiles one
@@ -243,6 +249,12 @@ static __device__ long long mer_gt_buf[1024 * 8];
   do { \
     if (threadIdx.x == 0 && blockIdx.x < 1024 && blockIdx.z == 0) mer_gt_buf[blockIdx.x * 8 + (k)] = wall_clock64(); \
   } while (0)
+// shader-clock stamp (s_memtime, cycles at the in-kernel clock) beside GT(k): slot k + 4 (k = 1, 2 only)
+#define GTC(k) \
+  do { \
+    if (threadIdx.x == 0 && blockIdx.x < 1024 && blockIdx.z == 0) \
+      mer_gt_buf[blockIdx.x * 8 + 4 + (k)] = (long long)__builtin_amdgcn_s_memtime(); \
+  } while (0)
 MER_API int mer_gt_reset() {
   static long long zeros[1024 * 8];
   return (int)hipMemcpyToSymbol(HIP_SYMBOL(mer_gt_buf), zeros, sizeof(zeros), 0, hipMemcpyHostToDevice);
@@ -253,6 +265,9 @@ MER_API int mer_gt_read(long long* host) {
 }
 #else
 #define GT(k) \
+  do { \
+  } while (0)
+#define GTC(k) \
   do { \
   } while (0)
 #endif
@@ -368,12 +383,17 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_pipe_kernel(GemmArgs g) {
     __builtin_amdgcn_s_waitcnt((15) | (7 << 4) | (0 << 8) | (3 << 14));  // lgkmcnt(0) only
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    if (kt == 0) GT(1);
+    if (kt == 0) {
+      GT(1);
+      GTC(1);
+    }
     const bf16_t* la;
     const bf16_t* lb;
     if constexpr (SPLIT) {
-      if (kt + 1 < nk) stage_b(ring_b + ((kt + 1) & 1) * CF::BN * CF::KS, ktile_off_k<CF::KS>(g, kt + 1));
-      if (kt + 2 < nk) stage_a(smem + ((kt + 2) % 3) * CF::BM * CF::KS, ktile_off_k<CF::KS>(g, kt + 2));
+      if constexpr (!CF::IL) {
+        if (kt + 1 < nk) stage_b(ring_b + ((kt + 1) & 1) * CF::BN * CF::KS, ktile_off_k<CF::KS>(g, kt + 1));
+        if (kt + 2 < nk) stage_a(smem + ((kt + 2) % 3) * CF::BM * CF::KS, ktile_off_k<CF::KS>(g, kt + 2));
+      }
       la = smem + (kt % 3) * CF::BM * CF::KS;
       lb = ring_b + (kt & 1) * CF::BN * CF::KS;
     } else {
@@ -396,17 +416,172 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_pipe_kernel(GemmArgs g) {
       }
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-      for (int i = 0; i < CF::FM; ++i)
+      for (int i = 0; i < CF::FM; ++i) {
 #pragma unroll
         for (int j = 0; j < CF::FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = CF::SW ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0)
+                             : __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        if constexpr (CF::IL && SPLIT) {
+          // same pieces, same issue order (B(kt+1) then A(kt+2)) as the non-interleaved ring: the vmcnt
+          // bookkeeping at the top of the next step is unchanged
+          if (s == 0 && i == 0 && kt + 1 < nk) {
+            __builtin_amdgcn_sched_barrier(0);
+            stage_b(ring_b + ((kt + 1) & 1) * CF::BN * CF::KS, ktile_off_k<CF::KS>(g, kt + 1));
+            __builtin_amdgcn_sched_barrier(0);
+          }
+          if (s == 0 && i == 1 && kt + 2 < nk) {
+            __builtin_amdgcn_sched_barrier(0);
+            stage_a(smem + ((kt + 2) % 3) * CF::BM * CF::KS, ktile_off_k<CF::KS>(g, kt + 2));
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        }
+      }
       __builtin_amdgcn_s_setprio(0);
     }
   }
 
+  GTC(2);
   GT(2);
   TOUT* C = reinterpret_cast<TOUT*>(g.C) + (long)z * g.c_zoff;
   const unsigned long long dseed = mer_site_seed(g.drop_seed, g.drop_site);
+  if constexpr (CF::SW) {
+    if (g.vec_epi) {
+      // Operand-swapped epilogue: a lane holds row i*16 + fr, columns j*16 + fq*4 .. +3 of each fragment.  Without
+      // residual or dropout on a bf16 output the result bf16(act(acc + bias)) is rounded before staging: 8-byte
+      // writes of [row][TN + 8] bf16 (half the LDS bytes of the fp32 image, the whole sub-tile in one pass); else
+      // act(acc + bias) is staged as fp32 [row][TN + 4], one 16-byte write per fragment, and the residual /
+      // dropout pass below is the unswapped one.  Same arithmetic and rounding as the direct path.
+      constexpr int WAVE_FLOATS = CF::LDS_ELEMS / 2 / CF::WAVES;
+      constexpr int LPR = CF::TN / 8, RPP = 64 / LPR;
+      // the lane's bias quads, loaded before the barrier that waits for the slowest wave's last MFMAs (their
+      // latency was exposed at the first staging write); N % 8 == 0 here, so a quad is all in or all out
+      // (bf16 outputs only: the fp32-output instantiation has no registers to spare and loads them per block j)
+      constexpr bool PRE = std::is_same<TOUT, bf16_t>::value;
+      f32x4 bq4[CF::FN];
+      auto bias_quad = [&](int j) {
+        const int col = n0 + wc * CF::TN + j * 16 + fq * 4;
+        f32x4 q = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (g.bias && col < g.N) {
+          const float* bp = g.bias + (long)z * g.c_zoff + col;
+          q = f32x4{bp[0], bp[1], bp[2], bp[3]};
+        }
+        return q;
+      };
+      if constexpr (PRE) {
+#pragma unroll
+        for (int j = 0; j < CF::FN; ++j) bq4[j] = bias_quad(j);
+      }
+      __syncthreads();
+      GT(4);
+      auto bias4 = [&](int j, float* bq) {
+        const f32x4 q = PRE ? bq4[j] : bias_quad(j);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) bq[e] = q[e];
+      };
+      const int lr = lane / LPR, lc = (lane % LPR) * 8;
+      const int colv = n0 + wc * CF::TN + lc;
+      if (std::is_same<TOUT, bf16_t>::value && !g.R && !(g.drop_p > 0.f)) {
+        constexpr int LDH = CF::TN + 8;
+        constexpr int GH0 = 2 * WAVE_FLOATS / (16 * LDH);
+        constexpr int GH = GH0 < CF::FM ? GH0 : CF::FM;
+        static_assert(GH >= 1, "epilogue staging slice too small");
+        bf16_t* hl = reinterpret_cast<bf16_t*>(smem) + w * 2 * WAVE_FLOATS;
+#pragma unroll
+        for (int i0 = 0; i0 < CF::FM; i0 += GH) {
+#pragma unroll
+          for (int j = 0; j < CF::FN; ++j) {
+            float bq[4];
+            bias4(j, bq);
+#pragma unroll
+            for (int ii = 0; ii < GH; ++ii) {
+              if (i0 + ii >= CF::FM) break;
+              uint32_t q[4];
+#pragma unroll
+              for (int e = 0; e < 4; ++e) q[e] = (uint32_t)f2bf(apply_act(acc[i0 + ii][j][e] + bq[e], g.act));
+              *reinterpret_cast<uint2*>(&hl[(ii * 16 + fr) * LDH + j * 16 + fq * 4]) =
+                  make_uint2(q[0] | (q[1] << 16), q[2] | (q[3] << 16));
+            }
+          }
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          const int nrows = (CF::FM - i0 < GH ? CF::FM - i0 : GH) * 16;
+#pragma unroll
+          for (int rr = 0; rr < GH * 16; rr += RPP) {
+            const int rl = rr + lr;
+            const int row = m0 + wr * CF::TM + i0 * 16 + rl;
+            if (rl < nrows && row < g.M && colv < g.N)
+              *reinterpret_cast<u32x4*>(C + (long)row * g.ldc + colv) = *reinterpret_cast<const u32x4*>(&hl[rl * LDH + lc]);
+          }
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+        GT(3);
+        return;
+      }
+      constexpr int LDT = CF::TN + 4;
+      constexpr int GI0 = WAVE_FLOATS / (16 * LDT);
+      constexpr int GI = GI0 < CF::FM ? GI0 : CF::FM;
+      static_assert(GI >= 1, "epilogue staging slice too small");
+      float* wl = reinterpret_cast<float*>(smem) + w * WAVE_FLOATS;
+#pragma unroll
+      for (int i0 = 0; i0 < CF::FM; i0 += GI) {
+        constexpr int NRR = (GI * 16 + RPP - 1) / RPP;
+        u32x4 rres[NRR];
+        if (g.R) {
+#pragma unroll
+          for (int q = 0; q < NRR; ++q) {
+            const int row = m0 + wr * CF::TM + i0 * 16 + q * RPP + lr;
+            const long rr = row < g.M ? row : g.M - 1;
+            rres[q] = *reinterpret_cast<const u32x4*>(g.R + rr * g.ldr + (long)z * g.c_zoff + (colv < g.N ? colv : 0));
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < CF::FN; ++j) {
+          float bq[4];
+          bias4(j, bq);
+#pragma unroll
+          for (int ii = 0; ii < GI; ++ii) {
+            if (i0 + ii >= CF::FM) break;
+            f32x4 v;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = apply_act(acc[i0 + ii][j][e] + bq[e], g.act);
+            *reinterpret_cast<f32x4*>(&wl[(ii * 16 + fr) * LDT + j * 16 + fq * 4]) = v;
+          }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const int nrows = (CF::FM - i0 < GI ? CF::FM - i0 : GI) * 16;
+#pragma unroll
+        for (int rr = 0; rr < GI * 16; rr += RPP) {
+          const int rl = rr + lr;
+          const int row = m0 + wr * CF::TM + i0 * 16 + rl;
+          if (rl < nrows && row < g.M && colv < g.N) {
+            const f32x4 lo = *reinterpret_cast<const f32x4*>(&wl[rl * LDT + lc]);
+            const f32x4 hi = *reinterpret_cast<const f32x4*>(&wl[rl * LDT + lc + 4]);
+            float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+            if (g.drop_p > 0.f) dropout_pairs<8>(v, dseed, (uint64_t)((long)row * g.N + colv), g.drop_p);
+            if (g.R) {
+              const u32x4 rv = rres[rr / RPP];
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                v[2 * e] += __uint_as_float(rv[e] << 16);
+                v[2 * e + 1] += __uint_as_float(rv[e] & 0xffff0000u);
+              }
+            }
+            store8<TOUT>(C + (long)row * g.ldc + colv, v);
+          }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      }
+      GT(3);
+      return;
+    }
+  }
   if (g.vec_epi) {
     // Epilogue through LDS (the ring is idle once every wave is past its last fragment read): each wave
     // stages act(acc + bias) of 16-row groups of its TM x TN sub-tile as fp32 [row][TN + 4] in its own slice
@@ -420,14 +595,15 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_pipe_kernel(GemmArgs g) {
     constexpr int GI = GI0 < CF::FM ? GI0 : CF::FM;
     static_assert(GI >= 1, "epilogue staging slice too small");
     constexpr int LPR = CF::TN / 8, RPP = 64 / LPR;  // lanes per row, rows per pass
-    __syncthreads();
-    float* wl = reinterpret_cast<float*>(smem) + w * WAVE_FLOATS;
-    float bv[CF::FN];
+    float bv[CF::FN];  // loaded before the barrier: its wait for the slowest wave covers their latency
 #pragma unroll
     for (int j = 0; j < CF::FN; ++j) {
       const int col = n0 + wc * CF::TN + j * 16 + fr;
       bv[j] = (g.bias && col < g.N) ? g.bias[(long)z * g.c_zoff + col] : 0.f;
     }
+    __syncthreads();
+    GT(4);
+    float* wl = reinterpret_cast<float*>(smem) + w * WAVE_FLOATS;
     const int lr = lane / LPR, lc = (lane % LPR) * 8;
     const int colv = n0 + wc * CF::TN + lc;
 #pragma unroll
@@ -485,6 +661,25 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_pipe_kernel(GemmArgs g) {
     GT(3);
     return;
   }
+  if constexpr (CF::SW) {
+#pragma unroll
+    for (int j = 0; j < CF::FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int col = n0 + wc * CF::TN + j * 16 + fq * 4 + r;  // swapped: element r is column fq*4 + r of row fr
+        if (col >= g.N) continue;
+        const float bv = g.bias ? g.bias[(long)z * g.c_zoff + col] : 0.f;
+#pragma unroll
+        for (int i = 0; i < CF::FM; ++i) {
+          const int row = m0 + wr * CF::TM + i * 16 + fr;
+          if (row >= g.M) continue;
+          float v = epi_act_drop(acc[i][j][r] + bv, g.act, g.drop_p, dseed, (long)row * g.N + col);
+          if (g.R) v += bf2f(g.R[(long)row * g.ldr + (long)z * g.c_zoff + col]);
+          stf<TOUT>(C, (long)row * g.ldc + col, v);
+        }
+      }
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < CF::FN; ++j) {
     const int col = n0 + wc * CF::TN + j * 16 + fr;
@@ -508,6 +703,9 @@ using CfgT3 = PipeCfg<128, 64, 2, 2, 3>;   // v7: 128x64 tiles, 3-deep ring, 72 
 using CfgW2 = PipeCfg<128, 128, 2, 4, 2>;  // v9: 8 waves (64x32 each), 2-deep, 64 KiB LDS (2 blocks / CU)
 using CfgY2 = PipeCfg<256, 256, 4, 4, 2>;  // v13: 16 waves (64x64 each), 2-deep, 128 KiB LDS
 using CfgY32 = PipeCfg<256, 256, 4, 4, 2, 64, 3>;  // v18: 16 waves, A 3-deep + B 2-deep rings, 160 KiB LDS
+using CfgY32s = PipeCfg<256, 256, 4, 4, 2, 64, 3, 1>;  // v21: v18 operand-swapped (bf16 staging, see the epilogue)
+using CfgY32i = PipeCfg<256, 256, 4, 4, 2, 64, 3, 0, 1>;  // v22: v18, DMA issue between MFMA rows
+using CfgY32si = PipeCfg<256, 256, 4, 4, 2, 64, 3, 1, 1>;  // v23: v21, DMA issue between MFMA rows
 
 template <class CF, typename TOUT, int AMODE>
 int launch_pipe_t(const GemmArgs& g, int groups, hipStream_t st) {
@@ -593,7 +791,7 @@ MER_API int mer_gemm_bf16_tr(int M, int N, int K, const void* A, long a_gstride,
   if (drop_p < 0.f || drop_p >= 1.f || (drop_p > 0.f && !drop_seed) || skip_bit < 0 || skip_bit > 62)
     return (int)hipErrorInvalidValue;
   if (!(variant == -2 || variant == -1 || variant == 0 || variant == 7 || variant == 9 || variant == 13 ||
-        variant == 18))
+        variant == 18 || variant == 21 || variant == 22 || variant == 23))
     return (int)hipErrorInvalidValue;
   if (K % 8 != 0 || a_rpg <= 0 || (a_rstride % 8) != 0 || (a_gstride % 8) != 0 || (ldw % 8) != 0)
     return (int)hipErrorInvalidValue;
@@ -617,12 +815,22 @@ MER_API int mer_gemm_bf16_tr(int M, int N, int K, const void* A, long a_gstride,
   }
   const hipStream_t st = (hipStream_t)stream;
   if (K % 64 != 0) variant = 0;  // the register-staged kernel takes any K (multiple of 8)
-  if (variant < 0) variant = pick_variant(M, N, K, variant);
+  if (variant < 0) {
+    variant = pick_variant(M, N, K, variant);
+    // the split ring issues its LDS-DMA between the first substep's MFMA rows (v22); a bf16 output without residual
+    // or dropout (QKV, FFN-up, the feature-extractor convs) also rounds before staging on the operand-swapped form
+    // (v23: half the epilogue's LDS bytes).  tools/bench_gemm.py, 20 back-to-back launches: conv1 with GELU 300 ->
+    // 274 us, conv2 150 -> 143, FFN-up 35.9 -> 33.9, QKV 28.9 -> 27.7 (profiles/r05/gemm_swap); bit-identical to v18
+    if (variant == 18) variant = (c_dtype == MER_BF16 && !R && !(drop_p > 0.f) && g.vec_epi) ? 23 : 22;
+  }
   switch (variant) {
     case 7: return launch_pipe<CfgT3>(g, c_dtype, st);
     case 9: return launch_pipe<CfgW2>(g, c_dtype, st);
     case 13: return launch_pipe<CfgY2>(g, c_dtype, st);
     case 18: return launch_pipe<CfgY32>(g, c_dtype, st);
+    case 21: return launch_pipe<CfgY32s>(g, c_dtype, st);
+    case 22: return launch_pipe<CfgY32i>(g, c_dtype, st);
+    case 23: return launch_pipe<CfgY32si>(g, c_dtype, st);
     default: return launch<0>(g, c_dtype, 1, st);
   }
 }

@@ -45,12 +45,15 @@ def main():
         resid = "--resid32" in sys.argv  # the WavLM residual GEMMs: fp32 output + bf16 residual + bias
         r = (torch.rand(M, N, device="cuda") * 2 - 1).bfloat16() if resid else None
         bias = torch.rand(N, device="cuda") if resid else None
+        gbias = bias if bias is not None else torch.rand(N, device="cuda")
         for odt in ((torch.float32,) if resid else (torch.bfloat16,)):
             for v in VARIANTS:
                 out = torch.empty(M, N, device="cuda", dtype=odt)
                 kw = dict(M=M, K=Kd, rows=rows) if rows else {}
                 if resid:
                     kw.update(residual=r, bias=bias)
+                if "--gelu" in sys.argv:  # bias + GELU epilogue (FFN-up, the feature-extractor convs)
+                    kw.update(bias=gbias, act="gelu")
                 for _ in range(3):
                     K.gemm_bf16(a, w, out, variant=v, **kw)
                 torch.cuda.synchronize()

@@ -6,9 +6,15 @@ TAG=${1:-abtree}; N=${2:-2}; OLDENV=${3:-}
 OUT=$PWD/gpurun_out/$TAG
 mkdir -p $OUT
 R=$PWD
+run_new() {
+  timeout -k 10 300 python -u bench.py --no-cpu-baseline --probe-launches 0 --probe-steps 0 > $OUT/new_$1.log 2>&1 || { echo "FAIL new"; tail -5 $OUT/new_$1.log; exit 1; }
+  echo "new run $1: $(grep '^{' $OUT/new_$1.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"], d["ms_per_step_median"])')"
+}
+run_old() {
+  (cd tools/scratch/abtree && env $OLDENV timeout -k 10 300 python -u bench.py --no-cpu-baseline --probe-launches 0 --probe-steps 0) > $OUT/old_$1.log 2>&1 || { echo "FAIL old"; tail -5 $OUT/old_$1.log; exit 1; }
+  echo "old run $1: $(grep '^{' $OUT/old_$1.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"], d["ms_per_step_median"])')"
+}
+# ABBA order: odd rounds run the working tree first, even rounds the old tree first
 for i in $(seq 1 $N); do
-  timeout -k 10 300 python -u bench.py --no-cpu-baseline --probe-launches 0 --probe-steps 0 > $OUT/new_$i.log 2>&1 || { echo "FAIL new"; tail -5 $OUT/new_$i.log; exit 1; }
-  echo "new run $i: $(grep '^{' $OUT/new_$i.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"], d["ms_per_step_median"])')"
-  (cd tools/scratch/abtree && env $OLDENV timeout -k 10 300 python -u bench.py --no-cpu-baseline --probe-launches 0 --probe-steps 0) > $OUT/old_$i.log 2>&1 || { echo "FAIL old"; tail -5 $OUT/old_$i.log; exit 1; }
-  echo "old run $i: $(grep '^{' $OUT/old_$i.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"], d["ms_per_step_median"])')"
+  if [ $((i % 2)) = 1 ]; then run_new $i; run_old $i; else run_old $i; run_new $i; fi
 done
