@@ -11,7 +11,7 @@ import sys
 from collections import defaultdict
 
 root = sys.argv[1]
-frag = sys.argv[2] if len(sys.argv) > 2 else "gemm_pipe_kernel<(anonymousnamespace)::PipeCfg<256,256,4,4,2>"
+frag = sys.argv[2] if len(sys.argv) > 2 else "gemm_pipe_kernel<(anonymousnamespace)::PipeCfg<256,256,4,4,2,64,3,0,0>"
 # the conv1 implicit GEMM's grid (threads) for the default probe; any grid for another kernel
 GRID = ((32 * 4799 + 255) // 256) * ((512 + 255) // 256) * 1024 if len(sys.argv) <= 2 else 0
 vals = defaultdict(lambda: defaultdict(float))
