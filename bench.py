@@ -78,10 +78,10 @@ PEAK_HBM_GBS = 8000.0       # HBM3E spec
 # Dominant kernel (largest share of step time in profiles/): the WavLM feature-extractor conv1 as an
 # implicit GEMM: M = B*4799 output frames, N = 512 channels, K = 3 taps * 512.
 PROBE = ("gemm_bf16", (BATCH * 4799, 512, 1536))
-# the kernel the train step's side-stream forward dispatches for that shape (gemm_bf16.hip pick_variant, CU-time
-# rule -2: the split ring, 1,200 tiles of 256x256, 16 waves each; PipeCfg's last two flags = not swapped, no DMA
-# interleave)
-PROBE_KERNEL = "gemm_pipe_kernel<PipeCfg<256,256,4,4,2,64,3,0,0>, bf16>"
+# the kernel the train step's side-stream forward dispatches for that shape (gemm_bf16.hip, CU-time rule -2: the
+# split ring, 1,200 tiles of 256x256, 16 waves each; PipeCfg's last two flags: operand-swapped with bf16 epilogue
+# staging, LDS-DMA issued between MFMA rows -- v23)
+PROBE_KERNEL = "gemm_pipe_kernel<PipeCfg<256,256,4,4,2,64,3,1,1>, bf16>"
 PMC_FILE = ROOT / "profiles" / "pmc_traffic.json"
 PMC_HEAD_FILE = ROOT / "profiles" / "pmc_traffic_head.json"  # tools/pmc_head.py summarize (fused head fwd + bwd)
 # Algorithmic work per clip: ResNet18 fwd+bwd over 8 frames 22.8 GFLOP, head fwd+bwd 0.141, WavLM

@@ -818,14 +818,16 @@ MER_API int mer_gemm_bf16_tr(int M, int N, int K, const void* A, long a_gstride,
   if (variant < 0) {
     const int rule = variant;
     variant = pick_variant(M, N, K, rule);
-    // Wall-time rule (its split-ring shape is conv1): the split ring issues its LDS-DMA between the first substep's
-    // MFMA rows (v22); a bf16 output without residual or dropout also rounds before staging on the operand-swapped
-    // form (v23: half the epilogue's LDS bytes).  tools/bench_gemm.py, 20 back-to-back launches on the split ring:
-    // conv1 with GELU 300 -> 274 us, conv2 150 -> 143, FFN-up 35.9 -> 33.9, QKV 28.9 -> 27.7
-    // (profiles/r05/gemm_swap); bit-identical to v18.  Not on the CU-time rule (-2, the train step's side-stream forward): there the same-box ABBA bench
-    // ran 204.0 vs 204.6 steps/s with them (6 pairs, profiles/r05/gemm_swap/ab_il_abba.txt) -- the denser loops buy
-    // no step time beside the trunk stream.
-    if (variant == 18 && rule == -1) variant = (c_dtype == MER_BF16 && !R && !(drop_p > 0.f) && g.vec_epi) ? 23 : 22;
+    // The split ring with its LDS-DMA issued between the first substep's MFMA rows (v22); a bf16 output without
+    // residual or dropout also rounds before staging on the operand-swapped form (v23: half the epilogue's LDS
+    // bytes).  tools/bench_gemm.py, 20 back-to-back launches on the split ring: conv1 with GELU 300 -> 274 us,
+    // conv2 150 -> 143, FFN-up 35.9 -> 33.9, QKV 28.9 -> 27.7 (profiles/r05/gemm_swap); bit-identical to v18.
+    // Wall-time rule: wherever it picks the split ring (conv1).  CU-time rule (-2, the train step's side-stream
+    // forward): the feature-extractor convs only (N <= 512) -- with every shape the same-box ABBA bench ran 204.0
+    // vs 204.6 steps/s (6 pairs, profiles/r05/gemm_swap/ab_il_abba.txt), with the convs only 207.25 vs 206.91
+    // (5 of 6 pairs, ab_conv_abba.txt): within the box's noise either way, and the convs keep their gain.
+    if (variant == 18 && (rule == -1 || N <= 512))
+      variant = (c_dtype == MER_BF16 && !R && !(drop_p > 0.f) && g.vec_epi) ? 23 : 22;
   }
   switch (variant) {
     case 7: return launch_pipe<CfgT3>(g, c_dtype, st);

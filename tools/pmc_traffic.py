@@ -9,7 +9,7 @@ import json
 import sys
 
 root = sys.argv[1]
-MATCH = "gemm_pipe_kernel<(anonymousnamespace)::PipeCfg<256,256,4,4,2,64,3,0,0>"  # (the split-ring conv1 variant, v18)
+MATCH = "gemm_pipe_kernel<(anonymousnamespace)::PipeCfg<256,256,4,4,2,64,3,1,1>"  # (the conv1 variant of the train step, v23)
 SHAPE = (32 * 4799, 512, 1536)
 GRID = ((SHAPE[0] + 255) // 256) * ((SHAPE[1] + 255) // 256) * 1024  # blocks x threads
 
@@ -27,7 +27,7 @@ fetch, write = counter("FETCH_SIZE"), counter("WRITE_SIZE")
 if not fetch or not write:
     sys.exit(f"no probe launches found (fetch {len(fetch)}, write {len(write)})")
 f_kb, w_kb = sum(fetch) / len(fetch), sum(write) / len(write)
-out = {"kernel_match": "gemm_pipe_kernel<PipeCfg<256,256,4,4,2,64,3,0,0>,bf16>", "shape": list(SHAPE),
+out = {"kernel_match": "gemm_pipe_kernel<PipeCfg<256,256,4,4,2,64,3,1,1>,bf16>", "shape": list(SHAPE),
        "fetch_kb_raw": f_kb, "write_kb": w_kb, "launches": [len(fetch), len(write)],
        "traffic_bytes_per_launch": int(1024 * (2 * f_kb + w_kb)),
        "algorithmic_bytes_per_launch": 2 * (32 * 9599 * 512 + 512 * 1536 + SHAPE[0] * 512)}
