@@ -19,6 +19,7 @@ SHAPES = {
     "ffn1": (B * 149, 3072, 768, None, None),
     "ffn2": (B * 149, 768, 3072, None, None),
     "out_proj": (B * 149, 768, 768, None, None),
+    "f1pair": (B * 149, 256, 768, None, None),  # the fused head's F1 product against stacked hi/lo planes (fp32 out)
     "sq4096": (4096, 4096, 4096, None, None),
     "sq8192": (8192, 8192, 8192, None, None),
 }
@@ -35,7 +36,7 @@ def main():
     for name, (M, N, Kd, rows, alen) in SHAPES.items():
         if quick and name not in ("conv1 (rows)", "qkv", "ffn2"):
             continue
-        if (ONLY is None and name.startswith("sq")) or (ONLY is not None and name.split()[0] not in ONLY):
+        if (ONLY is None and (name.startswith("sq") or name == "f1pair")) or (ONLY is not None and name.split()[0] not in ONLY):
             continue
         a = (torch.rand(alen if rows else M * Kd, device="cuda") * 2 - 1).bfloat16()
         if not rows:
@@ -46,7 +47,7 @@ def main():
         r = (torch.rand(M, N, device="cuda") * 2 - 1).bfloat16() if resid else None
         bias = torch.rand(N, device="cuda") if resid else None
         gbias = bias if bias is not None else torch.rand(N, device="cuda")
-        for odt in ((torch.float32,) if resid else (torch.bfloat16,)):
+        for odt in ((torch.float32,) if (resid or "--f32" in sys.argv) else (torch.bfloat16,)):
             for v in VARIANTS:
                 out = torch.empty(M, N, device="cuda", dtype=odt)
                 kw = dict(M=M, K=Kd, rows=rows) if rows else {}
