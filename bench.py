@@ -31,7 +31,6 @@ from __future__ import annotations
 import argparse
 import json
 import os
-import socket
 import subprocess
 import sys
 import time
@@ -47,12 +46,10 @@ def _launch_ranks_if_needed(argv) -> None:
     known, _ = pre.parse_known_args(argv)
     if known.gpus <= 1 or "WORLD_SIZE" in os.environ:
         return
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={known.gpus}",
-           "--master-addr", "127.0.0.1", f"--master-port={port}", str(Path(__file__).resolve()), *argv]
+    # --standalone: torchrun's own local rendezvous store binds a free port itself (no probe-then-close race for the
+    # port); --local-addr 127.0.0.1: the ranks connect over loopback, whatever the container's hostname resolves to
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--standalone", "--nnodes=1",
+           f"--nproc-per-node={known.gpus}", "--local-addr", "127.0.0.1", str(Path(__file__).resolve()), *argv]
     sys.exit(subprocess.run(cmd).returncode)
 
 
@@ -391,21 +388,73 @@ def main():
     return _bench(args, world, rank, local)
 
 
+def dp_fields(local_step_ms, sync, dev):
+    """The DP diagnostics of the bench line: per rank its own step time and the ``CommTimes``
+    summary of its ``GradAllReduce`` (exposed all-reduce ms per step, how early the head + layer4 bucket went out
+    before the backward's end), all-gathered to every rank; rank 0 reports them with the max and min over ranks, so
+    a shortfall of the 1 -> 8 curve can be traced to communication or to a slow rank from the run's own line."""
+    s = sync.times.summary() if sync is not None and sync.times is not None else {}
+    nan = float("nan")
+    vec = torch.tensor([local_step_ms, s.get("allreduce_exposed_ms") or nan, s.get("early_bucket_lead_ms") or nan,
+                        float(s.get("early_bucket_steps", 0)), float(s.get("steps", 0))], device=dev,
+                       dtype=torch.float64)
+    world = dist.get_world_size() if is_dist() else 1
+    rows = [torch.zeros_like(vec) for _ in range(world)]
+    if is_dist():
+        dist.all_gather(rows, vec)
+    else:
+        rows = [vec]
+    keys = ("step_ms", "allreduce_exposed_ms", "early_bucket_lead_ms", "early_bucket_steps", "timed_steps")
+    per = []
+    for r, row in enumerate(rows):
+        d = {"rank": r}
+        for k, v in zip(keys, row.tolist()):
+            d[k] = None if v != v else (int(v) if k.endswith("steps") else round(v, 4))
+        per.append(d)
+    agg = {}
+    for k in keys[:3]:
+        vals = [d[k] for d in per if d[k] is not None]
+        agg[k] = {"max": max(vals), "min": min(vals)} if vals else None
+    return {"per_rank": per, "over_ranks": agg,
+            "bytes_allreduced_per_step": sum(f.numel() * f.element_size() for f in sync.opt.flat_grads())
+            if sync is not None else None,
+            "measured": "HIP events on the compute stream (host clock under gloo/CPU): early-bucket hook, backward "
+                        "end, and around the waits on the launched all-reduces; means over the timed steps"}
+
+
 def _bench_stub(args, world, rank):
     """The launcher's test hook (tests/test_bench_launch_cpu.py): the same warm-up / barrier / timed region /
-    max-over-ranks structure as ``_bench`` around a CPU matmul + gloo all-reduce, one JSON line from rank 0 that
-    says how many ranks took part."""
+    max-over-ranks structure as ``_bench`` around a CPU matmul and the real ``GradAllReduce`` (gloo, FusedAdam's
+    flat buffers of a small model, the early-bucket hook fired mid-step), one JSON line from rank 0 that says how
+    many ranks took part, with the same ``dp`` diagnostics as the train-step line."""
+    from multimodalemotionrecognition_amd.optim import FusedAdam
+
     x = torch.full((64, 64), 1.0 / 64)
-    for _ in range(args.warmup):
+    m = torch.nn.Sequential(torch.nn.Linear(64, 64), torch.nn.Linear(64, 8))
+    opt = FusedAdam(list(m.parameters()))
+    sync = GradAllReduce(opt, model=m, early_params=list(m[1].parameters()), mask_sync=False, timing=True) \
+        if is_dist() else None
+    (flat,) = opt.flat_grads()
+
+    def one():
+        nonlocal x
         x = x @ x
+        flat.fill_(1.0)
+        if sync is not None:
+            sync.grads_ready()  # the early bucket, then the rest of the "backward"
+            x = x @ x
+            sync()
+
+    for _ in range(args.warmup):
+        one()
+    if sync is not None:
+        sync.times.reset()
     if is_dist():
         dist.barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        x = x @ x
-        if is_dist():
-            dist.all_reduce(x)
-            x /= world
+        one()
+    local_ms = (time.perf_counter() - t0) / max(1, args.steps) * 1e3
     if is_dist():
         dist.barrier()
     el = torch.tensor([time.perf_counter() - t0])
@@ -413,10 +462,11 @@ def _bench_stub(args, world, rank):
     if is_dist():
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
         dist.all_reduce(ranks)
+    dp = dp_fields(local_ms, sync, torch.device("cpu"))
     if rank == 0:
         print(json.dumps({"metric": "stub", "value": round(world * args.steps / float(el), 3), "unit": "steps/s",
                           "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-                          "ranks_reporting": int(ranks), "pid": os.getpid()}), flush=True)
+                          "ranks_reporting": int(ranks), "pid": os.getpid(), "dp": dp}), flush=True)
     if is_dist():
         dist.barrier()
         dist.destroy_process_group()
@@ -525,7 +575,8 @@ def _bench(args, world, rank, local):
         opt = build_fusion_stage_optimizer(model, stage=2, lr=1e-3, weight_decay=1e-4)
     else:
         opt = build_optimizer(model, lr=1e-3, weight_decay=1e-4)
-    step = TrainStep(model, opt, make_loss("xattn"), "xattn", GradAllReduce(opt, model=model) if is_dist() else None)
+    sync = GradAllReduce(opt, model=model, timing=True) if is_dist() else None
+    step = TrainStep(model, opt, make_loss("xattn"), "xattn", sync)
     video, audio, labels = synthetic_batch(dev, 20261015 + rank)
 
     # The synthetic stream repeats one resident batch, so the next step's waveform is `audio` itself:
@@ -537,6 +588,8 @@ def _bench(args, world, rank, local):
 
     wav = model.audio_model.wavlm
     lay0, fwd0 = wav.executed_layers, wav.train_forwards
+    if sync is not None:
+        sync.times.reset()  # the DP diagnostics cover the timed steps only
     if is_dist():
         dist.barrier()
     torch.cuda.synchronize()
@@ -548,6 +601,7 @@ def _bench(args, world, rank, local):
         loss, _ = step(video, audio, labels, next_audio=nxt)
         marks[i + 1].record()
     torch.cuda.synchronize()
+    local_ms = (time.perf_counter() - t0) / args.steps * 1e3  # this rank alone, before the closing barrier
     if is_dist():
         dist.barrier()
     elapsed = time.perf_counter() - t0
@@ -555,6 +609,7 @@ def _bench(args, world, rank, local):
     median_ms = step_ms[len(step_ms) // 2] if len(step_ms) % 2 else 0.5 * (step_ms[len(step_ms) // 2 - 1] +
                                                                            step_ms[len(step_ms) // 2])
     layers = (wav.executed_layers - lay0) / max(1, wav.train_forwards - fwd0)
+    dp = dp_fields(local_ms, sync, dev) if is_dist() else None
 
     # probe steps (after the timed region): the fused head's forward / backward graph replays bracketed by HIP
     # events on their stream
@@ -639,6 +694,7 @@ def _bench(args, world, rank, local):
         "step_tflops_achieved": round(step_gflop / 1e3 / (median_ms * 1e-3), 1),
         "roofline": roof,
         "roofline_head": roof_head,
+        "dp": dp,
         "peaks": peaks,
         "cpu_baseline": None,
     }

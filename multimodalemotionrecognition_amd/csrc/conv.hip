@@ -34,8 +34,25 @@ MER_API int mer_ct_reset() {
 MER_API int mer_ct_read(long long* host) {
   return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(mer_ct_buf), sizeof(long long) * 512 * 64, 0, hipMemcpyDeviceToHost);
 }
+// conv_pipe_kernel's phases (tools/pipe_phases.py): slot k of the linear block id (blockIdx.y * gridDim.x + blockIdx.x)
+static __device__ long long mer_ctp_buf[4096 * 8];
+#define CTP(k) \
+  do { \
+    const unsigned b_ = blockIdx.y * gridDim.x + blockIdx.x; \
+    if (threadIdx.x == 0 && b_ < 4096) mer_ctp_buf[b_ * 8 + (k)] = wall_clock64(); \
+  } while (0)
+MER_API int mer_ctp_reset() {
+  static long long zeros[4096 * 8];
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(mer_ctp_buf), zeros, sizeof(zeros), 0, hipMemcpyHostToDevice);
+}
+MER_API int mer_ctp_read(long long* host) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(mer_ctp_buf), sizeof(long long) * 4096 * 8, 0, hipMemcpyDeviceToHost);
+}
 #else
 #define CT(k) \
+  do { \
+  } while (0)
+#define CTP(k) \
   do { \
   } while (0)
 #endif
@@ -887,7 +904,7 @@ struct EpiPre {
 };
 struct EpiNone {};
 
-template <bool DGRAD, int FM, int FN, int WM, int WN, int WAVE_FLOATS, class OutRow, int NP>
+template <bool DGRAD, int FM, int FN, int WM, int WN, int WAVE_FLOATS, class OutRow, int NP, bool X2 = true>
 __device__ __forceinline__ void conv_epilogue_prefetch(const ConvGeom& g, EpiPre<NP>& pre, int w, int lane, int m0,
                                                        int n0, int M, OutRow out_row) {
   using E = EpiGeo<FM, FN, WAVE_FLOATS>;
@@ -897,7 +914,7 @@ __device__ __forceinline__ void conv_epilogue_prefetch(const ConvGeom& g, EpiPre
   const int colv = n0 + wc * E::TN + lc;
   const bool cok = colv < g.Ncols;
   const bool do_bnr = DGRAD && g.bnr_red != nullptr;
-  const bool has_x2 = do_bnr && g.bnr_x2 != nullptr;
+  const bool has_x2 = X2 && do_bnr && g.bnr_x2 != nullptr;
   const u32x4 z = {0u, 0u, 0u, 0u};
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
@@ -1122,20 +1139,49 @@ __device__ __forceinline__ void conv_epilogue_vec(const ConvGeom& g, f32x4 (&acc
   if (ct_slot >= 0) CT(ct_slot + 2);
 }
 
+// Minimum waves per SIMD of a conv_pipe_kernel block of nw waves: 16-wave blocks 1 per CU, 8-wave blocks 2 per CU --
+// except the tiles that would spill at 128 VGPRs (the 256-row dgrad tiles and the 3-deep 128 x 128 dgrad ring, none of
+// them a default pick), which keep one block per CU; 4-wave blocks 2 per CU.
+constexpr int conv_pipe_wpe(int nw, int bm, int bn, int stages, bool dgrad, bool par) {
+  return nw >= 16 ? nw / 4
+                  : nw == 8 ? ((dgrad && (bm == 256 || (!par && bm == 128 && bn == 128 && stages == 3))) ? 2 : 4) : 2;
+}
+
+// The wave layout of the in-workgroup split-K reduction (KG > 1): WAVES * KG waves over the BM x BN tile, 4 wave
+// rows when that leaves >= 16-row / 16-column sub-tiles.
+template <int BM_, int BN_, int NW>
+struct KgLayout {
+  static constexpr int WM = (NW >= 4 && BM_ / 4 >= 16) ? 4 : (NW >= 2 ? 2 : 1);
+  static constexpr int WN = NW / WM;
+  static_assert(WM * WN == NW && BM_ % (16 * WM) == 0 && BN_ % (16 * WN) == 0, "split-K epilogue layout");
+};
+
 // STAGES-deep LDS ring (cdna_hip_programming.md "Pipelining across barriers"): tiles kt+1 .. kt+STAGES-2 stay
 // in flight across the barrier that publishes tile kt (counted vmcnt, raw s_barrier); the barrier also retires
 // every wave's reads of tile kt-1, whose buffer the DMA of tile kt+STAGES-1 then reuses.
-template <bool DGRAD, bool PAR, int BM_, int BN_, int WM = 2, int WN = 2, int STAGES = 2, int KS = 64, bool X2 = true>
-__global__ __launch_bounds__(64 * WM * WN, WM * WN >= 16 ? 1 : 2) void conv_pipe_kernel(ConvGeom g) {  // 16 waves: 1 block / CU (2 would spill to scratch)
-  constexpr int WAVES = WM * WN;
+//
+// KG > 1: in-workgroup split-K.  The small-M layers (ResNet18 layer3 / layer4: 12,544 / 4,096 GEMM rows) have one
+// 64 x 128 tile per CU, and one 8-wave tile per CU leaves the K loop latency-bound (0.15-0.18 of the MFMA peak).
+// KG K-groups of WM x WN waves each own a ring of their own and a contiguous 1/KG of the K-steps, all groups stepping
+// through the same barriers; at the end every group stores its fp32 tile to LDS and the WAVES * KG waves re-split the
+// tile (KgLayout), each element summed over the groups in group order -- deterministic, no global partials, and the
+// fused epilogue (BN statistics / BN-backward sums) runs unchanged on the summed tile.
+template <bool DGRAD, bool PAR, int BM_, int BN_, int WM = 2, int WN = 2, int STAGES = 2, int KS = 64, bool X2 = true,
+          int KG = 1>
+// (__launch_bounds__'s second argument is amdgpu_waves_per_eu, a minimum of waves per SIMD: two 8-wave blocks per CU need
+// 4, i.e. <= 128 VGPRs -- with 2, the parity-class dgrad tile took 131 VGPRs and ran one block per CU)
+__global__ __launch_bounds__(64 * WM * WN * KG, conv_pipe_wpe(WM * WN * KG, BM_, BN_, STAGES, DGRAD, PAR)) void conv_pipe_kernel(ConvGeom g) {
+  constexpr int WAVES = WM * WN;  // per K-group
   constexpr int CW = KS / 8, RPG = 64 / CW;  // 16-byte chunks per LDS row, rows per glds instruction
   constexpr int IA = BM_ / RPG / WAVES, IB = BN_ / RPG / WAVES;  // glds per wave per K-tile
   static_assert(IA * RPG * WAVES == BM_ && IB * RPG * WAVES == BN_, "tile rows must split into whole glds pieces");
   static_assert(KS == 64 || KS == 32, "K-tile");
+  static_assert(KG == 1 || KG == 2 || KG == 4, "K-groups");
   constexpr int TM = BM_ / WM, TN = BN_ / WN, FM = TM / 16, FN = TN / 16;
   constexpr int BUF = (BM_ + BN_) * KS;
-  extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  extern __shared__ __attribute__((aligned(16))) bf16_t smem_all[];
+  const int t = threadIdx.x, lane = t & 63, kg = (t >> 6) / WAVES, w = (t >> 6) % WAVES;
+  bf16_t* const smem = smem_all + kg * STAGES * BUF;  // this K-group's ring
   ParClass pc{};
   int M, Kr, rowsH, rowsW;  // this launch's GEMM rows / reduction length, row -> (n, a, b) grid
   int Kr0 = 0;              // PAR: the 3x3 taps' share of Kr (the fused downsample segment follows it in class 0)
@@ -1154,6 +1200,7 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN >= 16 ? 1 : 2) void conv_pipe
   }
   const int nx = (g.Ncols + BN_ - 1) / BN_, ny = (M + BM_ - 1) / BM_;
   if ((int)blockIdx.x >= nx * ny) return;  // grid sized for the largest parity class
+  CTP(0);
   int tx, ty;
   xcd_tile(blockIdx.x, nx, nx * ny, tx, ty);
   const int m0 = ty * BM_, n0 = tx * BN_;
@@ -1229,17 +1276,25 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN >= 16 ? 1 : 2) void conv_pipe
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int fr = lane & 15, fq = lane >> 4;
-  const int nk = (Kr + KS - 1) / KS;
+  // this K-group's K-steps: [kb, kb + nk) of the tile's nk_all; every group runs the loop nkg times (the barriers are
+  // workgroup-wide), a group with fewer steps idles through its last ones
+  const int nk_all = (Kr + KS - 1) / KS;
+  const int nkg = (nk_all + KG - 1) / KG, kb = kg * nkg;
+  const int nk = nk_all - kb < nkg ? (nk_all - kb > 0 ? nk_all - kb : 0) : nkg;
+  const int kofs = kb * KS;
   constexpr int G = IA + IB;
   static_assert(STAGES >= 2 && STAGES <= 4, "ring depth");
 #pragma unroll
   for (int p = 0; p < STAGES - 1; ++p)
-    if (p < nk) stage(p, p * KS);
-  for (int kt = 0; kt < nk; ++kt) {
-    const int ahead = (nk - 1 - kt) < (STAGES - 2) ? (nk - 1 - kt) : (STAGES - 2);
+    if (p < nk) stage(p, kofs + p * KS);
+  CTP(1);
+  for (int kt = 0; kt < nkg; ++kt) {
+    const int left = nk - 1 - kt;
+    const int ahead = left < (STAGES - 2) ? left : (STAGES - 2);
     wait_tiles_in_flight<G>(ahead);
     lds_barrier();
-    if (kt + STAGES - 1 < nk) stage((kt + STAGES - 1) % STAGES, (kt + STAGES - 1) * KS);
+    if (kt + STAGES - 1 < nk) stage((kt + STAGES - 1) % STAGES, kofs + (kt + STAGES - 1) * KS);
+    if (KG > 1 && kt >= nk) continue;
     const bf16_t* la = smem + (kt % STAGES) * BUF;
     const bf16_t* lb = la + BM_ * KS;
 #pragma unroll
@@ -1263,7 +1318,7 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN >= 16 ? 1 : 2) void conv_pipe
       __builtin_amdgcn_s_setprio(0);
     }
   }
-  __syncthreads();  // every wave's last fragment reads are done before the epilogue reuses the ring
+  CTP(2);
 
   // output row -> element offset of the pixel in Y
   auto out_row = [&](int row) -> long {
@@ -1284,11 +1339,82 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN >= 16 ? 1 : 2) void conv_pipe
       }
     return row_id;
   };
+  // One-pass input-gradient epilogues load their operands (residual, its mask, the BN mask and input(s), BN (mean, rstd))
+  // right after the K loop, so the latency hides under the barrier / split-K exchange.  (Loading every pass's operands
+  // there for the multi-pass tiles needs 20 VGPRs per pass: the 128 x 128 tiles then spill.)
+  constexpr int EWF = STAGES * BUF / 2 / WAVES;  // epilogue staging floats per wave
+  const int ct_slot = 10;  // (timing build: stamps inside the epilogue, CT slots 10..12)
+  if constexpr (KG > 1) {  // (the launcher takes KG > 1 only with the 16-byte epilogue)
+    using L = KgLayout<BM_, BN_, WAVES * KG>;
+    constexpr int LDR = BN_ + 4;  // padded fp32 rows: a fragment's 4 row quads fall on distinct bank groups
+    constexpr int TM2 = BM_ / L::WM, TN2 = BN_ / L::WN, FM2 = TM2 / 16, FN2 = TN2 / 16;
+    using E2 = EpiGeo<FM2, FN2, EWF>;
+    const int w2 = t >> 6, wr2 = w2 / L::WN, wc2 = w2 % L::WN;
+    constexpr bool PF = DGRAD && E2::NP == 1;
+    EpiPre<E2::NP> pre;
+    if constexpr (PF)
+      conv_epilogue_prefetch<DGRAD, FM2, FN2, L::WM, L::WN, EWF, decltype(out_row), E2::NP, X2>(g, pre, w2, lane, m0,
+                                                                                                n0, M, out_row);
+    __syncthreads();  // every wave's last fragment reads are done before the exchange reuses the ring
+    float* const part = reinterpret_cast<float*>(smem_all);
+    {
+      float* mine = part + kg * BM_ * LDR;
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) mine[(wr * TM + i * 16 + fq * 4 + r) * LDR + wc * TN + j * 16 + fr] = acc[i][j][r];
+    }
+    lds_barrier();
+    f32x4 acc2[FM2][FN2];
+#pragma unroll
+    for (int i = 0; i < FM2; ++i)
+#pragma unroll
+      for (int j = 0; j < FN2; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int e = (wr2 * TM2 + i * 16 + fq * 4 + r) * LDR + wc2 * TN2 + j * 16 + fr;
+          float s = part[e];
+#pragma unroll
+          for (int q = 1; q < KG; ++q) s += part[q * BM_ * LDR + e];  // group order: fixed
+          acc2[i][j][r] = s;
+        }
+    lds_barrier();  // every wave holds its sums before the epilogue reuses the LDS
+    CTP(3);
+    if constexpr (PF)
+      conv_epilogue_vec<DGRAD, FM2, FN2, L::WM, L::WN, EWF, decltype(out_row), decltype(pre), false, X2>(
+          g, acc2, reinterpret_cast<float*>(smem_all), w2, lane, m0, n0, M, g.bnr_red ? red_row() : 0l, ty, out_row,
+          &pre, ct_slot);
+    else
+      conv_epilogue_vec<DGRAD, FM2, FN2, L::WM, L::WN, EWF, decltype(out_row), EpiNone, false, X2>(
+          g, acc2, reinterpret_cast<float*>(smem_all), w2, lane, m0, n0, M, (DGRAD && g.bnr_red) ? red_row() : 0l, ty,
+          out_row, static_cast<const EpiNone*>(nullptr), ct_slot);
+    CTP(4);
+    return;
+  }
   if (g.vec) {
-    conv_epilogue_vec<DGRAD, FM, FN, WM, WN, STAGES * BUF / 2 / WAVES, decltype(out_row), EpiNone, false, X2>(
-        g, acc, reinterpret_cast<float*>(smem), w, lane, m0, n0, M, (DGRAD && g.bnr_red) ? red_row() : 0l, ty, out_row);
+    using E1 = EpiGeo<FM, FN, EWF>;
+    if constexpr (DGRAD && E1::NP == 1) {
+      EpiPre<E1::NP> pre;
+      conv_epilogue_prefetch<DGRAD, FM, FN, WM, WN, EWF, decltype(out_row), E1::NP, X2>(g, pre, w, lane, m0, n0, M,
+                                                                                         out_row);
+      __syncthreads();  // every wave's last fragment reads are done before the epilogue reuses the ring
+      CTP(3);
+      conv_epilogue_vec<DGRAD, FM, FN, WM, WN, EWF, decltype(out_row), decltype(pre), false, X2>(
+          g, acc, reinterpret_cast<float*>(smem), w, lane, m0, n0, M, g.bnr_red ? red_row() : 0l, ty, out_row, &pre,
+          ct_slot);
+    } else {
+      __syncthreads();  // every wave's last fragment reads are done before the epilogue reuses the ring
+      CTP(3);
+      conv_epilogue_vec<DGRAD, FM, FN, WM, WN, EWF, decltype(out_row), EpiNone, false, X2>(
+          g, acc, reinterpret_cast<float*>(smem), w, lane, m0, n0, M, (DGRAD && g.bnr_red) ? red_row() : 0l, ty,
+          out_row, static_cast<const EpiNone*>(nullptr), ct_slot);
+    }
+    CTP(4);
     return;
   } else {
+  __syncthreads();
 #pragma unroll
   for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -1389,30 +1515,34 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN >= 16 ? 1 : 2) void conv_pipe
   if (g.stats) conv_tile_stats<FM, FN, WM, WN>(g, acc, reinterpret_cast<float*>(smem), w, lane, m0, n0, M, ty);
 }
 
-template <bool DGRAD, bool PAR, int BM_, int BN_, int WM = 2, int WN = 2, int STAGES = 2, int KS = 64>
+template <bool DGRAD, bool PAR, int BM_, int BN_, int WM = 2, int WN = 2, int STAGES = 2, int KS = 64, int KG = 1>
 int launch_conv_pipe_t(ConvGeom& g, hipStream_t st) {
   // PAR: grid.x covers the largest parity class (ph = pw = 0), grid.y = the 4 classes
   const int Mg = PAR ? g.N * ((g.OH + 1) / 2) * ((g.OW + 1) / 2) : g.N * g.OH * g.OW;
   const long tiles = (long)((Mg + BM_ - 1) / BM_) * ((g.Ncols + BN_ - 1) / BN_);
-  const size_t lds = STAGES * (BM_ + BN_) * KS * sizeof(bf16_t);
+  const size_t ring = (size_t)KG * STAGES * (BM_ + BN_) * KS * sizeof(bf16_t);
+  const size_t kgred = KG > 1 ? (size_t)KG * BM_ * (BN_ + 4) * sizeof(float) : 0;  // the split-K tile exchange
+  const size_t lds = ring > kgred ? ring : kgred;
+  if (KG > 1 && !g.vec) return (int)hipErrorInvalidValue;  // the split-K form has the 16-byte epilogue only
   // a stride-1 input gradient whose BN-backward target has no second (downsample) branch runs the instantiation
   // without the x2 terms: 24 fewer VGPRs, which keeps the 8-wave tiles at 2 blocks per CU
   if constexpr (DGRAD && !PAR) {
     if (!g.bnr_x2) {
       if (hipFuncSetAttribute(
-              reinterpret_cast<const void*>(&conv_pipe_kernel<DGRAD, PAR, BM_, BN_, WM, WN, STAGES, KS, false>),
+              reinterpret_cast<const void*>(&conv_pipe_kernel<DGRAD, PAR, BM_, BN_, WM, WN, STAGES, KS, false, KG>),
               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
         return (int)hipErrorInvalidConfiguration;
-      hipLaunchKernelGGL((conv_pipe_kernel<DGRAD, PAR, BM_, BN_, WM, WN, STAGES, KS, false>), dim3((unsigned)tiles, 1),
-                         dim3(64 * WM * WN), lds, st, g);
+      hipLaunchKernelGGL((conv_pipe_kernel<DGRAD, PAR, BM_, BN_, WM, WN, STAGES, KS, false, KG>),
+                         dim3((unsigned)tiles, 1), dim3(64 * WM * WN * KG), lds, st, g);
       return (int)hipGetLastError();
     }
   }
-  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_pipe_kernel<DGRAD, PAR, BM_, BN_, WM, WN, STAGES, KS>),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+  if (hipFuncSetAttribute(
+          reinterpret_cast<const void*>(&conv_pipe_kernel<DGRAD, PAR, BM_, BN_, WM, WN, STAGES, KS, true, KG>),
+          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return (int)hipErrorInvalidConfiguration;
-  hipLaunchKernelGGL((conv_pipe_kernel<DGRAD, PAR, BM_, BN_, WM, WN, STAGES, KS>), dim3((unsigned)tiles, PAR ? 4 : 1),
-                     dim3(64 * WM * WN), lds, st, g);
+  hipLaunchKernelGGL((conv_pipe_kernel<DGRAD, PAR, BM_, BN_, WM, WN, STAGES, KS, true, KG>),
+                     dim3((unsigned)tiles, PAR ? 4 : 1), dim3(64 * WM * WN * KG), lds, st, g);
   return (int)hipGetLastError();
 }
 
@@ -1426,6 +1556,17 @@ int launch_conv_pipe(ConvGeom& g, hipStream_t st, int variant) {
   const long tiles128 = (long)((M + 127) / 128) * ((g.Ncols + bn - 1) / bn) * (PAR ? 4 : 1);
   // below 384 128-row tiles, 64-row tiles (128-row tiles on the deep layers lose 3.5 % of the step)
   const bool small_m = tiles128 < 384;
+  if (variant == 7) {  // in-workgroup split-K (two K-groups) on the 64-row tiles
+    if (bn == 64)
+      return PAR ? launch_conv_pipe_t<DGRAD, PAR, 64, 64, 2, 2, 2, 64, 2>(g, st)
+                 : launch_conv_pipe_t<DGRAD, PAR, 64, 64, 2, 2, 3, 64, 2>(g, st);
+    return PAR ? launch_conv_pipe_t<DGRAD, PAR, 64, 128, 2, 4, 2, 64, 2>(g, st)
+               : launch_conv_pipe_t<DGRAD, PAR, 64, 128, 2, 4, 3, 64, 2>(g, st);
+  }
+  if (variant == 8) {  // in-workgroup split-K (two K-groups) on the 128-row tiles
+    if (bn == 64) return launch_conv_pipe_t<DGRAD, PAR, 128, 64, 4, 2, 2, 64, 2>(g, st);
+    return launch_conv_pipe_t<DGRAD, PAR, 128, 128, 2, 4, 2, 64, 2>(g, st);
+  }
   if (variant == 3 && !small_m) {  // 256-row tiles (8 / 16 waves) for the large-M layers
     // (the 16-wave dgrad tile needs more than 128 VGPRs and would spill to scratch: 8-wave 256 x 64 tiles instead;
     // tools/check_scratch.py keeps every kernel of the library scratch-free)
@@ -1707,6 +1848,21 @@ int launch_conv_halo(ConvGeom& g, hipStream_t st, int kind) {
   return (int)hipErrorInvalidValue;
 }
 
+// Default tile for a non-parity-class conv (forward, or stride-1 input gradient): the in-workgroup split-K forms on the
+// small-M layers -- 64-row tiles with two K-groups (7) when one such tile per CU covers the output (ResNet18 layer4:
+// 256 tiles), else 128-row tiles with two K-groups (8) when those do (layer3: 196 tiles) -- provided each K-group gets
+// >= 4 K-steps; otherwise the one-group tiles (`fallback`).  tools/pipe_phases.py / bench_conv.py at B = 32: layer4
+// 3x3 fwd 44.1 -> 35.8 us, dgrad 52.4 -> 43.1; layer3 3x3 fwd 34.1 -> 28.2, dgrad 40.3 -> 35.7; layer4.0 / layer3.0
+// stride-2 fwd 24.5 -> 20.6 / 19.8 -> 18.1 (profiles/r06/bench_conv_kg.txt).
+int conv_default_variant(const ConvGeom& g, int fallback) {
+  if (!g.vec || g.Kred < 8 * CBK) return fallback;
+  const long M = (long)g.N * g.OH * g.OW;
+  const long nt = (g.Ncols + (g.Ncols <= 64 ? 63 : 127)) / (g.Ncols <= 64 ? 64 : 128);
+  if (((M + 63) / 64) * nt <= cu_count()) return 7;
+  if (((M + 127) / 128) * nt <= cu_count()) return 8;
+  return fallback;
+}
+
 int wgrad_default_variant(int K) {
   (void)K;
   return 4;
@@ -1723,7 +1879,7 @@ MER_API int mer_conv_fwd(int N, int H, int W, int C, int K, int R, int S, int st
 
 MER_API int mer_conv_fwd_ex(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, const void* x,
                             const void* w_packed, void* y, float* stats, int variant, void* stream) {
-  if (C % 8 || variant < -1 || variant > 6) return (int)hipErrorInvalidValue;
+  if (C % 8 || variant < -1 || variant > 8) return (int)hipErrorInvalidValue;
   ConvGeom g{};
   g.N = N; g.IH = H; g.IW = W; g.IC = C;
   g.OH = (H + 2 * pad - R) / stride + 1; g.OW = (W + 2 * pad - S) / stride + 1;
@@ -1737,7 +1893,7 @@ MER_API int mer_conv_fwd_ex(int N, int H, int W, int C, int K, int R, int S, int
     if (hk) return launch_conv_halo<false>(g, (hipStream_t)stream, hk);
   }
   if (variant == 6) return (int)hipErrorInvalidValue;
-  if (variant == -1) variant = 2;
+  if (variant == -1) variant = conv_default_variant(g, 2);
   if (variant == 0) return launch_conv<false>(g, (hipStream_t)stream);
   return launch_conv_pipe<false, false>(g, (hipStream_t)stream, variant);
 }
@@ -1768,7 +1924,7 @@ MER_API int mer_conv_dgrad_ds(int N, int H, int W, int C, int K, int R, int S, i
                               const void* bn_mask, const void* bn_x, const float* bn_ms, float* bn_red,
                               const void* bn_x2, const float* bn_ms2, float* bn_red2, const void* ds_dy,
                               const void* ds_wt_packed, int ds_K, int variant, void* stream) {
-  if (K % 8 || C % 8 || variant < -1 || variant > 6) return (int)hipErrorInvalidValue;
+  if (K % 8 || C % 8 || variant < -1 || variant > 8) return (int)hipErrorInvalidValue;
   const bool auto_variant = variant == -1;
   // 64-channel outputs (layer1, the layer2.0 input gradients): 32-wide K-tiles on a 4-deep ring with 4-wave tiles
   // (tools/bench_conv.py --fused: layer1 101 -> 65 us, layer2.0 s2 74 -> 51, downsample 48 -> 31); wider outputs
@@ -1798,6 +1954,7 @@ MER_API int mer_conv_dgrad_ds(int N, int H, int W, int C, int K, int R, int S, i
     if (hk) return launch_conv_halo<true>(g, (hipStream_t)stream, hk);
   }
   if (variant == 6) return (int)hipErrorInvalidValue;
+  if (auto_variant && stride == 1) variant = conv_default_variant(g, variant);
   if (variant == 0 || stride > 2) return launch_conv<true>(g, (hipStream_t)stream);
   if (stride == 2) return launch_conv_pipe<true, true>(g, (hipStream_t)stream, variant);
   return launch_conv_pipe<true, false>(g, (hipStream_t)stream, variant);

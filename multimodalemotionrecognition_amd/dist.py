@@ -22,6 +22,7 @@ and the only data-path exchange is a SUM all-reduce of ``FusedAdam``'s flat fp32
 from __future__ import annotations
 
 import os
+import time
 from typing import List, Optional, Tuple
 
 import torch
@@ -70,6 +71,49 @@ def _ranges(lo: int, hi: int, n: int) -> List[Tuple[int, int]]:
     return [(i, min(hi, i + n)) for i in range(lo, hi, n)]
 
 
+class CommTimes:
+    """Per-step diagnostics of the gradient all-reduce schedule (bench.py's ``dp`` fields), recorded when
+    ``GradAllReduce(timing=True)``: marks on the compute stream (HIP events; host clock for a CPU / gloo run) at
+
+    * ``hook``: the early bucket's launch point (layer4's backward enqueued, ``grads_ready``),
+    * ``bwd_end``: ``__call__`` entry -- the whole backward is enqueued before it, so on the GPU the event completes
+      when the backward has finished,
+    * ``wait0`` / ``wait1``: around the waits on the launched collectives (for RCCL ``wait()`` makes the compute
+      stream wait for RCCL's stream, so wait0 -> wait1 is the communication the step could not hide).
+
+    ``summary()`` (after a device synchronise): per-step means of ``exposed_ms`` = wait0 -> wait1 and
+    ``early_lead_ms`` = hook -> bwd_end (how long before the backward's end the early bucket went out)."""
+
+    def __init__(self, cuda: bool):
+        self.cuda = cuda
+        self.steps, self.cur = [], {}
+
+    def mark(self, name: str) -> None:
+        if self.cuda:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            self.cur[name] = e
+        else:
+            self.cur[name] = time.perf_counter()
+
+    def end_step(self) -> None:
+        self.steps.append(self.cur)
+        self.cur = {}
+
+    def reset(self) -> None:
+        self.steps, self.cur = [], {}
+
+    def _ms(self, a, b) -> float:
+        return a.elapsed_time(b) if self.cuda else (b - a) * 1e3
+
+    def summary(self) -> dict:
+        exp = [self._ms(s["wait0"], s["wait1"]) for s in self.steps if "wait0" in s and "wait1" in s]
+        lead = [self._ms(s["hook"], s["bwd_end"]) for s in self.steps if "hook" in s and "bwd_end" in s]
+        mean = (lambda v: round(sum(v) / len(v), 4) if v else None)
+        return {"steps": len(self.steps), "allreduce_exposed_ms": mean(exp), "early_bucket_lead_ms": mean(lead),
+                "early_bucket_steps": len(lead)}
+
+
 class GradAllReduce:
     """Bucketed SUM all-reduce of the optimizer's flat gradient buffers; Adam then applies 1/world.
 
@@ -86,10 +130,15 @@ class GradAllReduce:
     chunking, before ``[E, N)``: every rank issues the same sequence of collectives."""
 
     def __init__(self, optimizer, bucket_bytes: int = BUCKET_BYTES, model: Optional[torch.nn.Module] = None,
-                 mask_sync: Optional[bool] = None, early_params=None, force: bool = False):
+                 mask_sync: Optional[bool] = None, early_params=None, force: bool = False, timing: bool = False):
         """``force``: run the bucket / hook / collective path even in a world of one process (an initialised
-        1-rank group: the RCCL wiring test on a single GPU; the sums are identities)."""
+        1-rank group: the RCCL wiring test on a single GPU; the sums are identities).  ``timing``: record
+        ``CommTimes`` marks every step (``self.times``)."""
         self.opt = optimizer
+        self.times = None
+        if timing:
+            flat = optimizer.flat_grads()
+            self.times = CommTimes(bool(flat) and flat[0].is_cuda)
         self.bucket_bytes = bucket_bytes
         self.world = dist.get_world_size() if is_dist() else 1
         self.active = self.world > 1 or (force and dist.is_available() and dist.is_initialized())
@@ -148,6 +197,8 @@ class GradAllReduce:
         Launches ``[0, E)`` of every flat buffer (once per step)."""
         if not self.active:
             return
+        if self.times is not None:
+            self.times.mark("hook")
         self._home_prefix()
         for gi, flat in enumerate(self.opt.flat_grads()):
             end, start = self._early_end.get(gi, 0), self._done.get(gi, 0)
@@ -156,6 +207,8 @@ class GradAllReduce:
                 self._done[gi] = end
 
     def __call__(self) -> None:
+        if self.times is not None and self.active:
+            self.times.mark("bwd_end")
         used = self.opt.gather_grads()
         if not self.active:
             self._done = {}
@@ -171,8 +224,13 @@ class GradAllReduce:
                 self._launch(gi, flat, start, end)
             if max(end, start) < flat.numel():
                 self._launch(gi, flat, max(end, start), flat.numel())
+        if self.times is not None:
+            self.times.mark("wait0")
         for w in self._pending:
             w.wait()
+        if self.times is not None:
+            self.times.mark("wait1")
+            self.times.end_step()
         self._pending, self._done = [], {}
 
 

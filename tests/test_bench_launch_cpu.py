@@ -31,6 +31,18 @@ def test_bench_gpus2_launches_two_ranks():
     line = lines[0]
     assert line["n_gpus"] == 2 and line["ranks_reporting"] == 2 and line["steps"] == 3
     assert line["pid"] != os.getpid()
+    # the DP diagnostics: per-rank step time, exposed all-reduce time and early-bucket lead
+    # from the real GradAllReduce, with the max / min over ranks
+    dp = line["dp"]
+    assert [d["rank"] for d in dp["per_rank"]] == [0, 1]
+    for d in dp["per_rank"]:
+        assert d["step_ms"] > 0 and d["allreduce_exposed_ms"] >= 0 and d["early_bucket_lead_ms"] >= 0
+        assert d["timed_steps"] == 3 and d["early_bucket_steps"] == 3
+    for k in ("step_ms", "allreduce_exposed_ms", "early_bucket_lead_ms"):
+        agg = dp["over_ranks"][k]
+        assert agg["min"] <= agg["max"]
+        assert agg["max"] == max(d[k] for d in dp["per_rank"])
+    assert dp["bytes_allreduced_per_step"] == 4 * (64 * 64 + 64 + 64 * 8 + 8)
 
 
 def test_bench_gpus1_runs_in_process():

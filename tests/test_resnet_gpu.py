@@ -333,6 +333,72 @@ def test_halo_stem_bit_identical(N):
     assert rel_rms(outs[6][0], ref) < 1e-2
 
 
+@pytest.mark.parametrize("N,H,C,Kc,stride", [(8, 7, 256, 256, 1), (16, 4, 512, 512, 1), (8, 14, 128, 256, 2),
+                                              (16, 7, 256, 512, 2), (5, 14, 128, 128, 1), (6, 28, 64, 64, 1),
+                                              (3, 28, 64, 128, 2)])
+@pytest.mark.parametrize("variant", [7, 8])
+def test_conv_split_k_groups(N, H, C, Kc, stride, variant):
+    """In-workgroup split-K (variants 7 / 8: two K-groups of waves, each a contiguous half of the K-steps on its own LDS
+    ring, tiles summed in group order in LDS) against the one-group kernel (variant 2) on the same tiles: the only
+    difference is where the fp32 sum splits, so outputs agree to one bf16 rounding and the fused BN statistics /
+    BN-backward sums (two BNs, residual under a ReLU mask, the stride-2 parity classes and the fused downsample
+    segment) to fp32 rounding; every launch is bitwise repeatable.  Also against torch."""
+    from multimodalemotionrecognition_amd import kernels as K
+
+    torch.manual_seed(11)
+    Ho = (H + 2 - 3) // stride + 1
+    x = torch.randn(N, H, H, C, device="cuda").bfloat16()
+    w = torch.randn(Kc, C, 3, 3, device="cuda") / (9 * C) ** 0.5
+    wp = torch.empty(Kc, 9 * C, device="cuda", dtype=torch.bfloat16)
+    K.pack_conv_weight(w, wp, C, False)
+    wt = torch.empty(C, 9 * Kc, device="cuda", dtype=torch.bfloat16)
+    K.pack_conv_weight(w, wt, C, True)
+    M, Mi = N * Ho * Ho, N * H * H
+
+    def fwd(v):
+        y = torch.full((N, Ho, Ho, Kc), float("nan"), device="cuda", dtype=torch.bfloat16)
+        st = K.bn_stats_buffer(Kc, "cuda", M)
+        K.conv_fwd(x, wp, y, st, 3, 3, stride, 1, variant=v)
+        return y, st.sum(0)
+
+    (y2, s2), (yk, sk), (yk2, sk2) = fwd(2), fwd(variant), fwd(variant)
+    assert torch.equal(yk, yk2) and torch.equal(sk, sk2)
+    assert rel_rms(yk, y2) < 4e-3
+    assert (yk.float() - y2.float()).abs().max() <= 2 ** -6 * y2.float().abs().max()
+    assert torch.allclose(sk, s2, rtol=1e-3, atol=0.5)
+    ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.bfloat16().float(), stride=stride, padding=1).permute(0, 2, 3, 1)
+    assert rel_rms(yk, ref) < 1e-2
+    dy = torch.randn(N, Ho, Ho, Kc, device="cuda").bfloat16()
+    mask = torch.randn(N, H, H, C, device="cuda").bfloat16()
+    xb = torch.randn(N, H, H, C, device="cuda").bfloat16()
+    xb2 = torch.randn(N, H, H, C, device="cuda").bfloat16()
+    ms = torch.stack([torch.randn(C), torch.rand(C) + 0.5], 1).cuda().contiguous()
+    ms2 = torch.stack([torch.randn(C), torch.rand(C) + 0.5], 1).cuda().contiguous()
+    kw = {}
+    if stride == 2 and Kc % 64 == 0:  # the fused 1x1 / stride-2 downsample segment of parity class (0, 0)
+        wd = torch.randn(Kc, C, 1, 1, device="cuda") / C ** 0.5
+        wdt = torch.empty(C, Kc, device="cuda", dtype=torch.bfloat16)
+        K.pack_conv_weight(wd, wdt, C, True)
+        kw["ds"] = (torch.randn(N, Ho, Ho, Kc, device="cuda").bfloat16(), wdt)
+    else:
+        kw.update(residual=torch.randn(N, H, H, C, device="cuda").bfloat16(), mask=mask)
+
+    def bwd(v, two):
+        dx = torch.full((N, H, H, C), float("nan"), device="cuda", dtype=torch.bfloat16)
+        rows = K.bn_red_rows(Mi)
+        red, red2 = torch.zeros(rows, C, 2, device="cuda"), torch.zeros(rows, C, 2, device="cuda")
+        bnr = (mask, xb, ms, red, xb2, ms2, red2) if two else (mask, xb, ms, red)
+        K.conv_dgrad(dy, wt, dx, 3, 3, stride, 1, variant=v, bnr=bnr, **kw)
+        return dx, red.sum(0), red2.sum(0)
+
+    for two in (False, True):
+        a, b, c = bwd(2, two), bwd(variant, two), bwd(variant, two)
+        assert all(torch.equal(p, q) for p, q in zip(b, c))
+        assert rel_rms(b[0], a[0]) < 4e-3
+        for p, q in zip(a[1:], b[1:]):
+            assert torch.allclose(p, q, rtol=1e-3, atol=0.5)
+
+
 @pytest.mark.parametrize("stride,ds", [(1, False), (2, True)])
 def test_dgrad_fused_bn_reduce_matches_standalone(stride, ds):
     """mer_conv_dgrad_bnr's epilogue reduction == mer_bn_bwd_reduce over the stored gradient (both BNs)."""

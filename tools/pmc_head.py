@@ -44,6 +44,24 @@ def run():
     print(f"ran {3 + ITERS} fused head steps", flush=True)
 
 
+def kernel_key(full: str) -> str:
+    """Kernel name without its argument list, return type and namespace: a demangled name can begin with
+    "void (anonymous namespace)::...", whose FIRST "(" is the namespace's, not the argument list's -- cutting there
+    dropped every anonymous-namespace kernel (F1's bf16 GEMM among them) from the sums."""
+    name = full.replace("(anonymous namespace)::", "")
+    depth, cut = 0, len(name)
+    for i, ch in enumerate(name):  # the argument list is the first "(" outside template brackets
+        if ch == "<":
+            depth += 1
+        elif ch == ">":
+            depth -= 1
+        elif ch == "(" and depth == 0:
+            cut = i
+            break
+    name = name[:cut]
+    return name[5:] if name.startswith("void ") else name
+
+
 def summarize(root):
     per = defaultdict(lambda: defaultdict(float))   # kernel -> counter -> sum over dispatches
     disp = defaultdict(set)
@@ -51,7 +69,7 @@ def summarize(root):
     rows = defaultdict(lambda: defaultdict(float))
     for f in glob.glob(f"{root}/**/*counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(f)):
-            name = r["Kernel_Name"].split("(")[0].replace("void ", "")
+            name = kernel_key(r["Kernel_Name"])
             if not any(k in name for k in HEAD_KERNELS):
                 continue
             rows[(r["Dispatch_Id"], name)][r["Counter_Name"]] += float(r["Counter_Value"])

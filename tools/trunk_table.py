@@ -118,11 +118,12 @@ def main():
     other = {}
     for r in win:
         n = r["Kernel_Name"]
-        if any(s in n for s in ("bn_", "wgrad_reduce", "wgrad_scatter", "pack_w", "pack_input", "stem_", "maxpool",
-                                "avgpool", "partials_sum")):
+        if any(s in n for s in ("bn_", "wgrad_reduce", "wgrad_scatter", "wgrad_fold", "pack_w", "pack_input", "stem_",
+                                "maxpool", "avgpool", "partials_sum")):
             key = n.split("(")[0][:60]
             other[key] = other.get(key, 0.0) + dur(r)
-    print(f"# conv total {sum(tot.values()):.1f} us; BN / pack / reduce / pool kernels {sum(other.values()):.1f} us:")
+    print(f"# conv total {sum(tot.values()):.1f} us; BN / pack / weight-gradient fold / pool kernels "
+          f"{sum(other.values()):.1f} us; serialized trunk {sum(tot.values()) + sum(other.values()):.1f} us:")
     for k, v in sorted(other.items(), key=lambda kv: -kv[1]):
         print(f"#   {v:8.1f} us  {k}")
 
