@@ -284,13 +284,13 @@ def roof_core(core_ms, peak_split):
                         "runs its out-projection, residual + LayerNorm; the whole duration is charged to the core)"}
 
 
-CORE_ATTN_FILE = Path(__file__).resolve().parent / "profiles" / "r05" / "core_attn.json"
+CORE_ATTN_FILE = Path(__file__).resolve().parent / "profiles" / "r06" / "core_attn.json"
 
 
 def roof_core_attn(peak_split):
     """The ``roofline_head.core_attn`` entry: the attention cores' FLOPs over the QK^T / softmax / PV phases alone
     (their backward too) -- phase stamps of the timing build (tools/xt_phases.py ... core), committed as
-    profiles/r05/core_attn.json; the four kernels' out-projection / residual / LayerNorm phases are excluded."""
+    profiles/r06/core_attn.json; the four kernels' out-projection / residual / LayerNorm phases are excluded."""
     if not CORE_ATTN_FILE.exists():
         return None
     rec = json.loads(CORE_ATTN_FILE.read_text())
@@ -302,7 +302,7 @@ def roof_core_attn(peak_split):
     return {"bound": "mfma" if peak_split < ai * PEAK_HBM_GBS / 1e3 else "hbm", "achieved": round(ach, 3),
             "peak": round(attain, 2), "unit": "TFLOP/s", "frac": round(ach / attain, 4), "ms": round(ms, 4),
             "kernel_us": {k: v["core_us"] for k, v in rec["kernels"].items()},
-            "source": "profiles/r05/core_attn.json (" + rec["method"] + ")"}
+            "source": "profiles/r06/core_attn.json (" + rec["method"] + ")"}
 
 
 def time_head_core(model, dev, reps: int):

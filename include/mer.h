@@ -191,8 +191,11 @@ int mer_gemm_bf16(int M, int N, int K, const void* A, long a_gstride, long a_rst
  * CU-time pick (every shape on the 256x256 split ring: the train step's side-stream encoder forward), 0 the
  * 128x128 register-staged kernel (any K % 8 == 0), and the global_load_lds pipelined kernel as 7 (128x64 tiles,
  * 3-deep ring), 9 (128x128, 8 waves, 2-deep), 13 (256x256, 16 waves, 2-deep), 18 (256x256, 16 waves, split
- * rings: A 3-deep, B 2-deep).  K % 64 == 0 for 7-18, otherwise variant 0 runs.  Every variant gives the same
- * bits.  Other values: hipErrorInvalidValue. */
+ * rings: A 3-deep, B 2-deep), 22 (v18 with the LDS-DMA issued between the MFMA rows) and 23 (v22 on operand-
+ * swapped MFMA: a bf16 output without residual or dropout is rounded before the LDS staging).  The automatic picks
+ * send the split-ring shapes to v23 / v22 (v23 where its epilogue applies): -1 wherever it picks the split ring,
+ * -2 for N <= 512 (the feature-extractor convs; the encoder layers keep v18).  K % 64 == 0 for 7-23, otherwise
+ * variant 0 runs.  Every variant gives the same bits.  Other values: hipErrorInvalidValue. */
 int mer_gemm_bf16_ex(int M, int N, int K, const void* A, long a_gstride, long a_rstride, int a_rpg, const void* W,
                      long ldw, void* C, int c_dtype, long ldc, const float* bias, const void* R, long ldr, int act,
                      int variant, void* stream);
@@ -542,7 +545,9 @@ int mer_xh_split(int n_items, const long long* desc, void* stream);
 
 /* F1 from a precomputed first product: pair [M][ldp] fp32 holds aseq Ws_hi^T in columns 0..127 and aseq Ws_lo^T in
  * 128..255 (one mer_gemm_bf16 of the bf16 WavLM features with the stacked [hi; lo] planes of audio_seq_proj);
- * a_s = pair[:, :128] + pair[:, 128:] + bs, then a, q2, kv1 and the video rows exactly as mer_xh_audio_fwd. */
+ * a_s = pair[:, :128] + pair[:, 128:] + bs, then a, q2, kv1 and the video rows as mer_xh_audio_fwd does.  The two
+ * halves are summed after their K loops, where mer_xh_audio_fwd folds hi and lo into one running sum per k step, so
+ * the two entries agree to fp32 rounding, not bit for bit (tests/test_xattn_fused_gpu.py::test_f1_pair_matches_in_kernel). */
 int mer_xh_audio_fwd_pair(int M, const float* pair, long ldp, const float* bs, const void* Wa_hi, const void* Wa_lo,
                           const float* ba, const void* Wc_hi, const void* Wc_lo, const float* bq2, const float* bkv1,
                           float* a_s, float* a, float* q2, float* kv1, int Mv, int vdim, const float* vfeat,

@@ -1563,6 +1563,10 @@ int launch_conv_pipe(ConvGeom& g, hipStream_t st, int variant) {
     return PAR ? launch_conv_pipe_t<DGRAD, PAR, 64, 128, 2, 4, 2, 64, 2>(g, st)
                : launch_conv_pipe_t<DGRAD, PAR, 64, 128, 2, 4, 3, 64, 2>(g, st);
   }
+  if (variant == 9) {  // (A/B) variant 2's tiles without the x2 exception: 128 x 128 for the two-BN stride-1 dgrad
+    if (bn == 64) return launch_conv_pipe_t<DGRAD, PAR, 128, 64, 4, 2>(g, st);
+    return launch_conv_pipe_t<DGRAD, PAR, 128, 128, 2, 4>(g, st);
+  }
   if (variant == 8) {  // in-workgroup split-K (two K-groups) on the 128-row tiles
     if (bn == 64) return launch_conv_pipe_t<DGRAD, PAR, 128, 64, 4, 2, 2, 64, 2>(g, st);
     return launch_conv_pipe_t<DGRAD, PAR, 128, 128, 2, 4, 2, 64, 2>(g, st);
@@ -1599,12 +1603,12 @@ int launch_conv_pipe(ConvGeom& g, hipStream_t st, int variant) {
       return small_m ? (PAR ? launch_conv_pipe_t<DGRAD, PAR, 64, 64, 2, 2>(g, st)
                             : launch_conv_pipe_t<DGRAD, PAR, 64, 64, 2, 2, 3>(g, st))
                      : launch_conv_pipe_t<DGRAD, PAR, 128, 64, 4, 2>(g, st);
-    // a stride-1 input gradient with a second BN-backward branch (x2: the block-0 output of layers 2-4) needs 138
-    // VGPRs on the 128 x 128 tile (1 block per CU): it takes the 64 x 128 tile (115 VGPRs, 2 blocks per CU)
-    const bool x2_tile = DGRAD && !PAR && g.bnr_x2 != nullptr;
-    return (small_m || x2_tile) ? (PAR ? launch_conv_pipe_t<DGRAD, PAR, 64, 128, 2, 4>(g, st)
-                                       : launch_conv_pipe_t<DGRAD, PAR, 64, 128, 2, 4, 3>(g, st))
-                                : launch_conv_pipe_t<DGRAD, PAR, 128, 128, 2, 4>(g, st);
+    // (a stride-1 input gradient with a second BN-backward branch -- x2: the block-0 output of layers 2-4 -- used to
+    // take the 64 x 128 tile because the 128 x 128 one needed 138 VGPRs; bounded to 128 (conv_pipe_wpe) it runs two
+    // blocks per CU without spilling: layer2.1.conv1's dgrad 54.0 -> 39.4 us, profiles/r06/bench_conv_x2.txt)
+    return small_m ? (PAR ? launch_conv_pipe_t<DGRAD, PAR, 64, 128, 2, 4>(g, st)
+                          : launch_conv_pipe_t<DGRAD, PAR, 64, 128, 2, 4, 3>(g, st))
+                   : launch_conv_pipe_t<DGRAD, PAR, 128, 128, 2, 4>(g, st);
   }
   if (bn == 64)
     return small_m ? launch_conv_pipe_t<DGRAD, PAR, 64, 64>(g, st) : launch_conv_pipe_t<DGRAD, PAR, 128, 64>(g, st);
@@ -1879,7 +1883,7 @@ MER_API int mer_conv_fwd(int N, int H, int W, int C, int K, int R, int S, int st
 
 MER_API int mer_conv_fwd_ex(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, const void* x,
                             const void* w_packed, void* y, float* stats, int variant, void* stream) {
-  if (C % 8 || variant < -1 || variant > 8) return (int)hipErrorInvalidValue;
+  if (C % 8 || variant < -1 || variant > 9) return (int)hipErrorInvalidValue;
   ConvGeom g{};
   g.N = N; g.IH = H; g.IW = W; g.IC = C;
   g.OH = (H + 2 * pad - R) / stride + 1; g.OW = (W + 2 * pad - S) / stride + 1;
@@ -1924,7 +1928,7 @@ MER_API int mer_conv_dgrad_ds(int N, int H, int W, int C, int K, int R, int S, i
                               const void* bn_mask, const void* bn_x, const float* bn_ms, float* bn_red,
                               const void* bn_x2, const float* bn_ms2, float* bn_red2, const void* ds_dy,
                               const void* ds_wt_packed, int ds_K, int variant, void* stream) {
-  if (K % 8 || C % 8 || variant < -1 || variant > 8) return (int)hipErrorInvalidValue;
+  if (K % 8 || C % 8 || variant < -1 || variant > 9) return (int)hipErrorInvalidValue;
   const bool auto_variant = variant == -1;
   // 64-channel outputs (layer1, the layer2.0 input gradients): 32-wide K-tiles on a 4-deep ring with 4-wave tiles
   // (tools/bench_conv.py --fused: layer1 101 -> 65 us, layer2.0 s2 74 -> 51, downsample 48 -> 31); wider outputs

@@ -703,9 +703,10 @@ using CfgT3 = PipeCfg<128, 64, 2, 2, 3>;   // v7: 128x64 tiles, 3-deep ring, 72 
 using CfgW2 = PipeCfg<128, 128, 2, 4, 2>;  // v9: 8 waves (64x32 each), 2-deep, 64 KiB LDS (2 blocks / CU)
 using CfgY2 = PipeCfg<256, 256, 4, 4, 2>;  // v13: 16 waves (64x64 each), 2-deep, 128 KiB LDS
 using CfgY32 = PipeCfg<256, 256, 4, 4, 2, 64, 3>;  // v18: 16 waves, A 3-deep + B 2-deep rings, 160 KiB LDS
-using CfgY32s = PipeCfg<256, 256, 4, 4, 2, 64, 3, 1>;  // v21: v18 operand-swapped (bf16 staging, see the epilogue)
 using CfgY32i = PipeCfg<256, 256, 4, 4, 2, 64, 3, 0, 1>;  // v22: v18, DMA issue between MFMA rows
-using CfgY32si = PipeCfg<256, 256, 4, 4, 2, 64, 3, 1, 1>;  // v23: v21, DMA issue between MFMA rows
+// v23: v18 operand-swapped (bf16 staging, see the epilogue) with the DMA issued between MFMA rows.  (The swapped form
+// without the DMA interleave, v21, lost its train-step A/B and was never picked: removed in round 6.)
+using CfgY32si = PipeCfg<256, 256, 4, 4, 2, 64, 3, 1, 1>;
 
 template <class CF, typename TOUT, int AMODE>
 int launch_pipe_t(const GemmArgs& g, int groups, hipStream_t st) {
@@ -791,7 +792,7 @@ MER_API int mer_gemm_bf16_tr(int M, int N, int K, const void* A, long a_gstride,
   if (drop_p < 0.f || drop_p >= 1.f || (drop_p > 0.f && !drop_seed) || skip_bit < 0 || skip_bit > 62)
     return (int)hipErrorInvalidValue;
   if (!(variant == -2 || variant == -1 || variant == 0 || variant == 7 || variant == 9 || variant == 13 ||
-        variant == 18 || variant == 21 || variant == 22 || variant == 23))
+        variant == 18 || variant == 22 || variant == 23))
     return (int)hipErrorInvalidValue;
   if (K % 8 != 0 || a_rpg <= 0 || (a_rstride % 8) != 0 || (a_gstride % 8) != 0 || (ldw % 8) != 0)
     return (int)hipErrorInvalidValue;
@@ -834,7 +835,6 @@ MER_API int mer_gemm_bf16_tr(int M, int N, int K, const void* A, long a_gstride,
     case 9: return launch_pipe<CfgW2>(g, c_dtype, st);
     case 13: return launch_pipe<CfgY2>(g, c_dtype, st);
     case 18: return launch_pipe<CfgY32>(g, c_dtype, st);
-    case 21: return launch_pipe<CfgY32s>(g, c_dtype, st);
     case 22: return launch_pipe<CfgY32i>(g, c_dtype, st);
     case 23: return launch_pipe<CfgY32si>(g, c_dtype, st);
     default: return launch<0>(g, c_dtype, 1, st);

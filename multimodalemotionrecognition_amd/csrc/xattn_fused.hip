@@ -513,78 +513,85 @@ constexpr int F2_KT = 10;  // 16-key tiles of the v2a attention (Ta <= 160: F4 f
 // keys --; F2b = its out-projection, drop-path + residual + LayerNorm, v-pool and [k2 v2] projection, one
 // workgroup per sample.
 //
-// F2a: wave w owns the 32-key chunks c = w, w + 4, ... of the sample's Ta keys.  Scores S = Q_h K^T (+ the
-// emotion-prior bias), the row max and then the row sum of exp(S - max) meet across the 4 waves in LDS (wave
-// order), P = exp / sum is saved (pre-dropout, as the unfused schedule saves it), and each wave's P' V_h partial
-// is summed in wave order into o1's 32 columns of head h.  Loads are issued up front (one memory latency).
+// F2a: wave w owns the 32-key chunk c = w of the sample's Ta keys (8 waves: Ta <= 256; with 4 waves and two chunks on
+// wave 0 at Ta = 149, the PV phase of that wave set the block time -- tools/xt_phases.py: 3.0 of 7.4 us).  Scores
+// S = Q_h K^T (+ the emotion-prior bias), the row max and then the row sum of exp(S - max) meet across the waves in LDS
+// (fixed order), P = exp / sum is saved (pre-dropout, as the unfused schedule saves it), and each wave's P' V_h partial
+// is summed in a fixed order into o1's 32 columns of head h.  Loads are issued up front (one memory latency).
 // ---------------------------------------------------------------------------------------------
-constexpr int F2A_MAXC = 2;               // 32-key chunks per wave: Ta <= 4 * 2 * 32 = 256
+constexpr int F2A_W = 8;                  // waves = 32-key chunks: Ta <= F2A_W * 32 = 256
 constexpr int F2A_PLD = 36;               // P' chunk stride
 
-__global__ __launch_bounds__(256) void xh_v2a_attn_kernel(int T, int Ta, const float* __restrict__ q1,
-                                                          const float* __restrict__ kv1, XhDrop dr, float scale,
-                                                          float* __restrict__ P1, float* __restrict__ o1,
-                                                          const float* __restrict__ bias) {
-  __shared__ float red[2][4][16];                                   // per-wave row max / row sum
-  __shared__ __attribute__((aligned(16))) float PL[4][16 * F2A_PLD];  // per-wave P' chunk (PV A operand)
-  __shared__ float oP[4][16][33];                                   // per-wave P' V partials
+// fixed-order sum of v[0..N) (N a power of two): pairwise, the same tree whatever the wave schedule
+template <int N>
+__device__ __forceinline__ float tree_sum(const float* v, int stride) {
+  if constexpr (N == 1) {
+    return v[0];
+  } else {
+    return tree_sum<N / 2>(v, stride) + tree_sum<N / 2>(v + (N / 2) * stride, stride);
+  }
+}
+
+__global__ __launch_bounds__(64 * F2A_W) void xh_v2a_attn_kernel(int T, int Ta, const float* __restrict__ q1,
+                                                                 const float* __restrict__ kv1, XhDrop dr, float scale,
+                                                                 float* __restrict__ P1, float* __restrict__ o1,
+                                                                 const float* __restrict__ bias) {
+  __shared__ float red[2][F2A_W][16];                                    // per-wave row max / row sum
+  __shared__ __attribute__((aligned(16))) float PL[F2A_W][16 * F2A_PLD];  // per-wave P' chunk (PV A operand)
+  __shared__ float oP[F2A_W][16][33];                                    // per-wave P' V partials
   XT(3, 0);
   const int b = blockIdx.x >> 2, h = blockIdx.x & 3;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, fr = lane & 15, fq = lane >> 4, fk = fq * 8;
   const long ldkv = 2 * XD;
   const float* Kr = kv1 + (long)b * Ta * ldkv + h * XDH;       // key j: Kr[j * ldkv + d]
   const float* Vr = Kr + XD;                                   // value j: Vr[j * ldkv + d]
-  const int nch = (Ta + 31) / 32;
+  const int c = w;                                             // this wave's chunk
+  const bool live = 32 * c < Ta;                               // (wave-uniform)
   const unsigned long long dseed = mer_site_seed(dr.seed, dr.site_attn);
-  // every global load first: K fragments and V gathers of this wave's chunks (clamped rows), the prior bias
-  f32x4 kraw[F2A_MAXC][2][2];
-  float vraw[F2A_MAXC][2][8];
-  float bv[F2A_MAXC][2][4];
+  // every global load first: K fragments and V gathers of this wave's chunk (clamped rows), the prior bias
+  f32x4 kraw[2][2];
+  float vraw[2][8];
+  float bv[2][4];
 #pragma unroll
-  for (int ci = 0; ci < F2A_MAXC; ++ci) {
-    const int c = w + 4 * ci;
+  for (int tt = 0; tt < 2; ++tt) {
+    const int j = 32 * c + 16 * tt + fr, jc = j < Ta ? j : Ta - 1;
+    kraw[tt][0] = *reinterpret_cast<const f32x4*>(Kr + (long)jc * ldkv + fk);
+    kraw[tt][1] = *reinterpret_cast<const f32x4*>(Kr + (long)jc * ldkv + fk + 4);
 #pragma unroll
-    for (int tt = 0; tt < 2; ++tt) {
-      const int j = 32 * c + 16 * tt + fr, jc = j < Ta ? j : Ta - 1;
-      kraw[ci][tt][0] = *reinterpret_cast<const f32x4*>(Kr + (long)jc * ldkv + fk);
-      kraw[ci][tt][1] = *reinterpret_cast<const f32x4*>(Kr + (long)jc * ldkv + fk + 4);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int i = 4 * fq + r;
-        const long bi = ((long)b * T + (i < T ? i : T - 1)) * Ta + jc;
-        bv[ci][tt][r] = bias ? bias[bi] : 0.f;
-      }
+    for (int r = 0; r < 4; ++r) {
+      const int i = 4 * fq + r;
+      const long bi = ((long)b * T + (i < T ? i : T - 1)) * Ta + jc;
+      bv[tt][r] = bias ? bias[bi] : 0.f;
     }
-#pragma unroll
-    for (int jt = 0; jt < 2; ++jt)
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int kk = 32 * c + fk + e;
-        vraw[ci][jt][e] = Vr[(long)(kk < Ta ? kk : Ta - 1) * ldkv + 16 * jt + fr];
-      }
   }
+#pragma unroll
+  for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int kk = 32 * c + fk + e;
+      vraw[jt][e] = Vr[(long)(kk < Ta ? kk : Ta - 1) * ldkv + 16 * jt + fr];
+    }
   bf16x8 qh, ql;
   frag_row(q1 + ((long)b * T + (fr < T ? fr : T - 1)) * XD + h * XDH + fk, fr < T, qh, ql);
-  f32x4 s[F2A_MAXC][2];
+  XT(3, 1);
+  f32x4 s[2];
   float mx[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
 #pragma unroll
-  for (int ci = 0; ci < F2A_MAXC; ++ci)
+  for (int tt = 0; tt < 2; ++tt) {
+    const int j = 32 * c + 16 * tt + fr;
+    float x[8] = {kraw[tt][0][0], kraw[tt][0][1], kraw[tt][0][2], kraw[tt][0][3],
+                  kraw[tt][1][0], kraw[tt][1][1], kraw[tt][1][2], kraw[tt][1][3]};
 #pragma unroll
-    for (int tt = 0; tt < 2; ++tt) {
-      const int j = 32 * (w + 4 * ci) + 16 * tt + fr;
-      float x[8] = {kraw[ci][tt][0][0], kraw[ci][tt][0][1], kraw[ci][tt][0][2], kraw[ci][tt][0][3],
-                    kraw[ci][tt][1][0], kraw[ci][tt][1][1], kraw[ci][tt][1][2], kraw[ci][tt][1][3]};
+    for (int e = 0; e < 8; ++e) x[e] = j < Ta ? x[e] : 0.f;
+    bf16x8 bh, bl;
+    split8(x, bh, bl);
+    s[tt] = mma3(qh, ql, bh, bl, f32x4{0.f, 0.f, 0.f, 0.f});
 #pragma unroll
-      for (int e = 0; e < 8; ++e) x[e] = j < Ta ? x[e] : 0.f;
-      bf16x8 bh, bl;
-      split8(x, bh, bl);
-      s[ci][tt] = mma3(qh, ql, bh, bl, f32x4{0.f, 0.f, 0.f, 0.f});
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        s[ci][tt][r] = j < Ta ? s[ci][tt][r] * scale + bv[ci][tt][r] : -INFINITY;
-        mx[r] = fmaxf(mx[r], s[ci][tt][r]);
-      }
+    for (int r = 0; r < 4; ++r) {
+      s[tt][r] = j < Ta ? s[tt][r] * scale + bv[tt][r] : -INFINITY;
+      mx[r] = fmaxf(mx[r], s[tt][r]);
     }
+  }
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
 #pragma unroll
@@ -596,20 +603,21 @@ __global__ __launch_bounds__(256) void xh_v2a_attn_kernel(int T, int Ta, const f
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int i = 4 * fq + r;
-    mx[r] = fmaxf(fmaxf(red[0][0][i], red[0][1][i]), fmaxf(red[0][2][i], red[0][3][i]));
+    float m = red[0][0][i];
+#pragma unroll
+    for (int q = 1; q < F2A_W; ++q) m = fmaxf(m, red[0][q][i]);
+    mx[r] = m;
     sum[r] = 0.f;
   }
 #pragma unroll
-  for (int ci = 0; ci < F2A_MAXC; ++ci)
+  for (int tt = 0; tt < 2; ++tt)
 #pragma unroll
-    for (int tt = 0; tt < 2; ++tt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int j = 32 * (w + 4 * ci) + 16 * tt + fr;
-        const float e = j < Ta ? __expf(s[ci][tt][r] - mx[r]) : 0.f;
-        s[ci][tt][r] = e;
-        sum[r] += e;
-      }
+    for (int r = 0; r < 4; ++r) {
+      const int j = 32 * c + 16 * tt + fr;
+      const float e = j < Ta ? __expf(s[tt][r] - mx[r]) : 0.f;
+      s[tt][r] = e;
+      sum[r] += e;
+    }
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
 #pragma unroll
@@ -618,17 +626,12 @@ __global__ __launch_bounds__(256) void xh_v2a_attn_kernel(int T, int Ta, const f
   }
   __syncthreads();
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int i = 4 * fq + r;
-    sum[r] = (red[1][0][i] + red[1][1][i]) + (red[1][2][i] + red[1][3][i]);
-  }
+  for (int r = 0; r < 4; ++r) sum[r] = tree_sum<F2A_W>(&red[1][0][4 * fq + r], 16);
+  XT(3, 2);
   // P (saved, pre-dropout), P' = dropout(P) through LDS into O_w = P'_w V_w
   f32x4 o[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
   float* pl = PL[w];
-#pragma unroll
-  for (int ci = 0; ci < F2A_MAXC; ++ci) {
-    const int c = w + 4 * ci;
-    if (c >= nch) break;  // (wave-uniform)
+  if (live) {
 #pragma unroll
     for (int tt = 0; tt < 2; ++tt)
 #pragma unroll
@@ -636,7 +639,7 @@ __global__ __launch_bounds__(256) void xh_v2a_attn_kernel(int T, int Ta, const f
         const int i = 4 * fq + r, j = 32 * c + 16 * tt + fr;
         float pd = 0.f;
         if (i < T && j < Ta) {
-          const float pr = s[ci][tt][r] / sum[r];
+          const float pr = s[tt][r] / sum[r];
           const long pi = (((long)b * XH + h) * T + i) * Ta + j;
           P1[pi] = pr;
           pd = pr * dropout_scale(dseed, pi, dr.attn);
@@ -650,23 +653,23 @@ __global__ __launch_bounds__(256) void xh_v2a_attn_kernel(int T, int Ta, const f
     for (int jt = 0; jt < 2; ++jt) {
       float x[8];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) x[e] = 32 * c + fk + e < Ta ? vraw[ci][jt][e] : 0.f;
+      for (int e = 0; e < 8; ++e) x[e] = 32 * c + fk + e < Ta ? vraw[jt][e] : 0.f;
       bf16x8 bh, bl;
       split8(x, bh, bl);
       o[jt] = mma3(ah, al, bh, bl, o[jt]);
     }
-    wave_sync_lds();  // the next chunk overwrites pl
   }
+  XT(3, 3);
 #pragma unroll
   for (int jt = 0; jt < 2; ++jt)
 #pragma unroll
     for (int r = 0; r < 4; ++r) oP[w][4 * fq + r][16 * jt + fr] = o[jt][r];
   __syncthreads();
-  for (int e = threadIdx.x; e < T * XDH; e += 256) {
+  for (int e = threadIdx.x; e < T * XDH; e += 64 * F2A_W) {
     const int i = e / XDH, d = e - i * XDH;
-    o1[((long)b * T + i) * XD + h * XDH + d] = (oP[0][i][d] + oP[1][i][d]) + (oP[2][i][d] + oP[3][i][d]);
+    o1[((long)b * T + i) * XD + h * XDH + d] = tree_sum<F2A_W>(&oP[0][i][d], 16 * 33);
   }
-  XT(3, 1);
+  XT(3, 4);
 }
 
 // F2b: F2's second half on o1 (one workgroup per sample): v2 = o1 Wo1^T + bo1, v1 = LN(v + keep_b v2), v-pool,
@@ -738,11 +741,11 @@ MER_API int mer_xh_v2a_fwd(int B, int T, int Ta, const float* v, const float* q1
                             float scale, float* P1, float* o1, float* s_v, float* mean_v, float* rstd_v, float* v1,
                             float* kv2, float* emb, long ld_emb, const float* bias, void* stream) {
   if (B <= 0) return 0;
-  if (T <= 0 || T > 16 || Ta <= 0 || Ta > 4 * F2A_MAXC * 32) return (int)hipErrorInvalidValue;
+  if (T <= 0 || T > 16 || Ta <= 0 || Ta > F2A_W * 32) return (int)hipErrorInvalidValue;
   if ((attn_p > 0.f || path_p > 0.f) && !seed) return (int)hipErrorInvalidValue;
   XhDrop dr{attn_p, path_p, seed, site_attn, site_path};
-  hipLaunchKernelGGL(xh_v2a_attn_kernel, dim3(B * XH), dim3(256), 0, (hipStream_t)stream, T, Ta, q1, kv1, dr, scale,
-                     P1, o1, bias);
+  hipLaunchKernelGGL(xh_v2a_attn_kernel, dim3(B * XH), dim3(64 * F2A_W), 0, (hipStream_t)stream, T, Ta, q1, kv1, dr,
+                     scale, P1, o1, bias);
   hipLaunchKernelGGL(xh_v2a_post_kernel, dim3(B), dim3(256), 0, (hipStream_t)stream, T, v, o1,
                      SplitW{(const bf16_t*)Wo1_hi, (const bf16_t*)Wo1_lo}, bo1, gamma, beta,
                      SplitW{(const bf16_t*)Wkv2_hi, (const bf16_t*)Wkv2_lo}, bkv2, dr, s_v, mean_v, rstd_v, v1, kv2,

@@ -343,7 +343,6 @@ MER_API int mer_xh_a2v_bwd(int B, int T, int Ta, const float* demb, const float*
 // ---------------------------------------------------------------------------------------------
 constexpr int G2_KT = 10;  // 16-key tiles of one sample's keys the dkv2 fold reads (Ta <= 160 in G2a's fold)
 constexpr int G2_KVLD = 2 * XD + 4;
-constexpr int G2B_MAXC = 2;  // 32-key chunks per wave (Ta <= 256)
 constexpr int G2B_TLD = 36;
 
 __global__ __launch_bounds__(256) void xh_v2a_pre_bwd_kernel(
@@ -431,48 +430,59 @@ __global__ __launch_bounds__(256) void xh_v2a_pre_bwd_kernel(
   }
 }
 
-__global__ __launch_bounds__(256) void xh_v2a_attn_bwd_kernel(
+// one wave per 32-key chunk (8 waves, Ta <= 256: with 4 waves wave 0 carried two chunks at Ta = 149 and its chunk
+// phase -- dS, dq1 partial, the chunk's dK1 / dV1 -- set the block time, tools/xt_phases.py: 5.2 of 10.4 us)
+constexpr int G2B_W = 8;
+
+// fixed-order sum of v[0..N) (N a power of two): pairwise, the same tree whatever the wave schedule
+template <int N>
+__device__ __forceinline__ float tree_sum(const float* v, int stride) {
+  if constexpr (N == 1) {
+    return v[0];
+  } else {
+    return tree_sum<N / 2>(v, stride) + tree_sum<N / 2>(v + (N / 2) * stride, stride);
+  }
+}
+
+__global__ __launch_bounds__(64 * G2B_W) void xh_v2a_attn_bwd_kernel(
     int T, int Ta, const float* __restrict__ do1, const float* __restrict__ P1, const float* __restrict__ kv1,
     const float* __restrict__ q1, XhDrop dr, float scale, float* __restrict__ dq1, float* __restrict__ dqkv,
     float* __restrict__ dS_heads) {
-  __shared__ float red[4][16];
-  __shared__ __attribute__((aligned(16))) float dSt[4][16 * G2B_TLD];  // per-wave dS chunk [query][key]
-  __shared__ __attribute__((aligned(16))) float Pdt[4][16 * G2B_TLD];  // per-wave P' chunk
-  __shared__ float oP[4][16][33];
+  __shared__ float red[G2B_W][16];
+  __shared__ __attribute__((aligned(16))) float dSt[G2B_W][16 * G2B_TLD];  // per-wave dS chunk [query][key]
+  __shared__ __attribute__((aligned(16))) float Pdt[G2B_W][16 * G2B_TLD];  // per-wave P' chunk
+  __shared__ float oP[G2B_W][16][33];
   XT(2, 0);
   const int b = blockIdx.x >> 2, h = blockIdx.x & 3;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, fr = lane & 15, fq = lane >> 4, fk = fq * 8;
   const long ldkv = 2 * XD, row0 = (long)b * T;
   const float* Kr = kv1 + (long)b * Ta * ldkv + h * XDH;
   const float* Vr = Kr + XD;
-  const int nch = (Ta + 31) / 32;
+  const int c = w;                  // this wave's chunk
+  const bool live = 32 * c < Ta;    // (wave-uniform)
   const unsigned long long seed_attn = mer_site_seed(dr.seed, dr.site_attn);
   // every global load first: V fragments (dP), the saved probabilities, K gathers (dq1), the q1 / do1 fragments
-  f32x4 vraw[G2B_MAXC][2][2];
-  float praw[G2B_MAXC][2][4];
-  float kraw[G2B_MAXC][2][8];
+  f32x4 vraw[2][2];
+  float praw[2][4];
+  float kraw[2][8];
 #pragma unroll
-  for (int ci = 0; ci < G2B_MAXC; ++ci) {
-    const int c = w + 4 * ci;
+  for (int tt = 0; tt < 2; ++tt) {
+    const int j = 32 * c + 16 * tt + fr, jc = j < Ta ? j : Ta - 1;
+    vraw[tt][0] = *reinterpret_cast<const f32x4*>(Vr + (long)jc * ldkv + fk);
+    vraw[tt][1] = *reinterpret_cast<const f32x4*>(Vr + (long)jc * ldkv + fk + 4);
 #pragma unroll
-    for (int tt = 0; tt < 2; ++tt) {
-      const int j = 32 * c + 16 * tt + fr, jc = j < Ta ? j : Ta - 1;
-      vraw[ci][tt][0] = *reinterpret_cast<const f32x4*>(Vr + (long)jc * ldkv + fk);
-      vraw[ci][tt][1] = *reinterpret_cast<const f32x4*>(Vr + (long)jc * ldkv + fk + 4);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int i = 4 * fq + r;
-        praw[ci][tt][r] = P1[(((long)b * XH + h) * T + (i < T ? i : T - 1)) * Ta + jc];  // always in range
-      }
+    for (int r = 0; r < 4; ++r) {
+      const int i = 4 * fq + r;
+      praw[tt][r] = P1[(((long)b * XH + h) * T + (i < T ? i : T - 1)) * Ta + jc];  // always in range
     }
-#pragma unroll
-    for (int jt = 0; jt < 2; ++jt)
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int kk = 32 * c + fk + e;
-        kraw[ci][jt][e] = Kr[(long)(kk < Ta ? kk : Ta - 1) * ldkv + 16 * jt + fr];
-      }
   }
+#pragma unroll
+  for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int kk = 32 * c + fk + e;
+      kraw[jt][e] = Kr[(long)(kk < Ta ? kk : Ta - 1) * ldkv + 16 * jt + fr];
+    }
   bf16x8 gh, gl;  // do1_h rows (A of dP)
   frag_row(do1 + (row0 + (fr < T ? fr : T - 1)) * XD + h * XDH + fk, fr < T, gh, gl);
   bf16x8 qch[2], qcl[2], gch[2], gcl[2];  // q1_h / do1_h as [dim][query] B operands of dK / dV
@@ -481,34 +491,33 @@ __global__ __launch_bounds__(256) void xh_v2a_attn_bwd_kernel(
     frag_col(q1 + (row0 + fk) * XD + h * XDH + 16 * jt + fr, XD, fk, T, qch[jt], qcl[jt]);
     frag_col(do1 + (row0 + fk) * XD + h * XDH + 16 * jt + fr, XD, fk, T, gch[jt], gcl[jt]);
   }
-  f32x4 dp[G2B_MAXC][2];
-  float pv[G2B_MAXC][2][4], mk[G2B_MAXC][2][4];
+  XT(2, 1);
+  f32x4 dp[2];
+  float pv[2][4], mk[2][4];
   float rs[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int ci = 0; ci < G2B_MAXC; ++ci)
+  for (int tt = 0; tt < 2; ++tt) {  // dP' = do1_h . V_h^T, dP = dP' * mask, rowsum partials of P dP
+    const int j = 32 * c + 16 * tt + fr;
+    float x[8] = {vraw[tt][0][0], vraw[tt][0][1], vraw[tt][0][2], vraw[tt][0][3],
+                  vraw[tt][1][0], vraw[tt][1][1], vraw[tt][1][2], vraw[tt][1][3]};
 #pragma unroll
-    for (int tt = 0; tt < 2; ++tt) {  // dP' = do1_h . V_h^T, dP = dP' * mask, rowsum partials of P dP
-      const int j = 32 * (w + 4 * ci) + 16 * tt + fr;
-      float x[8] = {vraw[ci][tt][0][0], vraw[ci][tt][0][1], vraw[ci][tt][0][2], vraw[ci][tt][0][3],
-                    vraw[ci][tt][1][0], vraw[ci][tt][1][1], vraw[ci][tt][1][2], vraw[ci][tt][1][3]};
+    for (int e = 0; e < 8; ++e) x[e] = j < Ta ? x[e] : 0.f;
+    bf16x8 bh, bl;
+    split8(x, bh, bl);
+    dp[tt] = mma3(gh, gl, bh, bl, f32x4{0.f, 0.f, 0.f, 0.f});
 #pragma unroll
-      for (int e = 0; e < 8; ++e) x[e] = j < Ta ? x[e] : 0.f;
-      bf16x8 bh, bl;
-      split8(x, bh, bl);
-      dp[ci][tt] = mma3(gh, gl, bh, bl, f32x4{0.f, 0.f, 0.f, 0.f});
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int i = 4 * fq + r;
-        const bool ok = i < T && j < Ta;
-        const long pi = (((long)b * XH + h) * T + i) * Ta + j;
-        const float m = ok ? dropout_scale(seed_attn, pi, dr.attn) : 0.f;
-        const float p = ok ? praw[ci][tt][r] : 0.f;
-        pv[ci][tt][r] = p;
-        mk[ci][tt][r] = m;
-        dp[ci][tt][r] *= m;
-        rs[r] += p * dp[ci][tt][r];
-      }
+    for (int r = 0; r < 4; ++r) {
+      const int i = 4 * fq + r;
+      const bool ok = i < T && j < Ta;
+      const long pi = (((long)b * XH + h) * T + i) * Ta + j;
+      const float m = ok ? dropout_scale(seed_attn, pi, dr.attn) : 0.f;
+      const float p = ok ? praw[tt][r] : 0.f;
+      pv[tt][r] = p;
+      mk[tt][r] = m;
+      dp[tt][r] *= m;
+      rs[r] += p * dp[tt][r];
     }
+  }
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
 #pragma unroll
@@ -517,25 +526,20 @@ __global__ __launch_bounds__(256) void xh_v2a_attn_bwd_kernel(
   }
   __syncthreads();
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int i = 4 * fq + r;
-    rs[r] = (red[0][i] + red[1][i]) + (red[2][i] + red[3][i]);
-  }
+  for (int r = 0; r < 4; ++r) rs[r] = tree_sum<G2B_W>(&red[0][4 * fq + r], 16);
+  XT(2, 2);
   f32x4 oq[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
   float* st = dSt[w];
   float* pt = Pdt[w];
-#pragma unroll
-  for (int ci = 0; ci < G2B_MAXC; ++ci) {
-    const int c = w + 4 * ci;
-    if (c >= nch) break;  // (wave-uniform)
+  if (live) {
 #pragma unroll
     for (int tt = 0; tt < 2; ++tt)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int i = 4 * fq + r, jj = 16 * tt + fr, j = 32 * c + jj;
-        const float ds = pv[ci][tt][r] * (dp[ci][tt][r] - rs[r]);
+        const float ds = pv[tt][r] * (dp[tt][r] - rs[r]);
         st[i * G2B_TLD + jj] = ds;
-        pt[i * G2B_TLD + jj] = pv[ci][tt][r] * mk[ci][tt][r];  // P' (zero outside the T x Ta block)
+        pt[i * G2B_TLD + jj] = pv[tt][r] * mk[tt][r];  // P' (zero outside the T x Ta block)
         if (dS_heads && i < T && j < Ta) dS_heads[(((long)b * XH + h) * T + i) * Ta + j] = ds;
       }
     wave_sync_lds();
@@ -546,7 +550,7 @@ __global__ __launch_bounds__(256) void xh_v2a_attn_bwd_kernel(
       for (int jt = 0; jt < 2; ++jt) {
         float x[8];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) x[e] = 32 * c + fk + e < Ta ? kraw[ci][jt][e] : 0.f;
+        for (int e = 0; e < 8; ++e) x[e] = 32 * c + fk + e < Ta ? kraw[jt][e] : 0.f;
         bf16x8 bh, bl;
         split8(x, bh, bl);
         oq[jt] = mma3(ah, al, bh, bl, oq[jt]);
@@ -573,18 +577,18 @@ __global__ __launch_bounds__(256) void xh_v2a_attn_bwd_kernel(
         }
       }
     }
-    wave_sync_lds();  // the next chunk overwrites st / pt
   }
+  XT(2, 3);
 #pragma unroll
   for (int jt = 0; jt < 2; ++jt)
 #pragma unroll
     for (int r = 0; r < 4; ++r) oP[w][4 * fq + r][16 * jt + fr] = oq[jt][r];
   __syncthreads();
-  for (int e = threadIdx.x; e < T * XDH; e += 256) {
+  for (int e = threadIdx.x; e < T * XDH; e += 64 * G2B_W) {
     const int i = e / XDH, d = e - i * XDH;
-    dq1[(row0 + i) * XD + h * XDH + d] = ((oP[0][i][d] + oP[1][i][d]) + (oP[2][i][d] + oP[3][i][d])) * scale;
+    dq1[(row0 + i) * XD + h * XDH + d] = tree_sum<G2B_W>(&oP[0][i][d], 16 * 33) * scale;
   }
-  XT(2, 1);
+  XT(2, 4);
 }
 
 // the prior bias gradient: dbias[b][i][j] = sum over heads of dS (head order, mha_dbias_kernel's order)
@@ -613,8 +617,8 @@ MER_API int mer_xh_v2a_bwd(int B, int T, int Ta, const float* dkv2_part, const v
   hipLaunchKernelGGL(xh_v2a_pre_bwd_kernel, dim3(B), dim3(256), 0, st, T, (Ta + 15) / 16, dkv2_part,
                      SplitW{(const bf16_t*)WkvT2_hi, (const bf16_t*)WkvT2_lo}, demb, s_v, mean_v, rstd_v, gamma,
                      SplitW{(const bf16_t*)WoT1_hi, (const bf16_t*)WoT1_lo}, dr, dkv2, dv2, dv, do1, ln_part);
-  hipLaunchKernelGGL(xh_v2a_attn_bwd_kernel, dim3(B * XH), dim3(256), 0, st, T, Ta, do1, P1, kv1, q1, dr, scale, dq1,
-                     dqkv, dbias ? dS_heads : nullptr);
+  hipLaunchKernelGGL(xh_v2a_attn_bwd_kernel, dim3(B * XH), dim3(64 * G2B_W), 0, st, T, Ta, do1, P1, kv1, q1, dr, scale,
+                     dq1, dqkv, dbias ? dS_heads : nullptr);
   if (dbias) {
     const long n = (long)B * T * Ta;
     hipLaunchKernelGGL(xh_dbias_heads_kernel, dim3((unsigned)((n + 255) / 256 < 1024 ? (n + 255) / 256 : 1024)),

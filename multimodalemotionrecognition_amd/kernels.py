@@ -972,7 +972,8 @@ def xh_audio_fwd(af, Ws, bs, Wa, ba, Wc, bq2, bkv1, a_s, a, q2, kv1, vf, Wv, bv,
 
 
 def xh_audio_fwd_pair(pair, bs, Wa, ba, Wc, bq2, bkv1, a_s, a, q2, kv1, vf, Wv, bv, Wq1, bq1, v, q1):
-    """F1 after the first product ran as one bf16 GEMM: ``pair`` = [aseq Ws_hi^T | aseq Ws_lo^T] fp32 [M, 256]."""
+    """F1 after the first product ran as one bf16 GEMM: ``pair`` = [aseq Ws_hi^T | aseq Ws_lo^T] fp32 [M, 256].
+    Equal to ``xh_audio_fwd`` up to fp32 rounding (its halves are summed after the K loop, not per k step)."""
     M = pair.shape[0]
     Mv, vdim = vf.shape
     if pair.shape[1] != 256 or pair.stride(1) != 1 or Wc[0].shape != (384, 128) or Wv[0].shape != (128, vdim) \

@@ -54,9 +54,17 @@ class _DropoutFn(torch.autograd.Function):
         return g, None, None
 
 
-def hip_dropout(x: torch.Tensor, p: float, training: bool) -> torch.Tensor:
+def draw_seed(p: float, training: bool):
+    """The host seed ``hip_dropout(x, p, training)`` would draw (None when it draws nothing)."""
+    if not training or p <= 0:
+        return None
+    return int(torch.randint(0, 2 ** 62, (1,)).item())  # host draw: torch.manual_seed reproduces it
+
+
+def hip_dropout(x: torch.Tensor, p: float, training: bool, seed=None) -> torch.Tensor:
+    """``seed``: drawn ahead by ``draw_seed`` (same draw, earlier), else drawn here."""
     if not training or p <= 0:
         return x
-    seed = int(torch.randint(0, 2 ** 62, (1,)).item())  # host draw: torch.manual_seed reproduces it
+    seed = draw_seed(p, training) if seed is None else seed
     rng = torch.full((1,), seed, dtype=torch.int64, device=x.device)  # a fill kernel: no host buffer in flight
     return _DropoutFn.apply(x, p, rng)

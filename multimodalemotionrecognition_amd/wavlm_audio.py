@@ -27,7 +27,7 @@ from torch import nn
 
 from . import graphs as G
 from . import kernels as K
-from .nn_ops import hip_dropout, hip_linear
+from .nn_ops import draw_seed, hip_dropout, hip_linear
 from .optim import weight_version
 from .temporal import TemporalPooler
 
@@ -764,9 +764,16 @@ class WavLMAudioEncoder(nn.Module):
             a_emb = hip_linear(a_emb, self.classifier[0])
         return a_emb
 
-    def forward(self, x: torch.Tensor, hidden: Optional[torch.Tensor] = None) -> torch.Tensor:
+    def draw_dropout_seed(self) -> Optional[int]:
+        """The classifier dropout's host seed drawn ahead of ``forward`` (None when the dropout is off): the late
+        fusion's early prefetch draws it before starting the next batch's encoder, keeping the inline RNG order."""
+        return draw_seed(float(self.classifier[2].p), self.training)
+
+    def forward(self, x: torch.Tensor, hidden: Optional[torch.Tensor] = None,
+                drop_seed: Optional[int] = None) -> torch.Tensor:
         hidden = self.encode_sequence(x, out_dtype=torch.float32) if hidden is None else hidden
         a_emb = self.temporal_pool(hidden)
         h = hip_linear(a_emb, self.classifier[0], act="relu")
-        h = hip_dropout(h, float(self.classifier[2].p), self.training)  # the nn.Dropout(0.2) of wavlm_audio.py:58
+        # the nn.Dropout(0.2) of wavlm_audio.py:58
+        h = hip_dropout(h, float(self.classifier[2].p), self.training, seed=drop_seed)
         return hip_linear(h, self.classifier[3])

@@ -112,3 +112,35 @@ def test_fused_backward_matches_unfused(head, training, prior):
     XH.head_backward(p, ctx, dl, g2, need_dv_feat=False, fused=True)
     for n in g1:
         assert _rel(g2[n], 2 * g1[n]) < 1e-6, n
+
+
+@pytest.mark.parametrize("training", [False, True])
+def test_f1_pair_matches_in_kernel(training):
+    """F1's first product as one bf16 GEMM against stacked hi / lo planes + mer_xh_audio_fwd_pair (the default,
+    ``xattn_fused.F1_PAIR``) against the in-kernel product of mer_xh_audio_fwd, which folds hi and lo into one running
+    sum per k step: the two round differently, so they agree to fp32 rounding (a_s), which the next split-bf16
+    products carry on (measured 2.3e-6 max-abs relative on a), and both forward paths give the same logits within the
+    fused-vs-unfused bar."""
+    from multimodalemotionrecognition_amd import xattn_fused as XF
+    from multimodalemotionrecognition_amd import xattn_head as XH
+
+    m = head_model("concat", False).train(training)
+    names, params = m.head_params()
+    p = dict(zip(names, params))
+    cfg = m.head_config()
+    v, a = feats(32, 8, 149, seed=7)
+    a = a.to(torch.bfloat16)
+    rng = torch.full((1,), 4242, dtype=torch.int64, device="cuda")
+    out = {}
+    prev = XF.F1_PAIR
+    try:
+        for pair in (False, True):
+            XF.F1_PAIR = pair
+            logits, ctx = XH.head_forward(p, cfg, v, a, training, rng)
+            out[pair] = (logits.clone(), {k: ctx.saved[k].clone() for k in ("a_s", "a", "q2", "kv1")})
+    finally:
+        XF.F1_PAIR = prev
+    (l0, s0), (l1, s1) = out[False], out[True]
+    for k in s0:
+        assert _rel(s1[k], s0[k]) < 1e-5, (k, _rel(s1[k], s0[k]))
+    assert _rel(l1, l0) < 1e-5

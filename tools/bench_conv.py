@@ -20,6 +20,7 @@ WGRAD_V = [int(v) for v in next((a.split("=")[1] for a in sys.argv if a.startswi
            if v]
 WGRAD = "--no-wgrad" not in sys.argv
 FUSED = "--fused" in sys.argv
+X2 = "--x2" in sys.argv  # the fused dgrad reduces a second BN (the block-0 output of layers 2-4: bn2 + downsample BN)
 ONLY = next((a.split("=")[1] for a in sys.argv if a.startswith("--layers=")), None)  # substring filter, e.g. layer1  # dgrad as in the train step: residual under a ReLU mask + the fused BN-backward sums
 
 
@@ -67,6 +68,9 @@ def main():
             ms = torch.stack([torch.zeros(C, device="cuda"), torch.ones(C, device="cuda")], 1).contiguous()
             red = torch.zeros(K.bn_red_rows(NF * H * H), C, 2, device="cuda")
             fk = dict(residual=res, mask=msk, bnr=(msk, xb, ms, red))
+            if X2:
+                red2 = torch.zeros_like(red)
+                fk["bnr"] = (msk, xb, ms, red, (torch.rand_like(dx.float()) * 2 - 1).bfloat16(), ms, red2)
         for v in VARIANTS:
             tf = timeit(lambda: K.conv_fwd(x, wp, y, stats, R, R, st, pad, variant=v))
             tb = timeit(lambda: K.conv_dgrad(dy, wt, dx, R, R, st, pad, variant=v, **fk)) if H != 59 else float("nan")

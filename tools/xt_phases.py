@@ -96,13 +96,13 @@ def run():
 
 # the attention cores (QK^T, softmax, PV and their backward) inside the fused head's kernels: (table, first
 # stamp, last stamp) of the attention phase and the kernel's last stamp
-CORE = {("fwd", 3): (0, 1, 1), ("fwd", 1): (0, 1, 2), ("bwd", 2): (0, 1, 1), ("bwd", 3): (1, 2, 3)}
+CORE = {("fwd", 3): (0, 4, 4), ("fwd", 1): (0, 1, 2), ("bwd", 2): (0, 4, 4), ("bwd", 3): (1, 2, 3)}
 
 
 def core(tabs, names):
     """roofline_head.core_attn: for each of the four kernels that hold an attention core, the attention phase's
     share of the median block time x the kernel's span (first block entry to last block end) in this replay;
-    written to gpurun_out/core_attn.json (committed as profiles/r05/core_attn.json, which bench.py reports)"""
+    written to gpurun_out/core_attn.json (committed as profiles/r06/core_attn.json, which bench.py reports)"""
     import json
     import numpy as np
     out, total = {}, 0.0
@@ -122,7 +122,7 @@ def core(tabs, names):
                      "one captured-graph replay of the fused head fwd+bwd at B=32, T=8, Ta=149; per kernel the "
                      "attention phase's share of the median block time times the kernel's span"}
     print(json.dumps(res, indent=1))
-    dst = ROOT / "gpurun_out" / "core_attn.json"  # (copied to profiles/r05/ by hand: only gpurun_out/ comes back)
+    dst = ROOT / "gpurun_out" / "core_attn.json"  # (copied to profiles/r06/ by hand: only gpurun_out/ comes back)
     if "save" in sys.argv[2:]:
         dst.write_text(json.dumps(res, indent=1) + "\n")
 
