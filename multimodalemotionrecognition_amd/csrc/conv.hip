@@ -1142,9 +1142,17 @@ __device__ __forceinline__ void conv_epilogue_vec(const ConvGeom& g, f32x4 (&acc
 // Minimum waves per SIMD of a conv_pipe_kernel block of nw waves: 16-wave blocks 1 per CU, 8-wave blocks 2 per CU --
 // except the tiles that would spill at 128 VGPRs (the 256-row dgrad tiles and the 3-deep 128 x 128 dgrad ring, none of
 // them a default pick), which keep one block per CU; 4-wave blocks 2 per CU.
-constexpr int conv_pipe_wpe(int nw, int bm, int bn, int stages, bool dgrad, bool par) {
-  return nw >= 16 ? nw / 4
-                  : nw == 8 ? ((dgrad && (bm == 256 || (!par && bm == 128 && bn == 128 && stages == 3))) ? 2 : 4) : 2;
+// A block whose LDS leaves no room for a second one on the CU (160 KB) asks for nw / 4 (its own waves only).
+constexpr int conv_pipe_wpe(int nw, int bm, int bn, int stages, bool dgrad, bool par, int lds_bytes = 0) {
+  return (nw >= 16 || 2 * lds_bytes > 160 * 1024)
+             ? (nw >= 4 ? nw / 4 : 1)
+             : nw == 8 ? ((dgrad && (bm == 256 || (!par && bm == 128 && bn == 128 && stages == 3))) ? 2 : 4) : 2;
+}
+// dynamic LDS of a conv_pipe_kernel instantiation: KG rings, or the split-K tile exchange if larger
+constexpr int conv_pipe_lds(int bm, int bn, int stages, int ks, int kg) {
+  return kg * stages * (bm + bn) * ks * 2 > (kg > 1 ? kg * bm * (bn + 4) * 4 : 0)
+             ? kg * stages * (bm + bn) * ks * 2
+             : kg * bm * (bn + 4) * 4;
 }
 
 // The wave layout of the in-workgroup split-K reduction (KG > 1): WAVES * KG waves over the BM x BN tile, 4 wave
@@ -1170,7 +1178,8 @@ template <bool DGRAD, bool PAR, int BM_, int BN_, int WM = 2, int WN = 2, int ST
           int KG = 1>
 // (__launch_bounds__'s second argument is amdgpu_waves_per_eu, a minimum of waves per SIMD: two 8-wave blocks per CU need
 // 4, i.e. <= 128 VGPRs -- with 2, the parity-class dgrad tile took 131 VGPRs and ran one block per CU)
-__global__ __launch_bounds__(64 * WM * WN * KG, conv_pipe_wpe(WM * WN * KG, BM_, BN_, STAGES, DGRAD, PAR)) void conv_pipe_kernel(ConvGeom g) {
+__global__ __launch_bounds__(64 * WM * WN * KG, conv_pipe_wpe(WM * WN * KG, BM_, BN_, STAGES, DGRAD, PAR,
+                                                              conv_pipe_lds(BM_, BN_, STAGES, KS, KG))) void conv_pipe_kernel(ConvGeom g) {
   constexpr int WAVES = WM * WN;  // per K-group
   constexpr int CW = KS / 8, RPG = 64 / CW;  // 16-byte chunks per LDS row, rows per glds instruction
   constexpr int IA = BM_ / RPG / WAVES, IB = BN_ / RPG / WAVES;  // glds per wave per K-tile
@@ -1563,10 +1572,6 @@ int launch_conv_pipe(ConvGeom& g, hipStream_t st, int variant) {
     return PAR ? launch_conv_pipe_t<DGRAD, PAR, 64, 128, 2, 4, 2, 64, 2>(g, st)
                : launch_conv_pipe_t<DGRAD, PAR, 64, 128, 2, 4, 3, 64, 2>(g, st);
   }
-  if (variant == 9) {  // (A/B) variant 2's tiles without the x2 exception: 128 x 128 for the two-BN stride-1 dgrad
-    if (bn == 64) return launch_conv_pipe_t<DGRAD, PAR, 128, 64, 4, 2>(g, st);
-    return launch_conv_pipe_t<DGRAD, PAR, 128, 128, 2, 4>(g, st);
-  }
   if (variant == 8) {  // in-workgroup split-K (two K-groups) on the 128-row tiles
     if (bn == 64) return launch_conv_pipe_t<DGRAD, PAR, 128, 64, 4, 2, 2, 64, 2>(g, st);
     return launch_conv_pipe_t<DGRAD, PAR, 128, 128, 2, 4, 2, 64, 2>(g, st);
@@ -1883,7 +1888,7 @@ MER_API int mer_conv_fwd(int N, int H, int W, int C, int K, int R, int S, int st
 
 MER_API int mer_conv_fwd_ex(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, const void* x,
                             const void* w_packed, void* y, float* stats, int variant, void* stream) {
-  if (C % 8 || variant < -1 || variant > 9) return (int)hipErrorInvalidValue;
+  if (C % 8 || variant < -1 || variant > 8) return (int)hipErrorInvalidValue;
   ConvGeom g{};
   g.N = N; g.IH = H; g.IW = W; g.IC = C;
   g.OH = (H + 2 * pad - R) / stride + 1; g.OW = (W + 2 * pad - S) / stride + 1;
@@ -1928,7 +1933,7 @@ MER_API int mer_conv_dgrad_ds(int N, int H, int W, int C, int K, int R, int S, i
                               const void* bn_mask, const void* bn_x, const float* bn_ms, float* bn_red,
                               const void* bn_x2, const float* bn_ms2, float* bn_red2, const void* ds_dy,
                               const void* ds_wt_packed, int ds_K, int variant, void* stream) {
-  if (K % 8 || C % 8 || variant < -1 || variant > 9) return (int)hipErrorInvalidValue;
+  if (K % 8 || C % 8 || variant < -1 || variant > 8) return (int)hipErrorInvalidValue;
   const bool auto_variant = variant == -1;
   // 64-channel outputs (layer1, the layer2.0 input gradients): 32-wide K-tiles on a 4-deep ring with 4-wave tiles
   // (tools/bench_conv.py --fused: layer1 101 -> 65 us, layer2.0 s2 74 -> 51, downsample 48 -> 31); wider outputs
