@@ -439,9 +439,13 @@ __device__ __attribute__((aligned(16))) uint32_t mer_conv_zero16[4] = {0u, 0u, 0
 
 __device__ __forceinline__ int wswz(int row, int nchunks) { return ((row & 7) << 1) & (nchunks - 1); }
 
-template <int BM_, int BN_, int WM, int WN, int STAGES, int KS = 64>
-__global__ __launch_bounds__(64 * WM * WN, 2) void wgrad_pipe_kernel(WgradGeom g) {
-  constexpr int WAVES = WM * WN;
+// KG > 1: in-workgroup split-K over the pixels, as in conv_pipe_kernel: KG groups of WM x WN waves, each with its own
+// ring and a contiguous 1/KG of the split's K-steps; the groups' tiles are summed in LDS in group order before the one
+// slab store.  A KG = 2 launch covers the pixels of two one-group splits with the same waves per CU, so it writes (and
+// the fold re-reads) half the fp32 slabs -- ~0.5 of the ~1 GB per step the trunk's weight gradients moved.
+template <int BM_, int BN_, int WM, int WN, int STAGES, int KS = 64, int KG = 1>
+__global__ __launch_bounds__(64 * WM * WN * KG, KG > 1 ? WM * WN * KG / 4 : 2) void wgrad_pipe_kernel(WgradGeom g) {
+  constexpr int WAVES = WM * WN;  // per K-group
   constexpr int ACW = BM_ / 8, BCW = BN_ / 8;           // 16-byte chunks per LDS row
   constexpr int ARI = 64 / ACW, BRI = 64 / BCW;         // rows per glds instruction
   constexpr int IA = KS / ARI / WAVES, IB = KS / BRI / WAVES;  // glds per wave per K-step of KS pixels
@@ -449,8 +453,9 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void wgrad_pipe_kernel(WgradGeom g
   static_assert(KS % 32 == 0, "MFMA k = 32 pixels");
   constexpr int IT = BM_ / WM / 16, JT = BN_ / WN / 16;
   constexpr int BUF = KS * (BM_ + BN_);                 // bf16 elements per ring slot
-  extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  extern __shared__ __attribute__((aligned(16))) bf16_t smem_all[];
+  const int t = threadIdx.x, lane = t & 63, kg = (t >> 6) / WAVES, w = (t >> 6) % WAVES;
+  bf16_t* const smem = smem_all + kg * STAGES * BUF;  // this K-group's ring
   const int Ntot = g.R * g.S * g.C;
   const int P = g.N * g.Ho * g.Wo;
   const int wnx = (Ntot + BN_ - 1) / BN_, wny = (g.K + BM_ - 1) / BM_;
@@ -542,16 +547,23 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void wgrad_pipe_kernel(WgradGeom g
   for (int i = 0; i < IT; ++i)
 #pragma unroll
     for (int j = 0; j < JT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int nk = (p_end - p_beg + KS - 1) / KS;
+  // this K-group's K-steps [kb, kb + nk) of the split's nk_all (every group runs the loop nkg times: workgroup-wide
+  // barriers)
+  const int nk_all = (p_end - p_beg + KS - 1) / KS;
+  const int nkg = (nk_all + KG - 1) / KG, kb = kg * nkg;
+  const int nk = nk_all - kb < nkg ? (nk_all - kb > 0 ? nk_all - kb : 0) : nkg;
+  const int pk0 = p_beg + kb * KS;
   constexpr int G = IA + IB;
 #pragma unroll
   for (int s = 0; s < STAGES - 1; ++s)
-    if (s < nk) stage(s, p_beg + s * KS);
-  for (int kt = 0; kt < nk; ++kt) {
-    const int ahead = (nk - 1 - kt) < (STAGES - 2) ? (nk - 1 - kt) : (STAGES - 2);
+    if (s < nk) stage(s, pk0 + s * KS);
+  for (int kt = 0; kt < nkg; ++kt) {
+    const int left = nk - 1 - kt;
+    const int ahead = left < (STAGES - 2) ? left : (STAGES - 2);
     wait_tiles_in_flight<G>(ahead);
     lds_barrier();
-    if (kt + STAGES - 1 < nk) stage((kt + STAGES - 1) % STAGES, p_beg + (kt + STAGES - 1) * KS);
+    if (kt + STAGES - 1 < nk) stage((kt + STAGES - 1) % STAGES, pk0 + (kt + STAGES - 1) * KS);
+    if (KG > 1 && kt >= nk) continue;
     const bf16_t* Aimg = smem + (kt % STAGES) * BUF;
     const bf16_t* Bimg = Aimg + KS * BM_;
 #pragma unroll
@@ -569,6 +581,33 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void wgrad_pipe_kernel(WgradGeom g
       __builtin_amdgcn_s_setprio(0);
     }
   }
+  if constexpr (KG > 1) {  // groups 1.. hand their tiles to group 0 through LDS; group 0 sums in group order
+    constexpr int LDR = BN_ + 4;
+    __syncthreads();  // every group's last fragment reads are done before the exchange reuses the rings
+    float* const part = reinterpret_cast<float*>(smem_all);
+    if (kg > 0) {
+      float* mine = part + (kg - 1) * BM_ * LDR;
+#pragma unroll
+      for (int i = 0; i < IT; ++i)
+#pragma unroll
+        for (int j = 0; j < JT; ++j)
+#pragma unroll
+          for (int rr = 0; rr < 4; ++rr)
+            mine[(wm + i * 16 + (lane >> 4) * 4 + rr) * LDR + wn + j * 16 + (lane & 15)] = acc[i][j][rr];
+    }
+    lds_barrier();
+    if (kg > 0) return;
+#pragma unroll
+    for (int i = 0; i < IT; ++i)
+#pragma unroll
+      for (int j = 0; j < JT; ++j)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr)
+#pragma unroll
+          for (int q = 1; q < KG; ++q)
+            acc[i][j][rr] += part[(q - 1) * BM_ * LDR + (wm + i * 16 + (lane >> 4) * 4 + rr) * LDR + wn + j * 16 +
+                                  (lane & 15)];
+  }
   float* slab = g.ws + (long)zs * g.K * Ntot;
 #pragma unroll
   for (int i = 0; i < IT; ++i)
@@ -584,10 +623,12 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void wgrad_pipe_kernel(WgradGeom g
     }
 }
 
-template <int BM_, int BN_, int WM, int WN, int STAGES, int KS = 64>
+template <int BM_, int BN_, int WM, int WN, int STAGES, int KS = 64, int KG = 1>
 void launch_wgrad_pipe(const WgradGeom& g0, dim3 grid, hipStream_t st) {
-  const size_t lds = (size_t)STAGES * KS * (BM_ + BN_) * sizeof(bf16_t);
-  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_pipe_kernel<BM_, BN_, WM, WN, STAGES, KS>),
+  const size_t ring = (size_t)KG * STAGES * KS * (BM_ + BN_) * sizeof(bf16_t);
+  const size_t xchg = (size_t)(KG - 1) * BM_ * (BN_ + 4) * sizeof(float);
+  const size_t lds = ring > xchg ? ring : xchg;
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_pipe_kernel<BM_, BN_, WM, WN, STAGES, KS, KG>),
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return;
   // split-major 1-D grid over xcd_tile's XCD chunks: the tiles of one split (same dY rows, same shifted X windows)
@@ -595,7 +636,7 @@ void launch_wgrad_pipe(const WgradGeom& g0, dim3 grid, hipStream_t st) {
   WgradGeom g = g0;
   g.flat = 1;
   const dim3 gr(grid.x * grid.z, 1, 1);
-  hipLaunchKernelGGL((wgrad_pipe_kernel<BM_, BN_, WM, WN, STAGES, KS>), gr, dim3(64 * WM * WN), lds, st, g);
+  hipLaunchKernelGGL((wgrad_pipe_kernel<BM_, BN_, WM, WN, STAGES, KS, KG>), gr, dim3(64 * WM * WN * KG), lds, st, g);
 }
 
 // slab0[i] = sum_z ws[z][i] over the flat [K][R*S*C] index.  A block owns E = 256/SG consecutive elements
@@ -1977,7 +2018,7 @@ MER_API int mer_conv_wgrad(int N, int H, int W, int C, int Creal, int K, int R, 
 static int conv_wgrad_impl(int N, int H, int W, int C, int Creal, int K, int R, int S, int stride, int pad,
                            const void* x, const void* dy, long ldy, float* dw, int splits, float* workspace,
                            int variant, void* stream, bool fold = true) {
-  if (C % 8 || K % 8 || variant < -1 || variant > 7 || R * S > 49) return (int)hipErrorInvalidValue;
+  if (C % 8 || K % 8 || variant < -1 || variant > 8 || R * S > 49) return (int)hipErrorInvalidValue;
   if (variant == -1) variant = wgrad_default_variant(K);
   WgradGeom g{};
   g.N = N; g.H = H; g.W = W; g.C = C; g.Creal = Creal;
@@ -1997,6 +2038,8 @@ static int conv_wgrad_impl(int N, int H, int W, int C, int Creal, int K, int R, 
       hipLaunchKernelGGL((wgrad_kernel<64, 128>), grid, dim3(256), 0, st, g);
     else if (variant == 4)
       launch_wgrad_pipe<64, 128, 2, 4, 2>(g, grid, st);
+    else if (variant == 8)
+      launch_wgrad_pipe<64, 128, 2, 4, 2, 64, 2>(g, grid, st);
     else if (variant == 5 || variant == 6)
       launch_wgrad_pipe<64, 128, 2, 4, 3>(g, grid, st);
     else if (variant == 3)
@@ -2009,6 +2052,8 @@ static int conv_wgrad_impl(int N, int H, int W, int C, int Creal, int K, int R, 
       hipLaunchKernelGGL((wgrad_kernel<128, 128>), grid, dim3(256), 0, st, g);
     else if (variant == 4)
       launch_wgrad_pipe<128, 128, 2, 4, 2>(g, grid, st);
+    else if (variant == 8)
+      launch_wgrad_pipe<128, 128, 2, 4, 2, 64, 2>(g, grid, st);
     else if (variant == 5)
       launch_wgrad_pipe<128, 128, 2, 4, 3>(g, grid, st);
     else if (variant == 6)

@@ -463,6 +463,41 @@ def test_wgrad_variants_bit_identical(N, H, C, Kc, R, stride, pad):
         assert torch.equal(out[0], o), f"variant {v} differs"
 
 
+@pytest.mark.parametrize("N,H,C,Kc,R,stride,pad", [(2, 28, 64, 64, 3, 1, 1), (2, 14, 128, 256, 3, 2, 1),
+                                                   (2, 30, 8, 64, 7, 2, 3), (4, 7, 512, 512, 3, 1, 1),
+                                                   (32, 28, 64, 64, 3, 1, 1), (64, 14, 128, 256, 3, 1, 1),
+                                                   (64, 7, 256, 512, 1, 2, 0), (256, 4, 512, 512, 3, 1, 1)])
+def test_wgrad_split_k_groups(N, H, C, Kc, R, stride, pad):
+    """The trunk's default weight gradient (variant 8: two K-groups of waves per workgroup, each a contiguous half of
+    the split's pixels on its own ring, their tiles summed in LDS in group order) against the one-group ring (variant
+    4) at the same split count: the fp32 sums split at a different place, so the two agree to fp32 rounding; every
+    launch is bitwise repeatable (ragged splits included: P not a multiple of the split's 64-pixel steps)."""
+    from multimodalemotionrecognition_amd import kernels as K
+
+    torch.manual_seed(12)
+    Ho = (H + 2 * pad - R) // stride + 1
+    x = torch.randn(N, H, H, C, device="cuda").bfloat16()
+    dy = torch.randn(N, Ho, Ho, Kc, device="cuda").bfloat16()
+    creal = 3 if C == 8 else C
+    P = N * Ho * Ho
+    out = {}
+    for v, splits in ((4, None), (8, None), (8, 3), (4, 3), (8, None)):
+        dw = torch.zeros(Kc, creal, R, R, device="cuda")
+        K.conv_wgrad(x, dy, dw, R, R, stride, pad, creal=creal, variant=v, splits=splits)
+        out.setdefault((v, splits), []).append(dw)
+    a, b = out[(8, None)]
+    assert torch.equal(a, b)
+    ref = (x.float().permute(0, 3, 1, 2)[:, :creal], dy.float().permute(0, 3, 1, 2))
+    dw_ref = torch.nn.grad.conv2d_weight(ref[0], (Kc, creal, R, R), ref[1], stride=stride, padding=pad)
+    scale = float(dw_ref.abs().max())
+    for key in ((4, None), (8, None), (8, 3)):
+        assert (out[key][0] - dw_ref).abs().max() <= 5e-3 * scale + 1e-3, key
+    # same split count: only the in-workgroup split point differs
+    assert (out[(8, 3)][0] - out[(4, 3)][0]).abs().max() <= 2e-5 * scale + 1e-6
+    if P > 64:
+        assert K.wgrad_split_count(P, 3) <= 3
+
+
 def test_wgrad_fold_batch_matches_immediate_fold():
     """Deferred slabs folded by ONE mer_wgrad_fold_batch launch == the per-conv fold (fold+scatter below 17 slabs,
     reduce + scatter above), for records of 1-12, 13-48 and > 48 slabs, Creal < C, and the stem's map record
