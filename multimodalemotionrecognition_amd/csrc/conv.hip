@@ -1613,10 +1613,6 @@ int launch_conv_pipe(ConvGeom& g, hipStream_t st, int variant) {
     return PAR ? launch_conv_pipe_t<DGRAD, PAR, 64, 128, 2, 4, 2, 64, 2>(g, st)
                : launch_conv_pipe_t<DGRAD, PAR, 64, 128, 2, 4, 3, 64, 2>(g, st);
   }
-  if (variant == 8) {  // in-workgroup split-K (two K-groups) on the 128-row tiles
-    if (bn == 64) return launch_conv_pipe_t<DGRAD, PAR, 128, 64, 4, 2, 2, 64, 2>(g, st);
-    return launch_conv_pipe_t<DGRAD, PAR, 128, 128, 2, 4, 2, 64, 2>(g, st);
-  }
   if (variant == 3 && !small_m) {  // 256-row tiles (8 / 16 waves) for the large-M layers
     // (the 16-wave dgrad tile needs more than 128 VGPRs and would spill to scratch: 8-wave 256 x 64 tiles instead;
     // tools/check_scratch.py keeps every kernel of the library scratch-free)
@@ -1898,18 +1894,18 @@ int launch_conv_halo(ConvGeom& g, hipStream_t st, int kind) {
   return (int)hipErrorInvalidValue;
 }
 
-// Default tile for a non-parity-class conv (forward, or stride-1 input gradient): the in-workgroup split-K forms on the
-// small-M layers -- 64-row tiles with two K-groups (7) when one such tile per CU covers the output (ResNet18 layer4:
-// 256 tiles), else 128-row tiles with two K-groups (8) when those do (layer3: 196 tiles) -- provided each K-group gets
-// >= 4 K-steps; otherwise the one-group tiles (`fallback`).  tools/pipe_phases.py / bench_conv.py at B = 32: layer4
-// 3x3 fwd 44.1 -> 35.8 us, dgrad 52.4 -> 43.1; layer3 3x3 fwd 34.1 -> 28.2, dgrad 40.3 -> 35.7; layer4.0 / layer3.0
-// stride-2 fwd 24.5 -> 20.6 / 19.8 -> 18.1 (profiles/r06/bench_conv_kg.txt).
+// Default tile for a non-parity-class conv (forward, or stride-1 input gradient): the in-workgroup split-K form (7: 64-row
+// tiles, two K-groups) when one such tile per CU covers the output (ResNet18 layer4: 256 tiles) and each K-group gets
+// >= 4 K-steps; otherwise the one-group tiles (`fallback`).  Serialized trunk at B = 32 (profiles/r06/trunk_table_serial
+// .txt vs r05): layer4 3x3 fwd 44 -> 36.5 us, dgrad 50-53 -> 41-46.5; layer4.0 stride-2 fwd 24.2 -> 22.1.  Measured and
+// dropped: 128-row tiles with two K-groups for layer3 (196 tiles) won standalone with warm operands (34.1 -> 28.2 us)
+// but not in the trunk (33.4 -> 34.0, dgrad 39 -> 42) nor in a same-box step A/B (205.17 vs 205.35 steps/s, 4 pairs);
+// 64 x 64 per-wave sub-tiles with four / two K-groups lost on every layer (profiles/r06/bench_conv_v10_v11_lost.txt).
 int conv_default_variant(const ConvGeom& g, int fallback) {
   if (!g.vec || g.Kred < 8 * CBK) return fallback;
   const long M = (long)g.N * g.OH * g.OW;
   const long nt = (g.Ncols + (g.Ncols <= 64 ? 63 : 127)) / (g.Ncols <= 64 ? 64 : 128);
   if (((M + 63) / 64) * nt <= cu_count()) return 7;
-  if (((M + 127) / 128) * nt <= cu_count()) return 8;
   return fallback;
 }
 
@@ -1929,7 +1925,7 @@ MER_API int mer_conv_fwd(int N, int H, int W, int C, int K, int R, int S, int st
 
 MER_API int mer_conv_fwd_ex(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, const void* x,
                             const void* w_packed, void* y, float* stats, int variant, void* stream) {
-  if (C % 8 || variant < -1 || variant > 8) return (int)hipErrorInvalidValue;
+  if (C % 8 || variant < -1 || variant > 7) return (int)hipErrorInvalidValue;
   ConvGeom g{};
   g.N = N; g.IH = H; g.IW = W; g.IC = C;
   g.OH = (H + 2 * pad - R) / stride + 1; g.OW = (W + 2 * pad - S) / stride + 1;
@@ -1974,7 +1970,7 @@ MER_API int mer_conv_dgrad_ds(int N, int H, int W, int C, int K, int R, int S, i
                               const void* bn_mask, const void* bn_x, const float* bn_ms, float* bn_red,
                               const void* bn_x2, const float* bn_ms2, float* bn_red2, const void* ds_dy,
                               const void* ds_wt_packed, int ds_K, int variant, void* stream) {
-  if (K % 8 || C % 8 || variant < -1 || variant > 8) return (int)hipErrorInvalidValue;
+  if (K % 8 || C % 8 || variant < -1 || variant > 7) return (int)hipErrorInvalidValue;
   const bool auto_variant = variant == -1;
   // 64-channel outputs (layer1, the layer2.0 input gradients): 32-wide K-tiles on a 4-deep ring with 4-wave tiles
   // (tools/bench_conv.py --fused: layer1 101 -> 65 us, layer2.0 s2 74 -> 51, downsample 48 -> 31); wider outputs

@@ -540,11 +540,13 @@ def partials_sum(parts_buf, out):
 # 1024 leaves only 4 splits (layer4 3x3: 65 -> 58 us).
 # Target workgroups per wgrad launch: 768 (256 / 384 / 512 lose 3.1 / 1.3 / 0.3 % of the step, 1024 loses 0.4 %).
 _WGRAD_WGS = 768
-# The trunk's default wgrad form for K > 64 output channels (round 6): conv.hip variant 8, two K-groups of 8 waves per
-# workgroup (in-workgroup split-K over the pixels).  A launch of it covers the pixels of two one-group splits: half the
-# splits -- and half the fp32 slabs written and folded -- for the same waves per CU, so it targets _WGRAD_WGS / 2
-# workgroups.  The 64-channel stem / layer1 wgrads keep the one-group ring (4): its 48 KB blocks run three per CU,
-# the 96 KB two-group block one (stem 78 -> 110 us standalone, profiles/r06/bench_wgrad_kg.txt).
+# The trunk's default wgrad form for the stride-1 3x3 convs with K > 64 output channels (round 6): conv.hip variant 8,
+# two K-groups of 8 waves per workgroup (in-workgroup split-K over the pixels).  A launch of it covers the pixels of two
+# one-group splits: half the splits -- and half the fp32 slabs written and folded (~340 of the ~520 MB per step) -- for
+# the same waves per CU, so it targets _WGRAD_WGS / 2 workgroups.  The others keep the one-group ring (4): the
+# 64-channel stem / layer1 (its 48 KB blocks run three per CU, the 96 KB two-group block one: stem 78 -> 110 us
+# standalone, profiles/r06/bench_wgrad_kg.txt), and the stride-2 / 1x1 wgrads, whose slabs are small and whose kernels
+# ran 2-8 us slower each in the serialized trunk (profiles/r06/trunk_table_serial.txt).
 WGRAD_VARIANT = 8
 
 
@@ -602,7 +604,7 @@ def conv_wgrad(x, dy, dw, R, S, stride, pad, creal=None, variant=-1, splits=None
     P = N * Ho * Wo
     tiles = ((Kc + 127) // 128) * ((R * S * C + 127) // 128)
     if variant == -1:
-        variant = WGRAD_VARIANT if Kc > 64 else 4
+        variant = WGRAD_VARIANT if (Kc > 64 and stride == 1 and R * S > 1) else 4
     kg = 2 if variant == 8 else 1  # K-groups per workgroup
     if splits is None:  # ~768 groups of 8 waves (3 per CU), >= _wgrad_min_pix pixels each
         splits = int(max(1, min(-(-_WGRAD_WGS // (kg * tiles)), P // (kg * _wgrad_min_pix(Kc * R * S * C, tiles)))))

@@ -336,9 +336,9 @@ def test_halo_stem_bit_identical(N):
 @pytest.mark.parametrize("N,H,C,Kc,stride", [(8, 7, 256, 256, 1), (16, 4, 512, 512, 1), (8, 14, 128, 256, 2),
                                               (16, 7, 256, 512, 2), (5, 14, 128, 128, 1), (6, 28, 64, 64, 1),
                                               (3, 28, 64, 128, 2)])
-@pytest.mark.parametrize("variant", [7, 8])
+@pytest.mark.parametrize("variant", [7])
 def test_conv_split_k_groups(N, H, C, Kc, stride, variant):
-    """In-workgroup split-K (variants 7 / 8: two K-groups of waves, each a contiguous half of the K-steps on its own LDS
+    """In-workgroup split-K (variant 7: two K-groups of waves, each a contiguous half of the K-steps on its own LDS
     ring, tiles summed in group order in LDS) against the one-group kernel (variant 2) on the same tiles: the only
     difference is where the fp32 sum splits, so outputs agree to one bf16 rounding and the fused BN statistics /
     BN-backward sums (two BNs, residual under a ReLU mask, the stride-2 parity classes and the fused downsample

@@ -9,6 +9,11 @@ the algorithmic bytes = the bf16 A source read once + the bf16 weights + the bf1
 the fp32 weight gradient), and frac = achieved / attainable.  tools/trunk_serial.py makes a serialized
 (single-stream, trunk-only) trace for this table."""
 import csv
+import sys as _sys
+from pathlib import Path as _Path
+
+_sys.path.insert(0, str(_Path(__file__).resolve().parent))
+from pmc_head import kernel_key  # noqa: E402  (demangled-name key that keeps anonymous-namespace kernels)
 import os
 import sys
 
@@ -120,7 +125,7 @@ def main():
         n = r["Kernel_Name"]
         if any(s in n for s in ("bn_", "wgrad_reduce", "wgrad_scatter", "wgrad_fold", "pack_w", "pack_input", "stem_",
                                 "maxpool", "avgpool", "partials_sum")):
-            key = n.split("(")[0][:60]
+            key = kernel_key(n)[:60]
             other[key] = other.get(key, 0.0) + dur(r)
     print(f"# conv total {sum(tot.values()):.1f} us; BN / pack / weight-gradient fold / pool kernels "
           f"{sum(other.values()):.1f} us; serialized trunk {sum(tot.values()) + sum(other.values()):.1f} us:")
