@@ -756,3 +756,47 @@ def test_dgrad_fused_downsample_vs_torch(C, Kc, H):
     dx2 = torch.empty_like(dx)
     K.conv_dgrad(dyh, wt, dx2, 3, 3, 2, 1, residual=dxd)
     assert rel_rms(got, dx2.float().permute(0, 3, 1, 2).cpu()) < 6e-3
+
+
+@pytest.mark.parametrize("M,C", [(4096, 512), (4097, 512), (12544, 256), (50176, 128), (65536, 64), (200704, 64)])
+def test_bn_finalize_and_partials_sum_all_row_counts(M, C):
+    """mer_bn_finalize / mer_partials_sum over every row-count regime of the trunk at B = 32: <= 64 partial rows (one
+    launch), 65..1024 rows (one 16-wave launch per 64 channels, round 6: layer2 / layer3), > 1024 rows (the two-stage
+    fold: stem / layer1).  Against float64 sums of the same rows; running statistics as torch (momentum, unbiased
+    variance); each launch bitwise repeatable."""
+    from multimodalemotionrecognition_amd import kernels as K
+
+    torch.manual_seed(13)
+    rows = K.bn_stat_rows(M)
+    st = torch.zeros(rows, C, 2, device="cuda")
+    data = rows - 64
+    vals = torch.randn(data, C, 2, device="cuda")
+    vals[..., 0] = vals[..., 0] * 3 + 1.0   # per-tile sums
+    vals[..., 1] = vals[..., 1].abs() * 40 + 64.0  # per-tile sums of squares
+    st[:data] = vals
+    ref_sum = vals.double().sum(0).cpu()
+    mean = ref_sum[:, 0] / M
+    var = (ref_sum[:, 1] / M - mean * mean).clamp_min(0)
+    outs = []
+    for _ in range(2):
+        ms = torch.empty(C, 2, device="cuda")
+        rm, rv = torch.zeros(C, device="cuda"), torch.ones(C, device="cuda")
+        nbt = torch.zeros((), dtype=torch.int64, device="cuda")
+        K.bn_finalize(st.clone(), M, 1e-5, 0.1, ms, rm, rv, nbt)
+        outs.append((ms, rm, rv, nbt))
+    (ms, rm, rv, nbt), (ms2, rm2, rv2, _) = outs
+    assert torch.equal(ms, ms2) and torch.equal(rm, rm2) and torch.equal(rv, rv2)
+    assert torch.allclose(ms[:, 0].cpu().double(), mean, rtol=1e-5, atol=1e-6)
+    assert torch.allclose(ms[:, 1].cpu().double(), (var + 1e-5).rsqrt(), rtol=1e-4)
+    assert torch.allclose(rm.cpu().double(), 0.1 * mean, rtol=1e-5, atol=1e-7)
+    assert torch.allclose(rv.cpu().double(), 0.9 + 0.1 * var * M / (M - 1), rtol=1e-4)
+    assert int(nbt) == 1
+    # the backward's partial-row fold: MER_BN_RED_ROWS(M) rows (+ the 64 scratch rows it may use)
+    prow = K.bn_red_rows(M)
+    parts = torch.zeros(prow, C, 2, device="cuda")
+    parts[:prow - 64] = torch.randn(prow - 64, C, 2, device="cuda")
+    s1 = K.partials_sum(parts.clone(), torch.empty(C, 2, device="cuda"))
+    s2 = K.partials_sum(parts.clone(), torch.empty(C, 2, device="cuda"))
+    assert torch.equal(s1, s2)
+    ref = parts[:prow - 64].double().sum(0).cpu()
+    assert torch.allclose(s1.cpu().double(), ref, rtol=1e-5, atol=1e-4)
