@@ -1123,9 +1123,11 @@ __device__ __forceinline__ void conv_epilogue_vec(const ConvGeom& g, f32x4 (&acc
       sB[e] += __shfl_xor(sB[e], o, 64);
       if (has_x2) sC[e] += __shfl_xor(sC[e], o, 64);
     }
+  if (ct_slot >= 0) CT(ct_slot + 3);
   // the WM waves of a column range meet in LDS: red[(wr*WN + wc)][TN][3]
   float* red = smemf;
   lds_barrier();  // every wave is past its staging slice
+  if (ct_slot >= 0) CT(ct_slot + 4);
   if (wr > 0 && lane < LPR)
 #pragma unroll
     for (int e = 0; e < 8; ++e) {

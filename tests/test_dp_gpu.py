@@ -123,14 +123,21 @@ def _worker_rccl1(port, out_dir, use_dp):
             dist.init_process_group(backend="nccl", rank=0, world_size=1)
         m, opt = _build()
         sync = None
-        if use_dp:
-            sync = GradAllReduce(opt, model=m, force=True, bucket_bytes=8 << 20)
+        if use_dp:  # (timing: bench.py's DP diagnostics, HIP events on the compute stream)
+            sync = GradAllReduce(opt, model=m, force=True, bucket_bytes=8 << 20, timing=True)
             assert sync.active and sync._early_end, "the early head+layer4 bucket must be armed"
         step = TrainStep(m, opt, make_loss("xattn"), "xattn", sync)
         for s in range(3):  # eager, capture, replay of the split trunk-backward graphs
             step(*_batch(0, s))
         torch.cuda.synchronize()
-        torch.save({"flat": [f.cpu() for f in opt.flat_params()]}, os.path.join(out_dir, f"dp{int(use_dp)}.pt"))
+        rec = {"flat": [f.cpu() for f in opt.flat_params()]}
+        if use_dp:
+            import json
+
+            import bench
+            dp = bench.dp_fields(4.0, sync, torch.device("cuda", 0))
+            rec["dp"] = json.dumps(dp)
+        torch.save(rec, os.path.join(out_dir, f"dp{int(use_dp)}.pt"))
     finally:
         if dist.is_initialized():
             dist.destroy_process_group()
@@ -148,6 +155,14 @@ def test_rccl_world1_bucket_path_bitwise(tmp_path):
         p.join(timeout=600)
         assert p.exitcode == 0
     a = torch.load(tmp_path / "dp0.pt", weights_only=True)["flat"]
-    b = torch.load(tmp_path / "dp1.pt", weights_only=True)["flat"]
+    rec = torch.load(tmp_path / "dp1.pt", weights_only=True)
+    b = rec["flat"]
     for x, y in zip(a, b):
         assert torch.equal(x, y), float((x - y).abs().max())
+    # the DP diagnostics the multi-GPU bench line carries, from HIP events of the same run
+    import json
+    dp = json.loads(rec["dp"])
+    (r0,) = dp["per_rank"]
+    assert r0["timed_steps"] == 3 and r0["early_bucket_steps"] == 3
+    assert r0["allreduce_exposed_ms"] >= 0 and r0["early_bucket_lead_ms"] > 0
+    assert dp["bytes_allreduced_per_step"] > 40e6

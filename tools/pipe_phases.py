@@ -77,6 +77,11 @@ def run(variants):
                     p2 = np.median(c[b, 11] - c[b, 10]) * tick_us
                     p3 = np.median(c[b, 12] - c[b, 11]) * tick_us
                     line += f" | epi: passes {p1:5.2f} reduce {p2:5.2f} flush {p3:5.2f}"
+                    if kind == "dgrad" and all(c[b, 13]) and all(c[b, 14]):  # reduce = xor tree | barrier | rest
+                        x1 = np.median(c[b, 13] - c[b, 10]) * tick_us
+                        x2 = np.median(c[b, 14] - c[b, 13]) * tick_us
+                        x3 = np.median(c[b, 11] - c[b, 14]) * tick_us
+                        line += f" (xor {x1:5.2f} barrier {x2:5.2f} meet+store {x3:5.2f})"
                 if st == 2 and kind == "dgrad":
                     # grid.y = parity class slot (3 - class); linear id = y * gridDim.x + x
                     gx = (max(used) // 4) + 1 if False else None
