@@ -24,7 +24,8 @@
 
 /* BatchNorm batch statistics of a conv forward (mer_conv_fwd `stats`): float[MER_BN_STAT_ROWS(M)][C][2]
  * (sum, sum of squares), zeroed by the caller, M = N*Ho*Wo output pixels.  Each output row tile of the
- * conv stores its own row (a single writer per element: deterministic), unused rows stay zero, and the last
+ * conv stores its own row (a single writer per element: deterministic) -- the persistent halo kernels (layer1, stem)
+ * instead store one row per workgroup, summed over its tiles in a fixed order -- unused rows stay zero, and the last
  * 64 rows are mer_bn_finalize's scratch.  The backward reductions use the same single-writer rows
  * (MER_BN_RED_ROWS, MER_BN_RED_WS_ROWS below), so the whole trunk step is free of fp32 atomics. */
 #define MER_BN_STAT_PARTS 64

@@ -860,12 +860,12 @@ __device__ __forceinline__ ParClass par_class(const ConvGeom& g, int cls) {
 // outstanding global store and DMA (vmcnt(0)), which the persistent halo kernel overlaps with its next tile.  The WM waves sharing a column meet in LDS (red: >= WM*WN*TN*2
 // idle floats) in wave order; the block then STORES its per-column (sum, sumsq) into stats row stat_row -- every (row
 // tile, column) has exactly one writer, so the statistics (and every BatchNorm output) are bitwise deterministic.
+// the lane's partial (sum, sumsq) of its accumulator-layout columns j * 16 + (lane & 15) over its rows (< M)
 template <int FM, int FN, int WM, int WN>
-__device__ __forceinline__ void conv_tile_stats(const ConvGeom& g, const f32x4 (&acc)[FM][FN], float* red, int w,
-                                                int lane, int m0, int n0, int M, long stat_row) {
+__device__ __forceinline__ void conv_tile_stats_lane(const ConvGeom& g, const f32x4 (&acc)[FM][FN], int w, int lane,
+                                                     int m0, int n0, int M, float (&part)[FN][2]) {
   constexpr int TM = FM * 16, TN = FN * 16;
   const int wr = w / WN, wc = w % WN, fr = lane & 15, fq = lane >> 4;
-  float part[FN][2];
 #pragma unroll
   for (int j = 0; j < FN; ++j) {
     const int col = n0 + wc * TN + j * 16 + fr;
@@ -881,13 +881,25 @@ __device__ __forceinline__ void conv_tile_stats(const ConvGeom& g, const f32x4 (
           csq += hv * hv;
         }
       }
-    csum += __shfl_xor(csum, 16, 64);
-    csum += __shfl_xor(csum, 32, 64);
-    csq += __shfl_xor(csq, 16, 64);
-    csq += __shfl_xor(csq, 32, 64);
     part[j][0] = csum;
     part[j][1] = csq;
   }
+}
+
+// lane partials -> the block's per-column (sum, sumsq) row: two shuffles per value, the WM waves of a column meet in
+// LDS (red) in wave order, one writer per element
+template <int FN, int WM, int WN>
+__device__ __forceinline__ void conv_stats_finish(const ConvGeom& g, float (&part)[FN][2], float* red, int w, int lane,
+                                                  int n0, long stat_row) {
+  constexpr int TN = FN * 16;
+  const int wr = w / WN, wc = w % WN, fr = lane & 15, fq = lane >> 4;
+#pragma unroll
+  for (int j = 0; j < FN; ++j)
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      part[j][q] += __shfl_xor(part[j][q], 16, 64);
+      part[j][q] += __shfl_xor(part[j][q], 32, 64);
+    }
   lds_barrier();
   if (wr > 0 && fq == 0)
 #pragma unroll
@@ -914,6 +926,32 @@ __device__ __forceinline__ void conv_tile_stats(const ConvGeom& g, const f32x4 (
     }
   }
 }
+
+template <int FM, int FN, int WM, int WN>
+__device__ __forceinline__ void conv_tile_stats(const ConvGeom& g, const f32x4 (&acc)[FM][FN], float* red, int w,
+                                                int lane, int m0, int n0, int M, long stat_row) {
+  float part[FN][2];
+  conv_tile_stats_lane<FM, FN, WM, WN>(g, acc, w, lane, m0, n0, M, part);
+  conv_stats_finish<FN, WM, WN>(g, part, red, w, lane, n0, stat_row);
+}
+
+// Running per-lane partial sums of a persistent workgroup's tiles (conv_halo_kernel): each tile's fused column
+// reductions add into these -- every tile of a workgroup covers the same output columns -- and the cross-lane /
+// cross-wave reduction and the partial-row store run ONCE per workgroup (conv_epilogue_acc_finish), not once per tile.
+// (vector types rather than arrays: a float[8] member left in scratch once the finish's 16-byte stores were
+// vectorised over it)
+typedef __attribute__((ext_vector_type(8))) float f32x8;
+template <int FN>
+struct EpiAcc {
+  f32x8 sA, sB, sC;  // dgrad: the BN-backward sums of the lane's 8 pass-layout columns
+  float fs[FN][2];   // fwd: the BN statistics of the lane's accumulator-layout columns
+  __device__ void zero() {
+    sA = sB = sC = f32x8{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < FN; ++j) fs[j][0] = fs[j][1] = 0.f;
+  }
+};
+struct EpiNoAcc {};
 
 // The 16-byte conv epilogue: each wave stages fp32 accumulators of 16-row groups of its TM x TN sub-tile in its own
 // slice (WAVE_FLOATS floats at smemf + w * WAVE_FLOATS, idle LDS), then every lane owns 8 consecutive columns of one
@@ -980,11 +1018,13 @@ __device__ __forceinline__ void conv_epilogue_prefetch(const ConvGeom& g, EpiPre
 }
 
 template <bool DGRAD, int FM, int FN, int WM, int WN, int WAVE_FLOATS, class OutRow, class Pre = EpiNone,
-          bool DEFER = false, bool X2 = true>
+          bool DEFER = false, bool X2 = true, class AccT = EpiNoAcc>
 __device__ __forceinline__ void conv_epilogue_vec(const ConvGeom& g, f32x4 (&acc)[FM][FN], float* smemf, int w,
                                                   int lane, int m0, int n0, int M, long red_row_id, long stat_row,
-                                                  OutRow out_row, const Pre* pre = nullptr, int ct_slot = -1) {
+                                                  OutRow out_row, const Pre* pre = nullptr, int ct_slot = -1,
+                                                  AccT* accp = nullptr) {
   constexpr bool PREF = !std::is_same<Pre, EpiNone>::value;
+  constexpr bool ACC = !std::is_same<AccT, EpiNoAcc>::value;  // add the reductions into *accp, store nothing
   using E = EpiGeo<FM, FN, WAVE_FLOATS>;
   constexpr int TM = FM * 16, TN = FN * 16;
   const int wr = w / WN, wc = w % WN, fr = lane & 15, fq = lane >> 4;
@@ -1113,6 +1153,18 @@ __device__ __forceinline__ void conv_epilogue_vec(const ConvGeom& g, f32x4 (&acc
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
   if (ct_slot >= 0) CT(ct_slot);
+  if constexpr (ACC) {
+    if (do_bnr) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        accp->sA[e] += sA[e];
+        accp->sB[e] += sB[e];
+        accp->sC[e] += sC[e];
+      }
+      flush();
+      return;
+    }
+  }
   if (do_bnr) {
   // lanes sharing this lane's 8 columns: lane % LPR equal -> xor over the row bits of the lane index
 #pragma unroll
@@ -1176,10 +1228,78 @@ __device__ __forceinline__ void conv_epilogue_vec(const ConvGeom& g, f32x4 (&acc
     for (int j = 0; j < FN; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) acc[i][j][r] = bf2f(f2bf(acc[i][j][r]));
+  if constexpr (ACC) {
+    float part[FN][2];
+    conv_tile_stats_lane<FM, FN, WM, WN>(g, acc, w, lane, m0, n0, M, part);
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      accp->fs[j][0] += part[j][0];
+      accp->fs[j][1] += part[j][1];
+    }
+    flush();
+    return;
+  }
   conv_tile_stats<FM, FN, WM, WN>(g, acc, smemf, w, lane, m0, n0, M, stat_row);
   if (ct_slot >= 0) CT(ct_slot + 1);
   flush();
   if (ct_slot >= 0) CT(ct_slot + 2);
+}
+
+// The workgroup's accumulated reductions (EpiAcc) -> its one partial row: the dgrad's BN-backward sums meet across the
+// lanes sharing columns (xor tree) and the WM waves (LDS, wave order) as in conv_epilogue_vec; the forward statistics
+// as in conv_stats_finish.  Called by every wave, with smemf free LDS.
+template <bool DGRAD, int FM, int FN, int WM, int WN, int WAVE_FLOATS, bool X2 = true>
+__device__ __forceinline__ void conv_epilogue_acc_finish(const ConvGeom& g, EpiAcc<FN>& a, float* smemf, int w,
+                                                         int lane, int n0, long row_id) {
+  if constexpr (DGRAD) {
+    if (!g.bnr_red) return;
+    using E = EpiGeo<FM, FN, WAVE_FLOATS>;
+    constexpr int TN = FN * 16, LPR = E::LPR;
+    const int wr = w / WN, wc = w % WN;
+    const int lc = (lane % LPR) * 8;
+    const int colv = n0 + wc * TN + lc;
+    const bool cok = colv < g.Ncols;
+    const bool has_x2 = X2 && g.bnr_x2 != nullptr;
+#pragma unroll
+    for (int o = LPR; o < 64; o <<= 1)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        a.sA[e] += __shfl_xor(a.sA[e], o, 64);
+        a.sB[e] += __shfl_xor(a.sB[e], o, 64);
+        if (has_x2) a.sC[e] += __shfl_xor(a.sC[e], o, 64);
+      }
+    float* red = smemf;
+    lds_barrier();
+    if (wr > 0 && lane < LPR)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float* o = red + ((wr * WN + wc) * TN + lc + e) * 3;
+        o[0] = a.sA[e];
+        o[1] = a.sB[e];
+        o[2] = a.sC[e];
+      }
+    lds_barrier();
+    if (wr != 0 || lane >= LPR || !cok) return;
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+#pragma unroll
+      for (int q = 1; q < WM; ++q) {
+        const float* o = red + ((q * WN + wc) * TN + lc + e) * 3;
+        a.sA[e] += o[0];
+        a.sB[e] += o[1];
+        a.sC[e] += o[2];
+      }
+    const long slab = row_id * g.Ncols * 2 + 2 * colv;
+#pragma unroll
+    for (int e = 0; e < 8; e += 2) {
+      *reinterpret_cast<f32x4*>(g.bnr_red + slab + 2 * e) = f32x4{a.sA[e], a.sB[e], a.sA[e + 1], a.sB[e + 1]};
+      if (g.bnr_red2)
+        *reinterpret_cast<f32x4*>(g.bnr_red2 + slab + 2 * e) = f32x4{a.sA[e], a.sC[e], a.sA[e + 1], a.sC[e + 1]};
+    }
+  } else {
+    if (!g.stats) return;
+    conv_stats_finish<FN, WM, WN>(g, a.fs, smemf, w, lane, n0, row_id);
+  }
 }
 
 // Minimum waves per SIMD of a conv_pipe_kernel block of nw waves: 16-wave blocks 1 per CU, 8-wave blocks 2 per CU --
@@ -1723,7 +1843,8 @@ __device__ __forceinline__ int wchunk(int n, int c) {
 }
 }  // namespace halo
 
-template <bool DGRAD, class GE, int WM, int WN, int OCC>
+// X2: the dgrad's second fused BN (bnr_x2) may be present (false: its sums and registers are compiled out)
+template <bool DGRAD, class GE, int WM, int WN, int OCC, bool X2 = true>
 __global__ __launch_bounds__(64 * WM * WN, OCC) void conv_halo_kernel(ConvGeom g) {
   constexpr int WAVES = WM * WN;
   constexpr int TM = halo::BM / WM, TN = 64 / WN, FM = TM / 16, FN = TN / 16;
@@ -1771,7 +1892,13 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void conv_halo_kernel(ConvGeom g
 
   // Per tile: issue the next tile's halo DMA, run the K loop on this one, wait for that DMA (and the previous tile's
   // epilogue stores -- both had the whole K loop to land), then the epilogue (staged through this tile's halo buffer,
-  // now free).  No vmcnt wait follows the epilogue: its stores drain under the next K loop.
+  // now free).  No vmcnt wait follows the epilogue: its stores drain under the next K loop.  The fused column
+  // reductions (forward BN statistics, the dgrad's BN-backward sums) accumulate per lane over the workgroup's tiles --
+  // all of them cover the same 64 output columns -- and are reduced and stored once, as partial row blockIdx.x, after
+  // the loop (round 6: one cross-lane / cross-wave reduction per workgroup instead of per tile, and grid-size partial
+  // rows instead of one per tile for the folds).
+  EpiAcc<FN> eacc;
+  eacc.zero();
   for (int cur = 0, it = 0; tile < ntiles; tile += gridDim.x, cur ^= 1, ++it) {
     bf16_t* const hb = hbuf + cur * GE::ELEMS;
     if (tile + (int)gridDim.x < ntiles) stage_halo(hbuf + (cur ^ 1) * GE::ELEMS, tile + gridDim.x);
@@ -1780,7 +1907,9 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void conv_halo_kernel(ConvGeom g
     const auto out_row = [](int row) { return (long)row; };
     constexpr int EWF = GE::ELEMS / 2 / WAVES;  // epilogue staging floats per wave (this tile's halo buffer)
     EpiPre<EpiGeo<FM, FN, EWF>::NP> pre;
-    if constexpr (DGRAD) conv_epilogue_prefetch<DGRAD, FM, FN, WM, WN, EWF>(g, pre, w, lane, m0, 0, M, out_row);
+    if constexpr (DGRAD)
+      conv_epilogue_prefetch<DGRAD, FM, FN, WM, WN, EWF, decltype(out_row), EpiGeo<FM, FN, EWF>::NP, X2>(
+          g, pre, w, lane, m0, 0, M, out_row);
     int hpb[FM], yv[FM];  // per fragment row of this lane: halo pixel of tap (0, 0), input row of tap row 0
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
@@ -1834,16 +1963,20 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void conv_halo_kernel(ConvGeom g
     CT(it < 11 ? 4 + 5 * it : 63);
     const int ct_slot = it == 1 ? 60 : -1;  // (timing build: stamps inside the second tile's epilogue)
     if constexpr (DGRAD)
-      conv_epilogue_vec<DGRAD, FM, FN, WM, WN, EWF, decltype(out_row), decltype(pre), true>(
-          g, acc, reinterpret_cast<float*>(hb), w, lane, m0, 0, M, (long)tile, (long)tile, out_row, &pre, ct_slot);
+      conv_epilogue_vec<DGRAD, FM, FN, WM, WN, EWF, decltype(out_row), decltype(pre), true, X2, EpiAcc<FN>>(
+          g, acc, reinterpret_cast<float*>(hb), w, lane, m0, 0, M, (long)tile, (long)tile, out_row, &pre, ct_slot,
+          &eacc);
     else
-      conv_epilogue_vec<DGRAD, FM, FN, WM, WN, EWF, decltype(out_row), EpiNone, true>(
+      conv_epilogue_vec<DGRAD, FM, FN, WM, WN, EWF, decltype(out_row), EpiNone, true, true, EpiAcc<FN>>(
           g, acc, reinterpret_cast<float*>(hb), w, lane, m0, 0, M, (long)tile, (long)tile, out_row,
-          static_cast<const EpiNone*>(nullptr), ct_slot);
+          static_cast<const EpiNone*>(nullptr), ct_slot, &eacc);
     CT(it < 11 ? 5 + 5 * it : 63);
     lds_barrier();    // every wave is past its epilogue's use of hb before the DMA two tiles on refills it
     CT(it < 11 ? 6 + 5 * it : 63);
   }
+  // (no DMA is in flight after the last tile: the halo buffers are free)
+  conv_epilogue_acc_finish<DGRAD, FM, FN, WM, WN, GE::ELEMS / 2 / WAVES, X2>(g, eacc, reinterpret_cast<float*>(hbuf), w,
+                                                                          lane, 0, (long)blockIdx.x);
 }
 
 using HaloL1 = halo::Geo<64, 3, 1, 28, 0>;    // layer1: 3x3 / pad 1, 64 -> 64, 28x28
@@ -1874,23 +2007,27 @@ int cu_count() {
   return n;
 }
 
-template <bool DGRAD, class GE, int OCC>
+template <bool DGRAD, class GE, int OCC, bool X2 = true>
 int launch_halo_t(ConvGeom& g, hipStream_t st) {
   constexpr int WM = 4, WN = 2;  // 8 waves, 32 x 32 each: conv_pipe_kernel's 128 x 64 tile (variant 2)
   const size_t lds = GE::LDS_ELEMS * sizeof(bf16_t);
   static_assert(GE::LDS_ELEMS * 2 * OCC <= 160 * 1024, "LDS per CU");
-  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_halo_kernel<DGRAD, GE, WM, WN, OCC>),
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_halo_kernel<DGRAD, GE, WM, WN, OCC, X2>),
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return (int)hipErrorInvalidConfiguration;
   const int M = g.N * g.OH * g.OW, ntiles = (M + halo::BM - 1) / halo::BM;
   const int slots = OCC * cu_count();
-  hipLaunchKernelGGL((conv_halo_kernel<DGRAD, GE, WM, WN, OCC>), dim3(ntiles < slots ? ntiles : slots),
+  hipLaunchKernelGGL((conv_halo_kernel<DGRAD, GE, WM, WN, OCC, X2>), dim3(ntiles < slots ? ntiles : slots),
                      dim3(64 * WM * WN), lds, st, g);
   return (int)hipGetLastError();
 }
 
 template <bool DGRAD>
 int launch_conv_halo(ConvGeom& g, hipStream_t st, int kind) {
+  // (the dgrad without a second fused BN -- every layer1 dgrad of the train step -- drops its registers: the
+  // per-workgroup accumulators otherwise spill)
+  if constexpr (DGRAD)
+    if (kind == 1 && !g.bnr_x2) return launch_halo_t<DGRAD, HaloL1, 1, false>(g, st);
   if (kind == 1) return launch_halo_t<DGRAD, HaloL1, 1>(g, st);
   if constexpr (!DGRAD) return launch_halo_t<false, HaloStem, 2>(g, st);  // 71 KB of LDS: two workgroups per CU
   return (int)hipErrorInvalidValue;
