@@ -2594,10 +2594,15 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(int C, long M, int row
   if (rvar) rvar[c] = (1.f - momentum) * rvar[c] + momentum * var * ((float)M / (float)(M > 1 ? M - 1 : 1));
   if (nbt && c == 0) *nbt += 1;
 }
-// 64 < rows <= BN_WIDE_ROWS: the fold and the finalize in ONE launch (round 6).  A 16-wave block per 64 channels:
-// wave w sums rows w, w + 16, ... of its 64 channels (lane = channel; 16 rows' loads issued before the first add), the
-// 16 wave partials meet in LDS and wave 0 adds them in a fixed pairwise order -- deterministic, like the two-stage
-// form it replaces for ResNet18 layer2 / layer3 (784 / 196 rows at B = 32), one ~5 us launch less per BatchNorm.
+// 64 < rows <= BN_WIDE_ROWS: the fold and the finalize in ONE launch (round 6).  16 waves per block; wave w sums rows
+// w, w + 16, ... of the block's 64 columns (lane = column), the 16 wave partials meet in LDS and wave 0 adds them in a
+// fixed pairwise order -- deterministic, like the two-stage form it replaces for ResNet18 layer2 / layer3 (784 / 196
+// rows at B = 32), one ~5 us launch less per BatchNorm.  Every load of a thread's rows (NB <= 64 of them) is issued
+// before the first add: the batches-of-16 loop waited one memory latency per batch, 4 per pass at 784 rows, and the
+// finalize ran its sums and its sums of squares as two such passes (13.4 us per launch in the step trace).  The
+// forward finalize's columns are the interleaved (sum, sumsq) pairs of 32 channels, so one pass carries both and the
+// grid has twice the blocks.  The per-element order (even-ordinal rows into a0, odd into a1, then the wave tree) is
+// the batched loop's, so the results are bitwise those of the round-6 kernels.
 constexpr int BN_WIDE_ROWS = 1024;
 
 template <int N>
@@ -2609,37 +2614,42 @@ __device__ __forceinline__ float pair_tree(const float* v, int stride) {
   }
 }
 
-// per-(wave, element) partial over rows w, w + 16, ...: x[r * ld + e] for r < rows
-__device__ __forceinline__ float wide_rows_sum(const float* __restrict__ x, int rows, long ld, long e, int w) {
+// per-(wave, element) partial over rows w, w + 16, ... (< rows <= 16 * NB): x[r * ld + e]
+// (32-bit offsets from the column's base: rows * ld < 2^31 for every caller, and 64 loads in flight fit in 128 VGPRs)
+template <int NB>
+__device__ __forceinline__ float wide_rows_sum(const float* __restrict__ x, int rows, int ld, int e, int w) {
+  float v[NB];
+  const float* __restrict__ xe = x + e;
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    const int r = w + 16 * i;
+    v[i] = xe[(r < rows ? r : rows - 1) * ld];
+  }
   float a0 = 0.f, a1 = 0.f;
-  for (int r0 = w; r0 < rows; r0 += 16 * 16) {
-    float v[16];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int r = r0 + 16 * i;
-      v[i] = x[(long)(r < rows ? r : rows - 1) * ld + e];
-    }
-#pragma unroll
-    for (int i = 0; i < 16; i += 2) {
-      if (r0 + 16 * i < rows) a0 += v[i];
-      if (r0 + 16 * (i + 1) < rows) a1 += v[i + 1];
-    }
+  for (int i = 0; i < NB; i += 2) {
+    if (w + 16 * i < rows) a0 += v[i];
+    if (w + 16 * (i + 1) < rows) a1 += v[i + 1];
   }
   return a0 + a1;
 }
 
+template <int NB>
 __global__ __launch_bounds__(1024) void bn_finalize_wide_kernel(int C, long M, int rows, const float* __restrict__ stats,
                                                                 float eps, float momentum, float* __restrict__ ms,
                                                                 float* __restrict__ rmean, float* __restrict__ rvar,
                                                                 long long* __restrict__ nbt) {
-  __shared__ float part[2][16][64];
-  const int cl = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + cl, cc = c < C ? c : C - 1;
-  part[0][w][cl] = wide_rows_sum(stats, rows, 2L * C, 2L * cc, w);
-  part[1][w][cl] = wide_rows_sum(stats, rows, 2L * C, 2L * cc + 1, w);
+  __shared__ float part[16][64];
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int col = blockIdx.x * 64 + l;  // column of the [rows][C][2] layout: channel col / 2, sum (even) / sumsq (odd)
+  part[w][l] = wide_rows_sum<NB>(stats, rows, 2 * C, col < 2 * C ? col : 2 * C - 1, w);
   __syncthreads();
-  if (w != 0 || c >= C) return;
-  const float sum = pair_tree<16>(&part[0][0][cl], 64), sq = pair_tree<16>(&part[1][0][cl], 64);
+  if (w != 0) return;
+  const float tot = pair_tree<16>(&part[0][l], 64);
+  const float sq = __shfl_xor(tot, 1, 64);
+  const int c = col >> 1;
+  if ((l & 1) || c >= C) return;
+  const float sum = tot;
   const float mean = sum / M;
   const float var = fmaxf(sq / M - mean * mean, 0.f);
   ms[2 * c] = mean;
@@ -2650,14 +2660,23 @@ __global__ __launch_bounds__(1024) void bn_finalize_wide_kernel(int C, long M, i
 }
 
 // out[e] = sum over parts rows of in[p][e], e < 2C, for 64 < parts <= BN_WIDE_ROWS (one launch; see above)
+template <int NB>
 __global__ __launch_bounds__(1024) void partials_sum_wide_kernel(int C2, int parts, const float* __restrict__ in,
                                                                  float* __restrict__ out) {
   __shared__ float part[16][64];
   const int el = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int e = blockIdx.x * 64 + el, ec = e < C2 ? e : C2 - 1;
-  part[w][el] = wide_rows_sum(in, parts, C2, ec, w);
+  part[w][el] = wide_rows_sum<NB>(in, parts, C2, ec, w);
   __syncthreads();
   if (w == 0 && e < C2) out[e] = pair_tree<16>(&part[0][el], 64);
+}
+
+// the wide launches by row count: NB = 16 / 32 / 64 loads per thread
+template <class F16, class F32, class F64>
+static inline void wide_pick(int rows, F16 f16, F32 f32, F64 f64) {
+  if (rows <= 256) f16();
+  else if (rows <= 512) f32();
+  else f64();
 }
 
 MER_API int mer_bn_finalize(int C, long M, const float* stats, float eps, float momentum, float* ms, float* rmean,
@@ -2668,8 +2687,14 @@ MER_API int mer_bn_finalize(int C, long M, const float* stats, float eps, float 
   const float* src = stats;
   int rows = tiles;
   if (stats && tiles > 64 && tiles <= BN_WIDE_ROWS) {
-    hipLaunchKernelGGL(bn_finalize_wide_kernel, dim3((C + 63) / 64), dim3(1024), 0, st, C, M, tiles, stats, eps,
-                       momentum, ms, rmean, rvar, num_batches_tracked);
+    const dim3 grid((2 * C + 63) / 64);
+#define MER_BN_FIN_WIDE(NB)                                                                                          \
+  [&] {                                                                                                              \
+    hipLaunchKernelGGL(bn_finalize_wide_kernel<NB>, grid, dim3(1024), 0, st, C, M, tiles, stats, eps, momentum, ms, \
+                       rmean, rvar, num_batches_tracked);                                                            \
+  }
+    wide_pick(tiles, MER_BN_FIN_WIDE(16), MER_BN_FIN_WIDE(32), MER_BN_FIN_WIDE(64));
+#undef MER_BN_FIN_WIDE
     MER_LAUNCH_CHECK();
   }
   if (stats && tiles > 64) {
@@ -2894,7 +2919,11 @@ __global__ __launch_bounds__(256) void partials_sum_kernel(int C, int parts, con
 static int partials_fold(int C, int parts, float* in, float* out, hipStream_t st) {
   const float* src = in;
   if (parts > 64 && parts <= BN_WIDE_ROWS) {
-    hipLaunchKernelGGL(partials_sum_wide_kernel, dim3((2 * C + 63) / 64), dim3(1024), 0, st, 2 * C, parts, in, out);
+    const dim3 grid((2 * C + 63) / 64);
+#define MER_PSUM_WIDE(NB) \
+  [&] { hipLaunchKernelGGL(partials_sum_wide_kernel<NB>, grid, dim3(1024), 0, st, 2 * C, parts, in, out); }
+    wide_pick(parts, MER_PSUM_WIDE(16), MER_PSUM_WIDE(32), MER_PSUM_WIDE(64));
+#undef MER_PSUM_WIDE
     MER_LAUNCH_CHECK();
   }
   if (parts > 64) {
