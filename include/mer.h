@@ -419,6 +419,17 @@ int mer_conv_dgrad_ds(int N, int H, int W, int C, int K, int R, int S, int strid
                       const float* bn_ms2, float* bn_red2, const void* ds_dy, const void* ds_wt_packed, int ds_K,
                       int variant, void* stream);
 
+/* The number of leading partial rows (BatchNorm statistics rows of mer_conv_fwd_ex / BN-backward reduction rows of
+ * mer_conv_dgrad_ds) the call with these arguments writes: one per output row tile (MER_BN_STAT_ROWS(M) - 64,
+ * MER_BN_RED_ROWS(M) - 64), or one per workgroup where the persistent halo kernel runs (layer1, the stem: 256 / 512
+ * at B = 32 instead of 3,136 / 12,544), whose rows past these stay zero.  The same geometry test as the launch; a
+ * negative hipError_t on invalid arguments.  Pass the count to mer_bn_finalize_rows / mer_partials_sum so the
+ * fold reads only written rows (one launch instead of two past 1,024 tile rows). */
+int mer_conv_fwd_rows(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, const void* x,
+                      const void* w_packed, int variant);
+int mer_conv_dgrad_rows(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, const void* dy,
+                        const void* wt_packed, const void* ds_dy, int variant);
+
 /* out[c][0:2] = sum_p in[p][c][0:2] over `parts` partial rows, in a fixed order.  parts > 64 needs 64 more
  * rows after them in `in` (fold scratch, overwritten). */
 int mer_partials_sum(int C, int parts, float* in, float* out, void* stream);
@@ -467,6 +478,10 @@ int mer_pack_conv_weights_flat(int n, const long long* desc, long total_blocks, 
  * stats == NULL is eval mode: ms = (running_mean, 1/sqrt(running_var + eps)), nothing updated. */
 int mer_bn_finalize(int C, long M, const float* stats, float eps, float momentum, float* ms, float* rmean,
                     float* rvar, long long* num_batches_tracked, void* stream);
+/* mer_bn_finalize summing only the first data_rows (<= MER_BN_STAT_ROWS(M) - 64) statistics rows -- the count
+ * mer_conv_fwd_rows returned for the conv that filled them; the scratch rows stay at the buffer's end. */
+int mer_bn_finalize_rows(int C, long M, int data_rows, const float* stats, float eps, float momentum, float* ms,
+                         float* rmean, float* rvar, long long* num_batches_tracked, void* stream);
 
 /* y = [relu](bn(x) + (ms2 ? bn2(res) : res)), ms = (mean, rstd) pairs; res may be NULL. */
 int mer_bn_apply(long M, int C, const void* x, const float* ms, const float* gamma, const float* beta, const void* res,

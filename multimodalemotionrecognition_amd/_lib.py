@@ -85,6 +85,11 @@ class _Lib:
         if rc != 0:
             raise MerKernelError(f"{name} failed with hipError_t {rc}")
 
+    def call_int(self, name: str, *args) -> int:
+        """An entry point whose int result is a value (e.g. mer_conv_fwd_rows), not a hipError_t."""
+        self.load()
+        return self._fns[name](*args)
+
 
 LIB = _Lib()
 

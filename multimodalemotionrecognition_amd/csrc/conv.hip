@@ -2062,9 +2062,9 @@ MER_API int mer_conv_fwd(int N, int H, int W, int C, int K, int R, int S, int st
   return mer_conv_fwd_ex(N, H, W, C, K, R, S, stride, pad, x, w_packed, y, stats, -1, stream);
 }
 
-MER_API int mer_conv_fwd_ex(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, const void* x,
-                            const void* w_packed, void* y, float* stats, int variant, void* stream) {
-  if (C % 8 || variant < -1 || variant > 7) return (int)hipErrorInvalidValue;
+namespace {
+ConvGeom fwd_geom(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, const void* x,
+                  const void* w_packed, void* y, float* stats) {
   ConvGeom g{};
   g.N = N; g.IH = H; g.IW = W; g.IC = C;
   g.OH = (H + 2 * pad - R) / stride + 1; g.OW = (W + 2 * pad - S) / stride + 1;
@@ -2072,7 +2072,58 @@ MER_API int mer_conv_fwd_ex(int N, int H, int W, int C, int K, int R, int S, int
   g.Ncols = K; g.Kred = R * S * C;
   g.X = (const bf16_t*)x; g.Wt = (const bf16_t*)w_packed; g.Y = (bf16_t*)y; g.ldy = K; g.stats = stats;
   g.vec = vec_epilogue_enabled() && conv_vec_ok(g);
+  return g;
+}
+
+ConvGeom dgrad_geom(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, const void* dy,
+                    const void* wt_packed, const void* ds_dy) {
+  ConvGeom g{};
+  g.N = N; g.OH = H; g.OW = W;
+  g.IH = (H + 2 * pad - R) / stride + 1; g.IW = (W + 2 * pad - S) / stride + 1; g.IC = K;
+  g.R = R; g.S = S; g.st = stride; g.pad = pad;
+  g.Ncols = C; g.Kred = R * S * K;
+  g.X = (const bf16_t*)dy; g.Wt = (const bf16_t*)wt_packed; g.ldy = C; g.stats = nullptr;
+  g.X2 = (const bf16_t*)ds_dy;
+  g.vec = vec_epilogue_enabled() && conv_vec_ok(g);
+  return g;
+}
+
+// workgroups of a halo launch (launch_halo_t): one partial row each
+int halo_rows(const ConvGeom& g, int kind) {
+  const long M = (long)g.N * g.OH * g.OW, ntiles = (M + halo::BM - 1) / halo::BM;
+  const long slots = (long)(kind == 1 ? 1 : 2) * cu_count();
+  return (int)(ntiles < slots ? ntiles : slots);
+}
+}  // namespace
+
+MER_API int mer_conv_fwd_rows(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, const void* x,
+                              const void* w_packed, int variant) {
+  if (N <= 0 || C % 8 || variant < -1 || variant > 7) return -(int)hipErrorInvalidValue;
+  const ConvGeom g = fwd_geom(N, H, W, C, K, R, S, stride, pad, x, w_packed, nullptr, nullptr);
+  if (variant == -1 || variant == 6) {
+    const int hk = halo_kind(g, false);
+    if (hk) return halo_rows(g, hk);
+  }
+  return (int)(((long)N * g.OH * g.OW + 63) / 64);
+}
+
+MER_API int mer_conv_dgrad_rows(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, const void* dy,
+                                const void* wt_packed, const void* ds_dy, int variant) {
+  if (N <= 0 || K % 8 || C % 8 || variant < -1 || variant > 7) return -(int)hipErrorInvalidValue;
+  const ConvGeom g = dgrad_geom(N, H, W, C, K, R, S, stride, pad, dy, wt_packed, ds_dy);
+  if (variant == -1 || variant == 6) {
+    const int hk = halo_kind(g, true);
+    if (hk) return halo_rows(g, hk);
+  }
+  return (int)(((long)N * H * W + 63) / 64 + 4);  // MER_BN_RED_ROWS(M) - 64
+}
+
+MER_API int mer_conv_fwd_ex(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, const void* x,
+                            const void* w_packed, void* y, float* stats, int variant, void* stream) {
+  if (C % 8 || variant < -1 || variant > 7) return (int)hipErrorInvalidValue;
+  ConvGeom g = fwd_geom(N, H, W, C, K, R, S, stride, pad, x, w_packed, y, stats);
   // default: the halo kernel where it applies (layer1), else the 8-wave pipelined tiles; variant 6 = halo or fail
+  // (mer_conv_fwd_rows makes the same choice from the same geometry)
   if (variant == -1 || variant == 6) {
     const int hk = halo_kind(g, false);
     if (hk) return launch_conv_halo<false>(g, (hipStream_t)stream, hk);
@@ -2123,17 +2174,13 @@ MER_API int mer_conv_dgrad_ds(int N, int H, int W, int C, int K, int R, int S, i
     return (int)hipErrorInvalidValue;
   if (bn_red && (!bn_mask || !bn_x || !bn_ms || (bn_x2 && (!bn_ms2 || !bn_red2)))) return (int)hipErrorInvalidValue;
   if (bn_red && (variant == 0 || stride > 2)) return (int)hipErrorInvalidValue;  // fused only in the pipelined kernel
-  ConvGeom g{};
-  g.N = N; g.OH = H; g.OW = W;
-  g.IH = (H + 2 * pad - R) / stride + 1; g.IW = (W + 2 * pad - S) / stride + 1; g.IC = K;
-  g.R = R; g.S = S; g.st = stride; g.pad = pad;
-  g.Ncols = C; g.Kred = R * S * K;
-  g.X = (const bf16_t*)dy; g.Wt = (const bf16_t*)wt_packed; g.Y = (bf16_t*)dx; g.ldy = C; g.stats = nullptr;
+  ConvGeom g = dgrad_geom(N, H, W, C, K, R, S, stride, pad, dy, wt_packed, ds_dy);
+  g.Y = (bf16_t*)dx;
   g.R_ = (const bf16_t*)residual; g.Rmask = (const bf16_t*)residual_mask;
   g.bnr_mask = (const bf16_t*)bn_mask; g.bnr_x = (const bf16_t*)bn_x; g.bnr_ms = bn_ms; g.bnr_red = bn_red;
   g.bnr_x2 = (const bf16_t*)bn_x2; g.bnr_ms2 = bn_ms2; g.bnr_red2 = bn_red2;
-  g.X2 = (const bf16_t*)ds_dy; g.Wt2 = (const bf16_t*)ds_wt_packed; g.K2 = ds_dy ? ds_K : 0;
-  g.vec = vec_epilogue_enabled() && conv_vec_ok(g);
+  g.Wt2 = (const bf16_t*)ds_wt_packed; g.K2 = ds_dy ? ds_K : 0;
+  // (mer_conv_dgrad_rows makes the same choice from the same geometry)
   if (auto_variant || variant == 6) {
     const int hk = halo_kind(g, true);
     if (hk) return launch_conv_halo<true>(g, (hipStream_t)stream, hk);
@@ -2681,9 +2728,17 @@ static inline void wide_pick(int rows, F16 f16, F32 f32, F64 f64) {
 
 MER_API int mer_bn_finalize(int C, long M, const float* stats, float eps, float momentum, float* ms, float* rmean,
                             float* rvar, long long* num_batches_tracked, void* stream) {
+  return mer_bn_finalize_rows(C, M, (int)((M + 63) / 64), stats, eps, momentum, ms, rmean, rvar, num_batches_tracked,
+                              stream);
+}
+
+MER_API int mer_bn_finalize_rows(int C, long M, int data_rows, const float* stats, float eps, float momentum, float* ms,
+                                 float* rmean, float* rvar, long long* num_batches_tracked, void* stream) {
   if (!stats && (!rmean || !rvar)) return (int)hipErrorInvalidValue;
+  const int all_rows = (int)((M + 63) / 64);  // MER_BN_STAT_ROWS(M) - 64: the scratch rows follow them
+  if (data_rows <= 0 || data_rows > all_rows) return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
-  const int tiles = (int)((M + 63) / 64);  // MER_BN_STAT_ROWS(M) - 64
+  const int tiles = data_rows;
   const float* src = stats;
   int rows = tiles;
   if (stats && tiles > 64 && tiles <= BN_WIDE_ROWS) {
@@ -2698,7 +2753,7 @@ MER_API int mer_bn_finalize(int C, long M, const float* stats, float eps, float 
     MER_LAUNCH_CHECK();
   }
   if (stats && tiles > 64) {
-    float* scratch = const_cast<float*>(stats) + (long)tiles * 2 * C;
+    float* scratch = const_cast<float*>(stats) + (long)all_rows * 2 * C;
     const int per = (tiles + 63) / 64;
     hipLaunchKernelGGL(bn_stat_rows_fold_kernel, dim3((2 * C + 63) / 64, 64), dim3(256), 0, st, 2 * C, tiles, per,
                        stats, scratch);

@@ -11,7 +11,7 @@ import os
 
 import torch
 
-from ._lib import LIB
+from ._lib import LIB, MerKernelError
 
 F32, BF16 = 0, 1
 ACT = {"none": 0, "relu": 1, "gelu": 2}
@@ -491,6 +491,31 @@ def conv_fwd(x, wp, y, stats, R, S, stride, pad, variant=-1):
         raise ValueError("conv_fwd stats must be a contiguous zeroed float[bn_stat_rows(M)][K][2] buffer")
     _launch("conv_fwd", (N, H, W, C, Kc, R, stride), "mer_conv_fwd_ex", N, H, W, C, Kc, R, S, stride, pad, x.data_ptr(),
             wp.data_ptr(), y.data_ptr(), _ptr(stats), int(variant), stream_ptr())
+    if stats is not None:
+        return _partial_rows("mer_conv_fwd_rows", N, H, W, C, Kc, R, S, stride, pad, x.data_ptr(), wp.data_ptr(),
+                             int(variant))
+    return None
+
+
+_ROWS_CACHE = {}
+# Fold only the partial rows a conv wrote (one per persistent workgroup on the halo kernel): the layer1 / stem
+# BatchNorms take the one-launch wide fold.  Same-box step +0.55 % (profiles/r06/step_ab_partial_rows).
+PARTIAL_ROWS = True
+
+
+def _partial_rows(fn, *args):
+    """mer_conv_fwd_rows / mer_conv_dgrad_rows: the partial rows the launch with these arguments wrote.  Cached on
+    the shapes, the variant and the 16-byte alignment of the pointers (all the halo test reads of them)."""
+    if not PARTIAL_ROWS:
+        return None
+    key = (fn,) + tuple(a % 16 == 0 if isinstance(a, int) and a > 1 << 20 else a for a in args)
+    r = _ROWS_CACHE.get(key)
+    if r is None:
+        r = int(LIB.call_int(fn, *args))
+        if r <= 0:
+            raise MerKernelError(f"{fn}{args[:9]} failed: {r}")
+        _ROWS_CACHE[key] = r
+    return r
 
 
 def conv_dgrad(dy, wt, dx, R, S, stride, pad, residual=None, mask=None, variant=-1, bnr=None, ds=None):
@@ -518,19 +543,28 @@ def conv_dgrad(dy, wt, dx, R, S, stride, pad, residual=None, mask=None, variant=
         _launch("conv_dgrad", (N, H, W, C, Kc, R, stride), "mer_conv_dgrad_ds", N, H, W, C, Kc, R, S, stride, pad,
                 dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), _ptr(residual), _ptr(mask), *[_ptr(t) for t in b],
                 ddy.data_ptr(), dwt.data_ptr(), Kd, int(variant), stream_ptr())
-        return
-    _launch("conv_dgrad", (N, H, W, C, Kc, R, stride), "mer_conv_dgrad_bnr", N, H, W, C, Kc, R, S, stride, pad,
-            dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), _ptr(residual), _ptr(mask), *[_ptr(t) for t in b],
-            int(variant), stream_ptr())
+    else:
+        _launch("conv_dgrad", (N, H, W, C, Kc, R, stride), "mer_conv_dgrad_bnr", N, H, W, C, Kc, R, S, stride, pad,
+                dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), _ptr(residual), _ptr(mask), *[_ptr(t) for t in b],
+                int(variant), stream_ptr())
+    if bnr is None:
+        return None
+    return _partial_rows("mer_conv_dgrad_rows", N, H, W, C, Kc, R, S, stride, pad, dy.data_ptr(), wt.data_ptr(),
+                         ds[0].data_ptr() if ds is not None else 0, int(variant))
 
 
-def partials_sum(parts_buf, out):
+def partials_sum(parts_buf, out, rows=None):
     """out[C,2] = fixed-order sum of the data rows of a [bn_red_rows(M), C, 2] fused-epilogue reduction
-    buffer (its last 64 rows are the fold scratch)."""
+    buffer (its last 64 rows are the fold scratch).  ``rows``: the leading rows the producing conv_dgrad wrote (its
+    return value; the rest are zero), else every data row."""
     P, C, _ = parts_buf.shape
     if P <= 64:
         raise ValueError("partials_sum expects a bn_red_rows(M) buffer (data rows + 64 scratch rows)")
-    LIB("mer_partials_sum", C, P - 64, parts_buf.data_ptr(), out.data_ptr(), stream_ptr())
+    if rows is None:
+        rows = P - 64
+    if not 0 < rows <= P - 64:
+        raise ValueError("partials_sum rows out of range")
+    LIB("mer_partials_sum", C, int(rows), parts_buf.data_ptr(), out.data_ptr(), stream_ptr())
     return out
 
 
@@ -649,12 +683,15 @@ def pack_conv_weights(desc, blocks, flat=True):
     LIB(name, desc.shape[0], desc.data_ptr(), int(blocks), stream_ptr())
 
 
-def bn_finalize(stats, M, eps, momentum, ms, rmean=None, rvar=None, nbt=None):
+def bn_finalize(stats, M, eps, momentum, ms, rmean=None, rvar=None, nbt=None, rows=None):
+    """``rows``: the leading statistics rows the producing conv_fwd wrote (its return value), else all of them."""
     C = ms.shape[0]
     if stats is not None and (stats.numel() != bn_stat_rows(int(M)) * C * 2 or not stats.is_contiguous()):
         raise ValueError("bn_finalize stats must be the conv_fwd float[bn_stat_rows(M)][C][2] buffer")
-    LIB("mer_bn_finalize", C, int(M), _ptr(stats), float(eps), float(momentum), ms.data_ptr(), _ptr(rmean),
-        _ptr(rvar), _ptr(nbt), stream_ptr())
+    if rows is None:
+        rows = bn_stat_rows(int(M)) - 64
+    LIB("mer_bn_finalize_rows", C, int(M), int(rows), _ptr(stats), float(eps), float(momentum), ms.data_ptr(),
+        _ptr(rmean), _ptr(rvar), _ptr(nbt), stream_ptr())
 
 
 def bn_apply(x, ms, gamma, beta, y, relu, res=None, ms2=None, gamma2=None, beta2=None):

@@ -307,13 +307,14 @@ class ResNet18Trunk(nn.Sequential):
         return buf
 
 
-def _bn_forward(bn: nn.BatchNorm2d, c: torch.Tensor, stats, training: bool):
+def _bn_forward(bn: nn.BatchNorm2d, c: torch.Tensor, stats, training: bool, rows=None):
+    """``rows``: the statistics rows the conv wrote (K.conv_fwd's return: one per workgroup on the halo kernel)."""
     C = c.shape[-1]
     ms = torch.empty(C, 2, device=c.device, dtype=torch.float32)
     M = c.numel() // C
     if training:
         mom = 0.1 if bn.momentum is None else bn.momentum
-        K.bn_finalize(stats, M, bn.eps, mom, ms, bn.running_mean, bn.running_var, bn.num_batches_tracked)
+        K.bn_finalize(stats, M, bn.eps, mom, ms, bn.running_mean, bn.running_var, bn.num_batches_tracked, rows=rows)
     else:
         K.bn_finalize(None, M, bn.eps, 0.0, ms, bn.running_mean, bn.running_var)
     return ms
@@ -401,8 +402,8 @@ def _conv_bn(trunk, conv, bn, x, stride, pad, training, arena=None, rs=None):
     if training:
         M = N * Ho * Wo
         stats = arena.take(Kc, M=M) if arena is not None else K.bn_stats_buffer(Kc, x.device, M)
-    K.conv_fwd(x, trunk.packed(conv, C, False), y, stats, R, S, stride, pad)
-    return y, _bn_forward(bn, y, stats, training)
+    rows = K.conv_fwd(x, trunk.packed(conv, C, False), y, stats, R, S, stride, pad)
+    return y, _bn_forward(bn, y, stats, training, rows)
 
 
 @torch.no_grad()
@@ -574,9 +575,10 @@ def block_backward(trunk, blk: BasicBlock, sv, dx: torch.Tensor, grads, training
     g_out = dx
     s = blk.stride
     C2 = bc2.shape[-1]
-    if pre is not None:
-        red2 = K.partials_sum(pre[0], torch.empty(C2, 2, device=dev, dtype=torch.float32))
-        redd = K.partials_sum(pre[1], torch.empty(C2, 2, device=dev, dtype=torch.float32)) if cd is not None else None
+    if pre is not None:  # (red2 rows, downsample-BN rows, rows the producing dgrad wrote)
+        red2 = K.partials_sum(pre[0], torch.empty(C2, 2, device=dev, dtype=torch.float32), pre[2])
+        redd = K.partials_sum(pre[1], torch.empty(C2, 2, device=dev, dtype=torch.float32), pre[2]) \
+            if cd is not None else None
     else:
         red2 = arena.take(C2, parts=1)
         K.bn_bwd_reduce(g_out, out, bc2, bms2, red2, arena.take(C2, parts=K.BN_RED_WS_ROWS))
@@ -593,8 +595,8 @@ def block_backward(trunk, blk: BasicBlock, sv, dx: torch.Tensor, grads, training
     da1 = torch.empty_like(ba1)
     C1 = bc1.shape[-1]
     red1p = arena.take(C1, parts=K.bn_red_rows(ba1.numel() // C1))
-    K.conv_dgrad(dc2, trunk.packed(blk.conv2, C2, True), da1, 3, 3, 1, 1, bnr=(ba1, bc1, bms1, red1p))
-    red1 = K.partials_sum(red1p, torch.empty(C1, 2, device=dev, dtype=torch.float32))
+    rows1 = K.conv_dgrad(dc2, trunk.packed(blk.conv2, C2, True), da1, 3, 3, 1, 1, bnr=(ba1, bc1, bms1, red1p))
+    red1 = K.partials_sum(red1p, torch.empty(C1, 2, device=dev, dtype=torch.float32), rows1)
     dc1 = _bn_bwd(da1, ba1, bc1, bms1, blk.bn1, red1, grads, training)
     # conv1 (+ downsample) -> dx of the block input (+ the preceding block's bn2 / downsample reductions)
     w1 = _grad(blk.conv1.weight, grads)
@@ -608,17 +610,18 @@ def block_backward(trunk, blk: BasicBlock, sv, dx: torch.Tensor, grads, training
         if wd is not None:
             lane.run(lambda: K.conv_wgrad(xin, dcd, wd, 1, 1, s, 0, defer=lane.folds), xin, dcd, wd, block=bidx)
         if FUSED_DS_DGRAD and s == 2:  # the downsample's input gradient as an extra K segment of conv1's dgrad
-            K.conv_dgrad(dc1, trunk.packed(blk.conv1, Cin, True), dxin, 3, 3, s, 1, bnr=bnr,
-                         ds=(dcd, trunk.packed(blk.downsample[0], Cin, True)))
+            rows = K.conv_dgrad(dc1, trunk.packed(blk.conv1, Cin, True), dxin, 3, 3, s, 1, bnr=bnr,
+                                ds=(dcd, trunk.packed(blk.downsample[0], Cin, True)))
         else:
             dxd = torch.empty_like(xin)
             K.conv_dgrad(dcd, trunk.packed(blk.downsample[0], Cin, True), dxd, 1, 1, s, 0)
-            K.conv_dgrad(dc1, trunk.packed(blk.conv1, Cin, True), dxin, 3, 3, s, 1, residual=dxd, bnr=bnr)
+            rows = K.conv_dgrad(dc1, trunk.packed(blk.conv1, Cin, True), dxin, 3, 3, s, 1, residual=dxd, bnr=bnr)
     else:
-        K.conv_dgrad(dc1, trunk.packed(blk.conv1, Cin, True), dxin, 3, 3, s, 1, residual=g_out, mask=out, bnr=bnr)
+        rows = K.conv_dgrad(dc1, trunk.packed(blk.conv1, Cin, True), dxin, 3, 3, s, 1, residual=g_out, mask=out,
+                            bnr=bnr)
     if own_lane:
         lane.join()
-    return dxin, nxt
+    return dxin, (nxt + (rows,) if nxt is not None else None)
 
 
 @torch.no_grad()

@@ -311,6 +311,76 @@ def test_halo_conv_bit_identical(N):
     assert rel_rms(outs[6][0], ref) < 1e-2
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("N", [3, 40, 256])
+def test_halo_partial_rows_fold(N):
+    """K.conv_fwd / K.conv_dgrad return the partial rows their launch wrote (mer_conv_fwd_rows / mer_conv_dgrad_rows):
+    one per persistent workgroup on the halo kernel (layer1; the stem), one per row tile otherwise.  Every row past
+    the count is still zero, and the folds over the written rows alone (mer_bn_finalize_rows, mer_partials_sum) equal
+    the folds over every row to fp32 rounding (the zero rows only change the fold's grouping)."""
+    from multimodalemotionrecognition_amd import kernels as K
+
+    torch.manual_seed(19)
+
+    def check_fwd(x, wp, Ho, R, pad, variants):
+        C = wp.shape[0]
+        M = x.shape[0] * Ho * Ho
+        for v in variants:
+            y = torch.empty(x.shape[0], Ho, Ho, C, device="cuda", dtype=torch.bfloat16)
+            st = K.bn_stats_buffer(C, "cuda", M)
+            rows = K.conv_fwd(x, wp, y, st, R, R, 1, pad, variant=v)
+            tiles = K.bn_stat_rows(M) - 64
+            if v == 2:
+                assert rows == tiles
+            else:
+                assert 0 < rows <= -(-M // 128), (v, rows)
+            assert not st[rows:].any()
+            res = []
+            for r in (rows, None):
+                ms = torch.empty(C, 2, device="cuda")
+                rm, rv = torch.zeros(C, device="cuda"), torch.ones(C, device="cuda")
+                K.bn_finalize(st.clone(), M, 1e-5, 0.1, ms, rm, rv, rows=r)
+                res.append(torch.cat([ms.flatten(), rm, rv]))
+            assert torch.allclose(res[0], res[1], rtol=2e-6, atol=1e-6), v
+
+    H, C = 28, 64
+    x = torch.randn(N, H, H, C, device="cuda").bfloat16()
+    w = torch.randn(C, C, 3, 3, device="cuda") / 24.0
+    wp = torch.empty(C, 9 * C, device="cuda", dtype=torch.bfloat16)
+    K.pack_conv_weight(w, wp, C, False)
+    wt = torch.empty(C, 9 * C, device="cuda", dtype=torch.bfloat16)
+    K.pack_conv_weight(w, wt, C, True)
+    check_fwd(x, wp, H, 3, 1, (2, 6, -1))
+    # the stem's space-to-depth form: 4x4 / stride 1 / pad 0 on 16 channels, 59 -> 56
+    xs = torch.randn(max(1, N // 8), 59, 59, 16, device="cuda").bfloat16()
+    ws = torch.randn(C, 16, 4, 4, device="cuda") / 16.0
+    wsp = torch.empty(C, 16 * 16, device="cuda", dtype=torch.bfloat16)
+    K.pack_conv_weight(ws, wsp, 16, False)
+    check_fwd(xs, wsp, 56, 4, 0, (6, -1))
+    # the dgrad's fused BN-backward rows (one and two BNs)
+    dy = torch.randn(N, H, H, C, device="cuda").bfloat16()
+    res = torch.randn(N, H, H, C, device="cuda").bfloat16()
+    mask = torch.randn(N, H, H, C, device="cuda").bfloat16()
+    xb = torch.randn(N, H, H, C, device="cuda").bfloat16()
+    ms = torch.stack([torch.randn(C), torch.rand(C) + 0.5], 1).cuda().contiguous()
+    M = N * H * H
+    for v in (5, 6, -1):
+        for two in (False, True):
+            dx = torch.empty(N, H, H, C, device="cuda", dtype=torch.bfloat16)
+            reds = [torch.zeros(K.bn_red_rows(M), C, 2, device="cuda") for _ in range(2)]
+            bnr = (mask, xb, ms, reds[0]) + ((xb, ms, reds[1]) if two else ())
+            rows = K.conv_dgrad(dy, wt, dx, 3, 3, 1, 1, residual=res, mask=mask, variant=v, bnr=bnr)
+            if v == 5:
+                assert rows == K.bn_red_rows(M) - 64
+            else:
+                assert 0 < rows <= -(-M // 128), (v, rows)
+            for red in reds[:2 if two else 1]:
+                assert not red[rows:].any()
+                a = K.partials_sum(red.clone(), torch.empty(C, 2, device="cuda"), rows)
+                b = K.partials_sum(red.clone(), torch.empty(C, 2, device="cuda"))
+                assert torch.allclose(a, b, rtol=1e-5, atol=1e-3), (v, two)
+
+
 @pytest.mark.parametrize("N", [3, 64])
 def test_halo_stem_bit_identical(N):
     """The stem's space-to-depth form (4x4 / stride 1 / pad 0, 16 -> 64 channels, 59x59 -> 56x56) on the halo kernel
