@@ -497,6 +497,14 @@ int mer_bn_bwd_reduce(long M, int C, const void* dy, const void* mask, const voi
 int mer_bn_bwd_apply(long M, int C, const void* dy, const void* mask, const void* x, const float* ms,
                      const float* gamma, const float* red, int batch_stats, void* dx, float* dgamma, float* dbeta,
                      void* stream);
+/* Two mer_bn_bwd_apply passes over the same dy and ReLU mask (non-NULL) in one launch -- a stride-2 BasicBlock's
+ * bn2 (x, ms, gamma, red -> dx) and downsample BN (x2, ms2, gamma2, red2 -> dx2), video.py:21-23 -> torchvision
+ * BasicBlock: g and the mask are read once; each output bit-identical to its own mer_bn_bwd_apply (dx, dx2 must not
+ * alias dy). */
+int mer_bn_bwd_apply2(long M, int C, const void* dy, const void* mask, const void* x, const float* ms,
+                      const float* gamma, const float* red, const void* x2, const float* ms2, const float* gamma2,
+                      const float* red2, int batch_stats, void* dx, void* dx2, float* dgamma, float* dbeta,
+                      float* dgamma2, float* dbeta2, void* stream);
 
 /* Fused stem tail (C % 8 == 0, C <= 512, N*H*W < 2^22; x = the stem conv output [N][H][W][C] bf16):
  * y = maxpool3x3s2p1(bf16(relu(bn(x)))) with argmax taps, the BN/ReLU activation never stored.

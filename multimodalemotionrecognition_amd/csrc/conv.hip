@@ -727,9 +727,12 @@ __global__ __launch_bounds__(256) void wgrad_scatter_kernel(int C, int Creal, in
 // instead of one or two per convolution (the folds were ~30 launches of 5-12 us each on the critical stream).
 // Record r: dw_r[k][c][tap] += sum_z ws_r[z][k][tap*C + c] (c < Creal), or with a scatter map
 // dw_r[k][map[j]] for source column j = tap*C + c (-1: dropped) -- the stem's 4x4 space-to-depth form
-// gathered back to 7x7x3.  Threads walk the SOURCE order (coalesced slab reads, the bulk of the bytes);
-// a block owns E = 256/SG source elements and SG split-groups (thread (sg, e) sums splits sg, sg+SG, ...
-// with 4 loads in flight, the SG partials meet in LDS in order) -- fixed order, deterministic.
+// gathered back to 7x7x3.  Threads walk the SOURCE order (coalesced slab reads, the bulk of the bytes): a thread
+// owns 4 consecutive source elements (one 16-byte load per split), a block E = 256/SG threads and SG split-groups
+// (thread (sg, e) sums splits sg, sg+SG, ... in batches of 8 loads issued before their adds, the SG partials meet in
+// LDS in order) -- fixed order, deterministic.  The thread's four read-modify-writes of dw issue their loads
+// together: written as four `+=`, each waited for the previous store (possible aliasing), and the 16-byte form ran
+// 245 us per trunk fold (tools/bench_fold.py) against 157 us for the 4-byte form it replaces; now ~146 us.
 struct FoldRec {
   const float* ws;
   float* dw;
@@ -743,42 +746,65 @@ struct FoldTable {
 };
 
 __global__ __launch_bounds__(256) void wgrad_fold_batch_kernel(FoldTable t) {
-  __shared__ float part[256];
+  __shared__ f32x4 part[256];
   const int v = blockIdx.x;
   const int ri = table_find(t.n, v, [&](int i) { return t.r[i].blk0; });
   const FoldRec& R = t.r[ri];
   const int SG = R.SG, E = 256 / SG, e = threadIdx.x % E, sg = threadIdx.x / E;
   const long row = (long)R.RS * R.C, total = (long)R.K * row;
   const int lb = v - R.blk0;
-  const long idx = (long)lb * E + e;
-  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  const long idx = ((long)lb * E + e) * 4;
+  const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
+  f32x4 a0 = zero4, a1 = zero4, a2 = zero4, a3 = zero4;
+  const int splits = R.splits;
   if (idx < total) {
-    const float* src = R.ws + idx;
-    int z = sg;
-    for (; z + 3 * SG < R.splits; z += 4 * SG) {
-      a0 += src[(long)z * total];
-      a1 += src[(long)(z + SG) * total];
-      a2 += src[(long)(z + 2 * SG) * total];
-      a3 += src[(long)(z + 3 * SG) * total];
+    const f32x4* __restrict__ src = reinterpret_cast<const f32x4*>(R.ws + idx);
+    const long st = total / 4;
+    // this thread's splits z = sg + SG * i, i < n: batches of 8 loads issued before their adds (clamped
+    // addresses, zero-selected), chains a0..a3 by i % 4 -- no serial tail
+    const int n = splits > sg ? (splits - sg + SG - 1) / SG : 0;
+    for (int i0 = 0; i0 < n; i0 += 8) {
+      f32x4 w[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int i = i0 + q < n ? i0 + q : n - 1;
+        w[q] = src[(long)(sg + SG * i) * st];
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        if (i0 + q < n) {
+          if ((q & 3) == 0) a0 += w[q];
+          else if ((q & 3) == 1) a1 += w[q];
+          else if ((q & 3) == 2) a2 += w[q];
+          else a3 += w[q];
+        }
     }
-    for (; z < R.splits; z += SG) a0 += src[(long)z * total];
   }
   part[threadIdx.x] = (a0 + a1) + (a2 + a3);
   __syncthreads();
   if (sg != 0 || idx >= total) return;
-  float s = 0.f;
-  for (int q = 0; q < SG; ++q) s += part[q * E + e];
-  const int k = (int)(idx / row), j = (int)(idx - (long)k * row);
-  int o;
-  if (R.map) {
-    o = R.map[j];
-  } else {
-    const int tap = j / R.C, c = j - tap * R.C;
-    o = c < R.Creal ? c * R.RS + tap : -1;
+  f32x4 s4 = zero4;
+  for (int q = 0; q < SG; ++q) s4 += part[q * E + e];
+  const long per_k = R.map ? (long)R.Creal : (long)R.Creal * R.RS;
+  const int k = (int)(idx / row), j0 = (int)(idx - (long)k * row);
+  int o[4];
+  float d[4];
+  float* __restrict__ dwk = R.dw + (long)k * per_k;
+#pragma unroll
+  for (int c4 = 0; c4 < 4; ++c4) {
+    const int j = j0 + c4;
+    if (R.map) {
+      o[c4] = R.map[j];
+    } else {
+      const int tap = j / R.C, c = j - tap * R.C;
+      o[c4] = c < R.Creal ? c * R.RS + tap : -1;
+    }
   }
-  if (o < 0) return;
-  const long per_k = R.map ? (long)R.Creal : (long)R.Creal * R.RS;  // map records: Creal = output floats per k
-  R.dw[(long)k * per_k + o] += s;
+#pragma unroll
+  for (int c4 = 0; c4 < 4; ++c4) d[c4] = dwk[o[c4] >= 0 ? o[c4] : 0];  // the 4 read-modify-writes' loads together
+#pragma unroll
+  for (int c4 = 0; c4 < 4; ++c4)
+    if (o[c4] >= 0) dwk[o[c4]] = d[c4] + s4[c4];
 }
 
 
@@ -2290,15 +2316,15 @@ MER_API int mer_wgrad_fold_batch(int n, const long long* rows, void* stream) {
     FoldRec& r = t.r[i];
     r.ws = (const float*)q[0]; r.dw = (float*)q[1]; r.map = (const int*)q[2];
     r.K = (int)q[3]; r.C = (int)q[4]; r.Creal = (int)q[5]; r.RS = (int)q[6]; r.splits = (int)q[7];
-    if (!r.ws || !r.dw || r.K < 1 || r.C < 1 || r.RS < 1 || r.splits < 1 || r.Creal < 1 ||
-        (!r.map && r.Creal > r.C))
+    if (!r.ws || !r.dw || r.K < 1 || r.C < 1 || r.C % 4 || r.RS < 1 || r.splits < 1 || r.Creal < 1 ||
+        (!r.map && r.Creal > r.C) || ((uintptr_t)r.ws & 15))
       return (int)hipErrorInvalidValue;
     // SG <= 8: E >= 32 consecutive floats per split group, i.e. whole 128-byte lines (SG 16 read half lines: the
     // slabs are cold by the time the segment folds, so half-used lines cost HBM bytes)
     r.SG = r.splits > 48 ? fold_sg_max() : (r.splits > 12 ? 4 : 1);
     const long total = (long)r.K * r.RS * r.C;
     r.blk0 = blk;
-    r.nblk = (int)((total + 256 / r.SG - 1) / (256 / r.SG));
+    r.nblk = (int)((total + 4 * (256 / r.SG) - 1) / (4 * (256 / r.SG)));
     blk += r.nblk;
   }
   hipLaunchKernelGGL(wgrad_fold_batch_kernel, dim3(blk), dim3(256), 0, (hipStream_t)stream, t);
@@ -3021,9 +3047,10 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(long M, int C, const 
     // batch statistics (train): the mean/var terms carry gradient; running stats (eval): they do not
     const float a = batch_stats ? red[2 * c] * invM : 0.f;
     const float b = batch_stats ? red[2 * c + 1] * invM : 0.f;
+    const float t = gr * b * rs;  // (explicit rounding steps, shared with bn_bwd_apply2_kernel)
     coef[0][c] = gr;
-    coef[1][c] = -gr * b * rs;
-    coef[2][c] = -gr * a + gr * b * rs * mu;
+    coef[1][c] = -t;
+    coef[2][c] = fmaf(-gr, a, t * mu);
     if (BNMASK) stem_bn_coef(c, ms, gamma, mbeta, coef[3][c], coef[4][c]);
   }
   __syncthreads();
@@ -3051,7 +3078,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(long M, int C, const 
       const bool live = BNMASK ? bf2f(f2bf(fmaxf(bf2f(xh[i]) * msc[i] + msh[i], 0.f))) > 0.f
                                : (!mask || bf2f(mh[i]) > 0.f);
       const float g = live ? bf2f(gh[i]) : 0.f;
-      oh[i] = f2bf(k1[i] * g + k2[i] * bf2f(xh[i]) + k0[i]);
+      oh[i] = f2bf(fmaf(k1[i], g, fmaf(k2[i], bf2f(xh[i]), k0[i])));  // explicit: apply2 rounds the same
     }
     return ov;
   };
@@ -3084,6 +3111,90 @@ MER_API int mer_bn_bwd_apply(long M, int C, const void* dy, const void* mask, co
   hipLaunchKernelGGL((bn_bwd_apply_kernel<false>), dim3(grid), dim3(256), 0, (hipStream_t)stream, M, C,
                      (const bf16_t*)dy, (const bf16_t*)mask, (const bf16_t*)x, ms, gamma, (const float*)nullptr, red,
                      batch_stats, (bf16_t*)dx, dgamma, dbeta);
+  MER_LAUNCH_CHECK();
+}
+
+// Two BatchNorm backward applies that read the same gradient and ReLU mask: a stride-2 BasicBlock's bn2 and its
+// downsample BN (the block output relu(bn2(c2) + bn_d(cd)) fans its gradient out to both).  One pass loads g and the
+// mask once for both outputs -- 12 instead of 16 bytes per element and one launch less -- with each output's
+// per-element arithmetic exactly bn_bwd_apply_kernel<false>'s (bit-identical to two launches).
+__global__ __launch_bounds__(256) void bn_bwd_apply2_kernel(long M, int C, const bf16_t* __restrict__ dy,
+                                                            const bf16_t* __restrict__ mask,
+                                                            const bf16_t* __restrict__ x, const float* __restrict__ ms,
+                                                            const float* __restrict__ gamma,
+                                                            const float* __restrict__ red,
+                                                            const bf16_t* __restrict__ x2,
+                                                            const float* __restrict__ ms2,
+                                                            const float* __restrict__ gamma2,
+                                                            const float* __restrict__ red2, int batch_stats,
+                                                            bf16_t* __restrict__ dx, bf16_t* __restrict__ dx2,
+                                                            float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                            float* __restrict__ dgamma2, float* __restrict__ dbeta2) {
+  __shared__ __attribute__((aligned(16))) float coef[6][512];
+  const float invM = 1.f / (float)M;
+  for (int c = threadIdx.x; c < C; c += 256) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const float* rd = h ? red2 : red;
+      const float* m = h ? ms2 : ms;
+      if (blockIdx.x == 0) {
+        float* dg = h ? dgamma2 : dgamma;
+        float* db = h ? dbeta2 : dbeta;
+        if (dg) dg[c] += rd[2 * c + 1];
+        if (db) db[c] += rd[2 * c];
+      }
+      const float mu = m[2 * c], rs = m[2 * c + 1], gr = (h ? gamma2 : gamma)[c] * rs;
+      const float a = batch_stats ? rd[2 * c] * invM : 0.f;
+      const float b = batch_stats ? rd[2 * c + 1] * invM : 0.f;
+      const float t = gr * b * rs;
+      coef[3 * h + 0][c] = gr;
+      coef[3 * h + 1][c] = -t;
+      coef[3 * h + 2][c] = fmaf(-gr, a, t * mu);
+    }
+  }
+  __syncthreads();
+  const long nvec = M * C / 8;
+  const long stride = (long)gridDim.x * blockDim.x;
+  const long tid0 = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  const int c0 = (int)(tid0 % (C / 8)) * 8;
+  float k[6][8];
+#pragma unroll
+  for (int j = 0; j < 6; ++j)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) k[j][i] = coef[j][c0 + i];
+  for (long e = tid0; e < nvec; e += stride) {
+    const u32x4 gv = *reinterpret_cast<const u32x4*>(dy + e * 8);
+    const u32x4 mv = *reinterpret_cast<const u32x4*>(mask + e * 8);
+    const u32x4 xv = *reinterpret_cast<const u32x4*>(x + e * 8);
+    const u32x4 x2v = *reinterpret_cast<const u32x4*>(x2 + e * 8);
+    const bf16_t* gh = reinterpret_cast<const bf16_t*>(&gv);
+    const bf16_t* mh = reinterpret_cast<const bf16_t*>(&mv);
+    const bf16_t* xh = reinterpret_cast<const bf16_t*>(&xv);
+    const bf16_t* x2h = reinterpret_cast<const bf16_t*>(&x2v);
+    u32x4 ov, o2v;
+    bf16_t* oh = reinterpret_cast<bf16_t*>(&ov);
+    bf16_t* o2h = reinterpret_cast<bf16_t*>(&o2v);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float g = bf2f(mh[i]) > 0.f ? bf2f(gh[i]) : 0.f;
+      oh[i] = f2bf(fmaf(k[0][i], g, fmaf(k[1][i], bf2f(xh[i]), k[2][i])));
+      o2h[i] = f2bf(fmaf(k[3][i], g, fmaf(k[4][i], bf2f(x2h[i]), k[5][i])));
+    }
+    *reinterpret_cast<u32x4*>(dx + e * 8) = ov;
+    *reinterpret_cast<u32x4*>(dx2 + e * 8) = o2v;
+  }
+}
+MER_API int mer_bn_bwd_apply2(long M, int C, const void* dy, const void* mask, const void* x, const float* ms,
+                              const float* gamma, const float* red, const void* x2, const float* ms2,
+                              const float* gamma2, const float* red2, int batch_stats, void* dx, void* dx2,
+                              float* dgamma, float* dbeta, float* dgamma2, float* dbeta2, void* stream) {
+  if (C % 8 || C > 512 || 256 % (C / 8) || !mask || !x2 || !dx2 || dx == dy || dx2 == dy)
+    return (int)hipErrorInvalidValue;
+  const long nvec = M * C / 8;
+  const int grid = bn_stream_grid(nvec);
+  hipLaunchKernelGGL(bn_bwd_apply2_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, M, C, (const bf16_t*)dy,
+                     (const bf16_t*)mask, (const bf16_t*)x, ms, gamma, red, (const bf16_t*)x2, ms2, gamma2, red2,
+                     batch_stats, (bf16_t*)dx, (bf16_t*)dx2, dgamma, dbeta, dgamma2, dbeta2);
   MER_LAUNCH_CHECK();
 }
 

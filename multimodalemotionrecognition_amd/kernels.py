@@ -718,6 +718,19 @@ def bn_bwd_apply(dy, mask, x, ms, gamma, red, dx, dgamma, dbeta, batch_stats=Tru
         gamma.data_ptr(), red.data_ptr(), int(batch_stats), dx.data_ptr(), _ptr(dgamma), _ptr(dbeta), stream_ptr())
 
 
+def bn_bwd_apply2(dy, mask, x, ms, gamma, red, dx, dgamma, dbeta, x2, ms2, gamma2, red2, dx2, dgamma2, dbeta2,
+                  batch_stats=True):
+    """Two bn_bwd_apply passes sharing dy and the (non-None) mask in one launch (mer_bn_bwd_apply2)."""
+    C = x.shape[-1]
+    for t in (dy, mask, x2, dx, dx2):
+        if tuple(t.shape) != tuple(x.shape):
+            raise ValueError("bn_bwd_apply2 tensors must share one shape")
+    LIB("mer_bn_bwd_apply2", x.numel() // C, C, dy.data_ptr(), mask.data_ptr(), x.data_ptr(), ms.data_ptr(),
+        gamma.data_ptr(), red.data_ptr(), x2.data_ptr(), ms2.data_ptr(), gamma2.data_ptr(), red2.data_ptr(),
+        int(batch_stats), dx.data_ptr(), dx2.data_ptr(), _ptr(dgamma), _ptr(dbeta), _ptr(dgamma2), _ptr(dbeta2),
+        stream_ptr())
+
+
 def maxpool_fwd(x, y, arg):
     N, H, W, C = x.shape
     LIB("mer_maxpool_fwd", N, H, W, C, x.data_ptr(), y.data_ptr(), arg.data_ptr(), stream_ptr())

@@ -537,6 +537,10 @@ def _bnr_target(blk_sv, blk, arena):
 # 5-12 us each off the critical stream per step (the stem's zero / gather / add included).  (Round 3 also measured
 # the weight gradients on a third stream and folding after every N blocks: both slower or inside the noise, removed.)
 WGRAD_DEFER = True
+# A stride-2 block's bn2 and downsample-BN backward applies in one pass over the shared gradient and mask
+# (mer_bn_bwd_apply2, bit-identical; 3 x 4 fewer bytes per element and one launch less per stride-2 block; the
+# same-box step did not move measurably: 211.51 vs 211.74 steps/s, profiles/r06/step_ab_fold_b8)
+BN_BWD_PAIR = True
 # The downsample's input gradient fused into conv1's stride-2 dgrad (mer_conv_dgrad_ds): +1.2 % same-box vs the
 # separate 1x1 dgrad whose bf16 output the 3x3 dgrad read back as its residual (profiles/r04/ab_runs.txt)
 FUSED_DS_DGRAD = True
@@ -586,8 +590,15 @@ def block_backward(trunk, blk: BasicBlock, sv, dx: torch.Tensor, grads, training
         if cd is not None:
             redd = arena.take(C2, parts=1)
             K.bn_bwd_reduce(g_out, out, cd, msd, redd, arena.take(C2, parts=K.BN_RED_WS_ROWS))
-    dc2 = _bn_bwd(g_out, out, bc2, bms2, blk.bn2, red2, grads, training)
-    dcd = _bn_bwd(g_out, out, cd, msd, blk.downsample[1], redd, grads, training) if cd is not None else None
+    if cd is not None and BN_BWD_PAIR:  # bn2 and the downsample BN read the same gradient and mask: one pass
+        dc2, dcd = torch.empty_like(bc2), torch.empty_like(cd)
+        bd = blk.downsample[1]
+        K.bn_bwd_apply2(g_out, out, bc2, bms2, blk.bn2.weight, red2, dc2, _grad(blk.bn2.weight, grads),
+                        _grad(blk.bn2.bias, grads), cd, msd, bd.weight, redd, dcd, _grad(bd.weight, grads),
+                        _grad(bd.bias, grads), training)
+    else:
+        dc2 = _bn_bwd(g_out, out, bc2, bms2, blk.bn2, red2, grads, training)
+        dcd = _bn_bwd(g_out, out, cd, msd, blk.downsample[1], redd, grads, training) if cd is not None else None
     # conv2 (its dgrad also reduces bn1's backward sums: g = da1 * (ba1 > 0))
     w2 = _grad(blk.conv2.weight, grads)
     if w2 is not None:

@@ -875,3 +875,28 @@ def test_bn_finalize_and_partials_sum_all_row_counts(M, C):
     assert torch.equal(s1, s2)
     ref = parts[:prow - 64].double().sum(0).cpu()
     assert torch.allclose(s1.cpu().double(), ref, rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("M,C", [(4096, 512), (12544, 256), (1000, 64)])
+def test_bn_bwd_apply2_matches_two_launches(M, C):
+    """mer_bn_bwd_apply2 (a stride-2 block's bn2 + downsample-BN backward applies over the shared gradient and ReLU
+    mask, one launch) == two mer_bn_bwd_apply launches, bitwise, dgamma / dbeta accumulated (+=) the same way."""
+    from multimodalemotionrecognition_amd import kernels as K
+
+    torch.manual_seed(23)
+    bf = torch.bfloat16
+    dy, mask, x, x2 = (torch.randn(M, C, device="cuda").to(bf) for _ in range(4))
+    mss = [torch.stack([torch.randn(C), torch.rand(C) + 0.5], 1).cuda().contiguous() for _ in range(2)]
+    gammas = [torch.randn(C, device="cuda") for _ in range(2)]
+    reds = [torch.randn(C, 2, device="cuda") * 100 for _ in range(2)]
+    for bs in (True, False):
+        acc = [torch.randn(C, device="cuda") for _ in range(4)]
+        ref = [a.clone() for a in acc]
+        d1, d2 = torch.empty_like(x), torch.empty_like(x2)
+        K.bn_bwd_apply(dy, mask, x, mss[0], gammas[0], reds[0], d1, ref[0], ref[1], bs)
+        K.bn_bwd_apply(dy, mask, x2, mss[1], gammas[1], reds[1], d2, ref[2], ref[3], bs)
+        e1, e2 = torch.empty_like(x), torch.empty_like(x2)
+        K.bn_bwd_apply2(dy, mask, x, mss[0], gammas[0], reds[0], e1, acc[0], acc[1], x2, mss[1], gammas[1], reds[1],
+                        e2, acc[2], acc[3], bs)
+        assert torch.equal(d1, e1) and torch.equal(d2, e2), bs
+        assert all(torch.equal(a, b) for a, b in zip(acc, ref)), bs
