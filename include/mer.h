@@ -433,6 +433,9 @@ int mer_conv_dgrad_rows(int N, int H, int W, int C, int K, int R, int S, int str
 /* out[c][0:2] = sum_p in[p][c][0:2] over `parts` partial rows, in a fixed order.  parts > 64 needs 64 more
  * rows after them in `in` (fold scratch, overwritten). */
 int mer_partials_sum(int C, int parts, float* in, float* out, void* stream);
+/* Two mer_partials_sum folds of the same shape (C, parts) in one launch (in, out) and (in2, out2): a stride-2
+ * BasicBlock's bn2 and downsample-BN backward sums, which one fused dgrad epilogue wrote. */
+int mer_partials_sum2(int C, int parts, float* in, float* out, float* in2, float* out2, void* stream);
 
 /* dw[k][c][r][s] += sum_p dy[p][k] x(p; r,s,c) for c < Creal, fp32 PyTorch layout (dw initialised).  The
  * pixel reduction is split `splits` ways; each split writes an fp32 slab [K][R*S*C] into `workspace`
@@ -482,6 +485,11 @@ int mer_bn_finalize(int C, long M, const float* stats, float eps, float momentum
  * mer_conv_fwd_rows returned for the conv that filled them; the scratch rows stay at the buffer's end. */
 int mer_bn_finalize_rows(int C, long M, int data_rows, const float* stats, float eps, float momentum, float* ms,
                          float* rmean, float* rvar, long long* num_batches_tracked, void* stream);
+/* Two train-mode mer_bn_finalize_rows in one launch (both stats non-NULL; shared eps / momentum): a stride-2
+ * BasicBlock's bn2 and downsample BN, both convs done before either BatchNorm is applied. */
+int mer_bn_finalize_rows2(int C, long M, int data_rows, const float* stats, float* ms, float* rmean, float* rvar,
+                          long long* nbt, int C2, long M2, int data_rows2, const float* stats2, float* ms2,
+                          float* rmean2, float* rvar2, long long* nbt2, float eps, float momentum, void* stream);
 
 /* y = [relu](bn(x) + (ms2 ? bn2(res) : res)), ms = (mean, rstd) pairs; res may be NULL. */
 int mer_bn_apply(long M, int C, const void* x, const float* ms, const float* gamma, const float* beta, const void* res,

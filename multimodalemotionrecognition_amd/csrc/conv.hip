@@ -2708,13 +2708,13 @@ __device__ __forceinline__ float wide_rows_sum(const float* __restrict__ x, int 
 }
 
 template <int NB>
-__global__ __launch_bounds__(1024) void bn_finalize_wide_kernel(int C, long M, int rows, const float* __restrict__ stats,
-                                                                float eps, float momentum, float* __restrict__ ms,
-                                                                float* __restrict__ rmean, float* __restrict__ rvar,
-                                                                long long* __restrict__ nbt) {
-  __shared__ float part[16][64];
+__device__ __forceinline__ void bn_finalize_wide_body(int C, long M, int rows, const float* __restrict__ stats,
+                                                      float eps, float momentum, float* __restrict__ ms,
+                                                      float* __restrict__ rmean, float* __restrict__ rvar,
+                                                      long long* __restrict__ nbt, float (*part)[64]) {
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int col = blockIdx.x * 64 + l;  // column of the [rows][C][2] layout: channel col / 2, sum (even) / sumsq (odd)
+  if (blockIdx.x * 64 >= 2 * C) return;  // (block-uniform: the paired launch's grid covers the wider record)
   part[w][l] = wide_rows_sum<NB>(stats, rows, 2 * C, col < 2 * C ? col : 2 * C - 1, w);
   __syncthreads();
   if (w != 0) return;
@@ -2732,11 +2732,58 @@ __global__ __launch_bounds__(1024) void bn_finalize_wide_kernel(int C, long M, i
   if (nbt && c == 0) *nbt += 1;
 }
 
+template <int NB>
+__global__ __launch_bounds__(1024) void bn_finalize_wide_kernel(int C, long M, int rows, const float* __restrict__ stats,
+                                                                float eps, float momentum, float* __restrict__ ms,
+                                                                float* __restrict__ rmean, float* __restrict__ rvar,
+                                                                long long* __restrict__ nbt) {
+  __shared__ float part[16][64];
+  bn_finalize_wide_body<NB>(C, M, rows, stats, eps, momentum, ms, rmean, rvar, nbt, part);
+}
+
+// Two BatchNorms' finalizes in one launch (blockIdx.y = record): a stride-2 BasicBlock's bn2 and downsample BN, whose
+// convs both end before either BatchNorm is applied -- one ~4-7 us launch less on the trunk stream per such block.
+struct BnFinRec {
+  int C, rows;
+  long M;
+  const float* stats;
+  float *ms, *rmean, *rvar;
+  long long* nbt;
+};
+struct BnFinPair {
+  BnFinRec r[2];
+};
+template <int NB>
+__global__ __launch_bounds__(1024) void bn_finalize_wide2_kernel(BnFinPair t, float eps, float momentum) {
+  __shared__ float part[16][64];
+  const bool y = blockIdx.y != 0;  // (uniform selects: an indexed kernel-argument record cost scratch at NB = 64)
+  bn_finalize_wide_body<NB>(y ? t.r[1].C : t.r[0].C, y ? t.r[1].M : t.r[0].M, y ? t.r[1].rows : t.r[0].rows,
+                            y ? t.r[1].stats : t.r[0].stats, eps, momentum, y ? t.r[1].ms : t.r[0].ms,
+                            y ? t.r[1].rmean : t.r[0].rmean, y ? t.r[1].rvar : t.r[0].rvar,
+                            y ? t.r[1].nbt : t.r[0].nbt, part);
+}
+
 // out[e] = sum over parts rows of in[p][e], e < 2C, for 64 < parts <= BN_WIDE_ROWS (one launch; see above)
 template <int NB>
 __global__ __launch_bounds__(1024) void partials_sum_wide_kernel(int C2, int parts, const float* __restrict__ in,
                                                                  float* __restrict__ out) {
   __shared__ float part[16][64];
+  const int el = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int e = blockIdx.x * 64 + el, ec = e < C2 ? e : C2 - 1;
+  part[w][el] = wide_rows_sum<NB>(in, parts, C2, ec, w);
+  __syncthreads();
+  if (w == 0 && e < C2) out[e] = pair_tree<16>(&part[0][el], 64);
+}
+// two buffers of the same shape in one launch (blockIdx.y): a stride-2 block's bn2 and downsample-BN backward sums,
+// which one fused dgrad epilogue produced
+template <int NB>
+__global__ __launch_bounds__(1024) void partials_sum_wide2_kernel(int C2, int parts, const float* __restrict__ in0,
+                                                                  float* __restrict__ out0,
+                                                                  const float* __restrict__ in1,
+                                                                  float* __restrict__ out1) {
+  __shared__ float part[16][64];
+  const float* in = blockIdx.y ? in1 : in0;
+  float* out = blockIdx.y ? out1 : out0;
   const int el = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int e = blockIdx.x * 64 + el, ec = e < C2 ? e : C2 - 1;
   part[w][el] = wide_rows_sum<NB>(in, parts, C2, ec, w);
@@ -2756,6 +2803,30 @@ MER_API int mer_bn_finalize(int C, long M, const float* stats, float eps, float 
                             float* rvar, long long* num_batches_tracked, void* stream) {
   return mer_bn_finalize_rows(C, M, (int)((M + 63) / 64), stats, eps, momentum, ms, rmean, rvar, num_batches_tracked,
                               stream);
+}
+
+MER_API int mer_bn_finalize_rows2(int C, long M, int data_rows, const float* stats, float* ms, float* rmean, float* rvar,
+                                  long long* nbt, int C2, long M2, int data_rows2, const float* stats2, float* ms2,
+                                  float* rmean2, float* rvar2, long long* nbt2, float eps, float momentum,
+                                  void* stream) {
+  if (!stats || !stats2 || C <= 0 || C2 <= 0 || data_rows <= 0 || data_rows > (M + 63) / 64 || data_rows2 <= 0 ||
+      data_rows2 > (M2 + 63) / 64)
+    return (int)hipErrorInvalidValue;
+  const int rows = data_rows > data_rows2 ? data_rows : data_rows2;
+  if (rows > BN_WIDE_ROWS) {  // the two-stage folds, one after the other
+    const int rc = mer_bn_finalize_rows(C, M, data_rows, stats, eps, momentum, ms, rmean, rvar, nbt, stream);
+    return rc ? rc : mer_bn_finalize_rows(C2, M2, data_rows2, stats2, eps, momentum, ms2, rmean2, rvar2, nbt2, stream);
+  }
+  BnFinPair t{};
+  t.r[0] = BnFinRec{C, data_rows, M, stats, ms, rmean, rvar, nbt};
+  t.r[1] = BnFinRec{C2, data_rows2, M2, stats2, ms2, rmean2, rvar2, nbt2};
+  const int cmax = C > C2 ? C : C2;
+  const dim3 grid((2 * cmax + 63) / 64, 2);
+  hipStream_t st = (hipStream_t)stream;
+#define MER_BN_FIN2(NB) [&] { hipLaunchKernelGGL(bn_finalize_wide2_kernel<NB>, grid, dim3(1024), 0, st, t, eps, momentum); }
+  wide_pick(rows, MER_BN_FIN2(16), MER_BN_FIN2(32), MER_BN_FIN2(64));
+#undef MER_BN_FIN2
+  MER_LAUNCH_CHECK();
 }
 
 MER_API int mer_bn_finalize_rows(int C, long M, int data_rows, const float* stats, float eps, float momentum, float* ms,
@@ -3021,6 +3092,21 @@ static int partials_fold(int C, int parts, float* in, float* out, hipStream_t st
 MER_API int mer_partials_sum(int C, int parts, float* in, float* out, void* stream) {
   if (C <= 0 || parts <= 0) return (int)hipErrorInvalidValue;
   return partials_fold(C, parts, in, out, (hipStream_t)stream);
+}
+
+MER_API int mer_partials_sum2(int C, int parts, float* in, float* out, float* in2, float* out2, void* stream) {
+  if (C <= 0 || parts <= 0 || !in || !out || !in2 || !out2) return (int)hipErrorInvalidValue;
+  hipStream_t st = (hipStream_t)stream;
+  if (parts > BN_WIDE_ROWS) {  // the two-stage folds, one after the other
+    const int rc = partials_fold(C, parts, in, out, st);
+    return rc ? rc : partials_fold(C, parts, in2, out2, st);
+  }
+  const dim3 grid((2 * C + 63) / 64, 2);
+#define MER_PSUM2(NB) \
+  [&] { hipLaunchKernelGGL(partials_sum_wide2_kernel<NB>, grid, dim3(1024), 0, st, 2 * C, parts, in, out, in2, out2); }
+  wide_pick(parts, MER_PSUM2(16), MER_PSUM2(32), MER_PSUM2(64));
+#undef MER_PSUM2
+  MER_LAUNCH_CHECK();
 }
 
 // dx = gamma*rstd*(g - s1/M - xhat*s2/M) (bf16), and (block 0) dgamma += s2, dbeta += s1.

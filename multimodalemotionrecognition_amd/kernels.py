@@ -694,6 +694,32 @@ def bn_finalize(stats, M, eps, momentum, ms, rmean=None, rvar=None, nbt=None, ro
         _ptr(rmean), _ptr(rvar), _ptr(nbt), stream_ptr())
 
 
+def bn_finalize_pair(a, b, eps, momentum):
+    """Two train-mode bn_finalize calls in one launch (mer_bn_finalize_rows2); a / b = (stats, M, ms, rmean, rvar,
+    nbt, rows) with rows the conv_fwd return value (None: every row)."""
+    args = []
+    for stats, M, ms, rmean, rvar, nbt, rows in (a, b):
+        C = ms.shape[0]
+        if stats is None or stats.numel() != bn_stat_rows(int(M)) * C * 2 or not stats.is_contiguous():
+            raise ValueError("bn_finalize_pair stats must be conv_fwd float[bn_stat_rows(M)][C][2] buffers")
+        rows = bn_stat_rows(int(M)) - 64 if rows is None else rows
+        args += [C, int(M), int(rows), stats.data_ptr(), ms.data_ptr(), _ptr(rmean), _ptr(rvar), _ptr(nbt)]
+    LIB("mer_bn_finalize_rows2", *args, float(eps), float(momentum), stream_ptr())
+
+
+def partials_sum_pair(buf_a, out_a, buf_b, out_b, rows=None):
+    """partials_sum of two same-shape buffers in one launch (mer_partials_sum2)."""
+    P, C, _ = buf_a.shape
+    if tuple(buf_b.shape) != (P, C, 2) or P <= 64:
+        raise ValueError("partials_sum_pair expects two bn_red_rows(M) buffers of one shape")
+    rows = P - 64 if rows is None else rows
+    if not 0 < rows <= P - 64:
+        raise ValueError("partials_sum_pair rows out of range")
+    LIB("mer_partials_sum2", C, int(rows), buf_a.data_ptr(), out_a.data_ptr(), buf_b.data_ptr(), out_b.data_ptr(),
+        stream_ptr())
+    return out_a, out_b
+
+
 def bn_apply(x, ms, gamma, beta, y, relu, res=None, ms2=None, gamma2=None, beta2=None):
     C = x.shape[-1]
     M = x.numel() // C

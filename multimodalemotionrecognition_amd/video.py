@@ -390,8 +390,8 @@ def _stem_wgrad_map(R: int, S: int, C: int, device) -> torch.Tensor:
     return m.to(device)
 
 
-def _conv_bn(trunk, conv, bn, x, stride, pad, training, arena=None, rs=None):
-    """conv (+ fused batch stats) -> (conv output, (mean, rstd))."""
+def _conv_bn(trunk, conv, bn, x, stride, pad, training, arena=None, rs=None, defer=False):
+    """conv (+ fused batch stats) -> (conv output, (mean, rstd)); ``defer`` (train mode): (output, stats, rows)."""
     Kc, _, R, S = conv.weight.shape
     if rs is not None:
         R, S = rs
@@ -403,7 +403,24 @@ def _conv_bn(trunk, conv, bn, x, stride, pad, training, arena=None, rs=None):
         M = N * Ho * Wo
         stats = arena.take(Kc, M=M) if arena is not None else K.bn_stats_buffer(Kc, x.device, M)
     rows = K.conv_fwd(x, trunk.packed(conv, C, False), y, stats, R, S, stride, pad)
+    if defer:  # the caller finalizes (a paired launch): (output, its statistics, rows written)
+        return y, stats, rows
     return y, _bn_forward(bn, y, stats, training, rows)
+
+
+def _bn_forward_pair(bns, ys, stats, rows):
+    """Two train-mode BatchNorm finalizes in one launch (K.bn_finalize_pair) -> their (mean, rstd) tables."""
+    recs, out = [], []
+    for bn, y, st, r in zip(bns, ys, stats, rows):
+        C = y.shape[-1]
+        ms = torch.empty(C, 2, device=y.device, dtype=torch.float32)
+        if (0.1 if bn.momentum is None else bn.momentum) != (0.1 if bns[0].momentum is None else bns[0].momentum) \
+                or bn.eps != bns[0].eps:
+            raise ValueError("paired BatchNorm finalize needs one eps / momentum")
+        recs.append((st, y.numel() // C, ms, bn.running_mean, bn.running_var, bn.num_batches_tracked, r))
+        out.append(ms)
+    K.bn_finalize_pair(recs[0], recs[1], bns[0].eps, 0.1 if bns[0].momentum is None else bns[0].momentum)
+    return out
 
 
 @torch.no_grad()
@@ -413,11 +430,18 @@ def block_forward(trunk, blk: BasicBlock, x: torch.Tensor, training: bool, arena
     bc1, bms1 = _conv_bn(trunk, blk.conv1, blk.bn1, x, s, 1, training, arena)
     ba1 = torch.empty_like(bc1)
     K.bn_apply(bc1, bms1, blk.bn1.weight, blk.bn1.bias, ba1, relu=True)
-    bc2, bms2 = _conv_bn(trunk, blk.conv2, blk.bn2, ba1, 1, 1, training, arena)
+    dbn = blk.downsample[1] if blk.downsample is not None else None
+    paired = dbn is not None and training and BN_FIN_PAIR
+    if paired:  # conv2 and the downsample conv first, then both BatchNorms' finalizes in one launch
+        bc2, st2, r2 = _conv_bn(trunk, blk.conv2, blk.bn2, ba1, 1, 1, training, arena, defer=True)
+        cd, std, rd = _conv_bn(trunk, blk.downsample[0], dbn, x, s, 0, training, arena, defer=True)
+        bms2, msd = _bn_forward_pair((blk.bn2, dbn), (bc2, cd), (st2, std), (r2, rd))
+    else:
+        bc2, bms2 = _conv_bn(trunk, blk.conv2, blk.bn2, ba1, 1, 1, training, arena)
     out = torch.empty_like(bc2)
     if blk.downsample is not None:
-        cd, msd = _conv_bn(trunk, blk.downsample[0], blk.downsample[1], x, s, 0, training, arena)
-        dbn = blk.downsample[1]
+        if not paired:
+            cd, msd = _conv_bn(trunk, blk.downsample[0], blk.downsample[1], x, s, 0, training, arena)
         K.bn_apply(bc2, bms2, blk.bn2.weight, blk.bn2.bias, out, relu=True, res=cd, ms2=msd, gamma2=dbn.weight,
                    beta2=dbn.bias)
     else:
@@ -541,6 +565,9 @@ WGRAD_DEFER = True
 # (mer_bn_bwd_apply2, bit-identical; 3 x 4 fewer bytes per element and one launch less per stride-2 block; the
 # same-box step did not move measurably: 211.51 vs 211.74 steps/s, profiles/r06/step_ab_fold_b8)
 BN_BWD_PAIR = True
+# A stride-2 block's bn2 and downsample-BN statistics folds paired into one launch, forward (mer_bn_finalize_rows2)
+# and backward (mer_partials_sum2)
+BN_FIN_PAIR = True  # same-box step +0.59 % (profiles/r06/step_ab_fin_pair)
 # The downsample's input gradient fused into conv1's stride-2 dgrad (mer_conv_dgrad_ds): +1.2 % same-box vs the
 # separate 1x1 dgrad whose bf16 output the 3x3 dgrad read back as its residual (profiles/r04/ab_runs.txt)
 FUSED_DS_DGRAD = True
@@ -580,9 +607,13 @@ def block_backward(trunk, blk: BasicBlock, sv, dx: torch.Tensor, grads, training
     s = blk.stride
     C2 = bc2.shape[-1]
     if pre is not None:  # (red2 rows, downsample-BN rows, rows the producing dgrad wrote)
-        red2 = K.partials_sum(pre[0], torch.empty(C2, 2, device=dev, dtype=torch.float32), pre[2])
-        redd = K.partials_sum(pre[1], torch.empty(C2, 2, device=dev, dtype=torch.float32), pre[2]) \
-            if cd is not None else None
+        if cd is not None and BN_FIN_PAIR:
+            red2, redd = K.partials_sum_pair(pre[0], torch.empty(C2, 2, device=dev, dtype=torch.float32), pre[1],
+                                             torch.empty(C2, 2, device=dev, dtype=torch.float32), pre[2])
+        else:
+            red2 = K.partials_sum(pre[0], torch.empty(C2, 2, device=dev, dtype=torch.float32), pre[2])
+            redd = K.partials_sum(pre[1], torch.empty(C2, 2, device=dev, dtype=torch.float32), pre[2]) \
+                if cd is not None else None
     else:
         red2 = arena.take(C2, parts=1)
         K.bn_bwd_reduce(g_out, out, bc2, bms2, red2, arena.take(C2, parts=K.BN_RED_WS_ROWS))

@@ -900,3 +900,48 @@ def test_bn_bwd_apply2_matches_two_launches(M, C):
                         e2, acc[2], acc[3], bs)
         assert torch.equal(d1, e1) and torch.equal(d2, e2), bs
         assert all(torch.equal(a, b) for a, b in zip(acc, ref)), bs
+
+
+@pytest.mark.parametrize("M,C", [(4096, 512), (12544, 256), (50176, 128), (200704, 64)])
+def test_bn_fold_pairs_match_single_launches(M, C):
+    """mer_bn_finalize_rows2 / mer_partials_sum2 (a stride-2 block's bn2 + downsample-BN folds in one launch) against
+    two single launches: bitwise where both take the wide kernel (65-1024 rows), to fp32 rounding where a single call
+    takes the <= 64-row or two-stage form; running statistics and num_batches_tracked updated per record."""
+    from multimodalemotionrecognition_amd import kernels as K
+
+    torch.manual_seed(29)
+    rows = K.bn_stat_rows(M)
+    data = rows - 64
+    recs = []
+    for _ in range(2):
+        st = torch.zeros(rows, C, 2, device="cuda")
+        st[:data, :, 0] = torch.randn(data, C, device="cuda") * 3 + 1.0
+        st[:data, :, 1] = torch.randn(data, C, device="cuda").abs() * 40 + 64.0
+        recs.append(st)
+    exact = 64 < data <= 1024
+    single, paired = [], []
+    for st in recs:
+        ms, rm, rv = torch.empty(C, 2, device="cuda"), torch.zeros(C, device="cuda"), torch.ones(C, device="cuda")
+        nbt = torch.zeros((), dtype=torch.int64, device="cuda")
+        K.bn_finalize(st.clone(), M, 1e-5, 0.1, ms, rm, rv, nbt)
+        single.append((ms, rm, rv, nbt))
+    args = []
+    for st in recs:
+        ms, rm, rv = torch.empty(C, 2, device="cuda"), torch.zeros(C, device="cuda"), torch.ones(C, device="cuda")
+        nbt = torch.zeros((), dtype=torch.int64, device="cuda")
+        args.append((st.clone(), M, ms, rm, rv, nbt, None))
+        paired.append((ms, rm, rv, nbt))
+    K.bn_finalize_pair(args[0], args[1], 1e-5, 0.1)
+    for a, b in zip(single, paired):
+        for x, y in zip(a, b):
+            assert torch.equal(x, y) if exact or x.dtype == torch.int64 else torch.allclose(x, y, rtol=2e-6, atol=1e-6)
+    prow = K.bn_red_rows(M)
+    bufs = [torch.randn(prow, C, 2, device="cuda") for _ in range(2)]
+    for b in bufs:
+        b[prow - 64:] = 0
+    s = [K.partials_sum(b.clone(), torch.empty(C, 2, device="cuda")) for b in bufs]
+    p = K.partials_sum_pair(bufs[0].clone(), torch.empty(C, 2, device="cuda"), bufs[1].clone(),
+                            torch.empty(C, 2, device="cuda"))
+    pexact = 64 < prow - 64 <= 1024
+    for x, y in zip(s, p):
+        assert torch.equal(x, y) if pexact else torch.allclose(x, y, rtol=1e-5, atol=1e-4)
