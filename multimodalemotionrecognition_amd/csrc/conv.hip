@@ -2130,7 +2130,15 @@ MER_API int mer_conv_fwd_rows(int N, int H, int W, int C, int K, int R, int S, i
     const int hk = halo_kind(g, false);
     if (hk) return halo_rows(g, hk);
   }
-  return (int)(((long)N * g.OH * g.OW + 63) / 64);
+  const long M = (long)N * g.OH * g.OW;
+  if (variant == -1) {  // the default pipelined tile: one statistics row per BM-row tile (launch_conv_pipe's choice)
+    const int v = conv_default_variant(g, 2);
+    const int bn = g.Ncols <= 64 ? 64 : 128;
+    const bool small_m = ((M + 127) / 128) * ((g.Ncols + bn - 1) / bn) < 384;
+    const int BM = (v == 7 || small_m) ? 64 : 128;
+    return (int)((M + BM - 1) / BM);
+  }
+  return (int)((M + 63) / 64);  // an upper bound: rows past the tiles stay as the caller left them (zeroed)
 }
 
 MER_API int mer_conv_dgrad_rows(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, const void* dy,

@@ -338,10 +338,12 @@ class _StatsArena:
     Forward: per-row-tile statistics rows (``take(C, M=...)``, float[MER_BN_STAT_ROWS(M)][C][2], sized by
     ``_fwd_stat_floats``); backward: striped reduction rows (float[MER_BN_STAT_PARTS][C][2] or [C][2])."""
 
-    def __init__(self, trunk, device, factor: int = 1, floats: int = 0):
+    def __init__(self, trunk, device, factor: int = 1, floats: int = 0, zero: bool = True):
         total = sum(m.out_channels for m in trunk.modules() if isinstance(m, nn.Conv2d))
         n = floats if floats else factor * K.BN_STAT_PARTS * 2 * total
-        self.buf = torch.zeros(n, device=device, dtype=torch.float32)
+        # zero=False: every row a reader folds is written first (the forward statistics of default-variant convs, whose
+        # exact row counts K.conv_fwd returns) -- no 22.6 MB memset on the trunk stream at B = 32
+        self.buf = (torch.zeros if zero else torch.empty)(n, device=device, dtype=torch.float32)
         self.off = 0
 
     def take(self, C, parts=None, M=None):
@@ -498,7 +500,9 @@ def _trunk_forward(trunk: ResNet18Trunk, video: torch.Tensor, training: bool, s2
         if tuple(s2d.shape) != (N, H // 2 + 3, W // 2 + 3, S2D_CH) or s2d.dtype != bf:
             raise ValueError(f"packed frames {tuple(s2d.shape)} do not match video {tuple(video.shape)}")
         x0 = s2d
-    arena = _StatsArena(trunk, dev, floats=_fwd_stat_floats(trunk, N, H, W)) if training else None
+    # (not zeroed when the finalizes read only written rows: same-box +0.1 %, profiles/r06/step_ab_fwd_rows_exact)
+    arena = _StatsArena(trunk, dev, floats=_fwd_stat_floats(trunk, N, H, W), zero=not K.PARTIAL_ROWS) \
+        if training else None
     c1, ms1 = _conv_bn(trunk, conv1, bn1, x0, 1, 0, training, arena, rs=(4, 4))
     Hp, Wp = (c1.shape[1] - 1) // 2 + 1, (c1.shape[2] - 1) // 2 + 1
     p1 = torch.empty(N, Hp, Wp, c1.shape[-1], device=dev, dtype=bf)

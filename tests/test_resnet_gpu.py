@@ -945,3 +945,33 @@ def test_bn_fold_pairs_match_single_launches(M, C):
     pexact = 64 < prow - 64 <= 1024
     for x, y in zip(s, p):
         assert torch.equal(x, y) if pexact else torch.allclose(x, y, rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("shape", [(256, 28, 64, 64, 3, 1), (256, 28, 64, 128, 3, 2), (256, 14, 128, 128, 3, 1),
+                                   (256, 28, 64, 128, 1, 2), (256, 14, 128, 256, 3, 2), (256, 7, 256, 256, 3, 1),
+                                   (256, 7, 256, 512, 3, 2), (256, 4, 512, 512, 3, 1), (40, 14, 128, 128, 3, 1)])
+def test_conv_fwd_rows_exact_for_default_variant(shape):
+    """With the default variant, K.conv_fwd's returned row count is exact: every statistics row below it is written
+    (the trunk's forward arena is therefore not zeroed), and the finalize over those rows of a NaN-filled buffer equals
+    the finalize of a zeroed one.  The ResNet18 forward convs at B = 32 (and a small batch)."""
+    from multimodalemotionrecognition_amd import kernels as K
+
+    N, H, C, Kc, R, s = shape
+    pad = R // 2
+    torch.manual_seed(31)
+    x = torch.randn(N, H, H, C, device="cuda").bfloat16()
+    w = torch.randn(Kc, C, R, R, device="cuda") / (R * (C ** 0.5))
+    wp = torch.empty(Kc, R * R * C, device="cuda", dtype=torch.bfloat16)
+    K.pack_conv_weight(w, wp, C, False)
+    Ho = (H + 2 * pad - R) // s + 1
+    M = N * Ho * Ho
+    outs = []
+    for fill in (0.0, float("nan")):
+        y = torch.empty(N, Ho, Ho, Kc, device="cuda", dtype=torch.bfloat16)
+        st = torch.full((K.bn_stat_rows(M), Kc, 2), fill, device="cuda")
+        rows = K.conv_fwd(x, wp, y, st, R, R, s, pad)
+        assert not torch.isnan(st[:rows]).any(), rows
+        ms = torch.empty(Kc, 2, device="cuda")
+        K.bn_finalize(st, M, 1e-5, 0.1, ms, rows=rows)
+        outs.append(ms)
+    assert torch.equal(outs[0], outs[1])
