@@ -424,7 +424,8 @@ int mer_conv_dgrad_ds(int N, int H, int W, int C, int K, int R, int S, int strid
  * MER_BN_RED_ROWS(M) - 64), or one per workgroup where the persistent halo kernel runs (layer1, the stem: 256 / 512
  * at B = 32 instead of 3,136 / 12,544), whose rows past these stay zero.  For mer_conv_fwd_ex with variant -1 the
  * count is exact (every row below it is written: one per BM-row tile of the default tile choice), so a statistics
- * buffer of such a call needs no zeroing; for an explicit variant it is an upper bound (zero the buffer).  The same geometry test as the launch; a
+ * buffer of such a call needs no zeroing; for an explicit variant it is an upper bound (zero the buffer).  Likewise
+ * mer_conv_dgrad_rows for a stride-1 / stride-2 dgrad with variant -1 (one row per BM-row tile, per parity class).   The same geometry test as the launch; a
  * negative hipError_t on invalid arguments.  Pass the count to mer_bn_finalize_rows / mer_partials_sum so the
  * fold reads only written rows (one launch instead of two past 1,024 tile rows). */
 int mer_conv_fwd_rows(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, const void* x,

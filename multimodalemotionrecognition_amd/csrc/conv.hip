@@ -2149,7 +2149,26 @@ MER_API int mer_conv_dgrad_rows(int N, int H, int W, int C, int K, int R, int S,
     const int hk = halo_kind(g, true);
     if (hk) return halo_rows(g, hk);
   }
-  return (int)(((long)N * H * W + 63) / 64 + 4);  // MER_BN_RED_ROWS(M) - 64
+  if (variant == -1 && (stride == 1 || stride == 2)) {
+    // the default pipelined tile (mer_conv_dgrad_ds's variant resolution, launch_conv_pipe's tile rule): one reduction
+    // row per BM-row tile, per parity class for the stride-2 form (red_row: the classes' tiles back to back) -- exact
+    int v = C <= 64 ? 5 : 2;
+    if (stride == 1) v = conv_default_variant(g, v);
+    const bool par = stride == 2;
+    const long Mq = par ? (long)N * H * W / 4 : (long)N * H * W;
+    const int bn = C <= 64 ? 64 : 128;
+    const bool small_m = ((Mq + 127) / 128) * ((C + bn - 1) / bn) * (par ? 4 : 1) < 384;
+    const int BM = (v == 7 || small_m) ? 64 : 128;
+    if (!par) return (int)(((long)N * H * W + BM - 1) / BM);
+    long rows = 0;
+    for (int cls = 0; cls < 4; ++cls) {
+      const int ph = cls >> 1, pw = cls & 1;
+      const long Mc = (long)N * ((H - ph + 1) >> 1) * ((W - pw + 1) >> 1);
+      rows += (Mc + BM - 1) / BM;
+    }
+    return (int)rows;
+  }
+  return (int)(((long)N * H * W + 63) / 64 + 4);  // MER_BN_RED_ROWS(M) - 64: an upper bound (zero the buffer)
 }
 
 MER_API int mer_conv_fwd_ex(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, const void* x,

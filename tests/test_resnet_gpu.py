@@ -975,3 +975,46 @@ def test_conv_fwd_rows_exact_for_default_variant(shape):
         K.bn_finalize(st, M, 1e-5, 0.1, ms, rows=rows)
         outs.append(ms)
     assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("shape", [(256, 28, 64, 64, 1, False, False), (256, 28, 64, 128, 2, True, False),
+                                   (256, 14, 128, 128, 1, False, True), (256, 14, 128, 256, 2, True, False),
+                                   (256, 7, 256, 256, 1, False, True), (256, 7, 256, 512, 2, True, False),
+                                   (256, 4, 512, 512, 1, False, False), (40, 14, 128, 128, 1, False, False),
+                                   (40, 14, 128, 256, 2, False, False)])
+def test_conv_dgrad_rows_exact_for_default_variant(shape):
+    """With the default variant, K.conv_dgrad's returned reduction row count is exact for the stride-1 and the
+    parity-class stride-2 dgrads (with the fused downsample segment and with a second BN): every row below it is
+    written (the trunk backward's reduction arena is not zeroed), and the fold over those rows of a NaN-filled buffer
+    equals the fold of a zeroed one.  The ResNet18 input gradients at B = 32 (and a small batch)."""
+    from multimodalemotionrecognition_amd import kernels as K
+
+    N, H, C, Kc, s, ds, two = shape  # dx [N, H, H, C] <- dy [N, H/s, H/s, Kc]
+    torch.manual_seed(37)
+    Ho = (H + 2 - 3) // s + 1
+    dy = torch.randn(N, Ho, Ho, Kc, device="cuda").bfloat16()
+    w = torch.randn(Kc, C, 3, 3, device="cuda") / (3 * Kc ** 0.5)
+    wt = torch.empty(C, 9 * Kc, device="cuda", dtype=torch.bfloat16)
+    K.pack_conv_weight(w, wt, C, True)
+    kw = {}
+    if ds:
+        wd = torch.randn(Kc, C, 1, 1, device="cuda") / Kc ** 0.5
+        wdt = torch.empty(C, Kc, device="cuda", dtype=torch.bfloat16)
+        K.pack_conv_weight(wd, wdt, C, True)
+        kw["ds"] = (torch.randn(N, Ho, Ho, Kc, device="cuda").bfloat16(), wdt)
+    mask, xb, xb2 = (torch.randn(N, H, H, C, device="cuda").bfloat16() for _ in range(3))
+    ms = torch.stack([torch.randn(C), torch.rand(C) + 0.5], 1).cuda().contiguous()
+    M = N * H * H
+    res = []
+    for fill in (0.0, float("nan")):
+        reds = [torch.full((K.bn_red_rows(M), C, 2), fill, device="cuda") for _ in range(2)]
+        bnr = (mask, xb, ms, reds[0]) + ((xb2, ms, reds[1]) if two else ())
+        dx = torch.empty(N, H, H, C, device="cuda", dtype=torch.bfloat16)
+        rows = K.conv_dgrad(dy, wt, dx, 3, 3, s, 1, bnr=bnr, **kw)
+        out = []
+        for red in reds[:2 if two else 1]:
+            assert not torch.isnan(red[:rows]).any(), rows
+            out.append(K.partials_sum(red, torch.empty(C, 2, device="cuda"), rows))
+        res.append(out)
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
