@@ -572,6 +572,10 @@ BN_BWD_PAIR = True
 # A stride-2 block's bn2 and downsample-BN statistics folds paired into one launch, forward (mer_bn_finalize_rows2)
 # and backward (mer_partials_sum2)
 BN_FIN_PAIR = True  # same-box step +0.59 % (profiles/r06/step_ab_fin_pair)
+# The deferred weight-gradient folds flushed at the end of every ResNet layer (every second BasicBlock) instead of once
+# after all blocks: each fold reads slabs written a layer earlier (more of them still in the 256 MB MALL), three
+# launches more per step; same-box +0.27 % (profiles/r06/step_ab_fold_per_layer)
+FOLD_EVERY = 2
 # The downsample's input gradient fused into conv1's stride-2 dgrad (mer_conv_dgrad_ds): +1.2 % same-box vs the
 # separate 1x1 dgrad whose bf16 output the 3x3 dgrad read back as its residual (profiles/r04/ab_runs.txt)
 FUSED_DS_DGRAD = True
@@ -710,6 +714,8 @@ def _backward_blocks(trunk, saved, state, lo, training):
         state["dx"], state["pre"] = block_backward(trunk, blocks[i], svs[i], state["dx"], state["grads"], training,
                                                    pre=state["pre"], prev=prev, arena=state["arena"],
                                                    lane=state["lane"], bidx=i)
+        if FOLD_EVERY and i % FOLD_EVERY == 0 and i > 0:
+            state["lane"].join()
         state["i"] = i - 1
 
 
